@@ -1,0 +1,25 @@
+# Builds the C-ABI HIP library for gfx950 in-tree (travels to the GPU box with the snapshot).
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+SRC_DIR := animatable_nerf_amd/csrc
+SRCS := $(SRC_DIR)/anr_capi.hip $(SRC_DIR)/anr_rays.hip $(SRC_DIR)/anr_mlp.hip $(SRC_DIR)/anr_pack.hip
+HDRS := $(wildcard $(SRC_DIR)/*.h) include/aninerf.h
+OBJS := $(SRCS:.hip=.o)
+LIB := animatable_nerf_amd/libaninerf_hip.so
+CXXFLAGS := -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -Wall -Wno-unused-function -Iinclude
+
+all: $(LIB)
+
+$(SRC_DIR)/%.o: $(SRC_DIR)/%.hip $(HDRS)
+	$(HIPCC) $(CXXFLAGS) -c $< -o $@
+
+$(LIB): $(OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)
+
+resources: $(SRC_DIR)/anr_mlp.hip $(HDRS)
+	$(HIPCC) $(CXXFLAGS) -c $(SRC_DIR)/anr_mlp.hip -o /tmp/anr_mlp_res.o -Rpass-analysis=kernel-resource-usage
+
+clean:
+	rm -f $(OBJS) $(LIB)
+
+.PHONY: all clean resources

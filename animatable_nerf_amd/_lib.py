@@ -1,0 +1,89 @@
+"""ctypes binding of the C-ABI library ``libaninerf_hip.so`` (include/aninerf.h).
+
+The library is built in-tree by ``make`` (``__graft_entry__.build()``). Loading it is mandatory:
+there is no CPU or PyTorch fallback for the render path, a missing or stale library raises.
+``torch`` is imported first so the HIP runtime torch ships (same SONAME ``libamdhip64.so.7``)
+is the one the library binds to — one runtime, one set of streams.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (must be loaded before the library, see module docstring)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, 'libaninerf_hip.so')
+NUM_TENSORS = 46
+
+EXPORTS = ('anr_near_far', 'anr_params_packed_bytes', 'anr_params_pack', 'anr_render_workspace_bytes',
+           'anr_render_fwd', 'anr_render_counts', 'anr_render_bw_rows', 'anr_profile_enable', 'anr_profile_read',
+           'anr_last_error', 'anr_version')
+
+c_float_p = ctypes.c_void_p
+
+
+class Params(ctypes.Structure):
+    _fields_ = [('t', ctypes.c_void_p * NUM_TENSORS), ('num_train_frame', ctypes.c_int),
+                ('packed', ctypes.c_void_p)]
+
+
+class Frame(ctypes.Structure):
+    _fields_ = [('A', ctypes.c_void_p), ('R', ctypes.c_void_p), ('Th', ctypes.c_void_p),
+                ('pbw', ctypes.c_void_p), ('pbw_dims', ctypes.c_int * 3), ('pbounds', ctypes.c_void_p),
+                ('tbw', ctypes.c_void_p), ('tbw_dims', ctypes.c_int * 3), ('tbounds', ctypes.c_void_p),
+                ('latent_index', ctypes.c_void_p)]
+
+
+class RenderOpts(ctypes.Structure):
+    _fields_ = [('n_samples', ctypes.c_int), ('chunk', ctypes.c_int), ('norm_th', ctypes.c_float),
+                ('train_th', ctypes.c_float), ('t_rand', ctypes.c_void_p)]
+
+
+class RenderOut(ctypes.Structure):
+    _fields_ = [('rgb_map', ctypes.c_void_p), ('acc_map', ctypes.c_void_p), ('depth_map', ctypes.c_void_p),
+                ('raw', ctypes.c_void_p)]
+
+
+_lib = None
+
+
+def load():
+    """Load (once) and return the library; raises if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f'{LIB_PATH} not built: run `make` (or __graft_entry__.build()) first; '
+                           'the HIP path has no fallback')
+    lib = ctypes.CDLL(LIB_PATH)
+    P = ctypes.c_void_p
+    lib.anr_near_far.argtypes = [P, P, ctypes.c_int, P, P, P, P, P]
+    lib.anr_params_packed_bytes.restype = ctypes.c_size_t
+    lib.anr_params_pack.argtypes = [ctypes.POINTER(Params), P, P]
+    lib.anr_render_workspace_bytes.restype = ctypes.c_size_t
+    lib.anr_render_workspace_bytes.argtypes = [ctypes.c_int, ctypes.POINTER(RenderOpts), ctypes.POINTER(Frame)]
+    lib.anr_render_fwd.argtypes = [ctypes.POINTER(Params), ctypes.POINTER(Frame), P, P, P, P, ctypes.c_int,
+                                   ctypes.POINTER(RenderOpts), ctypes.POINTER(RenderOut), P, ctypes.c_size_t, P]
+    lib.anr_render_counts.restype = P
+    lib.anr_render_counts.argtypes = [P, ctypes.c_int]
+    lib.anr_render_bw_rows.argtypes = [P, ctypes.c_int, P, P, P]
+    lib.anr_profile_enable.argtypes = [ctypes.c_int]
+    lib.anr_profile_read.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]
+    lib.anr_last_error.restype = ctypes.c_char_p
+    for name in EXPORTS:
+        getattr(lib, name)
+    _lib = lib
+    return lib
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = _lib.anr_last_error().decode() if _lib is not None else ''
+        raise RuntimeError(f'{what} failed (code {rc}): {msg}')
+
+
+def stream_ptr(device=None):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)

@@ -1,0 +1,113 @@
+"""yacs-compatible configuration for the hot path (lib/config/config.py:9-194, lib/config/yacs.py).
+
+Accepts the reference's yaml files (``parent_cfg`` inheritance, unknown keys kept) and CLI
+``key value`` pairs, so ``--cfg_file configs/aninerf_s9p.yaml exp_name x resume False`` means the
+same thing here. Only the keys the render/train path reads have typed defaults; the rest are
+carried through untouched.
+"""
+import ast
+import copy
+import os
+
+import yaml
+
+
+class CfgNode(dict):
+    """dict with attribute access (the subset of yacs.CfgNode the hot path uses)."""
+
+    def __init__(self, init=None):
+        super().__init__()
+        for k, v in (init or {}).items():
+            self[k] = CfgNode(v) if isinstance(v, dict) and not isinstance(v, CfgNode) else v
+
+    def __getattr__(self, name):
+        try:
+            return self[name]
+        except KeyError as e:
+            raise AttributeError(name) from e
+
+    def __setattr__(self, name, value):
+        self[name] = value
+
+    def merge(self, other):
+        for k, v in other.items():
+            if isinstance(v, dict):
+                if not isinstance(self.get(k), CfgNode):
+                    self[k] = CfgNode()
+                self[k].merge(v)
+            else:
+                self[k] = v
+        return self
+
+    def merge_from_list(self, opts):
+        """``key value`` pairs, dotted keys allowed (yacs.py:190-217); values parsed as literals."""
+        if len(opts) % 2:
+            raise ValueError(f'override list has odd length: {opts}')
+        for k, v in zip(opts[0::2], opts[1::2]):
+            node = self
+            parts = k.split('.')
+            for p in parts[:-1]:
+                node = node.setdefault(p, CfgNode())
+            node[parts[-1]] = _literal(v)
+        return self
+
+    def clone(self):
+        return copy.deepcopy(self)
+
+
+def _literal(v):
+    if not isinstance(v, str):
+        return v
+    try:
+        return ast.literal_eval(v)
+    except (ValueError, SyntaxError):
+        return v
+
+
+def defaults():
+    """Defaults of the keys the hot path reads (config.py:9-137 + configs/aninerf_s9p.yaml)."""
+    return CfgNode({
+        'task': 'deform', 'exp_name': 'hello', 'gpus': [0], 'distributed': False, 'local_rank': 0,
+        'num_train_frame': 260, 'num_eval_frame': 133, 'num_latent_code': -1,
+        'N_samples': 64, 'N_rand': 1024, 'perturb': 1, 'white_bkgd': False,
+        'xyz_res': 10, 'view_res': 4, 'norm_th': 0.05, 'train_th': 0.0, 'box_padding': 0.05,
+        'aninerf_animation': False, 'test_novel_pose': False, 'eval': False,
+        'chunk': 2048,
+        'train': {'lr': 5e-4, 'weight_decay': 0.0, 'optim': 'adam', 'epoch': 400,
+                  'scheduler': {'type': 'exponential', 'gamma': 0.1, 'decay_epochs': 1000}},
+        'ep_iter': 500, 'save_ep': 200, 'save_latest_ep': 5, 'eval_ep': 1000,
+        'trained_model_dir': 'data/trained_model', 'record_dir': 'data/record', 'result_dir': 'data/result',
+        'network_module': 'animatable_nerf_amd.network', 'renderer_module': 'animatable_nerf_amd.renderer',
+    })
+
+
+def load_cfg(cfg_file=None, opts=(), base_dir=None):
+    """Load ``cfg_file`` (resolving ``parent_cfg`` relative to ``base_dir``) over the defaults."""
+    cfg = defaults()
+    if cfg_file:
+        chain = []
+        path = cfg_file
+        while path:
+            full = path if os.path.isabs(path) or base_dir is None else os.path.join(base_dir, path)
+            with open(full) as f:
+                node = yaml.safe_load(f) or {}
+            chain.append(node)
+            path = node.get('parent_cfg')
+            if path and not os.path.exists(path if base_dir is None else os.path.join(base_dir, path)):
+                break
+        for node in reversed(chain):
+            node = {k: v for k, v in node.items() if k != 'parent_cfg'}
+            cfg.merge(CfgNode(node))
+    cfg.merge_from_list(list(opts))
+    for sub in ('aninerf_animation', 'vis_pose_sequence', 'vis_novel_view'):
+        key = {'aninerf_animation': 'aninerf_animation_cfg', 'vis_pose_sequence': 'pose_sequence_cfg',
+               'vis_novel_view': 'novel_view_cfg'}[sub]
+        if cfg.get(sub) and key in cfg:
+            cfg.merge(cfg[key])
+            cfg.merge_from_list(list(opts))
+    if cfg.num_latent_code < 0:
+        cfg.num_latent_code = cfg.num_train_frame
+    return cfg
+
+
+cfg = defaults()

@@ -1,0 +1,310 @@
+// anr_capi.hip — the C-ABI (include/aninerf.h): argument checks, workspace layout, launch order.
+// All launches are asynchronous on the caller's stream; no allocation, no synchronisation, so a
+// caller may capture a whole render into a hipGraph.
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "../../include/aninerf.h"
+#include "anr_common.h"
+#include "anr_kernels.h"
+#include "anr_layers.h"
+
+using namespace anr;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+int check_launch(const char* what) {
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(ANR_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
+  return ANR_OK;
+}
+
+#define ANR_TRY(x)                  \
+  do {                              \
+    const int _rc = (x);            \
+    if (_rc != ANR_OK) return _rc;  \
+  } while (0)
+
+size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
+
+// Workspace layout. Fields up to `tbw_rows` depend only on n_rays (anr_render_counts/bw_rows).
+struct Layout {
+  size_t counts, mask, ray_off, block_sum, list, sigma, flags, block_sum2, out_row, pbw_rows, tbw_rows;
+  size_t chunk_min, chunk_max, raw, pbw32, tbw32, fold, total;
+};
+
+Layout layout(int n_rays, int chunk, long np, long nt, bool need_raw) {
+  Layout L{};
+  const size_t R = (size_t)n_rays, N = R * 64;
+  size_t o = 0;
+  auto take = [&](size_t bytes) {
+    const size_t at = o;
+    o = align256(o + bytes);
+    return at;
+  };
+  L.counts = take(16);
+  L.mask = take(R * 8);
+  L.ray_off = take((R + 1) * 4);
+  L.block_sum = take(((R + 255) / 256) * 4);
+  L.list = take(N * 4);
+  L.sigma = take(N * 4);
+  L.flags = take(N);
+  L.block_sum2 = take(((N + 1023) / 1024) * 4);
+  L.out_row = take(N * 4);
+  L.pbw_rows = take(N * 24 * 4);
+  L.tbw_rows = take(N * 24 * 4);
+  const size_t nch = (R + chunk - 1) / (chunk > 0 ? chunk : 1);
+  L.chunk_min = take(nch * 8);
+  L.chunk_max = take(nch * 8);
+  L.raw = need_raw ? take(N * 16) : 0;
+  L.pbw32 = take((size_t)np * 32 * 4);
+  L.tbw32 = take((size_t)nt * 32 * 4);
+  L.fold = take(1280 * 4);
+  L.total = o;
+  return L;
+}
+
+int num_cus() {
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (cached[dev] == 0) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+    cached[dev] = v;
+  }
+  return cached[dev];
+}
+
+bool mlp_attr_set = false;
+
+// measurement: event pairs around k_mlp (anr_profile_enable / anr_profile_read)
+struct Prof {
+  bool on = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
+  size_t used = 0;
+} g_prof;
+
+}  // namespace
+
+extern "C" {
+
+int anr_version(void) { return 1; }
+
+const char* anr_last_error(void) { return g_err.c_str(); }
+
+int anr_near_far(const float* ray_o, const float* ray_d, int n, const float* bounds, uint8_t* mask, float* near_,
+                 float* far_, void* stream) {
+  if (n < 0 || (n > 0 && (!ray_o || !ray_d || !bounds || !mask || !near_ || !far_)))
+    return fail(ANR_E_ARG, "anr_near_far: bad arguments");
+  if (n == 0) return ANR_OK;
+  hipLaunchKernelGGL(k_near_far, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, ray_o, ray_d, n, bounds, mask,
+                     near_, far_);
+  return check_launch("k_near_far");
+}
+
+size_t anr_params_packed_bytes(void) { return (size_t)packed_bytes(); }
+
+int anr_params_pack(const anr_params* p, void* packed, void* stream) {
+  if (!p || !packed) return fail(ANR_E_ARG, "anr_params_pack: NULL");
+  PackArgs a{};
+  for (int i = 0; i < ANR_NUM_TENSORS; ++i) {
+    if (!p->t[i]) return fail(ANR_E_ARG, "anr_params_pack: tensor " + std::to_string(i) + " is NULL");
+    a.t[i] = p->t[i];
+  }
+  a.out = (unsigned char*)packed;
+  const int nw = weights_bytes() / 4;
+  hipLaunchKernelGGL(k_pack_weights, dim3((nw + 255) / 256), dim3(256), 0, (hipStream_t)stream, a);
+  ANR_TRY(check_launch("k_pack_weights"));
+  hipLaunchKernelGGL(k_pack_bias, dim3((bias_floats() + 255) / 256), dim3(256), 0, (hipStream_t)stream, a);
+  return check_launch("k_pack_bias");
+}
+
+size_t anr_render_workspace_bytes(int n_rays, const anr_render_opts* o, const anr_frame* f) {
+  if (!o || !f || n_rays < 0) return 0;
+  const long np = (long)f->pbw_dims[0] * f->pbw_dims[1] * f->pbw_dims[2];
+  const long nt = (long)f->tbw_dims[0] * f->tbw_dims[1] * f->tbw_dims[2];
+  return layout(n_rays, o->chunk, np, nt, true).total;
+}
+
+const int32_t* anr_render_counts(const void* workspace, int n_rays) {
+  return (const int32_t*)((const char*)workspace + layout(n_rays, 1, 0, 0, false).counts);
+}
+
+int anr_render_fwd(const anr_params* p, const anr_frame* f, const float* ray_o, const float* ray_d, const float* near_,
+                   const float* far_, int n_rays, const anr_render_opts* o, const anr_render_out* out, void* workspace,
+                   size_t ws_bytes, void* stream) {
+  if (!p || !f || !o || !out || !workspace) return fail(ANR_E_ARG, "anr_render_fwd: NULL argument");
+  if (o->n_samples != 64) return fail(ANR_E_ARG, "anr_render_fwd: only N_samples == 64 is supported");
+  if (o->chunk <= 0) return fail(ANR_E_ARG, "anr_render_fwd: chunk must be > 0");
+  if (n_rays <= 0) return fail(ANR_E_ARG, "anr_render_fwd: n_rays must be > 0");
+  if ((long)n_rays * 64 > 0x7fffffffL / 24) return fail(ANR_E_ARG, "anr_render_fwd: too many rays for one call");
+  if (!ray_o || !ray_d || !near_ || !far_ || !out->rgb_map || !out->acc_map || !out->depth_map || !p->packed)
+    return fail(ANR_E_ARG, "anr_render_fwd: NULL tensor");
+  for (int i = 0; i < 3; ++i)
+    if (f->pbw_dims[i] <= 0 || f->tbw_dims[i] <= 0) return fail(ANR_E_ARG, "anr_render_fwd: bad volume dims");
+  if (!f->A || !f->R || !f->Th || !f->pbw || !f->tbw || !f->pbounds || !f->tbounds || !f->latent_index)
+    return fail(ANR_E_ARG, "anr_render_fwd: NULL frame tensor");
+  const long np = (long)f->pbw_dims[0] * f->pbw_dims[1] * f->pbw_dims[2];
+  const long nt = (long)f->tbw_dims[0] * f->tbw_dims[1] * f->tbw_dims[2];
+  const Layout L = layout(n_rays, o->chunk, np, nt, out->raw == nullptr);
+  if (ws_bytes < L.total) return fail(ANR_E_WORKSPACE, "anr_render_fwd: workspace too small");
+
+  hipStream_t s = (hipStream_t)stream;
+  char* ws = (char*)workspace;
+  const int R = n_rays;
+  const long N = (long)R * 64;
+  const int nch = (R + o->chunk - 1) / o->chunk;
+  int* counts = (int*)(ws + L.counts);
+  float4* raw = out->raw ? (float4*)out->raw : (float4*)(ws + L.raw);
+
+  if (hipMemsetAsync(ws + L.counts, 0, 16, s) != hipSuccess ||
+      hipMemsetAsync(ws + L.chunk_min, 0xff, (size_t)nch * 8, s) != hipSuccess ||
+      hipMemsetAsync(ws + L.chunk_max, 0, (size_t)nch * 8, s) != hipSuccess)
+    return fail(ANR_E_HIP, "hipMemsetAsync failed");
+
+  // per-frame prep: 32-channel volumes + folded latent biases
+  PrepArgs pa{};
+  pa.pbw = f->pbw; pa.tbw = f->tbw;
+  pa.pbw32 = (float*)(ws + L.pbw32); pa.tbw32 = (float*)(ws + L.tbw32);
+  pa.np = (int)np; pa.nt = (int)nt;
+  pa.w_bw0 = p->t[28]; pa.b_bw0 = p->t[29]; pa.w_bw5 = p->t[38]; pa.b_bw5 = p->t[39];
+  pa.bw_latent = p->t[27]; pa.w_lat = p->t[21]; pa.b_lat = p->t[22]; pa.nf_latent = p->t[0];
+  pa.latent_index = f->latent_index;
+  pa.fold = (float*)(ws + L.fold);
+  const int nvb = (int)((np + nt + 7) / 8);
+  hipLaunchKernelGGL(k_prep, dim3(nvb + 1), dim3(256), 0, s, pa);
+  ANR_TRY(check_launch("k_prep"));
+
+  FrontArgs fa{};
+  fa.ray_o = ray_o; fa.ray_d = ray_d; fa.near_ = near_; fa.far_ = far_; fa.t_rand = o->t_rand;
+  fa.n_rays = R; fa.chunk = o->chunk;
+  fa.R = f->R; fa.Th = f->Th; fa.pbw = f->pbw; fa.pbounds = f->pbounds;
+  fa.X = f->pbw_dims[0]; fa.Y = f->pbw_dims[1]; fa.Z = f->pbw_dims[2];
+  fa.norm_th = o->norm_th;
+  fa.mask = (uint64_t*)(ws + L.mask);
+  fa.chunk_min = (uint64_t*)(ws + L.chunk_min);
+  fa.raw = raw;
+  hipLaunchKernelGGL(k_frontend, dim3((R + 3) / 4), dim3(256), 0, s, fa);
+  ANR_TRY(check_launch("k_frontend"));
+
+  CompactArgs ca{};
+  ca.n_rays = R; ca.chunk = o->chunk;
+  ca.mask = fa.mask; ca.chunk_min = fa.chunk_min;
+  ca.ray_off = (int*)(ws + L.ray_off);
+  ca.block_sum = (int*)(ws + L.block_sum);
+  ca.list = (int*)(ws + L.list);
+  const int nb = (R + 255) / 256;
+  hipLaunchKernelGGL(k_count, dim3(nb), dim3(256), 0, s, ca);
+  ANR_TRY(check_launch("k_count"));
+  hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, s, ca.block_sum, nb, counts);
+  ANR_TRY(check_launch("k_scan_blocks"));
+  hipLaunchKernelGGL(k_compact, dim3((R + 3) / 4), dim3(256), 0, s, ca);
+  ANR_TRY(check_launch("k_compact"));
+
+  MlpArgs ma{};
+  ma.wimg = (const unsigned char*)p->packed;
+  ma.bias = (const float*)((const unsigned char*)p->packed + weights_bytes());
+  ma.fold = pa.fold;
+  ma.A = f->A; ma.R = f->R; ma.Th = f->Th;
+  ma.pbw32 = pa.pbw32; ma.pbounds = f->pbounds; ma.tbw32 = pa.tbw32; ma.tbounds = f->tbounds;
+  ma.pX = f->pbw_dims[0]; ma.pY = f->pbw_dims[1]; ma.pZ = f->pbw_dims[2];
+  ma.tX = f->tbw_dims[0]; ma.tY = f->tbw_dims[1]; ma.tZ = f->tbw_dims[2];
+  ma.ray_o = ray_o; ma.ray_d = ray_d; ma.near_ = near_; ma.far_ = far_; ma.t_rand = o->t_rand;
+  ma.list = ca.list; ma.n_kept = counts;
+  ma.raw = raw;
+  ma.sigma = (float*)(ws + L.sigma);
+  ma.pbw_rows = (float*)(ws + L.pbw_rows);
+  ma.tbw_rows = (float*)(ws + L.tbw_rows);
+  const int lds = 2 * 8 * 5 * 1024 + 24 * 16 * 4;
+  if (!mlp_attr_set) {
+    if (hipFuncSetAttribute((const void*)k_mlp, hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
+      return fail(ANR_E_HIP, "hipFuncSetAttribute(k_mlp) failed");
+    mlp_attr_set = true;
+  }
+  const long max_tiles = (N + 127) / 128;
+  const int grid = (int)(max_tiles < num_cus() ? max_tiles : num_cus());
+  std::pair<hipEvent_t, hipEvent_t>* evp = nullptr;
+  if (g_prof.on) {
+    if (g_prof.used == g_prof.ev.size()) {
+      hipEvent_t a = nullptr, b = nullptr;
+      if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess)
+        return fail(ANR_E_HIP, "hipEventCreate failed");
+      g_prof.ev.emplace_back(a, b);
+    }
+    evp = &g_prof.ev[g_prof.used++];
+    if (hipEventRecord(evp->first, s) != hipSuccess) return fail(ANR_E_HIP, "hipEventRecord failed");
+  }
+  hipLaunchKernelGGL(k_mlp, dim3(grid), dim3(512), lds, s, ma);
+  ANR_TRY(check_launch("k_mlp"));
+  if (evp && hipEventRecord(evp->second, s) != hipSuccess) return fail(ANR_E_HIP, "hipEventRecord failed");
+
+  AlphaArgs aa{};
+  aa.n_rays = R; aa.chunk = o->chunk;
+  aa.ray_off = ca.ray_off; aa.n_kept = counts;
+  aa.sigma = ma.sigma;
+  aa.chunk_max = (uint64_t*)(ws + L.chunk_max);
+  aa.train_th = o->train_th;
+  aa.flags = (uint8_t*)(ws + L.flags);
+  aa.block_sum = (int*)(ws + L.block_sum2);
+  aa.out_row = (int*)(ws + L.out_row);
+  hipLaunchKernelGGL(k_chunk_argmax, dim3(nch, 16), dim3(256), 0, s, aa);
+  ANR_TRY(check_launch("k_chunk_argmax"));
+  const int nb2 = (int)((N + 1023) / 1024);
+  hipLaunchKernelGGL(k_flag_count, dim3(nb2), dim3(256), 0, s, aa);
+  ANR_TRY(check_launch("k_flag_count"));
+  hipLaunchKernelGGL(k_flag_force, dim3((nch + 255) / 256), dim3(256), 0, s, aa, nch);
+  ANR_TRY(check_launch("k_flag_force"));
+  hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, s, aa.block_sum, nb2, counts + 1);
+  ANR_TRY(check_launch("k_scan_blocks(alpha)"));
+  hipLaunchKernelGGL(k_flag_scatter, dim3(nb2), dim3(256), 0, s, aa);
+  ANR_TRY(check_launch("k_flag_scatter"));
+
+  CompositeArgs co{};
+  co.raw = raw; co.near_ = near_; co.far_ = far_; co.t_rand = o->t_rand; co.n_rays = R;
+  co.rgb = out->rgb_map; co.acc = out->acc_map; co.depth = out->depth_map; co.weights = nullptr;
+  hipLaunchKernelGGL(k_composite, dim3((R + 3) / 4), dim3(256), 0, s, co);
+  return check_launch("k_composite");
+}
+
+int anr_profile_enable(int on) {
+  g_prof.on = on != 0;
+  return ANR_OK;
+}
+
+int anr_profile_read(double* mlp_ms, int* launches) {
+  double tot = 0.0;
+  for (size_t i = 0; i < g_prof.used; ++i) {
+    if (hipEventSynchronize(g_prof.ev[i].second) != hipSuccess) return fail(ANR_E_HIP, "hipEventSynchronize failed");
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, g_prof.ev[i].first, g_prof.ev[i].second) != hipSuccess)
+      return fail(ANR_E_HIP, "hipEventElapsedTime failed");
+    tot += ms;
+  }
+  if (mlp_ms) *mlp_ms = tot;
+  if (launches) *launches = (int)g_prof.used;
+  g_prof.used = 0;
+  return ANR_OK;
+}
+
+int anr_render_bw_rows(const void* workspace, int n_rays, float* pbw, float* tbw, void* stream) {
+  if (!workspace || n_rays <= 0 || !pbw || !tbw) return fail(ANR_E_ARG, "anr_render_bw_rows: bad arguments");
+  const Layout L = layout(n_rays, 1, 0, 0, false);
+  const char* ws = (const char*)workspace;
+  const long N = (long)n_rays * 64;
+  const int grid = (int)((N * 6 + 255) / 256);
+  hipLaunchKernelGGL(k_gather_rows, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const int*)(ws + L.out_row),
+                     (const int*)(ws + L.counts), (const float4*)(ws + L.pbw_rows), (const float4*)(ws + L.tbw_rows),
+                     (float4*)pbw, (float4*)tbw);
+  return check_launch("k_gather_rows");
+}
+
+}  // extern "C"

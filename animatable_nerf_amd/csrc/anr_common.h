@@ -1,0 +1,132 @@
+// anr_common.h — shared device helpers for the Animatable-NeRF hot path on gfx950 (CDNA4).
+//
+// Everything here that feeds the sample keep-mask (linspace bits, z, world->pose, the trilinear
+// volume lookup) reproduces the reference's fp32 operation order exactly and must be compiled
+// without FP contraction (each TU that uses it sets `#pragma clang fp contract(off)` where needed).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define ANR_WAVE 64
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+namespace anr {
+
+// torch.linspace(start=0, end=1, steps=n) on CPU: symmetric formula (tpose_renderer.py:26)
+__device__ __forceinline__ float linspace01(int i, int n) {
+  const float step = 1.0f / (float)(n - 1);
+  const int half = n / 2;
+  return (i < half) ? fmaf(step, (float)i, 0.0f) : fmaf(-step, (float)(n - 1 - i), 1.0f);
+}
+
+// One trilinear lookup in the layout of blend_utils.py:119-149 / ATen grid_sampler_3d (CPU):
+// volume memory (X,Y,Z,C) viewed as (C, D=X, H=Y, W=Z); grid = normalised (z, y, x).
+struct TriCell {
+  int base[8];     // voxel offsets (in voxels) of the 8 corners, -1 if out of bounds
+  float w[8];      // tnw, tne, tsw, tse, bnw, bne, bsw, bse
+};
+
+__device__ __forceinline__ float grid_src(float g, int size) {
+#pragma clang fp contract(off)
+  float c = ((g + 1.0f) / 2.0f) * (float)(size - 1);
+  return fminf((float)(size - 1), fmaxf(c, 0.0f));
+}
+
+// p: point in the volume's frame; lo/hi: bounds (2,3); dims X,Y,Z.
+__device__ __forceinline__ void tri_cell(const float p[3], const float lo[3], const float hi[3],
+                                         int X, int Y, int Z, TriCell& t) {
+#pragma clang fp contract(off)
+  float g[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const float ext = hi[c] - lo[c];
+    float v = (p[c] - lo[c]) / ext;
+    g[c] = v * 2.0f - 1.0f;
+  }
+  const float ix = grid_src(g[2], Z);
+  const float iy = grid_src(g[1], Y);
+  const float iz = grid_src(g[0], X);
+  const int x0 = (int)floorf(ix), y0 = (int)floorf(iy), z0 = (int)floorf(iz);
+  const int x1 = x0 + 1, y1 = y0 + 1, z1 = z0 + 1;
+  const float fx0 = (float)x0, fy0 = (float)y0, fz0 = (float)z0;
+  const float fx1 = (float)x1, fy1 = (float)y1, fz1 = (float)z1;
+  const float ax = fx1 - ix, bx = ix - fx0, ay = fy1 - iy, by = iy - fy0, az = fz1 - iz, bz = iz - fz0;
+  t.w[0] = (ax * ay) * az;  t.w[1] = (bx * ay) * az;
+  t.w[2] = (ax * by) * az;  t.w[3] = (bx * by) * az;
+  t.w[4] = (ax * ay) * bz;  t.w[5] = (bx * ay) * bz;
+  t.w[6] = (ax * by) * bz;  t.w[7] = (bx * by) * bz;
+  const int xs[2] = {x0, x1}, ys[2] = {y0, y1}, zs[2] = {z0, z1};
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int cx = xs[k & 1], cy = ys[(k >> 1) & 1], cz = zs[k >> 2];
+    const bool ok = cx >= 0 && cx < Z && cy >= 0 && cy < Y && cz >= 0 && cz < X;
+    t.base[k] = ok ? ((cz * Y + cy) * Z + cx) : -1;
+  }
+}
+
+// Exact single-channel lookup (reference accumulation order, rounded after each add).
+__device__ __forceinline__ float tri_channel(const float* __restrict__ vol, int C, int ch, const TriCell& t) {
+#pragma clang fp contract(off)
+  float acc = 0.0f;
+#pragma unroll
+  for (int k = 0; k < 8; ++k)
+    if (t.base[k] >= 0) acc = acc + vol[(size_t)t.base[k] * C + ch] * t.w[k];
+  return acc;
+}
+
+// (x - Th) @ R  (blend_utils.py:6-16), no contraction.
+__device__ __forceinline__ void world_to_pose(const float x[3], const float* R, const float* Th, float out[3]) {
+#pragma clang fp contract(off)
+  const float d0 = x[0] - Th[0], d1 = x[1] - Th[1], d2 = x[2] - Th[2];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) out[j] = (d0 * R[0 * 3 + j] + d1 * R[1 * 3 + j]) + d2 * R[2 * 3 + j];
+}
+
+// Positional-encoding feature f of gamma(x) (embedder.py:5-54): [x, sin(2^0 x), cos(2^0 x), ...]
+__device__ __forceinline__ float embed_feature(const float x[3], int f, int nfreq) {
+  if (f < 3) return x[f];
+  const int g = f - 3;
+  const int freq = g / 6;
+  if (freq >= nfreq) return 0.0f;
+  const int w = g - freq * 6;
+  const int comp = (w >= 3) ? w - 3 : w;
+  const float v = x[comp] * (float)(1 << freq);
+  return (w >= 3) ? cosf(v) : sinf(v);
+}
+
+// ------------------------------------------------------------------------------------------
+// A2/A3: z of sample s (perturbed when t_rand != NULL), identical ops to tpose_renderer.py:26-36
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ float z_base(float nr, float fr, int i, int n) {
+#pragma clang fp contract(off)
+  const float t = linspace01(i, n);
+  const float a = nr * (1.0f - t);
+  const float b = fr * t;
+  return a + b;
+}
+
+__device__ __forceinline__ float z_sample(float nr, float fr, const float* __restrict__ trow, int s, int n) {
+#pragma clang fp contract(off)
+  if (trow == nullptr) return z_base(nr, fr, s, n);
+  float upper, lower;
+  if (s < n - 1) upper = 0.5f * (z_base(nr, fr, s + 1, n) + z_base(nr, fr, s, n));
+  else upper = z_base(nr, fr, n - 1, n);
+  if (s > 0) lower = 0.5f * (z_base(nr, fr, s, n) + z_base(nr, fr, s - 1, n));
+  else lower = z_base(nr, fr, 0, n);
+  return lower + (upper - lower) * trow[s];
+}
+
+__device__ __forceinline__ void sample_point(const float* __restrict__ ray_o, const float* __restrict__ ray_d, const float* __restrict__ near_,
+                             const float* __restrict__ far_, const float* __restrict__ t_rand, int ray, int s, int n,
+                             float& z, float& dist, float pts[3]) {
+#pragma clang fp contract(off)
+  const float nr = near_[ray], fr = far_[ray];
+  const float* trow = t_rand ? t_rand + (size_t)ray * n : nullptr;
+  z = z_sample(nr, fr, trow, s, n);
+  if (s < n - 1) dist = z_sample(nr, fr, trow, s + 1, n) - z;
+  else dist = z - z_sample(nr, fr, trow, s - 1, n);
+#pragma unroll
+  for (int c = 0; c < 3; ++c) pts[c] = ray_o[3 * ray + c] + ray_d[3 * ray + c] * z;
+}
+
+}  // namespace anr

@@ -1,0 +1,95 @@
+// anr_kernels.h — kernel argument blocks and launch declarations (internal to libaninerf_hip.so).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace anr {
+
+struct FrontArgs {
+  const float *ray_o, *ray_d, *near_, *far_, *t_rand;
+  int n_rays, chunk;
+  const float *R, *Th, *pbw, *pbounds;
+  int X, Y, Z;
+  float norm_th;
+  uint64_t* mask;        // (R) keep ballots
+  uint64_t* chunk_min;   // (nchunks) argmin keys, preset to ~0
+  float4* raw;           // (R*64) zeroed at non-kept samples (may be NULL)
+};
+
+struct CompactArgs {
+  int n_rays, chunk;
+  uint64_t* mask;
+  const uint64_t* chunk_min;
+  int* ray_off;    // (R+1) exclusive offsets (global after k_compact)
+  int* block_sum;  // (ceil(R/256))
+  int* list;       // (R*64) kept point ids (ray*64+sample)
+};
+
+struct AlphaArgs {
+  int n_rays, chunk;
+  const int* ray_off;
+  const int* n_kept;
+  const float* sigma;    // (n') sigma' in compact order
+  uint64_t* chunk_max;   // (nchunks) preset to 0
+  float train_th;
+  uint8_t* flags;        // (n')
+  int* block_sum;        // (ceil(n'/1024))
+  int* out_row;          // (n') output row or -1
+};
+
+struct CompositeArgs {
+  const float4* raw;
+  const float *near_, *far_, *t_rand;
+  int n_rays;
+  float *rgb, *acc, *depth, *weights;
+};
+
+// the fused deform + NeRF MLP kernel (anr_mlp.hip)
+struct MlpArgs {
+  const unsigned char* wimg;  // packed weight image (anr_layers.h)
+  const float* bias;          // packed bias section
+  const float* fold;          // per-frame folded biases: bw0[2][256], bw5[2][256], nlat[256]
+  const float *A, *R, *Th;
+  const float *pbw32, *pbounds, *tbw32, *tbounds;
+  int pX, pY, pZ, tX, tY, tZ;
+  const float *ray_o, *ray_d, *near_, *far_, *t_rand;
+  const int* list;
+  const int* n_kept;
+  float4* raw;
+  float* sigma;      // (n') sigma' (after the T-pose bbox mask)
+  float* pbw_rows;   // (n', 24)
+  float* tbw_rows;   // (n', 24)
+};
+
+struct PrepArgs {
+  const float *pbw, *tbw;  // (X,Y,Z,25)
+  float *pbw32, *tbw32;    // (X,Y,Z,32)
+  int np, nt;              // voxel counts
+  const float *w_bw0, *b_bw0, *w_bw5, *b_bw5, *bw_latent;
+  const float *w_lat, *b_lat, *nf_latent;
+  const int64_t* latent_index;
+  float* fold;
+};
+
+__global__ void k_near_far(const float*, const float*, int, const float*, uint8_t*, float*, float*);
+__global__ void k_frontend(FrontArgs a);
+__global__ void k_count(CompactArgs a);
+__global__ void k_scan_blocks(int* sums, int nb, int* total_out);
+__global__ void k_compact(CompactArgs a);
+__global__ void k_chunk_argmax(AlphaArgs a);
+__global__ void k_flag_count(AlphaArgs a);
+__global__ void k_flag_force(AlphaArgs a, int nchunks);
+__global__ void k_flag_scatter(AlphaArgs a);
+__global__ void k_gather_rows(const int*, const int*, const float4*, const float4*, float4*, float4*);
+__global__ void k_composite(CompositeArgs a);
+__global__ void k_prep(PrepArgs a);
+__global__ void k_mlp(MlpArgs a);
+
+struct PackArgs {
+  const float* t[46];
+  unsigned char* out;
+};
+__global__ void k_pack_weights(PackArgs a);
+__global__ void k_pack_bias(PackArgs a);
+
+}  // namespace anr

@@ -1,0 +1,124 @@
+// anr_layers.h — the MLP layer program shared by the weight packer (anr_pack) and the fused kernel.
+//
+// MFMA tiling (v_mfma_f32_16x16x4_f32, exact fp32):  D[i][j] = sum_k A[i][k] B[k][j]
+//   i = output neuron (16 per "out-block" ob), j = point (16 per wave), k = 4 inputs per "k-step".
+//   A (weights) lane l: A[l&15][l>>4];  B (activations) lane l: B[l>>4][l&15];
+//   C/D lane l: point l&15, neurons 4*(l>>4)+r in register r (r = 0..3).
+// So a layer's accumulators are directly the next layer's B operand: k-step (ob', r) feeds input
+// neurons ob'*16 + 4g + r in k-slot g = l>>4. Gamma features come as k-step s -> feature 4s+g.
+//
+// Weight image: for every layer, k-steps in program order; per k-step C = ceil(OB/4) chunks of
+// [64 lanes][4 floats] (lane reads one float4 per chunk = ds_read_b128, conflict-free), the float
+// (ob%4) of chunk ob/4 being W[ob*16 + (l&15)][col(kstep, l>>4)] (0 outside the tensor).
+// Layers are grouped into "slices" of 8 k-steps, the unit staged HBM->LDS.
+#pragma once
+
+namespace anr {
+
+enum SrcKind { SRC_EMB = 0, SRC_ACT = 1, SRC_VEMB = 2 };
+
+// A segment of a layer's K dimension: `ksteps` k-steps from one source; `col0` = first weight column.
+struct Seg { int kind; int ksteps; int col0; };
+
+struct LayerDesc {
+  int tensor_w;   // index into anr_params.t of the weight (out, in, 1)
+  int tensor_b;   // index of the bias
+  int tensor_w2;  // second weight stacked as extra out-blocks (alpha_fc beside feature_fc), or -1
+  int tensor_b2;
+  int nout;       // output neurons of tensor_w
+  int nout2;      // output neurons of tensor_w2 (0 if none)
+  int in_ch;      // columns of tensor_w (row stride)
+  int ob;         // out-blocks of 16 (incl. the tensor_w2 blocks)
+  int nseg;
+  Seg seg[2];
+};
+
+#define ANR_KSLICE 8  // k-steps per staged slice
+
+// BW MLP (tpose_nerf_network.py:21-29, 55-77): gamma(63) || latent(128) -> 8 x 256 (skip at 4) -> 24.
+// Latent columns (63..190 of layers 0 and 5) are folded into a per-frame bias.
+// NeRF (TPoseHuman :226-239, 252-275).
+#define ANR_NUM_LAYERS 19
+#define ANR_BW_LAYERS 9
+
+__host__ __device__ constexpr LayerDesc layer_desc(int i) {
+  // clang-format off
+  return i == 0  ? LayerDesc{28, 29, -1, -1, 256, 0, 191, 16, 1, {{SRC_EMB, 16, 0}, {0, 0, 0}}}
+       : i == 1  ? LayerDesc{30, 31, -1, -1, 256, 0, 256, 16, 1, {{SRC_ACT, 64, 0}, {0, 0, 0}}}
+       : i == 2  ? LayerDesc{32, 33, -1, -1, 256, 0, 256, 16, 1, {{SRC_ACT, 64, 0}, {0, 0, 0}}}
+       : i == 3  ? LayerDesc{34, 35, -1, -1, 256, 0, 256, 16, 1, {{SRC_ACT, 64, 0}, {0, 0, 0}}}
+       : i == 4  ? LayerDesc{36, 37, -1, -1, 256, 0, 256, 16, 1, {{SRC_ACT, 64, 0}, {0, 0, 0}}}
+       : i == 5  ? LayerDesc{38, 39, -1, -1, 256, 0, 447, 16, 2, {{SRC_EMB, 16, 0}, {SRC_ACT, 64, 191}}}
+       : i == 6  ? LayerDesc{40, 41, -1, -1, 256, 0, 256, 16, 1, {{SRC_ACT, 64, 0}, {0, 0, 0}}}
+       : i == 7  ? LayerDesc{42, 43, -1, -1, 256, 0, 256, 16, 1, {{SRC_ACT, 64, 0}, {0, 0, 0}}}
+       : i == 8  ? LayerDesc{44, 45, -1, -1, 24, 0, 256, 2, 1, {{SRC_ACT, 64, 0}, {0, 0, 0}}}
+       : i == 9  ? LayerDesc{1, 2, -1, -1, 256, 0, 63, 16, 1, {{SRC_EMB, 16, 0}, {0, 0, 0}}}
+       : i == 10 ? LayerDesc{3, 4, -1, -1, 256, 0, 256, 16, 1, {{SRC_ACT, 64, 0}, {0, 0, 0}}}
+       : i == 11 ? LayerDesc{5, 6, -1, -1, 256, 0, 256, 16, 1, {{SRC_ACT, 64, 0}, {0, 0, 0}}}
+       : i == 12 ? LayerDesc{7, 8, -1, -1, 256, 0, 256, 16, 1, {{SRC_ACT, 64, 0}, {0, 0, 0}}}
+       : i == 13 ? LayerDesc{9, 10, -1, -1, 256, 0, 256, 16, 1, {{SRC_ACT, 64, 0}, {0, 0, 0}}}
+       : i == 14 ? LayerDesc{11, 12, -1, -1, 256, 0, 319, 16, 2, {{SRC_EMB, 16, 0}, {SRC_ACT, 64, 63}}}
+       : i == 15 ? LayerDesc{13, 14, -1, -1, 256, 0, 256, 16, 1, {{SRC_ACT, 64, 0}, {0, 0, 0}}}
+       : i == 16 ? LayerDesc{15, 16, -1, -1, 256, 0, 256, 16, 1, {{SRC_ACT, 64, 0}, {0, 0, 0}}}
+       // feature_fc (16 blocks) + alpha_fc (block 16)
+       : i == 17 ? LayerDesc{19, 20, 17, 18, 256, 1, 256, 17, 1, {{SRC_ACT, 64, 0}, {0, 0, 0}}}
+       // latent_fc: feature part only (cols 0..255); nf_latent part folded into the bias
+       : i == 18 ? LayerDesc{21, 22, -1, -1, 256, 0, 384, 16, 1, {{SRC_ACT, 64, 0}, {0, 0, 0}}}
+       : LayerDesc{0, 0, -1, -1, 0, 0, 0, 0, 0, {{0, 0, 0}, {0, 0, 0}}};
+  // clang-format on
+}
+// view_fc (128, 283): latent_fc out (64 ksteps) || gamma(dir) 27 (8 ksteps, padded)
+// rgb_fc (3, 128): view out (32 ksteps)
+#define ANR_L_VIEW 19
+#define ANR_L_RGB 20
+#define ANR_NUM_LAYERS_ALL 21
+
+__host__ __device__ constexpr LayerDesc layer_desc_all(int i) {
+  return i < ANR_NUM_LAYERS ? layer_desc(i)
+       : i == ANR_L_VIEW ? LayerDesc{23, 24, -1, -1, 128, 0, 283, 8, 2, {{SRC_ACT, 64, 0}, {SRC_VEMB, 8, 256}}}
+       : i == ANR_L_RGB  ? LayerDesc{25, 26, -1, -1, 3, 0, 128, 1, 1, {{SRC_ACT, 32, 0}, {0, 0, 0}}}
+       : LayerDesc{0, 0, -1, -1, 0, 0, 0, 0, 0, {{0, 0, 0}, {0, 0, 0}}};
+}
+
+__host__ __device__ constexpr int layer_chunks(int i) { return (layer_desc_all(i).ob + 3) / 4; }
+__host__ __device__ constexpr int layer_ksteps(int i) {
+  return layer_desc_all(i).seg[0].ksteps + (layer_desc_all(i).nseg > 1 ? layer_desc_all(i).seg[1].ksteps : 0);
+}
+// bytes of a layer's weight image
+__host__ __device__ constexpr int layer_bytes(int i) { return layer_ksteps(i) * layer_chunks(i) * 1024; }
+__host__ __device__ constexpr int layer_offset(int i) {
+  int o = 0;
+  for (int k = 0; k < i; ++k) o += layer_bytes(k);
+  return o;
+}
+__host__ __device__ constexpr int weights_bytes() { return layer_offset(ANR_NUM_LAYERS_ALL); }
+
+// bias section (floats), padded to ob*16 per layer, after the weight image
+__host__ __device__ constexpr int layer_bias_floats(int i) { return layer_desc_all(i).ob * 16; }
+__host__ __device__ constexpr int bias_offset(int i) {
+  int o = 0;
+  for (int k = 0; k < i; ++k) o += layer_bias_floats(k);
+  return o;
+}
+template <int L> inline constexpr int kBiasOff = bias_offset(L);
+__host__ __device__ constexpr int bias_floats() { return bias_offset(ANR_NUM_LAYERS_ALL); }
+__host__ __device__ constexpr int packed_bytes() { return weights_bytes() + bias_floats() * 4; }
+
+// weight column fed by k-step t, k-slot g (-1 = padding)
+__host__ __device__ inline int layer_col(const LayerDesc& d, int t, int g) {
+  int s = 0;
+  for (; s < d.nseg; ++s) {
+    if (t < d.seg[s].ksteps) break;
+    t -= d.seg[s].ksteps;
+  }
+  const Seg sg = d.seg[s];
+  if (sg.kind == SRC_ACT) {
+    const int ob = t >> 2, r = t & 3;
+    return sg.col0 + ob * 16 + 4 * g + r;
+  }
+  const int f = 4 * t + g;  // gamma feature
+  const int nf = (sg.kind == SRC_EMB) ? 63 : 27;
+  return f < nf ? sg.col0 + f : -1;
+}
+
+}  // namespace anr

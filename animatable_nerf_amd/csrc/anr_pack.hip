@@ -1,0 +1,92 @@
+// anr_pack.hip — weight-image packing (per weight version) and per-frame preparation.
+//
+//   k_pack_weights  state_dict tensors -> the LDS-image order of anr_layers.h (one float per thread)
+//   k_pack_bias     biases padded per layer (feature_fc || alpha_fc stacked like their weights)
+//   k_prep          per render call: (X,Y,Z,25) volumes -> 32-channel float4-aligned copies, and the
+//                   latent columns of bw_linears.0/.5 and latent_fc folded into per-frame biases
+//                   (tpose_nerf_network.py:40-53 feature = [gamma(x), latent]; :264-267)
+#include "anr_common.h"
+#include "anr_kernels.h"
+#include "anr_layers.h"
+
+namespace anr {
+
+__global__ void k_pack_weights(PackArgs a) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;  // float index into the weight image
+  if (e >= weights_bytes() / 4) return;
+  int L = 0;
+  while (L + 1 < ANR_NUM_LAYERS_ALL && e >= layer_offset(L + 1) / 4) ++L;
+  const LayerDesc d = layer_desc_all(L);
+  const int C = layer_chunks(L);
+  const int local = e - layer_offset(L) / 4;
+  const int t = local / (C * 256);
+  const int rem = local - t * C * 256;
+  const int c = rem / 256;
+  const int l = (rem & 255) >> 2;
+  const int j = rem & 3;
+  const int ob = c * 4 + j;
+  const int col = layer_col(d, t, l >> 4);
+  float v = 0.0f;
+  const int main_ob = (d.nout + 15) / 16;
+  if (ob < d.ob && col >= 0) {
+    if (ob < main_ob) {
+      const int i = ob * 16 + (l & 15);
+      if (i < d.nout) v = a.t[d.tensor_w][(size_t)i * d.in_ch + col];
+    } else if (d.tensor_w2 >= 0) {
+      const int i2 = (ob - main_ob) * 16 + (l & 15);
+      if (i2 < d.nout2) v = a.t[d.tensor_w2][(size_t)i2 * d.in_ch + col];
+    }
+  }
+  ((float*)a.out)[e] = v;
+}
+
+__global__ void k_pack_bias(PackArgs a) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= bias_floats()) return;
+  int L = 0;
+  while (L + 1 < ANR_NUM_LAYERS_ALL && e >= bias_offset(L + 1)) ++L;
+  const LayerDesc d = layer_desc_all(L);
+  const int n = e - bias_offset(L);
+  const int main_n = ((d.nout + 15) / 16) * 16;
+  float v = 0.0f;
+  if (n < d.nout) v = a.t[d.tensor_b][n];
+  else if (d.tensor_w2 >= 0 && n >= main_n && n - main_n < d.nout2) v = a.t[d.tensor_b2][n - main_n];
+  ((float*)(a.out + weights_bytes()))[e] = v;
+}
+
+// grid: blocks [0, nvox_blocks) repack volumes; block 'fold' computes the five folded biases
+__global__ __launch_bounds__(256) void k_prep(PrepArgs a) {
+  const int nvb = (a.np + a.nt + 7) / 8;  // 8 voxels (x 32 channels) per block
+  if ((int)blockIdx.x < nvb) {
+    const int v = blockIdx.x * 8 + (threadIdx.x >> 5);
+    const int c = threadIdx.x & 31;
+    if (v < a.np) {
+      a.pbw32[(size_t)v * 32 + c] = c < 25 ? a.pbw[(size_t)v * 25 + c] : 0.0f;
+    } else if (v < a.np + a.nt) {
+      const int u = v - a.np;
+      a.tbw32[(size_t)u * 32 + c] = c < 25 ? a.tbw[(size_t)u * 25 + c] : 0.0f;
+    }
+    return;
+  }
+  // folded biases: which = 0,1 (bw0 pose/tpose), 2,3 (bw5 pose/tpose), 4 (latent_fc)
+  const int li = (int)a.latent_index[0];
+  for (int k = threadIdx.x; k < 5 * 256; k += blockDim.x) {
+    const int which = k >> 8, nn = k & 255;
+    float acc;
+    if (which < 4) {
+      const int row = (which & 1) ? 0 : li + 1;  // pose: latent_index + 1; T-pose: 0
+      const float* lat = a.bw_latent + (size_t)row * 128;
+      const float* W = which < 2 ? a.w_bw0 : a.w_bw5;
+      const int ld = which < 2 ? 191 : 447;
+      acc = which < 2 ? a.b_bw0[nn] : a.b_bw5[nn];
+      for (int q = 0; q < 128; ++q) acc = fmaf(W[(size_t)nn * ld + 63 + q], lat[q], acc);
+    } else {
+      const float* lat = a.nf_latent + (size_t)li * 128;
+      acc = a.b_lat[nn];
+      for (int q = 0; q < 128; ++q) acc = fmaf(a.w_lat[(size_t)nn * 384 + 256 + q], lat[q], acc);
+    }
+    a.fold[k] = acc;
+  }
+}
+
+}  // namespace anr

@@ -1,0 +1,173 @@
+"""Seeded synthetic Animatable-NeRF scene and deterministic weight recipe.
+
+The licensed H36M / ZJU-MoCap data and the pretrained checkpoints are not available offline,
+so every test, the golden generator and ``bench.py`` use this scene. Both the reference run
+(``oracle/gen_goldens.py``, this container only) and the HIP path draw it from here, so the
+same seed gives the same bytes on both sides.
+
+Scene (all numpy, PCG64):
+  * 6,890 "vertices" = Gaussian directions normalised to unit length (seed 0), scaled to an
+    ellipsoid with semi-axes (0.25, 0.85, 0.15) m;
+  * 24 joints ~ U(+-(0.2, 0.7, 0.1)) from the same generator; SMPL kinematic tree ``PARENTS``;
+  * skin weights exp(-d/0.05) over the vertex->joint distance, normalised per vertex;
+  * blend-weight volume laid out like ``tools/custom_dataset/prepare_blend_weights.py:156-209``:
+    an ``ij`` meshgrid with ``vsize`` spacing over the vertex bounds +-0.05, channels 0-23 = skin
+    weights of the nearest vertex, channel 24 = distance to that vertex, shape (X, Y, Z, 25) f32;
+  * pose = axis-angles N(0, 0.1^2) (seed 1, root zero) -> A (24,4,4) by the kinematic chain of
+    ``lib/utils/if_nerf/if_nerf_data_utils.py:414-458``; R = I, Th = 0, so world = pose space;
+  * bounds via ``get_bounds`` (``if_nerf_data_utils.py:566-579``): vertex min/max +- box_padding.
+
+Rays ("box" generator, seed 2): origin (0, 0, 3), targets U(pbounds), unit directions, then the
+float64 near/far slab test of A14 (``if_nerf_data_utils.py:156-196``).
+"""
+import numpy as np
+
+PARENTS = np.array([-1, 0, 0, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 9, 9, 12, 13, 14, 16, 17, 18, 19, 20, 21],
+                   dtype=np.int64)
+SEMI_AXES = np.array([0.25, 0.85, 0.15])
+JOINT_RANGE = np.array([0.2, 0.7, 0.1])
+BOX_PADDING = 0.05
+
+
+def batch_rodrigues(poses):
+    """Axis-angle (N,3) -> rotation matrices (N,3,3); same formula as
+    ``if_nerf_data_utils.py:392-411`` (angle = |poses + 1e-8|)."""
+    n = poses.shape[0]
+    angle = np.linalg.norm(poses + 1e-8, axis=1, keepdims=True)
+    axis = poses / angle
+    c = np.cos(angle)[:, None]
+    s = np.sin(angle)[:, None]
+    rx, ry, rz = axis[:, 0:1], axis[:, 1:2], axis[:, 2:3]
+    z = np.zeros((n, 1))
+    K = np.concatenate([z, -rz, ry, rz, z, -rx, -ry, rx, z], axis=1).reshape(n, 3, 3)
+    return np.eye(3)[None] + s * K + (1 - c) * np.matmul(K, K)
+
+
+def rigid_transformation(poses, joints, parents):
+    """24-joint chain -> A = G(pose, j_rel) G(0, j)^-1 as (24,4,4) f32.
+
+    Restates ``get_rigid_transformation`` (``if_nerf_data_utils.py:414-458``) in float64 and
+    casts once at the end, as the reference does.
+    """
+    rot = batch_rodrigues(poses)
+    rel = joints.copy()
+    rel[1:] -= joints[parents[1:]]
+    local = np.zeros((24, 4, 4))
+    local[:, :3, :3] = rot
+    local[:, :3, 3] = rel
+    local[:, 3, 3] = 1.0
+    chain = [local[0]]
+    for i in range(1, 24):
+        chain.append(np.dot(chain[parents[i]], local[i]))
+    G = np.stack(chain, axis=0)
+    jh = np.concatenate([joints, np.zeros((24, 1))], axis=1)
+    G[..., 3] = G[..., 3] - np.sum(G * jh[:, None], axis=2)
+    return G.astype(np.float32)
+
+
+def get_bounds(xyz, box_padding=BOX_PADDING):
+    lo = np.min(xyz, axis=0) - box_padding
+    hi = np.max(xyz, axis=0) + box_padding
+    return np.stack([lo, hi], axis=0).astype(np.float32)
+
+
+def _nearest_vertex(pts, verts, block=4096):
+    idx = np.empty(len(pts), dtype=np.int64)
+    dist = np.empty(len(pts), dtype=np.float64)
+    v2 = np.sum(verts * verts, axis=1)
+    for s in range(0, len(pts), block):
+        p = pts[s:s + block]
+        d2 = np.sum(p * p, axis=1)[:, None] - 2.0 * p @ verts.T + v2[None]
+        j = np.argmin(d2, axis=1)
+        idx[s:s + block] = j
+        dist[s:s + block] = np.linalg.norm(p - verts[j], axis=1)
+    return idx, dist
+
+
+def blend_weight_volume(verts, skin, vsize):
+    """(X,Y,Z,25) f32 volume over verts bounds +-0.05 (``prepare_blend_weights.py:156-209``)."""
+    lo = verts.min(axis=0) - 0.05
+    hi = verts.max(axis=0) + 0.05
+    axes = [np.arange(lo[i], hi[i] + vsize, vsize) for i in range(3)]
+    grid = np.stack(np.meshgrid(*axes, indexing='ij'), axis=-1)
+    sh = grid.shape[:3]
+    idx, dist = _nearest_vertex(grid.reshape(-1, 3), verts)
+    vol = np.concatenate([skin[idx], dist[:, None]], axis=1)
+    return vol.reshape(*sh, 25).astype(np.float32)
+
+
+class Scene:
+    """One frame of the synthetic subject; ``batch_arrays`` gives the collated batch keys."""
+
+    def __init__(self, vsize=0.025, pose_scale=0.1, seed=0):
+        rng = np.random.Generator(np.random.PCG64(seed))
+        d = rng.standard_normal((6890, 3))
+        d /= np.linalg.norm(d, axis=1, keepdims=True)
+        self.verts = (d * SEMI_AXES).astype(np.float32)
+        self.joints = rng.uniform(-JOINT_RANGE, JOINT_RANGE, size=(24, 3)).astype(np.float32)
+        dj = np.linalg.norm(self.verts[:, None].astype(np.float64) - self.joints[None], axis=2)
+        w = np.exp(-dj / 0.05)
+        self.skin = (w / w.sum(axis=1, keepdims=True)).astype(np.float32)
+        self.volume = blend_weight_volume(self.verts.astype(np.float64), self.skin, vsize)
+        prng = np.random.Generator(np.random.PCG64(seed + 1))
+        poses = prng.normal(0.0, pose_scale, size=(24, 3))
+        poses[0] = 0.0
+        self.poses = poses
+        self.A = rigid_transformation(poses, self.joints, PARENTS)
+        self.bounds = get_bounds(self.verts)
+        self.R = np.eye(3, dtype=np.float32)
+        self.Th = np.zeros(3, dtype=np.float32)
+
+    def box_rays(self, n, seed=2, origin=(0.0, 0.0, 3.0)):
+        """n rays from ``origin`` towards U(bounds) targets; unit f32 directions."""
+        rng = np.random.Generator(np.random.PCG64(seed))
+        tgt = rng.uniform(self.bounds[0].astype(np.float64), self.bounds[1].astype(np.float64), size=(n, 3))
+        o = np.broadcast_to(np.asarray(origin, dtype=np.float64), (n, 3))
+        d = tgt - o
+        d /= np.linalg.norm(d, axis=1, keepdims=True)
+        return o.astype(np.float32).copy(), d.astype(np.float32)
+
+    def batch_arrays(self, ray_o, ray_d, near, far, latent_index=0, rgb=None):
+        """Collated (batch-dim 1) numpy batch with the keys of ``tpose_dataset.py:236-277``."""
+        R = ray_o.shape[0]
+        if rgb is None:
+            rgb = np.zeros((R, 3), np.float32)
+        return {
+            'ray_o': ray_o[None].astype(np.float32), 'ray_d': ray_d[None].astype(np.float32),
+            'near': near[None].astype(np.float32), 'far': far[None].astype(np.float32),
+            'occupancy': np.ones((1, R), np.uint8), 'mask_at_box': np.ones((1, R), np.bool_),
+            'rgb': rgb[None].astype(np.float32),
+            'A': self.A[None], 'big_A': self.A[None],
+            'pbw': self.volume[None], 'tbw': self.volume[None],
+            'pbounds': self.bounds[None], 'wbounds': self.bounds[None], 'tbounds': self.bounds[None],
+            'R': self.R[None], 'Th': self.Th[None],
+            'H': np.array([0]), 'W': np.array([0]),
+            'latent_index': np.array([latent_index]), 'bw_latent_index': np.array([latent_index]),
+            'frame_index': np.array([0]), 'cam_ind': np.array([0]),
+        }
+
+
+def init_state_dict(shapes, seed=1234, alpha_bias=3.0):
+    """Deterministic weights for a state_dict given {name: shape} (insertion order matters).
+
+    Per tensor a PCG64 stream seeded with (seed, index): Conv1d weights and biases U(+-1/sqrt(fan_in))
+    (PyTorch's default Conv1d init bound), embeddings N(0,1); ``tpose_human.alpha_fc.bias`` = +3 so
+    densities are non-trivial.
+    """
+    out = {}
+    fan_in = {}
+    for name, shape in shapes.items():
+        if name.endswith('.weight') and len(shape) == 3:
+            fan_in[name[:-len('.weight')]] = shape[1] * shape[2]
+    for i, (name, shape) in enumerate(shapes.items()):
+        rng = np.random.Generator(np.random.PCG64([seed, i]))
+        if len(shape) == 2:  # nn.Embedding
+            arr = rng.standard_normal(shape)
+        else:
+            mod = name.rsplit('.', 1)[0]
+            bound = 1.0 / np.sqrt(fan_in[mod])
+            arr = rng.uniform(-bound, bound, size=shape)
+        out[name] = arr.astype(np.float32)
+    if 'tpose_human.alpha_fc.bias' in out:
+        out['tpose_human.alpha_fc.bias'][:] = alpha_bias
+    return out

@@ -1,0 +1,155 @@
+#!/usr/bin/env python
+"""Headline benchmark: BASELINE.json metric on config 2 (aninerf_s9p full 512x512 render, fp32,
+novel-view eval) through the drop-in ``Renderer.render_device`` (HIP C-ABI).
+
+step    = one full-frame render of 512x512 box rays x 64 samples (262,142 rays hit the box),
+          inputs resident in HBM, outputs (rgb/acc/depth/raw + pbw/tbw rows) left in HBM.
+N GPUs  = one process per GPU (torch.distributed.run), each rendering its own frame (rays seed
+          2 + rank): frames are independent, so no collective on the data path ("scaling": "weak");
+          the timed region is bracketed by barriers and the max over ranks is reported.
+roofline: k_mlp (fused deform + NeRF network, fp32 MFMA) is the dominant kernel; its per-launch
+          time is measured with hipEvents on the render stream (anr_profile_*), algorithmic work =
+          kept samples x 2,312,192 FLOP; peak = fp32 MFMA 157.3 TFLOP/s.
+cpu_baseline: the oracle (op-for-op PyTorch-CPU restatement of the reference) on the first 16
+          chunks (32,768 rays) of the same frame, rank 0 at N=1 only.
+"""
+import argparse
+import json
+import os
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+FLOP_PER_KEPT = 2_312_192          # render credit (BW pose + NeRF, latent folded)
+FLOP_PER_KEPT_EXECUTED = 3_306_496  # + T-pose BW MLP (tbw rows are part of the render outputs)
+PEAK_FP32_MFMA_TFLOPS = 157.3      # MI355X_MICROARCH.md, Peak FP32 (matrix)
+METRIC = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), 'BASELINE.json')))['metric']
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=5)
+    ap.add_argument('--warmup', type=int, default=2)
+    ap.add_argument('--rays', type=int, default=512 * 512)
+    ap.add_argument('--cpu-rays', type=int, default=16 * 2048)
+    ap.add_argument('--no-cpu', action='store_true')
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get('RANK', 0))
+    world = int(os.environ.get('WORLD_SIZE', 1))
+    local = int(os.environ.get('LOCAL_RANK', 0))
+    torch.cuda.set_device(local)
+    dev = torch.device('cuda', local)
+    if world > 1:
+        dist.init_process_group('nccl', device_id=dev)
+
+    from animatable_nerf_amd import _lib, config, network, synthetic
+    from animatable_nerf_amd.renderer import Renderer, near_far
+
+    sc = synthetic.Scene(vsize=0.025)
+    ro, rd = sc.box_rays(args.rays, seed=2 + rank)
+    nr, fr, m = near_far(torch.from_numpy(sc.bounds).to(dev), torch.from_numpy(ro).to(dev),
+                         torch.from_numpy(rd).to(dev))
+    m_np = m.cpu().numpy()
+    b = sc.batch_arrays(ro[m_np], rd[m_np], nr.cpu().numpy(), fr.cpu().numpy())
+    batch = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in b.items()}
+    R = int(batch['ray_o'].shape[1])
+
+    net = network.Network()
+    sd = synthetic.init_state_dict({k: tuple(v.shape) for k, v in net.state_dict().items()})
+    network.load_numpy_state(net, sd)
+    net = net.to(dev)
+    net.train()  # run.py evaluates in train() mode with perturb = 0
+    cfg = config.defaults()
+    cfg.perturb = 0
+    renderer = Renderer(net, cfg)
+    lib = _lib.load()
+
+    for _ in range(args.warmup):
+        out = renderer.render_device(batch)
+    torch.cuda.synchronize()
+    lib.anr_profile_enable(1)
+    lib.anr_profile_read(None, None)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = renderer.render_device(batch)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    mlp_ms = _lib.ctypes.c_double(0)
+    launches = _lib.ctypes.c_int(0)
+    _lib.check(lib.anr_profile_read(_lib.ctypes.byref(mlp_ms), _lib.ctypes.byref(launches)), 'anr_profile_read')
+    lib.anr_profile_enable(0)
+    n_kept, m_rows = renderer.last_counts
+
+    t = torch.tensor([dt], device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt_max = float(t.item())
+    samples_per_rank = R * 64 * args.steps
+    value = samples_per_rank * world / dt_max
+    kernel_ms = mlp_ms.value / max(1, launches.value)
+    achieved = n_kept * FLOP_PER_KEPT / (kernel_ms * 1e-3) / 1e12
+
+    result = {
+        'metric': METRIC, 'value': value, 'unit': 'ray-samples/s', 'n_gpus': world, 'steps': args.steps,
+        'warmup': args.warmup, 'ms_per_step': dt_max / args.steps * 1e3, 'higher_is_better': True,
+        'scaling': 'weak', 'vs_baseline': None, 'dtype': 'fp32', 'data': 'synthetic',
+        'config': {'workload': 'aninerf_s9p full 512x512 render (config 2), eval perturb=0, fp32',
+                   'rays_per_gpu': R, 'samples_per_ray': 64, 'chunk': 2048,
+                   'kept_fraction': n_kept / (R * 64), 'alpha_ind_rows': m_rows,
+                   'parallelism': f'replicas{world} (one frame per GPU)'},
+        'roofline': {'bound': 'mfma', 'kernel': 'k_mlp', 'achieved': achieved, 'peak': PEAK_FP32_MFMA_TFLOPS,
+                     'unit': 'TFLOP/s', 'frac': achieved / PEAK_FP32_MFMA_TFLOPS, 'traffic': None,
+                     'kernel_ms': kernel_ms, 'flop_per_kept': FLOP_PER_KEPT,
+                     'achieved_executed': n_kept * FLOP_PER_KEPT_EXECUTED / (kernel_ms * 1e-3) / 1e12},
+    }
+
+    if rank == 0 and world == 1 and not args.no_cpu:
+        result['cpu_baseline'], result['psnr_vs_fp32_oracle'] = cpu_baseline(sd, b, out, args.cpu_rays)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(sd, b, out, n_rays):
+    """Oracle (PyTorch-CPU restatement) on a bounded sample of the same frame; PSNR of the HIP
+    image against it over that sample (A18 formula)."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from oracle import restate
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    P = {k: torch.from_numpy(v) for k, v in sd.items()}
+    n_rays = min(n_rays, b['ray_o'].shape[1])
+    sub = {k: torch.from_numpy(np.ascontiguousarray(
+        v[:, :n_rays] if k in ('ray_o', 'ray_d', 'near', 'far', 'occupancy', 'mask_at_box', 'rgb') else v))
+        for k, v in b.items()}
+    warm = {k: (v[:, :2048] if k in ('ray_o', 'ray_d', 'near', 'far', 'occupancy', 'mask_at_box', 'rgb') else v)
+            for k, v in sub.items()}
+    with torch.no_grad():
+        restate.render(P, warm)
+        t0 = time.perf_counter()
+        ref = restate.render(P, sub)
+        dt = time.perf_counter() - t0
+    rgb = out['rgb_map'][0, :n_rays].cpu().numpy()
+    psnr = float(restate.psnr(rgb, ref['rgb_map'][0].numpy()))
+    cpu = {'value': n_rays * 64 / dt, 'unit': 'ray-samples/s', 'cores': threads, 'kind': 'port',
+           'sample': f'first {n_rays} rays ({n_rays // 2048} reference chunks) of the config-2 frame, '
+                     f'oracle/restate.py, torch CPU {threads} threads, {dt:.1f} s'}
+    return cpu, psnr
+
+
+if __name__ == '__main__':
+    main()

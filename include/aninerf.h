@@ -1,0 +1,120 @@
+/*
+ * aninerf.h — C-ABI of the MI355X-native Animatable-NeRF volume-rendering hot path.
+ *
+ * Plain C: device pointers + sizes + a hipStream_t passed as void*; no torch types. Every entry
+ * point is asynchronous on the given stream and returns 0 or an ANR_E* code (a hipError_t is
+ * returned as ANR_E_HIP, its text via anr_last_error()).
+ *
+ * Reference interfaces each entry point replaces (paths relative to the reference tree):
+ *   anr_near_far            lib/utils/if_nerf/if_nerf_data_utils.py:156-196   get_near_far (A14)
+ *   anr_params_pack         lib/networks/bw_deform/tpose_nerf_network.py:11-38, 218-239
+ *                           (state_dict -> the kernel's weight image; called when weights change)
+ *   anr_render_fwd          lib/networks/renderer/tpose_renderer.py:159-186   Renderer.render (A1)
+ *                             -> get_wsampling_points :14-39, get_density_color :41-69,
+ *                                Network.forward tpose_nerf_network.py:139-215,
+ *                                raw2outputs nerf_net_utils.py:6-36
+ *   anr_render_counts       the host syncs the reference makes at pind/alpha_ind (:153-157, :192-196)
+ *   anr_render_bw_rows      tpose_nerf_network.py:195-196 (pbw/tbw rows selected by alpha_ind)
+ *
+ * All float tensors are fp32, contiguous, row-major, with the reference's shapes (batch dim 1).
+ */
+#ifndef ANINERF_H
+#define ANINERF_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+  ANR_OK = 0,
+  ANR_E_HIP = 1,        /* a HIP runtime call failed; see anr_last_error() */
+  ANR_E_ARG = 2,        /* bad shape / NULL pointer / unsupported option */
+  ANR_E_WORKSPACE = 3   /* workspace too small */
+};
+
+/* Number of tensors of the aninerf Network state_dict (tpose_nerf_network.py:11-38, 218-239),
+ * in this order (weights are Conv1d (out, in, 1), embeddings (rows, 128)):
+ *   0 tpose_human.nf_latent.weight (F,128)
+ *   1..16  tpose_human.pts_linears.{0..7}.{weight,bias}   in: 63,256,256,256,256,319,256,256
+ *   17,18 tpose_human.alpha_fc.{weight,bias} (1,256,1)
+ *   19,20 tpose_human.feature_fc.{weight,bias} (256,256,1)
+ *   21,22 tpose_human.latent_fc.{weight,bias} (256,384,1)
+ *   23,24 tpose_human.view_fc.{weight,bias} (128,283,1)
+ *   25,26 tpose_human.rgb_fc.{weight,bias} (3,128,1)
+ *   27 bw_latent.weight (F+1,128)
+ *   28..43 bw_linears.{0..7}.{weight,bias}   in: 191,256,256,256,256,447,256,256
+ *   44,45 bw_fc.{weight,bias} (24,256,1)                                                     */
+#define ANR_NUM_TENSORS 46
+
+typedef struct anr_params {
+  const float* t[ANR_NUM_TENSORS];  /* device pointers, state_dict order above */
+  int num_train_frame;              /* F: rows of nf_latent (bw_latent has F+1) */
+  const void* packed;               /* device weight image written by anr_params_pack */
+} anr_params;
+
+typedef struct anr_frame {
+  const float* A;          /* (24,4,4) device */
+  const float* R;          /* (3,3) device (smpl->world rotation, Rodrigues(Rh)) */
+  const float* Th;         /* (3) device */
+  const float* pbw;        /* (X,Y,Z,25) device: posed blend-weight volume, ch 24 = distance */
+  int pbw_dims[3];
+  const float* pbounds;    /* (2,3) device */
+  const float* tbw;        /* (X',Y',Z',25) device: T-pose blend-weight volume */
+  int tbw_dims[3];
+  const float* tbounds;    /* (2,3) device */
+  const int64_t* latent_index;  /* (1) device: batch['latent_index'] */
+} anr_frame;
+
+typedef struct anr_render_opts {
+  int n_samples;     /* cfg.N_samples; only 64 is supported */
+  int chunk;         /* rays per reference chunk (2048, tpose_renderer.py:170); semantics depend on it */
+  float norm_th;     /* cfg.norm_th (0.05) */
+  float train_th;    /* cfg.train_th (0) */
+  const float* t_rand;  /* (R, n_samples) device stratification draws, or NULL (eval / perturb 0) */
+} anr_render_opts;
+
+/* Outputs (device). raw may be NULL (then kept in the workspace). */
+typedef struct anr_render_out {
+  float* rgb_map;    /* (R,3) */
+  float* acc_map;    /* (R)   */
+  float* depth_map;  /* (R)   */
+  float* raw;        /* (R*n_samples, 4) or NULL */
+} anr_render_out;
+
+/* ---- A14: ray / box intersection in float64 (bit-exact with numpy) ---------------------
+ * rays (n,3) f32, bounds (2,3) f32 -> mask (n) u8, near/far (n) f32 at EVERY ray
+ * (garbage where mask==0). */
+int anr_near_far(const float* ray_o, const float* ray_d, int n, const float* bounds,
+                 uint8_t* mask, float* near_, float* far_, void* stream);
+
+/* ---- weights --------------------------------------------------------------------------- */
+size_t anr_params_packed_bytes(void);
+int anr_params_pack(const anr_params* p, void* packed, void* stream);
+
+/* ---- render ---------------------------------------------------------------------------- */
+size_t anr_render_workspace_bytes(int n_rays, const anr_render_opts* o, const anr_frame* f);
+int anr_render_fwd(const anr_params* p, const anr_frame* f, const float* ray_o, const float* ray_d,
+                   const float* near_, const float* far_, int n_rays, const anr_render_opts* o,
+                   const anr_render_out* out, void* workspace, size_t ws_bytes, void* stream);
+/* device int32[2] inside the workspace: {kept points n', alpha_ind rows m}. */
+const int32_t* anr_render_counts(const void* workspace, int n_rays);
+/* Gather the m alpha_ind rows of pbw / tbw (each (m,24)) after the counts were read. */
+int anr_render_bw_rows(const void* workspace, int n_rays, float* pbw, float* tbw, void* stream);
+
+/* ---- measurement ----------------------------------------------------------------------
+ * When enabled, anr_render_fwd records a hipEvent pair around the fused network kernel (k_mlp)
+ * on the caller's stream. anr_profile_read waits for the recorded events, returns the summed
+ * kernel time (ms) and launch count since the last read, and resets. */
+int anr_profile_enable(int on);
+int anr_profile_read(double* mlp_ms, int* launches);
+
+const char* anr_last_error(void);
+int anr_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

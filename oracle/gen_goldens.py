@@ -1,0 +1,285 @@
+"""ORACLE — test infrastructure only. Generates tests/golden/*.npz by running the REAL reference
+(/root/reference, read-only) on CPU in THIS container. It never travels to the GPU box: only its
+outputs (small .npz fixtures) are committed.
+
+Recipe:
+  1. no bytecode writes (the tree is read-only);
+  2. dummy modules for third-party packages the hot path imports but never calls
+     (pytorch3d, cv2, trimesh, termcolor, imageio, tensorboardX, plyfile);
+  3. ``sys.argv`` set BEFORE ``import lib.config`` (it parses argv at import, config.py:183-194);
+  4. cwd = /root/reference (relative parent_cfg / network_path).
+Goldens use ``torch.set_num_threads(1)``.
+
+Run:  python oracle/gen_goldens.py            (writes tests/golden/)
+"""
+import os
+import sys
+import types
+import zlib
+
+import numpy as np
+
+REF = '/root/reference'
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+OUT = os.path.join(REPO, 'tests', 'golden')
+
+
+class _Stub(types.ModuleType):
+    def __getattr__(self, name):
+        if name.startswith('__'):
+            raise AttributeError(name)
+        return _StubObj()
+
+
+class _StubObj:
+    def __call__(self, *a, **k):
+        return _StubObj()
+
+    def __getattr__(self, name):
+        if name.startswith('__'):
+            raise AttributeError(name)
+        return _StubObj()
+
+
+def _install_stubs():
+    for name in ['pytorch3d', 'pytorch3d._C', 'pytorch3d.structures', 'pytorch3d.ops',
+                 'pytorch3d.ops.knn', 'pytorch3d.ops.packed_to_padded',
+                 'pytorch3d.ops.mesh_face_areas_normals', 'pytorch3d.ops.sample_points_from_meshes',
+                 'cv2', 'trimesh', 'termcolor', 'imageio', 'tensorboardX', 'plyfile']:
+        sys.modules[name] = _Stub(name)
+
+
+def import_reference(cfg_file='configs/aninerf_s9p.yaml', opts=()):
+    sys.dont_write_bytecode = True
+    os.environ['PYTHONDONTWRITEBYTECODE'] = '1'
+    _install_stubs()
+    os.chdir(REF)
+    sys.path.insert(0, REF)
+    sys.argv = ['gen_goldens', '--cfg_file', cfg_file, 'gpus', '[]'] + list(opts)
+    import lib.config  # noqa: F401  (parses argv)
+    from lib.config import cfg
+    from lib.networks import make_network
+    from lib.networks.renderer import make_renderer
+    return cfg, make_network, make_renderer
+
+
+def main():
+    import torch
+    torch.set_num_threads(1)
+    sys.path.insert(0, REPO)
+    from animatable_nerf_amd.synthetic import Scene, init_state_dict, rigid_transformation, PARENTS
+    cfg, make_network, make_renderer = import_reference()
+    import lib.networks.bw_deform.tpose_nerf_network as tnn
+    from lib.utils.if_nerf import if_nerf_data_utils as dutils
+
+    os.makedirs(OUT, exist_ok=True)
+    net = make_network(cfg)
+    shapes = {k: tuple(v.shape) for k, v in net.state_dict().items()}
+    sd = init_state_dict(shapes)
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
+    cfg.perturb = 0
+    net.train()  # run.py evaluates in train() mode with perturb=0 (run.py:53-58)
+    renderer = make_renderer(cfg, net)
+
+    scene = Scene(vsize=0.05)
+    meta = dict(vol_crc=zlib.crc32(scene.volume.tobytes()), A_crc=zlib.crc32(scene.A.tobytes()),
+                vol_shape=np.array(scene.volume.shape))
+
+    # ---- A15: rigid transformation + A14 near/far on the scene's own rays
+    A_ref = dutils.get_rigid_transformation(scene.poses, scene.joints, PARENTS)
+    assert np.array_equal(A_ref, rigid_transformation(scene.poses, scene.joints, PARENTS))
+
+    def batch_for(ray_o, ray_d):
+        near, far, mask = dutils.get_near_far(scene.bounds, ray_o, ray_d)
+        b = scene.batch_arrays(ray_o[mask], ray_d[mask], near.astype(np.float32), far.astype(np.float32))
+        return {k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in b.items()}, mask
+
+    # ---- G1 tiny: 64 rays, intermediates captured by wrapping the module-level helpers
+    rec = {}
+    orig_psbw = tnn.pts_sample_blend_weights
+    orig_p2t = tnn.pose_points_to_tpose_points
+    calls = []
+
+    def psbw(pts, bw, bounds):
+        out = orig_psbw(pts, bw, bounds)
+        calls.append(out.detach().clone())
+        return out
+
+    def p2t(ppts, bw, A):
+        out = orig_p2t(ppts, bw, A)
+        rec['tpose'] = out.detach().clone()
+        rec['pbw_full'] = bw.detach().clone()
+        return out
+
+    orig_nbw = tnn.Network.calculate_neural_blend_weights
+    bws = []
+
+    def nbw(self, pts, smpl_bw, idx):
+        out = orig_nbw(self, pts, smpl_bw, idx)
+        bws.append(out.detach().clone())
+        return out
+
+    orig_ar = tnn.TPoseHuman.calculate_alpha_rgb
+
+    def ar(self, pts, vd, ind):
+        a, c = orig_ar(self, pts, vd, ind)
+        rec['sigma_raw'] = a.detach().clone()
+        rec['rgb_raw'] = c.detach().clone()
+        return a, c
+
+    tnn.pts_sample_blend_weights = psbw
+    tnn.pose_points_to_tpose_points = p2t
+    tnn.Network.calculate_neural_blend_weights = nbw
+    tnn.TPoseHuman.calculate_alpha_rgb = ar
+    ro, rd = scene.box_rays(64, seed=2)
+    batch, mask = batch_for(ro, rd)
+    with torch.no_grad():
+        ret = renderer.render(batch)
+    tnn.pts_sample_blend_weights = orig_psbw
+    tnn.pose_points_to_tpose_points = orig_p2t
+    tnn.Network.calculate_neural_blend_weights = orig_nbw
+    tnn.TPoseHuman.calculate_alpha_rgb = orig_ar
+    g1 = dict(ray_seed=2, n_rays=64, mask=mask, near=batch['near'].numpy(), far=batch['far'].numpy(),
+              pre_bw=calls[0].numpy(), init_pbw=calls[1].numpy(), init_tbw=calls[2].numpy(),
+              pbw=bws[0].numpy(), tbw=bws[1].numpy(), tpose=rec['tpose'].numpy(),
+              sigma_raw=rec['sigma_raw'].numpy(), rgb_raw=rec['rgb_raw'].numpy(),
+              **{'out_' + k: v.numpy() for k, v in ret.items()}, **meta)
+    np.savez_compressed(os.path.join(OUT, 'g1_tiny.npz'), **g1)
+
+    # ---- G2 chunks: 4096 box rays + 512 corner-grazing rays (a chunk with pnorm >= th everywhere)
+    ro, rd = scene.box_rays(4096, seed=5)
+    rng = np.random.Generator(np.random.PCG64(7))
+    corners = np.array([[sx, sy, sz] for sx in (0, 1) for sy in (0, 1) for sz in (0, 1)])
+    b = scene.bounds.astype(np.float64)
+    tgt = b[corners[rng.integers(0, 8, 512)], [0, 1, 2]]
+    tgt = tgt - np.sign(tgt) * rng.uniform(0.0, 0.01, size=(512, 3))
+    o2 = np.broadcast_to(np.array([0.0, 0.0, 3.0]), (512, 3))
+    d2 = tgt - o2
+    d2 /= np.linalg.norm(d2, axis=1, keepdims=True)
+    ro = np.concatenate([ro, o2.astype(np.float32)])
+    rd = np.concatenate([rd, d2.astype(np.float32)])
+    batch, mask = batch_for(ro, rd)
+    with torch.no_grad():
+        ret = renderer.render(batch)
+    keep = (ret['raw'][0, :, :3].abs().sum(-1) != 0).numpy()
+    rows = np.arange(0, ret['pbw'].shape[1], 37)
+    g2 = dict(ray_o=ro, ray_d=rd, mask=mask, **{'out_' + k: ret[k].numpy() for k in
+                                                ('rgb_map', 'acc_map', 'depth_map')},
+              keep_bits=np.packbits(keep), kept_alpha=ret['raw'][0, keep, 3].numpy(),
+              bw_rows=np.int64(ret['pbw'].shape[1]), bw_sample_idx=rows,
+              pbw_sample=ret['pbw'][0, rows].numpy(), tbw_sample=ret['tbw'][0, rows].numpy(),
+              pbw_sum=ret['pbw'].double().sum(1).numpy(), tbw_sum=ret['tbw'].double().sum(1).numpy(), **meta)
+    np.savez_compressed(os.path.join(OUT, 'g2_chunks.npz'), **g2)
+
+    # ---- G3 hits: camera rays (64x64) + adversarial rays through get_near_far
+    K = np.array([[75.0, 0, 32.0], [0, 75.0, 32.0], [0, 0, 1]], np.float32)
+    Rc = np.array([[1, 0, 0], [0, -1, 0], [0, 0, -1]], np.float32)
+    Tc = np.array([[0.0], [0.0], [3.0]], np.float32)
+    cam_o, cam_d = dutils.get_rays(64, 64, K, Rc, Tc)
+    cam_o = cam_o.reshape(-1, 3).astype(np.float32)
+    cam_d = cam_d.reshape(-1, 3).astype(np.float32)
+    adv_o, adv_d = adversarial_rays(scene.bounds, 1024)
+    ray_o = np.concatenate([cam_o, adv_o])
+    ray_d = np.concatenate([cam_d, adv_d])
+    with np.errstate(all='ignore'):
+        near, far, mask = dutils.get_near_far(scene.bounds, ray_o, ray_d)
+    g3 = dict(K=K, Rc=Rc, Tc=Tc, cam_o=cam_o, cam_d=cam_d, ray_o=ray_o, ray_d=ray_d,
+              bounds=scene.bounds, mask=mask, near=near.astype(np.float32), far=far.astype(np.float32),
+              near64=near, far64=far, A_ref=A_ref, poses=scene.poses, joints=scene.joints)
+    np.savez_compressed(os.path.join(OUT, 'g3_hits.npz'), **g3)
+
+    # ---- G4 train step: 256 rays, perturb=1, recorded t_rand, grads, Adam update
+    from lib.train import make_optimizer
+    from lib.train.trainers.tpose_trainer import NetworkWrapper
+    cfg.perturb = 1
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
+    net.train()
+    wrapper = NetworkWrapper(net)
+    ro, rd = scene.box_rays(256, seed=11)
+    batch, mask = batch_for(ro, rd)
+    trng = np.random.Generator(np.random.PCG64(3))
+    R = batch['ray_o'].shape[1]
+    t_rand = torch.from_numpy(trng.random((R, 64)).astype(np.float32))
+    batch['rgb'] = torch.from_numpy(trng.random((1, R, 3)).astype(np.float32))
+    batch['mask_at_box'] = torch.ones((1, R), dtype=torch.bool)
+    orig_rand = torch.rand
+    pos = [0]
+
+    def fake_rand(shape, *a, **k):
+        n = shape[1]
+        out = t_rand[pos[0]:pos[0] + n][None].clone()
+        pos[0] += n
+        return out
+
+    torch.rand = fake_rand
+    optimizer = make_optimizer(cfg, net)
+    _, loss, stats, _ = wrapper(batch)
+    optimizer.zero_grad()
+    loss.backward()
+    torch.nn.utils.clip_grad_value_(net.parameters(), 40)
+    grads = {k: v.grad.detach().clone().numpy() for k, v in net.named_parameters() if v.grad is not None}
+    before = {k: v.detach().clone() for k, v in net.named_parameters()}
+    optimizer.step()
+    torch.rand = orig_rand
+    delta = {k: (v.detach() - before[k]).numpy() for k, v in net.named_parameters()}
+    keep = ['bw_linears.0.weight', 'bw_linears.7.bias', 'bw_fc.weight', 'tpose_human.pts_linears.0.weight',
+            'tpose_human.pts_linears.5.weight', 'tpose_human.rgb_fc.weight', 'tpose_human.alpha_fc.bias',
+            'bw_latent.weight', 'tpose_human.nf_latent.weight']
+    g4 = dict(ray_o=ro, ray_d=rd, mask=mask, t_rand=t_rand.numpy(), rgb=batch['rgb'].numpy(),
+              loss=loss.detach().numpy(), **{'stat_' + k: v.detach().numpy() for k, v in stats.items()},
+              **{'grad_' + k: grads[k] for k in keep if k in grads},
+              **{'delta_' + k: delta[k] for k in keep}, lr=np.float32(cfg.train.lr))
+    np.savez_compressed(os.path.join(OUT, 'g4_train.npz'), **g4)
+    cfg.perturb = 0
+    print('goldens written to', OUT)
+
+
+def adversarial_rays(bounds, n):
+    """Edge/corner-grazing, axis-parallel (zero components) and face-tangent rays."""
+    rng = np.random.Generator(np.random.PCG64(17))
+    b = bounds.astype(np.float64) + np.array([-0.01, 0.01])[:, None]   # the padded box the test uses
+    lo, hi = b[0], b[1]
+    o_list, d_list = [], []
+    q = n // 4
+    # 1) axis-parallel rays (two zero direction components) through / beside / on the box
+    for i in range(q):
+        ax = i % 3
+        o = rng.uniform(lo - 0.05, hi + 0.05)
+        o[ax] = (lo[ax] - 1.0) if (i // 3) % 2 == 0 else (hi[ax] + 1.0)
+        if i % 5 == 0:                            # exactly on a face plane
+            o[(ax + 1) % 3] = lo[(ax + 1) % 3]
+        d = np.zeros(3)
+        d[ax] = 1.0 if o[ax] < lo[ax] else -1.0
+        o_list.append(o)
+        d_list.append(d)
+    # 2) rays through box corners
+    for i in range(q):
+        c = np.where(rng.integers(0, 2, 3) == 1, hi, lo)
+        o = rng.uniform(-2.0, 2.0, 3) + np.array([0, 0, 3.0])
+        d = c - o
+        o_list.append(o)
+        d_list.append(d / np.linalg.norm(d))
+    # 3) rays through edge midpoints
+    for i in range(q):
+        c = np.where(rng.integers(0, 2, 3) == 1, hi, lo)
+        k = rng.integers(0, 3)
+        c[k] = rng.uniform(lo[k], hi[k])
+        o = rng.uniform(-2.0, 2.0, 3) + np.array([0, 0, 3.0])
+        d = c - o
+        o_list.append(o)
+        d_list.append(d / np.linalg.norm(d))
+    # 4) face-tangent rays (one zero component, lying in a face plane)
+    for i in range(n - 3 * q):
+        ax = i % 3
+        o = rng.uniform(lo - 0.5, hi + 0.5)
+        o[ax] = lo[ax] if i % 2 == 0 else hi[ax]
+        d = rng.standard_normal(3)
+        d[ax] = 0.0
+        o_list.append(o)
+        d_list.append(d / np.linalg.norm(d))
+    return np.array(o_list, np.float32), np.array(d_list, np.float32)
+
+
+if __name__ == '__main__':
+    main()
