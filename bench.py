@@ -115,6 +115,11 @@ def main():
                      'achieved_executed': n_kept * FLOP_PER_KEPT_EXECUTED / (kernel_ms * 1e-3) / 1e12},
     }
 
+    pmc = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'profiles', 'pmc_latest.json')
+    if os.path.exists(pmc):
+        t = json.load(open(pmc))
+        result['roofline']['traffic'] = t['bytes_per_launch']
+        result['roofline']['traffic_source'] = t['source'] + '; ' + t['correction']
     if rank == 0 and world == 1 and not args.no_cpu:
         result['cpu_baseline'], result['psnr_vs_fp32_oracle'] = cpu_baseline(sd, b, out, args.cpu_rays)
     if rank == 0:
