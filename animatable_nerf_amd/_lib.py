@@ -16,6 +16,7 @@ NUM_TENSORS = 46
 
 EXPORTS = ('anr_near_far', 'anr_params_packed_bytes', 'anr_params_pack', 'anr_render_workspace_bytes',
            'anr_render_fwd', 'anr_render_counts', 'anr_render_bw_rows', 'anr_profile_enable', 'anr_profile_read',
+           'anr_train_workspace_bytes', 'anr_train_fwd', 'anr_train_bwd', 'anr_train_step', 'anr_adam',
            'anr_last_error', 'anr_version')
 
 c_float_p = ctypes.c_void_p
@@ -66,6 +67,17 @@ def load():
     lib.anr_render_counts.restype = P
     lib.anr_render_counts.argtypes = [P, ctypes.c_int]
     lib.anr_render_bw_rows.argtypes = [P, ctypes.c_int, P, P, P]
+    lib.anr_train_workspace_bytes.restype = ctypes.c_size_t
+    lib.anr_train_workspace_bytes.argtypes = [ctypes.c_int, ctypes.POINTER(RenderOpts), ctypes.POINTER(Frame)]
+    lib.anr_train_fwd.argtypes = [ctypes.POINTER(Params), ctypes.POINTER(Frame), P, P, P, P, ctypes.c_int,
+                                  ctypes.POINTER(RenderOpts), ctypes.POINTER(RenderOut), P, ctypes.c_size_t, P]
+    lib.anr_train_bwd.argtypes = [ctypes.POINTER(Params), ctypes.c_void_p * NUM_TENSORS, ctypes.POINTER(Frame), P, P, P, P,
+                                  ctypes.c_int, ctypes.POINTER(RenderOpts), P, P, P, P, ctypes.c_size_t, P]
+    lib.anr_train_step.argtypes = [ctypes.POINTER(Params), ctypes.c_void_p * NUM_TENSORS, ctypes.POINTER(Frame), P, P, P,
+                                   P, ctypes.c_int, ctypes.POINTER(RenderOpts), P, P, ctypes.POINTER(RenderOut), P, P,
+                                   ctypes.c_size_t, P]
+    lib.anr_adam.argtypes = [P, P, P, P, ctypes.c_long, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                             ctypes.c_float, ctypes.c_int, ctypes.c_float, P]
     lib.anr_profile_enable.argtypes = [ctypes.c_int]
     lib.anr_profile_read.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]
     lib.anr_last_error.restype = ctypes.c_char_p

@@ -9,10 +9,11 @@
 #include "anr_common.h"
 #include "anr_kernels.h"
 #include "anr_layers.h"
+#include "anr_ws.h"
 
 using namespace anr;
 
-namespace {
+namespace anr {
 
 thread_local std::string g_err;
 
@@ -27,50 +28,10 @@ int check_launch(const char* what) {
   return ANR_OK;
 }
 
-#define ANR_TRY(x)                  \
-  do {                              \
-    const int _rc = (x);            \
-    if (_rc != ANR_OK) return _rc;  \
-  } while (0)
+}  // namespace anr
 
-size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
+namespace {
 
-// Workspace layout. Fields up to `tbw_rows` depend only on n_rays (anr_render_counts/bw_rows).
-struct Layout {
-  size_t counts, mask, ray_off, block_sum, list, sigma, flags, block_sum2, out_row, pbw_rows, tbw_rows;
-  size_t chunk_min, chunk_max, raw, pbw32, tbw32, fold, total;
-};
-
-Layout layout(int n_rays, int chunk, long np, long nt, bool need_raw) {
-  Layout L{};
-  const size_t R = (size_t)n_rays, N = R * 64;
-  size_t o = 0;
-  auto take = [&](size_t bytes) {
-    const size_t at = o;
-    o = align256(o + bytes);
-    return at;
-  };
-  L.counts = take(16);
-  L.mask = take(R * 8);
-  L.ray_off = take((R + 1) * 4);
-  L.block_sum = take(((R + 255) / 256) * 4);
-  L.list = take(N * 4);
-  L.sigma = take(N * 4);
-  L.flags = take(N);
-  L.block_sum2 = take(((N + 1023) / 1024) * 4);
-  L.out_row = take(N * 4);
-  L.pbw_rows = take(N * 24 * 4);
-  L.tbw_rows = take(N * 24 * 4);
-  const size_t nch = (R + chunk - 1) / (chunk > 0 ? chunk : 1);
-  L.chunk_min = take(nch * 8);
-  L.chunk_max = take(nch * 8);
-  L.raw = need_raw ? take(N * 16) : 0;
-  L.pbw32 = take((size_t)np * 32 * 4);
-  L.tbw32 = take((size_t)nt * 32 * 4);
-  L.fold = take(1280 * 4);
-  L.total = o;
-  return L;
-}
 
 int num_cus() {
   static int cached[64] = {0};
@@ -94,6 +55,144 @@ struct Prof {
 } g_prof;
 
 }  // namespace
+
+namespace anr {
+
+// A2-A6 + per-frame prep: memsets, volumes/folds, front-end, ordered compaction (counts[0] = n')
+int stage_frontend(const anr_params* p, const anr_frame* f, const float* ray_o, const float* ray_d, const float* near_,
+                   const float* far_, int R, const anr_render_opts* o, char* ws, const Layout& L, float4* raw,
+                   hipStream_t s) {
+  const long np = (long)f->pbw_dims[0] * f->pbw_dims[1] * f->pbw_dims[2];
+  const long nt = (long)f->tbw_dims[0] * f->tbw_dims[1] * f->tbw_dims[2];
+  const int nch = (R + o->chunk - 1) / o->chunk;
+  int* counts = (int*)(ws + L.counts);
+  if (hipMemsetAsync(ws + L.counts, 0, 16, s) != hipSuccess ||
+      hipMemsetAsync(ws + L.chunk_min, 0xff, (size_t)nch * 8, s) != hipSuccess ||
+      hipMemsetAsync(ws + L.chunk_max, 0, (size_t)nch * 8, s) != hipSuccess)
+    return fail(ANR_E_HIP, "hipMemsetAsync failed");
+
+  PrepArgs pa{};
+  pa.pbw = f->pbw; pa.tbw = f->tbw;
+  pa.pbw32 = (float*)(ws + L.pbw32); pa.tbw32 = (float*)(ws + L.tbw32);
+  pa.np = (int)np; pa.nt = (int)nt;
+  pa.w_bw0 = p->t[28]; pa.b_bw0 = p->t[29]; pa.w_bw5 = p->t[38]; pa.b_bw5 = p->t[39];
+  pa.bw_latent = p->t[27]; pa.w_lat = p->t[21]; pa.b_lat = p->t[22]; pa.nf_latent = p->t[0];
+  pa.latent_index = f->latent_index;
+  pa.fold = (float*)(ws + L.fold);
+  const int nvb = (int)((np + nt + 7) / 8);
+  hipLaunchKernelGGL(k_prep, dim3(nvb + 1), dim3(256), 0, s, pa);
+  ANR_TRY(check_launch("k_prep"));
+
+  FrontArgs fa{};
+  fa.ray_o = ray_o; fa.ray_d = ray_d; fa.near_ = near_; fa.far_ = far_; fa.t_rand = o->t_rand;
+  fa.n_rays = R; fa.chunk = o->chunk;
+  fa.R = f->R; fa.Th = f->Th; fa.pbw = f->pbw; fa.pbounds = f->pbounds;
+  fa.X = f->pbw_dims[0]; fa.Y = f->pbw_dims[1]; fa.Z = f->pbw_dims[2];
+  fa.norm_th = o->norm_th;
+  fa.mask = (uint64_t*)(ws + L.mask);
+  fa.chunk_min = (uint64_t*)(ws + L.chunk_min);
+  fa.raw = raw;
+  hipLaunchKernelGGL(k_frontend, dim3((R + 3) / 4), dim3(256), 0, s, fa);
+  ANR_TRY(check_launch("k_frontend"));
+
+  CompactArgs ca{};
+  ca.n_rays = R; ca.chunk = o->chunk;
+  ca.mask = fa.mask; ca.chunk_min = fa.chunk_min;
+  ca.ray_off = (int*)(ws + L.ray_off);
+  ca.block_sum = (int*)(ws + L.block_sum);
+  ca.list = (int*)(ws + L.list);
+  const int nb = (R + 255) / 256;
+  hipLaunchKernelGGL(k_count, dim3(nb), dim3(256), 0, s, ca);
+  ANR_TRY(check_launch("k_count"));
+  hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, s, ca.block_sum, nb, counts);
+  ANR_TRY(check_launch("k_scan_blocks"));
+  hipLaunchKernelGGL(k_compact, dim3((R + 3) / 4), dim3(256), 0, s, ca);
+  return check_launch("k_compact");
+}
+
+// the fused network kernel (render path)
+int stage_mlp(const anr_params* p, const anr_frame* f, const float* ray_o, const float* ray_d, const float* near_,
+              const float* far_, int R, const anr_render_opts* o, char* ws, const Layout& L, float4* raw,
+              hipStream_t s) {
+  const long N = (long)R * 64;
+  MlpArgs ma{};
+  ma.wimg = (const unsigned char*)p->packed;
+  ma.bias = (const float*)((const unsigned char*)p->packed + weights_bytes());
+  ma.fold = (const float*)(ws + L.fold);
+  ma.A = f->A; ma.R = f->R; ma.Th = f->Th;
+  ma.pbw32 = (const float*)(ws + L.pbw32); ma.pbounds = f->pbounds;
+  ma.tbw32 = (const float*)(ws + L.tbw32); ma.tbounds = f->tbounds;
+  ma.pX = f->pbw_dims[0]; ma.pY = f->pbw_dims[1]; ma.pZ = f->pbw_dims[2];
+  ma.tX = f->tbw_dims[0]; ma.tY = f->tbw_dims[1]; ma.tZ = f->tbw_dims[2];
+  ma.ray_o = ray_o; ma.ray_d = ray_d; ma.near_ = near_; ma.far_ = far_; ma.t_rand = o->t_rand;
+  ma.list = (const int*)(ws + L.list); ma.n_kept = (const int*)(ws + L.counts);
+  ma.raw = raw;
+  ma.sigma = (float*)(ws + L.sigma);
+  ma.pbw_rows = (float*)(ws + L.pbw_rows);
+  ma.tbw_rows = (float*)(ws + L.tbw_rows);
+  const int lds = 2 * 8 * 5 * 1024 + 24 * 16 * 4;
+  if (!mlp_attr_set) {
+    if (hipFuncSetAttribute((const void*)k_mlp, hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
+      return fail(ANR_E_HIP, "hipFuncSetAttribute(k_mlp) failed");
+    mlp_attr_set = true;
+  }
+  const long max_tiles = (N + 127) / 128;
+  const int grid = (int)(max_tiles < num_cus() ? max_tiles : num_cus());
+  std::pair<hipEvent_t, hipEvent_t>* evp = nullptr;
+  if (g_prof.on) {
+    if (g_prof.used == g_prof.ev.size()) {
+      hipEvent_t a = nullptr, b = nullptr;
+      if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess)
+        return fail(ANR_E_HIP, "hipEventCreate failed");
+      g_prof.ev.emplace_back(a, b);
+    }
+    evp = &g_prof.ev[g_prof.used++];
+    if (hipEventRecord(evp->first, s) != hipSuccess) return fail(ANR_E_HIP, "hipEventRecord failed");
+  }
+  hipLaunchKernelGGL(k_mlp, dim3(grid), dim3(512), lds, s, ma);
+  ANR_TRY(check_launch("k_mlp"));
+  if (evp && hipEventRecord(evp->second, s) != hipSuccess) return fail(ANR_E_HIP, "hipEventRecord failed");
+  return ANR_OK;
+}
+
+// A11 alpha_ind rows: sigma' > train_th plus per-chunk argmax (counts[1] = m)
+int stage_alpha_ind(int R, const anr_render_opts* o, char* ws, const Layout& L, hipStream_t s) {
+  const long N = (long)R * 64;
+  const int nch = (R + o->chunk - 1) / o->chunk;
+  int* counts = (int*)(ws + L.counts);
+  AlphaArgs aa{};
+  aa.n_rays = R; aa.chunk = o->chunk;
+  aa.ray_off = (const int*)(ws + L.ray_off); aa.n_kept = counts;
+  aa.sigma = (const float*)(ws + L.sigma);
+  aa.chunk_max = (uint64_t*)(ws + L.chunk_max);
+  aa.train_th = o->train_th;
+  aa.flags = (uint8_t*)(ws + L.flags);
+  aa.block_sum = (int*)(ws + L.block_sum2);
+  aa.out_row = (int*)(ws + L.out_row);
+  hipLaunchKernelGGL(k_chunk_argmax, dim3(nch, 16), dim3(256), 0, s, aa);
+  ANR_TRY(check_launch("k_chunk_argmax"));
+  const int nb2 = (int)((N + 1023) / 1024);
+  hipLaunchKernelGGL(k_flag_count, dim3(nb2), dim3(256), 0, s, aa);
+  ANR_TRY(check_launch("k_flag_count"));
+  hipLaunchKernelGGL(k_flag_force, dim3((nch + 255) / 256), dim3(256), 0, s, aa, nch);
+  ANR_TRY(check_launch("k_flag_force"));
+  hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, s, aa.block_sum, nb2, counts + 1);
+  ANR_TRY(check_launch("k_scan_blocks(alpha)"));
+  hipLaunchKernelGGL(k_flag_scatter, dim3(nb2), dim3(256), 0, s, aa);
+  return check_launch("k_flag_scatter");
+}
+
+// A12 compositing
+int stage_composite(const float* near_, const float* far_, int R, const anr_render_opts* o, const float4* raw,
+                    const anr_render_out* out, float* weights, hipStream_t s) {
+  CompositeArgs co{};
+  co.raw = raw; co.near_ = near_; co.far_ = far_; co.t_rand = o->t_rand; co.n_rays = R;
+  co.rgb = out->rgb_map; co.acc = out->acc_map; co.depth = out->depth_map; co.weights = weights;
+  hipLaunchKernelGGL(k_composite, dim3((R + 3) / 4), dim3(256), 0, s, co);
+  return check_launch("k_composite");
+}
+
+}  // namespace anr
 
 extern "C" {
 
@@ -160,119 +259,11 @@ int anr_render_fwd(const anr_params* p, const anr_frame* f, const float* ray_o, 
 
   hipStream_t s = (hipStream_t)stream;
   char* ws = (char*)workspace;
-  const int R = n_rays;
-  const long N = (long)R * 64;
-  const int nch = (R + o->chunk - 1) / o->chunk;
-  int* counts = (int*)(ws + L.counts);
   float4* raw = out->raw ? (float4*)out->raw : (float4*)(ws + L.raw);
-
-  if (hipMemsetAsync(ws + L.counts, 0, 16, s) != hipSuccess ||
-      hipMemsetAsync(ws + L.chunk_min, 0xff, (size_t)nch * 8, s) != hipSuccess ||
-      hipMemsetAsync(ws + L.chunk_max, 0, (size_t)nch * 8, s) != hipSuccess)
-    return fail(ANR_E_HIP, "hipMemsetAsync failed");
-
-  // per-frame prep: 32-channel volumes + folded latent biases
-  PrepArgs pa{};
-  pa.pbw = f->pbw; pa.tbw = f->tbw;
-  pa.pbw32 = (float*)(ws + L.pbw32); pa.tbw32 = (float*)(ws + L.tbw32);
-  pa.np = (int)np; pa.nt = (int)nt;
-  pa.w_bw0 = p->t[28]; pa.b_bw0 = p->t[29]; pa.w_bw5 = p->t[38]; pa.b_bw5 = p->t[39];
-  pa.bw_latent = p->t[27]; pa.w_lat = p->t[21]; pa.b_lat = p->t[22]; pa.nf_latent = p->t[0];
-  pa.latent_index = f->latent_index;
-  pa.fold = (float*)(ws + L.fold);
-  const int nvb = (int)((np + nt + 7) / 8);
-  hipLaunchKernelGGL(k_prep, dim3(nvb + 1), dim3(256), 0, s, pa);
-  ANR_TRY(check_launch("k_prep"));
-
-  FrontArgs fa{};
-  fa.ray_o = ray_o; fa.ray_d = ray_d; fa.near_ = near_; fa.far_ = far_; fa.t_rand = o->t_rand;
-  fa.n_rays = R; fa.chunk = o->chunk;
-  fa.R = f->R; fa.Th = f->Th; fa.pbw = f->pbw; fa.pbounds = f->pbounds;
-  fa.X = f->pbw_dims[0]; fa.Y = f->pbw_dims[1]; fa.Z = f->pbw_dims[2];
-  fa.norm_th = o->norm_th;
-  fa.mask = (uint64_t*)(ws + L.mask);
-  fa.chunk_min = (uint64_t*)(ws + L.chunk_min);
-  fa.raw = raw;
-  hipLaunchKernelGGL(k_frontend, dim3((R + 3) / 4), dim3(256), 0, s, fa);
-  ANR_TRY(check_launch("k_frontend"));
-
-  CompactArgs ca{};
-  ca.n_rays = R; ca.chunk = o->chunk;
-  ca.mask = fa.mask; ca.chunk_min = fa.chunk_min;
-  ca.ray_off = (int*)(ws + L.ray_off);
-  ca.block_sum = (int*)(ws + L.block_sum);
-  ca.list = (int*)(ws + L.list);
-  const int nb = (R + 255) / 256;
-  hipLaunchKernelGGL(k_count, dim3(nb), dim3(256), 0, s, ca);
-  ANR_TRY(check_launch("k_count"));
-  hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, s, ca.block_sum, nb, counts);
-  ANR_TRY(check_launch("k_scan_blocks"));
-  hipLaunchKernelGGL(k_compact, dim3((R + 3) / 4), dim3(256), 0, s, ca);
-  ANR_TRY(check_launch("k_compact"));
-
-  MlpArgs ma{};
-  ma.wimg = (const unsigned char*)p->packed;
-  ma.bias = (const float*)((const unsigned char*)p->packed + weights_bytes());
-  ma.fold = pa.fold;
-  ma.A = f->A; ma.R = f->R; ma.Th = f->Th;
-  ma.pbw32 = pa.pbw32; ma.pbounds = f->pbounds; ma.tbw32 = pa.tbw32; ma.tbounds = f->tbounds;
-  ma.pX = f->pbw_dims[0]; ma.pY = f->pbw_dims[1]; ma.pZ = f->pbw_dims[2];
-  ma.tX = f->tbw_dims[0]; ma.tY = f->tbw_dims[1]; ma.tZ = f->tbw_dims[2];
-  ma.ray_o = ray_o; ma.ray_d = ray_d; ma.near_ = near_; ma.far_ = far_; ma.t_rand = o->t_rand;
-  ma.list = ca.list; ma.n_kept = counts;
-  ma.raw = raw;
-  ma.sigma = (float*)(ws + L.sigma);
-  ma.pbw_rows = (float*)(ws + L.pbw_rows);
-  ma.tbw_rows = (float*)(ws + L.tbw_rows);
-  const int lds = 2 * 8 * 5 * 1024 + 24 * 16 * 4;
-  if (!mlp_attr_set) {
-    if (hipFuncSetAttribute((const void*)k_mlp, hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
-      return fail(ANR_E_HIP, "hipFuncSetAttribute(k_mlp) failed");
-    mlp_attr_set = true;
-  }
-  const long max_tiles = (N + 127) / 128;
-  const int grid = (int)(max_tiles < num_cus() ? max_tiles : num_cus());
-  std::pair<hipEvent_t, hipEvent_t>* evp = nullptr;
-  if (g_prof.on) {
-    if (g_prof.used == g_prof.ev.size()) {
-      hipEvent_t a = nullptr, b = nullptr;
-      if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess)
-        return fail(ANR_E_HIP, "hipEventCreate failed");
-      g_prof.ev.emplace_back(a, b);
-    }
-    evp = &g_prof.ev[g_prof.used++];
-    if (hipEventRecord(evp->first, s) != hipSuccess) return fail(ANR_E_HIP, "hipEventRecord failed");
-  }
-  hipLaunchKernelGGL(k_mlp, dim3(grid), dim3(512), lds, s, ma);
-  ANR_TRY(check_launch("k_mlp"));
-  if (evp && hipEventRecord(evp->second, s) != hipSuccess) return fail(ANR_E_HIP, "hipEventRecord failed");
-
-  AlphaArgs aa{};
-  aa.n_rays = R; aa.chunk = o->chunk;
-  aa.ray_off = ca.ray_off; aa.n_kept = counts;
-  aa.sigma = ma.sigma;
-  aa.chunk_max = (uint64_t*)(ws + L.chunk_max);
-  aa.train_th = o->train_th;
-  aa.flags = (uint8_t*)(ws + L.flags);
-  aa.block_sum = (int*)(ws + L.block_sum2);
-  aa.out_row = (int*)(ws + L.out_row);
-  hipLaunchKernelGGL(k_chunk_argmax, dim3(nch, 16), dim3(256), 0, s, aa);
-  ANR_TRY(check_launch("k_chunk_argmax"));
-  const int nb2 = (int)((N + 1023) / 1024);
-  hipLaunchKernelGGL(k_flag_count, dim3(nb2), dim3(256), 0, s, aa);
-  ANR_TRY(check_launch("k_flag_count"));
-  hipLaunchKernelGGL(k_flag_force, dim3((nch + 255) / 256), dim3(256), 0, s, aa, nch);
-  ANR_TRY(check_launch("k_flag_force"));
-  hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, s, aa.block_sum, nb2, counts + 1);
-  ANR_TRY(check_launch("k_scan_blocks(alpha)"));
-  hipLaunchKernelGGL(k_flag_scatter, dim3(nb2), dim3(256), 0, s, aa);
-  ANR_TRY(check_launch("k_flag_scatter"));
-
-  CompositeArgs co{};
-  co.raw = raw; co.near_ = near_; co.far_ = far_; co.t_rand = o->t_rand; co.n_rays = R;
-  co.rgb = out->rgb_map; co.acc = out->acc_map; co.depth = out->depth_map; co.weights = nullptr;
-  hipLaunchKernelGGL(k_composite, dim3((R + 3) / 4), dim3(256), 0, s, co);
-  return check_launch("k_composite");
+  ANR_TRY(stage_frontend(p, f, ray_o, ray_d, near_, far_, n_rays, o, ws, L, raw, s));
+  ANR_TRY(stage_mlp(p, f, ray_o, ray_d, near_, far_, n_rays, o, ws, L, raw, s));
+  ANR_TRY(stage_alpha_ind(n_rays, o, ws, L, s));
+  return stage_composite(near_, far_, n_rays, o, raw, out, nullptr, s);
 }
 
 int anr_profile_enable(int on) {

@@ -1,0 +1,97 @@
+// anr_train.h — internal structures of the layer-wise training executor (anr_train.hip, anr_gemm.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace anr {
+
+struct GemmSeg {
+  const float* A;
+  long a_rs, a_cs;
+  const float* B;
+  long b_rs, b_cs;
+  int K;
+};
+
+struct GemmArgs {
+  int M;
+  const int* M_dev;  // if set, M is read from device memory
+  int N;
+  int nseg;
+  GemmSeg seg[2];
+  float* C;
+  long ldc;
+  const float* bias;   // (N) or NULL
+  int relu;            // apply ReLU
+  const float* mask;   // multiply by (mask > 0) (ReLU derivative), or NULL
+  long ldm;
+  int accumulate;      // C += result (non-atomic)
+  int atomic;          // atomicAdd into C (split-K)
+  int ksplit;          // number of K splits (grid.z)
+};
+
+__global__ void k_gemm(GemmArgs g);
+__global__ void k_colsum(const float* X, long ld, int M, const int* M_dev, int N, float* out, int rows_per_block);
+
+// per-point training buffers (row-major, compact kept-sample order)
+struct TrainBufs {
+  const int* list;
+  const int* n_kept;
+  const float *ray_o, *ray_d, *near_, *far_, *t_rand;
+  const float *R, *Th, *A;
+  const float *pbw, *pbounds, *tbw, *tbounds;  // original (X,Y,Z,25) volumes
+  int pX, pY, pZ, tX, tY, tZ;
+  float* pt;     // [N][8]: pose xyz, dist, tpose xyz, inside
+  float* Gp;     // [N][64] gamma(pose)
+  float* Ip;     // [N][32] init_pbw
+  float* Gv;     // [N][32] gamma(dir)
+  float* Lp;     // [N][32] pose logits
+  float* Bp;     // [N][24] pbw (softmax)
+  float* lbs;    // [N][16] Rinv (9), y (3)
+  float* Gt;     // [N][64] gamma(tpose)
+  float* It;     // [N][32] init_tbw
+  float* Lt;     // [N][32]
+  float* Bt;     // [N][24]
+  float* Rgbl;   // [N][4] rgb logits
+  float* Alpha;  // [N] sigma (raw, before the bbox mask)
+  float* sigma;  // [N] sigma'
+  float4* raw;   // [R*64]
+  // backward
+  float4* draw;  // [R*64] (dc, dalpha)
+  float* dRgb;   // [N][4]
+  float* dAlpha; // [N]
+  float* dBp;    // [N][24]
+  float* dBt;    // [N][24]
+  float* dLp;    // [N][32]
+  float* dLt;    // [N][32]
+  float* dIt;    // [N][32]
+  float* dGt;    // [N][64]
+  const int* out_row;
+  const int* m_rows;
+  const float* d_rgb_map;  // (R,3) upstream or NULL
+  const float* d_pbw;      // (m,24) upstream or NULL
+  const float* d_tbw;
+  const float *rgb_map, *acc_map;
+  int n_rays;
+};
+
+__global__ void k_tr_point_prep(TrainBufs b);
+__global__ void k_tr_softmax_lbs(TrainBufs b);
+__global__ void k_tr_softmax_t(TrainBufs b);
+__global__ void k_tr_raw(TrainBufs b);
+__global__ void k_tr_composite_bwd(TrainBufs b);
+__global__ void k_tr_raw_bwd(TrainBufs b);
+__global__ void k_tr_rows_bwd(TrainBufs b);
+__global__ void k_tr_softmax_bwd_t(TrainBufs b);
+__global__ void k_tr_tpose_bwd(TrainBufs b);
+__global__ void k_tr_softmax_bwd_p(TrainBufs b);
+__global__ void k_tr_latent_grad(const float* dysum, const float* W, int in_ch, int col0, int nout, const float* table,
+                                 const int64_t* li, int add, float* dW, float* dtable);
+__global__ void k_adam(float* p, float* g, float* m, float* v, long n, float lr, float b1, float b2, float eps, float wd,
+                       float bc1, float bc2_sqrt, float clip);
+__global__ void k_tr_loss(TrainBufs b, const float* rgb_gt, const uint8_t* mask, float* acc3);
+__global__ void k_tr_loss_final(const float* acc3, const int* m_rows, float* loss3);
+__global__ void k_tr_loss_grads(TrainBufs b, const float* rgb_gt, const uint8_t* mask, const float* acc3, float* d_rgb,
+                                float* d_pbw_rows, float* d_tbw_rows);
+
+}  // namespace anr

@@ -1,0 +1,467 @@
+// anr_train_capi.hip — C-ABI of the training executor (include/aninerf.h, "training" section).
+//
+// Layer-wise: the kept samples of a 1,024-ray batch (~24k) are few enough that every layer is a
+// GEMM over the whole batch with its activation kept in HBM; the backward runs the same layers in
+// reverse (dX = dY W, dW += dY^T X) plus the per-sample kernels of anr_train.hip. One host read of
+// the kept-sample count per call sizes the GEMMs (the reference syncs ~6x per chunk).
+#include <algorithm>
+#include <cmath>
+#include <string>
+
+#include "../../include/aninerf.h"
+#include "anr_common.h"
+#include "anr_kernels.h"
+#include "anr_train.h"
+#include "anr_ws.h"
+
+using namespace anr;
+
+namespace {
+
+// training workspace = render layout (prefix, incl. raw) + per-sample activations / gradients
+struct TLayout {
+  Layout L;
+  size_t pt, Gp, Ip, Gv, Lp, lbs, Gt, It, Lt, Hp, Ht, Hn, Feat, Alpha, Lat, View, Rgbl;
+  size_t draw, dRgb, dAlpha, dBp, dBt, dLp, dLt, dIt, dGt, dA, dB, dFeat, dLat, dView;
+  size_t ysum, acc3, d_rgb, d_pbw, d_tbw, total;
+};
+
+TLayout tlayout(int n_rays, int chunk, long np, long nt) {
+  TLayout T{};
+  T.L = layout(n_rays, chunk, np, nt, true);
+  size_t o = T.L.total;
+  const size_t N = (size_t)n_rays * 64, R = (size_t)n_rays;
+  auto take = [&](size_t floats) {
+    const size_t at = o;
+    o = align256(o + floats * 4);
+    return at;
+  };
+  T.pt = take(N * 8); T.Gp = take(N * 64); T.Ip = take(N * 32); T.Gv = take(N * 32); T.Lp = take(N * 32);
+  T.lbs = take(N * 16); T.Gt = take(N * 64); T.It = take(N * 32); T.Lt = take(N * 32);
+  T.Hp = take(N * 256 * 8); T.Ht = take(N * 256 * 8); T.Hn = take(N * 256 * 8);
+  T.Feat = take(N * 256); T.Alpha = take(N); T.Lat = take(N * 256); T.View = take(N * 128); T.Rgbl = take(N * 4);
+  T.draw = take(N * 4); T.dRgb = take(N * 4); T.dAlpha = take(N); T.dBp = take(N * 24); T.dBt = take(N * 24);
+  T.dLp = take(N * 32); T.dLt = take(N * 32); T.dIt = take(N * 32); T.dGt = take(N * 64);
+  T.dA = take(N * 256); T.dB = take(N * 256); T.dFeat = take(N * 256); T.dLat = take(N * 256); T.dView = take(N * 128);
+  T.ysum = take(8 * 256); T.acc3 = take(4); T.d_rgb = take(R * 3); T.d_pbw = take(N * 24); T.d_tbw = take(N * 24);
+  T.total = o;
+  return T;
+}
+
+int check_args(const anr_params* p, const anr_frame* f, const float* ray_o, const float* ray_d, const float* near_,
+               const float* far_, int n_rays, const anr_render_opts* o, void* ws) {
+  if (!p || !f || !o || !ws || !ray_o || !ray_d || !near_ || !far_) return fail(ANR_E_ARG, "train: NULL argument");
+  if (o->n_samples != 64) return fail(ANR_E_ARG, "train: only N_samples == 64 is supported");
+  if (o->chunk <= 0 || n_rays <= 0) return fail(ANR_E_ARG, "train: bad chunk / n_rays");
+  for (int i = 0; i < ANR_NUM_TENSORS; ++i)
+    if (!p->t[i]) return fail(ANR_E_ARG, "train: NULL parameter tensor");
+  if (!f->A || !f->R || !f->Th || !f->pbw || !f->tbw || !f->pbounds || !f->tbounds || !f->latent_index)
+    return fail(ANR_E_ARG, "train: NULL frame tensor");
+  return ANR_OK;
+}
+
+struct Exec {
+  hipStream_t s;
+  int n;  // kept samples (host copy)
+
+  int gemm(GemmArgs g, int M) {
+    if (M <= 0 || g.N <= 0) return ANR_OK;
+    int Ktot = 0;
+    for (int q = 0; q < g.nseg; ++q) Ktot += g.seg[q].K;
+    if (g.ksplit < 1) g.ksplit = 1;
+    dim3 grid((g.N + 63) / 64, (M + 63) / 64, g.ksplit);
+    g.M = M;
+    hipLaunchKernelGGL(k_gemm, grid, dim3(256), 0, s, g);
+    return check_launch("k_gemm");
+  }
+
+  // Y[n][Nout] = act( X0[:, :K0] W[:, c0:c0+K0]^T (+ X1 W[:, c1:c1+K1]^T) + bias )
+  int fwd(float* Y, int ldY, int Nout, const float* W, int in_ch, const float* bias, bool relu, const float* X0, int ld0,
+          int K0, int c0, const float* X1 = nullptr, int ld1 = 0, int K1 = 0, int c1 = 0) {
+    GemmArgs g{};
+    g.N = Nout;
+    g.nseg = X1 ? 2 : 1;
+    g.seg[0] = GemmSeg{X0, ld0, 1, W + c0, 1, in_ch, K0};
+    if (X1) g.seg[1] = GemmSeg{X1, ld1, 1, W + c1, 1, in_ch, K1};
+    g.C = Y; g.ldc = ldY; g.bias = bias; g.relu = relu ? 1 : 0; g.ksplit = 1;
+    return gemm(g, n);
+  }
+
+  // dW[:, c0:c0+K] += dY^T X (split-K over samples, atomics)
+  int wgrad(float* dW, int in_ch, int c0, int Nout, const float* dY, int ldY, const float* X, int ldX, int K) {
+    GemmArgs g{};
+    g.N = K;
+    g.nseg = 1;
+    g.seg[0] = GemmSeg{dY, 1, ldY, X, ldX, 1, n};
+    g.C = dW + c0; g.ldc = in_ch; g.atomic = 1;
+    g.ksplit = (n + 511) / 512;
+    return gemm(g, Nout);
+  }
+
+  // dX (+)= dY W[:, c0:c0+K] (masked by mask > 0)
+  int xgrad(float* dX, int ldX, int K, const float* dY, int ldY, int Nout, const float* W, int in_ch, int c0,
+            const float* mask, int ldm, bool accumulate, const float* dY2 = nullptr, int ldY2 = 0, int Nout2 = 0,
+            const float* W2 = nullptr, int in_ch2 = 0) {
+    GemmArgs g{};
+    g.N = K;
+    g.nseg = dY2 ? 2 : 1;
+    g.seg[0] = GemmSeg{dY, ldY, 1, W + c0, in_ch, 1, Nout};
+    if (dY2) g.seg[1] = GemmSeg{dY2, ldY2, 1, W2 + c0, in_ch2, 1, Nout2};
+    g.C = dX; g.ldc = ldX; g.mask = mask; g.ldm = ldm; g.accumulate = accumulate ? 1 : 0; g.ksplit = 1;
+    return gemm(g, n);
+  }
+
+  int colsum(const float* X, int ld, int N, float* out) {
+    if (n <= 0) return ANR_OK;
+    const int rpb = 256;
+    hipLaunchKernelGGL(k_colsum, dim3((N + 63) / 64, (n + rpb - 1) / rpb), dim3(256), 0, s, X, (long)ld, n,
+                       (const int*)nullptr, N, out, rpb);
+    return check_launch("k_colsum");
+  }
+};
+
+int read_count(const int* dev, int* host, hipStream_t s) {
+  if (hipMemcpyAsync(host, dev, sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return fail(ANR_E_HIP, "kept-count readback failed");
+  return ANR_OK;
+}
+
+TrainBufs bufs(const TLayout& T, char* ws, const anr_frame* f, const float* ray_o, const float* ray_d,
+               const float* near_, const float* far_, int R, const anr_render_opts* o) {
+  TrainBufs b{};
+  const Layout& L = T.L;
+  b.list = (const int*)(ws + L.list);
+  b.n_kept = (const int*)(ws + L.counts);
+  b.m_rows = (const int*)(ws + L.counts) + 1;
+  b.out_row = (const int*)(ws + L.out_row);
+  b.ray_o = ray_o; b.ray_d = ray_d; b.near_ = near_; b.far_ = far_; b.t_rand = o->t_rand;
+  b.R = f->R; b.Th = f->Th; b.A = f->A;
+  b.pbw = f->pbw; b.pbounds = f->pbounds; b.tbw = f->tbw; b.tbounds = f->tbounds;
+  b.pX = f->pbw_dims[0]; b.pY = f->pbw_dims[1]; b.pZ = f->pbw_dims[2];
+  b.tX = f->tbw_dims[0]; b.tY = f->tbw_dims[1]; b.tZ = f->tbw_dims[2];
+  b.pt = (float*)(ws + T.pt); b.Gp = (float*)(ws + T.Gp); b.Ip = (float*)(ws + T.Ip); b.Gv = (float*)(ws + T.Gv);
+  b.Lp = (float*)(ws + T.Lp); b.Bp = (float*)(ws + L.pbw_rows); b.lbs = (float*)(ws + T.lbs);
+  b.Gt = (float*)(ws + T.Gt); b.It = (float*)(ws + T.It); b.Lt = (float*)(ws + T.Lt); b.Bt = (float*)(ws + L.tbw_rows);
+  b.Rgbl = (float*)(ws + T.Rgbl); b.Alpha = (float*)(ws + T.Alpha); b.sigma = (float*)(ws + L.sigma);
+  b.raw = (float4*)(ws + L.raw);
+  b.draw = (float4*)(ws + T.draw); b.dRgb = (float*)(ws + T.dRgb); b.dAlpha = (float*)(ws + T.dAlpha);
+  b.dBp = (float*)(ws + T.dBp); b.dBt = (float*)(ws + T.dBt); b.dLp = (float*)(ws + T.dLp);
+  b.dLt = (float*)(ws + T.dLt); b.dIt = (float*)(ws + T.dIt); b.dGt = (float*)(ws + T.dGt);
+  b.n_rays = R;
+  return b;
+}
+
+#define PT(i) (p->t[i])
+#define FOLD(k) ((const float*)(ws + T.L.fold) + 256 * (k))
+
+// BW MLP forward over n samples (tpose_nerf_network.py:55-77); H = 8 x [N][256], logits [N][32]
+int bw_forward(Exec& e, const anr_params* p, const float* G, float* H, float* logits, long N, const float* fold0,
+               const float* fold5) {
+  const long S = N * 256;
+  ANR_TRY(e.fwd(H, 256, 256, PT(28), 191, fold0, true, G, 64, 63, 0));
+  for (int l = 1; l < 8; ++l) {
+    const float* Xp = H + (l - 1) * S;
+    if (l == 5) {
+      ANR_TRY(e.fwd(H + l * S, 256, 256, PT(38), 447, fold5, true, G, 64, 63, 0, Xp, 256, 256, 191));
+    } else {
+      ANR_TRY(e.fwd(H + l * S, 256, 256, PT(28 + 2 * l), 256, PT(29 + 2 * l), true, Xp, 256, 256, 0));
+    }
+  }
+  return e.fwd(logits, 32, 24, PT(44), 256, PT(45), false, H + 7 * S, 256, 256, 0);
+}
+
+// BW MLP backward from d logits; accumulates weight/bias grads; dG (+)= input-gamma gradient if given.
+// ysum: 2 x 256 scratch for the latent-column gradients of layers 0 and 5.
+int bw_backward(Exec& e, const anr_params* p, float* const* g, const float* G, const float* H, const float* dlog,
+                float* dA, float* dB, float* dG, long N, float* ysum, const int64_t* li, int add, hipStream_t s) {
+  const long S = N * 256;
+  // bw_fc
+  ANR_TRY(e.wgrad(g[44], 256, 0, 24, dlog, 32, H + 7 * S, 256, 256));
+  ANR_TRY(e.colsum(dlog, 32, 24, g[45]));
+  ANR_TRY(e.xgrad(dA, 256, 256, dlog, 32, 24, PT(44), 256, 0, H + 7 * S, 256, false));
+  float* cur = dA;
+  float* nxt = dB;
+  for (int l = 7; l >= 0; --l) {
+    const int wi = 28 + 2 * l, bi = wi + 1;
+    const int in_ch = l == 0 ? 191 : (l == 5 ? 447 : 256);
+    if (l == 0 || l == 5) {
+      float* ys = ysum + (l == 5 ? 256 : 0);
+      if (hipMemsetAsync(ys, 0, 256 * 4, s) != hipSuccess) return fail(ANR_E_HIP, "memset");
+      ANR_TRY(e.colsum(cur, 256, 256, ys));
+      hipLaunchKernelGGL(k_tr_latent_grad, dim3(257), dim3(128), 0, s, (const float*)ys, PT(wi), in_ch, 63, 256,
+                         PT(27), li, add, g[wi], g[27]);
+      ANR_TRY(check_launch("k_tr_latent_grad"));
+      // bias grad = same column sum
+      ANR_TRY(e.colsum(cur, 256, 256, g[bi]));
+      ANR_TRY(e.wgrad(g[wi], in_ch, 0, 256, cur, 256, G, 64, 63));
+      if (dG) ANR_TRY(e.xgrad(dG, 64, 63, cur, 256, 256, PT(wi), in_ch, 0, nullptr, 0, true));
+      if (l == 5) {
+        ANR_TRY(e.wgrad(g[wi], in_ch, 191, 256, cur, 256, H + 4 * S, 256, 256));
+        ANR_TRY(e.xgrad(nxt, 256, 256, cur, 256, 256, PT(wi), in_ch, 191, H + 4 * S, 256, false));
+      }
+    } else {
+      ANR_TRY(e.colsum(cur, 256, 256, g[bi]));
+      ANR_TRY(e.wgrad(g[wi], 256, 0, 256, cur, 256, H + (l - 1) * S, 256, 256));
+      ANR_TRY(e.xgrad(nxt, 256, 256, cur, 256, 256, PT(wi), 256, 0, H + (l - 1) * S, 256, false));
+    }
+    if (l > 0) {
+      float* t = cur;
+      cur = nxt;
+      nxt = t;
+    }
+  }
+  return ANR_OK;
+}
+
+int train_forward(const anr_params* p, const anr_frame* f, const float* ray_o, const float* ray_d, const float* near_,
+                  const float* far_, int R, const anr_render_opts* o, const anr_render_out* out, char* ws,
+                  const TLayout& T, hipStream_t s, Exec& e) {
+  float4* raw = (float4*)(ws + T.L.raw);
+  ANR_TRY(stage_frontend(p, f, ray_o, ray_d, near_, far_, R, o, ws, T.L, raw, s));
+  ANR_TRY(read_count((const int*)(ws + T.L.counts), &e.n, s));
+  const int n = e.n;
+  const long N = (long)R * 64;
+  TrainBufs b = bufs(T, ws, f, ray_o, ray_d, near_, far_, R, o);
+  const int g1 = (n + 255) / 256;
+  if (n > 0) {
+    hipLaunchKernelGGL(k_tr_point_prep, dim3((n + 3) / 4), dim3(256), 0, s, b);
+    ANR_TRY(check_launch("k_tr_point_prep"));
+  }
+  // pose-space BW MLP (latent_index + 1), softmax + LBS, T-pose BW MLP (latent 0)
+  ANR_TRY(bw_forward(e, p, b.Gp, (float*)(ws + T.Hp), b.Lp, N, FOLD(0), FOLD(2)));
+  if (n > 0) {
+    hipLaunchKernelGGL(k_tr_softmax_lbs, dim3(g1), dim3(256), 0, s, b);
+    ANR_TRY(check_launch("k_tr_softmax_lbs"));
+  }
+  ANR_TRY(bw_forward(e, p, b.Gt, (float*)(ws + T.Ht), b.Lt, N, FOLD(1), FOLD(3)));
+  if (n > 0) {
+    hipLaunchKernelGGL(k_tr_softmax_t, dim3(g1), dim3(256), 0, s, b);
+    ANR_TRY(check_launch("k_tr_softmax_t"));
+  }
+  // canonical NeRF (TPoseHuman.calculate_alpha_rgb)
+  float* Hn = (float*)(ws + T.Hn);
+  const long S = N * 256;
+  ANR_TRY(e.fwd(Hn, 256, 256, PT(1), 63, PT(2), true, b.Gt, 64, 63, 0));
+  for (int l = 1; l < 8; ++l) {
+    if (l == 5) {
+      ANR_TRY(e.fwd(Hn + l * S, 256, 256, PT(11), 319, PT(12), true, b.Gt, 64, 63, 0, Hn + 4 * S, 256, 256, 63));
+    } else {
+      ANR_TRY(e.fwd(Hn + l * S, 256, 256, PT(1 + 2 * l), 256, PT(2 + 2 * l), true, Hn + (l - 1) * S, 256, 256, 0));
+    }
+  }
+  float* Feat = (float*)(ws + T.Feat);
+  float* Lat = (float*)(ws + T.Lat);
+  float* View = (float*)(ws + T.View);
+  ANR_TRY(e.fwd(b.Alpha, 1, 1, PT(17), 256, PT(18), false, Hn + 7 * S, 256, 256, 0));
+  ANR_TRY(e.fwd(Feat, 256, 256, PT(19), 256, PT(20), false, Hn + 7 * S, 256, 256, 0));
+  ANR_TRY(e.fwd(Lat, 256, 256, PT(21), 384, FOLD(4), false, Feat, 256, 256, 0));
+  ANR_TRY(e.fwd(View, 128, 128, PT(23), 283, PT(24), true, Lat, 256, 256, 0, b.Gv, 32, 27, 256));
+  ANR_TRY(e.fwd(b.Rgbl, 4, 3, PT(25), 128, PT(26), false, View, 128, 128, 0));
+  if (n > 0) {
+    hipLaunchKernelGGL(k_tr_raw, dim3(g1), dim3(256), 0, s, b);
+    ANR_TRY(check_launch("k_tr_raw"));
+  }
+  ANR_TRY(stage_alpha_ind(R, o, ws, T.L, s));
+  return stage_composite(near_, far_, R, o, raw, out, nullptr, s);
+}
+
+int train_backward(const anr_params* p, float* const* g, const anr_frame* f, const float* ray_o, const float* ray_d,
+                   const float* near_, const float* far_, int R, const anr_render_opts* o, const float* d_rgb,
+                   const float* d_pbw, const float* d_tbw, char* ws, const TLayout& T, hipStream_t s, Exec& e) {
+  const int n = e.n;
+  const long N = (long)R * 64;
+  const long S = N * 256;
+  TrainBufs b = bufs(T, ws, f, ray_o, ray_d, near_, far_, R, o);
+  b.d_rgb_map = d_rgb; b.d_pbw = d_pbw; b.d_tbw = d_tbw;
+  const int g1 = (n + 255) / 256;
+  if (n <= 0) return ANR_OK;
+  float* Hp = (float*)(ws + T.Hp);
+  float* Ht = (float*)(ws + T.Ht);
+  float* Hn = (float*)(ws + T.Hn);
+  float* Feat = (float*)(ws + T.Feat);
+  float* Lat = (float*)(ws + T.Lat);
+  float* View = (float*)(ws + T.View);
+  float* dA = (float*)(ws + T.dA);
+  float* dB = (float*)(ws + T.dB);
+  float* dFeat = (float*)(ws + T.dFeat);
+  float* dLat = (float*)(ws + T.dLat);
+  float* dView = (float*)(ws + T.dView);
+  float* ysum = (float*)(ws + T.ysum);
+  if (hipMemsetAsync(b.dGt, 0, (size_t)n * 64 * 4, s) != hipSuccess) return fail(ANR_E_HIP, "memset");
+
+  // compositing + raw activations
+  hipLaunchKernelGGL(k_tr_composite_bwd, dim3((R + 3) / 4), dim3(256), 0, s, b);
+  ANR_TRY(check_launch("k_tr_composite_bwd"));
+  hipLaunchKernelGGL(k_tr_raw_bwd, dim3(g1), dim3(256), 0, s, b);
+  ANR_TRY(check_launch("k_tr_raw_bwd"));
+  // rgb_fc, view_fc (ReLU), latent_fc (latent folded), feature_fc || alpha_fc
+  ANR_TRY(e.wgrad(g[25], 128, 0, 3, b.dRgb, 4, View, 128, 128));
+  ANR_TRY(e.colsum(b.dRgb, 4, 3, g[26]));
+  ANR_TRY(e.xgrad(dView, 128, 128, b.dRgb, 4, 3, PT(25), 128, 0, View, 128, false));
+  ANR_TRY(e.wgrad(g[23], 283, 0, 128, dView, 128, Lat, 256, 256));
+  ANR_TRY(e.wgrad(g[23], 283, 256, 128, dView, 128, b.Gv, 32, 27));
+  ANR_TRY(e.colsum(dView, 128, 128, g[24]));
+  ANR_TRY(e.xgrad(dLat, 256, 256, dView, 128, 128, PT(23), 283, 0, nullptr, 0, false));
+  {
+    float* ys = ysum + 512;
+    if (hipMemsetAsync(ys, 0, 256 * 4, s) != hipSuccess) return fail(ANR_E_HIP, "memset");
+    ANR_TRY(e.colsum(dLat, 256, 256, ys));
+    ANR_TRY(e.colsum(dLat, 256, 256, g[22]));
+    hipLaunchKernelGGL(k_tr_latent_grad, dim3(257), dim3(128), 0, s, (const float*)ys, PT(21), 384, 256, 256, PT(0),
+                       f->latent_index, 0, g[21], g[0]);
+    ANR_TRY(check_launch("k_tr_latent_grad(nf_latent)"));
+  }
+  ANR_TRY(e.wgrad(g[21], 384, 0, 256, dLat, 256, Feat, 256, 256));
+  ANR_TRY(e.xgrad(dFeat, 256, 256, dLat, 256, 256, PT(21), 384, 0, nullptr, 0, false));
+  ANR_TRY(e.wgrad(g[19], 256, 0, 256, dFeat, 256, Hn + 7 * S, 256, 256));
+  ANR_TRY(e.colsum(dFeat, 256, 256, g[20]));
+  ANR_TRY(e.wgrad(g[17], 256, 0, 1, b.dAlpha, 1, Hn + 7 * S, 256, 256));
+  ANR_TRY(e.colsum(b.dAlpha, 1, 1, g[18]));
+  ANR_TRY(e.xgrad(dA, 256, 256, dFeat, 256, 256, PT(19), 256, 0, Hn + 7 * S, 256, false, b.dAlpha, 1, 1, PT(17), 256));
+  // NeRF pts_linears 7..0 (skip at 5: [gamma(x_T), net])
+  float* cur = dA;
+  float* nxt = dB;
+  for (int l = 7; l >= 0; --l) {
+    const int wi = 1 + 2 * l, bi = wi + 1;
+    ANR_TRY(e.colsum(cur, 256, 256, g[bi]));
+    if (l == 0) {
+      ANR_TRY(e.wgrad(g[wi], 63, 0, 256, cur, 256, b.Gt, 64, 63));
+      ANR_TRY(e.xgrad(b.dGt, 64, 63, cur, 256, 256, PT(wi), 63, 0, nullptr, 0, true));
+    } else if (l == 5) {
+      ANR_TRY(e.wgrad(g[wi], 319, 0, 256, cur, 256, b.Gt, 64, 63));
+      ANR_TRY(e.wgrad(g[wi], 319, 63, 256, cur, 256, Hn + 4 * S, 256, 256));
+      ANR_TRY(e.xgrad(b.dGt, 64, 63, cur, 256, 256, PT(wi), 319, 0, nullptr, 0, true));
+      ANR_TRY(e.xgrad(nxt, 256, 256, cur, 256, 256, PT(wi), 319, 63, Hn + 4 * S, 256, false));
+    } else {
+      ANR_TRY(e.wgrad(g[wi], 256, 0, 256, cur, 256, Hn + (l - 1) * S, 256, 256));
+      ANR_TRY(e.xgrad(nxt, 256, 256, cur, 256, 256, PT(wi), 256, 0, Hn + (l - 1) * S, 256, false));
+    }
+    if (l > 0) {
+      float* t = cur;
+      cur = nxt;
+      nxt = t;
+    }
+  }
+  // upstream pbw / tbw row gradients; T-pose BW backward (latent row 0)
+  hipLaunchKernelGGL(k_tr_rows_bwd, dim3(g1), dim3(256), 0, s, b);
+  ANR_TRY(check_launch("k_tr_rows_bwd"));
+  hipLaunchKernelGGL(k_tr_softmax_bwd_t, dim3(g1), dim3(256), 0, s, b);
+  ANR_TRY(check_launch("k_tr_softmax_bwd_t"));
+  ANR_TRY(bw_backward(e, p, g, b.Gt, Ht, b.dLt, dA, dB, b.dGt, N, ysum, nullptr, 0, s));  // bw_latent row 0
+  // x_T gradient (gamma + init_tbw lookup) -> LBS -> d pbw; pose BW backward (latent row li + 1)
+  hipLaunchKernelGGL(k_tr_tpose_bwd, dim3(g1), dim3(256), 0, s, b);
+  ANR_TRY(check_launch("k_tr_tpose_bwd"));
+  hipLaunchKernelGGL(k_tr_softmax_bwd_p, dim3(g1), dim3(256), 0, s, b);
+  ANR_TRY(check_launch("k_tr_softmax_bwd_p"));
+  return ANR_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t anr_train_workspace_bytes(int n_rays, const anr_render_opts* o, const anr_frame* f) {
+  if (!o || !f || n_rays <= 0) return 0;
+  const long np = (long)f->pbw_dims[0] * f->pbw_dims[1] * f->pbw_dims[2];
+  const long nt = (long)f->tbw_dims[0] * f->tbw_dims[1] * f->tbw_dims[2];
+  return tlayout(n_rays, o->chunk, np, nt).total;
+}
+
+int anr_train_fwd(const anr_params* p, const anr_frame* f, const float* ray_o, const float* ray_d, const float* near_,
+                  const float* far_, int n_rays, const anr_render_opts* o, const anr_render_out* out, void* workspace,
+                  size_t ws_bytes, void* stream) {
+  ANR_TRY(check_args(p, f, ray_o, ray_d, near_, far_, n_rays, o, workspace));
+  if (!out || !out->rgb_map || !out->acc_map || !out->depth_map) return fail(ANR_E_ARG, "anr_train_fwd: NULL output");
+  const long np = (long)f->pbw_dims[0] * f->pbw_dims[1] * f->pbw_dims[2];
+  const long nt = (long)f->tbw_dims[0] * f->tbw_dims[1] * f->tbw_dims[2];
+  const TLayout T = tlayout(n_rays, o->chunk, np, nt);
+  if (ws_bytes < T.total) return fail(ANR_E_WORKSPACE, "anr_train_fwd: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  char* ws = (char*)workspace;
+  Exec e{s, 0};
+  ANR_TRY(train_forward(p, f, ray_o, ray_d, near_, far_, n_rays, o, out, ws, T, s, e));
+  if (out->raw &&
+      hipMemcpyAsync(out->raw, ws + T.L.raw, (size_t)n_rays * 64 * 16, hipMemcpyDeviceToDevice, s) != hipSuccess)
+    return fail(ANR_E_HIP, "raw copy failed");
+  return ANR_OK;
+}
+
+int anr_train_bwd(const anr_params* p, float* const* grads, const anr_frame* f, const float* ray_o, const float* ray_d,
+                  const float* near_, const float* far_, int n_rays, const anr_render_opts* o, const float* d_rgb_map,
+                  const float* d_pbw, const float* d_tbw, void* workspace, size_t ws_bytes, void* stream) {
+  ANR_TRY(check_args(p, f, ray_o, ray_d, near_, far_, n_rays, o, workspace));
+  if (!grads) return fail(ANR_E_ARG, "anr_train_bwd: NULL grads");
+  for (int i = 0; i < ANR_NUM_TENSORS; ++i)
+    if (!grads[i]) return fail(ANR_E_ARG, "anr_train_bwd: NULL grad tensor");
+  const long np = (long)f->pbw_dims[0] * f->pbw_dims[1] * f->pbw_dims[2];
+  const long nt = (long)f->tbw_dims[0] * f->tbw_dims[1] * f->tbw_dims[2];
+  const TLayout T = tlayout(n_rays, o->chunk, np, nt);
+  if (ws_bytes < T.total) return fail(ANR_E_WORKSPACE, "anr_train_bwd: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  char* ws = (char*)workspace;
+  Exec e{s, 0};
+  ANR_TRY(read_count((const int*)(ws + T.L.counts), &e.n, s));
+  ANR_TRY(train_backward(p, grads, f, ray_o, ray_d, near_, far_, n_rays, o, d_rgb_map, d_pbw, d_tbw, ws, T, s, e));
+  if (e.n <= 0) return ANR_OK;
+  // pose BW MLP backward: d logits were produced by k_tr_softmax_bwd_p
+  const long N = (long)n_rays * 64;
+  float* ysum = (float*)(ws + T.ysum);
+  ANR_TRY(bw_backward(e, p, grads, (const float*)(ws + T.Gp), (const float*)(ws + T.Hp), (const float*)(ws + T.dLp),
+                      (float*)(ws + T.dA), (float*)(ws + T.dB), nullptr, N, ysum + 1024, f->latent_index, 1, s));
+  return ANR_OK;
+}
+
+int anr_train_step(const anr_params* p, float* const* grads, const anr_frame* f, const float* ray_o,
+                   const float* ray_d, const float* near_, const float* far_, int n_rays, const anr_render_opts* o,
+                   const float* rgb_gt, const uint8_t* mask_at_box, const anr_render_out* out, float* loss3,
+                   void* workspace, size_t ws_bytes, void* stream) {
+  ANR_TRY(check_args(p, f, ray_o, ray_d, near_, far_, n_rays, o, workspace));
+  if (!grads || !rgb_gt || !loss3 || !out || !out->rgb_map || !out->acc_map || !out->depth_map)
+    return fail(ANR_E_ARG, "anr_train_step: NULL argument");
+  for (int i = 0; i < ANR_NUM_TENSORS; ++i)
+    if (!grads[i]) return fail(ANR_E_ARG, "anr_train_step: NULL grad tensor");
+  const long np = (long)f->pbw_dims[0] * f->pbw_dims[1] * f->pbw_dims[2];
+  const long nt = (long)f->tbw_dims[0] * f->tbw_dims[1] * f->tbw_dims[2];
+  const TLayout T = tlayout(n_rays, o->chunk, np, nt);
+  if (ws_bytes < T.total) return fail(ANR_E_WORKSPACE, "anr_train_step: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  char* ws = (char*)workspace;
+  Exec e{s, 0};
+  ANR_TRY(train_forward(p, f, ray_o, ray_d, near_, far_, n_rays, o, out, ws, T, s, e));
+  // fused losses (tpose_trainer.py:50-63) and their upstream gradients
+  TrainBufs b = bufs(T, ws, f, ray_o, ray_d, near_, far_, n_rays, o);
+  b.rgb_map = out->rgb_map;
+  float* acc3 = (float*)(ws + T.acc3);
+  if (hipMemsetAsync(acc3, 0, 16, s) != hipSuccess) return fail(ANR_E_HIP, "memset");
+  const long N = (long)n_rays * 64;
+  const int gx = (int)((std::max<long>(n_rays, N) + 255) / 256);
+  hipLaunchKernelGGL(k_tr_loss, dim3(gx, 2), dim3(256), 0, s, b, rgb_gt, mask_at_box, acc3);
+  ANR_TRY(check_launch("k_tr_loss"));
+  hipLaunchKernelGGL(k_tr_loss_final, dim3(1), dim3(1), 0, s, (const float*)acc3, b.m_rows, loss3);
+  ANR_TRY(check_launch("k_tr_loss_final"));
+  float* d_rgb = (float*)(ws + T.d_rgb);
+  float* d_pbw = (float*)(ws + T.d_pbw);
+  float* d_tbw = (float*)(ws + T.d_tbw);
+  hipLaunchKernelGGL(k_tr_loss_grads, dim3(gx, 2), dim3(256), 0, s, b, rgb_gt, mask_at_box, (const float*)acc3, d_rgb,
+                     d_pbw, d_tbw);
+  ANR_TRY(check_launch("k_tr_loss_grads"));
+  ANR_TRY(train_backward(p, grads, f, ray_o, ray_d, near_, far_, n_rays, o, d_rgb, d_pbw, d_tbw, ws, T, s, e));
+  if (e.n <= 0) return ANR_OK;
+  float* ysum = (float*)(ws + T.ysum);
+  return bw_backward(e, p, grads, (const float*)(ws + T.Gp), (const float*)(ws + T.Hp), (const float*)(ws + T.dLp),
+                     (float*)(ws + T.dA), (float*)(ws + T.dB), nullptr, N, ysum + 1024, f->latent_index, 1, s);
+}
+
+int anr_adam(float* param, float* grad, float* exp_avg, float* exp_avg_sq, long n, float lr, float beta1, float beta2,
+             float eps, float weight_decay, int step, float clip_value, void* stream) {
+  if (!param || !grad || !exp_avg || !exp_avg_sq || n < 0 || step < 1) return fail(ANR_E_ARG, "anr_adam: bad arguments");
+  if (n == 0) return ANR_OK;
+  const float bc1 = 1.0f - powf(beta1, (float)step);
+  const float bc2s = sqrtf(1.0f - powf(beta2, (float)step));
+  hipLaunchKernelGGL(k_adam, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, param, grad, exp_avg,
+                     exp_avg_sq, n, lr, beta1, beta2, eps, weight_decay, bc1, bc2s, clip_value);
+  return check_launch("k_adam");
+}
+
+}  // extern "C"

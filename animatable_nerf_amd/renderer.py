@@ -1,12 +1,17 @@
 """Renderer plugin: ``Renderer(net).render(batch)`` (tpose_renderer.py:159-186) on the HIP library.
 
-One call renders every ray of the batch through the C-ABI (``anr_render_fwd``): sampling,
-prefilter, deformation, canonical NeRF and compositing run as device kernels, with the reference's
-2048-ray chunk semantics (forced argmin keep, forced argmax loss row) preserved without a chunk
-loop on the host. Output keys and shapes are the reference's:
-``rgb_map (1,R,3)``, ``acc_map (1,R)``, ``depth_map (1,R)``, ``raw (1,R*64,4)``, ``pbw/tbw (1,m,24)``.
-As in the reference (tpose_renderer.py:154-155), outputs that do not require grad are returned on
-the CPU by ``render``; ``render_device`` keeps them in HBM.
+One call renders every ray of the batch through the C-ABI: sampling, prefilter, deformation,
+canonical NeRF and compositing run as device kernels, with the reference's 2048-ray chunk semantics
+(forced argmin keep, forced argmax loss row) preserved without a chunk loop on the host. Output keys
+and shapes are the reference's: ``rgb_map (1,R,3)``, ``acc_map (1,R)``, ``depth_map (1,R)``,
+``raw (1,R*64,4)``, ``pbw/tbw (1,m,24)``.
+
+* no grad (evaluation, run.py:63-69): the fused single-kernel network (``anr_render_fwd``); outputs
+  are moved to the CPU by ``render`` as the reference does (tpose_renderer.py:154-155),
+  ``render_device`` keeps them in HBM;
+* grad enabled (training, tpose_trainer.py:22): the layer-wise training executor
+  (``anr_train_fwd``) behind a ``torch.autograd.Function`` whose backward is ``anr_train_bwd``, so
+  the reference's ``loss.backward()`` / optimizer loop drives it unchanged.
 """
 import ctypes
 
@@ -16,10 +21,51 @@ from . import _lib
 from . import config as _config
 
 CHUNK = 2048  # tpose_renderer.py:170
+RAY_KEYS = ('ray_o', 'ray_d', 'near', 'far')
+FRAME_KEYS = ('A', 'R', 'Th', 'pbw', 'pbounds', 'tbw', 'tbounds')
 
 
 def _f32(t, device):
     return t.to(device=device, dtype=torch.float32).contiguous()
+
+
+class _Call:
+    """Device tensors + C structs of one render/train call (keeps the tensors alive)."""
+
+    def __init__(self, renderer, batch, t_rand):
+        cfg = renderer.cfg
+        self.dev = dev = renderer.device()
+        self.rays = {k: _f32(batch[k], dev) for k in RAY_KEYS}
+        self.R = R = self.rays['ray_o'].shape[1]
+        ns = int(cfg.N_samples)
+        self.t_rand = None if t_rand is None else _f32(t_rand, dev).reshape(R, ns)
+        fr = {k: _f32(batch[k], dev) for k in FRAME_KEYS}
+        self.fr = fr
+        self.li = batch['latent_index'].to(device=dev, dtype=torch.int64).reshape(-1).contiguous()
+        f = _lib.Frame()
+        f.A, f.R, f.Th = fr['A'].data_ptr(), fr['R'].data_ptr(), fr['Th'].data_ptr()
+        f.pbw, f.pbounds = fr['pbw'].data_ptr(), fr['pbounds'].data_ptr()
+        f.tbw, f.tbounds = fr['tbw'].data_ptr(), fr['tbounds'].data_ptr()
+        for i in range(3):
+            f.pbw_dims[i] = fr['pbw'].shape[1 + i]
+            f.tbw_dims[i] = fr['tbw'].shape[1 + i]
+        f.latent_index = self.li.data_ptr()
+        self.frame = f
+        o = _lib.RenderOpts()
+        o.n_samples = ns
+        o.chunk = int(cfg.get('chunk', CHUNK))
+        o.norm_th = float(cfg.norm_th)
+        o.train_th = float(cfg.train_th)
+        o.t_rand = self.t_rand.data_ptr() if self.t_rand is not None else None
+        self.opts = o
+        self.rgb = torch.empty((1, R, 3), device=dev)
+        self.acc = torch.empty((1, R), device=dev)
+        self.depth = torch.empty((1, R), device=dev)
+        self.raw = torch.empty((1, R * ns, 4), device=dev)
+        self.out = _lib.RenderOut(self.rgb.data_ptr(), self.acc.data_ptr(), self.depth.data_ptr(), self.raw.data_ptr())
+
+    def ray_ptrs(self):
+        return [_lib.ptr(self.rays[k]) for k in RAY_KEYS]
 
 
 class Renderer:
@@ -30,10 +76,14 @@ class Renderer:
         self._packed = None
         self._pack_key = None
         self._ws = None
+        self._tws = None
         self.last_counts = None
 
+    def device(self):
+        return next(self.net.parameters()).device
+
     # ---- weights --------------------------------------------------------------------------
-    def params(self):
+    def params(self, pack=True):
         ts = [t.detach() for t in self.net.core_tensors()]
         dev = ts[0].device
         if dev.type != 'cuda':
@@ -45,7 +95,9 @@ class Renderer:
         for i, t in enumerate(ts):
             p.t[i] = t.data_ptr()
         p.num_train_frame = self.net.num_train_frame
-        key = tuple((t.data_ptr(), t._version) for t in ts)
+        if not pack:
+            return p
+        key = (getattr(self.net, '_anr_weights_epoch', 0),) + tuple((t.data_ptr(), t._version) for t in ts)
         if self._packed is None or self._packed.device != dev:
             self._packed = torch.empty(self.lib.anr_params_packed_bytes(), dtype=torch.uint8, device=dev)
             self._pack_key = None
@@ -56,86 +108,109 @@ class Renderer:
             self._pack_key = key
         return p
 
+    def _workspace(self, attr, nbytes, dev):
+        ws = getattr(self, attr)
+        if ws is None or ws.numel() < nbytes or ws.device != dev:
+            ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+            setattr(self, attr, ws)
+        return ws
+
+    def _counts(self, ws, R):
+        addr = self.lib.anr_render_counts(_lib.ptr(ws), R)
+        base = ws.data_ptr()
+        c = ws[addr - base:addr - base + 8].view(torch.int32).cpu()  # host sync
+        self.last_counts = (int(c[0]), int(c[1]))
+        return self.last_counts
+
+    def _bw_rows(self, ws, R, dev):
+        _, m = self._counts(ws, R)
+        pbw = torch.empty((1, m, 24), device=dev)
+        tbw = torch.empty((1, m, 24), device=dev)
+        if m > 0:
+            _lib.check(self.lib.anr_render_bw_rows(_lib.ptr(ws), R, _lib.ptr(pbw), _lib.ptr(tbw), _lib.stream_ptr(dev)),
+                       'anr_render_bw_rows')
+        return pbw, tbw
+
+    def _t_rand(self, R, dev, t_rand):
+        if t_rand is None and self.cfg.perturb > 0 and self.net.training:
+            t_rand = torch.rand((R, int(self.cfg.N_samples)), device=dev)
+        return t_rand
+
     # ---- render -----------------------------------------------------------------------------
     def render_device(self, batch, t_rand=None, bw_rows=True):
-        """Render on the GPU; all returned tensors stay in HBM. ``t_rand`` (R, N_samples) overrides
-        the stratification draws (tests); by default they are drawn when perturb > 0 and the
-        network is in training mode (tpose_renderer.py:29-36)."""
+        """Evaluation render on the GPU (fused network kernel); all returned tensors stay in HBM.
+        ``t_rand`` (R, N_samples) overrides the stratification draws (tests); by default they are
+        drawn when perturb > 0 and the network is in training mode (tpose_renderer.py:29-36)."""
         p = self.params()
         dev = self._packed.device
-        ray_o = _f32(batch['ray_o'], dev)
-        ray_d = _f32(batch['ray_d'], dev)
-        near = _f32(batch['near'], dev)
-        far = _f32(batch['far'], dev)
-        R = ray_o.shape[1]
-        ns = int(self.cfg.N_samples)
-        if t_rand is None and self.cfg.perturb > 0 and self.net.training:
-            t_rand = torch.rand((R, ns), device=dev)
-        if t_rand is not None:
-            t_rand = _f32(t_rand, dev).reshape(R, ns)
-        keep_alive = [ray_o, ray_d, near, far, t_rand]
-
-        f = _lib.Frame()
-        fr = {k: _f32(batch[k], dev) for k in ('A', 'R', 'Th', 'pbw', 'pbounds', 'tbw', 'tbounds')}
-        li = batch['latent_index'].to(device=dev, dtype=torch.int64).reshape(-1).contiguous()
-        keep_alive += list(fr.values()) + [li]
-        f.A, f.R, f.Th = fr['A'].data_ptr(), fr['R'].data_ptr(), fr['Th'].data_ptr()
-        f.pbw, f.pbounds = fr['pbw'].data_ptr(), fr['pbounds'].data_ptr()
-        f.tbw, f.tbounds = fr['tbw'].data_ptr(), fr['tbounds'].data_ptr()
-        for i in range(3):
-            f.pbw_dims[i] = fr['pbw'].shape[1 + i]
-            f.tbw_dims[i] = fr['tbw'].shape[1 + i]
-        f.latent_index = li.data_ptr()
-
-        o = _lib.RenderOpts()
-        o.n_samples = ns
-        o.chunk = int(self.cfg.get('chunk', CHUNK))
-        o.norm_th = float(self.cfg.norm_th)
-        o.train_th = float(self.cfg.train_th)
-        o.t_rand = t_rand.data_ptr() if t_rand is not None else None
-
-        rgb = torch.empty((1, R, 3), device=dev)
-        acc = torch.empty((1, R), device=dev)
-        depth = torch.empty((1, R), device=dev)
-        raw = torch.empty((1, R * ns, 4), device=dev)
-        out = _lib.RenderOut(rgb.data_ptr(), acc.data_ptr(), depth.data_ptr(), raw.data_ptr())
-
-        ws_bytes = self.lib.anr_render_workspace_bytes(R, ctypes.byref(o), ctypes.byref(f))
-        if self._ws is None or self._ws.numel() < ws_bytes or self._ws.device != dev:
-            self._ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
-        stream = _lib.stream_ptr(dev)
-        _lib.check(self.lib.anr_render_fwd(ctypes.byref(p), ctypes.byref(f), _lib.ptr(ray_o), _lib.ptr(ray_d),
-                                           _lib.ptr(near), _lib.ptr(far), R, ctypes.byref(o), ctypes.byref(out),
-                                           _lib.ptr(self._ws), ws_bytes, stream), 'anr_render_fwd')
-        ret = {'rgb_map': rgb, 'acc_map': acc, 'depth_map': depth, 'raw': raw}
+        R = batch['ray_o'].shape[1]
+        c = _Call(self, batch, self._t_rand(R, dev, t_rand))
+        ws_bytes = self.lib.anr_render_workspace_bytes(R, ctypes.byref(c.opts), ctypes.byref(c.frame))
+        ws = self._workspace('_ws', ws_bytes, dev)
+        _lib.check(self.lib.anr_render_fwd(ctypes.byref(p), ctypes.byref(c.frame), *c.ray_ptrs(), R,
+                                           ctypes.byref(c.opts), ctypes.byref(c.out), _lib.ptr(ws), ws_bytes,
+                                           _lib.stream_ptr(dev)), 'anr_render_fwd')
+        ret = {'rgb_map': c.rgb, 'acc_map': c.acc, 'depth_map': c.depth, 'raw': c.raw}
         if bw_rows:
-            counts_addr = self.lib.anr_render_counts(_lib.ptr(self._ws), R)
-            base = self._ws.data_ptr()
-            counts = self._ws[counts_addr - base:counts_addr - base + 8].view(torch.int32).cpu()  # host sync
-            n_kept, m = int(counts[0]), int(counts[1])
-            self.last_counts = (n_kept, m)
-            pbw = torch.empty((1, m, 24), device=dev)
-            tbw = torch.empty((1, m, 24), device=dev)
-            if m > 0:
-                _lib.check(self.lib.anr_render_bw_rows(_lib.ptr(self._ws), R, _lib.ptr(pbw), _lib.ptr(tbw), stream),
-                           'anr_render_bw_rows')
-            ret['pbw'] = pbw
-            ret['tbw'] = tbw
-        del keep_alive
+            ret['pbw'], ret['tbw'] = self._bw_rows(ws, R, dev)
         return ret
+
+    def render_train(self, batch, t_rand=None):
+        """Training forward (autograd-enabled): returns the render dict; ``rgb_map``, ``pbw`` and
+        ``tbw`` carry gradients to every network parameter through ``anr_train_bwd``."""
+        dev = self.device()
+        R = batch['ray_o'].shape[1]
+        t_rand = self._t_rand(R, dev, t_rand)
+        params = self.net.core_tensors()
+        rgb, acc, depth, raw, pbw, tbw = _TrainRender.apply(self, batch, t_rand, *params)
+        return {'rgb_map': rgb, 'acc_map': acc, 'depth_map': depth, 'raw': raw, 'pbw': pbw, 'tbw': tbw}
 
     def render(self, batch):
-        ret = self.render_device(batch)
-        if not ret['rgb_map'].requires_grad:
-            ret = {k: v.detach().cpu() for k, v in ret.items()}
-        return ret
+        if torch.is_grad_enabled() and any(p.requires_grad for p in self.net.parameters()) and self.net.training:
+            return self.render_train(batch)
+        with torch.no_grad():
+            ret = self.render_device(batch)
+        return {k: v.cpu() for k, v in ret.items()}
 
     def counts(self, n_rays):
-        """(kept samples, alpha_ind rows) of the last render (device read, syncs)."""
-        addr = self.lib.anr_render_counts(_lib.ptr(self._ws), n_rays)
-        base = self._ws.data_ptr()
-        c = self._ws[addr - base:addr - base + 8].view(torch.int32).cpu()
-        return int(c[0]), int(c[1])
+        """(kept samples, alpha_ind rows) of the last evaluation render (device read, syncs)."""
+        return self._counts(self._ws, n_rays)
+
+
+class _TrainRender(torch.autograd.Function):
+    """forward = anr_train_fwd, backward = anr_train_bwd (parameter gradients accumulate)."""
+
+    @staticmethod
+    def forward(ctx, renderer, batch, t_rand, *params):
+        lib = renderer.lib
+        p = renderer.params(pack=False)
+        dev = params[0].device
+        R = batch['ray_o'].shape[1]
+        c = _Call(renderer, batch, t_rand)
+        ws_bytes = lib.anr_train_workspace_bytes(R, ctypes.byref(c.opts), ctypes.byref(c.frame))
+        ws = renderer._workspace('_tws', ws_bytes, dev)
+        _lib.check(lib.anr_train_fwd(ctypes.byref(p), ctypes.byref(c.frame), *c.ray_ptrs(), R, ctypes.byref(c.opts),
+                                     ctypes.byref(c.out), _lib.ptr(ws), ws_bytes, _lib.stream_ptr(dev)),
+                   'anr_train_fwd')
+        pbw, tbw = renderer._bw_rows(ws, R, dev)
+        ctx.renderer, ctx.call, ctx.ws, ctx.ws_bytes, ctx.m = renderer, c, ws, ws_bytes, pbw.shape[1]
+        ctx.mark_non_differentiable(c.acc, c.depth, c.raw)
+        return c.rgb, c.acc, c.depth, c.raw, pbw, tbw
+
+    @staticmethod
+    def backward(ctx, d_rgb, d_acc, d_depth, d_raw, d_pbw, d_tbw):
+        r, c = ctx.renderer, ctx.call
+        lib = r.lib
+        params = r.net.core_tensors()
+        dev = params[0].device
+        p = r.params(pack=False)
+        grads = [torch.zeros_like(t) for t in params]
+        gp = (ctypes.c_void_p * _lib.NUM_TENSORS)(*[g.data_ptr() for g in grads])
+        keep = [t.contiguous() if t is not None else None for t in (d_rgb, d_pbw, d_tbw)]
+        _lib.check(lib.anr_train_bwd(ctypes.byref(p), gp, ctypes.byref(c.frame), *c.ray_ptrs(), c.R,
+                                     ctypes.byref(c.opts), *[_lib.ptr(t) for t in keep], _lib.ptr(ctx.ws),
+                                     ctx.ws_bytes, _lib.stream_ptr(dev)), 'anr_train_bwd')
+        return (None, None, None, *grads)
 
 
 def near_far(bounds, ray_o, ray_d):

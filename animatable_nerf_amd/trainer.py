@@ -1,0 +1,135 @@
+"""Trainer plugin (lib/train/trainers/tpose_trainer.py:11-73, trainer.py:9-102, optimizer.py:12-27,
+lib/utils/optimizer/lr_scheduler.py:66-75).
+
+Two ways to train, same kernels:
+
+* ``NetworkWrapper(net)`` — the reference's wrapper: ``forward(batch) -> (ret, loss, scalar_stats,
+  image_stats)``; the render goes through ``Renderer.render_train`` (an autograd Function over
+  ``anr_train_fwd`` / ``anr_train_bwd``), so the reference ``Trainer.train`` loop
+  (``loss.backward(); clip_grad_value_(40); optimizer.step()``) runs unchanged.
+* ``FusedStep(net)`` — the native path: parameters and gradients live in one flat HBM blob, one
+  ``anr_train_step`` call runs forward + losses + backward, one ``anr_adam`` call clips and updates;
+  for N GPUs the flat gradient blob is all-reduced (mean, DDP semantics) over RCCL in one call.
+"""
+import ctypes
+import math
+
+import torch
+import torch.distributed as dist
+import torch.nn.functional as F
+
+from . import _lib
+from . import config as _config
+from .renderer import Renderer, _Call
+
+
+class NetworkWrapper(torch.nn.Module):
+    """tpose_trainer.NetworkWrapper: loss = smooth_l1(pbw, tbw) + mse(rgb_map[mask], rgb[mask])."""
+
+    def __init__(self, net, cfg=None):
+        super().__init__()
+        self.net = net
+        self.renderer = Renderer(net, cfg)
+        self.bw_crit = F.smooth_l1_loss
+        self.img2mse = lambda x, y: torch.mean((x - y) ** 2)
+
+    def forward(self, batch, t_rand=None):
+        ret = self.renderer.render_train(batch, t_rand=t_rand)
+        scalar_stats = {}
+        loss = 0
+        bw_loss = self.bw_crit(ret['pbw'], ret['tbw'])
+        scalar_stats.update({'bw_loss': bw_loss})
+        loss += bw_loss
+        mask = batch['mask_at_box'].to(ret['rgb_map'].device).bool()
+        rgb = batch['rgb'].to(ret['rgb_map'].device)
+        img_loss = self.img2mse(ret['rgb_map'][mask], rgb[mask])
+        scalar_stats.update({'img_loss': img_loss})
+        loss += img_loss
+        scalar_stats.update({'loss': loss})
+        return ret, loss, scalar_stats, {}
+
+
+def make_optimizer(cfg, net, lr=None, weight_decay=None):
+    """optimizer.py:12-27: Adam with one parameter group per tensor."""
+    lr = cfg.train.lr if lr is None else lr
+    wd = cfg.train.weight_decay if weight_decay is None else weight_decay
+    groups = [{'params': [v], 'lr': lr, 'weight_decay': wd} for _, v in net.named_parameters() if v.requires_grad]
+    return torch.optim.Adam(groups, lr, weight_decay=wd)
+
+
+def exponential_lr(base_lr, epoch, gamma=0.1, decay_epochs=1000):
+    """lr_scheduler.ExponentialLR (lr_scheduler.py:66-75): base_lr * gamma ** (epoch / decay_epochs)."""
+    return base_lr * gamma ** (epoch / decay_epochs)
+
+
+class FusedStep:
+    """Native training step on a flat parameter blob (configs 3 / 4).
+
+    ``step(batch)`` = forward + losses + backward (``anr_train_step``) + [RCCL all-reduce of the
+    gradient blob] + clip_grad_value_(40) + Adam (``anr_adam``). Returns the device loss triple
+    (loss, img_loss, bw_loss) without synchronising.
+    """
+
+    def __init__(self, net, cfg=None, lr=None, clip=40.0, betas=(0.9, 0.999), eps=1e-8, group=None):
+        self.cfg = cfg if cfg is not None else _config.cfg
+        self.net = net
+        self.renderer = Renderer(net, self.cfg)
+        self.lib = self.renderer.lib
+        self.lr = float(self.cfg.train.lr if lr is None else lr)
+        self.wd = float(self.cfg.train.weight_decay)
+        self.clip, self.betas, self.eps = clip, betas, eps
+        self.group = group
+        ps = net.core_tensors()
+        dev = ps[0].device
+        n = sum(p.numel() for p in ps)
+        self.flat = torch.empty(n, device=dev)
+        self.grad = torch.zeros(n, device=dev)
+        self.m = torch.zeros(n, device=dev)
+        self.v = torch.zeros(n, device=dev)
+        off = 0
+        self.grad_views = []
+        for p in ps:
+            k = p.numel()
+            self.flat[off:off + k].copy_(p.detach().reshape(-1))
+            p.data = self.flat[off:off + k].view_as(p)
+            g = self.grad[off:off + k].view_as(p)
+            p.grad = g
+            self.grad_views.append(g)
+            off += k
+        self.n = n
+        self.t = 0
+        self.loss3 = torch.zeros(4, device=dev)
+
+    def step(self, batch, t_rand=None, lr=None):
+        r = self.renderer
+        dev = self.flat.device
+        R = batch['ray_o'].shape[1]
+        if t_rand is None and self.cfg.perturb > 0:
+            t_rand = torch.rand((R, int(self.cfg.N_samples)), device=dev)
+        c = _Call(r, batch, t_rand)
+        rgb = batch['rgb'].to(device=dev, dtype=torch.float32).contiguous()
+        mask = batch['mask_at_box'].to(device=dev).reshape(-1).to(torch.uint8).contiguous()
+        p = r.params(pack=False)
+        ws_bytes = self.lib.anr_train_workspace_bytes(R, ctypes.byref(c.opts), ctypes.byref(c.frame))
+        ws = r._workspace('_tws', ws_bytes, dev)
+        self.grad.zero_()
+        gp = (ctypes.c_void_p * _lib.NUM_TENSORS)(*[g.data_ptr() for g in self.grad_views])
+        stream = _lib.stream_ptr(dev)
+        _lib.check(self.lib.anr_train_step(ctypes.byref(p), gp, ctypes.byref(c.frame), *c.ray_ptrs(), R,
+                                           ctypes.byref(c.opts), _lib.ptr(rgb), _lib.ptr(mask), ctypes.byref(c.out),
+                                           _lib.ptr(self.loss3), _lib.ptr(ws), ws_bytes, stream), 'anr_train_step')
+        if self.group is not None or (dist.is_available() and dist.is_initialized()):
+            dist.all_reduce(self.grad, op=dist.ReduceOp.SUM, group=self.group)
+            self.grad.div_(dist.get_world_size(self.group))
+        self.t += 1
+        _lib.check(self.lib.anr_adam(_lib.ptr(self.flat), _lib.ptr(self.grad), _lib.ptr(self.m), _lib.ptr(self.v),
+                                     self.n, float(self.lr if lr is None else lr), self.betas[0], self.betas[1],
+                                     self.eps, self.wd, self.t, self.clip, stream), 'anr_adam')
+        # the update bypassed torch's version counters: invalidate the renderer's packed weights
+        self.net._anr_weights_epoch = getattr(self.net, '_anr_weights_epoch', 0) + 1
+        self.last = c
+        return self.loss3
+
+
+def psnr_from_mse(mse):
+    return -10.0 * math.log10(mse)

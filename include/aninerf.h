@@ -104,6 +104,31 @@ const int32_t* anr_render_counts(const void* workspace, int n_rays);
 /* Gather the m alpha_ind rows of pbw / tbw (each (m,24)) after the counts were read. */
 int anr_render_bw_rows(const void* workspace, int n_rays, float* pbw, float* tbw, void* stream);
 
+/* ---- training (A16/A17; lib/train/trainers/tpose_trainer.py:21-73, trainer.py:50-68) ------
+ * anr_train_fwd: the render forward of the training step (perturb via o->t_rand), keeping every
+ *   activation in the workspace; same outputs as anr_render_fwd (+ anr_render_counts /
+ *   anr_render_bw_rows on this workspace). Reads the kept-sample count once (host sync).
+ * anr_train_bwd: given upstream gradients d rgb_map (R,3) and d pbw / d tbw rows (m,24) (any may
+ *   be NULL = zero), ACCUMULATES parameter gradients into grads[ANR_NUM_TENSORS] (state_dict
+ *   order, same shapes as anr_params.t) — what loss.backward() does in the reference.
+ * anr_train_step: forward + the reference losses (img MSE over mask_at_box rays + smooth-L1 of
+ *   the pbw/tbw rows; loss3 = {loss, img_loss, bw_loss} on device) + backward, one call.
+ * anr_adam: clip_grad_value_(clip) then torch.optim.Adam on a flat parameter blob (trainer.py:64-68). */
+size_t anr_train_workspace_bytes(int n_rays, const anr_render_opts* o, const anr_frame* f);
+int anr_train_fwd(const anr_params* p, const anr_frame* f, const float* ray_o, const float* ray_d,
+                  const float* near_, const float* far_, int n_rays, const anr_render_opts* o,
+                  const anr_render_out* out, void* workspace, size_t ws_bytes, void* stream);
+int anr_train_bwd(const anr_params* p, float* const* grads, const anr_frame* f, const float* ray_o,
+                  const float* ray_d, const float* near_, const float* far_, int n_rays,
+                  const anr_render_opts* o, const float* d_rgb_map, const float* d_pbw, const float* d_tbw,
+                  void* workspace, size_t ws_bytes, void* stream);
+int anr_train_step(const anr_params* p, float* const* grads, const anr_frame* f, const float* ray_o,
+                   const float* ray_d, const float* near_, const float* far_, int n_rays,
+                   const anr_render_opts* o, const float* rgb_gt, const uint8_t* mask_at_box,
+                   const anr_render_out* out, float* loss3, void* workspace, size_t ws_bytes, void* stream);
+int anr_adam(float* param, float* grad, float* exp_avg, float* exp_avg_sq, long n, float lr, float beta1,
+             float beta2, float eps, float weight_decay, int step, float clip_value, void* stream);
+
 /* ---- measurement ----------------------------------------------------------------------
  * When enabled, anr_render_fwd records a hipEvent pair around the fused network kernel (k_mlp)
  * on the caller's stream. anr_profile_read waits for the recorded events, returns the summed
