@@ -70,21 +70,31 @@ def test_gradients_match_oracle(dev):
     ref_loss.backward()
     assert abs(loss.item() - ref_loss.item()) <= 1e-5 * abs(ref_loss.item()) + 1e-7
     assert abs(stats['bw_loss'].item() - ref_stats['bw_loss'].item()) <= 1e-4 * abs(ref_stats['bw_loss'].item())
+    # float64 oracle = the true gradient; the fp32 reference itself deviates from it by up to
+    # ~2.3e-3 (max-relative) on this batch (gamma(x_T) up to 2^9 rad amplifies rounding), so the HIP
+    # gradients are held to the same band against the truth and to 5e-3 against the fp32 oracle.
+    P64 = {k: v.detach().double().requires_grad_(True) for k, v in oracle_params().items()}
+    b64 = {k: (v.double() if v.is_floating_point() else v) for k, v in bc.items()}
+    ret64 = restate.render(P64, b64, t_rand=t_rand.double())
+    restate.loss_terms(ret64, b64)[0].backward()
     worst = []
     for name, p in net.named_parameters():
         ref = P[name].grad
         assert p.grad is not None, name
         rel = _rel(p.grad.cpu(), ref)
-        worst.append((rel, name))
-        assert rel <= 2e-3, (name, rel)
+        rel64 = _rel(p.grad.cpu().double(), P64[name].grad)
+        ref64 = _rel(ref.double(), P64[name].grad)
+        worst.append((rel64, ref64, rel, name))
+        assert rel <= 5e-3, (name, rel)
+        assert rel64 <= max(3e-3, 2 * ref64), (name, rel64, ref64)
     worst.sort(reverse=True)
-    print('worst relative grad errors:', worst[:5])
+    print('worst (hip vs f64, ref fp32 vs f64, hip vs ref):', worst[:5])
     # the reference golden (clip at 40 is inactive at this scale)
     for k in g.files:
         if k.startswith('grad_'):
             name = k[5:]
             rel = _rel(dict(net.named_parameters())[name].grad.cpu(), torch.from_numpy(g[k]))
-            assert rel <= 2e-3, (name, rel)
+            assert rel <= 5e-3, (name, rel)
 
 
 def test_fused_step_matches_reference_adam(dev):
@@ -104,7 +114,17 @@ def test_fused_step_matches_reference_adam(dev):
             name = k[6:]
             d = (params[name].detach() - before[name]).cpu()
             ref = torch.from_numpy(g[k])
-            # Adam's first step is ~lr*sign(g): compare where the gradient is not tiny
-            big = ref.abs() > 0.5 * float(g['lr'])
-            assert torch.allclose(d[big], ref[big], rtol=1e-3, atol=1e-6), name
+            # Adam's first step is -lr g / (|g| + eps) ~ -lr sign(g): compare where the gradient is
+            # clearly away from zero (its sign is then fixed at fp32 gradient accuracy)
+            gr = torch.from_numpy(g['grad_' + name])
+            big = gr.abs() > torch.clamp(0.05 * gr.abs().max(), min=1e-6)
+            assert torch.allclose(d[big], ref[big], rtol=1e-3, atol=1e-8), name
             assert (d - ref).abs().max().item() <= 2 * float(g['lr']) + 1e-7, name
+    # the Adam kernel itself, against torch.optim.Adam's first-step formula on our own gradients
+    lr = float(g['lr'])
+    for name, p in params.items():
+        gg = p.grad.detach().cpu().double()
+        expect = -lr * gg / (gg.abs() + 1e-8)
+        d = (p.detach() - before[name]).cpu().double()
+        # d = p_new - p_old carries one fp32 ulp of |p| (embeddings are N(0,1)): atol 3e-7
+        assert torch.allclose(d, expect, rtol=1e-4, atol=3e-7), name
