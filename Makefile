@@ -4,23 +4,25 @@ ARCH ?= gfx950
 SRC_DIR := animatable_nerf_amd/csrc
 SRCS := $(SRC_DIR)/anr_capi.hip $(SRC_DIR)/anr_rays.hip $(SRC_DIR)/anr_mlp.hip $(SRC_DIR)/anr_pack.hip \
         $(SRC_DIR)/anr_gemm.hip $(SRC_DIR)/anr_train.hip $(SRC_DIR)/anr_train_capi.hip
-HDRS := $(wildcard $(SRC_DIR)/*.h) include/aninerf.h
 OBJS := $(SRCS:.hip=.o)
+DEPS := $(OBJS:.o=.d)
 LIB := animatable_nerf_amd/libaninerf_hip.so
 CXXFLAGS := -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -Wall -Wno-unused-function -Iinclude
 
 all: $(LIB)
 
-$(SRC_DIR)/%.o: $(SRC_DIR)/%.hip $(HDRS)
-	$(HIPCC) $(CXXFLAGS) -c $< -o $@
+$(SRC_DIR)/%.o: $(SRC_DIR)/%.hip
+	$(HIPCC) $(CXXFLAGS) -MMD -MP -c $< -o $@
 
 $(LIB): $(OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)
 
-resources: $(SRC_DIR)/anr_mlp.hip $(HDRS)
+-include $(DEPS)
+
+resources: $(SRC_DIR)/anr_mlp.hip
 	$(HIPCC) $(CXXFLAGS) -c $(SRC_DIR)/anr_mlp.hip -o /tmp/anr_mlp_res.o -Rpass-analysis=kernel-resource-usage
 
 clean:
-	rm -f $(OBJS) $(LIB)
+	rm -f $(OBJS) $(DEPS) $(LIB)
 
 .PHONY: all clean resources

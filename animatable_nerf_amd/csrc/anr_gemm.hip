@@ -3,15 +3,18 @@
 //   C[M][N] (+)= epi( sum_s A_s(m, k) * B_s(k, n) ),  A_s(m,k) = A_s[m*a_rs + k*a_cs],
 //                                                     B_s(k,n) = B_s[k*b_rs + n*b_cs]
 // One kernel serves the three products of a Conv1d(k=1) layer over the point batch:
-//   forward  Y  = X W^T   (A = X row-major, B(k,n) = W[n][k])
-//   backward dX = dY W    (A = dY row-major, B(k,n) = W[k][col0+n])
-//   weights  dW = dY^T X  (A(m=n_out,k=point) = dY[k][n], B = X row-major; split-K + atomics)
-// Up to two K segments (the skip concatenation [gamma(x), net] of layers 5 / pts_linears.5, or
-// the two heads feature_fc / alpha_fc feeding one input). Epilogue: bias, ReLU, or the ReLU mask of
-// the forward activation (dX of a ReLU layer), accumulate into C.
+//   forward  Y  = X W^T   (A = X row-major: contiguous in k;  B(k,n) = W[n][k]: contiguous in k)
+//   backward dX = dY W    (A = dY row-major: contiguous in k; B(k,n) = W[k][c0+n]: contiguous in n)
+//   weights  dW = dY^T X  (A(m,k) = dY[k][m]: contiguous in m; B = X row-major: contiguous in n;
+//                          split-K over samples, fp32 atomics into dW)
+// Up to two K segments (the skip concatenation [gamma(x), net] of layers 5 / pts_linears.5, or the
+// two heads feature_fc / alpha_fc feeding one input), each padded to the K tile separately.
+// Epilogue: bias, ReLU, or the ReLU mask of the forward activation (dX of a ReLU layer),
+// accumulate into C.
 //
-// Tile 64x64x16, 256 threads = 4 waves, each wave a 32x32 quadrant of v_mfma_f32_16x16x4_f32
-// (exact fp32). M may be taken from device memory (kept-sample count) so no host sync is needed.
+// Tile 64x64x32, 256 threads = 4 waves, each a 32x32 quadrant of v_mfma_f32_16x16x4_f32 (exact fp32).
+// Global -> registers with float4 loads along the contiguous dimension of each operand (template
+// flags), registers -> LDS [k][m|n] after the barrier so the next tile's loads overlap the MFMAs.
 #include "anr_common.h"
 #include "anr_train.h"
 
@@ -19,23 +22,94 @@ namespace anr {
 
 #define GBM 64
 #define GBN 64
-#define GBK 16
+#define GBK 32
+#define GLD (64 + 4)
 
-__global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
-  __shared__ float As[GBK][GBM + 4];
-  __shared__ float Bs[GBK][GBN + 4];
+// element (r, k) of a segment operand with r the M (or N) index; contiguous-in-k or in-r layouts
+struct Tile4 {
+  float v[2][4];
+};
+
+template <bool KCONTIG>
+__device__ __forceinline__ void load_tile(const float* __restrict__ P, long rs, long cs, int R, int r0, int K, int k0,
+                                          int tid, Tile4& t) {
+  // 64 (r) x 32 (k) elements = 512 float4 groups, 2 per thread
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int q = tid + h * 256;
+    int r, k;
+    if (KCONTIG) {
+      r = q >> 3;
+      k = (q & 7) * 4;
+    } else {
+      k = q >> 4;
+      r = (q & 15) * 4;
+    }
+    const int gr = r0 + r, gk = k0 + k;
+    float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (KCONTIG) {
+      // 4 consecutive k of row gr
+      if (gr < R) {
+        const float* p = P + (long)gr * rs + (long)gk * cs;
+        if (gk + 3 < K) {
+          x.x = p[0]; x.y = p[1]; x.z = p[2]; x.w = p[3];
+        } else {
+          if (gk < K) x.x = p[0];
+          if (gk + 1 < K) x.y = p[1];
+          if (gk + 2 < K) x.z = p[2];
+        }
+      }
+    } else {
+      // 4 consecutive r of k-row gk
+      if (gk < K) {
+        const float* p = P + (long)gr * rs + (long)gk * cs;
+        if (gr + 3 < R) {
+          x.x = p[0]; x.y = p[rs]; x.z = p[2 * rs]; x.w = p[3 * rs];
+        } else {
+          if (gr < R) x.x = p[0];
+          if (gr + 1 < R) x.y = p[rs];
+          if (gr + 2 < R) x.z = p[2 * rs];
+        }
+      }
+    }
+    t.v[h][0] = x.x; t.v[h][1] = x.y; t.v[h][2] = x.z; t.v[h][3] = x.w;
+  }
+}
+
+template <bool KCONTIG>
+__device__ __forceinline__ void store_tile(float (*S)[GLD], int tid, const Tile4& t) {
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int q = tid + h * 256;
+    if (KCONTIG) {
+      const int r = q >> 3, k = (q & 7) * 4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) S[k + e][r] = t.v[h][e];
+    } else {
+      const int k = q >> 4, r = (q & 15) * 4;
+      *(float4*)&S[k][r] = make_float4(t.v[h][0], t.v[h][1], t.v[h][2], t.v[h][3]);
+    }
+  }
+}
+
+template <bool A_K, bool B_K>
+__global__ __launch_bounds__(256) void k_gemm_t(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) float As[GBK][GLD];
+  __shared__ __attribute__((aligned(16))) float Bs[GBK][GLD];
   const int M = g.M_dev ? *g.M_dev : g.M;
   const int m0 = blockIdx.y * GBM, n0 = blockIdx.x * GBN;
   if (m0 >= M) return;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wr = (w >> 1) * 32, wc = (w & 1) * 32;
-  // split-K over the concatenated K of all segments
-  int Ktot = 0;
-  for (int s = 0; s < g.nseg; ++s) Ktot += g.seg[s].K;
-  const int per = (((Ktot + g.ksplit - 1) / g.ksplit) + GBK - 1) / GBK * GBK;
-  const int kb = blockIdx.z * per;
-  const int ke = min(Ktot, kb + per);
-  if (kb >= ke) return;
+
+  // k range of this split (split-K only with one segment)
+  int kb = 0, ke = g.seg[0].K;
+  if (g.ksplit > 1) {
+    const int per = ((g.seg[0].K + g.ksplit - 1) / g.ksplit + GBK - 1) / GBK * GBK;
+    kb = blockIdx.z * per;
+    ke = min(g.seg[0].K, kb + per);
+    if (kb >= ke) return;
+  }
 
   f32x4 acc[2][2];
 #pragma unroll
@@ -43,36 +117,28 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  for (int k0 = kb; k0 < ke; k0 += GBK) {
-    // stage A (64 x 16) and B (16 x 64): 4 elements per thread each
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int idx = tid + e * 256;
-      // A: element (m = idx % 64, k = idx / 64) -> consecutive threads walk m (row-major dY^T reads)
-      {
-        const int mm = idx & 63, kk = idx >> 6;
-        const int m = m0 + mm, k = k0 + kk;
-        float v = 0.f;
-        if (m < M && k < ke) {
-          int kl = k, s = 0;
-          while (s + 1 < g.nseg && kl >= g.seg[s].K) { kl -= g.seg[s].K; ++s; }
-          v = g.seg[s].A[(long)m * g.seg[s].a_rs + (long)kl * g.seg[s].a_cs];
-        }
-        As[kk][mm] = v;
-      }
-      {
-        const int nn = idx & 63, kk = idx >> 6;
-        const int n = n0 + nn, k = k0 + kk;
-        float v = 0.f;
-        if (n < g.N && k < ke) {
-          int kl = k, s = 0;
-          while (s + 1 < g.nseg && kl >= g.seg[s].K) { kl -= g.seg[s].K; ++s; }
-          v = g.seg[s].B[(long)kl * g.seg[s].b_rs + (long)n * g.seg[s].b_cs];
-        }
-        Bs[kk][nn] = v;
-      }
-    }
+  // flattened (segment, k0) iteration
+  int s = 0, k0 = kb;
+  int kend = (g.ksplit > 1) ? ke : g.seg[0].K;
+  Tile4 ta, tb;
+  load_tile<A_K>(g.seg[0].A, g.seg[0].a_rs, g.seg[0].a_cs, M, m0, kend, k0, tid, ta);
+  load_tile<B_K>(g.seg[0].B, g.seg[0].b_cs, g.seg[0].b_rs, g.N, n0, kend, k0, tid, tb);
+  while (true) {
+    store_tile<A_K>(As, tid, ta);
+    store_tile<B_K>(Bs, tid, tb);
     __syncthreads();
+    // next tile position
+    int ns = s, nk = k0 + GBK;
+    if (nk >= kend) {
+      ns = s + 1;
+      nk = 0;
+    }
+    const bool more = ns < g.nseg && (g.ksplit == 1 || ns == 0);
+    if (more) {
+      const int kend2 = (g.ksplit > 1) ? ke : g.seg[ns].K;
+      load_tile<A_K>(g.seg[ns].A, g.seg[ns].a_rs, g.seg[ns].a_cs, M, m0, kend2, nk, tid, ta);
+      load_tile<B_K>(g.seg[ns].B, g.seg[ns].b_cs, g.seg[ns].b_rs, g.N, n0, kend2, nk, tid, tb);
+    }
 #pragma unroll
     for (int ks = 0; ks < GBK; ks += 4) {
       const int kr = ks + (lane >> 4);
@@ -87,6 +153,10 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
         for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b[j], acc[i][j], 0, 0, 0);
     }
     __syncthreads();
+    if (!more) break;
+    s = ns;
+    k0 = nk;
+    kend = (g.ksplit > 1) ? ke : g.seg[s].K;
   }
   // epilogue: lane holds C[wr + i*16 + 4*(lane>>4) + r][wc + j*16 + (lane&15)]
   const bool first_split = blockIdx.z == 0;
@@ -114,6 +184,21 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
       }
 }
 
+template __global__ void k_gemm_t<true, true>(GemmArgs);
+template __global__ void k_gemm_t<true, false>(GemmArgs);
+template __global__ void k_gemm_t<false, true>(GemmArgs);
+template __global__ void k_gemm_t<false, false>(GemmArgs);
+
+// host-side dispatch on the operand layouts
+void launch_gemm(GemmArgs g, dim3 grid, hipStream_t s) {
+  const bool a_k = g.seg[0].a_cs == 1;
+  const bool b_k = g.seg[0].b_rs == 1;
+  if (a_k && b_k) hipLaunchKernelGGL((k_gemm_t<true, true>), grid, dim3(256), 0, s, g);
+  else if (a_k) hipLaunchKernelGGL((k_gemm_t<true, false>), grid, dim3(256), 0, s, g);
+  else if (b_k) hipLaunchKernelGGL((k_gemm_t<false, true>), grid, dim3(256), 0, s, g);
+  else hipLaunchKernelGGL((k_gemm_t<false, false>), grid, dim3(256), 0, s, g);
+}
+
 // column sums of X[M][N] (ld) into out[N] (+=), M from device when given: bias gradients
 __global__ __launch_bounds__(256) void k_colsum(const float* __restrict__ X, long ld, int M, const int* M_dev, int N,
                                                 float* __restrict__ out, int rows_per_block) {
@@ -127,7 +212,8 @@ __global__ __launch_bounds__(256) void k_colsum(const float* __restrict__ X, lon
   __shared__ float sh[4][64];
   sh[threadIdx.x >> 6][threadIdx.x & 63] = s;
   __syncthreads();
-  if (threadIdx.x < 64 && n < N && r0 < r1) atomicAdd(out + n, sh[0][threadIdx.x] + sh[1][threadIdx.x] + sh[2][threadIdx.x] + sh[3][threadIdx.x]);
+  if (threadIdx.x < 64 && n < N && r0 < r1)
+    atomicAdd(out + n, sh[0][threadIdx.x] + sh[1][threadIdx.x] + sh[2][threadIdx.x] + sh[3][threadIdx.x]);
 }
 
 }  // namespace anr

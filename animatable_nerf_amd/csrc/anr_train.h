@@ -30,7 +30,7 @@ struct GemmArgs {
   int ksplit;          // number of K splits (grid.z)
 };
 
-__global__ void k_gemm(GemmArgs g);
+void launch_gemm(GemmArgs g, dim3 grid, hipStream_t s);
 __global__ void k_colsum(const float* X, long ld, int M, const int* M_dev, int N, float* out, int rows_per_block);
 
 // per-point training buffers (row-major, compact kept-sample order)

@@ -71,7 +71,7 @@ struct Exec {
     if (g.ksplit < 1) g.ksplit = 1;
     dim3 grid((g.N + 63) / 64, (M + 63) / 64, g.ksplit);
     g.M = M;
-    hipLaunchKernelGGL(k_gemm, grid, dim3(256), 0, s, g);
+    launch_gemm(g, grid, s);
     return check_launch("k_gemm");
   }
 
@@ -94,7 +94,7 @@ struct Exec {
     g.nseg = 1;
     g.seg[0] = GemmSeg{dY, 1, ldY, X, ldX, 1, n};
     g.C = dW + c0; g.ldc = in_ch; g.atomic = 1;
-    g.ksplit = (n + 511) / 512;
+    g.ksplit = (n + 1023) / 1024;
     return gemm(g, Nout);
   }
 

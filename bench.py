@@ -36,6 +36,9 @@ def parse():
     ap.add_argument('--rays', type=int, default=512 * 512)
     ap.add_argument('--cpu-rays', type=int, default=16 * 2048)
     ap.add_argument('--no-cpu', action='store_true')
+    ap.add_argument('--mode', choices=('render', 'train'), default='render',
+                    help='render: config 2 (headline); train: config 3/4 training step (1024 rays/GPU)')
+    ap.add_argument('--train-rays', type=int, default=1024)
     return ap.parse_args()
 
 
@@ -51,6 +54,8 @@ def main():
 
     from animatable_nerf_amd import _lib, config, network, synthetic
     from animatable_nerf_amd.renderer import Renderer, near_far
+    if args.mode == 'train':
+        return bench_train(args, rank, world, dev)
 
     sc = synthetic.Scene(vsize=0.025)
     ro, rd = sc.box_rays(args.rays, seed=2 + rank)
@@ -122,6 +127,82 @@ def main():
         result['roofline']['traffic_source'] = t['source'] + '; ' + t['correction']
     if rank == 0 and world == 1 and not args.no_cpu:
         result['cpu_baseline'], result['psnr_vs_fp32_oracle'] = cpu_baseline(sd, b, out, args.cpu_rays)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+FLOP_PER_KEPT_TRAIN = 9_919_488  # 3 x 2 x (2 x 497,152 + 658,944)
+
+
+def bench_train(args, rank, world, dev):
+    """Configs 3/4: one training iteration (trainer.py:50-68) per step on 1,024 rays per GPU:
+    forward + losses + backward (anr_train_step) + RCCL mean all-reduce of the 5.3 MB gradient blob
+    (N > 1) + clip + Adam (anr_adam). Weak scaling: every rank trains on its own ray batch, which is
+    the reference's DDP semantics (one image per rank, samplers.py:75-131)."""
+    from animatable_nerf_amd import config, network, synthetic
+    from animatable_nerf_amd.renderer import near_far
+    from animatable_nerf_amd.trainer import FusedStep
+    sc = synthetic.Scene(vsize=0.025)
+    batches = []
+    nb = max(1, min(8, args.steps + args.warmup))
+    for j in range(nb):
+        ro, rd = sc.box_rays(args.train_rays * 2, seed=1000 + 97 * rank + j)
+        nr, fr, m = near_far(torch.from_numpy(sc.bounds).to(dev), torch.from_numpy(ro).to(dev),
+                             torch.from_numpy(rd).to(dev))
+        m_np = m.cpu().numpy()
+        rgb = np.random.default_rng(j + 31 * rank).random((len(ro), 3)).astype(np.float32)
+        b = sc.batch_arrays(ro[m_np][:args.train_rays], rd[m_np][:args.train_rays],
+                            nr.cpu().numpy()[:args.train_rays], fr.cpu().numpy()[:args.train_rays],
+                            rgb=rgb[m_np][:args.train_rays])
+        batches.append({k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in b.items()})
+    net = network.Network()
+    sd = synthetic.init_state_dict({k: tuple(v.shape) for k, v in net.state_dict().items()})
+    network.load_numpy_state(net, sd)
+    net = net.to(dev)
+    net.train()
+    cfg = config.defaults()
+    cfg.perturb = 1
+    step = FusedStep(net, cfg)
+    for j in range(args.warmup):
+        step.step(batches[j % nb])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    kept = 0
+    for j in range(args.steps):
+        step.step(batches[(args.warmup + j) % nb])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    kept = step.renderer.last_counts[0] if step.renderer.last_counts else 0
+    t = torch.tensor([dt], device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt_max = float(t.item())
+    R = int(batches[0]['ray_o'].shape[1])
+    loss = step.loss3.cpu().tolist()
+    # kept samples of the last step (host read inside anr_train_step)
+    from animatable_nerf_amd import _lib as L  # noqa: F401
+    n_kept = step.renderer._counts(step.renderer._tws, R)[0]
+    achieved = n_kept * FLOP_PER_KEPT_TRAIN * args.steps / dt_max / 1e12
+    result = {
+        'metric': 'training ray-samples/s (1024 rays x 64 samples per GPU per step), aninerf training step',
+        'value': R * 64 * args.steps * world / dt_max, 'unit': 'ray-samples/s', 'n_gpus': world, 'steps': args.steps,
+        'warmup': args.warmup, 'ms_per_step': dt_max / args.steps * 1e3, 'higher_is_better': True, 'scaling': 'weak',
+        'vs_baseline': None, 'dtype': 'fp32', 'data': 'synthetic',
+        'config': {'workload': 'aninerf training step (configs 3/4 shape: 1024 rays/GPU, perturb 1, Adam)',
+                   'rays_per_gpu': R, 'kept_samples_last_step': n_kept,
+                   'parallelism': f'dp{world} (RCCL mean all-reduce of the flat gradient blob)'},
+        'roofline': {'bound': 'mfma', 'kernel': 'whole step', 'achieved': achieved, 'peak': PEAK_FP32_MFMA_TFLOPS,
+                     'unit': 'TFLOP/s', 'frac': achieved / PEAK_FP32_MFMA_TFLOPS, 'traffic': None,
+                     'flop_per_kept': FLOP_PER_KEPT_TRAIN},
+        'loss_last_step': loss[:3],
+    }
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
