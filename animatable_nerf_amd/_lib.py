@@ -13,6 +13,7 @@ import torch  # noqa: F401  (must be loaded before the library, see module docst
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, 'libaninerf_hip.so')
 NUM_TENSORS = 46
+NUM_NOVEL_TENSORS = 19
 
 EXPORTS = ('anr_near_far', 'anr_params_packed_bytes', 'anr_params_pack', 'anr_render_workspace_bytes',
            'anr_render_fwd', 'anr_render_counts', 'anr_render_bw_rows', 'anr_profile_enable', 'anr_profile_read',
@@ -24,19 +25,19 @@ c_float_p = ctypes.c_void_p
 
 class Params(ctypes.Structure):
     _fields_ = [('t', ctypes.c_void_p * NUM_TENSORS), ('num_train_frame', ctypes.c_int),
-                ('packed', ctypes.c_void_p)]
+                ('packed', ctypes.c_void_p), ('novel', ctypes.c_void_p * NUM_NOVEL_TENSORS)]
 
 
 class Frame(ctypes.Structure):
     _fields_ = [('A', ctypes.c_void_p), ('R', ctypes.c_void_p), ('Th', ctypes.c_void_p),
                 ('pbw', ctypes.c_void_p), ('pbw_dims', ctypes.c_int * 3), ('pbounds', ctypes.c_void_p),
                 ('tbw', ctypes.c_void_p), ('tbw_dims', ctypes.c_int * 3), ('tbounds', ctypes.c_void_p),
-                ('latent_index', ctypes.c_void_p)]
+                ('latent_index', ctypes.c_void_p), ('bw_latent_index', ctypes.c_void_p)]
 
 
 class RenderOpts(ctypes.Structure):
     _fields_ = [('n_samples', ctypes.c_int), ('chunk', ctypes.c_int), ('norm_th', ctypes.c_float),
-                ('train_th', ctypes.c_float), ('t_rand', ctypes.c_void_p)]
+                ('train_th', ctypes.c_float), ('t_rand', ctypes.c_void_p), ('novel_pose', ctypes.c_int)]
 
 
 class RenderOut(ctypes.Structure):

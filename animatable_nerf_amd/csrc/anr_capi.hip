@@ -79,6 +79,13 @@ int stage_frontend(const anr_params* p, const anr_frame* f, const float* ray_o, 
   pa.bw_latent = p->t[27]; pa.w_lat = p->t[21]; pa.b_lat = p->t[22]; pa.nf_latent = p->t[0];
   pa.latent_index = f->latent_index;
   pa.fold = (float*)(ws + L.fold);
+  if (o->novel_pose) {
+    pa.novel = 1;
+    pa.n_latent = p->novel[0];
+    pa.nw_bw0 = p->novel[1]; pa.nb_bw0 = p->novel[2];
+    pa.nw_bw5 = p->novel[11]; pa.nb_bw5 = p->novel[12];
+    pa.bw_latent_index = f->bw_latent_index;
+  }
   const int nvb = (int)((np + nt + 7) / 8);
   hipLaunchKernelGGL(k_prep, dim3(nvb + 1), dim3(256), 0, s, pa);
   ANR_TRY(check_launch("k_prep"));
@@ -130,6 +137,8 @@ int stage_mlp(const anr_params* p, const anr_frame* f, const float* ray_o, const
   ma.sigma = (float*)(ws + L.sigma);
   ma.pbw_rows = (float*)(ws + L.pbw_rows);
   ma.tbw_rows = (float*)(ws + L.tbw_rows);
+  ma.pose_woff = o->novel_pose ? ANR_NOVEL_WOFF : 0;
+  ma.pose_boff = o->novel_pose ? ANR_NOVEL_BOFF : 0;
   const int lds = 2 * 8 * 5 * 1024 + 24 * 16 * 4;
   if (!mlp_attr_set) {
     if (hipFuncSetAttribute((const void*)k_mlp, hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
@@ -219,6 +228,7 @@ int anr_params_pack(const anr_params* p, void* packed, void* stream) {
     if (!p->t[i]) return fail(ANR_E_ARG, "anr_params_pack: tensor " + std::to_string(i) + " is NULL");
     a.t[i] = p->t[i];
   }
+  for (int i = 0; i < ANR_NUM_NOVEL_TENSORS; ++i) a.t[ANR_NOVEL_T0 + i] = p->novel[i];  // may be NULL
   a.out = (unsigned char*)packed;
   const int nw = weights_bytes() / 4;
   hipLaunchKernelGGL(k_pack_weights, dim3((nw + 255) / 256), dim3(256), 0, (hipStream_t)stream, a);
@@ -252,6 +262,11 @@ int anr_render_fwd(const anr_params* p, const anr_frame* f, const float* ray_o, 
     if (f->pbw_dims[i] <= 0 || f->tbw_dims[i] <= 0) return fail(ANR_E_ARG, "anr_render_fwd: bad volume dims");
   if (!f->A || !f->R || !f->Th || !f->pbw || !f->tbw || !f->pbounds || !f->tbounds || !f->latent_index)
     return fail(ANR_E_ARG, "anr_render_fwd: NULL frame tensor");
+  if (o->novel_pose) {
+    for (int i = 0; i < ANR_NUM_NOVEL_TENSORS; ++i)
+      if (!p->novel[i]) return fail(ANR_E_ARG, "anr_render_fwd: novel_pose needs the novel_pose_bw tensors");
+    if (!f->bw_latent_index) return fail(ANR_E_ARG, "anr_render_fwd: novel_pose needs bw_latent_index");
+  }
   const long np = (long)f->pbw_dims[0] * f->pbw_dims[1] * f->pbw_dims[2];
   const long nt = (long)f->tbw_dims[0] * f->tbw_dims[1] * f->tbw_dims[2];
   const Layout L = layout(n_rays, o->chunk, np, nt, out->raw == nullptr);

@@ -59,6 +59,8 @@ struct MlpArgs {
   float* sigma;      // (n') sigma' (after the T-pose bbox mask)
   float* pbw_rows;   // (n', 24)
   float* tbw_rows;   // (n', 24)
+  int pose_woff;     // byte offset of the pose-pass BW weight slices (novel_pose_bw copy or 0)
+  int pose_boff;     // float offset of the pose-pass BW biases
 };
 
 struct PrepArgs {
@@ -69,6 +71,10 @@ struct PrepArgs {
   const float *w_lat, *b_lat, *nf_latent;
   const int64_t* latent_index;
   float* fold;
+  // novel pose: pose-pass folds from novel_pose_bw with bw_latent_index (no +1)
+  int novel;
+  const float *nw_bw0, *nb_bw0, *nw_bw5, *nb_bw5, *n_latent;
+  const int64_t* bw_latent_index;
 };
 
 __global__ void k_near_far(const float*, const float*, int, const float*, uint8_t*, float*, float*);
@@ -86,7 +92,7 @@ __global__ void k_prep(PrepArgs a);
 __global__ void k_mlp(MlpArgs a);
 
 struct PackArgs {
-  const float* t[46];
+  const float* t[65];  // 46 core tensors + 19 novel_pose_bw tensors (NULL when absent)
   unsigned char* out;
 };
 __global__ void k_pack_weights(PackArgs a);

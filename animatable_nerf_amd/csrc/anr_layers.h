@@ -71,12 +71,22 @@ __host__ __device__ constexpr LayerDesc layer_desc(int i) {
 // rgb_fc (3, 128): view out (32 ksteps)
 #define ANR_L_VIEW 19
 #define ANR_L_RGB 20
-#define ANR_NUM_LAYERS_ALL 21
+// layers 21..29: novel_pose_bw (BackwardBlendWeight), same shapes as 0..8, tensors 46 + (0..18)
+#define ANR_L_NOVEL0 21
+#define ANR_NUM_LAYERS_ALL 30
+#define ANR_NOVEL_T0 46  // tensor index of novel_pose_bw.bw_latent.weight in the packer's list
+
+__host__ __device__ constexpr LayerDesc novel_desc(int i) {
+  return LayerDesc{layer_desc(i).tensor_w + 19, layer_desc(i).tensor_b + 19, -1, -1, layer_desc(i).nout, 0,
+                   layer_desc(i).in_ch, layer_desc(i).ob, layer_desc(i).nseg,
+                   {layer_desc(i).seg[0], layer_desc(i).seg[1]}};
+}
 
 __host__ __device__ constexpr LayerDesc layer_desc_all(int i) {
   return i < ANR_NUM_LAYERS ? layer_desc(i)
        : i == ANR_L_VIEW ? LayerDesc{23, 24, -1, -1, 128, 0, 283, 8, 2, {{SRC_ACT, 64, 0}, {SRC_VEMB, 8, 256}}}
        : i == ANR_L_RGB  ? LayerDesc{25, 26, -1, -1, 3, 0, 128, 1, 1, {{SRC_ACT, 32, 0}, {0, 0, 0}}}
+       : i < ANR_NUM_LAYERS_ALL ? novel_desc(i - ANR_L_NOVEL0)
        : LayerDesc{0, 0, -1, -1, 0, 0, 0, 0, 0, {{0, 0, 0}, {0, 0, 0}}};
 }
 
@@ -101,6 +111,9 @@ __host__ __device__ constexpr int bias_offset(int i) {
   return o;
 }
 template <int L> inline constexpr int kBiasOff = bias_offset(L);
+// byte / float offsets from a base BW layer to its novel_pose_bw copy
+#define ANR_NOVEL_WOFF (layer_offset(ANR_L_NOVEL0) - layer_offset(0))
+#define ANR_NOVEL_BOFF (bias_offset(ANR_L_NOVEL0) - bias_offset(0))
 __host__ __device__ constexpr int bias_floats() { return bias_offset(ANR_NUM_LAYERS_ALL); }
 __host__ __device__ constexpr int packed_bytes() { return weights_bytes() + bias_floats() * 4; }
 

@@ -39,6 +39,7 @@ struct Pipe {
   int cur;
   int wave;
   int lane;
+  int pose_woff;  // added to slices of the pose-space BW pass (novel_pose_bw weights)
 
   __device__ __forceinline__ void stage(int off, int chunks, int buf) {
     unsigned char* dst = lds + buf * SLICE_MAX;
@@ -54,16 +55,18 @@ struct Pipe {
   }
 
   // Enter slice Q of layer L: wait for it, prefetch the slice that follows (next layer NL).
-  template <int L, int Q, int NL>
+  // CUR_POSE / NL_POSE: whether this layer / the next one belongs to the pose-space BW pass.
+  template <int L, int Q, int NL, bool CUR_POSE, bool NL_POSE>
   __device__ __forceinline__ const unsigned char* next() {
     constexpr int NS = layer_ksteps(L) / ANR_KSLICE;
     constexpr int nL = (Q + 1 < NS) ? L : NL;
     constexpr int nQ = (Q + 1 < NS) ? Q + 1 : 0;
+    constexpr bool tgt_pose = (Q + 1 < NS) ? CUR_POSE : NL_POSE;
     constexpr int nC = layer_chunks(nL);
     constexpr int noff = layer_offset(nL) + nQ * nC * ANR_KSLICE * 1024;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    stage(noff, nC, cur ^ 1);
+    stage(noff + (tgt_pose ? pose_woff : 0), nC, cur ^ 1);
     const unsigned char* r = lds + cur * SLICE_MAX;
     cur ^= 1;
     return r;
@@ -71,7 +74,7 @@ struct Pipe {
 };
 
 // One MLP layer: out = W * src + bias (acc layout), k-steps from the layer's segments.
-template <int L, int NL, bool RELU, int NIN, int NOUT>
+template <int L, int NL, bool RELU, bool CUR_POSE, bool NL_POSE, int NIN, int NOUT>
 __device__ __forceinline__ void layer(Pipe& p, const f32x4 (&in)[NIN], const float (&emb)[16], const float (&vemb)[8],
                                       f32x4 (&out)[NOUT], const float* __restrict__ bias, int g, int lane) {
   constexpr LayerDesc D = layer_desc_all(L);
@@ -88,7 +91,7 @@ __device__ __forceinline__ void layer(Pipe& p, const f32x4 (&in)[NIN], const flo
   const unsigned char* buf = nullptr;
   static_for<0, K>([&](auto t) {
     constexpr int tt = decltype(t)::value;
-    if constexpr (tt % ANR_KSLICE == 0) buf = p.template next<L, tt / ANR_KSLICE, NL>();
+    if constexpr (tt % ANR_KSLICE == 0) buf = p.template next<L, tt / ANR_KSLICE, NL, CUR_POSE, NL_POSE>();
     f32x4 w[C];
     static_for<0, C>([&](auto c) {
       constexpr int cc = decltype(c)::value;
@@ -238,21 +241,25 @@ __device__ __forceinline__ void store_rows(float* __restrict__ rows, int idx, co
   if (g < 2) *(f32x4*)(rows + (size_t)idx * 24 + 16 + 4 * g) = bw[1];
 }
 
-// BW MLP pass; NL = layer after bw_fc in the slice stream (0 for the second pass -> 9)
+// BW MLP pass; NL_AFTER = layer after bw_fc in the slice stream (0: this is the pose pass and the
+// T-pose pass follows; 9: this is the T-pose pass and the NeRF follows). The pose pass may read the
+// novel_pose_bw copy of the weights (p.pose_woff, boff).
 template <int NL_AFTER>
 __device__ __forceinline__ void bw_mlp(Pipe& p, const float (&emb)[16], const float (&vemb)[8], const float* __restrict__ bias,
-                                       const float* __restrict__ fold0, const float* __restrict__ fold5, f32x4 (&A)[17],
-                                       f32x4 (&B)[17], f32x4 (&fc)[2], int g, int lane) {
+                                       int boff, const float* __restrict__ fold0, const float* __restrict__ fold5,
+                                       f32x4 (&A)[17], f32x4 (&B)[17], f32x4 (&fc)[2], int g, int lane) {
+  constexpr bool P = NL_AFTER == 0;  // pose pass
   f32x4 dummy[1];
-  layer<0, 1, true>(p, dummy, emb, vemb, A, fold0, g, lane);
-  layer<1, 2, true>(p, A, emb, vemb, B, bias + kBiasOff<1>, g, lane);
-  layer<2, 3, true>(p, B, emb, vemb, A, bias + kBiasOff<2>, g, lane);
-  layer<3, 4, true>(p, A, emb, vemb, B, bias + kBiasOff<3>, g, lane);
-  layer<4, 5, true>(p, B, emb, vemb, A, bias + kBiasOff<4>, g, lane);
-  layer<5, 6, true>(p, A, emb, vemb, B, fold5, g, lane);
-  layer<6, 7, true>(p, B, emb, vemb, A, bias + kBiasOff<6>, g, lane);
-  layer<7, 8, true>(p, A, emb, vemb, B, bias + kBiasOff<7>, g, lane);
-  layer<8, NL_AFTER, false>(p, B, emb, vemb, fc, bias + kBiasOff<8>, g, lane);
+  const float* b = bias + boff;
+  layer<0, 1, true, P, P>(p, dummy, emb, vemb, A, fold0, g, lane);
+  layer<1, 2, true, P, P>(p, A, emb, vemb, B, b + kBiasOff<1>, g, lane);
+  layer<2, 3, true, P, P>(p, B, emb, vemb, A, b + kBiasOff<2>, g, lane);
+  layer<3, 4, true, P, P>(p, A, emb, vemb, B, b + kBiasOff<3>, g, lane);
+  layer<4, 5, true, P, P>(p, B, emb, vemb, A, b + kBiasOff<4>, g, lane);
+  layer<5, 6, true, P, P>(p, A, emb, vemb, B, fold5, g, lane);
+  layer<6, 7, true, P, P>(p, B, emb, vemb, A, b + kBiasOff<6>, g, lane);
+  layer<7, 8, true, P, P>(p, A, emb, vemb, B, b + kBiasOff<7>, g, lane);
+  layer<8, NL_AFTER, false, P, false>(p, B, emb, vemb, fc, b + kBiasOff<8>, g, lane);
 }
 
 __global__ __launch_bounds__(512) void k_mlp(MlpArgs a) {
@@ -269,8 +276,8 @@ __global__ __launch_bounds__(512) void k_mlp(MlpArgs a) {
   const int ntiles = (n + 127) / 128;
   if ((int)blockIdx.x >= ntiles) return;  // uniform per workgroup, before any LDS-DMA
 
-  Pipe p{smem, a.wimg, 0, wave, lane};
-  p.stage(layer_offset(0), layer_chunks(0), 0);
+  Pipe p{smem, a.wimg, 0, wave, lane, a.pose_woff};
+  p.stage(layer_offset(0) + a.pose_woff, layer_chunks(0), 0);
 
   const float* fold = a.fold;
   float tb_lo[3], tb_hi[3];
@@ -295,7 +302,7 @@ __global__ __launch_bounds__(512) void k_mlp(MlpArgs a) {
     lookup24(a.pbw32, pose, a.pbounds, a.pX, a.pY, a.pZ, g, init);
 #pragma unroll
     for (int s8 = 0; s8 < 8; ++s8) vemb[s8] = 0.f;
-    bw_mlp<0>(p, emb, vemb, a.bias, fold + 0, fold + 512, A, B, fc, g, lane);
+    bw_mlp<0>(p, emb, vemb, a.bias, a.pose_boff, fold + 0, fold + 512, A, B, fc, g, lane);
     blend_softmax(fc, init, g, bw);
     store_rows(a.pbw_rows, idx, bw, g, valid);
     float xt[3];
@@ -304,27 +311,27 @@ __global__ __launch_bounds__(512) void k_mlp(MlpArgs a) {
     // ---- T-pose: tbw lookup, BW MLP (latent 0) -> tbw rows (training loss only)
     embed<16>(xt, g, 10, emb);
     lookup24(a.tbw32, xt, a.tbounds, a.tX, a.tY, a.tZ, g, init);
-    bw_mlp<9>(p, emb, vemb, a.bias, fold + 256, fold + 768, A, B, fc, g, lane);
+    bw_mlp<9>(p, emb, vemb, a.bias, 0, fold + 256, fold + 768, A, B, fc, g, lane);
     blend_softmax(fc, init, g, bw);
     store_rows(a.tbw_rows, idx, bw, g, valid);
 
     // ---- canonical NeRF (TPoseHuman.calculate_alpha_rgb)
     f32x4 dummy[1];
     const float* bias = a.bias;
-    layer<9, 10, true>(p, dummy, emb, vemb, A, bias + kBiasOff<9>, g, lane);
-    layer<10, 11, true>(p, A, emb, vemb, B, bias + kBiasOff<10>, g, lane);
-    layer<11, 12, true>(p, B, emb, vemb, A, bias + kBiasOff<11>, g, lane);
-    layer<12, 13, true>(p, A, emb, vemb, B, bias + kBiasOff<12>, g, lane);
-    layer<13, 14, true>(p, B, emb, vemb, A, bias + kBiasOff<13>, g, lane);
-    layer<14, 15, true>(p, A, emb, vemb, B, bias + kBiasOff<14>, g, lane);
-    layer<15, 16, true>(p, B, emb, vemb, A, bias + kBiasOff<15>, g, lane);
-    layer<16, 17, true>(p, A, emb, vemb, B, bias + kBiasOff<16>, g, lane);
-    layer<17, 18, false>(p, B, emb, vemb, A, bias + kBiasOff<17>, g, lane);  // feature || alpha
+    layer<9, 10, true, false, false>(p, dummy, emb, vemb, A, bias + kBiasOff<9>, g, lane);
+    layer<10, 11, true, false, false>(p, A, emb, vemb, B, bias + kBiasOff<10>, g, lane);
+    layer<11, 12, true, false, false>(p, B, emb, vemb, A, bias + kBiasOff<11>, g, lane);
+    layer<12, 13, true, false, false>(p, A, emb, vemb, B, bias + kBiasOff<12>, g, lane);
+    layer<13, 14, true, false, false>(p, B, emb, vemb, A, bias + kBiasOff<13>, g, lane);
+    layer<14, 15, true, false, false>(p, A, emb, vemb, B, bias + kBiasOff<14>, g, lane);
+    layer<15, 16, true, false, false>(p, B, emb, vemb, A, bias + kBiasOff<15>, g, lane);
+    layer<16, 17, true, false, false>(p, A, emb, vemb, B, bias + kBiasOff<16>, g, lane);
+    layer<17, 18, false, false, false>(p, B, emb, vemb, A, bias + kBiasOff<17>, g, lane);  // feature || alpha
     const float sigma_raw = __shfl(A[16][0], pl);
-    layer<18, 19, false>(p, A, emb, vemb, B, fold + 1024, g, lane);  // latent_fc
+    layer<18, 19, false, false, false>(p, A, emb, vemb, B, fold + 1024, g, lane);  // latent_fc
     embed<8>(dir, g, 4, vemb);
-    layer<19, 20, true>(p, B, emb, vemb, A, bias + kBiasOff<19>, g, lane);  // view_fc
-    layer<20, 0, false>(p, A, emb, vemb, B, bias + kBiasOff<20>, g, lane);  // rgb_fc
+    layer<19, 20, true, false, false>(p, B, emb, vemb, A, bias + kBiasOff<19>, g, lane);  // view_fc
+    layer<20, 0, false, false, true>(p, A, emb, vemb, B, bias + kBiasOff<20>, g, lane);  // rgb_fc
 
     // ---- bbox mask, activations, outputs
     bool inside = true;

@@ -28,7 +28,8 @@ __global__ void k_pack_weights(PackArgs a) {
   const int col = layer_col(d, t, l >> 4);
   float v = 0.0f;
   const int main_ob = (d.nout + 15) / 16;
-  if (ob < d.ob && col >= 0) {
+  const bool present = a.t[d.tensor_w] != nullptr;
+  if (present && ob < d.ob && col >= 0) {
     if (ob < main_ob) {
       const int i = ob * 16 + (l & 15);
       if (i < d.nout) v = a.t[d.tensor_w][(size_t)i * d.in_ch + col];
@@ -49,7 +50,8 @@ __global__ void k_pack_bias(PackArgs a) {
   const int n = e - bias_offset(L);
   const int main_n = ((d.nout + 15) / 16) * 16;
   float v = 0.0f;
-  if (n < d.nout) v = a.t[d.tensor_b][n];
+  if (a.t[d.tensor_b] == nullptr) v = 0.0f;
+  else if (n < d.nout) v = a.t[d.tensor_b][n];
   else if (d.tensor_w2 >= 0 && n >= main_n && n - main_n < d.nout2) v = a.t[d.tensor_b2][n - main_n];
   ((float*)(a.out + weights_bytes()))[e] = v;
 }
@@ -74,11 +76,12 @@ __global__ __launch_bounds__(256) void k_prep(PrepArgs a) {
     const int which = k >> 8, nn = k & 255;
     float acc;
     if (which < 4) {
-      const int row = (which & 1) ? 0 : li + 1;  // pose: latent_index + 1; T-pose: 0
-      const float* lat = a.bw_latent + (size_t)row * 128;
-      const float* W = which < 2 ? a.w_bw0 : a.w_bw5;
+      const bool novel = a.novel && !(which & 1);  // pose pass of a novel-pose render
+      const int row = (which & 1) ? 0 : (novel ? (int)a.bw_latent_index[0] : li + 1);
+      const float* lat = (novel ? a.n_latent : a.bw_latent) + (size_t)row * 128;
+      const float* W = which < 2 ? (novel ? a.nw_bw0 : a.w_bw0) : (novel ? a.nw_bw5 : a.w_bw5);
       const int ld = which < 2 ? 191 : 447;
-      acc = which < 2 ? a.b_bw0[nn] : a.b_bw5[nn];
+      acc = which < 2 ? (novel ? a.nb_bw0 : a.b_bw0)[nn] : (novel ? a.nb_bw5 : a.b_bw5)[nn];
       for (int q = 0; q < 128; ++q) acc = fmaf(W[(size_t)nn * ld + 63 + q], lat[q], acc);
     } else {
       const float* lat = a.nf_latent + (size_t)li * 128;

@@ -53,6 +53,7 @@ int check_args(const anr_params* p, const anr_frame* f, const float* ray_o, cons
   if (!p || !f || !o || !ws || !ray_o || !ray_d || !near_ || !far_) return fail(ANR_E_ARG, "train: NULL argument");
   if (o->n_samples != 64) return fail(ANR_E_ARG, "train: only N_samples == 64 is supported");
   if (o->chunk <= 0 || n_rays <= 0) return fail(ANR_E_ARG, "train: bad chunk / n_rays");
+  if (o->novel_pose) return fail(ANR_E_ARG, "train: novel_pose is a render-only option");
   for (int i = 0; i < ANR_NUM_TENSORS; ++i)
     if (!p->t[i]) return fail(ANR_E_ARG, "train: NULL parameter tensor");
   if (!f->A || !f->R || !f->Th || !f->pbw || !f->tbw || !f->pbounds || !f->tbounds || !f->latent_index)

@@ -69,6 +69,14 @@ class Network(nn.Module):
         assert len(ts) == self.TENSOR_ORDER_LEN, len(ts)
         return ts
 
+    def novel_tensors(self):
+        """The 19 novel_pose_bw tensors (state_dict order) or [] (include/aninerf.h)."""
+        if not hasattr(self, 'novel_pose_bw'):
+            return []
+        ts = [t for _, t in self.novel_pose_bw.named_parameters()]
+        assert len(ts) == 19, len(ts)
+        return ts
+
     def forward(self, *args, **kwargs):
         raise RuntimeError('Network is a parameter container on this backend; call '
                            'Renderer(net).render(batch) (tpose_renderer.py:159) instead')

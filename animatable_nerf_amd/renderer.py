@@ -42,6 +42,8 @@ class _Call:
         fr = {k: _f32(batch[k], dev) for k in FRAME_KEYS}
         self.fr = fr
         self.li = batch['latent_index'].to(device=dev, dtype=torch.int64).reshape(-1).contiguous()
+        bli = batch.get('bw_latent_index', batch['latent_index'])
+        self.bli = bli.to(device=dev, dtype=torch.int64).reshape(-1).contiguous()
         f = _lib.Frame()
         f.A, f.R, f.Th = fr['A'].data_ptr(), fr['R'].data_ptr(), fr['Th'].data_ptr()
         f.pbw, f.pbounds = fr['pbw'].data_ptr(), fr['pbounds'].data_ptr()
@@ -50,6 +52,7 @@ class _Call:
             f.pbw_dims[i] = fr['pbw'].shape[1 + i]
             f.tbw_dims[i] = fr['tbw'].shape[1 + i]
         f.latent_index = self.li.data_ptr()
+        f.bw_latent_index = self.bli.data_ptr()
         self.frame = f
         o = _lib.RenderOpts()
         o.n_samples = ns
@@ -57,6 +60,7 @@ class _Call:
         o.norm_th = float(cfg.norm_th)
         o.train_th = float(cfg.train_th)
         o.t_rand = self.t_rand.data_ptr() if self.t_rand is not None else None
+        o.novel_pose = 1 if cfg.get('test_novel_pose', False) else 0
         self.opts = o
         self.rgb = torch.empty((1, R, 3), device=dev)
         self.acc = torch.empty((1, R), device=dev)
@@ -95,6 +99,10 @@ class Renderer:
         for i, t in enumerate(ts):
             p.t[i] = t.data_ptr()
         p.num_train_frame = self.net.num_train_frame
+        novel = self.net.novel_tensors()
+        for i, t in enumerate(novel):
+            p.novel[i] = t.detach().data_ptr()
+        ts = ts + [t.detach() for t in novel]
         if not pack:
             return p
         key = (getattr(self.net, '_anr_weights_epoch', 0),) + tuple((t.data_ptr(), t._version) for t in ts)

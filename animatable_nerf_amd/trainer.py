@@ -15,11 +15,11 @@ import ctypes
 import math
 
 import torch
-import torch.distributed as dist
 import torch.nn.functional as F
 
 from . import _lib
 from . import config as _config
+from .parallel import allreduce_mean_
 from .renderer import Renderer, _Call
 
 
@@ -118,9 +118,7 @@ class FusedStep:
         _lib.check(self.lib.anr_train_step(ctypes.byref(p), gp, ctypes.byref(c.frame), *c.ray_ptrs(), R,
                                            ctypes.byref(c.opts), _lib.ptr(rgb), _lib.ptr(mask), ctypes.byref(c.out),
                                            _lib.ptr(self.loss3), _lib.ptr(ws), ws_bytes, stream), 'anr_train_step')
-        if self.group is not None or (dist.is_available() and dist.is_initialized()):
-            dist.all_reduce(self.grad, op=dist.ReduceOp.SUM, group=self.group)
-            self.grad.div_(dist.get_world_size(self.group))
+        allreduce_mean_(self.grad, self.group)
         self.t += 1
         _lib.check(self.lib.anr_adam(_lib.ptr(self.flat), _lib.ptr(self.grad), _lib.ptr(self.m), _lib.ptr(self.v),
                                      self.n, float(self.lr if lr is None else lr), self.betas[0], self.betas[1],

@@ -48,11 +48,16 @@ enum {
  *   28..43 bw_linears.{0..7}.{weight,bias}   in: 191,256,256,256,256,447,256,256
  *   44,45 bw_fc.{weight,bias} (24,256,1)                                                     */
 #define ANR_NUM_TENSORS 46
+/* novel_pose_bw (BackwardBlendWeight, tpose_nerf_network.py:278-315; present when
+ * cfg.aninerf_animation): bw_latent.weight (E,128), bw_linears.{0..7}.{weight,bias},
+ * bw_fc.{weight,bias} — 19 tensors, state_dict order. */
+#define ANR_NUM_NOVEL_TENSORS 19
 
 typedef struct anr_params {
   const float* t[ANR_NUM_TENSORS];  /* device pointers, state_dict order above */
   int num_train_frame;              /* F: rows of nf_latent (bw_latent has F+1) */
   const void* packed;               /* device weight image written by anr_params_pack */
+  const float* novel[ANR_NUM_NOVEL_TENSORS];  /* novel_pose_bw tensors or all NULL */
 } anr_params;
 
 typedef struct anr_frame {
@@ -66,6 +71,7 @@ typedef struct anr_frame {
   int tbw_dims[3];
   const float* tbounds;    /* (2,3) device */
   const int64_t* latent_index;  /* (1) device: batch['latent_index'] */
+  const int64_t* bw_latent_index;  /* (1) device: batch['bw_latent_index'] (novel pose only) */
 } anr_frame;
 
 typedef struct anr_render_opts {
@@ -74,6 +80,8 @@ typedef struct anr_render_opts {
   float norm_th;     /* cfg.norm_th (0.05) */
   float train_th;    /* cfg.train_th (0) */
   const float* t_rand;  /* (R, n_samples) device stratification draws, or NULL (eval / perturb 0) */
+  int novel_pose;    /* cfg.test_novel_pose: pose-space blend weights from novel_pose_bw
+                        with bw_latent_index (tpose_nerf_network.py:93-94); render only */
 } anr_render_opts;
 
 /* Outputs (device). raw may be NULL (then kept in the workspace). */

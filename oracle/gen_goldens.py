@@ -281,5 +281,37 @@ def adversarial_rays(bounds, n):
     return np.array(o_list, np.float32), np.array(d_list, np.float32)
 
 
+def main_novel():
+    """G5: novel-pose render (cfg.test_novel_pose: pose-space blend weights from novel_pose_bw with
+    bw_latent_index, tpose_nerf_network.py:93-94), 64 rays, latent_index 3, bw_latent_index 5."""
+    import torch
+    torch.set_num_threads(1)
+    sys.path.insert(0, REPO)
+    from animatable_nerf_amd.synthetic import Scene, init_state_dict
+    cfg, make_network, make_renderer = import_reference(opts=('aninerf_animation', 'True', 'test_novel_pose', 'True'))
+    from lib.utils.if_nerf import if_nerf_data_utils as dutils
+    net = make_network(cfg)
+    shapes = {k: tuple(v.shape) for k, v in net.state_dict().items()}
+    sd = init_state_dict(shapes)
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
+    cfg.perturb = 0
+    net.train()
+    renderer = make_renderer(cfg, net)
+    scene = Scene(vsize=0.05)
+    ro, rd = scene.box_rays(64, seed=2)
+    near, far, mask = dutils.get_near_far(scene.bounds, ro, rd)
+    b = scene.batch_arrays(ro[mask], rd[mask], near.astype(np.float32), far.astype(np.float32), latent_index=3)
+    b['bw_latent_index'] = np.array([5])
+    batch = {k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in b.items()}
+    with torch.no_grad():
+        ret = renderer.render(batch)
+    np.savez_compressed(os.path.join(OUT, 'g5_novel_pose.npz'), latent_index=3, bw_latent_index=5,
+                        num_eval_frame=cfg.num_eval_frame, **{'out_' + k: v.numpy() for k, v in ret.items()})
+    print('novel-pose golden written')
+
+
 if __name__ == '__main__':
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == '--novel':
+        main_novel()
+    else:
+        main()

@@ -47,3 +47,35 @@ def batch_np(sc, ray_o, ray_d, rgb=None):
 
 def to_torch(b, device='cpu'):
     return {k: torch.from_numpy(np.ascontiguousarray(v)).to(device) for k, v in b.items()}
+
+
+def novel_cfg():
+    from animatable_nerf_amd import config
+    cfg = config.defaults()
+    cfg.aninerf_animation = True
+    cfg.test_novel_pose = True
+    cfg.num_eval_frame = 133
+    cfg.perturb = 0
+    return cfg
+
+
+@functools.lru_cache(maxsize=1)
+def state_dict_novel_np():
+    net = network.Network(novel_cfg())
+    shapes = {k: tuple(v.shape) for k, v in net.state_dict().items()}
+    return synthetic.init_state_dict(shapes)
+
+
+def make_net_novel(device='cpu'):
+    net = network.Network(novel_cfg())
+    network.load_numpy_state(net, state_dict_novel_np())
+    return net.to(device)
+
+
+def novel_batch_np():
+    sc = scene(0.05)
+    ro, rd = sc.box_rays(64, seed=2)
+    b, mask = batch_np(sc, ro, rd)
+    b['latent_index'] = np.array([3])
+    b['bw_latent_index'] = np.array([5])
+    return b

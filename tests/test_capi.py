@@ -36,7 +36,8 @@ def test_library_exports_every_declared_symbol(lib):
 def test_version_and_sizes(lib):
     assert lib.anr_version() == 1
     # 19 weight layers + view/rgb heads, fp32 weight image + padded biases
-    assert lib.anr_params_packed_bytes() == 4_767_744 + 4 * 4_800
+    # + 9 novel_pose_bw layers (same image as the 9 BW layers)
+    assert lib.anr_params_packed_bytes() == 4_767_744 + 2_031_616 + 4 * (4_800 + 2_080)
 
 
 def test_workspace_grows_with_rays(lib):

@@ -1,0 +1,81 @@
+"""CPU, world_size 2 over gloo: the N>1 plumbing of animatable_nerf_amd.parallel — the mean
+all-reduce of the flat gradient blob (training, DDP semantics of trainer.py:13-18) reproduces the
+average of the per-rank oracle gradients, the max-over-ranks timing, and chunk-aligned ray shards."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from animatable_nerf_amd import parallel
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def _grads(seed):
+    from oracle import restate
+    from tests._common import batch_np, oracle_params, scene, to_torch
+    torch.set_num_threads(1)
+    sc = scene(0.05)
+    ro, rd = sc.box_rays(48, seed=seed)
+    rgb = np.random.default_rng(seed).random((48, 3)).astype(np.float32)
+    b, _ = batch_np(sc, ro, rd, rgb=rgb)
+    bt = to_torch(b)
+    P = oracle_params(requires_grad=True)
+    t_rand = torch.from_numpy(np.random.default_rng(seed + 1).random((bt['ray_o'].shape[1], 64)).astype(np.float32))
+    ret = restate.render(P, bt, t_rand=t_rand)
+    loss, _ = restate.loss_terms(ret, bt)
+    loss.backward()
+    return torch.cat([v.grad.reshape(-1) for v in P.values()])
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    try:
+        r, w = parallel.init_from_env('gloo')
+        assert (r, w) == (rank, world) and parallel.is_dist()
+        g = _grads(100 + rank).clone()
+        expect = (_grads(100) + _grads(101)) / 2
+        parallel.allreduce_mean_(g)
+        ok_grad = torch.allclose(g, expect, rtol=1e-6, atol=1e-12)
+        tmax = parallel.max_over_ranks(1.0 + rank, 'cpu')
+        q.put((rank, ok_grad, tmax))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_gloo_world2_gradient_mean_and_timing():
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, ok_grad, tmax in res:
+        assert ok_grad, rank
+        assert tmax == 2.0
+
+
+@pytest.mark.parametrize('n,world', [(262142, 8), (262142, 3), (1024, 2), (5000, 4), (2048, 8)])
+def test_shard_chunks_cover_whole_chunks(n, world):
+    spans = [parallel.shard_chunks(n, r, world) for r in range(world)]
+    assert spans[0][0] == 0 and spans[-1][1] == n
+    for (a0, a1), (b0, b1) in zip(spans, spans[1:]):
+        assert a1 == b0
+    for a0, a1 in spans:
+        if a0 == a1:  # more ranks than chunks: trailing ranks are empty
+            continue
+        assert a0 % 2048 == 0 and (a1 % 2048 == 0 or a1 == n)

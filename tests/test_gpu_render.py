@@ -147,3 +147,26 @@ def test_full_frame_properties(renderer, dev):
     for k in ('rgb_map', 'acc_map', 'depth_map'):
         err = (r1[k][:, i0:i0 + 2048].cpu() - ref[k]).abs().max().item()
         assert err <= TOL, (k, err)
+
+
+def test_novel_pose_render_matches_reference(dev):
+    """A19: cfg.test_novel_pose renders with novel_pose_bw + bw_latent_index (golden G5)."""
+    from animatable_nerf_amd.renderer import Renderer
+    from ._common import make_net_novel, novel_batch_np, novel_cfg
+    g = golden('g5_novel_pose')
+    net = make_net_novel(dev)
+    net.train()
+    r = Renderer(net, novel_cfg())
+    ret = r.render_device(to_torch(novel_batch_np(), dev))
+    ret = {k: v.cpu() for k, v in ret.items()}
+    assert torch.equal(_keep(ret['raw']), torch.from_numpy(g['out_raw'][0, :, :3].sum(-1) != 0))
+    for k in ('rgb_map', 'acc_map', 'depth_map', 'raw', 'pbw', 'tbw'):
+        assert ret[k].shape == g['out_' + k].shape, k
+        err = (ret[k] - torch.from_numpy(g['out_' + k])).abs().max().item()
+        assert err <= TOL, (k, err)
+    # the same network without the flag renders the training-pose path (different weights)
+    cfg = novel_cfg()
+    cfg.test_novel_pose = False
+    r2 = Renderer(net, cfg)
+    ret2 = r2.render_device(to_torch(novel_batch_np(), dev))
+    assert (ret2['rgb_map'].cpu() - ret['rgb_map']).abs().max().item() > 1e-3

@@ -149,3 +149,13 @@ def test_g4_train_step():
         if k.startswith('delta_'):
             np.testing.assert_allclose((P[k[6:]].detach() - before[k[6:]]).numpy(), g[k], rtol=1e-4, atol=1e-8,
                                        err_msg=k)
+
+
+def test_g5_novel_pose_bit_exact():
+    from ._common import novel_batch_np, state_dict_novel_np
+    g = golden('g5_novel_pose')
+    P = {k: torch.from_numpy(v.copy()) for k, v in state_dict_novel_np().items()}
+    with torch.no_grad():
+        ret = restate.render(P, to_torch(novel_batch_np()), novel_pose=True)
+    for k in ('rgb_map', 'acc_map', 'depth_map', 'raw', 'pbw', 'tbw'):
+        np.testing.assert_array_equal(ret[k].numpy(), g['out_' + k], err_msg=k)
