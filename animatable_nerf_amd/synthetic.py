@@ -147,6 +147,127 @@ class Scene:
         }
 
 
+def lbs_vertices(verts, skin, A):
+    """Forward LBS of (V,3) vertices with per-vertex weights (V,24) and A (24,4,4), float64 -> f32."""
+    T = np.einsum('vj,jab->vab', skin.astype(np.float64), A.astype(np.float64))
+    v = np.einsum('vab,vb->va', T[:, :3, :3], verts.astype(np.float64)) + T[:, :3, 3]
+    return v.astype(np.float32)
+
+
+def big_pose_A(joints):
+    """``tpose_pdf_dataset.py:91-100`` load_bigpose: float32 axis-angles, joints 1/2 z = +-30 deg."""
+    big = np.zeros([24, 3]).astype(np.float32).ravel()
+    big[5] = np.deg2rad(30)
+    big[8] = np.deg2rad(-30)
+    return rigid_transformation(big.reshape(-1, 3), joints, PARENTS), big
+
+
+class PdfScene(Scene):
+    """Config 5 (sdf_pdf) frame: the same subject as ``Scene`` with the keys of
+    ``tpose_pdf_dataset.py:270-291``. The ellipsoid vertices are the T pose; ``pvertices`` = LBS with
+    the frame's A, ``tvertices`` = LBS with ``big_A``; ``weights`` = the per-vertex skin weights;
+    pbounds = wbounds = bounds of pvertices (R = I, Th = 0), tbounds = bounds of tvertices.
+    ``occupancy`` is a seeded random pixel mask (PCG64 seed 9) so both ``msk_sdf`` branches are hit.
+    """
+
+    def __init__(self, vsize=0.05, pose_scale=0.1, seed=0):
+        super().__init__(vsize=vsize, pose_scale=pose_scale, seed=seed)
+        self.big_A, self.big_poses = big_pose_A(self.joints)
+        self.pvertices = lbs_vertices(self.verts, self.skin, self.A)
+        self.tvertices = lbs_vertices(self.verts, self.skin, self.big_A)
+        self.pbounds = get_bounds(self.pvertices)
+        self.tbounds = get_bounds(self.tvertices)
+        self.bounds = self.pbounds  # box rays and near/far use the posed body
+        self.pose_vec = self.poses.ravel().astype(np.float32)
+
+    def batch_arrays(self, ray_o, ray_d, near, far, latent_index=0, rgb=None, occ_seed=9):
+        R = ray_o.shape[0]
+        if rgb is None:
+            rgb = np.zeros((R, 3), np.float32)
+        occ = np.random.Generator(np.random.PCG64(occ_seed)).integers(0, 2, R).astype(np.uint8)
+        return {
+            'ray_o': ray_o[None].astype(np.float32), 'ray_d': ray_d[None].astype(np.float32),
+            'near': near[None].astype(np.float32), 'far': far[None].astype(np.float32),
+            'occupancy': occ[None], 'mask_at_box': np.ones((1, R), np.bool_),
+            'rgb': rgb[None].astype(np.float32),
+            'A': self.A[None], 'big_A': self.big_A[None], 'poses': self.pose_vec[None],
+            'weights': self.skin[None], 'tvertices': self.tvertices[None], 'pvertices': self.pvertices[None],
+            'pbounds': self.pbounds[None], 'wbounds': self.pbounds[None], 'tbounds': self.tbounds[None],
+            'R': self.R[None], 'Th': self.Th[None],
+            'H': np.array([0]), 'W': np.array([0]),
+            'latent_index': np.array([latent_index]), 'bw_latent_index': np.array([latent_index]),
+            'frame_index': np.array([0]), 'cam_ind': np.array([0]),
+        }
+
+
+def init_state_dict_sdf(shapes, seed=4321):
+    """Deterministic weights for the sdf_pdf network (``anisdf_pdf_network.py``), per tensor a PCG64
+    stream seeded with (seed, index):
+
+      * ``sdf_network.lin*``: the geometric init of ``anisdf_pdf_network.py:388-410`` (last layer
+        N(sqrt(pi)/sqrt(256), 1e-4) with bias -0.5; lin0 only on xyz; lin4 zero on the gamma part),
+        hidden biases U(+-0.01) instead of 0 so the bias path is exercised;
+      * ``weight_v`` of the colour net U(+-1/sqrt(in)), its biases likewise;
+      * every ``weight_g`` = row norm of its ``weight_v`` times U(0.8, 1.2) (so weight-norm is not
+        the identity);
+      * Conv1d (``resd_linears``/``resd_fc``) U(+-1/sqrt(fan_in)), ``resd_fc.weight`` x16 (so the
+        displacement reaches a few cm), ``resd_fc.bias`` = 0 (``anisdf_pdf_network.py:31``);
+        embeddings N(0,1); ``beta`` = 0.1.
+    """
+    out = {}
+    names = list(shapes)
+    rngs = {n: np.random.Generator(np.random.PCG64([seed, i])) for i, n in enumerate(names)}
+    d0 = 39
+    for name in names:
+        shape = shapes[name]
+        rng = rngs[name]
+        if name.endswith('beta'):
+            out[name] = np.array(0.1, np.float32)
+            continue
+        if len(shape) == 2 and name.endswith('.weight') and 'latent' in name:
+            out[name] = rng.standard_normal(shape).astype(np.float32)
+            continue
+        mod, leaf = name.rsplit('.', 1)
+        if 'sdf_network' in mod:
+            l = int(mod[-1])
+            if leaf == 'weight_v':
+                o, i = shape
+                if l == 8:
+                    v = rng.normal(np.sqrt(np.pi) / np.sqrt(i), 1e-4, size=shape)
+                elif l == 0:
+                    v = np.zeros(shape)
+                    v[:, :3] = rng.normal(0.0, np.sqrt(2) / np.sqrt(o), size=(o, 3))
+                else:
+                    v = rng.normal(0.0, np.sqrt(2) / np.sqrt(o), size=shape)
+                    if l == 4:
+                        v[:, -(d0 - 3):] = 0.0
+                out[name] = v.astype(np.float32)
+            elif leaf == 'bias':
+                out[name] = (np.full(shape, -0.5) if l == 8 else rng.uniform(-0.01, 0.01, size=shape)).astype(np.float32)
+            continue
+        if 'color_network' in mod:
+            if leaf == 'weight_v':
+                out[name] = rng.uniform(-1, 1, size=shape).astype(np.float32) / np.float32(np.sqrt(shape[1]))
+            elif leaf == 'bias':
+                fan = shapes[mod + '.weight_v'][1]
+                out[name] = rng.uniform(-1, 1, size=shape).astype(np.float32) / np.float32(np.sqrt(fan))
+            continue
+        if leaf in ('weight', 'bias') and len(shapes[mod + '.weight']) == 3:
+            fan = shapes[mod + '.weight'][1]
+            arr = rng.uniform(-1, 1, size=shape) / np.sqrt(fan)
+            if name == 'resd_fc.bias':
+                arr = np.zeros(shape)
+            elif name == 'resd_fc.weight':
+                arr = arr * 16.0  # displacements of a few cm, so 0.05*tanh is not ~linear
+            out[name] = arr.astype(np.float32)
+    for name in names:  # weight_g after every weight_v exists
+        if name.endswith('weight_g'):
+            v = out[name[:-1] + 'v'].astype(np.float64)
+            s = rngs[name].uniform(0.8, 1.2, size=(v.shape[0], 1))
+            out[name] = (np.linalg.norm(v, axis=1, keepdims=True) * s).astype(np.float32)
+    return {n: out[n] for n in names}
+
+
 def init_state_dict(shapes, seed=1234, alpha_bias=3.0):
     """Deterministic weights for a state_dict given {name: shape} (insertion order matters).
 

@@ -50,10 +50,12 @@ def _install_stubs():
         sys.modules[name] = _Stub(name)
 
 
-def import_reference(cfg_file='configs/aninerf_s9p.yaml', opts=()):
+def import_reference(cfg_file='configs/aninerf_s9p.yaml', opts=(), knn=None):
     sys.dont_write_bytecode = True
     os.environ['PYTHONDONTWRITEBYTECODE'] = '1'
     _install_stubs()
+    if knn is not None:  # the KNN restatement stands in for pytorch3d (unpinned boundary)
+        sys.modules['pytorch3d.ops.knn'].knn_points = knn
     os.chdir(REF)
     sys.path.insert(0, REF)
     sys.argv = ['gen_goldens', '--cfg_file', cfg_file, 'gpus', '[]'] + list(opts)
@@ -310,8 +312,134 @@ def main_novel():
     print('novel-pose golden written')
 
 
+def main_sdf():
+    """G6 / G7: the sdf_pdf variant (configs/sdf_pdf/anisdf_pdf_s9p.yaml, config 5), eval render.
+
+    pytorch3d.ops.knn.knn_points is replaced by ``oracle.restate_sdf.knn_points`` (pytorch3d is not
+    installed, so parity at the KNN boundary is unpinned); everything after it is the reference.
+    G6: 64 rays with intermediates. G7: 4,608 rays = 3 chunks (the in-place tbounds widening per
+    chunk, anisdf_pdf_network.py:203-205; forced argmin in the corner-grazing chunk; msk_sdf lists).
+    """
+    import torch
+    from collections import namedtuple
+    torch.set_num_threads(1)
+    sys.path.insert(0, REPO)
+    from oracle.restate_sdf import knn_points as knn_restated
+    from animatable_nerf_amd.synthetic import PdfScene, init_state_dict_sdf, PARENTS
+    KNN = namedtuple('KNN', ['dists', 'idx', 'knn'])
+
+    def knn_stub(src, ref, K=1, **kw):
+        d, i = knn_restated(src, ref, K)
+        return KNN(d, i, None)
+
+    cfg, make_network, make_renderer = import_reference('configs/sdf_pdf/anisdf_pdf_s9p.yaml',
+                                                        opts=('init_sdf', "''"), knn=knn_stub)
+    import lib.networks.bw_deform.anisdf_pdf_network as sdfn
+    from lib.utils import sample_utils
+    from lib.utils.if_nerf import if_nerf_data_utils as dutils
+    net = make_network(cfg)
+    shapes = {k: tuple(v.shape) for k, v in net.state_dict().items()}
+    sd = init_state_dict_sdf(shapes)
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
+    cfg.perturb = 0
+    net.train()
+    renderer = make_renderer(cfg, net)
+    scene = PdfScene(vsize=0.05)
+    big_ref = dutils.get_rigid_transformation(scene.big_poses.reshape(-1, 3), scene.joints, PARENTS)
+    assert np.array_equal(big_ref.astype(np.float32), scene.big_A)
+
+    def batch_for(ray_o, ray_d):
+        near, far, mask = dutils.get_near_far(scene.pbounds, ray_o, ray_d)
+        b = scene.batch_arrays(ray_o[mask], ray_d[mask], near.astype(np.float32), far.astype(np.float32),
+                               latent_index=7)
+        return {k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in b.items()}, mask
+
+    rec = {'sbc': [], 'resd': [], 'th': []}
+    orig_sbc = sample_utils.sample_blend_closest_points
+    orig_resd = sdfn.Network.calculate_residual_deformation
+    orig_th = sdfn.TPoseHuman.forward
+
+    def sbc(src, ref, values, K=5, exp=1e-8):
+        out = orig_sbc(src, ref, values, K, exp)
+        rec['sbc'].append(tuple(o.detach().clone() for o in out))
+        return out
+
+    def resd_fn(self, tpose, batch):
+        out = orig_resd(self, tpose, batch)
+        rec['resd'].append((tpose.detach().clone(), out.detach().clone()))
+        return out
+
+    def th_fn(self, wpts, viewdir, dists, batch):
+        x, v = wpts.detach().clone(), viewdir.detach().clone()
+        out = orig_th(self, wpts, viewdir, dists, batch)
+        rec['th'].append((x, v, {k: t.detach().clone() for k, t in out.items()}))
+        return out
+
+    sample_utils.sample_blend_closest_points = sbc
+    sdfn.Network.calculate_residual_deformation = resd_fn
+    sdfn.TPoseHuman.forward = th_fn
+
+    # ---- G6 tiny
+    ro, rd = scene.box_rays(64, seed=2)
+    batch, mask = batch_for(ro, rd)
+    tb0 = batch['tbounds'].clone()
+    with torch.no_grad():
+        ret = renderer.render(batch)
+    pre_bw, pnorm = rec['sbc'][0]
+    kbw, _ = rec['sbc'][1]
+    bigpose, resd = rec['resd'][0]
+    tpose, tdirs, th = rec['th'][0]
+    g6 = dict(mask=mask, near=batch['near'].numpy(), far=batch['far'].numpy(), tbounds_before=tb0.numpy(),
+              tbounds_after=batch['tbounds'].numpy(), occupancy=batch['occupancy'].numpy(),
+              pre_bw=pre_bw.numpy(), pnorm=pnorm.numpy(), kept_bw=kbw.numpy(), init_bigpose=bigpose.numpy(),
+              resd=resd.numpy(), tpose=tpose.numpy(), tpose_dirs=tdirs.numpy(),
+              th_sdf=th['sdf'].numpy(), th_gradients=th['gradients'].numpy(), th_raw=th['raw'].numpy(),
+              **{'out_' + k: v.numpy() for k, v in ret.items()})
+    np.savez_compressed(os.path.join(OUT, 'g6_sdf_tiny.npz'), **g6)
+
+    # ---- G7 chunks: 4096 box rays + 512 corner-grazing rays
+    for v in rec.values():
+        v.clear()
+    ro, rd = scene.box_rays(4096, seed=5)
+    rng = np.random.Generator(np.random.PCG64(7))
+    corners = np.array([[sx, sy, sz] for sx in (0, 1) for sy in (0, 1) for sz in (0, 1)])
+    b = scene.pbounds.astype(np.float64)
+    tgt = b[corners[rng.integers(0, 8, 512)], [0, 1, 2]]
+    tgt = tgt - np.sign(tgt) * rng.uniform(0.0, 0.01, size=(512, 3))
+    o2 = np.broadcast_to(np.array([0.0, 0.0, 3.0]), (512, 3))
+    d2 = tgt - o2
+    d2 /= np.linalg.norm(d2, axis=1, keepdims=True)
+    ro = np.concatenate([ro, o2.astype(np.float32)])
+    rd = np.concatenate([rd, d2.astype(np.float32)])
+    batch, mask = batch_for(ro, rd)
+    with torch.no_grad():
+        ret = renderer.render(batch)
+    keep = []
+    for c in range(0, len(rec['sbc']), 2):
+        pn = rec['sbc'][c][1][..., 0]
+        k = pn < 0.1
+        k[torch.arange(len(pn)), pn.argmin(dim=1)] = True
+        keep.append(k[0])
+    keep = torch.cat(keep).numpy()
+    n_kept = int(keep.sum())
+    rows = np.arange(0, n_kept, 29)
+    g7 = dict(ray_o=ro, ray_d=rd, mask=mask, keep_bits=np.packbits(keep), n_kept=np.int64(n_kept),
+              tbounds_after=batch['tbounds'].numpy(),
+              **{'out_' + k: ret[k].numpy() for k in ('rgb_map', 'acc_map', 'depth_map', 'msk_sdf', 'msk_label')},
+              kept_raw=ret['raw'][0, keep].numpy(), kept_sdf=ret['sdf'][0, keep, 0].numpy(),
+              row_idx=rows, resd_rows=ret['resd'][0, rows].numpy(), grad_rows=ret['gradients'][0, rows].numpy(),
+              resd_sum=ret['resd'].double().sum(1).numpy(), grad_sum=ret['gradients'].double().sum(1).numpy())
+    np.savez_compressed(os.path.join(OUT, 'g7_sdf_chunks.npz'), **g7)
+    sample_utils.sample_blend_closest_points = orig_sbc
+    sdfn.Network.calculate_residual_deformation = orig_resd
+    sdfn.TPoseHuman.forward = orig_th
+    print('sdf_pdf goldens written')
+
+
 if __name__ == '__main__':
     if len(sys.argv) > 1 and sys.argv[1] == '--novel':
         main_novel()
+    elif len(sys.argv) > 1 and sys.argv[1] == '--sdf':
+        main_sdf()
     else:
         main()

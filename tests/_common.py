@@ -79,3 +79,51 @@ def novel_batch_np():
     b['latent_index'] = np.array([3])
     b['bw_latent_index'] = np.array([5])
     return b
+
+
+# ---- sdf_pdf (config 5)
+@functools.lru_cache(maxsize=2)
+def pdf_scene(vsize=0.05):
+    return synthetic.PdfScene(vsize=vsize)
+
+
+@functools.lru_cache(maxsize=1)
+def state_dict_sdf_np():
+    from animatable_nerf_amd import network_sdf
+    net = network_sdf.Network(sdf_cfg())
+    shapes = {k: tuple(v.shape) for k, v in net.state_dict().items()}
+    return synthetic.init_state_dict_sdf(shapes)
+
+
+def oracle_params_sdf():
+    return {k: torch.from_numpy(v.copy()) for k, v in state_dict_sdf_np().items()}
+
+
+def sdf_cfg():
+    from animatable_nerf_amd import config
+    cfg = config.defaults()
+    cfg.num_train_frame = 260
+    cfg.num_latent_code = 260
+    cfg.perturb = 0
+    return cfg
+
+
+def make_net_sdf(device='cpu'):
+    from animatable_nerf_amd import network_sdf
+    net = network_sdf.Network(sdf_cfg())
+    network.load_numpy_state(net, state_dict_sdf_np())
+    return net.to(device)
+
+
+def pdf_batch_np(sc, ray_o, ray_d, latent_index=7):
+    from oracle import restate
+    near, far, mask = restate.near_far(sc.pbounds, ray_o, ray_d)
+    b = sc.batch_arrays(ray_o[mask], ray_d[mask], near.astype(np.float32), far.astype(np.float32),
+                        latent_index=latent_index)
+    return b, mask
+
+
+def pdf_g7_rays():
+    """The 4,608 G7 rays (oracle/gen_goldens.py main_sdf)."""
+    g = golden('g7_sdf_chunks')
+    return g['ray_o'], g['ray_d']
