@@ -14,10 +14,12 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, 'libaninerf_hip.so')
 NUM_TENSORS = 46
 NUM_NOVEL_TENSORS = 19
+NUM_SDF_TENSORS = 63
 
 EXPORTS = ('anr_near_far', 'anr_params_packed_bytes', 'anr_params_pack', 'anr_render_workspace_bytes',
            'anr_render_fwd', 'anr_render_counts', 'anr_render_bw_rows', 'anr_profile_enable', 'anr_profile_read',
            'anr_train_workspace_bytes', 'anr_train_fwd', 'anr_train_bwd', 'anr_train_step', 'anr_adam',
+           'anr_sdf_render_workspace_bytes', 'anr_sdf_render_fwd', 'anr_sdf_render_counts', 'anr_sdf_render_rows',
            'anr_last_error', 'anr_version')
 
 c_float_p = ctypes.c_void_p
@@ -43,6 +45,22 @@ class RenderOpts(ctypes.Structure):
 class RenderOut(ctypes.Structure):
     _fields_ = [('rgb_map', ctypes.c_void_p), ('acc_map', ctypes.c_void_p), ('depth_map', ctypes.c_void_p),
                 ('raw', ctypes.c_void_p)]
+
+
+class SdfParams(ctypes.Structure):
+    _fields_ = [('t', ctypes.c_void_p * NUM_SDF_TENSORS)]
+
+
+class SdfFrame(ctypes.Structure):
+    _fields_ = [('A', ctypes.c_void_p), ('big_A', ctypes.c_void_p), ('R', ctypes.c_void_p), ('Th', ctypes.c_void_p),
+                ('poses', ctypes.c_void_p), ('pvertices', ctypes.c_void_p), ('weights', ctypes.c_void_p),
+                ('n_verts', ctypes.c_int), ('tbounds', ctypes.c_void_p), ('latent_index', ctypes.c_void_p),
+                ('occupancy', ctypes.c_void_p)]
+
+
+class SdfRenderOut(ctypes.Structure):
+    _fields_ = [('rgb_map', ctypes.c_void_p), ('acc_map', ctypes.c_void_p), ('depth_map', ctypes.c_void_p),
+                ('raw', ctypes.c_void_p), ('sdf', ctypes.c_void_p), ('tbounds_out', ctypes.c_void_p)]
 
 
 _lib = None
@@ -79,6 +97,13 @@ def load():
                                    ctypes.c_size_t, P]
     lib.anr_adam.argtypes = [P, P, P, P, ctypes.c_long, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float,
                              ctypes.c_float, ctypes.c_int, ctypes.c_float, P]
+    lib.anr_sdf_render_workspace_bytes.restype = ctypes.c_size_t
+    lib.anr_sdf_render_workspace_bytes.argtypes = [ctypes.c_int, ctypes.POINTER(RenderOpts)]
+    lib.anr_sdf_render_fwd.argtypes = [ctypes.POINTER(SdfParams), ctypes.POINTER(SdfFrame), P, P, P, P, ctypes.c_int,
+                                       ctypes.POINTER(RenderOpts), ctypes.POINTER(SdfRenderOut), P, ctypes.c_size_t, P]
+    lib.anr_sdf_render_counts.restype = P
+    lib.anr_sdf_render_counts.argtypes = [P, ctypes.c_int, ctypes.POINTER(RenderOpts)]
+    lib.anr_sdf_render_rows.argtypes = [P, ctypes.c_int, ctypes.POINTER(RenderOpts), P, P, P, P, P]
     lib.anr_profile_enable.argtypes = [ctypes.c_int]
     lib.anr_profile_read.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]
     lib.anr_last_error.restype = ctypes.c_char_p

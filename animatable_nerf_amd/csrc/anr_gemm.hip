@@ -178,8 +178,20 @@ __global__ __launch_bounds__(256) void k_gemm_t(GemmArgs g) {
         }
         if (g.bias) v += g.bias[n];
         if (g.accumulate) v += *c;
+        if (g.div_pre != 0.f) v = v / g.div_pre;
         if (g.relu) v = fmaxf(v, 0.f);
+        if (g.softplus) {  // torch softplus(beta=100, threshold=20) and the factor its backward uses
+          const float z = v * 100.f;
+          const float e = expf(z);
+          g.deriv[(long)m * g.ldd + n] = z > 20.f ? -1.f : e;
+          v = z > 20.f ? v : log1pf(e) / 100.f;
+        }
+        if (g.spd && n < g.spd_n) {
+          const float d = g.spd[(long)m * g.ldsd + n];
+          if (d >= 0.f) v = v * d / (d + 1.f);
+        }
         if (g.mask && !(g.mask[(long)m * g.ldm + n] > 0.f)) v = 0.f;
+        if (g.div_post != 0.f) v = v / g.div_post;
         *c = v;
       }
 }

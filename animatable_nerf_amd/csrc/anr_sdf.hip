@@ -1,0 +1,392 @@
+// anr_sdf.hip — per-sample kernels of the sdf_pdf render path (config 5).
+//
+//   k_sdf_front     B1 + A2-A6: z, world->pose, exact 5-NN over the posed SMPL vertices (LDS-resident),
+//                   inverse-distance weights, keep ballot (pnorm < 0.1) + per-chunk argmin
+//                   (anisdf_pdf_network.py:156-177, sample_utils.py:309-348)
+//   k_sdf_wnorm     effective weights v * (g / |v|_row) of the 14 weight-normed layers
+//   k_sdf_fold      per-frame folded biases: poses into resd_linears.0/.5, color_latent into lin3
+//   k_sdf_tbtab     per-chunk tbounds after the reference's in-place widening (:203-205)
+//   k_sdf_prep      B2: KNN blend, LBS pose -> T -> big pose (points and directions), gamma_10
+//   k_sdf_mid       B3 tail: 0.05 tanh, tpose, gamma_6 / gamma_4 inputs of the SDF / colour nets
+//   k_sdf_gtop      B4: d sdf / d h7 = softplus'(z7) * W8[0]
+//   k_sdf_gamma_bwd B4: gamma_6 backward -> gradients (the normal fed to the colour net)
+//   k_sdf_raw       B5/B6 tail: Laplace density, alpha with 0.005, sigmoid rgb, tbounds mask, scatter
+//   k_sdf_msk_*     B7: per-ray min sdf, sign-change intersection, ordered msk_sdf / msk_label lists
+// The GEMMs between them run on anr_gemm.hip (anr_sdf_capi.hip drives the sequence).
+#include "anr_common.h"
+#include "anr_sdf.h"
+
+#pragma clang fp contract(off)
+
+namespace anr {
+
+#define SDF_MAX_VERTS 6912
+
+// ------------------------------------------------------------------------------------------
+// B1 front-end. Persistent: one 1024-thread workgroup per CU holds the posed vertices in LDS
+// (float4, 110 KB); wave = ray, lane = sample. Every lane scans all vertices in index order with a
+// strict '<' sorted insertion, which keeps the K lexicographically smallest (d^2, index) pairs —
+// pytorch3d knn_points' bounded max-heap result. d^2 = (dx*dx + dy*dy) + dz*dz, no contraction.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void k_sdf_front(SdfFrontArgs a) {
+  __shared__ float4 sv[SDF_MAX_VERTS];
+  for (int j = threadIdx.x; j < a.nv; j += blockDim.x)
+    sv[j] = make_float4(a.verts[3 * j], a.verts[3 * j + 1], a.verts[3 * j + 2], 0.f);
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int wpb = blockDim.x >> 6;
+  for (int ray = blockIdx.x * wpb + (threadIdx.x >> 6); ray < a.n_rays; ray += gridDim.x * wpb) {
+    float z, dist, pts[3], p[3];
+    sample_point(a.ray_o, a.ray_d, a.near_, a.far_, a.t_rand, ray, lane, 64, z, dist, pts);
+    world_to_pose(pts, a.R, a.Th, p);
+    float b0 = INFINITY, b1 = INFINITY, b2 = INFINITY, b3 = INFINITY, b4 = INFINITY;
+    int i0 = 0, i1 = 0, i2 = 0, i3 = 0, i4 = 0;
+#pragma unroll 4
+    for (int j = 0; j < a.nv; ++j) {
+      const float4 v = sv[j];
+      const float dx = p[0] - v.x, dy = p[1] - v.y, dz = p[2] - v.z;
+      const float d = (dx * dx + dy * dy) + dz * dz;
+      if (d < b4) {
+        if (d < b3) {
+          b4 = b3; i4 = i3;
+          if (d < b2) {
+            b3 = b2; i3 = i2;
+            if (d < b1) {
+              b2 = b1; i2 = i1;
+              if (d < b0) { b1 = b0; i1 = i0; b0 = d; i0 = j; }
+              else { b1 = d; i1 = j; }
+            } else { b2 = d; i2 = j; }
+          } else { b3 = d; i3 = j; }
+        } else { b4 = d; i4 = j; }
+      }
+    }
+    // sample_blend_closest_points: dists = sqrt(d^2); disp = 1 / (dists + 1e-8); torch's 5-element
+    // sum order is ((((x0 + x4) + x1) + x2) + x3); weights = disp / sum; pnorm = sequential sum d*w
+    const float d0 = sqrtf(b0), d1 = sqrtf(b1), d2 = sqrtf(b2), d3 = sqrtf(b3), d4 = sqrtf(b4);
+    const float q0 = 1.0f / (d0 + 1e-8f), q1 = 1.0f / (d1 + 1e-8f), q2 = 1.0f / (d2 + 1e-8f);
+    const float q3 = 1.0f / (d3 + 1e-8f), q4 = 1.0f / (d4 + 1e-8f);
+    const float S = (((q0 + q4) + q1) + q2) + q3;
+    const float w0 = q0 / S, w1 = q1 / S, w2 = q2 / S, w3 = q3 / S, w4 = q4 / S;
+    const float pn = (((d0 * w0 + d1 * w1) + d2 * w2) + d3 * w3) + d4 * w4;
+    const size_t pid = (size_t)ray * 64 + lane;
+    uint4* rec = (uint4*)(a.knn + pid * 8);
+    rec[0] = make_uint4(__float_as_uint(w0), __float_as_uint(w1), __float_as_uint(w2), __float_as_uint(w3));
+    rec[1] = make_uint4(__float_as_uint(w4), (uint32_t)i0 | ((uint32_t)i1 << 16), (uint32_t)i2 | ((uint32_t)i3 << 16),
+                        (uint32_t)i4);
+    const bool keep = pn < a.norm_th;
+    const uint64_t m = __ballot(keep);
+    if (lane == 0) a.mask[ray] = m;
+    if (!keep) {
+      a.raw[pid] = make_float4(0.f, 0.f, 0.f, 0.f);
+      a.sdf[pid] = 10.f;
+    }
+    const int rc = ray % a.chunk;
+    uint64_t key = ((uint64_t)__float_as_uint(pn) << 32) | (uint32_t)(rc * 64 + lane);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const uint64_t o = __shfl_xor(key, off);
+      key = o < key ? o : key;
+    }
+    if (lane == 0) atomicMin((unsigned long long*)&a.chunk_min[ray / a.chunk], (unsigned long long)key);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// weight norm (nn.utils.weight_norm, dim 0): one block per output row of the 14 layers
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_sdf_wnorm(SdfTensors T, float* wimg) {
+  const float* const* t = T.t;
+  int row = blockIdx.x, L = 0;
+  while (L < SDF_NUM_WN - 1 && row >= wn_layer(L).out) { row -= wn_layer(L).out; ++L; }
+  const WnLayer d = wn_layer(L);
+  const float* v = t[d.v] + (size_t)row * d.in;
+  float s = 0.f;
+  for (int k = threadIdx.x; k < d.in; k += 256) s += v[k] * v[k];
+  __shared__ float sh[256];
+  sh[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) sh[threadIdx.x] += sh[threadIdx.x + w];
+    __syncthreads();
+  }
+  const float scale = t[d.g][row] / sqrtf(sh[0]);
+  float* o = wimg + d.off + (size_t)row * d.in;
+  for (int k = threadIdx.x; k < d.in; k += 256) o[k] = v[k] * scale;
+}
+
+// fold[0:256] = resd_linears.0 bias + W0[:, 63:135] poses; fold[256:512] = same for .5;
+// fold[512:768] = colour lin3 bias + W3[:, 256:384] color_latent[latent_index]
+__global__ __launch_bounds__(256) void k_sdf_fold(SdfTensors T, const float* wimg, const float* poses,
+                                                  const int64_t* li, float* fold) {
+  const float* const* t = T.t;
+  const int which = blockIdx.x, n = threadIdx.x;
+  float acc;
+  if (which < 2) {
+    const int l = which == 0 ? 0 : 5;
+    const int in_ch = which == 0 ? 135 : 391;
+    const float* W = t[SDF_RLIN0 + 2 * l] + (size_t)n * in_ch;
+    acc = t[SDF_RLIN0 + 2 * l + 1][n];
+    for (int q = 0; q < 72; ++q) acc = fmaf(W[63 + q], poses[q], acc);
+  } else {
+    const WnLayer d = wn_layer(12);
+    const float* W = wimg + d.off + (size_t)n * 384;
+    const float* lat = t[SDF_COLOR_LAT] + (size_t)li[0] * 128;
+    acc = t[d.v - 2][n];
+    for (int q = 0; q < 128; ++q) acc = fmaf(W[256 + q], lat[q], acc);
+  }
+  fold[which * 256 + n] = acc;
+}
+
+// tbounds[0] -= 0.05; tbounds[1] += 0.05 once per chunk, in place on the batch (fp32)
+__global__ void k_sdf_tbtab(const float* tbounds, int nchunks, float* tbtab, float* tb_out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  float b[6];
+  for (int k = 0; k < 6; ++k) b[k] = tbounds[k];
+  for (int c = 0; c < nchunks; ++c) {
+    for (int k = 0; k < 3; ++k) { b[k] = b[k] - 0.05f; b[3 + k] = b[3 + k] + 0.05f; }
+    for (int k = 0; k < 6; ++k) tbtab[c * 6 + k] = b[k];
+  }
+  if (tb_out)
+    for (int k = 0; k < 6; ++k) tb_out[k] = b[k];
+}
+
+// ------------------------------------------------------------------------------------------
+// B2: thread per kept sample
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ void blend16(const float bw[24], const float* __restrict__ A, float Ab[16]) {
+#pragma clang fp contract(fast)
+  for (int m = 0; m < 16; ++m) Ab[m] = 0.f;
+  for (int j = 0; j < 24; ++j)
+    for (int m = 0; m < 16; ++m) Ab[m] += bw[j] * A[j * 16 + m];
+}
+
+__device__ __forceinline__ void inv33(const float Ab[16], float Ri[9]) {
+  const float a = Ab[0], b = Ab[1], c = Ab[2], d = Ab[4], e = Ab[5], f = Ab[6], g = Ab[8], h = Ab[9], k = Ab[10];
+  const float c00 = e * k - f * h, c01 = c * h - b * k, c02 = b * f - c * e;
+  const float c10 = f * g - d * k, c11 = a * k - c * g, c12 = c * d - a * f;
+  const float c20 = d * h - e * g, c21 = b * g - a * h, c22 = a * e - b * d;
+  const float rd = 1.0f / (a * c00 + b * c10 + c * c20);
+  Ri[0] = c00 * rd; Ri[1] = c01 * rd; Ri[2] = c02 * rd;
+  Ri[3] = c10 * rd; Ri[4] = c11 * rd; Ri[5] = c12 * rd;
+  Ri[6] = c20 * rd; Ri[7] = c21 * rd; Ri[8] = c22 * rd;
+}
+
+__global__ __launch_bounds__(256) void k_sdf_prep(SdfPointArgs a) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.cnt) return;
+  const int pid = a.list[a.b0 + i];
+  const int ray = pid >> 6, s = pid & 63;
+  float z, dist, pts[3], p[3], pd[3];
+  sample_point(a.ray_o, a.ray_d, a.near_, a.far_, a.t_rand, ray, s, 64, z, dist, pts);
+  world_to_pose(pts, a.R, a.Th, p);
+  // world_dirs_to_pose_dirs: d @ R
+  {
+    const float* d = a.ray_d + 3 * ray;
+    for (int j = 0; j < 3; ++j) pd[j] = (d[0] * a.R[j] + d[1] * a.R[3 + j]) + d[2] * a.R[6 + j];
+  }
+  const uint4* rec = (const uint4*)(a.knn + (size_t)pid * 8);
+  const uint4 r0 = rec[0], r1 = rec[1];
+  const float w[5] = {__uint_as_float(r0.x), __uint_as_float(r0.y), __uint_as_float(r0.z), __uint_as_float(r0.w),
+                      __uint_as_float(r1.x)};
+  const int idx[5] = {(int)(r1.y & 0xffff), (int)(r1.y >> 16), (int)(r1.z & 0xffff), (int)(r1.z >> 16), (int)r1.w};
+  float bw[24];
+  for (int l = 0; l < 24; ++l) {
+    float acc = a.weights[idx[0] * 24 + l] * w[0];
+    for (int k = 1; k < 5; ++k) acc = acc + a.weights[idx[k] * 24 + l] * w[k];
+    bw[l] = acc;
+  }
+  float Ab[16], Bb[16], Ri[9];
+  blend16(bw, a.A, Ab);
+  blend16(bw, a.bigA, Bb);
+  inv33(Ab, Ri);
+  const float y[3] = {p[0] - Ab[3], p[1] - Ab[7], p[2] - Ab[11]};
+  float tp[3], td[3], bp[3], bd[3];
+  for (int r = 0; r < 3; ++r) {
+    tp[r] = (Ri[3 * r] * y[0] + Ri[3 * r + 1] * y[1]) + Ri[3 * r + 2] * y[2];
+    td[r] = (Ri[3 * r] * pd[0] + Ri[3 * r + 1] * pd[1]) + Ri[3 * r + 2] * pd[2];
+  }
+  for (int r = 0; r < 3; ++r) {
+    bp[r] = ((Bb[4 * r] * tp[0] + Bb[4 * r + 1] * tp[1]) + Bb[4 * r + 2] * tp[2]) + Bb[4 * r + 3];
+    bd[r] = (Bb[4 * r] * td[0] + Bb[4 * r + 1] * td[1]) + Bb[4 * r + 2] * td[2];
+  }
+  float* pt = a.ptb + (size_t)i * 8;
+  pt[0] = bp[0]; pt[1] = bp[1]; pt[2] = bp[2];
+  pt[3] = bd[0]; pt[4] = bd[1]; pt[5] = bd[2];
+  float* g = a.Gr + (size_t)i * 64;
+  for (int q = 0; q < 64; ++q) g[q] = q < 63 ? embed_feature(bp, q, 10) : 0.f;
+}
+
+// resd = 0.05 tanh(y); tpose = bigpose + resd; gamma_6(tpose) -> Xs0 and X4[:, 217:] / sqrt(2);
+// colour input [tpose, gamma_4(bigdir), gradient (k_sdf_gamma_bwd)]
+__global__ __launch_bounds__(256) void k_sdf_mid(SdfPointArgs a) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.cnt) return;
+  const float* pt = a.ptb + (size_t)i * 8;
+  const float* y = a.Yr + (size_t)i * 4;
+  float tp[3];
+  for (int r = 0; r < 3; ++r) {
+    const float rs = 0.05f * tanhf(y[r]);
+    a.resd_rows[(size_t)(a.b0 + i) * 3 + r] = rs;
+    tp[r] = pt[r] + rs;
+  }
+  const float sqrt2 = 1.41421356237309515f;
+  float* xs = a.Xs0 + (size_t)i * 40;
+  float* x4 = a.X4 + (size_t)i * 256;
+  for (int q = 0; q < 40; ++q) {
+    const float v = q < 39 ? embed_feature(tp, q, 6) : 0.f;
+    xs[q] = v;
+    if (q < 39) x4[217 + q] = v / sqrt2;
+  }
+  const float bd[3] = {pt[3], pt[4], pt[5]};
+  float* c = a.C0 + (size_t)i * 36;
+  c[0] = tp[0]; c[1] = tp[1]; c[2] = tp[2];
+  for (int q = 0; q < 27; ++q) c[3 + q] = embed_feature(bd, q, 4);
+  c[33] = 0.f; c[34] = 0.f; c[35] = 0.f;
+}
+
+// d sdf / d z7 = softplus_backward(W8[0], z7)
+__global__ __launch_bounds__(256) void k_sdf_gtop(SdfPointArgs a) {
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (long)a.cnt * 256) return;
+  const int k = (int)(e & 255);
+  const float g = a.wimg[wn_layer(8).off + k];
+  const float d = a.D7[e];
+  a.G7[e] = d >= 0.f ? g * d / (d + 1.f) : g;
+}
+
+// gamma_6 backward: x.grad = g_x + sum_f f*(g_sin cos(f x)) + f*(g_cos * -sin(f x))
+__global__ __launch_bounds__(256) void k_sdf_gamma_bwd(SdfPointArgs a) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.cnt) return;
+  const float* gA = a.Gc + (size_t)i * 256 + 217;
+  const float* gB = a.gB + (size_t)i * 40;
+  const float* c = a.C0 + (size_t)i * 36;
+  const float tp[3] = {c[0], c[1], c[2]};
+  float gr[3];
+  for (int r = 0; r < 3; ++r) gr[r] = gA[r] + gB[r];
+  for (int f = 0; f < 6; ++f) {
+    const float fr = (float)(1 << f);
+    for (int r = 0; r < 3; ++r) {
+      const float v = tp[r] * fr;
+      const float gs = gA[3 + 6 * f + r] + gB[3 + 6 * f + r];
+      const float gc = gA[6 + 6 * f + r] + gB[6 + 6 * f + r];
+      gr[r] = gr[r] + (gs * cosf(v)) * fr;
+      gr[r] = gr[r] + (gc * -sinf(v)) * fr;
+    }
+  }
+  float* cc = a.C0 + (size_t)i * 36;
+  for (int r = 0; r < 3; ++r) {
+    cc[30 + r] = gr[r];
+    a.grad_rows[(size_t)(a.b0 + i) * 3 + r] = gr[r];
+  }
+}
+
+// sdf_to_alpha (Laplace CDF, beta clamped) -> 1 - exp(-relu(s) * 0.005); rgb = sigmoid; tbounds mask
+__global__ __launch_bounds__(256) void k_sdf_raw(SdfPointArgs a) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.cnt) return;
+  const int pid = a.list[a.b0 + i];
+  const int ray = pid >> 6;
+  const float sdf = a.Y8[(size_t)i * 264];
+  const float beta = fminf(fmaxf(a.beta, 1e-9f), 1e6f);
+  const float x = -sdf;
+  const float ib = 1.0f / beta;
+  const float sig = x <= 0.f ? ib * (0.5f * expf(x / beta)) : ib * (1.0f - 0.5f * expf(-x / beta));
+  const float alpha = 1.0f - expf(-fmaxf(sig, 0.f) * 0.005f);
+  const float* yc = a.Yc + (size_t)i * 4;
+  float4 raw = make_float4(1.0f / (1.0f + expf(-yc[0])), 1.0f / (1.0f + expf(-yc[1])), 1.0f / (1.0f + expf(-yc[2])),
+                           alpha);
+  const float* tb = a.tbtab + (size_t)(ray / a.chunk) * 6;
+  const float* c = a.C0 + (size_t)i * 36;
+  bool inside = true;
+  for (int r = 0; r < 3; ++r) inside = inside && c[r] > tb[r] && c[r] < tb[3 + r];
+  if (!inside) raw = make_float4(0.f, 0.f, 0.f, 0.f);
+  a.raw[pid] = raw;
+  a.sdf[pid] = sdf;
+}
+
+// ------------------------------------------------------------------------------------------
+// B7 msk_sdf (tpose_renderer.py:134-152): wave per ray for min / sign change, then per-chunk lists
+// [min_sdf where no intersection and occ == 1] ++ [min_sdf where occ == 0], chunks concatenated
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_sdf_msk_rays(SdfMskArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int ray = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (ray >= a.n_rays) return;
+  const float s = a.sdf[(size_t)ray * 64 + lane];
+  const float nx = __shfl_down(s, 1);
+  float mn = s;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) mn = fminf(mn, __shfl_xor(mn, off));
+  const float prod = s * nx;
+  const bool neg = lane < 63 && prod < 0.f;  // sign(...).min() == -1
+  const bool inter = __ballot(neg) != 0ull;
+  if (lane == 0) {
+    const uint8_t o = a.occ[ray];
+    a.min_sdf[ray] = mn;
+    a.flags[ray] = (uint8_t)(((!inter && o == 1) ? 1 : 0) | (o == 0 ? 2 : 0));
+  }
+}
+
+__device__ __forceinline__ int block_scan_1024(int v, int* sh, int& total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int x = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int y = __shfl_up(x, off);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) sh[w] = x;
+  __syncthreads();
+  int base = 0;
+  total = 0;
+  for (int k = 0; k < 16; ++k) {
+    if (k < w) base += sh[k];
+    total += sh[k];
+  }
+  __syncthreads();
+  return base + x - v;
+}
+
+// block per chunk (1024 threads, 2 rays each): list lengths
+__global__ __launch_bounds__(1024) void k_sdf_msk_count(SdfMskArgs a) {
+  __shared__ int sh[16];
+  const int r0 = blockIdx.x * a.chunk;
+  const int r1 = min(a.n_rays, r0 + a.chunk);
+  int cnt = 0;
+  for (int r = r0 + threadIdx.x; r < r1; r += 1024) {
+    const uint8_t f = a.flags[r];
+    cnt += (f & 1) + ((f >> 1) & 1);
+  }
+  int total;
+  block_scan_1024(cnt, sh, total);
+  if (threadIdx.x == 0) a.chunk_cnt[blockIdx.x] = total;
+}
+
+// chunk_cnt now holds exclusive chunk offsets; write the two ordered lists of each chunk
+__global__ __launch_bounds__(1024) void k_sdf_msk_write(SdfMskArgs a) {
+  __shared__ int sh[16];
+  const int r0 = blockIdx.x * a.chunk;
+  const int r1 = min(a.n_rays, r0 + a.chunk);
+  const int base = a.chunk_cnt[blockIdx.x];
+  int n_ind_total = 0;
+  // pass 1: the "ind" list (rays in order), pass 2: the "free" list
+  for (int pass = 0; pass < 2; ++pass) {
+    int carry = 0;
+    for (int r = r0; r < r1; r += 1024) {
+      const int rr = r + threadIdx.x;
+      const int f = rr < r1 ? ((a.flags[rr] >> pass) & 1) : 0;
+      int tot;
+      const int ex = block_scan_1024(f, sh, tot);
+      if (f) {
+        const int pos = base + (pass ? n_ind_total : 0) + carry + ex;
+        a.msk_sdf[pos] = a.min_sdf[rr];
+        a.msk_label[pos] = pass ? 0.f : 1.f;
+      }
+      carry += tot;
+    }
+    if (pass == 0) n_ind_total = carry;
+  }
+}
+
+}  // namespace anr

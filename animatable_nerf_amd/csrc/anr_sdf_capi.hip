@@ -1,0 +1,310 @@
+// anr_sdf_capi.hip — C-ABI of the sdf_pdf render path (include/aninerf.h, "sdf_pdf variant").
+//
+// Sequence per render call (anisdf_pdf_network.py:156-223 under tpose_renderer.py:159-186):
+//   k_sdf_front (KNN keep mask, all samples) -> ordered compaction -> one host read of n'
+//   -> per batch of <= SDF_BATCH kept samples: prep, 9 residual-MLP GEMMs, mid, 9 SDF GEMMs
+//      (softplus + its backward factor in the epilogue), 8 input-gradient GEMMs (reverse mode
+//      through the stored factors), gamma backward, 5 colour GEMMs, raw
+//   -> compositing (k_composite) -> msk_sdf lists.
+// Layer-wise GEMMs (anr_gemm.hip, exact fp32 MFMA) keep each activation in HBM: the input gradient
+// needs every softplus factor of the forward, which does not fit a fused register pipeline.
+#include <algorithm>
+#include <cmath>
+
+#include "../../include/aninerf.h"
+#include "anr_common.h"
+#include "anr_kernels.h"
+#include "anr_sdf.h"
+#include "anr_train.h"
+#include "anr_ws.h"
+
+using namespace anr;
+
+namespace {
+
+constexpr long SDF_BATCH = 1L << 19;
+
+struct SLayout {
+  size_t counts, mask, chunk_min, ray_off, block_sum, list, knn, tbtab, wimg, fold, resd_rows, grad_rows;
+  size_t min_sdf, flags, chunk_cnt, msk_sdf, msk_label;
+  size_t ptb, Gr, Ha, Hb, Yr, Xs0, X4, D, Y8, Ga, Gb, Gc, gB, C0, Yc;
+  long P;
+  size_t total;
+};
+
+SLayout slayout(int n_rays, int chunk) {
+  SLayout L{};
+  const size_t R = (size_t)n_rays, N = R * 64;
+  const size_t nch = (R + chunk - 1) / (size_t)std::max(chunk, 1);
+  size_t o = 0;
+  auto take = [&](size_t bytes) {
+    const size_t at = o;
+    o = align256(o + bytes);
+    return at;
+  };
+  L.counts = take(16);
+  L.mask = take(R * 8);
+  L.chunk_min = take(nch * 8);
+  L.ray_off = take((R + 1) * 4);
+  L.block_sum = take(((R + 255) / 256) * 4);
+  L.list = take(N * 4);
+  L.knn = take(N * 32);
+  L.tbtab = take(nch * 6 * 4);
+  L.wimg = take(SDF_WN_FLOATS * 4);
+  L.fold = take(768 * 4);
+  L.resd_rows = take(N * 3 * 4);
+  L.grad_rows = take(N * 3 * 4);
+  L.min_sdf = take(R * 4);
+  L.flags = take(R);
+  L.chunk_cnt = take(nch * 4);
+  L.msk_sdf = take(R * 4);
+  L.msk_label = take(R * 4);
+  const long P = (long)std::min<size_t>(N, SDF_BATCH);
+  L.P = P;
+  auto f = [&](long w) { return take((size_t)P * w * 4); };
+  L.ptb = f(8); L.Gr = f(64); L.Ha = f(256); L.Hb = f(256); L.Yr = f(4); L.Xs0 = f(40); L.X4 = f(256);
+  L.D = f(8 * 256); L.Y8 = f(264); L.Ga = f(256); L.Gb = f(256); L.Gc = f(256); L.gB = f(40); L.C0 = f(36);
+  L.Yc = f(4);
+  L.total = o;
+  return L;
+}
+
+int sdf_cus() {
+  int dev = 0, v = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 256;
+  if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) return 256;
+  return v;
+}
+
+struct G {
+  hipStream_t s;
+  int M;
+  int run(GemmArgs g) {
+    if (M <= 0 || g.N <= 0) return ANR_OK;
+    g.M = M;
+    g.ksplit = 1;
+    launch_gemm(g, dim3((g.N + 63) / 64, (M + 63) / 64, 1), s);
+    return check_launch("k_gemm (sdf)");
+  }
+  // Y = epi([X0 | X1] [W[:, c0:c0+K0] | W[:, c1:c1+K1]]^T + bias)
+  int fwd(float* Y, long ldY, int N, const float* W, int in_ch, const float* bias, const float* X0, long ld0, int K0,
+          int c0, bool relu, float* deriv = nullptr, float div_post = 0.f, const float* X1 = nullptr, long ld1 = 0,
+          int K1 = 0, int c1 = 0) {
+    GemmArgs g{};
+    g.N = N;
+    g.nseg = X1 ? 2 : 1;
+    g.seg[0] = GemmSeg{X0, ld0, 1, W + c0, 1, in_ch, K0};
+    if (X1) g.seg[1] = GemmSeg{X1, ld1, 1, W + c1, 1, in_ch, K1};
+    g.C = Y; g.ldc = ldY; g.bias = bias; g.relu = relu ? 1 : 0;
+    if (deriv) { g.softplus = 1; g.deriv = deriv; g.ldd = 256; }
+    g.div_post = div_post;
+    return run(g);
+  }
+  // dX[:, :K] = softplus_bwd((dY W[:, :K]) / div_pre, spd) (pass-through at n >= spd_n)
+  int bwd(float* dX, long ldX, int K, const float* dY, long ldY, int Nout, const float* W, int in_ch, const float* spd,
+          int spd_n, float div_pre = 0.f) {
+    GemmArgs g{};
+    g.N = K;
+    g.nseg = 1;
+    g.seg[0] = GemmSeg{dY, ldY, 1, W, in_ch, 1, Nout};
+    g.C = dX; g.ldc = ldX;
+    g.spd = spd; g.ldsd = 256; g.spd_n = spd_n;
+    g.div_pre = div_pre;
+    return run(g);
+  }
+};
+
+int check(const anr_sdf_params* p, const anr_sdf_frame* f, const float* ray_o, const float* ray_d, const float* near_,
+          const float* far_, int R, const anr_render_opts* o, const anr_sdf_render_out* out, void* ws) {
+  if (!p || !f || !o || !out || !ws || !ray_o || !ray_d || !near_ || !far_)
+    return fail(ANR_E_ARG, "sdf render: NULL argument");
+  if (o->n_samples != 64) return fail(ANR_E_ARG, "sdf render: only N_samples == 64 is supported");
+  if (o->chunk <= 0 || R <= 0) return fail(ANR_E_ARG, "sdf render: bad chunk / n_rays");
+  if (o->novel_pose) return fail(ANR_E_ARG, "sdf render: novel_pose is an aninerf option");
+  for (int i = 0; i < ANR_SDF_NUM_TENSORS; ++i)
+    if (!p->t[i] && i != SDF_RESD_LAT) return fail(ANR_E_ARG, "sdf render: NULL parameter tensor");
+  if (!f->A || !f->big_A || !f->R || !f->Th || !f->poses || !f->pvertices || !f->weights || !f->tbounds ||
+      !f->latent_index || !f->occupancy)
+    return fail(ANR_E_ARG, "sdf render: NULL frame tensor");
+  if (f->n_verts <= 0 || f->n_verts > 6912) return fail(ANR_E_ARG, "sdf render: n_verts must be in [1, 6912]");
+  if (!out->rgb_map || !out->acc_map || !out->depth_map || !out->raw || !out->sdf)
+    return fail(ANR_E_ARG, "sdf render: NULL output");
+  return ANR_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t anr_sdf_render_workspace_bytes(int n_rays, const anr_render_opts* o) {
+  if (n_rays <= 0 || !o || o->chunk <= 0) return 0;
+  return slayout(n_rays, o->chunk).total;
+}
+
+const int32_t* anr_sdf_render_counts(const void* workspace, int n_rays, const anr_render_opts* o) {
+  if (!workspace || !o || o->chunk <= 0) return nullptr;
+  return (const int32_t*)((const char*)workspace + slayout(n_rays, o->chunk).counts);
+}
+
+int anr_sdf_render_rows(const void* workspace, int n_rays, const anr_render_opts* o, float* resd, float* gradients,
+                        float* msk_sdf, float* msk_label, void* stream) {
+  if (!workspace || !o || o->chunk <= 0) return fail(ANR_E_ARG, "anr_sdf_render_rows: bad arguments");
+  const SLayout L = slayout(n_rays, o->chunk);
+  const char* ws = (const char*)workspace;
+  int cnt[2];
+  hipStream_t s = (hipStream_t)stream;
+  if (hipMemcpyAsync(cnt, ws + L.counts, 8, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+    return fail(ANR_E_HIP, "anr_sdf_render_rows: count readback");
+  auto cp = [&](void* dst, size_t off, size_t bytes) {
+    if (!dst || bytes == 0) return hipSuccess;
+    return hipMemcpyAsync(dst, ws + off, bytes, hipMemcpyDeviceToDevice, s);
+  };
+  if (cp(resd, L.resd_rows, (size_t)cnt[0] * 12) != hipSuccess || cp(gradients, L.grad_rows, (size_t)cnt[0] * 12) != hipSuccess ||
+      cp(msk_sdf, L.msk_sdf, (size_t)cnt[1] * 4) != hipSuccess || cp(msk_label, L.msk_label, (size_t)cnt[1] * 4) != hipSuccess)
+    return fail(ANR_E_HIP, "anr_sdf_render_rows: copy");
+  return ANR_OK;
+}
+
+int anr_sdf_render_fwd(const anr_sdf_params* p, const anr_sdf_frame* f, const float* ray_o, const float* ray_d,
+                       const float* near_, const float* far_, int R, const anr_render_opts* o,
+                       const anr_sdf_render_out* out, void* workspace, size_t ws_bytes, void* stream) {
+  ANR_TRY(check(p, f, ray_o, ray_d, near_, far_, R, o, out, workspace));
+  const SLayout L = slayout(R, o->chunk);
+  if (ws_bytes < L.total) return fail(ANR_E_WORKSPACE, "sdf render: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  char* ws = (char*)workspace;
+  const int nch = (R + o->chunk - 1) / o->chunk;
+  int* counts = (int*)(ws + L.counts);
+  float4* raw = (float4*)out->raw;
+
+  if (hipMemsetAsync(ws + L.counts, 0, 16, s) != hipSuccess ||
+      hipMemsetAsync(ws + L.chunk_min, 0xff, (size_t)nch * 8, s) != hipSuccess)
+    return fail(ANR_E_HIP, "sdf render: memset");
+
+  // per-call weight preparation (weight norm, folds, per-chunk tbounds)
+  const float* const* tp = p->t;
+  float* wimg = (float*)(ws + L.wimg);
+  float* fold = (float*)(ws + L.fold);
+  float* tbtab = (float*)(ws + L.tbtab);
+  SdfTensors T{};
+  for (int i = 0; i < ANR_SDF_NUM_TENSORS; ++i) T.t[i] = tp[i];
+  hipLaunchKernelGGL(k_sdf_wnorm, dim3(sdf_wn_rows()), dim3(256), 0, s, T, wimg);
+  ANR_TRY(check_launch("k_sdf_wnorm"));
+  hipLaunchKernelGGL(k_sdf_fold, dim3(3), dim3(256), 0, s, T, (const float*)wimg, f->poses, f->latent_index, fold);
+  ANR_TRY(check_launch("k_sdf_fold"));
+  hipLaunchKernelGGL(k_sdf_tbtab, dim3(1), dim3(64), 0, s, f->tbounds, nch, tbtab, out->tbounds_out);
+  ANR_TRY(check_launch("k_sdf_tbtab"));
+
+  // B1 front-end + ordered compaction
+  SdfFrontArgs fa{};
+  fa.ray_o = ray_o; fa.ray_d = ray_d; fa.near_ = near_; fa.far_ = far_; fa.t_rand = o->t_rand;
+  fa.n_rays = R; fa.chunk = o->chunk; fa.R = f->R; fa.Th = f->Th; fa.verts = f->pvertices; fa.nv = f->n_verts;
+  fa.norm_th = o->norm_th; fa.mask = (uint64_t*)(ws + L.mask); fa.chunk_min = (uint64_t*)(ws + L.chunk_min);
+  fa.knn = (uint32_t*)(ws + L.knn); fa.raw = raw; fa.sdf = out->sdf;
+  const int grid_front = std::min(sdf_cus(), (R + 15) / 16);
+  hipLaunchKernelGGL(k_sdf_front, dim3(grid_front), dim3(1024), 0, s, fa);
+  ANR_TRY(check_launch("k_sdf_front"));
+  CompactArgs ca{};
+  ca.n_rays = R; ca.chunk = o->chunk; ca.mask = fa.mask; ca.chunk_min = fa.chunk_min;
+  ca.ray_off = (int*)(ws + L.ray_off); ca.block_sum = (int*)(ws + L.block_sum); ca.list = (int*)(ws + L.list);
+  const int nb = (R + 255) / 256;
+  hipLaunchKernelGGL(k_count, dim3(nb), dim3(256), 0, s, ca);
+  hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, s, ca.block_sum, nb, counts);
+  hipLaunchKernelGGL(k_compact, dim3((R + 3) / 4), dim3(256), 0, s, ca);
+  ANR_TRY(check_launch("k_compact (sdf)"));
+  int n = 0;
+  if (hipMemcpyAsync(&n, counts, 4, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+    return fail(ANR_E_HIP, "sdf render: kept-count readback");
+
+  // per batch of kept samples
+  float beta = 0.f;
+  if (hipMemcpyAsync(&beta, tp[SDF_BETA], 4, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+    return fail(ANR_E_HIP, "sdf render: beta readback");
+  auto F = [&](size_t off) { return (float*)(ws + off); };
+  float *Ha = F(L.Ha), *Hb = F(L.Hb), *Ga = F(L.Ga), *Gb = F(L.Gb), *Gc = F(L.Gc), *D = F(L.D);
+  const long P = L.P;
+  auto Dl = [&](int l) { return D + (size_t)l * P * 256; };
+  auto WN = [&](int l) { return (const float*)wimg + wn_layer(l).off; };
+  const float sqrt2 = 1.41421356237309515f;
+  for (long b0 = 0; b0 < n; b0 += P) {
+    const int cnt = (int)std::min<long>(P, n - b0);
+    SdfPointArgs a{};
+    a.list = ca.list; a.b0 = (int)b0; a.cnt = cnt;
+    a.ray_o = ray_o; a.ray_d = ray_d; a.near_ = near_; a.far_ = far_; a.t_rand = o->t_rand; a.chunk = o->chunk;
+    a.R = f->R; a.Th = f->Th; a.A = f->A; a.bigA = f->big_A; a.weights = f->weights; a.knn = fa.knn;
+    a.wimg = wimg; a.tbtab = tbtab;
+    a.ptb = F(L.ptb); a.Gr = F(L.Gr); a.Yr = F(L.Yr); a.Xs0 = F(L.Xs0); a.X4 = F(L.X4); a.C0 = F(L.C0);
+    a.D7 = Dl(7); a.G7 = Ga; a.Gc = Gc; a.gB = F(L.gB); a.Y8 = F(L.Y8); a.Yc = F(L.Yc); a.beta = beta;
+    a.resd_rows = F(L.resd_rows); a.grad_rows = F(L.grad_rows); a.raw = raw; a.sdf = out->sdf;
+    const dim3 pg((cnt + 255) / 256), pb(256);
+    G g{s, cnt};
+
+    // B2 + B3: LBS to the big pose, residual deformation MLP (poses folded into layers 0 / 5)
+    hipLaunchKernelGGL(k_sdf_prep, pg, pb, 0, s, a);
+    ANR_TRY(check_launch("k_sdf_prep"));
+    const float* Wr[8];
+    for (int l = 0; l < 8; ++l) Wr[l] = tp[SDF_RLIN0 + 2 * l];
+    ANR_TRY(g.fwd(Ha, 256, 256, Wr[0], 135, fold, a.Gr, 64, 63, 0, true));
+    ANR_TRY(g.fwd(Hb, 256, 256, Wr[1], 256, tp[SDF_RLIN0 + 3], Ha, 256, 256, 0, true));
+    ANR_TRY(g.fwd(Ha, 256, 256, Wr[2], 256, tp[SDF_RLIN0 + 5], Hb, 256, 256, 0, true));
+    ANR_TRY(g.fwd(Hb, 256, 256, Wr[3], 256, tp[SDF_RLIN0 + 7], Ha, 256, 256, 0, true));
+    ANR_TRY(g.fwd(Ha, 256, 256, Wr[4], 256, tp[SDF_RLIN0 + 9], Hb, 256, 256, 0, true));
+    ANR_TRY(g.fwd(Hb, 256, 256, Wr[5], 391, fold + 256, a.Gr, 64, 63, 0, true, nullptr, 0.f, Ha, 256, 256, 135));
+    ANR_TRY(g.fwd(Ha, 256, 256, Wr[6], 256, tp[SDF_RLIN0 + 13], Hb, 256, 256, 0, true));
+    ANR_TRY(g.fwd(Hb, 256, 256, Wr[7], 256, tp[SDF_RLIN0 + 15], Ha, 256, 256, 0, true));
+    ANR_TRY(g.fwd(F(L.Yr), 4, 3, tp[SDF_RFC_W], 256, tp[SDF_RFC_B], Hb, 256, 256, 0, false));
+    hipLaunchKernelGGL(k_sdf_mid, pg, pb, 0, s, a);
+    ANR_TRY(check_launch("k_sdf_mid"));
+
+    // B4 SDF network forward (softplus factors kept for the input gradient)
+    ANR_TRY(g.fwd(Ha, 256, 256, WN(0), 39, tp[0], a.Xs0, 40, 39, 0, false, Dl(0)));
+    ANR_TRY(g.fwd(Hb, 256, 256, WN(1), 256, tp[3], Ha, 256, 256, 0, false, Dl(1)));
+    ANR_TRY(g.fwd(Ha, 256, 256, WN(2), 256, tp[6], Hb, 256, 256, 0, false, Dl(2)));
+    ANR_TRY(g.fwd(a.X4, 256, 217, WN(3), 256, tp[9], Ha, 256, 256, 0, false, Dl(3), sqrt2));
+    ANR_TRY(g.fwd(Ha, 256, 256, WN(4), 256, tp[12], a.X4, 256, 256, 0, false, Dl(4)));
+    ANR_TRY(g.fwd(Hb, 256, 256, WN(5), 256, tp[15], Ha, 256, 256, 0, false, Dl(5)));
+    ANR_TRY(g.fwd(Ha, 256, 256, WN(6), 256, tp[18], Hb, 256, 256, 0, false, Dl(6)));
+    ANR_TRY(g.fwd(Hb, 256, 256, WN(7), 256, tp[21], Ha, 256, 256, 0, false, Dl(7)));
+    ANR_TRY(g.fwd(F(L.Y8), 264, 257, WN(8), 256, tp[24], Hb, 256, 256, 0, false));
+
+    // B4 gradient of sdf w.r.t. the canonical point (reverse mode through the stored factors)
+    hipLaunchKernelGGL(k_sdf_gtop, dim3((unsigned)(((long)cnt * 256 + 255) / 256)), pb, 0, s, a);
+    ANR_TRY(check_launch("k_sdf_gtop"));
+    ANR_TRY(g.bwd(Gb, 256, 256, Ga, 256, 256, WN(7), 256, Dl(6), 256));
+    ANR_TRY(g.bwd(Ga, 256, 256, Gb, 256, 256, WN(6), 256, Dl(5), 256));
+    ANR_TRY(g.bwd(Gb, 256, 256, Ga, 256, 256, WN(5), 256, Dl(4), 256));
+    ANR_TRY(g.bwd(Gc, 256, 256, Gb, 256, 256, WN(4), 256, Dl(3), 217, sqrt2));
+    ANR_TRY(g.bwd(Ga, 256, 256, Gc, 256, 217, WN(3), 256, Dl(2), 256));
+    ANR_TRY(g.bwd(Gb, 256, 256, Ga, 256, 256, WN(2), 256, Dl(1), 256));
+    ANR_TRY(g.bwd(Ga, 256, 256, Gb, 256, 256, WN(1), 256, Dl(0), 256));
+    ANR_TRY(g.bwd(F(L.gB), 40, 39, Ga, 256, 256, WN(0), 39, nullptr, 0));
+    hipLaunchKernelGGL(k_sdf_gamma_bwd, pg, pb, 0, s, a);
+    ANR_TRY(check_launch("k_sdf_gamma_bwd"));
+
+    // B6 colour network (color_latent folded into lin3)
+    ANR_TRY(g.fwd(Ha, 256, 256, WN(9), 289, tp[29], a.C0, 36, 33, 0, true, nullptr, 0.f, F(L.Y8) + 1, 264, 256, 33));
+    ANR_TRY(g.fwd(Hb, 256, 256, WN(10), 256, tp[32], Ha, 256, 256, 0, true));
+    ANR_TRY(g.fwd(Ha, 256, 256, WN(11), 256, tp[35], Hb, 256, 256, 0, true));
+    ANR_TRY(g.fwd(Hb, 256, 256, WN(12), 384, fold + 512, Ha, 256, 256, 0, true));
+    ANR_TRY(g.fwd(F(L.Yc), 4, 3, WN(13), 256, tp[41], Hb, 256, 256, 0, false));
+
+    // B5 density, raw assembly with the (widened) tbounds mask
+    hipLaunchKernelGGL(k_sdf_raw, pg, pb, 0, s, a);
+    ANR_TRY(check_launch("k_sdf_raw"));
+  }
+
+  // A12 compositing over the full raw, then B7 msk_sdf / msk_label
+  const anr_render_out ro{out->rgb_map, out->acc_map, out->depth_map, out->raw};
+  ANR_TRY(stage_composite(near_, far_, R, o, raw, &ro, nullptr, s));
+  SdfMskArgs ma{};
+  ma.sdf = out->sdf; ma.occ = f->occupancy; ma.n_rays = R; ma.chunk = o->chunk;
+  ma.min_sdf = F(L.min_sdf); ma.flags = (uint8_t*)(ws + L.flags); ma.chunk_cnt = (int*)(ws + L.chunk_cnt);
+  ma.total = counts + 1; ma.msk_sdf = F(L.msk_sdf); ma.msk_label = F(L.msk_label);
+  hipLaunchKernelGGL(k_sdf_msk_rays, dim3((R + 3) / 4), dim3(256), 0, s, ma);
+  hipLaunchKernelGGL(k_sdf_msk_count, dim3(nch), dim3(1024), 0, s, ma);
+  hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, s, ma.chunk_cnt, nch, ma.total);
+  hipLaunchKernelGGL(k_sdf_msk_write, dim3(nch), dim3(1024), 0, s, ma);
+  return check_launch("k_sdf_msk_write");
+}
+
+}  // extern "C"

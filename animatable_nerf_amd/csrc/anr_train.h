@@ -28,6 +28,15 @@ struct GemmArgs {
   int accumulate;      // C += result (non-atomic)
   int atomic;          // atomicAdd into C (split-K)
   int ksplit;          // number of K splits (grid.z)
+  // sdf_pdf epilogues (anr_sdf*.hip); all off when zero / NULL
+  float div_pre;       // v = v / div_pre before the activation (backward of cat(...)/sqrt(2))
+  int softplus;        // v = Softplus(beta=100)(v); deriv[m][n] = exp(100 v) or -1 above the threshold
+  float* deriv;
+  long ldd;
+  const float* spd;    // softplus backward: v = d < 0 ? v : v * d / (d + 1), d = spd[m][n], n < spd_n
+  long ldsd;
+  int spd_n;
+  float div_post;      // v = v / div_post after the activation (cat(...)/sqrt(2) forward)
 };
 
 void launch_gemm(GemmArgs g, dim3 grid, hipStream_t s);

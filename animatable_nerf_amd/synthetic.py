@@ -192,7 +192,8 @@ class PdfScene(Scene):
             'rgb': rgb[None].astype(np.float32),
             'A': self.A[None], 'big_A': self.big_A[None], 'poses': self.pose_vec[None],
             'weights': self.skin[None], 'tvertices': self.tvertices[None], 'pvertices': self.pvertices[None],
-            'pbounds': self.pbounds[None], 'wbounds': self.pbounds[None], 'tbounds': self.tbounds[None],
+            'pbounds': self.pbounds[None], 'wbounds': self.pbounds[None],
+            'tbounds': self.tbounds[None].copy(),  # the network widens it in place (own copy per batch)
             'R': self.R[None], 'Th': self.Th[None],
             'H': np.array([0]), 'W': np.array([0]),
             'latent_index': np.array([latent_index]), 'bw_latent_index': np.array([latent_index]),

@@ -15,6 +15,12 @@
  *                                raw2outputs nerf_net_utils.py:6-36
  *   anr_render_counts       the host syncs the reference makes at pind/alpha_ind (:153-157, :192-196)
  *   anr_render_bw_rows      tpose_nerf_network.py:195-196 (pbw/tbw rows selected by alpha_ind)
+ *   anr_sdf_render_fwd      the same Renderer.render over the sdf_pdf network (config 5):
+ *                             lib/networks/bw_deform/anisdf_pdf_network.py:156-223 Network.forward,
+ *                             sample_utils.py:309-348 (KNN blend), TPoseHuman :288-338,
+ *                             tpose_renderer.py:134-152 (msk_sdf / msk_label)
+ *   anr_sdf_render_counts / anr_sdf_render_rows   the compact outputs 'resd', 'gradients',
+ *                             'msk_sdf', 'msk_label' (sizes known only after the keep mask)
  *
  * All float tensors are fp32, contiguous, row-major, with the reference's shapes (batch dim 1).
  */
@@ -136,6 +142,59 @@ int anr_train_step(const anr_params* p, float* const* grads, const anr_frame* f,
                    const anr_render_out* out, float* loss3, void* workspace, size_t ws_bytes, void* stream);
 int anr_adam(float* param, float* grad, float* exp_avg, float* exp_avg_sq, long n, float lr, float beta1,
              float beta2, float eps, float weight_decay, int step, float clip_value, void* stream);
+
+/* ---- sdf_pdf variant (config 5, anisdf_pdf_network.py) ------------------------------------
+ * Parameters: the 63 tensors of anisdf_pdf_network.Network's state_dict, in order:
+ *   0..26  tpose_human.sdf_network.lin{0..8}.{bias, weight_g (o,1), weight_v (o,i)}
+ *          i/o: 39/256, 256/256, 256/256, 256/217, 256/256 x4, 256/257
+ *   27     tpose_human.beta_network.beta ()
+ *   28     tpose_human.color_network.color_latent.weight (L,128)
+ *   29..43 tpose_human.color_network.lin{0..4}.{bias, weight_g, weight_v}  i: 289,256,256,384,256
+ *   44     resd_latent.weight (L,128)            (not read by the render)
+ *   45..60 resd_linears.{0..7}.{weight,bias}     Conv1d, in: 135,256,256,256,256,391,256,256
+ *   61,62  resd_fc.{weight,bias} (3,256,1)                                                   */
+#define ANR_SDF_NUM_TENSORS 63
+
+typedef struct anr_sdf_params {
+  const float* t[ANR_SDF_NUM_TENSORS];  /* device pointers, state_dict order above */
+} anr_sdf_params;
+
+typedef struct anr_sdf_frame {
+  const float* A;          /* (24,4,4) device */
+  const float* big_A;      /* (24,4,4) device: big pose (tpose_pdf_dataset.py:91-100) */
+  const float* R;          /* (3,3) */
+  const float* Th;         /* (3) */
+  const float* poses;      /* (72) batch['poses'] */
+  const float* pvertices;  /* (V,3) posed SMPL vertices in the pose frame, V <= 6912 */
+  const float* weights;    /* (V,24) skin weights */
+  int n_verts;
+  const float* tbounds;    /* (2,3) batch['tbounds'] as passed in */
+  const int64_t* latent_index;  /* (1) colour latent row */
+  const uint8_t* occupancy;     /* (R) batch['occupancy'] */
+} anr_sdf_frame;
+
+typedef struct anr_sdf_render_out {
+  float* rgb_map;      /* (R,3) */
+  float* acc_map;      /* (R) */
+  float* depth_map;    /* (R) */
+  float* raw;          /* (R*64,4) */
+  float* sdf;          /* (R*64) (10 at samples the KNN filter drops) */
+  float* tbounds_out;  /* (2,3) or NULL: batch['tbounds'] after the reference's in-place widening
+                          by 0.05 per chunk (anisdf_pdf_network.py:203-205) */
+} anr_sdf_render_out;
+
+/* o->norm_th is the KNN distance threshold (0.1 in the reference, :172). Reads the kept-sample
+ * count once (host sync) to size the layer GEMMs. Eval path: the training-only
+ * 'observed_gradients' (:187-193) are not produced. */
+size_t anr_sdf_render_workspace_bytes(int n_rays, const anr_render_opts* o);
+int anr_sdf_render_fwd(const anr_sdf_params* p, const anr_sdf_frame* f, const float* ray_o, const float* ray_d,
+                       const float* near_, const float* far_, int n_rays, const anr_render_opts* o,
+                       const anr_sdf_render_out* out, void* workspace, size_t ws_bytes, void* stream);
+/* device int32[2] inside the workspace: {kept samples n', msk_sdf length}. */
+const int32_t* anr_sdf_render_counts(const void* workspace, int n_rays, const anr_render_opts* o);
+/* copy resd (n',3), gradients (n',3), msk_sdf / msk_label (len) out of the workspace */
+int anr_sdf_render_rows(const void* workspace, int n_rays, const anr_render_opts* o, float* resd, float* gradients,
+                        float* msk_sdf, float* msk_label, void* stream);
 
 /* ---- measurement ----------------------------------------------------------------------
  * When enabled, anr_render_fwd records a hipEvent pair around the fused network kernel (k_mlp)
