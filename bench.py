@@ -36,8 +36,10 @@ def parse():
     ap.add_argument('--rays', type=int, default=512 * 512)
     ap.add_argument('--cpu-rays', type=int, default=16 * 2048)
     ap.add_argument('--no-cpu', action='store_true')
-    ap.add_argument('--mode', choices=('render', 'train'), default='render',
-                    help='render: config 2 (headline); train: config 3/4 training step (1024 rays/GPU)')
+    ap.add_argument('--mode', choices=('render', 'train', 'sdf'), default='render',
+                    help='render: config 2 (headline); train: config 3/4 training step (1024 rays/GPU); '
+                         'sdf: config 5 sdf_pdf full-frame render')
+    ap.add_argument('--sdf-cpu-rays', type=int, default=2048)
     ap.add_argument('--train-rays', type=int, default=1024)
     return ap.parse_args()
 
@@ -56,6 +58,8 @@ def main():
     from animatable_nerf_amd.renderer import Renderer, near_far
     if args.mode == 'train':
         return bench_train(args, rank, world, dev)
+    if args.mode == 'sdf':
+        return bench_sdf(args, rank, world, dev)
 
     sc = synthetic.Scene(vsize=0.025)
     ro, rd = sc.box_rays(args.rays, seed=2 + rank)
@@ -203,6 +207,92 @@ def bench_train(args, rank, world, dev):
                      'flop_per_kept': FLOP_PER_KEPT_TRAIN},
         'loss_last_step': loss[:3],
     }
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+# sdf_pdf per kept sample, exact from the layer shapes (anisdf_pdf_network.py): residual MLP 528,640 MAC
+# + SDF forward 524,544 + its input gradient 459,008 (lin8 row 0, lin7..lin1, lin0 to gamma) + colour 304,128
+FLOP_PER_KEPT_SDF = 2 * (528_640 + 524_544 + 459_008 + 304_128)
+
+
+def bench_sdf(args, rank, world, dev):
+    """Config 5 (sdf_pdf) geometry at the config-2 size: a 512x512 box-ray frame per GPU through
+    renderer_sdf.Renderer.render_device (anr_sdf_render_fwd); replicas, no collective."""
+    from animatable_nerf_amd import config, network, network_sdf, synthetic
+    from animatable_nerf_amd.renderer import near_far
+    from animatable_nerf_amd.renderer_sdf import Renderer
+    sc = synthetic.PdfScene(vsize=0.05)
+    ro, rd = sc.box_rays(args.rays, seed=2 + rank)
+    nr, fr, m = near_far(torch.from_numpy(sc.pbounds).to(dev), torch.from_numpy(ro).to(dev),
+                         torch.from_numpy(rd).to(dev))
+    m_np = m.cpu().numpy()
+    b = sc.batch_arrays(ro[m_np], rd[m_np], nr.cpu().numpy(), fr.cpu().numpy(), latent_index=7)
+    batch = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in b.items()}
+    tb0 = batch['tbounds'].clone()
+    R = int(batch['ray_o'].shape[1])
+    cfg = config.defaults()
+    cfg.num_train_frame = 260
+    cfg.perturb = 0
+    net = network_sdf.Network(cfg)
+    sd = synthetic.init_state_dict_sdf({k: tuple(v.shape) for k, v in net.state_dict().items()})
+    network.load_numpy_state(net, sd)
+    net = net.to(dev)
+    net.train()
+    renderer = Renderer(net, cfg)
+    for _ in range(args.warmup):
+        batch['tbounds'].copy_(tb0)
+        out = renderer.render_device(batch)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        batch['tbounds'].copy_(tb0)
+        out = renderer.render_device(batch)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt_max = float(t.item())
+    n_kept = renderer.last_counts[0]
+    achieved = n_kept * FLOP_PER_KEPT_SDF * args.steps / dt_max / 1e12
+    result = {
+        'metric': 'ray-samples/sec (512x512 rays x 64 samples), sdf_pdf render', 'value': R * 64 * args.steps * world / dt_max,
+        'unit': 'ray-samples/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
+        'ms_per_step': dt_max / args.steps * 1e3, 'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
+        'dtype': 'fp32', 'data': 'synthetic',
+        'config': {'workload': 'sdf_pdf (config 5 network) full 512x512 box-ray render, eval, fp32',
+                   'rays_per_gpu': R, 'kept_fraction': n_kept / (R * 64), 'parallelism': f'replicas{world}'},
+        'roofline': {'bound': 'mfma', 'kernel': 'whole render (layer GEMMs dominate)', 'achieved': achieved,
+                     'peak': PEAK_FP32_MFMA_TFLOPS, 'unit': 'TFLOP/s', 'frac': achieved / PEAK_FP32_MFMA_TFLOPS,
+                     'traffic': None, 'flop_per_kept': FLOP_PER_KEPT_SDF},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        import sys
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+        from oracle import restate_sdf
+        threads = min(16, os.cpu_count() or 1)
+        torch.set_num_threads(threads)
+        n = min(args.sdf_cpu_rays, R)
+        sub = {k: torch.from_numpy(np.ascontiguousarray(
+            v[:, :n] if k in ('ray_o', 'ray_d', 'near', 'far', 'occupancy', 'mask_at_box', 'rgb') else v).copy())
+            for k, v in b.items()}
+        P = {k: torch.from_numpy(v) for k, v in sd.items()}
+        with torch.no_grad():
+            t1 = time.perf_counter()
+            ref = restate_sdf.render(P, sub)
+            dtc = time.perf_counter() - t1
+        result['cpu_baseline'] = {'value': n * 64 / dtc, 'unit': 'ray-samples/s', 'cores': threads, 'kind': 'port',
+                                  'sample': f'first {n} rays of the frame, oracle/restate_sdf.py, {dtc:.1f} s'}
+        from oracle import restate
+        result['psnr_vs_fp32_oracle'] = float(restate.psnr(out['rgb_map'][0, :n].cpu().numpy(), ref['rgb_map'][0].numpy()))
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
