@@ -39,7 +39,11 @@ class Frame(ctypes.Structure):
 
 class RenderOpts(ctypes.Structure):
     _fields_ = [('n_samples', ctypes.c_int), ('chunk', ctypes.c_int), ('norm_th', ctypes.c_float),
-                ('train_th', ctypes.c_float), ('t_rand', ctypes.c_void_p), ('novel_pose', ctypes.c_int)]
+                ('train_th', ctypes.c_float), ('t_rand', ctypes.c_void_p), ('novel_pose', ctypes.c_int),
+                ('precision', ctypes.c_int)]
+
+
+FP32, BF16, BF16_ALL = 0, 1, 2  # anr_render_opts.precision
 
 
 class RenderOut(ctypes.Structure):

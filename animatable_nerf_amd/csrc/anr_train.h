@@ -37,6 +37,7 @@ struct GemmArgs {
   long ldsd;
   int spd_n;
   float div_post;      // v = v / div_post after the activation (cat(...)/sqrt(2) forward)
+  int bf16;            // operands rounded to bf16, bf16 MFMA, fp32 accumulate (training precision)
 };
 
 void launch_gemm(GemmArgs g, dim3 grid, hipStream_t s);

@@ -54,6 +54,8 @@ int check_args(const anr_params* p, const anr_frame* f, const float* ray_o, cons
   if (o->n_samples != 64) return fail(ANR_E_ARG, "train: only N_samples == 64 is supported");
   if (o->chunk <= 0 || n_rays <= 0) return fail(ANR_E_ARG, "train: bad chunk / n_rays");
   if (o->novel_pose) return fail(ANR_E_ARG, "train: novel_pose is a render-only option");
+  if (o->precision != ANR_FP32 && o->precision != ANR_BF16 && o->precision != ANR_BF16_ALL)
+    return fail(ANR_E_ARG, "train: bad precision");
   for (int i = 0; i < ANR_NUM_TENSORS; ++i)
     if (!p->t[i]) return fail(ANR_E_ARG, "train: NULL parameter tensor");
   if (!f->A || !f->R || !f->Th || !f->pbw || !f->tbw || !f->pbounds || !f->tbounds || !f->latent_index)
@@ -63,7 +65,9 @@ int check_args(const anr_params* p, const anr_frame* f, const float* ray_o, cons
 
 struct Exec {
   hipStream_t s;
-  int n;  // kept samples (host copy)
+  int n;         // kept samples (host copy)
+  int bf16 = 0;       // current GEMMs take bf16 operands
+  int pose_fp32 = 0;  // precision ANR_BF16 keeps the pose-space BW MLP in fp32 (ANR_BF16_ALL does not)
 
   int gemm(GemmArgs g, int M) {
     if (M <= 0 || g.N <= 0) return ANR_OK;
@@ -72,6 +76,7 @@ struct Exec {
     if (g.ksplit < 1) g.ksplit = 1;
     dim3 grid((g.N + 63) / 64, (M + 63) / 64, g.ksplit);
     g.M = M;
+    g.bf16 = bf16;
     launch_gemm(g, grid, s);
     return check_launch("k_gemm");
   }
@@ -119,6 +124,17 @@ struct Exec {
                        (const int*)nullptr, N, out, rpb);
     return check_launch("k_colsum");
   }
+};
+
+// the pose-space BW MLP under precision ANR_BF16 runs exact fp32 (its output moves the canonical
+// point that the 2^9-frequency encoding amplifies); restores the executor's mode on scope exit
+struct PoseScope {
+  Exec& e;
+  int keep;
+  explicit PoseScope(Exec& x) : e(x), keep(x.bf16) {
+    if (e.pose_fp32) e.bf16 = 0;
+  }
+  ~PoseScope() { e.bf16 = keep; }
 };
 
 int read_count(const int* dev, int* host, hipStream_t s) {
@@ -230,7 +246,10 @@ int train_forward(const anr_params* p, const anr_frame* f, const float* ray_o, c
     ANR_TRY(check_launch("k_tr_point_prep"));
   }
   // pose-space BW MLP (latent_index + 1), softmax + LBS, T-pose BW MLP (latent 0)
-  ANR_TRY(bw_forward(e, p, b.Gp, (float*)(ws + T.Hp), b.Lp, N, FOLD(0), FOLD(2)));
+  {
+    PoseScope ps(e);
+    ANR_TRY(bw_forward(e, p, b.Gp, (float*)(ws + T.Hp), b.Lp, N, FOLD(0), FOLD(2)));
+  }
   if (n > 0) {
     hipLaunchKernelGGL(k_tr_softmax_lbs, dim3(g1), dim3(256), 0, s, b);
     ANR_TRY(check_launch("k_tr_softmax_lbs"));
@@ -380,7 +399,7 @@ int anr_train_fwd(const anr_params* p, const anr_frame* f, const float* ray_o, c
   if (ws_bytes < T.total) return fail(ANR_E_WORKSPACE, "anr_train_fwd: workspace too small");
   hipStream_t s = (hipStream_t)stream;
   char* ws = (char*)workspace;
-  Exec e{s, 0};
+  Exec e{s, 0, o->precision != ANR_FP32 ? 1 : 0, o->precision == ANR_BF16 ? 1 : 0};
   ANR_TRY(train_forward(p, f, ray_o, ray_d, near_, far_, n_rays, o, out, ws, T, s, e));
   if (out->raw &&
       hipMemcpyAsync(out->raw, ws + T.L.raw, (size_t)n_rays * 64 * 16, hipMemcpyDeviceToDevice, s) != hipSuccess)
@@ -401,13 +420,14 @@ int anr_train_bwd(const anr_params* p, float* const* grads, const anr_frame* f, 
   if (ws_bytes < T.total) return fail(ANR_E_WORKSPACE, "anr_train_bwd: workspace too small");
   hipStream_t s = (hipStream_t)stream;
   char* ws = (char*)workspace;
-  Exec e{s, 0};
+  Exec e{s, 0, o->precision != ANR_FP32 ? 1 : 0, o->precision == ANR_BF16 ? 1 : 0};
   ANR_TRY(read_count((const int*)(ws + T.L.counts), &e.n, s));
   ANR_TRY(train_backward(p, grads, f, ray_o, ray_d, near_, far_, n_rays, o, d_rgb_map, d_pbw, d_tbw, ws, T, s, e));
   if (e.n <= 0) return ANR_OK;
   // pose BW MLP backward: d logits were produced by k_tr_softmax_bwd_p
   const long N = (long)n_rays * 64;
   float* ysum = (float*)(ws + T.ysum);
+  PoseScope ps(e);
   ANR_TRY(bw_backward(e, p, grads, (const float*)(ws + T.Gp), (const float*)(ws + T.Hp), (const float*)(ws + T.dLp),
                       (float*)(ws + T.dA), (float*)(ws + T.dB), nullptr, N, ysum + 1024, f->latent_index, 1, s));
   return ANR_OK;
@@ -428,7 +448,7 @@ int anr_train_step(const anr_params* p, float* const* grads, const anr_frame* f,
   if (ws_bytes < T.total) return fail(ANR_E_WORKSPACE, "anr_train_step: workspace too small");
   hipStream_t s = (hipStream_t)stream;
   char* ws = (char*)workspace;
-  Exec e{s, 0};
+  Exec e{s, 0, o->precision != ANR_FP32 ? 1 : 0, o->precision == ANR_BF16 ? 1 : 0};
   ANR_TRY(train_forward(p, f, ray_o, ray_d, near_, far_, n_rays, o, out, ws, T, s, e));
   // fused losses (tpose_trainer.py:50-63) and their upstream gradients
   TrainBufs b = bufs(T, ws, f, ray_o, ray_d, near_, far_, n_rays, o);
@@ -450,6 +470,7 @@ int anr_train_step(const anr_params* p, float* const* grads, const anr_frame* f,
   ANR_TRY(train_backward(p, grads, f, ray_o, ray_d, near_, far_, n_rays, o, d_rgb, d_pbw, d_tbw, ws, T, s, e));
   if (e.n <= 0) return ANR_OK;
   float* ysum = (float*)(ws + T.ysum);
+  PoseScope ps(e);
   return bw_backward(e, p, grads, (const float*)(ws + T.Gp), (const float*)(ws + T.Hp), (const float*)(ws + T.dLp),
                      (float*)(ws + T.dA), (float*)(ws + T.dB), nullptr, N, ysum + 1024, f->latent_index, 1, s);
 }

@@ -61,6 +61,11 @@ class _Call:
         o.train_th = float(cfg.train_th)
         o.t_rand = self.t_rand.data_ptr() if self.t_rand is not None else None
         o.novel_pose = 1 if cfg.get('test_novel_pose', False) else 0
+        prec = cfg.get('train_precision', 'fp32')
+        precs = {'fp32': _lib.FP32, 'bf16': _lib.BF16, 'bf16_all': _lib.BF16_ALL}
+        if prec not in precs:
+            raise ValueError(f"train_precision must be one of {sorted(precs)}, got {prec!r}")
+        o.precision = precs[prec]
         self.opts = o
         self.rgb = torch.empty((1, R, 3), device=dev)
         self.acc = torch.empty((1, R), device=dev)

@@ -25,6 +25,7 @@ import torch.distributed as dist
 FLOP_PER_KEPT = 2_312_192          # render credit (BW pose + NeRF, latent folded)
 FLOP_PER_KEPT_EXECUTED = 3_306_496  # + T-pose BW MLP (tbw rows are part of the render outputs)
 PEAK_FP32_MFMA_TFLOPS = 157.3      # MI355X_MICROARCH.md, Peak FP32 (matrix)
+PEAK_BF16_MFMA_TFLOPS = 2500.0     # MI355X_MICROARCH.md, BF16 dense (no sparsity)
 METRIC = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), 'BASELINE.json')))['metric']
 
 
@@ -41,6 +42,8 @@ def parse():
                          'sdf: config 5 sdf_pdf full-frame render')
     ap.add_argument('--sdf-cpu-rays', type=int, default=2048)
     ap.add_argument('--train-rays', type=int, default=1024)
+    ap.add_argument('--precision', choices=('fp32', 'bf16'), default='bf16',
+                    help='training GEMM operand precision (config 3 is bf16; fp32 = exact reference arithmetic)')
     return ap.parse_args()
 
 
@@ -168,6 +171,7 @@ def bench_train(args, rank, world, dev):
     net.train()
     cfg = config.defaults()
     cfg.perturb = 1
+    cfg.train_precision = args.precision
     step = FusedStep(net, cfg)
     for j in range(args.warmup):
         step.step(batches[j % nb])
@@ -194,16 +198,18 @@ def bench_train(args, rank, world, dev):
     from animatable_nerf_amd import _lib as L  # noqa: F401
     n_kept = step.renderer._counts(step.renderer._tws, R)[0]
     achieved = n_kept * FLOP_PER_KEPT_TRAIN * args.steps / dt_max / 1e12
+    peak = PEAK_BF16_MFMA_TFLOPS if args.precision == 'bf16' else PEAK_FP32_MFMA_TFLOPS
     result = {
         'metric': 'training ray-samples/s (1024 rays x 64 samples per GPU per step), aninerf training step',
         'value': R * 64 * args.steps * world / dt_max, 'unit': 'ray-samples/s', 'n_gpus': world, 'steps': args.steps,
         'warmup': args.warmup, 'ms_per_step': dt_max / args.steps * 1e3, 'higher_is_better': True, 'scaling': 'weak',
-        'vs_baseline': None, 'dtype': 'fp32', 'data': 'synthetic',
+        'vs_baseline': None, 'dtype': args.precision, 'data': 'synthetic',
         'config': {'workload': 'aninerf training step (configs 3/4 shape: 1024 rays/GPU, perturb 1, Adam)',
+                   'precision': f'{args.precision} GEMM operands, fp32 accumulation / master weights / Adam',
                    'rays_per_gpu': R, 'kept_samples_last_step': n_kept,
                    'parallelism': f'dp{world} (RCCL mean all-reduce of the flat gradient blob)'},
-        'roofline': {'bound': 'mfma', 'kernel': 'whole step', 'achieved': achieved, 'peak': PEAK_FP32_MFMA_TFLOPS,
-                     'unit': 'TFLOP/s', 'frac': achieved / PEAK_FP32_MFMA_TFLOPS, 'traffic': None,
+        'roofline': {'bound': 'mfma', 'kernel': 'whole step', 'achieved': achieved, 'peak': peak,
+                     'unit': 'TFLOP/s', 'frac': achieved / peak, 'traffic': None,
                      'flop_per_kept': FLOP_PER_KEPT_TRAIN},
         'loss_last_step': loss[:3],
     }

@@ -88,7 +88,13 @@ typedef struct anr_render_opts {
   const float* t_rand;  /* (R, n_samples) device stratification draws, or NULL (eval / perturb 0) */
   int novel_pose;    /* cfg.test_novel_pose: pose-space blend weights from novel_pose_bw
                         with bw_latent_index (tpose_nerf_network.py:93-94); render only */
+  int precision;     /* training GEMM operands: ANR_FP32 (exact fp32 MFMA); ANR_BF16 (config 3:
+                        operands rounded to bf16, fp32 accumulation, fp32 master weights and Adam,
+                        the pose-space blend-weight MLP kept fp32); ANR_BF16_ALL (every GEMM bf16).
+                        The render entry points always run fp32. */
 } anr_render_opts;
+
+enum { ANR_FP32 = 0, ANR_BF16 = 1, ANR_BF16_ALL = 2 };
 
 /* Outputs (device). raw may be NULL (then kept in the workspace). */
 typedef struct anr_render_out {

@@ -128,3 +128,31 @@ def test_fused_step_matches_reference_adam(dev):
         d = (p.detach() - before[name]).cpu().double()
         # d = p_new - p_old carries one fp32 ulp of |p| (embeddings are N(0,1)): atol 3e-7
         assert torch.allclose(d, expect, rtol=1e-4, atol=3e-7), name
+
+
+@pytest.mark.parametrize('prec', ['bf16', 'bf16_all'])
+def test_bf16_step_close_to_fp32(dev, prec):
+    """Config 3 precision policy: the same G4 step with bf16 GEMM operands (fp32 accumulation).
+    Bound: per-tensor relative L2 error of the gradients <= 3e-2 (bf16 unit roundoff 2^-9 = 2e-3
+    per operand, grown through ~20 layers), losses within 1e-3 relative, forward rgb within 5e-3."""
+    from animatable_nerf_amd.trainer import FusedStep
+    g, bt, t_rand = _g4_batch(dev)
+    out = {}
+    for p in ('fp32', prec):
+        cfg = _cfg()
+        cfg.train_precision = p
+        net = make_net(dev)
+        net.train()
+        step = FusedStep(net, cfg)
+        loss3 = step.step(bt, t_rand=t_rand.to(dev)).clone()
+        out[p] = (loss3, [gv.clone() for gv in step.grad_views], step.last.rgb.clone())
+    l32, g32, rgb32 = out['fp32']
+    lb, gb, rgbb = out[prec]
+    assert torch.allclose(lb[:3], l32[:3], rtol=1e-3, atol=0), (lb, l32)
+    assert (rgbb - rgb32).abs().max().item() <= 5e-3
+    worst = 0.0
+    for a, b in zip(gb, g32):
+        nb = b.norm().item()
+        if nb > 0:
+            worst = max(worst, (a - b).norm().item() / nb)
+    assert worst <= 3e-2, worst
