@@ -4,7 +4,7 @@ ARCH ?= gfx950
 SRC_DIR := animatable_nerf_amd/csrc
 SRCS := $(SRC_DIR)/anr_capi.hip $(SRC_DIR)/anr_rays.hip $(SRC_DIR)/anr_mlp.hip $(SRC_DIR)/anr_pack.hip \
         $(SRC_DIR)/anr_gemm.hip $(SRC_DIR)/anr_train.hip $(SRC_DIR)/anr_train_capi.hip \
-        $(SRC_DIR)/anr_sdf.hip $(SRC_DIR)/anr_sdf_capi.hip
+        $(SRC_DIR)/anr_sdf.hip $(SRC_DIR)/anr_sdf_capi.hip $(SRC_DIR)/anr_mlp_b16.hip
 OBJS := $(SRCS:.hip=.o)
 DEPS := $(OBJS:.o=.d)
 LIB := animatable_nerf_amd/libaninerf_hip.so
@@ -20,8 +20,9 @@ $(LIB): $(OBJS)
 
 -include $(DEPS)
 
-resources: $(SRC_DIR)/anr_mlp.hip
+resources: $(SRC_DIR)/anr_mlp.hip $(SRC_DIR)/anr_mlp_b16.hip
 	$(HIPCC) $(CXXFLAGS) -c $(SRC_DIR)/anr_mlp.hip -o /tmp/anr_mlp_res.o -Rpass-analysis=kernel-resource-usage
+	$(HIPCC) $(CXXFLAGS) -c $(SRC_DIR)/anr_mlp_b16.hip -o /tmp/anr_mlp_b16_res.o -Rpass-analysis=kernel-resource-usage
 
 clean:
 	rm -f $(OBJS) $(DEPS) $(LIB)

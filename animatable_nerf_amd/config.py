@@ -71,7 +71,7 @@ def defaults():
         'num_train_frame': 260, 'num_eval_frame': 133, 'num_latent_code': -1,
         'N_samples': 64, 'N_rand': 1024, 'perturb': 1, 'white_bkgd': False,
         'xyz_res': 10, 'view_res': 4, 'norm_th': 0.05, 'train_th': 0.0, 'box_padding': 0.05,
-        'aninerf_animation': False, 'test_novel_pose': False, 'eval': False, 'train_precision': 'fp32',
+        'aninerf_animation': False, 'test_novel_pose': False, 'eval': False, 'train_precision': 'fp32', 'render_precision': 'fp32',
         'chunk': 2048,
         'train': {'lr': 5e-4, 'weight_decay': 0.0, 'optim': 'adam', 'epoch': 400,
                   'scheduler': {'type': 'exponential', 'gamma': 0.1, 'decay_epochs': 1000}},

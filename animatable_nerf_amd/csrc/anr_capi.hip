@@ -141,10 +141,12 @@ int stage_mlp(const anr_params* p, const anr_frame* f, const float* ray_o, const
   ma.pose_boff = o->novel_pose ? ANR_NOVEL_BOFF : 0;
   const int lds = 2 * 8 * 5 * 1024 + 24 * 16 * 4;
   if (!mlp_attr_set) {
-    if (hipFuncSetAttribute((const void*)k_mlp, hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
+    if (hipFuncSetAttribute((const void*)k_mlp, hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess ||
+        hipFuncSetAttribute((const void*)k_mlp_b16, hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
       return fail(ANR_E_HIP, "hipFuncSetAttribute(k_mlp) failed");
     mlp_attr_set = true;
   }
+  const bool b16 = o->precision == ANR_BF16X3;
   const long max_tiles = (N + 127) / 128;
   const int grid = (int)(max_tiles < num_cus() ? max_tiles : num_cus());
   std::pair<hipEvent_t, hipEvent_t>* evp = nullptr;
@@ -158,7 +160,8 @@ int stage_mlp(const anr_params* p, const anr_frame* f, const float* ray_o, const
     evp = &g_prof.ev[g_prof.used++];
     if (hipEventRecord(evp->first, s) != hipSuccess) return fail(ANR_E_HIP, "hipEventRecord failed");
   }
-  hipLaunchKernelGGL(k_mlp, dim3(grid), dim3(512), lds, s, ma);
+  if (b16) hipLaunchKernelGGL(k_mlp_b16, dim3(grid), dim3(512), lds, s, ma);
+  else hipLaunchKernelGGL(k_mlp, dim3(grid), dim3(512), lds, s, ma);
   ANR_TRY(check_launch("k_mlp"));
   if (evp && hipEventRecord(evp->second, s) != hipSuccess) return fail(ANR_E_HIP, "hipEventRecord failed");
   return ANR_OK;
@@ -219,7 +222,7 @@ int anr_near_far(const float* ray_o, const float* ray_d, int n, const float* bou
   return check_launch("k_near_far");
 }
 
-size_t anr_params_packed_bytes(void) { return (size_t)packed_bytes(); }
+size_t anr_params_packed_bytes(void) { return (size_t)packed_bytes_all(); }
 
 int anr_params_pack(const anr_params* p, void* packed, void* stream) {
   if (!p || !packed) return fail(ANR_E_ARG, "anr_params_pack: NULL");
@@ -234,7 +237,9 @@ int anr_params_pack(const anr_params* p, void* packed, void* stream) {
   hipLaunchKernelGGL(k_pack_weights, dim3((nw + 255) / 256), dim3(256), 0, (hipStream_t)stream, a);
   ANR_TRY(check_launch("k_pack_weights"));
   hipLaunchKernelGGL(k_pack_bias, dim3((bias_floats() + 255) / 256), dim3(256), 0, (hipStream_t)stream, a);
-  return check_launch("k_pack_bias");
+  ANR_TRY(check_launch("k_pack_bias"));
+  hipLaunchKernelGGL(k_pack_b16, dim3((b16_bytes() / 32 + 255) / 256), dim3(256), 0, (hipStream_t)stream, a);
+  return check_launch("k_pack_b16");
 }
 
 size_t anr_render_workspace_bytes(int n_rays, const anr_render_opts* o, const anr_frame* f) {

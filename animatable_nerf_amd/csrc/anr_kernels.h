@@ -90,6 +90,7 @@ __global__ void k_gather_rows(const int*, const int*, const float4*, const float
 __global__ void k_composite(CompositeArgs a);
 __global__ void k_prep(PrepArgs a);
 __global__ void k_mlp(MlpArgs a);
+__global__ void k_mlp_b16(MlpArgs a);  // T-pose BW + NeRF in bf16x3 (render precision ANR_BF16X3)
 
 struct PackArgs {
   const float* t[65];  // 46 core tensors + 19 novel_pose_bw tensors (NULL when absent)
@@ -97,5 +98,6 @@ struct PackArgs {
 };
 __global__ void k_pack_weights(PackArgs a);
 __global__ void k_pack_bias(PackArgs a);
+__global__ void k_pack_b16(PackArgs a);
 
 }  // namespace anr

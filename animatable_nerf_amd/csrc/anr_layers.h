@@ -134,4 +134,43 @@ __host__ __device__ inline int layer_col(const LayerDesc& d, int t, int g) {
   return f < nf ? sg.col0 + f : -1;
 }
 
+// ------------------------------------------------------------------------------------------
+// bf16x3 image (render precision ANR_BF16X3): layers 0..20 again, for v_mfma_f32_16x16x32_bf16.
+//   A (weights) lane l: A[row l&15][k = 8(l>>4) + j], j = 0..7;  B (activations) the same k map.
+//   Each weight w is stored as hi = bf16(w), lo = bf16(w - hi); a product is accumulated as
+//   lo*bh + hi*bl + hi*bh (the dropped lo*bl and rounding terms are ~2^-16 relative).
+// k-step s of 32 inputs:
+//   ACT segment: previous out-blocks 2s, 2s+1; lane half h element j <-> neuron
+//                32s + (j < 4 ? 4h + j : 16 + 4h + j - 4), i.e. the two accumulators of the
+//                previous layer as they sit in the lane (no data movement);
+//   EMB / VEMB : feature 32s + 8h + j.
+// Per k-step, per out-block: [hi: 64 lanes x 16 B][lo: 64 lanes x 16 B] = 2 KiB; a k-step is the
+// staging slice (OB x 2 KiB <= 34 KiB).
+__host__ __device__ constexpr int ks32(int i) { return layer_ksteps(i) / 8; }
+__host__ __device__ constexpr int b16_layer_bytes(int i) { return ks32(i) * layer_desc_all(i).ob * 2048; }
+#define ANR_B16_LAYERS 21  // layers 0..20 (the pose pass and the novel-pose copy stay fp32)
+__host__ __device__ constexpr int b16_layer_offset(int i) {
+  int o = 0;
+  for (int k = 0; k < i; ++k) o += b16_layer_bytes(k);
+  return o;
+}
+__host__ __device__ constexpr int b16_bytes() { return b16_layer_offset(ANR_B16_LAYERS); }
+// byte offset of the bf16 image inside the packed buffer (after the fp32 weights and the biases)
+__host__ __device__ constexpr int b16_base() { return (packed_bytes() + 255) / 256 * 256; }
+__host__ __device__ constexpr int packed_bytes_all() { return b16_base() + b16_bytes(); }
+
+// weight column for bf16 k-step t, lane half h, element j (-1 = padding)
+__host__ __device__ inline int b16_col(const LayerDesc& d, int t, int h, int j) {
+  int s = 0;
+  for (; s < d.nseg; ++s) {
+    if (t < d.seg[s].ksteps / 8) break;
+    t -= d.seg[s].ksteps / 8;
+  }
+  const Seg sg = d.seg[s];
+  if (sg.kind == SRC_ACT) return sg.col0 + 32 * t + (j < 4 ? 4 * h + j : 16 + 4 * h + j - 4);
+  const int f = 32 * t + 8 * h + j;
+  const int nf = (sg.kind == SRC_EMB) ? 63 : 27;
+  return f < nf ? sg.col0 + f : -1;
+}
+
 }  // namespace anr

@@ -1,354 +1,8 @@
-// anr_mlp.hip — the fused per-kept-sample network kernel (A5, A7-A11) on fp32 MFMA.
-//
-// One launch processes every kept sample of the render call (persistent grid, 1 workgroup per CU,
-// 8 waves x 16 samples = 128 samples per tile). Per sample, entirely on chip:
-//   pose-space blend-weight lookup (pbw, 24 ch)            blend_utils.py:119-149
-//   gamma(x) -> BW MLP (latent folded into bias) -> softmax tpose_nerf_network.py:40-77
-//   LBS inverse warp to the T-pose                          blend_utils.py:41-59
-//   T-pose blend-weight lookup + BW MLP (tbw, for the loss) tpose_nerf_network.py:169-174
-//   gamma(x_T) -> NeRF 8x256 MLP, alpha/feature/latent/view/rgb heads   :252-275
-//   T-pose bbox mask, sigmoid, 1-exp(-relu(sigma) dist)     :186-212
-// Activations never leave registers: the 16x16x4 f32 MFMA accumulator of one layer is the B
-// operand of the next (anr_layers.h). Weights stream through LDS in 8-k-step slices (8-40 KiB),
-// double-buffered with global_load_lds, one slice stream across layers and tiles.
-#include <type_traits>
-
-#include "anr_common.h"
-#include "anr_kernels.h"
-#include "anr_layers.h"
+// anr_mlp.hip — k_mlp: the fused network kernel with exact fp32 MFMA everywhere (anr_mlp_body.h).
+#include "anr_mlp_body.h"
 
 namespace anr {
 
-#define SLICE_MAX (8 * 5 * 1024)  // largest slice: 8 k-steps x 5 chunks x 1 KiB
-#define LDS_A_OFF (2 * SLICE_MAX)
-#define MLP_LDS_BYTES (2 * SLICE_MAX + 24 * 16 * 4)
-
-template <int B, int E, typename F>
-__device__ __forceinline__ void static_for(F&& f) {
-  if constexpr (B < E) {
-    f(std::integral_constant<int, B>{});
-    static_for<B + 1, E>(f);
-  }
-}
-
-typedef __attribute__((address_space(3))) void lds_void;
-
-struct Pipe {
-  unsigned char* lds;
-  const unsigned char* wimg;
-  int cur;
-  int wave;
-  int lane;
-  int pose_woff;  // added to slices of the pose-space BW pass (novel_pose_bw weights)
-
-  __device__ __forceinline__ void stage(int off, int chunks, int buf) {
-    unsigned char* dst = lds + buf * SLICE_MAX;
-    // launder the base so the per-slice addresses are formed here, not hoisted out of the tile
-    // loop (hundreds of loop-invariant 64-bit addresses otherwise spill)
-    const unsigned char* w = wimg;
-    asm volatile("" : "+s"(w));
-    for (int i = 0; i < chunks; ++i) {
-      const int piece = wave + 8 * i;
-      __builtin_amdgcn_global_load_lds((const void*)(w + off + piece * 1024 + lane * 16),
-                                       (lds_void*)(dst + piece * 1024), 16, 0, 0);
-    }
-  }
-
-  // Enter slice Q of layer L: wait for it, prefetch the slice that follows (next layer NL).
-  // CUR_POSE / NL_POSE: whether this layer / the next one belongs to the pose-space BW pass.
-  template <int L, int Q, int NL, bool CUR_POSE, bool NL_POSE>
-  __device__ __forceinline__ const unsigned char* next() {
-    constexpr int NS = layer_ksteps(L) / ANR_KSLICE;
-    constexpr int nL = (Q + 1 < NS) ? L : NL;
-    constexpr int nQ = (Q + 1 < NS) ? Q + 1 : 0;
-    constexpr bool tgt_pose = (Q + 1 < NS) ? CUR_POSE : NL_POSE;
-    constexpr int nC = layer_chunks(nL);
-    constexpr int noff = layer_offset(nL) + nQ * nC * ANR_KSLICE * 1024;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    stage(noff + (tgt_pose ? pose_woff : 0), nC, cur ^ 1);
-    const unsigned char* r = lds + cur * SLICE_MAX;
-    cur ^= 1;
-    return r;
-  }
-};
-
-// One MLP layer: out = W * src + bias (acc layout), k-steps from the layer's segments.
-template <int L, int NL, bool RELU, bool CUR_POSE, bool NL_POSE, int NIN, int NOUT>
-__device__ __forceinline__ void layer(Pipe& p, const f32x4 (&in)[NIN], const float (&emb)[16], const float (&vemb)[8],
-                                      f32x4 (&out)[NOUT], const float* __restrict__ bias, int g, int lane) {
-  constexpr LayerDesc D = layer_desc_all(L);
-  constexpr int C = layer_chunks(L);
-  constexpr int K = layer_ksteps(L);
-  constexpr int K0 = D.seg[0].ksteps;
-  static_assert(NOUT >= D.ob, "output array too small");
-  const float* bptr = bias + 4 * g;
-  asm volatile("" : "+v"(bptr));  // keep the bias addresses local to the layer (see Pipe::stage)
-  static_for<0, D.ob>([&](auto ob) {
-    constexpr int o = decltype(ob)::value;
-    out[o] = *(const f32x4*)(bptr + o * 16);
-  });
-  const unsigned char* buf = nullptr;
-  static_for<0, K>([&](auto t) {
-    constexpr int tt = decltype(t)::value;
-    if constexpr (tt % ANR_KSLICE == 0) buf = p.template next<L, tt / ANR_KSLICE, NL, CUR_POSE, NL_POSE>();
-    f32x4 w[C];
-    static_for<0, C>([&](auto c) {
-      constexpr int cc = decltype(c)::value;
-      w[cc] = *(const f32x4*)(buf + (((tt % ANR_KSLICE) * C + cc) * 64 + lane) * 16);
-    });
-    constexpr int seg = tt < K0 ? 0 : 1;
-    constexpr int ts = tt < K0 ? tt : tt - K0;
-    constexpr int kind = D.seg[seg].kind;
-    float b;
-    if constexpr (kind == SRC_EMB) b = emb[ts];
-    else if constexpr (kind == SRC_VEMB) b = vemb[ts];
-    else b = in[ts >> 2][ts & 3];
-    static_for<0, D.ob>([&](auto ob) {
-      constexpr int o = decltype(ob)::value;
-      out[o] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[o >> 2][o & 3], b, out[o], 0, 0, 0);
-    });
-  });
-  if constexpr (RELU) {
-    static_for<0, D.ob>([&](auto ob) {
-      constexpr int o = decltype(ob)::value;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) out[o][r] = fmaxf(out[o][r], 0.0f);
-    });
-  }
-}
-
-// gamma(x) features 4s+g, s = 0..NS-1 (embedder.py:5-54); sincos once per feature
-template <int NS>
-__device__ __forceinline__ void embed(const float x[3], int g, int nfreq, float (&e)[NS]) {
-#pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    const int f = 4 * s + g;
-    float v;
-    if (f < 3) {
-      v = x[f == 0 ? 0 : (f == 1 ? 1 : 2)];
-    } else {
-      const int q = f - 3;
-      const int freq = q / 6;
-      const int w = q - freq * 6;
-      const int comp = w >= 3 ? w - 3 : w;
-      const float xc = comp == 0 ? x[0] : (comp == 1 ? x[1] : x[2]);
-      const float arg = xc * (float)(1 << (freq < 15 ? freq : 0));
-      float sv, cv;
-      sincosf(arg, &sv, &cv);
-      v = freq >= nfreq ? 0.0f : (w >= 3 ? cv : sv);
-    }
-    e[s] = v;
-  }
-}
-
-// 24-channel lookup from the 32-channel repacked volume, reference accumulation order.
-// block 0 -> channels 4g..4g+3, block 1 -> 16+4g..16+4g+3
-__device__ __forceinline__ void lookup24(const float* __restrict__ vol32, const float p[3], const float* __restrict__ bounds,
-                                         int X, int Y, int Z, int g, f32x4 (&out)[2]) {
-#pragma clang fp contract(off)
-  float lo[3], hi[3];
-#pragma unroll
-  for (int c = 0; c < 3; ++c) { lo[c] = bounds[c]; hi[c] = bounds[3 + c]; }
-  TriCell t;
-  tri_cell(p, lo, hi, X, Y, Z, t);
-  f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    if (t.base[k] >= 0) {
-      const f32x4 v0 = *(const f32x4*)(vol32 + (size_t)t.base[k] * 32 + 4 * g);
-      const f32x4 v1 = *(const f32x4*)(vol32 + (size_t)t.base[k] * 32 + 16 + 4 * g);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        a0[r] = a0[r] + v0[r] * t.w[k];
-        a1[r] = a1[r] + v1[r] * t.w[k];
-      }
-    }
-  }
-  out[0] = a0;
-  out[1] = a1;
-}
-
-// softmax over 24 channels of log(init + 1e-9) + fc (tpose_nerf_network.py:74-76); lanes
-// l, l^16, l^32, l^48 hold one point's channels.
-__device__ __forceinline__ void blend_softmax(const f32x4 (&fc)[2], const f32x4 (&init)[2], int g, f32x4 (&bw)[2]) {
-  float lg[2][4];
-  float m = -INFINITY;
-#pragma unroll
-  for (int b = 0; b < 2; ++b)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const bool valid = b == 0 || g < 2;
-      const float v = logf(init[b][r] + 1e-9f) + fc[b][r];
-      lg[b][r] = valid ? v : -INFINITY;
-      m = fmaxf(m, lg[b][r]);
-    }
-  m = fmaxf(m, __shfl_xor(m, 16));
-  m = fmaxf(m, __shfl_xor(m, 32));
-  float s = 0.f;
-#pragma unroll
-  for (int b = 0; b < 2; ++b)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      lg[b][r] = expf(lg[b][r] - m);
-      s += lg[b][r];
-    }
-  s += __shfl_xor(s, 16);
-  s += __shfl_xor(s, 32);
-#pragma unroll
-  for (int b = 0; b < 2; ++b)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) bw[b][r] = lg[b][r] / s;
-}
-
-// LBS inverse warp: A_b = sum_j bw_j A_j; x_T = inv(A_b[:3,:3]) (x - A_b[:3,3])
-__device__ __forceinline__ void lbs_inverse(const f32x4 (&bw)[2], const float* __restrict__ sA, int g, const float x[3],
-                                            float xt[3]) {
-  float Ab[16];
-#pragma unroll
-  for (int m = 0; m < 16; ++m) Ab[m] = 0.f;
-#pragma unroll
-  for (int b = 0; b < 2; ++b)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int j = b * 16 + 4 * g + r;
-      if (j < 24) {
-        const float wj = bw[b][r];
-#pragma unroll
-        for (int m = 0; m < 16; ++m) Ab[m] += wj * sA[j * 16 + m];
-      }
-    }
-#pragma unroll
-  for (int m = 0; m < 16; ++m) {
-    Ab[m] += __shfl_xor(Ab[m], 16);
-    Ab[m] += __shfl_xor(Ab[m], 32);
-  }
-  const float a = Ab[0], b = Ab[1], c = Ab[2], d = Ab[4], e = Ab[5], f = Ab[6], gg = Ab[8], h = Ab[9], i = Ab[10];
-  const float c00 = e * i - f * h, c01 = c * h - b * i, c02 = b * f - c * e;
-  const float c10 = f * gg - d * i, c11 = a * i - c * gg, c12 = c * d - a * f;
-  const float c20 = d * h - e * gg, c21 = b * gg - a * h, c22 = a * e - b * d;
-  const float det = a * c00 + b * c10 + c * c20;
-  const float rd = 1.0f / det;
-  const float y0 = x[0] - Ab[3], y1 = x[1] - Ab[7], y2 = x[2] - Ab[11];
-  xt[0] = (c00 * rd) * y0 + (c01 * rd) * y1 + (c02 * rd) * y2;
-  xt[1] = (c10 * rd) * y0 + (c11 * rd) * y1 + (c12 * rd) * y2;
-  xt[2] = (c20 * rd) * y0 + (c21 * rd) * y1 + (c22 * rd) * y2;
-}
-
-__device__ __forceinline__ void store_rows(float* __restrict__ rows, int idx, const f32x4 (&bw)[2], int g, bool valid) {
-  if (!valid) return;
-  *(f32x4*)(rows + (size_t)idx * 24 + 4 * g) = bw[0];
-  if (g < 2) *(f32x4*)(rows + (size_t)idx * 24 + 16 + 4 * g) = bw[1];
-}
-
-// BW MLP pass; NL_AFTER = layer after bw_fc in the slice stream (0: this is the pose pass and the
-// T-pose pass follows; 9: this is the T-pose pass and the NeRF follows). The pose pass may read the
-// novel_pose_bw copy of the weights (p.pose_woff, boff).
-template <int NL_AFTER>
-__device__ __forceinline__ void bw_mlp(Pipe& p, const float (&emb)[16], const float (&vemb)[8], const float* __restrict__ bias,
-                                       int boff, const float* __restrict__ fold0, const float* __restrict__ fold5,
-                                       f32x4 (&A)[17], f32x4 (&B)[17], f32x4 (&fc)[2], int g, int lane) {
-  constexpr bool P = NL_AFTER == 0;  // pose pass
-  f32x4 dummy[1];
-  const float* b = bias + boff;
-  layer<0, 1, true, P, P>(p, dummy, emb, vemb, A, fold0, g, lane);
-  layer<1, 2, true, P, P>(p, A, emb, vemb, B, b + kBiasOff<1>, g, lane);
-  layer<2, 3, true, P, P>(p, B, emb, vemb, A, b + kBiasOff<2>, g, lane);
-  layer<3, 4, true, P, P>(p, A, emb, vemb, B, b + kBiasOff<3>, g, lane);
-  layer<4, 5, true, P, P>(p, B, emb, vemb, A, b + kBiasOff<4>, g, lane);
-  layer<5, 6, true, P, P>(p, A, emb, vemb, B, fold5, g, lane);
-  layer<6, 7, true, P, P>(p, B, emb, vemb, A, b + kBiasOff<6>, g, lane);
-  layer<7, 8, true, P, P>(p, A, emb, vemb, B, b + kBiasOff<7>, g, lane);
-  layer<8, NL_AFTER, false, P, false>(p, B, emb, vemb, fc, b + kBiasOff<8>, g, lane);
-}
-
-__global__ __launch_bounds__(512) void k_mlp(MlpArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int g = lane >> 4;
-  const int pl = lane & 15;
-  float* sA = (float*)(smem + LDS_A_OFF);
-  for (int i = tid; i < 384; i += 512) sA[i] = a.A[i];
-
-  const int n = *a.n_kept;
-  const int ntiles = (n + 127) / 128;
-  if ((int)blockIdx.x >= ntiles) return;  // uniform per workgroup, before any LDS-DMA
-
-  Pipe p{smem, a.wimg, 0, wave, lane, a.pose_woff};
-  p.stage(layer_offset(0) + a.pose_woff, layer_chunks(0), 0);
-
-  const float* fold = a.fold;
-  float tb_lo[3], tb_hi[3];
-#pragma unroll
-  for (int c = 0; c < 3; ++c) { tb_lo[c] = a.tbounds[c]; tb_hi[c] = a.tbounds[3 + c]; }
-
-  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const int idx = tile * 128 + wave * 16 + pl;
-    const bool valid = idx < n;
-    const int pid = a.list[valid ? idx : n - 1];
-    const int ray = pid >> 6, s = pid & 63;
-    float z, dist, pts[3], pose[3];
-    sample_point(a.ray_o, a.ray_d, a.near_, a.far_, a.t_rand, ray, s, 64, z, dist, pts);
-    world_to_pose(pts, a.R, a.Th, pose);
-    const float dir[3] = {a.ray_d[3 * ray], a.ray_d[3 * ray + 1], a.ray_d[3 * ray + 2]};
-
-    float emb[16], vemb[8];
-    f32x4 A[17], B[17], fc[2], init[2], bw[2];
-
-    // ---- pose space: pbw lookup, BW MLP (latent_index + 1), softmax, LBS
-    embed<16>(pose, g, 10, emb);
-    lookup24(a.pbw32, pose, a.pbounds, a.pX, a.pY, a.pZ, g, init);
-#pragma unroll
-    for (int s8 = 0; s8 < 8; ++s8) vemb[s8] = 0.f;
-    bw_mlp<0>(p, emb, vemb, a.bias, a.pose_boff, fold + 0, fold + 512, A, B, fc, g, lane);
-    blend_softmax(fc, init, g, bw);
-    store_rows(a.pbw_rows, idx, bw, g, valid);
-    float xt[3];
-    lbs_inverse(bw, sA, g, pose, xt);
-
-    // ---- T-pose: tbw lookup, BW MLP (latent 0) -> tbw rows (training loss only)
-    embed<16>(xt, g, 10, emb);
-    lookup24(a.tbw32, xt, a.tbounds, a.tX, a.tY, a.tZ, g, init);
-    bw_mlp<9>(p, emb, vemb, a.bias, 0, fold + 256, fold + 768, A, B, fc, g, lane);
-    blend_softmax(fc, init, g, bw);
-    store_rows(a.tbw_rows, idx, bw, g, valid);
-
-    // ---- canonical NeRF (TPoseHuman.calculate_alpha_rgb)
-    f32x4 dummy[1];
-    const float* bias = a.bias;
-    layer<9, 10, true, false, false>(p, dummy, emb, vemb, A, bias + kBiasOff<9>, g, lane);
-    layer<10, 11, true, false, false>(p, A, emb, vemb, B, bias + kBiasOff<10>, g, lane);
-    layer<11, 12, true, false, false>(p, B, emb, vemb, A, bias + kBiasOff<11>, g, lane);
-    layer<12, 13, true, false, false>(p, A, emb, vemb, B, bias + kBiasOff<12>, g, lane);
-    layer<13, 14, true, false, false>(p, B, emb, vemb, A, bias + kBiasOff<13>, g, lane);
-    layer<14, 15, true, false, false>(p, A, emb, vemb, B, bias + kBiasOff<14>, g, lane);
-    layer<15, 16, true, false, false>(p, B, emb, vemb, A, bias + kBiasOff<15>, g, lane);
-    layer<16, 17, true, false, false>(p, A, emb, vemb, B, bias + kBiasOff<16>, g, lane);
-    layer<17, 18, false, false, false>(p, B, emb, vemb, A, bias + kBiasOff<17>, g, lane);  // feature || alpha
-    const float sigma_raw = __shfl(A[16][0], pl);
-    layer<18, 19, false, false, false>(p, A, emb, vemb, B, fold + 1024, g, lane);  // latent_fc
-    embed<8>(dir, g, 4, vemb);
-    layer<19, 20, true, false, false>(p, B, emb, vemb, A, bias + kBiasOff<19>, g, lane);  // view_fc
-    layer<20, 0, false, false, true>(p, A, emb, vemb, B, bias + kBiasOff<20>, g, lane);  // rgb_fc
-
-    // ---- bbox mask, activations, outputs
-    bool inside = true;
-#pragma unroll
-    for (int c = 0; c < 3; ++c) inside = inside && (xt[c] > tb_lo[c]) && (xt[c] < tb_hi[c]);
-    const float sig = inside ? sigma_raw : 0.0f;
-    if (valid && g == 0) {
-      float4 r;
-      r.x = 1.0f / (1.0f + expf(-B[0][0]));
-      r.y = 1.0f / (1.0f + expf(-B[0][1]));
-      r.z = 1.0f / (1.0f + expf(-B[0][2]));
-      r.w = 1.0f - expf(-fmaxf(sig, 0.0f) * dist);
-      a.raw[pid] = r;
-      a.sigma[idx] = sig;
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the last (unused) prefetch
-}
+__global__ __launch_bounds__(512) void k_mlp(MlpArgs a) { mlp_body<false>(a); }
 
 }  // namespace anr

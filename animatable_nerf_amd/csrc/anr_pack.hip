@@ -56,6 +56,53 @@ __global__ void k_pack_bias(PackArgs a) {
   ((float*)(a.out + weights_bytes()))[e] = v;
 }
 
+// bf16x3 image (anr_layers.h): one thread per (layer, k-step, out-block, lane) writes the 8 hi and
+// the 8 lo bf16 of its fragment
+__device__ __forceinline__ unsigned short bf16_rne(float f) {
+  uint32_t u = __float_as_uint(f);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (unsigned short)(u >> 16);
+}
+
+__global__ void k_pack_b16(PackArgs a) {
+  const int u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= b16_bytes() / 32) return;
+  const int byte = u * 32;
+  int L = 0;
+  while (L + 1 < ANR_B16_LAYERS && byte >= b16_layer_offset(L + 1)) ++L;
+  const LayerDesc d = layer_desc_all(L);
+  const int local = (byte - b16_layer_offset(L)) / 32;  // (s, ob, lane)
+  const int lane = local & 63;
+  const int so = local >> 6;
+  const int ob = so % d.ob, t = so / d.ob;
+  const int row16 = lane & 15, h = lane >> 4;
+  const int main_ob = (d.nout + 15) / 16;
+  unsigned short hi[8], lo[8];
+  for (int j = 0; j < 8; ++j) {
+    const int col = b16_col(d, t, h, j);
+    float v = 0.0f;
+    if (col >= 0 && a.t[d.tensor_w] != nullptr) {
+      if (ob < main_ob) {
+        const int i = ob * 16 + row16;
+        if (i < d.nout) v = a.t[d.tensor_w][(size_t)i * d.in_ch + col];
+      } else if (d.tensor_w2 >= 0) {
+        const int i2 = (ob - main_ob) * 16 + row16;
+        if (i2 < d.nout2) v = a.t[d.tensor_w2][(size_t)i2 * d.in_ch + col];
+      }
+    }
+    hi[j] = bf16_rne(v);
+    lo[j] = bf16_rne(v - __uint_as_float((uint32_t)hi[j] << 16));
+  }
+  unsigned char* base = a.out + b16_base() + b16_layer_offset(L) + (size_t)so * 2048;
+  uint4 vh, vl;
+  vh.x = hi[0] | ((uint32_t)hi[1] << 16); vh.y = hi[2] | ((uint32_t)hi[3] << 16);
+  vh.z = hi[4] | ((uint32_t)hi[5] << 16); vh.w = hi[6] | ((uint32_t)hi[7] << 16);
+  vl.x = lo[0] | ((uint32_t)lo[1] << 16); vl.y = lo[2] | ((uint32_t)lo[3] << 16);
+  vl.z = lo[4] | ((uint32_t)lo[5] << 16); vl.w = lo[6] | ((uint32_t)lo[7] << 16);
+  *(uint4*)(base + lane * 16) = vh;
+  *(uint4*)(base + 1024 + lane * 16) = vl;
+}
+
 // grid: blocks [0, nvox_blocks) repack volumes; block 'fold' computes the five folded biases
 __global__ __launch_bounds__(256) void k_prep(PrepArgs a) {
   const int nvb = (a.np + a.nt + 7) / 8;  // 8 voxels (x 32 channels) per block

@@ -54,7 +54,7 @@ int check_args(const anr_params* p, const anr_frame* f, const float* ray_o, cons
   if (o->n_samples != 64) return fail(ANR_E_ARG, "train: only N_samples == 64 is supported");
   if (o->chunk <= 0 || n_rays <= 0) return fail(ANR_E_ARG, "train: bad chunk / n_rays");
   if (o->novel_pose) return fail(ANR_E_ARG, "train: novel_pose is a render-only option");
-  if (o->precision != ANR_FP32 && o->precision != ANR_BF16 && o->precision != ANR_BF16_ALL)
+  if (o->precision < ANR_FP32 || o->precision > ANR_BF16X3)
     return fail(ANR_E_ARG, "train: bad precision");
   for (int i = 0; i < ANR_NUM_TENSORS; ++i)
     if (!p->t[i]) return fail(ANR_E_ARG, "train: NULL parameter tensor");
@@ -399,7 +399,7 @@ int anr_train_fwd(const anr_params* p, const anr_frame* f, const float* ray_o, c
   if (ws_bytes < T.total) return fail(ANR_E_WORKSPACE, "anr_train_fwd: workspace too small");
   hipStream_t s = (hipStream_t)stream;
   char* ws = (char*)workspace;
-  Exec e{s, 0, o->precision != ANR_FP32 ? 1 : 0, o->precision == ANR_BF16 ? 1 : 0};
+  Exec e{s, 0, (o->precision == ANR_BF16 || o->precision == ANR_BF16_ALL) ? 1 : 0, o->precision == ANR_BF16 ? 1 : 0};
   ANR_TRY(train_forward(p, f, ray_o, ray_d, near_, far_, n_rays, o, out, ws, T, s, e));
   if (out->raw &&
       hipMemcpyAsync(out->raw, ws + T.L.raw, (size_t)n_rays * 64 * 16, hipMemcpyDeviceToDevice, s) != hipSuccess)
@@ -420,7 +420,7 @@ int anr_train_bwd(const anr_params* p, float* const* grads, const anr_frame* f, 
   if (ws_bytes < T.total) return fail(ANR_E_WORKSPACE, "anr_train_bwd: workspace too small");
   hipStream_t s = (hipStream_t)stream;
   char* ws = (char*)workspace;
-  Exec e{s, 0, o->precision != ANR_FP32 ? 1 : 0, o->precision == ANR_BF16 ? 1 : 0};
+  Exec e{s, 0, (o->precision == ANR_BF16 || o->precision == ANR_BF16_ALL) ? 1 : 0, o->precision == ANR_BF16 ? 1 : 0};
   ANR_TRY(read_count((const int*)(ws + T.L.counts), &e.n, s));
   ANR_TRY(train_backward(p, grads, f, ray_o, ray_d, near_, far_, n_rays, o, d_rgb_map, d_pbw, d_tbw, ws, T, s, e));
   if (e.n <= 0) return ANR_OK;
@@ -448,7 +448,7 @@ int anr_train_step(const anr_params* p, float* const* grads, const anr_frame* f,
   if (ws_bytes < T.total) return fail(ANR_E_WORKSPACE, "anr_train_step: workspace too small");
   hipStream_t s = (hipStream_t)stream;
   char* ws = (char*)workspace;
-  Exec e{s, 0, o->precision != ANR_FP32 ? 1 : 0, o->precision == ANR_BF16 ? 1 : 0};
+  Exec e{s, 0, (o->precision == ANR_BF16 || o->precision == ANR_BF16_ALL) ? 1 : 0, o->precision == ANR_BF16 ? 1 : 0};
   ANR_TRY(train_forward(p, f, ray_o, ray_d, near_, far_, n_rays, o, out, ws, T, s, e));
   // fused losses (tpose_trainer.py:50-63) and their upstream gradients
   TrainBufs b = bufs(T, ws, f, ray_o, ray_d, near_, far_, n_rays, o);

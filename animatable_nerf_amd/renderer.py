@@ -66,6 +66,11 @@ class _Call:
         if prec not in precs:
             raise ValueError(f"train_precision must be one of {sorted(precs)}, got {prec!r}")
         o.precision = precs[prec]
+        self.render_precision = _lib.FP32
+        rprec = cfg.get('render_precision', 'fp32')
+        if rprec not in ('fp32', 'bf16x3'):
+            raise ValueError(f"render_precision must be 'fp32' or 'bf16x3', got {rprec!r}")
+        self.render_precision = _lib.BF16X3 if rprec == 'bf16x3' else _lib.FP32
         self.opts = o
         self.rgb = torch.empty((1, R, 3), device=dev)
         self.acc = torch.empty((1, R), device=dev)
@@ -160,6 +165,7 @@ class Renderer:
         c = _Call(self, batch, self._t_rand(R, dev, t_rand))
         ws_bytes = self.lib.anr_render_workspace_bytes(R, ctypes.byref(c.opts), ctypes.byref(c.frame))
         ws = self._workspace('_ws', ws_bytes, dev)
+        c.opts.precision = c.render_precision
         _lib.check(self.lib.anr_render_fwd(ctypes.byref(p), ctypes.byref(c.frame), *c.ray_ptrs(), R,
                                            ctypes.byref(c.opts), ctypes.byref(c.out), _lib.ptr(ws), ws_bytes,
                                            _lib.stream_ptr(dev)), 'anr_render_fwd')

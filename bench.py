@@ -41,6 +41,9 @@ def parse():
                     help='render: config 2 (headline); train: config 3/4 training step (1024 rays/GPU); '
                          'sdf: config 5 sdf_pdf full-frame render')
     ap.add_argument('--sdf-cpu-rays', type=int, default=2048)
+    ap.add_argument('--render-precision', choices=('fp32', 'bf16x3'), default='fp32',
+                    help='fp32: exact fp32 MFMA; bf16x3: T-pose BW MLP + NeRF as hi/lo-split bf16 MFMA '
+                         '(outputs within the 1e-4 fp32 tolerance, tests/test_gpu_render.py)')
     ap.add_argument('--train-rays', type=int, default=1024)
     ap.add_argument('--precision', choices=('fp32', 'bf16'), default='bf16',
                     help='training GEMM operand precision (config 3 is bf16; fp32 = exact reference arithmetic)')
@@ -80,6 +83,7 @@ def main():
     net.train()  # run.py evaluates in train() mode with perturb = 0
     cfg = config.defaults()
     cfg.perturb = 0
+    cfg.render_precision = args.render_precision
     renderer = Renderer(net, cfg)
     lib = _lib.load()
 

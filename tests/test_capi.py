@@ -37,7 +37,12 @@ def test_version_and_sizes(lib):
     assert lib.anr_version() == 1
     # 19 weight layers + view/rgb heads, fp32 weight image + padded biases
     # + 9 novel_pose_bw layers (same image as the 9 BW layers)
-    assert lib.anr_params_packed_bytes() == 4_767_744 + 2_031_616 + 4 * (4_800 + 2_080)
+    fp32 = 4_767_744 + 2_031_616 + 4 * (4_800 + 2_080)  # fp32 image (+ novel-pose copy) + biases
+    # bf16x3 image: per layer ceil(in/32) k-steps x out-blocks x 2 KiB (hi + lo fragments)
+    ks_ob = [(2, 16), (8, 16), (8, 16), (8, 16), (8, 16), (10, 16), (8, 16), (8, 16), (8, 2),
+             (2, 16), (8, 16), (8, 16), (8, 16), (8, 16), (10, 16), (8, 16), (8, 16), (8, 17), (8, 16), (9, 8), (4, 1)]
+    b16 = sum(k * o for k, o in ks_ob) * 2048
+    assert lib.anr_params_packed_bytes() == (fp32 + 255) // 256 * 256 + b16
 
 
 def test_workspace_grows_with_rays(lib):

@@ -23,14 +23,17 @@ def dev():
     return torch.device('cuda:0')
 
 
-@pytest.fixture(scope='module')
-def renderer(dev):
+@pytest.fixture(scope='module', params=['fp32', 'bf16x3'])
+def renderer(dev, request):
+    """Both render precisions are held to the same fp32 tolerance (north_star): exact fp32 MFMA, and
+    the hi/lo-split bf16 MFMA of the T-pose BW MLP + NeRF (include/aninerf.h ANR_BF16X3)."""
     from animatable_nerf_amd.renderer import Renderer
     net = make_net(dev)
     net.train()  # run.py evaluates in train() mode with perturb = 0
     from animatable_nerf_amd import config
     cfg = config.defaults()
     cfg.perturb = 0
+    cfg.render_precision = request.param
     return Renderer(net, cfg)
 
 
