@@ -137,16 +137,18 @@ int stage_mlp(const anr_params* p, const anr_frame* f, const float* ray_o, const
   ma.sigma = (float*)(ws + L.sigma);
   ma.pbw_rows = (float*)(ws + L.pbw_rows);
   ma.tbw_rows = (float*)(ws + L.tbw_rows);
-  ma.pose_woff = o->novel_pose ? ANR_NOVEL_WOFF : 0;
+  const bool b16 = o->precision == ANR_BF16X3;
+  ma.pose_woff = o->novel_pose ? (b16 ? ANR_X6_NOVEL_WOFF : ANR_NOVEL_WOFF) : 0;
   ma.pose_boff = o->novel_pose ? ANR_NOVEL_BOFF : 0;
-  const int lds = 2 * 8 * 5 * 1024 + 24 * 16 * 4;
+  const int lds = b16 ? mlp_lds_bytes<true>() : mlp_lds_bytes<false>();
   if (!mlp_attr_set) {
-    if (hipFuncSetAttribute((const void*)k_mlp, hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess ||
-        hipFuncSetAttribute((const void*)k_mlp_b16, hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess)
+    if (hipFuncSetAttribute((const void*)k_mlp, hipFuncAttributeMaxDynamicSharedMemorySize, mlp_lds_bytes<false>()) !=
+            hipSuccess ||
+        hipFuncSetAttribute((const void*)k_mlp_b16, hipFuncAttributeMaxDynamicSharedMemorySize, mlp_lds_bytes<true>()) !=
+            hipSuccess)
       return fail(ANR_E_HIP, "hipFuncSetAttribute(k_mlp) failed");
     mlp_attr_set = true;
   }
-  const bool b16 = o->precision == ANR_BF16X3;
   const long max_tiles = (N + 127) / 128;
   const int grid = (int)(max_tiles < num_cus() ? max_tiles : num_cus());
   std::pair<hipEvent_t, hipEvent_t>* evp = nullptr;
@@ -239,7 +241,9 @@ int anr_params_pack(const anr_params* p, void* packed, void* stream) {
   hipLaunchKernelGGL(k_pack_bias, dim3((bias_floats() + 255) / 256), dim3(256), 0, (hipStream_t)stream, a);
   ANR_TRY(check_launch("k_pack_bias"));
   hipLaunchKernelGGL(k_pack_b16, dim3((b16_bytes() / 32 + 255) / 256), dim3(256), 0, (hipStream_t)stream, a);
-  return check_launch("k_pack_b16");
+  ANR_TRY(check_launch("k_pack_b16"));
+  hipLaunchKernelGGL(k_pack_x6, dim3((x6_bytes() / 48 + 255) / 256), dim3(256), 0, (hipStream_t)stream, a);
+  return check_launch("k_pack_x6");
 }
 
 size_t anr_render_workspace_bytes(int n_rays, const anr_render_opts* o, const anr_frame* f) {

@@ -99,5 +99,6 @@ struct PackArgs {
 __global__ void k_pack_weights(PackArgs a);
 __global__ void k_pack_bias(PackArgs a);
 __global__ void k_pack_b16(PackArgs a);
+__global__ void k_pack_x6(PackArgs a);
 
 }  // namespace anr

@@ -157,7 +157,23 @@ __host__ __device__ constexpr int b16_layer_offset(int i) {
 __host__ __device__ constexpr int b16_bytes() { return b16_layer_offset(ANR_B16_LAYERS); }
 // byte offset of the bf16 image inside the packed buffer (after the fp32 weights and the biases)
 __host__ __device__ constexpr int b16_base() { return (packed_bytes() + 255) / 256 * 256; }
-__host__ __device__ constexpr int packed_bytes_all() { return b16_base() + b16_bytes(); }
+
+
+// bf16x6 image (the pose-space BW pass under ANR_BF16X3): layers 0..8 and their novel_pose_bw copy
+// 21..29, each weight as hi/mid/lo bf16 (w = hi + mid + lo to 24 bits), the activation likewise;
+// products hl + lh + mm + hm + mh + hh (dropped terms ~2^-24: fp32-level). Per k-step, per
+// out-block [hi][mid][lo] fragments = 3 KiB; x6 index i <-> layer (i < 9 ? i : 21 + i - 9).
+#define ANR_X6_LAYERS 18
+__host__ __device__ constexpr int x6_layer(int i) { return i < 9 ? i : ANR_L_NOVEL0 + i - 9; }
+__host__ __device__ constexpr int x6_layer_bytes(int i) { return ks32(x6_layer(i)) * layer_desc_all(x6_layer(i)).ob * 3072; }
+__host__ __device__ constexpr int x6_layer_offset(int i) {
+  int o = 0;
+  for (int k = 0; k < i; ++k) o += x6_layer_bytes(k);
+  return o;
+}
+__host__ __device__ constexpr int x6_bytes() { return x6_layer_offset(ANR_X6_LAYERS); }
+__host__ __device__ constexpr int x6_base() { return (b16_base() + b16_bytes() + 255) / 256 * 256; }
+#define ANR_X6_NOVEL_WOFF (x6_layer_offset(9) - x6_layer_offset(0))
 
 // weight column for bf16 k-step t, lane half h, element j (-1 = padding)
 __host__ __device__ inline int b16_col(const LayerDesc& d, int t, int h, int j) {
@@ -172,5 +188,14 @@ __host__ __device__ inline int b16_col(const LayerDesc& d, int t, int h, int j) 
   const int nf = (sg.kind == SRC_EMB) ? 63 : 27;
   return f < nf ? sg.col0 + f : -1;
 }
+
+__host__ __device__ constexpr int packed_bytes_all() { return x6_base() + x6_bytes(); }
+
+// LDS of the fused kernel: two staging buffers of the largest slice + the 24 joint transforms
+// (fp32: 8 k-steps x 5 chunks x 1 KiB; bf16 kernel: a bf16x6 k-step of 16 out-blocks x 3 KiB)
+template <bool B16>
+__host__ __device__ constexpr int mlp_slice_max() { return B16 ? 16 * 3072 : 8 * 5 * 1024; }
+template <bool B16>
+__host__ __device__ constexpr int mlp_lds_bytes() { return 2 * mlp_slice_max<B16>() + 24 * 16 * 4; }
 
 }  // namespace anr

@@ -21,9 +21,6 @@
 
 namespace anr {
 
-#define SLICE_MAX (8 * 5 * 1024)  // largest slice: 8 k-steps x 5 chunks x 1 KiB
-#define LDS_A_OFF (2 * SLICE_MAX)
-#define MLP_LDS_BYTES (2 * SLICE_MAX + 24 * 16 * 4)
 
 template <int B, int E, typename F>
 __device__ __forceinline__ void static_for(F&& f) {
@@ -36,30 +33,39 @@ __device__ __forceinline__ void static_for(F&& f) {
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
-// The per-tile layer program: entries 0..8 the pose-space BW MLP (always exact fp32, it moves the
-// canonical point that the 2^9-frequency encoding amplifies), 9..17 the T-pose BW MLP (layers 0..8
-// again), 18..29 the NeRF (layers 9..20). With B16 the entries >= 9 run bf16x3 (anr_layers.h).
+// The per-tile layer program: entries 0..8 the pose-space BW MLP, 9..17 the T-pose BW MLP (layers
+// 0..8 again), 18..29 the NeRF (layers 9..20). Arithmetic per entry (anr_layers.h):
+//   mode 0 exact fp32 MFMA (k_mlp, every entry);
+//   mode 2 bf16x6, fp32-level (k_mlp_b16, the pose pass: its output moves the canonical point that
+//          the 2^9-frequency encoding amplifies);
+//   mode 1 bf16x3 (k_mlp_b16, entries >= 9).
 #define ANR_PROG_LEN 30
 __host__ __device__ constexpr int prog_layer(int e) { return e < 9 ? e : e - 9; }
 __host__ __device__ constexpr bool prog_pose(int e) { return e < 9; }
 template <bool B16>
-__host__ __device__ constexpr bool prog_b16(int e) { return B16 && e >= 9; }
+__host__ __device__ constexpr int prog_mode(int e) { return B16 ? (e < 9 ? 2 : 1) : 0; }
 template <bool B16>
 __host__ __device__ constexpr int prog_slices(int e) {
-  return prog_b16<B16>(e) ? ks32(prog_layer(e)) : layer_ksteps(prog_layer(e)) / ANR_KSLICE;
+  return prog_mode<B16>(e) ? ks32(prog_layer(e)) : layer_ksteps(prog_layer(e)) / ANR_KSLICE;
 }
 template <bool B16>
 __host__ __device__ constexpr int prog_slice_kb(int e) {
-  return prog_b16<B16>(e) ? layer_desc_all(prog_layer(e)).ob * 2 : layer_chunks(prog_layer(e)) * ANR_KSLICE;
+  return prog_mode<B16>(e) == 2   ? layer_desc_all(prog_layer(e)).ob * 3
+         : prog_mode<B16>(e) == 1 ? layer_desc_all(prog_layer(e)).ob * 2
+                                  : layer_chunks(prog_layer(e)) * ANR_KSLICE;
 }
 template <bool B16>
 __host__ __device__ constexpr int prog_slice_off(int e, int q) {
-  return prog_b16<B16>(e) ? b16_base() + b16_layer_offset(prog_layer(e)) + q * layer_desc_all(prog_layer(e)).ob * 2048
-                          : layer_offset(prog_layer(e)) + q * layer_chunks(prog_layer(e)) * ANR_KSLICE * 1024;
+  return prog_mode<B16>(e) == 2
+             ? x6_base() + x6_layer_offset(prog_layer(e)) + q * layer_desc_all(prog_layer(e)).ob * 3072
+         : prog_mode<B16>(e) == 1
+             ? b16_base() + b16_layer_offset(prog_layer(e)) + q * layer_desc_all(prog_layer(e)).ob * 2048
+             : layer_offset(prog_layer(e)) + q * layer_chunks(prog_layer(e)) * ANR_KSLICE * 1024;
 }
 
 struct Pipe {
   unsigned char* lds;
+  int smax;  // bytes per staging buffer
   const unsigned char* wimg;
   int cur;
   int wave;
@@ -68,7 +74,7 @@ struct Pipe {
 
   // issue the HBM/L2 -> LDS copy of `kb` KiB at byte `off` of the packed image into buffer `buf`
   __device__ __forceinline__ void stage(int off, int kb, int buf) {
-    unsigned char* dst = lds + buf * SLICE_MAX;
+    unsigned char* dst = lds + buf * smax;
     // launder the base so the per-slice addresses are formed here, not hoisted out of the tile
     // loop (hundreds of loop-invariant 64-bit addresses otherwise spill)
     const unsigned char* w = wimg;
@@ -89,7 +95,7 @@ struct Pipe {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     stage(noff + (prog_pose(nE) ? pose_woff : 0), nkb, cur ^ 1);
-    const unsigned char* r = lds + cur * SLICE_MAX;
+    const unsigned char* r = lds + cur * smax;
     cur ^= 1;
     return r;
   }
@@ -102,6 +108,19 @@ __device__ __forceinline__ void split8(const float (&x)[8], bf16x8& hi, bf16x8& 
     const __bf16 h = (__bf16)x[j];
     hi[j] = h;
     lo[j] = (__bf16)(x[j] - (float)h);
+  }
+}
+
+// x -> hi + mid + lo, each bf16 (RNE), x == hi + mid + lo to 24 bits
+__device__ __forceinline__ void split8x3(const float (&x)[8], bf16x8& hi, bf16x8& mid, bf16x8& lo) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const __bf16 h = (__bf16)x[j];
+    const float r1 = x[j] - (float)h;
+    const __bf16 m = (__bf16)r1;
+    hi[j] = h;
+    mid[j] = m;
+    lo[j] = (__bf16)(r1 - (float)m);
   }
 }
 
@@ -118,8 +137,10 @@ __device__ __forceinline__ void layer(Pipe& p, const f32x4 (&in)[NIN], const flo
     constexpr int o = decltype(ob)::value;
     out[o] = *(const f32x4*)(bptr + o * 16);
   });
-  if constexpr (prog_b16<B16>(E)) {
-    // bf16x3: per k-step of 32 one hi/lo split of the B fragment, per out-block 2 A reads, 3 MFMAs
+  if constexpr (prog_mode<B16>(E) != 0) {
+    // bf16x3 (mode 1): per k-step of 32 one hi/lo split of the B fragment, per out-block 2 A reads,
+    // 3 MFMAs; bf16x6 (mode 2): hi/mid/lo, 3 A reads, 6 MFMAs (smallest terms first)
+    constexpr bool X6 = prog_mode<B16>(E) == 2;
     constexpr int KS = ks32(L);
     constexpr int K0 = D.seg[0].ksteps / 8;
     static_for<0, KS>([&](auto t) {
@@ -142,16 +163,33 @@ __device__ __forceinline__ void layer(Pipe& p, const f32x4 (&in)[NIN], const flo
           x[4 + j] = in[2 * ts + 1][j];
         }
       }
-      bf16x8 bh, bl;
-      split8(x, bh, bl);
-      static_for<0, D.ob>([&](auto ob) {
-        constexpr int o = decltype(ob)::value;
-        const bf16x8 ah = *(const bf16x8*)(buf + o * 2048 + lane * 16);
-        const bf16x8 al = *(const bf16x8*)(buf + o * 2048 + 1024 + lane * 16);
-        out[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, out[o], 0, 0, 0);
-        out[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, out[o], 0, 0, 0);
-        out[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, out[o], 0, 0, 0);
-      });
+      if constexpr (X6) {
+        bf16x8 bh, bm, bl;
+        split8x3(x, bh, bm, bl);
+        static_for<0, D.ob>([&](auto ob) {
+          constexpr int o = decltype(ob)::value;
+          const bf16x8 ah = *(const bf16x8*)(buf + o * 3072 + lane * 16);
+          const bf16x8 am = *(const bf16x8*)(buf + o * 3072 + 1024 + lane * 16);
+          const bf16x8 al = *(const bf16x8*)(buf + o * 3072 + 2048 + lane * 16);
+          out[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, out[o], 0, 0, 0);
+          out[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, out[o], 0, 0, 0);
+          out[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bm, out[o], 0, 0, 0);
+          out[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bm, out[o], 0, 0, 0);
+          out[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bh, out[o], 0, 0, 0);
+          out[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, out[o], 0, 0, 0);
+        });
+      } else {
+        bf16x8 bh, bl;
+        split8(x, bh, bl);
+        static_for<0, D.ob>([&](auto ob) {
+          constexpr int o = decltype(ob)::value;
+          const bf16x8 ah = *(const bf16x8*)(buf + o * 2048 + lane * 16);
+          const bf16x8 al = *(const bf16x8*)(buf + o * 2048 + 1024 + lane * 16);
+          out[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, out[o], 0, 0, 0);
+          out[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, out[o], 0, 0, 0);
+          out[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, out[o], 0, 0, 0);
+        });
+      }
     });
   } else {
     constexpr int C = layer_chunks(L);
@@ -362,14 +400,14 @@ __device__ __forceinline__ void mlp_body(const MlpArgs& a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4;
   const int pl = lane & 15;
-  float* sA = (float*)(smem + LDS_A_OFF);
+  float* sA = (float*)(smem + 2 * mlp_slice_max<B16>());
   for (int i = tid; i < 384; i += 512) sA[i] = a.A[i];
 
   const int n = *a.n_kept;
   const int ntiles = (n + 127) / 128;
   if ((int)blockIdx.x >= ntiles) return;  // uniform per workgroup, before any LDS-DMA
 
-  Pipe p{smem, a.wimg, 0, wave, lane, a.pose_woff};
+  Pipe p{smem, mlp_slice_max<B16>(), a.wimg, 0, wave, lane, a.pose_woff};
   p.stage(prog_slice_off<B16>(0, 0) + a.pose_woff, prog_slice_kb<B16>(0), 0);
 
   const float* fold = a.fold;
@@ -391,7 +429,8 @@ __device__ __forceinline__ void mlp_body(const MlpArgs& a) {
     f32x4 A[17], B[17], fc[2], init[2], bw[2];
 
     // ---- pose space: pbw lookup, BW MLP (latent_index + 1), softmax, LBS
-    embed<16>(pose, g, 10, emb);
+    if constexpr (B16) embed_b<2>(pose, g, 10, emb);
+    else embed<16>(pose, g, 10, emb);
     lookup24(a.pbw32, pose, a.pbounds, a.pX, a.pY, a.pZ, g, init);
 #pragma unroll
     for (int s8 = 0; s8 < 8; ++s8) vemb[s8] = 0.f;

@@ -103,6 +103,38 @@ __global__ void k_pack_b16(PackArgs a) {
   *(uint4*)(base + 1024 + lane * 16) = vl;
 }
 
+// bf16x6 image: one thread per (x6 layer, k-step, out-block, lane) writes hi, mid, lo fragments
+__global__ void k_pack_x6(PackArgs a) {
+  const int u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= x6_bytes() / 48) return;
+  const int byte = u * 48;
+  int X = 0;
+  while (X + 1 < ANR_X6_LAYERS && byte >= x6_layer_offset(X + 1)) ++X;
+  const LayerDesc d = layer_desc_all(x6_layer(X));
+  const int local = (byte - x6_layer_offset(X)) / 48;
+  const int lane = local & 63;
+  const int so = local >> 6;
+  const int ob = so % d.ob, t = so / d.ob;
+  const int row = ob * 16 + (lane & 15), h = lane >> 4;
+  unsigned short q[3][8];
+  for (int j = 0; j < 8; ++j) {
+    const int col = b16_col(d, t, h, j);
+    float v = 0.0f;
+    if (col >= 0 && row < d.nout && a.t[d.tensor_w] != nullptr) v = a.t[d.tensor_w][(size_t)row * d.in_ch + col];
+    q[0][j] = bf16_rne(v);
+    const float r1 = v - __uint_as_float((uint32_t)q[0][j] << 16);
+    q[1][j] = bf16_rne(r1);
+    q[2][j] = bf16_rne(r1 - __uint_as_float((uint32_t)q[1][j] << 16));
+  }
+  unsigned char* base = a.out + x6_base() + x6_layer_offset(X) + (size_t)so * 3072;
+  for (int k = 0; k < 3; ++k) {
+    uint4 v;
+    v.x = q[k][0] | ((uint32_t)q[k][1] << 16); v.y = q[k][2] | ((uint32_t)q[k][3] << 16);
+    v.z = q[k][4] | ((uint32_t)q[k][5] << 16); v.w = q[k][6] | ((uint32_t)q[k][7] << 16);
+    *(uint4*)(base + k * 1024 + lane * 16) = v;
+  }
+}
+
 // grid: blocks [0, nvox_blocks) repack volumes; block 'fold' computes the five folded biases
 __global__ __launch_bounds__(256) void k_prep(PrepArgs a) {
   const int nvb = (a.np + a.nt + 7) / 8;  // 8 voxels (x 32 channels) per block

@@ -7,9 +7,15 @@ step    = one full-frame render of 512x512 box rays x 64 samples (262,142 rays h
 N GPUs  = one process per GPU (torch.distributed.run), each rendering its own frame (rays seed
           2 + rank): frames are independent, so no collective on the data path ("scaling": "weak");
           the timed region is bracketed by barriers and the max over ranks is reported.
-roofline: k_mlp (fused deform + NeRF network, fp32 MFMA) is the dominant kernel; its per-launch
-          time is measured with hipEvents on the render stream (anr_profile_*), algorithmic work =
-          kept samples x 2,312,192 FLOP; peak = fp32 MFMA 157.3 TFLOP/s.
+precision: --render-precision bf16x3 (default) runs the fused network kernel k_mlp_b16 — the pose
+          BW MLP as a 3-way (x6) and the T-pose BW MLP + NeRF as a 2-way (x3) hi/lo split onto bf16
+          MFMA with fp32 accumulation, outputs held to the same 1e-4 fp32 tolerance as the exact path
+          by the parity tests; the exact-fp32 kernel k_mlp is timed in the same run ("fp32_exact").
+roofline: the fused network kernel is the dominant kernel; its per-launch time is measured with
+          hipEvents on the render stream (anr_profile_*); achieved = executed MFMA FLOP per kept
+          sample (bf16x3: 2*(6*497,152 + 3*(497,152 + 658,944)); fp32: 3,306,496) x kept / time,
+          peak = the dense MFMA peak of the operand type (bf16 2.5 PF, fp32 157.3 TF);
+          achieved_credited uses SURVEY.md §8(d)'s 2,312,192 FLOP per kept sample.
 cpu_baseline: the oracle (op-for-op PyTorch-CPU restatement of the reference) on the first 16
           chunks (32,768 rays) of the same frame, rank 0 at N=1 only.
 """
@@ -24,6 +30,7 @@ import torch.distributed as dist
 
 FLOP_PER_KEPT = 2_312_192          # render credit (BW pose + NeRF, latent folded)
 FLOP_PER_KEPT_EXECUTED = 3_306_496  # + T-pose BW MLP (tbw rows are part of the render outputs)
+MAC_BW, MAC_NERF = 497_152, 658_944  # per kept sample, latent folded
 PEAK_FP32_MFMA_TFLOPS = 157.3      # MI355X_MICROARCH.md, Peak FP32 (matrix)
 PEAK_BF16_MFMA_TFLOPS = 2500.0     # MI355X_MICROARCH.md, BF16 dense (no sparsity)
 METRIC = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), 'BASELINE.json')))['metric']
@@ -41,7 +48,8 @@ def parse():
                     help='render: config 2 (headline); train: config 3/4 training step (1024 rays/GPU); '
                          'sdf: config 5 sdf_pdf full-frame render')
     ap.add_argument('--sdf-cpu-rays', type=int, default=2048)
-    ap.add_argument('--render-precision', choices=('fp32', 'bf16x3'), default='fp32',
+    ap.add_argument('--no-exact', action='store_true', help='skip timing the other render precision')
+    ap.add_argument('--render-precision', choices=('fp32', 'bf16x3'), default='bf16x3',
                     help='fp32: exact fp32 MFMA; bf16x3: T-pose BW MLP + NeRF as hi/lo-split bf16 MFMA '
                          '(outputs within the 1e-4 fp32 tolerance, tests/test_gpu_render.py)')
     ap.add_argument('--train-rays', type=int, default=1024)
@@ -81,61 +89,84 @@ def main():
     network.load_numpy_state(net, sd)
     net = net.to(dev)
     net.train()  # run.py evaluates in train() mode with perturb = 0
-    cfg = config.defaults()
-    cfg.perturb = 0
-    cfg.render_precision = args.render_precision
-    renderer = Renderer(net, cfg)
     lib = _lib.load()
 
-    for _ in range(args.warmup):
-        out = renderer.render_device(batch)
-    torch.cuda.synchronize()
-    lib.anr_profile_enable(1)
-    lib.anr_profile_read(None, None)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        out = renderer.render_device(batch)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    mlp_ms = _lib.ctypes.c_double(0)
-    launches = _lib.ctypes.c_int(0)
-    _lib.check(lib.anr_profile_read(_lib.ctypes.byref(mlp_ms), _lib.ctypes.byref(launches)), 'anr_profile_read')
-    lib.anr_profile_enable(0)
-    n_kept, m_rows = renderer.last_counts
+    def timed(precision):
+        cfg = config.defaults()
+        cfg.perturb = 0
+        cfg.render_precision = precision
+        renderer = Renderer(net, cfg)
+        for _ in range(args.warmup):
+            out = renderer.render_device(batch)
+        torch.cuda.synchronize()
+        lib.anr_profile_enable(1)
+        lib.anr_profile_read(None, None)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            out = renderer.render_device(batch)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        dt = time.perf_counter() - t0
+        mlp_ms = _lib.ctypes.c_double(0)
+        launches = _lib.ctypes.c_int(0)
+        _lib.check(lib.anr_profile_read(_lib.ctypes.byref(mlp_ms), _lib.ctypes.byref(launches)), 'anr_profile_read')
+        lib.anr_profile_enable(0)
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return out, float(t.item()), mlp_ms.value / max(1, launches.value), renderer.last_counts
 
-    t = torch.tensor([dt], device=dev, dtype=torch.float64)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    dt_max = float(t.item())
+    others = [p for p in ('fp32', 'bf16x3') if p != args.render_precision]
+    side = {}
+    for prec in others if not args.no_exact else []:
+        o2, dt2, kms2, _ = timed(prec)
+        side[prec] = {'value': R * 64 * args.steps * world / dt2, 'ms_per_step': dt2 / args.steps * 1e3,
+                      'kernel_ms': kms2}
+        del o2
+    out, dt_max, kernel_ms, (n_kept, m_rows) = timed(args.render_precision)
     samples_per_rank = R * 64 * args.steps
     value = samples_per_rank * world / dt_max
-    kernel_ms = mlp_ms.value / max(1, launches.value)
-    achieved = n_kept * FLOP_PER_KEPT / (kernel_ms * 1e-3) / 1e12
+    split = args.render_precision == 'bf16x3'
+    if split:
+        # executed bf16 MFMA work per kept sample: pose BW x6 + (T-pose BW + NeRF) x3 products
+        flop_exec = 2 * (6 * MAC_BW + 3 * (MAC_BW + MAC_NERF))
+        peak = PEAK_BF16_MFMA_TFLOPS
+        dtype = 'bf16 MFMA operands (hi/lo split: x6 pose BW, x3 T-pose BW + NeRF), fp32 accumulate'
+    else:
+        flop_exec = FLOP_PER_KEPT_EXECUTED
+        peak = PEAK_FP32_MFMA_TFLOPS
+        dtype = 'fp32'
+    achieved = n_kept * flop_exec / (kernel_ms * 1e-3) / 1e12
 
     result = {
         'metric': METRIC, 'value': value, 'unit': 'ray-samples/s', 'n_gpus': world, 'steps': args.steps,
         'warmup': args.warmup, 'ms_per_step': dt_max / args.steps * 1e3, 'higher_is_better': True,
-        'scaling': 'weak', 'vs_baseline': None, 'dtype': 'fp32', 'data': 'synthetic',
-        'config': {'workload': 'aninerf_s9p full 512x512 render (config 2), eval perturb=0, fp32',
+        'scaling': 'weak', 'vs_baseline': None, 'dtype': dtype, 'data': 'synthetic',
+        'config': {'workload': 'aninerf_s9p full 512x512 render (config 2), eval perturb=0; outputs held to the '
+                               'fp32 tolerance (1e-4, tests/test_gpu_render.py) in both render precisions',
+                   'render_precision': args.render_precision,
                    'rays_per_gpu': R, 'samples_per_ray': 64, 'chunk': 2048,
                    'kept_fraction': n_kept / (R * 64), 'alpha_ind_rows': m_rows,
                    'parallelism': f'replicas{world} (one frame per GPU)'},
-        'roofline': {'bound': 'mfma', 'kernel': 'k_mlp', 'achieved': achieved, 'peak': PEAK_FP32_MFMA_TFLOPS,
-                     'unit': 'TFLOP/s', 'frac': achieved / PEAK_FP32_MFMA_TFLOPS, 'traffic': None,
-                     'kernel_ms': kernel_ms, 'flop_per_kept': FLOP_PER_KEPT,
-                     'achieved_executed': n_kept * FLOP_PER_KEPT_EXECUTED / (kernel_ms * 1e-3) / 1e12},
+        'roofline': {'bound': 'mfma', 'kernel': 'k_mlp_b16' if split else 'k_mlp', 'achieved': achieved,
+                     'peak': peak, 'unit': 'TFLOP/s', 'frac': achieved / peak, 'traffic': None,
+                     'kernel_ms': kernel_ms, 'flop_per_kept_executed': flop_exec,
+                     'flop_per_kept_credited': FLOP_PER_KEPT,
+                     'achieved_credited': n_kept * FLOP_PER_KEPT / (kernel_ms * 1e-3) / 1e12},
     }
+    for prec, v in side.items():
+        result['fp32_exact' if prec == 'fp32' else 'bf16x3_split'] = v
 
     pmc = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'profiles', 'pmc_latest.json')
     if os.path.exists(pmc):
         t = json.load(open(pmc))
-        result['roofline']['traffic'] = t['bytes_per_launch']
-        result['roofline']['traffic_source'] = t['source'] + '; ' + t['correction']
+        if t.get('kernel', 'k_mlp') == result['roofline']['kernel']:
+            result['roofline']['traffic'] = t['bytes_per_launch']
+            result['roofline']['traffic_source'] = t['source'] + '; ' + t['correction']
     if rank == 0 and world == 1 and not args.no_cpu:
         result['cpu_baseline'], result['psnr_vs_fp32_oracle'] = cpu_baseline(sd, b, out, args.cpu_rays)
     if rank == 0:

@@ -42,7 +42,9 @@ def test_version_and_sizes(lib):
     ks_ob = [(2, 16), (8, 16), (8, 16), (8, 16), (8, 16), (10, 16), (8, 16), (8, 16), (8, 2),
              (2, 16), (8, 16), (8, 16), (8, 16), (8, 16), (10, 16), (8, 16), (8, 16), (8, 17), (8, 16), (9, 8), (4, 1)]
     b16 = sum(k * o for k, o in ks_ob) * 2048
-    assert lib.anr_params_packed_bytes() == (fp32 + 255) // 256 * 256 + b16
+    x6 = 2 * sum(k * o for k, o in ks_ob[:9]) * 3072  # pose-pass bf16x6 image (+ novel-pose copy)
+    base16 = (fp32 + 255) // 256 * 256
+    assert lib.anr_params_packed_bytes() == (base16 + b16 + 255) // 256 * 256 + x6
 
 
 def test_workspace_grows_with_rays(lib):
