@@ -152,14 +152,17 @@ def test_full_frame_properties(renderer, dev):
         assert err <= TOL, (k, err)
 
 
-def test_novel_pose_render_matches_reference(dev):
+@pytest.mark.parametrize('precision', ['fp32', 'bf16x3'])
+def test_novel_pose_render_matches_reference(dev, precision):
     """A19: cfg.test_novel_pose renders with novel_pose_bw + bw_latent_index (golden G5)."""
     from animatable_nerf_amd.renderer import Renderer
     from ._common import make_net_novel, novel_batch_np, novel_cfg
     g = golden('g5_novel_pose')
     net = make_net_novel(dev)
     net.train()
-    r = Renderer(net, novel_cfg())
+    ncfg = novel_cfg()
+    ncfg.render_precision = precision
+    r = Renderer(net, ncfg)
     ret = r.render_device(to_torch(novel_batch_np(), dev))
     ret = {k: v.cpu() for k, v in ret.items()}
     assert torch.equal(_keep(ret['raw']), torch.from_numpy(g['out_raw'][0, :, :3].sum(-1) != 0))
@@ -170,6 +173,7 @@ def test_novel_pose_render_matches_reference(dev):
     # the same network without the flag renders the training-pose path (different weights)
     cfg = novel_cfg()
     cfg.test_novel_pose = False
+    cfg.render_precision = precision
     r2 = Renderer(net, cfg)
     ret2 = r2.render_device(to_torch(novel_batch_np(), dev))
     assert (ret2['rgb_map'].cpu() - ret['rgb_map']).abs().max().item() > 1e-3
