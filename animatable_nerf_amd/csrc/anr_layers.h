@@ -191,11 +191,15 @@ __host__ __device__ inline int b16_col(const LayerDesc& d, int t, int h, int j) 
 
 __host__ __device__ constexpr int packed_bytes_all() { return x6_base() + x6_bytes(); }
 
-// LDS of the fused kernel: two staging buffers of the largest slice + the 24 joint transforms
-// (fp32: 8 k-steps x 5 chunks x 1 KiB; bf16 kernel: a bf16x6 k-step of 16 out-blocks x 3 KiB)
+// LDS of the fused kernel: a ring of staging buffers of the largest slice + the 24 joint transforms.
+// fp32 kernel: 2 x (8 k-steps x 5 chunks x 1 KiB). bf16 kernel: 4 x 34 KiB (a bf16x3 k-step of 17
+// out-blocks x 2 KiB; bf16x6 k-steps are staged as groups of <= 8 out-blocks x 3 KiB = 24 KiB), so
+// three slices are in flight while one is consumed.
 template <bool B16>
-__host__ __device__ constexpr int mlp_slice_max() { return B16 ? 16 * 3072 : 8 * 5 * 1024; }
+__host__ __device__ constexpr int mlp_slice_max() { return B16 ? 17 * 2048 : 8 * 5 * 1024; }
 template <bool B16>
-__host__ __device__ constexpr int mlp_lds_bytes() { return 2 * mlp_slice_max<B16>() + 24 * 16 * 4; }
+__host__ __device__ constexpr int mlp_nbuf() { return B16 ? 4 : 2; }
+template <bool B16>
+__host__ __device__ constexpr int mlp_lds_bytes() { return mlp_nbuf<B16>() * mlp_slice_max<B16>() + 24 * 16 * 4; }
 
 }  // namespace anr

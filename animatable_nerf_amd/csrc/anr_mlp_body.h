@@ -44,59 +44,123 @@ __host__ __device__ constexpr int prog_layer(int e) { return e < 9 ? e : e - 9; 
 __host__ __device__ constexpr bool prog_pose(int e) { return e < 9; }
 template <bool B16>
 __host__ __device__ constexpr int prog_mode(int e) { return B16 ? (e < 9 ? 2 : 1) : 0; }
+// Slices = the staging unit: mode 0 8 fp32 k-steps; mode 1 one 32-input k-step (OB x 2 KiB);
+// mode 2 one 32-input k-step of a group of <= 8 out-blocks (x 3 KiB).
+__host__ __device__ constexpr int prog_nobg(int e) { return (layer_desc_all(prog_layer(e)).ob + 7) / 8; }
 template <bool B16>
 __host__ __device__ constexpr int prog_slices(int e) {
-  return prog_mode<B16>(e) ? ks32(prog_layer(e)) : layer_ksteps(prog_layer(e)) / ANR_KSLICE;
+  return prog_mode<B16>(e) == 2   ? ks32(prog_layer(e)) * prog_nobg(e)
+         : prog_mode<B16>(e) == 1 ? ks32(prog_layer(e))
+                                  : layer_ksteps(prog_layer(e)) / ANR_KSLICE;
+}
+__host__ __device__ constexpr int x6_group_obs(int e, int gidx) {
+  return layer_desc_all(prog_layer(e)).ob - 8 * gidx < 8 ? layer_desc_all(prog_layer(e)).ob - 8 * gidx : 8;
 }
 template <bool B16>
-__host__ __device__ constexpr int prog_slice_kb(int e) {
-  return prog_mode<B16>(e) == 2   ? layer_desc_all(prog_layer(e)).ob * 3
+__host__ __device__ constexpr int prog_slice_kb(int e, int q) {
+  return prog_mode<B16>(e) == 2   ? x6_group_obs(e, q % prog_nobg(e)) * 3
          : prog_mode<B16>(e) == 1 ? layer_desc_all(prog_layer(e)).ob * 2
                                   : layer_chunks(prog_layer(e)) * ANR_KSLICE;
 }
 template <bool B16>
 __host__ __device__ constexpr int prog_slice_off(int e, int q) {
   return prog_mode<B16>(e) == 2
-             ? x6_base() + x6_layer_offset(prog_layer(e)) + q * layer_desc_all(prog_layer(e)).ob * 3072
+             ? x6_base() + x6_layer_offset(prog_layer(e)) +
+                   ((q / prog_nobg(e)) * layer_desc_all(prog_layer(e)).ob + 8 * (q % prog_nobg(e))) * 3072
          : prog_mode<B16>(e) == 1
              ? b16_base() + b16_layer_offset(prog_layer(e)) + q * layer_desc_all(prog_layer(e)).ob * 2048
              : layer_offset(prog_layer(e)) + q * layer_chunks(prog_layer(e)) * ANR_KSLICE * 1024;
+}
+// loads per wave for a slice (every wave issues the same count, see Pipe::stage)
+template <bool B16>
+__host__ __device__ constexpr int prog_slice_loads(int e, int q) { return (prog_slice_kb<B16>(e, q) + 7) / 8; }
+// the slice d steps after (e, q) in the cyclic program, packed as e * 1024 + q
+template <bool B16>
+__host__ __device__ constexpr int prog_advance(int e, int q, int d) {
+  for (int i = 0; i < d; ++i) {
+    if (q + 1 < prog_slices<B16>(e)) {
+      ++q;
+    } else {
+      q = 0;
+      e = (e + 1) % ANR_PROG_LEN;
+    }
+  }
+  return e * 1024 + q;
+}
+// loads this wave issued after slice (e, q) that may still be in flight when (e, q) is consumed
+template <bool B16>
+__host__ __device__ constexpr int prog_later_loads(int e, int q) {
+  int n = 0;
+  for (int d = 1; d <= mlp_nbuf<B16>() - 2; ++d) {
+    const int eq = prog_advance<B16>(e, q, d);
+    n += prog_slice_loads<B16>(eq / 1024, eq % 1024);
+  }
+  return n;
+}
+
+// s_waitcnt with only vmcnt constrained (gfx9 encoding: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt_hi[15:14])
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt out of range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
 }
 
 struct Pipe {
   unsigned char* lds;
   int smax;  // bytes per staging buffer
+  int nbuf;  // ring size
   const unsigned char* wimg;
-  int cur;
+  int cur;   // ring slot of the slice consumed next
   int wave;
   int lane;
   int pose_woff;  // added to slices of the pose-space BW pass (novel_pose_bw weights)
 
-  // issue the HBM/L2 -> LDS copy of `kb` KiB at byte `off` of the packed image into buffer `buf`
-  __device__ __forceinline__ void stage(int off, int kb, int buf) {
+  // issue the HBM/L2 -> LDS copy of `kb` KiB at byte `off` of the packed image into ring slot `buf`;
+  // every wave issues exactly `loads` 1-KiB pieces (pieces past the end repeat the last one: same
+  // bytes to the same place), so the per-wave vmcnt bookkeeping is a compile-time constant
+  __device__ __forceinline__ void stage(int off, int kb, int loads, int buf) {
     unsigned char* dst = lds + buf * smax;
     // launder the base so the per-slice addresses are formed here, not hoisted out of the tile
     // loop (hundreds of loop-invariant 64-bit addresses otherwise spill)
     const unsigned char* w = wimg;
     asm volatile("" : "+s"(w));
-    for (int piece = wave; piece < kb; piece += 8)
+    for (int i = 0; i < loads; ++i) {
+      int piece = wave + 8 * i;
+      piece = piece < kb ? piece : kb - 1;
       __builtin_amdgcn_global_load_lds((const void*)(w + off + piece * 1024 + lane * 16),
                                        (lds_void*)(dst + piece * 1024), 16, 0, 0);
+    }
   }
 
-  // Enter slice Q of program entry E: wait for it, prefetch the slice that follows.
+  template <bool B16, int E, int Q>
+  __device__ __forceinline__ void stage_slice(int buf) {
+    constexpr int off = prog_slice_off<B16>(E, Q);
+    stage(off + (prog_pose(E) ? pose_woff : 0), prog_slice_kb<B16>(E, Q), prog_slice_loads<B16>(E, Q), buf);
+  }
+
+  // prologue: slices 0 .. nbuf-2 of the program
+  template <bool B16>
+  __device__ __forceinline__ void start() {
+    static_for<0, mlp_nbuf<B16>() - 1>([&](auto d) {
+      constexpr int eq = prog_advance<B16>(0, 0, decltype(d)::value);
+      stage_slice<B16, eq / 1024, eq % 1024>(decltype(d)::value);
+    });
+    cur = 0;
+  }
+
+  // Enter slice Q of program entry E: wait for it (its own loads; the barrier covers the other
+  // waves'), then refill the slot freed by the previous slice with the slice nbuf-1 ahead.
   template <bool B16, int E, int Q>
   __device__ __forceinline__ const unsigned char* next() {
-    constexpr int NS = prog_slices<B16>(E);
-    constexpr int nE = (Q + 1 < NS) ? E : (E + 1) % ANR_PROG_LEN;
-    constexpr int nQ = (Q + 1 < NS) ? Q + 1 : 0;
-    constexpr int noff = prog_slice_off<B16>(nE, nQ);
-    constexpr int nkb = prog_slice_kb<B16>(nE);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    constexpr int NB = mlp_nbuf<B16>();
+    constexpr int eq = prog_advance<B16>(E, Q, NB - 1);
+    wait_vmcnt<prog_later_loads<B16>(E, Q)>();
     __syncthreads();
-    stage(noff + (prog_pose(nE) ? pose_woff : 0), nkb, cur ^ 1);
+    int slot = cur + NB - 1;
+    slot = slot >= NB ? slot - NB : slot;
+    stage_slice<B16, eq / 1024, eq % 1024>(slot);
     const unsigned char* r = lds + cur * smax;
-    cur ^= 1;
+    cur = cur + 1 >= NB ? 0 : cur + 1;
     return r;
   }
 };
@@ -145,7 +209,8 @@ __device__ __forceinline__ void layer(Pipe& p, const f32x4 (&in)[NIN], const flo
     constexpr int K0 = D.seg[0].ksteps / 8;
     static_for<0, KS>([&](auto t) {
       constexpr int tt = decltype(t)::value;
-      const unsigned char* buf = p.template next<B16, E, tt>();
+      const unsigned char* buf = nullptr;
+      if constexpr (!X6) buf = p.template next<B16, E, tt>();
       constexpr int seg = tt < K0 ? 0 : 1;
       constexpr int ts = tt < K0 ? tt : tt - K0;
       constexpr int kind = D.seg[seg].kind;
@@ -166,11 +231,13 @@ __device__ __forceinline__ void layer(Pipe& p, const f32x4 (&in)[NIN], const flo
       if constexpr (X6) {
         bf16x8 bh, bm, bl;
         split8x3(x, bh, bm, bl);
+        constexpr int NOBG = prog_nobg(E);
         static_for<0, D.ob>([&](auto ob) {
           constexpr int o = decltype(ob)::value;
-          const bf16x8 ah = *(const bf16x8*)(buf + o * 3072 + lane * 16);
-          const bf16x8 am = *(const bf16x8*)(buf + o * 3072 + 1024 + lane * 16);
-          const bf16x8 al = *(const bf16x8*)(buf + o * 3072 + 2048 + lane * 16);
+          if constexpr (o % 8 == 0) buf = p.template next<B16, E, tt * NOBG + o / 8>();
+          const bf16x8 ah = *(const bf16x8*)(buf + (o % 8) * 3072 + lane * 16);
+          const bf16x8 am = *(const bf16x8*)(buf + (o % 8) * 3072 + 1024 + lane * 16);
+          const bf16x8 al = *(const bf16x8*)(buf + (o % 8) * 3072 + 2048 + lane * 16);
           out[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, out[o], 0, 0, 0);
           out[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, out[o], 0, 0, 0);
           out[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bm, out[o], 0, 0, 0);
@@ -400,15 +467,15 @@ __device__ __forceinline__ void mlp_body(const MlpArgs& a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4;
   const int pl = lane & 15;
-  float* sA = (float*)(smem + 2 * mlp_slice_max<B16>());
+  float* sA = (float*)(smem + mlp_nbuf<B16>() * mlp_slice_max<B16>());
   for (int i = tid; i < 384; i += 512) sA[i] = a.A[i];
 
   const int n = *a.n_kept;
   const int ntiles = (n + 127) / 128;
   if ((int)blockIdx.x >= ntiles) return;  // uniform per workgroup, before any LDS-DMA
 
-  Pipe p{smem, mlp_slice_max<B16>(), a.wimg, 0, wave, lane, a.pose_woff};
-  p.stage(prog_slice_off<B16>(0, 0) + a.pose_woff, prog_slice_kb<B16>(0), 0);
+  Pipe p{smem, mlp_slice_max<B16>(), mlp_nbuf<B16>(), a.wimg, 0, wave, lane, a.pose_woff};
+  p.template start<B16>();
 
   const float* fold = a.fold;
   float tb_lo[3], tb_hi[3];
