@@ -19,7 +19,7 @@ NUM_SDF_TENSORS = 63
 EXPORTS = ('anr_near_far', 'anr_params_packed_bytes', 'anr_params_pack', 'anr_render_workspace_bytes',
            'anr_render_fwd', 'anr_render_counts', 'anr_render_bw_rows', 'anr_profile_enable', 'anr_profile_read',
            'anr_train_workspace_bytes', 'anr_train_fwd', 'anr_train_bwd', 'anr_train_step', 'anr_adam',
-           'anr_sdf_render_workspace_bytes', 'anr_sdf_render_fwd', 'anr_sdf_render_counts', 'anr_sdf_render_rows',
+           'anr_camera_rays_workspace_bytes', 'anr_camera_rays', 'anr_sdf_render_workspace_bytes', 'anr_sdf_render_fwd', 'anr_sdf_render_counts', 'anr_sdf_render_rows',
            'anr_last_error', 'anr_version')
 
 c_float_p = ctypes.c_void_p
@@ -108,6 +108,11 @@ def load():
     lib.anr_sdf_render_counts.restype = P
     lib.anr_sdf_render_counts.argtypes = [P, ctypes.c_int, ctypes.POINTER(RenderOpts)]
     lib.anr_sdf_render_rows.argtypes = [P, ctypes.c_int, ctypes.POINTER(RenderOpts), P, P, P, P, P]
+    lib.anr_camera_rays_workspace_bytes.restype = ctypes.c_size_t
+    lib.anr_camera_rays_workspace_bytes.argtypes = [ctypes.c_int, ctypes.c_int]
+    D = ctypes.POINTER(ctypes.c_double)
+    lib.anr_camera_rays.argtypes = [ctypes.c_int, ctypes.c_int, D, D, D, D, ctypes.c_int, P, P, P, P, P, P, P, P, P,
+                                    ctypes.c_size_t, P]
     lib.anr_profile_enable.argtypes = [ctypes.c_int]
     lib.anr_profile_read.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]
     lib.anr_last_error.restype = ctypes.c_char_p

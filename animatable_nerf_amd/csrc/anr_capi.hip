@@ -224,6 +224,43 @@ int anr_near_far(const float* ray_o, const float* ray_d, int n, const float* bou
   return check_launch("k_near_far");
 }
 
+size_t anr_camera_rays_workspace_bytes(int H, int W) {
+  if (H <= 0 || W <= 0) return 0;
+  const size_t P = (size_t)H * W;
+  return align256(P * 12) * 2 + align256(P * 4) * 2 + align256(((P + 255) / 256) * 4);
+}
+
+int anr_camera_rays(int H, int W, const double* Kinv, const double* R, const double* T, const double* origin, int fp64,
+                    const float* bounds, float* ray_o, float* ray_d, float* near_, float* far_, int32_t* coord,
+                    uint8_t* mask, int32_t* count, void* workspace, size_t ws_bytes, void* stream) {
+  if (H <= 0 || W <= 0 || !Kinv || !R || !T || !origin || !bounds || !ray_o || !ray_d || !near_ || !far_ || !coord ||
+      !mask || !count || !workspace)
+    return fail(ANR_E_ARG, "anr_camera_rays: bad arguments");
+  if ((long)H * W > (1L << 30)) return fail(ANR_E_ARG, "anr_camera_rays: image too large");
+  if (ws_bytes < anr_camera_rays_workspace_bytes(H, W)) return fail(ANR_E_WORKSPACE, "anr_camera_rays: workspace");
+  const size_t P = (size_t)H * W;
+  char* ws = (char*)workspace;
+  CamArgs a{};
+  a.H = H; a.W = W; a.fp64 = fp64 ? 1 : 0;
+  for (int k = 0; k < 9; ++k) { a.Kinv[k] = Kinv[k]; a.R[k] = R[k]; }
+  for (int k = 0; k < 3; ++k) { a.T[k] = T[k]; a.o[k] = origin[k]; }
+  a.bounds = bounds;
+  a.all_o = (float*)ws;
+  a.all_d = (float*)(ws + align256(P * 12));
+  a.all_near = (float*)(ws + 2 * align256(P * 12));
+  a.all_far = (float*)(ws + 2 * align256(P * 12) + align256(P * 4));
+  a.block_sum = (int*)(ws + 2 * align256(P * 12) + 2 * align256(P * 4));
+  a.mask = mask;
+  a.ray_o = ray_o; a.ray_d = ray_d; a.near_ = near_; a.far_ = far_; a.coord = coord;
+  hipStream_t s = (hipStream_t)stream;
+  const int nb = (int)((P + 255) / 256);
+  hipLaunchKernelGGL(k_cam_rays, dim3(nb), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_cam_count, dim3(nb), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, s, a.block_sum, nb, count);
+  hipLaunchKernelGGL(k_cam_scatter, dim3(nb), dim3(256), 0, s, a);
+  return check_launch("anr_camera_rays");
+}
+
 size_t anr_params_packed_bytes(void) { return (size_t)packed_bytes_all(); }
 
 int anr_params_pack(const anr_params* p, void* packed, void* stream) {

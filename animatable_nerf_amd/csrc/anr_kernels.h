@@ -37,6 +37,19 @@ struct AlphaArgs {
   int* out_row;          // (n') output row or -1
 };
 
+// (f) eval-split camera rays (get_rays_within_bounds)
+struct CamArgs {
+  int H, W, fp64;
+  double Kinv[9], R[9], T[3], o[3];
+  const float* bounds;            // (2,3) or NULL (rays only)
+  float *all_o, *all_d;           // (H*W, 3)
+  uint8_t* mask;                  // (H*W)
+  float *all_near, *all_far;      // (H*W)
+  int* block_sum;                 // (ceil(H*W/256))
+  float *ray_o, *ray_d, *near_, *far_;  // compacted hits
+  int* coord;                     // (n, 2) (row, col)
+};
+
 struct CompositeArgs {
   const float4* raw;
   const float *near_, *far_, *t_rand;
@@ -78,6 +91,9 @@ struct PrepArgs {
 };
 
 __global__ void k_near_far(const float*, const float*, int, const float*, uint8_t*, float*, float*);
+__global__ void k_cam_rays(CamArgs a);
+__global__ void k_cam_count(CamArgs a);
+__global__ void k_cam_scatter(CamArgs a);
 __global__ void k_frontend(FrontArgs a);
 __global__ void k_count(CompactArgs a);
 __global__ void k_scan_blocks(int* sums, int nb, int* total_out);

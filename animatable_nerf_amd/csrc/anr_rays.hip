@@ -19,18 +19,15 @@ namespace anr {
 // ------------------------------------------------------------------------------------------
 // A14 near/far, fp64, numpy operation order; eps 1e-6, padding 0.01; hit <=> exactly 2 planes.
 // ------------------------------------------------------------------------------------------
-__global__ void k_near_far(const float* __restrict__ ray_o, const float* __restrict__ ray_d, int n,
-                           const float* __restrict__ bounds, uint8_t* __restrict__ mask,
-                           float* __restrict__ near_, float* __restrict__ far_) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+__device__ __forceinline__ void near_far_one(const float ro[3], const float rd[3], const float* __restrict__ bounds,
+                                             uint8_t& hit_out, float& near_out, float& far_out) {
   double b[2][3];
   for (int c = 0; c < 3; ++c) {
     b[0][c] = (double)bounds[c] + (-0.01);
     b[1][c] = (double)bounds[3 + c] + 0.01;
   }
-  const double o[3] = {(double)ray_o[3 * i], (double)ray_o[3 * i + 1], (double)ray_o[3 * i + 2]};
-  const double d[3] = {(double)ray_d[3 * i], (double)ray_d[3 * i + 1], (double)ray_d[3 * i + 2]};
+  const double o[3] = {(double)ro[0], (double)ro[1], (double)ro[2]};
+  const double d[3] = {(double)rd[0], (double)rd[1], (double)rd[2]};
   const double eps = 1e-6;
   int hits = 0;
   double pin[2][3] = {{0, 0, 0}, {0, 0, 0}};
@@ -47,19 +44,99 @@ __global__ void k_near_far(const float* __restrict__ ray_o, const float* __restr
       ++hits;
     }
   }
-  const bool hit = hits == 2;
-  mask[i] = hit ? 1 : 0;
+  hit_out = hits == 2 ? 1 : 0;
   // np.linalg.norm(axis=1): sqrt((x0*x0 + x1*x1) + x2*x2); ray_d is float32 in the test split,
   // so |d| is evaluated in float32 and promoted at the division (if_nerf_data_utils.py:189-191)
-  const float df[3] = {ray_d[3 * i], ray_d[3 * i + 1], ray_d[3 * i + 2]};
-  const double nd = (double)sqrtf((df[0] * df[0] + df[1] * df[1]) + df[2] * df[2]);
+  const double nd = (double)sqrtf((rd[0] * rd[0] + rd[1] * rd[1]) + rd[2] * rd[2]);
   double dd[2];
   for (int h = 0; h < 2; ++h) {
     const double e0 = pin[h][0] - o[0], e1 = pin[h][1] - o[1], e2 = pin[h][2] - o[2];
     dd[h] = sqrt((e0 * e0 + e1 * e1) + e2 * e2) / nd;
   }
-  near_[i] = (float)fmin(dd[0], dd[1]);
-  far_[i] = (float)fmax(dd[0], dd[1]);
+  near_out = (float)fmin(dd[0], dd[1]);
+  far_out = (float)fmax(dd[0], dd[1]);
+}
+
+__global__ void k_near_far(const float* __restrict__ ray_o, const float* __restrict__ ray_d, int n,
+                           const float* __restrict__ bounds, uint8_t* __restrict__ mask,
+                           float* __restrict__ near_, float* __restrict__ far_) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float ro[3] = {ray_o[3 * i], ray_o[3 * i + 1], ray_o[3 * i + 2]};
+  const float rd[3] = {ray_d[3 * i], ray_d[3 * i + 1], ray_d[3 * i + 2]};
+  near_far_one(ro, rd, bounds, mask[i], near_[i], far_[i]);
+}
+
+// ------------------------------------------------------------------------------------------
+// (f) eval-split ray pipeline: get_rays (if_nerf_data_utils.py:64-89) per pixel + A14, then ordered
+// compaction of the hits (get_rays_within_bounds :310-339). Arithmetic follows what numpy's np.dot
+// does in the reference run: a sequential FMA chain for float64 cameras (dgemm kernel), separate
+// multiply/add for float32 ones; |d| as sqrt((x*x + y*y) + z*z). Kinv and the origin -R^T T are
+// computed by the caller with numpy exactly as the reference does.
+// ------------------------------------------------------------------------------------------
+__global__ void k_cam_rays(CamArgs a) {
+  const int pix = blockIdx.x * blockDim.x + threadIdx.x;
+  if (pix >= a.H * a.W) return;
+  const int r = pix / a.W, c = pix - r * a.W;
+  float d32[3];
+  if (a.fp64) {
+    const double xy[3] = {(double)c, (double)r, 1.0};
+    double pc[3], q[3], pw[3], d[3];
+    for (int j = 0; j < 3; ++j) pc[j] = fma(xy[2], a.Kinv[3 * j + 2], fma(xy[1], a.Kinv[3 * j + 1], xy[0] * a.Kinv[3 * j]));
+    for (int k = 0; k < 3; ++k) q[k] = pc[k] - a.T[k];
+    for (int j = 0; j < 3; ++j) pw[j] = fma(q[2], a.R[6 + j], fma(q[1], a.R[3 + j], q[0] * a.R[j]));
+    for (int k = 0; k < 3; ++k) d[k] = pw[k] - a.o[k];
+    const double n = sqrt((d[0] * d[0] + d[1] * d[1]) + d[2] * d[2]);
+    for (int k = 0; k < 3; ++k) d32[k] = (float)(d[k] / n);
+  } else {
+    const float xy[3] = {(float)c, (float)r, 1.0f};
+    float kinv[9], R[9], T[3], o[3], pc[3], q[3], pw[3], d[3];
+    for (int k = 0; k < 9; ++k) { kinv[k] = (float)a.Kinv[k]; R[k] = (float)a.R[k]; }
+    for (int k = 0; k < 3; ++k) { T[k] = (float)a.T[k]; o[k] = (float)a.o[k]; }
+    for (int j = 0; j < 3; ++j) pc[j] = (xy[0] * kinv[3 * j] + xy[1] * kinv[3 * j + 1]) + xy[2] * kinv[3 * j + 2];
+    for (int k = 0; k < 3; ++k) q[k] = pc[k] - T[k];
+    for (int j = 0; j < 3; ++j) pw[j] = (q[0] * R[j] + q[1] * R[3 + j]) + q[2] * R[6 + j];
+    for (int k = 0; k < 3; ++k) d[k] = pw[k] - o[k];
+    const float n = sqrtf((d[0] * d[0] + d[1] * d[1]) + d[2] * d[2]);
+    for (int k = 0; k < 3; ++k) d32[k] = d[k] / n;
+  }
+  const float o32[3] = {(float)a.o[0], (float)a.o[1], (float)a.o[2]};
+  for (int k = 0; k < 3; ++k) {
+    a.all_o[3 * (size_t)pix + k] = o32[k];
+    a.all_d[3 * (size_t)pix + k] = d32[k];
+  }
+  if (a.bounds) near_far_one(o32, d32, a.bounds, a.mask[pix], a.all_near[pix], a.all_far[pix]);
+}
+
+// ordered compaction of the hit pixels: per-256-pixel counts, k_scan_blocks, scatter
+__device__ __forceinline__ int block_excl_scan_256(int v, int* sh, int& total);
+
+__global__ __launch_bounds__(256) void k_cam_count(CamArgs a) {
+  __shared__ int sh[4];
+  const int pix = blockIdx.x * 256 + threadIdx.x;
+  const int v = pix < a.H * a.W ? (int)a.mask[pix] : 0;
+  int total;
+  block_excl_scan_256(v, sh, total);
+  if (threadIdx.x == 0) a.block_sum[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(256) void k_cam_scatter(CamArgs a) {
+  __shared__ int sh[4];
+  const int pix = blockIdx.x * 256 + threadIdx.x;
+  const int v = pix < a.H * a.W ? (int)a.mask[pix] : 0;
+  int total;
+  const int ex = block_excl_scan_256(v, sh, total);
+  if (v) {
+    const int pos = a.block_sum[blockIdx.x] + ex;
+    for (int k = 0; k < 3; ++k) {
+      a.ray_o[3 * (size_t)pos + k] = a.all_o[3 * (size_t)pix + k];
+      a.ray_d[3 * (size_t)pos + k] = a.all_d[3 * (size_t)pix + k];
+    }
+    a.near_[pos] = a.all_near[pix];
+    a.far_[pos] = a.all_far[pix];
+    a.coord[2 * (size_t)pos] = pix / a.W;
+    a.coord[2 * (size_t)pos + 1] = pix % a.W;
+  }
 }
 
 // ------------------------------------------------------------------------------------------

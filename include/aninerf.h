@@ -7,6 +7,7 @@
  *
  * Reference interfaces each entry point replaces (paths relative to the reference tree):
  *   anr_near_far            lib/utils/if_nerf/if_nerf_data_utils.py:156-196   get_near_far (A14)
+ *   anr_camera_rays         if_nerf_data_utils.py:64-89, 310-339  get_rays + get_rays_within_bounds
  *   anr_params_pack         lib/networks/bw_deform/tpose_nerf_network.py:11-38, 218-239
  *                           (state_dict -> the kernel's weight image; called when weights change)
  *   anr_render_fwd          lib/networks/renderer/tpose_renderer.py:159-186   Renderer.render (A1)
@@ -113,6 +114,18 @@ typedef struct anr_render_out {
  * (garbage where mask==0). */
 int anr_near_far(const float* ray_o, const float* ray_d, int n, const float* bounds,
                  uint8_t* mask, float* near_, float* far_, void* stream);
+
+/* ---- (f) eval-split ray pipeline: get_rays_within_bounds (if_nerf_data_utils.py:310-339) ------
+ * get_rays (:64-89) for every pixel of an H x W camera, the A14 box test, and the ordered list of
+ * the hit pixels (row-major, like np.argwhere). Kinv = np.linalg.inv(K) and origin = -R^T T are
+ * passed in as the reference computes them on the host (LAPACK / BLAS results); fp64 selects the
+ * float64 arithmetic of float64 camera annotations, else float32 (float32 cameras). Outputs
+ * (device, capacity H*W): ray_o/ray_d (n,3), near/far (n), coord (n,2) (row, col), mask (H*W);
+ * count (device int32) = n. */
+size_t anr_camera_rays_workspace_bytes(int H, int W);
+int anr_camera_rays(int H, int W, const double* Kinv, const double* R, const double* T, const double* origin, int fp64,
+                    const float* bounds, float* ray_o, float* ray_d, float* near_, float* far_, int32_t* coord,
+                    uint8_t* mask, int32_t* count, void* workspace, size_t ws_bytes, void* stream);
 
 /* ---- weights --------------------------------------------------------------------------- */
 size_t anr_params_packed_bytes(void);

@@ -436,8 +436,37 @@ def main_sdf():
     print('sdf_pdf goldens written')
 
 
+def main_rays():
+    """G8: the eval-split ray pipeline (get_rays + get_near_far + filtering =
+    get_rays_within_bounds, if_nerf_data_utils.py:64-89, 310-339) for a float64 camera (the dtype of
+    the datasets' annots) and a float32 one, on the synthetic subject's bounds."""
+    sys.path.insert(0, REPO)
+    from animatable_nerf_amd.synthetic import Scene
+    import_reference()
+    from lib.utils.if_nerf import if_nerf_data_utils as dutils
+    scene = Scene(vsize=0.05)
+    out = {}
+    for tag, dt in (('f64', np.float64), ('f32', np.float32)):
+        H, W = 120, 100
+        a = np.deg2rad(20.0)
+        K = np.array([[140.5, 0.0, 49.3], [0.0, 141.25, 61.7], [0.0, 0.0, 1.0]], dtype=dt)
+        R = np.array([[np.cos(a), 0.0, -np.sin(a)], [0.0, -1.0, 0.0], [-np.sin(a), 0.0, -np.cos(a)]], dtype=dt)
+        T = np.array([[0.05], [-0.02], [2.9]], dtype=dt)
+        ray_o, ray_d = dutils.get_rays(H, W, K, R, T)
+        ro, rd, near, far, mask = dutils.get_rays_within_bounds(H, W, K, R, T, scene.bounds)
+        out.update({f'{tag}_K': K, f'{tag}_R': R, f'{tag}_T': T, f'{tag}_H': H, f'{tag}_W': W,
+                    f'{tag}_all_o': ray_o, f'{tag}_all_d': ray_d, f'{tag}_Kinv': np.linalg.inv(K),
+                    f'{tag}_ray_o': ro, f'{tag}_ray_d': rd, f'{tag}_near': near, f'{tag}_far': far,
+                    f'{tag}_mask': mask})
+    out['bounds'] = scene.bounds
+    np.savez_compressed(os.path.join(OUT, 'g8_rays.npz'), **out)
+    print('ray goldens written')
+
+
 if __name__ == '__main__':
-    if len(sys.argv) > 1 and sys.argv[1] == '--novel':
+    if len(sys.argv) > 1 and sys.argv[1] == '--rays':
+        main_rays()
+    elif len(sys.argv) > 1 and sys.argv[1] == '--novel':
         main_novel()
     elif len(sys.argv) > 1 and sys.argv[1] == '--sdf':
         main_sdf()

@@ -159,3 +159,16 @@ def test_g5_novel_pose_bit_exact():
         ret = restate.render(P, to_torch(novel_batch_np()), novel_pose=True)
     for k in ('rgb_map', 'acc_map', 'depth_map', 'raw', 'pbw', 'tbw'):
         np.testing.assert_array_equal(ret[k].numpy(), g['out_' + k], err_msg=k)
+
+
+@pytest.mark.parametrize('tag', ['f64', 'f32'])
+def test_eval_ray_pipeline_bit_exact(tag):
+    """(f) get_rays / get_rays_within_bounds restated, vs the reference run (golden G8)."""
+    g = golden('g8_rays')
+    H, W = int(g[tag + '_H']), int(g[tag + '_W'])
+    o, d = restate.get_rays(H, W, g[tag + '_K'], g[tag + '_R'], g[tag + '_T'])
+    assert np.array_equal(o, g[tag + '_all_o']) and np.array_equal(d, g[tag + '_all_d'])
+    ro, rd, near, far, mask = restate.get_rays_within_bounds(H, W, g[tag + '_K'], g[tag + '_R'], g[tag + '_T'],
+                                                             g['bounds'])
+    for k, v in (('ray_o', ro), ('ray_d', rd), ('near', near), ('far', far), ('mask', mask)):
+        assert np.array_equal(v, g[tag + '_' + k]), k
