@@ -100,6 +100,15 @@ class FusedStep:
         self.t = 0
         self.loss3 = torch.zeros(4, device=dev)
 
+    def adam_state_dict(self):
+        """torch.optim.Adam-format state (one group per tensor, optimizer.py:12-27)."""
+        from .checkpoint import adam_state_dict
+        return adam_state_dict(self.net.core_tensors(), self.m, self.v, self.t, self.lr, self.betas, self.eps, self.wd)
+
+    def load_adam_state_dict(self, sd):
+        from .checkpoint import load_adam_state_dict
+        self.t, self.lr = load_adam_state_dict(sd, self.net.core_tensors(), self.m, self.v)
+
     def step(self, batch, t_rand=None, lr=None):
         r = self.renderer
         dev = self.flat.device
