@@ -74,12 +74,14 @@ __device__ __forceinline__ float tri_channel(const float* __restrict__ vol, int 
   return acc;
 }
 
-// (x - Th) @ R  (blend_utils.py:6-16), no contraction.
+// (x - Th) @ R  (blend_utils.py:6-16). torch's CPU matmul of a (1, n, 3) x (1, 3, 3) float32 product
+// with n >= 45 (every chunk: n = rays x 64) runs a BLAS kernel whose dot is the FMA chain
+// fma(d2, R2j, fma(d1, R1j, d0 * R0j)) (measured bit-exact; n < 45 takes a plain multiply-add path)
 __device__ __forceinline__ void world_to_pose(const float x[3], const float* R, const float* Th, float out[3]) {
 #pragma clang fp contract(off)
   const float d0 = x[0] - Th[0], d1 = x[1] - Th[1], d2 = x[2] - Th[2];
 #pragma unroll
-  for (int j = 0; j < 3; ++j) out[j] = (d0 * R[0 * 3 + j] + d1 * R[1 * 3 + j]) + d2 * R[2 * 3 + j];
+  for (int j = 0; j < 3; ++j) out[j] = fmaf(d2, R[2 * 3 + j], fmaf(d1, R[1 * 3 + j], d0 * R[0 * 3 + j]));
 }
 
 // Positional-encoding feature f of gamma(x) (embedder.py:5-54): [x, sin(2^0 x), cos(2^0 x), ...]

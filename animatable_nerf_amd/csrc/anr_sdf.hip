@@ -182,7 +182,7 @@ __global__ __launch_bounds__(256) void k_sdf_prep(SdfPointArgs a) {
   // world_dirs_to_pose_dirs: d @ R
   {
     const float* d = a.ray_d + 3 * ray;
-    for (int j = 0; j < 3; ++j) pd[j] = (d[0] * a.R[j] + d[1] * a.R[3 + j]) + d[2] * a.R[6 + j];
+    for (int j = 0; j < 3; ++j) pd[j] = fmaf(d[2], a.R[6 + j], fmaf(d[1], a.R[3 + j], d[0] * a.R[j]));  // torch matmul (n >= 45)
   }
   const uint4* rec = (const uint4*)(a.knn + (size_t)pid * 8);
   const uint4 r0 = rec[0], r1 = rec[1];

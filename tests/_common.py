@@ -127,3 +127,26 @@ def pdf_g7_rays():
     """The 4,608 G7 rays (oracle/gen_goldens.py main_sdf)."""
     g = golden('g7_sdf_chunks')
     return g['ray_o'], g['ray_d']
+
+
+def rotated_batch_np(n_rays=3000, seed=23, vsize=0.05):
+    """A frame with a non-trivial smpl->world transform (R = Rodrigues(0.3, -0.2, 0.5),
+    Th = (0.1, -0.05, 0.2)): world rays towards the world-space box, pbw/tbw in the pose frame."""
+    from oracle import restate
+    sc = scene(vsize)
+    R = synthetic.batch_rodrigues(np.array([[0.3, -0.2, 0.5]]))[0].astype(np.float32)
+    Th = np.array([0.1, -0.05, 0.2], np.float32)
+    wverts = (sc.verts.astype(np.float64) @ R.T.astype(np.float64) + Th).astype(np.float32)
+    wb = synthetic.get_bounds(wverts)
+    rng = np.random.Generator(np.random.PCG64(seed))
+    tgt = rng.uniform(wb[0].astype(np.float64), wb[1].astype(np.float64), size=(n_rays, 3))
+    o = np.broadcast_to(np.array([0.0, 0.0, 3.0]), (n_rays, 3))
+    d = tgt - o
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    ro, rd = o.astype(np.float32).copy(), d.astype(np.float32)
+    near, far, mask = restate.near_far(wb, ro, rd)
+    b = sc.batch_arrays(ro[mask], rd[mask], near.astype(np.float32), far.astype(np.float32))
+    b['R'] = R[None]
+    b['Th'] = Th[None]
+    b['wbounds'] = wb[None]
+    return b
