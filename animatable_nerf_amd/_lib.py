@@ -34,7 +34,9 @@ class Frame(ctypes.Structure):
     _fields_ = [('A', ctypes.c_void_p), ('R', ctypes.c_void_p), ('Th', ctypes.c_void_p),
                 ('pbw', ctypes.c_void_p), ('pbw_dims', ctypes.c_int * 3), ('pbounds', ctypes.c_void_p),
                 ('tbw', ctypes.c_void_p), ('tbw_dims', ctypes.c_int * 3), ('tbounds', ctypes.c_void_p),
-                ('latent_index', ctypes.c_void_p), ('bw_latent_index', ctypes.c_void_p)]
+                ('latent_index', ctypes.c_void_p), ('bw_latent_index', ctypes.c_void_p),
+                ('n_views', ctypes.c_int), ('Ks', ctypes.c_void_p), ('RT', ctypes.c_void_p), ('msks', ctypes.c_void_p),
+                ('img_h', ctypes.c_int), ('img_w', ctypes.c_int)]
 
 
 class RenderOpts(ctypes.Structure):

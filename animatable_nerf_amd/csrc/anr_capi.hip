@@ -99,6 +99,11 @@ int stage_frontend(const anr_params* p, const anr_frame* f, const float* ray_o, 
   fa.mask = (uint64_t*)(ws + L.mask);
   fa.chunk_min = (uint64_t*)(ws + L.chunk_min);
   fa.raw = raw;
+  fa.n_views = f->n_views;
+  fa.Ks = f->Ks; fa.RT = f->RT; fa.msks = f->msks;
+  fa.img_h = f->img_h; fa.img_w = f->img_w;
+  if (f->n_views < 0 || (f->n_views > 0 && (!f->Ks || !f->RT || !f->msks || f->img_h <= 0 || f->img_w <= 0)))
+    return fail(ANR_E_ARG, "render: bad visibility-filter views");
   hipLaunchKernelGGL(k_frontend, dim3((R + 3) / 4), dim3(256), 0, s, fa);
   ANR_TRY(check_launch("k_frontend"));
 

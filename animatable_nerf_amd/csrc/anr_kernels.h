@@ -14,6 +14,10 @@ struct FrontArgs {
   uint64_t* mask;        // (R) keep ballots
   uint64_t* chunk_min;   // (nchunks) argmin keys, preset to ~0
   float4* raw;           // (R*64) zeroed at non-kept samples (may be NULL)
+  int n_views;           // visibility filter (anr_frame), 0 = off
+  const float *Ks, *RT;
+  const uint8_t* msks;
+  int img_h, img_w;
 };
 
 struct CompactArgs {

@@ -155,13 +155,30 @@ __global__ __launch_bounds__(256) void k_frontend(FrontArgs a) {
   TriCell cell;
   tri_cell(pose, lo, hi, a.X, a.Y, a.Z, cell);
   const float pn = tri_channel(a.pbw, 25, 24, cell);
-  const bool keep = pn < a.norm_th;
+  // novel-view filter (tpose_renderer_mmsk.py:14-57): world point -> every training view, rounded
+  // half-to-even, clamped, looked up in its mask; the network then sees only visible samples, so
+  // the per-chunk argmin runs over them (a chunk with none keeps nothing)
+  bool vis = true;
+  for (int v = 0; v < a.n_views; ++v) {
+    const float* R = a.RT + 12 * v;
+    const float* K = a.Ks + 9 * v;
+    float q[3], s3[3];
+    for (int j = 0; j < 3; ++j) q[j] = fmaf(pts[2], R[4 * j + 2], fmaf(pts[1], R[4 * j + 1], pts[0] * R[4 * j])) + R[4 * j + 3];
+    for (int j = 0; j < 3; ++j) s3[j] = fmaf(q[2], K[3 * j + 2], fmaf(q[1], K[3 * j + 1], q[0] * K[3 * j]));
+    long long xi = (long long)rintf(s3[0] / s3[2]);
+    long long yi = (long long)rintf(s3[1] / s3[2]);
+    xi = xi < 0 ? 0 : (xi > a.img_w - 1 ? a.img_w - 1 : xi);
+    yi = yi < 0 ? 0 : (yi > a.img_h - 1 ? a.img_h - 1 : yi);
+    vis = vis && a.msks[((size_t)v * a.img_h + yi) * a.img_w + xi] != 0;
+  }
+  const bool keep = vis && pn < a.norm_th;
   const uint64_t m = __ballot(keep);
   if (lane == 0) a.mask[ray] = m;
   if (a.raw != nullptr && !keep) a.raw[(size_t)ray * 64 + lane] = make_float4(0.f, 0.f, 0.f, 0.f);
-  // per-chunk argmin of pnorm (first index on ties): key = bits(pn) << 32 | index-in-chunk
+  // per-chunk argmin of pnorm over the visible samples (first index on ties):
+  // key = bits(pn) << 32 | index-in-chunk
   const int rc = ray % a.chunk;
-  uint64_t key = ((uint64_t)__float_as_uint(pn) << 32) | (uint32_t)(rc * 64 + lane);
+  uint64_t key = vis ? (((uint64_t)__float_as_uint(pn) << 32) | (uint32_t)(rc * 64 + lane)) : ~0ull;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
     const uint64_t o = __shfl_xor(key, off);

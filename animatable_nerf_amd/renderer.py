@@ -53,6 +53,17 @@ class _Call:
             f.tbw_dims[i] = fr['tbw'].shape[1 + i]
         f.latent_index = self.li.data_ptr()
         f.bw_latent_index = self.bli.data_ptr()
+        f.n_views = 0
+        if renderer.visibility_filter and 'msks' in batch:
+            # tpose_renderer_mmsk.py:14-57 keys (tpose_novel_view_dataset.py:191)
+            self.Ks = _f32(batch['Ks'], dev).reshape(-1, 3, 3)
+            self.RT = _f32(batch['RT'], dev).reshape(-1, 3, 4)
+            self.msks = batch['msks'].to(device=dev, dtype=torch.uint8).contiguous()
+            f.n_views = self.Ks.shape[0]
+            f.Ks, f.RT, f.msks = self.Ks.data_ptr(), self.RT.data_ptr(), self.msks.data_ptr()
+            f.img_h, f.img_w = int(batch['H'].reshape(-1)[0]), int(batch['W'].reshape(-1)[0])
+            if tuple(self.msks.shape[-2:]) != (f.img_h, f.img_w):
+                raise ValueError(f"msks {tuple(self.msks.shape)} do not match H, W = {f.img_h}, {f.img_w}")
         self.frame = f
         o = _lib.RenderOpts()
         o.n_samples = ns
@@ -83,6 +94,8 @@ class _Call:
 
 
 class Renderer:
+    visibility_filter = False  # renderer_mmsk.Renderer turns it on
+
     def __init__(self, net, cfg=None):
         self.net = net
         self.cfg = cfg if cfg is not None else _config.cfg

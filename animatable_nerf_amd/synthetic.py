@@ -147,6 +147,42 @@ class Scene:
         }
 
 
+def training_views(verts, n_views=3, H=100, W=100, focal=80.0, dist=3.0, dilate=1):
+    """Training cameras + silhouettes for the novel-view visibility filter
+    (``tpose_renderer_mmsk.py:14-57``; keys of ``tpose_novel_view_dataset.py:191``): cameras on a
+    circle around the y axis (0, 90, 200 degrees, ...) looking at the origin, K with the principal
+    point at the image centre, RT = [R | T] world->camera (float32); msks = the vertices splatted into
+    each image and dilated by ``dilate`` pixels (uint8 0/1), i.e. the subject's silhouette."""
+    angles = np.deg2rad(np.array([0.0, 90.0, 200.0, 300.0, 45.0, 135.0])[:n_views])
+    K = np.array([[focal, 0.0, (W - 1) / 2.0], [0.0, focal, (H - 1) / 2.0], [0.0, 0.0, 1.0]], np.float32)
+    Ks, RTs, msks = [], [], []
+    for a in angles:
+        c = np.array([dist * np.sin(a), 0.0, dist * np.cos(a)])   # camera centre, looking at 0
+        fwd = -c / np.linalg.norm(c)
+        up = np.array([0.0, 1.0, 0.0])
+        right = np.cross(up, fwd)
+        right /= np.linalg.norm(right)
+        down = np.cross(fwd, right)
+        R = np.stack([right, down, fwd], 0)                       # rows: camera x, y, z in world
+        T = -R @ c
+        RT = np.concatenate([R, T[:, None]], 1).astype(np.float32)
+        cam = verts.astype(np.float64) @ R.T + T
+        uv = cam @ K.astype(np.float64).T
+        uv = uv[:, :2] / uv[:, 2:]
+        m = np.zeros((H, W), np.uint8)
+        ij = np.round(uv).astype(int)
+        ok = (ij[:, 0] >= 0) & (ij[:, 0] < W) & (ij[:, 1] >= 0) & (ij[:, 1] < H)
+        m[ij[ok, 1], ij[ok, 0]] = 1
+        for _ in range(dilate):
+            m2 = m.copy()
+            m2[1:] |= m[:-1]; m2[:-1] |= m[1:]; m2[:, 1:] |= m[:, :-1]; m2[:, :-1] |= m[:, 1:]
+            m = m2
+        Ks.append(K)
+        RTs.append(RT)
+        msks.append(m)
+    return np.stack(Ks), np.stack(RTs), np.stack(msks), H, W
+
+
 def lbs_vertices(verts, skin, A):
     """Forward LBS of (V,3) vertices with per-vertex weights (V,24) and A (24,4,4), float64 -> f32."""
     T = np.einsum('vj,jab->vab', skin.astype(np.float64), A.astype(np.float64))

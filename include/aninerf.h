@@ -79,6 +79,13 @@ typedef struct anr_frame {
   const float* tbounds;    /* (2,3) device */
   const int64_t* latent_index;  /* (1) device: batch['latent_index'] */
   const int64_t* bw_latent_index;  /* (1) device: batch['bw_latent_index'] (novel pose only) */
+  /* novel-view visibility filter (tpose_renderer_mmsk.py:14-57); n_views = 0 disables it:
+   * a sample is kept only if it projects inside every training view's mask. */
+  int n_views;
+  const float* Ks;         /* (V,3,3) device */
+  const float* RT;         /* (V,3,4) device, world -> camera */
+  const uint8_t* msks;     /* (V,img_h,img_w) device */
+  int img_h, img_w;
 } anr_frame;
 
 typedef struct anr_render_opts {

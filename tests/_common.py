@@ -150,3 +150,12 @@ def rotated_batch_np(n_rays=3000, seed=23, vsize=0.05):
     b['Th'] = Th[None]
     b['wbounds'] = wb[None]
     return b
+
+
+def mmsk_batch_np(ro, rd):
+    """Batch with the training-view keys of tpose_novel_view_dataset.py:191 (synthetic views)."""
+    sc = scene(0.05)
+    b, mask = batch_np(sc, ro, rd)
+    Ks, RTs, msks, H, W = synthetic.training_views(sc.verts)
+    b.update(Ks=Ks[None], RT=RTs[None], msks=msks[None], H=np.array([H]), W=np.array([W]))
+    return b, mask

@@ -172,3 +172,26 @@ def test_eval_ray_pipeline_bit_exact(tag):
                                                              g['bounds'])
     for k, v in (('ray_o', ro), ('ray_d', rd), ('near', near), ('far', far), ('mask', mask)):
         assert np.array_equal(v, g[tag + '_' + k]), k
+
+
+def test_mmsk_render_bit_exact():
+    """(f) novel-view renderer with the visibility filter (tpose_renderer_mmsk.py) vs golden G9."""
+    from ._common import mmsk_batch_np
+    g = golden('g9_mmsk')
+    sc = scene(0.05)
+    ro, rd = sc.box_rays(64, seed=2)
+    b, _ = mmsk_batch_np(ro, rd)
+    trace = {}
+    with torch.no_grad():
+        ret = restate.render_mmsk(oracle_params(), to_torch(b), trace=trace)
+    assert np.array_equal(trace['inside'][0].numpy(), g['tiny_inside'])
+    for k in ('rgb_map', 'acc_map', 'depth_map'):
+        np.testing.assert_array_equal(ret[k].numpy(), g['tiny_' + k], err_msg=k)
+    b, _ = mmsk_batch_np(g['chunks_ray_o'], g['chunks_ray_d'])
+    trace = {}
+    with torch.no_grad():
+        ret = restate.render_mmsk(oracle_params(), to_torch(b), trace=trace)
+    bits = np.packbits(torch.cat([x[0] for x in trace['inside']]).numpy())
+    assert np.array_equal(bits, g['chunks_inside_bits'])
+    for k in ('rgb_map', 'acc_map', 'depth_map'):
+        np.testing.assert_array_equal(ret[k].numpy(), g['chunks_' + k], err_msg=k)
