@@ -143,7 +143,7 @@ int stage_mlp(const anr_params* p, const anr_frame* f, const float* ray_o, const
   ma.pbw_rows = (float*)(ws + L.pbw_rows);
   ma.tbw_rows = (float*)(ws + L.tbw_rows);
   const bool b16 = o->precision == ANR_BF16X3;
-  ma.pose_woff = o->novel_pose ? (b16 ? ANR_X6_NOVEL_WOFF : ANR_NOVEL_WOFF) : 0;
+  ma.pose_woff = o->novel_pose ? (b16 ? (ANR_POSE_MODE == 2 ? ANR_X6_NOVEL_WOFF : ANR_B16_NOVEL_WOFF) : ANR_NOVEL_WOFF) : 0;
   ma.pose_boff = o->novel_pose ? ANR_NOVEL_BOFF : 0;
   const int lds = b16 ? mlp_lds_bytes<true>() : mlp_lds_bytes<false>();
   if (!mlp_attr_set) {

@@ -148,13 +148,18 @@ __host__ __device__ inline int layer_col(const LayerDesc& d, int t, int g) {
 // staging slice (OB x 2 KiB <= 34 KiB).
 __host__ __device__ constexpr int ks32(int i) { return layer_ksteps(i) / 8; }
 __host__ __device__ constexpr int b16_layer_bytes(int i) { return ks32(i) * layer_desc_all(i).ob * 2048; }
-#define ANR_B16_LAYERS 21  // layers 0..20 (the pose pass and the novel-pose copy stay fp32)
+#define ANR_B16_LAYERS 30  // layers 0..29 (incl. the novel_pose_bw copy 21..29)
 __host__ __device__ constexpr int b16_layer_offset(int i) {
   int o = 0;
   for (int k = 0; k < i; ++k) o += b16_layer_bytes(k);
   return o;
 }
 __host__ __device__ constexpr int b16_bytes() { return b16_layer_offset(ANR_B16_LAYERS); }
+#define ANR_B16_NOVEL_WOFF (b16_layer_offset(ANR_L_NOVEL0) - b16_layer_offset(0))
+// arithmetic of the pose-space pass in the bf16 kernel: 1 = bf16x3 (default), 2 = bf16x6
+#ifndef ANR_POSE_MODE
+#define ANR_POSE_MODE 1
+#endif
 // byte offset of the bf16 image inside the packed buffer (after the fp32 weights and the biases)
 __host__ __device__ constexpr int b16_base() { return (packed_bytes() + 255) / 256 * 256; }
 

@@ -36,14 +36,14 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 // The per-tile layer program: entries 0..8 the pose-space BW MLP, 9..17 the T-pose BW MLP (layers
 // 0..8 again), 18..29 the NeRF (layers 9..20). Arithmetic per entry (anr_layers.h):
 //   mode 0 exact fp32 MFMA (k_mlp, every entry);
-//   mode 2 bf16x6, fp32-level (k_mlp_b16, the pose pass: its output moves the canonical point that
-//          the 2^9-frequency encoding amplifies);
-//   mode 1 bf16x3 (k_mlp_b16, entries >= 9).
+//   mode 1 bf16x3 (k_mlp_b16; the pose pass too unless built with ANR_POSE_MODE=2);
+//   mode 2 bf16x6, fp32-level (the pose pass with ANR_POSE_MODE=2: measured unnecessary, the
+//          outputs' error vs the fp32 oracle stays <= 4e-6 with x3, tools/precision_report.py).
 #define ANR_PROG_LEN 30
 __host__ __device__ constexpr int prog_layer(int e) { return e < 9 ? e : e - 9; }
 __host__ __device__ constexpr bool prog_pose(int e) { return e < 9; }
 template <bool B16>
-__host__ __device__ constexpr int prog_mode(int e) { return B16 ? (e < 9 ? 2 : 1) : 0; }
+__host__ __device__ constexpr int prog_mode(int e) { return B16 ? (e < 9 ? ANR_POSE_MODE : 1) : 0; }
 // Slices = the staging unit: mode 0 8 fp32 k-steps; mode 1 one 32-input k-step (OB x 2 KiB);
 // mode 2 one 32-input k-step of a group of <= 8 out-blocks (x 3 KiB).
 __host__ __device__ constexpr int prog_nobg(int e) { return (layer_desc_all(prog_layer(e)).ob + 7) / 8; }

@@ -7,13 +7,13 @@ step    = one full-frame render of 512x512 box rays x 64 samples (262,142 rays h
 N GPUs  = one process per GPU (torch.distributed.run), each rendering its own frame (rays seed
           2 + rank): frames are independent, so no collective on the data path ("scaling": "weak");
           the timed region is bracketed by barriers and the max over ranks is reported.
-precision: --render-precision bf16x3 (default) runs the fused network kernel k_mlp_b16 — the pose
-          BW MLP as a 3-way (x6) and the T-pose BW MLP + NeRF as a 2-way (x3) hi/lo split onto bf16
-          MFMA with fp32 accumulation, outputs held to the same 1e-4 fp32 tolerance as the exact path
-          by the parity tests; the exact-fp32 kernel k_mlp is timed in the same run ("fp32_exact").
+precision: --render-precision bf16x3 (default) runs the fused network kernel k_mlp_b16 — every
+          layer as a 2-way hi/lo split onto bf16 MFMA (3 products per MAC) with fp32 accumulation,
+          outputs held to the same 1e-4 fp32 tolerance as the exact path by the parity tests (measured
+          <= 4e-6, tools/precision_report.py); the exact-fp32 kernel k_mlp is timed in the same run.
 roofline: the fused network kernel is the dominant kernel; its per-launch time is measured with
           hipEvents on the render stream (anr_profile_*); achieved = executed MFMA FLOP per kept
-          sample (bf16x3: 2*(6*497,152 + 3*(497,152 + 658,944)); fp32: 3,306,496) x kept / time,
+          sample (bf16x3: 2*3*(2*497,152 + 658,944); fp32: 3,306,496) x kept / time,
           peak = the dense MFMA peak of the operand type (bf16 2.5 PF, fp32 157.3 TF);
           achieved_credited uses SURVEY.md §8(d)'s 2,312,192 FLOP per kept sample.
 cpu_baseline: the oracle (op-for-op PyTorch-CPU restatement of the reference) on the first 16
@@ -132,10 +132,10 @@ def main():
     value = samples_per_rank * world / dt_max
     split = args.render_precision == 'bf16x3'
     if split:
-        # executed bf16 MFMA work per kept sample: pose BW x6 + (T-pose BW + NeRF) x3 products
-        flop_exec = 2 * (6 * MAC_BW + 3 * (MAC_BW + MAC_NERF))
+        # executed bf16 MFMA work per kept sample: 3 products per MAC (lo*bh + hi*bl + hi*bh)
+        flop_exec = 2 * 3 * (2 * MAC_BW + MAC_NERF)
         peak = PEAK_BF16_MFMA_TFLOPS
-        dtype = 'bf16 MFMA operands (hi/lo split: x6 pose BW, x3 T-pose BW + NeRF), fp32 accumulate'
+        dtype = 'bf16 MFMA operands (hi/lo split, 3 products per MAC), fp32 accumulate'
     else:
         flop_exec = FLOP_PER_KEPT_EXECUTED
         peak = PEAK_FP32_MFMA_TFLOPS

@@ -41,7 +41,7 @@ def test_version_and_sizes(lib):
     # bf16x3 image: per layer ceil(in/32) k-steps x out-blocks x 2 KiB (hi + lo fragments)
     ks_ob = [(2, 16), (8, 16), (8, 16), (8, 16), (8, 16), (10, 16), (8, 16), (8, 16), (8, 2),
              (2, 16), (8, 16), (8, 16), (8, 16), (8, 16), (10, 16), (8, 16), (8, 16), (8, 17), (8, 16), (9, 8), (4, 1)]
-    b16 = sum(k * o for k, o in ks_ob) * 2048
+    b16 = (sum(k * o for k, o in ks_ob) + sum(k * o for k, o in ks_ob[:9])) * 2048  # + novel-pose copy
     x6 = 2 * sum(k * o for k, o in ks_ob[:9]) * 3072  # pose-pass bf16x6 image (+ novel-pose copy)
     base16 = (fp32 + 255) // 256 * 256
     assert lib.anr_params_packed_bytes() == (base16 + b16 + 255) // 256 * 256 + x6
