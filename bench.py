@@ -36,6 +36,16 @@ PEAK_BF16_MFMA_TFLOPS = 2500.0     # MI355X_MICROARCH.md, BF16 dense (no sparsit
 METRIC = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), 'BASELINE.json')))['metric']
 
 
+def max_over_ranks(x, dev, world):
+    """max of a host float over ranks (the timed region's max, bench contract)"""
+    if world == 1:
+        return float(x)
+    on_cpu = dist.get_backend() == 'gloo'
+    t = torch.tensor([float(x)], dtype=torch.float64, device='cpu' if on_cpu else dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -63,10 +73,18 @@ def main():
     rank = int(os.environ.get('RANK', 0))
     world = int(os.environ.get('WORLD_SIZE', 1))
     local = int(os.environ.get('LOCAL_RANK', 0))
+    # rehearsal knobs for the N > 1 path on a one-GPU box (never set by the driver):
+    # ANR_BENCH_BACKEND=gloo, ANR_BENCH_ONE_DEVICE=1 maps every rank to cuda:0
+    backend = os.environ.get('ANR_BENCH_BACKEND', 'nccl')
+    if os.environ.get('ANR_BENCH_ONE_DEVICE') == '1':
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device('cuda', local)
     if world > 1:
-        dist.init_process_group('nccl', device_id=dev)
+        if backend == 'nccl':
+            dist.init_process_group('nccl', device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from animatable_nerf_amd import _lib, config, network, synthetic
     from animatable_nerf_amd.renderer import Renderer, near_far
@@ -115,10 +133,7 @@ def main():
         launches = _lib.ctypes.c_int(0)
         _lib.check(lib.anr_profile_read(_lib.ctypes.byref(mlp_ms), _lib.ctypes.byref(launches)), 'anr_profile_read')
         lib.anr_profile_enable(0)
-        t = torch.tensor([dt], device=dev, dtype=torch.float64)
-        if world > 1:
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return out, float(t.item()), mlp_ms.value / max(1, launches.value), renderer.last_counts
+        return out, max_over_ranks(dt, dev, world), mlp_ms.value / max(1, launches.value), renderer.last_counts
 
     others = [p for p in ('fp32', 'bf16x3') if p != args.render_precision]
     side = {}
@@ -223,10 +238,7 @@ def bench_train(args, rank, world, dev):
         dist.barrier()
     dt = time.perf_counter() - t0
     kept = step.renderer.last_counts[0] if step.renderer.last_counts else 0
-    t = torch.tensor([dt], device=dev, dtype=torch.float64)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    dt_max = float(t.item())
+    dt_max = max_over_ranks(dt, dev, world)
     R = int(batches[0]['ray_o'].shape[1])
     loss = step.loss3.cpu().tolist()
     # kept samples of the last step (host read inside anr_train_step)
@@ -298,10 +310,7 @@ def bench_sdf(args, rank, world, dev):
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    t = torch.tensor([dt], device=dev, dtype=torch.float64)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    dt_max = float(t.item())
+    dt_max = max_over_ranks(dt, dev, world)
     n_kept = renderer.last_counts[0]
     achieved = n_kept * FLOP_PER_KEPT_SDF * args.steps / dt_max / 1e12
     result = {
