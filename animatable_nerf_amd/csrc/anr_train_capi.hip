@@ -71,8 +71,6 @@ struct Exec {
 
   int gemm(GemmArgs g, int M) {
     if (M <= 0 || g.N <= 0) return ANR_OK;
-    int Ktot = 0;
-    for (int q = 0; q < g.nseg; ++q) Ktot += g.seg[q].K;
     if (g.ksplit < 1) g.ksplit = 1;
     dim3 grid((g.N + 63) / 64, (M + 63) / 64, g.ksplit);
     g.M = M;
@@ -296,7 +294,6 @@ int train_backward(const anr_params* p, float* const* g, const anr_frame* f, con
   b.d_rgb_map = d_rgb; b.d_pbw = d_pbw; b.d_tbw = d_tbw;
   const int g1 = (n + 255) / 256;
   if (n <= 0) return ANR_OK;
-  float* Hp = (float*)(ws + T.Hp);
   float* Ht = (float*)(ws + T.Ht);
   float* Hn = (float*)(ws + T.Hn);
   float* Feat = (float*)(ws + T.Feat);
