@@ -20,6 +20,8 @@ EXPORTS = ('anr_near_far', 'anr_params_packed_bytes', 'anr_params_pack', 'anr_re
            'anr_render_fwd', 'anr_render_counts', 'anr_render_bw_rows', 'anr_profile_enable', 'anr_profile_read',
            'anr_train_workspace_bytes', 'anr_train_fwd', 'anr_train_bwd', 'anr_train_step', 'anr_adam',
            'anr_camera_rays_workspace_bytes', 'anr_camera_rays', 'anr_sdf_render_workspace_bytes', 'anr_sdf_render_fwd', 'anr_sdf_render_counts', 'anr_sdf_render_rows',
+           'anr_alpha_workspace_bytes', 'anr_alpha_points', 'anr_alpha_counts', 'anr_mc_workspace_bytes',
+           'anr_mc_count', 'anr_mc_emit',
            'anr_last_error', 'anr_version')
 
 c_float_p = ctypes.c_void_p
@@ -51,6 +53,11 @@ FP32, BF16, BF16_ALL, BF16X3 = 0, 1, 2, 3  # anr_render_opts.precision
 class RenderOut(ctypes.Structure):
     _fields_ = [('rgb_map', ctypes.c_void_p), ('acc_map', ctypes.c_void_p), ('depth_map', ctypes.c_void_p),
                 ('raw', ctypes.c_void_p)]
+
+
+class AlphaOpts(ctypes.Structure):
+    _fields_ = [('chunk_pts', ctypes.c_int), ('norm_th', ctypes.c_float), ('novel_pose', ctypes.c_int),
+                ('precision', ctypes.c_int)]
 
 
 class SdfParams(ctypes.Structure):
@@ -115,6 +122,18 @@ def load():
     D = ctypes.POINTER(ctypes.c_double)
     lib.anr_camera_rays.argtypes = [ctypes.c_int, ctypes.c_int, D, D, D, D, ctypes.c_int, P, P, P, P, P, P, P, P, P,
                                     ctypes.c_size_t, P]
+    lib.anr_alpha_workspace_bytes.restype = ctypes.c_size_t
+    lib.anr_alpha_workspace_bytes.argtypes = [ctypes.c_long, ctypes.POINTER(AlphaOpts), ctypes.POINTER(Frame)]
+    lib.anr_alpha_points.argtypes = [ctypes.POINTER(Params), ctypes.POINTER(Frame), P, ctypes.c_long,
+                                     ctypes.POINTER(AlphaOpts), P, P, ctypes.c_size_t, P]
+    lib.anr_alpha_counts.restype = P
+    lib.anr_alpha_counts.argtypes = [P]
+    lib.anr_mc_workspace_bytes.restype = ctypes.c_size_t
+    lib.anr_mc_workspace_bytes.argtypes = [ctypes.c_int] * 4
+    lib.anr_mc_count.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double, P, P,
+                                 ctypes.c_size_t, P]
+    lib.anr_mc_emit.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double, P, P, P,
+                                ctypes.c_size_t, P]
     lib.anr_profile_enable.argtypes = [ctypes.c_int]
     lib.anr_profile_read.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]
     lib.anr_last_error.restype = ctypes.c_char_p

@@ -72,7 +72,7 @@ def defaults():
         'N_samples': 64, 'N_rand': 1024, 'perturb': 1, 'white_bkgd': False,
         'xyz_res': 10, 'view_res': 4, 'norm_th': 0.05, 'train_th': 0.0, 'box_padding': 0.05,
         'aninerf_animation': False, 'test_novel_pose': False, 'eval': False, 'train_precision': 'fp32', 'render_precision': 'fp32',
-        'chunk': 2048,
+        'chunk': 2048, 'mesh_th': 50.0, 'voxel_size': [0.005, 0.005, 0.005],
         'train': {'lr': 5e-4, 'weight_decay': 0.0, 'optim': 'adam', 'epoch': 400,
                   'scheduler': {'type': 'exponential', 'gamma': 0.1, 'decay_epochs': 1000}},
         'ep_iter': 500, 'save_ep': 200, 'save_latest_ep': 5, 'eval_ep': 1000,
@@ -99,9 +99,10 @@ def load_cfg(cfg_file=None, opts=(), base_dir=None):
             node = {k: v for k, v in node.items() if k != 'parent_cfg'}
             cfg.merge(CfgNode(node))
     cfg.merge_from_list(list(opts))
-    for sub in ('aninerf_animation', 'vis_pose_sequence', 'vis_novel_view'):
+    for sub in ('aninerf_animation', 'vis_pose_sequence', 'vis_novel_view', 'vis_tpose_mesh', 'vis_posed_mesh'):
         key = {'aninerf_animation': 'aninerf_animation_cfg', 'vis_pose_sequence': 'pose_sequence_cfg',
-               'vis_novel_view': 'novel_view_cfg'}[sub]
+               'vis_novel_view': 'novel_view_cfg', 'vis_tpose_mesh': 'mesh_cfg',
+               'vis_posed_mesh': 'mesh_cfg'}[sub]  # config.py:160-176
         if cfg.get(sub) and key in cfg:
             cfg.merge(cfg[key])
             cfg.merge_from_list(list(opts))

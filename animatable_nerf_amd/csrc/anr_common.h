@@ -84,6 +84,25 @@ __device__ __forceinline__ void world_to_pose(const float x[3], const float* R, 
   for (int j = 0; j < 3; ++j) out[j] = fmaf(d2, R[2 * 3 + j], fmaf(d1, R[1 * 3 + j], d0 * R[0 * 3 + j]));
 }
 
+// the same product when torch's matmul takes its small path (n < 45 points, measured): separate
+// multiplies, left-to-right adds. Free points (the mesh path's get_alpha) can end in such a chunk.
+__device__ __forceinline__ void world_to_pose_small(const float x[3], const float* R, const float* Th, float out[3]) {
+#pragma clang fp contract(off)
+  const float d0 = x[0] - Th[0], d1 = x[1] - Th[1], d2 = x[2] - Th[2];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) out[j] = (d0 * R[0 * 3 + j] + d1 * R[1 * 3 + j]) + d2 * R[2 * 3 + j];
+}
+
+// world -> pose of free point i of a call split into chunks of chunk_pts points (matmul per chunk)
+__device__ __forceinline__ void world_to_pose_pt(const float* __restrict__ wpts, long i, long n_pts, int chunk_pts,
+                                                 const float* R, const float* Th, float out[3]) {
+  const float x[3] = {wpts[3 * i], wpts[3 * i + 1], wpts[3 * i + 2]};
+  const long c0 = (i / chunk_pts) * chunk_pts;
+  const long len = n_pts - c0 < chunk_pts ? n_pts - c0 : chunk_pts;
+  if (len >= 45) world_to_pose(x, R, Th, out);
+  else world_to_pose_small(x, R, Th, out);
+}
+
 // Positional-encoding feature f of gamma(x) (embedder.py:5-54): [x, sin(2^0 x), cos(2^0 x), ...]
 __device__ __forceinline__ float embed_feature(const float x[3], int f, int nfreq) {
   if (f < 3) return x[f];
@@ -129,6 +148,25 @@ __device__ __forceinline__ void sample_point(const float* __restrict__ ray_o, co
   else dist = z - z_sample(nr, fr, trow, s - 1, n);
 #pragma unroll
   for (int c = 0; c < 3; ++c) pts[c] = ray_o[3 * ray + c] + ray_d[3 * ray + c] * z;
+}
+
+// exclusive scan of one int per thread over a 256-thread block (sh: 4 ints of LDS); total = block sum
+__device__ __forceinline__ int block_excl_scan_256(int v, int* sh, int& total) {
+  // 256 threads: wave inclusive scans + wave totals in LDS
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int x = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int y = __shfl_up(x, off);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) sh[w] = x;
+  __syncthreads();
+  int base = 0;
+  for (int k = 0; k < w; ++k) base += sh[k];
+  total = sh[0] + sh[1] + sh[2] + sh[3];
+  __syncthreads();
+  return base + x - v;
 }
 
 }  // namespace anr

@@ -18,6 +18,11 @@ struct FrontArgs {
   const float *Ks, *RT;
   const uint8_t* msks;
   int img_h, img_w;
+  // free-point mode (k_frontend_pts, the mesh path's get_alpha): n_rays = ceil(n_pts / 64) groups
+  // of 64 points, chunk = chunk_pts / 64 groups
+  const float* wpts;     // (n_pts, 3) world points
+  long n_pts;
+  int chunk_pts;
 };
 
 struct CompactArgs {
@@ -78,6 +83,11 @@ struct MlpArgs {
   float* tbw_rows;   // (n', 24)
   int pose_woff;     // byte offset of the pose-pass BW weight slices (novel_pose_bw copy or 0)
   int pose_boff;     // float offset of the pose-pass BW biases
+  // density program (k_alpha*, get_alpha): kept point ids index wpts; alpha_out[id] = raw sigma
+  const float* wpts;
+  long n_pts;
+  int chunk_pts;
+  float* alpha_out;
 };
 
 struct PrepArgs {
@@ -99,6 +109,7 @@ __global__ void k_cam_rays(CamArgs a);
 __global__ void k_cam_count(CamArgs a);
 __global__ void k_cam_scatter(CamArgs a);
 __global__ void k_frontend(FrontArgs a);
+__global__ void k_frontend_pts(FrontArgs a);
 __global__ void k_count(CompactArgs a);
 __global__ void k_scan_blocks(int* sums, int nb, int* total_out);
 __global__ void k_compact(CompactArgs a);
@@ -111,6 +122,8 @@ __global__ void k_composite(CompositeArgs a);
 __global__ void k_prep(PrepArgs a);
 __global__ void k_mlp(MlpArgs a);
 __global__ void k_mlp_b16(MlpArgs a);  // T-pose BW + NeRF in bf16x3 (render precision ANR_BF16X3)
+__global__ void k_alpha(MlpArgs a);      // density program (get_alpha), exact fp32 MFMA
+__global__ void k_alpha_b16(MlpArgs a);  // density program, NeRF trunk in bf16x3
 
 struct PackArgs {
   const float* t[65];  // 46 core tensors + 19 novel_pose_bw tensors (NULL when absent)

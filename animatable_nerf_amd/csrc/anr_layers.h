@@ -73,7 +73,10 @@ __host__ __device__ constexpr LayerDesc layer_desc(int i) {
 #define ANR_L_RGB 20
 // layers 21..29: novel_pose_bw (BackwardBlendWeight), same shapes as 0..8, tensors 46 + (0..18)
 #define ANR_L_NOVEL0 21
-#define ANR_NUM_LAYERS_ALL 30
+// layer 30: alpha_fc alone (TPoseHuman.calculate_alpha :241-250, the density-only program of the
+// mesh path's get_alpha); the same weights as out-block 16 of layer 17
+#define ANR_L_ALPHA 30
+#define ANR_NUM_LAYERS_ALL 31
 #define ANR_NOVEL_T0 46  // tensor index of novel_pose_bw.bw_latent.weight in the packer's list
 
 __host__ __device__ constexpr LayerDesc novel_desc(int i) {
@@ -86,7 +89,8 @@ __host__ __device__ constexpr LayerDesc layer_desc_all(int i) {
   return i < ANR_NUM_LAYERS ? layer_desc(i)
        : i == ANR_L_VIEW ? LayerDesc{23, 24, -1, -1, 128, 0, 283, 8, 2, {{SRC_ACT, 64, 0}, {SRC_VEMB, 8, 256}}}
        : i == ANR_L_RGB  ? LayerDesc{25, 26, -1, -1, 3, 0, 128, 1, 1, {{SRC_ACT, 32, 0}, {0, 0, 0}}}
-       : i < ANR_NUM_LAYERS_ALL ? novel_desc(i - ANR_L_NOVEL0)
+       : i < ANR_L_ALPHA ? novel_desc(i - ANR_L_NOVEL0)
+       : i == ANR_L_ALPHA ? LayerDesc{17, 18, -1, -1, 1, 0, 256, 1, 1, {{SRC_ACT, 64, 0}, {0, 0, 0}}}
        : LayerDesc{0, 0, -1, -1, 0, 0, 0, 0, 0, {{0, 0, 0}, {0, 0, 0}}};
 }
 
@@ -148,7 +152,7 @@ __host__ __device__ inline int layer_col(const LayerDesc& d, int t, int g) {
 // staging slice (OB x 2 KiB <= 34 KiB).
 __host__ __device__ constexpr int ks32(int i) { return layer_ksteps(i) / 8; }
 __host__ __device__ constexpr int b16_layer_bytes(int i) { return ks32(i) * layer_desc_all(i).ob * 2048; }
-#define ANR_B16_LAYERS 30  // layers 0..29 (incl. the novel_pose_bw copy 21..29)
+#define ANR_B16_LAYERS 31  // layers 0..30 (incl. the novel_pose_bw copy 21..29, alpha_fc 30)
 __host__ __device__ constexpr int b16_layer_offset(int i) {
   int o = 0;
   for (int k = 0; k < i; ++k) o += b16_layer_bytes(k);

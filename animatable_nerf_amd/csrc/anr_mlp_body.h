@@ -33,67 +33,77 @@ __device__ __forceinline__ void static_for(F&& f) {
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
-// The per-tile layer program: entries 0..8 the pose-space BW MLP, 9..17 the T-pose BW MLP (layers
-// 0..8 again), 18..29 the NeRF (layers 9..20). Arithmetic per entry (anr_layers.h):
+// The per-tile layer program, variant V:
+//   V = 0 (render): entries 0..8 the pose-space BW MLP, 9..17 the T-pose BW MLP (layers 0..8
+//         again), 18..29 the NeRF (layers 9..20);
+//   V = 1 (density, get_alpha of the mesh path, tpose_nerf_network.py:105-135): entries 0..8 the
+//         pose-space BW MLP, 9..16 the NeRF trunk (layers 9..16), 17 alpha_fc alone (layer 30).
+// Arithmetic per entry (anr_layers.h):
 //   mode 0 exact fp32 MFMA (k_mlp, every entry);
 //   mode 1 bf16x3 (k_mlp_b16; the pose pass too unless built with ANR_POSE_MODE=2);
 //   mode 2 bf16x6, fp32-level (the pose pass with ANR_POSE_MODE=2: measured unnecessary, the
 //          outputs' error vs the fp32 oracle stays <= 4e-6 with x3, tools/precision_report.py).
-#define ANR_PROG_LEN 30
-__host__ __device__ constexpr int prog_layer(int e) { return e < 9 ? e : e - 9; }
+template <int V>
+__host__ __device__ constexpr int prog_len() { return V == 0 ? 30 : 18; }
+template <int V>
+__host__ __device__ constexpr int prog_layer(int e) {
+  return e < 9 ? e : (V == 0 ? e - 9 : (e < 17 ? e : ANR_L_ALPHA));
+}
 __host__ __device__ constexpr bool prog_pose(int e) { return e < 9; }
 template <bool B16>
 __host__ __device__ constexpr int prog_mode(int e) { return B16 ? (e < 9 ? ANR_POSE_MODE : 1) : 0; }
 // Slices = the staging unit: mode 0 8 fp32 k-steps; mode 1 one 32-input k-step (OB x 2 KiB);
 // mode 2 one 32-input k-step of a group of <= 8 out-blocks (x 3 KiB).
-__host__ __device__ constexpr int prog_nobg(int e) { return (layer_desc_all(prog_layer(e)).ob + 7) / 8; }
-template <bool B16>
+template <int V>
+__host__ __device__ constexpr int prog_nobg(int e) { return (layer_desc_all(prog_layer<V>(e)).ob + 7) / 8; }
+template <bool B16, int V>
 __host__ __device__ constexpr int prog_slices(int e) {
-  return prog_mode<B16>(e) == 2   ? ks32(prog_layer(e)) * prog_nobg(e)
-         : prog_mode<B16>(e) == 1 ? ks32(prog_layer(e))
-                                  : layer_ksteps(prog_layer(e)) / ANR_KSLICE;
+  return prog_mode<B16>(e) == 2   ? ks32(prog_layer<V>(e)) * prog_nobg<V>(e)
+         : prog_mode<B16>(e) == 1 ? ks32(prog_layer<V>(e))
+                                  : layer_ksteps(prog_layer<V>(e)) / ANR_KSLICE;
 }
+template <int V>
 __host__ __device__ constexpr int x6_group_obs(int e, int gidx) {
-  return layer_desc_all(prog_layer(e)).ob - 8 * gidx < 8 ? layer_desc_all(prog_layer(e)).ob - 8 * gidx : 8;
+  return layer_desc_all(prog_layer<V>(e)).ob - 8 * gidx < 8 ? layer_desc_all(prog_layer<V>(e)).ob - 8 * gidx : 8;
 }
-template <bool B16>
+template <bool B16, int V>
 __host__ __device__ constexpr int prog_slice_kb(int e, int q) {
-  return prog_mode<B16>(e) == 2   ? x6_group_obs(e, q % prog_nobg(e)) * 3
-         : prog_mode<B16>(e) == 1 ? layer_desc_all(prog_layer(e)).ob * 2
-                                  : layer_chunks(prog_layer(e)) * ANR_KSLICE;
+  return prog_mode<B16>(e) == 2   ? x6_group_obs<V>(e, q % prog_nobg<V>(e)) * 3
+         : prog_mode<B16>(e) == 1 ? layer_desc_all(prog_layer<V>(e)).ob * 2
+                                  : layer_chunks(prog_layer<V>(e)) * ANR_KSLICE;
 }
-template <bool B16>
+template <bool B16, int V>
 __host__ __device__ constexpr int prog_slice_off(int e, int q) {
   return prog_mode<B16>(e) == 2
-             ? x6_base() + x6_layer_offset(prog_layer(e)) +
-                   ((q / prog_nobg(e)) * layer_desc_all(prog_layer(e)).ob + 8 * (q % prog_nobg(e))) * 3072
+             ? x6_base() + x6_layer_offset(prog_layer<V>(e)) +
+                   ((q / prog_nobg<V>(e)) * layer_desc_all(prog_layer<V>(e)).ob + 8 * (q % prog_nobg<V>(e))) * 3072
          : prog_mode<B16>(e) == 1
-             ? b16_base() + b16_layer_offset(prog_layer(e)) + q * layer_desc_all(prog_layer(e)).ob * 2048
-             : layer_offset(prog_layer(e)) + q * layer_chunks(prog_layer(e)) * ANR_KSLICE * 1024;
+             ? b16_base() + b16_layer_offset(prog_layer<V>(e)) + q * layer_desc_all(prog_layer<V>(e)).ob * 2048
+             : layer_offset(prog_layer<V>(e)) + q * layer_chunks(prog_layer<V>(e)) * ANR_KSLICE * 1024;
 }
 // loads per wave for a slice (every wave issues the same count, see Pipe::stage)
-template <bool B16>
-__host__ __device__ constexpr int prog_slice_loads(int e, int q) { return (prog_slice_kb<B16>(e, q) + 7) / 8; }
+template <bool B16, int V>
+__host__ __device__ constexpr int prog_slice_loads(int e, int q) { return (prog_slice_kb<B16, V>(e, q) + 7) / 8; }
 // the slice d steps after (e, q) in the cyclic program, packed as e * 1024 + q
-template <bool B16>
+template <bool B16, int V>
 __host__ __device__ constexpr int prog_advance(int e, int q, int d) {
   for (int i = 0; i < d; ++i) {
-    if (q + 1 < prog_slices<B16>(e)) {
+    if (q + 1 < prog_slices<B16, V>(e)) {
       ++q;
     } else {
       q = 0;
-      e = (e + 1) % ANR_PROG_LEN;
+      e = (e + 1) % prog_len<V>();
     }
   }
   return e * 1024 + q;
 }
 // loads this wave issued after slice (e, q) that may still be in flight when (e, q) is consumed
-template <bool B16>
+template <bool B16, int V>
 __host__ __device__ constexpr int prog_later_loads(int e, int q) {
   int n = 0;
   for (int d = 1; d <= mlp_nbuf<B16>() - 2; ++d) {
-    const int eq = prog_advance<B16>(e, q, d);
-    n += prog_slice_loads<B16>(eq / 1024, eq % 1024);
+    const int eq = prog_advance<B16, V>(e, q, d);
+    n += prog_slice_loads<B16, V>(eq / 1024, eq % 1024);
   }
   return n;
 }
@@ -132,33 +142,33 @@ struct Pipe {
     }
   }
 
-  template <bool B16, int E, int Q>
+  template <bool B16, int V, int E, int Q>
   __device__ __forceinline__ void stage_slice(int buf) {
-    constexpr int off = prog_slice_off<B16>(E, Q);
-    stage(off + (prog_pose(E) ? pose_woff : 0), prog_slice_kb<B16>(E, Q), prog_slice_loads<B16>(E, Q), buf);
+    constexpr int off = prog_slice_off<B16, V>(E, Q);
+    stage(off + (prog_pose(E) ? pose_woff : 0), prog_slice_kb<B16, V>(E, Q), prog_slice_loads<B16, V>(E, Q), buf);
   }
 
   // prologue: slices 0 .. nbuf-2 of the program
-  template <bool B16>
+  template <bool B16, int V>
   __device__ __forceinline__ void start() {
     static_for<0, mlp_nbuf<B16>() - 1>([&](auto d) {
-      constexpr int eq = prog_advance<B16>(0, 0, decltype(d)::value);
-      stage_slice<B16, eq / 1024, eq % 1024>(decltype(d)::value);
+      constexpr int eq = prog_advance<B16, V>(0, 0, decltype(d)::value);
+      stage_slice<B16, V, eq / 1024, eq % 1024>(decltype(d)::value);
     });
     cur = 0;
   }
 
   // Enter slice Q of program entry E: wait for it (its own loads; the barrier covers the other
   // waves'), then refill the slot freed by the previous slice with the slice nbuf-1 ahead.
-  template <bool B16, int E, int Q>
+  template <bool B16, int V, int E, int Q>
   __device__ __forceinline__ const unsigned char* next() {
     constexpr int NB = mlp_nbuf<B16>();
-    constexpr int eq = prog_advance<B16>(E, Q, NB - 1);
-    wait_vmcnt<prog_later_loads<B16>(E, Q)>();
+    constexpr int eq = prog_advance<B16, V>(E, Q, NB - 1);
+    wait_vmcnt<prog_later_loads<B16, V>(E, Q)>();
     __syncthreads();
     int slot = cur + NB - 1;
     slot = slot >= NB ? slot - NB : slot;
-    stage_slice<B16, eq / 1024, eq % 1024>(slot);
+    stage_slice<B16, V, eq / 1024, eq % 1024>(slot);
     const unsigned char* r = lds + cur * smax;
     cur = cur + 1 >= NB ? 0 : cur + 1;
     return r;
@@ -189,10 +199,10 @@ __device__ __forceinline__ void split8x3(const float (&x)[8], bf16x8& hi, bf16x8
 }
 
 // One MLP layer (program entry E): out = W * src + bias (acc layout), k-steps from its segments.
-template <bool B16, int E, bool RELU, int NIN, int NOUT>
+template <bool B16, int V, int E, bool RELU, int NIN, int NOUT>
 __device__ __forceinline__ void layer(Pipe& p, const f32x4 (&in)[NIN], const float (&emb)[16], const float (&vemb)[8],
                                       f32x4 (&out)[NOUT], const float* __restrict__ bias, int g, int lane) {
-  constexpr int L = prog_layer(E);
+  constexpr int L = prog_layer<V>(E);
   constexpr LayerDesc D = layer_desc_all(L);
   static_assert(NOUT >= D.ob, "output array too small");
   const float* bptr = bias + 4 * g;
@@ -210,7 +220,7 @@ __device__ __forceinline__ void layer(Pipe& p, const f32x4 (&in)[NIN], const flo
     static_for<0, KS>([&](auto t) {
       constexpr int tt = decltype(t)::value;
       const unsigned char* buf = nullptr;
-      if constexpr (!X6) buf = p.template next<B16, E, tt>();
+      if constexpr (!X6) buf = p.template next<B16, V, E, tt>();
       constexpr int seg = tt < K0 ? 0 : 1;
       constexpr int ts = tt < K0 ? tt : tt - K0;
       constexpr int kind = D.seg[seg].kind;
@@ -231,10 +241,10 @@ __device__ __forceinline__ void layer(Pipe& p, const f32x4 (&in)[NIN], const flo
       if constexpr (X6) {
         bf16x8 bh, bm, bl;
         split8x3(x, bh, bm, bl);
-        constexpr int NOBG = prog_nobg(E);
+        constexpr int NOBG = prog_nobg<V>(E);
         static_for<0, D.ob>([&](auto ob) {
           constexpr int o = decltype(ob)::value;
-          if constexpr (o % 8 == 0) buf = p.template next<B16, E, tt * NOBG + o / 8>();
+          if constexpr (o % 8 == 0) buf = p.template next<B16, V, E, tt * NOBG + o / 8>();
           const bf16x8 ah = *(const bf16x8*)(buf + (o % 8) * 3072 + lane * 16);
           const bf16x8 am = *(const bf16x8*)(buf + (o % 8) * 3072 + 1024 + lane * 16);
           const bf16x8 al = *(const bf16x8*)(buf + (o % 8) * 3072 + 2048 + lane * 16);
@@ -265,7 +275,7 @@ __device__ __forceinline__ void layer(Pipe& p, const f32x4 (&in)[NIN], const flo
     const unsigned char* buf = nullptr;
     static_for<0, K>([&](auto t) {
       constexpr int tt = decltype(t)::value;
-      if constexpr (tt % ANR_KSLICE == 0) buf = p.template next<B16, E, tt / ANR_KSLICE>();
+      if constexpr (tt % ANR_KSLICE == 0) buf = p.template next<B16, V, E, tt / ANR_KSLICE>();
       f32x4 w[C];
       static_for<0, C>([&](auto c) {
         constexpr int cc = decltype(c)::value;
@@ -442,25 +452,26 @@ __device__ __forceinline__ void store_rows(float* __restrict__ rows, int idx, co
 
 // BW MLP pass starting at program entry E0 (0: pose pass, fp32; 9: T-pose pass). The pose pass
 // may read the novel_pose_bw copy of the weights (p.pose_woff, boff).
-template <bool B16, int E0>
+template <bool B16, int V, int E0>
 __device__ __forceinline__ void bw_mlp(Pipe& p, const float (&emb)[16], const float (&vemb)[8], const float* __restrict__ bias,
                                        int boff, const float* __restrict__ fold0, const float* __restrict__ fold5,
                                        f32x4 (&A)[17], f32x4 (&B)[17], f32x4 (&fc)[2], int g, int lane) {
   f32x4 dummy[1];
   const float* b = bias + boff;
-  layer<B16, E0 + 0, true>(p, dummy, emb, vemb, A, fold0, g, lane);
-  layer<B16, E0 + 1, true>(p, A, emb, vemb, B, b + kBiasOff<1>, g, lane);
-  layer<B16, E0 + 2, true>(p, B, emb, vemb, A, b + kBiasOff<2>, g, lane);
-  layer<B16, E0 + 3, true>(p, A, emb, vemb, B, b + kBiasOff<3>, g, lane);
-  layer<B16, E0 + 4, true>(p, B, emb, vemb, A, b + kBiasOff<4>, g, lane);
-  layer<B16, E0 + 5, true>(p, A, emb, vemb, B, fold5, g, lane);
-  layer<B16, E0 + 6, true>(p, B, emb, vemb, A, b + kBiasOff<6>, g, lane);
-  layer<B16, E0 + 7, true>(p, A, emb, vemb, B, b + kBiasOff<7>, g, lane);
-  layer<B16, E0 + 8, false>(p, B, emb, vemb, fc, b + kBiasOff<8>, g, lane);
+  layer<B16, V, E0 + 0, true>(p, dummy, emb, vemb, A, fold0, g, lane);
+  layer<B16, V, E0 + 1, true>(p, A, emb, vemb, B, b + kBiasOff<1>, g, lane);
+  layer<B16, V, E0 + 2, true>(p, B, emb, vemb, A, b + kBiasOff<2>, g, lane);
+  layer<B16, V, E0 + 3, true>(p, A, emb, vemb, B, b + kBiasOff<3>, g, lane);
+  layer<B16, V, E0 + 4, true>(p, B, emb, vemb, A, b + kBiasOff<4>, g, lane);
+  layer<B16, V, E0 + 5, true>(p, A, emb, vemb, B, fold5, g, lane);
+  layer<B16, V, E0 + 6, true>(p, B, emb, vemb, A, b + kBiasOff<6>, g, lane);
+  layer<B16, V, E0 + 7, true>(p, A, emb, vemb, B, b + kBiasOff<7>, g, lane);
+  layer<B16, V, E0 + 8, false>(p, B, emb, vemb, fc, b + kBiasOff<8>, g, lane);
 }
 
 template <bool B16>
 __device__ __forceinline__ void mlp_body(const MlpArgs& a) {
+  constexpr int V = 0;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -475,7 +486,7 @@ __device__ __forceinline__ void mlp_body(const MlpArgs& a) {
   if ((int)blockIdx.x >= ntiles) return;  // uniform per workgroup, before any LDS-DMA
 
   Pipe p{smem, mlp_slice_max<B16>(), mlp_nbuf<B16>(), a.wimg, 0, wave, lane, a.pose_woff};
-  p.template start<B16>();
+  p.template start<B16, V>();
 
   const float* fold = a.fold;
   float tb_lo[3], tb_hi[3];
@@ -501,7 +512,7 @@ __device__ __forceinline__ void mlp_body(const MlpArgs& a) {
     lookup24(a.pbw32, pose, a.pbounds, a.pX, a.pY, a.pZ, g, init);
 #pragma unroll
     for (int s8 = 0; s8 < 8; ++s8) vemb[s8] = 0.f;
-    bw_mlp<B16, 0>(p, emb, vemb, a.bias, a.pose_boff, fold + 0, fold + 512, A, B, fc, g, lane);
+    bw_mlp<B16, V, 0>(p, emb, vemb, a.bias, a.pose_boff, fold + 0, fold + 512, A, B, fc, g, lane);
     blend_softmax(fc, init, g, bw);
     store_rows(a.pbw_rows, idx, bw, g, valid);
     float xt[3];
@@ -511,28 +522,28 @@ __device__ __forceinline__ void mlp_body(const MlpArgs& a) {
     if constexpr (B16) embed_b<2>(xt, g, 10, emb);
     else embed<16>(xt, g, 10, emb);
     lookup24(a.tbw32, xt, a.tbounds, a.tX, a.tY, a.tZ, g, init);
-    bw_mlp<B16, 9>(p, emb, vemb, a.bias, 0, fold + 256, fold + 768, A, B, fc, g, lane);
+    bw_mlp<B16, V, 9>(p, emb, vemb, a.bias, 0, fold + 256, fold + 768, A, B, fc, g, lane);
     blend_softmax(fc, init, g, bw);
     store_rows(a.tbw_rows, idx, bw, g, valid);
 
     // ---- canonical NeRF (TPoseHuman.calculate_alpha_rgb)
     f32x4 dummy[1];
     const float* bias = a.bias;
-    layer<B16, 18, true>(p, dummy, emb, vemb, A, bias + kBiasOff<9>, g, lane);
-    layer<B16, 19, true>(p, A, emb, vemb, B, bias + kBiasOff<10>, g, lane);
-    layer<B16, 20, true>(p, B, emb, vemb, A, bias + kBiasOff<11>, g, lane);
-    layer<B16, 21, true>(p, A, emb, vemb, B, bias + kBiasOff<12>, g, lane);
-    layer<B16, 22, true>(p, B, emb, vemb, A, bias + kBiasOff<13>, g, lane);
-    layer<B16, 23, true>(p, A, emb, vemb, B, bias + kBiasOff<14>, g, lane);
-    layer<B16, 24, true>(p, B, emb, vemb, A, bias + kBiasOff<15>, g, lane);
-    layer<B16, 25, true>(p, A, emb, vemb, B, bias + kBiasOff<16>, g, lane);
-    layer<B16, 26, false>(p, B, emb, vemb, A, bias + kBiasOff<17>, g, lane);  // feature || alpha
+    layer<B16, V, 18, true>(p, dummy, emb, vemb, A, bias + kBiasOff<9>, g, lane);
+    layer<B16, V, 19, true>(p, A, emb, vemb, B, bias + kBiasOff<10>, g, lane);
+    layer<B16, V, 20, true>(p, B, emb, vemb, A, bias + kBiasOff<11>, g, lane);
+    layer<B16, V, 21, true>(p, A, emb, vemb, B, bias + kBiasOff<12>, g, lane);
+    layer<B16, V, 22, true>(p, B, emb, vemb, A, bias + kBiasOff<13>, g, lane);
+    layer<B16, V, 23, true>(p, A, emb, vemb, B, bias + kBiasOff<14>, g, lane);
+    layer<B16, V, 24, true>(p, B, emb, vemb, A, bias + kBiasOff<15>, g, lane);
+    layer<B16, V, 25, true>(p, A, emb, vemb, B, bias + kBiasOff<16>, g, lane);
+    layer<B16, V, 26, false>(p, B, emb, vemb, A, bias + kBiasOff<17>, g, lane);  // feature || alpha
     const float sigma_raw = __shfl(A[16][0], pl);
-    layer<B16, 27, false>(p, A, emb, vemb, B, fold + 1024, g, lane);  // latent_fc
+    layer<B16, V, 27, false>(p, A, emb, vemb, B, fold + 1024, g, lane);  // latent_fc
     if constexpr (B16) embed_b<1>(dir, g, 4, vemb);
     else embed<8>(dir, g, 4, vemb);
-    layer<B16, 28, true>(p, B, emb, vemb, A, bias + kBiasOff<19>, g, lane);   // view_fc
-    layer<B16, 29, false>(p, A, emb, vemb, B, bias + kBiasOff<20>, g, lane);  // rgb_fc
+    layer<B16, V, 28, true>(p, B, emb, vemb, A, bias + kBiasOff<19>, g, lane);   // view_fc
+    layer<B16, V, 29, false>(p, A, emb, vemb, B, bias + kBiasOff<20>, g, lane);  // rgb_fc
 
     // ---- bbox mask, activations, outputs
     bool inside = true;
@@ -548,6 +559,68 @@ __device__ __forceinline__ void mlp_body(const MlpArgs& a) {
       a.raw[pid] = r;
       a.sigma[idx] = sig;
     }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the last (unused) prefetch
+}
+
+// Density program (V = 1): Network.calculate_alpha (tpose_nerf_network.py:105-135) per kept free
+// point — pose-space blend-weight lookup + BW MLP (latent_index + 1, or novel_pose_bw), softmax,
+// LBS inverse, then TPoseHuman.calculate_alpha (:241-250): NeRF trunk + alpha_fc. The T-pose BW MLP
+// the reference also evaluates there does not reach the returned alpha and is not run; no bbox
+// mask, no activation: alpha_out[id] = the raw alpha_fc output.
+template <bool B16>
+__device__ __forceinline__ void alpha_body(const MlpArgs& a) {
+  constexpr int V = 1;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4;
+  const int pl = lane & 15;
+  float* sA = (float*)(smem + mlp_nbuf<B16>() * mlp_slice_max<B16>());
+  for (int i = tid; i < 384; i += 512) sA[i] = a.A[i];
+
+  const int n = *a.n_kept;
+  const int ntiles = (n + 127) / 128;
+  if ((int)blockIdx.x >= ntiles) return;  // uniform per workgroup, before any LDS-DMA
+
+  Pipe p{smem, mlp_slice_max<B16>(), mlp_nbuf<B16>(), a.wimg, 0, wave, lane, a.pose_woff};
+  p.template start<B16, V>();
+  const float* fold = a.fold;
+
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int idx = tile * 128 + wave * 16 + pl;
+    const bool valid = idx < n;
+    const int pid = a.list[valid ? idx : n - 1];
+    float pose[3];
+    world_to_pose_pt(a.wpts, pid, a.n_pts, a.chunk_pts, a.R, a.Th, pose);
+
+    float emb[16], vemb[8];
+    f32x4 A[17], B[17], fc[2], init[2], bw[2];
+    if constexpr (B16) embed_b<2>(pose, g, 10, emb);
+    else embed<16>(pose, g, 10, emb);
+    lookup24(a.pbw32, pose, a.pbounds, a.pX, a.pY, a.pZ, g, init);
+#pragma unroll
+    for (int s8 = 0; s8 < 8; ++s8) vemb[s8] = 0.f;
+    bw_mlp<B16, V, 0>(p, emb, vemb, a.bias, a.pose_boff, fold + 0, fold + 512, A, B, fc, g, lane);
+    blend_softmax(fc, init, g, bw);
+    float xt[3];
+    lbs_inverse(bw, sA, g, pose, xt);
+
+    if constexpr (B16) embed_b<2>(xt, g, 10, emb);
+    else embed<16>(xt, g, 10, emb);
+    f32x4 dummy[1];
+    const float* bias = a.bias;
+    layer<B16, V, 9, true>(p, dummy, emb, vemb, A, bias + kBiasOff<9>, g, lane);
+    layer<B16, V, 10, true>(p, A, emb, vemb, B, bias + kBiasOff<10>, g, lane);
+    layer<B16, V, 11, true>(p, B, emb, vemb, A, bias + kBiasOff<11>, g, lane);
+    layer<B16, V, 12, true>(p, A, emb, vemb, B, bias + kBiasOff<12>, g, lane);
+    layer<B16, V, 13, true>(p, B, emb, vemb, A, bias + kBiasOff<13>, g, lane);
+    layer<B16, V, 14, true>(p, A, emb, vemb, B, bias + kBiasOff<14>, g, lane);
+    layer<B16, V, 15, true>(p, B, emb, vemb, A, bias + kBiasOff<15>, g, lane);
+    layer<B16, V, 16, true>(p, A, emb, vemb, B, bias + kBiasOff<16>, g, lane);
+    layer<B16, V, 17, false>(p, B, emb, vemb, A, bias + kBiasOff<ANR_L_ALPHA>, g, lane);  // alpha_fc
+    if (valid && g == 0) a.alpha_out[pid] = A[0][0];
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the last (unused) prefetch
 }

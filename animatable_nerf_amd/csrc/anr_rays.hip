@@ -109,7 +109,6 @@ __global__ void k_cam_rays(CamArgs a) {
 }
 
 // ordered compaction of the hit pixels: per-256-pixel counts, k_scan_blocks, scatter
-__device__ __forceinline__ int block_excl_scan_256(int v, int* sh, int& total);
 
 __global__ __launch_bounds__(256) void k_cam_count(CamArgs a) {
   __shared__ int sh[4];
@@ -187,26 +186,42 @@ __global__ __launch_bounds__(256) void k_frontend(FrontArgs a) {
   if (lane == 0) atomicMin((unsigned long long*)&a.chunk_min[ray / a.chunk], (unsigned long long)key);
 }
 
+// (f) mesh path: the prefilter of get_alpha over free points (tpose_nerf_network.py:105-116):
+// pnorm < norm_th (0.1 there) plus the argmin of pnorm over each batchify chunk
+// (aninerf_mesh_renderer.py:14-23, 2048 x 64 points). One wave per 64 consecutive points, so the
+// keep ballots, per-chunk argmin keys and ordered compaction are the render path's, unchanged.
+__global__ __launch_bounds__(256) void k_frontend_pts(FrontArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int grp = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (grp >= a.n_rays) return;
+  const long i = (long)grp * 64 + lane;
+  const bool valid = i < a.n_pts;
+  float pn = 0.0f;
+  if (valid) {
+    float pose[3], lo[3], hi[3];
+    world_to_pose_pt(a.wpts, i, a.n_pts, a.chunk_pts, a.R, a.Th, pose);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) { lo[c] = a.pbounds[c]; hi[c] = a.pbounds[3 + c]; }
+    TriCell cell;
+    tri_cell(pose, lo, hi, a.X, a.Y, a.Z, cell);
+    pn = tri_channel(a.pbw, 25, 24, cell);
+  }
+  const bool keep = valid && pn < a.norm_th;
+  const uint64_t m = __ballot(keep);
+  if (lane == 0) a.mask[grp] = m;
+  const int rc = grp % a.chunk;
+  uint64_t key = valid ? (((uint64_t)__float_as_uint(pn) << 32) | (uint32_t)(rc * 64 + lane)) : ~0ull;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const uint64_t o = __shfl_xor(key, off);
+    key = o < key ? o : key;
+  }
+  if (lane == 0) atomicMin((unsigned long long*)&a.chunk_min[grp / a.chunk], (unsigned long long)key);
+}
+
 // ------------------------------------------------------------------------------------------
 // ordered compaction of kept samples: count (+ forced argmin bit), scan, write
 // ------------------------------------------------------------------------------------------
-__device__ __forceinline__ int block_excl_scan_256(int v, int* sh, int& total) {
-  // 256 threads: wave inclusive scans + wave totals in LDS
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  int x = v;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const int y = __shfl_up(x, off);
-    if (lane >= off) x += y;
-  }
-  if (lane == 63) sh[w] = x;
-  __syncthreads();
-  int base = 0;
-  for (int k = 0; k < w; ++k) base += sh[k];
-  total = sh[0] + sh[1] + sh[2] + sh[3];
-  __syncthreads();
-  return base + x - v;
-}
 
 __global__ __launch_bounds__(256) void k_count(CompactArgs a) {
   __shared__ int sh[4];

@@ -147,6 +147,26 @@ class Scene:
         }
 
 
+def mesh_scene(voxel=0.02, vsize=0.05, inside_frac=0.8, seed=11):
+    """The mesh path's batch (aninerf_mesh_dataset.py:126-174) for the synthetic subject in a rotated
+    and translated world frame: world vertices w = p R^T + Th so that (w - Th) R = p; pbounds /
+    wbounds from the pose / world vertices; the voxel grid over wbounds; a seeded `inside` mask
+    standing in for the training-view mask test (prepare_inside_pts :93-117)."""
+    sc = Scene(vsize=vsize)
+    R = batch_rodrigues(np.array([[0.2, -0.3, 0.1]]))[0].astype(np.float32)
+    Th = np.array([0.1, -0.05, 0.2], np.float32)
+    wverts = (sc.verts.astype(np.float64) @ R.T.astype(np.float64) + Th).astype(np.float32)
+    wbounds = get_bounds(wverts)
+    axes = [np.arange(wbounds[0, c], wbounds[1, c] + voxel, voxel) for c in range(3)]
+    pts = np.stack(np.meshgrid(*axes, indexing='ij'), axis=-1).astype(np.float32)
+    rng = np.random.Generator(np.random.PCG64(seed))
+    inside = (rng.random(pts.shape[:-1]) < inside_frac).astype(np.uint8)
+    return {'pts': pts[None], 'inside': inside[None], 'A': sc.A[None], 'pbw': sc.volume[None],
+            'tbw': sc.volume[None], 'pbounds': sc.bounds[None], 'wbounds': wbounds[None],
+            'tbounds': sc.bounds[None], 'R': R[None], 'Th': Th[None, None],
+            'latent_index': np.array([2]), 'frame_index': np.array([0])}
+
+
 def training_views(verts, n_views=3, H=100, W=100, focal=80.0, dist=3.0, dilate=1):
     """Training cameras + silhouettes for the novel-view visibility filter
     (``tpose_renderer_mmsk.py:14-57``; keys of ``tpose_novel_view_dataset.py:191``): cameras on a

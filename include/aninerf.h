@@ -22,6 +22,10 @@
  *                             tpose_renderer.py:134-152 (msk_sdf / msk_label)
  *   anr_sdf_render_counts / anr_sdf_render_rows   the compact outputs 'resd', 'gradients',
  *                             'msk_sdf', 'msk_label' (sizes known only after the keep mask)
+ *   anr_alpha_points        lib/networks/bw_deform/tpose_nerf_network.py:105-137 Network.get_alpha
+ *                             over the batchify chunks of aninerf_mesh_renderer.py:14-23, 34-36
+ *   anr_mc_count/anr_mc_emit  mcubes.marching_cubes(np.pad(cube, 10), cfg.mesh_th)
+ *                             (aninerf_mesh_renderer.py:38-45; PyMCubes, third-party, not installed)
  *
  * All float tensors are fp32, contiguous, row-major, with the reference's shapes (batch dim 1).
  */
@@ -225,6 +229,36 @@ const int32_t* anr_sdf_render_counts(const void* workspace, int n_rays, const an
 /* copy resd (n',3), gradients (n',3), msk_sdf / msk_label (len) out of the workspace */
 int anr_sdf_render_rows(const void* workspace, int n_rays, const anr_render_opts* o, float* resd, float* gradients,
                         float* msk_sdf, float* msk_label, void* stream);
+
+/* ---- (f) mesh path (lib/networks/renderer/aninerf_mesh_renderer.py) ----------------------
+ * anr_alpha_points: raw alpha (no activation, no bbox mask) of n free world points, zero where the
+ *   pbw prefilter drops the point: pnorm < o->norm_th (0.1 in get_alpha) plus the argmin of pnorm
+ *   over each chunk of o->chunk_pts points (2048 * 64 in the reference; a multiple of 64). Uses
+ *   the pose-space BW MLP (or novel_pose_bw with o->novel_pose), the LBS inverse, the NeRF trunk
+ *   and alpha_fc; o->precision ANR_FP32 (exact fp32 MFMA) or ANR_BF16X3. Frame fields read: A, R,
+ *   Th, pbw(+dims), pbounds, latent_index (bw_latent_index for novel_pose). No host sync.
+ *   anr_alpha_counts: device int32 {kept points} inside the workspace. */
+typedef struct anr_alpha_opts {
+  int chunk_pts;   /* points per reference chunk (2048 * 64) */
+  float norm_th;   /* 0.1 (tpose_nerf_network.py:113) */
+  int novel_pose;  /* cfg.test_novel_pose */
+  int precision;   /* ANR_FP32 or ANR_BF16X3 */
+} anr_alpha_opts;
+size_t anr_alpha_workspace_bytes(long n_pts, const anr_alpha_opts* o, const anr_frame* f);
+int anr_alpha_points(const anr_params* p, const anr_frame* f, const float* wpts, long n_pts, const anr_alpha_opts* o,
+                     float* alpha, void* workspace, size_t ws_bytes, void* stream);
+const int32_t* anr_alpha_counts(const void* workspace);
+/* Marching cubes over vol (X,Y,Z) f32 padded by `pad` zero voxels on every side (virtually):
+ * anr_mc_count writes device int32 {V, T} to counts; anr_mc_emit (same vol / workspace, after the
+ * caller sized the outputs) writes vertices (V,3) f64 in padded index coordinates and triangles
+ * (T,3) int64. A corner is outside iff value <= iso. One vertex per crossing grid edge, numbered in
+ * grid order (C order of the padded grid, then axis x, y, z); triangles per cube in grid order from
+ * the case table of tools/gen_mc_table.py, wound with the normal towards the outside. */
+size_t anr_mc_workspace_bytes(int X, int Y, int Z, int pad);
+int anr_mc_count(const float* vol, int X, int Y, int Z, int pad, double iso, int32_t* counts, void* workspace,
+                 size_t ws_bytes, void* stream);
+int anr_mc_emit(const float* vol, int X, int Y, int Z, int pad, double iso, double* vertices, int64_t* triangles,
+                void* workspace, size_t ws_bytes, void* stream);
 
 /* ---- measurement ----------------------------------------------------------------------
  * When enabled, anr_render_fwd records a hipEvent pair around the fused network kernel (k_mlp)

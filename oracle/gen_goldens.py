@@ -46,7 +46,7 @@ def _install_stubs():
     for name in ['pytorch3d', 'pytorch3d._C', 'pytorch3d.structures', 'pytorch3d.ops',
                  'pytorch3d.ops.knn', 'pytorch3d.ops.packed_to_padded',
                  'pytorch3d.ops.mesh_face_areas_normals', 'pytorch3d.ops.sample_points_from_meshes',
-                 'cv2', 'trimesh', 'termcolor', 'imageio', 'tensorboardX', 'plyfile']:
+                 'cv2', 'trimesh', 'termcolor', 'imageio', 'tensorboardX', 'plyfile', 'mcubes']:
         sys.modules[name] = _Stub(name)
 
 
@@ -532,8 +532,56 @@ def main_mmsk():
     print('mmsk golden written; visible samples per chunk:', out['chunks_visible_per_chunk'])
 
 
+def main_mesh():
+    """G10: the mesh renderer's density volume (lib/networks/renderer/aninerf_mesh_renderer.py:26-41
+    over Network.get_alpha, tpose_nerf_network.py:105-137) in a rotated / translated world frame:
+    (a) the reference render() on a 0.02 m voxel grid with a seeded `inside` mask — the cube it hands
+    to mcubes.marching_cubes is recorded (mcubes itself is not installed: stubbed); (b) its
+    batchify_rays with 4096-point chunks over the inside points plus a trailing chunk of far points
+    (all pnorm >= 0.1: the forced argmin alone) and a 30-point chunk (torch's small-matmul path)."""
+    import torch
+    torch.set_num_threads(1)
+    sys.path.insert(0, REPO)
+    from animatable_nerf_amd.synthetic import init_state_dict, mesh_scene
+    cfg, make_network, make_renderer = import_reference(opts=('vis_posed_mesh', 'True'))
+    import mcubes
+    net = make_network(cfg)
+    sd = init_state_dict({k: tuple(v.shape) for k, v in net.state_dict().items()})
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
+    net.train()
+    renderer = make_renderer(cfg, net)
+    b = mesh_scene(voxel=0.02)
+    batch = {k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in b.items()}
+    seen = {}
+
+    def mc(cube, th):
+        seen['cube'], seen['th'] = np.array(cube), th
+        return np.zeros((0, 3)), np.zeros((0, 3), np.int64)
+
+    mcubes.marching_cubes = mc
+    with torch.no_grad():
+        renderer.render(batch)
+    cube = seen['cube'][10:-10, 10:-10, 10:-10]
+    inside = b['inside'][0].astype(bool)
+    assert np.all(cube[~inside] == 0)
+    pts_in = b['pts'][0][inside]
+    far = pts_in[:4096] + np.float32(5.0)  # far outside the pbw volume: pnorm = border value
+    tail = pts_in[:30] + np.float32(0.001)
+    pts_b = np.concatenate([pts_in[:16 * 4096], far, tail]).astype(np.float32)  # far = chunk 16, tail = 17
+    with torch.no_grad():
+        alpha_b = renderer.batchify_rays(torch.from_numpy(pts_b), lambda x: net.get_alpha(x, batch), net, 4096, batch)
+    out = {k: v for k, v in b.items() if k not in ('pts',)}
+    out.update(mesh_th=seen['th'], alpha_inside=cube[inside].astype(np.float32), pts_b=pts_b,
+               alpha_b=np.asarray(alpha_b, np.float32), chunk_b=4096)
+    np.savez_compressed(os.path.join(OUT, 'g10_mesh.npz'), **out)
+    print('mesh golden written: grid', b['pts'].shape, 'inside', int(inside.sum()), 'nonzero alpha',
+          int((cube != 0).sum()), 'batchify points', len(pts_b))
+
+
 if __name__ == '__main__':
-    if len(sys.argv) > 1 and sys.argv[1] == '--mmsk':
+    if len(sys.argv) > 1 and sys.argv[1] == '--mesh':
+        main_mesh()
+    elif len(sys.argv) > 1 and sys.argv[1] == '--mmsk':
         main_mmsk()
     elif len(sys.argv) > 1 and sys.argv[1] == '--rays':
         main_rays()

@@ -37,11 +37,12 @@ def test_version_and_sizes(lib):
     assert lib.anr_version() == 1
     # 19 weight layers + view/rgb heads, fp32 weight image + padded biases
     # + 9 novel_pose_bw layers (same image as the 9 BW layers)
-    fp32 = 4_767_744 + 2_031_616 + 4 * (4_800 + 2_080)  # fp32 image (+ novel-pose copy) + biases
+    # + alpha_fc alone (layer 30, the mesh path's density program): 64 k-steps x 1 KiB, 16 biases
+    fp32 = 4_767_744 + 2_031_616 + 65_536 + 4 * (4_800 + 2_080 + 16)  # fp32 image (+ novel copy, alpha) + biases
     # bf16x3 image: per layer ceil(in/32) k-steps x out-blocks x 2 KiB (hi + lo fragments)
     ks_ob = [(2, 16), (8, 16), (8, 16), (8, 16), (8, 16), (10, 16), (8, 16), (8, 16), (8, 2),
              (2, 16), (8, 16), (8, 16), (8, 16), (8, 16), (10, 16), (8, 16), (8, 16), (8, 17), (8, 16), (9, 8), (4, 1)]
-    b16 = (sum(k * o for k, o in ks_ob) + sum(k * o for k, o in ks_ob[:9])) * 2048  # + novel-pose copy
+    b16 = (sum(k * o for k, o in ks_ob) + sum(k * o for k, o in ks_ob[:9]) + 8 * 1) * 2048  # + novel copy, alpha
     x6 = 2 * sum(k * o for k, o in ks_ob[:9]) * 3072  # pose-pass bf16x6 image (+ novel-pose copy)
     base16 = (fp32 + 255) // 256 * 256
     assert lib.anr_params_packed_bytes() == (base16 + b16 + 255) // 256 * 256 + x6
