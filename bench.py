@@ -54,9 +54,11 @@ def parse():
     ap.add_argument('--rays', type=int, default=512 * 512)
     ap.add_argument('--cpu-rays', type=int, default=16 * 2048)
     ap.add_argument('--no-cpu', action='store_true')
-    ap.add_argument('--mode', choices=('render', 'train', 'sdf'), default='render',
+    ap.add_argument('--mode', choices=('render', 'train', 'sdf', 'mesh'), default='render',
                     help='render: config 2 (headline); train: config 3/4 training step (1024 rays/GPU); '
-                         'sdf: config 5 sdf_pdf full-frame render')
+                         'sdf: config 5 sdf_pdf full-frame render; mesh: aninerf mesh extraction '
+                         '(get_alpha on the 5 mm voxel grid + marching cubes)')
+    ap.add_argument('--voxel', type=float, default=0.005, help='mesh mode: cfg.voxel_size (aninerf_s9p.yaml:95)')
     ap.add_argument('--sdf-cpu-rays', type=int, default=2048)
     ap.add_argument('--no-exact', action='store_true', help='skip timing the other render precision')
     ap.add_argument('--render-precision', choices=('fp32', 'bf16x3'), default='bf16x3',
@@ -92,6 +94,8 @@ def main():
         return bench_train(args, rank, world, dev)
     if args.mode == 'sdf':
         return bench_sdf(args, rank, world, dev)
+    if args.mode == 'mesh':
+        return bench_mesh(args, rank, world, dev)
 
     sc = synthetic.Scene(vsize=0.025)
     ro, rd = sc.box_rays(args.rays, seed=2 + rank)
@@ -343,6 +347,105 @@ def bench_sdf(args, rank, world, dev):
                                   'sample': f'first {n} rays of the frame, oracle/restate_sdf.py, {dtc:.1f} s'}
         from oracle import restate
         result['psnr_vs_fp32_oracle'] = float(restate.psnr(out['rgb_map'][0, :n].cpu().numpy(), ref['rgb_map'][0].numpy()))
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+# get_alpha per kept point, latent folded: pose-space BW MLP 497,152 MAC + NeRF trunk and alpha_fc
+# (63*256 + 6*256*256 + 319*256 + 256 = 491,264 MAC)
+MAC_NERF_TRUNK = 491_264
+FLOP_PER_KEPT_ALPHA = 2 * (MAC_BW + MAC_NERF_TRUNK)
+
+
+def bench_mesh(args, rank, world, dev):
+    """Mesh extraction (aninerf_mesh_renderer.py:26-63) of one frame per GPU at the reference's
+    voxel size (5 mm): get_alpha over every grid voxel (`inside` all ones: an upper bound of the
+    masked grid the dataset produces), the density volume, device marching cubes. Replicas."""
+    from animatable_nerf_amd import config, network, synthetic
+    from animatable_nerf_amd.renderer_mesh import Renderer, marching_cubes
+    b = synthetic.mesh_scene(voxel=args.voxel, inside_frac=1.01)
+    batch = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in b.items()}
+    net = network.Network()
+    sd = synthetic.init_state_dict({k: tuple(v.shape) for k, v in net.state_dict().items()})
+    network.load_numpy_state(net, sd)
+    net = net.to(dev)
+    cfg = config.load_cfg(opts=['vis_posed_mesh', 'True', 'render_precision', args.render_precision])
+    renderer = Renderer(net, cfg)
+    inside = batch['inside'][0].bool()
+    wpts = batch['pts'][0][inside].contiguous()
+    n = int(wpts.shape[0])
+    iso = 2.95  # raw alpha of the synthetic weights sits near the alpha_fc bias (3); cfg.mesh_th = 5 is empty
+
+    def once():
+        alpha = renderer.alpha_points(wpts, batch)
+        cube = torch.zeros(tuple(inside.shape), device=dev)
+        cube[inside] = alpha
+        return cube
+
+    for _ in range(args.warmup):
+        cube = once()
+        marching_cubes(cube, iso)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * args.steps)]
+    t0 = time.perf_counter()
+    for j in range(args.steps):
+        ev[2 * j].record()
+        alpha = renderer.alpha_points(wpts, batch)
+        ev[2 * j + 1].record()
+        cube = torch.zeros(tuple(inside.shape), device=dev)
+        cube[inside] = alpha
+        verts, tris = marching_cubes(cube, iso)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    dt_max = max_over_ranks(dt, dev, world)
+    alpha_ms = sum(ev[2 * j].elapsed_time(ev[2 * j + 1]) for j in range(args.steps)) / args.steps
+    n_kept = int(renderer._aws[:4].view(torch.int32).item())  # anr_alpha_counts: kept points
+    split = args.render_precision == 'bf16x3'
+    flop_exec = 3 * FLOP_PER_KEPT_ALPHA if split else FLOP_PER_KEPT_ALPHA
+    peak = PEAK_BF16_MFMA_TFLOPS if split else PEAK_FP32_MFMA_TFLOPS
+    achieved = n_kept * flop_exec / (alpha_ms * 1e-3) / 1e12
+    t1 = time.perf_counter()
+    verts, tris = marching_cubes(cube, iso)
+    torch.cuda.synchronize()
+    mc_ms = (time.perf_counter() - t1) * 1e3
+    result = {
+        'metric': 'mesh grid points/s (get_alpha + marching cubes), aninerf_s9p mesh extraction',
+        'value': n * args.steps * world / dt_max, 'unit': 'points/s', 'n_gpus': world, 'steps': args.steps,
+        'warmup': args.warmup, 'ms_per_step': dt_max / args.steps * 1e3, 'higher_is_better': True,
+        'scaling': 'weak', 'vs_baseline': None,
+        'dtype': 'bf16 MFMA operands (hi/lo split), fp32 accumulate' if split else 'fp32', 'data': 'synthetic',
+        'config': {'workload': f'mesh extraction, {args.voxel * 1000:g} mm voxel grid over wbounds, inside = all voxels',
+                   'grid': list(inside.shape), 'points': n, 'kept_fraction': n_kept / n, 'iso': iso,
+                   'vertices': int(verts.shape[0]), 'triangles': int(tris.shape[0]),
+                   'alpha_ms': alpha_ms, 'marching_cubes_ms': mc_ms, 'parallelism': f'replicas{world}'},
+        'roofline': {'bound': 'mfma', 'kernel': 'anr_alpha_points (k_alpha%s dominates)' % ('_b16' if split else ''),
+                     'achieved': achieved, 'peak': peak, 'unit': 'TFLOP/s', 'frac': achieved / peak, 'traffic': None,
+                     'flop_per_kept_executed': flop_exec, 'flop_per_kept_credited': FLOP_PER_KEPT_ALPHA},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        import sys
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+        from oracle import restate
+        threads = min(16, os.cpu_count() or 1)
+        torch.set_num_threads(threads)
+        m = min(16 * 2048 * 64, n)  # 16 reference chunks, ~10 s on 16 host threads
+        P = {k: torch.from_numpy(v) for k, v in sd.items()}
+        cb = {k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in b.items() if k not in ('pts', 'inside')}
+        sub = wpts[:m].cpu()
+        with torch.no_grad():
+            t2 = time.perf_counter()
+            ref = restate.mesh_alpha(P, sub, cb)
+            dtc = time.perf_counter() - t2
+        result['cpu_baseline'] = {'value': m / dtc, 'unit': 'points/s', 'cores': threads, 'kind': 'port',
+                                  'sample': f'first {m} grid points ({m // (2048 * 64)} reference chunks), oracle/restate.py '
+                                            f'mesh_alpha (get_alpha only), {dtc:.1f} s'}
+        result['alpha_max_abs_err_vs_oracle'] = float((alpha[:m].cpu() - ref).abs().max())
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
