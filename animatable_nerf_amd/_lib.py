@@ -21,7 +21,7 @@ EXPORTS = ('anr_near_far', 'anr_params_packed_bytes', 'anr_params_pack', 'anr_re
            'anr_train_workspace_bytes', 'anr_train_fwd', 'anr_train_bwd', 'anr_train_step', 'anr_adam',
            'anr_camera_rays_workspace_bytes', 'anr_camera_rays', 'anr_sdf_render_workspace_bytes', 'anr_sdf_render_fwd', 'anr_sdf_render_counts', 'anr_sdf_render_rows',
            'anr_alpha_workspace_bytes', 'anr_alpha_points', 'anr_alpha_counts', 'anr_mc_workspace_bytes',
-           'anr_mc_count', 'anr_mc_emit',
+           'anr_mc_count', 'anr_mc_emit', 'anr_anim_workspace_bytes', 'anr_anim_step',
            'anr_last_error', 'anr_version')
 
 c_float_p = ctypes.c_void_p
@@ -134,6 +134,10 @@ def load():
                                  ctypes.c_size_t, P]
     lib.anr_mc_emit.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double, P, P, P,
                                 ctypes.c_size_t, P]
+    lib.anr_anim_workspace_bytes.restype = ctypes.c_size_t
+    lib.anr_anim_workspace_bytes.argtypes = [ctypes.c_int]
+    lib.anr_anim_step.argtypes = [ctypes.POINTER(Params), ctypes.c_void_p * NUM_NOVEL_TENSORS, ctypes.POINTER(Frame), P,
+                                  ctypes.c_int, P, ctypes.c_int, ctypes.POINTER(RenderOpts), P, P, ctypes.c_size_t, P]
     lib.anr_profile_enable.argtypes = [ctypes.c_int]
     lib.anr_profile_read.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]
     lib.anr_last_error.restype = ctypes.c_char_p

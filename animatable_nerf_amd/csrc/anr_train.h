@@ -97,6 +97,15 @@ __global__ void k_tr_tpose_bwd(TrainBufs b);
 __global__ void k_tr_softmax_bwd_p(TrainBufs b);
 __global__ void k_tr_latent_grad(const float* dysum, const float* W, int in_ch, int col0, int nout, const float* table,
                                  const int64_t* li, int add, float* dW, float* dtable);
+__global__ void k_an_prep_obs(TrainBufs b, const float* wpts);
+__global__ void k_an_prep_can(TrainBufs b, const float* tpts);
+__global__ void k_an_lbs_fwd(TrainBufs b);
+__global__ void k_an_softmax_p(TrainBufs b);
+__global__ void k_an_select(TrainBufs b, int masked, float norm_th, unsigned long long* amax);
+__global__ void k_an_loss(TrainBufs b, float train_th, const unsigned long long* amax, float* acc, int* rows);
+__global__ void k_an_loss_grads(TrainBufs b, const int* rows, int need_dt);
+__global__ void k_an_set(int* c, int n);
+__global__ void k_an_loss_final(const float* acc, const int* rows, float* loss3);
 __global__ void k_adam(float* p, float* g, float* m, float* v, long n, float lr, float b1, float b2, float eps, float wd,
                        float bc1, float bc2_sqrt, float clip);
 __global__ void k_tr_loss(TrainBufs b, const float* rgb_gt, const uint8_t* mask, float* acc3);

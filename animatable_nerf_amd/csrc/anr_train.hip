@@ -414,4 +414,179 @@ __global__ __launch_bounds__(256) void k_adam(float* p, float* g, float* m, floa
   p[i] -= (lr / bc1) * mi / denom;
 }
 
+// ------------------------------------------------------------------------------------------
+// (f) animation stage (lib/train/trainers/aninerf_animation_trainer.py:33-140): free points, no
+// compaction (every point of a path is processed; n = b.n_kept[0]), frozen network except
+// novel_pose_bw. Buffers are the training executor's (TrainBufs), reused by the two paths.
+// ------------------------------------------------------------------------------------------
+// path 1 (observation space): world -> pose ((x - Th) R, :132-139), gamma(pose), init_pbw and pnorm
+// (pt[3]); wave per point, lane = feature
+__global__ __launch_bounds__(256) void k_an_prep_obs(TrainBufs b, const float* __restrict__ wpts) {
+  const int lane = threadIdx.x & 63;
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int n = *b.n_kept;
+  if (i >= n) return;
+  float pose[3];
+  world_to_pose_pt(wpts, i, n, n, b.R, b.Th, pose);
+  b.Gp[(long)i * 64 + lane] = lane < 63 ? embed_feature(pose, lane, 10) : 0.f;
+  if (lane < 32) {
+    float lo[3], hi[3];
+    for (int c = 0; c < 3; ++c) { lo[c] = b.pbounds[c]; hi[c] = b.pbounds[3 + c]; }
+    TriCell cell;
+    tri_cell(pose, lo, hi, b.pX, b.pY, b.pZ, cell);
+    const float v = lane < 25 ? tri_channel(b.pbw, 25, lane, cell) : 0.f;
+    b.Ip[(long)i * 32 + lane] = lane < 24 ? v : 0.f;
+    if (lane == 24) b.pt[(long)i * 8 + 3] = v;  // pnorm
+  }
+  if (lane == 0) {
+    float* p = b.pt + (long)i * 8;
+    p[0] = pose[0]; p[1] = pose[1]; p[2] = pose[2];
+  }
+}
+
+// path 2 (canonical space): x_T given; gamma(x_T), init_tbw (:82-88)
+__global__ __launch_bounds__(256) void k_an_prep_can(TrainBufs b, const float* __restrict__ tpts) {
+  const int lane = threadIdx.x & 63;
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int n = *b.n_kept;
+  if (i >= n) return;
+  const float tp[3] = {tpts[3 * (long)i], tpts[3 * (long)i + 1], tpts[3 * (long)i + 2]};
+  b.Gt[(long)i * 64 + lane] = lane < 63 ? embed_feature(tp, lane, 10) : 0.f;
+  if (lane < 32) {
+    float lo[3], hi[3];
+    for (int c = 0; c < 3; ++c) { lo[c] = b.tbounds[c]; hi[c] = b.tbounds[3 + c]; }
+    TriCell cell;
+    tri_cell(tp, lo, hi, b.tX, b.tY, b.tZ, cell);
+    b.It[(long)i * 32 + lane] = lane < 24 ? tri_channel(b.tbw, 25, lane, cell) : 0.f;
+  }
+  if (lane == 0) {
+    float* p = b.pt + (long)i * 8;
+    p[4] = tp[0]; p[5] = tp[1]; p[6] = tp[2];
+  }
+}
+
+// path 2: tpose_points_to_pose_points (blend_utils.py:77-90) with the frozen tbw, then gamma(pose)
+// and init_pbw of the posed point
+__global__ __launch_bounds__(256) void k_an_lbs_fwd(TrainBufs b) {
+#pragma clang fp contract(fast)
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int n = *b.n_kept;
+  if (i >= n) return;
+  float Ab[16];
+  for (int m = 0; m < 16; ++m) Ab[m] = 0.f;
+  for (int j = 0; j < 24; ++j) {
+    const float w = b.Bt[(long)i * 24 + j];
+    for (int m = 0; m < 16; ++m) Ab[m] += w * b.A[j * 16 + m];
+  }
+  const float* pt = b.pt + (long)i * 8;
+  const float tp[3] = {pt[4], pt[5], pt[6]};
+  float pose[3];
+  for (int r = 0; r < 3; ++r) pose[r] = (Ab[4 * r] * tp[0] + Ab[4 * r + 1] * tp[1] + Ab[4 * r + 2] * tp[2]) + Ab[4 * r + 3];
+  for (int q = 0; q < 64; ++q) b.Gp[(long)i * 64 + q] = q < 63 ? embed_feature(pose, q, 10) : 0.f;
+  float lo[3], hi[3];
+  for (int r = 0; r < 3; ++r) { lo[r] = b.pbounds[r]; hi[r] = b.pbounds[3 + r]; }
+  TriCell cell;
+  tri_cell(pose, lo, hi, b.pX, b.pY, b.pZ, cell);
+  for (int j = 0; j < 32; ++j) b.Ip[(long)i * 32 + j] = j < 24 ? tri_channel(b.pbw, 25, j, cell) : 0.f;
+}
+
+__global__ __launch_bounds__(256) void k_an_softmax_p(TrainBufs b) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int n = *b.n_kept;
+  if (i >= n) return;
+  float bw[24];
+  softmax24(b.Lp + (long)i * 32, b.Ip + (long)i * 32, bw);
+  for (int j = 0; j < 24; ++j) b.Bp[(long)i * 24 + j] = bw[j];
+}
+
+// float -> order-preserving uint32
+__device__ __forceinline__ uint32_t ord_bits(float f) {
+  const uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+// alpha (path 1: zeroed outside the T-pose bbox or where pnorm >= norm_th, :117-124; path 2: as
+// is), then the argmax key (first index on ties, torch.argmax)
+__global__ __launch_bounds__(256) void k_an_select(TrainBufs b, int masked, float norm_th, unsigned long long* amax) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int n = *b.n_kept;
+  unsigned long long key = 0ull;
+  if (i < n) {
+    float a = b.Alpha[i];
+    if (masked) {
+      const float* pt = b.pt + (long)i * 8;
+      bool inside = true;
+      for (int r = 0; r < 3; ++r) inside = inside && pt[4 + r] > b.tbounds[r] && pt[4 + r] < b.tbounds[3 + r];
+      inside = inside && pt[3] < norm_th;
+      a = inside ? a : 0.f;
+      b.Alpha[i] = a;
+    }
+    key = ((unsigned long long)ord_bits(a) << 32) | (0xffffffffu - (uint32_t)i);
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    const unsigned long long o = __shfl_xor(key, off);
+    key = o > key ? o : key;
+  }
+  if ((threadIdx.x & 63) == 0 && key) atomicMax(amax, key);
+}
+
+// alpha_ind = alpha > train_th plus the argmax (:126-130); smooth-L1 sum and row count (m) into acc
+__global__ __launch_bounds__(256) void k_an_loss(TrainBufs b, float train_th, const unsigned long long* amax,
+                                                 float* acc, int* rows) {
+  __shared__ float sh[4];
+  __shared__ int shc[4];
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int n = *b.n_kept;
+  const int forced = (int)(0xffffffffu - (uint32_t)(*amax & 0xffffffffull));
+  float v = 0.f;
+  int c = 0;
+  if (i < n) {
+    const bool sel = b.Alpha[i] > train_th || i == forced;
+    b.sigma[i] = sel ? 1.f : 0.f;
+    if (sel) {
+      c = 1;
+      for (int j = 0; j < 24; ++j) {
+        const float x = b.Bp[(long)i * 24 + j] - b.Bt[(long)i * 24 + j];
+        const float ax = fabsf(x);
+        v += ax < 1.f ? 0.5f * x * x : ax - 0.5f;
+      }
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    v += __shfl_xor(v, off);
+    c += __shfl_xor(c, off);
+  }
+  if ((threadIdx.x & 63) == 0) { sh[threadIdx.x >> 6] = v; shc[threadIdx.x >> 6] = c; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    atomicAdd(acc, sh[0] + sh[1] + sh[2] + sh[3]);
+    atomicAdd(rows, shc[0] + shc[1] + shc[2] + shc[3]);
+  }
+}
+
+// d loss / d pbw rows and d tbw rows (smooth_l1_loss mean over m x 24) scattered per point
+__global__ __launch_bounds__(256) void k_an_loss_grads(TrainBufs b, const int* rows, int need_dt) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int n = *b.n_kept;
+  if (i >= n) return;
+  const bool sel = b.sigma[i] > 0.f;
+  const float sc = 1.0f / (24.0f * (float)(*rows));
+  for (int j = 0; j < 24; ++j) {
+    const float x = b.Bp[(long)i * 24 + j] - b.Bt[(long)i * 24 + j];
+    const float d = sel ? (fabsf(x) < 1.f ? x : (x > 0.f ? 1.f : -1.f)) * sc : 0.f;
+    b.dBp[(long)i * 24 + j] = d;
+    if (need_dt) b.dBt[(long)i * 24 + j] = -d;
+  }
+}
+
+__global__ void k_an_set(int* c, int n) { c[0] = n; }
+
+__global__ void k_an_loss_final(const float* acc, const int* rows, float* loss3) {
+  const float l0 = acc[0] / (24.0f * (float)rows[0]);
+  const float l1 = acc[1] / (24.0f * (float)rows[1]);
+  loss3[0] = l0 + l1;
+  loss3[1] = l0;
+  loss3[2] = l1;
+}
+
 }  // namespace anr

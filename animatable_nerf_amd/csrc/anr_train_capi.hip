@@ -170,55 +170,64 @@ TrainBufs bufs(const TLayout& T, char* ws, const anr_frame* f, const float* ray_
 #define PT(i) (p->t[i])
 #define FOLD(k) ((const float*)(ws + T.L.fold) + 256 * (k))
 
-// BW MLP forward over n samples (tpose_nerf_network.py:55-77); H = 8 x [N][256], logits [N][32]
-int bw_forward(Exec& e, const anr_params* p, const float* G, float* H, float* logits, long N, const float* fold0,
+// BW MLP forward over n samples (tpose_nerf_network.py:55-77); H = 8 x [N][256], logits [N][32].
+// W = the 19 tensors of one blend-weight field in state_dict order: [bw_latent, bw_linears.{0..7}
+// .{weight,bias}, bw_fc.{weight,bias}] (p->t + 27, or p->novel for novel_pose_bw).
+int bw_forward(Exec& e, const float* const* W, const float* G, float* H, float* logits, long N, const float* fold0,
                const float* fold5) {
   const long S = N * 256;
-  ANR_TRY(e.fwd(H, 256, 256, PT(28), 191, fold0, true, G, 64, 63, 0));
+  ANR_TRY(e.fwd(H, 256, 256, W[1], 191, fold0, true, G, 64, 63, 0));
   for (int l = 1; l < 8; ++l) {
     const float* Xp = H + (l - 1) * S;
     if (l == 5) {
-      ANR_TRY(e.fwd(H + l * S, 256, 256, PT(38), 447, fold5, true, G, 64, 63, 0, Xp, 256, 256, 191));
+      ANR_TRY(e.fwd(H + l * S, 256, 256, W[11], 447, fold5, true, G, 64, 63, 0, Xp, 256, 256, 191));
     } else {
-      ANR_TRY(e.fwd(H + l * S, 256, 256, PT(28 + 2 * l), 256, PT(29 + 2 * l), true, Xp, 256, 256, 0));
+      ANR_TRY(e.fwd(H + l * S, 256, 256, W[1 + 2 * l], 256, W[2 + 2 * l], true, Xp, 256, 256, 0));
     }
   }
-  return e.fwd(logits, 32, 24, PT(44), 256, PT(45), false, H + 7 * S, 256, 256, 0);
+  return e.fwd(logits, 32, 24, W[17], 256, W[18], false, H + 7 * S, 256, 256, 0);
 }
 
-// BW MLP backward from d logits; accumulates weight/bias grads; dG (+)= input-gamma gradient if given.
+// BW MLP backward from d logits; accumulates weight/bias grads into g (same table order as W; NULL:
+// input gradient only, a frozen field); dG (+)= input-gamma gradient if given.
 // ysum: 2 x 256 scratch for the latent-column gradients of layers 0 and 5.
-int bw_backward(Exec& e, const anr_params* p, float* const* g, const float* G, const float* H, const float* dlog,
+int bw_backward(Exec& e, const float* const* W, float* const* g, const float* G, const float* H, const float* dlog,
                 float* dA, float* dB, float* dG, long N, float* ysum, const int64_t* li, int add, hipStream_t s) {
   const long S = N * 256;
   // bw_fc
-  ANR_TRY(e.wgrad(g[44], 256, 0, 24, dlog, 32, H + 7 * S, 256, 256));
-  ANR_TRY(e.colsum(dlog, 32, 24, g[45]));
-  ANR_TRY(e.xgrad(dA, 256, 256, dlog, 32, 24, PT(44), 256, 0, H + 7 * S, 256, false));
+  if (g) {
+    ANR_TRY(e.wgrad(g[17], 256, 0, 24, dlog, 32, H + 7 * S, 256, 256));
+    ANR_TRY(e.colsum(dlog, 32, 24, g[18]));
+  }
+  ANR_TRY(e.xgrad(dA, 256, 256, dlog, 32, 24, W[17], 256, 0, H + 7 * S, 256, false));
   float* cur = dA;
   float* nxt = dB;
   for (int l = 7; l >= 0; --l) {
-    const int wi = 28 + 2 * l, bi = wi + 1;
+    const int wi = 1 + 2 * l, bi = wi + 1;
     const int in_ch = l == 0 ? 191 : (l == 5 ? 447 : 256);
     if (l == 0 || l == 5) {
-      float* ys = ysum + (l == 5 ? 256 : 0);
-      if (hipMemsetAsync(ys, 0, 256 * 4, s) != hipSuccess) return fail(ANR_E_HIP, "memset");
-      ANR_TRY(e.colsum(cur, 256, 256, ys));
-      hipLaunchKernelGGL(k_tr_latent_grad, dim3(257), dim3(128), 0, s, (const float*)ys, PT(wi), in_ch, 63, 256,
-                         PT(27), li, add, g[wi], g[27]);
-      ANR_TRY(check_launch("k_tr_latent_grad"));
-      // bias grad = same column sum
-      ANR_TRY(e.colsum(cur, 256, 256, g[bi]));
-      ANR_TRY(e.wgrad(g[wi], in_ch, 0, 256, cur, 256, G, 64, 63));
-      if (dG) ANR_TRY(e.xgrad(dG, 64, 63, cur, 256, 256, PT(wi), in_ch, 0, nullptr, 0, true));
+      if (g) {
+        float* ys = ysum + (l == 5 ? 256 : 0);
+        if (hipMemsetAsync(ys, 0, 256 * 4, s) != hipSuccess) return fail(ANR_E_HIP, "memset");
+        ANR_TRY(e.colsum(cur, 256, 256, ys));
+        hipLaunchKernelGGL(k_tr_latent_grad, dim3(257), dim3(128), 0, s, (const float*)ys, W[wi], in_ch, 63, 256,
+                           W[0], li, add, g[wi], g[0]);
+        ANR_TRY(check_launch("k_tr_latent_grad"));
+        // bias grad = same column sum
+        ANR_TRY(e.colsum(cur, 256, 256, g[bi]));
+        ANR_TRY(e.wgrad(g[wi], in_ch, 0, 256, cur, 256, G, 64, 63));
+      }
+      if (dG) ANR_TRY(e.xgrad(dG, 64, 63, cur, 256, 256, W[wi], in_ch, 0, nullptr, 0, true));
       if (l == 5) {
-        ANR_TRY(e.wgrad(g[wi], in_ch, 191, 256, cur, 256, H + 4 * S, 256, 256));
-        ANR_TRY(e.xgrad(nxt, 256, 256, cur, 256, 256, PT(wi), in_ch, 191, H + 4 * S, 256, false));
+        if (g) ANR_TRY(e.wgrad(g[wi], in_ch, 191, 256, cur, 256, H + 4 * S, 256, 256));
+        ANR_TRY(e.xgrad(nxt, 256, 256, cur, 256, 256, W[wi], in_ch, 191, H + 4 * S, 256, false));
       }
     } else {
-      ANR_TRY(e.colsum(cur, 256, 256, g[bi]));
-      ANR_TRY(e.wgrad(g[wi], 256, 0, 256, cur, 256, H + (l - 1) * S, 256, 256));
-      ANR_TRY(e.xgrad(nxt, 256, 256, cur, 256, 256, PT(wi), 256, 0, H + (l - 1) * S, 256, false));
+      if (g) {
+        ANR_TRY(e.colsum(cur, 256, 256, g[bi]));
+        ANR_TRY(e.wgrad(g[wi], 256, 0, 256, cur, 256, H + (l - 1) * S, 256, 256));
+      }
+      ANR_TRY(e.xgrad(nxt, 256, 256, cur, 256, 256, W[wi], 256, 0, H + (l - 1) * S, 256, false));
     }
     if (l > 0) {
       float* t = cur;
@@ -246,13 +255,13 @@ int train_forward(const anr_params* p, const anr_frame* f, const float* ray_o, c
   // pose-space BW MLP (latent_index + 1), softmax + LBS, T-pose BW MLP (latent 0)
   {
     PoseScope ps(e);
-    ANR_TRY(bw_forward(e, p, b.Gp, (float*)(ws + T.Hp), b.Lp, N, FOLD(0), FOLD(2)));
+    ANR_TRY(bw_forward(e, p->t + 27, b.Gp, (float*)(ws + T.Hp), b.Lp, N, FOLD(0), FOLD(2)));
   }
   if (n > 0) {
     hipLaunchKernelGGL(k_tr_softmax_lbs, dim3(g1), dim3(256), 0, s, b);
     ANR_TRY(check_launch("k_tr_softmax_lbs"));
   }
-  ANR_TRY(bw_forward(e, p, b.Gt, (float*)(ws + T.Ht), b.Lt, N, FOLD(1), FOLD(3)));
+  ANR_TRY(bw_forward(e, p->t + 27, b.Gt, (float*)(ws + T.Ht), b.Lt, N, FOLD(1), FOLD(3)));
   if (n > 0) {
     hipLaunchKernelGGL(k_tr_softmax_t, dim3(g1), dim3(256), 0, s, b);
     ANR_TRY(check_launch("k_tr_softmax_t"));
@@ -365,13 +374,134 @@ int train_backward(const anr_params* p, float* const* g, const anr_frame* f, con
   ANR_TRY(check_launch("k_tr_rows_bwd"));
   hipLaunchKernelGGL(k_tr_softmax_bwd_t, dim3(g1), dim3(256), 0, s, b);
   ANR_TRY(check_launch("k_tr_softmax_bwd_t"));
-  ANR_TRY(bw_backward(e, p, g, b.Gt, Ht, b.dLt, dA, dB, b.dGt, N, ysum, nullptr, 0, s));  // bw_latent row 0
+  ANR_TRY(bw_backward(e, p->t + 27, g + 27, b.Gt, Ht, b.dLt, dA, dB, b.dGt, N, ysum, nullptr, 0, s));  // bw_latent row 0
   // x_T gradient (gamma + init_tbw lookup) -> LBS -> d pbw; pose BW backward (latent row li + 1)
   hipLaunchKernelGGL(k_tr_tpose_bwd, dim3(g1), dim3(256), 0, s, b);
   ANR_TRY(check_launch("k_tr_tpose_bwd"));
   hipLaunchKernelGGL(k_tr_softmax_bwd_p, dim3(g1), dim3(256), 0, s, b);
   ANR_TRY(check_launch("k_tr_softmax_bwd_p"));
   return ANR_OK;
+}
+
+// ---- (f) animation stage: aninerf_animation_trainer.NetworkWrapper.forward + backward ----------
+struct ALayout {
+  size_t counts, amax, acc, pt, Gp, Ip, Lp, Bp, lbs, Gt, It, Lt, Bt, Hp, Ht, Hn, Alpha, sel;
+  size_t dBp, dBt, dLp, dLt, dIt, dGt, dA, dB, ysum, fold, total;
+};
+
+ALayout alayout(long N) {
+  ALayout T{};
+  size_t o = 0;
+  auto take = [&](size_t bytes) {
+    const size_t at = o;
+    o = align256(o + bytes);
+    return at;
+  };
+  const size_t n = (size_t)N;
+  T.counts = take(16); T.amax = take(8); T.acc = take(16);
+  T.pt = take(n * 32); T.Gp = take(n * 256); T.Ip = take(n * 128); T.Lp = take(n * 128); T.Bp = take(n * 96);
+  T.lbs = take(n * 64); T.Gt = take(n * 256); T.It = take(n * 128); T.Lt = take(n * 128); T.Bt = take(n * 96);
+  T.Hp = take(n * 256 * 8 * 4); T.Ht = take(n * 256 * 8 * 4); T.Hn = take(n * 256 * 2 * 4);
+  T.Alpha = take(n * 4); T.sel = take(n * 4);
+  T.dBp = take(n * 96); T.dBt = take(n * 96); T.dLp = take(n * 128); T.dLt = take(n * 128); T.dIt = take(n * 128);
+  T.dGt = take(n * 256); T.dA = take(n * 1024); T.dB = take(n * 1024); T.ysum = take(8 * 256 * 4);
+  T.fold = take(1280 * 4);
+  T.total = o;
+  return T;
+}
+
+TrainBufs abufs(const ALayout& T, char* ws, const anr_frame* f) {
+  TrainBufs b{};
+  b.n_kept = (const int*)(ws + T.counts);
+  b.R = f->R; b.Th = f->Th; b.A = f->A;
+  b.pbw = f->pbw; b.pbounds = f->pbounds; b.tbw = f->tbw; b.tbounds = f->tbounds;
+  b.pX = f->pbw_dims[0]; b.pY = f->pbw_dims[1]; b.pZ = f->pbw_dims[2];
+  b.tX = f->tbw_dims[0]; b.tY = f->tbw_dims[1]; b.tZ = f->tbw_dims[2];
+  b.pt = (float*)(ws + T.pt); b.Gp = (float*)(ws + T.Gp); b.Ip = (float*)(ws + T.Ip); b.Lp = (float*)(ws + T.Lp);
+  b.Bp = (float*)(ws + T.Bp); b.lbs = (float*)(ws + T.lbs); b.Gt = (float*)(ws + T.Gt); b.It = (float*)(ws + T.It);
+  b.Lt = (float*)(ws + T.Lt); b.Bt = (float*)(ws + T.Bt); b.Alpha = (float*)(ws + T.Alpha);
+  b.sigma = (float*)(ws + T.sel);
+  b.dBp = (float*)(ws + T.dBp); b.dBt = (float*)(ws + T.dBt); b.dLp = (float*)(ws + T.dLp);
+  b.dLt = (float*)(ws + T.dLt); b.dIt = (float*)(ws + T.dIt); b.dGt = (float*)(ws + T.dGt);
+  return b;
+}
+
+#define AFOLD(k) ((const float*)(ws + T.fold) + 256 * (k))
+
+// TPoseHuman.calculate_alpha (tpose_nerf_network.py:241-250) over the n points of Gt -> b.Alpha
+int nerf_alpha_fwd(Exec& e, const anr_params* p, const TrainBufs& b, float* Hn, long N) {
+  const long S = N * 256;
+  float* cur = Hn;
+  float* prv = Hn + S;
+  ANR_TRY(e.fwd(cur, 256, 256, PT(1), 63, PT(2), true, b.Gt, 64, 63, 0));
+  for (int l = 1; l < 8; ++l) {
+    float* t = prv;
+    prv = cur;
+    cur = t;
+    if (l == 5) ANR_TRY(e.fwd(cur, 256, 256, PT(11), 319, PT(12), true, b.Gt, 64, 63, 0, prv, 256, 256, 63));
+    else ANR_TRY(e.fwd(cur, 256, 256, PT(1 + 2 * l), 256, PT(2 + 2 * l), true, prv, 256, 256, 0));
+  }
+  return e.fwd(b.Alpha, 1, 1, PT(17), 256, PT(18), false, cur, 256, 256, 0);
+}
+
+int anim_path(const anr_params* p, float* const* grads, const anr_frame* f, const float* pts, int n, bool obs,
+              const anr_render_opts* o, char* ws, const ALayout& T, hipStream_t s, Exec& e) {
+  e.n = n;
+  TrainBufs b = abufs(T, ws, f);
+  int* counts = (int*)(ws + T.counts);
+  unsigned long long* amax = (unsigned long long*)(ws + T.amax);
+  float* acc = (float*)(ws + T.acc);
+  const int g1 = (n + 255) / 256, g4 = (n + 3) / 4;
+  const long N = n;
+  float* Hp = (float*)(ws + T.Hp);
+  float* Ht = (float*)(ws + T.Ht);
+  float* dA = (float*)(ws + T.dA);
+  float* dB = (float*)(ws + T.dB);
+  float* ysum = (float*)(ws + T.ysum);
+  hipLaunchKernelGGL(k_an_set, dim3(1), dim3(1), 0, s, counts, n);
+  if (hipMemsetAsync(amax, 0, 8, s) != hipSuccess) return fail(ANR_E_HIP, "memset");
+  if (obs) {
+    // ppts_to_tpose (aninerf_animation_trainer.py:63-99)
+    hipLaunchKernelGGL(k_an_prep_obs, dim3(g4), dim3(256), 0, s, b, pts);
+    {
+      PoseScope ps(e);
+      ANR_TRY(bw_forward(e, p->novel, b.Gp, Hp, b.Lp, N, AFOLD(0), AFOLD(2)));
+    }
+    hipLaunchKernelGGL(k_tr_softmax_lbs, dim3(g1), dim3(256), 0, s, b);
+    ANR_TRY(bw_forward(e, p->t + 27, b.Gt, Ht, b.Lt, N, AFOLD(1), AFOLD(3)));
+    hipLaunchKernelGGL(k_tr_softmax_t, dim3(g1), dim3(256), 0, s, b);
+    ANR_TRY(nerf_alpha_fwd(e, p, b, (float*)(ws + T.Hn), N));
+  } else {
+    // tpose_to_ppts (:102-131)
+    hipLaunchKernelGGL(k_an_prep_can, dim3(g4), dim3(256), 0, s, b, pts);
+    ANR_TRY(bw_forward(e, p->t + 27, b.Gt, Ht, b.Lt, N, AFOLD(1), AFOLD(3)));
+    hipLaunchKernelGGL(k_tr_softmax_t, dim3(g1), dim3(256), 0, s, b);
+    ANR_TRY(nerf_alpha_fwd(e, p, b, (float*)(ws + T.Hn), N));
+    hipLaunchKernelGGL(k_an_lbs_fwd, dim3(g1), dim3(256), 0, s, b);
+    {
+      PoseScope ps(e);
+      ANR_TRY(bw_forward(e, p->novel, b.Gp, Hp, b.Lp, N, AFOLD(0), AFOLD(2)));
+    }
+    hipLaunchKernelGGL(k_an_softmax_p, dim3(g1), dim3(256), 0, s, b);
+  }
+  const int k = obs ? 0 : 1;
+  hipLaunchKernelGGL(k_an_select, dim3(g1), dim3(256), 0, s, b, obs ? 1 : 0, o->norm_th, amax);
+  hipLaunchKernelGGL(k_an_loss, dim3(g1), dim3(256), 0, s, b, o->train_th, (const unsigned long long*)amax, acc + k,
+                     counts + 1 + k);
+  hipLaunchKernelGGL(k_an_loss_grads, dim3(g1), dim3(256), 0, s, b, (const int*)(counts + 1 + k), obs ? 1 : 0);
+  ANR_TRY(check_launch("anim forward"));
+  if (obs) {
+    // tbw0 depends on novel_pose_bw through x_T: frozen T-pose BW MLP (input gradient only),
+    // gamma + init_tbw lookup, LBS inverse -> d pbw (k_tr_tpose_bwd)
+    hipLaunchKernelGGL(k_tr_softmax_bwd_t, dim3(g1), dim3(256), 0, s, b);
+    if (hipMemsetAsync(b.dGt, 0, (size_t)n * 64 * 4, s) != hipSuccess) return fail(ANR_E_HIP, "memset");
+    ANR_TRY(bw_backward(e, p->t + 27, nullptr, b.Gt, Ht, b.dLt, dA, dB, b.dGt, N, ysum, nullptr, 0, s));
+    hipLaunchKernelGGL(k_tr_tpose_bwd, dim3(g1), dim3(256), 0, s, b);
+  }
+  hipLaunchKernelGGL(k_tr_softmax_bwd_p, dim3(g1), dim3(256), 0, s, b);
+  ANR_TRY(check_launch("anim backward"));
+  PoseScope ps(e);
+  return bw_backward(e, p->novel, grads, b.Gp, Hp, b.dLp, dA, dB, nullptr, N, ysum + 512, f->bw_latent_index, 0, s);
 }
 
 }  // namespace
@@ -425,7 +555,7 @@ int anr_train_bwd(const anr_params* p, float* const* grads, const anr_frame* f, 
   const long N = (long)n_rays * 64;
   float* ysum = (float*)(ws + T.ysum);
   PoseScope ps(e);
-  ANR_TRY(bw_backward(e, p, grads, (const float*)(ws + T.Gp), (const float*)(ws + T.Hp), (const float*)(ws + T.dLp),
+  ANR_TRY(bw_backward(e, p->t + 27, grads + 27, (const float*)(ws + T.Gp), (const float*)(ws + T.Hp), (const float*)(ws + T.dLp),
                       (float*)(ws + T.dA), (float*)(ws + T.dB), nullptr, N, ysum + 1024, f->latent_index, 1, s));
   return ANR_OK;
 }
@@ -468,8 +598,56 @@ int anr_train_step(const anr_params* p, float* const* grads, const anr_frame* f,
   if (e.n <= 0) return ANR_OK;
   float* ysum = (float*)(ws + T.ysum);
   PoseScope ps(e);
-  return bw_backward(e, p, grads, (const float*)(ws + T.Gp), (const float*)(ws + T.Hp), (const float*)(ws + T.dLp),
+  return bw_backward(e, p->t + 27, grads + 27, (const float*)(ws + T.Gp), (const float*)(ws + T.Hp), (const float*)(ws + T.dLp),
                      (float*)(ws + T.dA), (float*)(ws + T.dB), nullptr, N, ysum + 1024, f->latent_index, 1, s);
+}
+
+size_t anr_anim_workspace_bytes(int n_points) {
+  if (n_points <= 0) return 0;
+  return alayout(n_points).total;
+}
+
+int anr_anim_step(const anr_params* p, float* const* grads, const anr_frame* f, const float* wpts, int n_obs,
+                  const float* tpts, int n_can, const anr_render_opts* o, float* loss3, void* workspace,
+                  size_t ws_bytes, void* stream) {
+  if (!p || !grads || !f || !wpts || !tpts || !o || !loss3 || !workspace) return fail(ANR_E_ARG, "anr_anim_step: NULL argument");
+  if (n_obs <= 0 || n_can <= 0) return fail(ANR_E_ARG, "anr_anim_step: empty point set");
+  for (int i = 0; i < ANR_NUM_TENSORS; ++i)
+    if (!p->t[i]) return fail(ANR_E_ARG, "anr_anim_step: NULL parameter tensor");
+  for (int i = 0; i < ANR_NUM_NOVEL_TENSORS; ++i)
+    if (!p->novel[i] || !grads[i]) return fail(ANR_E_ARG, "anr_anim_step: the novel_pose_bw tensors and their grads are required");
+  if (!f->A || !f->R || !f->Th || !f->pbw || !f->tbw || !f->pbounds || !f->tbounds || !f->bw_latent_index)
+    return fail(ANR_E_ARG, "anr_anim_step: NULL frame tensor");
+  for (int i = 0; i < 3; ++i)
+    if (f->pbw_dims[i] <= 0 || f->tbw_dims[i] <= 0) return fail(ANR_E_ARG, "anr_anim_step: bad volume dims");
+  if (o->precision < ANR_FP32 || o->precision > ANR_BF16X3) return fail(ANR_E_ARG, "anr_anim_step: bad precision");
+  const int N = n_obs > n_can ? n_obs : n_can;
+  const ALayout T = alayout(N);
+  if (ws_bytes < T.total) return fail(ANR_E_WORKSPACE, "anr_anim_step: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  char* ws = (char*)workspace;
+  if (hipMemsetAsync(ws + T.counts, 0, 16, s) != hipSuccess || hipMemsetAsync(ws + T.acc, 0, 16, s) != hipSuccess)
+    return fail(ANR_E_HIP, "memset");
+  // folded biases: pose pass from novel_pose_bw (bw_latent_index), T-pose pass from bw_latent row 0
+  PrepArgs pa{};
+  pa.np = 0; pa.nt = 0;
+  pa.w_bw0 = p->t[28]; pa.b_bw0 = p->t[29]; pa.w_bw5 = p->t[38]; pa.b_bw5 = p->t[39];
+  pa.bw_latent = p->t[27]; pa.w_lat = p->t[21]; pa.b_lat = p->t[22]; pa.nf_latent = p->t[0];
+  pa.latent_index = f->latent_index ? f->latent_index : f->bw_latent_index;  // only the unused nf fold reads it
+  pa.fold = (float*)(ws + T.fold);
+  pa.novel = 1;
+  pa.n_latent = p->novel[0];
+  pa.nw_bw0 = p->novel[1]; pa.nb_bw0 = p->novel[2];
+  pa.nw_bw5 = p->novel[11]; pa.nb_bw5 = p->novel[12];
+  pa.bw_latent_index = f->bw_latent_index;
+  hipLaunchKernelGGL(k_prep, dim3(1), dim3(256), 0, s, pa);
+  ANR_TRY(check_launch("k_prep(anim)"));
+  Exec e{s, 0, (o->precision == ANR_BF16 || o->precision == ANR_BF16_ALL) ? 1 : 0, o->precision == ANR_BF16 ? 1 : 0};
+  ANR_TRY(anim_path(p, grads, f, wpts, n_obs, true, o, ws, T, s, e));
+  ANR_TRY(anim_path(p, grads, f, tpts, n_can, false, o, ws, T, s, e));
+  hipLaunchKernelGGL(k_an_loss_final, dim3(1), dim3(1), 0, s, (const float*)(ws + T.acc),
+                     (const int*)(ws + T.counts) + 1, loss3);
+  return check_launch("k_an_loss_final");
 }
 
 int anr_adam(float* param, float* grad, float* exp_avg, float* exp_avg_sq, long n, float lr, float beta1, float beta2,

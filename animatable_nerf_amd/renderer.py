@@ -140,7 +140,7 @@ class Renderer:
         return p
 
     def _workspace(self, attr, nbytes, dev):
-        ws = getattr(self, attr)
+        ws = getattr(self, attr, None)
         if ws is None or ws.numel() < nbytes or ws.device != dev:
             ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
             setattr(self, attr, ws)

@@ -24,6 +24,7 @@
  *                             'msk_sdf', 'msk_label' (sizes known only after the keep mask)
  *   anr_alpha_points        lib/networks/bw_deform/tpose_nerf_network.py:105-137 Network.get_alpha
  *                             over the batchify chunks of aninerf_mesh_renderer.py:14-23, 34-36
+ *   anr_anim_step           lib/train/trainers/aninerf_animation_trainer.py:33-140 (forward + backward)
  *   anr_mc_count/anr_mc_emit  mcubes.marching_cubes(np.pad(cube, 10), cfg.mesh_th)
  *                             (aninerf_mesh_renderer.py:38-45; PyMCubes, third-party, not installed)
  *
@@ -176,6 +177,24 @@ int anr_train_step(const anr_params* p, float* const* grads, const anr_frame* f,
                    const anr_render_out* out, float* loss3, void* workspace, size_t ws_bytes, void* stream);
 int anr_adam(float* param, float* grad, float* exp_avg, float* exp_avg_sq, long n, float lr, float beta1,
              float beta2, float eps, float weight_decay, int step, float clip_value, void* stream);
+
+/* ---- (f) animation stage (lib/train/trainers/aninerf_animation_trainer.py:33-140) -------------
+ * anr_anim_step: NetworkWrapper.forward + loss.backward of the second training stage, which fits
+ *   novel_pose_bw with every other parameter frozen. wpts (n_obs,3): points drawn in wbounds
+ *   (observation space, world frame; get_sampling_points :143-160); tpts (n_can,3): points drawn in
+ *   tbounds (canonical). Path 1 (ppts_to_tpose :63-99): pbw0 = novel_pose_bw at the posed point,
+ *   tbw0 = the frozen blend-weight MLP at its LBS-inverse T-pose point (differentiable through x_T),
+ *   rows where alpha (zeroed outside tbounds or pnorm >= o->norm_th) > o->train_th plus the argmax.
+ *   Path 2 (tpose_to_ppts :102-131): tbw1 frozen at the canonical point, pbw1 = novel_pose_bw at its
+ *   forward-LBS posed point, rows alpha > train_th plus the argmax. loss3 = {bw_loss0 + bw_loss1,
+ *   bw_loss0, bw_loss1} (smooth_l1 means, device). ACCUMULATES the gradients of the 19
+ *   novel_pose_bw tensors into grads (anr_params.novel order). Reads frame A, R, Th, pbw, pbounds,
+ *   tbw, tbounds, bw_latent_index; o->precision as for training (ANR_BF16 keeps the pose-space
+ *   novel_pose_bw MLP fp32). No host sync. */
+size_t anr_anim_workspace_bytes(int n_points);
+int anr_anim_step(const anr_params* p, float* const* grads, const anr_frame* f, const float* wpts, int n_obs,
+                  const float* tpts, int n_can, const anr_render_opts* o, float* loss3, void* workspace,
+                  size_t ws_bytes, void* stream);
 
 /* ---- sdf_pdf variant (config 5, anisdf_pdf_network.py) ------------------------------------
  * Parameters: the 63 tensors of anisdf_pdf_network.Network's state_dict, in order:

@@ -578,8 +578,62 @@ def main_mesh():
           int((cube != 0).sum()), 'batchify points', len(pts_b))
 
 
+ANIM_N = 4096  # points per path (the reference's get_sampling_points hardcodes 1024 * 64)
+ANIM_GRADS = ('bw_latent.weight', 'bw_linears.0.weight', 'bw_linears.0.bias', 'bw_linears.4.bias',
+              'bw_linears.5.bias', 'bw_linears.7.weight', 'bw_linears.7.bias', 'bw_fc.weight', 'bw_fc.bias')
+
+
+def main_anim():
+    """G11: one forward + backward of the animation stage (lib/train/trainers/
+    aninerf_animation_trainer.py NetworkWrapper, configs aninerf_animation True) in a rotated world
+    frame. The module's get_sampling_points is replaced by the same formula (:143-160) at
+    ANIM_N points per path with the torch.rand draws recorded; loss, the two bw losses and the
+    gradients of novel_pose_bw tensors (bw_latent row bw_latent_index) are stored."""
+    import torch
+    torch.set_num_threads(1)
+    sys.path.insert(0, REPO)
+    from animatable_nerf_amd.synthetic import init_state_dict, mesh_scene
+    cfg, make_network, _ = import_reference(opts=('aninerf_animation', 'True'))
+    import importlib
+    at = importlib.import_module('lib.train.trainers.aninerf_animation_trainer')
+    net = make_network(cfg)
+    sd = init_state_dict({k: tuple(v.shape) for k, v in net.state_dict().items()})
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
+    net.train()
+    wrapper = at.NetworkWrapper(net)
+    b = mesh_scene(voxel=0.1)
+    b.pop('pts')
+    b.pop('inside')
+    b['bw_latent_index'] = np.array([7])
+    batch = {k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in b.items()}
+    draws = []
+
+    def sampling(bounds):
+        sh = bounds.shape
+        min_xyz, max_xyz = bounds[:, 0], bounds[:, 1]
+        vals = [torch.rand([sh[0], ANIM_N]) for _ in range(3)]
+        draws.append(torch.stack(vals, dim=2).numpy().copy())
+        vals = torch.stack(vals, dim=2).to(bounds.device)
+        return (max_xyz - min_xyz)[:, None] * vals + min_xyz[:, None]
+
+    at.get_sampling_points = sampling
+    torch.manual_seed(5)
+    ret, loss, stats, _ = wrapper(batch)
+    loss.backward()
+    grads = {'grad_' + k: net.novel_pose_bw.state_dict(keep_vars=True)[k].grad.numpy().copy() for k in ANIM_GRADS}
+    grads['grad_bw_latent.weight'] = grads['grad_bw_latent.weight'][7]
+    out = dict(b, wvals=draws[0], tvals=draws[1], loss=loss.item(), bw_loss0=stats['bw_loss0'].item(),
+               bw_loss1=stats['bw_loss1'].item(), norm_th=cfg.norm_th, train_th=cfg.train_th,
+               m0=len(ret['pbw0']), **grads)
+    assert all(np.all(np.isfinite(v)) for v in grads.values())
+    np.savez_compressed(os.path.join(OUT, 'g11_anim.npz'), **out)
+    print('anim golden written: loss', out['loss'], 'rows path 1', out['m0'])
+
+
 if __name__ == '__main__':
-    if len(sys.argv) > 1 and sys.argv[1] == '--mesh':
+    if len(sys.argv) > 1 and sys.argv[1] == '--anim':
+        main_anim()
+    elif len(sys.argv) > 1 and sys.argv[1] == '--mesh':
         main_mesh()
     elif len(sys.argv) > 1 and sys.argv[1] == '--mmsk':
         main_mmsk()
