@@ -383,18 +383,26 @@ __global__ __launch_bounds__(256) void k_tr_tpose_bwd(TrainBufs b) {
 // latent columns folded into the bias (row = li[0] + add when li, else add):
 //   d table[row][k] += sum_n dysum[n] W[n][col0+k];  d W[n][col0+k] += dysum[n] table[row][k]
 // (dysum = column sum over samples of the layer's d pre-activation)
-__global__ void k_tr_latent_grad(const float* dysum, const float* W, int in_ch, int col0, int nout, const float* table,
-                                 const int64_t* li, int add, float* dW, float* dtable) {
-  const int k = threadIdx.x;  // 128
+// grid = nout + 128 blocks of 128 threads: blocks < nout update one dW row, block nout + k reduces
+// the 128-wide table column k over the nout outputs
+__global__ __launch_bounds__(128) void k_tr_latent_grad(const float* dysum, const float* W, int in_ch, int col0,
+                                                        int nout, const float* table, const int64_t* li, int add,
+                                                        float* dW, float* dtable) {
   const long row = (li ? li[0] : 0) + add;
   if ((int)blockIdx.x < nout) {
+    const int k = threadIdx.x;
     const int nn = blockIdx.x;
     dW[(long)nn * in_ch + col0 + k] += dysum[nn] * table[row * 128 + k];
-  } else {
-    float acc = 0.f;
-    for (int nn = 0; nn < nout; ++nn) acc += dysum[nn] * W[(long)nn * in_ch + col0 + k];
-    dtable[row * 128 + k] += acc;
+    return;
   }
+  __shared__ float sh[2];
+  const int k = blockIdx.x - nout;
+  float acc = 0.f;
+  for (int nn = threadIdx.x; nn < nout; nn += 128) acc += dysum[nn] * W[(long)nn * in_ch + col0 + k];
+  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) dtable[row * 128 + k] += sh[0] + sh[1];
 }
 
 // clip_grad_value_(clip) + torch.optim.Adam step (decoupled bias corrections as in torch)

@@ -210,7 +210,7 @@ int bw_backward(Exec& e, const float* const* W, float* const* g, const float* G,
         float* ys = ysum + (l == 5 ? 256 : 0);
         if (hipMemsetAsync(ys, 0, 256 * 4, s) != hipSuccess) return fail(ANR_E_HIP, "memset");
         ANR_TRY(e.colsum(cur, 256, 256, ys));
-        hipLaunchKernelGGL(k_tr_latent_grad, dim3(257), dim3(128), 0, s, (const float*)ys, W[wi], in_ch, 63, 256,
+        hipLaunchKernelGGL(k_tr_latent_grad, dim3(256 + 128), dim3(128), 0, s, (const float*)ys, W[wi], in_ch, 63, 256,
                            W[0], li, add, g[wi], g[0]);
         ANR_TRY(check_launch("k_tr_latent_grad"));
         // bias grad = same column sum
@@ -334,7 +334,7 @@ int train_backward(const anr_params* p, float* const* g, const anr_frame* f, con
     if (hipMemsetAsync(ys, 0, 256 * 4, s) != hipSuccess) return fail(ANR_E_HIP, "memset");
     ANR_TRY(e.colsum(dLat, 256, 256, ys));
     ANR_TRY(e.colsum(dLat, 256, 256, g[22]));
-    hipLaunchKernelGGL(k_tr_latent_grad, dim3(257), dim3(128), 0, s, (const float*)ys, PT(21), 384, 256, 256, PT(0),
+    hipLaunchKernelGGL(k_tr_latent_grad, dim3(256 + 128), dim3(128), 0, s, (const float*)ys, PT(21), 384, 256, 256, PT(0),
                        f->latent_index, 0, g[21], g[0]);
     ANR_TRY(check_launch("k_tr_latent_grad(nf_latent)"));
   }

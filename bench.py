@@ -54,10 +54,11 @@ def parse():
     ap.add_argument('--rays', type=int, default=512 * 512)
     ap.add_argument('--cpu-rays', type=int, default=16 * 2048)
     ap.add_argument('--no-cpu', action='store_true')
-    ap.add_argument('--mode', choices=('render', 'train', 'sdf', 'mesh'), default='render',
+    ap.add_argument('--mode', choices=('render', 'train', 'sdf', 'mesh', 'anim'), default='render',
                     help='render: config 2 (headline); train: config 3/4 training step (1024 rays/GPU); '
                          'sdf: config 5 sdf_pdf full-frame render; mesh: aninerf mesh extraction '
-                         '(get_alpha on the 5 mm voxel grid + marching cubes)')
+                         '(get_alpha on the 5 mm voxel grid + marching cubes); anim: animation-stage '
+                         'training step (2 x 65,536 points, novel_pose_bw)')
     ap.add_argument('--voxel', type=float, default=0.005, help='mesh mode: cfg.voxel_size (aninerf_s9p.yaml:95)')
     ap.add_argument('--sdf-cpu-rays', type=int, default=2048)
     ap.add_argument('--no-exact', action='store_true', help='skip timing the other render precision')
@@ -96,6 +97,8 @@ def main():
         return bench_sdf(args, rank, world, dev)
     if args.mode == 'mesh':
         return bench_mesh(args, rank, world, dev)
+    if args.mode == 'anim':
+        return bench_anim(args, rank, world, dev)
 
     sc = synthetic.Scene(vsize=0.025)
     ro, rd = sc.box_rays(args.rays, seed=2 + rank)
@@ -446,6 +449,53 @@ def bench_mesh(args, rank, world, dev):
                                   'sample': f'first {m} grid points ({m // (2048 * 64)} reference chunks), oracle/restate.py '
                                             f'mesh_alpha (get_alpha only), {dtc:.1f} s'}
         result['alpha_max_abs_err_vs_oracle'] = float((alpha[:m].cpu() - ref).abs().max())
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def bench_anim(args, rank, world, dev):
+    """Animation stage (aninerf_animation_trainer.py): one step = 65,536 observation-space + 65,536
+    canonical points (get_sampling_points), forward + backward of both paths (anr_anim_step), RCCL
+    mean all-reduce of the novel_pose_bw gradient blob (N > 1), clip + Adam. Weak scaling."""
+    from animatable_nerf_amd import config, network, synthetic
+    from animatable_nerf_amd.trainer_anim import AnimationStep, sample_unit
+    cfg = config.defaults()
+    cfg.aninerf_animation = True
+    cfg.train_precision = args.precision
+    b = synthetic.mesh_scene(voxel=0.1)
+    b['bw_latent_index'] = np.array([7])
+    batch = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in b.items() if k not in ('pts', 'inside')}
+    net = network.Network(cfg)
+    sd = synthetic.init_state_dict({k: tuple(v.shape) for k, v in net.state_dict().items()})
+    network.load_numpy_state(net, sd)
+    net = net.to(dev)
+    st = AnimationStep(net, cfg)
+    gen = torch.Generator().manual_seed(rank)
+    draws = [(sample_unit(generator=gen), sample_unit(generator=gen)) for _ in range(4)]
+    for j in range(args.warmup):
+        st.step(batch, *draws[j % 4])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for j in range(args.steps):
+        st.step(batch, *draws[j % 4])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt_max = max_over_ranks(time.perf_counter() - t0, dev, world)
+    pts = 2 * 65536
+    result = {
+        'metric': 'animation-stage points/s (2 x 65,536 sampled points per step, novel_pose_bw training)',
+        'value': pts * args.steps * world / dt_max, 'unit': 'points/s', 'n_gpus': world, 'steps': args.steps,
+        'warmup': args.warmup, 'ms_per_step': dt_max / args.steps * 1e3, 'higher_is_better': True,
+        'scaling': 'weak', 'vs_baseline': None, 'dtype': args.precision, 'data': 'synthetic',
+        'config': {'workload': 'aninerf animation stage step (forward + backward of both paths, Adam)',
+                   'points_per_step': pts, 'parallelism': f'dp{world} (RCCL mean all-reduce of the novel_pose_bw blob)'},
+        'roofline': None, 'loss_last_step': st.loss3.cpu().tolist(),
+    }
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
