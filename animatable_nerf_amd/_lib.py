@@ -12,6 +12,9 @@ import torch  # noqa: F401  (must be loaded before the library, see module docst
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, 'libaninerf_hip.so')
+# kernel experiments (tools/): an alternative build of the same C-ABI, e.g. with other -D options
+if os.environ.get('ANR_LIB_PATH'):
+    LIB_PATH = os.environ['ANR_LIB_PATH']
 NUM_TENSORS = 46
 NUM_NOVEL_TENSORS = 19
 NUM_SDF_TENSORS = 63

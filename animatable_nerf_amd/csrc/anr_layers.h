@@ -148,9 +148,13 @@ __host__ __device__ inline int layer_col(const LayerDesc& d, int t, int g) {
 //                32s + (j < 4 ? 4h + j : 16 + 4h + j - 4), i.e. the two accumulators of the
 //                previous layer as they sit in the lane (no data movement);
 //   EMB / VEMB : feature 32s + 8h + j.
-// Per k-step, per out-block: [hi: 64 lanes x 16 B][lo: 64 lanes x 16 B] = 2 KiB; a k-step is the
-// staging slice (OB x 2 KiB <= 34 KiB).
+// Per k-step, per out-block: [hi: 64 lanes x 16 B][lo: 64 lanes x 16 B] = 2 KiB; a k-step of the
+// first 16 out-blocks is the staging slice (<= 32 KiB). A layer wider than 16 out-blocks (feature_fc
+// || alpha_fc, 17) stores its extra blocks after the main part, [k-step][tail block], and stages
+// them as one more slice after its k-steps, so a ring slot stays 32 KiB.
 __host__ __device__ constexpr int ks32(int i) { return layer_ksteps(i) / 8; }
+__host__ __device__ constexpr int b16_main_ob(int i) { return layer_desc_all(i).ob < 16 ? layer_desc_all(i).ob : 16; }
+__host__ __device__ constexpr int b16_tail_ob(int i) { return layer_desc_all(i).ob - b16_main_ob(i); }
 __host__ __device__ constexpr int b16_layer_bytes(int i) { return ks32(i) * layer_desc_all(i).ob * 2048; }
 #define ANR_B16_LAYERS 31  // layers 0..30 (incl. the novel_pose_bw copy 21..29, alpha_fc 30)
 __host__ __device__ constexpr int b16_layer_offset(int i) {
@@ -200,15 +204,23 @@ __host__ __device__ inline int b16_col(const LayerDesc& d, int t, int h, int j) 
 
 __host__ __device__ constexpr int packed_bytes_all() { return x6_base() + x6_bytes(); }
 
-// LDS of the fused kernel: a ring of staging buffers of the largest slice + the 24 joint transforms.
-// fp32 kernel: 2 x (8 k-steps x 5 chunks x 1 KiB). bf16 kernel: 4 x 34 KiB (a bf16x3 k-step of 17
-// out-blocks x 2 KiB; bf16x6 k-steps are staged as groups of <= 8 out-blocks x 3 KiB = 24 KiB), so
-// three slices are in flight while one is consumed.
+// LDS of the fused kernel: a ring of staging buffers of the largest slice, the 24 joint transforms
+// and the bias table (mlp_bias_floats, every program entry's bias, filled once per launch so no
+// global load sits between the staging loads). fp32 kernel: 2 x (8 k-steps x 5 chunks x 1 KiB).
+// bf16 kernel: 4 x 32 KiB (a bf16x3 k-step of 16 out-blocks x 2 KiB; bf16x6 k-steps are staged as
+// groups of <= 8 out-blocks x 3 KiB = 24 KiB), so three slices are in flight while one is consumed.
 template <bool B16>
-__host__ __device__ constexpr int mlp_slice_max() { return B16 ? 17 * 2048 : 8 * 5 * 1024; }
+__host__ __device__ constexpr int mlp_slice_max() { return B16 ? 16 * 2048 : 8 * 5 * 1024; }
 template <bool B16>
-__host__ __device__ constexpr int mlp_nbuf() { return B16 ? 4 : 2; }
+__host__ __device__ constexpr int mlp_nbuf() { return B16 ? 4 : 3; }
+// LDS layout: [bias table][24 joint transforms, T-pose bounds][ring]. The table sits at LDS address 0 so every
+// bias read is one base register + an immediate offset (< 64 KiB); the ring starts 256-B aligned.
+// bias-table floats of the render program (the larger of the two programs, anr_mlp_body.h)
+#define ANR_BIAS_TABLE_FLOATS 6880
+__host__ __device__ constexpr int mlp_sa_off() { return ANR_BIAS_TABLE_FLOATS * 4; }
+// after the joint transforms: the T-pose bounds (6 floats), read once per tile from LDS
+__host__ __device__ constexpr int mlp_ring_off() { return (mlp_sa_off() + 24 * 16 * 4 + 32 + 255) / 256 * 256; }
 template <bool B16>
-__host__ __device__ constexpr int mlp_lds_bytes() { return mlp_nbuf<B16>() * mlp_slice_max<B16>() + 24 * 16 * 4; }
+__host__ __device__ constexpr int mlp_lds_bytes() { return mlp_ring_off() + mlp_nbuf<B16>() * mlp_slice_max<B16>(); }
 
 }  // namespace anr

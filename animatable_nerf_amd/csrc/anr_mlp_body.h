@@ -9,9 +9,9 @@
 //   T-pose blend-weight lookup + BW MLP (tbw, for the loss) tpose_nerf_network.py:169-174
 //   gamma(x_T) -> NeRF 8x256 MLP, alpha/feature/latent/view/rgb heads   :252-275
 //   T-pose bbox mask, sigmoid, 1-exp(-relu(sigma) dist)     :186-212
-// Activations never leave registers: the 16x16x4 f32 MFMA accumulator of one layer is the B
-// operand of the next (anr_layers.h). Weights stream through LDS in 8-k-step slices (8-40 KiB),
-// double-buffered with global_load_lds, one slice stream across layers and tiles.
+// Activations never leave registers: the MFMA accumulator of one layer is the B operand of the
+// next (anr_layers.h). Weights stream through an LDS ring of slices (LDS-DMA, Pipe), one slice
+// stream across layers and tiles; biases sit in an LDS table filled once per launch.
 #pragma once
 #include <type_traits>
 
@@ -32,6 +32,14 @@ __device__ __forceinline__ void static_for(F&& f) {
 
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+// slice certification halfway through the previous slice (Pipe::mid) instead of at slice entry
+#ifndef ANR_MIDSYNC
+#define ANR_MIDSYNC 1
+#endif
+// LDS fragment reads in flight ahead of the MFMAs (bf16x3 layers)
+#ifndef ANR_FRAG_PF
+#define ANR_FRAG_PF 1
+#endif
 
 // The per-tile layer program, variant V:
 //   V = 0 (render): entries 0..8 the pose-space BW MLP, 9..17 the T-pose BW MLP (layers 0..8
@@ -59,7 +67,7 @@ __host__ __device__ constexpr int prog_nobg(int e) { return (layer_desc_all(prog
 template <bool B16, int V>
 __host__ __device__ constexpr int prog_slices(int e) {
   return prog_mode<B16>(e) == 2   ? ks32(prog_layer<V>(e)) * prog_nobg<V>(e)
-         : prog_mode<B16>(e) == 1 ? ks32(prog_layer<V>(e))
+         : prog_mode<B16>(e) == 1 ? ks32(prog_layer<V>(e)) + (b16_tail_ob(prog_layer<V>(e)) > 0 ? 1 : 0)
                                   : layer_ksteps(prog_layer<V>(e)) / ANR_KSLICE;
 }
 template <int V>
@@ -68,9 +76,11 @@ __host__ __device__ constexpr int x6_group_obs(int e, int gidx) {
 }
 template <bool B16, int V>
 __host__ __device__ constexpr int prog_slice_kb(int e, int q) {
-  return prog_mode<B16>(e) == 2   ? x6_group_obs<V>(e, q % prog_nobg<V>(e)) * 3
-         : prog_mode<B16>(e) == 1 ? layer_desc_all(prog_layer<V>(e)).ob * 2
-                                  : layer_chunks(prog_layer<V>(e)) * ANR_KSLICE;
+  return prog_mode<B16>(e) == 2 ? x6_group_obs<V>(e, q % prog_nobg<V>(e)) * 3
+         : prog_mode<B16>(e) == 1
+             ? (q < ks32(prog_layer<V>(e)) ? b16_main_ob(prog_layer<V>(e)) * 2
+                                          : b16_tail_ob(prog_layer<V>(e)) * ks32(prog_layer<V>(e)) * 2)
+             : layer_chunks(prog_layer<V>(e)) * ANR_KSLICE;
 }
 template <bool B16, int V>
 __host__ __device__ constexpr int prog_slice_off(int e, int q) {
@@ -78,7 +88,7 @@ __host__ __device__ constexpr int prog_slice_off(int e, int q) {
              ? x6_base() + x6_layer_offset(prog_layer<V>(e)) +
                    ((q / prog_nobg<V>(e)) * layer_desc_all(prog_layer<V>(e)).ob + 8 * (q % prog_nobg<V>(e))) * 3072
          : prog_mode<B16>(e) == 1
-             ? b16_base() + b16_layer_offset(prog_layer<V>(e)) + q * layer_desc_all(prog_layer<V>(e)).ob * 2048
+             ? b16_base() + b16_layer_offset(prog_layer<V>(e)) + q * b16_main_ob(prog_layer<V>(e)) * 2048
              : layer_offset(prog_layer<V>(e)) + q * layer_chunks(prog_layer<V>(e)) * ANR_KSLICE * 1024;
 }
 // loads per wave for a slice (every wave issues the same count, see Pipe::stage)
@@ -101,7 +111,7 @@ __host__ __device__ constexpr int prog_advance(int e, int q, int d) {
 template <bool B16, int V>
 __host__ __device__ constexpr int prog_later_loads(int e, int q) {
   int n = 0;
-  for (int d = 1; d <= mlp_nbuf<B16>() - 2; ++d) {
+  for (int d = 1; d <= mlp_nbuf<B16>() - 2 - ANR_MIDSYNC; ++d) {
     const int eq = prog_advance<B16, V>(e, q, d);
     n += prog_slice_loads<B16, V>(eq / 1024, eq % 1024);
   }
@@ -127,18 +137,28 @@ struct Pipe {
 
   // issue the HBM/L2 -> LDS copy of `kb` KiB at byte `off` of the packed image into ring slot `buf`;
   // every wave issues exactly `loads` 1-KiB pieces (pieces past the end repeat the last one: same
-  // bytes to the same place), so the per-wave vmcnt bookkeeping is a compile-time constant
+  // bytes to the same place), so the per-wave vmcnt bookkeeping is a compile-time constant.
+  // The DMA is issued by inline asm, not __builtin_amdgcn_global_load_lds: with the builtin the
+  // compiler cannot tell which LDS bytes a pending DMA writes and puts `s_waitcnt vmcnt(0)` before
+  // the first ds_read after it, which drains the whole ring (every slice still in flight) once per
+  // slice. Hidden from the compiler, the only waits on the stream are ours (wait_vmcnt in next());
+  // the compiler's own vmcnt waits stay correct, only stricter (loads return in order).
   __device__ __forceinline__ void stage(int off, int kb, int loads, int buf) {
-    unsigned char* dst = lds + buf * smax;
+    const unsigned dst = (unsigned)(uintptr_t)(lds + buf * smax);
     // launder the base so the per-slice addresses are formed here, not hoisted out of the tile
     // loop (hundreds of loop-invariant 64-bit addresses otherwise spill)
     const unsigned char* w = wimg;
     asm volatile("" : "+s"(w));
+#ifdef ANR_EXP_NODMA
+    return;  // timing experiment only: no weight stream (results are garbage)
+#endif
     for (int i = 0; i < loads; ++i) {
       int piece = wave + 8 * i;
       piece = piece < kb ? piece : kb - 1;
-      __builtin_amdgcn_global_load_lds((const void*)(w + off + piece * 1024 + lane * 16),
-                                       (lds_void*)(dst + piece * 1024), 16, 0, 0);
+      const unsigned char* src = w + off + piece * 1024 + lane * 16;
+      const unsigned m0 = dst + piece * 1024;
+      asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(m0)
+                   : "memory");
     }
   }
 
@@ -148,7 +168,7 @@ struct Pipe {
     stage(off + (prog_pose(E) ? pose_woff : 0), prog_slice_kb<B16, V>(E, Q), prog_slice_loads<B16, V>(E, Q), buf);
   }
 
-  // prologue: slices 0 .. nbuf-2 of the program
+  // prologue: slices 0 .. nbuf-2 of the program; with ANR_MIDSYNC slice 0 is certified here
   template <bool B16, int V>
   __device__ __forceinline__ void start() {
     static_for<0, mlp_nbuf<B16>() - 1>([&](auto d) {
@@ -156,27 +176,58 @@ struct Pipe {
       stage_slice<B16, V, eq / 1024, eq % 1024>(decltype(d)::value);
     });
     cur = 0;
+    if constexpr (ANR_MIDSYNC) {
+      wait_vmcnt<prog_later_loads<B16, V>(0, 0)>();
+      __syncthreads();
+    }
   }
 
-  // Enter slice Q of program entry E: wait for it (its own loads; the barrier covers the other
-  // waves'), then refill the slot freed by the previous slice with the slice nbuf-1 ahead.
+  // Enter slice Q of program entry E.
+  //   ANR_MIDSYNC = 0: wait for it (its own loads; the barrier covers the other waves'), then
+  //   refill the slot freed by the previous slice with the slice nbuf-1 ahead.
+  //   ANR_MIDSYNC = 1: it was certified by mid() of the previous slice: no wait, no barrier, so the
+  //   first MFMAs of a slice follow the last ones of the previous slice without a pipe bubble.
   template <bool B16, int V, int E, int Q>
-  __device__ __forceinline__ const unsigned char* next() {
-    constexpr int NB = mlp_nbuf<B16>();
-    constexpr int eq = prog_advance<B16, V>(E, Q, NB - 1);
-    wait_vmcnt<prog_later_loads<B16, V>(E, Q)>();
-    __syncthreads();
-    int slot = cur + NB - 1;
-    slot = slot >= NB ? slot - NB : slot;
-    stage_slice<B16, V, eq / 1024, eq % 1024>(slot);
-    const unsigned char* r = lds + cur * smax;
-    cur = cur + 1 >= NB ? 0 : cur + 1;
-    return r;
+  __device__ __forceinline__ const unsigned char* enter() {
+    if constexpr (!ANR_MIDSYNC) {
+      constexpr int NB = mlp_nbuf<B16>();
+      constexpr int eq = prog_advance<B16, V>(E, Q, NB - 1);
+      wait_vmcnt<prog_later_loads<B16, V>(E, Q)>();
+      __syncthreads();
+      int slot = cur + NB - 1;
+      slot = slot >= NB ? slot - NB : slot;
+      stage_slice<B16, V, eq / 1024, eq % 1024>(slot);
+    }
+    return lds + cur * smax;
   }
+  // ANR_MIDSYNC: called halfway through slice (E, Q), while its MFMAs are in flight: certify the next
+  // slice (own loads landed + barrier: everyone's landed, and everyone is past the previous slice),
+  // then refill the previous slice's slot with the slice nbuf-1 ahead.
+  template <bool B16, int V, int E, int Q>
+  __device__ __forceinline__ void mid() {
+    if constexpr (ANR_MIDSYNC) {
+      constexpr int NB = mlp_nbuf<B16>();
+      constexpr int e1 = prog_advance<B16, V>(E, Q, 1);
+      constexpr int eq = prog_advance<B16, V>(E, Q, NB - 1);
+      wait_vmcnt<prog_later_loads<B16, V>(e1 / 1024, e1 % 1024)>();
+#ifndef ANR_EXP_NOBAR
+      __syncthreads();
+#endif
+      int slot = cur + NB - 1;
+      slot = slot >= NB ? slot - NB : slot;
+      stage_slice<B16, V, eq / 1024, eq % 1024>(slot);
+    }
+  }
+  __device__ __forceinline__ void leave() { cur = cur + 1 >= nbuf ? 0 : cur + 1; }
 };
 
 // x -> hi = bf16(x), lo = bf16(x - hi)   (RNE both)
 __device__ __forceinline__ void split8(const float (&x)[8], bf16x8& hi, bf16x8& lo) {
+#ifdef ANR_EXP_NOSPLIT
+#pragma unroll
+  for (int j = 0; j < 8; ++j) hi[j] = lo[j] = (__bf16)x[j];  // timing experiment only
+  return;
+#endif
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const __bf16 h = (__bf16)x[j];
@@ -198,19 +249,56 @@ __device__ __forceinline__ void split8x3(const float (&x)[8], bf16x8& hi, bf16x8
   }
 }
 
+// LDS bias table: program entry e's biases (ob x 16 floats) at float offset prog_bias_off<V>(e)
+template <int V>
+__host__ __device__ constexpr int prog_bias_off(int e) {
+  int o = 0;
+  for (int k = 0; k < e; ++k) o += layer_desc_all(prog_layer<V>(k)).ob * 16;
+  return o;
+}
+static_assert(prog_bias_off<0>(prog_len<0>()) == ANR_BIAS_TABLE_FLOATS, "bias table size (anr_layers.h)");
+static_assert(prog_bias_off<1>(prog_len<1>()) <= ANR_BIAS_TABLE_FLOATS, "bias table size (anr_layers.h)");
+
+// Fill the bias table once per launch (before the first barrier of the slice stream). Sources:
+// the packed bias section, the novel_pose_bw copy for the pose pass (pose_boff), and the per-frame
+// folds (bw0/bw5 pose and T-pose, latent_fc) for the entries whose latent columns were folded.
+template <int V>
+__device__ __forceinline__ void fill_bias_table(const MlpArgs& a, float* __restrict__ sb, int tid) {
+  static_for<0, prog_len<V>()>([&](auto ee) {
+    constexpr int e = decltype(ee)::value;
+    constexpr int L = prog_layer<V>(e);
+    constexpr int n = layer_desc_all(L).ob * 16;
+    constexpr int boff = bias_offset(L);  // constexpr: evaluated by the compiler, not per launch
+    constexpr int toff = prog_bias_off<V>(e);
+    const float* src;
+    if constexpr (e < 9) {
+      src = L == 0 ? a.fold + 0 : L == 5 ? a.fold + 512 : a.bias + a.pose_boff + boff;
+    } else if constexpr (V == 0 && e < 18) {
+      src = L == 0 ? a.fold + 256 : L == 5 ? a.fold + 768 : a.bias + boff;
+    } else {
+      src = L == 18 ? a.fold + 1024 : a.bias + boff;
+    }
+    for (int i = tid; i < n; i += 512) sb[toff + i] = src[i];
+  });
+}
+
 // One MLP layer (program entry E): out = W * src + bias (acc layout), k-steps from its segments.
 template <bool B16, int V, int E, bool RELU, int NIN, int NOUT>
 __device__ __forceinline__ void layer(Pipe& p, const f32x4 (&in)[NIN], const float (&emb)[16], const float (&vemb)[8],
-                                      f32x4 (&out)[NOUT], const float* __restrict__ bias, int g, int lane) {
+                                      f32x4 (&out)[NOUT], const float* __restrict__ sbias, int g, int lane) {
   constexpr int L = prog_layer<V>(E);
   constexpr LayerDesc D = layer_desc_all(L);
   static_assert(NOUT >= D.ob, "output array too small");
-  const float* bptr = bias + 4 * g;
-  asm volatile("" : "+v"(bptr));  // keep the bias addresses local to the layer (see Pipe::stage)
-  static_for<0, D.ob>([&](auto ob) {
-    constexpr int o = decltype(ob)::value;
-    out[o] = *(const f32x4*)(bptr + o * 16);
-  });
+  // accumulators start at the bias; read right after the layer's first slice barrier, so the
+  // compiler cannot hoist the reads (64 registers) into the previous layer
+  constexpr int BOFF = prog_bias_off<V>(E);
+  auto init_bias = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    static_for<0, D.ob>([&](auto ob) {
+      constexpr int o = decltype(ob)::value;
+      out[o] = *(const f32x4*)(sbias + BOFF + o * 16 + 4 * g);
+    });
+  };
   if constexpr (prog_mode<B16>(E) != 0) {
     // bf16x3 (mode 1): per k-step of 32 one hi/lo split of the B fragment, per out-block 2 A reads,
     // 3 MFMAs; bf16x6 (mode 2): hi/mid/lo, 3 A reads, 6 MFMAs (smallest terms first)
@@ -220,7 +308,10 @@ __device__ __forceinline__ void layer(Pipe& p, const f32x4 (&in)[NIN], const flo
     static_for<0, KS>([&](auto t) {
       constexpr int tt = decltype(t)::value;
       const unsigned char* buf = nullptr;
-      if constexpr (!X6) buf = p.template next<B16, V, E, tt>();
+      if constexpr (!X6) {
+        buf = p.template enter<B16, V, E, tt>();
+        if constexpr (tt == 0) init_bias();
+      }
       constexpr int seg = tt < K0 ? 0 : 1;
       constexpr int ts = tt < K0 ? tt : tt - K0;
       constexpr int kind = D.seg[seg].kind;
@@ -244,7 +335,9 @@ __device__ __forceinline__ void layer(Pipe& p, const f32x4 (&in)[NIN], const flo
         constexpr int NOBG = prog_nobg<V>(E);
         static_for<0, D.ob>([&](auto ob) {
           constexpr int o = decltype(ob)::value;
-          if constexpr (o % 8 == 0) buf = p.template next<B16, V, E, tt * NOBG + o / 8>();
+          constexpr int SQ = tt * NOBG + o / 8;  // the slice of this out-block group
+          if constexpr (o % 8 == 0) buf = p.template enter<B16, V, E, SQ>();
+          if constexpr (tt == 0 && o == 0) init_bias();
           const bf16x8 ah = *(const bf16x8*)(buf + (o % 8) * 3072 + lane * 16);
           const bf16x8 am = *(const bf16x8*)(buf + (o % 8) * 3072 + 1024 + lane * 16);
           const bf16x8 al = *(const bf16x8*)(buf + (o % 8) * 3072 + 2048 + lane * 16);
@@ -254,20 +347,71 @@ __device__ __forceinline__ void layer(Pipe& p, const f32x4 (&in)[NIN], const flo
           out[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bm, out[o], 0, 0, 0);
           out[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bh, out[o], 0, 0, 0);
           out[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, out[o], 0, 0, 0);
+          constexpr int GOB = x6_group_obs<V>(E, o / 8);
+          if constexpr (o % 8 == (GOB - 1) / 2) p.template mid<B16, V, E, SQ>();
+          if constexpr (o % 8 == GOB - 1) p.leave();
         });
       } else {
         bf16x8 bh, bl;
         split8(x, bh, bl);
-        static_for<0, D.ob>([&](auto ob) {
-          constexpr int o = decltype(ob)::value;
-          const bf16x8 ah = *(const bf16x8*)(buf + o * 2048 + lane * 16);
-          const bf16x8 al = *(const bf16x8*)(buf + o * 2048 + 1024 + lane * 16);
-          out[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, out[o], 0, 0, 0);
-          out[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, out[o], 0, 0, 0);
-          out[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, out[o], 0, 0, 0);
+        // fragments of out-block o+PF are read while the MFMAs of o run (register double buffer),
+        // pinned by scheduling barriers: left alone the compiler reads each pair right before its
+        // MFMAs and the LDS latency (> the 48 MFMA cycles of one out-block) is exposed
+        constexpr int MOB = b16_main_ob(L);
+        constexpr int PF = ANR_FRAG_PF;
+        bf16x8 fh[PF + 1], fl[PF + 1];
+        static_for<0, PF>([&](auto pp) {
+          constexpr int o = decltype(pp)::value;
+          if constexpr (o < MOB) {
+            fh[o] = *(const bf16x8*)(buf + o * 2048 + lane * 16);
+            fl[o] = *(const bf16x8*)(buf + o * 2048 + 1024 + lane * 16);
+          }
         });
+        static_for<0, MOB>([&](auto ob) {
+          constexpr int o = decltype(ob)::value;
+          constexpr int r = o % (PF + 1), rn = (o + PF) % (PF + 1);
+          if constexpr (o + PF < MOB) {
+            fh[rn] = *(const bf16x8*)(buf + (o + PF) * 2048 + lane * 16);
+            fl[rn] = *(const bf16x8*)(buf + (o + PF) * 2048 + 1024 + lane * 16);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          out[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fl[r], bh, out[o], 0, 0, 0);
+          out[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fh[r], bl, out[o], 0, 0, 0);
+          out[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fh[r], bh, out[o], 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
+          if constexpr (o == (MOB - 1) / 2) p.template mid<B16, V, E, tt>();
+        });
+        p.leave();
       }
     });
+    if constexpr (!X6 && b16_tail_ob(L) > 0) {
+      // the out-blocks past 16 (alpha_fc beside feature_fc): one slice [k-step][tail block]
+      constexpr int TOB = b16_tail_ob(L);
+      const unsigned char* buf = p.template enter<B16, V, E, KS>();
+      static_for<0, KS>([&](auto t) {
+        constexpr int tt = decltype(t)::value;
+        static_assert(D.nseg == 1 && D.seg[0].kind == SRC_ACT, "tail blocks only on activation-input layers");
+        float x[8];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          x[j] = in[2 * tt][j];
+          x[4 + j] = in[2 * tt + 1][j];
+        }
+        bf16x8 bh, bl;
+        split8(x, bh, bl);
+        static_for<0, TOB>([&](auto ob) {
+          constexpr int o = decltype(ob)::value;
+          const unsigned char* f = buf + (tt * TOB + o) * 2048 + lane * 16;
+          const bf16x8 ah = *(const bf16x8*)f;
+          const bf16x8 al = *(const bf16x8*)(f + 1024);
+          out[16 + o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, out[16 + o], 0, 0, 0);
+          out[16 + o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, out[16 + o], 0, 0, 0);
+          out[16 + o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, out[16 + o], 0, 0, 0);
+        });
+        if constexpr (tt == (KS - 1) / 2) p.template mid<B16, V, E, KS>();
+      });
+      p.leave();
+    }
   } else {
     constexpr int C = layer_chunks(L);
     constexpr int K = layer_ksteps(L);
@@ -275,7 +419,8 @@ __device__ __forceinline__ void layer(Pipe& p, const f32x4 (&in)[NIN], const flo
     const unsigned char* buf = nullptr;
     static_for<0, K>([&](auto t) {
       constexpr int tt = decltype(t)::value;
-      if constexpr (tt % ANR_KSLICE == 0) buf = p.template next<B16, V, E, tt / ANR_KSLICE>();
+      if constexpr (tt % ANR_KSLICE == 0) buf = p.template enter<B16, V, E, tt / ANR_KSLICE>();
+      if constexpr (tt == 0) init_bias();
       f32x4 w[C];
       static_for<0, C>([&](auto c) {
         constexpr int cc = decltype(c)::value;
@@ -292,6 +437,8 @@ __device__ __forceinline__ void layer(Pipe& p, const f32x4 (&in)[NIN], const flo
         constexpr int o = decltype(ob)::value;
         out[o] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[o >> 2][o & 3], b, out[o], 0, 0, 0);
       });
+      if constexpr (tt % ANR_KSLICE == ANR_KSLICE / 2 - 1) p.template mid<B16, V, E, tt / ANR_KSLICE>();
+      if constexpr (tt % ANR_KSLICE == ANR_KSLICE - 1) p.leave();
     });
   }
   if constexpr (RELU) {
@@ -306,6 +453,9 @@ __device__ __forceinline__ void layer(Pipe& p, const f32x4 (&in)[NIN], const flo
 // gamma(x) in the bf16 fragment layout: e[8s + j] = feature 32s + 8h + j (embedder.py:5-54)
 template <int NS>
 __device__ __forceinline__ void embed_b(const float x[3], int h, int nfreq, float (&e)[8 * NS]) {
+  // launder the lane half: otherwise the per-lane frequency scales and component selects of all
+  // 8*NS features are hoisted out of the tile loop and pin ~30 registers for the whole kernel
+  asm volatile("" : "+v"(h));
 #pragma unroll
   for (int s = 0; s < NS; ++s)
 #pragma unroll
@@ -321,7 +471,11 @@ __device__ __forceinline__ void embed_b(const float x[3], int h, int nfreq, floa
         const int comp = w >= 3 ? w - 3 : w;
         const float xc = comp == 0 ? x[0] : (comp == 1 ? x[1] : x[2]);
         const float arg = xc * (float)(1 << (freq < 15 ? freq : 0));
+#ifdef ANR_EXP_FASTSIN
+        v = freq >= nfreq ? 0.0f : (w >= 3 ? __cosf(arg) : __sinf(arg));  // timing experiment only
+#else
         v = freq >= nfreq ? 0.0f : (w >= 3 ? cosf(arg) : sinf(arg));
+#endif
       }
       e[8 * s + j] = v;
     }
@@ -356,9 +510,16 @@ __device__ __forceinline__ void embed(const float x[3], int g, int nfreq, float 
 __device__ __forceinline__ void lookup24(const float* __restrict__ vol32, const float p[3], const float* __restrict__ bounds,
                                          int X, int Y, int Z, int g, f32x4 (&out)[2]) {
 #pragma clang fp contract(off)
+  // formed per call (see embed_b): the float dims and bounds are not worth a register per tile
+  asm volatile("" : "+s"(X), "+s"(Y), "+s"(Z), "+s"(bounds));
   float lo[3], hi[3];
 #pragma unroll
   for (int c = 0; c < 3; ++c) { lo[c] = bounds[c]; hi[c] = bounds[3 + c]; }
+#ifdef ANR_EXP_NOLOOKUP
+  out[0] = f32x4{0.04f, 0.04f, 0.04f, 0.04f};  // timing experiment only
+  out[1] = out[0];
+  return;
+#endif
   TriCell t;
   tri_cell(p, lo, hi, X, Y, Z, t);
   f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
@@ -450,23 +611,21 @@ __device__ __forceinline__ void store_rows(float* __restrict__ rows, int idx, co
   if (g < 2) *(f32x4*)(rows + (size_t)idx * 24 + 16 + 4 * g) = bw[1];
 }
 
-// BW MLP pass starting at program entry E0 (0: pose pass, fp32; 9: T-pose pass). The pose pass
-// may read the novel_pose_bw copy of the weights (p.pose_woff, boff).
+// BW MLP pass starting at program entry E0 (0: pose pass; 9: T-pose pass). The pose pass may read
+// the novel_pose_bw copy of the weights (p.pose_woff); its biases are in the LDS table (fill_bias_table).
 template <bool B16, int V, int E0>
-__device__ __forceinline__ void bw_mlp(Pipe& p, const float (&emb)[16], const float (&vemb)[8], const float* __restrict__ bias,
-                                       int boff, const float* __restrict__ fold0, const float* __restrict__ fold5,
+__device__ __forceinline__ void bw_mlp(Pipe& p, const float (&emb)[16], const float (&vemb)[8], const float* __restrict__ sb,
                                        f32x4 (&A)[17], f32x4 (&B)[17], f32x4 (&fc)[2], int g, int lane) {
   f32x4 dummy[1];
-  const float* b = bias + boff;
-  layer<B16, V, E0 + 0, true>(p, dummy, emb, vemb, A, fold0, g, lane);
-  layer<B16, V, E0 + 1, true>(p, A, emb, vemb, B, b + kBiasOff<1>, g, lane);
-  layer<B16, V, E0 + 2, true>(p, B, emb, vemb, A, b + kBiasOff<2>, g, lane);
-  layer<B16, V, E0 + 3, true>(p, A, emb, vemb, B, b + kBiasOff<3>, g, lane);
-  layer<B16, V, E0 + 4, true>(p, B, emb, vemb, A, b + kBiasOff<4>, g, lane);
-  layer<B16, V, E0 + 5, true>(p, A, emb, vemb, B, fold5, g, lane);
-  layer<B16, V, E0 + 6, true>(p, B, emb, vemb, A, b + kBiasOff<6>, g, lane);
-  layer<B16, V, E0 + 7, true>(p, A, emb, vemb, B, b + kBiasOff<7>, g, lane);
-  layer<B16, V, E0 + 8, false>(p, B, emb, vemb, fc, b + kBiasOff<8>, g, lane);
+  layer<B16, V, E0 + 0, true>(p, dummy, emb, vemb, A, sb, g, lane);
+  layer<B16, V, E0 + 1, true>(p, A, emb, vemb, B, sb, g, lane);
+  layer<B16, V, E0 + 2, true>(p, B, emb, vemb, A, sb, g, lane);
+  layer<B16, V, E0 + 3, true>(p, A, emb, vemb, B, sb, g, lane);
+  layer<B16, V, E0 + 4, true>(p, B, emb, vemb, A, sb, g, lane);
+  layer<B16, V, E0 + 5, true>(p, A, emb, vemb, B, sb, g, lane);
+  layer<B16, V, E0 + 6, true>(p, B, emb, vemb, A, sb, g, lane);
+  layer<B16, V, E0 + 7, true>(p, A, emb, vemb, B, sb, g, lane);
+  layer<B16, V, E0 + 8, false>(p, B, emb, vemb, fc, sb, g, lane);
 }
 
 template <bool B16>
@@ -478,20 +637,19 @@ __device__ __forceinline__ void mlp_body(const MlpArgs& a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4;
   const int pl = lane & 15;
-  float* sA = (float*)(smem + mlp_nbuf<B16>() * mlp_slice_max<B16>());
+  float* sb = (float*)smem;  // bias table (anr_layers.h LDS layout)
+  float* sA = (float*)(smem + mlp_sa_off());
   for (int i = tid; i < 384; i += 512) sA[i] = a.A[i];
+  fill_bias_table<V>(a, sb, tid);
 
+  float* sT = sA + 384;  // T-pose bounds
+  if (tid < 6) sT[tid] = a.tbounds[tid];
   const int n = *a.n_kept;
   const int ntiles = (n + 127) / 128;
   if ((int)blockIdx.x >= ntiles) return;  // uniform per workgroup, before any LDS-DMA
 
-  Pipe p{smem, mlp_slice_max<B16>(), mlp_nbuf<B16>(), a.wimg, 0, wave, lane, a.pose_woff};
+  Pipe p{smem + mlp_ring_off(), mlp_slice_max<B16>(), mlp_nbuf<B16>(), a.wimg, 0, wave, lane, a.pose_woff};
   p.template start<B16, V>();
-
-  const float* fold = a.fold;
-  float tb_lo[3], tb_hi[3];
-#pragma unroll
-  for (int c = 0; c < 3; ++c) { tb_lo[c] = a.tbounds[c]; tb_hi[c] = a.tbounds[3 + c]; }
 
   for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int idx = tile * 128 + wave * 16 + pl;
@@ -512,7 +670,7 @@ __device__ __forceinline__ void mlp_body(const MlpArgs& a) {
     lookup24(a.pbw32, pose, a.pbounds, a.pX, a.pY, a.pZ, g, init);
 #pragma unroll
     for (int s8 = 0; s8 < 8; ++s8) vemb[s8] = 0.f;
-    bw_mlp<B16, V, 0>(p, emb, vemb, a.bias, a.pose_boff, fold + 0, fold + 512, A, B, fc, g, lane);
+    bw_mlp<B16, V, 0>(p, emb, vemb, sb, A, B, fc, g, lane);
     blend_softmax(fc, init, g, bw);
     store_rows(a.pbw_rows, idx, bw, g, valid);
     float xt[3];
@@ -522,33 +680,32 @@ __device__ __forceinline__ void mlp_body(const MlpArgs& a) {
     if constexpr (B16) embed_b<2>(xt, g, 10, emb);
     else embed<16>(xt, g, 10, emb);
     lookup24(a.tbw32, xt, a.tbounds, a.tX, a.tY, a.tZ, g, init);
-    bw_mlp<B16, V, 9>(p, emb, vemb, a.bias, 0, fold + 256, fold + 768, A, B, fc, g, lane);
+    bw_mlp<B16, V, 9>(p, emb, vemb, sb, A, B, fc, g, lane);
     blend_softmax(fc, init, g, bw);
     store_rows(a.tbw_rows, idx, bw, g, valid);
 
     // ---- canonical NeRF (TPoseHuman.calculate_alpha_rgb)
     f32x4 dummy[1];
-    const float* bias = a.bias;
-    layer<B16, V, 18, true>(p, dummy, emb, vemb, A, bias + kBiasOff<9>, g, lane);
-    layer<B16, V, 19, true>(p, A, emb, vemb, B, bias + kBiasOff<10>, g, lane);
-    layer<B16, V, 20, true>(p, B, emb, vemb, A, bias + kBiasOff<11>, g, lane);
-    layer<B16, V, 21, true>(p, A, emb, vemb, B, bias + kBiasOff<12>, g, lane);
-    layer<B16, V, 22, true>(p, B, emb, vemb, A, bias + kBiasOff<13>, g, lane);
-    layer<B16, V, 23, true>(p, A, emb, vemb, B, bias + kBiasOff<14>, g, lane);
-    layer<B16, V, 24, true>(p, B, emb, vemb, A, bias + kBiasOff<15>, g, lane);
-    layer<B16, V, 25, true>(p, A, emb, vemb, B, bias + kBiasOff<16>, g, lane);
-    layer<B16, V, 26, false>(p, B, emb, vemb, A, bias + kBiasOff<17>, g, lane);  // feature || alpha
+    layer<B16, V, 18, true>(p, dummy, emb, vemb, A, sb, g, lane);
+    layer<B16, V, 19, true>(p, A, emb, vemb, B, sb, g, lane);
+    layer<B16, V, 20, true>(p, B, emb, vemb, A, sb, g, lane);
+    layer<B16, V, 21, true>(p, A, emb, vemb, B, sb, g, lane);
+    layer<B16, V, 22, true>(p, B, emb, vemb, A, sb, g, lane);
+    layer<B16, V, 23, true>(p, A, emb, vemb, B, sb, g, lane);
+    layer<B16, V, 24, true>(p, B, emb, vemb, A, sb, g, lane);
+    layer<B16, V, 25, true>(p, A, emb, vemb, B, sb, g, lane);
+    layer<B16, V, 26, false>(p, B, emb, vemb, A, sb, g, lane);  // feature || alpha
     const float sigma_raw = __shfl(A[16][0], pl);
-    layer<B16, V, 27, false>(p, A, emb, vemb, B, fold + 1024, g, lane);  // latent_fc
+    layer<B16, V, 27, false>(p, A, emb, vemb, B, sb, g, lane);  // latent_fc
     if constexpr (B16) embed_b<1>(dir, g, 4, vemb);
     else embed<8>(dir, g, 4, vemb);
-    layer<B16, V, 28, true>(p, B, emb, vemb, A, bias + kBiasOff<19>, g, lane);   // view_fc
-    layer<B16, V, 29, false>(p, A, emb, vemb, B, bias + kBiasOff<20>, g, lane);  // rgb_fc
+    layer<B16, V, 28, true>(p, B, emb, vemb, A, sb, g, lane);   // view_fc
+    layer<B16, V, 29, false>(p, A, emb, vemb, B, sb, g, lane);  // rgb_fc
 
     // ---- bbox mask, activations, outputs
     bool inside = true;
 #pragma unroll
-    for (int c = 0; c < 3; ++c) inside = inside && (xt[c] > tb_lo[c]) && (xt[c] < tb_hi[c]);
+    for (int c = 0; c < 3; ++c) inside = inside && (xt[c] > sT[c]) && (xt[c] < sT[3 + c]);
     const float sig = inside ? sigma_raw : 0.0f;
     if (valid && g == 0) {
       float4 r;
@@ -577,16 +734,17 @@ __device__ __forceinline__ void alpha_body(const MlpArgs& a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4;
   const int pl = lane & 15;
-  float* sA = (float*)(smem + mlp_nbuf<B16>() * mlp_slice_max<B16>());
+  float* sb = (float*)smem;  // bias table (anr_layers.h LDS layout)
+  float* sA = (float*)(smem + mlp_sa_off());
   for (int i = tid; i < 384; i += 512) sA[i] = a.A[i];
+  fill_bias_table<V>(a, sb, tid);
 
   const int n = *a.n_kept;
   const int ntiles = (n + 127) / 128;
   if ((int)blockIdx.x >= ntiles) return;  // uniform per workgroup, before any LDS-DMA
 
-  Pipe p{smem, mlp_slice_max<B16>(), mlp_nbuf<B16>(), a.wimg, 0, wave, lane, a.pose_woff};
+  Pipe p{smem + mlp_ring_off(), mlp_slice_max<B16>(), mlp_nbuf<B16>(), a.wimg, 0, wave, lane, a.pose_woff};
   p.template start<B16, V>();
-  const float* fold = a.fold;
 
   for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int idx = tile * 128 + wave * 16 + pl;
@@ -602,7 +760,7 @@ __device__ __forceinline__ void alpha_body(const MlpArgs& a) {
     lookup24(a.pbw32, pose, a.pbounds, a.pX, a.pY, a.pZ, g, init);
 #pragma unroll
     for (int s8 = 0; s8 < 8; ++s8) vemb[s8] = 0.f;
-    bw_mlp<B16, V, 0>(p, emb, vemb, a.bias, a.pose_boff, fold + 0, fold + 512, A, B, fc, g, lane);
+    bw_mlp<B16, V, 0>(p, emb, vemb, sb, A, B, fc, g, lane);
     blend_softmax(fc, init, g, bw);
     float xt[3];
     lbs_inverse(bw, sA, g, pose, xt);
@@ -610,16 +768,15 @@ __device__ __forceinline__ void alpha_body(const MlpArgs& a) {
     if constexpr (B16) embed_b<2>(xt, g, 10, emb);
     else embed<16>(xt, g, 10, emb);
     f32x4 dummy[1];
-    const float* bias = a.bias;
-    layer<B16, V, 9, true>(p, dummy, emb, vemb, A, bias + kBiasOff<9>, g, lane);
-    layer<B16, V, 10, true>(p, A, emb, vemb, B, bias + kBiasOff<10>, g, lane);
-    layer<B16, V, 11, true>(p, B, emb, vemb, A, bias + kBiasOff<11>, g, lane);
-    layer<B16, V, 12, true>(p, A, emb, vemb, B, bias + kBiasOff<12>, g, lane);
-    layer<B16, V, 13, true>(p, B, emb, vemb, A, bias + kBiasOff<13>, g, lane);
-    layer<B16, V, 14, true>(p, A, emb, vemb, B, bias + kBiasOff<14>, g, lane);
-    layer<B16, V, 15, true>(p, B, emb, vemb, A, bias + kBiasOff<15>, g, lane);
-    layer<B16, V, 16, true>(p, A, emb, vemb, B, bias + kBiasOff<16>, g, lane);
-    layer<B16, V, 17, false>(p, B, emb, vemb, A, bias + kBiasOff<ANR_L_ALPHA>, g, lane);  // alpha_fc
+    layer<B16, V, 9, true>(p, dummy, emb, vemb, A, sb, g, lane);
+    layer<B16, V, 10, true>(p, A, emb, vemb, B, sb, g, lane);
+    layer<B16, V, 11, true>(p, B, emb, vemb, A, sb, g, lane);
+    layer<B16, V, 12, true>(p, A, emb, vemb, B, sb, g, lane);
+    layer<B16, V, 13, true>(p, B, emb, vemb, A, sb, g, lane);
+    layer<B16, V, 14, true>(p, A, emb, vemb, B, sb, g, lane);
+    layer<B16, V, 15, true>(p, B, emb, vemb, A, sb, g, lane);
+    layer<B16, V, 16, true>(p, A, emb, vemb, B, sb, g, lane);
+    layer<B16, V, 17, false>(p, B, emb, vemb, A, sb, g, lane);  // alpha_fc
     if (valid && g == 0) a.alpha_out[pid] = A[0][0];
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the last (unused) prefetch

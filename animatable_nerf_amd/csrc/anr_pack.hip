@@ -74,7 +74,10 @@ __global__ void k_pack_b16(PackArgs a) {
   const int local = (byte - b16_layer_offset(L)) / 32;  // (s, ob, lane)
   const int lane = local & 63;
   const int so = local >> 6;
-  const int ob = so % d.ob, t = so / d.ob;
+  // main part [k-step][16 out-blocks], then the tail blocks [k-step][tail] (anr_layers.h)
+  const int mob = b16_main_ob(L), tob = b16_tail_ob(L), ks = ks32(L);
+  const int ob = so < ks * mob ? so % mob : mob + (so - ks * mob) % tob;
+  const int t = so < ks * mob ? so / mob : (so - ks * mob) / tob;
   const int row16 = lane & 15, h = lane >> 4;
   const int main_ob = (d.nout + 15) / 16;
   unsigned short hi[8], lo[8];
