@@ -25,6 +25,7 @@ EXPORTS = ('anr_near_far', 'anr_params_packed_bytes', 'anr_params_pack', 'anr_re
            'anr_camera_rays_workspace_bytes', 'anr_camera_rays', 'anr_sdf_render_workspace_bytes', 'anr_sdf_render_fwd', 'anr_sdf_render_counts', 'anr_sdf_render_rows',
            'anr_alpha_workspace_bytes', 'anr_alpha_points', 'anr_alpha_counts', 'anr_mc_workspace_bytes',
            'anr_mc_count', 'anr_mc_emit', 'anr_anim_workspace_bytes', 'anr_anim_step',
+           'anr_train_ray_workspace_bytes', 'anr_train_ray_lists', 'anr_train_ray_gather',
            'anr_last_error', 'anr_version')
 
 c_float_p = ctypes.c_void_p
@@ -125,6 +126,12 @@ def load():
     D = ctypes.POINTER(ctypes.c_double)
     lib.anr_camera_rays.argtypes = [ctypes.c_int, ctypes.c_int, D, D, D, D, ctypes.c_int, P, P, P, P, P, P, P, P, P,
                                     ctypes.c_size_t, P]
+    lib.anr_train_ray_workspace_bytes.restype = ctypes.c_size_t
+    lib.anr_train_ray_workspace_bytes.argtypes = [ctypes.c_int, ctypes.c_int]
+    lib.anr_train_ray_lists.argtypes = [ctypes.c_int, ctypes.c_int, P, P, P, P, P, ctypes.c_size_t, P]
+    lib.anr_train_ray_gather.argtypes = [ctypes.c_int, ctypes.c_int, D, D, D, D, ctypes.c_int, P, P, P, ctypes.c_int,
+                                         P, P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                         P, P, P, P, P, P, P, P]
     lib.anr_alpha_workspace_bytes.restype = ctypes.c_size_t
     lib.anr_alpha_workspace_bytes.argtypes = [ctypes.c_long, ctypes.POINTER(AlphaOpts), ctypes.POINTER(Frame)]
     lib.anr_alpha_points.argtypes = [ctypes.POINTER(Params), ctypes.POINTER(Frame), P, ctypes.c_long,

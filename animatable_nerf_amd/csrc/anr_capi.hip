@@ -266,6 +266,57 @@ int anr_camera_rays(int H, int W, const double* Kinv, const double* R, const dou
   return check_launch("anr_camera_rays");
 }
 
+size_t anr_train_ray_workspace_bytes(int H, int W) {
+  if (H <= 0 || W <= 0) return 0;
+  return align256((((size_t)H * W + 255) / 256) * 4 * 3);
+}
+
+int anr_train_ray_lists(int H, int W, const uint8_t* msk, const uint8_t* bound_mask, int32_t* lists, int32_t* counts,
+                        void* workspace, size_t ws_bytes, void* stream) {
+  if (H <= 0 || W <= 0 || !msk || !bound_mask || !lists || !counts || !workspace)
+    return fail(ANR_E_ARG, "anr_train_ray_lists: bad arguments");
+  if ((long)H * W > (1L << 29)) return fail(ANR_E_ARG, "anr_train_ray_lists: image too large");
+  if (ws_bytes < anr_train_ray_workspace_bytes(H, W)) return fail(ANR_E_WORKSPACE, "anr_train_ray_lists: workspace");
+  TrainRayArgs a{};
+  a.cam.H = H; a.cam.W = W;
+  a.msk = msk; a.bound_mask = bound_mask;
+  a.block_sum = (int*)workspace;
+  a.lists = lists;
+  hipStream_t s = (hipStream_t)stream;
+  const int nb = (int)(((size_t)H * W + 255) / 256);
+  hipLaunchKernelGGL(k_trl_count, dim3(nb), dim3(256), 0, s, a);
+  for (int k = 0; k < 3; ++k)
+    hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, s, a.block_sum + k * nb, nb, counts + k);
+  hipLaunchKernelGGL(k_trl_scatter, dim3(nb), dim3(256), 0, s, a);
+  return check_launch("anr_train_ray_lists");
+}
+
+int anr_train_ray_gather(int H, int W, const double* Kinv, const double* R, const double* T, const double* origin,
+                         int fp64, const float* bounds, const float* img, const uint8_t* bound_mask, int mask_bkgd,
+                         const int32_t* lists, const int32_t* draws, int n_body, int n_face, int n_rand, int cap,
+                         float* ray_o, float* ray_d, float* rgb, float* near_, float* far_, int32_t* coord,
+                         int32_t* n_out, void* stream) {
+  if (H <= 0 || W <= 0 || !Kinv || !R || !T || !origin || !bounds || !img || !bound_mask || !lists || !ray_o ||
+      !ray_d || !rgb || !near_ || !far_ || !coord || !n_out || n_body < 0 || n_face < 0 || n_rand < 0 || cap < 0)
+    return fail(ANR_E_ARG, "anr_train_ray_gather: bad arguments");
+  const long n = (long)n_body + n_face + n_rand;
+  if (n > 0 && !draws) return fail(ANR_E_ARG, "anr_train_ray_gather: draws is NULL");
+  if (n > (1L << 24)) return fail(ANR_E_ARG, "anr_train_ray_gather: too many draws");
+  if (n == 0) return ANR_OK;
+  TrainRayArgs a{};
+  a.cam.H = H; a.cam.W = W; a.cam.fp64 = fp64 ? 1 : 0;
+  for (int k = 0; k < 9; ++k) { a.cam.Kinv[k] = Kinv[k]; a.cam.R[k] = R[k]; }
+  for (int k = 0; k < 3; ++k) { a.cam.T[k] = T[k]; a.cam.o[k] = origin[k]; }
+  a.cam.bounds = bounds;
+  a.img = img; a.bound_mask = bound_mask; a.mask_bkgd = mask_bkgd ? 1 : 0;
+  a.lists = const_cast<int*>(lists); a.draws = draws;
+  a.n_seg[0] = n_body; a.n_seg[1] = n_face; a.n_seg[2] = n_rand;
+  a.cap = cap; a.n_out = n_out;
+  a.ray_o = ray_o; a.ray_d = ray_d; a.rgb = rgb; a.near_ = near_; a.far_ = far_; a.coord = coord;
+  hipLaunchKernelGGL(k_trl_gather, dim3(1), dim3(1024), 0, (hipStream_t)stream, a);
+  return check_launch("anr_train_ray_gather");
+}
+
 size_t anr_params_packed_bytes(void) { return (size_t)packed_bytes_all(); }
 
 int anr_params_pack(const anr_params* p, void* packed, void* stream) {

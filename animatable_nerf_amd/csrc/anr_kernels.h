@@ -59,6 +59,22 @@ struct CamArgs {
   int* coord;                     // (n, 2) (row, col)
 };
 
+// (f) train-split ray sampler (anr_rays.hip, k_trl_*)
+struct TrainRayArgs {
+  CamArgs cam;                    // H, W, fp64, Kinv, R, T, o, bounds
+  const uint8_t *msk, *bound_mask;  // (H*W) u8
+  const float* img;               // (H*W, 3)
+  int mask_bkgd;
+  int* block_sum;                 // 3 x ceil(H*W/256)
+  int* lists;                     // 3 x H*W pixel ids: body, face, bound
+  const int* draws;               // one round of list-relative draws
+  int n_seg[3];
+  int cap;                        // output capacity (nrays)
+  int* n_out;                     // device: rays so far (in/out)
+  float *ray_o, *ray_d, *rgb, *near_, *far_;
+  int* coord;
+};
+
 struct CompositeArgs {
   const float4* raw;
   const float *near_, *far_, *t_rand;
@@ -108,6 +124,9 @@ __global__ void k_near_far(const float*, const float*, int, const float*, uint8_
 __global__ void k_cam_rays(CamArgs a);
 __global__ void k_cam_count(CamArgs a);
 __global__ void k_cam_scatter(CamArgs a);
+__global__ void k_trl_count(TrainRayArgs a);
+__global__ void k_trl_scatter(TrainRayArgs a);
+__global__ void k_trl_gather(TrainRayArgs a);
 __global__ void k_frontend(FrontArgs a);
 __global__ void k_frontend_pts(FrontArgs a);
 __global__ void k_count(CompactArgs a);

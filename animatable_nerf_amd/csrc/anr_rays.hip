@@ -9,6 +9,8 @@
 //
 // One wave per ray everywhere a ray is touched: lane = sample (N_samples == 64 == wave width),
 // so every per-ray access is one coalesced 256-B (or 1-KiB for float4 raw) wave instruction.
+#include <type_traits>
+
 #include "anr_common.h"
 #include "anr_kernels.h"
 
@@ -19,7 +21,10 @@ namespace anr {
 // ------------------------------------------------------------------------------------------
 // A14 near/far, fp64, numpy operation order; eps 1e-6, padding 0.01; hit <=> exactly 2 planes.
 // ------------------------------------------------------------------------------------------
-__device__ __forceinline__ void near_far_one(const float ro[3], const float rd[3], const float* __restrict__ bounds,
+// T = float: test-split rays (cast to float32 before get_near_far, :330-333); T = double: the
+// train split, where get_near_far sees get_rays' float64 arrays (:256-262), |d| included.
+template <typename T>
+__device__ __forceinline__ void near_far_one(const T ro[3], const T rd[3], const float* __restrict__ bounds,
                                              uint8_t& hit_out, float& near_out, float& far_out) {
   double b[2][3];
   for (int c = 0; c < 3; ++c) {
@@ -47,7 +52,9 @@ __device__ __forceinline__ void near_far_one(const float ro[3], const float rd[3
   hit_out = hits == 2 ? 1 : 0;
   // np.linalg.norm(axis=1): sqrt((x0*x0 + x1*x1) + x2*x2); ray_d is float32 in the test split,
   // so |d| is evaluated in float32 and promoted at the division (if_nerf_data_utils.py:189-191)
-  const double nd = (double)sqrtf((rd[0] * rd[0] + rd[1] * rd[1]) + rd[2] * rd[2]);
+  double nd;
+  if constexpr (std::is_same<T, float>::value) nd = (double)sqrtf((rd[0] * rd[0] + rd[1] * rd[1]) + rd[2] * rd[2]);
+  else nd = sqrt((d[0] * d[0] + d[1] * d[1]) + d[2] * d[2]);
   double dd[2];
   for (int h = 0; h < 2; ++h) {
     const double e0 = pin[h][0] - o[0], e1 = pin[h][1] - o[1], e2 = pin[h][2] - o[2];
@@ -64,7 +71,7 @@ __global__ void k_near_far(const float* __restrict__ ray_o, const float* __restr
   if (i >= n) return;
   const float ro[3] = {ray_o[3 * i], ray_o[3 * i + 1], ray_o[3 * i + 2]};
   const float rd[3] = {ray_d[3 * i], ray_d[3 * i + 1], ray_d[3 * i + 2]};
-  near_far_one(ro, rd, bounds, mask[i], near_[i], far_[i]);
+  near_far_one<float>(ro, rd, bounds, mask[i], near_[i], far_[i]);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -74,11 +81,9 @@ __global__ void k_near_far(const float* __restrict__ ray_o, const float* __restr
 // multiply/add for float32 ones; |d| as sqrt((x*x + y*y) + z*z). Kinv and the origin -R^T T are
 // computed by the caller with numpy exactly as the reference does.
 // ------------------------------------------------------------------------------------------
-__global__ void k_cam_rays(CamArgs a) {
-  const int pix = blockIdx.x * blockDim.x + threadIdx.x;
-  if (pix >= a.H * a.W) return;
-  const int r = pix / a.W, c = pix - r * a.W;
-  float d32[3];
+// get_rays for pixel (r, c): d32 = the float32 direction the caller sees; for a float64 camera also
+// d64 = the float64 direction before the cast (the train split tests the box with it)
+__device__ __forceinline__ void cam_ray(const CamArgs& a, int r, int c, float d32[3], double d64[3]) {
   if (a.fp64) {
     const double xy[3] = {(double)c, (double)r, 1.0};
     double pc[3], q[3], pw[3], d[3];
@@ -87,7 +92,10 @@ __global__ void k_cam_rays(CamArgs a) {
     for (int j = 0; j < 3; ++j) pw[j] = fma(q[2], a.R[6 + j], fma(q[1], a.R[3 + j], q[0] * a.R[j]));
     for (int k = 0; k < 3; ++k) d[k] = pw[k] - a.o[k];
     const double n = sqrt((d[0] * d[0] + d[1] * d[1]) + d[2] * d[2]);
-    for (int k = 0; k < 3; ++k) d32[k] = (float)(d[k] / n);
+    for (int k = 0; k < 3; ++k) {
+      d64[k] = d[k] / n;
+      d32[k] = (float)d64[k];
+    }
   } else {
     const float xy[3] = {(float)c, (float)r, 1.0f};
     float kinv[9], R[9], T[3], o[3], pc[3], q[3], pw[3], d[3];
@@ -98,14 +106,26 @@ __global__ void k_cam_rays(CamArgs a) {
     for (int j = 0; j < 3; ++j) pw[j] = (q[0] * R[j] + q[1] * R[3 + j]) + q[2] * R[6 + j];
     for (int k = 0; k < 3; ++k) d[k] = pw[k] - o[k];
     const float n = sqrtf((d[0] * d[0] + d[1] * d[1]) + d[2] * d[2]);
-    for (int k = 0; k < 3; ++k) d32[k] = d[k] / n;
+    for (int k = 0; k < 3; ++k) {
+      d32[k] = d[k] / n;
+      d64[k] = (double)d32[k];
+    }
   }
+}
+
+__global__ void k_cam_rays(CamArgs a) {
+  const int pix = blockIdx.x * blockDim.x + threadIdx.x;
+  if (pix >= a.H * a.W) return;
+  const int r = pix / a.W, c = pix - r * a.W;
+  float d32[3];
+  double d64[3];
+  cam_ray(a, r, c, d32, d64);
   const float o32[3] = {(float)a.o[0], (float)a.o[1], (float)a.o[2]};
   for (int k = 0; k < 3; ++k) {
     a.all_o[3 * (size_t)pix + k] = o32[k];
     a.all_d[3 * (size_t)pix + k] = d32[k];
   }
-  if (a.bounds) near_far_one(o32, d32, a.bounds, a.mask[pix], a.all_near[pix], a.all_far[pix]);
+  if (a.bounds) near_far_one<float>(o32, d32, a.bounds, a.mask[pix], a.all_near[pix], a.all_far[pix]);
 }
 
 // ordered compaction of the hit pixels: per-256-pixel counts, k_scan_blocks, scatter
@@ -136,6 +156,111 @@ __global__ __launch_bounds__(256) void k_cam_scatter(CamArgs a) {
     a.coord[2 * (size_t)pos] = pix / a.W;
     a.coord[2 * (size_t)pos + 1] = pix % a.W;
   }
+}
+
+// ------------------------------------------------------------------------------------------
+// (f) train-split ray sampler: sample_ray_h36m(split='train') (if_nerf_data_utils.py:198-283).
+// The pixel lists np.argwhere(msk == 1), (msk == 13) and (bound_mask == 1) (:238-249), row-major
+// like argwhere, with msk = msk * bound_mask (u8, wrapping) and bound_mask[msk == 100] = 0
+// (:230-231); the random draws into them stay on the host (np.random, so the stream of draws is
+// the reference's), then k_trl_gather turns one round of draws into rays.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ void trl_flags(const TrainRayArgs& a, int pix, int f[3]) {
+  const int P = a.cam.H * a.cam.W;
+  f[0] = f[1] = f[2] = 0;
+  if (pix >= P) return;
+  const uint8_t bm = a.bound_mask[pix];
+  const uint8_t m = (uint8_t)(a.msk[pix] * bm);
+  f[0] = m == 1;
+  f[1] = m == 13;
+  f[2] = bm == 1 && m != 100;
+}
+
+__global__ __launch_bounds__(256) void k_trl_count(TrainRayArgs a) {
+  __shared__ int sh[4];
+  int f[3];
+  trl_flags(a, blockIdx.x * 256 + threadIdx.x, f);
+  const int nb = gridDim.x;
+  for (int k = 0; k < 3; ++k) {
+    int total;
+    block_excl_scan_256(f[k], sh, total);
+    if (threadIdx.x == 0) a.block_sum[k * nb + blockIdx.x] = total;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_trl_scatter(TrainRayArgs a) {
+  __shared__ int sh[4];
+  const int pix = blockIdx.x * 256 + threadIdx.x;
+  int f[3];
+  trl_flags(a, pix, f);
+  const int nb = gridDim.x;
+  const size_t P = (size_t)a.cam.H * a.cam.W;
+  for (int k = 0; k < 3; ++k) {
+    int total;
+    const int ex = block_excl_scan_256(f[k], sh, total);
+    if (f[k]) a.lists[k * P + a.block_sum[k * nb + blockIdx.x] + ex] = pix;
+  }
+}
+
+// One round of the sampling loop (:236-271): draws[i] indexes list 0 for i < n_seg[0], list 1 for
+// the next n_seg[1], list 2 for the rest (the reference's concatenation order). Per draw: get_rays
+// at the pixel, get_near_far on get_rays' arrays (float64 for a float64 camera), rgb = img (zero
+// outside the bound mask when mask_bkgd, :228); the hits are appended in draw order at *n_out.
+// One 1024-thread workgroup (a round draws at most nrays).
+__global__ __launch_bounds__(1024) void k_trl_gather(TrainRayArgs a) {
+  __shared__ int wsum[16];
+  __shared__ int base;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (threadIdx.x == 0) base = *a.n_out;
+  __syncthreads();
+  const size_t P = (size_t)a.cam.H * a.cam.W;
+  const int n = a.n_seg[0] + a.n_seg[1] + a.n_seg[2];
+  for (int i0 = 0; i0 < n; i0 += 1024) {
+    const int i = i0 + threadIdx.x;
+    int hit = 0, pix = 0;
+    float d32[3] = {0.f, 0.f, 0.f}, nr = 0.f, fr = 0.f;
+    if (i < n) {
+      const int seg = i < a.n_seg[0] ? 0 : (i < a.n_seg[0] + a.n_seg[1] ? 1 : 2);
+      pix = a.lists[seg * P + a.draws[i]];
+      const int r = pix / a.cam.W, c = pix - r * a.cam.W;
+      double d64[3];
+      cam_ray(a.cam, r, c, d32, d64);
+      uint8_t h;
+      if (a.cam.fp64) {
+        near_far_one<double>(a.cam.o, d64, a.cam.bounds, h, nr, fr);
+      } else {
+        const float o32[3] = {(float)a.cam.o[0], (float)a.cam.o[1], (float)a.cam.o[2]};
+        near_far_one<float>(o32, d32, a.cam.bounds, h, nr, fr);
+      }
+      hit = h;
+    }
+    // block-wide exclusive scan of the hit flags (16 waves)
+    const uint64_t bal = __ballot(hit);
+    const int before = __popcll(bal & ((1ull << lane) - 1));
+    if (lane == 0) wsum[w] = __popcll(bal);
+    __syncthreads();
+    int off = base, tot = 0;
+    for (int k = 0; k < 16; ++k) {
+      if (k < w) off += wsum[k];
+      tot += wsum[k];
+    }
+    const int pos = off + before;
+    if (hit && pos < a.cap) {
+      for (int k = 0; k < 3; ++k) {
+        a.ray_o[3 * (size_t)pos + k] = (float)a.cam.o[k];
+        a.ray_d[3 * (size_t)pos + k] = d32[k];
+        a.rgb[3 * (size_t)pos + k] = (a.mask_bkgd && a.bound_mask[pix] != 1) ? 0.0f : a.img[3 * (size_t)pix + k];
+      }
+      a.near_[pos] = nr;
+      a.far_[pos] = fr;
+      a.coord[2 * (size_t)pos] = pix / a.cam.W;
+      a.coord[2 * (size_t)pos + 1] = pix % a.cam.W;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) base += tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *a.n_out = base;
 }
 
 // ------------------------------------------------------------------------------------------

@@ -1,8 +1,14 @@
-"""Eval-split ray pipeline on the device: ``get_rays`` /
-``get_rays_within_bounds`` of ``lib/utils/if_nerf/if_nerf_data_utils.py:64-89, 310-339`` through
-``anr_camera_rays`` (include/aninerf.h). The 3x3 inverse of K and the camera origin -R^T T are
-formed with numpy on the host exactly as the reference does; the per-pixel rays, the box test and
-the ordered hit list run on the GPU, so a full-resolution render needs no host ray generation.
+"""Ray pipelines on the device, ``lib/utils/if_nerf/if_nerf_data_utils.py``:
+
+* eval split: ``get_rays`` / ``get_rays_within_bounds`` (:64-89, 310-339) through ``anr_camera_rays``;
+* train split: ``sample_ray_h36m(split='train')`` (:198-283) through ``anr_train_ray_lists`` /
+  ``anr_train_ray_gather``: the pixel lists, rays, float64 box test, rgb gather and hit compaction
+  run on the GPU; the np.random draws stay on the host so the random stream is the reference's.
+
+The 3x3 inverse of K and the camera origin -R^T T are formed with numpy on the host exactly as the
+reference does. ``get_bound_2d_mask`` (:114-136) is per-frame host work like the reference's; it
+uses cv2.fillPoly there (cv2 is not installed here), restated below as the filled convex hull of
+the projected box corners (unpinned at the polygon boundary).
 """
 import ctypes
 
@@ -47,3 +53,122 @@ def get_rays_within_bounds(H, W, K, R, T, bounds, device='cuda'):
                'anr_camera_rays')
     n = int(count.item())
     return ray_o[:n], ray_d[:n], near[:n], far[:n], mask.view(H, W).bool(), coord[:n]
+
+
+def _project(xyz, K, RT):
+    """lib/utils/base_utils.py:86-95."""
+    xyz = np.dot(xyz, RT[:, :3].T) + RT[:, 3:].T
+    xyz = np.dot(xyz, K.T)
+    return xyz[:, :2] / xyz[:, 2:]
+
+
+def get_bound_corners(bounds):
+    """if_nerf_data_utils.py:92-111 (x-major corner order)."""
+    (x0, y0, z0), (x1, y1, z1) = bounds
+    return np.array([[x0, y0, z0], [x0, y0, z1], [x0, y1, z0], [x0, y1, z1],
+                     [x1, y0, z0], [x1, y0, z1], [x1, y1, z0], [x1, y1, z1]])
+
+
+def get_bound_2d_mask(bounds, K, pose, H, W):
+    """if_nerf_data_utils.py:114-136: the six projected box faces filled with 1 (u8 (H, W)). Their
+    union is the convex hull of the 8 rounded projected corners; filled here as every pixel inside
+    or on that hull (cv2.fillPoly's boundary rasterisation is not reproduced: cv2 is absent)."""
+    c2 = np.round(_project(get_bound_corners(np.asarray(bounds)), np.asarray(K), np.asarray(pose))).astype(np.int64)
+    mask = np.zeros((H, W), dtype=np.uint8)
+    pts = sorted(set(map(tuple, c2.tolist())))
+    if len(pts) < 3:
+        return mask
+
+    def cross(o, a, b):
+        return (a[0] - o[0]) * (b[1] - o[1]) - (a[1] - o[1]) * (b[0] - o[0])
+
+    lower, upper = [], []
+    for p in pts:  # monotone chain, counter-clockwise in (x, y)
+        while len(lower) >= 2 and cross(lower[-2], lower[-1], p) <= 0:
+            lower.pop()
+        lower.append(p)
+    for p in reversed(pts):
+        while len(upper) >= 2 and cross(upper[-2], upper[-1], p) <= 0:
+            upper.pop()
+        upper.append(p)
+    hull = lower[:-1] + upper[:-1]
+    if len(hull) < 3:
+        return mask
+    xs = [p[0] for p in hull]
+    ys = [p[1] for p in hull]
+    x0, x1 = max(min(xs), 0), min(max(xs), W - 1)
+    y0, y1 = max(min(ys), 0), min(max(ys), H - 1)
+    if x0 > x1 or y0 > y1:
+        return mask
+    gx, gy = np.meshgrid(np.arange(x0, x1 + 1), np.arange(y0, y1 + 1), indexing='xy')
+    inside = np.ones(gx.shape, dtype=bool)
+    for k in range(len(hull)):
+        a, b = hull[k], hull[(k + 1) % len(hull)]
+        inside &= (b[0] - a[0]) * (gy - a[1]) - (b[1] - a[1]) * (gx - a[0]) >= 0
+    mask[y0:y1 + 1, x0:x1 + 1] = inside
+    return mask
+
+
+def sample_ray_h36m(img, msk, K, R, T, bounds, nrays, split, mask_bkgd=True, body_sample_ratio=0.5,
+                    face_sample_ratio=0.0, bound_mask=None, rng=None, device='cuda'):
+    """if_nerf_data_utils.py:198-307 on the device. -> rgb (n,3), ray_o (n,3), ray_d (n,3), near (n,),
+    far (n,), coord (n,2) int32, mask_at_box (torch tensors on ``device``; the reference returns the
+    same values as numpy arrays). ``cfg.mask_bkgd`` / ``cfg.body_sample_ratio`` /
+    ``cfg.face_sample_ratio`` are arguments; ``rng`` (default ``np.random``) makes the draws, in the
+    reference's call order, so a seeded run draws exactly the reference's pixels. ``bound_mask``
+    overrides ``get_bound_2d_mask``."""
+    lib = _lib.load()
+    dev = torch.device(device)
+    rng = np.random if rng is None else rng
+    H, W = img.shape[:2]
+    if bound_mask is None:
+        pose = np.concatenate([np.asarray(R), np.asarray(T).reshape(3, 1)], axis=1)
+        bound_mask = get_bound_2d_mask(bounds, K, pose, H, W)
+    Kinv, Rd, Td, o, fp64 = _camera(K, R, T)
+    b = torch.as_tensor(np.asarray(bounds, dtype=np.float32).reshape(2, 3)).to(dev)
+    img_d = torch.as_tensor(np.ascontiguousarray(img, dtype=np.float32)).to(dev)
+    bm_d = torch.as_tensor(np.ascontiguousarray(bound_mask, dtype=np.uint8)).to(dev)
+    dp = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+    stream = _lib.stream_ptr(dev)
+    if split != 'train':
+        ray_o, ray_d, near, far, mask, coord = get_rays_within_bounds(H, W, K, R, T, bounds, device=device)
+        img_z = img_d * (bm_d == 1).unsqueeze(-1) if mask_bkgd else img_d  # :228
+        rgb = img_z[coord[:, 0].long(), coord[:, 1].long()]
+        return rgb, ray_o, ray_d, near, far, coord, mask.reshape(-1)
+    msk_d = torch.as_tensor(np.ascontiguousarray(msk, dtype=np.uint8)).to(dev)
+    P = H * W
+    lists = torch.empty(3 * P, dtype=torch.int32, device=dev)
+    counts = torch.zeros(3, dtype=torch.int32, device=dev)
+    ws_bytes = lib.anr_train_ray_workspace_bytes(H, W)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    _lib.check(lib.anr_train_ray_lists(H, W, _lib.ptr(msk_d), _lib.ptr(bm_d), _lib.ptr(lists), _lib.ptr(counts),
+                                       _lib.ptr(ws), ws_bytes, stream), 'anr_train_ray_lists')
+    n_body_px, n_face_px, n_bound_px = (int(v) for v in counts.cpu())
+    ray_o = torch.empty((nrays, 3), device=dev)
+    ray_d = torch.empty((nrays, 3), device=dev)
+    rgb = torch.empty((nrays, 3), device=dev)
+    near = torch.empty(nrays, device=dev)
+    far = torch.empty(nrays, device=dev)
+    coord = torch.empty((nrays, 2), dtype=torch.int32, device=dev)
+    n_out = torch.zeros(1, dtype=torch.int32, device=dev)
+    nsampled = 0
+    while nsampled < nrays:  # :236-271, one device round per loop iteration
+        n_body = int((nrays - nsampled) * body_sample_ratio)
+        n_face = int((nrays - nsampled) * face_sample_ratio)
+        n_rand = (nrays - nsampled) - n_body - n_face
+        d_body = rng.randint(0, n_body_px, n_body)
+        if n_face_px > 0:
+            d_face = rng.randint(0, n_face_px, n_face)
+        else:
+            d_face = np.zeros(0, dtype=np.int64)
+        d_rand = rng.randint(0, n_bound_px, n_rand)
+        draws = torch.as_tensor(np.concatenate([d_body, d_face, d_rand]).astype(np.int32)).to(dev)
+        _lib.check(lib.anr_train_ray_gather(H, W, dp(Kinv), dp(Rd), dp(Td), dp(o), 1 if fp64 else 0, _lib.ptr(b),
+                                            _lib.ptr(img_d), _lib.ptr(bm_d), 1 if mask_bkgd else 0, _lib.ptr(lists),
+                                            _lib.ptr(draws), len(d_body), len(d_face), len(d_rand), nrays,
+                                            _lib.ptr(ray_o), _lib.ptr(ray_d), _lib.ptr(rgb), _lib.ptr(near),
+                                            _lib.ptr(far), _lib.ptr(coord), _lib.ptr(n_out), stream),
+                   'anr_train_ray_gather')
+        nsampled = int(n_out.item())
+    mask_at_box = torch.ones(nrays, dtype=torch.bool, device=dev)
+    return rgb, ray_o, ray_d, near, far, coord, mask_at_box

@@ -139,6 +139,28 @@ int anr_camera_rays(int H, int W, const double* Kinv, const double* R, const dou
                     const float* bounds, float* ray_o, float* ray_d, float* near_, float* far_, int32_t* coord,
                     uint8_t* mask, int32_t* count, void* workspace, size_t ws_bytes, void* stream);
 
+/* ---- (f) train-split ray sampler: sample_ray_h36m(split='train') (if_nerf_data_utils.py:198-283) ----
+ * Replaces the float64 numpy sampler the reference runs in its DataLoader workers
+ * (tpose_dataset.py:228). Two calls, both asynchronous on `stream`:
+ *  anr_train_ray_lists: the pixel lists np.argwhere(msk == 1), (msk == 13), (bound_mask == 1) of
+ *    :238-249 (row-major), after msk = msk * bound_mask and bound_mask[msk == 100] = 0 (:230-231).
+ *    msk / bound_mask (H*W) u8 device; lists (3 * H*W) int32 device; counts (3) int32 device.
+ *  anr_train_ray_gather: one round of the sampling loop (:236-271). draws (n_body + n_face + n_rand)
+ *    int32 device = the np.random.randint draws into lists 0, 1, 2 in that order (the caller makes
+ *    them with numpy, so the random stream is the reference's); per draw get_rays (:64-89) at the
+ *    pixel, get_near_far (:156-196) on get_rays' arrays (float64 for a float64 camera), rgb = img
+ *    (H*W,3) f32, zero outside bound_mask when mask_bkgd (:228). Hits are appended in draw order
+ *    at index *n_out (device int32, updated), at most cap; outputs ray_o/ray_d/rgb (cap,3),
+ *    near/far (cap), coord (cap,2) (row, col). Camera arguments as anr_camera_rays. */
+size_t anr_train_ray_workspace_bytes(int H, int W);
+int anr_train_ray_lists(int H, int W, const uint8_t* msk, const uint8_t* bound_mask, int32_t* lists, int32_t* counts,
+                        void* workspace, size_t ws_bytes, void* stream);
+int anr_train_ray_gather(int H, int W, const double* Kinv, const double* R, const double* T, const double* origin,
+                         int fp64, const float* bounds, const float* img, const uint8_t* bound_mask, int mask_bkgd,
+                         const int32_t* lists, const int32_t* draws, int n_body, int n_face, int n_rand, int cap,
+                         float* ray_o, float* ray_d, float* rgb, float* near_, float* far_, int32_t* coord,
+                         int32_t* n_out, void* stream);
+
 /* ---- weights --------------------------------------------------------------------------- */
 size_t anr_params_packed_bytes(void);
 int anr_params_pack(const anr_params* p, void* packed, void* stream);

@@ -463,6 +463,71 @@ def main_rays():
     print('ray goldens written')
 
 
+def main_train_rays():
+    """G12: the train-split sampler sample_ray_h36m(split='train') (if_nerf_data_utils.py:198-283)
+    of the real reference, for a float64 and a float32 camera, the second with face pixels
+    (msk == 13) and cfg.face_sample_ratio = 0.2. get_bound_2d_mask uses cv2.fillPoly (cv2 absent):
+    the reference is run with it replaced by animatable_nerf_amd.data.get_bound_2d_mask (case 1: that
+    mask dilated by 8 px, so some drawn rays miss the box and the sampling loop runs again) and the
+    mask is recorded as an input; every np.random.randint call is recorded too."""
+    sys.path.insert(0, REPO)
+    from animatable_nerf_amd.synthetic import Scene
+    from animatable_nerf_amd.data import get_bound_2d_mask
+    cfg, _, _ = import_reference()
+    from lib.utils.if_nerf import if_nerf_data_utils as dutils
+    scene = Scene(vsize=0.05)
+    real_randint = np.random.randint
+    draws = []
+
+    def rec_randint(lo, hi, n):
+        r = real_randint(lo, hi, n)
+        draws.append(np.asarray(r, dtype=np.int64))
+        return r
+    np.random.randint = rec_randint
+    out = {'bounds': scene.bounds}
+    for case, dt, face_ratio in ((0, np.float64, 0.0), (1, np.float32, 0.2)):
+        H, W = 120, 100
+        a = np.deg2rad(20.0 + 15.0 * case)
+        K = np.array([[140.5, 0.0, 49.3], [0.0, 141.25, 61.7], [0.0, 0.0, 1.0]], dtype=dt)
+        R = np.array([[np.cos(a), 0.0, -np.sin(a)], [0.0, -1.0, 0.0], [-np.sin(a), 0.0, -np.cos(a)]], dtype=dt)
+        T = np.array([[0.05], [-0.02], [2.9]], dtype=dt)
+        g = np.random.default_rng(40 + case)
+        img = g.random((H, W, 3), dtype=np.float32)
+        yy, xx = np.mgrid[0:H, 0:W]
+        e = ((xx - 50.0) / 16.0) ** 2 + ((yy - 58.0) / 40.0) ** 2
+        msk = np.zeros((H, W), dtype=np.uint8)
+        msk[e < 1.0] = 1
+        msk[(e >= 1.0) & (e < 1.3)] = 100  # the dataset's eroded/dilated border band
+        if case == 1:
+            msk[(np.abs(xx - 50) < 4) & (np.abs(yy - 26) < 4)] = 13
+        cfg.face_sample_ratio = face_ratio
+        cfg.body_sample_ratio = 0.5
+        cfg.mask_bkgd = True
+        pose = np.concatenate([R, T], axis=1)
+        bm = get_bound_2d_mask(scene.bounds, K, pose, H, W)
+        if case == 1:  # a mask wider than the box (8 px) so that rays miss and the loop runs again
+            d = np.zeros_like(bm)
+            for dy in range(-8, 9):
+                for dx in range(-8, 9):
+                    d |= np.roll(np.roll(bm, dy, 0), dx, 1)
+            bm = d
+        dutils.get_bound_2d_mask = lambda *a, _bm=bm: _bm.copy()
+        np.random.seed(100 + case)
+        draws.clear()
+        rgb, ro, rd, near, far, coord, mab = dutils.sample_ray_h36m(img.copy(), msk.copy(), K, R, T, scene.bounds,
+                                                                  512, 'train')
+        pre = f'c{case}_'
+        out.update({pre + 'K': K, pre + 'R': R, pre + 'T': T, pre + 'img': img, pre + 'msk': msk, pre + 'bound_mask': bm,
+                    pre + 'seed': 100 + case, pre + 'face_ratio': face_ratio, pre + 'rgb': rgb, pre + 'ray_o': ro,
+                    pre + 'ray_d': rd, pre + 'near': near, pre + 'far': far, pre + 'coord': coord,
+                    pre + 'n_randint': len(draws), pre + 'draws': np.concatenate(draws)})
+        print('case', case, 'rounds', len(draws), 'rays', len(near))
+    np.random.randint = real_randint
+    out['nrays'] = 512
+    np.savez_compressed(os.path.join(OUT, 'g12_train_rays.npz'), **out)
+    print('train-ray goldens written')
+
+
 def main_mmsk():
     """G9: the novel-view renderer with the training-view visibility filter
     (lib/networks/renderer/tpose_renderer_mmsk.py) over the aninerf network: 3 training views
@@ -637,6 +702,8 @@ if __name__ == '__main__':
         main_mesh()
     elif len(sys.argv) > 1 and sys.argv[1] == '--mmsk':
         main_mmsk()
+    elif len(sys.argv) > 1 and sys.argv[1] == '--train-rays':
+        main_train_rays()
     elif len(sys.argv) > 1 and sys.argv[1] == '--rays':
         main_rays()
     elif len(sys.argv) > 1 and sys.argv[1] == '--novel':

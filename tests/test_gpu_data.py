@@ -46,3 +46,56 @@ def test_camera_rays_feed_render():
     out = Renderer(net, cfg).render_device(batch, bw_rows=False)
     assert out['rgb_map'].shape == (1, int(mask.sum()), 3)
     assert torch.isfinite(out['rgb_map']).all() and out['acc_map'].max() > 0.1
+
+
+class _CountingRNG:
+    """np.random.RandomState that counts randint calls (the reference's call sequence)."""
+
+    def __init__(self, seed):
+        self.rs = np.random.RandomState(seed)
+        self.calls = []
+
+    def randint(self, lo, hi, n):
+        r = self.rs.randint(lo, hi, n)
+        self.calls.append(np.asarray(r, dtype=np.int64))
+        return r
+
+
+@pytest.mark.parametrize('case', [0, 1])
+def test_train_ray_sampler_bit_exact(case):
+    """(f) train-split sampler sample_ray_h36m(split='train') through anr_train_ray_lists/gather vs the
+    reference run (golden G12): same draws, and rays, float64 box test, rgb and coords bit-exact."""
+    if not torch.cuda.is_available():
+        pytest.fail('GPU test run without a GPU')
+    from animatable_nerf_amd import data
+    g = golden('g12_train_rays')
+    p = f'c{case}_'
+    rng = _CountingRNG(int(g[p + 'seed']))
+    rgb, ro, rd, near, far, coord, mab = data.sample_ray_h36m(
+        g[p + 'img'], g[p + 'msk'], g[p + 'K'], g[p + 'R'], g[p + 'T'], g['bounds'], int(g['nrays']), 'train',
+        mask_bkgd=True, body_sample_ratio=0.5, face_sample_ratio=float(g[p + 'face_ratio']),
+        bound_mask=g[p + 'bound_mask'], rng=rng)
+    assert len(rng.calls) == int(g[p + 'n_randint'])
+    assert np.array_equal(np.concatenate(rng.calls), g[p + 'draws'])
+    for k, v in (('rgb', rgb), ('ray_o', ro), ('ray_d', rd), ('near', near), ('far', far), ('coord', coord)):
+        assert np.array_equal(v.cpu().numpy(), g[p + k].astype(v.cpu().numpy().dtype)), k
+    assert bool(mab.all()) and mab.numel() == int(g['nrays'])
+
+
+def test_train_ray_sampler_edge_cases():
+    """Edge cases of the device sampler: an empty body list raises like np.random.randint(0, 0, n);
+    the pixel lists equal np.argwhere order; the test split returns the eval pipeline's rays with
+    rgb zeroed outside the bound mask."""
+    from animatable_nerf_amd import data
+    g = golden('g12_train_rays')
+    img, msk, bm = g['c1_img'], g['c1_msk'], g['c1_bound_mask']
+    with pytest.raises(ValueError):
+        data.sample_ray_h36m(img, np.zeros_like(msk), g['c1_K'], g['c1_R'], g['c1_T'], g['bounds'], 64, 'train',
+                             bound_mask=bm, rng=np.random.RandomState(0))
+    rgb, ro, rd, near, far, coord, mab = data.sample_ray_h36m(img, msk, g['c1_K'], g['c1_R'], g['c1_T'], g['bounds'],
+                                                              0, 'test', bound_mask=bm)
+    m = mab.cpu().numpy().reshape(120, 100)
+    c = coord.cpu().numpy()
+    assert np.array_equal(c, np.argwhere(m))
+    ref = np.where((bm == 1)[..., None], img, 0)[c[:, 0], c[:, 1]]
+    assert np.array_equal(rgb.cpu().numpy(), ref)

@@ -195,3 +195,42 @@ def test_mmsk_render_bit_exact():
     assert np.array_equal(bits, g['chunks_inside_bits'])
     for k in ('rgb_map', 'acc_map', 'depth_map'):
         np.testing.assert_array_equal(ret[k].numpy(), g['chunks_' + k], err_msg=k)
+
+
+@pytest.mark.parametrize('case', [0, 1])
+def test_train_ray_sampler_bit_exact(case):
+    """G12: sample_ray_h36m(split='train') of the reference (float64 camera; float32 camera with face
+    pixels, face ratio 0.2 and a widened bound mask that makes the sampling loop run 8 rounds) vs the
+    restatement replaying the same seeded np.random stream."""
+    g = golden('g12_train_rays')
+    p = f'c{case}_'
+    rng = np.random.RandomState(int(g[p + 'seed']))
+    res = restate.sample_ray_train(g[p + 'img'], g[p + 'msk'], g[p + 'K'], g[p + 'R'], g[p + 'T'], g['bounds'],
+                                   int(g['nrays']), g[p + 'bound_mask'], True, 0.5, float(g[p + 'face_ratio']), rng)
+    for k in ('rgb', 'ray_o', 'ray_d', 'near', 'far', 'coord'):
+        assert res[k].dtype == g[p + k].dtype, k
+        assert np.array_equal(res[k], g[p + k]), k
+
+
+def test_bound_2d_mask_is_projected_box():
+    """get_bound_2d_mask restatement (cv2.fillPoly absent: unpinned at the boundary): every pixel
+    of the mask lies inside the convex hull of the projected corners, and the rays through its
+    interior hit the box."""
+    from animatable_nerf_amd import data
+    g = golden('g12_train_rays')
+    K, R, T = g['c0_K'], g['c0_R'], g['c0_T']
+    pose = np.concatenate([R, T], axis=1)
+    bm = data.get_bound_2d_mask(g['bounds'], K, pose, 120, 100)
+    assert np.array_equal(bm, g['c0_bound_mask'])
+    c2 = data._project(data.get_bound_corners(g['bounds']), K, pose)
+    ys, xs = np.nonzero(bm)
+    assert xs.min() >= np.floor(c2[:, 0].min()) and xs.max() <= np.ceil(c2[:, 0].max())
+    assert ys.min() >= np.floor(c2[:, 1].min()) and ys.max() <= np.ceil(c2[:, 1].max())
+    ro, rd = restate.get_rays(120, 100, K, R, T)
+    inner = bm.copy()
+    for dy in (-1, 0, 1):
+        for dx in (-1, 0, 1):
+            inner &= np.roll(np.roll(bm, dy, 0), dx, 1)
+    sel = inner.astype(bool)
+    _, _, hit = restate.near_far(g['bounds'], ro[sel], rd[sel])
+    assert hit.all()
