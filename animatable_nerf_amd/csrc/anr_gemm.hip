@@ -32,7 +32,7 @@ struct Tile4 {
 
 template <bool KCONTIG>
 __device__ __forceinline__ void load_tile(const float* __restrict__ P, long rs, long cs, int R, int r0, int K, int k0,
-                                          int tid, Tile4& t) {
+                                          int tid, Tile4& t, bool vec) {
   // 64 (r) x 32 (k) elements = 512 float4 groups, 2 per thread
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
@@ -51,7 +51,9 @@ __device__ __forceinline__ void load_tile(const float* __restrict__ P, long rs, 
       // 4 consecutive k of row gr
       if (gr < R) {
         const float* p = P + (long)gr * rs + (long)gk * cs;
-        if (gk + 3 < K) {
+        if (gk + 3 < K && vec) {
+          x = *(const float4*)p;
+        } else if (gk + 3 < K) {
           x.x = p[0]; x.y = p[1]; x.z = p[2]; x.w = p[3];
         } else {
           if (gk < K) x.x = p[0];
@@ -63,7 +65,9 @@ __device__ __forceinline__ void load_tile(const float* __restrict__ P, long rs, 
       // 4 consecutive r of k-row gk
       if (gk < K) {
         const float* p = P + (long)gr * rs + (long)gk * cs;
-        if (gr + 3 < R) {
+        if (gr + 3 < R && vec) {
+          x = *(const float4*)p;
+        } else if (gr + 3 < R) {
           x.x = p[0]; x.y = p[rs]; x.z = p[2 * rs]; x.w = p[3 * rs];
         } else {
           if (gr < R) x.x = p[0];
@@ -88,6 +92,28 @@ __device__ __forceinline__ void store_tile(float (*S)[GLD], int tid, const Tile4
     } else {
       const int k = q >> 4, r = (q & 15) * 4;
       *(float4*)&S[k][r] = make_float4(t.v[h][0], t.v[h][1], t.v[h][2], t.v[h][3]);
+    }
+  }
+}
+
+// rows r = 4 (tid & 15) .. +3 of the A tile are summed by the threads sharing tid & 15: lanes l, l^16,
+// l^32, l^48 of each wave, then one atomic per row and wave
+__device__ __forceinline__ void rowsum_flush(const GemmArgs& g, int m0, float (&rsum)[4]) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int M = g.M_dev ? *g.M_dev : g.M;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    rsum[e] += __shfl_xor(rsum[e], 16);
+    rsum[e] += __shfl_xor(rsum[e], 32);
+  }
+  if (lane < 16) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int m = m0 + 4 * lane + e;
+      if (m < M) {
+        atomicAdd(g.rowsum + m, rsum[e]);
+        if (g.rowsum2) atomicAdd(g.rowsum2 + m, rsum[e]);
+      }
     }
   }
 }
@@ -121,9 +147,15 @@ __global__ __launch_bounds__(256) void k_gemm_t(GemmArgs g) {
   int s = 0, k0 = kb;
   int kend = (g.ksplit > 1) ? ke : g.seg[0].K;
   Tile4 ta, tb;
-  load_tile<A_K>(g.seg[0].A, g.seg[0].a_rs, g.seg[0].a_cs, M, m0, kend, k0, tid, ta);
-  load_tile<B_K>(g.seg[0].B, g.seg[0].b_cs, g.seg[0].b_rs, g.N, n0, kend, k0, tid, tb);
+  load_tile<A_K>(g.seg[0].A, g.seg[0].a_rs, g.seg[0].a_cs, M, m0, kend, k0, tid, ta, g.a_vec[0]);
+  load_tile<B_K>(g.seg[0].B, g.seg[0].b_cs, g.seg[0].b_rs, g.N, n0, kend, k0, tid, tb, g.b_vec[0]);
+  float rsum[4] = {0.f, 0.f, 0.f, 0.f};
+  const bool do_rsum = !A_K && g.rowsum != nullptr && blockIdx.x == 0;
   while (true) {
+    if (do_rsum) {  // A(r..r+3, k) in the thread's registers (!A_K layout), out-of-range entries are 0
+#pragma unroll
+      for (int e = 0; e < 4; ++e) rsum[e] += ta.v[0][e] + ta.v[1][e];
+    }
     store_tile<A_K>(As, tid, ta);
     store_tile<B_K>(Bs, tid, tb);
     __syncthreads();
@@ -136,8 +168,8 @@ __global__ __launch_bounds__(256) void k_gemm_t(GemmArgs g) {
     const bool more = ns < g.nseg && (g.ksplit == 1 || ns == 0);
     if (more) {
       const int kend2 = (g.ksplit > 1) ? ke : g.seg[ns].K;
-      load_tile<A_K>(g.seg[ns].A, g.seg[ns].a_rs, g.seg[ns].a_cs, M, m0, kend2, nk, tid, ta);
-      load_tile<B_K>(g.seg[ns].B, g.seg[ns].b_cs, g.seg[ns].b_rs, g.N, n0, kend2, nk, tid, tb);
+      load_tile<A_K>(g.seg[ns].A, g.seg[ns].a_rs, g.seg[ns].a_cs, M, m0, kend2, nk, tid, ta, g.a_vec[ns]);
+      load_tile<B_K>(g.seg[ns].B, g.seg[ns].b_cs, g.seg[ns].b_rs, g.N, n0, kend2, nk, tid, tb, g.b_vec[ns]);
     }
 #pragma unroll
     for (int ks = 0; ks < GBK; ks += 4) {
@@ -159,6 +191,7 @@ __global__ __launch_bounds__(256) void k_gemm_t(GemmArgs g) {
     kend = (g.ksplit > 1) ? ke : g.seg[s].K;
   }
   // epilogue: lane holds C[wr + i*16 + 4*(lane>>4) + r][wc + j*16 + (lane&15)]
+  if (do_rsum) rowsum_flush(g, m0, rsum);
   const bool first_split = blockIdx.z == 0;
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -218,7 +251,7 @@ struct Tile16 {
 
 template <bool KCONTIG>
 __device__ __forceinline__ void load_tile16(const float* __restrict__ P, long rs, long cs, int R, int r0, int K, int k0,
-                                            int tid, Tile16& t) {
+                                            int tid, Tile16& t, bool vec) {
   // 64 (r) x 64 (k) elements = 1024 groups of 4, 4 per thread
 #pragma unroll
   for (int h = 0; h < 4; ++h) {
@@ -236,7 +269,10 @@ __device__ __forceinline__ void load_tile16(const float* __restrict__ P, long rs
     if (KCONTIG) {
       if (gr < R) {
         const float* p = P + (long)gr * rs + (long)gk * cs;
-        if (gk + 3 < K) {
+        if (gk + 3 < K && vec) {
+          const float4 v = *(const float4*)p;
+          x0 = v.x; x1 = v.y; x2 = v.z; x3 = v.w;
+        } else if (gk + 3 < K) {
           x0 = p[0]; x1 = p[1]; x2 = p[2]; x3 = p[3];
         } else {
           if (gk < K) x0 = p[0];
@@ -247,7 +283,10 @@ __device__ __forceinline__ void load_tile16(const float* __restrict__ P, long rs
     } else {
       if (gk < K) {
         const float* p = P + (long)gr * rs + (long)gk * cs;
-        if (gr + 3 < R) {
+        if (gr + 3 < R && vec) {
+          const float4 v = *(const float4*)p;
+          x0 = v.x; x1 = v.y; x2 = v.z; x3 = v.w;
+        } else if (gr + 3 < R) {
           x0 = p[0]; x1 = p[rs]; x2 = p[2 * rs]; x3 = p[3 * rs];
         } else {
           if (gr < R) x0 = p[0];
@@ -260,28 +299,50 @@ __device__ __forceinline__ void load_tile16(const float* __restrict__ P, long rs
   }
 }
 
+// LDS images: a k-contiguous operand as [r][k] (row stride BLD), read as 16-B fragments; an
+// r-contiguous one (weight gradients, dY W) as [k][r] (row stride RLD), written as it was loaded
+// (8 B per 4 consecutive r) and read with the transposing ds_read_b64_tr_b16 (two per fragment).
+#define RLD (64 + 4)
+typedef short v4s __attribute__((ext_vector_type(4)));
+
 template <bool KCONTIG>
-__device__ __forceinline__ void store_tile16(unsigned short (*S)[BLD], int tid, const Tile16& t) {
+__device__ __forceinline__ void store_tile16(unsigned short* S, int tid, const Tile16& t) {
 #pragma unroll
   for (int h = 0; h < 4; ++h) {
     const int q = tid + h * 256;
+    const uint32_t lo = (uint32_t)f2bf(t.v[h][0]) | ((uint32_t)f2bf(t.v[h][1]) << 16);
+    const uint32_t hi = (uint32_t)f2bf(t.v[h][2]) | ((uint32_t)f2bf(t.v[h][3]) << 16);
     if (KCONTIG) {
       const int r = q >> 4, k = (q & 15) * 4;
-      const uint32_t lo = (uint32_t)f2bf(t.v[h][0]) | ((uint32_t)f2bf(t.v[h][1]) << 16);
-      const uint32_t hi = (uint32_t)f2bf(t.v[h][2]) | ((uint32_t)f2bf(t.v[h][3]) << 16);
-      *(uint2*)&S[r][k] = make_uint2(lo, hi);
+      *(uint2*)&S[r * BLD + k] = make_uint2(lo, hi);
     } else {
       const int k = q >> 4, r = (q & 15) * 4;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) S[r + e][k] = f2bf(t.v[h][e]);
+      *(uint2*)&S[k * RLD + r] = make_uint2(lo, hi);
     }
   }
 }
 
+// MFMA 16x16x32 operand fragment of rows rb..rb+15, k = ks + 8 (lane >> 4) .. + 7
+template <bool KCONTIG>
+__device__ __forceinline__ bf16x8 frag16(const unsigned short* S, int rb, int ks, int lane) {
+  if (KCONTIG) return *(const bf16x8*)&S[(rb + (lane & 15)) * BLD + ks + 8 * (lane >> 4)];
+  // 16-lane group g reads rows k = ks + 8g + q (q = 0..3, then 4..7), lane 4q + p supplying columns
+  // rb + 4p .. +3 of row q; lane i receives column rb + i, element q = row q
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  typedef __attribute__((address_space(3))) v4s lds_v4s;
+  const unsigned short* a0 = S + (ks + 8 * g + q) * RLD + rb + 4 * p;
+  const v4s x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(uintptr_t)(unsigned)(uintptr_t)a0);
+  const v4s x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(uintptr_t)(unsigned)(uintptr_t)(a0 + 4 * RLD));
+  bf16x8 f;
+  const short e[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+  __builtin_memcpy(&f, e, 16);
+  return f;
+}
+
 template <bool A_K, bool B_K>
 __global__ __launch_bounds__(256) void k_gemm_b(GemmArgs g) {
-  __shared__ __attribute__((aligned(16))) unsigned short As[GBM][BLD];
-  __shared__ __attribute__((aligned(16))) unsigned short Bs[GBN][BLD];
+  __shared__ __attribute__((aligned(16))) unsigned short As[GBM * BLD];
+  __shared__ __attribute__((aligned(16))) unsigned short Bs[GBN * BLD];
   const int M = g.M_dev ? *g.M_dev : g.M;
   const int m0 = blockIdx.y * GBM, n0 = blockIdx.x * GBN;
   if (m0 >= M) return;
@@ -302,9 +363,15 @@ __global__ __launch_bounds__(256) void k_gemm_b(GemmArgs g) {
   int s = 0, k0 = kb;
   int kend = (g.ksplit > 1) ? ke : g.seg[0].K;
   Tile16 ta, tb;
-  load_tile16<A_K>(g.seg[0].A, g.seg[0].a_rs, g.seg[0].a_cs, M, m0, kend, k0, tid, ta);
-  load_tile16<B_K>(g.seg[0].B, g.seg[0].b_cs, g.seg[0].b_rs, g.N, n0, kend, k0, tid, tb);
+  load_tile16<A_K>(g.seg[0].A, g.seg[0].a_rs, g.seg[0].a_cs, M, m0, kend, k0, tid, ta, g.a_vec[0]);
+  load_tile16<B_K>(g.seg[0].B, g.seg[0].b_cs, g.seg[0].b_rs, g.N, n0, kend, k0, tid, tb, g.b_vec[0]);
+  float rsum[4] = {0.f, 0.f, 0.f, 0.f};
+  const bool do_rsum = !A_K && g.rowsum != nullptr && blockIdx.x == 0;
   while (true) {
+    if (do_rsum) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) rsum[e] += (ta.v[0][e] + ta.v[1][e]) + (ta.v[2][e] + ta.v[3][e]);
+    }
     store_tile16<A_K>(As, tid, ta);
     store_tile16<B_K>(Bs, tid, tb);
     __syncthreads();
@@ -316,17 +383,16 @@ __global__ __launch_bounds__(256) void k_gemm_b(GemmArgs g) {
     const bool more = ns < g.nseg && (g.ksplit == 1 || ns == 0);
     if (more) {
       const int kend2 = (g.ksplit > 1) ? ke : g.seg[ns].K;
-      load_tile16<A_K>(g.seg[ns].A, g.seg[ns].a_rs, g.seg[ns].a_cs, M, m0, kend2, nk, tid, ta);
-      load_tile16<B_K>(g.seg[ns].B, g.seg[ns].b_cs, g.seg[ns].b_rs, g.N, n0, kend2, nk, tid, tb);
+      load_tile16<A_K>(g.seg[ns].A, g.seg[ns].a_rs, g.seg[ns].a_cs, M, m0, kend2, nk, tid, ta, g.a_vec[ns]);
+      load_tile16<B_K>(g.seg[ns].B, g.seg[ns].b_cs, g.seg[ns].b_rs, g.N, n0, kend2, nk, tid, tb, g.b_vec[ns]);
     }
 #pragma unroll
     for (int ks = 0; ks < BBK; ks += 32) {
-      const int kk = ks + 8 * (lane >> 4);
       bf16x8 a[2], b[2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) a[i] = *(const bf16x8*)&As[wr + i * 16 + (lane & 15)][kk];
+      for (int i = 0; i < 2; ++i) a[i] = frag16<A_K>(As, wr + i * 16, ks, lane);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) b[j] = *(const bf16x8*)&Bs[wc + j * 16 + (lane & 15)][kk];
+      for (int j = 0; j < 2; ++j) b[j] = frag16<B_K>(Bs, wc + j * 16, ks, lane);
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -338,6 +404,7 @@ __global__ __launch_bounds__(256) void k_gemm_b(GemmArgs g) {
     k0 = nk;
     kend = (g.ksplit > 1) ? ke : g.seg[s].K;
   }
+  if (do_rsum) rowsum_flush(g, m0, rsum);
   const bool first_split = blockIdx.z == 0;
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -375,8 +442,18 @@ template __global__ void k_gemm_t<false, false>(GemmArgs);
 
 // host-side dispatch on the operand layouts
 void launch_gemm(GemmArgs g, dim3 grid, hipStream_t s) {
-  const bool a_k = g.seg[0].a_cs == 1;
+  // a one-row A (a_rs == a_cs == 1: the weight gradient of a 1-output layer) is contiguous both ways;
+  // with row sums requested it takes the m-contiguous path, the one that computes them
+  const bool a_k = g.seg[0].a_cs == 1 && !(g.rowsum && g.seg[0].a_rs == 1);
   const bool b_k = g.seg[0].b_rs == 1;
+  // 16-B operand loads where every 4-group the tile reads is aligned: base aligned and the stride
+  // between the groups a multiple of 4 floats (the groups run along the contiguous dimension)
+  for (int i = 0; i < g.nseg; ++i) {
+    const GemmSeg& q = g.seg[i];
+    const long a_stride = a_k ? q.a_rs : q.a_cs, b_stride = b_k ? q.b_cs : q.b_rs;
+    g.a_vec[i] = ((uintptr_t)q.A % 16 == 0) && (a_stride % 4 == 0) && (a_k || q.a_rs == 1);
+    g.b_vec[i] = ((uintptr_t)q.B % 16 == 0) && (b_stride % 4 == 0) && (b_k || q.b_cs == 1);
+  }
   if (g.bf16) {  // the sdf epilogues (softplus, div) are fp32-path only
     if (a_k && b_k) hipLaunchKernelGGL((k_gemm_b<true, true>), grid, dim3(256), 0, s, g);
     else if (a_k) hipLaunchKernelGGL((k_gemm_b<true, false>), grid, dim3(256), 0, s, g);
@@ -388,23 +465,6 @@ void launch_gemm(GemmArgs g, dim3 grid, hipStream_t s) {
   else if (a_k) hipLaunchKernelGGL((k_gemm_t<true, false>), grid, dim3(256), 0, s, g);
   else if (b_k) hipLaunchKernelGGL((k_gemm_t<false, true>), grid, dim3(256), 0, s, g);
   else hipLaunchKernelGGL((k_gemm_t<false, false>), grid, dim3(256), 0, s, g);
-}
-
-// column sums of X[M][N] (ld) into out[N] (+=), M from device when given: bias gradients
-__global__ __launch_bounds__(256) void k_colsum(const float* __restrict__ X, long ld, int M, const int* M_dev, int N,
-                                                float* __restrict__ out, int rows_per_block) {
-  const int MM = M_dev ? *M_dev : M;
-  const int n = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int r0 = blockIdx.y * rows_per_block;
-  const int r1 = min(MM, r0 + rows_per_block);
-  float s = 0.f;
-  for (int m = r0 + (threadIdx.x >> 6); m < r1; m += 4)
-    if (n < N) s += X[(long)m * ld + n];
-  __shared__ float sh[4][64];
-  sh[threadIdx.x >> 6][threadIdx.x & 63] = s;
-  __syncthreads();
-  if (threadIdx.x < 64 && n < N && r0 < r1)
-    atomicAdd(out + n, sh[0][threadIdx.x] + sh[1][threadIdx.x] + sh[2][threadIdx.x] + sh[3][threadIdx.x]);
 }
 
 }  // namespace anr

@@ -36,6 +36,11 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 #ifndef ANR_MIDSYNC
 #define ANR_MIDSYNC 1
 #endif
+// waves that issue the weight stream: 8 (all, default) or 4 (one per SIMD: waves w and w+4 share a
+// SIMD, so while one issues its LDS-DMA pieces the other keeps the SIMD's MFMA pipe busy)
+#ifndef ANR_DMA_WAVES
+#define ANR_DMA_WAVES 8
+#endif
 // LDS fragment reads in flight ahead of the MFMAs (bf16x3 layers)
 #ifndef ANR_FRAG_PF
 #define ANR_FRAG_PF 1
@@ -152,13 +157,34 @@ struct Pipe {
 #ifdef ANR_EXP_NODMA
     return;  // timing experiment only: no weight stream (results are garbage)
 #endif
+#ifdef ANR_EXP_HALFDMA
+    loads = (loads + 1) / 2;  // timing experiment only: half the pieces (results are garbage)
+#endif
+#ifdef ANR_EXP_SAMEDMA
+    off = 0;  // timing experiment only: every slice re-reads the first 32 KiB (L2-resident footprint)
+#endif
+    if constexpr (ANR_DMA_WAVES == 4) {
+      if (wave >= 4) return;
+      loads *= 2;
+    }
     for (int i = 0; i < loads; ++i) {
-      int piece = wave + 8 * i;
+      int piece = wave + ANR_DMA_WAVES * i;
       piece = piece < kb ? piece : kb - 1;
       const unsigned char* src = w + off + piece * 1024 + lane * 16;
       const unsigned m0 = dst + piece * 1024;
       asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(m0)
                    : "memory");
+    }
+  }
+
+  // wait until this wave's pieces of all but the last N (8-wave count) issued pieces have landed
+  template <int N>
+  __device__ __forceinline__ void wait_stream() {
+    if constexpr (ANR_DMA_WAVES == 4) {
+      if (wave < 4) wait_vmcnt<2 * N>();
+      else wait_vmcnt<0>();
+    } else {
+      wait_vmcnt<N>();
     }
   }
 
@@ -177,7 +203,7 @@ struct Pipe {
     });
     cur = 0;
     if constexpr (ANR_MIDSYNC) {
-      wait_vmcnt<prog_later_loads<B16, V>(0, 0)>();
+      wait_stream<prog_later_loads<B16, V>(0, 0)>();
       __syncthreads();
     }
   }
@@ -192,7 +218,7 @@ struct Pipe {
     if constexpr (!ANR_MIDSYNC) {
       constexpr int NB = mlp_nbuf<B16>();
       constexpr int eq = prog_advance<B16, V>(E, Q, NB - 1);
-      wait_vmcnt<prog_later_loads<B16, V>(E, Q)>();
+      wait_stream<prog_later_loads<B16, V>(E, Q)>();
       __syncthreads();
       int slot = cur + NB - 1;
       slot = slot >= NB ? slot - NB : slot;
@@ -209,7 +235,7 @@ struct Pipe {
       constexpr int NB = mlp_nbuf<B16>();
       constexpr int e1 = prog_advance<B16, V>(E, Q, 1);
       constexpr int eq = prog_advance<B16, V>(E, Q, NB - 1);
-      wait_vmcnt<prog_later_loads<B16, V>(e1 / 1024, e1 % 1024)>();
+      wait_stream<prog_later_loads<B16, V>(e1 / 1024, e1 % 1024)>();
 #ifndef ANR_EXP_NOBAR
       __syncthreads();
 #endif

@@ -38,10 +38,16 @@ struct GemmArgs {
   int spd_n;
   float div_post;      // v = v / div_post after the activation (cat(...)/sqrt(2) forward)
   int bf16;            // operands rounded to bf16, bf16 MFMA, fp32 accumulate (training precision)
+  // weight-gradient GEMMs (A(m,k) = dY[k][m]): the fp32 row sums of A over this launch's k range
+  // (= the bias gradient, the column sums of dY) are atomically added into rowsum[m] (and rowsum2[m])
+  // by the workgroups of the first N tile; NULL: off
+  float* rowsum;
+  float* rowsum2;
+  // per segment: the operand tiles may be read with 16-B loads (aligned base, stride a multiple of 4)
+  int a_vec[2], b_vec[2];
 };
 
 void launch_gemm(GemmArgs g, dim3 grid, hipStream_t s);
-__global__ void k_colsum(const float* X, long ld, int M, const int* M_dev, int N, float* out, int rows_per_block);
 
 // per-point training buffers (row-major, compact kept-sample order)
 struct TrainBufs {

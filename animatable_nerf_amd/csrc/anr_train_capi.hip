@@ -91,14 +91,18 @@ struct Exec {
     return gemm(g, n);
   }
 
-  // dW[:, c0:c0+K] += dY^T X (split-K over samples, atomics)
-  int wgrad(float* dW, int in_ch, int c0, int Nout, const float* dY, int ldY, const float* X, int ldX, int K) {
+  // dW[:, c0:c0+K] += dY^T X (split-K over samples, atomics); the column sums of dY (the bias
+  // gradient) are added into bsum (and bsum2) in the same pass when given
+  int wgrad(float* dW, int in_ch, int c0, int Nout, const float* dY, int ldY, const float* X, int ldX, int K,
+            float* bsum = nullptr, float* bsum2 = nullptr) {
     GemmArgs g{};
+    g.rowsum = bsum;
+    g.rowsum2 = bsum2;
     g.N = K;
     g.nseg = 1;
     g.seg[0] = GemmSeg{dY, 1, ldY, X, ldX, 1, n};
     g.C = dW + c0; g.ldc = in_ch; g.atomic = 1;
-    g.ksplit = (n + 1023) / 1024;
+    g.ksplit = (n + 511) / 512;  // 512 samples per split (measured: 1024 / 512 / 256 / 2048)
     return gemm(g, Nout);
   }
 
@@ -113,14 +117,6 @@ struct Exec {
     if (dY2) g.seg[1] = GemmSeg{dY2, ldY2, 1, W2 + c0, in_ch2, 1, Nout2};
     g.C = dX; g.ldc = ldX; g.mask = mask; g.ldm = ldm; g.accumulate = accumulate ? 1 : 0; g.ksplit = 1;
     return gemm(g, n);
-  }
-
-  int colsum(const float* X, int ld, int N, float* out) {
-    if (n <= 0) return ANR_OK;
-    const int rpb = 256;
-    hipLaunchKernelGGL(k_colsum, dim3((N + 63) / 64, (n + rpb - 1) / rpb), dim3(256), 0, s, X, (long)ld, n,
-                       (const int*)nullptr, N, out, rpb);
-    return check_launch("k_colsum");
   }
 };
 
@@ -196,8 +192,7 @@ int bw_backward(Exec& e, const float* const* W, float* const* g, const float* G,
   const long S = N * 256;
   // bw_fc
   if (g) {
-    ANR_TRY(e.wgrad(g[17], 256, 0, 24, dlog, 32, H + 7 * S, 256, 256));
-    ANR_TRY(e.colsum(dlog, 32, 24, g[18]));
+    ANR_TRY(e.wgrad(g[17], 256, 0, 24, dlog, 32, H + 7 * S, 256, 256, g[18]));
   }
   ANR_TRY(e.xgrad(dA, 256, 256, dlog, 32, 24, W[17], 256, 0, H + 7 * S, 256, false));
   float* cur = dA;
@@ -209,13 +204,11 @@ int bw_backward(Exec& e, const float* const* W, float* const* g, const float* G,
       if (g) {
         float* ys = ysum + (l == 5 ? 256 : 0);
         if (hipMemsetAsync(ys, 0, 256 * 4, s) != hipSuccess) return fail(ANR_E_HIP, "memset");
-        ANR_TRY(e.colsum(cur, 256, 256, ys));
+        // bias grad and the latent-row gradient's column sum, in the weight-gradient pass
+        ANR_TRY(e.wgrad(g[wi], in_ch, 0, 256, cur, 256, G, 64, 63, g[bi], ys));
         hipLaunchKernelGGL(k_tr_latent_grad, dim3(256 + 128), dim3(128), 0, s, (const float*)ys, W[wi], in_ch, 63, 256,
                            W[0], li, add, g[wi], g[0]);
         ANR_TRY(check_launch("k_tr_latent_grad"));
-        // bias grad = same column sum
-        ANR_TRY(e.colsum(cur, 256, 256, g[bi]));
-        ANR_TRY(e.wgrad(g[wi], in_ch, 0, 256, cur, 256, G, 64, 63));
       }
       if (dG) ANR_TRY(e.xgrad(dG, 64, 63, cur, 256, 256, W[wi], in_ch, 0, nullptr, 0, true));
       if (l == 5) {
@@ -223,10 +216,7 @@ int bw_backward(Exec& e, const float* const* W, float* const* g, const float* G,
         ANR_TRY(e.xgrad(nxt, 256, 256, cur, 256, 256, W[wi], in_ch, 191, H + 4 * S, 256, false));
       }
     } else {
-      if (g) {
-        ANR_TRY(e.colsum(cur, 256, 256, g[bi]));
-        ANR_TRY(e.wgrad(g[wi], 256, 0, 256, cur, 256, H + (l - 1) * S, 256, 256));
-      }
+      if (g) ANR_TRY(e.wgrad(g[wi], 256, 0, 256, cur, 256, H + (l - 1) * S, 256, 256, g[bi]));
       ANR_TRY(e.xgrad(nxt, 256, 256, cur, 256, 256, W[wi], 256, 0, H + (l - 1) * S, 256, false));
     }
     if (l > 0) {
@@ -322,45 +312,38 @@ int train_backward(const anr_params* p, float* const* g, const anr_frame* f, con
   hipLaunchKernelGGL(k_tr_raw_bwd, dim3(g1), dim3(256), 0, s, b);
   ANR_TRY(check_launch("k_tr_raw_bwd"));
   // rgb_fc, view_fc (ReLU), latent_fc (latent folded), feature_fc || alpha_fc
-  ANR_TRY(e.wgrad(g[25], 128, 0, 3, b.dRgb, 4, View, 128, 128));
-  ANR_TRY(e.colsum(b.dRgb, 4, 3, g[26]));
+  ANR_TRY(e.wgrad(g[25], 128, 0, 3, b.dRgb, 4, View, 128, 128, g[26]));
   ANR_TRY(e.xgrad(dView, 128, 128, b.dRgb, 4, 3, PT(25), 128, 0, View, 128, false));
-  ANR_TRY(e.wgrad(g[23], 283, 0, 128, dView, 128, Lat, 256, 256));
+  ANR_TRY(e.wgrad(g[23], 283, 0, 128, dView, 128, Lat, 256, 256, g[24]));
   ANR_TRY(e.wgrad(g[23], 283, 256, 128, dView, 128, b.Gv, 32, 27));
-  ANR_TRY(e.colsum(dView, 128, 128, g[24]));
   ANR_TRY(e.xgrad(dLat, 256, 256, dView, 128, 128, PT(23), 283, 0, nullptr, 0, false));
   {
     float* ys = ysum + 512;
     if (hipMemsetAsync(ys, 0, 256 * 4, s) != hipSuccess) return fail(ANR_E_HIP, "memset");
-    ANR_TRY(e.colsum(dLat, 256, 256, ys));
-    ANR_TRY(e.colsum(dLat, 256, 256, g[22]));
+    ANR_TRY(e.wgrad(g[21], 384, 0, 256, dLat, 256, Feat, 256, 256, g[22], ys));
     hipLaunchKernelGGL(k_tr_latent_grad, dim3(256 + 128), dim3(128), 0, s, (const float*)ys, PT(21), 384, 256, 256, PT(0),
                        f->latent_index, 0, g[21], g[0]);
     ANR_TRY(check_launch("k_tr_latent_grad(nf_latent)"));
   }
-  ANR_TRY(e.wgrad(g[21], 384, 0, 256, dLat, 256, Feat, 256, 256));
   ANR_TRY(e.xgrad(dFeat, 256, 256, dLat, 256, 256, PT(21), 384, 0, nullptr, 0, false));
-  ANR_TRY(e.wgrad(g[19], 256, 0, 256, dFeat, 256, Hn + 7 * S, 256, 256));
-  ANR_TRY(e.colsum(dFeat, 256, 256, g[20]));
-  ANR_TRY(e.wgrad(g[17], 256, 0, 1, b.dAlpha, 1, Hn + 7 * S, 256, 256));
-  ANR_TRY(e.colsum(b.dAlpha, 1, 1, g[18]));
+  ANR_TRY(e.wgrad(g[19], 256, 0, 256, dFeat, 256, Hn + 7 * S, 256, 256, g[20]));
+  ANR_TRY(e.wgrad(g[17], 256, 0, 1, b.dAlpha, 1, Hn + 7 * S, 256, 256, g[18]));
   ANR_TRY(e.xgrad(dA, 256, 256, dFeat, 256, 256, PT(19), 256, 0, Hn + 7 * S, 256, false, b.dAlpha, 1, 1, PT(17), 256));
   // NeRF pts_linears 7..0 (skip at 5: [gamma(x_T), net])
   float* cur = dA;
   float* nxt = dB;
   for (int l = 7; l >= 0; --l) {
     const int wi = 1 + 2 * l, bi = wi + 1;
-    ANR_TRY(e.colsum(cur, 256, 256, g[bi]));
     if (l == 0) {
-      ANR_TRY(e.wgrad(g[wi], 63, 0, 256, cur, 256, b.Gt, 64, 63));
+      ANR_TRY(e.wgrad(g[wi], 63, 0, 256, cur, 256, b.Gt, 64, 63, g[bi]));
       ANR_TRY(e.xgrad(b.dGt, 64, 63, cur, 256, 256, PT(wi), 63, 0, nullptr, 0, true));
     } else if (l == 5) {
-      ANR_TRY(e.wgrad(g[wi], 319, 0, 256, cur, 256, b.Gt, 64, 63));
+      ANR_TRY(e.wgrad(g[wi], 319, 0, 256, cur, 256, b.Gt, 64, 63, g[bi]));
       ANR_TRY(e.wgrad(g[wi], 319, 63, 256, cur, 256, Hn + 4 * S, 256, 256));
       ANR_TRY(e.xgrad(b.dGt, 64, 63, cur, 256, 256, PT(wi), 319, 0, nullptr, 0, true));
       ANR_TRY(e.xgrad(nxt, 256, 256, cur, 256, 256, PT(wi), 319, 63, Hn + 4 * S, 256, false));
     } else {
-      ANR_TRY(e.wgrad(g[wi], 256, 0, 256, cur, 256, Hn + (l - 1) * S, 256, 256));
+      ANR_TRY(e.wgrad(g[wi], 256, 0, 256, cur, 256, Hn + (l - 1) * S, 256, 256, g[bi]));
       ANR_TRY(e.xgrad(nxt, 256, 256, cur, 256, 256, PT(wi), 256, 0, Hn + (l - 1) * S, 256, false));
     }
     if (l > 0) {
