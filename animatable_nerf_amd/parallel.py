@@ -51,3 +51,71 @@ def shard_chunks(n_rays, rank, world, chunk=2048):
     c0 = min(n_chunks, rank * per)
     c1 = min(n_chunks, c0 + per)
     return min(n_rays, c0 * chunk), min(n_rays, c1 * chunk)
+
+
+# ---- one frame split over ranks (north_star "rays shard across the GPUs") ----
+# Per-ray batch keys (tpose_dataset.py:236-277, batch dim 1): sliced per rank; everything else
+# (A, volumes, bounds, R, Th, latent indices) is per frame and replicated.
+RAY_KEYS = ('ray_o', 'ray_d', 'near', 'far', 'occupancy', 'mask_at_box', 'rgb')
+
+
+def shard_batch(batch, rank, world, chunk=2048):
+    """-> (this rank's batch, (start, end)): the rays of shard_chunks(R, rank, world, chunk)."""
+    R = int(batch['ray_o'].shape[1])
+    s, e = shard_chunks(R, rank, world, chunk)
+    sub = dict(batch)
+    for k in RAY_KEYS:
+        v = batch.get(k)
+        if torch.is_tensor(v) and v.dim() >= 2 and v.shape[1] == R:
+            sub[k] = v[:, s:e]
+    return sub, (s, e)
+
+
+def gather_rays(t, n_rays, world, chunk=2048, group=None):
+    """(1, r_local, ...) per rank -> (1, n_rays, ...) on every rank, in ray order: one all_gather of
+    shards padded to the common size ceil(chunks / world) * chunk, then trimmed."""
+    if world == 1 or not is_dist():
+        return t
+    n_chunks = (n_rays + chunk - 1) // chunk
+    per = (n_chunks + world - 1) // world * chunk
+    pad = torch.zeros((t.shape[0], per) + tuple(t.shape[2:]), dtype=t.dtype, device=t.device)
+    pad[:, :t.shape[1]] = t
+    parts = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(parts, pad.contiguous(), group=group)
+    out = []
+    for r in range(world):
+        s, e = shard_chunks(n_rays, r, world, chunk)
+        out.append(parts[r][:, :e - s])
+    return torch.cat(out, dim=1)
+
+
+def render_sharded(renderer, batch, chunk=2048, group=None):
+    """Renderer.render_device over a whole frame with its rays split across the ranks by whole
+    reference chunks (so every per-chunk argmin / argmax is the single-GPU one); rgb_map, acc_map
+    and depth_map are all-gathered to every rank in ray order (the 'raw' samples stay local:
+    'raw_local', this rank's rays [start, end) in 'span')."""
+    rank = dist.get_rank(group) if is_dist() else 0
+    world = dist.get_world_size(group) if is_dist() else 1
+    R = int(batch['ray_o'].shape[1])
+    sub, (s, e) = shard_batch(batch, rank, world, chunk)
+    if e > s:
+        out = renderer.render_device(sub, bw_rows=False)
+    else:  # more ranks than chunks: an empty shard
+        dev = batch['ray_o'].device
+        out = {'rgb_map': torch.zeros((1, 0, 3), device=dev), 'acc_map': torch.zeros((1, 0), device=dev),
+               'depth_map': torch.zeros((1, 0), device=dev), 'raw': torch.zeros((1, 0, 4), device=dev)}
+    ret = {k: gather_rays(out[k], R, world, chunk, group) for k in ('rgb_map', 'acc_map', 'depth_map')}
+    ret['raw_local'] = out['raw']
+    ret['span'] = (s, e)
+    return ret
+
+
+def psnr_sharded(rgb_pred, rgb_gt, group=None):
+    """A18 PSNR (lib/evaluators/if_nerf.py:15-18: mse over the rendered in-box rays, -10 log10 mse)
+    of a frame whose rays are split over the ranks: one all-reduce of [sum of squared errors,
+    element count] (float64)."""
+    d = (rgb_pred.double() - rgb_gt.double())
+    t = torch.stack([(d * d).sum(), torch.tensor(float(d.numel()), dtype=torch.float64, device=d.device)])
+    if is_dist():
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    return float(-10.0 * torch.log10(t[0] / t[1]))

@@ -62,6 +62,9 @@ def parse():
     ap.add_argument('--voxel', type=float, default=0.005, help='mesh mode: cfg.voxel_size (aninerf_s9p.yaml:95)')
     ap.add_argument('--sdf-cpu-rays', type=int, default=2048)
     ap.add_argument('--no-exact', action='store_true', help='skip timing the other render precision')
+    ap.add_argument('--shard-frame', action='store_true',
+                    help='render: split ONE frame over the ranks by whole chunks and all-gather rgb/acc/depth '
+                         '(strong scaling, parallel.render_sharded) instead of one frame per GPU')
     ap.add_argument('--render-precision', choices=('fp32', 'bf16x3'), default='bf16x3',
                     help='fp32: exact fp32 MFMA; bf16x3: T-pose BW MLP + NeRF as hi/lo-split bf16 MFMA '
                          '(outputs within the 1e-4 fp32 tolerance, tests/test_gpu_render.py)')
@@ -89,7 +92,7 @@ def main():
         else:
             dist.init_process_group(backend)
 
-    from animatable_nerf_amd import _lib, config, network, synthetic
+    from animatable_nerf_amd import _lib, config, network, parallel, synthetic
     from animatable_nerf_amd.renderer import Renderer, near_far
     if args.mode == 'train':
         return bench_train(args, rank, world, dev)
@@ -101,7 +104,7 @@ def main():
         return bench_anim(args, rank, world, dev)
 
     sc = synthetic.Scene(vsize=0.025)
-    ro, rd = sc.box_rays(args.rays, seed=2 + rank)
+    ro, rd = sc.box_rays(args.rays, seed=2 if args.shard_frame else 2 + rank)
     nr, fr, m = near_far(torch.from_numpy(sc.bounds).to(dev), torch.from_numpy(ro).to(dev),
                          torch.from_numpy(rd).to(dev))
     m_np = m.cpu().numpy()
@@ -121,8 +124,10 @@ def main():
         cfg.perturb = 0
         cfg.render_precision = precision
         renderer = Renderer(net, cfg)
+        render = (lambda: parallel.render_sharded(renderer, batch)) if args.shard_frame else \
+            (lambda: renderer.render_device(batch))
         for _ in range(args.warmup):
-            out = renderer.render_device(batch)
+            out = render()
         torch.cuda.synchronize()
         lib.anr_profile_enable(1)
         lib.anr_profile_read(None, None)
@@ -131,7 +136,7 @@ def main():
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(args.steps):
-            out = renderer.render_device(batch)
+            out = render()
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -140,18 +145,21 @@ def main():
         launches = _lib.ctypes.c_int(0)
         _lib.check(lib.anr_profile_read(_lib.ctypes.byref(mlp_ms), _lib.ctypes.byref(launches)), 'anr_profile_read')
         lib.anr_profile_enable(0)
-        return out, max_over_ranks(dt, dev, world), mlp_ms.value / max(1, launches.value), renderer.last_counts
+        counts = renderer.counts(R_local) if args.shard_frame else renderer.last_counts
+        return out, max_over_ranks(dt, dev, world), mlp_ms.value / max(1, launches.value), counts
 
+    frames = 1 if args.shard_frame else world  # frames rendered per timed step, all ranks together
+    s0, s1 = parallel.shard_chunks(R, rank, world) if args.shard_frame else (0, R)
+    R_local = max(1, s1 - s0)  # this rank's rays (n_kept, kernel_ms are this rank's)
     others = [p for p in ('fp32', 'bf16x3') if p != args.render_precision]
     side = {}
     for prec in others if not args.no_exact else []:
         o2, dt2, kms2, _ = timed(prec)
-        side[prec] = {'value': R * 64 * args.steps * world / dt2, 'ms_per_step': dt2 / args.steps * 1e3,
+        side[prec] = {'value': R * 64 * args.steps * frames / dt2, 'ms_per_step': dt2 / args.steps * 1e3,
                       'kernel_ms': kms2}
         del o2
     out, dt_max, kernel_ms, (n_kept, m_rows) = timed(args.render_precision)
-    samples_per_rank = R * 64 * args.steps
-    value = samples_per_rank * world / dt_max
+    value = R * 64 * args.steps * frames / dt_max
     split = args.render_precision == 'bf16x3'
     if split:
         # executed bf16 MFMA work per kept sample: 3 products per MAC (lo*bh + hi*bl + hi*bh)
@@ -167,13 +175,15 @@ def main():
     result = {
         'metric': METRIC, 'value': value, 'unit': 'ray-samples/s', 'n_gpus': world, 'steps': args.steps,
         'warmup': args.warmup, 'ms_per_step': dt_max / args.steps * 1e3, 'higher_is_better': True,
-        'scaling': 'weak', 'vs_baseline': None, 'dtype': dtype, 'data': 'synthetic',
+        'scaling': 'strong' if args.shard_frame else 'weak', 'vs_baseline': None, 'dtype': dtype, 'data': 'synthetic',
         'config': {'workload': 'aninerf_s9p full 512x512 render (config 2), eval perturb=0; outputs held to the '
                                'fp32 tolerance (1e-4, tests/test_gpu_render.py) in both render precisions',
                    'render_precision': args.render_precision,
                    'rays_per_gpu': R, 'samples_per_ray': 64, 'chunk': 2048,
-                   'kept_fraction': n_kept / (R * 64), 'alpha_ind_rows': m_rows,
-                   'parallelism': f'replicas{world} (one frame per GPU)'},
+                   'kept_fraction': n_kept / (R_local * 64), 'alpha_ind_rows': m_rows,
+                   'parallelism': (f'frame-split{world} (whole 2048-ray chunks per rank, rgb/acc/depth '
+                                   'all-gathered over RCCL)') if args.shard_frame else
+                                  f'replicas{world} (one frame per GPU)'},
         'roofline': {'bound': 'mfma', 'kernel': 'k_mlp_b16' if split else 'k_mlp', 'achieved': achieved,
                      'peak': peak, 'unit': 'TFLOP/s', 'frac': achieved / peak, 'traffic': None,
                      'kernel_ms': kernel_ms, 'flop_per_kept_executed': flop_exec,

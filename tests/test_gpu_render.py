@@ -222,3 +222,25 @@ def test_mmsk_visibility_filter_matches_reference(renderer, dev):
         restate.render_mmsk(oracle_params(), to_torch(b), trace=tr)
     ref_raw = torch.cat(tr['raw'], dim=1)
     assert torch.equal(_keep(ret['raw']).cpu(), _keep(ref_raw))
+
+
+@pytest.mark.parametrize('world', [3, 8])
+def test_frame_shards_equal_whole_frame(renderer, dev, world):
+    """§8(e): one frame split over `world` ranks by whole chunks (parallel.shard_batch, as
+    render_sharded does per rank), each shard rendered on its own: concatenated in rank order the
+    rgb/acc/depth/raw equal the unsplit render bit for bit (per-chunk argmin/argmax and per-sample
+    arithmetic do not depend on the split). The all-gather itself: tests/test_distributed.py."""
+    from animatable_nerf_amd import parallel
+    sc = scene(0.025)
+    ro, rd = sc.box_rays(9 * 2048 + 777, seed=4)
+    b, _ = batch_np(sc, ro, rd)
+    bt = to_torch(b, dev)
+    full = renderer.render_device(bt, bw_rows=False)
+    parts = []
+    for r in range(world):
+        sub, (s, e) = parallel.shard_batch(bt, r, world)
+        if e > s:
+            parts.append(renderer.render_device(sub, bw_rows=False))
+    for k in ('rgb_map', 'acc_map', 'depth_map', 'raw'):
+        cat = torch.cat([p[k] for p in parts], dim=1)
+        assert torch.equal(cat, full[k]), k
