@@ -118,6 +118,46 @@ __device__ __forceinline__ void rowsum_flush(const GemmArgs& g, int m0, float (&
   }
 }
 
+// epilogue shared by the GEMM kernels: lane holds C[wr + i*16 + 4*(lane>>4) + r][wc + j*16 + (lane&15)]
+__device__ __forceinline__ void epilogue(const GemmArgs& g, const f32x4 (&acc)[2][2], int M, int m0, int n0, int wr,
+                                         int wc, int lane) {
+  const bool first_split = blockIdx.z == 0;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wr + i * 16 + 4 * (lane >> 4) + r;
+        const int n = n0 + wc + j * 16 + (lane & 15);
+        if (m >= M || n >= g.N) continue;
+        float v = acc[i][j][r];
+        float* c = g.C + (long)m * g.ldc + n;
+        if (g.atomic) {
+          if (g.bias && first_split) v += g.bias[n];
+          atomicAdd(c, v);
+          continue;
+        }
+        if (g.bias) v += g.bias[n];
+        if (g.accumulate) v += *c;
+        if (g.div_pre != 0.f) v = v / g.div_pre;
+        if (g.relu) v = fmaxf(v, 0.f);
+        if (g.softplus) {  // torch softplus(beta=100, threshold=20) and the factor its backward uses
+          const float z = v * 100.f;
+          const float e = expf(z);
+          g.deriv[(long)m * g.ldd + n] = z > 20.f ? -1.f : e;
+          v = z > 20.f ? v : log1pf(e) / 100.f;
+        }
+        if (g.spd && n < g.spd_n) {
+          const float d = g.spd[(long)m * g.ldsd + n];
+          if (d >= 0.f) v = v * d / (d + 1.f);
+        }
+        if (g.mask && !(g.mask[(long)m * g.ldm + n] > 0.f)) v = 0.f;
+        if (g.div_post != 0.f) v = v / g.div_post;
+        *c = v;
+      }
+}
+
 template <bool A_K, bool B_K>
 __global__ __launch_bounds__(256) void k_gemm_t(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) float As[GBK][GLD];
@@ -190,43 +230,8 @@ __global__ __launch_bounds__(256) void k_gemm_t(GemmArgs g) {
     k0 = nk;
     kend = (g.ksplit > 1) ? ke : g.seg[s].K;
   }
-  // epilogue: lane holds C[wr + i*16 + 4*(lane>>4) + r][wc + j*16 + (lane&15)]
   if (do_rsum) rowsum_flush(g, m0, rsum);
-  const bool first_split = blockIdx.z == 0;
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wr + i * 16 + 4 * (lane >> 4) + r;
-        const int n = n0 + wc + j * 16 + (lane & 15);
-        if (m >= M || n >= g.N) continue;
-        float v = acc[i][j][r];
-        float* c = g.C + (long)m * g.ldc + n;
-        if (g.atomic) {
-          if (g.bias && first_split) v += g.bias[n];
-          atomicAdd(c, v);
-          continue;
-        }
-        if (g.bias) v += g.bias[n];
-        if (g.accumulate) v += *c;
-        if (g.div_pre != 0.f) v = v / g.div_pre;
-        if (g.relu) v = fmaxf(v, 0.f);
-        if (g.softplus) {  // torch softplus(beta=100, threshold=20) and the factor its backward uses
-          const float z = v * 100.f;
-          const float e = expf(z);
-          g.deriv[(long)m * g.ldd + n] = z > 20.f ? -1.f : e;
-          v = z > 20.f ? v : log1pf(e) / 100.f;
-        }
-        if (g.spd && n < g.spd_n) {
-          const float d = g.spd[(long)m * g.ldsd + n];
-          if (d >= 0.f) v = v * d / (d + 1.f);
-        }
-        if (g.mask && !(g.mask[(long)m * g.ldm + n] > 0.f)) v = 0.f;
-        if (g.div_post != 0.f) v = v / g.div_post;
-        *c = v;
-      }
+  epilogue(g, acc, M, m0, n0, wr, wc, lane);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -305,20 +310,24 @@ __device__ __forceinline__ void load_tile16(const float* __restrict__ P, long rs
 #define RLD (64 + 4)
 typedef short v4s __attribute__((ext_vector_type(4)));
 
-template <bool KCONTIG>
-__device__ __forceinline__ void store_tile16(unsigned short* S, int tid, const Tile16& t) {
+__device__ __forceinline__ float bf2f(unsigned short h) { return __uint_as_float((uint32_t)h << 16); }
+
+// X3: also the low part lo = bf16(x - hi) into SL (x = hi + lo to ~2^-16 relative)
+template <bool KCONTIG, bool X3>
+__device__ __forceinline__ void store_tile16(unsigned short* S, unsigned short* SL, int tid, const Tile16& t) {
 #pragma unroll
   for (int h = 0; h < 4; ++h) {
     const int q = tid + h * 256;
-    const uint32_t lo = (uint32_t)f2bf(t.v[h][0]) | ((uint32_t)f2bf(t.v[h][1]) << 16);
-    const uint32_t hi = (uint32_t)f2bf(t.v[h][2]) | ((uint32_t)f2bf(t.v[h][3]) << 16);
-    if (KCONTIG) {
-      const int r = q >> 4, k = (q & 15) * 4;
-      *(uint2*)&S[r * BLD + k] = make_uint2(lo, hi);
-    } else {
-      const int k = q >> 4, r = (q & 15) * 4;
-      *(uint2*)&S[k * RLD + r] = make_uint2(lo, hi);
+    unsigned short e[4], l[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      e[c] = f2bf(t.v[h][c]);
+      if (X3) l[c] = f2bf(t.v[h][c] - bf2f(e[c]));
     }
+    const int off = KCONTIG ? (q >> 4) * BLD + (q & 15) * 4 : (q >> 4) * RLD + (q & 15) * 4;
+    *(uint2*)&S[off] = make_uint2((uint32_t)e[0] | ((uint32_t)e[1] << 16), (uint32_t)e[2] | ((uint32_t)e[3] << 16));
+    if (X3)
+      *(uint2*)&SL[off] = make_uint2((uint32_t)l[0] | ((uint32_t)l[1] << 16), (uint32_t)l[2] | ((uint32_t)l[3] << 16));
   }
 }
 
@@ -339,10 +348,14 @@ __device__ __forceinline__ bf16x8 frag16(const unsigned short* S, int rb, int ks
   return f;
 }
 
-template <bool A_K, bool B_K>
+// X3 (render precision bf16x3, the sdf_pdf GEMMs): hi/lo images of both operands and three MFMAs per
+// fragment pair, lo*bh + hi*bl + hi*bh, fp32 accumulation (~2^-16 relative per product).
+template <bool A_K, bool B_K, bool X3>
 __global__ __launch_bounds__(256) void k_gemm_b(GemmArgs g) {
-  __shared__ __attribute__((aligned(16))) unsigned short As[GBM * BLD];
-  __shared__ __attribute__((aligned(16))) unsigned short Bs[GBN * BLD];
+  __shared__ __attribute__((aligned(16))) unsigned short As[(X3 ? 2 : 1) * GBM * BLD];
+  __shared__ __attribute__((aligned(16))) unsigned short Bs[(X3 ? 2 : 1) * GBN * BLD];
+  unsigned short* const Al = As + GBM * BLD;
+  unsigned short* const Bl = Bs + GBN * BLD;
   const int M = g.M_dev ? *g.M_dev : g.M;
   const int m0 = blockIdx.y * GBM, n0 = blockIdx.x * GBN;
   if (m0 >= M) return;
@@ -372,8 +385,8 @@ __global__ __launch_bounds__(256) void k_gemm_b(GemmArgs g) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) rsum[e] += (ta.v[0][e] + ta.v[1][e]) + (ta.v[2][e] + ta.v[3][e]);
     }
-    store_tile16<A_K>(As, tid, ta);
-    store_tile16<B_K>(Bs, tid, tb);
+    store_tile16<A_K, X3>(As, Al, tid, ta);
+    store_tile16<B_K, X3>(Bs, Bl, tid, tb);
     __syncthreads();
     int ns = s, nk = k0 + BBK;
     if (nk >= kend) {
@@ -393,6 +406,20 @@ __global__ __launch_bounds__(256) void k_gemm_b(GemmArgs g) {
       for (int i = 0; i < 2; ++i) a[i] = frag16<A_K>(As, wr + i * 16, ks, lane);
 #pragma unroll
       for (int j = 0; j < 2; ++j) b[j] = frag16<B_K>(Bs, wc + j * 16, ks, lane);
+      if constexpr (X3) {
+        bf16x8 al[2], bl[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) al[i] = frag16<A_K>(Al, wr + i * 16, ks, lane);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) bl[j] = frag16<B_K>(Bl, wc + j * 16, ks, lane);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], b[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], bl[j], acc[i][j], 0, 0, 0);
+          }
+      }
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -405,35 +432,15 @@ __global__ __launch_bounds__(256) void k_gemm_b(GemmArgs g) {
     kend = (g.ksplit > 1) ? ke : g.seg[s].K;
   }
   if (do_rsum) rowsum_flush(g, m0, rsum);
-  const bool first_split = blockIdx.z == 0;
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wr + i * 16 + 4 * (lane >> 4) + r;
-        const int n = n0 + wc + j * 16 + (lane & 15);
-        if (m >= M || n >= g.N) continue;
-        float v = acc[i][j][r];
-        float* c = g.C + (long)m * g.ldc + n;
-        if (g.atomic) {
-          if (g.bias && first_split) v += g.bias[n];
-          atomicAdd(c, v);
-          continue;
-        }
-        if (g.bias) v += g.bias[n];
-        if (g.accumulate) v += *c;
-        if (g.relu) v = fmaxf(v, 0.f);
-        if (g.mask && !(g.mask[(long)m * g.ldm + n] > 0.f)) v = 0.f;
-        *c = v;
-      }
+  epilogue(g, acc, M, m0, n0, wr, wc, lane);
 }
 
-template __global__ void k_gemm_b<true, true>(GemmArgs);
-template __global__ void k_gemm_b<true, false>(GemmArgs);
-template __global__ void k_gemm_b<false, true>(GemmArgs);
-template __global__ void k_gemm_b<false, false>(GemmArgs);
+template __global__ void k_gemm_b<true, true, false>(GemmArgs);
+template __global__ void k_gemm_b<true, false, false>(GemmArgs);
+template __global__ void k_gemm_b<false, true, false>(GemmArgs);
+template __global__ void k_gemm_b<false, false, false>(GemmArgs);
+template __global__ void k_gemm_b<true, true, true>(GemmArgs);
+template __global__ void k_gemm_b<true, false, true>(GemmArgs);
 
 template __global__ void k_gemm_t<true, true>(GemmArgs);
 template __global__ void k_gemm_t<true, false>(GemmArgs);
@@ -454,11 +461,16 @@ void launch_gemm(GemmArgs g, dim3 grid, hipStream_t s) {
     g.a_vec[i] = ((uintptr_t)q.A % 16 == 0) && (a_stride % 4 == 0) && (a_k || q.a_rs == 1);
     g.b_vec[i] = ((uintptr_t)q.B % 16 == 0) && (b_stride % 4 == 0) && (b_k || q.b_cs == 1);
   }
-  if (g.bf16) {  // the sdf epilogues (softplus, div) are fp32-path only
-    if (a_k && b_k) hipLaunchKernelGGL((k_gemm_b<true, true>), grid, dim3(256), 0, s, g);
-    else if (a_k) hipLaunchKernelGGL((k_gemm_b<true, false>), grid, dim3(256), 0, s, g);
-    else if (b_k) hipLaunchKernelGGL((k_gemm_b<false, true>), grid, dim3(256), 0, s, g);
-    else hipLaunchKernelGGL((k_gemm_b<false, false>), grid, dim3(256), 0, s, g);
+  if (g.x3 && a_k) {  // split-bf16 (the sdf_pdf forward and input-gradient GEMMs)
+    if (b_k) hipLaunchKernelGGL((k_gemm_b<true, true, true>), grid, dim3(256), 0, s, g);
+    else hipLaunchKernelGGL((k_gemm_b<true, false, true>), grid, dim3(256), 0, s, g);
+    return;
+  }
+  if (g.bf16) {
+    if (a_k && b_k) hipLaunchKernelGGL((k_gemm_b<true, true, false>), grid, dim3(256), 0, s, g);
+    else if (a_k) hipLaunchKernelGGL((k_gemm_b<true, false, false>), grid, dim3(256), 0, s, g);
+    else if (b_k) hipLaunchKernelGGL((k_gemm_b<false, true, false>), grid, dim3(256), 0, s, g);
+    else hipLaunchKernelGGL((k_gemm_b<false, false, false>), grid, dim3(256), 0, s, g);
     return;
   }
   if (a_k && b_k) hipLaunchKernelGGL((k_gemm_t<true, true>), grid, dim3(256), 0, s, g);

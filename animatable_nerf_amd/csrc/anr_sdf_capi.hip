@@ -79,9 +79,11 @@ int sdf_cus() {
 struct G {
   hipStream_t s;
   int M;
+  int x3;  // render precision ANR_BF16X3: split-bf16 MFMA GEMMs (k_gemm_b<.., .., true>)
   int run(GemmArgs g) {
     if (M <= 0 || g.N <= 0) return ANR_OK;
     g.M = M;
+    g.x3 = x3;
     g.ksplit = 1;
     launch_gemm(g, dim3((g.N + 63) / 64, (M + 63) / 64, 1), s);
     return check_launch("k_gemm (sdf)");
@@ -237,7 +239,7 @@ int anr_sdf_render_fwd(const anr_sdf_params* p, const anr_sdf_frame* f, const fl
     a.D7 = Dl(7); a.G7 = Ga; a.Gc = Gc; a.gB = F(L.gB); a.Y8 = F(L.Y8); a.Yc = F(L.Yc); a.beta = beta;
     a.resd_rows = F(L.resd_rows); a.grad_rows = F(L.grad_rows); a.raw = raw; a.sdf = out->sdf;
     const dim3 pg((cnt + 255) / 256), pb(256);
-    G g{s, cnt};
+    G g{s, cnt, o->precision == ANR_BF16X3 ? 1 : 0};
 
     // B2 + B3: LBS to the big pose, residual deformation MLP (poses folded into layers 0 / 5)
     hipLaunchKernelGGL(k_sdf_prep, pg, pb, 0, s, a);

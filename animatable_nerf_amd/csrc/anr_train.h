@@ -38,6 +38,7 @@ struct GemmArgs {
   int spd_n;
   float div_post;      // v = v / div_post after the activation (cat(...)/sqrt(2) forward)
   int bf16;            // operands rounded to bf16, bf16 MFMA, fp32 accumulate (training precision)
+  int x3;              // operands split hi + lo (bf16 each), three bf16 MFMAs per product (fp32-level)
   // weight-gradient GEMMs (A(m,k) = dY[k][m]): the fp32 row sums of A over this launch's k range
   // (= the bias gradient, the column sums of dY) are atomically added into rowsum[m] (and rowsum2[m])
   // by the workgroups of the first N tile; NULL: off

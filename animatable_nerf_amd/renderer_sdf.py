@@ -74,6 +74,12 @@ class Renderer:
         o.n_samples, o.chunk, o.norm_th, o.train_th = ns, int(self.cfg.get('chunk', CHUNK)), NORM_TH, 0.0
         o.t_rand = tr.data_ptr() if tr is not None else None
         o.novel_pose = 0
+        # cfg.render_precision 'fp32' (exact fp32 MFMA GEMMs) or 'bf16x3' (split-bf16 MFMA GEMMs for the
+        # forward and input-gradient layers, fp32-level; include/aninerf.h anr_render_opts.precision)
+        rprec = self.cfg.get('render_precision', 'fp32')
+        if rprec not in ('fp32', 'bf16x3'):
+            raise ValueError(f"render_precision must be 'fp32' or 'bf16x3', got {rprec!r}")
+        o.precision = _lib.BF16X3 if rprec == 'bf16x3' else _lib.FP32
         rgb = torch.empty((1, R, 3), device=dev)
         acc = torch.empty((1, R), device=dev)
         depth = torch.empty((1, R), device=dev)

@@ -61,6 +61,9 @@ def parse():
                          'training step (2 x 65,536 points, novel_pose_bw)')
     ap.add_argument('--voxel', type=float, default=0.005, help='mesh mode: cfg.voxel_size (aninerf_s9p.yaml:95)')
     ap.add_argument('--sdf-cpu-rays', type=int, default=2048)
+    ap.add_argument('--sdf-precision', choices=('fp32', 'bf16x3'), default='fp32',
+                    help='sdf mode GEMMs: exact fp32 MFMA, or split-bf16 (measured no faster: the sdf GEMMs '
+                         'are load-latency bound, not MFMA bound)')
     ap.add_argument('--no-exact', action='store_true', help='skip timing the other render precision')
     ap.add_argument('--shard-frame', action='store_true',
                     help='render: split ONE frame over the ranks by whole chunks and all-gather rgb/acc/depth '
@@ -306,6 +309,7 @@ def bench_sdf(args, rank, world, dev):
     cfg = config.defaults()
     cfg.num_train_frame = 260
     cfg.perturb = 0
+    cfg.render_precision = args.sdf_precision
     net = network_sdf.Network(cfg)
     sd = synthetic.init_state_dict_sdf({k: tuple(v.shape) for k, v in net.state_dict().items()})
     network.load_numpy_state(net, sd)
@@ -329,17 +333,24 @@ def bench_sdf(args, rank, world, dev):
     dt = time.perf_counter() - t0
     dt_max = max_over_ranks(dt, dev, world)
     n_kept = renderer.last_counts[0]
-    achieved = n_kept * FLOP_PER_KEPT_SDF * args.steps / dt_max / 1e12
+    split = args.sdf_precision == 'bf16x3'
+    # bf16x3: every layer GEMM of the path is split (3 bf16 MFMA products per MAC) -> bf16 peak
+    flop_exec = FLOP_PER_KEPT_SDF * (3 if split else 1)
+    peak = PEAK_BF16_MFMA_TFLOPS if split else PEAK_FP32_MFMA_TFLOPS
+    achieved = n_kept * flop_exec * args.steps / dt_max / 1e12
     result = {
         'metric': 'ray-samples/sec (512x512 rays x 64 samples), sdf_pdf render', 'value': R * 64 * args.steps * world / dt_max,
         'unit': 'ray-samples/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
         'ms_per_step': dt_max / args.steps * 1e3, 'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
-        'dtype': 'fp32', 'data': 'synthetic',
-        'config': {'workload': 'sdf_pdf (config 5 network) full 512x512 box-ray render, eval, fp32',
+        'dtype': ('bf16 MFMA operands (hi/lo split, 3 products per MAC), fp32 accumulate' if split else 'fp32'),
+        'data': 'synthetic',
+        'config': {'workload': 'sdf_pdf (config 5 network) full 512x512 box-ray render, eval; outputs held to the '
+                               'fp32 tolerances of tests/test_gpu_sdf.py in both render precisions',
+                   'render_precision': args.sdf_precision,
                    'rays_per_gpu': R, 'kept_fraction': n_kept / (R * 64), 'parallelism': f'replicas{world}'},
         'roofline': {'bound': 'mfma', 'kernel': 'whole render (layer GEMMs dominate)', 'achieved': achieved,
-                     'peak': PEAK_FP32_MFMA_TFLOPS, 'unit': 'TFLOP/s', 'frac': achieved / PEAK_FP32_MFMA_TFLOPS,
-                     'traffic': None, 'flop_per_kept': FLOP_PER_KEPT_SDF},
+                     'peak': peak, 'unit': 'TFLOP/s', 'frac': achieved / peak,
+                     'traffic': None, 'flop_per_kept': FLOP_PER_KEPT_SDF, 'flop_per_kept_executed': flop_exec},
     }
     if rank == 0 and world == 1 and not args.no_cpu:
         import sys

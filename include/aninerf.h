@@ -104,11 +104,11 @@ typedef struct anr_render_opts {
   int precision;     /* training GEMM operands: ANR_FP32 (exact fp32 MFMA); ANR_BF16 (config 3:
                         operands rounded to bf16, fp32 accumulation, fp32 master weights and Adam,
                         the pose-space blend-weight MLP kept fp32); ANR_BF16_ALL (every GEMM bf16).
-                        anr_render_fwd: ANR_FP32 (exact fp32 MFMA everywhere) or ANR_BF16X3 (the
-                        T-pose BW MLP and the NeRF as hi/lo-split bf16 MFMA, lo*bh + hi*bl + hi*bh
+                        anr_render_fwd / anr_alpha_points: ANR_FP32 (exact fp32 MFMA everywhere) or
+                        ANR_BF16X3 (every MLP layer as hi/lo-split bf16 MFMA, lo*bh + hi*bl + hi*bh
                         with fp32 accumulation: ~2^-16 relative per product, outputs within the
-                        1e-4 fp32 tolerance; the pose-space BW MLP stays exact fp32).
-                        Other entry points treat ANR_BF16X3 as ANR_FP32. */
+                        1e-4 fp32 tolerance). anr_sdf_render_fwd: ANR_BF16X3 splits its layer GEMMs
+                        the same way. Other entry points treat ANR_BF16X3 as ANR_FP32. */
 } anr_render_opts;
 
 enum { ANR_FP32 = 0, ANR_BF16 = 1, ANR_BF16_ALL = 2, ANR_BF16X3 = 3 };

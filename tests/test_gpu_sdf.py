@@ -26,12 +26,16 @@ def dev():
     return torch.device('cuda:0')
 
 
-@pytest.fixture(scope='module')
-def renderer(dev):
+@pytest.fixture(scope='module', params=['fp32', 'bf16x3'])
+def renderer(dev, request):
+    """Both render precisions at the same tolerances: exact fp32 MFMA GEMMs, and split-bf16
+    (hi/lo, three bf16 MFMAs per product) for the forward and input-gradient GEMMs."""
     from animatable_nerf_amd.renderer_sdf import Renderer
     net = make_net_sdf(dev)
     net.train()
-    return Renderer(net, sdf_cfg())
+    cfg = sdf_cfg()
+    cfg.render_precision = request.param
+    return Renderer(net, cfg)
 
 
 def _close(a, b, tol, what):
