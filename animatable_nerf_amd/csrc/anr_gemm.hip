@@ -241,8 +241,13 @@ __global__ __launch_bounds__(256) void k_gemm_t(GemmArgs g) {
 // (8 consecutive k) is one 16-B read.
 // ------------------------------------------------------------------------------------------
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-#define BBK 64
-#define BLD (64 + 8)
+#ifndef ANR_GEMM_BK
+#define ANR_GEMM_BK 64
+#endif
+#define BBK ANR_GEMM_BK
+#define BLD (BBK + 8)
+#define BNH (BBK / 16)                    // 4-element groups per thread per 64-row operand tile
+#define BKSH (BBK == 128 ? 5 : 4)         // log2(groups per k-contiguous row)
 
 __device__ __forceinline__ unsigned short f2bf(float f) {
   uint32_t u = __float_as_uint(f);
@@ -251,7 +256,7 @@ __device__ __forceinline__ unsigned short f2bf(float f) {
 }
 
 struct Tile16 {
-  float v[4][4];
+  float v[BNH][4];
 };
 
 template <bool KCONTIG>
@@ -259,12 +264,12 @@ __device__ __forceinline__ void load_tile16(const float* __restrict__ P, long rs
                                             int tid, Tile16& t, bool vec) {
   // 64 (r) x 64 (k) elements = 1024 groups of 4, 4 per thread
 #pragma unroll
-  for (int h = 0; h < 4; ++h) {
+  for (int h = 0; h < BNH; ++h) {
     const int q = tid + h * 256;
     int r, k;
     if (KCONTIG) {
-      r = q >> 4;
-      k = (q & 15) * 4;
+      r = q >> BKSH;
+      k = (q & ((1 << BKSH) - 1)) * 4;
     } else {
       k = q >> 4;
       r = (q & 15) * 4;
@@ -316,7 +321,7 @@ __device__ __forceinline__ float bf2f(unsigned short h) { return __uint_as_float
 template <bool KCONTIG, bool X3>
 __device__ __forceinline__ void store_tile16(unsigned short* S, unsigned short* SL, int tid, const Tile16& t) {
 #pragma unroll
-  for (int h = 0; h < 4; ++h) {
+  for (int h = 0; h < BNH; ++h) {
     const int q = tid + h * 256;
     unsigned short e[4], l[4];
 #pragma unroll
@@ -324,7 +329,7 @@ __device__ __forceinline__ void store_tile16(unsigned short* S, unsigned short* 
       e[c] = f2bf(t.v[h][c]);
       if (X3) l[c] = f2bf(t.v[h][c] - bf2f(e[c]));
     }
-    const int off = KCONTIG ? (q >> 4) * BLD + (q & 15) * 4 : (q >> 4) * RLD + (q & 15) * 4;
+    const int off = KCONTIG ? (q >> BKSH) * BLD + (q & ((1 << BKSH) - 1)) * 4 : (q >> 4) * RLD + (q & 15) * 4;
     *(uint2*)&S[off] = make_uint2((uint32_t)e[0] | ((uint32_t)e[1] << 16), (uint32_t)e[2] | ((uint32_t)e[3] << 16));
     if (X3)
       *(uint2*)&SL[off] = make_uint2((uint32_t)l[0] | ((uint32_t)l[1] << 16), (uint32_t)l[2] | ((uint32_t)l[3] << 16));
@@ -383,7 +388,9 @@ __global__ __launch_bounds__(256) void k_gemm_b(GemmArgs g) {
   while (true) {
     if (do_rsum) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) rsum[e] += (ta.v[0][e] + ta.v[1][e]) + (ta.v[2][e] + ta.v[3][e]);
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int h = 0; h < BNH; ++h) rsum[e] += ta.v[h][e];
     }
     store_tile16<A_K, X3>(As, Al, tid, ta);
     store_tile16<B_K, X3>(Bs, Bl, tid, tb);
