@@ -172,3 +172,55 @@ def sample_ray_h36m(img, msk, K, R, T, bounds, nrays, split, mask_bkgd=True, bod
         nsampled = int(n_out.item())
     mask_at_box = torch.ones(nrays, dtype=torch.bool, device=dev)
     return rgb, ray_o, ray_d, near, far, coord, mask_at_box
+
+
+class ResidentFrames:
+    """Per-frame batch tensors kept resident in HBM across steps ("the
+    per-image H2D of pbw/tbw volumes"). The reference's ``Trainer.to_cuda`` (trainer.py:39-48) moves
+    the frame's blend-weight volumes (~29 MB, tpose_dataset.py:157-217) and transforms host to device
+    with every batch; a whole sequence fits in one MI355X's 288 GB (300 frames x 29 MB = 8.7 GB),
+    so here each frame's tensors cross PCIe once and later batches of that frame reuse them.
+
+    ``to_device(batch)`` -> a batch on ``device``: the ``keys`` (per-frame, never written by the
+    renderers) come from the cache keyed by (frame_index, key); everything else is copied as usual.
+    ``tbounds`` is not cached: the sdf_pdf renderer widens it in place per chunk, as the reference does."""
+
+    KEYS = ('pbw', 'tbw', 'A', 'big_A', 'pbounds', 'wbounds', 'R', 'Th')
+
+    def __init__(self, device='cuda', keys=KEYS):
+        self.device = torch.device(device)
+        self.keys = tuple(keys)
+        self._cache = {}
+        self.uploads = 0
+
+    def _frame(self, batch):
+        fi = batch.get('frame_index')
+        if fi is None:
+            raise KeyError("ResidentFrames needs the batch's 'frame_index' (tpose_dataset.py:277)")
+        return int(torch.as_tensor(fi).reshape(-1)[0])
+
+    def to_device(self, batch):
+        fi = self._frame(batch)
+        out = {}
+        for k, v in batch.items():
+            if k in self.keys:
+                t = self._cache.get((fi, k))
+                if t is None:
+                    t = torch.as_tensor(np.ascontiguousarray(v) if isinstance(v, np.ndarray) else v)
+                    t = t.to(self.device).contiguous()
+                    self._cache[(fi, k)] = t
+                    self.uploads += 1
+                out[k] = t
+            elif isinstance(v, np.ndarray):
+                out[k] = torch.from_numpy(np.ascontiguousarray(v)).to(self.device)
+            elif torch.is_tensor(v):
+                out[k] = v.to(self.device)
+            else:
+                out[k] = v
+        return out
+
+    def resident_bytes(self):
+        return sum(t.numel() * t.element_size() for t in self._cache.values())
+
+    def clear(self):
+        self._cache.clear()

@@ -99,3 +99,27 @@ def test_train_ray_sampler_edge_cases():
     assert np.array_equal(c, np.argwhere(m))
     ref = np.where((bm == 1)[..., None], img, 0)[c[:, 0], c[:, 1]]
     assert np.array_equal(rgb.cpu().numpy(), ref)
+
+
+def test_resident_frames_feed_render():
+    """ResidentFrames batches render on the device; a second batch of the same frame moves no
+    per-frame tensor host to device and renders the same rays identically."""
+    from animatable_nerf_amd import config
+    from animatable_nerf_amd.data import ResidentFrames
+    from animatable_nerf_amd.renderer import Renderer
+    from ._common import batch_np, make_net, scene
+    sc = scene(0.05)
+    ro, rd = sc.box_rays(4096, seed=6)
+    b, _ = batch_np(sc, ro, rd)
+    rf = ResidentFrames('cuda:0')
+    cfg = config.defaults()
+    cfg.perturb = 0
+    net = make_net(torch.device('cuda:0'))
+    net.train()
+    r = Renderer(net, cfg)
+    o1 = r.render_device(rf.to_device(b), bw_rows=False)
+    n = rf.uploads
+    o2 = r.render_device(rf.to_device(b), bw_rows=False)
+    assert rf.uploads == n > 0
+    for k in ('rgb_map', 'acc_map', 'depth_map'):
+        assert torch.equal(o1[k], o2[k]), k
