@@ -11,7 +11,7 @@ import torch
 from animatable_nerf_amd import synthetic
 from oracle import restate_sdf
 
-from ._common import golden, oracle_params_sdf, pdf_batch_np, pdf_g7_rays, pdf_scene, to_torch
+from ._common import assert_golden_equal, golden, oracle_params_sdf, pdf_batch_np, pdf_g7_rays, pdf_scene, to_torch
 
 torch.set_num_threads(1)
 
@@ -19,7 +19,7 @@ torch.set_num_threads(1)
 def test_pdf_scene_matches_generator():
     g = golden('g6_sdf_tiny')
     sc = pdf_scene()
-    np.testing.assert_array_equal(g['tbounds_before'][0], sc.tbounds)
+    assert_golden_equal(g['tbounds_before'][0], sc.tbounds)
     ro, rd = sc.box_rays(64, seed=2)
     b, mask = pdf_batch_np(sc, ro, rd)
     assert np.array_equal(mask, g['mask'])
@@ -51,16 +51,16 @@ def test_g6_sdf_render_and_intermediates():
     trace = {}
     with torch.no_grad():
         ret = restate_sdf.render(oracle_params_sdf(), bt, trace=trace)
-    np.testing.assert_array_equal(trace['pnorm'].numpy(), g['pnorm'][..., 0])
+    assert_golden_equal(trace['pnorm'].numpy(), g['pnorm'][..., 0])
     for k, gk, tol in (('pbw', 'kept_bw', 0), ('init_bigpose', 'init_bigpose', 0), ('resd', 'resd', 0),
                        ('tpose', 'tpose', 0), ('tpose_dirs', 'tpose_dirs', 0), ('sdf_c', 'th_sdf', 0)):
         v = trace[k].numpy()
         if k == 'pbw':
             v = v.transpose(0, 2, 1)
-        np.testing.assert_allclose(v, g[gk], rtol=0, atol=tol, err_msg=k)
+        assert_golden_equal(v, g[gk], err_msg=k)
     for k in ('raw', 'sdf', 'resd', 'gradients', 'rgb_map', 'acc_map', 'depth_map', 'msk_sdf', 'msk_label'):
-        np.testing.assert_array_equal(ret[k].numpy(), g['out_' + k], err_msg=k)
-    np.testing.assert_array_equal(bt['tbounds'].numpy(), g['tbounds_after'])
+        assert_golden_equal(ret[k].numpy(), g['out_' + k], err_msg=k)
+    assert_golden_equal(bt['tbounds'].numpy(), g['tbounds_after'])
 
 
 @pytest.mark.slow
@@ -85,6 +85,6 @@ def test_g7_sdf_chunks():
         rows = g['row_idx']
         np.testing.assert_allclose(ret['resd'][0, rows].numpy(), g['resd_rows'], rtol=0, atol=1e-6)
         np.testing.assert_allclose(ret['gradients'][0, rows].numpy(), g['grad_rows'], rtol=0, atol=1e-4)
-        np.testing.assert_array_equal(bt['tbounds'].numpy(), g['tbounds_after'])
+        assert_golden_equal(bt['tbounds'].numpy(), g['tbounds_after'])
     finally:
         torch.set_num_threads(1)
