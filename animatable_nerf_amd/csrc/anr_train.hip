@@ -411,7 +411,10 @@ __global__ __launch_bounds__(256) void k_adam(float* p, float* g, float* m, floa
 #pragma clang fp contract(fast)
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  float gi = fminf(fmaxf(g[i], -clip), clip);
+  // clip_grad_value_ is torch.clamp: a NaN gradient stays NaN (fminf/fmaxf would turn it into
+  // -clip and hide a diverged loss behind a full-size Adam step)
+  const float g0 = g[i];
+  float gi = g0 != g0 ? g0 : fminf(fmaxf(g0, -clip), clip);
   g[i] = gi;
   if (wd != 0.f) gi += wd * p[i];
   const float mi = m[i] + (1.0f - b1) * (gi - m[i]);

@@ -182,10 +182,15 @@ class ResidentFrames:
     so here each frame's tensors cross PCIe once and later batches of that frame reuse them.
 
     ``to_device(batch)`` -> a batch on ``device``: the ``keys`` (per-frame, never written by the
-    renderers) come from the cache keyed by (frame_index, key); everything else is copied as usual.
+    renderers) come from the cache keyed by (frame_index, key) — or by the subject for ``SUBJECT_KEYS`` —
+    and everything else is copied as usual. A batch must hold a single frame (all frame_index equal).
     ``tbounds`` is not cached: the sdf_pdf renderer widens it in place per chunk, as the reference does."""
 
     KEYS = ('pbw', 'tbw', 'A', 'big_A', 'pbounds', 'wbounds', 'R', 'Th')
+    # the same tensor for every frame of a subject: tbw is the T-pose template's volume
+    # (lbs_root/tbw.npy, tpose_dataset.py:213-216), big_A the fixed big pose (tpose_pdf_dataset.py:81,
+    # 91-100); cached once, not once per frame (~11 MB per frame saved for tbw)
+    SUBJECT_KEYS = ('tbw', 'big_A')
 
     def __init__(self, device='cuda', keys=KEYS):
         self.device = torch.device(device)
@@ -197,18 +202,26 @@ class ResidentFrames:
         fi = batch.get('frame_index')
         if fi is None:
             raise KeyError("ResidentFrames needs the batch's 'frame_index' (tpose_dataset.py:277)")
-        return int(torch.as_tensor(fi).reshape(-1)[0])
+        fis = torch.as_tensor(fi).reshape(-1)
+        if fis.numel() == 0:
+            raise ValueError('ResidentFrames: empty frame_index')
+        # the cached tensors are one frame's: a batch that mixes frames (train.batch_size > 1 over
+        # several images) would silently get the first frame's volumes and transforms
+        if not bool((fis == fis[0]).all()):
+            raise ValueError(f'ResidentFrames: a batch must hold one frame, got frame_index {fis.tolist()}')
+        return int(fis[0])
 
     def to_device(self, batch):
         fi = self._frame(batch)
         out = {}
         for k, v in batch.items():
             if k in self.keys:
-                t = self._cache.get((fi, k))
+                key = ('subject', k) if k in self.SUBJECT_KEYS else (fi, k)
+                t = self._cache.get(key)
                 if t is None:
                     t = torch.as_tensor(np.ascontiguousarray(v) if isinstance(v, np.ndarray) else v)
                     t = t.to(self.device).contiguous()
-                    self._cache[(fi, k)] = t
+                    self._cache[key] = t
                     self.uploads += 1
                 out[k] = t
             elif isinstance(v, np.ndarray):

@@ -36,6 +36,14 @@ def allreduce_mean_(t, group=None):
     return t
 
 
+def broadcast_(t, src=0, group=None):
+    """In-place copy of rank ``src``'s tensor to every rank (what DistributedDataParallel does to
+    the parameters and buffers when it is constructed, trainer.py:13-18)."""
+    if is_dist():
+        dist.broadcast(t, src=src, group=group)
+    return t
+
+
 def max_over_ranks(x, device):
     t = torch.tensor([float(x)], device=device, dtype=torch.float64)
     if is_dist():

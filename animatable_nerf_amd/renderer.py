@@ -220,7 +220,10 @@ class _TrainRender(torch.autograd.Function):
         R = batch['ray_o'].shape[1]
         c = _Call(renderer, batch, t_rand)
         ws_bytes = lib.anr_train_workspace_bytes(R, ctypes.byref(c.opts), ctypes.byref(c.frame))
-        ws = renderer._workspace('_tws', ws_bytes, dev)
+        # each forward owns its activations until its backward: a second render_train before the
+        # first backward (gradient accumulation, two forwards and one loss) must not overwrite them
+        # (torch's caching allocator makes the per-call allocation cheap)
+        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
         _lib.check(lib.anr_train_fwd(ctypes.byref(p), ctypes.byref(c.frame), *c.ray_ptrs(), R, ctypes.byref(c.opts),
                                      ctypes.byref(c.out), _lib.ptr(ws), ws_bytes, _lib.stream_ptr(dev)),
                    'anr_train_fwd')

@@ -19,7 +19,7 @@ import torch.nn.functional as F
 
 from . import _lib
 from . import config as _config
-from .parallel import allreduce_mean_
+from .parallel import allreduce_mean_, broadcast_
 from .renderer import Renderer, _Call
 
 
@@ -99,6 +99,9 @@ class FusedStep:
         self.n = n
         self.t = 0
         self.loss3 = torch.zeros(4, device=dev)
+        # DDP semantics (trainer.py:13-18): every replica starts from rank 0's weights, so the
+        # averaged gradient describes one model and the replicas stay identical
+        broadcast_(self.flat, 0, group)
 
     def adam_state_dict(self):
         """torch.optim.Adam-format state (one group per tensor, optimizer.py:12-27)."""
@@ -108,6 +111,13 @@ class FusedStep:
     def load_adam_state_dict(self, sd):
         from .checkpoint import load_adam_state_dict
         self.t, self.lr = load_adam_state_dict(sd, self.net.core_tensors(), self.m, self.v)
+        # a checkpoint read on one rank only must not leave the other replicas' moments (or their
+        # step count, which sets Adam's bias corrections) behind
+        broadcast_(self.m, 0, self.group)
+        broadcast_(self.v, 0, self.group)
+        tl = broadcast_(torch.tensor([float(self.t), float(self.lr)], dtype=torch.float64, device=self.m.device),
+                        0, self.group)
+        self.t, self.lr = int(tl[0]), float(tl[1])
 
     def step(self, batch, t_rand=None, lr=None):
         r = self.renderer

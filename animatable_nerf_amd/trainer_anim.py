@@ -17,7 +17,7 @@ import torch
 
 from . import _lib
 from . import config as _config
-from .parallel import allreduce_mean_
+from .parallel import allreduce_mean_, broadcast_
 from .renderer import Renderer, _f32
 
 N_POINTS = 1024 * 64  # get_sampling_points (aninerf_animation_trainer.py:153)
@@ -156,6 +156,7 @@ class AnimationStep:
             off += k
         self.n, self.t = n, 0
         self.loss3 = torch.zeros(3, device=dev)
+        broadcast_(self.flat, 0, group)  # DDP semantics: start every replica from rank 0's weights
 
     def step(self, batch, wvals=None, tvals=None, lr=None):
         wvals = sample_unit() if wvals is None else wvals

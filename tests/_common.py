@@ -14,23 +14,54 @@ def golden(name):
     return np.load(os.path.join(GOLDEN, name + '.npz'))
 
 
-def assert_golden_equal(got, ref, err_msg='', rel=3e-5):
-    """Oracle-vs-golden check. Bool / integer arrays (masks, indices, labels): bit-exact.
+# CPU the goldens were generated on (oracle/gen_goldens.py, 1 thread): PyTorch's CPU kernels (MKL
+# GEMM, vectorised reductions, transcendentals) dispatch on the vendor and the ISA level, and only
+# with the same dispatch does the oracle reproduce the reference's fp32 bits.
+GOLDEN_HOST = ('GenuineIntel', 'AVX512')
 
-    Float arrays: bit-exact on a host whose PyTorch CPU kernels (MKL GEMM, vectorised reductions
-    and transcendentals) match those of the host that generated the goldens; on a host with another
-    CPU ISA (AVX-512 vs AVX2 kernel selection) the same ops reorder fp32 sums, so the bar there is
-    fp32 roundoff: max |got - ref| <= rel * max|ref| (rel = 3e-5, three times tighter than the GPU
-    north_star tolerance; the largest cross-host mismatch seen, sdf_pdf `resd`, was 1.02e-5)."""
+
+def host_fingerprint():
+    vendor = ''
+    try:
+        with open('/proc/cpuinfo') as f:
+            for line in f:
+                if line.startswith('vendor_id'):
+                    vendor = line.split(':', 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return vendor, torch.backends.cpu.get_cpu_capability()
+
+
+def golden_strict():
+    """Bit-exact oracle-vs-golden checks: on the generating host's CPU dispatch, or when forced
+    (ANR_GOLDEN_STRICT=1); ANR_GOLDEN_STRICT=0 forces the roundoff bar."""
+    env = os.environ.get('ANR_GOLDEN_STRICT')
+    if env is not None:
+        return env == '1'
+    return host_fingerprint() == GOLDEN_HOST
+
+
+def assert_golden_equal(got, ref, err_msg='', rtol=3e-5, atol=1e-6):
+    """Oracle-vs-golden check.
+
+    * Bool / integer arrays (masks, indices, labels): bit-exact everywhere.
+    * Float arrays: bit-exact on the goldens' host dispatch (``golden_strict``). On a host with
+      another CPU dispatch (an AMD EPYC's MKL path, another ISA level) the same ops reorder fp32
+      sums, so there the bar is fp32 roundoff PER ELEMENT: |got - ref| <= atol + rtol * |ref|
+      (rtol 3e-5, three times tighter than the GPU north_star tolerance; the largest cross-host
+      mismatch seen, sdf_pdf `resd`, was 1.02e-5 of its array's max)."""
     got = np.asarray(got.detach().numpy() if hasattr(got, 'detach') else got)
     ref = np.asarray(ref)
     assert got.shape == ref.shape, (err_msg, got.shape, ref.shape)
     if np.array_equal(got, ref):
         return
     assert np.issubdtype(ref.dtype, np.floating), f'{err_msg}: integer/bool golden differs'
-    scale = max(float(np.abs(ref).max()), 1e-30)
-    err = float(np.abs(got.astype(np.float64) - ref.astype(np.float64)).max())
-    assert err <= rel * scale, f'{err_msg}: max |diff| {err:.3e} > {rel:g} x {scale:.3e}'
+    if golden_strict():
+        n = int(np.sum(got != ref))
+        raise AssertionError(f'{err_msg}: {n} of {ref.size} elements differ from the golden bits '
+                             f'(host {host_fingerprint()} = golden host; ANR_GOLDEN_STRICT=0 relaxes)')
+    np.testing.assert_allclose(got, ref, rtol=rtol, atol=atol, err_msg=err_msg)
 
 
 @functools.lru_cache(maxsize=4)

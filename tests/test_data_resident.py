@@ -2,6 +2,7 @@
 per-frame tensors are transferred once and reused by later batches of that frame; per-ray keys and
 the in-place-widened tbounds travel with every batch."""
 import numpy as np
+import pytest
 import torch
 
 from animatable_nerf_amd.data import ResidentFrames
@@ -32,6 +33,20 @@ def test_frames_upload_once_and_are_reused():
     assert not torch.equal(d0['ray_d'], d1['ray_d'])     # per-ray keys are fresh
     assert d1['tbounds'] is not d0['tbounds']            # not cached (widened in place by sdf_pdf)
     d2 = rf.to_device(_batch(4, 1))                      # another frame
-    assert rf.uploads == 2 * n_keys
+    n_frame = sum(1 for k in ResidentFrames.KEYS if k in b0 and k not in ResidentFrames.SUBJECT_KEYS)
+    assert rf.uploads == n_keys + n_frame                # subject keys (tbw) are not uploaded again
     assert not torch.equal(d2['pbw'], d0['pbw'])
-    assert rf.resident_bytes() == 2 * sum(d0[k].numel() * d0[k].element_size() for k in ResidentFrames.KEYS)
+    assert d2['tbw'] is d0['tbw']
+    per_frame = sum(d0[k].numel() * d0[k].element_size() for k in ResidentFrames.KEYS if k in b0)
+    subject = sum(d0[k].numel() * d0[k].element_size() for k in ResidentFrames.SUBJECT_KEYS if k in b0)
+    assert rf.resident_bytes() == 2 * per_frame - subject
+
+
+def test_mixed_frame_batch_is_refused():
+    rf = ResidentFrames('cpu')
+    b = _batch(3, 1)
+    b['frame_index'] = np.array([3, 5])
+    with pytest.raises(ValueError, match='one frame'):
+        rf.to_device(b)
+    b['frame_index'] = np.array([3, 3])                  # several images of one frame are fine
+    rf.to_device(b)

@@ -138,3 +138,61 @@ def test_gloo_sharded_frame_render_gather_psnr(n, world):
         assert p.exitcode == 0
     for rank, ok in res:
         assert ok is True, (rank, ok)
+
+
+def _fused_init_worker(rank, world, port, q):
+    """FusedStep's constructor on CPU tensors (the C-ABI library loads without a GPU; nothing is
+    launched): replicas that start from different weights, and an Adam state loaded on rank 0 only."""
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    try:
+        from animatable_nerf_amd import config, network
+        from animatable_nerf_amd.trainer import FusedStep
+        parallel.init_from_env('gloo')
+        torch.manual_seed(1000 + rank)  # a different init per rank (unseeded DDP-style start)
+        net = network.Network()
+        step = FusedStep(net, config.defaults())
+        flat0 = step.flat.clone()
+        got = [torch.empty_like(flat0) for _ in range(world)]
+        dist.all_gather(got, flat0)
+        same = all(torch.equal(got[0], x) for x in got)
+        views_ok = torch.equal(torch.cat([p.detach().reshape(-1) for p in net.core_tensors()]), flat0)
+        torch.manual_seed(7)
+        ref_m = torch.rand(step.n)
+        if rank == 0:  # a checkpoint read by rank 0 only
+            sd = {'state': {}, 'param_groups': [{'lr': 3e-4}]}
+            off = 0
+            for i, p in enumerate(net.core_tensors()):
+                k = p.numel()
+                sd['state'][i] = {'exp_avg': ref_m[off:off + k].reshape(p.shape),
+                                  'exp_avg_sq': 2 * ref_m[off:off + k].reshape(p.shape), 'step': torch.tensor(17.)}
+                off += k
+            step.load_adam_state_dict(sd)
+        else:
+            step.load_adam_state_dict({'state': {}, 'param_groups': [{'lr': 5e-4}]})
+        adam_ok = torch.equal(step.m, ref_m) and torch.equal(step.v, 2 * ref_m) and step.t == 17 and \
+            abs(step.lr - 3e-4) < 1e-12
+        q.put((rank, bool(same and views_ok and adam_ok)))
+    except Exception as ex:  # pragma: no cover
+        q.put((rank, repr(ex)))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_gloo_fused_step_replicas_start_from_rank0():
+    """DDP semantics of FusedStep (trainer.py:13-18): ranks built from different random weights all
+    hold rank 0's blob after construction (and their parameter views alias it), and Adam moments /
+    step count loaded on rank 0 only reach every rank."""
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fused_init_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, ok in res:
+        assert ok is True, (rank, ok)

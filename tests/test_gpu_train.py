@@ -103,7 +103,7 @@ def test_fused_step_matches_reference_adam(dev):
     net = make_net(dev)
     net.train()
     before = {k: v.detach().clone() for k, v in net.named_parameters()}
-    step = FusedStep(net, _cfg(), lr=float(g['lr']))
+    step = FusedStep(net, _cfg(), lr=float(str(np.float32(g['lr']))))
     loss3 = step.step(bt, t_rand=t_rand.to(dev)).cpu()
     assert abs(loss3[0].item() - float(g['loss'])) <= 1e-5 * abs(float(g['loss']))
     assert abs(loss3[1].item() - float(g['stat_img_loss'])) <= 1e-5 * abs(float(g['stat_img_loss']))
@@ -121,7 +121,7 @@ def test_fused_step_matches_reference_adam(dev):
             assert torch.allclose(d[big], ref[big], rtol=1e-3, atol=1e-8), name
             assert (d - ref).abs().max().item() <= 2 * float(g['lr']) + 1e-7, name
     # the Adam kernel itself, against torch.optim.Adam's first-step formula on our own gradients
-    lr = float(g['lr'])
+    lr = step.lr
     for name, p in params.items():
         gg = p.grad.detach().cpu().double()
         expect = -lr * gg / (gg.abs() + 1e-8)
@@ -156,3 +156,116 @@ def test_bf16_step_close_to_fp32(dev, prec):
         if nb > 0:
             worst = max(worst, (a - b).norm().item() / nb)
     assert worst <= 3e-2, worst
+
+
+def test_two_forwards_before_backward(dev):
+    """Each autograd forward owns its activations: forward(A), forward(B), backward(A) gives A's
+    gradients (the workspace of A must not be the one B overwrote)."""
+    from animatable_nerf_amd.trainer import NetworkWrapper
+    g, bt, t_rand = _g4_batch(dev)
+    sc = scene(0.05)
+    ro, rd = sc.box_rays(200, seed=77)
+    b2, _ = batch_np(sc, ro, rd, rgb=np.random.default_rng(5).random((200, 3)).astype(np.float32))
+    bt2 = to_torch(b2, dev)
+    t2 = torch.rand((bt2['ray_o'].shape[1], 64), device=dev)
+
+    def grads_of(run):
+        net = make_net(dev)
+        net.train()
+        wrap = NetworkWrapper(net, _cfg())
+        run(wrap)
+        return [p.grad.clone() for p in net.parameters()]
+
+    def alone(wrap):
+        wrap(bt, t_rand=t_rand.to(dev))[1].backward()
+
+    def interleaved(wrap):
+        _, loss_a, _, _ = wrap(bt, t_rand=t_rand.to(dev))
+        _, loss_b, _, _ = wrap(bt2, t_rand=t2)  # a second forward before the first backward
+        loss_a.backward()
+        del loss_b
+
+    ga, gi = grads_of(alone), grads_of(interleaved)
+    for a, b in zip(ga, gi):
+        # split-K weight gradients use fp32 atomics: equal up to summation order
+        assert _rel(b.cpu(), a.cpu()) <= 1e-5
+
+
+def test_adam_keeps_nan_gradients(dev):
+    """clip_grad_value_ (torch.clamp) passes NaN through, so a NaN gradient makes a NaN parameter
+    (the reference's failure signal) instead of a silent full-size step; finite entries are clipped
+    at 40 and updated as torch.optim.Adam's first step."""
+    from animatable_nerf_amd import _lib
+    lib = _lib.load()
+    n = 4096
+    gen = torch.Generator().manual_seed(3)
+    p = torch.randn(n, generator=gen).to(dev)
+    gr = (torch.randn(n, generator=gen) * 30).to(dev)
+    gr[::97] = float('nan')
+    gr[5] = 1e4  # clipped to 40
+    m, v = torch.zeros(n, device=dev), torch.zeros(n, device=dev)
+    p0, g0 = p.clone(), gr.clone()
+    lr = 1e-3
+    _lib.check(lib.anr_adam(_lib.ptr(p), _lib.ptr(gr), _lib.ptr(m), _lib.ptr(v), n, lr, 0.9, 0.999, 1e-8, 0.0, 1,
+                            40.0, _lib.stream_ptr(dev)), 'anr_adam')
+    torch.cuda.synchronize()
+    nan = torch.isnan(g0)
+    assert torch.isnan(p[nan]).all() and torch.isnan(gr[nan]).all()
+    assert torch.isfinite(p[~nan]).all()
+    gc = g0.clamp(-40, 40)
+    expect = p0 - lr * gc / (gc.abs() + 1e-8)
+    assert torch.allclose(p[~nan], expect[~nan], rtol=0, atol=1e-6)
+    assert gr[5].item() == 40.0
+
+
+def _ddp_worker(rank, world, port, q):
+    import os
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), HSA_ENABLE_IPC_MODE_LEGACY='0')
+    try:
+        from animatable_nerf_amd import parallel
+        from animatable_nerf_amd.trainer import FusedStep
+        dev = torch.device('cuda:0')  # both ranks share the one GPU of the box (gloo moves the blob)
+        parallel.init_from_env('gloo')
+        net = make_net(dev)
+        if rank == 1:  # a replica that starts from other weights
+            with torch.no_grad():
+                for prm in net.parameters():
+                    prm.add_(0.01 * torch.randn_like(prm))
+        net.train()
+        step = FusedStep(net, _cfg())
+        sc = scene(0.05)
+        ro, rd = sc.box_rays(128, seed=300 + rank)  # a different batch per rank
+        b, _ = batch_np(sc, ro, rd, rgb=np.random.default_rng(rank).random((128, 3)).astype(np.float32))
+        step.step(to_torch(b, dev), t_rand=torch.rand((int(b['ray_o'].shape[1]), 64), device=dev))
+        torch.cuda.synchronize()
+        got = [torch.empty_like(step.flat) for _ in range(world)]
+        dist.all_gather(got, step.flat)
+        q.put((rank, bool(torch.equal(got[0], got[1])), bool(torch.isfinite(step.flat).all())))
+    except Exception as ex:  # pragma: no cover
+        q.put((rank, repr(ex), False))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_fused_step_two_ranks_stay_identical(dev):
+    """World 2 over gloo on the one GPU: ranks built from different weights, each stepping its own
+    batch, hold identical blobs after one step (rank 0's start broadcast, mean gradient, same Adam)."""
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_ddp_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, same, finite in res:
+        assert same is True and finite, (rank, same)
