@@ -79,6 +79,12 @@ int stage_frontend(const anr_params* p, const anr_frame* f, const float* ray_o, 
   pa.bw_latent = p->t[27]; pa.w_lat = p->t[21]; pa.b_lat = p->t[22]; pa.nf_latent = p->t[0];
   pa.latent_index = f->latent_index;
   pa.fold = (float*)(ws + L.fold);
+  if (p->packed) {  // the bf16x3 program's folded head (anr_layers.h ANR_L_HEAD)
+    const float* head = (const float*)((const unsigned char*)p->packed + head_base());
+    pa.head_P = head + ANR_HEAD_P_OFF;
+    pa.head_q = head + ANR_HEAD_Q_OFF;
+    pa.b_alpha = p->t[18];
+  }
   if (o->novel_pose) {
     pa.novel = 1;
     pa.n_latent = p->novel[0];
@@ -328,6 +334,11 @@ int anr_params_pack(const anr_params* p, void* packed, void* stream) {
   }
   for (int i = 0; i < ANR_NUM_NOVEL_TENSORS; ++i) a.t[ANR_NOVEL_T0 + i] = p->novel[i];  // may be NULL
   a.out = (unsigned char*)packed;
+  a.t[ANR_HEAD_T] = (const float*)((unsigned char*)packed + head_base());
+  hipLaunchKernelGGL(k_pack_head_a, dim3((128 * 256 + 256 + 255) / 256), dim3(256), 0, (hipStream_t)stream, a);
+  ANR_TRY(check_launch("k_pack_head_a"));
+  hipLaunchKernelGGL(k_pack_head_b, dim3((ANR_HEAD_FLOATS + 255) / 256), dim3(256), 0, (hipStream_t)stream, a);
+  ANR_TRY(check_launch("k_pack_head_b"));
   const int nw = weights_bytes() / 4;
   hipLaunchKernelGGL(k_pack_weights, dim3((nw + 255) / 256), dim3(256), 0, (hipStream_t)stream, a);
   ANR_TRY(check_launch("k_pack_weights"));

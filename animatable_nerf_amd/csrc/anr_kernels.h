@@ -118,6 +118,9 @@ struct PrepArgs {
   int novel;
   const float *nw_bw0, *nb_bw0, *nw_bw5, *nb_bw5, *n_latent;
   const int64_t* bw_latent_index;
+  // folded colour head (anr_layers.h ANR_L_HEAD): fold[ANR_FOLD_HEAD + i] = P nf_latent[li] + q, row 128
+  // = alpha_fc's bias; skipped when head_P is NULL (callers without the bf16x3 render program)
+  const float *head_P, *head_q, *b_alpha;
 };
 
 __global__ void k_near_far(const float*, const float*, int, const float*, uint8_t*, float*, float*);
@@ -145,9 +148,11 @@ __global__ void k_alpha(MlpArgs a);      // density program (get_alpha), exact f
 __global__ void k_alpha_b16(MlpArgs a);  // density program, NeRF trunk in bf16x3
 
 struct PackArgs {
-  const float* t[65];  // 46 core tensors + 19 novel_pose_bw tensors (NULL when absent)
+  const float* t[66];  // 46 core tensors + 19 novel_pose_bw tensors (NULL when absent) + the head H
   unsigned char* out;
 };
+__global__ void k_pack_head_a(PackArgs a);
+__global__ void k_pack_head_b(PackArgs a);
 __global__ void k_pack_weights(PackArgs a);
 __global__ void k_pack_bias(PackArgs a);
 __global__ void k_pack_b16(PackArgs a);

@@ -76,7 +76,15 @@ __host__ __device__ constexpr LayerDesc layer_desc(int i) {
 // layer 30: alpha_fc alone (TPoseHuman.calculate_alpha :241-250, the density-only program of the
 // mesh path's get_alpha); the same weights as out-block 16 of layer 17
 #define ANR_L_ALPHA 30
-#define ANR_NUM_LAYERS_ALL 31
+#define ANR_NUM_LAYERS_ALL 31  // layers of the fp32 image (the folded head below is bf16x3-only)
+// layer 31 (bf16x3 image only): the folded colour head. feature_fc -> [|| nf_latent] latent_fc ->
+// [|| gamma(dir)] view_fc has no activation before view_fc's ReLU (tpose_nerf_network.py:260-272), so
+// view_fc's pre-activation is (Wv_f Wl_f Wf) net + Wv_d gamma(dir) + c(latent): one 283-input layer
+// of 128 outputs, with alpha_fc stacked as output row 128 (out-block 8, no ReLU). Weights: the head
+// tensor H (129 x 283) that k_pack_head composes in fp64 inside the packed buffer; per-frame bias
+// c = P nf_latent[li] + q (k_prep). Render program V = 2 (anr_mlp_body.h).
+#define ANR_L_HEAD 31
+#define ANR_HEAD_T 65  // PackArgs tensor index of H
 #define ANR_NOVEL_T0 46  // tensor index of novel_pose_bw.bw_latent.weight in the packer's list
 
 __host__ __device__ constexpr LayerDesc novel_desc(int i) {
@@ -91,6 +99,7 @@ __host__ __device__ constexpr LayerDesc layer_desc_all(int i) {
        : i == ANR_L_RGB  ? LayerDesc{25, 26, -1, -1, 3, 0, 128, 1, 1, {{SRC_ACT, 32, 0}, {0, 0, 0}}}
        : i < ANR_L_ALPHA ? novel_desc(i - ANR_L_NOVEL0)
        : i == ANR_L_ALPHA ? LayerDesc{17, 18, -1, -1, 1, 0, 256, 1, 1, {{SRC_ACT, 64, 0}, {0, 0, 0}}}
+       : i == ANR_L_HEAD ? LayerDesc{ANR_HEAD_T, -1, -1, -1, 129, 0, 283, 9, 2, {{SRC_ACT, 64, 0}, {SRC_VEMB, 8, 256}}}
        : LayerDesc{0, 0, -1, -1, 0, 0, 0, 0, 0, {{0, 0, 0}, {0, 0, 0}}};
 }
 
@@ -156,7 +165,7 @@ __host__ __device__ constexpr int ks32(int i) { return layer_ksteps(i) / 8; }
 __host__ __device__ constexpr int b16_main_ob(int i) { return layer_desc_all(i).ob < 16 ? layer_desc_all(i).ob : 16; }
 __host__ __device__ constexpr int b16_tail_ob(int i) { return layer_desc_all(i).ob - b16_main_ob(i); }
 __host__ __device__ constexpr int b16_layer_bytes(int i) { return ks32(i) * layer_desc_all(i).ob * 2048; }
-#define ANR_B16_LAYERS 31  // layers 0..30 (incl. the novel_pose_bw copy 21..29, alpha_fc 30)
+#define ANR_B16_LAYERS 32  // layers 0..31 (incl. the novel_pose_bw copy 21..29, alpha_fc 30, head 31)
 __host__ __device__ constexpr int b16_layer_offset(int i) {
   int o = 0;
   for (int k = 0; k < i; ++k) o += b16_layer_bytes(k);
@@ -202,7 +211,19 @@ __host__ __device__ inline int b16_col(const LayerDesc& d, int t, int h, int j) 
   return f < nf ? sg.col0 + f : -1;
 }
 
-__host__ __device__ constexpr int packed_bytes_all() { return x6_base() + x6_bytes(); }
+// folded-head region (k_pack_head): H (129 x 283 f32), P = Wv_f Wl_l (128 x 128 f32), q (128 f32),
+// then fp64 scratch G = Wv_f Wl_f (128 x 256) and u = Wl_f bf + bl (256)
+#define ANR_HEAD_H_FLOATS (129 * 283)
+#define ANR_HEAD_P_OFF ANR_HEAD_H_FLOATS
+#define ANR_HEAD_Q_OFF (ANR_HEAD_P_OFF + 128 * 128)
+#define ANR_HEAD_FLOATS (ANR_HEAD_Q_OFF + 128)
+__host__ __device__ constexpr int head_base() { return (x6_base() + x6_bytes() + 255) / 256 * 256; }
+__host__ __device__ constexpr int head_scratch_base() { return (head_base() + ANR_HEAD_FLOATS * 4 + 255) / 256 * 256; }
+#define ANR_HEAD_SCRATCH_DOUBLES (128 * 256 + 256)
+__host__ __device__ constexpr int packed_bytes_all() { return head_scratch_base() + ANR_HEAD_SCRATCH_DOUBLES * 8; }
+// per-frame fold buffer (floats): bw0 pose/T, bw5 pose/T, latent_fc (5 x 256), head bias (144)
+#define ANR_FOLD_HEAD 1280
+#define ANR_FOLD_FLOATS 1536
 
 // LDS of the fused kernel: a ring of staging buffers of the largest slice, the 24 joint transforms
 // and the bias table (mlp_bias_floats, every program entry's bias, filled once per launch so no

@@ -56,11 +56,16 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 //   mode 1 bf16x3 (k_mlp_b16; the pose pass too unless built with ANR_POSE_MODE=2);
 //   mode 2 bf16x6, fp32-level (the pose pass with ANR_POSE_MODE=2: measured unnecessary, the
 //          outputs' error vs the fp32 oracle stays <= 4e-6 with x3, tools/precision_report.py).
+//   V = 2 (render, bf16x3 kernel): entries 0..25 as V = 0, 26 the folded colour head (layer 31:
+//         view_fc's pre-activation || alpha_fc, anr_layers.h ANR_L_HEAD), 27 rgb_fc.
 template <int V>
-__host__ __device__ constexpr int prog_len() { return V == 0 ? 30 : 18; }
+__host__ __device__ constexpr int prog_len() { return V == 0 ? 30 : V == 2 ? 28 : 18; }
 template <int V>
 __host__ __device__ constexpr int prog_layer(int e) {
-  return e < 9 ? e : (V == 0 ? e - 9 : (e < 17 ? e : ANR_L_ALPHA));
+  return e < 9 ? e
+         : V == 0 ? e - 9
+         : V == 2 ? (e < 26 ? e - 9 : (e == 26 ? ANR_L_HEAD : ANR_L_RGB))
+                  : (e < 17 ? e : ANR_L_ALPHA);
 }
 __host__ __device__ constexpr bool prog_pose(int e) { return e < 9; }
 template <bool B16>
@@ -284,6 +289,7 @@ __host__ __device__ constexpr int prog_bias_off(int e) {
 }
 static_assert(prog_bias_off<0>(prog_len<0>()) == ANR_BIAS_TABLE_FLOATS, "bias table size (anr_layers.h)");
 static_assert(prog_bias_off<1>(prog_len<1>()) <= ANR_BIAS_TABLE_FLOATS, "bias table size (anr_layers.h)");
+static_assert(prog_bias_off<2>(prog_len<2>()) <= ANR_BIAS_TABLE_FLOATS, "bias table size (anr_layers.h)");
 
 // Fill the bias table once per launch (before the first barrier of the slice stream). Sources:
 // the packed bias section, the novel_pose_bw copy for the pose pass (pose_boff), and the per-frame
@@ -299,10 +305,10 @@ __device__ __forceinline__ void fill_bias_table(const MlpArgs& a, float* __restr
     const float* src;
     if constexpr (e < 9) {
       src = L == 0 ? a.fold + 0 : L == 5 ? a.fold + 512 : a.bias + a.pose_boff + boff;
-    } else if constexpr (V == 0 && e < 18) {
+    } else if constexpr (V != 1 && e < 18) {
       src = L == 0 ? a.fold + 256 : L == 5 ? a.fold + 768 : a.bias + boff;
     } else {
-      src = L == 18 ? a.fold + 1024 : a.bias + boff;
+      src = L == 18 ? a.fold + 1024 : L == ANR_L_HEAD ? a.fold + ANR_FOLD_HEAD : a.bias + boff;
     }
     for (int i = tid; i < n; i += 512) sb[toff + i] = src[i];
   });
@@ -656,7 +662,8 @@ __device__ __forceinline__ void bw_mlp(Pipe& p, const float (&emb)[16], const fl
 
 template <bool B16>
 __device__ __forceinline__ void mlp_body(const MlpArgs& a) {
-  constexpr int V = 0;
+  // the exact fp32 kernel runs the reference's layer sequence; the bf16x3 kernel the folded head
+  constexpr int V = B16 ? 2 : 0;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -720,13 +727,26 @@ __device__ __forceinline__ void mlp_body(const MlpArgs& a) {
     layer<B16, V, 23, true>(p, A, emb, vemb, B, sb, g, lane);
     layer<B16, V, 24, true>(p, B, emb, vemb, A, sb, g, lane);
     layer<B16, V, 25, true>(p, A, emb, vemb, B, sb, g, lane);
-    layer<B16, V, 26, false>(p, B, emb, vemb, A, sb, g, lane);  // feature || alpha
-    const float sigma_raw = __shfl(A[16][0], pl);
-    layer<B16, V, 27, false>(p, A, emb, vemb, B, sb, g, lane);  // latent_fc
-    if constexpr (B16) embed_b<1>(dir, g, 4, vemb);
-    else embed<8>(dir, g, 4, vemb);
-    layer<B16, V, 28, true>(p, B, emb, vemb, A, sb, g, lane);   // view_fc
-    layer<B16, V, 29, false>(p, A, emb, vemb, B, sb, g, lane);  // rgb_fc
+    float sigma_raw;
+    if constexpr (V == 2) {
+      embed_b<1>(dir, g, 4, vemb);
+      layer<B16, V, 26, false>(p, B, emb, vemb, A, sb, g, lane);  // view_fc pre-activation || alpha
+      sigma_raw = __shfl(A[8][0], pl);
+      static_for<0, 8>([&](auto ob) {
+        constexpr int o = decltype(ob)::value;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) A[o][r] = fmaxf(A[o][r], 0.0f);
+      });
+      layer<B16, V, 27, false>(p, A, emb, vemb, B, sb, g, lane);  // rgb_fc
+    } else {
+      layer<B16, V, 26, false>(p, B, emb, vemb, A, sb, g, lane);  // feature || alpha
+      sigma_raw = __shfl(A[16][0], pl);
+      layer<B16, V, 27, false>(p, A, emb, vemb, B, sb, g, lane);  // latent_fc
+      if constexpr (B16) embed_b<1>(dir, g, 4, vemb);
+      else embed<8>(dir, g, 4, vemb);
+      layer<B16, V, 28, true>(p, B, emb, vemb, A, sb, g, lane);   // view_fc
+      layer<B16, V, 29, false>(p, A, emb, vemb, B, sb, g, lane);  // rgb_fc
+    }
 
     // ---- bbox mask, activations, outputs
     bool inside = true;

@@ -138,6 +138,62 @@ __global__ void k_pack_x6(PackArgs a) {
   }
 }
 
+// Folded colour head (anr_layers.h ANR_L_HEAD), composed in fp64 from the state_dict tensors
+// (feature_fc 19/20, latent_fc 21/22, view_fc 23/24, alpha_fc 17):
+//   a: G = Wv[:, :256] Wl[:, :256] (128 x 256), u = Wl[:, :256] bf + bl (256)      (fp64 scratch)
+//   b: H[i < 128] = [G Wf | Wv[:, 256:283]], H[128] = [alpha_fc | 0];
+//      P = Wv[:, :256] Wl[:, 256:384] (128 x 128); q = Wv[:, :256] u + bv          (f32)
+__global__ void k_pack_head_a(PackArgs a) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  double* G = (double*)(a.out + head_scratch_base());
+  double* u = G + 128 * 256;
+  const float *Wf = a.t[19], *bf = a.t[20], *Wl = a.t[21], *bl = a.t[22], *Wv = a.t[23];
+  if (e < 128 * 256) {
+    const int i = e >> 8, k = e & 255;
+    double acc = 0.0;
+    for (int m = 0; m < 256; ++m) acc += (double)Wv[i * 283 + m] * (double)Wl[m * 384 + k];
+    G[e] = acc;
+  } else if (e < 128 * 256 + 256) {
+    const int m = e - 128 * 256;
+    double acc = bl[m];
+    for (int k = 0; k < 256; ++k) acc += (double)Wl[m * 384 + k] * (double)bf[k];
+    u[m] = acc;
+  }
+  (void)Wf;
+}
+
+__global__ void k_pack_head_b(PackArgs a) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  const double* G = (const double*)(a.out + head_scratch_base());
+  const double* u = G + 128 * 256;
+  float* H = (float*)(a.out + head_base());
+  const float *Wf = a.t[19], *Wl = a.t[21], *Wv = a.t[23], *bv = a.t[24], *Wa = a.t[17];
+  if (e < ANR_HEAD_H_FLOATS) {
+    const int i = e / 283, c = e - i * 283;
+    float v;
+    if (i == 128) {
+      v = c < 256 ? Wa[c] : 0.0f;
+    } else if (c >= 256) {
+      v = Wv[i * 283 + c];
+    } else {
+      double acc = 0.0;
+      for (int k = 0; k < 256; ++k) acc += G[i * 256 + k] * (double)Wf[k * 256 + c];
+      v = (float)acc;
+    }
+    H[e] = v;
+  } else if (e < ANR_HEAD_Q_OFF) {
+    const int pe = e - ANR_HEAD_P_OFF, i = pe >> 7, j = pe & 127;
+    double acc = 0.0;
+    for (int m = 0; m < 256; ++m) acc += (double)Wv[i * 283 + m] * (double)Wl[m * 384 + 256 + j];
+    H[e] = (float)acc;
+  } else if (e < ANR_HEAD_FLOATS) {
+    const int i = e - ANR_HEAD_Q_OFF;
+    double acc = bv[i];
+    for (int m = 0; m < 256; ++m) acc += (double)Wv[i * 283 + m] * u[m];
+    H[e] = (float)acc;
+  }
+}
+
 // grid: blocks [0, nvox_blocks) repack volumes; block 'fold' computes the five folded biases
 __global__ __launch_bounds__(256) void k_prep(PrepArgs a) {
   const int nvb = (a.np + a.nt + 7) / 8;  // 8 voxels (x 32 channels) per block
@@ -171,6 +227,20 @@ __global__ __launch_bounds__(256) void k_prep(PrepArgs a) {
       for (int q = 0; q < 128; ++q) acc = fmaf(a.w_lat[(size_t)nn * 384 + 256 + q], lat[q], acc);
     }
     a.fold[k] = acc;
+  }
+  if (a.head_P) {
+    const float* lat = a.nf_latent + (size_t)li * 128;
+    for (int i = threadIdx.x; i < ANR_FOLD_FLOATS - ANR_FOLD_HEAD; i += blockDim.x) {
+      float v = 0.0f;
+      if (i < 128) {
+        double acc = a.head_q[i];
+        for (int j = 0; j < 128; ++j) acc += (double)a.head_P[i * 128 + j] * (double)lat[j];
+        v = (float)acc;
+      } else if (i == 128) {
+        v = a.b_alpha[0];
+      }
+      a.fold[ANR_FOLD_HEAD + i] = v;
+    }
   }
 }
 

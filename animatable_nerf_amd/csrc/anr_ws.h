@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include "../../include/aninerf.h"
+#include "anr_layers.h"
 
 namespace anr {
 
@@ -43,7 +44,7 @@ inline Layout layout(int n_rays, int chunk, long np, long nt, bool need_raw) {
   L.raw = need_raw ? take(N * 16) : 0;
   L.pbw32 = take((size_t)np * 32 * 4);
   L.tbw32 = take((size_t)nt * 32 * 4);
-  L.fold = take(1280 * 4);
+  L.fold = take(ANR_FOLD_FLOATS * 4);
   L.total = o;
   return L;
 }

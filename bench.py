@@ -13,7 +13,7 @@ precision: --render-precision bf16x3 (default) runs the fused network kernel k_m
           <= 4e-6, tools/precision_report.py); the exact-fp32 kernel k_mlp is timed in the same run.
 roofline: the fused network kernel is the dominant kernel; its per-launch time is measured with
           hipEvents on the render stream (anr_profile_*); achieved = executed MFMA FLOP per kept
-          sample (bf16x3: 2*3*(2*497,152 + 658,944); fp32: 3,306,496) x kept / time,
+          sample (bf16x3: 2*3*(2*497,152 + 527,872), the NeRF head folded; fp32: 3,306,496) x kept / time,
           peak = the dense MFMA peak of the operand type (bf16 2.5 PF, fp32 157.3 TF);
           achieved_credited uses SURVEY.md §8(d)'s 2,312,192 FLOP per kept sample.
 cpu_baseline: the oracle (op-for-op PyTorch-CPU restatement of the reference) on the first 16
@@ -31,6 +31,9 @@ import torch.distributed as dist
 FLOP_PER_KEPT = 2_312_192          # render credit (BW pose + NeRF, latent folded)
 FLOP_PER_KEPT_EXECUTED = 3_306_496  # + T-pose BW MLP (tbw rows are part of the render outputs)
 MAC_BW, MAC_NERF = 497_152, 658_944  # per kept sample, latent folded
+# the bf16x3 kernel's NeRF with the folded colour head (anr_layers.h ANR_L_HEAD): trunk 491,008 +
+# alpha_fc 256 + (Wv_f Wl_f Wf || Wv_d) 128 x 283 + rgb_fc 384
+MAC_NERF_FOLDED = 491_008 + 256 + 128 * 283 + 384
 PEAK_FP32_MFMA_TFLOPS = 157.3      # MI355X_MICROARCH.md, Peak FP32 (matrix)
 PEAK_BF16_MFMA_TFLOPS = 2500.0     # MI355X_MICROARCH.md, BF16 dense (no sparsity)
 METRIC = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), 'BASELINE.json')))['metric']
@@ -166,7 +169,7 @@ def main():
     split = args.render_precision == 'bf16x3'
     if split:
         # executed bf16 MFMA work per kept sample: 3 products per MAC (lo*bh + hi*bl + hi*bh)
-        flop_exec = 2 * 3 * (2 * MAC_BW + MAC_NERF)
+        flop_exec = 2 * 3 * (2 * MAC_BW + MAC_NERF_FOLDED)
         peak = PEAK_BF16_MFMA_TFLOPS
         dtype = 'bf16 MFMA operands (hi/lo split, 3 products per MAC), fp32 accumulate'
     else:

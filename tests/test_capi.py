@@ -42,10 +42,15 @@ def test_version_and_sizes(lib):
     # bf16x3 image: per layer ceil(in/32) k-steps x out-blocks x 2 KiB (hi + lo fragments)
     ks_ob = [(2, 16), (8, 16), (8, 16), (8, 16), (8, 16), (10, 16), (8, 16), (8, 16), (8, 2),
              (2, 16), (8, 16), (8, 16), (8, 16), (8, 16), (10, 16), (8, 16), (8, 16), (8, 17), (8, 16), (9, 8), (4, 1)]
-    b16 = (sum(k * o for k, o in ks_ob) + sum(k * o for k, o in ks_ob[:9]) + 8 * 1) * 2048  # + novel copy, alpha
+    # + novel copy, alpha, the folded colour head (layer 31: 9 k-steps x 9 out-blocks)
+    b16 = (sum(k * o for k, o in ks_ob) + sum(k * o for k, o in ks_ob[:9]) + 8 * 1 + 9 * 9) * 2048
     x6 = 2 * sum(k * o for k, o in ks_ob[:9]) * 3072  # pose-pass bf16x6 image (+ novel-pose copy)
     base16 = (fp32 + 255) // 256 * 256
-    assert lib.anr_params_packed_bytes() == (base16 + b16 + 255) // 256 * 256 + x6
+    end_x6 = (base16 + b16 + 255) // 256 * 256 + x6
+    # head region: H (129 x 283), P (128 x 128), q (128) f32, then fp64 scratch G (128 x 256) and u (256)
+    head = (end_x6 + 255) // 256 * 256
+    scratch = (head + 4 * (129 * 283 + 128 * 128 + 128) + 255) // 256 * 256
+    assert lib.anr_params_packed_bytes() == scratch + 8 * (128 * 256 + 256)
 
 
 def test_workspace_grows_with_rays(lib):
