@@ -43,7 +43,13 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 #endif
 // LDS fragment reads in flight ahead of the MFMAs (bf16x3 layers)
 #ifndef ANR_FRAG_PF
-#define ANR_FRAG_PF 1
+#define ANR_FRAG_PF 2
+#endif
+// bf16x3 layers: issue a refill's LDS-DMA pieces one by one between the out-blocks of the slice's
+// second half (after its mid() barrier) instead of as one burst right after the barrier, where every
+// wave of the workgroup queues its pieces at the texture unit at the same time
+#ifndef ANR_DMA_SPREAD
+#define ANR_DMA_SPREAD 1
 #endif
 
 // The per-tile layer program, variant V:
@@ -144,6 +150,7 @@ struct Pipe {
   int wave;
   int lane;
   int pose_woff;  // added to slices of the pose-space BW pass (novel_pose_bw weights)
+  int pend;       // ring slot of the refill whose pieces are being spread (ANR_DMA_SPREAD)
 
   // issue the HBM/L2 -> LDS copy of `kb` KiB at byte `off` of the packed image into ring slot `buf`;
   // every wave issues exactly `loads` 1-KiB pieces (pieces past the end repeat the last one: same
@@ -153,7 +160,7 @@ struct Pipe {
   // the first ds_read after it, which drains the whole ring (every slice still in flight) once per
   // slice. Hidden from the compiler, the only waits on the stream are ours (wait_vmcnt in next());
   // the compiler's own vmcnt waits stay correct, only stricter (loads return in order).
-  __device__ __forceinline__ void stage(int off, int kb, int loads, int buf) {
+  __device__ __forceinline__ void stage(int off, int kb, int loads, int buf, int first = 0) {
     const unsigned dst = (unsigned)(uintptr_t)(lds + buf * smax);
     // launder the base so the per-slice addresses are formed here, not hoisted out of the tile
     // loop (hundreds of loop-invariant 64-bit addresses otherwise spill)
@@ -172,7 +179,7 @@ struct Pipe {
       if (wave >= 4) return;
       loads *= 2;
     }
-    for (int i = 0; i < loads; ++i) {
+    for (int i = first; i < loads; ++i) {
       int piece = wave + ANR_DMA_WAVES * i;
       piece = piece < kb ? piece : kb - 1;
       const unsigned char* src = w + off + piece * 1024 + lane * 16;
@@ -234,7 +241,8 @@ struct Pipe {
   // ANR_MIDSYNC: called halfway through slice (E, Q), while its MFMAs are in flight: certify the next
   // slice (own loads landed + barrier: everyone's landed, and everyone is past the previous slice),
   // then refill the previous slice's slot with the slice nbuf-1 ahead.
-  template <bool B16, int V, int E, int Q>
+  // SPREAD: only certify and pick the slot here; the refill's pieces follow through piece<>().
+  template <bool B16, int V, int E, int Q, bool SPREAD = false>
   __device__ __forceinline__ void mid() {
     if constexpr (ANR_MIDSYNC) {
       constexpr int NB = mlp_nbuf<B16>();
@@ -246,8 +254,20 @@ struct Pipe {
 #endif
       int slot = cur + NB - 1;
       slot = slot >= NB ? slot - NB : slot;
-      stage_slice<B16, V, eq / 1024, eq % 1024>(slot);
+      if constexpr (SPREAD) pend = slot;
+      else stage_slice<B16, V, eq / 1024, eq % 1024>(slot);
     }
+  }
+  // pieces [I0, I1) of this wave's share of the refill picked by mid<..., true>() of slice (E, Q)
+  template <bool B16, int V, int E, int Q, int I0, int I1>
+  __device__ __forceinline__ void piece() {
+    constexpr int NB = mlp_nbuf<B16>();
+    constexpr int eq = prog_advance<B16, V>(E, Q, NB - 1);
+    constexpr int EE = eq / 1024, QQ = eq % 1024;
+    constexpr int off = prog_slice_off<B16, V>(EE, QQ);
+    constexpr int loads = prog_slice_loads<B16, V>(EE, QQ);
+    constexpr int i1 = I1 < loads ? I1 : loads;
+    if constexpr (I0 < i1) stage(off + (prog_pose(EE) ? pose_woff : 0), prog_slice_kb<B16, V>(EE, QQ), i1, pend, I0);
   }
   __device__ __forceinline__ void leave() { cur = cur + 1 >= nbuf ? 0 : cur + 1; }
 };
@@ -315,12 +335,150 @@ __device__ __forceinline__ void fill_bias_table(const MlpArgs& a, float* __restr
 }
 
 // One MLP layer (program entry E): out = W * src + bias (acc layout), k-steps from its segments.
-template <bool B16, int V, int E, bool RELU, int NIN, int NOUT>
+// bf16x3 layers as one continuous MFMA stream (ANR_X3_STREAM): the B fragment of k-step t+1 is split
+// while k-step t's MFMAs run, A fragments are read ANR_FRAG_PF out-blocks ahead across k-step (slice)
+// boundaries, and the ReLU of the previous layer is applied in this layer's split (RELU_IN) instead
+// of as a pass over the previous layer's outputs.
+#ifndef ANR_X3_STREAM
+#define ANR_X3_STREAM 1
+#endif
+template <int L>
+__host__ __device__ constexpr bool x3_stream_layer() {
+  return ANR_X3_STREAM && b16_tail_ob(L) == 0;
+}
+
+// iteration (k-step * MOB + out-block) at which fragment G is read; < 0: the layer's prologue
+template <int MOB, int PF>
+__host__ __device__ constexpr int x3_issue_at(int G) {
+  const int t = G / MOB;
+  const int a = G - PF;
+  if (t == 0) return a;
+  const int m = (t - 1) * MOB + (MOB - 1) / 2;
+  return a > m ? a : m;
+}
+
+template <bool B16, int V, int E, bool RELU_IN, int NIN, int NOUT>
+__device__ __forceinline__ void layer_x3(Pipe& p, const f32x4 (&in)[NIN], const float (&emb)[16], const float (&vemb)[8],
+                                         f32x4 (&out)[NOUT], const float* __restrict__ sbias, int g, int lane) {
+  constexpr int L = prog_layer<V>(E);
+  constexpr LayerDesc D = layer_desc_all(L);
+  constexpr int KS = ks32(L);
+  constexpr int K0 = D.seg[0].ksteps / 8;
+  constexpr int MOB = b16_main_ob(L);
+  constexpr int PF = ANR_FRAG_PF;
+  constexpr int NF = PF + 1;
+  constexpr int MID = (MOB - 1) / 2;
+  constexpr int BOFF = prog_bias_off<V>(E);
+  static_assert(b16_tail_ob(L) == 0, "streamed x3 layers have no tail slice");
+  // the B operand of k-step t: 8 inputs (ReLU of the previous layer applied here), hi/lo split
+  auto split_k = [&](auto tc, bf16x8& bh, bf16x8& bl) {
+    constexpr int t = decltype(tc)::value;
+    constexpr int seg = t < K0 ? 0 : 1;
+    constexpr int ts = t < K0 ? t : t - K0;
+    constexpr int kind = D.seg[seg].kind;
+    float x[8];
+    if constexpr (kind == SRC_EMB) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] = emb[8 * ts + j];
+    } else if constexpr (kind == SRC_VEMB) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] = vemb[j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        x[j] = RELU_IN ? fmaxf(in[2 * ts][j], 0.0f) : in[2 * ts][j];
+        x[4 + j] = RELU_IN ? fmaxf(in[2 * ts + 1][j], 0.0f) : in[2 * ts + 1][j];
+      }
+    }
+    split8(x, bh, bl);
+  };
+  // fragment G = t * MOB + o (k-step t, out-block o) lives in register set G % NF. Same-slice
+  // fragments are read PF out-blocks ahead; a fragment of slice t >= 1 read from slice t - 1 waits
+  // for that slice's mid() (which certifies slice t), i.e. no earlier than out-block MID.
+  bf16x8 fh[NF], fl[NF];
+  bf16x8 bh[2], bl[2];
+  const unsigned char* buf = p.template enter<B16, V, E, 0>();
+  __builtin_amdgcn_sched_barrier(0);
+  static_for<0, D.ob>([&](auto ob) {
+    constexpr int o = decltype(ob)::value;
+    out[o] = *(const f32x4*)(sbias + BOFF + o * 16 + 4 * g);
+  });
+  split_k(std::integral_constant<int, 0>{}, bh[0], bl[0]);
+  static_for<0, PF>([&](auto gg) {
+    constexpr int G = decltype(gg)::value;
+    if constexpr (G < MOB && x3_issue_at<MOB, PF>(G) < 0) {
+      fh[G % NF] = *(const bf16x8*)(buf + G * 2048 + lane * 16);
+      fl[G % NF] = *(const bf16x8*)(buf + G * 2048 + 1024 + lane * 16);
+    }
+  });
+  static_for<0, KS>([&](auto t) {
+    constexpr int tt = decltype(t)::value;
+    if constexpr (tt > 0) buf = p.template enter<B16, V, E, tt>();
+    const unsigned char* nbuf = p.lds + (p.cur + 1 >= p.nbuf ? 0 : p.cur + 1) * p.smax;
+    static_for<0, MOB>([&](auto ob) {
+      constexpr int o = decltype(ob)::value;
+      constexpr int F = tt * MOB + o;
+      // fragments due at this out-block: same slice, or the next one once it is certified (o > MID)
+      static_for<1, PF + 1>([&](auto dd) {
+        constexpr int G = F + decltype(dd)::value;
+        if constexpr (G / MOB == tt && x3_issue_at<MOB, PF>(G) == F) {
+          fh[G % NF] = *(const bf16x8*)(buf + (G % MOB) * 2048 + lane * 16);
+          fl[G % NF] = *(const bf16x8*)(buf + (G % MOB) * 2048 + 1024 + lane * 16);
+        } else if constexpr (o > MID && tt + 1 < KS && G / MOB == tt + 1 && x3_issue_at<MOB, PF>(G) == F) {
+          fh[G % NF] = *(const bf16x8*)(nbuf + (G % MOB) * 2048 + lane * 16);
+          fl[G % NF] = *(const bf16x8*)(nbuf + (G % MOB) * 2048 + 1024 + lane * 16);
+        }
+      });
+      __builtin_amdgcn_sched_barrier(0);
+      constexpr int r = F % NF, c = tt & 1;
+      out[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fl[r], bh[c], out[o], 0, 0, 0);
+      out[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fh[r], bl[c], out[o], 0, 0, 0);
+      out[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fh[r], bh[c], out[o], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      // the next k-step's B fragment, early in this k-step
+      if constexpr (o == (MOB > 1 ? 1 : 0) && tt + 1 < KS)
+        split_k(std::integral_constant<int, tt + 1>{}, bh[c ^ 1], bl[c ^ 1]);
+      if constexpr (!ANR_DMA_SPREAD) {
+        if constexpr (o == MID) p.template mid<B16, V, E, tt>();
+      } else {
+        constexpr int eqr = prog_advance<B16, V>(E, tt, mlp_nbuf<B16>() - 1);
+        constexpr int NL = prog_slice_loads<B16, V>(eqr / 1024, eqr % 1024);
+        constexpr int SPAN = MOB - 1 - MID;
+        if constexpr (o == MID) p.template mid<B16, V, E, tt, true>();
+        if constexpr (SPAN == 0) {
+          if constexpr (o == MID) p.template piece<B16, V, E, tt, 0, NL>();
+        } else if constexpr (o > MID) {
+          constexpr int lo = ((o - MID - 1) * NL + SPAN - 1) / SPAN;
+          constexpr int hi = o == MOB - 1 ? NL : ((o - MID) * NL + SPAN - 1) / SPAN;
+          p.template piece<B16, V, E, tt, lo, hi>();
+        }
+      }
+      // next-slice fragments due at out-block MID: after mid(), which certifies the next slice
+      if constexpr (tt + 1 < KS && o == MID) {
+        static_for<1, PF + 1>([&](auto dd) {
+          constexpr int G = F + decltype(dd)::value;
+          if constexpr (G / MOB == tt + 1 && x3_issue_at<MOB, PF>(G) == F) {
+            fh[G % NF] = *(const bf16x8*)(nbuf + (G % MOB) * 2048 + lane * 16);
+            fl[G % NF] = *(const bf16x8*)(nbuf + (G % MOB) * 2048 + 1024 + lane * 16);
+          }
+        });
+      }
+    });
+    p.leave();
+  });
+}
+
+template <bool B16, int V, int E, bool RELU, bool RELU_IN = false, int NIN, int NOUT>
 __device__ __forceinline__ void layer(Pipe& p, const f32x4 (&in)[NIN], const float (&emb)[16], const float (&vemb)[8],
                                       f32x4 (&out)[NOUT], const float* __restrict__ sbias, int g, int lane) {
   constexpr int L = prog_layer<V>(E);
   constexpr LayerDesc D = layer_desc_all(L);
   static_assert(NOUT >= D.ob, "output array too small");
+  if constexpr (prog_mode<B16>(E) == 1 && x3_stream_layer<L>()) {
+    // output ReLU deferred to the consumer's split (RELU_IN of the next layer)
+    layer_x3<B16, V, E, RELU_IN>(p, in, emb, vemb, out, sbias, g, lane);
+    return;
+  }
   // accumulators start at the bias; read right after the layer's first slice barrier, so the
   // compiler cannot hoist the reads (64 registers) into the previous layer
   constexpr int BOFF = prog_bias_off<V>(E);
@@ -411,7 +569,25 @@ __device__ __forceinline__ void layer(Pipe& p, const f32x4 (&in)[NIN], const flo
           out[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fh[r], bl, out[o], 0, 0, 0);
           out[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fh[r], bh, out[o], 0, 0, 0);
           __builtin_amdgcn_sched_barrier(0);
-          if constexpr (o == (MOB - 1) / 2) p.template mid<B16, V, E, tt>();
+          constexpr int MID = (MOB - 1) / 2;
+          if constexpr (!ANR_DMA_SPREAD) {
+            if constexpr (o == MID) p.template mid<B16, V, E, tt>();
+          } else {
+            // refill pieces i at out-block MID + 1 + i * (MOB - 1 - MID) / NL (all at MID when the
+            // slice has no second half); every piece is out before the next slice's mid()
+            constexpr int eqr = prog_advance<B16, V>(E, tt, mlp_nbuf<B16>() - 1);
+            constexpr int NL = prog_slice_loads<B16, V>(eqr / 1024, eqr % 1024);
+            constexpr int SPAN = MOB - 1 - MID;
+            if constexpr (o == MID) p.template mid<B16, V, E, tt, true>();
+            if constexpr (SPAN == 0) {
+              if constexpr (o == MID) p.template piece<B16, V, E, tt, 0, NL>();
+            } else if constexpr (o > MID) {
+              // pieces whose slot is this out-block: i with MID + 1 + i * SPAN / NL == o
+              constexpr int lo = ((o - MID - 1) * NL + SPAN - 1) / SPAN;
+              constexpr int hi = o == MOB - 1 ? NL : ((o - MID) * NL + SPAN - 1) / SPAN;
+              p.template piece<B16, V, E, tt, lo, hi>();
+            }
+          }
         });
         p.leave();
       }
@@ -488,6 +664,11 @@ __device__ __forceinline__ void embed_b(const float x[3], int h, int nfreq, floa
   // launder the lane half: otherwise the per-lane frequency scales and component selects of all
   // 8*NS features are hoisted out of the tile loop and pin ~30 registers for the whole kernel
   asm volatile("" : "+v"(h));
+#ifdef ANR_EXP_NOSTRETCH
+#pragma unroll
+  for (int k = 0; k < 8 * NS; ++k) e[k] = x[k % 3] * (0.1f + 0.01f * k);  // timing experiment only
+  return;
+#endif
 #pragma unroll
   for (int s = 0; s < NS; ++s)
 #pragma unroll
@@ -547,7 +728,7 @@ __device__ __forceinline__ void lookup24(const float* __restrict__ vol32, const 
   float lo[3], hi[3];
 #pragma unroll
   for (int c = 0; c < 3; ++c) { lo[c] = bounds[c]; hi[c] = bounds[3 + c]; }
-#ifdef ANR_EXP_NOLOOKUP
+#if defined(ANR_EXP_NOLOOKUP) || defined(ANR_EXP_NOSTRETCH)
   out[0] = f32x4{0.04f, 0.04f, 0.04f, 0.04f};  // timing experiment only
   out[1] = out[0];
   return;
@@ -574,6 +755,11 @@ __device__ __forceinline__ void lookup24(const float* __restrict__ vol32, const 
 // softmax over 24 channels of log(init + 1e-9) + fc (tpose_nerf_network.py:74-76); lanes
 // l, l^16, l^32, l^48 hold one point's channels.
 __device__ __forceinline__ void blend_softmax(const f32x4 (&fc)[2], const f32x4 (&init)[2], int g, f32x4 (&bw)[2]) {
+#ifdef ANR_EXP_NOSTRETCH
+  bw[0] = fc[0] * 0.01f + init[0];  // timing experiment only
+  bw[1] = fc[1] * 0.01f + init[1];
+  return;
+#endif
   float lg[2][4];
   float m = -INFINITY;
 #pragma unroll
@@ -606,6 +792,10 @@ __device__ __forceinline__ void blend_softmax(const f32x4 (&fc)[2], const f32x4 
 // LBS inverse warp: A_b = sum_j bw_j A_j; x_T = inv(A_b[:3,:3]) (x - A_b[:3,3])
 __device__ __forceinline__ void lbs_inverse(const f32x4 (&bw)[2], const float* __restrict__ sA, int g, const float x[3],
                                             float xt[3]) {
+#ifdef ANR_EXP_NOSTRETCH
+  xt[0] = x[0] + bw[0][0]; xt[1] = x[1] + bw[0][1]; xt[2] = x[2] + bw[1][0];  // timing experiment only
+  return;
+#endif
   float Ab[16];
 #pragma unroll
   for (int m = 0; m < 16; ++m) Ab[m] = 0.f;
@@ -650,14 +840,14 @@ __device__ __forceinline__ void bw_mlp(Pipe& p, const float (&emb)[16], const fl
                                        f32x4 (&A)[17], f32x4 (&B)[17], f32x4 (&fc)[2], int g, int lane) {
   f32x4 dummy[1];
   layer<B16, V, E0 + 0, true>(p, dummy, emb, vemb, A, sb, g, lane);
-  layer<B16, V, E0 + 1, true>(p, A, emb, vemb, B, sb, g, lane);
-  layer<B16, V, E0 + 2, true>(p, B, emb, vemb, A, sb, g, lane);
-  layer<B16, V, E0 + 3, true>(p, A, emb, vemb, B, sb, g, lane);
-  layer<B16, V, E0 + 4, true>(p, B, emb, vemb, A, sb, g, lane);
-  layer<B16, V, E0 + 5, true>(p, A, emb, vemb, B, sb, g, lane);
-  layer<B16, V, E0 + 6, true>(p, B, emb, vemb, A, sb, g, lane);
-  layer<B16, V, E0 + 7, true>(p, A, emb, vemb, B, sb, g, lane);
-  layer<B16, V, E0 + 8, false>(p, B, emb, vemb, fc, sb, g, lane);
+  layer<B16, V, E0 + 1, true, true>(p, A, emb, vemb, B, sb, g, lane);
+  layer<B16, V, E0 + 2, true, true>(p, B, emb, vemb, A, sb, g, lane);
+  layer<B16, V, E0 + 3, true, true>(p, A, emb, vemb, B, sb, g, lane);
+  layer<B16, V, E0 + 4, true, true>(p, B, emb, vemb, A, sb, g, lane);
+  layer<B16, V, E0 + 5, true, true>(p, A, emb, vemb, B, sb, g, lane);
+  layer<B16, V, E0 + 6, true, true>(p, B, emb, vemb, A, sb, g, lane);
+  layer<B16, V, E0 + 7, true, true>(p, A, emb, vemb, B, sb, g, lane);
+  layer<B16, V, E0 + 8, false, true>(p, B, emb, vemb, fc, sb, g, lane);
 }
 
 template <bool B16>
@@ -720,24 +910,26 @@ __device__ __forceinline__ void mlp_body(const MlpArgs& a) {
     // ---- canonical NeRF (TPoseHuman.calculate_alpha_rgb)
     f32x4 dummy[1];
     layer<B16, V, 18, true>(p, dummy, emb, vemb, A, sb, g, lane);
-    layer<B16, V, 19, true>(p, A, emb, vemb, B, sb, g, lane);
-    layer<B16, V, 20, true>(p, B, emb, vemb, A, sb, g, lane);
-    layer<B16, V, 21, true>(p, A, emb, vemb, B, sb, g, lane);
-    layer<B16, V, 22, true>(p, B, emb, vemb, A, sb, g, lane);
-    layer<B16, V, 23, true>(p, A, emb, vemb, B, sb, g, lane);
-    layer<B16, V, 24, true>(p, B, emb, vemb, A, sb, g, lane);
-    layer<B16, V, 25, true>(p, A, emb, vemb, B, sb, g, lane);
+    layer<B16, V, 19, true, true>(p, A, emb, vemb, B, sb, g, lane);
+    layer<B16, V, 20, true, true>(p, B, emb, vemb, A, sb, g, lane);
+    layer<B16, V, 21, true, true>(p, A, emb, vemb, B, sb, g, lane);
+    layer<B16, V, 22, true, true>(p, B, emb, vemb, A, sb, g, lane);
+    layer<B16, V, 23, true, true>(p, A, emb, vemb, B, sb, g, lane);
+    layer<B16, V, 24, true, true>(p, B, emb, vemb, A, sb, g, lane);
+    layer<B16, V, 25, true, true>(p, A, emb, vemb, B, sb, g, lane);
     float sigma_raw;
     if constexpr (V == 2) {
       embed_b<1>(dir, g, 4, vemb);
-      layer<B16, V, 26, false>(p, B, emb, vemb, A, sb, g, lane);  // view_fc pre-activation || alpha
+      layer<B16, V, 26, false, true>(p, B, emb, vemb, A, sb, g, lane);  // view_fc pre-activation || alpha
       sigma_raw = __shfl(A[8][0], pl);
-      static_for<0, 8>([&](auto ob) {
-        constexpr int o = decltype(ob)::value;
+      if constexpr (!x3_stream_layer<ANR_L_RGB>()) {  // else rgb_fc applies view_fc's ReLU in its split
+        static_for<0, 8>([&](auto ob) {
+          constexpr int o = decltype(ob)::value;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) A[o][r] = fmaxf(A[o][r], 0.0f);
-      });
-      layer<B16, V, 27, false>(p, A, emb, vemb, B, sb, g, lane);  // rgb_fc
+          for (int r = 0; r < 4; ++r) A[o][r] = fmaxf(A[o][r], 0.0f);
+        });
+      }
+      layer<B16, V, 27, false, true>(p, A, emb, vemb, B, sb, g, lane);  // rgb_fc
     } else {
       layer<B16, V, 26, false>(p, B, emb, vemb, A, sb, g, lane);  // feature || alpha
       sigma_raw = __shfl(A[16][0], pl);
@@ -815,14 +1007,14 @@ __device__ __forceinline__ void alpha_body(const MlpArgs& a) {
     else embed<16>(xt, g, 10, emb);
     f32x4 dummy[1];
     layer<B16, V, 9, true>(p, dummy, emb, vemb, A, sb, g, lane);
-    layer<B16, V, 10, true>(p, A, emb, vemb, B, sb, g, lane);
-    layer<B16, V, 11, true>(p, B, emb, vemb, A, sb, g, lane);
-    layer<B16, V, 12, true>(p, A, emb, vemb, B, sb, g, lane);
-    layer<B16, V, 13, true>(p, B, emb, vemb, A, sb, g, lane);
-    layer<B16, V, 14, true>(p, A, emb, vemb, B, sb, g, lane);
-    layer<B16, V, 15, true>(p, B, emb, vemb, A, sb, g, lane);
-    layer<B16, V, 16, true>(p, A, emb, vemb, B, sb, g, lane);
-    layer<B16, V, 17, false>(p, B, emb, vemb, A, sb, g, lane);  // alpha_fc
+    layer<B16, V, 10, true, true>(p, A, emb, vemb, B, sb, g, lane);
+    layer<B16, V, 11, true, true>(p, B, emb, vemb, A, sb, g, lane);
+    layer<B16, V, 12, true, true>(p, A, emb, vemb, B, sb, g, lane);
+    layer<B16, V, 13, true, true>(p, B, emb, vemb, A, sb, g, lane);
+    layer<B16, V, 14, true, true>(p, A, emb, vemb, B, sb, g, lane);
+    layer<B16, V, 15, true, true>(p, B, emb, vemb, A, sb, g, lane);
+    layer<B16, V, 16, true, true>(p, A, emb, vemb, B, sb, g, lane);
+    layer<B16, V, 17, false, true>(p, B, emb, vemb, A, sb, g, lane);  // alpha_fc
     if (valid && g == 0) a.alpha_out[pid] = A[0][0];
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the last (unused) prefetch
