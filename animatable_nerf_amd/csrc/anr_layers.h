@@ -197,6 +197,23 @@ __host__ __device__ constexpr int x6_bytes() { return x6_layer_offset(ANR_X6_LAY
 __host__ __device__ constexpr int x6_base() { return (b16_base() + b16_bytes() + 255) / 256 * 256; }
 #define ANR_X6_NOVEL_WOFF (x6_layer_offset(9) - x6_layer_offset(0))
 
+// Gamma features in the bf16 image (EMB / VEMB segments of NS k-steps): element pairs (2p, 2p+1) of
+// lane half h in k-step t hold (sin, cos) of one argument x[comp] * 2^freq, so a lane evaluates one
+// shared-reduction sincos per pair (anr_mlp_body.h embed_b). Pair slot u = 4 NS h + 4 t + p: slots
+// 0 and 1 hold x, y, z and a zero pad; slot u >= 2 holds pair P = u - 2 = 3 freq + comp (zero past
+// 3 nfreq). Reference feature order (embedder.py:5-54): [x, sin(2^0 x), cos(2^0 x), sin(2^1 x), ...].
+__host__ __device__ constexpr int gamma_slot_feature(int ns, int nfreq, int t, int h, int j) {
+  const int u = 4 * ns * h + 4 * t + (j >> 1);
+  if (u < 2) {
+    const int f = 2 * u + (j & 1);
+    return f < 3 ? f : -1;
+  }
+  const int P = u - 2;
+  if (P >= 3 * nfreq) return -1;
+  const int freq = P / 3, comp = P - 3 * freq;
+  return 3 + 6 * freq + 3 * (j & 1) + comp;
+}
+
 // weight column for bf16 k-step t, lane half h, element j (-1 = padding)
 __host__ __device__ inline int b16_col(const LayerDesc& d, int t, int h, int j) {
   int s = 0;
@@ -206,9 +223,8 @@ __host__ __device__ inline int b16_col(const LayerDesc& d, int t, int h, int j) 
   }
   const Seg sg = d.seg[s];
   if (sg.kind == SRC_ACT) return sg.col0 + 32 * t + (j < 4 ? 4 * h + j : 16 + 4 * h + j - 4);
-  const int f = 32 * t + 8 * h + j;
-  const int nf = (sg.kind == SRC_EMB) ? 63 : 27;
-  return f < nf ? sg.col0 + f : -1;
+  const int f = gamma_slot_feature(sg.ksteps / 8, sg.kind == SRC_EMB ? 10 : 4, t, h, j);
+  return f >= 0 ? sg.col0 + f : -1;
 }
 
 // folded-head region (k_pack_head): H (129 x 283 f32), P = Wv_f Wl_l (128 x 128 f32), q (128 f32),

@@ -658,39 +658,65 @@ __device__ __forceinline__ void layer(Pipe& p, const f32x4 (&in)[NIN], const flo
   }
 }
 
-// gamma(x) in the bf16 fragment layout: e[8s + j] = feature 32s + 8h + j (embedder.py:5-54)
+// sin and cos of x sharing one Cody-Waite reduction (three-constant FMA split of pi/2, accurate for
+// |x| <= 1e5) and cephes' minimax polynomials on [-pi/4, pi/4]: <= 1.5 ulp, 7e-8 absolute (checked
+// against float64 over |x| <= 5e4). Branch-free; embed_b keeps larger arguments on the library path.
+__device__ __forceinline__ void sincos_fast(float x, float& s, float& c) {
+  const float k = __builtin_rintf(x * 0.636619772367581343f);
+  float r = __builtin_fmaf(-k, 1.57079601287841796875f, x);      // 0x1.921fb0p+0
+  r = __builtin_fmaf(-k, 3.1391647326017846e-07f, r);             // 0x1.5110b4p-22
+  r = __builtin_fmaf(-k, 5.3903025299577648e-15f, r);             // 0x1.846988p-48
+  const float z = r * r;
+  float ps = __builtin_fmaf(z, -1.9515295891e-4f, 8.3321608736e-3f);
+  ps = __builtin_fmaf(ps, z, -1.6666654611e-1f);
+  const float sn = __builtin_fmaf(ps * z, r, r);
+  float pc = __builtin_fmaf(z, 2.443315711809948e-5f, -1.388731625493765e-3f);
+  pc = __builtin_fmaf(pc, z, 4.166664568298827e-2f);
+  pc = __builtin_fmaf(pc, z, -0.5f);
+  const float cs = __builtin_fmaf(pc, z, 1.0f);
+  const int q = (int)k;
+  const float s0 = (q & 1) ? cs : sn, c0 = (q & 1) ? sn : cs;
+  s = (q & 2) ? -s0 : s0;
+  c = ((q + 1) & 2) ? -c0 : c0;
+}
+
+// gamma(x) in the bf16 fragment layout (anr_layers.h gamma_slot_feature): e[8s + 2p], e[8s + 2p + 1]
+// = sin, cos of pair P = 4 NS h + 4 s + p - 2 (x, y, z, 0 in the first two slots of lane half 0)
 template <int NS>
 __device__ __forceinline__ void embed_b(const float x[3], int h, int nfreq, float (&e)[8 * NS]) {
-  // launder the lane half: otherwise the per-lane frequency scales and component selects of all
-  // 8*NS features are hoisted out of the tile loop and pin ~30 registers for the whole kernel
+  // launder the lane half: otherwise the per-lane pair indices of all slots are hoisted out of the
+  // tile loop and pin registers for the whole kernel
   asm volatile("" : "+v"(h));
 #ifdef ANR_EXP_NOSTRETCH
 #pragma unroll
   for (int k = 0; k < 8 * NS; ++k) e[k] = x[k % 3] * (0.1f + 0.01f * k);  // timing experiment only
   return;
 #endif
+  const float m = fmaxf(fabsf(x[0]), fmaxf(fabsf(x[1]), fabsf(x[2])));
+  // any lane with arguments past the fast reduction's range takes the library sincos (wave-uniform)
+  const bool slow = __builtin_amdgcn_ballot_w64(!(m * (float)(1 << (nfreq - 1)) <= 65536.0f)) != 0;
+  const int hb = 4 * NS * h - 2;
 #pragma unroll
   for (int s = 0; s < NS; ++s)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int f = 32 * s + 8 * h + j;
-      float v;
-      if (f < 3) {
-        v = x[f == 0 ? 0 : (f == 1 ? 1 : 2)];
-      } else {
-        const int q = f - 3;
-        const int freq = q / 6;
-        const int w = q - freq * 6;
-        const int comp = w >= 3 ? w - 3 : w;
-        const float xc = comp == 0 ? x[0] : (comp == 1 ? x[1] : x[2]);
-        const float arg = xc * (float)(1 << (freq < 15 ? freq : 0));
-#ifdef ANR_EXP_FASTSIN
-        v = freq >= nfreq ? 0.0f : (w >= 3 ? __cosf(arg) : __sinf(arg));  // timing experiment only
-#else
-        v = freq >= nfreq ? 0.0f : (w >= 3 ? cosf(arg) : sinf(arg));
-#endif
+    for (int p = 0; p < 4; ++p) {
+      const int P = hb + 4 * s + p;        // pair index (< 0: the raw slots of lane half 0)
+      const int freq = (P * 11) >> 5;      // P / 3 for 0 <= P < 30
+      const int comp = P - 3 * freq;
+      const float xc = comp == 0 ? x[0] : (comp == 1 ? x[1] : x[2]);
+      const float arg = __builtin_ldexpf(xc, freq);
+      float sv, cv;
+      if (!slow) sincos_fast(arg, sv, cv);
+      else sincosf(arg, &sv, &cv);
+      const bool valid = (unsigned)P < (unsigned)(3 * nfreq);
+      float v0 = valid ? sv : 0.0f, v1 = valid ? cv : 0.0f;
+      if (s == 0 && p < 2) {  // lane half 0: x, y | z, 0
+        const bool raw = h == 0;
+        v0 = raw ? x[2 * p] : v0;
+        v1 = raw ? (p == 0 ? x[1] : 0.0f) : v1;
       }
-      e[8 * s + j] = v;
+      e[8 * s + 2 * p] = v0;
+      e[8 * s + 2 * p + 1] = v1;
     }
 }
 
