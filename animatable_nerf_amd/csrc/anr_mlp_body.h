@@ -51,6 +51,19 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 #ifndef ANR_DMA_SPREAD
 #define ANR_DMA_SPREAD 1
 #endif
+// LDS-DMA source as scalar base + constant lane offset (global_load_lds saddr form)
+#ifndef ANR_DMA_SADDR
+#define ANR_DMA_SADDR 1
+#endif
+// outputs (raw, sigma', pbw/tbw rows) stored non-temporal, keeping them out of the L2 the weight
+// stream lives in
+#ifndef ANR_NT_OUT
+#define ANR_NT_OUT 0
+#endif
+// slice certification by a raw s_barrier instead of __syncthreads() (whose fence waits lgkmcnt(0))
+#ifndef ANR_RAW_BARRIER
+#define ANR_RAW_BARRIER 0
+#endif
 
 // The per-tile layer program, variant V:
 //   V = 0 (render): entries 0..8 the pose-space BW MLP, 9..17 the T-pose BW MLP (layers 0..8
@@ -182,10 +195,19 @@ struct Pipe {
     for (int i = first; i < loads; ++i) {
       int piece = wave + ANR_DMA_WAVES * i;
       piece = piece < kb ? piece : kb - 1;
-      const unsigned char* src = w + off + piece * 1024 + lane * 16;
       const unsigned m0 = dst + piece * 1024;
+#if ANR_DMA_SADDR
+      // wave-uniform piece: the whole source offset in the scalar base, the lane's 16 B in a
+      // constant VGPR (no per-piece vector address arithmetic)
+      const unsigned char* sbase = w + off + piece * 1024;
+      asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(lane * 16), "s"(sbase),
+                   "s"(m0)
+                   : "memory");
+#else
+      const unsigned char* src = w + off + piece * 1024 + lane * 16;
       asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(m0)
                    : "memory");
+#endif
     }
   }
 
@@ -248,9 +270,17 @@ struct Pipe {
       constexpr int NB = mlp_nbuf<B16>();
       constexpr int e1 = prog_advance<B16, V>(E, Q, 1);
       constexpr int eq = prog_advance<B16, V>(E, Q, NB - 1);
+#ifndef ANR_EXP_NOWAIT
       wait_stream<prog_later_loads<B16, V>(e1 / 1024, e1 % 1024)>();
+#endif
 #ifndef ANR_EXP_NOBAR
+#if ANR_RAW_BARRIER
+      // raw barrier: no fence, so fragment reads still in flight (this slice's, out-blocks ahead)
+      // survive it; every read of the slot refilled next was consumed by the previous slice's MFMAs
+      __builtin_amdgcn_s_barrier();
+#else
       __syncthreads();
+#endif
 #endif
       int slot = cur + NB - 1;
       slot = slot >= NB ? slot - NB : slot;
@@ -855,8 +885,13 @@ __device__ __forceinline__ void lbs_inverse(const f32x4 (&bw)[2], const float* _
 
 __device__ __forceinline__ void store_rows(float* __restrict__ rows, int idx, const f32x4 (&bw)[2], int g, bool valid) {
   if (!valid) return;
+#if ANR_NT_OUT
+  __builtin_nontemporal_store(bw[0], (f32x4*)(rows + (size_t)idx * 24 + 4 * g));
+  if (g < 2) __builtin_nontemporal_store(bw[1], (f32x4*)(rows + (size_t)idx * 24 + 16 + 4 * g));
+#else
   *(f32x4*)(rows + (size_t)idx * 24 + 4 * g) = bw[0];
   if (g < 2) *(f32x4*)(rows + (size_t)idx * 24 + 16 + 4 * g) = bw[1];
+#endif
 }
 
 // BW MLP pass starting at program entry E0 (0: pose pass; 9: T-pose pass). The pose pass may read
@@ -977,8 +1012,13 @@ __device__ __forceinline__ void mlp_body(const MlpArgs& a) {
       r.y = 1.0f / (1.0f + expf(-B[0][1]));
       r.z = 1.0f / (1.0f + expf(-B[0][2]));
       r.w = 1.0f - expf(-fmaxf(sig, 0.0f) * dist);
+#if ANR_NT_OUT
+      __builtin_nontemporal_store(f32x4{r.x, r.y, r.z, r.w}, (f32x4*)(a.raw + pid));
+      __builtin_nontemporal_store(sig, a.sigma + idx);
+#else
       a.raw[pid] = r;
       a.sigma[idx] = sig;
+#endif
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the last (unused) prefetch
