@@ -79,6 +79,7 @@ int stage_frontend(const anr_params* p, const anr_frame* f, const float* ray_o, 
   pa.bw_latent = p->t[27]; pa.w_lat = p->t[21]; pa.b_lat = p->t[22]; pa.nf_latent = p->t[0];
   pa.latent_index = f->latent_index;
   pa.fold = (float*)(ws + L.fold);
+  pa.pn24 = (float*)(ws + L.pn24);
   if (p->packed) {  // the bf16x3 program's folded head (anr_layers.h ANR_L_HEAD)
     const float* head = (const float*)((const unsigned char*)p->packed + head_base());
     pa.head_P = head + ANR_HEAD_P_OFF;
@@ -100,6 +101,7 @@ int stage_frontend(const anr_params* p, const anr_frame* f, const float* ray_o, 
   fa.ray_o = ray_o; fa.ray_d = ray_d; fa.near_ = near_; fa.far_ = far_; fa.t_rand = o->t_rand;
   fa.n_rays = R; fa.chunk = o->chunk;
   fa.R = f->R; fa.Th = f->Th; fa.pbw = f->pbw; fa.pbounds = f->pbounds;
+  fa.pn24 = pa.pn24;
   fa.X = f->pbw_dims[0]; fa.Y = f->pbw_dims[1]; fa.Z = f->pbw_dims[2];
   fa.norm_th = o->norm_th;
   fa.mask = (uint64_t*)(ws + L.mask);
@@ -110,7 +112,7 @@ int stage_frontend(const anr_params* p, const anr_frame* f, const float* ray_o, 
   fa.img_h = f->img_h; fa.img_w = f->img_w;
   if (f->n_views < 0 || (f->n_views > 0 && (!f->Ks || !f->RT || !f->msks || f->img_h <= 0 || f->img_w <= 0)))
     return fail(ANR_E_ARG, "render: bad visibility-filter views");
-  hipLaunchKernelGGL(k_frontend, dim3((R + 3) / 4), dim3(256), 0, s, fa);
+  hipLaunchKernelGGL(k_frontend, dim3((R + 15) / 16), dim3(1024), 0, s, fa);
   ANR_TRY(check_launch("k_frontend"));
 
   CompactArgs ca{};

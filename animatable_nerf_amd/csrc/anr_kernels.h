@@ -23,6 +23,7 @@ struct FrontArgs {
   const float* wpts;     // (n_pts, 3) world points
   long n_pts;
   int chunk_pts;
+  const float* pn24;     // channel 24 of pbw as a compact (X,Y,Z) array (k_prep), or NULL: read pbw
 };
 
 struct CompactArgs {
@@ -121,6 +122,7 @@ struct PrepArgs {
   // folded colour head (anr_layers.h ANR_L_HEAD): fold[ANR_FOLD_HEAD + i] = P nf_latent[li] + q, row 128
   // = alpha_fc's bias; skipped when head_P is NULL (callers without the bf16x3 render program)
   const float *head_P, *head_q, *b_alpha;
+  float* pn24;  // (np) channel 24 of pbw, compact, for the front-end's prefilter lookups (or NULL)
 };
 
 __global__ void k_near_far(const float*, const float*, int, const float*, uint8_t*, float*, float*);

@@ -201,7 +201,9 @@ __global__ __launch_bounds__(256) void k_prep(PrepArgs a) {
     const int v = blockIdx.x * 8 + (threadIdx.x >> 5);
     const int c = threadIdx.x & 31;
     if (v < a.np) {
-      a.pbw32[(size_t)v * 32 + c] = c < 25 ? a.pbw[(size_t)v * 25 + c] : 0.0f;
+      const float val = c < 25 ? a.pbw[(size_t)v * 25 + c] : 0.0f;
+      a.pbw32[(size_t)v * 32 + c] = val;
+      if (c == 24 && a.pn24) a.pn24[v] = val;
     } else if (v < a.np + a.nt) {
       const int u = v - a.np;
       a.tbw32[(size_t)u * 32 + c] = c < 25 ? a.tbw[(size_t)u * 25 + c] : 0.0f;

@@ -266,49 +266,72 @@ __global__ __launch_bounds__(1024) void k_trl_gather(TrainRayArgs a) {
 // ------------------------------------------------------------------------------------------
 // A4-A6 front-end: one wave per ray, lane = sample.
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_frontend(FrontArgs a) {
+// One wave per ray (lane = sample), 16 rays per 1024-thread block. The prefilter lookup reads the
+// compact channel-24 copy of pbw (4 B per voxel, k_prep): the 8 corners of a sample share lines
+// and the whole array stays L2-resident. Per-chunk argmin keys are reduced inside the block first
+// (one atomic per chunk present in the block instead of one per ray).
+__global__ __launch_bounds__(1024) void k_frontend(FrontArgs a) {
+  __shared__ uint64_t skey[16];
+  __shared__ int schunk[16];
   const int lane = threadIdx.x & 63;
-  const int ray = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (ray >= a.n_rays) return;
-  float z, dist, pts[3], pose[3];
-  sample_point(a.ray_o, a.ray_d, a.near_, a.far_, a.t_rand, ray, lane, 64, z, dist, pts);
-  world_to_pose(pts, a.R, a.Th, pose);
-  float lo[3], hi[3];
+  const int w = threadIdx.x >> 6;
+  const int ray = blockIdx.x * 16 + w;
+  const bool live = ray < a.n_rays;
+  uint64_t key = ~0ull;
+  if (live) {
+    float z, dist, pts[3], pose[3];
+    sample_point(a.ray_o, a.ray_d, a.near_, a.far_, a.t_rand, ray, lane, 64, z, dist, pts);
+    world_to_pose(pts, a.R, a.Th, pose);
+    float lo[3], hi[3];
 #pragma unroll
-  for (int c = 0; c < 3; ++c) { lo[c] = a.pbounds[c]; hi[c] = a.pbounds[3 + c]; }
-  TriCell cell;
-  tri_cell(pose, lo, hi, a.X, a.Y, a.Z, cell);
-  const float pn = tri_channel(a.pbw, 25, 24, cell);
-  // novel-view filter (tpose_renderer_mmsk.py:14-57): world point -> every training view, rounded
-  // half-to-even, clamped, looked up in its mask; the network then sees only visible samples, so
-  // the per-chunk argmin runs over them (a chunk with none keeps nothing)
-  bool vis = true;
-  for (int v = 0; v < a.n_views; ++v) {
-    const float* R = a.RT + 12 * v;
-    const float* K = a.Ks + 9 * v;
-    float q[3], s3[3];
-    for (int j = 0; j < 3; ++j) q[j] = fmaf(pts[2], R[4 * j + 2], fmaf(pts[1], R[4 * j + 1], pts[0] * R[4 * j])) + R[4 * j + 3];
-    for (int j = 0; j < 3; ++j) s3[j] = fmaf(q[2], K[3 * j + 2], fmaf(q[1], K[3 * j + 1], q[0] * K[3 * j]));
-    long long xi = (long long)rintf(s3[0] / s3[2]);
-    long long yi = (long long)rintf(s3[1] / s3[2]);
-    xi = xi < 0 ? 0 : (xi > a.img_w - 1 ? a.img_w - 1 : xi);
-    yi = yi < 0 ? 0 : (yi > a.img_h - 1 ? a.img_h - 1 : yi);
-    vis = vis && a.msks[((size_t)v * a.img_h + yi) * a.img_w + xi] != 0;
-  }
-  const bool keep = vis && pn < a.norm_th;
-  const uint64_t m = __ballot(keep);
-  if (lane == 0) a.mask[ray] = m;
-  if (a.raw != nullptr && !keep) a.raw[(size_t)ray * 64 + lane] = make_float4(0.f, 0.f, 0.f, 0.f);
-  // per-chunk argmin of pnorm over the visible samples (first index on ties):
-  // key = bits(pn) << 32 | index-in-chunk
-  const int rc = ray % a.chunk;
-  uint64_t key = vis ? (((uint64_t)__float_as_uint(pn) << 32) | (uint32_t)(rc * 64 + lane)) : ~0ull;
+    for (int c = 0; c < 3; ++c) { lo[c] = a.pbounds[c]; hi[c] = a.pbounds[3 + c]; }
+    TriCell cell;
+    tri_cell(pose, lo, hi, a.X, a.Y, a.Z, cell);
+    const float pn = a.pn24 ? tri_channel(a.pn24, 1, 0, cell) : tri_channel(a.pbw, 25, 24, cell);
+    // novel-view filter (tpose_renderer_mmsk.py:14-57): world point -> every training view, rounded
+    // half-to-even, clamped, looked up in its mask; the network then sees only visible samples, so
+    // the per-chunk argmin runs over them (a chunk with none keeps nothing)
+    bool vis = true;
+    for (int v = 0; v < a.n_views; ++v) {
+      const float* R = a.RT + 12 * v;
+      const float* K = a.Ks + 9 * v;
+      float q[3], s3[3];
+      for (int j = 0; j < 3; ++j) q[j] = fmaf(pts[2], R[4 * j + 2], fmaf(pts[1], R[4 * j + 1], pts[0] * R[4 * j])) + R[4 * j + 3];
+      for (int j = 0; j < 3; ++j) s3[j] = fmaf(q[2], K[3 * j + 2], fmaf(q[1], K[3 * j + 1], q[0] * K[3 * j]));
+      long long xi = (long long)rintf(s3[0] / s3[2]);
+      long long yi = (long long)rintf(s3[1] / s3[2]);
+      xi = xi < 0 ? 0 : (xi > a.img_w - 1 ? a.img_w - 1 : xi);
+      yi = yi < 0 ? 0 : (yi > a.img_h - 1 ? a.img_h - 1 : yi);
+      vis = vis && a.msks[((size_t)v * a.img_h + yi) * a.img_w + xi] != 0;
+    }
+    const bool keep = vis && pn < a.norm_th;
+    const uint64_t m = __ballot(keep);
+    if (lane == 0) a.mask[ray] = m;
+    if (a.raw != nullptr && !keep) a.raw[(size_t)ray * 64 + lane] = make_float4(0.f, 0.f, 0.f, 0.f);
+    // per-chunk argmin of pnorm over the visible samples (first index on ties):
+    // key = bits(pn) << 32 | index-in-chunk
+    const int rc = ray % a.chunk;
+    key = vis ? (((uint64_t)__float_as_uint(pn) << 32) | (uint32_t)(rc * 64 + lane)) : ~0ull;
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    const uint64_t o = __shfl_xor(key, off);
-    key = o < key ? o : key;
+    for (int off = 32; off > 0; off >>= 1) {
+      const uint64_t o = __shfl_xor(key, off);
+      key = o < key ? o : key;
+    }
   }
-  if (lane == 0) atomicMin((unsigned long long*)&a.chunk_min[ray / a.chunk], (unsigned long long)key);
+  if (lane == 0) {
+    skey[w] = key;
+    schunk[w] = live ? ray / a.chunk : -1;
+  }
+  __syncthreads();
+  // one thread per run of equal chunk ids: min over the run, one atomic
+  if (threadIdx.x < 16) {
+    const int c = schunk[threadIdx.x];
+    if (c >= 0 && (threadIdx.x == 0 || schunk[threadIdx.x - 1] != c)) {
+      uint64_t k = skey[threadIdx.x];
+      for (int j = threadIdx.x + 1; j < 16 && schunk[j] == c; ++j) k = skey[j] < k ? skey[j] : k;
+      if (k != ~0ull) atomicMin((unsigned long long*)&a.chunk_min[c], (unsigned long long)k);
+    }
+  }
 }
 
 // (f) mesh path: the prefilter of get_alpha over free points (tpose_nerf_network.py:105-116):

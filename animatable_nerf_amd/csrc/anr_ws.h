@@ -15,7 +15,7 @@ inline size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
 // Workspace layout. Fields up to `tbw_rows` depend only on n_rays (anr_render_counts/bw_rows).
 struct Layout {
   size_t counts, mask, ray_off, block_sum, list, sigma, flags, block_sum2, out_row, pbw_rows, tbw_rows;
-  size_t chunk_min, chunk_max, raw, pbw32, tbw32, fold, total;
+  size_t chunk_min, chunk_max, raw, pbw32, tbw32, pn24, fold, total;
 };
 
 inline Layout layout(int n_rays, int chunk, long np, long nt, bool need_raw) {
@@ -44,6 +44,7 @@ inline Layout layout(int n_rays, int chunk, long np, long nt, bool need_raw) {
   L.raw = need_raw ? take(N * 16) : 0;
   L.pbw32 = take((size_t)np * 32 * 4);
   L.tbw32 = take((size_t)nt * 32 * 4);
+  L.pn24 = take((size_t)np * 4);
   L.fold = take(ANR_FOLD_FLOATS * 4);
   L.total = o;
   return L;
