@@ -32,6 +32,9 @@ __device__ __forceinline__ float grid_src(float g, int size) {
   return fminf((float)(size - 1), fmaxf(c, 0.0f));
 }
 
+// corner offsets and weights from the unnormalised source coordinates (ix along Z, iy along Y, iz along X)
+__device__ __forceinline__ void tri_cell_src(float ix, float iy, float iz, int X, int Y, int Z, TriCell& t);
+
 // p: point in the volume's frame; lo/hi: bounds (2,3); dims X,Y,Z.
 __device__ __forceinline__ void tri_cell(const float p[3], const float lo[3], const float hi[3],
                                          int X, int Y, int Z, TriCell& t) {
@@ -43,9 +46,11 @@ __device__ __forceinline__ void tri_cell(const float p[3], const float lo[3], co
     float v = (p[c] - lo[c]) / ext;
     g[c] = v * 2.0f - 1.0f;
   }
-  const float ix = grid_src(g[2], Z);
-  const float iy = grid_src(g[1], Y);
-  const float iz = grid_src(g[0], X);
+  tri_cell_src(grid_src(g[2], Z), grid_src(g[1], Y), grid_src(g[0], X), X, Y, Z, t);
+}
+
+__device__ __forceinline__ void tri_cell_src(float ix, float iy, float iz, int X, int Y, int Z, TriCell& t) {
+#pragma clang fp contract(off)
   const int x0 = (int)floorf(ix), y0 = (int)floorf(iy), z0 = (int)floorf(iz);
   const int x1 = x0 + 1, y1 = y0 + 1, z1 = z0 + 1;
   const float fx0 = (float)x0, fy0 = (float)y0, fz0 = (float)z0;

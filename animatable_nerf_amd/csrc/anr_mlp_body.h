@@ -43,7 +43,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 #endif
 // LDS fragment reads in flight ahead of the MFMAs (bf16x3 layers)
 #ifndef ANR_FRAG_PF
-#define ANR_FRAG_PF 2
+#define ANR_FRAG_PF 3
 #endif
 // bf16x3 layers: issue a refill's LDS-DMA pieces one by one between the out-blocks of the slice's
 // second half (after its mid() barrier) instead of as one burst right after the barrier, where every
@@ -55,10 +55,25 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 #ifndef ANR_DMA_SADDR
 #define ANR_DMA_SADDR 1
 #endif
+// cache policy bits of the weight-stream LDS-DMA (e.g. " nt"); default policy
+#ifndef ANR_DMA_CPOL_ID
+#define ANR_DMA_CPOL_ID 0
+#endif
+#if ANR_DMA_CPOL_ID == 1
+#define ANR_DMA_CPOL " nt"
+#elif ANR_DMA_CPOL_ID == 2
+#define ANR_DMA_CPOL " sc1"
+#else
+#define ANR_DMA_CPOL ""
+#endif
 // outputs (raw, sigma', pbw/tbw rows) stored non-temporal, keeping them out of the L2 the weight
 // stream lives in
 #ifndef ANR_NT_OUT
 #define ANR_NT_OUT 0
+#endif
+// bf16x3 kernels: hardware log/exp/rcp in the blend softmax and reciprocal-based lookup coordinates
+#ifndef ANR_FAST_MATH
+#define ANR_FAST_MATH 1
 #endif
 // slice certification by a raw s_barrier instead of __syncthreads() (whose fence waits lgkmcnt(0))
 #ifndef ANR_RAW_BARRIER
@@ -200,7 +215,7 @@ struct Pipe {
       // wave-uniform piece: the whole source offset in the scalar base, the lane's 16 B in a
       // constant VGPR (no per-piece vector address arithmetic)
       const unsigned char* sbase = w + off + piece * 1024;
-      asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(lane * 16), "s"(sbase),
+      asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ANR_DMA_CPOL ::"v"(lane * 16), "s"(sbase),
                    "s"(m0)
                    : "memory");
 #else
@@ -776,6 +791,9 @@ __device__ __forceinline__ void embed(const float x[3], int g, int nfreq, float 
 
 // 24-channel lookup from the 32-channel repacked volume, reference accumulation order.
 // block 0 -> channels 4g..4g+3, block 1 -> 16+4g..16+4g+3
+// FAST (bf16x3 kernels, whose outputs are held to the 1e-4 tolerance, not to the bits of init_pbw):
+// the normalised coordinate from one reciprocal per axis instead of an IEEE division.
+template <bool FAST = false>
 __device__ __forceinline__ void lookup24(const float* __restrict__ vol32, const float p[3], const float* __restrict__ bounds,
                                          int X, int Y, int Z, int g, f32x4 (&out)[2]) {
 #pragma clang fp contract(off)
@@ -790,7 +808,16 @@ __device__ __forceinline__ void lookup24(const float* __restrict__ vol32, const 
   return;
 #endif
   TriCell t;
-  tri_cell(p, lo, hi, X, Y, Z, t);
+  if constexpr (FAST) {
+    // (p - lo) / ext as (p - lo) * rcp(ext): within 1-2 ulp of the division
+    float gq[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) gq[c] = (p[c] - lo[c]) * __builtin_amdgcn_rcpf(hi[c] - lo[c]) * 2.0f - 1.0f;
+    const float ix = grid_src(gq[2], Z), iy = grid_src(gq[1], Y), iz = grid_src(gq[0], X);
+    tri_cell_src(ix, iy, iz, X, Y, Z, t);
+  } else {
+    tri_cell(p, lo, hi, X, Y, Z, t);
+  }
   f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
@@ -810,6 +837,9 @@ __device__ __forceinline__ void lookup24(const float* __restrict__ vol32, const 
 
 // softmax over 24 channels of log(init + 1e-9) + fc (tpose_nerf_network.py:74-76); lanes
 // l, l^16, l^32, l^48 hold one point's channels.
+// FAST (bf16x3 kernels): hardware log2/exp2 and one reciprocal instead of the library logf/expf and
+// eight divisions (relative error ~1e-6 on the weights, inside the 1e-4 output tolerance).
+template <bool FAST = false>
 __device__ __forceinline__ void blend_softmax(const f32x4 (&fc)[2], const f32x4 (&init)[2], int g, f32x4 (&bw)[2]) {
 #ifdef ANR_EXP_NOSTRETCH
   bw[0] = fc[0] * 0.01f + init[0];  // timing experiment only
@@ -823,7 +853,7 @@ __device__ __forceinline__ void blend_softmax(const f32x4 (&fc)[2], const f32x4 
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const bool valid = b == 0 || g < 2;
-      const float v = logf(init[b][r] + 1e-9f) + fc[b][r];
+      const float v = (FAST ? __logf(init[b][r] + 1e-9f) : logf(init[b][r] + 1e-9f)) + fc[b][r];
       lg[b][r] = valid ? v : -INFINITY;
       m = fmaxf(m, lg[b][r]);
     }
@@ -834,7 +864,7 @@ __device__ __forceinline__ void blend_softmax(const f32x4 (&fc)[2], const f32x4 
   for (int b = 0; b < 2; ++b)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      lg[b][r] = expf(lg[b][r] - m);
+      lg[b][r] = FAST ? __expf(lg[b][r] - m) : expf(lg[b][r] - m);
       s += lg[b][r];
     }
   s += __shfl_xor(s, 16);
@@ -842,7 +872,7 @@ __device__ __forceinline__ void blend_softmax(const f32x4 (&fc)[2], const f32x4 
 #pragma unroll
   for (int b = 0; b < 2; ++b)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) bw[b][r] = lg[b][r] / s;
+    for (int r = 0; r < 4; ++r) bw[b][r] = FAST ? lg[b][r] * __builtin_amdgcn_rcpf(s) : lg[b][r] / s;
 }
 
 // LBS inverse warp: A_b = sum_j bw_j A_j; x_T = inv(A_b[:3,:3]) (x - A_b[:3,3])
@@ -951,11 +981,11 @@ __device__ __forceinline__ void mlp_body(const MlpArgs& a) {
     // ---- pose space: pbw lookup, BW MLP (latent_index + 1), softmax, LBS
     if constexpr (B16) embed_b<2>(pose, g, 10, emb);
     else embed<16>(pose, g, 10, emb);
-    lookup24(a.pbw32, pose, a.pbounds, a.pX, a.pY, a.pZ, g, init);
+    lookup24<B16 && ANR_FAST_MATH>(a.pbw32, pose, a.pbounds, a.pX, a.pY, a.pZ, g, init);
 #pragma unroll
     for (int s8 = 0; s8 < 8; ++s8) vemb[s8] = 0.f;
     bw_mlp<B16, V, 0>(p, emb, vemb, sb, A, B, fc, g, lane);
-    blend_softmax(fc, init, g, bw);
+    blend_softmax<B16 && ANR_FAST_MATH>(fc, init, g, bw);
     store_rows(a.pbw_rows, idx, bw, g, valid);
     float xt[3];
     lbs_inverse(bw, sA, g, pose, xt);
@@ -963,9 +993,9 @@ __device__ __forceinline__ void mlp_body(const MlpArgs& a) {
     // ---- T-pose: tbw lookup, BW MLP (latent 0) -> tbw rows (training loss only)
     if constexpr (B16) embed_b<2>(xt, g, 10, emb);
     else embed<16>(xt, g, 10, emb);
-    lookup24(a.tbw32, xt, a.tbounds, a.tX, a.tY, a.tZ, g, init);
+    lookup24<B16 && ANR_FAST_MATH>(a.tbw32, xt, a.tbounds, a.tX, a.tY, a.tZ, g, init);
     bw_mlp<B16, V, 9>(p, emb, vemb, sb, A, B, fc, g, lane);
-    blend_softmax(fc, init, g, bw);
+    blend_softmax<B16 && ANR_FAST_MATH>(fc, init, g, bw);
     store_rows(a.tbw_rows, idx, bw, g, valid);
 
     // ---- canonical NeRF (TPoseHuman.calculate_alpha_rgb)
@@ -1061,11 +1091,11 @@ __device__ __forceinline__ void alpha_body(const MlpArgs& a) {
     f32x4 A[17], B[17], fc[2], init[2], bw[2];
     if constexpr (B16) embed_b<2>(pose, g, 10, emb);
     else embed<16>(pose, g, 10, emb);
-    lookup24(a.pbw32, pose, a.pbounds, a.pX, a.pY, a.pZ, g, init);
+    lookup24<B16 && ANR_FAST_MATH>(a.pbw32, pose, a.pbounds, a.pX, a.pY, a.pZ, g, init);
 #pragma unroll
     for (int s8 = 0; s8 < 8; ++s8) vemb[s8] = 0.f;
     bw_mlp<B16, V, 0>(p, emb, vemb, sb, A, B, fc, g, lane);
-    blend_softmax(fc, init, g, bw);
+    blend_softmax<B16 && ANR_FAST_MATH>(fc, init, g, bw);
     float xt[3];
     lbs_inverse(bw, sA, g, pose, xt);
 
