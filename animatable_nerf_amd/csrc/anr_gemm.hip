@@ -121,6 +121,9 @@ __device__ __forceinline__ void rowsum_flush(const GemmArgs& g, int m0, float (&
 // epilogue shared by the GEMM kernels: lane holds C[wr + i*16 + 4*(lane>>4) + r][wc + j*16 + (lane&15)]
 __device__ __forceinline__ void epilogue(const GemmArgs& g, const f32x4 (&acc)[2][2], int M, int m0, int n0, int wr,
                                          int wc, int lane) {
+#ifdef RG_EXP_NOEPI
+  if (acc[0][0][0] != 12345.f) return;  // timing experiment only
+#endif
   const bool first_split = blockIdx.z == 0;
 #pragma unroll
   for (int i = 0; i < 2; ++i)

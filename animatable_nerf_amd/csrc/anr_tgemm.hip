@@ -1,0 +1,551 @@
+// anr_tgemm.hip — the bf16 row GEMM of the training executor (precision 'bf16', config 3) for the two
+// products whose B operand is a layer's weight:
+//   forward  Y  = act(X W^T + b)          rows of W   (k = input column)
+//   backward dX = (dY W) * (H > 0)        rows of W^T (k = output neuron)
+// Weights are converted once per training call into bf16 images (k_wimg_pack) whose rows are
+// k-contiguous and padded to whole 64-wide K chunks (segments of a concatenated input start on a
+// chunk), so both products read B the same way. One workgroup (4 waves) owns 64 rows x up to 256
+// output columns; every K chunk of 64 is brought in by LDS-DMA — the activations as fp32 (16 KiB),
+// the weight rows as bf16 (32 KiB) — into a 3-slot ring with two chunks in flight behind counted
+// vmcnt waits, and each wave runs 4 x 4 v_mfma_f32_16x16x32_bf16 per 32-deep k-step (fp32
+// accumulation; the activations rounded to bf16 RNE as their fragments are read, as the generic
+// kernel rounds them at staging). LDS images are XOR-swizzled through the DMA source addresses.
+// Epilogue order as anr_gemm.hip: bias, accumulate, ReLU, mask.
+#include <vector>
+
+#include "anr_common.h"
+#include "anr_train.h"
+
+namespace anr {
+
+// ------------------------------------------------------------------------------------------
+// weight images
+// ------------------------------------------------------------------------------------------
+struct WDesc {
+  int t, n, in_ch, nseg, c0[2], k[2];
+};
+// the Conv1d weights the training GEMMs read (tensor index, out, in, used column segments)
+static const WDesc kWDesc[] = {
+    {28, 256, 191, 1, {0, 0}, {63, 0}},    {30, 256, 256, 1, {0, 0}, {256, 0}}, {32, 256, 256, 1, {0, 0}, {256, 0}},
+    {34, 256, 256, 1, {0, 0}, {256, 0}},   {36, 256, 256, 1, {0, 0}, {256, 0}}, {38, 256, 447, 2, {0, 191}, {63, 256}},
+    {40, 256, 256, 1, {0, 0}, {256, 0}},   {42, 256, 256, 1, {0, 0}, {256, 0}}, {44, 24, 256, 1, {0, 0}, {256, 0}},
+    {1, 256, 63, 1, {0, 0}, {63, 0}},      {3, 256, 256, 1, {0, 0}, {256, 0}},  {5, 256, 256, 1, {0, 0}, {256, 0}},
+    {7, 256, 256, 1, {0, 0}, {256, 0}},    {9, 256, 256, 1, {0, 0}, {256, 0}},  {11, 256, 319, 2, {0, 63}, {63, 256}},
+    {13, 256, 256, 1, {0, 0}, {256, 0}},   {15, 256, 256, 1, {0, 0}, {256, 0}}, {17, 1, 256, 1, {0, 0}, {256, 0}},
+    {19, 256, 256, 1, {0, 0}, {256, 0}},   {21, 256, 384, 1, {0, 0}, {256, 0}}, {23, 128, 283, 2, {0, 256}, {256, 27}},
+    {25, 3, 128, 1, {0, 0}, {128, 0}},
+};
+constexpr int kNW = sizeof(kWDesc) / sizeof(kWDesc[0]);
+
+static int rup64(int v) { return (v + 63) / 64 * 64; }
+
+struct WPackJob {
+  const float* W;
+  int n, in_ch, ld, bwd;  // bwd: transposed image (rows = input columns)
+  int c0[2], k[2], col[2], nseg;
+  long start, dst;        // first element (flat) and destination offset (elements)
+};
+struct WPackArgs {
+  WPackJob job[2 * kNW];
+  int njob;
+  long total;
+  unsigned short* out;
+};
+
+__device__ __forceinline__ unsigned short f2bf_rne(float f) {
+  uint32_t u = __float_as_uint(f);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (unsigned short)(u >> 16);
+}
+
+__global__ void k_wimg_pack(WPackArgs a) {
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= a.total) return;
+  int j = 0;
+  while (j + 1 < a.njob && e >= a.job[j + 1].start) ++j;
+  const WPackJob& J = a.job[j];
+  const long local = e - J.start;
+  const int row = (int)(local / J.ld), col = (int)(local - (long)row * J.ld);
+  float v = 0.0f;
+  if (J.bwd) {
+    // row = input column c, col = output neuron
+    if (col < J.n) v = J.W[(long)col * J.in_ch + row];
+  } else {
+    for (int s = 0; s < J.nseg; ++s)
+      if (col >= J.col[s] && col < J.col[s] + J.k[s]) v = J.W[(long)row * J.in_ch + J.c0[s] + col - J.col[s]];
+  }
+  a.out[J.dst + local] = f2bf_rne(v);
+}
+
+// layout of the images: per descriptor a forward image (n rows x sum of 64-padded segments) and a
+// backward image (in_ch rows x 64-padded n)
+static long wimg_layout(std::vector<WPackJob>* jobs) {
+  long off = 0, start = 0;
+  for (int i = 0; i < kNW; ++i) {
+    const WDesc& d = kWDesc[i];
+    WPackJob f{};
+    f.n = d.n; f.in_ch = d.in_ch; f.nseg = d.nseg; f.bwd = 0;
+    int ld = 0;
+    for (int s = 0; s < d.nseg; ++s) {
+      f.c0[s] = d.c0[s]; f.k[s] = d.k[s]; f.col[s] = ld;
+      ld += rup64(d.k[s]);
+    }
+    f.ld = ld;
+    f.dst = off; f.start = start;
+    off += (long)d.n * ld; start += (long)d.n * ld;
+    WPackJob b = f;
+    b.bwd = 1; b.ld = rup64(d.n);
+    b.dst = off; b.start = start;
+    off += (long)d.in_ch * b.ld; start += (long)d.in_ch * b.ld;
+    if (jobs) { jobs->push_back(f); jobs->push_back(b); }
+  }
+  return off;
+}
+
+size_t wimg_bytes() { return (size_t)wimg_layout(nullptr) * 2; }
+
+int wimg_pack(const float* const* t, void* dst, hipStream_t s) {
+  std::vector<WPackJob> jobs;
+  const long total = wimg_layout(&jobs);
+  WPackArgs a{};
+  for (size_t j = 0; j < jobs.size(); ++j) {
+    a.job[j] = jobs[j];
+    a.job[j].W = t[kWDesc[j / 2].t];
+  }
+  a.njob = (int)jobs.size();
+  a.total = total;
+  a.out = (unsigned short*)dst;
+  hipLaunchKernelGGL(k_wimg_pack, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, a);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+bool wimg_view(const void* base, const float* const* t, const float* W, int c0, int K, bool bwd, WView* v) {
+  long off = 0;
+  for (int i = 0; i < kNW; ++i) {
+    const WDesc& d = kWDesc[i];
+    int fld = 0, col[2] = {0, 0};
+    for (int s = 0; s < d.nseg; ++s) { col[s] = fld; fld += rup64(d.k[s]); }
+    const long foff = off, boff = off + (long)d.n * fld;
+    const int bld = rup64(d.n);
+    off = boff + (long)d.in_ch * bld;
+    if (t[d.t] != W) continue;
+    if (bwd) {
+      // rows c0 .. c0 + (output columns) of the transposed image, K = d.n
+      if (K != d.n) return false;
+      v->B = (const unsigned short*)base + boff + (long)c0 * bld;
+      v->ldb = bld;
+      v->bcol = 0;
+      v->rows = d.in_ch - c0;
+      return true;
+    }
+    for (int s = 0; s < d.nseg; ++s)
+      if (d.c0[s] == c0 && K <= d.k[s]) {
+        v->B = (const unsigned short*)base + foff;
+        v->ldb = fld;
+        v->bcol = col[s];
+        v->rows = d.n;
+        return true;
+      }
+    return false;
+  }
+  return false;
+}
+
+// ------------------------------------------------------------------------------------------
+// the row GEMM
+// ------------------------------------------------------------------------------------------
+#define RG_BM 64
+#define RG_NS 3
+#define RG_A_BYTES (RG_BM * 64 * 4)   // fp32 activations, 64 rows x 64 k
+#define RG_B_BYTES (256 * 64 * 2)     // bf16 weight rows, 256 rows x 64 k
+#define RG_SLOT (RG_A_BYTES + RG_B_BYTES)
+#define RG_PIECES_A (RG_A_BYTES / 1024 / 4)  // per wave
+#define RG_PIECES_B (RG_B_BYTES / 1024 / 4)
+#define RG_OPS (RG_PIECES_A + RG_PIECES_B)   // vmem ops per wave per chunk
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+
+template <int N>
+__device__ __forceinline__ void rg_wait() {
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+
+__device__ __forceinline__ void rg_dma(const void* src, unsigned m0) {
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(m0) : "memory");
+}
+
+// issue chunk c (segment-relative K offset kk) into ring slot `slot`
+__device__ __forceinline__ void rg_issue(const RGemm& g, int seg, int kk, int m0, int M, int N, unsigned slot_lds, int w,
+                                         int lane) {
+  const float* A = seg ? g.seg[1].A : g.seg[0].A;
+  const long lda = seg ? g.seg[1].lda : g.seg[0].lda;
+  const unsigned short* B = seg ? g.seg[1].B : g.seg[0].B;
+  const long ldb = seg ? g.seg[1].ldb : g.seg[0].ldb;
+  const int bcol = seg ? g.seg[1].bcol : g.seg[0].bcol;
+  const int brows = seg ? g.seg[1].rows : g.seg[0].rows;
+  // A: 64 rows x 256 B; piece p = 4 rows; lane -> row 4p + (lane >> 4), LDS chunk (lane & 15) holds
+  // source chunk (lane & 15) ^ (row & 15)
+#pragma unroll
+  for (int i = 0; i < RG_PIECES_A; ++i) {
+    const int p = w + 4 * i;
+    const int r = 4 * p + (lane >> 4);
+    const int gr = min(m0 + r, M - 1);
+    const int ch = (lane & 15) ^ (r & 15);
+    rg_dma(A + (long)gr * lda + kk + ch * 4, slot_lds + p * 1024);
+  }
+  // B: 256 rows x 128 B; piece p = 8 rows; lane -> row 8p + (lane >> 3), chunk (lane & 7) ^ (row & 7)
+#pragma unroll
+  for (int i = 0; i < RG_PIECES_B; ++i) {
+    const int p = w + 4 * i;
+    const int r = 8 * p + (lane >> 3);
+    const int br = min(r, brows - 1);
+    const int ch = (lane & 7) ^ (r & 7);
+    rg_dma(B + (long)br * ldb + bcol + kk + ch * 8, slot_lds + RG_A_BYTES + p * 1024);
+  }
+  (void)N;
+}
+
+__global__ __launch_bounds__(256) void k_rgemm(RGemm g) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const int M = g.M_dev ? *g.M_dev : g.M;
+  const int N = g.N;
+  const int m0 = blockIdx.x * RG_BM;
+  if (m0 >= M) return;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const unsigned base = (unsigned)(uintptr_t)lds;
+  const int nc0 = (g.seg[0].K + 63) >> 6;
+  const int nch = nc0 + (g.nseg > 1 ? (g.seg[1].K + 63) >> 6 : 0);
+  auto issue = [&](int c) {
+#ifdef RG_EXP_NODMA
+    return;  // timing experiment only (results garbage)
+#endif
+    const int seg = c < nc0 ? 0 : 1;
+    const int kk = (c - (seg ? nc0 : 0)) * 64;
+    rg_issue(g, seg, kk, m0, M, N, base + (c % RG_NS) * RG_SLOT, w, lane);
+  };
+  const int pro = nch < RG_NS ? nch : RG_NS;
+  for (int c = 0; c < pro; ++c) issue(c);
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool active = 64 * w < N;  // this wave's 64 output columns hold some of the N
+  const int sw = lane & 7;         // row & 7 of every fragment row this lane reads (rows 16i + (lane & 15))
+
+  for (int c = 0; c < nch; ++c) {
+    // chunks issued after c: min(nch, c + RG_NS) - c - 1 (the refill of c - 1's slot went out last iteration)
+    const int later = (nch < c + RG_NS ? nch : c + RG_NS) - c - 1;
+    if (later >= 2) rg_wait<2 * RG_OPS>();
+    else if (later == 1) rg_wait<RG_OPS>();
+    else rg_wait<0>();
+    __builtin_amdgcn_s_barrier();
+    const int seg = c < nc0 ? 0 : 1;
+    const int kk = (c - (seg ? nc0 : 0)) * 64;
+    const int K = seg ? g.seg[1].K : g.seg[0].K;
+    const unsigned char* sA = lds + (c % RG_NS) * RG_SLOT;
+    const unsigned char* sB = sA + RG_A_BYTES;
+#ifdef RG_EXP_NOMFMA
+    if (false) {  // timing experiment only
+#else
+    if (active) {
+#endif
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8_t af[4], bfr[4];
+        const int kc = 4 * ks + (lane >> 4);  // 8-element k group of this lane
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = 16 * i + (lane & 15);
+          // fp32 row r, k = 8 kc .. 8 kc + 7: 16-B chunks 2 kc, 2 kc + 1 (swizzled by r & 15)
+          const f32x4 x0 = *(const f32x4*)(sA + r * 256 + (((2 * kc) ^ (r & 15)) * 16));
+          const f32x4 x1 = *(const f32x4*)(sA + r * 256 + (((2 * kc + 1) ^ (r & 15)) * 16));
+          float x[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+          if (kk + 64 > K) {  // the last, partial chunk of a segment: columns past K read as zero
+#pragma unroll
+            for (int e = 0; e < 8; ++e) x[e] = (kk + 8 * kc + e < K) ? x[e] : 0.0f;
+          }
+#pragma unroll
+          for (int e = 0; e < 8; ++e) af[i][e] = (__bf16)x[e];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int r = 64 * w + 16 * j + (lane & 15);
+          bfr[j] = *(const bf16x8_t*)(sB + r * 128 + ((kc ^ sw) * 16));
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+      }
+    }
+    // everyone is past this slot's reads (lgkmcnt drained by the barrier's wait) before it is refilled
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (c + RG_NS < nch) issue(c + RG_NS);
+  }
+  rg_wait<0>();
+#ifdef RG_EXP_NOEPI
+  if (acc[0][0][0] != 12345.f) return;  // timing experiment only
+#endif
+  if (!active) return;
+  // weights are the MFMA A operand, so lane l holds C[16 i + (l & 15)][64 w + 16 j + 4 (l >> 4) + r],
+  // r = 0..3: four consecutive columns of one row, stored as one 16-B store (vec_out). Every
+  // operand load of the epilogue is issued before the first use.
+  if (g.vec_out) {
+    f32x4 cv[4][4], mk[4][4], bj[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = min(64 * w + 16 * j + 4 * (lane >> 4), N - 4);
+      bj[j] = g.bias ? *(const f32x4*)(g.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const long m = min(m0 + 16 * i + (lane & 15), M - 1);
+        const int n = min(64 * w + 16 * j + 4 * (lane >> 4), N - 4);
+        if (g.accumulate) cv[i][j] = *(const f32x4*)(g.C + m * g.ldc + n);
+        if (g.mask) mk[i][j] = *(const f32x4*)(g.mask + m * g.ldm + n);
+      }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = m0 + 16 * i + (lane & 15);
+        const int n = 64 * w + 16 * j + 4 * (lane >> 4);
+        f32x4 v = acc[i][j];
+        if (g.bias) v += bj[j];
+        if (g.accumulate) v += cv[i][j];
+        if (g.relu) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+        }
+        if (g.mask) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = mk[i][j][e] > 0.f ? v[e] : 0.f;
+        }
+        if (m < M && n < N) *(f32x4*)(g.C + (long)m * g.ldc + n) = v;
+      }
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + 16 * i + (lane & 15);
+        const int n = 64 * w + 16 * j + 4 * (lane >> 4) + r;
+        if (m >= M || n >= N) continue;
+        float v = acc[i][j][r];
+        float* cp = g.C + (long)m * g.ldc + n;
+        if (g.bias) v += g.bias[n];
+        if (g.accumulate) v += *cp;
+        if (g.relu) v = fmaxf(v, 0.f);
+        if (g.mask && !(g.mask[(long)m * g.ldm + n] > 0.f)) v = 0.f;
+        *cp = v;
+      }
+}
+
+size_t rgemm_lds_bytes() { return RG_NS * RG_SLOT; }
+
+void launch_rgemm(const RGemm& g0, int M_host, hipStream_t s) {
+  RGemm g = g0;
+  g.vec_out = (g.N % 4 == 0) && (g.ldc % 4 == 0) && ((uintptr_t)g.C % 16 == 0) &&
+              (!g.mask || ((g.ldm % 4 == 0) && ((uintptr_t)g.mask % 16 == 0))) && ((uintptr_t)g.bias % 16 == 0);
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)k_rgemm, hipFuncAttributeMaxDynamicSharedMemorySize, (int)rgemm_lds_bytes());
+    attr = true;
+  }
+  hipLaunchKernelGGL(k_rgemm, dim3((M_host + RG_BM - 1) / RG_BM), dim3(256), rgemm_lds_bytes(), s, g);
+}
+
+}  // namespace anr
+
+namespace anr {
+
+// ------------------------------------------------------------------------------------------
+// weight gradient dW[:, c0:c0+K] += dY^T X (+ column sums of dY into bsum / bsum2), bf16 operands,
+// fp32 accumulation: the reduction runs over the kept samples. Each workgroup (4 waves, 2 x 2 of
+// 64 x 64) owns a 128 (outputs) x 128 (inputs) tile and a contiguous range of samples; it stages
+// 32 samples per step through registers (fp32 -> bf16 RNE) into [sample][column] LDS images read
+// with ds_read_b64_tr_b16 (8 consecutive samples per MFMA fragment), double-buffered, and writes its
+// partial tile to a slab in the accumulator's own layout (16 B per lane, coalesced). k_wgrad_reduce
+// sums the slabs in sample-range order and adds them into dW: no atomics, deterministic.
+// ------------------------------------------------------------------------------------------
+#define WG_T 128        // tile edge
+#define WG_S 32         // samples per step
+#define WG_LD 136       // LDS row stride (bf16 elements)
+#define WG_TILE_FLOATS (WG_T * WG_T)
+
+typedef short wv4s __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ bf16x8_t wg_frag(const unsigned short* S, int cb, int lane) {
+  // 16-lane group g: rows 8g + q (q = 0..3, then 4..7), lane 4q + p supplies columns cb + 4p .. +3;
+  // lane i receives column cb + i, element q = row q (anr_gemm.hip frag16)
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  typedef __attribute__((address_space(3))) wv4s lds_v4s;
+  const unsigned short* a0 = S + (8 * g + q) * WG_LD + cb + 4 * p;
+  const wv4s x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(uintptr_t)(unsigned)(uintptr_t)a0);
+  const wv4s x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(uintptr_t)(unsigned)(uintptr_t)(a0 + 4 * WG_LD));
+  bf16x8_t f;
+  const short e[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+  __builtin_memcpy(&f, e, 16);
+  return f;
+}
+
+// thread's share of one 32 x 128 fp32 operand step: 4 float4 (sample 8h + (tid >> 5), columns 4 (tid & 31))
+__device__ __forceinline__ void wg_load(const float* P, long ld, int ncol, int c0, int s, int s1, int tid, f32x4 (&v)[4]) {
+#pragma unroll
+  for (int h = 0; h < 4; ++h) {
+    const int ss = s + 8 * h + (tid >> 5);
+    const int c = c0 + 4 * (tid & 31);
+    const bool ok = ss < s1 && c < ncol;
+    const f32x4 x = *(const f32x4*)(P + (long)(ok ? ss : s) * ld + (ok ? c : 0));
+    // columns past ncol (inside the 16-B group) and samples past the range read as zero
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[h][e] = (ok && c + e < ncol) ? x[e] : 0.0f;
+  }
+}
+
+__device__ __forceinline__ void wg_store(unsigned short* S, int tid, const f32x4 (&v)[4]) {
+#pragma unroll
+  for (int h = 0; h < 4; ++h) {
+    const int row = 8 * h + (tid >> 5), col = 4 * (tid & 31);
+    unsigned short e[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) e[k] = f2bf_rne(v[h][k]);
+    *(uint2*)(S + row * WG_LD + col) = make_uint2((uint32_t)e[0] | ((uint32_t)e[1] << 16), (uint32_t)e[2] | ((uint32_t)e[3] << 16));
+  }
+}
+
+__global__ __launch_bounds__(256) void k_wgrad(WGrad g) {
+  __shared__ __attribute__((aligned(16))) unsigned short sY[2][WG_S * WG_LD];
+  __shared__ __attribute__((aligned(16))) unsigned short sX[2][WG_S * WG_LD];
+  __shared__ float srs[8][WG_T];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int ti = blockIdx.x, tj = blockIdx.y, z = blockIdx.z;
+  const int n = g.M_dev ? *g.M_dev : g.n;
+  const int s0 = z * g.spb, s1 = min(n, s0 + g.spb);
+  const int i0 = ti * WG_T, j0 = tj * WG_T;
+  const int wi = (w >> 1) * 64, wj = (w & 1) * 64;
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 rsum = {0.f, 0.f, 0.f, 0.f};  // column sums of this thread's dY share (tile row 0 only)
+  const bool do_rs = g.rs_slab != nullptr && tj == 0;
+  f32x4 vy[4], vx[4];
+  if (s0 < s1) {
+    wg_load(g.dY, g.ldY, g.nout, i0, s0, s1, tid, vy);
+    wg_load(g.X, g.ldX, g.K, j0, s0, s1, tid, vx);
+  }
+  int buf = 0;
+  for (int s = s0; s < s1; s += WG_S) {
+    if (do_rs) {
+#pragma unroll
+      for (int h = 0; h < 4; ++h) rsum += vy[h];
+    }
+    wg_store(sY[buf], tid, vy);
+    wg_store(sX[buf], tid, vx);
+    __syncthreads();
+    if (s + WG_S < s1) {  // the next step's operands load while this step's MFMAs run
+      wg_load(g.dY, g.ldY, g.nout, i0, s + WG_S, s1, tid, vy);
+      wg_load(g.X, g.ldX, g.K, j0, s + WG_S, s1, tid, vx);
+    }
+    bf16x8_t fa[4], fb[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) fa[a] = wg_frag(sY[buf], wi + 16 * a, lane);
+#pragma unroll
+    for (int b = 0; b < 4; ++b) fb[b] = wg_frag(sX[buf], wj + 16 * b, lane);
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a], fb[b], acc[a][b], 0, 0, 0);
+    buf ^= 1;
+  }
+  // partial tile, accumulator layout: slab[z][tile][w][a][b][lane][r]
+  float* slab = g.slab + ((long)(z * g.tiles + ti * g.tj + tj) * 4 + w) * 16 * 256;
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) *(f32x4*)(slab + (a * 4 + b) * 256 + lane * 4) = acc[a][b];
+  if (do_rs) {
+    // threads with equal tid & 31 hold the same 4 columns: combine their 8 partial sums
+    *(f32x4*)&srs[tid >> 5][4 * (tid & 31)] = rsum;
+    __syncthreads();
+    if (tid < WG_T) {
+      float t = 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) t += srs[k][tid];
+      g.rs_slab[(long)z * 256 + i0 + tid] = t;
+    }
+  }
+}
+
+// dW[i][c0 + j] += sum_z slab; bsum[i] (+ bsum2[i]) += sum_z rs_slab[z][i]. One thread per 4 rows of
+// one column (a slab lane's float4) and per group of WG_ZG consecutive slabs; the groups' sums meet
+// in fp32 atomics (as the generic kernel's split-K does).
+#define WG_ZG 8
+__global__ void k_wgrad_reduce(WGrad g) {
+  const int per_tile = 4 * 16 * 64;
+  const int nu = g.tiles * per_tile;
+  const int u = blockIdx.x * blockDim.x + threadIdx.x;  // (z group, tile, w, a, b, lane)
+  const int zg = u / nu, v = u - zg * nu;
+  const int z0 = zg * WG_ZG, z1 = min(g.nz, z0 + WG_ZG);
+  if (z0 < g.nz) {
+    const int t = v / per_tile, rem = v - t * per_tile;
+    const int w = rem / (16 * 64), ab = (rem / 64) & 15, lane = rem & 63;
+    const int a = ab >> 2, b = ab & 3;
+    const int ti = t / g.tj, tj = t - ti * g.tj;
+    const int i = ti * WG_T + (w >> 1) * 64 + 16 * a + 4 * (lane >> 4);
+    const int j = tj * WG_T + (w & 1) * 64 + 16 * b + (lane & 15);
+    f32x4 s = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < WG_ZG; ++k)
+      if (z0 + k < z1) s += *(const f32x4*)(g.slab + ((long)((z0 + k) * g.tiles + t) * 4 + w) * 16 * 256 + ab * 256 + lane * 4);
+    if (j < g.K) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (i + r < g.nout) atomicAdd(g.dW + (long)(i + r) * g.ldw + j, s[r]);
+    }
+  }
+  // column sums: thread (z group, column) for the first nout * z-groups threads
+  if (g.rs_slab && u < g.nout * ((g.nz + WG_ZG - 1) / WG_ZG)) {
+    const int c = u % g.nout, q0 = (u / g.nout) * WG_ZG;
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < WG_ZG; ++k)
+      if (q0 + k < g.nz) t += g.rs_slab[(long)(q0 + k) * 256 + c];
+    if (g.bsum) atomicAdd(g.bsum + c, t);
+    if (g.bsum2) atomicAdd(g.bsum2 + c, t);
+  }
+}
+
+size_t wgrad_slab_floats() { return (size_t)WG_MAX_Z * 4 * WG_TILE_FLOATS + (size_t)WG_MAX_Z * 256; }
+
+int launch_wgrad(WGrad g, int n_host, hipStream_t s) {
+  if (n_host <= 0) return 0;
+  const int ti = (g.nout + WG_T - 1) / WG_T, tj = (g.K + WG_T - 1) / WG_T;
+  g.tj = tj;
+  g.tiles = ti * tj;
+  // samples per workgroup: enough workgroups to cover the CUs, at most WG_MAX_Z slabs
+  int nz = (n_host + 383) / 384;
+  nz = nz < 1 ? 1 : (nz > WG_MAX_Z ? WG_MAX_Z : nz);
+  g.spb = ((n_host + nz - 1) / nz + WG_S - 1) / WG_S * WG_S;
+  g.nz = (n_host + g.spb - 1) / g.spb;
+  g.n = n_host;
+  g.rs_slab = (g.bsum || g.bsum2) ? g.slab + (size_t)WG_MAX_Z * 4 * WG_TILE_FLOATS : nullptr;
+  hipLaunchKernelGGL(k_wgrad, dim3(ti, tj, g.nz), dim3(256), 0, s, g);
+  const int nred = g.tiles * 4 * 16 * 64 * ((g.nz + WG_ZG - 1) / WG_ZG);
+  const int nthr = nred > 256 ? nred : 256;
+  hipLaunchKernelGGL(k_wgrad_reduce, dim3((nthr + 255) / 256), dim3(256), 0, s, g);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace anr

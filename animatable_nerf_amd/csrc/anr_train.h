@@ -50,6 +50,70 @@ struct GemmArgs {
 
 void launch_gemm(GemmArgs g, dim3 grid, hipStream_t s);
 
+// bf16 row GEMM with a weight-image B operand (anr_tgemm.hip): C[M][N] = epi(sum_s A_s[M][K_s] B_s^T),
+// A_s fp32 rows (stride lda, 16-B aligned, lda >= K_s rounded up to 64), B_s bf16 image rows
+// (k-contiguous, stride ldb, chunk-aligned column offset bcol, `rows` valid rows), N <= 256
+struct RGemmSeg {
+  const float* A;
+  long lda;
+  int K;
+  const unsigned short* B;
+  long ldb;
+  int bcol;
+  int rows;
+};
+struct RGemm {
+  int M;
+  const int* M_dev;
+  int N;
+  int nseg;
+  RGemmSeg seg[2];
+  float* C;
+  long ldc;
+  const float* bias;
+  int relu;
+  const float* mask;
+  long ldm;
+  int accumulate;
+  int vec_out;  // set by launch_rgemm: C (and mask) rows 16-B addressable, N % 4 == 0
+};
+void launch_rgemm(const RGemm& g, int M_host, hipStream_t s);
+// bf16 weight images of the training GEMM weights: forward (rows = outputs, k = used input columns,
+// segments padded to 64) and backward (rows = input columns, k = outputs padded to 64)
+size_t wimg_bytes();
+int wimg_pack(const float* const* t, void* dst, hipStream_t s);
+struct WView {
+  const unsigned short* B;
+  long ldb;
+  int bcol;
+  int rows;
+};
+bool wimg_view(const void* base, const float* const* t, const float* W, int c0, int K, bool bwd, WView* v);
+
+// bf16 weight gradient with per-sample-range partial slabs (anr_tgemm.hip): dW[i][j] (ldw) +=
+// sum_s dY[s][i] X[s][j], i < nout <= 256, j < K <= 256; column sums of dY into bsum / bsum2.
+// dY, X: fp32 rows, 16-B aligned, ld % 4 == 0. slab: wgrad_slab_floats() of workspace.
+#define WG_MAX_Z 64
+struct WGrad {
+  const float* dY;
+  long ldY;
+  int nout;
+  const float* X;
+  long ldX;
+  int K;
+  float* dW;
+  long ldw;
+  float* bsum;
+  float* bsum2;
+  int n;
+  const int* M_dev;
+  float* slab;
+  float* rs_slab;
+  int spb, nz, tiles, tj;
+};
+size_t wgrad_slab_floats();
+int launch_wgrad(WGrad g, int n_host, hipStream_t s);
+
 // per-point training buffers (row-major, compact kept-sample order)
 struct TrainBufs {
   const int* list;

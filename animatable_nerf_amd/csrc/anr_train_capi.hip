@@ -23,7 +23,7 @@ struct TLayout {
   Layout L;
   size_t pt, Gp, Ip, Gv, Lp, lbs, Gt, It, Lt, Hp, Ht, Hn, Feat, Alpha, Lat, View, Rgbl;
   size_t draw, dRgb, dAlpha, dBp, dBt, dLp, dLt, dIt, dGt, dA, dB, dFeat, dLat, dView;
-  size_t ysum, acc3, d_rgb, d_pbw, d_tbw, total;
+  size_t ysum, acc3, d_rgb, d_pbw, d_tbw, wimg, wslab, total;
 };
 
 TLayout tlayout(int n_rays, int chunk, long np, long nt) {
@@ -44,6 +44,8 @@ TLayout tlayout(int n_rays, int chunk, long np, long nt) {
   T.dLp = take(N * 32); T.dLt = take(N * 32); T.dIt = take(N * 32); T.dGt = take(N * 64);
   T.dA = take(N * 256); T.dB = take(N * 256); T.dFeat = take(N * 256); T.dLat = take(N * 256); T.dView = take(N * 128);
   T.ysum = take(8 * 256); T.acc3 = take(4); T.d_rgb = take(R * 3); T.d_pbw = take(N * 24); T.d_tbw = take(N * 24);
+  T.wimg = take((wimg_bytes() + 3) / 4);
+  T.wslab = take(wgrad_slab_floats());
   T.total = o;
   return T;
 }
@@ -68,6 +70,24 @@ struct Exec {
   int n;         // kept samples (host copy)
   int bf16 = 0;       // current GEMMs take bf16 operands
   int pose_fp32 = 0;  // precision ANR_BF16 keeps the pose-space BW MLP in fp32 (ANR_BF16_ALL does not)
+  const void* wimg = nullptr;          // bf16 weight images (anr_tgemm.hip), packed for this call
+  const float* const* pt = nullptr;    // the parameter tensors the images were packed from
+  float* wslab = nullptr;              // weight-gradient partial slabs (anr_tgemm.hip k_wgrad)
+
+  // the bf16 row GEMM when every operand fits it (anr_train.h RGemm); false: use the generic kernel
+  bool row_seg(RGemmSeg& q, const float* A, long lda, int K, const float* W, int c0, bool bwd) {
+    if (!A || K <= 0 || lda % 4 != 0 || ((uintptr_t)A & 15) != 0 || lda < (long)((K + 63) / 64 * 64)) return false;
+    WView v;
+    if (!wimg_view(wimg, pt, W, c0, K, bwd, &v)) return false;
+    q = RGemmSeg{A, lda, K, v.B, v.ldb, v.bcol, v.rows};
+    return true;
+  }
+  int rgemm(RGemm& g) {
+    if (n <= 0 || g.N <= 0) return ANR_OK;
+    g.M = n;
+    launch_rgemm(g, n, s);
+    return check_launch("k_rgemm");
+  }
 
   int gemm(GemmArgs g, int M) {
     if (M <= 0 || g.N <= 0) return ANR_OK;
@@ -82,6 +102,15 @@ struct Exec {
   // Y[n][Nout] = act( X0[:, :K0] W[:, c0:c0+K0]^T (+ X1 W[:, c1:c1+K1]^T) + bias )
   int fwd(float* Y, int ldY, int Nout, const float* W, int in_ch, const float* bias, bool relu, const float* X0, int ld0,
           int K0, int c0, const float* X1 = nullptr, int ld1 = 0, int K1 = 0, int c1 = 0) {
+    if (bf16 && wimg && Nout <= 256) {
+      RGemm r{};
+      r.N = Nout;
+      r.nseg = X1 ? 2 : 1;
+      if (row_seg(r.seg[0], X0, ld0, K0, W, c0, false) && (!X1 || row_seg(r.seg[1], X1, ld1, K1, W, c1, false))) {
+        r.C = Y; r.ldc = ldY; r.bias = bias; r.relu = relu ? 1 : 0;
+        return rgemm(r);
+      }
+    }
     GemmArgs g{};
     g.N = Nout;
     g.nseg = X1 ? 2 : 1;
@@ -95,6 +124,14 @@ struct Exec {
   // gradient) are added into bsum (and bsum2) in the same pass when given
   int wgrad(float* dW, int in_ch, int c0, int Nout, const float* dY, int ldY, const float* X, int ldX, int K,
             float* bsum = nullptr, float* bsum2 = nullptr) {
+    if (bf16 && wslab && Nout <= 256 && K <= 256 && ldY % 4 == 0 && ldX % 4 == 0 && ((uintptr_t)dY & 15) == 0 &&
+        ((uintptr_t)X & 15) == 0 && n > 0) {
+      WGrad w{};
+      w.dY = dY; w.ldY = ldY; w.nout = Nout; w.X = X; w.ldX = ldX; w.K = K;
+      w.dW = dW + c0; w.ldw = in_ch; w.bsum = bsum; w.bsum2 = bsum2; w.slab = wslab;
+      if (launch_wgrad(w, n, s) != 0) return check_launch("k_wgrad");
+      return ANR_OK;
+    }
     GemmArgs g{};
     g.rowsum = bsum;
     g.rowsum2 = bsum2;
@@ -110,6 +147,16 @@ struct Exec {
   int xgrad(float* dX, int ldX, int K, const float* dY, int ldY, int Nout, const float* W, int in_ch, int c0,
             const float* mask, int ldm, bool accumulate, const float* dY2 = nullptr, int ldY2 = 0, int Nout2 = 0,
             const float* W2 = nullptr, int in_ch2 = 0) {
+    if (bf16 && wimg && K <= 256) {
+      RGemm r{};
+      r.N = K;
+      r.nseg = dY2 ? 2 : 1;
+      if (row_seg(r.seg[0], dY, ldY, Nout, W, c0, true) && (!dY2 || row_seg(r.seg[1], dY2, ldY2, Nout2, W2, c0, true)) &&
+          r.seg[0].rows >= K && (!dY2 || r.seg[1].rows >= K)) {
+        r.C = dX; r.ldc = ldX; r.mask = mask; r.ldm = ldm; r.accumulate = accumulate ? 1 : 0;
+        return rgemm(r);
+      }
+    }
     GemmArgs g{};
     g.N = K;
     g.nseg = dY2 ? 2 : 1;
@@ -130,6 +177,17 @@ struct PoseScope {
   }
   ~PoseScope() { e.bf16 = keep; }
 };
+
+// bf16 weight images for the row GEMM (bf16 policies only; refreshed on every call, the weights may
+// have changed since the last)
+int pack_images(Exec& e, const anr_params* p, char* dst, hipStream_t s, float* wslab) {
+  if (!e.bf16) return ANR_OK;
+  e.wslab = wslab;
+  if (wimg_pack(p->t, dst, s) != 0) return check_launch("k_wimg_pack");
+  e.wimg = dst;
+  e.pt = p->t;
+  return ANR_OK;
+}
 
 int read_count(const int* dev, int* host, hipStream_t s) {
   if (hipMemcpyAsync(host, dev, sizeof(int), hipMemcpyDeviceToHost, s) != hipSuccess ||
@@ -510,6 +568,7 @@ int anr_train_fwd(const anr_params* p, const anr_frame* f, const float* ray_o, c
   hipStream_t s = (hipStream_t)stream;
   char* ws = (char*)workspace;
   Exec e{s, 0, (o->precision == ANR_BF16 || o->precision == ANR_BF16_ALL) ? 1 : 0, o->precision == ANR_BF16 ? 1 : 0};
+  ANR_TRY(pack_images(e, p, ws + T.wimg, s, (float*)(ws + T.wslab)));
   ANR_TRY(train_forward(p, f, ray_o, ray_d, near_, far_, n_rays, o, out, ws, T, s, e));
   if (out->raw &&
       hipMemcpyAsync(out->raw, ws + T.L.raw, (size_t)n_rays * 64 * 16, hipMemcpyDeviceToDevice, s) != hipSuccess)
@@ -531,6 +590,7 @@ int anr_train_bwd(const anr_params* p, float* const* grads, const anr_frame* f, 
   hipStream_t s = (hipStream_t)stream;
   char* ws = (char*)workspace;
   Exec e{s, 0, (o->precision == ANR_BF16 || o->precision == ANR_BF16_ALL) ? 1 : 0, o->precision == ANR_BF16 ? 1 : 0};
+  ANR_TRY(pack_images(e, p, ws + T.wimg, s, (float*)(ws + T.wslab)));
   ANR_TRY(read_count((const int*)(ws + T.L.counts), &e.n, s));
   ANR_TRY(train_backward(p, grads, f, ray_o, ray_d, near_, far_, n_rays, o, d_rgb_map, d_pbw, d_tbw, ws, T, s, e));
   if (e.n <= 0) return ANR_OK;
@@ -559,6 +619,7 @@ int anr_train_step(const anr_params* p, float* const* grads, const anr_frame* f,
   hipStream_t s = (hipStream_t)stream;
   char* ws = (char*)workspace;
   Exec e{s, 0, (o->precision == ANR_BF16 || o->precision == ANR_BF16_ALL) ? 1 : 0, o->precision == ANR_BF16 ? 1 : 0};
+  ANR_TRY(pack_images(e, p, ws + T.wimg, s, (float*)(ws + T.wslab)));
   ANR_TRY(train_forward(p, f, ray_o, ray_d, near_, far_, n_rays, o, out, ws, T, s, e));
   // fused losses (tpose_trainer.py:50-63) and their upstream gradients
   TrainBufs b = bufs(T, ws, f, ray_o, ray_d, near_, far_, n_rays, o);

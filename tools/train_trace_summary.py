@@ -1,0 +1,21 @@
+"""Summarise one training step from a rocprofv3 kernel trace: per-kernel totals between the last two
+k_adam dispatches. usage: python tools/train_trace_summary.py <run_kernel_trace.csv>"""
+import collections
+import csv
+import sys
+
+rows = list(csv.DictReader(open(sys.argv[1])))
+rows.sort(key=lambda r: int(r['Start_Timestamp']))
+idx = [i for i, r in enumerate(rows) if 'k_adam' in r['Kernel_Name']]
+a, b = idx[-2], idx[-1]
+step = rows[a + 1:b + 1]
+t0, t1 = int(step[0]['Start_Timestamp']), int(step[-1]['End_Timestamp'])
+busy = sum(int(r['End_Timestamp']) - int(r['Start_Timestamp']) for r in step)
+print('step span %.1f us, kernels %d, busy %.1f us' % ((t1 - t0) / 1e3, len(step), busy / 1e3))
+agg = collections.defaultdict(lambda: [0, 0.0])
+for r in step:
+    d = (int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e3
+    agg[r['Kernel_Name'].replace('anr::', '')[:60]][0] += 1
+    agg[r['Kernel_Name'].replace('anr::', '')[:60]][1] += d
+for n, (c, t) in sorted(agg.items(), key=lambda x: -x[1][1])[:14]:
+    print('%-60s %3d %8.1f %6.1f' % (n, c, t, t / c))
