@@ -74,7 +74,9 @@ __global__ void k_wimg_pack(WPackArgs a) {
     for (int s = 0; s < J.nseg; ++s)
       if (col >= J.col[s] && col < J.col[s] + J.k[s]) v = J.W[(long)row * J.in_ch + J.c0[s] + col - J.col[s]];
   }
-  a.out[J.dst + local] = f2bf_rne(v);
+  const unsigned short hi = f2bf_rne(v);
+  a.out[J.dst + local] = hi;
+  a.out[a.total + J.dst + local] = f2bf_rne(v - __uint_as_float((uint32_t)hi << 16));  // lo image
 }
 
 // layout of the images: per descriptor a forward image (n rows x sum of 64-padded segments) and a
@@ -102,7 +104,8 @@ static long wimg_layout(std::vector<WPackJob>* jobs) {
   return off;
 }
 
-size_t wimg_bytes() { return (size_t)wimg_layout(nullptr) * 2; }
+// hi images, then the lo images (w - hi, for the split-bf16 products) at the same offsets + total
+size_t wimg_bytes() { return (size_t)wimg_layout(nullptr) * 2 * 2; }
 
 int wimg_pack(const float* const* t, void* dst, hipStream_t s) {
   std::vector<WPackJob> jobs;
@@ -129,6 +132,8 @@ bool wimg_view(const void* base, const float* const* t, const float* W, int c0, 
     const int bld = rup64(d.n);
     off = boff + (long)d.in_ch * bld;
     if (t[d.t] != W) continue;
+    const long lo_off = wimg_layout(nullptr);
+    v->lo_off = lo_off;
     if (bwd) {
       // rows c0 .. c0 + (output columns) of the transposed image, K = d.n
       if (K != d.n) return false;
@@ -155,13 +160,16 @@ bool wimg_view(const void* base, const float* const* t, const float* W, int c0, 
 // the row GEMM
 // ------------------------------------------------------------------------------------------
 #define RG_BM 64
-#define RG_NS 3
 #define RG_A_BYTES (RG_BM * 64 * 4)   // fp32 activations, 64 rows x 64 k
 #define RG_B_BYTES (256 * 64 * 2)     // bf16 weight rows, 256 rows x 64 k
-#define RG_SLOT (RG_A_BYTES + RG_B_BYTES)
 #define RG_PIECES_A (RG_A_BYTES / 1024 / 4)  // per wave
 #define RG_PIECES_B (RG_B_BYTES / 1024 / 4)
-#define RG_OPS (RG_PIECES_A + RG_PIECES_B)   // vmem ops per wave per chunk
+// X3 (split-bf16, fp32-level: lo*h + h*lo + h*h): the weight rows' lo image rides in the same slot
+template <bool X3> struct RgCfg {
+  static constexpr int NS = X3 ? 2 : 3;                                // ring slots
+  static constexpr int SLOT = RG_A_BYTES + RG_B_BYTES * (X3 ? 2 : 1);  // bytes per slot
+  static constexpr int OPS = RG_PIECES_A + RG_PIECES_B * (X3 ? 2 : 1); // vmem ops per wave per chunk
+};
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 
@@ -176,6 +184,7 @@ __device__ __forceinline__ void rg_dma(const void* src, unsigned m0) {
 }
 
 // issue chunk c (segment-relative K offset kk) into ring slot `slot`
+template <bool X3>
 __device__ __forceinline__ void rg_issue(const RGemm& g, int seg, int kk, int m0, int M, int N, unsigned slot_lds, int w,
                                          int lane) {
   const float* A = seg ? g.seg[1].A : g.seg[0].A;
@@ -203,10 +212,23 @@ __device__ __forceinline__ void rg_issue(const RGemm& g, int seg, int kk, int m0
     const int ch = (lane & 7) ^ (r & 7);
     rg_dma(B + (long)br * ldb + bcol + kk + ch * 8, slot_lds + RG_A_BYTES + p * 1024);
   }
+  if constexpr (X3) {
+    const long lo = seg ? g.seg[1].lo_off : g.seg[0].lo_off;
+#pragma unroll
+    for (int i = 0; i < RG_PIECES_B; ++i) {
+      const int p = w + 4 * i;
+      const int r = 8 * p + (lane >> 3);
+      const int br = min(r, brows - 1);
+      const int ch = (lane & 7) ^ (r & 7);
+      rg_dma(B + lo + (long)br * ldb + bcol + kk + ch * 8, slot_lds + RG_A_BYTES + RG_B_BYTES + p * 1024);
+    }
+  }
   (void)N;
 }
 
+template <bool X3>
 __global__ __launch_bounds__(256) void k_rgemm(RGemm g) {
+  constexpr int RG_NS = RgCfg<X3>::NS, RG_SLOT = RgCfg<X3>::SLOT, RG_OPS = RgCfg<X3>::OPS;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int M = g.M_dev ? *g.M_dev : g.M;
   const int N = g.N;
@@ -222,7 +244,7 @@ __global__ __launch_bounds__(256) void k_rgemm(RGemm g) {
 #endif
     const int seg = c < nc0 ? 0 : 1;
     const int kk = (c - (seg ? nc0 : 0)) * 64;
-    rg_issue(g, seg, kk, m0, M, N, base + (c % RG_NS) * RG_SLOT, w, lane);
+    rg_issue<X3>(g, seg, kk, m0, M, N, base + (c % RG_NS) * RG_SLOT, w, lane);
   };
   const int pro = nch < RG_NS ? nch : RG_NS;
   for (int c = 0; c < pro; ++c) issue(c);
@@ -238,7 +260,7 @@ __global__ __launch_bounds__(256) void k_rgemm(RGemm g) {
   for (int c = 0; c < nch; ++c) {
     // chunks issued after c: min(nch, c + RG_NS) - c - 1 (the refill of c - 1's slot went out last iteration)
     const int later = (nch < c + RG_NS ? nch : c + RG_NS) - c - 1;
-    if (later >= 2) rg_wait<2 * RG_OPS>();
+    if (later >= 2) rg_wait<(RG_NS > 2 ? 2 * RG_OPS : 0)>();
     else if (later == 1) rg_wait<RG_OPS>();
     else rg_wait<0>();
     __builtin_amdgcn_s_barrier();
@@ -254,7 +276,7 @@ __global__ __launch_bounds__(256) void k_rgemm(RGemm g) {
 #endif
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        bf16x8_t af[4], bfr[4];
+        bf16x8_t af[4], bfr[4], al[4], bl[4];
         const int kc = 4 * ks + (lane >> 4);  // 8-element k group of this lane
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -268,17 +290,27 @@ __global__ __launch_bounds__(256) void k_rgemm(RGemm g) {
             for (int e = 0; e < 8; ++e) x[e] = (kk + 8 * kc + e < K) ? x[e] : 0.0f;
           }
 #pragma unroll
-          for (int e = 0; e < 8; ++e) af[i][e] = (__bf16)x[e];
+          for (int e = 0; e < 8; ++e) {
+            af[i][e] = (__bf16)x[e];
+            if constexpr (X3) al[i][e] = (__bf16)(x[e] - (float)af[i][e]);
+          }
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int r = 64 * w + 16 * j + (lane & 15);
           bfr[j] = *(const bf16x8_t*)(sB + r * 128 + ((kc ^ sw) * 16));
+          if constexpr (X3) bl[j] = *(const bf16x8_t*)(sB + RG_B_BYTES + r * 128 + ((kc ^ sw) * 16));
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+          for (int j = 0; j < 4; ++j) {
+            if constexpr (X3) {
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl[j], af[i], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], al[i], acc[i][j], 0, 0, 0);
+            }
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+          }
       }
     }
     // everyone is past this slot's reads (lgkmcnt drained by the barrier's wait) before it is refilled
@@ -350,7 +382,8 @@ __global__ __launch_bounds__(256) void k_rgemm(RGemm g) {
       }
 }
 
-size_t rgemm_lds_bytes() { return RG_NS * RG_SLOT; }
+template <bool X3>
+size_t rgemm_lds_bytes() { return (size_t)RgCfg<X3>::NS * RgCfg<X3>::SLOT; }
 
 void launch_rgemm(const RGemm& g0, int M_host, hipStream_t s) {
   RGemm g = g0;
@@ -358,10 +391,15 @@ void launch_rgemm(const RGemm& g0, int M_host, hipStream_t s) {
               (!g.mask || ((g.ldm % 4 == 0) && ((uintptr_t)g.mask % 16 == 0))) && ((uintptr_t)g.bias % 16 == 0);
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)k_rgemm, hipFuncAttributeMaxDynamicSharedMemorySize, (int)rgemm_lds_bytes());
+    (void)hipFuncSetAttribute((const void*)k_rgemm<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)rgemm_lds_bytes<false>());
+    (void)hipFuncSetAttribute((const void*)k_rgemm<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)rgemm_lds_bytes<true>());
     attr = true;
   }
-  hipLaunchKernelGGL(k_rgemm, dim3((M_host + RG_BM - 1) / RG_BM), dim3(256), rgemm_lds_bytes(), s, g);
+  const dim3 grid((M_host + RG_BM - 1) / RG_BM);
+  if (g.x3) hipLaunchKernelGGL(k_rgemm<true>, grid, dim3(256), rgemm_lds_bytes<true>(), s, g);
+  else hipLaunchKernelGGL(k_rgemm<false>, grid, dim3(256), rgemm_lds_bytes<false>(), s, g);
 }
 
 }  // namespace anr
@@ -412,20 +450,29 @@ __device__ __forceinline__ void wg_load(const float* P, long ld, int ncol, int c
   }
 }
 
-__device__ __forceinline__ void wg_store(unsigned short* S, int tid, const f32x4 (&v)[4]) {
+// X3: also the lo image (x - hi) into SL
+template <bool X3>
+__device__ __forceinline__ void wg_store(unsigned short* S, unsigned short* SL, int tid, const f32x4 (&v)[4]) {
 #pragma unroll
   for (int h = 0; h < 4; ++h) {
     const int row = 8 * h + (tid >> 5), col = 4 * (tid & 31);
-    unsigned short e[4];
+    unsigned short e[4], l[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) e[k] = f2bf_rne(v[h][k]);
+    for (int k = 0; k < 4; ++k) {
+      e[k] = f2bf_rne(v[h][k]);
+      if constexpr (X3) l[k] = f2bf_rne(v[h][k] - __uint_as_float((uint32_t)e[k] << 16));
+    }
     *(uint2*)(S + row * WG_LD + col) = make_uint2((uint32_t)e[0] | ((uint32_t)e[1] << 16), (uint32_t)e[2] | ((uint32_t)e[3] << 16));
+    if constexpr (X3)
+      *(uint2*)(SL + row * WG_LD + col) = make_uint2((uint32_t)l[0] | ((uint32_t)l[1] << 16), (uint32_t)l[2] | ((uint32_t)l[3] << 16));
   }
 }
 
+template <bool X3>
 __global__ __launch_bounds__(256) void k_wgrad(WGrad g) {
-  __shared__ __attribute__((aligned(16))) unsigned short sY[2][WG_S * WG_LD];
-  __shared__ __attribute__((aligned(16))) unsigned short sX[2][WG_S * WG_LD];
+  constexpr int NI = X3 ? 2 : 1;  // images per operand: hi (and lo)
+  __shared__ __attribute__((aligned(16))) unsigned short sY[2][NI][WG_S * WG_LD];
+  __shared__ __attribute__((aligned(16))) unsigned short sX[2][NI][WG_S * WG_LD];
   __shared__ float srs[8][WG_T];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int ti = blockIdx.x, tj = blockIdx.y, z = blockIdx.z;
@@ -451,22 +498,34 @@ __global__ __launch_bounds__(256) void k_wgrad(WGrad g) {
 #pragma unroll
       for (int h = 0; h < 4; ++h) rsum += vy[h];
     }
-    wg_store(sY[buf], tid, vy);
-    wg_store(sX[buf], tid, vx);
+    wg_store<X3>(sY[buf][0], sY[buf][NI - 1], tid, vy);
+    wg_store<X3>(sX[buf][0], sX[buf][NI - 1], tid, vx);
     __syncthreads();
     if (s + WG_S < s1) {  // the next step's operands load while this step's MFMAs run
       wg_load(g.dY, g.ldY, g.nout, i0, s + WG_S, s1, tid, vy);
       wg_load(g.X, g.ldX, g.K, j0, s + WG_S, s1, tid, vx);
     }
-    bf16x8_t fa[4], fb[4];
+    bf16x8_t fa[4], fb[4], la[4], lb[4];
 #pragma unroll
-    for (int a = 0; a < 4; ++a) fa[a] = wg_frag(sY[buf], wi + 16 * a, lane);
+    for (int a = 0; a < 4; ++a) {
+      fa[a] = wg_frag(sY[buf][0], wi + 16 * a, lane);
+      if constexpr (X3) la[a] = wg_frag(sY[buf][NI - 1], wi + 16 * a, lane);
+    }
 #pragma unroll
-    for (int b = 0; b < 4; ++b) fb[b] = wg_frag(sX[buf], wj + 16 * b, lane);
+    for (int b = 0; b < 4; ++b) {
+      fb[b] = wg_frag(sX[buf][0], wj + 16 * b, lane);
+      if constexpr (X3) lb[b] = wg_frag(sX[buf][NI - 1], wj + 16 * b, lane);
+    }
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
-      for (int b = 0; b < 4; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a], fb[b], acc[a][b], 0, 0, 0);
+      for (int b = 0; b < 4; ++b) {
+        if constexpr (X3) {
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(la[a], fb[b], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a], lb[b], acc[a][b], 0, 0, 0);
+        }
+        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a], fb[b], acc[a][b], 0, 0, 0);
+      }
     buf ^= 1;
   }
   // partial tile, accumulator layout: slab[z][tile][w][a][b][lane][r]
@@ -541,7 +600,8 @@ int launch_wgrad(WGrad g, int n_host, hipStream_t s) {
   g.nz = (n_host + g.spb - 1) / g.spb;
   g.n = n_host;
   g.rs_slab = (g.bsum || g.bsum2) ? g.slab + (size_t)WG_MAX_Z * 4 * WG_TILE_FLOATS : nullptr;
-  hipLaunchKernelGGL(k_wgrad, dim3(ti, tj, g.nz), dim3(256), 0, s, g);
+  if (g.x3) hipLaunchKernelGGL(k_wgrad<true>, dim3(ti, tj, g.nz), dim3(256), 0, s, g);
+  else hipLaunchKernelGGL(k_wgrad<false>, dim3(ti, tj, g.nz), dim3(256), 0, s, g);
   const int nred = g.tiles * 4 * 16 * 64 * ((g.nz + WG_ZG - 1) / WG_ZG);
   const int nthr = nred > 256 ? nred : 256;
   hipLaunchKernelGGL(k_wgrad_reduce, dim3((nthr + 255) / 256), dim3(256), 0, s, g);

@@ -61,6 +61,7 @@ struct RGemmSeg {
   long ldb;
   int bcol;
   int rows;
+  long lo_off;  // elements from B to the same rows of the lo image (x3)
 };
 struct RGemm {
   int M;
@@ -76,6 +77,7 @@ struct RGemm {
   long ldm;
   int accumulate;
   int vec_out;  // set by launch_rgemm: C (and mask) rows 16-B addressable, N % 4 == 0
+  int x3;       // split-bf16 products (fp32-level): activations hi/lo, weights hi/lo images
 };
 void launch_rgemm(const RGemm& g, int M_host, hipStream_t s);
 // bf16 weight images of the training GEMM weights: forward (rows = outputs, k = used input columns,
@@ -87,6 +89,7 @@ struct WView {
   long ldb;
   int bcol;
   int rows;
+  long lo_off;
 };
 bool wimg_view(const void* base, const float* const* t, const float* W, int c0, int K, bool bwd, WView* v);
 
@@ -110,6 +113,7 @@ struct WGrad {
   float* slab;
   float* rs_slab;
   int spb, nz, tiles, tj;
+  int x3;  // split-bf16 products (fp32-level)
 };
 size_t wgrad_slab_floats();
 int launch_wgrad(WGrad g, int n_host, hipStream_t s);

@@ -73,13 +73,14 @@ struct Exec {
   const void* wimg = nullptr;          // bf16 weight images (anr_tgemm.hip), packed for this call
   const float* const* pt = nullptr;    // the parameter tensors the images were packed from
   float* wslab = nullptr;              // weight-gradient partial slabs (anr_tgemm.hip k_wgrad)
+  int x3 = 0;  // inside the pose scope of ANR_BF16: split-bf16 (fp32-level) row GEMMs instead of fp32
 
   // the bf16 row GEMM when every operand fits it (anr_train.h RGemm); false: use the generic kernel
   bool row_seg(RGemmSeg& q, const float* A, long lda, int K, const float* W, int c0, bool bwd) {
     if (!A || K <= 0 || lda % 4 != 0 || ((uintptr_t)A & 15) != 0 || lda < (long)((K + 63) / 64 * 64)) return false;
     WView v;
     if (!wimg_view(wimg, pt, W, c0, K, bwd, &v)) return false;
-    q = RGemmSeg{A, lda, K, v.B, v.ldb, v.bcol, v.rows};
+    q = RGemmSeg{A, lda, K, v.B, v.ldb, v.bcol, v.rows, v.lo_off};
     return true;
   }
   int rgemm(RGemm& g) {
@@ -102,8 +103,9 @@ struct Exec {
   // Y[n][Nout] = act( X0[:, :K0] W[:, c0:c0+K0]^T (+ X1 W[:, c1:c1+K1]^T) + bias )
   int fwd(float* Y, int ldY, int Nout, const float* W, int in_ch, const float* bias, bool relu, const float* X0, int ld0,
           int K0, int c0, const float* X1 = nullptr, int ld1 = 0, int K1 = 0, int c1 = 0) {
-    if (bf16 && wimg && Nout <= 256) {
+    if ((bf16 || x3) && wimg && Nout <= 256) {
       RGemm r{};
+      r.x3 = bf16 ? 0 : 1;
       r.N = Nout;
       r.nseg = X1 ? 2 : 1;
       if (row_seg(r.seg[0], X0, ld0, K0, W, c0, false) && (!X1 || row_seg(r.seg[1], X1, ld1, K1, W, c1, false))) {
@@ -124,9 +126,10 @@ struct Exec {
   // gradient) are added into bsum (and bsum2) in the same pass when given
   int wgrad(float* dW, int in_ch, int c0, int Nout, const float* dY, int ldY, const float* X, int ldX, int K,
             float* bsum = nullptr, float* bsum2 = nullptr) {
-    if (bf16 && wslab && Nout <= 256 && K <= 256 && ldY % 4 == 0 && ldX % 4 == 0 && ((uintptr_t)dY & 15) == 0 &&
+    if ((bf16 || x3) && wslab && Nout <= 256 && K <= 256 && ldY % 4 == 0 && ldX % 4 == 0 && ((uintptr_t)dY & 15) == 0 &&
         ((uintptr_t)X & 15) == 0 && n > 0) {
       WGrad w{};
+      w.x3 = bf16 ? 0 : 1;
       w.dY = dY; w.ldY = ldY; w.nout = Nout; w.X = X; w.ldX = ldX; w.K = K;
       w.dW = dW + c0; w.ldw = in_ch; w.bsum = bsum; w.bsum2 = bsum2; w.slab = wslab;
       if (launch_wgrad(w, n, s) != 0) return check_launch("k_wgrad");
@@ -147,8 +150,9 @@ struct Exec {
   int xgrad(float* dX, int ldX, int K, const float* dY, int ldY, int Nout, const float* W, int in_ch, int c0,
             const float* mask, int ldm, bool accumulate, const float* dY2 = nullptr, int ldY2 = 0, int Nout2 = 0,
             const float* W2 = nullptr, int in_ch2 = 0) {
-    if (bf16 && wimg && K <= 256) {
+    if ((bf16 || x3) && wimg && K <= 256) {
       RGemm r{};
+      r.x3 = bf16 ? 0 : 1;
       r.N = K;
       r.nseg = dY2 ? 2 : 1;
       if (row_seg(r.seg[0], dY, ldY, Nout, W, c0, true) && (!dY2 || row_seg(r.seg[1], dY2, ldY2, Nout2, W2, c0, true)) &&
@@ -173,9 +177,15 @@ struct PoseScope {
   Exec& e;
   int keep;
   explicit PoseScope(Exec& x) : e(x), keep(x.bf16) {
-    if (e.pose_fp32) e.bf16 = 0;
+    if (e.pose_fp32) {
+      e.bf16 = 0;
+      e.x3 = 1;
+    }
   }
-  ~PoseScope() { e.bf16 = keep; }
+  ~PoseScope() {
+    e.bf16 = keep;
+    e.x3 = 0;
+  }
 };
 
 // bf16 weight images for the row GEMM (bf16 policies only; refreshed on every call, the weights may
