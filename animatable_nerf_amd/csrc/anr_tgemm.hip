@@ -159,16 +159,19 @@ bool wimg_view(const void* base, const float* const* t, const float* W, int c0, 
 // ------------------------------------------------------------------------------------------
 // the row GEMM
 // ------------------------------------------------------------------------------------------
-#define RG_BM 64
-#define RG_A_BYTES (RG_BM * 64 * 4)   // fp32 activations, 64 rows x 64 k
 #define RG_B_BYTES (256 * 64 * 2)     // bf16 weight rows, 256 rows x 64 k
-#define RG_PIECES_A (RG_A_BYTES / 1024 / 4)  // per wave
-#define RG_PIECES_B (RG_B_BYTES / 1024 / 4)
-// X3 (split-bf16, fp32-level: lo*h + h*lo + h*h): the weight rows' lo image rides in the same slot
+// bf16: 128 rows per workgroup (8 waves = 2 row groups x 4 column groups of 64), 2-slot ring, so the
+// weight image each workgroup streams serves twice the rows; X3 (split-bf16, fp32-level: lo*h + h*lo
+// + h*h, the weight rows' lo image riding in the same slot): 64 rows, 4 waves, 2 slots
 template <bool X3> struct RgCfg {
-  static constexpr int NS = X3 ? 2 : 3;                                // ring slots
-  static constexpr int SLOT = RG_A_BYTES + RG_B_BYTES * (X3 ? 2 : 1);  // bytes per slot
-  static constexpr int OPS = RG_PIECES_A + RG_PIECES_B * (X3 ? 2 : 1); // vmem ops per wave per chunk
+  static constexpr int BM = X3 ? 64 : 128;
+  static constexpr int WAVES = BM / 16;
+  static constexpr int A_BYTES = BM * 64 * 4;                          // fp32 activations, BM rows x 64 k
+  static constexpr int NS = 2;                                         // ring slots
+  static constexpr int SLOT = A_BYTES + RG_B_BYTES * (X3 ? 2 : 1);     // bytes per slot
+  static constexpr int PIECES_A = A_BYTES / 1024 / WAVES;              // per wave
+  static constexpr int PIECES_B = RG_B_BYTES / 1024 / WAVES;
+  static constexpr int OPS = PIECES_A + PIECES_B * (X3 ? 2 : 1);       // vmem ops per wave per chunk
 };
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
@@ -193,11 +196,12 @@ __device__ __forceinline__ void rg_issue(const RGemm& g, int seg, int kk, int m0
   const long ldb = seg ? g.seg[1].ldb : g.seg[0].ldb;
   const int bcol = seg ? g.seg[1].bcol : g.seg[0].bcol;
   const int brows = seg ? g.seg[1].rows : g.seg[0].rows;
-  // A: 64 rows x 256 B; piece p = 4 rows; lane -> row 4p + (lane >> 4), LDS chunk (lane & 15) holds
+  // A: BM rows x 256 B; piece p = 4 rows; lane -> row 4p + (lane >> 4), LDS chunk (lane & 15) holds
   // source chunk (lane & 15) ^ (row & 15)
+  using C = RgCfg<X3>;
 #pragma unroll
-  for (int i = 0; i < RG_PIECES_A; ++i) {
-    const int p = w + 4 * i;
+  for (int i = 0; i < C::PIECES_A; ++i) {
+    const int p = w + C::WAVES * i;
     const int r = 4 * p + (lane >> 4);
     const int gr = min(m0 + r, M - 1);
     const int ch = (lane & 15) ^ (r & 15);
@@ -205,30 +209,31 @@ __device__ __forceinline__ void rg_issue(const RGemm& g, int seg, int kk, int m0
   }
   // B: 256 rows x 128 B; piece p = 8 rows; lane -> row 8p + (lane >> 3), chunk (lane & 7) ^ (row & 7)
 #pragma unroll
-  for (int i = 0; i < RG_PIECES_B; ++i) {
-    const int p = w + 4 * i;
+  for (int i = 0; i < C::PIECES_B; ++i) {
+    const int p = w + C::WAVES * i;
     const int r = 8 * p + (lane >> 3);
     const int br = min(r, brows - 1);
     const int ch = (lane & 7) ^ (r & 7);
-    rg_dma(B + (long)br * ldb + bcol + kk + ch * 8, slot_lds + RG_A_BYTES + p * 1024);
+    rg_dma(B + (long)br * ldb + bcol + kk + ch * 8, slot_lds + C::A_BYTES + p * 1024);
   }
   if constexpr (X3) {
     const long lo = seg ? g.seg[1].lo_off : g.seg[0].lo_off;
 #pragma unroll
-    for (int i = 0; i < RG_PIECES_B; ++i) {
-      const int p = w + 4 * i;
+    for (int i = 0; i < C::PIECES_B; ++i) {
+      const int p = w + C::WAVES * i;
       const int r = 8 * p + (lane >> 3);
       const int br = min(r, brows - 1);
       const int ch = (lane & 7) ^ (r & 7);
-      rg_dma(B + lo + (long)br * ldb + bcol + kk + ch * 8, slot_lds + RG_A_BYTES + RG_B_BYTES + p * 1024);
+      rg_dma(B + lo + (long)br * ldb + bcol + kk + ch * 8, slot_lds + C::A_BYTES + RG_B_BYTES + p * 1024);
     }
   }
   (void)N;
 }
 
 template <bool X3>
-__global__ __launch_bounds__(256) void k_rgemm(RGemm g) {
+__global__ __launch_bounds__(RgCfg<X3>::WAVES * 64) void k_rgemm(RGemm g) {
   constexpr int RG_NS = RgCfg<X3>::NS, RG_SLOT = RgCfg<X3>::SLOT, RG_OPS = RgCfg<X3>::OPS;
+  constexpr int RG_BM = RgCfg<X3>::BM, RG_A_BYTES = RgCfg<X3>::A_BYTES;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int M = g.M_dev ? *g.M_dev : g.M;
   const int N = g.N;
@@ -254,7 +259,9 @@ __global__ __launch_bounds__(256) void k_rgemm(RGemm g) {
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const bool active = 64 * w < N;  // this wave's 64 output columns hold some of the N
+  const int wr = (w >> 2) * 64;   // this wave's 64 rows of the tile
+  const int wc = (w & 3) * 64;    // and 64 output columns
+  const bool active = wc < N;     // which hold some of the N
   const int sw = lane & 7;         // row & 7 of every fragment row this lane reads (rows 16i + (lane & 15))
 
   for (int c = 0; c < nch; ++c) {
@@ -280,7 +287,7 @@ __global__ __launch_bounds__(256) void k_rgemm(RGemm g) {
         const int kc = 4 * ks + (lane >> 4);  // 8-element k group of this lane
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const int r = 16 * i + (lane & 15);
+          const int r = wr + 16 * i + (lane & 15);
           // fp32 row r, k = 8 kc .. 8 kc + 7: 16-B chunks 2 kc, 2 kc + 1 (swizzled by r & 15)
           const f32x4 x0 = *(const f32x4*)(sA + r * 256 + (((2 * kc) ^ (r & 15)) * 16));
           const f32x4 x1 = *(const f32x4*)(sA + r * 256 + (((2 * kc + 1) ^ (r & 15)) * 16));
@@ -297,7 +304,7 @@ __global__ __launch_bounds__(256) void k_rgemm(RGemm g) {
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const int r = 64 * w + 16 * j + (lane & 15);
+          const int r = wc + 16 * j + (lane & 15);
           bfr[j] = *(const bf16x8_t*)(sB + r * 128 + ((kc ^ sw) * 16));
           if constexpr (X3) bl[j] = *(const bf16x8_t*)(sB + RG_B_BYTES + r * 128 + ((kc ^ sw) * 16));
         }
@@ -330,15 +337,15 @@ __global__ __launch_bounds__(256) void k_rgemm(RGemm g) {
     f32x4 cv[4][4], mk[4][4], bj[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int n = min(64 * w + 16 * j + 4 * (lane >> 4), N - 4);
+      const int n = min(wc + 16 * j + 4 * (lane >> 4), N - 4);
       bj[j] = g.bias ? *(const f32x4*)(g.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const long m = min(m0 + 16 * i + (lane & 15), M - 1);
-        const int n = min(64 * w + 16 * j + 4 * (lane >> 4), N - 4);
+        const long m = min(m0 + wr + 16 * i + (lane & 15), M - 1);
+        const int n = min(wc + 16 * j + 4 * (lane >> 4), N - 4);
         if (g.accumulate) cv[i][j] = *(const f32x4*)(g.C + m * g.ldc + n);
         if (g.mask) mk[i][j] = *(const f32x4*)(g.mask + m * g.ldm + n);
       }
@@ -346,8 +353,8 @@ __global__ __launch_bounds__(256) void k_rgemm(RGemm g) {
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int m = m0 + 16 * i + (lane & 15);
-        const int n = 64 * w + 16 * j + 4 * (lane >> 4);
+        const int m = m0 + wr + 16 * i + (lane & 15);
+        const int n = wc + 16 * j + 4 * (lane >> 4);
         f32x4 v = acc[i][j];
         if (g.bias) v += bj[j];
         if (g.accumulate) v += cv[i][j];
@@ -369,8 +376,8 @@ __global__ __launch_bounds__(256) void k_rgemm(RGemm g) {
     for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int m = m0 + 16 * i + (lane & 15);
-        const int n = 64 * w + 16 * j + 4 * (lane >> 4) + r;
+        const int m = m0 + wr + 16 * i + (lane & 15);
+        const int n = wc + 16 * j + 4 * (lane >> 4) + r;
         if (m >= M || n >= N) continue;
         float v = acc[i][j][r];
         float* cp = g.C + (long)m * g.ldc + n;
@@ -397,9 +404,12 @@ void launch_rgemm(const RGemm& g0, int M_host, hipStream_t s) {
                               (int)rgemm_lds_bytes<true>());
     attr = true;
   }
-  const dim3 grid((M_host + RG_BM - 1) / RG_BM);
-  if (g.x3) hipLaunchKernelGGL(k_rgemm<true>, grid, dim3(256), rgemm_lds_bytes<true>(), s, g);
-  else hipLaunchKernelGGL(k_rgemm<false>, grid, dim3(256), rgemm_lds_bytes<false>(), s, g);
+  if (g.x3)
+    hipLaunchKernelGGL(k_rgemm<true>, dim3((M_host + RgCfg<true>::BM - 1) / RgCfg<true>::BM),
+                       dim3(RgCfg<true>::WAVES * 64), rgemm_lds_bytes<true>(), s, g);
+  else
+    hipLaunchKernelGGL(k_rgemm<false>, dim3((M_host + RgCfg<false>::BM - 1) / RgCfg<false>::BM),
+                       dim3(RgCfg<false>::WAVES * 64), rgemm_lds_bytes<false>(), s, g);
 }
 
 }  // namespace anr
