@@ -480,9 +480,10 @@ __device__ __forceinline__ void wg_store(unsigned short* S, unsigned short* SL, 
 
 template <bool X3>
 __global__ __launch_bounds__(256) void k_wgrad(WGrad g) {
-  constexpr int NI = X3 ? 2 : 1;  // images per operand: hi (and lo)
-  __shared__ __attribute__((aligned(16))) unsigned short sY[2][NI][WG_S * WG_LD];
-  __shared__ __attribute__((aligned(16))) unsigned short sX[2][NI][WG_S * WG_LD];
+  constexpr int NI = X3 ? 2 : 1;   // images per operand: hi (and lo)
+  constexpr int NH = X3 ? 1 : 2;   // 32-sample halves per step (bf16: 64 samples, two MFMA k-steps)
+  __shared__ __attribute__((aligned(16))) unsigned short sY[2][NI][NH * WG_S * WG_LD];
+  __shared__ __attribute__((aligned(16))) unsigned short sX[2][NI][NH * WG_S * WG_LD];
   __shared__ float srs[8][WG_T];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int ti = blockIdx.x, tj = blockIdx.y, z = blockIdx.z;
@@ -497,45 +498,53 @@ __global__ __launch_bounds__(256) void k_wgrad(WGrad g) {
     for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
   f32x4 rsum = {0.f, 0.f, 0.f, 0.f};  // column sums of this thread's dY share (tile row 0 only)
   const bool do_rs = g.rs_slab != nullptr && tj == 0;
-  f32x4 vy[4], vx[4];
-  if (s0 < s1) {
-    wg_load(g.dY, g.ldY, g.nout, i0, s0, s1, tid, vy);
-    wg_load(g.X, g.ldX, g.K, j0, s0, s1, tid, vx);
-  }
+  f32x4 vy[NH][4], vx[NH][4];
+  auto load = [&](int s) {
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+      wg_load(g.dY, g.ldY, g.nout, i0, s + h * WG_S, s1, tid, vy[h]);
+      wg_load(g.X, g.ldX, g.K, j0, s + h * WG_S, s1, tid, vx[h]);
+    }
+  };
+  constexpr int STEP = NH * WG_S;
+  if (s0 < s1) load(s0);
   int buf = 0;
-  for (int s = s0; s < s1; s += WG_S) {
-    if (do_rs) {
+  for (int s = s0; s < s1; s += STEP) {
 #pragma unroll
-      for (int h = 0; h < 4; ++h) rsum += vy[h];
+    for (int h = 0; h < NH; ++h) {
+      if (do_rs) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) rsum += vy[h][q];
+      }
+      wg_store<X3>(sY[buf][0] + h * WG_S * WG_LD, sY[buf][NI - 1] + h * WG_S * WG_LD, tid, vy[h]);
+      wg_store<X3>(sX[buf][0] + h * WG_S * WG_LD, sX[buf][NI - 1] + h * WG_S * WG_LD, tid, vx[h]);
     }
-    wg_store<X3>(sY[buf][0], sY[buf][NI - 1], tid, vy);
-    wg_store<X3>(sX[buf][0], sX[buf][NI - 1], tid, vx);
     __syncthreads();
-    if (s + WG_S < s1) {  // the next step's operands load while this step's MFMAs run
-      wg_load(g.dY, g.ldY, g.nout, i0, s + WG_S, s1, tid, vy);
-      wg_load(g.X, g.ldX, g.K, j0, s + WG_S, s1, tid, vx);
-    }
-    bf16x8_t fa[4], fb[4], la[4], lb[4];
+    if (s + STEP < s1) load(s + STEP);  // the next step's operands load while this step's MFMAs run
 #pragma unroll
-    for (int a = 0; a < 4; ++a) {
-      fa[a] = wg_frag(sY[buf][0], wi + 16 * a, lane);
-      if constexpr (X3) la[a] = wg_frag(sY[buf][NI - 1], wi + 16 * a, lane);
-    }
+    for (int h = 0; h < NH; ++h) {
+      bf16x8_t fa[4], fb[4], la[4], lb[4];
 #pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      fb[b] = wg_frag(sX[buf][0], wj + 16 * b, lane);
-      if constexpr (X3) lb[b] = wg_frag(sX[buf][NI - 1], wj + 16 * b, lane);
-    }
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
+      for (int a = 0; a < 4; ++a) {
+        fa[a] = wg_frag(sY[buf][0] + h * WG_S * WG_LD, wi + 16 * a, lane);
+        if constexpr (X3) la[a] = wg_frag(sY[buf][NI - 1] + h * WG_S * WG_LD, wi + 16 * a, lane);
+      }
 #pragma unroll
       for (int b = 0; b < 4; ++b) {
-        if constexpr (X3) {
-          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(la[a], fb[b], acc[a][b], 0, 0, 0);
-          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a], lb[b], acc[a][b], 0, 0, 0);
-        }
-        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a], fb[b], acc[a][b], 0, 0, 0);
+        fb[b] = wg_frag(sX[buf][0] + h * WG_S * WG_LD, wj + 16 * b, lane);
+        if constexpr (X3) lb[b] = wg_frag(sX[buf][NI - 1] + h * WG_S * WG_LD, wj + 16 * b, lane);
       }
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          if constexpr (X3) {
+            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(la[a], fb[b], acc[a][b], 0, 0, 0);
+            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a], lb[b], acc[a][b], 0, 0, 0);
+          }
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a], fb[b], acc[a][b], 0, 0, 0);
+        }
+    }
     buf ^= 1;
   }
   // partial tile, accumulator layout: slab[z][tile][w][a][b][lane][r]
@@ -606,7 +615,7 @@ int launch_wgrad(WGrad g, int n_host, hipStream_t s) {
   // samples per workgroup: enough workgroups to cover the CUs, at most WG_MAX_Z slabs
   int nz = (n_host + 383) / 384;
   nz = nz < 1 ? 1 : (nz > WG_MAX_Z ? WG_MAX_Z : nz);
-  g.spb = ((n_host + nz - 1) / nz + WG_S - 1) / WG_S * WG_S;
+  g.spb = ((n_host + nz - 1) / nz + 2 * WG_S - 1) / (2 * WG_S) * (2 * WG_S);  // whole 64-sample steps
   g.nz = (n_host + g.spb - 1) / g.spb;
   g.n = n_host;
   g.rs_slab = (g.bsum || g.bsum2) ? g.slab + (size_t)WG_MAX_Z * 4 * WG_TILE_FLOATS : nullptr;
