@@ -161,7 +161,99 @@ __device__ __forceinline__ void epilogue(const GemmArgs& g, const f32x4 (&acc)[2
       }
 }
 
-template <bool A_K, bool B_K>
+// epilogue of the swapped product (non-atomic launches): the MFMAs take the B fragment as their A
+// operand, so lane l holds C[m0 + wr + 16 i + (l & 15)][n0 + wc + 16 j + 4 (l >> 4) + r], r = 0..3 —
+// four consecutive columns of one row, finished and stored as one 16-B access when every operand is
+// 16-B addressable (g.vec_out). All operand loads precede the first use.
+__device__ __forceinline__ void epilogue_sw(const GemmArgs& g, const f32x4 (&acc)[2][2], int M, int m0, int n0, int wr,
+                                            int wc, int lane) {
+#ifdef RG_EXP_NOEPI
+  if (acc[0][0][0] != 12345.f) return;  // timing experiment only
+#endif
+  if (g.vec_out) {
+    f32x4 bj[2], cv[2][2], mk[2][2], sp[2][2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = min(n0 + wc + 16 * j + 4 * (lane >> 4), g.N - 4);
+      bj[j] = g.bias ? *(const f32x4*)(g.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const long m = min(m0 + wr + 16 * i + (lane & 15), M - 1);
+        const int n = min(n0 + wc + 16 * j + 4 * (lane >> 4), g.N - 4);
+        if (g.accumulate) cv[i][j] = *(const f32x4*)(g.C + m * g.ldc + n);
+        if (g.mask) mk[i][j] = *(const f32x4*)(g.mask + m * g.ldm + n);
+        if (g.spd) sp[i][j] = *(const f32x4*)(g.spd + m * g.ldsd + n);
+      }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int m = m0 + wr + 16 * i + (lane & 15);
+        const int n = n0 + wc + 16 * j + 4 * (lane >> 4);
+        if (m >= M || n >= g.N) continue;
+        f32x4 v = acc[i][j], dv;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float x = v[e];
+          if (g.bias) x += bj[j][e];
+          if (g.accumulate) x += cv[i][j][e];
+          if (g.div_pre != 0.f) x = x / g.div_pre;
+          if (g.relu) x = fmaxf(x, 0.f);
+          if (g.softplus) {  // torch softplus(beta=100, threshold=20) and the factor its backward uses
+            const float z = x * 100.f;
+            const float ez = expf(z);
+            dv[e] = z > 20.f ? -1.f : ez;
+            x = z > 20.f ? x : log1pf(ez) / 100.f;
+          }
+          if (g.spd && n + e < g.spd_n) {
+            const float d = sp[i][j][e];
+            if (d >= 0.f) x = x * d / (d + 1.f);
+          }
+          if (g.mask && !(mk[i][j][e] > 0.f)) x = 0.f;
+          if (g.div_post != 0.f) x = x / g.div_post;
+          v[e] = x;
+        }
+        if (g.softplus) *(f32x4*)(g.deriv + (long)m * g.ldd + n) = dv;
+        *(f32x4*)(g.C + (long)m * g.ldc + n) = v;
+      }
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wr + 16 * i + (lane & 15);
+        const int n = n0 + wc + 16 * j + 4 * (lane >> 4) + r;
+        if (m >= M || n >= g.N) continue;
+        float v = acc[i][j][r];
+        float* c = g.C + (long)m * g.ldc + n;
+        if (g.bias) v += g.bias[n];
+        if (g.accumulate) v += *c;
+        if (g.div_pre != 0.f) v = v / g.div_pre;
+        if (g.relu) v = fmaxf(v, 0.f);
+        if (g.softplus) {
+          const float z = v * 100.f;
+          const float e = expf(z);
+          g.deriv[(long)m * g.ldd + n] = z > 20.f ? -1.f : e;
+          v = z > 20.f ? v : log1pf(e) / 100.f;
+        }
+        if (g.spd && n < g.spd_n) {
+          const float d = g.spd[(long)m * g.ldsd + n];
+          if (d >= 0.f) v = v * d / (d + 1.f);
+        }
+        if (g.mask && !(g.mask[(long)m * g.ldm + n] > 0.f)) v = 0.f;
+        if (g.div_post != 0.f) v = v / g.div_post;
+        *c = v;
+      }
+}
+
+// SW: the swapped MFMA operand order and epilogue_sw (non-atomic launches)
+template <bool A_K, bool B_K, bool SW>
 __global__ __launch_bounds__(256) void k_gemm_t(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) float As[GBK][GLD];
   __shared__ __attribute__((aligned(16))) float Bs[GBK][GLD];
@@ -225,7 +317,9 @@ __global__ __launch_bounds__(256) void k_gemm_t(GemmArgs g) {
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = SW ? __builtin_amdgcn_mfma_f32_16x16x4f32(b[j], a[i], acc[i][j], 0, 0, 0)
+                         : __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b[j], acc[i][j], 0, 0, 0);
     }
     __syncthreads();
     if (!more) break;
@@ -234,7 +328,8 @@ __global__ __launch_bounds__(256) void k_gemm_t(GemmArgs g) {
     kend = (g.ksplit > 1) ? ke : g.seg[s].K;
   }
   if (do_rsum) rowsum_flush(g, m0, rsum);
-  epilogue(g, acc, M, m0, n0, wr, wc, lane);
+  if constexpr (SW) epilogue_sw(g, acc, M, m0, n0, wr, wc, lane);
+  else epilogue(g, acc, M, m0, n0, wr, wc, lane);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -358,7 +453,7 @@ __device__ __forceinline__ bf16x8 frag16(const unsigned short* S, int rb, int ks
 
 // X3 (render precision bf16x3, the sdf_pdf GEMMs): hi/lo images of both operands and three MFMAs per
 // fragment pair, lo*bh + hi*bl + hi*bh, fp32 accumulation (~2^-16 relative per product).
-template <bool A_K, bool B_K, bool X3>
+template <bool A_K, bool B_K, bool X3, bool SW>
 __global__ __launch_bounds__(256) void k_gemm_b(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) unsigned short As[(X3 ? 2 : 1) * GBM * BLD];
   __shared__ __attribute__((aligned(16))) unsigned short Bs[(X3 ? 2 : 1) * GBN * BLD];
@@ -426,14 +521,21 @@ __global__ __launch_bounds__(256) void k_gemm_b(GemmArgs g) {
         for (int i = 0; i < 2; ++i)
 #pragma unroll
           for (int j = 0; j < 2; ++j) {
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], b[j], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], bl[j], acc[i][j], 0, 0, 0);
+            if constexpr (SW) {
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], al[i], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl[j], a[i], acc[i][j], 0, 0, 0);
+            } else {
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], b[j], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], bl[j], acc[i][j], 0, 0, 0);
+            }
           }
       }
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = SW ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0)
+                         : __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
     }
     __syncthreads();
     if (!more) break;
@@ -442,20 +544,43 @@ __global__ __launch_bounds__(256) void k_gemm_b(GemmArgs g) {
     kend = (g.ksplit > 1) ? ke : g.seg[s].K;
   }
   if (do_rsum) rowsum_flush(g, m0, rsum);
-  epilogue(g, acc, M, m0, n0, wr, wc, lane);
+  if constexpr (SW) epilogue_sw(g, acc, M, m0, n0, wr, wc, lane);
+  else epilogue(g, acc, M, m0, n0, wr, wc, lane);
 }
 
-template __global__ void k_gemm_b<true, true, false>(GemmArgs);
-template __global__ void k_gemm_b<true, false, false>(GemmArgs);
-template __global__ void k_gemm_b<false, true, false>(GemmArgs);
-template __global__ void k_gemm_b<false, false, false>(GemmArgs);
-template __global__ void k_gemm_b<true, true, true>(GemmArgs);
-template __global__ void k_gemm_b<true, false, true>(GemmArgs);
+#define ANR_GEMM_INST(SW)                                            \
+  template __global__ void k_gemm_b<true, true, false, SW>(GemmArgs);  \
+  template __global__ void k_gemm_b<true, false, false, SW>(GemmArgs); \
+  template __global__ void k_gemm_b<false, true, false, SW>(GemmArgs); \
+  template __global__ void k_gemm_b<false, false, false, SW>(GemmArgs); \
+  template __global__ void k_gemm_b<true, true, true, SW>(GemmArgs);   \
+  template __global__ void k_gemm_b<true, false, true, SW>(GemmArgs);  \
+  template __global__ void k_gemm_t<true, true, SW>(GemmArgs);         \
+  template __global__ void k_gemm_t<true, false, SW>(GemmArgs);        \
+  template __global__ void k_gemm_t<false, true, SW>(GemmArgs);        \
+  template __global__ void k_gemm_t<false, false, SW>(GemmArgs);
+ANR_GEMM_INST(false)
+ANR_GEMM_INST(true)
 
-template __global__ void k_gemm_t<true, true>(GemmArgs);
-template __global__ void k_gemm_t<true, false>(GemmArgs);
-template __global__ void k_gemm_t<false, true>(GemmArgs);
-template __global__ void k_gemm_t<false, false>(GemmArgs);
+template <bool SW>
+static void launch_gemm_sw(const GemmArgs& g, dim3 grid, hipStream_t s, bool a_k, bool b_k) {
+  if (g.x3 && a_k) {  // split-bf16 (the sdf_pdf forward and input-gradient GEMMs)
+    if (b_k) hipLaunchKernelGGL((k_gemm_b<true, true, true, SW>), grid, dim3(256), 0, s, g);
+    else hipLaunchKernelGGL((k_gemm_b<true, false, true, SW>), grid, dim3(256), 0, s, g);
+    return;
+  }
+  if (g.bf16) {
+    if (a_k && b_k) hipLaunchKernelGGL((k_gemm_b<true, true, false, SW>), grid, dim3(256), 0, s, g);
+    else if (a_k) hipLaunchKernelGGL((k_gemm_b<true, false, false, SW>), grid, dim3(256), 0, s, g);
+    else if (b_k) hipLaunchKernelGGL((k_gemm_b<false, true, false, SW>), grid, dim3(256), 0, s, g);
+    else hipLaunchKernelGGL((k_gemm_b<false, false, false, SW>), grid, dim3(256), 0, s, g);
+    return;
+  }
+  if (a_k && b_k) hipLaunchKernelGGL((k_gemm_t<true, true, SW>), grid, dim3(256), 0, s, g);
+  else if (a_k) hipLaunchKernelGGL((k_gemm_t<true, false, SW>), grid, dim3(256), 0, s, g);
+  else if (b_k) hipLaunchKernelGGL((k_gemm_t<false, true, SW>), grid, dim3(256), 0, s, g);
+  else hipLaunchKernelGGL((k_gemm_t<false, false, SW>), grid, dim3(256), 0, s, g);
+}
 
 // host-side dispatch on the operand layouts
 void launch_gemm(GemmArgs g, dim3 grid, hipStream_t s) {
@@ -471,22 +596,14 @@ void launch_gemm(GemmArgs g, dim3 grid, hipStream_t s) {
     g.a_vec[i] = ((uintptr_t)q.A % 16 == 0) && (a_stride % 4 == 0) && (a_k || q.a_rs == 1);
     g.b_vec[i] = ((uintptr_t)q.B % 16 == 0) && (b_stride % 4 == 0) && (b_k || q.b_cs == 1);
   }
-  if (g.x3 && a_k) {  // split-bf16 (the sdf_pdf forward and input-gradient GEMMs)
-    if (b_k) hipLaunchKernelGGL((k_gemm_b<true, true, true>), grid, dim3(256), 0, s, g);
-    else hipLaunchKernelGGL((k_gemm_b<true, false, true>), grid, dim3(256), 0, s, g);
-    return;
-  }
-  if (g.bf16) {
-    if (a_k && b_k) hipLaunchKernelGGL((k_gemm_b<true, true, false>), grid, dim3(256), 0, s, g);
-    else if (a_k) hipLaunchKernelGGL((k_gemm_b<true, false, false>), grid, dim3(256), 0, s, g);
-    else if (b_k) hipLaunchKernelGGL((k_gemm_b<false, true, false>), grid, dim3(256), 0, s, g);
-    else hipLaunchKernelGGL((k_gemm_b<false, false, false>), grid, dim3(256), 0, s, g);
-    return;
-  }
-  if (a_k && b_k) hipLaunchKernelGGL((k_gemm_t<true, true>), grid, dim3(256), 0, s, g);
-  else if (a_k) hipLaunchKernelGGL((k_gemm_t<true, false>), grid, dim3(256), 0, s, g);
-  else if (b_k) hipLaunchKernelGGL((k_gemm_t<false, true>), grid, dim3(256), 0, s, g);
-  else hipLaunchKernelGGL((k_gemm_t<false, false>), grid, dim3(256), 0, s, g);
+  // non-atomic launches: swapped product + vectorised epilogue where every operand is 16-B addressable
+  const bool sw = !g.atomic;
+  auto al16 = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
+  g.vec_out = sw && g.N % 4 == 0 && g.ldc % 4 == 0 && al16(g.C) && (!g.bias || al16(g.bias)) &&
+              (!g.mask || (g.ldm % 4 == 0 && al16(g.mask))) && (!g.spd || (g.ldsd % 4 == 0 && al16(g.spd))) &&
+              (!g.softplus || (g.ldd % 4 == 0 && al16(g.deriv)));
+  if (sw) launch_gemm_sw<true>(g, grid, s, a_k, b_k);
+  else launch_gemm_sw<false>(g, grid, s, a_k, b_k);
 }
 
 }  // namespace anr

@@ -46,6 +46,7 @@ struct GemmArgs {
   float* rowsum2;
   // per segment: the operand tiles may be read with 16-B loads (aligned base, stride a multiple of 4)
   int a_vec[2], b_vec[2];
+  int vec_out;  // set by launch_gemm: non-atomic epilogue with 16-B accesses
 };
 
 void launch_gemm(GemmArgs g, dim3 grid, hipStream_t s);
