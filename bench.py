@@ -64,9 +64,9 @@ def parse():
                          'training step (2 x 65,536 points, novel_pose_bw)')
     ap.add_argument('--voxel', type=float, default=0.005, help='mesh mode: cfg.voxel_size (aninerf_s9p.yaml:95)')
     ap.add_argument('--sdf-cpu-rays', type=int, default=2048)
-    ap.add_argument('--sdf-precision', choices=('fp32', 'bf16x3'), default='fp32',
-                    help='sdf mode GEMMs: exact fp32 MFMA, or split-bf16 (measured no faster: the sdf GEMMs '
-                         'are load-latency bound, not MFMA bound)')
+    ap.add_argument('--sdf-precision', choices=('fp32', 'bf16x3'), default='bf16x3',
+                    help='sdf mode GEMMs: exact fp32 MFMA, or split-bf16 (outputs held to the same tolerances by '
+                         'tests/test_gpu_sdf.py; 472 vs 559 ms per frame with the round-2 GEMM epilogue)')
     ap.add_argument('--no-exact', action='store_true', help='skip timing the other render precision')
     ap.add_argument('--shard-frame', action='store_true',
                     help='render: split ONE frame over the ranks by whole chunks and all-gather rgb/acc/depth '
