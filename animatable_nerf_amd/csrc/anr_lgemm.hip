@@ -1,0 +1,428 @@
+// anr_lgemm.hip — the split-bf16 layer GEMM of the sdf_pdf batches (config 5, precision 'bf16x3'):
+// C[M][N] = epi(sum_s A_s[M][K_s] B_s) with M up to 524,288 kept samples and one layer's weights.
+//
+// At this M the weights are tiny next to the activations, so each workgroup keeps the bf16 hi/lo
+// image of one column group (<= 128 output columns x <= 320 k) RESIDENT in LDS for the whole launch
+// and streams only activations: every wave owns 16-sample row tiles and reads each tile's fp32
+// activation fragments straight from HBM into registers one tile ahead (8 consecutive k of one
+// sample per lane — the MFMA B operand layout, two 16-B loads per k-step), splits them hi/lo in
+// registers and runs lo·hi + hi·lo + hi·hi v_mfma_f32_16x16x32_bf16 against the LDS fragments
+// (weights as the A operand, so a lane ends holding four consecutive output columns of one sample and
+// stores them as one 16-B store). No barriers after the image load: waves run independently, the
+// wave loop has no divergent control flow (the compiler's vmcnt waits stay exact, the next tile's
+// loads in flight across the MFMAs and the epilogue), and epilogues (softplus + its backward factor,
+// the softplus-backward multiply) overlap other waves' MFMAs. Products and epilogue order match
+// k_gemm_b<.., .., true> (anr_gemm.hip).
+#include <algorithm>
+
+#include "anr_common.h"
+#include "anr_train.h"
+
+namespace anr {
+
+namespace {
+
+typedef __bf16 lbf16x8 __attribute__((ext_vector_type(8)));
+
+#ifndef LG_PERM
+#define LG_PERM 0  // 1: lane group j's 8 k are columns 4j..4j+3 and 16+4j..16+4j+3 (64 contiguous B per load)
+#endif
+#ifndef LG_NT
+#define LG_NT 0    // 1: nontemporal output stores
+#endif
+
+// physical column (within a 32-deep k-step) of lane group j's fragment element e
+__host__ __device__ constexpr int lg_kcol(int j, int e) { return LG_PERM ? (e < 4 ? 4 * j + e : 16 + 4 * j + e - 4) : 8 * j + e; }
+
+constexpr int LG_WAVES = 8;
+constexpr int LG_FRAG = 1024;  // one 16x32 bf16 fragment image (64 lanes x 16 B)
+constexpr int LG_MAX_LDS = 160 * 1024;
+
+struct LSeg {
+  const float* A;
+  long lda;
+  int K;
+};
+
+struct LGemm {
+  LSeg seg[2];
+  int kst0, kst;     // k-steps (32 deep) of segment 0, of both
+  int M, N, G, bpg;  // rows, columns, column groups, workgroups per group
+  const uint4* img;  // [G][kst][NOB][hi, lo][64 lanes] 16-B fragments
+  float* C;
+  long ldc;
+  const float* bias;
+  int relu, softplus;
+  float* deriv;
+  long ldd;
+  const float* spd;
+  long ldsd;
+  int spd_n;
+  float div_pre, div_post;
+};
+
+struct LPack {
+  const float* B[2];
+  long b_rs[2], b_cs[2];
+  int K[2], kst0, kst, N, NOB;
+  long total;  // fragment elements of one hi (or lo) image
+  unsigned short* out;
+};
+
+__device__ __forceinline__ unsigned short lg_bf16_rne(float f) {
+  uint32_t u = __float_as_uint(f);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (unsigned short)(u >> 16);
+}
+
+// image element ((((g kst + ks) NOB + ob) 2 + hl) 64 + lane) 8 + e = weight (n, k), n = 16 (g NOB + ob)
+// + (lane & 15), k = 32 t + 8 (lane >> 4) + e of the segment holding k-step ks; zero past N / K_s
+__global__ void k_limg_pack(LPack p) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= p.total) return;
+  const int e = (int)(i & 7), lane = (int)((i >> 3) & 63);
+  const long f = i >> 9;  // fragment index (g, ks, ob)
+  const int ob = (int)(f % p.NOB);
+  const long gk = f / p.NOB;
+  const int ks = (int)(gk % p.kst), g = (int)(gk / p.kst);
+  const int s = ks >= p.kst0 ? 1 : 0;
+  const int kk = 32 * (ks - (s ? p.kst0 : 0)) + lg_kcol(lane >> 4, e);
+  const int n = 16 * (g * p.NOB + ob) + (lane & 15);
+  float v = 0.0f;
+  if (n < p.N && kk < p.K[s]) v = p.B[s][(long)kk * p.b_rs[s] + (long)n * p.b_cs[s]];
+  const unsigned short hi = lg_bf16_rne(v);
+  const unsigned short lo = lg_bf16_rne(v - __uint_as_float((uint32_t)hi << 16));
+  const long o = ((f * 2) * 64 + lane) * 8 + e;
+  p.out[o] = hi;
+  p.out[o + 512] = lo;
+}
+
+// exp(z) within ~2 ulp: exact-split exponent, v_exp_f32 on the reduced argument, ldexp (the
+// libm-accurate expf costs ~3x the instructions, and the softplus layers are VALU-bound on it)
+__device__ __forceinline__ float lg_exp(float z) {
+  const float n = rintf(z * 1.44269502f);
+  const float r = fmaf(z, 1.44269502f, -n) + z * 1.92596299e-8f;
+  return ldexpf(__builtin_amdgcn_exp2f(r), (int)n);
+}
+
+// log1p(e), e >= 0, within a few ulp: a 6-term series below 1/32, else log(u) e / (u - 1) with
+// u = 1 + e (Goldberg's correction of the rounding in u; u - 1 is exact)
+__device__ __forceinline__ float lg_log1p(float e) {
+  const float s = e * (1.f + e * (-0.5f + e * (0.333333343f + e * (-0.25f + e * (0.2f + e * -0.166666672f)))));
+  const float u = 1.f + e;
+  const float l = __builtin_amdgcn_logf(u) * 0.693147182f * (e * __builtin_amdgcn_rcpf(u - 1.f));
+  return e < 0.03125f ? s : l;
+}
+
+// epilogue of one 16-sample tile: lane holds C[16 t + (lane & 15)][n0 + 16 ob + 4 (lane >> 4) + r].
+// Bias comes from LDS, the softplus-backward factors were loaded before the tile's MFMAs (sp); the
+// epilogue issues no global loads, so the next tile's activation loads stay in flight across it.
+template <int NOB, bool SPD>
+__device__ __forceinline__ void lg_epilogue(const LGemm& g, const f32x4 (&acc)[NOB], const f32x4 (&sp)[NOB],
+                                            const float* bias_lds, int tile, int n0, int lane) {
+  const int m = tile * 16 + (lane & 15);
+  const bool row_ok = m < g.M;
+#pragma unroll
+  for (int ob = 0; ob < NOB; ++ob) {
+    const int nl = 16 * ob + 4 * (lane >> 4);
+    const int n = n0 + nl;
+    const f32x4 bv = *(const f32x4*)(bias_lds + nl);
+    f32x4 v = acc[ob], dv;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float x = v[e] + bv[e];
+      if (g.div_pre != 0.f) x = x / g.div_pre;
+      if (g.relu) x = fmaxf(x, 0.f);
+      if (g.softplus) {  // torch softplus(beta=100, threshold=20) and the factor its backward uses
+        const float z = x * 100.f;
+        const float ez = lg_exp(z);
+        dv[e] = z > 20.f ? -1.f : ez;
+        x = z > 20.f ? x : lg_log1p(ez) * 0.01f;
+      }
+      if constexpr (SPD) {
+        const float d = sp[ob][e];
+        if (n + e < g.spd_n && d >= 0.f) x = x * d / (d + 1.f);
+      }
+      if (g.div_post != 0.f) x = x / g.div_post;
+      v[e] = x;
+    }
+    if (!row_ok) continue;
+    float* c = g.C + (long)m * g.ldc + n;
+    float* d = g.deriv + (long)m * g.ldd + n;
+    if (n + 3 < g.N) {
+#if LG_NT
+      __builtin_nontemporal_store(v, (f32x4*)c);
+      if (g.softplus) __builtin_nontemporal_store(dv, (f32x4*)d);
+#else
+      *(f32x4*)c = v;
+      if (g.softplus) *(f32x4*)d = dv;
+#endif
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (n + e < g.N) {
+          c[e] = v[e];
+          if (g.softplus) d[e] = dv[e];
+        }
+    }
+  }
+}
+
+// the activation fragments of one 16-sample tile: k-step ks, lane -> sample 16 t + (lane & 15), k =
+// 32 ks' + 8 (lane >> 4) .. + 7 of the segment holding ks (rows past M read row M - 1, k groups
+// wholly past K read column 0; both masked later)
+template <int KST, int KST0, bool UNAL>
+__device__ __forceinline__ void lg_load_tile(const LGemm& g, f32x4 (&buf)[KST][2], int tile, int lane) {
+  const int m = min(tile * 16 + (lane & 15), g.M - 1);
+  const int j = lane >> 4;
+#pragma unroll
+  for (int ks = 0; ks < KST; ++ks) {
+    const bool s1 = ks >= KST0;
+    const float* A = s1 ? g.seg[1].A : g.seg[0].A;
+    const long lda = s1 ? g.seg[1].lda : g.seg[0].lda;
+    const int K = s1 ? g.seg[1].K : g.seg[0].K;
+    const int k0 = 32 * (ks - (s1 ? KST0 : 0));
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      int kc = k0 + lg_kcol(j, 4 * h);
+      kc = kc < K ? kc : 0;  // 4-groups wholly past K read column 0 (masked at use)
+      const float* p = A + (long)m * lda + kc;
+      if constexpr (UNAL) {  // a segment that is not 16-B addressable: 4-B loads
+#pragma unroll
+        for (int e = 0; e < 4; ++e) buf[ks][h][e] = p[e];
+      } else {
+        buf[ks][h] = *(const f32x4*)p;
+      }
+    }
+  }
+}
+
+template <int NOB, bool SPD>
+__device__ __forceinline__ void lg_load_spd(const LGemm& g, f32x4 (&sp)[NOB], int tile, int n0, int lane) {
+  if constexpr (SPD) {
+    const int m = min(tile * 16 + (lane & 15), g.M - 1);
+#pragma unroll
+    for (int ob = 0; ob < NOB; ++ob) {
+      const int n = min(n0 + 16 * ob + 4 * (lane >> 4), g.N - 4);
+      sp[ob] = *(const f32x4*)(g.spd + (long)m * g.ldsd + n);
+    }
+  }
+}
+
+// one tile: the factor loads of this tile and the activation loads of the next go out first, then the
+// MFMAs on `cur` (whose loads went out one tile earlier), then the epilogue
+template <int NOB, int KST, int KST0, bool SPD, bool UNAL>
+__device__ __forceinline__ void lg_tile(const LGemm& g, const f32x4 (&cur)[KST][2], f32x4 (&nxt)[KST][2], int tile,
+                                        int next, int n0, int lane, const unsigned char* lds, const float* bias_lds) {
+  f32x4 sp[NOB];
+  lg_load_spd<NOB, SPD>(g, sp, tile, n0, lane);
+  lg_load_tile<KST, KST0, UNAL>(g, nxt, next, lane);
+  f32x4 acc[NOB];
+#pragma unroll
+  for (int ob = 0; ob < NOB; ++ob) acc[ob] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int kg = lane >> 4;
+  // the weight fragments are the same every tile: launder their address so they are re-read from LDS
+  // per tile instead of being hoisted out of the tile loop into (spilled) registers
+  int frag_off = lane * 16;
+  asm volatile("" : "+v"(frag_off));
+#pragma unroll
+  for (int ks = 0; ks < KST; ++ks) {
+    const bool s1 = ks >= KST0;
+    const int K = s1 ? g.seg[1].K : g.seg[0].K;
+    const int k0 = 32 * (ks - (s1 ? KST0 : 0));
+    float x[8] = {cur[ks][0][0], cur[ks][0][1], cur[ks][0][2], cur[ks][0][3],
+                  cur[ks][1][0], cur[ks][1][1], cur[ks][1][2], cur[ks][1][3]};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) x[e] = (k0 + lg_kcol(kg, e) < K) ? x[e] : 0.0f;
+    lbf16x8 xh, xl;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      xh[e] = (__bf16)x[e];
+      xl[e] = (__bf16)(x[e] - (float)xh[e]);
+    }
+    const unsigned char* fr = lds + ks * NOB * 2 * LG_FRAG + frag_off;
+#pragma unroll
+    for (int ob = 0; ob < NOB; ++ob) {
+      const lbf16x8 wh = *(const lbf16x8*)(fr + (2 * ob) * LG_FRAG);
+      const lbf16x8 wl = *(const lbf16x8*)(fr + (2 * ob + 1) * LG_FRAG);
+      acc[ob] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl, xh, acc[ob], 0, 0, 0);
+      acc[ob] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, xl, acc[ob], 0, 0, 0);
+      acc[ob] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, xh, acc[ob], 0, 0, 0);
+    }
+  }
+  lg_epilogue<NOB, SPD>(g, acc, sp, bias_lds, tile, n0, lane);
+}
+
+template <int NOB, int KST, int KST0, bool SPD, bool UNAL>
+__global__ __launch_bounds__(LG_WAVES * 64) void k_lgemm(LGemm g) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  // workgroup -> (column group, rank): the workgroups of one rank sit on one XCD (blockIdx % 8), so
+  // the groups reading the same row tiles share that XCD's L2
+  const int b = blockIdx.x;
+  const int gi = (b >> 3) % g.G;
+  const int rank = (b / (8 * g.G)) * 8 + (b & 7);
+  const int n0 = 16 * NOB * gi;
+  constexpr int IMG = KST * NOB * 2 * LG_FRAG;
+  float* bias_lds = (float*)(lds + IMG);
+  {
+    const uint4* src = g.img + (long)gi * (IMG / 16);
+    uint4* dst = (uint4*)lds;
+    constexpr int N16 = IMG / 16, PER = (N16 + LG_WAVES * 64 - 1) / (LG_WAVES * 64);
+    uint4 t[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) t[j] = src[min((int)threadIdx.x + j * LG_WAVES * 64, N16 - 1)];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int i = threadIdx.x + j * LG_WAVES * 64;
+      if (i < N16) dst[i] = t[j];
+    }
+    if (threadIdx.x < 16 * NOB) {
+      const int n = n0 + threadIdx.x;
+      bias_lds[threadIdx.x] = (g.bias && n < g.N) ? g.bias[n] : 0.0f;
+    }
+  }
+  __syncthreads();
+  // wave-uniform cursors live in SGPRs: the loop below has no divergent control flow
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nw = g.bpg * LG_WAVES;
+  const int T = (g.M + 15) >> 4;
+  int t = rank * LG_WAVES + w;
+  if (t >= T) return;
+  f32x4 ba[KST][2], bb[KST][2];
+  lg_load_tile<KST, KST0, UNAL>(g, ba, t, lane);
+  while (true) {
+    lg_tile<NOB, KST, KST0, SPD, UNAL>(g, ba, bb, t, t + nw, n0, lane, lds, bias_lds);
+    t += nw;
+    if (t >= T) break;
+    lg_tile<NOB, KST, KST0, SPD, UNAL>(g, bb, ba, t, t + nw, n0, lane, lds, bias_lds);
+    t += nw;
+    if (t >= T) break;
+  }
+}
+
+size_t lg_lds_bytes(int kst, int nob) { return (size_t)kst * nob * 2 * LG_FRAG + (size_t)nob * 64; }
+
+// output columns per workgroup (16 x NOB) and column groups G for N outputs at kst k-steps
+int lg_nob(int N, int kst, int* G) {
+  const int tot = (N + 15) / 16;
+  for (int g = (tot + 7) / 8; g <= tot; ++g) {
+    const int need = (tot + g - 1) / g;
+    const int nob = need <= 1 ? 1 : need <= 4 ? 4 : need <= 6 ? 6 : 8;
+    if (lg_lds_bytes(kst, nob) <= (size_t)LG_MAX_LDS) {
+      *G = g;
+      return nob;
+    }
+  }
+  *G = tot;
+  return 1;
+}
+
+int lg_kst(const GemmArgs& g, int* kst0) {
+  *kst0 = (g.seg[0].K + 31) / 32;
+  return *kst0 + (g.nseg > 1 ? (g.seg[1].K + 31) / 32 : 0);
+}
+
+template <int NOB, int KST, int KST0, bool SPD, bool UNAL>
+void lg_launch(const LGemm& a, int cus, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)k_lgemm<NOB, KST, KST0, SPD, UNAL>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              LG_MAX_LDS);
+    attr = true;
+  }
+  LGemm g = a;
+  g.bpg = std::max(1, cus / (8 * g.G)) * 8;
+  hipLaunchKernelGGL((k_lgemm<NOB, KST, KST0, SPD, UNAL>), dim3((unsigned)(g.bpg * g.G)), dim3(LG_WAVES * 64),
+                     lg_lds_bytes(KST, NOB), s, g);
+}
+
+// the instantiated shapes (the sdf_pdf layers); false for any other
+bool lg_dispatch(const LGemm& a, int nob, bool spd, bool unal, int cus, hipStream_t s, bool launch) {
+#define LG_CASE(N_, K_, K0_, S_, U_)                                            \
+  if (nob == N_ && a.kst == K_ && a.kst0 == K0_ && spd == S_ && unal == U_) {   \
+    if (launch) lg_launch<N_, K_, K0_, S_, U_>(a, cus, s);                      \
+    return true;                                                                \
+  }
+  LG_CASE(8, 8, 8, false, false)
+  LG_CASE(8, 8, 8, true, false)
+  LG_CASE(8, 7, 7, true, false)
+  LG_CASE(8, 2, 2, false, false)
+  LG_CASE(6, 10, 2, false, false)
+  LG_CASE(6, 10, 2, false, true)
+  LG_CASE(6, 8, 8, false, false)
+  LG_CASE(4, 8, 8, false, false)
+  LG_CASE(1, 8, 8, false, false)
+#undef LG_CASE
+  return false;
+}
+
+bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+// some activation segment is not 16-B addressable (base or row stride): the 4-B load variant
+bool lg_unal(const GemmArgs& g) {
+  for (int s = 0; s < g.nseg; ++s)
+    if (!al16(g.seg[s].A) || g.seg[s].a_rs % 4 != 0) return true;
+  return false;
+}
+
+LGemm lg_args(const GemmArgs& g, int* nob) {
+  LGemm a{};
+  for (int i = 0; i < g.nseg; ++i) a.seg[i] = LSeg{g.seg[i].A, g.seg[i].a_rs, g.seg[i].K};
+  a.kst = lg_kst(g, &a.kst0);
+  a.M = g.M;
+  a.N = g.N;
+  *nob = lg_nob(g.N, a.kst, &a.G);
+  a.C = g.C; a.ldc = g.ldc; a.bias = g.bias; a.relu = g.relu; a.softplus = g.softplus; a.deriv = g.deriv;
+  a.ldd = g.ldd; a.spd = g.spd; a.ldsd = g.ldsd; a.spd_n = g.spd_n; a.div_pre = g.div_pre; a.div_post = g.div_post;
+  return a;
+}
+
+}  // namespace
+
+size_t lgemm_image_bytes(const GemmArgs& g) {
+  int G = 1, kst0 = 0;
+  const int kst = lg_kst(g, &kst0);
+  const int NOB = lg_nob(g.N, kst, &G);
+  return (size_t)G * kst * NOB * 2 * LG_FRAG;
+}
+
+bool lgemm_supported(const GemmArgs& g) {
+  if (!g.x3 || g.accumulate || g.atomic || g.mask || g.rowsum || g.rowsum2 || g.M_dev || g.ksplit > 1) return false;
+  if (g.N < 1 || (g.spd && g.N < 4) || g.M <= 0 || g.nseg < 1 || g.nseg > 2) return false;
+  for (int s = 0; s < g.nseg; ++s) {
+    const GemmSeg& q = g.seg[s];
+    if (q.a_cs != 1 || q.a_rs < (q.K + 7) / 8 * 8) return false;
+  }
+  if (!al16(g.C) || g.ldc % 4 != 0) return false;
+  if (g.softplus && (!al16(g.deriv) || g.ldd % 4 != 0)) return false;
+  if (g.spd && (!al16(g.spd) || g.ldsd % 4 != 0)) return false;
+  int nob = 0;
+  const LGemm a = lg_args(g, &nob);
+  return lg_dispatch(a, nob, g.spd != nullptr, lg_unal(g), 0, nullptr, false);
+}
+
+int lgemm_pack(const GemmArgs& g, void* img, hipStream_t s) {
+  LPack p{};
+  int G = 1;
+  p.kst = lg_kst(g, &p.kst0);
+  p.NOB = lg_nob(g.N, p.kst, &G);
+  p.N = g.N;
+  for (int i = 0; i < g.nseg; ++i) {
+    p.B[i] = g.seg[i].B; p.b_rs[i] = g.seg[i].b_rs; p.b_cs[i] = g.seg[i].b_cs; p.K[i] = g.seg[i].K;
+  }
+  p.total = (long)G * p.kst * p.NOB * 512;
+  p.out = (unsigned short*)img;
+  // hi and lo fragments interleave; one thread per (fragment, lane, element)
+  hipLaunchKernelGGL(k_limg_pack, dim3((unsigned)((p.total + 255) / 256)), dim3(256), 0, s, p);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int lgemm_run(const GemmArgs& g, const void* img, int cus, hipStream_t s) {
+  int nob = 0;
+  LGemm a = lg_args(g, &nob);
+  a.img = (const uint4*)img;
+  if (!lg_dispatch(a, nob, g.spd != nullptr, lg_unal(g), cus, s, true)) return -1;
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace anr

@@ -69,7 +69,7 @@ struct SdfPointArgs {
   const float* Yr;       // [P][4] resd_fc output
   float* Xs0;            // [P][40] gamma_6(tpose)
   float* X4;             // [P][256] lin4 input: cols 217..255 = gamma_6 / sqrt(2)
-  float* C0;             // [P][36] colour input: tpose, gamma_4(bigdir), gradient
+  float* C0;             // [P][40] colour input: tpose, gamma_4(bigdir), gradient
   const float* D7;       // [P][256] softplus factor of lin7
   float* G7;             // [P][256]
   const float* Gc;       // [P][256] lin4 input gradient (cols 217..255: gamma part)

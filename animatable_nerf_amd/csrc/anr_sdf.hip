@@ -238,7 +238,7 @@ __global__ __launch_bounds__(256) void k_sdf_mid(SdfPointArgs a) {
     if (q < 39) x4[217 + q] = v / sqrt2;
   }
   const float bd[3] = {pt[3], pt[4], pt[5]};
-  float* c = a.C0 + (size_t)i * 36;
+  float* c = a.C0 + (size_t)i * 40;
   c[0] = tp[0]; c[1] = tp[1]; c[2] = tp[2];
   for (int q = 0; q < 27; ++q) c[3 + q] = embed_feature(bd, q, 4);
   c[33] = 0.f; c[34] = 0.f; c[35] = 0.f;
@@ -260,7 +260,7 @@ __global__ __launch_bounds__(256) void k_sdf_gamma_bwd(SdfPointArgs a) {
   if (i >= a.cnt) return;
   const float* gA = a.Gc + (size_t)i * 256 + 217;
   const float* gB = a.gB + (size_t)i * 40;
-  const float* c = a.C0 + (size_t)i * 36;
+  const float* c = a.C0 + (size_t)i * 40;
   const float tp[3] = {c[0], c[1], c[2]};
   float gr[3];
   for (int r = 0; r < 3; ++r) gr[r] = gA[r] + gB[r];
@@ -274,7 +274,7 @@ __global__ __launch_bounds__(256) void k_sdf_gamma_bwd(SdfPointArgs a) {
       gr[r] = gr[r] + (gc * -sinf(v)) * fr;
     }
   }
-  float* cc = a.C0 + (size_t)i * 36;
+  float* cc = a.C0 + (size_t)i * 40;
   for (int r = 0; r < 3; ++r) {
     cc[30 + r] = gr[r];
     a.grad_rows[(size_t)(a.b0 + i) * 3 + r] = gr[r];
@@ -297,7 +297,7 @@ __global__ __launch_bounds__(256) void k_sdf_raw(SdfPointArgs a) {
   float4 raw = make_float4(1.0f / (1.0f + expf(-yc[0])), 1.0f / (1.0f + expf(-yc[1])), 1.0f / (1.0f + expf(-yc[2])),
                            alpha);
   const float* tb = a.tbtab + (size_t)(ray / a.chunk) * 6;
-  const float* c = a.C0 + (size_t)i * 36;
+  const float* c = a.C0 + (size_t)i * 40;
   bool inside = true;
   for (int r = 0; r < 3; ++r) inside = inside && c[r] > tb[r] && c[r] < tb[3 + r];
   if (!inside) raw = make_float4(0.f, 0.f, 0.f, 0.f);

@@ -6,7 +6,7 @@
 //      (softplus + its backward factor in the epilogue), 8 input-gradient GEMMs (reverse mode
 //      through the stored factors), gamma backward, 5 colour GEMMs, raw
 //   -> compositing (k_composite) -> msk_sdf lists.
-// Layer-wise GEMMs (anr_gemm.hip, exact fp32 MFMA) keep each activation in HBM: the input gradient
+// Layer-wise GEMMs (anr_gemm.hip exact fp32 MFMA, or anr_lgemm.hip split-bf16) keep each activation in HBM: the input gradient
 // needs every softplus factor of the forward, which does not fit a fused register pipeline.
 #include <algorithm>
 #include <cmath>
@@ -23,9 +23,10 @@ using namespace anr;
 namespace {
 
 constexpr long SDF_BATCH = 1L << 19;
+constexpr size_t SDF_LIMG_BYTES = 16u << 20;  // split-bf16 layer-GEMM weight images (31 GEMMs, <= 384 KiB each)
 
 struct SLayout {
-  size_t counts, mask, chunk_min, ray_off, block_sum, list, knn, tbtab, wimg, fold, resd_rows, grad_rows;
+  size_t counts, mask, chunk_min, ray_off, block_sum, list, knn, tbtab, wimg, fold, limg, resd_rows, grad_rows;
   size_t min_sdf, flags, chunk_cnt, msk_sdf, msk_label;
   size_t ptb, Gr, Ha, Hb, Yr, Xs0, X4, D, Y8, Ga, Gb, Gc, gB, C0, Yc;
   long P;
@@ -52,6 +53,7 @@ SLayout slayout(int n_rays, int chunk) {
   L.tbtab = take(nch * 6 * 4);
   L.wimg = take(SDF_WN_FLOATS * 4);
   L.fold = take(768 * 4);
+  L.limg = take(SDF_LIMG_BYTES);
   L.resd_rows = take(N * 3 * 4);
   L.grad_rows = take(N * 3 * 4);
   L.min_sdf = take(R * 4);
@@ -63,7 +65,7 @@ SLayout slayout(int n_rays, int chunk) {
   L.P = P;
   auto f = [&](long w) { return take((size_t)P * w * 4); };
   L.ptb = f(8); L.Gr = f(64); L.Ha = f(256); L.Hb = f(256); L.Yr = f(4); L.Xs0 = f(40); L.X4 = f(256);
-  L.D = f(8 * 256); L.Y8 = f(264); L.Ga = f(256); L.Gb = f(256); L.Gc = f(256); L.gB = f(40); L.C0 = f(36);
+  L.D = f(8 * 256); L.Y8 = f(264); L.Ga = f(256); L.Gb = f(256); L.Gc = f(256); L.gB = f(40); L.C0 = f(40);
   L.Yc = f(4);
   L.total = o;
   return L;
@@ -76,15 +78,57 @@ int sdf_cus() {
   return v;
 }
 
+// weight images of the split-bf16 layer GEMM (anr_lgemm.hip), packed on first use in a render call
+// (the weights are fixed for its batches) and reused by every later batch
+struct LImgCache {
+  char* base = nullptr;
+  size_t cap = 0, used = 0;
+  struct E {
+    const float* B[2];
+    long rs[2], cs[2];
+    int K[2], N;
+    size_t off;
+  } e[48];
+  int n = 0;
+  const void* get(const GemmArgs& g, hipStream_t s) {
+    E k{};
+    for (int i = 0; i < g.nseg; ++i) {
+      k.B[i] = g.seg[i].B; k.rs[i] = g.seg[i].b_rs; k.cs[i] = g.seg[i].b_cs; k.K[i] = g.seg[i].K;
+    }
+    k.N = g.N;
+    for (int i = 0; i < n; ++i) {
+      const E& c = e[i];
+      bool same = c.N == k.N;
+      for (int j = 0; j < 2; ++j) same = same && c.B[j] == k.B[j] && c.rs[j] == k.rs[j] && c.cs[j] == k.cs[j] && c.K[j] == k.K[j];
+      if (same) return base + c.off;
+    }
+    const size_t bytes = lgemm_image_bytes(g);
+    if (n == 48 || used + bytes > cap) return nullptr;
+    k.off = used;
+    if (lgemm_pack(g, base + used, s) != 0) return nullptr;
+    used = align256(used + bytes);
+    e[n++] = k;
+    return base + k.off;
+  }
+};
+
 struct G {
   hipStream_t s;
   int M;
-  int x3;  // render precision ANR_BF16X3: split-bf16 MFMA GEMMs (k_gemm_b<.., .., true>)
+  int x3;  // render precision ANR_BF16X3: split-bf16 MFMA GEMMs (k_lgemm; k_gemm_b<.., .., true> otherwise)
+  LImgCache* limg;
+  int cus;
   int run(GemmArgs g) {
     if (M <= 0 || g.N <= 0) return ANR_OK;
     g.M = M;
     g.x3 = x3;
     g.ksplit = 1;
+    if (x3 && limg && lgemm_supported(g)) {
+      if (const void* img = limg->get(g, s)) {
+        (void)lgemm_run(g, img, cus, s);
+        return check_launch("k_lgemm (sdf)");
+      }
+    }
     launch_gemm(g, dim3((g.N + 63) / 64, (M + 63) / 64, 1), s);
     return check_launch("k_gemm (sdf)");
   }
@@ -228,6 +272,10 @@ int anr_sdf_render_fwd(const anr_sdf_params* p, const anr_sdf_frame* f, const fl
   auto Dl = [&](int l) { return D + (size_t)l * P * 256; };
   auto WN = [&](int l) { return (const float*)wimg + wn_layer(l).off; };
   const float sqrt2 = 1.41421356237309515f;
+  LImgCache limg;
+  limg.base = ws + L.limg;
+  limg.cap = SDF_LIMG_BYTES;
+  const int cus = sdf_cus();
   for (long b0 = 0; b0 < n; b0 += P) {
     const int cnt = (int)std::min<long>(P, n - b0);
     SdfPointArgs a{};
@@ -239,7 +287,7 @@ int anr_sdf_render_fwd(const anr_sdf_params* p, const anr_sdf_frame* f, const fl
     a.D7 = Dl(7); a.G7 = Ga; a.Gc = Gc; a.gB = F(L.gB); a.Y8 = F(L.Y8); a.Yc = F(L.Yc); a.beta = beta;
     a.resd_rows = F(L.resd_rows); a.grad_rows = F(L.grad_rows); a.raw = raw; a.sdf = out->sdf;
     const dim3 pg((cnt + 255) / 256), pb(256);
-    G g{s, cnt, o->precision == ANR_BF16X3 ? 1 : 0};
+    G g{s, cnt, o->precision == ANR_BF16X3 ? 1 : 0, &limg, cus};
 
     // B2 + B3: LBS to the big pose, residual deformation MLP (poses folded into layers 0 / 5)
     hipLaunchKernelGGL(k_sdf_prep, pg, pb, 0, s, a);
@@ -284,7 +332,7 @@ int anr_sdf_render_fwd(const anr_sdf_params* p, const anr_sdf_frame* f, const fl
     ANR_TRY(check_launch("k_sdf_gamma_bwd"));
 
     // B6 colour network (color_latent folded into lin3)
-    ANR_TRY(g.fwd(Ha, 256, 256, WN(9), 289, tp[29], a.C0, 36, 33, 0, true, nullptr, 0.f, F(L.Y8) + 1, 264, 256, 33));
+    ANR_TRY(g.fwd(Ha, 256, 256, WN(9), 289, tp[29], a.C0, 40, 33, 0, true, nullptr, 0.f, F(L.Y8) + 1, 264, 256, 33));
     ANR_TRY(g.fwd(Hb, 256, 256, WN(10), 256, tp[32], Ha, 256, 256, 0, true));
     ANR_TRY(g.fwd(Ha, 256, 256, WN(11), 256, tp[35], Hb, 256, 256, 0, true));
     ANR_TRY(g.fwd(Hb, 256, 256, WN(12), 384, fold + 512, Ha, 256, 256, 0, true));

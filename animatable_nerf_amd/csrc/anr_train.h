@@ -119,6 +119,14 @@ struct WGrad {
 size_t wgrad_slab_floats();
 int launch_wgrad(WGrad g, int n_host, hipStream_t s);
 
+// split-bf16 layer GEMM with LDS-resident weight images for large M (anr_lgemm.hip; the sdf_pdf
+// batches): lgemm_supported(g) (g.x3, no accumulate / mask / atomics, 16-B addressable operands),
+// the weight image (lgemm_image_bytes, packed once per weight set by lgemm_pack), then lgemm_run.
+bool lgemm_supported(const GemmArgs& g);
+size_t lgemm_image_bytes(const GemmArgs& g);
+int lgemm_pack(const GemmArgs& g, void* img, hipStream_t s);
+int lgemm_run(const GemmArgs& g, const void* img, int cus, hipStream_t s);
+
 // per-point training buffers (row-major, compact kept-sample order)
 struct TrainBufs {
   const int* list;
