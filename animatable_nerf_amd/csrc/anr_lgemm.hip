@@ -49,6 +49,7 @@ struct LGemm {
   int kst0, kst;     // k-steps (32 deep) of segment 0, of both
   int M, N, G, bpg;  // rows, columns, column groups, workgroups per group
   const uint4* img;  // [G][kst][NOB][hi, lo][64 lanes] 16-B fragments
+  const f32x4* bimg; // [G][NOB][16] bias (zeros without one), after the fragments
   float* C;
   long ldc;
   const float* bias;
@@ -59,6 +60,7 @@ struct LGemm {
   long ldsd;
   int spd_n;
   float div_pre, div_post;
+  const float* atr;  // ATR: the activations are softplus factors d, used as (d >= 0 ? atr[k] d / (d + 1) : atr[k])
 };
 
 struct LPack {
@@ -67,6 +69,9 @@ struct LPack {
   int K[2], kst0, kst, N, NOB;
   long total;  // fragment elements of one hi (or lo) image
   unsigned short* out;
+  const float* bias;
+  float* bout;  // G NOB 16 floats
+  int nbias;
 };
 
 __device__ __forceinline__ unsigned short lg_bf16_rne(float f) {
@@ -79,7 +84,11 @@ __device__ __forceinline__ unsigned short lg_bf16_rne(float f) {
 // + (lane & 15), k = 32 t + 8 (lane >> 4) + e of the segment holding k-step ks; zero past N / K_s
 __global__ void k_limg_pack(LPack p) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= p.total) return;
+  if (i >= p.total) {
+    const long j = i - p.total;  // column j of the bias image
+    if (j < p.nbias) p.bout[j] = (p.bias && j < p.N) ? p.bias[j] : 0.0f;
+    return;
+  }
   const int e = (int)(i & 7), lane = (int)((i >> 3) & 63);
   const long f = i >> 9;  // fragment index (g, ks, ob)
   const int ob = (int)(f % p.NOB);
@@ -118,19 +127,19 @@ __device__ __forceinline__ float lg_log1p(float e) {
 // Bias comes from LDS, the softplus-backward factors were loaded before the tile's MFMAs (sp); the
 // epilogue issues no global loads, so the next tile's activation loads stay in flight across it.
 template <int NOB, bool SPD>
-__device__ __forceinline__ void lg_epilogue(const LGemm& g, const f32x4 (&acc)[NOB], const f32x4 (&sp)[NOB],
-                                            const float* bias_lds, int tile, int n0, int lane) {
-  const int m = tile * 16 + (lane & 15);
-  const bool row_ok = m < g.M;
+__device__ __forceinline__ void lg_epilogue(const LGemm& g, const f32x4 (&acc)[NOB], const f32x4* sp,
+                                            const f32x4* bv, int tile, int n0, int lane) {
+  // rows past M were computed from row M - 1's activations (the loads clamp), so their results are
+  // row M - 1's: storing them there is a same-value duplicate and the stores need no row predicate
+  const int m = min(tile * 16 + (lane & 15), g.M - 1);
 #pragma unroll
   for (int ob = 0; ob < NOB; ++ob) {
     const int nl = 16 * ob + 4 * (lane >> 4);
     const int n = n0 + nl;
-    const f32x4 bv = *(const f32x4*)(bias_lds + nl);
     f32x4 v = acc[ob], dv;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      float x = v[e] + bv[e];
+      float x = v[e] + bv[ob][e];
       if (g.div_pre != 0.f) x = x / g.div_pre;
       if (g.relu) x = fmaxf(x, 0.f);
       if (g.softplus) {  // torch softplus(beta=100, threshold=20) and the factor its backward uses
@@ -146,17 +155,11 @@ __device__ __forceinline__ void lg_epilogue(const LGemm& g, const f32x4 (&acc)[N
       if (g.div_post != 0.f) x = x / g.div_post;
       v[e] = x;
     }
-    if (!row_ok) continue;
     float* c = g.C + (long)m * g.ldc + n;
     float* d = g.deriv + (long)m * g.ldd + n;
-    if (n + 3 < g.N) {
-#if LG_NT
-      __builtin_nontemporal_store(v, (f32x4*)c);
-      if (g.softplus) __builtin_nontemporal_store(dv, (f32x4*)d);
-#else
+    if (n0 + 16 * ob + 16 <= g.N) {  // uniform: the whole 16-column block is inside N
       *(f32x4*)c = v;
       if (g.softplus) *(f32x4*)d = dv;
-#endif
     } else {
 #pragma unroll
       for (int e = 0; e < 4; ++e)
@@ -168,31 +171,28 @@ __device__ __forceinline__ void lg_epilogue(const LGemm& g, const f32x4 (&acc)[N
   }
 }
 
-// the activation fragments of one 16-sample tile: k-step ks, lane -> sample 16 t + (lane & 15), k =
-// 32 ks' + 8 (lane >> 4) .. + 7 of the segment holding ks (rows past M read row M - 1, k groups
+// the activation fragments of k-step ks of a 16-sample tile: lane -> sample 16 t + (lane & 15), k =
+// 32 ks' + lg_kcol(lane >> 4, 0..7) of the segment holding ks (rows past M read row M - 1, 4-groups
 // wholly past K read column 0; both masked later)
-template <int KST, int KST0, bool UNAL>
-__device__ __forceinline__ void lg_load_tile(const LGemm& g, f32x4 (&buf)[KST][2], int tile, int lane) {
+template <int KST0, bool UNAL>
+__device__ __forceinline__ void lg_load_ks(const LGemm& g, f32x4 (&buf)[2], int tile, int ks, int lane) {
   const int m = min(tile * 16 + (lane & 15), g.M - 1);
   const int j = lane >> 4;
+  const bool s1 = ks >= KST0;
+  const float* A = s1 ? g.seg[1].A : g.seg[0].A;
+  const long lda = s1 ? g.seg[1].lda : g.seg[0].lda;
+  const int K = s1 ? g.seg[1].K : g.seg[0].K;
+  const int k0 = 32 * (ks - (s1 ? KST0 : 0));
 #pragma unroll
-  for (int ks = 0; ks < KST; ++ks) {
-    const bool s1 = ks >= KST0;
-    const float* A = s1 ? g.seg[1].A : g.seg[0].A;
-    const long lda = s1 ? g.seg[1].lda : g.seg[0].lda;
-    const int K = s1 ? g.seg[1].K : g.seg[0].K;
-    const int k0 = 32 * (ks - (s1 ? KST0 : 0));
+  for (int h = 0; h < 2; ++h) {
+    int kc = k0 + lg_kcol(j, 4 * h);
+    kc = kc < K ? kc : 0;
+    const float* p = A + (long)m * lda + kc;
+    if constexpr (UNAL) {  // a segment that is not 16-B addressable: 4-B loads
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      int kc = k0 + lg_kcol(j, 4 * h);
-      kc = kc < K ? kc : 0;  // 4-groups wholly past K read column 0 (masked at use)
-      const float* p = A + (long)m * lda + kc;
-      if constexpr (UNAL) {  // a segment that is not 16-B addressable: 4-B loads
-#pragma unroll
-        for (int e = 0; e < 4; ++e) buf[ks][h][e] = p[e];
-      } else {
-        buf[ks][h] = *(const f32x4*)p;
-      }
+      for (int e = 0; e < 4; ++e) buf[h][e] = p[e];
+    } else {
+      buf[h] = *(const f32x4*)p;
     }
   }
 }
@@ -209,18 +209,24 @@ __device__ __forceinline__ void lg_load_spd(const LGemm& g, f32x4 (&sp)[NOB], in
   }
 }
 
-// one tile: the factor loads of this tile and the activation loads of the next go out first, then the
-// MFMAs on `cur` (whose loads went out one tile earlier), then the epilogue
-template <int NOB, int KST, int KST0, bool SPD, bool UNAL>
-__device__ __forceinline__ void lg_tile(const LGemm& g, const f32x4 (&cur)[KST][2], f32x4 (&nxt)[KST][2], int tile,
-                                        int next, int n0, int lane, const unsigned char* lds, const float* bias_lds) {
-  f32x4 sp[NOB];
+// one tile on a k-step ring: this tile's factor loads go out first; each k-step's activations are
+// split hi/lo and their registers immediately refilled with the same k-step of the wave's next tile
+// (so one tile of loads is always in flight, in one tile's worth of registers), then the MFMAs;
+// the epilogue last. The loop is straight-line, so the compiler's vmcnt waits stay exact.
+template <int NOB, int KST, int KST0, bool SPD, bool UNAL, bool ATR>
+__device__ __forceinline__ void lg_tile(const LGemm& g, f32x4 (&buf)[KST][2], int tile, int next, int n0, int lane,
+                                        const unsigned char* lds, const float* atr_lds) {
+  // the tile's bias columns (from the image, L1-resident) and factors load first: both are used in this
+  // tile's epilogue, and issuing them ahead of the refills keeps every wait in the loop graded
+  // (the softplus-backward GEMMs have no bias: with SPD the bias registers are not needed)
+  f32x4 bv[NOB], sp[NOB];
+#pragma unroll
+  for (int ob = 0; ob < NOB; ++ob) bv[ob] = SPD ? f32x4{0.f, 0.f, 0.f, 0.f} : g.bimg[n0 / 4 + 4 * ob + (lane >> 4)];
   lg_load_spd<NOB, SPD>(g, sp, tile, n0, lane);
-  lg_load_tile<KST, KST0, UNAL>(g, nxt, next, lane);
+  const int kg = lane >> 4;
   f32x4 acc[NOB];
 #pragma unroll
   for (int ob = 0; ob < NOB; ++ob) acc[ob] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int kg = lane >> 4;
   // the weight fragments are the same every tile: launder their address so they are re-read from LDS
   // per tile instead of being hoisted out of the tile loop into (spilled) registers
   int frag_off = lane * 16;
@@ -230,8 +236,15 @@ __device__ __forceinline__ void lg_tile(const LGemm& g, const f32x4 (&cur)[KST][
     const bool s1 = ks >= KST0;
     const int K = s1 ? g.seg[1].K : g.seg[0].K;
     const int k0 = 32 * (ks - (s1 ? KST0 : 0));
-    float x[8] = {cur[ks][0][0], cur[ks][0][1], cur[ks][0][2], cur[ks][0][3],
-                  cur[ks][1][0], cur[ks][1][1], cur[ks][1][2], cur[ks][1][3]};
+    float x[8] = {buf[ks][0][0], buf[ks][0][1], buf[ks][0][2], buf[ks][0][3],
+                  buf[ks][1][0], buf[ks][1][1], buf[ks][1][2], buf[ks][1][3]};
+    if constexpr (ATR) {  // d sdf / d z7 = softplus_backward(W8[0], z7) from the stored factors (k_sdf_gtop)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float w = atr_lds[k0 + lg_kcol(kg, e)];
+        x[e] = x[e] >= 0.f ? w * x[e] / (x[e] + 1.f) : w;
+      }
+    }
 #pragma unroll
     for (int e = 0; e < 8; ++e) x[e] = (k0 + lg_kcol(kg, e) < K) ? x[e] : 0.0f;
     lbf16x8 xh, xl;
@@ -240,6 +253,10 @@ __device__ __forceinline__ void lg_tile(const LGemm& g, const f32x4 (&cur)[KST][
       xh[e] = (__bf16)x[e];
       xl[e] = (__bf16)(x[e] - (float)xh[e]);
     }
+    // refill with the next tile's k-step ks once the split has consumed the registers (so the loads
+    // land in the same registers and the loop carries no copies that would wait on them)
+    lg_load_ks<KST0, UNAL>(g, buf[ks], next, ks, lane);
+    __builtin_amdgcn_sched_barrier(0);  // keep the refill here (issue order = ring order)
     const unsigned char* fr = lds + ks * NOB * 2 * LG_FRAG + frag_off;
 #pragma unroll
     for (int ob = 0; ob < NOB; ++ob) {
@@ -250,10 +267,10 @@ __device__ __forceinline__ void lg_tile(const LGemm& g, const f32x4 (&cur)[KST][
       acc[ob] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, xh, acc[ob], 0, 0, 0);
     }
   }
-  lg_epilogue<NOB, SPD>(g, acc, sp, bias_lds, tile, n0, lane);
+  lg_epilogue<NOB, SPD>(g, acc, sp, bv, tile, n0, lane);
 }
 
-template <int NOB, int KST, int KST0, bool SPD, bool UNAL>
+template <int NOB, int KST, int KST0, bool SPD, bool UNAL, bool ATR>
 __global__ __launch_bounds__(LG_WAVES * 64) void k_lgemm(LGemm g) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   // workgroup -> (column group, rank): the workgroups of one rank sit on one XCD (blockIdx % 8), so
@@ -263,7 +280,7 @@ __global__ __launch_bounds__(LG_WAVES * 64) void k_lgemm(LGemm g) {
   const int rank = (b / (8 * g.G)) * 8 + (b & 7);
   const int n0 = 16 * NOB * gi;
   constexpr int IMG = KST * NOB * 2 * LG_FRAG;
-  float* bias_lds = (float*)(lds + IMG);
+  float* atr_lds = (float*)(lds + IMG);
   {
     const uint4* src = g.img + (long)gi * (IMG / 16);
     uint4* dst = (uint4*)lds;
@@ -276,9 +293,8 @@ __global__ __launch_bounds__(LG_WAVES * 64) void k_lgemm(LGemm g) {
       const int i = threadIdx.x + j * LG_WAVES * 64;
       if (i < N16) dst[i] = t[j];
     }
-    if (threadIdx.x < 16 * NOB) {
-      const int n = n0 + threadIdx.x;
-      bias_lds[threadIdx.x] = (g.bias && n < g.N) ? g.bias[n] : 0.0f;
+    if constexpr (ATR) {
+      if (threadIdx.x < 32 * KST) atr_lds[threadIdx.x] = threadIdx.x < g.seg[0].K ? g.atr[threadIdx.x] : 0.0f;
     }
   }
   __syncthreads();
@@ -288,19 +304,14 @@ __global__ __launch_bounds__(LG_WAVES * 64) void k_lgemm(LGemm g) {
   const int T = (g.M + 15) >> 4;
   int t = rank * LG_WAVES + w;
   if (t >= T) return;
-  f32x4 ba[KST][2], bb[KST][2];
-  lg_load_tile<KST, KST0, UNAL>(g, ba, t, lane);
-  while (true) {
-    lg_tile<NOB, KST, KST0, SPD, UNAL>(g, ba, bb, t, t + nw, n0, lane, lds, bias_lds);
-    t += nw;
-    if (t >= T) break;
-    lg_tile<NOB, KST, KST0, SPD, UNAL>(g, bb, ba, t, t + nw, n0, lane, lds, bias_lds);
-    t += nw;
-    if (t >= T) break;
-  }
+  f32x4 buf[KST][2];
+#pragma unroll
+  for (int ks = 0; ks < KST; ++ks) lg_load_ks<KST0, UNAL>(g, buf[ks], t, ks, lane);
+  for (; t < T; t += nw) lg_tile<NOB, KST, KST0, SPD, UNAL, ATR>(g, buf, t, t + nw, n0, lane, lds, atr_lds);
 }
 
-size_t lg_lds_bytes(int kst, int nob) { return (size_t)kst * nob * 2 * LG_FRAG + (size_t)nob * 64; }
+// weight image, ATR column weights (32 kst floats)
+size_t lg_lds_bytes(int kst, int nob) { return (size_t)kst * nob * 2 * LG_FRAG + (size_t)kst * 128; }
 
 // output columns per workgroup (16 x NOB) and column groups G for N outputs at kst k-steps
 int lg_nob(int N, int kst, int* G) {
@@ -322,36 +333,38 @@ int lg_kst(const GemmArgs& g, int* kst0) {
   return *kst0 + (g.nseg > 1 ? (g.seg[1].K + 31) / 32 : 0);
 }
 
-template <int NOB, int KST, int KST0, bool SPD, bool UNAL>
+template <int NOB, int KST, int KST0, bool SPD, bool UNAL, bool ATR>
 void lg_launch(const LGemm& a, int cus, hipStream_t s) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)k_lgemm<NOB, KST, KST0, SPD, UNAL>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)k_lgemm<NOB, KST, KST0, SPD, UNAL, ATR>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               LG_MAX_LDS);
     attr = true;
   }
   LGemm g = a;
   g.bpg = std::max(1, cus / (8 * g.G)) * 8;
-  hipLaunchKernelGGL((k_lgemm<NOB, KST, KST0, SPD, UNAL>), dim3((unsigned)(g.bpg * g.G)), dim3(LG_WAVES * 64),
+  hipLaunchKernelGGL((k_lgemm<NOB, KST, KST0, SPD, UNAL, ATR>), dim3((unsigned)(g.bpg * g.G)), dim3(LG_WAVES * 64),
                      lg_lds_bytes(KST, NOB), s, g);
 }
 
 // the instantiated shapes (the sdf_pdf layers); false for any other
 bool lg_dispatch(const LGemm& a, int nob, bool spd, bool unal, int cus, hipStream_t s, bool launch) {
-#define LG_CASE(N_, K_, K0_, S_, U_)                                            \
-  if (nob == N_ && a.kst == K_ && a.kst0 == K0_ && spd == S_ && unal == U_) {   \
-    if (launch) lg_launch<N_, K_, K0_, S_, U_>(a, cus, s);                      \
-    return true;                                                                \
+  const bool atr = a.atr != nullptr;
+#define LG_CASE(N_, K_, K0_, S_, U_, T_)                                                    \
+  if (nob == N_ && a.kst == K_ && a.kst0 == K0_ && spd == S_ && unal == U_ && atr == T_) {  \
+    if (launch) lg_launch<N_, K_, K0_, S_, U_, T_>(a, cus, s);                              \
+    return true;                                                                            \
   }
-  LG_CASE(8, 8, 8, false, false)
-  LG_CASE(8, 8, 8, true, false)
-  LG_CASE(8, 7, 7, true, false)
-  LG_CASE(8, 2, 2, false, false)
-  LG_CASE(6, 10, 2, false, false)
-  LG_CASE(6, 10, 2, false, true)
-  LG_CASE(6, 8, 8, false, false)
-  LG_CASE(4, 8, 8, false, false)
-  LG_CASE(1, 8, 8, false, false)
+  LG_CASE(8, 8, 8, false, false, false)
+  LG_CASE(8, 8, 8, true, false, false)
+  LG_CASE(8, 8, 8, true, false, true)
+  LG_CASE(8, 7, 7, true, false, false)
+  LG_CASE(8, 2, 2, false, false, false)
+  LG_CASE(6, 10, 2, false, false, false)
+  LG_CASE(6, 10, 2, false, true, false)
+  LG_CASE(6, 8, 8, false, false, false)
+  LG_CASE(4, 8, 8, false, false, false)
+  LG_CASE(1, 8, 8, false, false, false)
 #undef LG_CASE
   return false;
 }
@@ -374,6 +387,7 @@ LGemm lg_args(const GemmArgs& g, int* nob) {
   *nob = lg_nob(g.N, a.kst, &a.G);
   a.C = g.C; a.ldc = g.ldc; a.bias = g.bias; a.relu = g.relu; a.softplus = g.softplus; a.deriv = g.deriv;
   a.ldd = g.ldd; a.spd = g.spd; a.ldsd = g.ldsd; a.spd_n = g.spd_n; a.div_pre = g.div_pre; a.div_post = g.div_post;
+  a.atr = g.a_softplus_w;
   return a;
 }
 
@@ -383,7 +397,7 @@ size_t lgemm_image_bytes(const GemmArgs& g) {
   int G = 1, kst0 = 0;
   const int kst = lg_kst(g, &kst0);
   const int NOB = lg_nob(g.N, kst, &G);
-  return (size_t)G * kst * NOB * 2 * LG_FRAG;
+  return (size_t)G * kst * NOB * 2 * LG_FRAG + (size_t)G * NOB * 64;
 }
 
 bool lgemm_supported(const GemmArgs& g) {
@@ -395,7 +409,7 @@ bool lgemm_supported(const GemmArgs& g) {
   }
   if (!al16(g.C) || g.ldc % 4 != 0) return false;
   if (g.softplus && (!al16(g.deriv) || g.ldd % 4 != 0)) return false;
-  if (g.spd && (!al16(g.spd) || g.ldsd % 4 != 0)) return false;
+  if (g.spd && (!al16(g.spd) || g.ldsd % 4 != 0 || g.bias)) return false;
   int nob = 0;
   const LGemm a = lg_args(g, &nob);
   return lg_dispatch(a, nob, g.spd != nullptr, lg_unal(g), 0, nullptr, false);
@@ -412,8 +426,11 @@ int lgemm_pack(const GemmArgs& g, void* img, hipStream_t s) {
   }
   p.total = (long)G * p.kst * p.NOB * 512;
   p.out = (unsigned short*)img;
-  // hi and lo fragments interleave; one thread per (fragment, lane, element)
-  hipLaunchKernelGGL(k_limg_pack, dim3((unsigned)((p.total + 255) / 256)), dim3(256), 0, s, p);
+  p.bias = g.bias;
+  p.bout = (float*)((char*)img + (size_t)G * p.kst * p.NOB * 2 * LG_FRAG);
+  p.nbias = G * p.NOB * 16;
+  // hi and lo fragments interleave; one thread per (fragment, lane, element), then the bias columns
+  hipLaunchKernelGGL(k_limg_pack, dim3((unsigned)((p.total + p.nbias + 255) / 256)), dim3(256), 0, s, p);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -421,6 +438,7 @@ int lgemm_run(const GemmArgs& g, const void* img, int cus, hipStream_t s) {
   int nob = 0;
   LGemm a = lg_args(g, &nob);
   a.img = (const uint4*)img;
+  a.bimg = (const f32x4*)((const char*)img + (size_t)a.G * a.kst * nob * 2 * LG_FRAG);
   if (!lg_dispatch(a, nob, g.spd != nullptr, lg_unal(g), cus, s, true)) return -1;
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

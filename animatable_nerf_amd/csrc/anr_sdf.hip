@@ -171,9 +171,29 @@ __device__ __forceinline__ void inv33(const float Ab[16], float Ri[9]) {
   Ri[6] = c20 * rd; Ri[7] = c21 * rd; Ri[8] = c22 * rd;
 }
 
+// the workgroup's 256 rows of a [P][W] block, written column-fastest by all threads (coalesced):
+// value(row, col) from the per-row values staged in LDS by the thread-per-sample phase
+template <int W, typename F>
+__device__ __forceinline__ void sdf_rows_store(float* base, int i0, int cnt, F value) {
+  const int rows = min(256, cnt - i0);
+  for (int f = threadIdx.x; f < rows * W; f += 256) {
+    const int r = f / W, c = f - r * W;
+    base[(size_t)(i0 + r) * W + c] = value(r, c);
+  }
+}
+
+__device__ void sdf_prep_point(const SdfPointArgs& a, int i, float (*sp)[4]);
+
+// thread per kept sample (LBS to the big pose), then gamma_10(bigpose) rows written coalesced
 __global__ __launch_bounds__(256) void k_sdf_prep(SdfPointArgs a) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= a.cnt) return;
+  __shared__ float sp[256][4];
+  const int i0 = blockIdx.x * 256, i = i0 + threadIdx.x;
+  if (i < a.cnt) sdf_prep_point(a, i, sp);
+  __syncthreads();
+  sdf_rows_store<64>(a.Gr, i0, a.cnt, [&](int r, int c) { return c < 63 ? embed_feature(sp[r], c, 10) : 0.f; });
+}
+
+__device__ void sdf_prep_point(const SdfPointArgs& a, int i, float (*sp)[4]) {
   const int pid = a.list[a.b0 + i];
   const int ray = pid >> 6, s = pid & 63;
   float z, dist, pts[3], p[3], pd[3];
@@ -212,36 +232,39 @@ __global__ __launch_bounds__(256) void k_sdf_prep(SdfPointArgs a) {
   float* pt = a.ptb + (size_t)i * 8;
   pt[0] = bp[0]; pt[1] = bp[1]; pt[2] = bp[2];
   pt[3] = bd[0]; pt[4] = bd[1]; pt[5] = bd[2];
-  float* g = a.Gr + (size_t)i * 64;
-  for (int q = 0; q < 64; ++q) g[q] = q < 63 ? embed_feature(bp, q, 10) : 0.f;
+  sp[threadIdx.x][0] = bp[0]; sp[threadIdx.x][1] = bp[1]; sp[threadIdx.x][2] = bp[2];
 }
 
 // resd = 0.05 tanh(y); tpose = bigpose + resd; gamma_6(tpose) -> Xs0 and X4[:, 217:] / sqrt(2);
-// colour input [tpose, gamma_4(bigdir), gradient (k_sdf_gamma_bwd)]
+// colour input [tpose, gamma_4(bigdir), gradient (k_sdf_gamma_bwd)]. Thread per sample for tpose,
+// then the rows are written column-fastest by the whole workgroup.
 __global__ __launch_bounds__(256) void k_sdf_mid(SdfPointArgs a) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= a.cnt) return;
-  const float* pt = a.ptb + (size_t)i * 8;
-  const float* y = a.Yr + (size_t)i * 4;
-  float tp[3];
-  for (int r = 0; r < 3; ++r) {
-    const float rs = 0.05f * tanhf(y[r]);
-    a.resd_rows[(size_t)(a.b0 + i) * 3 + r] = rs;
-    tp[r] = pt[r] + rs;
+  __shared__ float sp[256][8];
+  const int i0 = blockIdx.x * 256, i = i0 + threadIdx.x;
+  if (i < a.cnt) {
+    const float* pt = a.ptb + (size_t)i * 8;
+    const float* y = a.Yr + (size_t)i * 4;
+    for (int r = 0; r < 3; ++r) {
+      const float rs = 0.05f * tanhf(y[r]);
+      a.resd_rows[(size_t)(a.b0 + i) * 3 + r] = rs;
+      sp[threadIdx.x][r] = pt[r] + rs;
+      sp[threadIdx.x][4 + r] = pt[3 + r];
+    }
   }
+  __syncthreads();
   const float sqrt2 = 1.41421356237309515f;
-  float* xs = a.Xs0 + (size_t)i * 40;
-  float* x4 = a.X4 + (size_t)i * 256;
-  for (int q = 0; q < 40; ++q) {
-    const float v = q < 39 ? embed_feature(tp, q, 6) : 0.f;
-    xs[q] = v;
-    if (q < 39) x4[217 + q] = v / sqrt2;
+  sdf_rows_store<40>(a.Xs0, i0, a.cnt, [&](int r, int c) { return c < 39 ? embed_feature(sp[r], c, 6) : 0.f; });
+  const int rows = min(256, a.cnt - i0);
+  for (int f = threadIdx.x; f < rows * 39; f += 256) {
+    const int r = f / 39, c = f - r * 39;
+    a.X4[(size_t)(i0 + r) * 256 + 217 + c] = embed_feature(sp[r], c, 6) / sqrt2;
   }
-  const float bd[3] = {pt[3], pt[4], pt[5]};
-  float* c = a.C0 + (size_t)i * 40;
-  c[0] = tp[0]; c[1] = tp[1]; c[2] = tp[2];
-  for (int q = 0; q < 27; ++q) c[3 + q] = embed_feature(bd, q, 4);
-  c[33] = 0.f; c[34] = 0.f; c[35] = 0.f;
+  // C0: tpose (0..2), gamma_4(bigdir) (3..29); 30..32 (gradient) belong to k_sdf_gamma_bwd
+  for (int f = threadIdx.x; f < rows * 40; f += 256) {
+    const int r = f / 40, c = f - r * 40;
+    if (c >= 30 && c < 33) continue;
+    a.C0[(size_t)(i0 + r) * 40 + c] = c < 3 ? sp[r][c] : c < 30 ? embed_feature(sp[r] + 4, c - 3, 4) : 0.f;
+  }
 }
 
 // d sdf / d z7 = softplus_backward(W8[0], z7)
@@ -254,22 +277,29 @@ __global__ __launch_bounds__(256) void k_sdf_gtop(SdfPointArgs a) {
   a.G7[e] = d >= 0.f ? g * d / (d + 1.f) : g;
 }
 
-// gamma_6 backward: x.grad = g_x + sum_f f*(g_sin cos(f x)) + f*(g_cos * -sin(f x))
+// gamma_6 backward: x.grad = g_x + sum_f f*(g_sin cos(f x)) + f*(g_cos * -sin(f x)). The two input
+// gradients (lin4's gamma columns, lin0's input) are summed into LDS by coalesced row reads first.
 __global__ __launch_bounds__(256) void k_sdf_gamma_bwd(SdfPointArgs a) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  __shared__ float gs_[256][40];
+  const int i0 = blockIdx.x * 256, i = i0 + threadIdx.x;
+  const int rows = min(256, a.cnt - i0);
+  for (int f = threadIdx.x; f < rows * 39; f += 256) {
+    const int r = f / 39, c = f - r * 39;
+    gs_[r][c] = a.Gc[(size_t)(i0 + r) * 256 + 217 + c] + a.gB[(size_t)(i0 + r) * 40 + c];
+  }
+  __syncthreads();
   if (i >= a.cnt) return;
-  const float* gA = a.Gc + (size_t)i * 256 + 217;
-  const float* gB = a.gB + (size_t)i * 40;
+  const float* g = gs_[threadIdx.x];
   const float* c = a.C0 + (size_t)i * 40;
   const float tp[3] = {c[0], c[1], c[2]};
   float gr[3];
-  for (int r = 0; r < 3; ++r) gr[r] = gA[r] + gB[r];
+  for (int r = 0; r < 3; ++r) gr[r] = g[r];
   for (int f = 0; f < 6; ++f) {
     const float fr = (float)(1 << f);
     for (int r = 0; r < 3; ++r) {
       const float v = tp[r] * fr;
-      const float gs = gA[3 + 6 * f + r] + gB[3 + 6 * f + r];
-      const float gc = gA[6 + 6 * f + r] + gB[6 + 6 * f + r];
+      const float gs = g[3 + 6 * f + r];
+      const float gc = g[6 + 6 * f + r];
       gr[r] = gr[r] + (gs * cosf(v)) * fr;
       gr[r] = gr[r] + (gc * -sinf(v)) * fr;
     }

@@ -78,13 +78,14 @@ int sdf_cus() {
   return v;
 }
 
-// weight images of the split-bf16 layer GEMM (anr_lgemm.hip), packed on first use in a render call
+// weight (and bias) images of the split-bf16 layer GEMM (anr_lgemm.hip), packed on first use in a render call
 // (the weights are fixed for its batches) and reused by every later batch
 struct LImgCache {
   char* base = nullptr;
   size_t cap = 0, used = 0;
   struct E {
     const float* B[2];
+    const float* bias;
     long rs[2], cs[2];
     int K[2], N;
     size_t off;
@@ -96,9 +97,10 @@ struct LImgCache {
       k.B[i] = g.seg[i].B; k.rs[i] = g.seg[i].b_rs; k.cs[i] = g.seg[i].b_cs; k.K[i] = g.seg[i].K;
     }
     k.N = g.N;
+    k.bias = g.bias;
     for (int i = 0; i < n; ++i) {
       const E& c = e[i];
-      bool same = c.N == k.N;
+      bool same = c.N == k.N && c.bias == k.bias;
       for (int j = 0; j < 2; ++j) same = same && c.B[j] == k.B[j] && c.rs[j] == k.rs[j] && c.cs[j] == k.cs[j] && c.K[j] == k.K[j];
       if (same) return base + c.off;
     }
@@ -131,6 +133,24 @@ struct G {
     }
     launch_gemm(g, dim3((g.N + 63) / 64, (M + 63) / 64, 1), s);
     return check_launch("k_gemm (sdf)");
+  }
+  // the first reverse GEMM with d sdf / d z7 = softplus_backward(W8[0], z7) applied to the stored
+  // lin7 factors D7 as they are loaded (k_lgemm ATR); false (nothing launched) where k_lgemm does not
+  // run, and the caller materialises G7 with k_sdf_gtop instead
+  bool bwd_top(float* dX, long ldX, int K, const float* D7, const float* w8, int Nout, const float* W, int in_ch,
+               const float* spd, int spd_n) {
+    if (!x3 || !limg || M <= 0) return false;
+    GemmArgs g{};
+    g.M = M; g.N = K; g.nseg = 1; g.x3 = 1; g.ksplit = 1;
+    g.seg[0] = GemmSeg{D7, 256, 1, W, in_ch, 1, Nout};
+    g.C = dX; g.ldc = ldX;
+    g.spd = spd; g.ldsd = 256; g.spd_n = spd_n;
+    g.a_softplus_w = w8;
+    if (!lgemm_supported(g)) return false;
+    const void* img = limg->get(g, s);
+    if (!img) return false;
+    (void)lgemm_run(g, img, cus, s);
+    return true;
   }
   // Y = epi([X0 | X1] [W[:, c0:c0+K0] | W[:, c1:c1+K1]]^T + bias)
   int fwd(float* Y, long ldY, int N, const float* W, int in_ch, const float* bias, const float* X0, long ld0, int K0,
@@ -318,9 +338,13 @@ int anr_sdf_render_fwd(const anr_sdf_params* p, const anr_sdf_frame* f, const fl
     ANR_TRY(g.fwd(F(L.Y8), 264, 257, WN(8), 256, tp[24], Hb, 256, 256, 0, false));
 
     // B4 gradient of sdf w.r.t. the canonical point (reverse mode through the stored factors)
-    hipLaunchKernelGGL(k_sdf_gtop, dim3((unsigned)(((long)cnt * 256 + 255) / 256)), pb, 0, s, a);
-    ANR_TRY(check_launch("k_sdf_gtop"));
-    ANR_TRY(g.bwd(Gb, 256, 256, Ga, 256, 256, WN(7), 256, Dl(6), 256));
+    if (g.bwd_top(Gb, 256, 256, Dl(7), WN(8), 256, WN(7), 256, Dl(6), 256)) {
+      ANR_TRY(check_launch("k_lgemm (sdf, fused top)"));
+    } else {
+      hipLaunchKernelGGL(k_sdf_gtop, dim3((unsigned)(((long)cnt * 256 + 255) / 256)), pb, 0, s, a);
+      ANR_TRY(check_launch("k_sdf_gtop"));
+      ANR_TRY(g.bwd(Gb, 256, 256, Ga, 256, 256, WN(7), 256, Dl(6), 256));
+    }
     ANR_TRY(g.bwd(Ga, 256, 256, Gb, 256, 256, WN(6), 256, Dl(5), 256));
     ANR_TRY(g.bwd(Gb, 256, 256, Ga, 256, 256, WN(5), 256, Dl(4), 256));
     ANR_TRY(g.bwd(Gc, 256, 256, Gb, 256, 256, WN(4), 256, Dl(3), 217, sqrt2));
