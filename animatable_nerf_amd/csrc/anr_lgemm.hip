@@ -150,7 +150,7 @@ __device__ __forceinline__ void lg_epilogue(const LGemm& g, const f32x4 (&acc)[N
       }
       if constexpr (SPD) {
         const float d = sp[ob][e];
-        if (n + e < g.spd_n && d >= 0.f) x = x * d / (d + 1.f);
+        if (n + e < g.spd_n && d >= 0.f) x = x * d * __builtin_amdgcn_rcpf(d + 1.f);
       }
       if (g.div_post != 0.f) x = x / g.div_post;
       v[e] = x;
@@ -170,6 +170,9 @@ __device__ __forceinline__ void lg_epilogue(const LGemm& g, const f32x4 (&acc)[N
     }
   }
 }
+
+// (the softplus-backward factor d / (d + 1) uses the hardware reciprocal, ~1 ulp: these layers are
+// VALU-heavy enough that the IEEE division sequence shows in their time)
 
 // the activation fragments of k-step ks of a 16-sample tile: lane -> sample 16 t + (lane & 15), k =
 // 32 ks' + lg_kcol(lane >> 4, 0..7) of the segment holding ks (rows past M read row M - 1, 4-groups
@@ -242,7 +245,7 @@ __device__ __forceinline__ void lg_tile(const LGemm& g, f32x4 (&buf)[KST][2], in
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const float w = atr_lds[k0 + lg_kcol(kg, e)];
-        x[e] = x[e] >= 0.f ? w * x[e] / (x[e] + 1.f) : w;
+        x[e] = x[e] >= 0.f ? w * x[e] * __builtin_amdgcn_rcpf(x[e] + 1.f) : w;
       }
     }
 #pragma unroll
