@@ -22,7 +22,10 @@ using namespace anr;
 
 namespace {
 
-constexpr long SDF_BATCH = 1L << 19;
+#ifndef ANR_SDF_BATCH_LOG2
+#define ANR_SDF_BATCH_LOG2 19
+#endif
+constexpr long SDF_BATCH = 1L << ANR_SDF_BATCH_LOG2;  // kept samples per layer-GEMM batch
 constexpr size_t SDF_LIMG_BYTES = 16u << 20;  // split-bf16 layer-GEMM weight images (31 GEMMs, <= 384 KiB each)
 
 struct SLayout {

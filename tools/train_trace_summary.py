@@ -19,3 +19,10 @@ for r in step:
     agg[r['Kernel_Name'].replace('anr::', '')[:60]][1] += d
 for n, (c, t) in sorted(agg.items(), key=lambda x: -x[1][1])[:14]:
     print('%-60s %3d %8.1f %6.1f' % (n, c, t, t / c))
+gaps = []
+for p, q in zip(step[:-1], step[1:]):
+    g = (int(q['Start_Timestamp']) - int(p['End_Timestamp'])) / 1e3
+    gaps.append((g, p['Kernel_Name'].replace('anr::', '')[:40], q['Kernel_Name'].replace('anr::', '')[:40]))
+print('idle between kernels %.1f us; largest gaps:' % sum(max(g[0], 0) for g in gaps))
+for g in sorted(gaps, reverse=True)[:8]:
+    print('  %7.1f us  %s -> %s' % g)
