@@ -34,8 +34,17 @@ static const WDesc kWDesc[] = {
     {13, 256, 256, 1, {0, 0}, {256, 0}},   {15, 256, 256, 1, {0, 0}, {256, 0}}, {17, 1, 256, 1, {0, 0}, {256, 0}},
     {19, 256, 256, 1, {0, 0}, {256, 0}},   {21, 256, 384, 1, {0, 0}, {256, 0}}, {23, 128, 283, 2, {0, 256}, {256, 27}},
     {25, 3, 128, 1, {0, 0}, {128, 0}},
+    // novel_pose_bw (animation stage; index ANR_NUM_TENSORS + its state_dict position, kept last so
+    // a call without it packs only the entries above)
+    {46 + 1, 256, 191, 1, {0, 0}, {63, 0}},  {46 + 3, 256, 256, 1, {0, 0}, {256, 0}},
+    {46 + 5, 256, 256, 1, {0, 0}, {256, 0}},  {46 + 7, 256, 256, 1, {0, 0}, {256, 0}},
+    {46 + 9, 256, 256, 1, {0, 0}, {256, 0}},  {46 + 11, 256, 447, 2, {0, 191}, {63, 256}},
+    {46 + 13, 256, 256, 1, {0, 0}, {256, 0}}, {46 + 15, 256, 256, 1, {0, 0}, {256, 0}},
+    {46 + 17, 24, 256, 1, {0, 0}, {256, 0}},
 };
+constexpr int kNWBase = 22;  // entries of the network's own tensors (the rest: novel_pose_bw)
 constexpr int kNW = sizeof(kWDesc) / sizeof(kWDesc[0]);
+static_assert(kNW - kNWBase <= kNWBase, "WPackArgs holds one range");
 
 static int rup64(int v) { return (v + 63) / 64 * 64; }
 
@@ -46,9 +55,9 @@ struct WPackJob {
   long start, dst;        // first element (flat) and destination offset (elements)
 };
 struct WPackArgs {
-  WPackJob job[2 * kNW];
+  WPackJob job[2 * 22];  // one launch per descriptor range (kernel arguments stay < 4 KiB)
   int njob;
-  long total;
+  long total, first, packed;  // image elements (hi); this launch's element range [first, packed)
   unsigned short* out;
 };
 
@@ -59,8 +68,8 @@ __device__ __forceinline__ unsigned short f2bf_rne(float f) {
 }
 
 __global__ void k_wimg_pack(WPackArgs a) {
-  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= a.total) return;
+  const long e = a.first + (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= a.packed) return;
   int j = 0;
   while (j + 1 < a.njob && e >= a.job[j + 1].start) ++j;
   const WPackJob& J = a.job[j];
@@ -110,21 +119,29 @@ size_t wimg_bytes() { return (size_t)wimg_layout(nullptr) * 2 * 2; }
 int wimg_pack(const float* const* t, void* dst, hipStream_t s) {
   std::vector<WPackJob> jobs;
   const long total = wimg_layout(&jobs);
-  WPackArgs a{};
-  for (size_t j = 0; j < jobs.size(); ++j) {
-    a.job[j] = jobs[j];
-    a.job[j].W = t[kWDesc[j / 2].t];
+  // the network's own images, then (when given) the novel_pose_bw images: one launch per range
+  const bool novel = t[kWDesc[kNWBase].t] != nullptr;
+  const int ranges[3] = {0, 2 * kNWBase, 2 * kNW};
+  for (int r = 0; r < (novel ? 2 : 1); ++r) {
+    WPackArgs a{};
+    a.njob = ranges[r + 1] - ranges[r];
+    for (int j = 0; j < a.njob; ++j) {
+      a.job[j] = jobs[ranges[r] + j];
+      a.job[j].W = t[kWDesc[(ranges[r] + j) / 2].t];
+    }
+    a.total = total;
+    a.first = jobs[ranges[r]].start;
+    a.packed = ranges[r + 1] < 2 * kNW ? jobs[ranges[r + 1]].start : total;
+    a.out = (unsigned short*)dst;
+    hipLaunchKernelGGL(k_wimg_pack, dim3((unsigned)((a.packed - a.first + 255) / 256)), dim3(256), 0, s, a);
   }
-  a.njob = (int)jobs.size();
-  a.total = total;
-  a.out = (unsigned short*)dst;
-  hipLaunchKernelGGL(k_wimg_pack, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, a);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 bool wimg_view(const void* base, const float* const* t, const float* W, int c0, int K, bool bwd, WView* v) {
   long off = 0;
-  for (int i = 0; i < kNW; ++i) {
+  const int nw = t[kWDesc[kNWBase].t] != nullptr ? kNW : kNWBase;
+  for (int i = 0; i < nw; ++i) {
     const WDesc& d = kWDesc[i];
     int fld = 0, col[2] = {0, 0};
     for (int s = 0; s < d.nseg; ++s) { col[s] = fld; fld += rup64(d.k[s]); }

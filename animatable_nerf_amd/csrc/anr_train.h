@@ -84,7 +84,9 @@ struct RGemm {
 };
 void launch_rgemm(const RGemm& g, int M_host, hipStream_t s);
 // bf16 weight images of the training GEMM weights: forward (rows = outputs, k = used input columns,
-// segments padded to 64) and backward (rows = input columns, k = outputs padded to 64)
+// segments padded to 64) and backward (rows = input columns, k = outputs padded to 64). t: the
+// ANR_NUM_TENSORS network tensors followed by the ANR_NUM_NOVEL_TENSORS novel_pose_bw tensors
+// (NULL when absent: their images are then neither packed nor viewable)
 size_t wimg_bytes();
 int wimg_pack(const float* const* t, void* dst, hipStream_t s);
 struct WView {

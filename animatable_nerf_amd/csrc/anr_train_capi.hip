@@ -71,7 +71,7 @@ struct Exec {
   int bf16 = 0;       // current GEMMs take bf16 operands
   int pose_fp32 = 0;  // precision ANR_BF16 keeps the pose-space BW MLP in fp32 (ANR_BF16_ALL does not)
   const void* wimg = nullptr;          // bf16 weight images (anr_tgemm.hip), packed for this call
-  const float* const* pt = nullptr;    // the parameter tensors the images were packed from
+  const float* pt[ANR_NUM_TENSORS + ANR_NUM_NOVEL_TENSORS] = {};  // the tensors they were packed from
   float* wslab = nullptr;              // weight-gradient partial slabs (anr_tgemm.hip k_wgrad)
   int x3 = 0;  // inside the pose scope of ANR_BF16: split-bf16 (fp32-level) row GEMMs instead of fp32
 
@@ -190,12 +190,13 @@ struct PoseScope {
 
 // bf16 weight images for the row GEMM (bf16 policies only; refreshed on every call, the weights may
 // have changed since the last)
-int pack_images(Exec& e, const anr_params* p, char* dst, hipStream_t s, float* wslab) {
+int pack_images(Exec& e, const anr_params* p, char* dst, hipStream_t s, float* wslab, bool novel = false) {
   if (!e.bf16) return ANR_OK;
   e.wslab = wslab;
-  if (wimg_pack(p->t, dst, s) != 0) return check_launch("k_wimg_pack");
+  for (int i = 0; i < ANR_NUM_TENSORS; ++i) e.pt[i] = p->t[i];
+  for (int i = 0; i < ANR_NUM_NOVEL_TENSORS; ++i) e.pt[ANR_NUM_TENSORS + i] = novel ? p->novel[i] : nullptr;
+  if (wimg_pack(e.pt, dst, s) != 0) return check_launch("k_wimg_pack");
   e.wimg = dst;
-  e.pt = p->t;
   return ANR_OK;
 }
 
@@ -437,7 +438,7 @@ int train_backward(const anr_params* p, float* const* g, const anr_frame* f, con
 // ---- (f) animation stage: aninerf_animation_trainer.NetworkWrapper.forward + backward ----------
 struct ALayout {
   size_t counts, amax, acc, pt, Gp, Ip, Lp, Bp, lbs, Gt, It, Lt, Bt, Hp, Ht, Hn, Alpha, sel;
-  size_t dBp, dBt, dLp, dLt, dIt, dGt, dA, dB, ysum, fold, total;
+  size_t dBp, dBt, dLp, dLt, dIt, dGt, dA, dB, ysum, fold, wimg, wslab, total;
 };
 
 ALayout alayout(long N) {
@@ -457,6 +458,8 @@ ALayout alayout(long N) {
   T.dBp = take(n * 96); T.dBt = take(n * 96); T.dLp = take(n * 128); T.dLt = take(n * 128); T.dIt = take(n * 128);
   T.dGt = take(n * 256); T.dA = take(n * 1024); T.dB = take(n * 1024); T.ysum = take(8 * 256 * 4);
   T.fold = take(1280 * 4);
+  T.wimg = take(wimg_bytes());
+  T.wslab = take(wgrad_slab_floats() * 4);
   T.total = o;
   return T;
 }
@@ -697,6 +700,7 @@ int anr_anim_step(const anr_params* p, float* const* grads, const anr_frame* f, 
   hipLaunchKernelGGL(k_prep, dim3(1), dim3(256), 0, s, pa);
   ANR_TRY(check_launch("k_prep(anim)"));
   Exec e{s, 0, (o->precision == ANR_BF16 || o->precision == ANR_BF16_ALL) ? 1 : 0, o->precision == ANR_BF16 ? 1 : 0};
+  ANR_TRY(pack_images(e, p, ws + T.wimg, s, (float*)(ws + T.wslab), true));
   ANR_TRY(anim_path(p, grads, f, wpts, n_obs, true, o, ws, T, s, e));
   ANR_TRY(anim_path(p, grads, f, tpts, n_can, false, o, ws, T, s, e));
   hipLaunchKernelGGL(k_an_loss_final, dim3(1), dim3(1), 0, s, (const float*)(ws + T.acc),
