@@ -176,19 +176,25 @@ bool wimg_view(const void* base, const float* const* t, const float* W, int c0, 
 // ------------------------------------------------------------------------------------------
 // the row GEMM
 // ------------------------------------------------------------------------------------------
-#define RG_B_BYTES (256 * 64 * 2)     // bf16 weight rows, 256 rows x 64 k
-// bf16: 128 rows per workgroup (8 waves = 2 row groups x 4 column groups of 64), 2-slot ring, so the
-// weight image each workgroup streams serves twice the rows; X3 (split-bf16, fp32-level: lo*h + h*lo
-// + h*h, the weight rows' lo image riding in the same slot): 64 rows, 4 waves, 2 slots
+// 128 rows per workgroup (8 waves = 2 row groups x 4 column groups of 64), 2-slot ring, so the
+// weight image each workgroup streams serves 128 rows. bf16: 64-deep K chunks. X3 (split-bf16,
+// fp32-level: lo*h + h*lo + h*h, the weight rows' lo image riding in the same slot): 32-deep chunks
+// so that three 128-row operand images fit two slots.
 template <bool X3> struct RgCfg {
-  static constexpr int BM = X3 ? 64 : 128;
+  static constexpr int BM = 128;
   static constexpr int WAVES = BM / 16;
-  static constexpr int A_BYTES = BM * 64 * 4;                          // fp32 activations, BM rows x 64 k
+  static constexpr int KC = X3 ? 32 : 64;                              // K chunk
+  static constexpr int A_BYTES = BM * KC * 4;                          // fp32 activations, BM rows x KC
+  static constexpr int B_BYTES = 256 * KC * 2;                         // bf16 weight rows, 256 x KC
   static constexpr int NS = 2;                                         // ring slots
-  static constexpr int SLOT = A_BYTES + RG_B_BYTES * (X3 ? 2 : 1);     // bytes per slot
+  static constexpr int SLOT = A_BYTES + B_BYTES * (X3 ? 2 : 1);        // bytes per slot
   static constexpr int PIECES_A = A_BYTES / 1024 / WAVES;              // per wave
-  static constexpr int PIECES_B = RG_B_BYTES / 1024 / WAVES;
+  static constexpr int PIECES_B = B_BYTES / 1024 / WAVES;
   static constexpr int OPS = PIECES_A + PIECES_B * (X3 ? 2 : 1);       // vmem ops per wave per chunk
+  static constexpr int CHA = KC / 4, CHB = KC / 8;                     // 16-B chunks per A / B row
+  // XOR swizzle of a row's 16-B chunks, chosen so the 16 rows of one fragment read hit distinct banks
+  static __device__ __forceinline__ int swa(int r) { return X3 ? ((r >> 1) & 7) : (r & 15); }
+  static __device__ __forceinline__ int swb(int r) { return X3 ? ((r >> 2) & 3) : (r & 7); }
 };
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
@@ -207,30 +213,31 @@ __device__ __forceinline__ void rg_dma(const void* src, unsigned m0) {
 template <bool X3>
 __device__ __forceinline__ void rg_issue(const RGemm& g, int seg, int kk, int m0, int M, int N, unsigned slot_lds, int w,
                                          int lane) {
+  using C = RgCfg<X3>;
   const float* A = seg ? g.seg[1].A : g.seg[0].A;
   const long lda = seg ? g.seg[1].lda : g.seg[0].lda;
   const unsigned short* B = seg ? g.seg[1].B : g.seg[0].B;
   const long ldb = seg ? g.seg[1].ldb : g.seg[0].ldb;
   const int bcol = seg ? g.seg[1].bcol : g.seg[0].bcol;
   const int brows = seg ? g.seg[1].rows : g.seg[0].rows;
-  // A: BM rows x 256 B; piece p = 4 rows; lane -> row 4p + (lane >> 4), LDS chunk (lane & 15) holds
-  // source chunk (lane & 15) ^ (row & 15)
-  using C = RgCfg<X3>;
+  // A: BM rows x CHA chunks; a 1 KiB piece holds 64 / CHA rows; LDS chunk q of row r holds source
+  // chunk q ^ swa(r)
+  constexpr int RPA = 64 / C::CHA, RPB = 64 / C::CHB;
 #pragma unroll
   for (int i = 0; i < C::PIECES_A; ++i) {
     const int p = w + C::WAVES * i;
-    const int r = 4 * p + (lane >> 4);
+    const int r = RPA * p + lane / C::CHA;
     const int gr = min(m0 + r, M - 1);
-    const int ch = (lane & 15) ^ (r & 15);
+    const int ch = (lane % C::CHA) ^ C::swa(r);
     rg_dma(A + (long)gr * lda + kk + ch * 4, slot_lds + p * 1024);
   }
-  // B: 256 rows x 128 B; piece p = 8 rows; lane -> row 8p + (lane >> 3), chunk (lane & 7) ^ (row & 7)
+  // B: 256 rows x CHB chunks, chunk q of row r holds source chunk q ^ swb(r)
 #pragma unroll
   for (int i = 0; i < C::PIECES_B; ++i) {
     const int p = w + C::WAVES * i;
-    const int r = 8 * p + (lane >> 3);
+    const int r = RPB * p + lane / C::CHB;
     const int br = min(r, brows - 1);
-    const int ch = (lane & 7) ^ (r & 7);
+    const int ch = (lane % C::CHB) ^ C::swb(r);
     rg_dma(B + (long)br * ldb + bcol + kk + ch * 8, slot_lds + C::A_BYTES + p * 1024);
   }
   if constexpr (X3) {
@@ -238,10 +245,10 @@ __device__ __forceinline__ void rg_issue(const RGemm& g, int seg, int kk, int m0
 #pragma unroll
     for (int i = 0; i < C::PIECES_B; ++i) {
       const int p = w + C::WAVES * i;
-      const int r = 8 * p + (lane >> 3);
+      const int r = RPB * p + lane / C::CHB;
       const int br = min(r, brows - 1);
-      const int ch = (lane & 7) ^ (r & 7);
-      rg_dma(B + lo + (long)br * ldb + bcol + kk + ch * 8, slot_lds + C::A_BYTES + RG_B_BYTES + p * 1024);
+      const int ch = (lane % C::CHB) ^ C::swb(r);
+      rg_dma(B + lo + (long)br * ldb + bcol + kk + ch * 8, slot_lds + C::A_BYTES + C::B_BYTES + p * 1024);
     }
   }
   (void)N;
@@ -258,14 +265,15 @@ __global__ __launch_bounds__(RgCfg<X3>::WAVES * 64) void k_rgemm(RGemm g) {
   if (m0 >= M) return;
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const unsigned base = (unsigned)(uintptr_t)lds;
-  const int nc0 = (g.seg[0].K + 63) >> 6;
-  const int nch = nc0 + (g.nseg > 1 ? (g.seg[1].K + 63) >> 6 : 0);
+  constexpr int KC = RgCfg<X3>::KC;
+  const int nc0 = (g.seg[0].K + KC - 1) / KC;
+  const int nch = nc0 + (g.nseg > 1 ? (g.seg[1].K + KC - 1) / KC : 0);
   auto issue = [&](int c) {
 #ifdef RG_EXP_NODMA
     return;  // timing experiment only (results garbage)
 #endif
     const int seg = c < nc0 ? 0 : 1;
-    const int kk = (c - (seg ? nc0 : 0)) * 64;
+    const int kk = (c - (seg ? nc0 : 0)) * KC;
     rg_issue<X3>(g, seg, kk, m0, M, N, base + (c % RG_NS) * RG_SLOT, w, lane);
   };
   const int pro = nch < RG_NS ? nch : RG_NS;
@@ -279,7 +287,6 @@ __global__ __launch_bounds__(RgCfg<X3>::WAVES * 64) void k_rgemm(RGemm g) {
   const int wr = (w >> 2) * 64;   // this wave's 64 rows of the tile
   const int wc = (w & 3) * 64;    // and 64 output columns
   const bool active = wc < N;     // which hold some of the N
-  const int sw = lane & 7;         // row & 7 of every fragment row this lane reads (rows 16i + (lane & 15))
 
   for (int c = 0; c < nch; ++c) {
     // chunks issued after c: min(nch, c + RG_NS) - c - 1 (the refill of c - 1's slot went out last iteration)
@@ -289,7 +296,7 @@ __global__ __launch_bounds__(RgCfg<X3>::WAVES * 64) void k_rgemm(RGemm g) {
     else rg_wait<0>();
     __builtin_amdgcn_s_barrier();
     const int seg = c < nc0 ? 0 : 1;
-    const int kk = (c - (seg ? nc0 : 0)) * 64;
+    const int kk = (c - (seg ? nc0 : 0)) * KC;
     const int K = seg ? g.seg[1].K : g.seg[0].K;
     const unsigned char* sA = lds + (c % RG_NS) * RG_SLOT;
     const unsigned char* sB = sA + RG_A_BYTES;
@@ -299,17 +306,18 @@ __global__ __launch_bounds__(RgCfg<X3>::WAVES * 64) void k_rgemm(RGemm g) {
     if (active) {
 #endif
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
+      for (int ks = 0; ks < KC / 32; ++ks) {
         bf16x8_t af[4], bfr[4], al[4], bl[4];
         const int kc = 4 * ks + (lane >> 4);  // 8-element k group of this lane
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int r = wr + 16 * i + (lane & 15);
-          // fp32 row r, k = 8 kc .. 8 kc + 7: 16-B chunks 2 kc, 2 kc + 1 (swizzled by r & 15)
-          const f32x4 x0 = *(const f32x4*)(sA + r * 256 + (((2 * kc) ^ (r & 15)) * 16));
-          const f32x4 x1 = *(const f32x4*)(sA + r * 256 + (((2 * kc + 1) ^ (r & 15)) * 16));
+          // fp32 row r, k = 8 kc .. 8 kc + 7: 16-B chunks 2 kc, 2 kc + 1 (swizzled by swa(r))
+          const int sa = RgCfg<X3>::swa(r);
+          const f32x4 x0 = *(const f32x4*)(sA + r * (KC * 4) + (((2 * kc) ^ sa) * 16));
+          const f32x4 x1 = *(const f32x4*)(sA + r * (KC * 4) + (((2 * kc + 1) ^ sa) * 16));
           float x[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
-          if (kk + 64 > K) {  // the last, partial chunk of a segment: columns past K read as zero
+          if (kk + KC > K) {  // the last, partial chunk of a segment: columns past K read as zero
 #pragma unroll
             for (int e = 0; e < 8; ++e) x[e] = (kk + 8 * kc + e < K) ? x[e] : 0.0f;
           }
@@ -322,8 +330,9 @@ __global__ __launch_bounds__(RgCfg<X3>::WAVES * 64) void k_rgemm(RGemm g) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int r = wc + 16 * j + (lane & 15);
-          bfr[j] = *(const bf16x8_t*)(sB + r * 128 + ((kc ^ sw) * 16));
-          if constexpr (X3) bl[j] = *(const bf16x8_t*)(sB + RG_B_BYTES + r * 128 + ((kc ^ sw) * 16));
+          const int sb = RgCfg<X3>::swb(r);
+          bfr[j] = *(const bf16x8_t*)(sB + r * (KC * 2) + ((kc ^ sb) * 16));
+          if constexpr (X3) bl[j] = *(const bf16x8_t*)(sB + RgCfg<X3>::B_BYTES + r * (KC * 2) + ((kc ^ sb) * 16));
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i)
