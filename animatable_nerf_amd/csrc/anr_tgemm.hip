@@ -45,6 +45,7 @@ static const WDesc kWDesc[] = {
 constexpr int kNWBase = 22;  // entries of the network's own tensors (the rest: novel_pose_bw)
 constexpr int kNW = sizeof(kWDesc) / sizeof(kWDesc[0]);
 static_assert(kNW - kNWBase <= kNWBase, "WPackArgs holds one range");
+static_assert(WG_MAX_Z % 8 == 0, "k_wgrad XCD order");
 
 static int rup64(int v) { return (v + 63) / 64 * 64; }
 
@@ -512,7 +513,14 @@ __global__ __launch_bounds__(256) void k_wgrad(WGrad g) {
   __shared__ __attribute__((aligned(16))) unsigned short sX[2][NI][NH * WG_S * WG_LD];
   __shared__ float srs[8][WG_T];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int ti = blockIdx.x, tj = blockIdx.y, z = blockIdx.z;
+  // XCD-aware order: workgroups are dealt to the 8 XCDs round-robin by linear id, so the tiles of
+  // one sample range (which read the same dY and X rows) are given ids on one XCD and share its L2
+  // (launch_wgrad makes the range count a multiple of 8)
+  const int tiles = gridDim.x * gridDim.y;
+  const int L = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+  const int slot = L >> 3, tile = slot % tiles;
+  const int z = (slot / tiles) * 8 + (L & 7);
+  const int ti = tile % gridDim.x, tj = tile / gridDim.x;
   const int n = g.M_dev ? *g.M_dev : g.n;
   const int s0 = z * g.spb, s1 = min(n, s0 + g.spb);
   const int i0 = ti * WG_T, j0 = tj * WG_T;
@@ -641,8 +649,9 @@ int launch_wgrad(WGrad g, int n_host, hipStream_t s) {
   // samples per workgroup: enough workgroups to cover the CUs, at most WG_MAX_Z slabs
   int nz = (n_host + 383) / 384;
   nz = nz < 1 ? 1 : (nz > WG_MAX_Z ? WG_MAX_Z : nz);
+  nz = (nz + 7) / 8 * 8;  // a multiple of 8 for the XCD-aware order (trailing ranges may be empty)
   g.spb = ((n_host + nz - 1) / nz + 2 * WG_S - 1) / (2 * WG_S) * (2 * WG_S);  // whole 64-sample steps
-  g.nz = (n_host + g.spb - 1) / g.spb;
+  g.nz = nz;
   g.n = n_host;
   g.rs_slab = (g.bsum || g.bsum2) ? g.slab + (size_t)WG_MAX_Z * 4 * WG_TILE_FLOATS : nullptr;
   if (g.x3) hipLaunchKernelGGL(k_wgrad<true>, dim3(ti, tj, g.nz), dim3(256), 0, s, g);
