@@ -20,7 +20,9 @@
 
 namespace anr {
 
-#define SDF_MAX_VERTS 6912
+#define SDF_MAX_VERTS 6912  // even: the scan pads an odd count with one far vertex
+
+typedef float pf2 __attribute__((ext_vector_type(2)));
 
 // ------------------------------------------------------------------------------------------
 // B1 front-end. Persistent: one 1024-thread workgroup per CU holds the posed vertices in LDS
@@ -32,6 +34,7 @@ __global__ __launch_bounds__(1024) void k_sdf_front(SdfFrontArgs a) {
   __shared__ float4 sv[SDF_MAX_VERTS];
   for (int j = threadIdx.x; j < a.nv; j += blockDim.x)
     sv[j] = make_float4(a.verts[3 * j], a.verts[3 * j + 1], a.verts[3 * j + 2], 0.f);
+  if ((a.nv & 1) && threadIdx.x == 0) sv[a.nv] = make_float4(INFINITY, INFINITY, INFINITY, 0.f);
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int wpb = blockDim.x >> 6;
@@ -41,11 +44,7 @@ __global__ __launch_bounds__(1024) void k_sdf_front(SdfFrontArgs a) {
     world_to_pose(pts, a.R, a.Th, p);
     float b0 = INFINITY, b1 = INFINITY, b2 = INFINITY, b3 = INFINITY, b4 = INFINITY;
     int i0 = 0, i1 = 0, i2 = 0, i3 = 0, i4 = 0;
-#pragma unroll 4
-    for (int j = 0; j < a.nv; ++j) {
-      const float4 v = sv[j];
-      const float dx = p[0] - v.x, dy = p[1] - v.y, dz = p[2] - v.z;
-      const float d = (dx * dx + dy * dy) + dz * dz;
+    auto insert = [&](float d, int j) {
       if (d < b4) {
         if (d < b3) {
           b4 = b3; i4 = i3;
@@ -59,6 +58,18 @@ __global__ __launch_bounds__(1024) void k_sdf_front(SdfFrontArgs a) {
           } else { b3 = d; i3 = j; }
         } else { b4 = d; i4 = j; }
       }
+    };
+    // two vertices per step on packed fp32 (v_pk_add / v_pk_mul: per-element IEEE, no contraction,
+    // so each d^2 is the scalar formula's), inserted in index order; the vertex array is padded to
+    // an even count with a far-away vertex that never enters the 5-NN
+    const pf2 P0 = {p[0], p[0]}, P1 = {p[1], p[1]}, P2 = {p[2], p[2]};
+#pragma unroll 2
+    for (int j = 0; j < a.nv; j += 2) {
+      const float4 va = sv[j], vb = sv[j + 1];
+      const pf2 dx = P0 - pf2{va.x, vb.x}, dy = P1 - pf2{va.y, vb.y}, dz = P2 - pf2{va.z, vb.z};
+      const pf2 d = (dx * dx + dy * dy) + dz * dz;
+      insert(d[0], j);
+      insert(d[1], j + 1);
     }
     // sample_blend_closest_points: dists = sqrt(d^2); disp = 1 / (dists + 1e-8); torch's 5-element
     // sum order is ((((x0 + x4) + x1) + x2) + x3); weights = disp / sum; pnorm = sequential sum d*w
