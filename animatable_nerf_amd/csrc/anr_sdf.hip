@@ -31,10 +31,15 @@ typedef float pf2 __attribute__((ext_vector_type(2)));
 // pytorch3d knn_points' bounded max-heap result. d^2 = (dx*dx + dy*dy) + dz*dz, no contraction.
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(1024) void k_sdf_front(SdfFrontArgs a) {
+  // vertex pairs (2i, 2i + 1) as {x, x', y, y', z, z', -, -}: two 16-B reads give the packed operands
   __shared__ float4 sv[SDF_MAX_VERTS];
-  for (int j = threadIdx.x; j < a.nv; j += blockDim.x)
-    sv[j] = make_float4(a.verts[3 * j], a.verts[3 * j + 1], a.verts[3 * j + 2], 0.f);
-  if ((a.nv & 1) && threadIdx.x == 0) sv[a.nv] = make_float4(INFINITY, INFINITY, INFINITY, 0.f);
+  for (int j = threadIdx.x; j < a.nv + 1; j += blockDim.x) {
+    const bool in = j < a.nv;
+    const float x = in ? a.verts[3 * j] : INFINITY, y = in ? a.verts[3 * j + 1] : INFINITY;
+    const float z = in ? a.verts[3 * j + 2] : INFINITY;
+    float* q = (float*)&sv[(j >> 1) * 2] + (j & 1);
+    if (j < a.nv || (a.nv & 1)) { q[0] = x; q[2] = y; q[4] = z; }
+  }
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int wpb = blockDim.x >> 6;
@@ -66,10 +71,12 @@ __global__ __launch_bounds__(1024) void k_sdf_front(SdfFrontArgs a) {
 #pragma unroll 2
     for (int j = 0; j < a.nv; j += 2) {
       const float4 va = sv[j], vb = sv[j + 1];
-      const pf2 dx = P0 - pf2{va.x, vb.x}, dy = P1 - pf2{va.y, vb.y}, dz = P2 - pf2{va.z, vb.z};
+      const pf2 dx = P0 - pf2{va.x, va.y}, dy = P1 - pf2{va.z, va.w}, dz = P2 - pf2{vb.x, vb.y};
       const pf2 d = (dx * dx + dy * dy) + dz * dz;
-      insert(d[0], j);
-      insert(d[1], j + 1);
+      if (fminf(d[0], d[1]) < b4) {  // one test per pair: most pairs insert nothing
+        insert(d[0], j);
+        insert(d[1], j + 1);
+      }
     }
     // sample_blend_closest_points: dists = sqrt(d^2); disp = 1 / (dists + 1e-8); torch's 5-element
     // sum order is ((((x0 + x4) + x1) + x2) + x3); weights = disp / sum; pnorm = sequential sum d*w
