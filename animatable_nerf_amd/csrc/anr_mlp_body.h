@@ -405,9 +405,6 @@ __host__ __device__ constexpr int x3_issue_at(int G) {
 template <bool B16, int V, int E, bool RELU_IN, int NIN, int NOUT>
 __device__ __forceinline__ void layer_x3(Pipe& p, const f32x4 (&in)[NIN], const float (&emb)[16], const float (&vemb)[8],
                                          f32x4 (&out)[NOUT], const float* __restrict__ sbias, int g, int lane) {
-#ifdef ANR_EXP_PRIO
-  __builtin_amdgcn_s_setprio(ANR_EXP_PRIO);  // experiment: MFMA-stream waves first
-#endif
   constexpr int L = prog_layer<V>(E);
   constexpr LayerDesc D = layer_desc_all(L);
   constexpr int KS = ks32(L);
@@ -514,9 +511,6 @@ __device__ __forceinline__ void layer_x3(Pipe& p, const f32x4 (&in)[NIN], const 
     });
     p.leave();
   });
-#ifdef ANR_EXP_PRIO
-  __builtin_amdgcn_s_setprio(0);
-#endif
 }
 
 template <bool B16, int V, int E, bool RELU, bool RELU_IN = false, int NIN, int NOUT>
