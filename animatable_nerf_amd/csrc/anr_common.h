@@ -174,4 +174,14 @@ __device__ __forceinline__ int block_excl_scan_256(int v, int* sh, int& total) {
   return base + x - v;
 }
 
+// softplus(beta=100, threshold=20) backward factor sigmoid(100 z) recomputed from the layer's OUTPUT
+// h = softplus(z) instead of a stored exp(100 z): sigmoid(100 z) = 1 - exp(-100 h) exactly (above the
+// threshold h = z and the factor rounds to 1, as torch's pass-through). One hardware exp2: the factor
+// is within ~1.5e-7 ABSOLUTE of the stored-factor path's everywhere (relative precision is lost only
+// where the factor itself is < ~1e-3 and its gradient contribution with it; the sdf backward is held
+// to 2e-4 absolute).
+__device__ __forceinline__ float softplus_factor_h(float h) {
+  return 1.f - __builtin_amdgcn_exp2f(h * -144.269504f);
+}
+
 }  // namespace anr

@@ -148,12 +148,13 @@ __device__ __forceinline__ void epilogue(const GemmArgs& g, const f32x4 (&acc)[2
         if (g.softplus) {  // torch softplus(beta=100, threshold=20) and the factor its backward uses
           const float z = v * 100.f;
           const float e = expf(z);
-          g.deriv[(long)m * g.ldd + n] = z > 20.f ? -1.f : e;
+          if (g.deriv) g.deriv[(long)m * g.ldd + n] = z > 20.f ? -1.f : e;
           v = z > 20.f ? v : log1pf(e) / 100.f;
         }
         if (g.spd && n < g.spd_n) {
           const float d = g.spd[(long)m * g.ldsd + n];
-          if (d >= 0.f) v = v * d / (d + 1.f);
+          if (g.spd_h) v = v * softplus_factor_h(d);
+          else if (d >= 0.f) v = v * d / (d + 1.f);
         }
         if (g.mask && !(g.mask[(long)m * g.ldm + n] > 0.f)) v = 0.f;
         if (g.div_post != 0.f) v = v / g.div_post;
@@ -210,13 +211,14 @@ __device__ __forceinline__ void epilogue_sw(const GemmArgs& g, const f32x4 (&acc
           }
           if (g.spd && n + e < g.spd_n) {
             const float d = sp[i][j][e];
-            if (d >= 0.f) x = x * d / (d + 1.f);
+            if (g.spd_h) x = x * softplus_factor_h(d);
+            else if (d >= 0.f) x = x * d / (d + 1.f);
           }
           if (g.mask && !(mk[i][j][e] > 0.f)) x = 0.f;
           if (g.div_post != 0.f) x = x / g.div_post;
           v[e] = x;
         }
-        if (g.softplus) *(f32x4*)(g.deriv + (long)m * g.ldd + n) = dv;
+        if (g.softplus && g.deriv) *(f32x4*)(g.deriv + (long)m * g.ldd + n) = dv;
         *(f32x4*)(g.C + (long)m * g.ldc + n) = v;
       }
     return;
@@ -239,12 +241,13 @@ __device__ __forceinline__ void epilogue_sw(const GemmArgs& g, const f32x4 (&acc
         if (g.softplus) {
           const float z = v * 100.f;
           const float e = expf(z);
-          g.deriv[(long)m * g.ldd + n] = z > 20.f ? -1.f : e;
+          if (g.deriv) g.deriv[(long)m * g.ldd + n] = z > 20.f ? -1.f : e;
           v = z > 20.f ? v : log1pf(e) / 100.f;
         }
         if (g.spd && n < g.spd_n) {
           const float d = g.spd[(long)m * g.ldsd + n];
-          if (d >= 0.f) v = v * d / (d + 1.f);
+          if (g.spd_h) v = v * softplus_factor_h(d);
+          else if (d >= 0.f) v = v * d / (d + 1.f);
         }
         if (g.mask && !(g.mask[(long)m * g.ldm + n] > 0.f)) v = 0.f;
         if (g.div_post != 0.f) v = v / g.div_post;
@@ -601,7 +604,7 @@ void launch_gemm(GemmArgs g, dim3 grid, hipStream_t s) {
   auto al16 = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
   g.vec_out = sw && g.N % 4 == 0 && g.ldc % 4 == 0 && al16(g.C) && (!g.bias || al16(g.bias)) &&
               (!g.mask || (g.ldm % 4 == 0 && al16(g.mask))) && (!g.spd || (g.ldsd % 4 == 0 && al16(g.spd))) &&
-              (!g.softplus || (g.ldd % 4 == 0 && al16(g.deriv)));
+              (!g.softplus || !g.deriv || (g.ldd % 4 == 0 && al16(g.deriv)));
   if (sw) launch_gemm_sw<true>(g, grid, s, a_k, b_k);
   else launch_gemm_sw<false>(g, grid, s, a_k, b_k);
 }

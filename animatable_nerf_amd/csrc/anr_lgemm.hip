@@ -59,6 +59,7 @@ struct LGemm {
   const float* spd;
   long ldsd;
   int spd_n;
+  int spd_h;         // spd / ATR activations are softplus outputs h (factor softplus_factor_h) instead of exp factors
   float div_pre, div_post;
   const float* atr;  // ATR: the activations are softplus factors d, used as (d >= 0 ? atr[k] d / (d + 1) : atr[k])
 };
@@ -150,7 +151,11 @@ __device__ __forceinline__ void lg_epilogue(const LGemm& g, const f32x4 (&acc)[N
       }
       if constexpr (SPD) {
         const float d = sp[ob][e];
-        if (n + e < g.spd_n && d >= 0.f) x = x * d * __builtin_amdgcn_rcpf(d + 1.f);
+        if (g.spd_h) {
+          if (n + e < g.spd_n) x = x * softplus_factor_h(d);
+        } else if (n + e < g.spd_n && d >= 0.f) {
+          x = x * d * __builtin_amdgcn_rcpf(d + 1.f);
+        }
       }
       if (g.div_post != 0.f) x = x / g.div_post;
       v[e] = x;
@@ -159,13 +164,13 @@ __device__ __forceinline__ void lg_epilogue(const LGemm& g, const f32x4 (&acc)[N
     float* d = g.deriv + (long)m * g.ldd + n;
     if (n0 + 16 * ob + 16 <= g.N) {  // uniform: the whole 16-column block is inside N
       *(f32x4*)c = v;
-      if (g.softplus) *(f32x4*)d = dv;
+      if (g.softplus && g.deriv) *(f32x4*)d = dv;
     } else {
 #pragma unroll
       for (int e = 0; e < 4; ++e)
         if (n + e < g.N) {
           c[e] = v[e];
-          if (g.softplus) d[e] = dv[e];
+          if (g.softplus && g.deriv) d[e] = dv[e];
         }
     }
   }
@@ -245,7 +250,7 @@ __device__ __forceinline__ void lg_tile(const LGemm& g, f32x4 (&buf)[KST][2], in
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const float w = atr_lds[k0 + lg_kcol(kg, e)];
-        x[e] = x[e] >= 0.f ? w * x[e] * __builtin_amdgcn_rcpf(x[e] + 1.f) : w;
+        x[e] = g.spd_h ? w * softplus_factor_h(x[e]) : x[e] >= 0.f ? w * x[e] * __builtin_amdgcn_rcpf(x[e] + 1.f) : w;
       }
     }
 #pragma unroll
@@ -389,7 +394,7 @@ LGemm lg_args(const GemmArgs& g, int* nob) {
   a.N = g.N;
   *nob = lg_nob(g.N, a.kst, &a.G);
   a.C = g.C; a.ldc = g.ldc; a.bias = g.bias; a.relu = g.relu; a.softplus = g.softplus; a.deriv = g.deriv;
-  a.ldd = g.ldd; a.spd = g.spd; a.ldsd = g.ldsd; a.spd_n = g.spd_n; a.div_pre = g.div_pre; a.div_post = g.div_post;
+  a.ldd = g.ldd; a.spd = g.spd; a.ldsd = g.ldsd; a.spd_n = g.spd_n; a.spd_h = g.spd_h; a.div_pre = g.div_pre; a.div_post = g.div_post;
   a.atr = g.a_softplus_w;
   return a;
 }
@@ -411,7 +416,7 @@ bool lgemm_supported(const GemmArgs& g) {
     if (q.a_cs != 1 || q.a_rs < (q.K + 7) / 8 * 8) return false;
   }
   if (!al16(g.C) || g.ldc % 4 != 0) return false;
-  if (g.softplus && (!al16(g.deriv) || g.ldd % 4 != 0)) return false;
+  if (g.softplus && g.deriv && (!al16(g.deriv) || g.ldd % 4 != 0)) return false;
   if (g.spd && (!al16(g.spd) || g.ldsd % 4 != 0 || g.bias)) return false;
   int nob = 0;
   const LGemm a = lg_args(g, &nob);

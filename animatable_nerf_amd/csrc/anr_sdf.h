@@ -70,7 +70,8 @@ struct SdfPointArgs {
   float* Xs0;            // [P][40] gamma_6(tpose)
   float* X4;             // [P][256] lin4 input: cols 217..255 = gamma_6 / sqrt(2)
   float* C0;             // [P][40] colour input: tpose, gamma_4(bigdir), gradient
-  const float* D7;       // [P][256] softplus factor of lin7
+  const float* D7;       // [P][256] softplus factor of lin7 (d7_h: lin7's softplus output h)
+  int d7_h;
   float* G7;             // [P][256]
   const float* Gc;       // [P][256] lin4 input gradient (cols 217..255: gamma part)
   const float* gB;       // [P][40] lin0 input gradient

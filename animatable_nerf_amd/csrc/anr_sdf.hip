@@ -20,62 +20,196 @@
 
 namespace anr {
 
-#define SDF_MAX_VERTS 6912  // even: the scan pads an odd count with one far vertex
+#define SDF_MAX_VERTS 6912  // 108 cells of 64 vertices
+#define SDF_CELL 64
+#define SDF_MAX_CELLS (SDF_MAX_VERTS / SDF_CELL)
+#define SDF_SORT_N 8192     // power-of-two key array for the in-LDS bitonic sort
 
 typedef float pf2 __attribute__((ext_vector_type(2)));
 
+// squared distance from p to an axis-aligned box, in the vertex formula's association
+// ((dx*dx + dy*dy) + dz*dz). Each |dx| here is the rounded distance to the box face between p and
+// any vertex inside, so by the monotonicity of IEEE rounding it is <= that vertex's rounded |dx|,
+// and the sum is <= every in-box vertex's d^2 exactly — a bound with no margin.
+__device__ __forceinline__ float box_d2(const float p[3], float4 lo, float4 hi) {
+  const float dx = p[0] < lo.x ? p[0] - lo.x : (p[0] > hi.x ? p[0] - hi.x : 0.f);
+  const float dy = p[1] < lo.y ? p[1] - lo.y : (p[1] > hi.y ? p[1] - hi.y : 0.f);
+  const float dz = p[2] < lo.z ? p[2] - lo.z : (p[2] > hi.z ? p[2] - hi.z : 0.f);
+  return (dx * dx + dy * dy) + dz * dz;
+}
+
+__device__ __forceinline__ uint32_t spread3(uint32_t v) {  // 6 bits -> every third bit
+  uint32_t r = 0;
+#pragma unroll
+  for (int b = 0; b < 6; ++b) r |= ((v >> b) & 1u) << (3 * b);
+  return r;
+}
+
 // ------------------------------------------------------------------------------------------
-// B1 front-end. Persistent: one 1024-thread workgroup per CU holds the posed vertices in LDS
-// (float4, 110 KB); wave = ray, lane = sample. Every lane scans all vertices in index order with a
-// strict '<' sorted insertion, which keeps the K lexicographically smallest (d^2, index) pairs —
-// pytorch3d knn_points' bounded max-heap result. d^2 = (dx*dx + dy*dy) + dz*dz, no contraction.
+// B1 front-end. Persistent: one 1024-thread workgroup per CU. Prologue (per workgroup, ~tens of µs):
+// the posed vertices are Morton-sorted in LDS (18-bit cell code above the 13-bit vertex index,
+// bitonic sort of 8192 keys) and stored in cells of 64 consecutive sorted vertices with their
+// bounding boxes. Wave = ray, lane = sample. The wave visits the cells nearest its middle sample
+// first (a 128-key bitonic sort across the lanes) and skips a cell when no lane's 5th-best d^2
+// reaches the cell's box bound (box_d2: exact, so a skipped cell holds no vertex that could enter
+// or tie). Insertion compares (d^2, index) lexicographically, so the result is the K smallest
+// (d^2, index) pairs whatever the visiting order — pytorch3d knn_points' bounded max-heap result,
+// bit-identical to the earlier full index-order scan. d^2 = (dx*dx + dy*dy) + dz*dz, no contraction.
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(1024) void k_sdf_front(SdfFrontArgs a) {
-  // vertex pairs (2i, 2i + 1) as {x, x', y, y', z, z', -, -}: two 16-B reads give the packed operands
+  // sorted vertex pairs (2i, 2i + 1) as {x, x', y, y', z, z', idx, idx'}: two 16-B reads per pair
   __shared__ float4 sv[SDF_MAX_VERTS];
-  for (int j = threadIdx.x; j < a.nv + 1; j += blockDim.x) {
-    const bool in = j < a.nv;
-    const float x = in ? a.verts[3 * j] : INFINITY, y = in ? a.verts[3 * j + 1] : INFINITY;
-    const float z = in ? a.verts[3 * j + 2] : INFINITY;
-    float* q = (float*)&sv[(j >> 1) * 2] + (j & 1);
-    if (j < a.nv || (a.nv & 1)) { q[0] = x; q[2] = y; q[4] = z; }
+  __shared__ uint32_t keys[SDF_SORT_N];
+  __shared__ float4 cbox[2 * SDF_MAX_CELLS];
+  __shared__ float red[16][6];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int nv = a.nv, ncell = (nv + SDF_CELL - 1) / SDF_CELL;
+
+  // vertex bounds -> 64^3 Morton cells
+  float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+  for (int j = tid; j < nv; j += blockDim.x)
+    for (int c = 0; c < 3; ++c) {
+      const float v = a.verts[3 * j + c];
+      mn[c] = fminf(mn[c], v); mx[c] = fmaxf(mx[c], v);
+    }
+  for (int c = 0; c < 3; ++c)
+    for (int off = 32; off > 0; off >>= 1) {
+      mn[c] = fminf(mn[c], __shfl_xor(mn[c], off));
+      mx[c] = fmaxf(mx[c], __shfl_xor(mx[c], off));
+    }
+  if (lane == 0)
+    for (int c = 0; c < 3; ++c) { red[wid][c] = mn[c]; red[wid][3 + c] = mx[c]; }
+  __syncthreads();
+  for (int w = 0; w < (int)(blockDim.x >> 6); ++w)
+    for (int c = 0; c < 3; ++c) { mn[c] = fminf(mn[c], red[w][c]); mx[c] = fmaxf(mx[c], red[w][3 + c]); }
+  float sc[3];
+  for (int c = 0; c < 3; ++c) sc[c] = mx[c] > mn[c] ? 63.99f / (mx[c] - mn[c]) : 0.f;
+  for (int j = tid; j < SDF_SORT_N; j += blockDim.x) {
+    uint32_t k = 0xffffffffu;
+    if (j < nv) {
+      uint32_t m = 0;
+      for (int c = 0; c < 3; ++c) {
+        const float f = (a.verts[3 * j + c] - mn[c]) * sc[c];
+        const uint32_t q = f >= 0.f ? min((uint32_t)f, 63u) : 0u;  // NaN -> 0
+        m |= spread3(q) << c;
+      }
+      k = (m << 13) | (uint32_t)j;
+    }
+    keys[j] = k;
   }
   __syncthreads();
-  const int lane = threadIdx.x & 63;
+  for (int k = 2; k <= SDF_SORT_N; k <<= 1)
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = tid; i < SDF_SORT_N; i += blockDim.x) {
+        const int l = i ^ j;
+        if (l > i) {
+          const uint32_t x = keys[i], y = keys[l];
+          if (((i & k) == 0) == (x > y)) { keys[i] = y; keys[l] = x; }
+        }
+      }
+      __syncthreads();
+    }
+  for (int s = tid; s < ncell * SDF_CELL; s += blockDim.x) {
+    const bool in = s < nv;
+    const uint32_t j = in ? (keys[s] & 8191u) : 0x7fffu;
+    float* q = (float*)&sv[(s >> 1) * 2] + (s & 1);
+    q[0] = in ? a.verts[3 * j] : INFINITY;
+    q[2] = in ? a.verts[3 * j + 1] : INFINITY;
+    q[4] = in ? a.verts[3 * j + 2] : INFINITY;
+    ((uint32_t*)q)[6] = j;  // index bits (a plain store: never touched by float arithmetic)
+  }
+  __syncthreads();
+  for (int c = wid; c < ncell; c += blockDim.x >> 6) {
+    const int s = c * SDF_CELL + lane;
+    const float* q = (const float*)&sv[(s >> 1) * 2] + (s & 1);
+    float lo[3], hi[3];
+    for (int e = 0; e < 3; ++e) {
+      lo[e] = s < nv ? q[2 * e] : INFINITY;
+      hi[e] = s < nv ? q[2 * e] : -INFINITY;
+      for (int off = 32; off > 0; off >>= 1) {
+        lo[e] = fminf(lo[e], __shfl_xor(lo[e], off));
+        hi[e] = fmaxf(hi[e], __shfl_xor(hi[e], off));
+      }
+    }
+    if (lane == 0) {
+      cbox[2 * c] = make_float4(lo[0], lo[1], lo[2], 0.f);
+      cbox[2 * c + 1] = make_float4(hi[0], hi[1], hi[2], 0.f);
+    }
+  }
+  __syncthreads();
+
   const int wpb = blockDim.x >> 6;
-  for (int ray = blockIdx.x * wpb + (threadIdx.x >> 6); ray < a.n_rays; ray += gridDim.x * wpb) {
+  for (int ray = blockIdx.x * wpb + wid; ray < a.n_rays; ray += gridDim.x * wpb) {
     float z, dist, pts[3], p[3];
     sample_point(a.ray_o, a.ray_d, a.near_, a.far_, a.t_rand, ray, lane, 64, z, dist, pts);
     world_to_pose(pts, a.R, a.Th, p);
     float b0 = INFINITY, b1 = INFINITY, b2 = INFINITY, b3 = INFINITY, b4 = INFINITY;
     int i0 = 0, i1 = 0, i2 = 0, i3 = 0, i4 = 0;
+    auto lt = [](float d, int j, float b, int i) { return d < b || (d == b && j < i); };
     auto insert = [&](float d, int j) {
-      if (d < b4) {
-        if (d < b3) {
+      if (lt(d, j, b4, i4)) {
+        if (lt(d, j, b3, i3)) {
           b4 = b3; i4 = i3;
-          if (d < b2) {
+          if (lt(d, j, b2, i2)) {
             b3 = b2; i3 = i2;
-            if (d < b1) {
+            if (lt(d, j, b1, i1)) {
               b2 = b1; i2 = i1;
-              if (d < b0) { b1 = b0; i1 = i0; b0 = d; i0 = j; }
+              if (lt(d, j, b0, i0)) { b1 = b0; i1 = i0; b0 = d; i0 = j; }
               else { b1 = d; i1 = j; }
             } else { b2 = d; i2 = j; }
           } else { b3 = d; i3 = j; }
         } else { b4 = d; i4 = j; }
       }
     };
+    // visiting order: cells by box distance from the ray's middle sample (keys carry the cell id in
+    // their low 7 bits; only the order changes, never the result)
+    const float pm[3] = {__shfl(p[0], 32), __shfl(p[1], 32), __shfl(p[2], 32)};
+    uint32_t ck[2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int c = lane + 64 * r;
+      ck[r] = 0xffffffffu;
+      if (c < ncell) {
+        const float d = box_d2(pm, cbox[2 * c], cbox[2 * c + 1]);
+        ck[r] = ((d == d ? __float_as_uint(d) : 0x7f800000u) & ~127u) | (uint32_t)c;
+      }
+    }
+#pragma unroll
+    for (int k = 2; k <= 128; k <<= 1)
+#pragma unroll
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        if (j == 64) {  // element l vs l + 64: both in this lane
+          const uint32_t x = ck[0], y = ck[1];
+          const bool up = (lane & k) == 0;  // k == 128: always ascending
+          ck[0] = up ? min(x, y) : max(x, y);
+          ck[1] = up ? max(x, y) : min(x, y);
+        } else {
+#pragma unroll
+          for (int r = 0; r < 2; ++r) {
+            const int i = lane + 64 * r;
+            const uint32_t o = __shfl_xor(ck[r], j);
+            const bool up = (i & k) == 0, low = (i & j) == 0;
+            ck[r] = (up == low) ? min(ck[r], o) : max(ck[r], o);
+          }
+        }
+      }
     // two vertices per step on packed fp32 (v_pk_add / v_pk_mul: per-element IEEE, no contraction,
-    // so each d^2 is the scalar formula's), inserted in index order; the vertex array is padded to
-    // an even count with a far-away vertex that never enters the 5-NN
+    // so each d^2 is the scalar formula's); padding vertices sit at infinity and never enter
     const pf2 P0 = {p[0], p[0]}, P1 = {p[1], p[1]}, P2 = {p[2], p[2]};
+    for (int t = 0; t < ncell; ++t) {
+      const uint32_t key = __builtin_amdgcn_readlane(t < 64 ? ck[0] : ck[1], t & 63);
+      const int c = (int)(key & 127u);
+      if (!__any(box_d2(p, cbox[2 * c], cbox[2 * c + 1]) <= b4)) continue;
+      const int j0 = c * SDF_CELL;
 #pragma unroll 2
-    for (int j = 0; j < a.nv; j += 2) {
-      const float4 va = sv[j], vb = sv[j + 1];
-      const pf2 dx = P0 - pf2{va.x, va.y}, dy = P1 - pf2{va.z, va.w}, dz = P2 - pf2{vb.x, vb.y};
-      const pf2 d = (dx * dx + dy * dy) + dz * dz;
-      if (fminf(d[0], d[1]) < b4) {  // one test per pair: most pairs insert nothing
-        insert(d[0], j);
-        insert(d[1], j + 1);
+      for (int j = j0; j < j0 + SDF_CELL; j += 2) {
+        const float4 va = sv[j], vb = sv[j + 1];
+        const pf2 dx = P0 - pf2{va.x, va.y}, dy = P1 - pf2{va.z, va.w}, dz = P2 - pf2{vb.x, vb.y};
+        const pf2 d = (dx * dx + dy * dy) + dz * dz;
+        if (fminf(d[0], d[1]) <= b4) {  // one test per pair: most pairs insert nothing
+          insert(d[0], (int)__float_as_uint(vb.z));
+          insert(d[1], (int)__float_as_uint(vb.w));
+        }
       }
     }
     // sample_blend_closest_points: dists = sqrt(d^2); disp = 1 / (dists + 1e-8); torch's 5-element
@@ -292,7 +426,7 @@ __global__ __launch_bounds__(256) void k_sdf_gtop(SdfPointArgs a) {
   const int k = (int)(e & 255);
   const float g = a.wimg[wn_layer(8).off + k];
   const float d = a.D7[e];
-  a.G7[e] = d >= 0.f ? g * d / (d + 1.f) : g;
+  a.G7[e] = a.d7_h ? g * softplus_factor_h(d) : d >= 0.f ? g * d / (d + 1.f) : g;
 }
 
 // gamma_6 backward: x.grad = g_x + sum_f f*(g_sin cos(f x)) + f*(g_cos * -sin(f x)). The two input

@@ -123,6 +123,7 @@ struct G {
   int x3;  // render precision ANR_BF16X3: split-bf16 MFMA GEMMs (k_lgemm; k_gemm_b<.., .., true> otherwise)
   LImgCache* limg;
   int cus;
+  int spd_h = 0;  // the spd operands of bwd / bwd_top hold softplus outputs h (GemmArgs::spd_h)
   int run(GemmArgs g) {
     if (M <= 0 || g.N <= 0) return ANR_OK;
     g.M = M;
@@ -147,7 +148,7 @@ struct G {
     g.M = M; g.N = K; g.nseg = 1; g.x3 = 1; g.ksplit = 1;
     g.seg[0] = GemmSeg{D7, 256, 1, W, in_ch, 1, Nout};
     g.C = dX; g.ldc = ldX;
-    g.spd = spd; g.ldsd = 256; g.spd_n = spd_n;
+    g.spd = spd; g.ldsd = 256; g.spd_n = spd_n; g.spd_h = spd_h;
     g.a_softplus_w = w8;
     if (!lgemm_supported(g)) return false;
     const void* img = limg->get(g, s);
@@ -169,6 +170,16 @@ struct G {
     g.div_post = div_post;
     return run(g);
   }
+  // Y[:, :256] = softplus(X W^T + bias), with its backward factors in deriv (or none: deriv NULL)
+  int fwd_sp(float* Y, const float* W, int in_ch, const float* bias, const float* X, long ldX, float* deriv) {
+    GemmArgs g{};
+    g.N = 256;
+    g.nseg = 1;
+    g.seg[0] = GemmSeg{X, ldX, 1, W, 1, in_ch, in_ch};
+    g.C = Y; g.ldc = 256; g.bias = bias;
+    g.softplus = 1; g.deriv = deriv; g.ldd = 256;
+    return run(g);
+  }
   // dX[:, :K] = softplus_bwd((dY W[:, :K]) / div_pre, spd) (pass-through at n >= spd_n)
   int bwd(float* dX, long ldX, int K, const float* dY, long ldY, int Nout, const float* W, int in_ch, const float* spd,
           int spd_n, float div_pre = 0.f) {
@@ -177,7 +188,7 @@ struct G {
     g.nseg = 1;
     g.seg[0] = GemmSeg{dY, ldY, 1, W, in_ch, 1, Nout};
     g.C = dX; g.ldc = ldX;
-    g.spd = spd; g.ldsd = 256; g.spd_n = spd_n;
+    g.spd = spd; g.ldsd = 256; g.spd_n = spd_n; g.spd_h = spd ? spd_h : 0;
     g.div_pre = div_pre;
     return run(g);
   }
@@ -329,18 +340,33 @@ int anr_sdf_render_fwd(const anr_sdf_params* p, const anr_sdf_frame* f, const fl
     hipLaunchKernelGGL(k_sdf_mid, pg, pb, 0, s, a);
     ANR_TRY(check_launch("k_sdf_mid"));
 
-    // B4 SDF network forward (softplus factors kept for the input gradient)
-    ANR_TRY(g.fwd(Ha, 256, 256, WN(0), 39, tp[0], a.Xs0, 40, 39, 0, false, Dl(0)));
-    ANR_TRY(g.fwd(Hb, 256, 256, WN(1), 256, tp[3], Ha, 256, 256, 0, false, Dl(1)));
-    ANR_TRY(g.fwd(Ha, 256, 256, WN(2), 256, tp[6], Hb, 256, 256, 0, false, Dl(2)));
-    ANR_TRY(g.fwd(a.X4, 256, 217, WN(3), 256, tp[9], Ha, 256, 256, 0, false, Dl(3), sqrt2));
-    ANR_TRY(g.fwd(Ha, 256, 256, WN(4), 256, tp[12], a.X4, 256, 256, 0, false, Dl(4)));
-    ANR_TRY(g.fwd(Hb, 256, 256, WN(5), 256, tp[15], Ha, 256, 256, 0, false, Dl(5)));
-    ANR_TRY(g.fwd(Ha, 256, 256, WN(6), 256, tp[18], Hb, 256, 256, 0, false, Dl(6)));
-    ANR_TRY(g.fwd(Hb, 256, 256, WN(7), 256, tp[21], Ha, 256, 256, 0, false, Dl(7)));
-    ANR_TRY(g.fwd(F(L.Y8), 264, 257, WN(8), 256, tp[24], Hb, 256, 256, 0, false));
+    // B4 SDF network forward. Split-bf16 precision: every softplus layer but lin3 writes its output h
+    // to its own D slot and nothing else; the next layer reads it there and the reverse pass recomputes
+    // the backward factor from it (softplus_factor_h) — one 0.54 GB write per layer fewer than storing
+    // exp(100 z) beside a ping-pong activation. lin3 (217 outputs, /sqrt2 and the gamma columns in X4)
+    // and the exact-fp32 precision keep the stored factors.
+    const bool sph = g.x3 != 0;
+    const float* hin = nullptr;
+    auto sp_fwd = [&](int l, int K, float* pingpong) -> int {
+      float* out = sph ? Dl(l) : pingpong;
+      const int r = g.fwd_sp(out, WN(l), K, tp[3 * l], l == 0 ? a.Xs0 : hin, l == 0 ? 40 : 256, sph ? nullptr : Dl(l));
+      hin = out;
+      return r;
+    };
+    ANR_TRY(sp_fwd(0, 39, Ha));
+    ANR_TRY(sp_fwd(1, 256, Hb));
+    ANR_TRY(sp_fwd(2, 256, Ha));
+    ANR_TRY(g.fwd(a.X4, 256, 217, WN(3), 256, tp[9], hin, 256, 256, 0, false, Dl(3), sqrt2));
+    hin = a.X4;
+    ANR_TRY(sp_fwd(4, 256, Ha));
+    ANR_TRY(sp_fwd(5, 256, Hb));
+    ANR_TRY(sp_fwd(6, 256, Ha));
+    ANR_TRY(sp_fwd(7, 256, Hb));
+    ANR_TRY(g.fwd(F(L.Y8), 264, 257, WN(8), 256, tp[24], hin, 256, 256, 0, false));
 
-    // B4 gradient of sdf w.r.t. the canonical point (reverse mode through the stored factors)
+    // B4 gradient of sdf w.r.t. the canonical point (reverse mode through the stored factors / outputs)
+    g.spd_h = sph ? 1 : 0;
+    a.d7_h = sph ? 1 : 0;
     if (g.bwd_top(Gb, 256, 256, Dl(7), WN(8), 256, WN(7), 256, Dl(6), 256)) {
       ANR_TRY(check_launch("k_lgemm (sdf, fused top)"));
     } else {
@@ -350,10 +376,13 @@ int anr_sdf_render_fwd(const anr_sdf_params* p, const anr_sdf_frame* f, const fl
     }
     ANR_TRY(g.bwd(Ga, 256, 256, Gb, 256, 256, WN(6), 256, Dl(5), 256));
     ANR_TRY(g.bwd(Gb, 256, 256, Ga, 256, 256, WN(5), 256, Dl(4), 256));
+    g.spd_h = 0;  // lin3's stored factors
     ANR_TRY(g.bwd(Gc, 256, 256, Gb, 256, 256, WN(4), 256, Dl(3), 217, sqrt2));
+    g.spd_h = sph ? 1 : 0;
     ANR_TRY(g.bwd(Ga, 256, 256, Gc, 256, 217, WN(3), 256, Dl(2), 256));
     ANR_TRY(g.bwd(Gb, 256, 256, Ga, 256, 256, WN(2), 256, Dl(1), 256));
     ANR_TRY(g.bwd(Ga, 256, 256, Gb, 256, 256, WN(1), 256, Dl(0), 256));
+    g.spd_h = 0;
     ANR_TRY(g.bwd(F(L.gB), 40, 39, Ga, 256, 256, WN(0), 39, nullptr, 0));
     hipLaunchKernelGGL(k_sdf_gamma_bwd, pg, pb, 0, s, a);
     ANR_TRY(check_launch("k_sdf_gamma_bwd"));

@@ -30,12 +30,13 @@ struct GemmArgs {
   int ksplit;          // number of K splits (grid.z)
   // sdf_pdf epilogues (anr_sdf*.hip); all off when zero / NULL
   float div_pre;       // v = v / div_pre before the activation (backward of cat(...)/sqrt(2))
-  int softplus;        // v = Softplus(beta=100)(v); deriv[m][n] = exp(100 v) or -1 above the threshold
+  int softplus;        // v = Softplus(beta=100)(v); deriv[m][n] = exp(100 v) or -1 above the threshold (deriv may be NULL)
   float* deriv;
   long ldd;
   const float* spd;    // softplus backward: v = d < 0 ? v : v * d / (d + 1), d = spd[m][n], n < spd_n
   long ldsd;
   int spd_n;
+  int spd_h;           // spd (and the ATR activations) hold softplus OUTPUTS h instead: factor = softplus_factor_h(h)
   float div_post;      // v = v / div_post after the activation (cat(...)/sqrt(2) forward)
   // activations are softplus factors d: A(m, k) = d >= 0 ? w[k] d / (d + 1) : w[k] (k_lgemm only)
   const float* a_softplus_w;

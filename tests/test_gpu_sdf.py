@@ -140,3 +140,52 @@ def test_full_frame_properties(renderer, dev):
     occ = bt['occupancy'][0]
     assert r1['msk_sdf'].shape[1] >= int((occ == 0).sum())
     assert int((r1['msk_label'] == 0).sum()) == int((occ == 0).sum())
+
+
+def _knn_records(renderer, R):
+    """The front-end's per-sample KNN records (8 uint32: w0..w4 bits, i0|i1<<16, i2|i3<<16, i4) read
+    from the workspace at the offset anr_sdf_capi.hip slayout() gives them."""
+    a256 = lambda x: (x + 255) // 256 * 256
+    N = R * 64
+    nch = (R + 2047) // 2048
+    o = 0
+    for nbytes in (16, R * 8, nch * 8, (R + 1) * 4, ((R + 255) // 256) * 4, N * 4):
+        o = a256(o + nbytes)
+    rec = renderer._ws[o:o + N * 32].view(torch.int32).view(N, 8).cpu().numpy().view(np.uint32)
+    idx = np.stack([rec[:, 5] & 0xffff, rec[:, 5] >> 16, rec[:, 6] & 0xffff, rec[:, 6] >> 16, rec[:, 7]], 1)
+    return rec[:, :5].view(np.float32), idx.astype(np.int64)
+
+
+def test_knn_ties_resolved_by_vertex_index(renderer, dev):
+    """B1 ties: 600 vertices duplicated onto lower-index ones (equal d^2 for every sample). The
+    pruned, Morton-ordered scan must still return pytorch3d's K smallest (d^2, index) pairs: a
+    selected vertex's lower-index duplicate is selected too and comes first; indices are distinct."""
+    sc = pdf_scene()
+    ro, rd = sc.box_rays(256, seed=41)
+    b, _ = pdf_batch_np(sc, ro, rd)
+    V = b['pvertices'].shape[1]
+    rng = np.random.Generator(np.random.PCG64(9))
+    src = rng.choice(V // 2, 600, replace=False)
+    dst = V // 2 + rng.choice(V - V // 2, 600, replace=False)
+    b['pvertices'] = b['pvertices'].copy()
+    b['pvertices'][0, dst] = b['pvertices'][0, src]
+    bt = to_torch(b, dev)
+    renderer.render_device(bt)
+    R = b['ray_o'].shape[1]
+    w, idx = _knn_records(renderer, R)
+    assert np.all(idx < V)
+    assert np.all(np.sort(idx, 1)[:, 1:] != np.sort(idx, 1)[:, :-1])
+    partner = np.full(V, -1)
+    partner[dst] = src
+    sel = np.zeros((idx.shape[0], V), bool)
+    np.put_along_axis(sel, idx, True, 1)
+    hit = partner[idx] >= 0  # a selected high-index duplicate ...
+    rows = np.nonzero(hit)[0]
+    assert rows.size > 100
+    assert np.all(sel[rows, partner[idx][hit]])  # ... has its lower-index twin selected
+    # lexicographic order within the record: weights non-increasing; twins (equal d^2) by ascending index
+    assert np.all(w[:, :-1] >= w[:, 1:])
+    pv = b['pvertices'][0]
+    twin = np.all(pv[idx[:, :-1]] == pv[idx[:, 1:]], -1)
+    assert twin.sum() > 100
+    assert np.all(idx[:, :-1][twin] < idx[:, 1:][twin])
