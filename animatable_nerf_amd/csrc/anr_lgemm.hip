@@ -62,6 +62,13 @@ struct LGemm {
   int spd_h;         // spd / ATR activations are softplus outputs h (factor softplus_factor_h) instead of exp factors
   float div_pre, div_post;
   const float* atr;  // ATR: the activations are softplus factors d, used as (d >= 0 ? atr[k] d / (d + 1) : atr[k])
+  // HEAD: a following 256 -> head_n (<= 4) layer fused into the epilogue: the activation C is not stored;
+  // each workgroup adds its column group's partial head_w . h (plus head_b for group 0) into head_out
+  const float* head_w;
+  const float* head_b;
+  float* head_out;
+  long ldh;
+  int head_n;
 };
 
 struct LPack {
@@ -127,9 +134,10 @@ __device__ __forceinline__ float lg_log1p(float e) {
 // epilogue of one 16-sample tile: lane holds C[16 t + (lane & 15)][n0 + 16 ob + 4 (lane >> 4) + r].
 // Bias comes from LDS, the softplus-backward factors were loaded before the tile's MFMAs (sp); the
 // epilogue issues no global loads, so the next tile's activation loads stay in flight across it.
-template <int NOB, bool SPD>
+template <int NOB, bool SPD, bool HEAD>
 __device__ __forceinline__ void lg_epilogue(const LGemm& g, const f32x4 (&acc)[NOB], const f32x4* sp,
-                                            const f32x4* bv, int tile, int n0, int lane) {
+                                            const float* bias_lds, int tile, int n0, int lane, const float* head_lds) {
+  float hp[4] = {0.f, 0.f, 0.f, 0.f};  // HEAD partials of this lane's columns
   // rows past M were computed from row M - 1's activations (the loads clamp), so their results are
   // row M - 1's: storing them there is a same-value duplicate and the stores need no row predicate
   const int m = min(tile * 16 + (lane & 15), g.M - 1);
@@ -138,9 +146,10 @@ __device__ __forceinline__ void lg_epilogue(const LGemm& g, const f32x4 (&acc)[N
     const int nl = 16 * ob + 4 * (lane >> 4);
     const int n = n0 + nl;
     f32x4 v = acc[ob], dv;
+    const f32x4 bo = SPD ? f32x4{0.f, 0.f, 0.f, 0.f} : *(const f32x4*)(bias_lds + nl);
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      float x = v[e] + bv[ob][e];
+      float x = v[e] + bo[e];
       if (g.div_pre != 0.f) x = x / g.div_pre;
       if (g.relu) x = fmaxf(x, 0.f);
       if (g.softplus) {  // torch softplus(beta=100, threshold=20) and the factor its backward uses
@@ -160,6 +169,13 @@ __device__ __forceinline__ void lg_epilogue(const LGemm& g, const f32x4 (&acc)[N
       if (g.div_post != 0.f) x = x / g.div_post;
       v[e] = x;
     }
+    if constexpr (HEAD) {
+#pragma unroll
+      for (int o = 0; o < 4; ++o)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) hp[o] = fmaf(head_lds[o * 256 + n + e], v[e], hp[o]);
+      continue;
+    }
     float* c = g.C + (long)m * g.ldc + n;
     float* d = g.deriv + (long)m * g.ldd + n;
     if (n0 + 16 * ob + 16 <= g.N) {  // uniform: the whole 16-column block is inside N
@@ -173,6 +189,19 @@ __device__ __forceinline__ void lg_epilogue(const LGemm& g, const f32x4 (&acc)[N
           if (g.softplus && g.deriv) d[e] = dv[e];
         }
     }
+  }
+  if constexpr (HEAD) {  // lane groups (lane >> 4) hold disjoint columns of the same sample: sum them
+    const int row = tile * 16 + (lane & 15);
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+      hp[o] += __shfl_xor(hp[o], 16);
+      hp[o] += __shfl_xor(hp[o], 32);
+    }
+    // two column groups add into a zeroed output: (0 + a) + b == (0 + b) + a, so the result is
+    // order-independent (lgemm_supported admits HEAD only at G == 2)
+    if (lane < 16 && row < g.M)
+      for (int o = 0; o < g.head_n; ++o)
+        atomicAdd(g.head_out + (long)row * g.ldh + o, hp[o] + (n0 == 0 ? g.head_b[o] : 0.f));
   }
 }
 
@@ -221,15 +250,12 @@ __device__ __forceinline__ void lg_load_spd(const LGemm& g, f32x4 (&sp)[NOB], in
 // split hi/lo and their registers immediately refilled with the same k-step of the wave's next tile
 // (so one tile of loads is always in flight, in one tile's worth of registers), then the MFMAs;
 // the epilogue last. The loop is straight-line, so the compiler's vmcnt waits stay exact.
-template <int NOB, int KST, int KST0, bool SPD, bool UNAL, bool ATR>
+template <int NOB, int KST, int KST0, bool SPD, bool UNAL, bool ATR, bool HEAD>
 __device__ __forceinline__ void lg_tile(const LGemm& g, f32x4 (&buf)[KST][2], int tile, int next, int n0, int lane,
                                         const unsigned char* lds, const float* atr_lds) {
-  // the tile's bias columns (from the image, L1-resident) and factors load first: both are used in this
-  // tile's epilogue, and issuing them ahead of the refills keeps every wait in the loop graded
-  // (the softplus-backward GEMMs have no bias: with SPD the bias registers are not needed)
-  f32x4 bv[NOB], sp[NOB];
-#pragma unroll
-  for (int ob = 0; ob < NOB; ++ob) bv[ob] = SPD ? f32x4{0.f, 0.f, 0.f, 0.f} : g.bimg[n0 / 4 + 4 * ob + (lane >> 4)];
+  // the tile's softplus-backward factors load first: used in this tile's epilogue, and issuing them
+  // ahead of the refills keeps every wait in the loop graded (the bias columns sit in LDS)
+  f32x4 sp[NOB];
   lg_load_spd<NOB, SPD>(g, sp, tile, n0, lane);
   const int kg = lane >> 4;
   f32x4 acc[NOB];
@@ -275,10 +301,10 @@ __device__ __forceinline__ void lg_tile(const LGemm& g, f32x4 (&buf)[KST][2], in
       acc[ob] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, xh, acc[ob], 0, 0, 0);
     }
   }
-  lg_epilogue<NOB, SPD>(g, acc, sp, bv, tile, n0, lane);
+  lg_epilogue<NOB, SPD, HEAD>(g, acc, sp, atr_lds + 32 * KST + 1024, tile, n0, lane, atr_lds + 32 * KST);
 }
 
-template <int NOB, int KST, int KST0, bool SPD, bool UNAL, bool ATR>
+template <int NOB, int KST, int KST0, bool SPD, bool UNAL, bool ATR, bool HEAD>
 __global__ __launch_bounds__(LG_WAVES * 64) void k_lgemm(LGemm g) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   // workgroup -> (column group, rank): the workgroups of one rank sit on one XCD (blockIdx % 8), so
@@ -304,6 +330,18 @@ __global__ __launch_bounds__(LG_WAVES * 64) void k_lgemm(LGemm g) {
     if constexpr (ATR) {
       if (threadIdx.x < 32 * KST) atr_lds[threadIdx.x] = threadIdx.x < g.seg[0].K ? g.atr[threadIdx.x] : 0.0f;
     }
+    {  // this column group's bias (from the image's bias columns, zeros without one)
+      float* bl = atr_lds + 32 * KST + 1024;
+      const float* bsrc = (const float*)g.bimg + n0;
+      if (threadIdx.x < 16 * NOB) bl[threadIdx.x] = bsrc[threadIdx.x];
+    }
+    if constexpr (HEAD) {  // head rows 0..3 x the 256 columns (zero past head_n / N)
+      float* hl = atr_lds + 32 * KST;
+      for (int i = threadIdx.x; i < 4 * 256; i += LG_WAVES * 64) {
+        const int o = i >> 8, n = i & 255;
+        hl[i] = (o < g.head_n && n < g.N) ? g.head_w[(long)o * g.N + n] : 0.0f;
+      }
+    }
   }
   __syncthreads();
   // wave-uniform cursors live in SGPRs: the loop below has no divergent control flow
@@ -315,11 +353,11 @@ __global__ __launch_bounds__(LG_WAVES * 64) void k_lgemm(LGemm g) {
   f32x4 buf[KST][2];
 #pragma unroll
   for (int ks = 0; ks < KST; ++ks) lg_load_ks<KST0, UNAL>(g, buf[ks], t, ks, lane);
-  for (; t < T; t += nw) lg_tile<NOB, KST, KST0, SPD, UNAL, ATR>(g, buf, t, t + nw, n0, lane, lds, atr_lds);
+  for (; t < T; t += nw) lg_tile<NOB, KST, KST0, SPD, UNAL, ATR, HEAD>(g, buf, t, t + nw, n0, lane, lds, atr_lds);
 }
 
-// weight image, ATR column weights (32 kst floats)
-size_t lg_lds_bytes(int kst, int nob) { return (size_t)kst * nob * 2 * LG_FRAG + (size_t)kst * 128; }
+// weight image, ATR column weights (32 kst floats), HEAD weights (4 x 256 floats), bias (128 floats)
+size_t lg_lds_bytes(int kst, int nob) { return (size_t)kst * nob * 2 * LG_FRAG + (size_t)kst * 128 + 4096 + 512; }
 
 // output columns per workgroup (16 x NOB) and column groups G for N outputs at kst k-steps
 int lg_nob(int N, int kst, int* G) {
@@ -341,38 +379,39 @@ int lg_kst(const GemmArgs& g, int* kst0) {
   return *kst0 + (g.nseg > 1 ? (g.seg[1].K + 31) / 32 : 0);
 }
 
-template <int NOB, int KST, int KST0, bool SPD, bool UNAL, bool ATR>
+template <int NOB, int KST, int KST0, bool SPD, bool UNAL, bool ATR, bool HEAD>
 void lg_launch(const LGemm& a, int cus, hipStream_t s) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)k_lgemm<NOB, KST, KST0, SPD, UNAL, ATR>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              LG_MAX_LDS);
+    (void)hipFuncSetAttribute((const void*)k_lgemm<NOB, KST, KST0, SPD, UNAL, ATR, HEAD>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, LG_MAX_LDS);
     attr = true;
   }
   LGemm g = a;
   g.bpg = std::max(1, cus / (8 * g.G)) * 8;
-  hipLaunchKernelGGL((k_lgemm<NOB, KST, KST0, SPD, UNAL, ATR>), dim3((unsigned)(g.bpg * g.G)), dim3(LG_WAVES * 64),
+  hipLaunchKernelGGL((k_lgemm<NOB, KST, KST0, SPD, UNAL, ATR, HEAD>), dim3((unsigned)(g.bpg * g.G)), dim3(LG_WAVES * 64),
                      lg_lds_bytes(KST, NOB), s, g);
 }
 
 // the instantiated shapes (the sdf_pdf layers); false for any other
 bool lg_dispatch(const LGemm& a, int nob, bool spd, bool unal, int cus, hipStream_t s, bool launch) {
-  const bool atr = a.atr != nullptr;
-#define LG_CASE(N_, K_, K0_, S_, U_, T_)                                                    \
-  if (nob == N_ && a.kst == K_ && a.kst0 == K0_ && spd == S_ && unal == U_ && atr == T_) {  \
-    if (launch) lg_launch<N_, K_, K0_, S_, U_, T_>(a, cus, s);                              \
-    return true;                                                                            \
+  const bool atr = a.atr != nullptr, head = a.head_out != nullptr;
+#define LG_CASE(N_, K_, K0_, S_, U_, T_, H_)                                                                 \
+  if (nob == N_ && a.kst == K_ && a.kst0 == K0_ && spd == S_ && unal == U_ && atr == T_ && head == H_) {  \
+    if (launch) lg_launch<N_, K_, K0_, S_, U_, T_, H_>(a, cus, s);                                         \
+    return true;                                                                                           \
   }
-  LG_CASE(8, 8, 8, false, false, false)
-  LG_CASE(8, 8, 8, true, false, false)
-  LG_CASE(8, 8, 8, true, false, true)
-  LG_CASE(8, 7, 7, true, false, false)
-  LG_CASE(8, 2, 2, false, false, false)
-  LG_CASE(6, 10, 2, false, false, false)
-  LG_CASE(6, 10, 2, false, true, false)
-  LG_CASE(6, 8, 8, false, false, false)
-  LG_CASE(4, 8, 8, false, false, false)
-  LG_CASE(1, 8, 8, false, false, false)
+  LG_CASE(8, 8, 8, false, false, false, true)
+  LG_CASE(8, 8, 8, false, false, false, false)
+  LG_CASE(8, 8, 8, true, false, false, false)
+  LG_CASE(8, 8, 8, true, false, true, false)
+  LG_CASE(8, 7, 7, true, false, false, false)
+  LG_CASE(8, 2, 2, false, false, false, false)
+  LG_CASE(6, 10, 2, false, false, false, false)
+  LG_CASE(6, 10, 2, false, true, false, false)
+  LG_CASE(6, 8, 8, false, false, false, false)
+  LG_CASE(4, 8, 8, false, false, false, false)
+  LG_CASE(1, 8, 8, false, false, false, false)
 #undef LG_CASE
   return false;
 }
@@ -396,6 +435,7 @@ LGemm lg_args(const GemmArgs& g, int* nob) {
   a.C = g.C; a.ldc = g.ldc; a.bias = g.bias; a.relu = g.relu; a.softplus = g.softplus; a.deriv = g.deriv;
   a.ldd = g.ldd; a.spd = g.spd; a.ldsd = g.ldsd; a.spd_n = g.spd_n; a.spd_h = g.spd_h; a.div_pre = g.div_pre; a.div_post = g.div_post;
   a.atr = g.a_softplus_w;
+  a.head_w = g.head_w; a.head_b = g.head_b; a.head_out = g.head_out; a.ldh = g.ldh; a.head_n = g.head_n;
   return a;
 }
 
@@ -420,6 +460,9 @@ bool lgemm_supported(const GemmArgs& g) {
   if (g.spd && (!al16(g.spd) || g.ldsd % 4 != 0 || g.bias)) return false;
   int nob = 0;
   const LGemm a = lg_args(g, &nob);
+  if (g.head_out && (a.G != 2 || g.N != 256 || g.head_n < 1 || g.head_n > 4 || !g.head_w || !g.head_b ||
+                     g.softplus || g.spd || g.a_softplus_w))
+    return false;
   return lg_dispatch(a, nob, g.spd != nullptr, lg_unal(g), 0, nullptr, false);
 }
 

@@ -170,6 +170,25 @@ struct G {
     g.div_post = div_post;
     return run(g);
   }
+  // split-bf16 only: Yh = Wh relu(X W^T + bias) + bh with the 256-wide hidden activation never stored
+  // (k_lgemm HEAD epilogue, two column groups adding into a zeroed Yh); false: nothing launched, the
+  // caller runs the two GEMMs
+  bool fwd_head(float* Yh, long ldh, int nh, const float* Wh, const float* bh, const float* W, int in_ch,
+                const float* bias, const float* X, long ldX, int K) {
+    if (!x3 || !limg || M <= 0) return false;
+    GemmArgs g{};
+    g.M = M; g.N = 256; g.nseg = 1; g.x3 = 1; g.ksplit = 1;
+    g.seg[0] = GemmSeg{X, ldX, 1, W, 1, in_ch, K};
+    g.C = Yh; g.ldc = 4;  // not written (HEAD); kept valid for the support checks
+    g.bias = bias; g.relu = 1;
+    g.head_w = Wh; g.head_b = bh; g.head_out = Yh; g.ldh = ldh; g.head_n = nh;
+    if (!lgemm_supported(g)) return false;
+    const void* img = limg->get(g, s);
+    if (!img) return false;
+    if (hipMemsetAsync(Yh, 0, (size_t)M * ldh * sizeof(float), s) != hipSuccess) return false;
+    (void)lgemm_run(g, img, cus, s);
+    return true;
+  }
   // Y[:, :256] = softplus(X W^T + bias), with its backward factors in deriv (or none: deriv NULL)
   int fwd_sp(float* Y, const float* W, int in_ch, const float* bias, const float* X, long ldX, float* deriv) {
     GemmArgs g{};
@@ -335,8 +354,12 @@ int anr_sdf_render_fwd(const anr_sdf_params* p, const anr_sdf_frame* f, const fl
     ANR_TRY(g.fwd(Ha, 256, 256, Wr[4], 256, tp[SDF_RLIN0 + 9], Hb, 256, 256, 0, true));
     ANR_TRY(g.fwd(Hb, 256, 256, Wr[5], 391, fold + 256, a.Gr, 64, 63, 0, true, nullptr, 0.f, Ha, 256, 256, 135));
     ANR_TRY(g.fwd(Ha, 256, 256, Wr[6], 256, tp[SDF_RLIN0 + 13], Hb, 256, 256, 0, true));
-    ANR_TRY(g.fwd(Hb, 256, 256, Wr[7], 256, tp[SDF_RLIN0 + 15], Ha, 256, 256, 0, true));
-    ANR_TRY(g.fwd(F(L.Yr), 4, 3, tp[SDF_RFC_W], 256, tp[SDF_RFC_B], Hb, 256, 256, 0, false));
+    if (g.fwd_head(F(L.Yr), 4, 3, tp[SDF_RFC_W], tp[SDF_RFC_B], Wr[7], 256, tp[SDF_RLIN0 + 15], Ha, 256, 256)) {
+      ANR_TRY(check_launch("k_lgemm (sdf, resd_linears.7 + resd_fc)"));
+    } else {
+      ANR_TRY(g.fwd(Hb, 256, 256, Wr[7], 256, tp[SDF_RLIN0 + 15], Ha, 256, 256, 0, true));
+      ANR_TRY(g.fwd(F(L.Yr), 4, 3, tp[SDF_RFC_W], 256, tp[SDF_RFC_B], Hb, 256, 256, 0, false));
+    }
     hipLaunchKernelGGL(k_sdf_mid, pg, pb, 0, s, a);
     ANR_TRY(check_launch("k_sdf_mid"));
 
@@ -391,8 +414,12 @@ int anr_sdf_render_fwd(const anr_sdf_params* p, const anr_sdf_frame* f, const fl
     ANR_TRY(g.fwd(Ha, 256, 256, WN(9), 289, tp[29], a.C0, 40, 33, 0, true, nullptr, 0.f, F(L.Y8) + 1, 264, 256, 33));
     ANR_TRY(g.fwd(Hb, 256, 256, WN(10), 256, tp[32], Ha, 256, 256, 0, true));
     ANR_TRY(g.fwd(Ha, 256, 256, WN(11), 256, tp[35], Hb, 256, 256, 0, true));
-    ANR_TRY(g.fwd(Hb, 256, 256, WN(12), 384, fold + 512, Ha, 256, 256, 0, true));
-    ANR_TRY(g.fwd(F(L.Yc), 4, 3, WN(13), 256, tp[41], Hb, 256, 256, 0, false));
+    if (g.fwd_head(F(L.Yc), 4, 3, WN(13), tp[41], WN(12), 384, fold + 512, Ha, 256, 256)) {
+      ANR_TRY(check_launch("k_lgemm (sdf, colour lin3 + lin4)"));
+    } else {
+      ANR_TRY(g.fwd(Hb, 256, 256, WN(12), 384, fold + 512, Ha, 256, 256, 0, true));
+      ANR_TRY(g.fwd(F(L.Yc), 4, 3, WN(13), 256, tp[41], Hb, 256, 256, 0, false));
+    }
 
     // B5 density, raw assembly with the (widened) tbounds mask
     hipLaunchKernelGGL(k_sdf_raw, pg, pb, 0, s, a);

@@ -40,6 +40,13 @@ struct GemmArgs {
   float div_post;      // v = v / div_post after the activation (cat(...)/sqrt(2) forward)
   // activations are softplus factors d: A(m, k) = d >= 0 ? w[k] d / (d + 1) : w[k] (k_lgemm only)
   const float* a_softplus_w;
+  // k_lgemm only: a following small layer (head_n <= 4 outputs of head_w (head_n, N) + head_b) fused into
+  // the epilogue; C is then not written and head_out (ld ldh, zeroed by the caller) receives the result
+  const float* head_w;
+  const float* head_b;
+  float* head_out;
+  long ldh;
+  int head_n;
   int bf16;            // operands rounded to bf16, bf16 MFMA, fp32 accumulate (training precision)
   int x3;              // operands split hi + lo (bf16 each), three bf16 MFMAs per product (fp32-level)
   // weight-gradient GEMMs (A(m,k) = dY[k][m]): the fp32 row sums of A over this launch's k range
