@@ -153,7 +153,7 @@ __device__ __forceinline__ void epilogue(const GemmArgs& g, const f32x4 (&acc)[2
         }
         if (g.spd && n < g.spd_n) {
           const float d = g.spd[(long)m * g.ldsd + n];
-          if (g.spd_h) v = v * softplus_factor_h(d);
+          if (g.spd_h) v = v * softplus_factor_h(g.spd_scale != 0.f ? d * g.spd_scale : d);
           else if (d >= 0.f) v = v * d / (d + 1.f);
         }
         if (g.mask && !(g.mask[(long)m * g.ldm + n] > 0.f)) v = 0.f;
@@ -211,7 +211,7 @@ __device__ __forceinline__ void epilogue_sw(const GemmArgs& g, const f32x4 (&acc
           }
           if (g.spd && n + e < g.spd_n) {
             const float d = sp[i][j][e];
-            if (g.spd_h) x = x * softplus_factor_h(d);
+            if (g.spd_h) x = x * softplus_factor_h(g.spd_scale != 0.f ? d * g.spd_scale : d);
             else if (d >= 0.f) x = x * d / (d + 1.f);
           }
           if (g.mask && !(mk[i][j][e] > 0.f)) x = 0.f;
@@ -246,7 +246,7 @@ __device__ __forceinline__ void epilogue_sw(const GemmArgs& g, const f32x4 (&acc
         }
         if (g.spd && n < g.spd_n) {
           const float d = g.spd[(long)m * g.ldsd + n];
-          if (g.spd_h) v = v * softplus_factor_h(d);
+          if (g.spd_h) v = v * softplus_factor_h(g.spd_scale != 0.f ? d * g.spd_scale : d);
           else if (d >= 0.f) v = v * d / (d + 1.f);
         }
         if (g.mask && !(g.mask[(long)m * g.ldm + n] > 0.f)) v = 0.f;

@@ -60,6 +60,7 @@ struct LGemm {
   long ldsd;
   int spd_n;
   int spd_h;         // spd / ATR activations are softplus outputs h (factor softplus_factor_h) instead of exp factors
+  float spd_scale;   // spd_h: stored values are h / spd_scale (0: 1)
   float div_pre, div_post;
   const float* atr;  // ATR: the activations are softplus factors d, used as (d >= 0 ? atr[k] d / (d + 1) : atr[k])
   // HEAD: a following 256 -> head_n (<= 4) layer fused into the epilogue: the activation C is not stored;
@@ -161,7 +162,7 @@ __device__ __forceinline__ void lg_epilogue(const LGemm& g, const f32x4 (&acc)[N
       if constexpr (SPD) {
         const float d = sp[ob][e];
         if (g.spd_h) {
-          if (n + e < g.spd_n) x = x * softplus_factor_h(d);
+          if (n + e < g.spd_n) x = x * softplus_factor_h(g.spd_scale != 0.f ? d * g.spd_scale : d);
         } else if (n + e < g.spd_n && d >= 0.f) {
           x = x * d * __builtin_amdgcn_rcpf(d + 1.f);
         }
@@ -433,7 +434,7 @@ LGemm lg_args(const GemmArgs& g, int* nob) {
   a.N = g.N;
   *nob = lg_nob(g.N, a.kst, &a.G);
   a.C = g.C; a.ldc = g.ldc; a.bias = g.bias; a.relu = g.relu; a.softplus = g.softplus; a.deriv = g.deriv;
-  a.ldd = g.ldd; a.spd = g.spd; a.ldsd = g.ldsd; a.spd_n = g.spd_n; a.spd_h = g.spd_h; a.div_pre = g.div_pre; a.div_post = g.div_post;
+  a.ldd = g.ldd; a.spd = g.spd; a.ldsd = g.ldsd; a.spd_n = g.spd_n; a.spd_h = g.spd_h; a.spd_scale = g.spd_scale; a.div_pre = g.div_pre; a.div_post = g.div_post;
   a.atr = g.a_softplus_w;
   a.head_w = g.head_w; a.head_b = g.head_b; a.head_out = g.head_out; a.ldh = g.ldh; a.head_n = g.head_n;
   return a;

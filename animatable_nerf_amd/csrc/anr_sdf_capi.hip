@@ -124,6 +124,7 @@ struct G {
   LImgCache* limg;
   int cus;
   int spd_h = 0;  // the spd operands of bwd / bwd_top hold softplus outputs h (GemmArgs::spd_h)
+  float spd_scale = 0.f;  // ... stored as h / spd_scale (GemmArgs::spd_scale)
   int run(GemmArgs g) {
     if (M <= 0 || g.N <= 0) return ANR_OK;
     g.M = M;
@@ -157,16 +158,17 @@ struct G {
     return true;
   }
   // Y = epi([X0 | X1] [W[:, c0:c0+K0] | W[:, c1:c1+K1]]^T + bias)
+  // (sp_out_only: softplus with no factor written — deriv only selects the softplus epilogue)
   int fwd(float* Y, long ldY, int N, const float* W, int in_ch, const float* bias, const float* X0, long ld0, int K0,
-          int c0, bool relu, float* deriv = nullptr, float div_post = 0.f, const float* X1 = nullptr, long ld1 = 0,
-          int K1 = 0, int c1 = 0) {
+          int c0, bool relu, float* deriv = nullptr, float div_post = 0.f, bool sp_out_only = false,
+          const float* X1 = nullptr, long ld1 = 0, int K1 = 0, int c1 = 0) {
     GemmArgs g{};
     g.N = N;
     g.nseg = X1 ? 2 : 1;
     g.seg[0] = GemmSeg{X0, ld0, 1, W + c0, 1, in_ch, K0};
     if (X1) g.seg[1] = GemmSeg{X1, ld1, 1, W + c1, 1, in_ch, K1};
     g.C = Y; g.ldc = ldY; g.bias = bias; g.relu = relu ? 1 : 0;
-    if (deriv) { g.softplus = 1; g.deriv = deriv; g.ldd = 256; }
+    if (deriv) { g.softplus = 1; g.deriv = sp_out_only ? nullptr : deriv; g.ldd = 256; }
     g.div_post = div_post;
     return run(g);
   }
@@ -207,7 +209,7 @@ struct G {
     g.nseg = 1;
     g.seg[0] = GemmSeg{dY, ldY, 1, W, in_ch, 1, Nout};
     g.C = dX; g.ldc = ldX;
-    g.spd = spd; g.ldsd = 256; g.spd_n = spd_n; g.spd_h = spd ? spd_h : 0;
+    g.spd = spd; g.ldsd = 256; g.spd_n = spd_n; g.spd_h = spd ? spd_h : 0; g.spd_scale = spd_scale;
     g.div_pre = div_pre;
     return run(g);
   }
@@ -352,7 +354,7 @@ int anr_sdf_render_fwd(const anr_sdf_params* p, const anr_sdf_frame* f, const fl
     ANR_TRY(g.fwd(Ha, 256, 256, Wr[2], 256, tp[SDF_RLIN0 + 5], Hb, 256, 256, 0, true));
     ANR_TRY(g.fwd(Hb, 256, 256, Wr[3], 256, tp[SDF_RLIN0 + 7], Ha, 256, 256, 0, true));
     ANR_TRY(g.fwd(Ha, 256, 256, Wr[4], 256, tp[SDF_RLIN0 + 9], Hb, 256, 256, 0, true));
-    ANR_TRY(g.fwd(Hb, 256, 256, Wr[5], 391, fold + 256, a.Gr, 64, 63, 0, true, nullptr, 0.f, Ha, 256, 256, 135));
+    ANR_TRY(g.fwd(Hb, 256, 256, Wr[5], 391, fold + 256, a.Gr, 64, 63, 0, true, nullptr, 0.f, false, Ha, 256, 256, 135));
     ANR_TRY(g.fwd(Ha, 256, 256, Wr[6], 256, tp[SDF_RLIN0 + 13], Hb, 256, 256, 0, true));
     if (g.fwd_head(F(L.Yr), 4, 3, tp[SDF_RFC_W], tp[SDF_RFC_B], Wr[7], 256, tp[SDF_RLIN0 + 15], Ha, 256, 256)) {
       ANR_TRY(check_launch("k_lgemm (sdf, resd_linears.7 + resd_fc)"));
@@ -379,7 +381,7 @@ int anr_sdf_render_fwd(const anr_sdf_params* p, const anr_sdf_frame* f, const fl
     ANR_TRY(sp_fwd(0, 39, Ha));
     ANR_TRY(sp_fwd(1, 256, Hb));
     ANR_TRY(sp_fwd(2, 256, Ha));
-    ANR_TRY(g.fwd(a.X4, 256, 217, WN(3), 256, tp[9], hin, 256, 256, 0, false, Dl(3), sqrt2));
+    ANR_TRY(g.fwd(a.X4, 256, 217, WN(3), 256, tp[9], hin, 256, 256, 0, false, Dl(3), sqrt2, sph));
     hin = a.X4;
     ANR_TRY(sp_fwd(4, 256, Ha));
     ANR_TRY(sp_fwd(5, 256, Hb));
@@ -399,9 +401,13 @@ int anr_sdf_render_fwd(const anr_sdf_params* p, const anr_sdf_frame* f, const fl
     }
     ANR_TRY(g.bwd(Ga, 256, 256, Gb, 256, 256, WN(6), 256, Dl(5), 256));
     ANR_TRY(g.bwd(Gb, 256, 256, Ga, 256, 256, WN(5), 256, Dl(4), 256));
-    g.spd_h = 0;  // lin3's stored factors
-    ANR_TRY(g.bwd(Gc, 256, 256, Gb, 256, 256, WN(4), 256, Dl(3), 217, sqrt2));
-    g.spd_h = sph ? 1 : 0;
+    if (sph) {  // lin3's outputs h3 / sqrt2 in X4
+      g.spd_scale = sqrt2;
+      ANR_TRY(g.bwd(Gc, 256, 256, Gb, 256, 256, WN(4), 256, a.X4, 217, sqrt2));
+      g.spd_scale = 0.f;
+    } else {
+      ANR_TRY(g.bwd(Gc, 256, 256, Gb, 256, 256, WN(4), 256, Dl(3), 217, sqrt2));
+    }
     ANR_TRY(g.bwd(Ga, 256, 256, Gc, 256, 217, WN(3), 256, Dl(2), 256));
     ANR_TRY(g.bwd(Gb, 256, 256, Ga, 256, 256, WN(2), 256, Dl(1), 256));
     ANR_TRY(g.bwd(Ga, 256, 256, Gb, 256, 256, WN(1), 256, Dl(0), 256));
@@ -411,7 +417,7 @@ int anr_sdf_render_fwd(const anr_sdf_params* p, const anr_sdf_frame* f, const fl
     ANR_TRY(check_launch("k_sdf_gamma_bwd"));
 
     // B6 colour network (color_latent folded into lin3)
-    ANR_TRY(g.fwd(Ha, 256, 256, WN(9), 289, tp[29], a.C0, 40, 33, 0, true, nullptr, 0.f, F(L.Y8) + 1, 264, 256, 33));
+    ANR_TRY(g.fwd(Ha, 256, 256, WN(9), 289, tp[29], a.C0, 40, 33, 0, true, nullptr, 0.f, false, F(L.Y8) + 1, 264, 256, 33));
     ANR_TRY(g.fwd(Hb, 256, 256, WN(10), 256, tp[32], Ha, 256, 256, 0, true));
     ANR_TRY(g.fwd(Ha, 256, 256, WN(11), 256, tp[35], Hb, 256, 256, 0, true));
     if (g.fwd_head(F(L.Yc), 4, 3, WN(13), tp[41], WN(12), 384, fold + 512, Ha, 256, 256)) {

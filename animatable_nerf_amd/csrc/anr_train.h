@@ -37,6 +37,7 @@ struct GemmArgs {
   long ldsd;
   int spd_n;
   int spd_h;           // spd (and the ATR activations) hold softplus OUTPUTS h instead: factor = softplus_factor_h(h)
+  float spd_scale;     // spd_h: the stored values are h / spd_scale (0: 1), e.g. lin3's cat(...)/sqrt(2) output
   float div_post;      // v = v / div_post after the activation (cat(...)/sqrt(2) forward)
   // activations are softplus factors d: A(m, k) = d >= 0 ? w[k] d / (d + 1) : w[k] (k_lgemm only)
   const float* a_softplus_w;
