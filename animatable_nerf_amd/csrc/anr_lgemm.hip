@@ -212,7 +212,7 @@ __device__ __forceinline__ void lg_epilogue(const LGemm& g, const f32x4 (&acc)[N
 // the activation fragments of k-step ks of a 16-sample tile: lane -> sample 16 t + (lane & 15), k =
 // 32 ks' + lg_kcol(lane >> 4, 0..7) of the segment holding ks (rows past M read row M - 1, 4-groups
 // wholly past K read column 0; both masked later)
-template <int KST0, bool UNAL>
+template <int KST0, bool UNAL, bool FULLK = false>
 __device__ __forceinline__ void lg_load_ks(const LGemm& g, f32x4 (&buf)[2], int tile, int ks, int lane) {
   const int m = min(tile * 16 + (lane & 15), g.M - 1);
   const int j = lane >> 4;
@@ -224,7 +224,7 @@ __device__ __forceinline__ void lg_load_ks(const LGemm& g, f32x4 (&buf)[2], int 
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     int kc = k0 + lg_kcol(j, 4 * h);
-    kc = kc < K ? kc : 0;
+    if constexpr (!FULLK) kc = kc < K ? kc : 0;
     const float* p = A + (long)m * lda + kc;
     if constexpr (UNAL) {  // a segment that is not 16-B addressable: 4-B loads
 #pragma unroll
@@ -251,7 +251,7 @@ __device__ __forceinline__ void lg_load_spd(const LGemm& g, f32x4 (&sp)[NOB], in
 // split hi/lo and their registers immediately refilled with the same k-step of the wave's next tile
 // (so one tile of loads is always in flight, in one tile's worth of registers), then the MFMAs;
 // the epilogue last. The loop is straight-line, so the compiler's vmcnt waits stay exact.
-template <int NOB, int KST, int KST0, bool SPD, bool UNAL, bool ATR, bool HEAD>
+template <int NOB, int KST, int KST0, bool SPD, bool UNAL, bool ATR, bool HEAD, bool FULLK>
 __device__ __forceinline__ void lg_tile(const LGemm& g, f32x4 (&buf)[KST][2], int tile, int next, int n0, int lane,
                                         const unsigned char* lds, const float* atr_lds) {
   // the tile's softplus-backward factors load first: used in this tile's epilogue, and issuing them
@@ -281,7 +281,8 @@ __device__ __forceinline__ void lg_tile(const LGemm& g, f32x4 (&buf)[KST][2], in
       }
     }
 #pragma unroll
-    for (int e = 0; e < 8; ++e) x[e] = (k0 + lg_kcol(kg, e) < K) ? x[e] : 0.0f;
+    for (int e = 0; e < 8; ++e)
+      if constexpr (!FULLK) x[e] = (k0 + lg_kcol(kg, e) < K) ? x[e] : 0.0f;
     lbf16x8 xh, xl;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -290,7 +291,7 @@ __device__ __forceinline__ void lg_tile(const LGemm& g, f32x4 (&buf)[KST][2], in
     }
     // refill with the next tile's k-step ks once the split has consumed the registers (so the loads
     // land in the same registers and the loop carries no copies that would wait on them)
-    lg_load_ks<KST0, UNAL>(g, buf[ks], next, ks, lane);
+    lg_load_ks<KST0, UNAL, FULLK>(g, buf[ks], next, ks, lane);
     __builtin_amdgcn_sched_barrier(0);  // keep the refill here (issue order = ring order)
     const unsigned char* fr = lds + ks * NOB * 2 * LG_FRAG + frag_off;
 #pragma unroll
@@ -305,7 +306,9 @@ __device__ __forceinline__ void lg_tile(const LGemm& g, f32x4 (&buf)[KST][2], in
   lg_epilogue<NOB, SPD, HEAD>(g, acc, sp, atr_lds + 32 * KST + 1024, tile, n0, lane, atr_lds + 32 * KST);
 }
 
-template <int NOB, int KST, int KST0, bool SPD, bool UNAL, bool ATR, bool HEAD>
+// FULLK: every segment is a whole number of 32-deep k-steps (the 256-wide layers), so the loop has no
+// per-element K masks and no column clamps (chosen per launch on the host: one loop per kernel)
+template <int NOB, int KST, int KST0, bool SPD, bool UNAL, bool ATR, bool HEAD, bool FULLK>
 __global__ __launch_bounds__(LG_WAVES * 64) void k_lgemm(LGemm g) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   // workgroup -> (column group, rank): the workgroups of one rank sit on one XCD (blockIdx % 8), so
@@ -354,7 +357,7 @@ __global__ __launch_bounds__(LG_WAVES * 64) void k_lgemm(LGemm g) {
   f32x4 buf[KST][2];
 #pragma unroll
   for (int ks = 0; ks < KST; ++ks) lg_load_ks<KST0, UNAL>(g, buf[ks], t, ks, lane);
-  for (; t < T; t += nw) lg_tile<NOB, KST, KST0, SPD, UNAL, ATR, HEAD>(g, buf, t, t + nw, n0, lane, lds, atr_lds);
+  for (; t < T; t += nw) lg_tile<NOB, KST, KST0, SPD, UNAL, ATR, HEAD, FULLK>(g, buf, t, t + nw, n0, lane, lds, atr_lds);
 }
 
 // weight image, ATR column weights (32 kst floats), HEAD weights (4 x 256 floats), bias (128 floats)
@@ -380,39 +383,41 @@ int lg_kst(const GemmArgs& g, int* kst0) {
   return *kst0 + (g.nseg > 1 ? (g.seg[1].K + 31) / 32 : 0);
 }
 
-template <int NOB, int KST, int KST0, bool SPD, bool UNAL, bool ATR, bool HEAD>
+template <int NOB, int KST, int KST0, bool SPD, bool UNAL, bool ATR, bool HEAD, bool FULLK>
 void lg_launch(const LGemm& a, int cus, hipStream_t s) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)k_lgemm<NOB, KST, KST0, SPD, UNAL, ATR, HEAD>,
+    (void)hipFuncSetAttribute((const void*)k_lgemm<NOB, KST, KST0, SPD, UNAL, ATR, HEAD, FULLK>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, LG_MAX_LDS);
     attr = true;
   }
   LGemm g = a;
   g.bpg = std::max(1, cus / (8 * g.G)) * 8;
-  hipLaunchKernelGGL((k_lgemm<NOB, KST, KST0, SPD, UNAL, ATR, HEAD>), dim3((unsigned)(g.bpg * g.G)), dim3(LG_WAVES * 64),
+  hipLaunchKernelGGL((k_lgemm<NOB, KST, KST0, SPD, UNAL, ATR, HEAD, FULLK>), dim3((unsigned)(g.bpg * g.G)), dim3(LG_WAVES * 64),
                      lg_lds_bytes(KST, NOB), s, g);
 }
 
 // the instantiated shapes (the sdf_pdf layers); false for any other
 bool lg_dispatch(const LGemm& a, int nob, bool spd, bool unal, int cus, hipStream_t s, bool launch) {
   const bool atr = a.atr != nullptr, head = a.head_out != nullptr;
-#define LG_CASE(N_, K_, K0_, S_, U_, T_, H_)                                                                 \
-  if (nob == N_ && a.kst == K_ && a.kst0 == K0_ && spd == S_ && unal == U_ && atr == T_ && head == H_) {  \
-    if (launch) lg_launch<N_, K_, K0_, S_, U_, T_, H_>(a, cus, s);                                         \
-    return true;                                                                                           \
+  const bool fullk = a.seg[0].K == 32 * a.kst0 && (a.kst == a.kst0 || a.seg[1].K == 32 * (a.kst - a.kst0));
+#define LG_CASE(N_, K_, K0_, S_, U_, T_, H_, F_)                                                        \
+  if (nob == N_ && a.kst == K_ && a.kst0 == K0_ && spd == S_ && unal == U_ && atr == T_ && head == H_ && \
+      fullk == F_) {                                                                                    \
+    if (launch) lg_launch<N_, K_, K0_, S_, U_, T_, H_, F_>(a, cus, s);                                  \
+    return true;                                                                                        \
   }
-  LG_CASE(8, 8, 8, false, false, false, true)
-  LG_CASE(8, 8, 8, false, false, false, false)
-  LG_CASE(8, 8, 8, true, false, false, false)
-  LG_CASE(8, 8, 8, true, false, true, false)
-  LG_CASE(8, 7, 7, true, false, false, false)
-  LG_CASE(8, 2, 2, false, false, false, false)
-  LG_CASE(6, 10, 2, false, false, false, false)
-  LG_CASE(6, 10, 2, false, true, false, false)
-  LG_CASE(6, 8, 8, false, false, false, false)
-  LG_CASE(4, 8, 8, false, false, false, false)
-  LG_CASE(1, 8, 8, false, false, false, false)
+  LG_CASE(8, 8, 8, false, false, false, true, true)
+  LG_CASE(8, 8, 8, false, false, false, false, true)
+  LG_CASE(8, 8, 8, true, false, false, false, true)
+  LG_CASE(8, 8, 8, true, false, true, false, true)
+  LG_CASE(8, 7, 7, true, false, false, false, false)
+  LG_CASE(8, 2, 2, false, false, false, false, false)
+  LG_CASE(6, 10, 2, false, false, false, false, false)
+  LG_CASE(6, 10, 2, false, true, false, false, false)
+  LG_CASE(6, 8, 8, false, false, false, false, true)
+  LG_CASE(4, 8, 8, false, false, false, false, true)
+  LG_CASE(1, 8, 8, false, false, false, false, true)
 #undef LG_CASE
   return false;
 }
