@@ -26,6 +26,9 @@ EXPORTS = ('anr_near_far', 'anr_params_packed_bytes', 'anr_params_pack', 'anr_re
            'anr_alpha_workspace_bytes', 'anr_alpha_points', 'anr_alpha_counts', 'anr_mc_workspace_bytes',
            'anr_mc_count', 'anr_mc_emit', 'anr_anim_workspace_bytes', 'anr_anim_step',
            'anr_train_ray_workspace_bytes', 'anr_train_ray_lists', 'anr_train_ray_gather',
+           'anr_network_workspace_bytes', 'anr_network_fwd', 'anr_network_counts', 'anr_network_bw_rows',
+           'anr_network_train_workspace_bytes', 'anr_network_train_fwd', 'anr_network_train_bwd',
+           'anr_points_workspace_bytes', 'anr_blend_weights', 'anr_canonical_alpha', 'anr_train_step_hooked',
            'anr_last_error', 'anr_version')
 
 c_float_p = ctypes.c_void_p
@@ -57,6 +60,15 @@ FP32, BF16, BF16_ALL, BF16X3 = 0, 1, 2, 3  # anr_render_opts.precision
 class RenderOut(ctypes.Structure):
     _fields_ = [('rgb_map', ctypes.c_void_p), ('acc_map', ctypes.c_void_p), ('depth_map', ctypes.c_void_p),
                 ('raw', ctypes.c_void_p)]
+
+
+class Samples(ctypes.Structure):
+    _fields_ = [('wpts', ctypes.c_void_p), ('viewdir', ctypes.c_void_p), ('dists', ctypes.c_void_p),
+                ('n_pts', ctypes.c_int)]
+
+
+class TrainHooks(ctypes.Structure):
+    _fields_ = [('nerf_grads_ready', ctypes.c_void_p)]
 
 
 class AlphaOpts(ctypes.Structure):
@@ -112,6 +124,9 @@ def load():
     lib.anr_train_step.argtypes = [ctypes.POINTER(Params), ctypes.c_void_p * NUM_TENSORS, ctypes.POINTER(Frame), P, P, P,
                                    P, ctypes.c_int, ctypes.POINTER(RenderOpts), P, P, ctypes.POINTER(RenderOut), P, P,
                                    ctypes.c_size_t, P]
+    lib.anr_train_step_hooked.argtypes = [ctypes.POINTER(Params), ctypes.c_void_p * NUM_TENSORS, ctypes.POINTER(Frame), P,
+                                          P, P, P, ctypes.c_int, ctypes.POINTER(RenderOpts), P, P,
+                                          ctypes.POINTER(RenderOut), P, ctypes.POINTER(TrainHooks), P, ctypes.c_size_t, P]
     lib.anr_adam.argtypes = [P, P, P, P, ctypes.c_long, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float,
                              ctypes.c_float, ctypes.c_int, ctypes.c_float, P]
     lib.anr_sdf_render_workspace_bytes.restype = ctypes.c_size_t
@@ -148,6 +163,20 @@ def load():
     lib.anr_anim_workspace_bytes.argtypes = [ctypes.c_int]
     lib.anr_anim_step.argtypes = [ctypes.POINTER(Params), ctypes.c_void_p * NUM_NOVEL_TENSORS, ctypes.POINTER(Frame), P,
                                   ctypes.c_int, P, ctypes.c_int, ctypes.POINTER(RenderOpts), P, P, ctypes.c_size_t, P]
+    S, PP, PF, PO = ctypes.POINTER(Samples), ctypes.POINTER(Params), ctypes.POINTER(Frame), ctypes.POINTER(RenderOpts)
+    for name in ('anr_network_workspace_bytes', 'anr_network_train_workspace_bytes'):
+        getattr(lib, name).restype = ctypes.c_size_t
+        getattr(lib, name).argtypes = [ctypes.c_int, PO, PF]
+    lib.anr_network_fwd.argtypes = [PP, PF, S, PO, P, P, ctypes.c_size_t, P]
+    lib.anr_network_train_fwd.argtypes = [PP, PF, S, PO, P, P, ctypes.c_size_t, P]
+    lib.anr_network_train_bwd.argtypes = [PP, ctypes.c_void_p * NUM_TENSORS, PF, S, PO, P, P, P, P, ctypes.c_size_t, P]
+    lib.anr_network_counts.restype = P
+    lib.anr_network_counts.argtypes = [P, ctypes.c_int]
+    lib.anr_network_bw_rows.argtypes = [P, ctypes.c_int, P, P, P]
+    lib.anr_points_workspace_bytes.restype = ctypes.c_size_t
+    lib.anr_points_workspace_bytes.argtypes = [ctypes.c_int]
+    lib.anr_blend_weights.argtypes = [PP, ctypes.c_int, P, P, ctypes.c_int, P, ctypes.c_int, P, P, ctypes.c_size_t, P]
+    lib.anr_canonical_alpha.argtypes = [PP, P, ctypes.c_int, P, P, ctypes.c_size_t, P]
     lib.anr_profile_enable.argtypes = [ctypes.c_int]
     lib.anr_profile_read.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]
     lib.anr_last_error.restype = ctypes.c_char_p

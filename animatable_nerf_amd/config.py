@@ -111,4 +111,55 @@ def load_cfg(cfg_file=None, opts=(), base_dir=None):
     return cfg
 
 
+class LayeredCfg:
+    """Live view of the reference's global ``lib.config.cfg`` (yacs) over this package's defaults:
+    a key the reference sets (its yaml, CLI pairs, run.py:50's ``cfg.perturb = 0`` made after the
+    plugins were built) wins; a key only this backend defines (``render_precision``, ``chunk`` ...)
+    comes from the defaults. Attribute reads and ``get`` are resolved on every access."""
+
+    def __init__(self, ref, base):
+        object.__setattr__(self, '_ref', ref)
+        object.__setattr__(self, '_base', base)
+
+    def __getattr__(self, name):
+        ref = object.__getattribute__(self, '_ref')
+        if name in ref:
+            return ref[name]
+        base = object.__getattribute__(self, '_base')
+        if name in base:
+            return base[name]
+        raise AttributeError(name)
+
+    def __setattr__(self, name, value):
+        self._ref[name] = value
+
+    def __contains__(self, name):
+        return name in self._ref or name in self._base
+
+    def __getitem__(self, name):
+        try:
+            return self.__getattr__(name)
+        except AttributeError as e:
+            raise KeyError(name) from e
+
+    def get(self, name, default=None):
+        try:
+            return self.__getattr__(name)
+        except AttributeError:
+            return default
+
+
+def active():
+    """The configuration a plugin built without an explicit cfg reads: the reference's global
+    ``lib.config.cfg`` when the reference's config module is loaded (its factories call
+    ``Network()``, ``Renderer(net)``, ``NetworkWrapper(net)`` with no cfg: make_network.py:5-9,
+    make_renderer.py:5-9, make_trainer.py:5-14), else this package's ``cfg``."""
+    import sys
+    mod = sys.modules.get('lib.config')
+    ref = getattr(mod, 'cfg', None) if mod is not None else None
+    if ref is None:
+        return cfg
+    return LayeredCfg(ref, cfg)
+
+
 cfg = defaults()

@@ -61,7 +61,7 @@ namespace anr {
 // A2-A6 + per-frame prep: memsets, volumes/folds, front-end, ordered compaction (counts[0] = n')
 int stage_frontend(const anr_params* p, const anr_frame* f, const float* ray_o, const float* ray_d, const float* near_,
                    const float* far_, int R, const anr_render_opts* o, char* ws, const Layout& L, float4* raw,
-                   hipStream_t s) {
+                   hipStream_t s, const anr_samples* x) {
   const long np = (long)f->pbw_dims[0] * f->pbw_dims[1] * f->pbw_dims[2];
   const long nt = (long)f->tbw_dims[0] * f->tbw_dims[1] * f->tbw_dims[2];
   const int nch = (R + o->chunk - 1) / o->chunk;
@@ -112,8 +112,17 @@ int stage_frontend(const anr_params* p, const anr_frame* f, const float* ray_o, 
   fa.img_h = f->img_h; fa.img_w = f->img_w;
   if (f->n_views < 0 || (f->n_views > 0 && (!f->Ks || !f->RT || !f->msks || f->img_h <= 0 || f->img_w <= 0)))
     return fail(ANR_E_ARG, "render: bad visibility-filter views");
-  hipLaunchKernelGGL(k_frontend, dim3((R + 15) / 16), dim3(1024), 0, s, fa);
-  ANR_TRY(check_launch("k_frontend"));
+  if (x) {  // free samples: world->pose with the matmul path of an n_pts-point call, argmin over the call
+    if (f->n_views) return fail(ANR_E_ARG, "network forward: the visibility filter is a renderer option");
+    fa.wpts = x->wpts;
+    fa.n_pts = x->n_pts;
+    fa.chunk_pts = x->n_pts;
+    hipLaunchKernelGGL(k_frontend_pts, dim3((R + 3) / 4), dim3(256), 0, s, fa);
+    ANR_TRY(check_launch("k_frontend_pts"));
+  } else {
+    hipLaunchKernelGGL(k_frontend, dim3((R + 15) / 16), dim3(1024), 0, s, fa);
+    ANR_TRY(check_launch("k_frontend"));
+  }
 
   CompactArgs ca{};
   ca.n_rays = R; ca.chunk = o->chunk;
@@ -133,9 +142,13 @@ int stage_frontend(const anr_params* p, const anr_frame* f, const float* ray_o, 
 // the fused network kernel (render path)
 int stage_mlp(const anr_params* p, const anr_frame* f, const float* ray_o, const float* ray_d, const float* near_,
               const float* far_, int R, const anr_render_opts* o, char* ws, const Layout& L, float4* raw,
-              hipStream_t s) {
+              hipStream_t s, const anr_samples* x) {
   const long N = (long)R * 64;
   MlpArgs ma{};
+  if (x) {
+    ma.wpts = x->wpts; ma.vdir = x->viewdir; ma.dists = x->dists;
+    ma.n_pts = x->n_pts; ma.chunk_pts = x->n_pts;
+  }
   ma.wimg = (const unsigned char*)p->packed;
   ma.bias = (const float*)((const unsigned char*)p->packed + weights_bytes());
   ma.fold = (const float*)(ws + L.fold);
@@ -394,6 +407,67 @@ int anr_render_fwd(const anr_params* p, const anr_frame* f, const float* ray_o, 
   ANR_TRY(stage_mlp(p, f, ray_o, ray_d, near_, far_, n_rays, o, ws, L, raw, s));
   ANR_TRY(stage_alpha_ind(n_rays, o, ws, L, s));
   return stage_composite(near_, far_, n_rays, o, raw, out, nullptr, s);
+}
+
+// ---- Network.forward over free samples (include/aninerf.h) --------------------------------
+static int check_network_args(const anr_params* p, const anr_frame* f, const anr_samples* x, const anr_render_opts* o,
+                              const void* ws, const char* who) {
+  const std::string w(who);
+  if (!p || !f || !x || !o || !ws) return fail(ANR_E_ARG, w + ": NULL argument");
+  if (!x->wpts || !x->viewdir || !x->dists) return fail(ANR_E_ARG, w + ": NULL sample tensor");
+  if (x->n_pts <= 0 || (long)x->n_pts > 0x7fffffffL / 24 - 64) return fail(ANR_E_ARG, w + ": bad n_pts");
+  for (int i = 0; i < 3; ++i)
+    if (f->pbw_dims[i] <= 0 || f->tbw_dims[i] <= 0) return fail(ANR_E_ARG, w + ": bad volume dims");
+  if (!f->A || !f->R || !f->Th || !f->pbw || !f->tbw || !f->pbounds || !f->tbounds || !f->latent_index)
+    return fail(ANR_E_ARG, w + ": NULL frame tensor");
+  if (f->n_views) return fail(ANR_E_ARG, w + ": the visibility filter is a renderer option (n_views must be 0)");
+  for (int i = 0; i < ANR_NUM_TENSORS; ++i)
+    if (!p->t[i]) return fail(ANR_E_ARG, w + ": NULL parameter tensor");
+  return ANR_OK;
+}
+
+size_t anr_network_workspace_bytes(int n_pts, const anr_render_opts* o, const anr_frame* f) {
+  if (!o || !f || n_pts <= 0) return 0;
+  const int G = (n_pts + 63) / 64;
+  const long np = (long)f->pbw_dims[0] * f->pbw_dims[1] * f->pbw_dims[2];
+  const long nt = (long)f->tbw_dims[0] * f->tbw_dims[1] * f->tbw_dims[2];
+  return layout(G, G, np, nt, true).total;
+}
+
+const int32_t* anr_network_counts(const void* workspace, int n_pts) {
+  return anr_render_counts(workspace, (n_pts + 63) / 64);
+}
+
+int anr_network_bw_rows(const void* workspace, int n_pts, float* pbw, float* tbw, void* stream) {
+  return anr_render_bw_rows(workspace, (n_pts + 63) / 64, pbw, tbw, stream);
+}
+
+int anr_network_fwd(const anr_params* p, const anr_frame* f, const anr_samples* x, const anr_render_opts* o, float* raw,
+                    void* workspace, size_t ws_bytes, void* stream) {
+  ANR_TRY(check_network_args(p, f, x, o, workspace, "anr_network_fwd"));
+  if (!raw || !p->packed) return fail(ANR_E_ARG, "anr_network_fwd: NULL raw / weights not packed");
+  if (o->novel_pose) {
+    for (int i = 0; i < ANR_NUM_NOVEL_TENSORS; ++i)
+      if (!p->novel[i]) return fail(ANR_E_ARG, "anr_network_fwd: novel_pose needs the novel_pose_bw tensors");
+    if (!f->bw_latent_index) return fail(ANR_E_ARG, "anr_network_fwd: novel_pose needs bw_latent_index");
+  }
+  const int G = (x->n_pts + 63) / 64;
+  anr_render_opts oo = *o;
+  oo.chunk = G;  // one call = one reference chunk
+  oo.t_rand = nullptr;
+  const long np = (long)f->pbw_dims[0] * f->pbw_dims[1] * f->pbw_dims[2];
+  const long nt = (long)f->tbw_dims[0] * f->tbw_dims[1] * f->tbw_dims[2];
+  const Layout L = layout(G, G, np, nt, true);
+  if (ws_bytes < L.total) return fail(ANR_E_WORKSPACE, "anr_network_fwd: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  char* ws = (char*)workspace;
+  float4* wraw = (float4*)(ws + L.raw);
+  ANR_TRY(stage_frontend(p, f, nullptr, nullptr, nullptr, nullptr, G, &oo, ws, L, wraw, s, x));
+  ANR_TRY(stage_mlp(p, f, nullptr, nullptr, nullptr, nullptr, G, &oo, ws, L, wraw, s, x));
+  ANR_TRY(stage_alpha_ind(G, &oo, ws, L, s));
+  if (hipMemcpyAsync(raw, wraw, (size_t)x->n_pts * 16, hipMemcpyDeviceToDevice, s) != hipSuccess)
+    return fail(ANR_E_HIP, "anr_network_fwd: raw copy failed");
+  return ANR_OK;
 }
 
 int anr_profile_enable(int on) {

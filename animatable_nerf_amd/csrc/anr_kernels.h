@@ -24,6 +24,7 @@ struct FrontArgs {
   long n_pts;
   int chunk_pts;
   const float* pn24;     // channel 24 of pbw as a compact (X,Y,Z) array (k_prep), or NULL: read pbw
+  // (k_frontend_pts also zeroes raw at the dropped points when raw != NULL: Network.forward's raw_full)
 };
 
 struct CompactArgs {
@@ -105,6 +106,10 @@ struct MlpArgs {
   long n_pts;
   int chunk_pts;
   float* alpha_out;
+  // free samples (anr_network_fwd, Network.forward): when dists != NULL the render program reads
+  // sample id's world point wpts[id], view direction vdir[id] and dists[id] instead of a ray sample
+  const float* vdir;
+  const float* dists;
 };
 
 struct PrepArgs {

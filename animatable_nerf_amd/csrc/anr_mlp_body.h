@@ -969,11 +969,20 @@ __device__ __forceinline__ void mlp_body(const MlpArgs& a) {
     const int idx = tile * 128 + wave * 16 + pl;
     const bool valid = idx < n;
     const int pid = a.list[valid ? idx : n - 1];
-    const int ray = pid >> 6, s = pid & 63;
-    float z, dist, pts[3], pose[3];
-    sample_point(a.ray_o, a.ray_d, a.near_, a.far_, a.t_rand, ray, s, 64, z, dist, pts);
-    world_to_pose(pts, a.R, a.Th, pose);
-    const float dir[3] = {a.ray_d[3 * ray], a.ray_d[3 * ray + 1], a.ray_d[3 * ray + 2]};
+    float dist, pose[3], dir[3];
+    if (a.dists) {  // free samples (Network.forward): the caller's world point, view direction, dist
+      world_to_pose_pt(a.wpts, pid, a.n_pts, a.chunk_pts, a.R, a.Th, pose);
+      dist = a.dists[pid];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) dir[c] = a.vdir[3 * (size_t)pid + c];
+    } else {
+      const int ray = pid >> 6, s = pid & 63;
+      float z, pts[3];
+      sample_point(a.ray_o, a.ray_d, a.near_, a.far_, a.t_rand, ray, s, 64, z, dist, pts);
+      world_to_pose(pts, a.R, a.Th, pose);
+#pragma unroll
+      for (int c = 0; c < 3; ++c) dir[c] = a.ray_d[3 * ray + c];
+    }
 
     float emb[16], vemb[8];
     f32x4 A[17], B[17], fc[2], init[2], bw[2];

@@ -357,6 +357,7 @@ __global__ __launch_bounds__(256) void k_frontend_pts(FrontArgs a) {
   const bool keep = valid && pn < a.norm_th;
   const uint64_t m = __ballot(keep);
   if (lane == 0) a.mask[grp] = m;
+  if (a.raw != nullptr && !keep) a.raw[i] = make_float4(0.f, 0.f, 0.f, 0.f);
   const int rc = grp % a.chunk;
   uint64_t key = valid ? (((uint64_t)__float_as_uint(pn) << 32) | (uint32_t)(rc * 64 + lane)) : ~0ull;
 #pragma unroll

@@ -180,9 +180,25 @@ struct TrainBufs {
   const float* d_tbw;
   const float *rgb_map, *acc_map;
   int n_rays;
+  // free samples (anr_network_train_fwd, Network.forward under autograd): sample id -> wpts[id],
+  // vdir[id], dists[id] (n_pts of them, one reference call) instead of a ray sample; NULL: rays
+  const float *wpts, *vdir, *dists;
+  long n_pts;
 };
 
 __global__ void k_tr_point_prep(TrainBufs b);
+// free-point helpers (anr_blend_weights / anr_canonical_alpha): gamma(x) rows [n][64] and the initial
+// blend weights (24,n) -> rows [n][32]; softmax(log(init + 1e-9) + logits) -> (24,n); the latent row
+// of one blend-weight field folded into the biases of its layers 0 and 5
+__global__ void k_pt_prep(const float* pts, const float* smpl_bw, int n, float* G, float* I);
+__global__ void k_pt_softmax_out(const float* logits, const float* I, int n, float* bw_out);
+struct FoldArgs {
+  const float *w0, *b0, *w5, *b5, *table;
+  const int64_t* row;
+  int add;
+  float* fold;  // [2][256]
+};
+__global__ void k_fold_latent(FoldArgs a);
 __global__ void k_tr_softmax_lbs(TrainBufs b);
 __global__ void k_tr_softmax_t(TrainBufs b);
 __global__ void k_tr_raw(TrainBufs b);

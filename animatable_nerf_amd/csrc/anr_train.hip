@@ -24,10 +24,18 @@ __global__ __launch_bounds__(256) void k_tr_point_prep(TrainBufs b) {
   const int n = *b.n_kept;
   if (i >= n) return;
   const int pid = b.list[i];
-  const int ray = pid >> 6, s = pid & 63;
-  float z, dist, pts[3], pose[3];
-  sample_point(b.ray_o, b.ray_d, b.near_, b.far_, b.t_rand, ray, s, 64, z, dist, pts);
-  world_to_pose(pts, b.R, b.Th, pose);
+  float dist, pose[3], dir[3];
+  if (b.dists) {  // free samples (Network.forward)
+    world_to_pose_pt(b.wpts, pid, b.n_pts, (int)b.n_pts, b.R, b.Th, pose);
+    dist = b.dists[pid];
+    for (int c = 0; c < 3; ++c) dir[c] = b.vdir[3 * (long)pid + c];
+  } else {
+    const int ray = pid >> 6, s = pid & 63;
+    float z, pts[3];
+    sample_point(b.ray_o, b.ray_d, b.near_, b.far_, b.t_rand, ray, s, 64, z, dist, pts);
+    world_to_pose(pts, b.R, b.Th, pose);
+    for (int c = 0; c < 3; ++c) dir[c] = b.ray_d[3 * ray + c];
+  }
   b.Gp[(long)i * 64 + lane] = lane < 63 ? embed_feature(pose, lane, 10) : 0.f;
   if (lane < 32) {
     float lo[3], hi[3];
@@ -35,7 +43,6 @@ __global__ __launch_bounds__(256) void k_tr_point_prep(TrainBufs b) {
     TriCell cell;
     tri_cell(pose, lo, hi, b.pX, b.pY, b.pZ, cell);
     b.Ip[(long)i * 32 + lane] = lane < 24 ? tri_channel(b.pbw, 25, lane, cell) : 0.f;
-    const float dir[3] = {b.ray_d[3 * ray], b.ray_d[3 * ray + 1], b.ray_d[3 * ray + 2]};
     b.Gv[(long)i * 32 + lane] = lane < 27 ? embed_feature(dir, lane, 4) : 0.f;
   }
   if (lane == 0) {
@@ -96,6 +103,42 @@ __global__ __launch_bounds__(256) void k_tr_softmax_lbs(TrainBufs b) {
   TriCell cell;
   tri_cell(tp, lo, hi, b.tX, b.tY, b.tZ, cell);
   for (int j = 0; j < 32; ++j) b.It[(long)i * 32 + j] = j < 24 ? tri_channel(b.tbw, 25, j, cell) : 0.f;
+}
+
+// free points (Network.calculate_neural_blend_weights / TPoseHuman.calculate_alpha): one wave per
+// point, lane f -> gamma(x)_f (embedder.py:5-54), init row f < 24 from the reference's (24, n) layout
+__global__ __launch_bounds__(256) void k_pt_prep(const float* __restrict__ pts, const float* __restrict__ smpl_bw, int n,
+                                                 float* G, float* I) {
+  const int lane = threadIdx.x & 63;
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= n) return;
+  const float x[3] = {pts[3 * (long)i], pts[3 * (long)i + 1], pts[3 * (long)i + 2]};
+  G[(long)i * 64 + lane] = lane < 63 ? embed_feature(x, lane, 10) : 0.f;
+  if (I && lane < 32) I[(long)i * 32 + lane] = lane < 24 ? smpl_bw[(long)lane * n + i] : 0.f;
+}
+
+__global__ __launch_bounds__(256) void k_pt_softmax_out(const float* __restrict__ logits, const float* __restrict__ I,
+                                                        int n, float* bw_out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float bw[24];
+  softmax24(logits + (long)i * 32, I + (long)i * 32, bw);
+  for (int j = 0; j < 24; ++j) bw_out[(long)j * n + i] = bw[j];
+}
+
+// the latent columns of layers 0 (191 inputs) and 5 (447) times table[row (+ add)], plus the bias:
+// the per-call constant part of get_bw_feature's [gamma(x), latent] input (tpose_nerf_network.py:40-53)
+__global__ __launch_bounds__(256) void k_fold_latent(FoldArgs a) {
+  const int row = (int)a.row[0] + a.add;
+  const float* lat = a.table + (size_t)row * 128;
+  for (int k = threadIdx.x; k < 512; k += blockDim.x) {
+    const int which = k >> 8, nn = k & 255;
+    const float* W = which ? a.w5 : a.w0;
+    const int ld = which ? 447 : 191;
+    float acc = (which ? a.b5 : a.b0)[nn];
+    for (int q = 0; q < 128; ++q) acc = fmaf(W[(size_t)nn * ld + 63 + q], lat[q], acc);
+    a.fold[k] = acc;
+  }
 }
 
 __global__ __launch_bounds__(256) void k_tr_softmax_t(TrainBufs b) {

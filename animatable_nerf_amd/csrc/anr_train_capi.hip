@@ -208,8 +208,12 @@ int read_count(const int* dev, int* host, hipStream_t s) {
 }
 
 TrainBufs bufs(const TLayout& T, char* ws, const anr_frame* f, const float* ray_o, const float* ray_d,
-               const float* near_, const float* far_, int R, const anr_render_opts* o) {
+               const float* near_, const float* far_, int R, const anr_render_opts* o,
+               const anr_samples* x = nullptr) {
   TrainBufs b{};
+  if (x) {
+    b.wpts = x->wpts; b.vdir = x->viewdir; b.dists = x->dists; b.n_pts = x->n_pts;
+  }
   const Layout& L = T.L;
   b.list = (const int*)(ws + L.list);
   b.n_kept = (const int*)(ws + L.counts);
@@ -297,15 +301,16 @@ int bw_backward(Exec& e, const float* const* W, float* const* g, const float* G,
   return ANR_OK;
 }
 
+// x != NULL: free samples (Network.forward, anr_network_train_fwd): R groups of 64, no compositing
 int train_forward(const anr_params* p, const anr_frame* f, const float* ray_o, const float* ray_d, const float* near_,
                   const float* far_, int R, const anr_render_opts* o, const anr_render_out* out, char* ws,
-                  const TLayout& T, hipStream_t s, Exec& e) {
+                  const TLayout& T, hipStream_t s, Exec& e, const anr_samples* x = nullptr) {
   float4* raw = (float4*)(ws + T.L.raw);
-  ANR_TRY(stage_frontend(p, f, ray_o, ray_d, near_, far_, R, o, ws, T.L, raw, s));
+  ANR_TRY(stage_frontend(p, f, ray_o, ray_d, near_, far_, R, o, ws, T.L, raw, s, x));
   ANR_TRY(read_count((const int*)(ws + T.L.counts), &e.n, s));
   const int n = e.n;
   const long N = (long)R * 64;
-  TrainBufs b = bufs(T, ws, f, ray_o, ray_d, near_, far_, R, o);
+  TrainBufs b = bufs(T, ws, f, ray_o, ray_d, near_, far_, R, o, x);
   const int g1 = (n + 255) / 256;
   if (n > 0) {
     hipLaunchKernelGGL(k_tr_point_prep, dim3((n + 3) / 4), dim3(256), 0, s, b);
@@ -349,16 +354,19 @@ int train_forward(const anr_params* p, const anr_frame* f, const float* ray_o, c
     ANR_TRY(check_launch("k_tr_raw"));
   }
   ANR_TRY(stage_alpha_ind(R, o, ws, T.L, s));
+  if (x) return ANR_OK;
   return stage_composite(near_, far_, R, o, raw, out, nullptr, s);
 }
 
+// x != NULL: free samples; the upstream gradient is d raw (x->n_pts, 4) (NULL: zero) instead of d rgb_map
 int train_backward(const anr_params* p, float* const* g, const anr_frame* f, const float* ray_o, const float* ray_d,
                    const float* near_, const float* far_, int R, const anr_render_opts* o, const float* d_rgb,
-                   const float* d_pbw, const float* d_tbw, char* ws, const TLayout& T, hipStream_t s, Exec& e) {
+                   const float* d_pbw, const float* d_tbw, char* ws, const TLayout& T, hipStream_t s, Exec& e,
+                   const anr_samples* x = nullptr, const float* d_raw = nullptr, hipEvent_t nerf_done = nullptr) {
   const int n = e.n;
   const long N = (long)R * 64;
   const long S = N * 256;
-  TrainBufs b = bufs(T, ws, f, ray_o, ray_d, near_, far_, R, o);
+  TrainBufs b = bufs(T, ws, f, ray_o, ray_d, near_, far_, R, o, x);
   b.d_rgb_map = d_rgb; b.d_pbw = d_pbw; b.d_tbw = d_tbw;
   const int g1 = (n + 255) / 256;
   if (n <= 0) return ANR_OK;
@@ -375,9 +383,15 @@ int train_backward(const anr_params* p, float* const* g, const anr_frame* f, con
   float* ysum = (float*)(ws + T.ysum);
   if (hipMemsetAsync(b.dGt, 0, (size_t)n * 64 * 4, s) != hipSuccess) return fail(ANR_E_HIP, "memset");
 
-  // compositing + raw activations
-  hipLaunchKernelGGL(k_tr_composite_bwd, dim3((R + 3) / 4), dim3(256), 0, s, b);
-  ANR_TRY(check_launch("k_tr_composite_bwd"));
+  // compositing (or the caller's d raw) + raw activations
+  if (x) {
+    const hipError_t r = d_raw ? hipMemcpyAsync(b.draw, d_raw, (size_t)x->n_pts * 16, hipMemcpyDeviceToDevice, s)
+                               : hipMemsetAsync(b.draw, 0, (size_t)x->n_pts * 16, s);
+    if (r != hipSuccess) return fail(ANR_E_HIP, "d raw copy failed");
+  } else {
+    hipLaunchKernelGGL(k_tr_composite_bwd, dim3((R + 3) / 4), dim3(256), 0, s, b);
+    ANR_TRY(check_launch("k_tr_composite_bwd"));
+  }
   hipLaunchKernelGGL(k_tr_raw_bwd, dim3(g1), dim3(256), 0, s, b);
   ANR_TRY(check_launch("k_tr_raw_bwd"));
   // rgb_fc, view_fc (ReLU), latent_fc (latent folded), feature_fc || alpha_fc
@@ -421,6 +435,9 @@ int train_backward(const anr_params* p, float* const* g, const anr_frame* f, con
       nxt = t;
     }
   }
+  // the canonical NeRF's gradients (tensors 0..26) are final here: a caller may start reducing them
+  // while the blend-weight backward below runs (bucketed all-reduce, anr_train_hooks)
+  if (nerf_done && hipEventRecord(nerf_done, s) != hipSuccess) return fail(ANR_E_HIP, "hipEventRecord failed");
   // upstream pbw / tbw row gradients; T-pose BW backward (latent row 0)
   hipLaunchKernelGGL(k_tr_rows_bwd, dim3(g1), dim3(256), 0, s, b);
   ANR_TRY(check_launch("k_tr_rows_bwd"));
@@ -620,6 +637,15 @@ int anr_train_step(const anr_params* p, float* const* grads, const anr_frame* f,
                    const float* ray_d, const float* near_, const float* far_, int n_rays, const anr_render_opts* o,
                    const float* rgb_gt, const uint8_t* mask_at_box, const anr_render_out* out, float* loss3,
                    void* workspace, size_t ws_bytes, void* stream) {
+  return anr_train_step_hooked(p, grads, f, ray_o, ray_d, near_, far_, n_rays, o, rgb_gt, mask_at_box, out, loss3,
+                               nullptr, workspace, ws_bytes, stream);
+}
+
+int anr_train_step_hooked(const anr_params* p, float* const* grads, const anr_frame* f, const float* ray_o,
+                          const float* ray_d, const float* near_, const float* far_, int n_rays,
+                          const anr_render_opts* o, const float* rgb_gt, const uint8_t* mask_at_box,
+                          const anr_render_out* out, float* loss3, const anr_train_hooks* hooks, void* workspace,
+                          size_t ws_bytes, void* stream) {
   ANR_TRY(check_args(p, f, ray_o, ray_d, near_, far_, n_rays, o, workspace));
   if (!grads || !rgb_gt || !loss3 || !out || !out->rgb_map || !out->acc_map || !out->depth_map)
     return fail(ANR_E_ARG, "anr_train_step: NULL argument");
@@ -651,8 +677,13 @@ int anr_train_step(const anr_params* p, float* const* grads, const anr_frame* f,
   hipLaunchKernelGGL(k_tr_loss_grads, dim3(gx, 2), dim3(256), 0, s, b, rgb_gt, mask_at_box, (const float*)acc3, d_rgb,
                      d_pbw, d_tbw);
   ANR_TRY(check_launch("k_tr_loss_grads"));
-  ANR_TRY(train_backward(p, grads, f, ray_o, ray_d, near_, far_, n_rays, o, d_rgb, d_pbw, d_tbw, ws, T, s, e));
-  if (e.n <= 0) return ANR_OK;
+  hipEvent_t nerf_done = hooks ? (hipEvent_t)hooks->nerf_grads_ready : nullptr;
+  ANR_TRY(train_backward(p, grads, f, ray_o, ray_d, near_, far_, n_rays, o, d_rgb, d_pbw, d_tbw, ws, T, s, e, nullptr,
+                         nullptr, nerf_done));
+  if (e.n <= 0) {
+    if (nerf_done && hipEventRecord(nerf_done, s) != hipSuccess) return fail(ANR_E_HIP, "hipEventRecord failed");
+    return ANR_OK;
+  }
   float* ysum = (float*)(ws + T.ysum);
   PoseScope ps(e);
   return bw_backward(e, p->t + 27, grads + 27, (const float*)(ws + T.Gp), (const float*)(ws + T.Hp), (const float*)(ws + T.dLp),
@@ -706,6 +737,143 @@ int anr_anim_step(const anr_params* p, float* const* grads, const anr_frame* f, 
   hipLaunchKernelGGL(k_an_loss_final, dim3(1), dim3(1), 0, s, (const float*)(ws + T.acc),
                      (const int*)(ws + T.counts) + 1, loss3);
   return check_launch("k_an_loss_final");
+}
+
+// ---- Network.forward under autograd (free samples) -------------------------------------------
+static int check_network_train(const anr_params* p, const anr_frame* f, const anr_samples* x, const anr_render_opts* o,
+                               void* ws) {
+  if (!x || !x->wpts || !x->viewdir || !x->dists || x->n_pts <= 0 || (long)x->n_pts > 0x7fffffffL / 24 - 64)
+    return fail(ANR_E_ARG, "network train: bad samples");
+  if (f && f->n_views) return fail(ANR_E_ARG, "network train: the visibility filter is a renderer option");
+  // check_args wants ray pointers: the samples stand in for them
+  return check_args(p, f, x->wpts, x->viewdir, x->dists, x->dists, (x->n_pts + 63) / 64, o, ws);
+}
+
+size_t anr_network_train_workspace_bytes(int n_pts, const anr_render_opts* o, const anr_frame* f) {
+  if (!o || !f || n_pts <= 0) return 0;
+  const int G = (n_pts + 63) / 64;
+  const long np = (long)f->pbw_dims[0] * f->pbw_dims[1] * f->pbw_dims[2];
+  const long nt = (long)f->tbw_dims[0] * f->tbw_dims[1] * f->tbw_dims[2];
+  return tlayout(G, G, np, nt).total;
+}
+
+int anr_network_train_fwd(const anr_params* p, const anr_frame* f, const anr_samples* x, const anr_render_opts* o,
+                          float* raw, void* workspace, size_t ws_bytes, void* stream) {
+  ANR_TRY(check_network_train(p, f, x, o, workspace));
+  if (!raw) return fail(ANR_E_ARG, "anr_network_train_fwd: NULL raw");
+  const int G = (x->n_pts + 63) / 64;
+  anr_render_opts oo = *o;
+  oo.chunk = G;
+  oo.t_rand = nullptr;
+  const long np = (long)f->pbw_dims[0] * f->pbw_dims[1] * f->pbw_dims[2];
+  const long nt = (long)f->tbw_dims[0] * f->tbw_dims[1] * f->tbw_dims[2];
+  const TLayout T = tlayout(G, G, np, nt);
+  if (ws_bytes < T.total) return fail(ANR_E_WORKSPACE, "anr_network_train_fwd: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  char* ws = (char*)workspace;
+  Exec e{s, 0, (o->precision == ANR_BF16 || o->precision == ANR_BF16_ALL) ? 1 : 0, o->precision == ANR_BF16 ? 1 : 0};
+  ANR_TRY(pack_images(e, p, ws + T.wimg, s, (float*)(ws + T.wslab)));
+  ANR_TRY(train_forward(p, f, nullptr, nullptr, nullptr, nullptr, G, &oo, nullptr, ws, T, s, e, x));
+  if (hipMemcpyAsync(raw, ws + T.L.raw, (size_t)x->n_pts * 16, hipMemcpyDeviceToDevice, s) != hipSuccess)
+    return fail(ANR_E_HIP, "anr_network_train_fwd: raw copy failed");
+  return ANR_OK;
+}
+
+int anr_network_train_bwd(const anr_params* p, float* const* grads, const anr_frame* f, const anr_samples* x,
+                          const anr_render_opts* o, const float* d_raw, const float* d_pbw, const float* d_tbw,
+                          void* workspace, size_t ws_bytes, void* stream) {
+  ANR_TRY(check_network_train(p, f, x, o, workspace));
+  if (!grads) return fail(ANR_E_ARG, "anr_network_train_bwd: NULL grads");
+  for (int i = 0; i < ANR_NUM_TENSORS; ++i)
+    if (!grads[i]) return fail(ANR_E_ARG, "anr_network_train_bwd: NULL grad tensor");
+  const int G = (x->n_pts + 63) / 64;
+  anr_render_opts oo = *o;
+  oo.chunk = G;
+  oo.t_rand = nullptr;
+  const long np = (long)f->pbw_dims[0] * f->pbw_dims[1] * f->pbw_dims[2];
+  const long nt = (long)f->tbw_dims[0] * f->tbw_dims[1] * f->tbw_dims[2];
+  const TLayout T = tlayout(G, G, np, nt);
+  if (ws_bytes < T.total) return fail(ANR_E_WORKSPACE, "anr_network_train_bwd: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  char* ws = (char*)workspace;
+  Exec e{s, 0, (o->precision == ANR_BF16 || o->precision == ANR_BF16_ALL) ? 1 : 0, o->precision == ANR_BF16 ? 1 : 0};
+  ANR_TRY(pack_images(e, p, ws + T.wimg, s, (float*)(ws + T.wslab)));
+  ANR_TRY(read_count((const int*)(ws + T.L.counts), &e.n, s));
+  ANR_TRY(train_backward(p, grads, f, nullptr, nullptr, nullptr, nullptr, G, &oo, nullptr, d_pbw, d_tbw, ws, T, s, e, x,
+                         d_raw));
+  if (e.n <= 0) return ANR_OK;
+  const long N = (long)G * 64;
+  float* ysum = (float*)(ws + T.ysum);
+  PoseScope ps(e);
+  return bw_backward(e, p->t + 27, grads + 27, (const float*)(ws + T.Gp), (const float*)(ws + T.Hp),
+                     (const float*)(ws + T.dLp), (float*)(ws + T.dA), (float*)(ws + T.dB), nullptr, N, ysum + 1024,
+                     f->latent_index, 1, s);
+}
+
+// ---- free-point helpers: calculate_neural_blend_weights / novel_pose_bw, TPoseHuman.calculate_alpha --
+static size_t points_take(size_t& o, size_t floats) {
+  const size_t at = o;
+  o = align256(o + floats * 4);
+  return at;
+}
+
+size_t anr_points_workspace_bytes(int n) {
+  if (n <= 0) return 0;
+  size_t o = 0;
+  const size_t N = (size_t)n;
+  points_take(o, N * 64); points_take(o, N * 32); points_take(o, N * 32); points_take(o, N * 256 * 8);
+  points_take(o, 512);
+  return o;
+}
+
+int anr_blend_weights(const anr_params* p, int field, const float* pts, const float* smpl_bw, int n,
+                      const int64_t* latent_row, int row_add, float* bw, void* workspace, size_t ws_bytes, void* stream) {
+  if (!p || !pts || !smpl_bw || !latent_row || !bw || !workspace || n <= 0 || (field != 0 && field != 1))
+    return fail(ANR_E_ARG, "anr_blend_weights: bad arguments");
+  const float* const* W = field ? p->novel : p->t + 27;
+  for (int i = 0; i < 19; ++i)
+    if (!W[i]) return fail(ANR_E_ARG, "anr_blend_weights: NULL blend-weight field tensor");
+  if (ws_bytes < anr_points_workspace_bytes(n)) return fail(ANR_E_WORKSPACE, "anr_blend_weights: workspace too small");
+  char* ws = (char*)workspace;
+  size_t o = 0;
+  const size_t N = (size_t)n;
+  float* G = (float*)(ws + points_take(o, N * 64));
+  float* I = (float*)(ws + points_take(o, N * 32));
+  float* Lg = (float*)(ws + points_take(o, N * 32));
+  float* H = (float*)(ws + points_take(o, N * 256 * 8));
+  float* fold = (float*)(ws + points_take(o, 512));
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_pt_prep, dim3((n + 3) / 4), dim3(256), 0, s, pts, smpl_bw, n, G, I);
+  FoldArgs fa{W[1], W[2], W[11], W[12], W[0], latent_row, row_add, fold};
+  hipLaunchKernelGGL(k_fold_latent, dim3(1), dim3(256), 0, s, fa);
+  ANR_TRY(check_launch("anr_blend_weights prep"));
+  Exec e{s, n, 0, 0};
+  ANR_TRY(bw_forward(e, W, G, H, Lg, n, fold, fold + 256));
+  hipLaunchKernelGGL(k_pt_softmax_out, dim3((n + 255) / 256), dim3(256), 0, s, (const float*)Lg, (const float*)I, n, bw);
+  return check_launch("k_pt_softmax_out");
+}
+
+int anr_canonical_alpha(const anr_params* p, const float* pts, int n, float* alpha, void* workspace, size_t ws_bytes,
+                        void* stream) {
+  if (!p || !pts || !alpha || !workspace || n <= 0) return fail(ANR_E_ARG, "anr_canonical_alpha: bad arguments");
+  for (int i = 1; i <= 18; ++i)
+    if (!p->t[i]) return fail(ANR_E_ARG, "anr_canonical_alpha: NULL parameter tensor");
+  if (ws_bytes < anr_points_workspace_bytes(n)) return fail(ANR_E_WORKSPACE, "anr_canonical_alpha: workspace too small");
+  char* ws = (char*)workspace;
+  size_t o = 0;
+  const size_t N = (size_t)n;
+  float* G = (float*)(ws + points_take(o, N * 64));
+  points_take(o, N * 32);
+  points_take(o, N * 32);
+  float* H = (float*)(ws + points_take(o, N * 256 * 8));
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_pt_prep, dim3((n + 3) / 4), dim3(256), 0, s, pts, (const float*)nullptr, n, G, (float*)nullptr);
+  ANR_TRY(check_launch("k_pt_prep"));
+  Exec e{s, n, 0, 0};
+  TrainBufs b{};
+  b.Gt = G;
+  b.Alpha = alpha;
+  return nerf_alpha_fwd(e, p, b, H, n);
 }
 
 int anr_adam(float* param, float* grad, float* exp_avg, float* exp_avg_sq, long n, float lr, float beta1, float beta2,

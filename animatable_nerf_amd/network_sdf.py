@@ -67,7 +67,7 @@ class Network(nn.Module):
 
     def __init__(self, cfg=None):
         super().__init__()
-        cfg = cfg if cfg is not None else _config.cfg
+        cfg = cfg if cfg is not None else _config.active()
         nlc = int(cfg.get('num_latent_code', -1))
         if nlc < 0:
             nlc = int(cfg.num_train_frame)  # config.py:144-145

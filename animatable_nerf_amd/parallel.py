@@ -3,8 +3,9 @@
 Render (config 2): frames / 2048-ray chunks are independent, so ranks never exchange data on the
 hot path; ``shard_chunks`` gives each rank a contiguous run of whole reference chunks (preserving
 the per-chunk argmin / argmax semantics) when one frame is split.
-Training (configs 3/4): the only exchange is one mean all-reduce of the flat gradient blob per step
-(DDP semantics of trainer.py:13-18), plus scalar loss statistics.
+Training (configs 3/4): the only exchange is the mean all-reduce of the flat gradient blob per step
+(DDP semantics of trainer.py:13-18), in two buckets overlapped with the backward (GradBuckets); the
+loss scalars ride in the blob's tail, so the reported loss is the mean over ranks.
 """
 import os
 
@@ -34,6 +35,41 @@ def allreduce_mean_(t, group=None):
         dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
         t.div_(dist.get_world_size(group))
     return t
+
+
+class GradBuckets:
+    """Mean all-reduce of a flat gradient blob in buckets, each issued as soon as the backward has
+    finished it (DDP's reducer buckets parameters in reverse layer order and overlaps their all-reduce
+    with the rest of the backward, trainer.py:13-18).
+
+    ``bounds``: [(start, end), ...] in the order the backward finishes them. On a GPU blob the
+    collectives run from a side stream: ``reduce(i, ready)`` makes it wait for the event ``ready``
+    (recorded on the compute stream when bucket i is final; None: everything enqueued so far) and
+    returns at once; ``wait()`` makes the current stream wait for every issued bucket. On a CPU blob
+    (gloo) each ``reduce`` completes in place."""
+
+    def __init__(self, blob, bounds, group=None):
+        self.views = [blob[s:e] for s, e in bounds]
+        self.group = group
+        self.comm = torch.cuda.Stream(device=blob.device) if blob.is_cuda else None
+
+    def reduce(self, i, ready=None):
+        if not is_dist():
+            return
+        if self.comm is None:
+            allreduce_mean_(self.views[i], self.group)
+            return
+        cur = torch.cuda.current_stream(self.views[i].device)
+        with torch.cuda.stream(self.comm):
+            if ready is not None:
+                self.comm.wait_event(ready)
+            else:
+                self.comm.wait_stream(cur)
+            allreduce_mean_(self.views[i], self.group)
+
+    def wait(self):
+        if self.comm is not None and is_dist():
+            torch.cuda.current_stream(self.views[0].device).wait_stream(self.comm)
 
 
 def broadcast_(t, src=0, group=None):
@@ -105,13 +141,21 @@ def render_sharded(renderer, batch, chunk=2048, group=None):
     rank = dist.get_rank(group) if is_dist() else 0
     world = dist.get_world_size(group) if is_dist() else 1
     R = int(batch['ray_o'].shape[1])
+    widens = getattr(renderer, 'widens_tbounds', False)
+    tb0 = batch['tbounds'].detach().clone() if widens else None
     sub, (s, e) = shard_batch(batch, rank, world, chunk)
     if e > s:
-        out = renderer.render_device(sub, bw_rows=False)
+        # the sdf_pdf renderer widens tbounds per chunk: this shard starts at reference chunk s / chunk
+        out = renderer.render_device(sub, bw_rows=False, chunk_offset=s // chunk) \
+            if getattr(renderer, 'widens_tbounds', False) else renderer.render_device(sub, bw_rows=False)
     else:  # more ranks than chunks: an empty shard
         dev = batch['ray_o'].device
         out = {'rgb_map': torch.zeros((1, 0, 3), device=dev), 'acc_map': torch.zeros((1, 0), device=dev),
                'depth_map': torch.zeros((1, 0), device=dev), 'raw': torch.zeros((1, 0, 4), device=dev)}
+    if widens:  # every rank leaves the frame's bounds as the whole single-GPU render does
+        from .renderer_sdf import widen_tbounds
+        with torch.no_grad():
+            batch['tbounds'].copy_(widen_tbounds(tb0, (R + chunk - 1) // chunk))
     ret = {k: gather_rays(out[k], R, world, chunk, group) for k in ('rgb_map', 'acc_map', 'depth_map')}
     ret['raw_local'] = out['raw']
     ret['span'] = (s, e)

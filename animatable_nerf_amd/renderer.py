@@ -32,13 +32,26 @@ def _f32(t, device):
 class _Call:
     """Device tensors + C structs of one render/train call (keeps the tensors alive)."""
 
-    def __init__(self, renderer, batch, t_rand):
+    def __init__(self, renderer, batch, t_rand, samples=None):
         cfg = renderer.cfg
         self.dev = dev = renderer.device()
-        self.rays = {k: _f32(batch[k], dev) for k in RAY_KEYS}
-        self.R = R = self.rays['ray_o'].shape[1]
         ns = int(cfg.N_samples)
-        self.t_rand = None if t_rand is None else _f32(t_rand, dev).reshape(R, ns)
+        if samples is None:
+            self.rays = {k: _f32(batch[k], dev) for k in RAY_KEYS}
+            self.R = R = self.rays['ray_o'].shape[1]
+            self.t_rand = None if t_rand is None else _f32(t_rand, dev).reshape(R, ns)
+        else:  # Network.forward(wpts, viewdir, dists, batch): free samples instead of rays
+            wpts, viewdir, dists = samples
+            self.wpts = _f32(wpts, dev).reshape(-1, 3)
+            self.vdir = _f32(viewdir, dev).reshape(-1, 3)
+            self.dists = _f32(dists, dev).reshape(-1)
+            n = self.wpts.shape[0]
+            if self.vdir.shape[0] != n or self.dists.shape[0] != n:
+                raise ValueError(f'Network.forward: wpts {tuple(wpts.shape)}, viewdir {tuple(viewdir.shape)}, '
+                                 f'dists {tuple(dists.shape)} disagree on the sample count')
+            self.samples = _lib.Samples(self.wpts.data_ptr(), self.vdir.data_ptr(), self.dists.data_ptr(), n)
+            self.n = n
+            self.t_rand = None
         fr = {k: _f32(batch[k], dev) for k in FRAME_KEYS}
         self.fr = fr
         self.li = batch['latent_index'].to(device=dev, dtype=torch.int64).reshape(-1).contiguous()
@@ -83,6 +96,8 @@ class _Call:
             raise ValueError(f"render_precision must be 'fp32' or 'bf16x3', got {rprec!r}")
         self.render_precision = _lib.BF16X3 if rprec == 'bf16x3' else _lib.FP32
         self.opts = o
+        if samples is not None:
+            return
         self.rgb = torch.empty((1, R, 3), device=dev)
         self.acc = torch.empty((1, R), device=dev)
         self.depth = torch.empty((1, R), device=dev)
@@ -98,7 +113,7 @@ class Renderer:
 
     def __init__(self, net, cfg=None):
         self.net = net
-        self.cfg = cfg if cfg is not None else _config.cfg
+        self.cfg = cfg if cfg is not None else _config.active()
         self.lib = _lib.load()
         self._packed = None
         self._pack_key = None
@@ -202,11 +217,98 @@ class Renderer:
             return self.render_train(batch)
         with torch.no_grad():
             ret = self.render_device(batch)
-        return {k: v.cpu() for k, v in ret.items()}
+        return to_host(ret)
 
     def counts(self, n_rays):
         """(kept samples, alpha_ind rows) of the last evaluation render (device read, syncs)."""
         return self._counts(self._ws, n_rays)
+
+    # ---- Network.forward over free samples (tpose_nerf_network.py:139-215) -----------------
+    def network_forward(self, wpts, viewdir, dists, batch):
+        """``Network.forward(wpts (n,3), viewdir (n,3), dists (n), batch)`` -> {'raw' (1,n,4), 'pbw' (1,m,24),
+        'tbw' (1,m,24)}: one reference network call (its forced argmin / argmax span the call). Under autograd
+        with a training network: the layer-wise executor (anr_network_train_fwd/bwd); else the fused kernel."""
+        if torch.is_grad_enabled() and self.net.training and any(p.requires_grad for p in self.net.parameters()):
+            raw, pbw, tbw = _TrainNetwork.apply(self, batch, (wpts, viewdir, dists), *self.net.core_tensors())
+            return {'pbw': pbw, 'tbw': tbw, 'raw': raw}
+        with torch.no_grad():
+            p = self.params()
+            dev = self._packed.device
+            c = _Call(self, batch, None, samples=(wpts, viewdir, dists))
+            c.opts.precision = c.render_precision
+            ws_bytes = self.lib.anr_network_workspace_bytes(c.n, ctypes.byref(c.opts), ctypes.byref(c.frame))
+            ws = self._workspace('_nws', ws_bytes, dev)
+            raw = torch.empty((1, c.n, 4), device=dev)
+            _lib.check(self.lib.anr_network_fwd(ctypes.byref(p), ctypes.byref(c.frame), ctypes.byref(c.samples),
+                                                ctypes.byref(c.opts), _lib.ptr(raw), _lib.ptr(ws), ws_bytes,
+                                                _lib.stream_ptr(dev)), 'anr_network_fwd')
+            pbw, tbw = self._net_rows(ws, c.n, dev)
+        return {'pbw': pbw, 'tbw': tbw, 'raw': raw}
+
+    def _net_rows(self, ws, n, dev):
+        addr = self.lib.anr_network_counts(_lib.ptr(ws), n)
+        base = ws.data_ptr()
+        cnt = ws[addr - base:addr - base + 8].view(torch.int32).cpu()  # host sync (the reference's alpha_ind)
+        self.last_counts = (int(cnt[0]), int(cnt[1]))
+        m = self.last_counts[1]
+        pbw = torch.empty((1, m, 24), device=dev)
+        tbw = torch.empty((1, m, 24), device=dev)
+        if m > 0:
+            _lib.check(self.lib.anr_network_bw_rows(_lib.ptr(ws), n, _lib.ptr(pbw), _lib.ptr(tbw), _lib.stream_ptr(dev)),
+                       'anr_network_bw_rows')
+        return pbw, tbw
+
+    def blend_weights(self, pts, smpl_bw, latent_index, field=0, row_add=0):
+        """calculate_neural_blend_weights (field 0, tpose_nerf_network.py:55-77) / novel_pose_bw (field 1,
+        :304-315): pts (1,n,3), smpl_bw (1,24,n), latent_index (int64 tensor) -> bw (1,24,n). Forward only."""
+        p = self.params(pack=False)
+        dev = self.device()
+        pts = _f32(pts, dev).reshape(-1, 3)
+        n = pts.shape[0]
+        sbw = _f32(smpl_bw, dev).reshape(24, n)
+        li = latent_index.to(device=dev, dtype=torch.int64).reshape(-1).contiguous()
+        if field == 1 and not self.net.novel_tensors():
+            raise RuntimeError('novel_pose_bw is absent (cfg.aninerf_animation is False)')
+        bw = torch.empty((1, 24, n), device=dev)
+        if n == 0:
+            return bw
+        ws_bytes = self.lib.anr_points_workspace_bytes(n)
+        ws = self._workspace('_pws', ws_bytes, dev)
+        _lib.check(self.lib.anr_blend_weights(ctypes.byref(p), field, _lib.ptr(pts), _lib.ptr(sbw), n, _lib.ptr(li),
+                                              row_add, _lib.ptr(bw), _lib.ptr(ws), ws_bytes, _lib.stream_ptr(dev)),
+                   'anr_blend_weights')
+        return bw
+
+    def canonical_alpha(self, nf_pts):
+        """TPoseHuman.calculate_alpha (tpose_nerf_network.py:241-250): nf_pts (1,n,3) -> alpha (1,1,n)."""
+        p = self.params(pack=False)
+        dev = self.device()
+        pts = _f32(nf_pts, dev).reshape(-1, 3)
+        n = pts.shape[0]
+        alpha = torch.empty((1, 1, n), device=dev)
+        if n == 0:
+            return alpha
+        ws_bytes = self.lib.anr_points_workspace_bytes(n)
+        ws = self._workspace('_pws', ws_bytes, dev)
+        _lib.check(self.lib.anr_canonical_alpha(ctypes.byref(p), _lib.ptr(pts), n, _lib.ptr(alpha), _lib.ptr(ws),
+                                                ws_bytes, _lib.stream_ptr(dev)), 'anr_canonical_alpha')
+        return alpha
+
+
+def to_host(ret):
+    """the eval outputs on the CPU, as tpose_renderer.py:154-155 leaves them: copied into page-locked
+    buffers (torch's caching host allocator reuses them call after call) with one stream sync, so the
+    ~1.4 GB of a 512x512 frame (raw + pbw / tbw rows) moves at the link's DMA rate."""
+    out = {}
+    for k, v in ret.items():
+        if v.is_cuda:
+            h = torch.empty(v.shape, dtype=v.dtype, pin_memory=True)
+            h.copy_(v, non_blocking=True)
+            out[k] = h
+        else:
+            out[k] = v
+    torch.cuda.current_stream().synchronize()
+    return out
 
 
 class _TrainRender(torch.autograd.Function):
@@ -245,6 +347,41 @@ class _TrainRender(torch.autograd.Function):
         _lib.check(lib.anr_train_bwd(ctypes.byref(p), gp, ctypes.byref(c.frame), *c.ray_ptrs(), c.R,
                                      ctypes.byref(c.opts), *[_lib.ptr(t) for t in keep], _lib.ptr(ctx.ws),
                                      ctx.ws_bytes, _lib.stream_ptr(dev)), 'anr_train_bwd')
+        return (None, None, None, *grads)
+
+
+class _TrainNetwork(torch.autograd.Function):
+    """Network.forward under autograd: forward = anr_network_train_fwd, backward = anr_network_train_bwd
+    from the upstream d raw and d pbw / d tbw rows (parameter gradients)."""
+
+    @staticmethod
+    def forward(ctx, renderer, batch, samples, *params):
+        lib = renderer.lib
+        p = renderer.params(pack=False)
+        dev = params[0].device
+        c = _Call(renderer, batch, None, samples=samples)
+        ws_bytes = lib.anr_network_train_workspace_bytes(c.n, ctypes.byref(c.opts), ctypes.byref(c.frame))
+        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+        raw = torch.empty((1, c.n, 4), device=dev)
+        _lib.check(lib.anr_network_train_fwd(ctypes.byref(p), ctypes.byref(c.frame), ctypes.byref(c.samples),
+                                             ctypes.byref(c.opts), _lib.ptr(raw), _lib.ptr(ws), ws_bytes,
+                                             _lib.stream_ptr(dev)), 'anr_network_train_fwd')
+        pbw, tbw = renderer._net_rows(ws, c.n, dev)
+        ctx.renderer, ctx.call, ctx.ws, ctx.ws_bytes = renderer, c, ws, ws_bytes
+        return raw, pbw, tbw
+
+    @staticmethod
+    def backward(ctx, d_raw, d_pbw, d_tbw):
+        r, c = ctx.renderer, ctx.call
+        params = r.net.core_tensors()
+        dev = params[0].device
+        p = r.params(pack=False)
+        grads = [torch.zeros_like(t) for t in params]
+        gp = (ctypes.c_void_p * _lib.NUM_TENSORS)(*[g.data_ptr() for g in grads])
+        keep = [t.contiguous() if t is not None else None for t in (d_raw, d_pbw, d_tbw)]
+        _lib.check(r.lib.anr_network_train_bwd(ctypes.byref(p), gp, ctypes.byref(c.frame), ctypes.byref(c.samples),
+                                               ctypes.byref(c.opts), *[_lib.ptr(t) for t in keep], _lib.ptr(ctx.ws),
+                                               ctx.ws_bytes, _lib.stream_ptr(dev)), 'anr_network_train_bwd')
         return (None, None, None, *grads)
 
 

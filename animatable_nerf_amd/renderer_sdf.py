@@ -30,10 +30,22 @@ def _f32(t, device):
     return t.to(device=device, dtype=torch.float32).contiguous()
 
 
+def widen_tbounds(tbounds, k):
+    """tbounds after the reference's in-place widening ran k times (anisdf_pdf_network.py:204-206):
+    the same fp32 subtract / add per chunk as the device's k_sdf_tbtab, so the bits agree."""
+    tb = tbounds.detach().clone().reshape(2, 3)
+    for _ in range(int(k)):
+        tb[0] -= 0.05
+        tb[1] += 0.05
+    return tb.reshape(tbounds.shape).contiguous()
+
+
 class Renderer:
+    widens_tbounds = True  # per chunk, in place (anisdf_pdf_network.py:204-206)
+
     def __init__(self, net, cfg=None):
         self.net = net
-        self.cfg = cfg if cfg is not None else _config.cfg
+        self.cfg = cfg if cfg is not None else _config.active()
         self.lib = _lib.load()
         self._ws = None
         self.last_counts = None
@@ -52,8 +64,12 @@ class Renderer:
             p.t[i] = t.data_ptr()
         return p
 
-    def render_device(self, batch, t_rand=None):
-        """All outputs stay in HBM; ``batch['tbounds']`` is widened in place (reference quirk)."""
+    def render_device(self, batch, t_rand=None, chunk_offset=0, bw_rows=True):
+        """All outputs stay in HBM; ``batch['tbounds']`` is widened in place (reference quirk).
+        ``chunk_offset`` c0 > 0: these rays are the reference's chunks c0, c0+1, ... of a larger frame
+        (a rank's shard, parallel.render_sharded): the reference has widened tbounds c0 times before
+        them (anisdf_pdf_network.py:204-206), so the device starts from those bounds. ``bw_rows`` is
+        accepted for the aninerf renderer's signature (this network has no pbw / tbw rows)."""
         p = self.params()
         dev = self.device()
         R = batch['ray_o'].shape[1]
@@ -62,6 +78,8 @@ class Renderer:
             t_rand = torch.rand((R, ns), device=dev)
         rays = {k: _f32(batch[k], dev) for k in RAY_KEYS}
         fr = {k: _f32(batch[k], dev) for k in FRAME_KEYS}
+        if chunk_offset > 0:
+            fr['tbounds'] = widen_tbounds(fr['tbounds'], chunk_offset)
         tr = None if t_rand is None else _f32(t_rand, dev).reshape(R, ns)
         li = batch['latent_index'].to(device=dev, dtype=torch.int64).reshape(-1).contiguous()
         occ = batch['occupancy'].to(device=dev, dtype=torch.uint8).reshape(-1).contiguous()
@@ -117,4 +135,5 @@ class Renderer:
                                'torch.no_grad() for evaluation')
         with torch.no_grad():
             ret = self.render_device(batch)
-        return {k: v.cpu() for k, v in ret.items()}
+        from .renderer import to_host
+        return to_host(ret)

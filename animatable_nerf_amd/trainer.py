@@ -8,8 +8,9 @@ Two ways to train, same kernels:
   ``anr_train_fwd`` / ``anr_train_bwd``), so the reference ``Trainer.train`` loop
   (``loss.backward(); clip_grad_value_(40); optimizer.step()``) runs unchanged.
 * ``FusedStep(net)`` — the native path: parameters and gradients live in one flat HBM blob, one
-  ``anr_train_step`` call runs forward + losses + backward, one ``anr_adam`` call clips and updates;
-  for N GPUs the flat gradient blob is all-reduced (mean, DDP semantics) over RCCL in one call.
+  ``anr_train_step_hooked`` call runs forward + losses + backward, one ``anr_adam`` call clips and
+  updates; for N GPUs the blob (with the loss statistics in its tail) is mean-all-reduced over RCCL
+  in two buckets, the canonical NeRF's while the blend-weight backward still runs (DDP semantics).
 """
 import ctypes
 import math
@@ -19,7 +20,7 @@ import torch.nn.functional as F
 
 from . import _lib
 from . import config as _config
-from .parallel import allreduce_mean_, broadcast_
+from .parallel import GradBuckets, broadcast_, is_dist
 from .renderer import Renderer, _Call
 
 
@@ -71,7 +72,7 @@ class FusedStep:
     """
 
     def __init__(self, net, cfg=None, lr=None, clip=40.0, betas=(0.9, 0.999), eps=1e-8, group=None):
-        self.cfg = cfg if cfg is not None else _config.cfg
+        self.cfg = cfg if cfg is not None else _config.active()
         self.net = net
         self.renderer = Renderer(net, self.cfg)
         self.lib = self.renderer.lib
@@ -83,7 +84,9 @@ class FusedStep:
         dev = ps[0].device
         n = sum(p.numel() for p in ps)
         self.flat = torch.empty(n, device=dev)
-        self.grad = torch.zeros(n, device=dev)
+        # gradient blob + 4 floats of loss statistics in its tail: one all-reduce carries both (the
+        # north_star's "all-reduce of the image/PSNR loss" next to DDP's gradient mean)
+        self.grad = torch.zeros(n + 4, device=dev)
         self.m = torch.zeros(n, device=dev)
         self.v = torch.zeros(n, device=dev)
         off = 0
@@ -98,7 +101,15 @@ class FusedStep:
             off += k
         self.n = n
         self.t = 0
-        self.loss3 = torch.zeros(4, device=dev)
+        self.loss3 = self.grad[n:n + 4]
+        # buckets in the order anr_train_step_hooked finishes them: the canonical NeRF (tensors 0..26,
+        # final before the blend-weight backward runs), then the blend-weight MLP (27..45) + losses
+        n_nerf = sum(p.numel() for p in ps[:27])
+        self.buckets = GradBuckets(self.grad, [(0, n_nerf), (n_nerf, n + 4)], group)
+        self.nerf_ready = None
+        if dev.type == 'cuda':
+            self.nerf_ready = torch.cuda.Event()
+            self.nerf_ready.record()  # creates the underlying hipEvent (re-recorded by the library)
         # DDP semantics (trainer.py:13-18): every replica starts from rank 0's weights, so the
         # averaged gradient describes one model and the replicas stay identical
         broadcast_(self.flat, 0, group)
@@ -111,8 +122,10 @@ class FusedStep:
     def load_adam_state_dict(self, sd):
         from .checkpoint import load_adam_state_dict
         self.t, self.lr = load_adam_state_dict(sd, self.net.core_tensors(), self.m, self.v)
-        # a checkpoint read on one rank only must not leave the other replicas' moments (or their
-        # step count, which sets Adam's bias corrections) behind
+        # every rank must call this (a collective): the replicas then continue from rank 0's weights
+        # (the views of self.flat that load_model filled), moments and step count (which sets Adam's
+        # bias corrections), whatever each rank's checkpoint read produced
+        broadcast_(self.flat, 0, self.group)
         broadcast_(self.m, 0, self.group)
         broadcast_(self.v, 0, self.group)
         tl = broadcast_(torch.tensor([float(self.t), float(self.lr)], dtype=torch.float64, device=self.m.device),
@@ -134,10 +147,16 @@ class FusedStep:
         self.grad.zero_()
         gp = (ctypes.c_void_p * _lib.NUM_TENSORS)(*[g.data_ptr() for g in self.grad_views])
         stream = _lib.stream_ptr(dev)
-        _lib.check(self.lib.anr_train_step(ctypes.byref(p), gp, ctypes.byref(c.frame), *c.ray_ptrs(), R,
-                                           ctypes.byref(c.opts), _lib.ptr(rgb), _lib.ptr(mask), ctypes.byref(c.out),
-                                           _lib.ptr(self.loss3), _lib.ptr(ws), ws_bytes, stream), 'anr_train_step')
-        allreduce_mean_(self.grad, self.group)
+        overlap = is_dist() and self.nerf_ready is not None
+        hooks = _lib.TrainHooks(self.nerf_ready.cuda_event if overlap else None)
+        _lib.check(self.lib.anr_train_step_hooked(ctypes.byref(p), gp, ctypes.byref(c.frame), *c.ray_ptrs(), R,
+                                                  ctypes.byref(c.opts), _lib.ptr(rgb), _lib.ptr(mask),
+                                                  ctypes.byref(c.out), _lib.ptr(self.loss3), ctypes.byref(hooks),
+                                                  _lib.ptr(ws), ws_bytes, stream), 'anr_train_step_hooked')
+        # N > 1: the NeRF bucket's all-reduce runs beside the blend-weight backward, then the rest
+        self.buckets.reduce(0, self.nerf_ready if overlap else None)
+        self.buckets.reduce(1)
+        self.buckets.wait()
         self.t += 1
         _lib.check(self.lib.anr_adam(_lib.ptr(self.flat), _lib.ptr(self.grad), _lib.ptr(self.m), _lib.ptr(self.v),
                                      self.n, float(self.lr if lr is None else lr), self.betas[0], self.betas[1],

@@ -130,7 +130,7 @@ class AnimationStep:
     the novel_pose_bw blob (optimizer.py:12-27 groups, trainer.py:64-68 clip_grad_value_(40))."""
 
     def __init__(self, net, cfg=None, lr=None, clip=40.0, betas=(0.9, 0.999), eps=1e-8, group=None):
-        self.cfg = cfg if cfg is not None else _config.cfg
+        self.cfg = cfg if cfg is not None else _config.active()
         self.net = net
         self.renderer = Renderer(net, self.cfg)
         self.lib = self.renderer.lib

@@ -1,23 +1,29 @@
 #!/usr/bin/env python
 """Headline benchmark: BASELINE.json metric on config 2 (aninerf_s9p full 512x512 render, fp32,
-novel-view eval) through the drop-in ``Renderer.render_device`` (HIP C-ABI).
+novel-view eval) through the drop-in renderer (HIP C-ABI).
 
 step    = one full-frame render of 512x512 box rays x 64 samples (262,142 rays hit the box),
-          inputs resident in HBM, outputs (rgb/acc/depth/raw + pbw/tbw rows) left in HBM.
-N GPUs  = one process per GPU (torch.distributed.run), each rendering its own frame (rays seed
-          2 + rank): frames are independent, so no collective on the data path ("scaling": "weak");
-          the timed region is bracketed by barriers and the max over ranks is reported.
-precision: --render-precision bf16x3 (default) runs the fused network kernel k_mlp_b16 — every
-          layer as a 2-way hi/lo split onto bf16 MFMA (3 products per MAC) with fp32 accumulation,
-          outputs held to the same 1e-4 fp32 tolerance as the exact path by the parity tests (measured
-          <= 4e-6, tools/precision_report.py); the exact-fp32 kernel k_mlp is timed in the same run.
-roofline: the fused network kernel is the dominant kernel; its per-launch time is measured with
-          hipEvents on the render stream (anr_profile_*); achieved = executed MFMA FLOP per kept
-          sample (bf16x3: 2*3*(2*497,152 + 527,872), the NeRF head folded; fp32: 3,306,496) x kept / time,
-          peak = the dense MFMA peak of the operand type (bf16 2.5 PF, fp32 157.3 TF);
-          achieved_credited uses SURVEY.md §8(d)'s 2,312,192 FLOP per kept sample.
-cpu_baseline: the oracle (op-for-op PyTorch-CPU restatement of the reference) on the first 16
-          chunks (32,768 rays) of the same frame, rank 0 at N=1 only.
+          inputs resident in HBM, outputs (rgb/acc/depth/raw + pbw/tbw rows) left in HBM
+          (Renderer.render_device). ``render_s`` reports the drop-in Renderer.render(batch) with its
+          eval D2H of every output (tpose_renderer.py:154-155) beside it.
+N GPUs  = one process per GPU (torch.distributed.run, or ``--gpus N`` spawns them itself), each
+          rendering its own frame (rays seed 2 + rank): frames are independent, so no collective on
+          the data path ("scaling": "weak"); the timed region is bracketed by barriers and the max
+          over ranks is reported.
+precision: the headline is config 2's fp32: the exact-fp32-MFMA fused kernel k_mlp. The split-bf16
+          kernel k_mlp_b16 (every layer as hi/lo bf16 pieces, 3 MFMA products per MAC, fp32
+          accumulation; outputs held to the same 1e-4 fp32 tolerance by the parity tests) is timed in
+          the same run and reported under ``bf16x3_split`` with its own roofline.
+roofline: the fused network kernel dominates; its per-launch time is measured with hipEvents on the
+          render stream (anr_profile_*). k_mlp: SURVEY.md §8(d)'s 2,312,192 credited FLOP per kept
+          sample against the 157.3 TF fp32 MFMA peak (the 3,306,496 FLOP it executes, T-pose BW MLP
+          included, beside it). k_mlp_b16: the bf16 MFMA FLOP it executes against the 2.5 PF dense bf16
+          peak, credited figure beside it. traffic: HBM bytes per launch from the committed PMC passes
+          (profiles/pmc_latest.json, per kernel).
+baselines (rank 0 at N=1, outside the timed region): cpu_baseline = the oracle (op-for-op PyTorch-CPU
+          restatement) on the first 16 chunks of the frame with every host thread this job may use;
+          torch_gpu_baseline = the same restatement with PyTorch-ROCm on this GPU over the whole frame
+          (BASELINE.md §3's denominator of the 30x target) -> vs_baseline.
 """
 import argparse
 import json
@@ -68,10 +74,14 @@ def parse():
                     help='sdf mode GEMMs: exact fp32 MFMA, or split-bf16 (outputs held to the same tolerances by '
                          'tests/test_gpu_sdf.py; 472 vs 559 ms per frame with the round-2 GEMM epilogue)')
     ap.add_argument('--no-exact', action='store_true', help='skip timing the other render precision')
+    ap.add_argument('--torch-rays', type=int, default=16 * 2048,
+                    help='rays of the frame the PyTorch-ROCm denominator renders (cold pass ~0.8 s per chunk)')
+    ap.add_argument('--no-torch-baseline', action='store_true',
+                    help='skip the PyTorch-ROCm restatement denominator (vs_baseline)')
     ap.add_argument('--shard-frame', action='store_true',
                     help='render: split ONE frame over the ranks by whole chunks and all-gather rgb/acc/depth '
                          '(strong scaling, parallel.render_sharded) instead of one frame per GPU')
-    ap.add_argument('--render-precision', choices=('fp32', 'bf16x3'), default='bf16x3',
+    ap.add_argument('--render-precision', choices=('fp32', 'bf16x3'), default='fp32',
                     help='fp32: exact fp32 MFMA; bf16x3: T-pose BW MLP + NeRF as hi/lo-split bf16 MFMA '
                          '(outputs within the 1e-4 fp32 tolerance, tests/test_gpu_render.py)')
     ap.add_argument('--train-rays', type=int, default=1024)
@@ -80,14 +90,115 @@ def parse():
     return ap.parse_args()
 
 
+def host_threads():
+    """CPU threads the baseline legs may use on this host: os.cpu_count(), limited by the process's
+    affinity mask and by a cgroup CPU quota when one is set (on a shared GPU box the quota is the
+    job's share of the node; running more threads than that only time-slices them)."""
+    n = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = n
+    quota = None
+    try:
+        q, period = open('/sys/fs/cgroup/cpu.max').read().split()
+        if q != 'max':
+            quota = max(1, int(int(q) // int(period)))
+    except (OSError, ValueError):
+        pass
+    model = ''
+    try:
+        for line in open('/proc/cpuinfo'):
+            if line.startswith('model name'):
+                model = line.split(':', 1)[1].strip()
+                break
+    except OSError:
+        pass
+    omp = None
+    try:
+        omp = int(os.environ['OMP_NUM_THREADS'])
+    except (KeyError, ValueError):
+        pass
+    threads = min(x for x in (n, aff, quota, omp) if x)
+    return threads, {'nproc': n, 'affinity': aff, 'cgroup_cpu_quota': quota, 'OMP_NUM_THREADS': omp,
+                     'cpu_model': model}
+
+
+def progress(msg):
+    """one line per finished leg on stderr (the GPU box kills a command that is silent for 3 min)"""
+    import sys
+    print(f'[bench {time.strftime("%H:%M:%S")}] {msg}', file=sys.stderr, flush=True)
+
+
+def render_roofline(prec, n_kept, kernel_ms):
+    """roofline of the fused network kernel of one render precision: k_mlp (exact fp32 MFMA) is
+    priced on SURVEY.md §8(d)'s credited 2,312,192 FLOP per kept sample against the fp32 MFMA peak;
+    k_mlp_b16 (split bf16, 3 products per MAC) on the bf16 MFMA FLOP it executes against the dense
+    bf16 peak, with the credited figure beside it."""
+    split = prec == 'bf16x3'
+    kernel = 'k_mlp_b16' if split else 'k_mlp'
+    t = kernel_ms * 1e-3
+    credited = n_kept * FLOP_PER_KEPT / t / 1e12
+    if split:
+        flop_exec = 2 * 3 * (2 * MAC_BW + MAC_NERF_FOLDED)
+        executed = n_kept * flop_exec / t / 1e12
+        r = {'bound': 'mfma', 'kernel': kernel, 'achieved': executed, 'peak': PEAK_BF16_MFMA_TFLOPS,
+             'unit': 'TFLOP/s', 'frac': executed / PEAK_BF16_MFMA_TFLOPS, 'traffic': None,
+             'flop_per_kept': flop_exec, 'flop_basis': 'executed bf16 MFMA FLOP (3 products per MAC)',
+             'achieved_credited': credited, 'frac_credited_vs_bf16_peak': credited / PEAK_BF16_MFMA_TFLOPS,
+             'flop_per_kept_credited': FLOP_PER_KEPT}
+    else:
+        executed = n_kept * FLOP_PER_KEPT_EXECUTED / t / 1e12
+        r = {'bound': 'mfma', 'kernel': kernel, 'achieved': credited, 'peak': PEAK_FP32_MFMA_TFLOPS,
+             'unit': 'TFLOP/s', 'frac': credited / PEAK_FP32_MFMA_TFLOPS, 'traffic': None,
+             'flop_per_kept': FLOP_PER_KEPT, 'flop_basis': 'SURVEY.md §8(d) credit (BW pose + NeRF, latent folded)',
+             'achieved_executed': executed, 'frac_executed': executed / PEAK_FP32_MFMA_TFLOPS,
+             'flop_per_kept_executed': FLOP_PER_KEPT_EXECUTED}
+    r['kernel_ms'] = kernel_ms
+    r['kept_samples_per_launch'] = n_kept
+    pmc = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'profiles', 'pmc_latest.json')
+    if os.path.exists(pmc):
+        t = json.load(open(pmc)).get(kernel)
+        if t:
+            r['traffic'] = t['bytes_per_launch']
+            r['traffic_source'] = t['source'] + '; ' + t['correction']
+    return r
+
+
+def launch_workers(args):
+    """``python bench.py --gpus N`` without a launcher: one process per GPU, spawned before this
+    process touches the GPU, rendezvous on 127.0.0.1 (the torch.distributed.run contract)."""
+    import socket
+    import subprocess
+    import sys
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable] + sys.argv, env=env))
+    codes = [p.wait() for p in procs]
+    bad = [c for c in codes if c != 0]
+    return bad[0] if bad else 0
+
+
 def main():
     args = parse()
+    if 'WORLD_SIZE' not in os.environ and args.gpus > 1:
+        raise SystemExit(launch_workers(args))
     rank = int(os.environ.get('RANK', 0))
     world = int(os.environ.get('WORLD_SIZE', 1))
     local = int(os.environ.get('LOCAL_RANK', 0))
-    # rehearsal knobs for the N > 1 path on a one-GPU box (never set by the driver):
-    # ANR_BENCH_BACKEND=gloo, ANR_BENCH_ONE_DEVICE=1 maps every rank to cuda:0
+    if world != args.gpus:
+        raise SystemExit(f'bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks')
+    # rehearsal knobs for the N > 1 path on a one-GPU box or a CPU host (never set by the driver):
+    # ANR_BENCH_BACKEND=gloo, ANR_BENCH_ONE_DEVICE=1 maps every rank to cuda:0, ANR_BENCH_DRYRUN=1
+    # runs the launch / rendezvous / timing / max-over-ranks logic with no GPU work at all
     backend = os.environ.get('ANR_BENCH_BACKEND', 'nccl')
+    if os.environ.get('ANR_BENCH_DRYRUN') == '1':
+        return dry_run(args, rank, world)
     if os.environ.get('ANR_BENCH_ONE_DEVICE') == '1':
         local = 0
     torch.cuda.set_device(local)
@@ -124,12 +235,18 @@ def main():
     net = net.to(dev)
     net.train()  # run.py evaluates in train() mode with perturb = 0
     lib = _lib.load()
+    frames = 1 if args.shard_frame else world  # frames rendered per timed step, all ranks together
+    s0, s1 = parallel.shard_chunks(R, rank, world) if args.shard_frame else (0, R)
+    R_local = max(1, s1 - s0)  # this rank's rays (n_kept, kernel_ms are this rank's)
 
-    def timed(precision):
+    def make_renderer(precision):
         cfg = config.defaults()
         cfg.perturb = 0
         cfg.render_precision = precision
-        renderer = Renderer(net, cfg)
+        return Renderer(net, cfg)
+
+    def timed(precision):
+        renderer = make_renderer(precision)
         render = (lambda: parallel.render_sharded(renderer, batch)) if args.shard_frame else \
             (lambda: renderer.render_device(batch))
         for _ in range(args.warmup):
@@ -154,63 +271,103 @@ def main():
         counts = renderer.counts(R_local) if args.shard_frame else renderer.last_counts
         return out, max_over_ranks(dt, dev, world), mlp_ms.value / max(1, launches.value), counts
 
-    frames = 1 if args.shard_frame else world  # frames rendered per timed step, all ranks together
-    s0, s1 = parallel.shard_chunks(R, rank, world) if args.shard_frame else (0, R)
-    R_local = max(1, s1 - s0)  # this rank's rays (n_kept, kernel_ms are this rank's)
-    others = [p for p in ('fp32', 'bf16x3') if p != args.render_precision]
-    side = {}
-    for prec in others if not args.no_exact else []:
-        o2, dt2, kms2, _ = timed(prec)
-        side[prec] = {'value': R * 64 * args.steps * frames / dt2, 'ms_per_step': dt2 / args.steps * 1e3,
-                      'kernel_ms': kms2}
-        del o2
-    out, dt_max, kernel_ms, (n_kept, m_rows) = timed(args.render_precision)
+    prec = args.render_precision
+    out, dt_max, kernel_ms, (n_kept, m_rows) = timed(prec)
+    progress(f'{prec}: {dt_max / args.steps * 1e3:.2f} ms/frame, kernel {kernel_ms:.2f} ms')
     value = R * 64 * args.steps * frames / dt_max
-    split = args.render_precision == 'bf16x3'
-    if split:
-        # executed bf16 MFMA work per kept sample: 3 products per MAC (lo*bh + hi*bl + hi*bh)
-        flop_exec = 2 * 3 * (2 * MAC_BW + MAC_NERF_FOLDED)
-        peak = PEAK_BF16_MFMA_TFLOPS
-        dtype = 'bf16 MFMA operands (hi/lo split, 3 products per MAC), fp32 accumulate'
-    else:
-        flop_exec = FLOP_PER_KEPT_EXECUTED
-        peak = PEAK_FP32_MFMA_TFLOPS
-        dtype = 'fp32'
-    achieved = n_kept * flop_exec / (kernel_ms * 1e-3) / 1e12
-
     result = {
         'metric': METRIC, 'value': value, 'unit': 'ray-samples/s', 'n_gpus': world, 'steps': args.steps,
         'warmup': args.warmup, 'ms_per_step': dt_max / args.steps * 1e3, 'higher_is_better': True,
-        'scaling': 'strong' if args.shard_frame else 'weak', 'vs_baseline': None, 'dtype': dtype, 'data': 'synthetic',
-        'config': {'workload': 'aninerf_s9p full 512x512 render (config 2), eval perturb=0; outputs held to the '
-                               'fp32 tolerance (1e-4, tests/test_gpu_render.py) in both render precisions',
-                   'render_precision': args.render_precision,
+        'scaling': 'strong' if args.shard_frame else 'weak', 'vs_baseline': None,
+        'dtype': 'fp32' if prec == 'fp32' else 'bf16 MFMA operands (hi/lo split, 3 products per MAC), fp32 accumulate',
+        'data': 'synthetic',
+        'config': {'workload': 'aninerf_s9p full 512x512 render (config 2: fp32, novel-view eval, perturb=0)',
+                   'render_precision': prec,
                    'rays_per_gpu': R, 'samples_per_ray': 64, 'chunk': 2048,
                    'kept_fraction': n_kept / (R_local * 64), 'alpha_ind_rows': m_rows,
+                   'timed_call': 'Renderer.render_device (outputs left in HBM); render_s below adds the D2H',
                    'parallelism': (f'frame-split{world} (whole 2048-ray chunks per rank, rgb/acc/depth '
                                    'all-gathered over RCCL)') if args.shard_frame else
                                   f'replicas{world} (one frame per GPU)'},
-        'roofline': {'bound': 'mfma', 'kernel': 'k_mlp_b16' if split else 'k_mlp', 'achieved': achieved,
-                     'peak': peak, 'unit': 'TFLOP/s', 'frac': achieved / peak, 'traffic': None,
-                     'kernel_ms': kernel_ms, 'flop_per_kept_executed': flop_exec,
-                     'flop_per_kept_credited': FLOP_PER_KEPT,
-                     'achieved_credited': n_kept * FLOP_PER_KEPT / (kernel_ms * 1e-3) / 1e12},
+        'roofline': render_roofline(prec, n_kept, kernel_ms),
     }
-    for prec, v in side.items():
-        result['fp32_exact' if prec == 'fp32' else 'bf16x3_split'] = v
-
-    pmc = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'profiles', 'pmc_latest.json')
-    if os.path.exists(pmc):
-        t = json.load(open(pmc))
-        if t.get('kernel', 'k_mlp') == result['roofline']['kernel']:
-            result['roofline']['traffic'] = t['bytes_per_launch']
-            result['roofline']['traffic_source'] = t['source'] + '; ' + t['correction']
+    if not args.no_exact:
+        other = 'bf16x3' if prec == 'fp32' else 'fp32'
+        o2, dt2, kms2, (nk2, _) = timed(other)
+        progress(f'{other}: {dt2 / args.steps * 1e3:.2f} ms/frame, kernel {kms2:.2f} ms')
+        result['bf16x3_split' if other == 'bf16x3' else 'fp32_exact'] = {
+            'value': R * 64 * args.steps * frames / dt2, 'ms_per_step': dt2 / args.steps * 1e3,
+            'render_precision': other,
+            'note': ('same frame, every MLP layer as hi/lo-split bf16 MFMA (outputs held to the same 1e-4 fp32 '
+                     'tolerance by tests/test_gpu_render.py)' if other == 'bf16x3' else 'exact fp32 MFMA'),
+            'roofline': render_roofline(other, nk2, kms2)}
+        del o2
+    if not args.shard_frame:
+        # the drop-in call as run.py:63-69 makes it: Renderer.render(batch) with the eval D2H of every
+        # output (tpose_renderer.py:154-155) inside the measured time
+        renderer = make_renderer(prec)
+        with torch.no_grad():
+            renderer.render(batch)
+            ts = []
+            for _ in range(3):
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                host = renderer.render(batch)
+                ts.append(time.perf_counter() - t0)
+        rs = float(np.median(ts))
+        progress(f'Renderer.render with D2H: {rs * 1e3:.2f} ms')
+        result['render_s'] = {'seconds': rs, 'value': R * 64 / rs, 'unit': 'ray-samples/s',
+                              'call': 'Renderer.render(batch): fused render + .cpu() of rgb/acc/depth/raw/pbw/tbw '
+                                      '(%.0f MB to the host)' % (sum(v.numel() * v.element_size()
+                                                                      for v in host.values()) / 1e6),
+                              'median_of': 3}
+        del host
     if rank == 0 and world == 1 and not args.no_cpu:
         result['cpu_baseline'], result['psnr_vs_fp32_oracle'] = cpu_baseline(sd, b, out, args.cpu_rays)
+        progress(f"cpu_baseline: {result['cpu_baseline']['value']:.4g} ray-samples/s, "
+                 f"{result['cpu_baseline']['cores']} threads")
+    if rank == 0 and world == 1 and not args.no_torch_baseline:
+        tg = torch_gpu_baseline(sd, b, dev, args.torch_rays)
+        progress(f"torch_gpu_baseline: {tg['value']:.4g} ray-samples/s")
+        result['torch_gpu_baseline'] = tg
+        result['vs_baseline'] = value / tg['value']
+        result['vs_baseline_denominator'] = ('BASELINE.md §3 GPU denominator: the reference op-for-op PyTorch-ROCm '
+                                             'restatement on this GPU, same frame (torch_gpu_baseline)')
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def dry_run(args, rank, world):
+    """ANR_BENCH_DRYRUN=1: the N-process contract without GPU work (CPU rehearsal of --gpus N):
+    gloo rendezvous, barriers around K empty steps, max over ranks, one JSON line from rank 0."""
+    if world > 1:
+        dist.init_process_group('gloo')
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        if world > 1:
+            dist.barrier()
+    dt = max_over_ranks(time.perf_counter() - t0, None, world)
+    if rank == 0:
+        print(json.dumps({'metric': METRIC, 'value': None, 'unit': 'ray-samples/s', 'n_gpus': world,
+                          'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': dt / max(1, args.steps) * 1e3,
+                          'dry_run': True, 'ranks_seen': world}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def torch_gpu_baseline(sd, b, dev, n_rays, reps=3):
+    """BASELINE.md §3's GPU denominator, outside the timed region: the op-for-op PyTorch restatement
+    of the reference (oracle/restate.py) with PyTorch-ROCm on this GPU, fp32, 2048-ray chunks, over
+    the first ``n_rays`` rays of the same frame: one untimed pass (MIOpen meets every chunk's Conv1d
+    size for the first time), then the median of ``reps`` warm passes."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from oracle import torch_gpu_baseline as tgb
+    r = tgb.measure(sd, b, dev, reps, n_rays)
+    r['sample'] = f'first {r["rays"]} rays ({r["rays"] // 2048} reference chunks) of the config-2 frame'
+    return r
 
 
 FLOP_PER_KEPT_TRAIN = 9_919_488  # SURVEY.md §8(d): 3 x 2 x (2 x 497,152 + 658,944)
@@ -359,7 +516,7 @@ def bench_sdf(args, rank, world, dev):
         import sys
         sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
         from oracle import restate_sdf
-        threads = min(16, os.cpu_count() or 1)
+        threads, host = host_threads()
         torch.set_num_threads(threads)
         n = min(args.sdf_cpu_rays, R)
         sub = {k: torch.from_numpy(np.ascontiguousarray(
@@ -459,7 +616,7 @@ def bench_mesh(args, rank, world, dev):
         import sys
         sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
         from oracle import restate
-        threads = min(16, os.cpu_count() or 1)
+        threads, host = host_threads()
         torch.set_num_threads(threads)
         m = min(16 * 2048 * 64, n)  # 16 reference chunks, ~10 s on 16 host threads
         P = {k: torch.from_numpy(v) for k, v in sd.items()}
@@ -532,7 +689,7 @@ def cpu_baseline(sd, b, out, n_rays):
     import sys
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from oracle import restate
-    threads = min(16, os.cpu_count() or 1)
+    threads, host = host_threads()
     torch.set_num_threads(threads)
     P = {k: torch.from_numpy(v) for k, v in sd.items()}
     n_rays = min(n_rays, b['ray_o'].shape[1])
@@ -550,7 +707,7 @@ def cpu_baseline(sd, b, out, n_rays):
     psnr = float(restate.psnr(rgb, ref['rgb_map'][0].numpy()))
     cpu = {'value': n_rays * 64 / dt, 'unit': 'ray-samples/s', 'cores': threads, 'kind': 'port',
            'sample': f'first {n_rays} rays ({n_rays // 2048} reference chunks) of the config-2 frame, '
-                     f'oracle/restate.py, torch CPU {threads} threads, {dt:.1f} s'}
+                     f'oracle/restate.py, torch CPU {threads} threads, {dt:.1f} s', 'host': host}
     return cpu, psnr
 
 

@@ -22,6 +22,12 @@
  *                             tpose_renderer.py:134-152 (msk_sdf / msk_label)
  *   anr_sdf_render_counts / anr_sdf_render_rows   the compact outputs 'resd', 'gradients',
  *                             'msk_sdf', 'msk_label' (sizes known only after the keep mask)
+ *   anr_network_fwd         lib/networks/bw_deform/tpose_nerf_network.py:139-215 Network.forward
+ *                             (wpts, viewdir, dists, batch), the per-chunk call of tpose_renderer.py:95
+ *   anr_network_train_fwd/bwd  the same call under autograd (forward + loss.backward() through it)
+ *   anr_blend_weights       tpose_nerf_network.py:55-77 calculate_neural_blend_weights and
+ *                             :304-315 BackwardBlendWeight.forward (novel_pose_bw)
+ *   anr_canonical_alpha     tpose_nerf_network.py:241-250 TPoseHuman.calculate_alpha
  *   anr_alpha_points        lib/networks/bw_deform/tpose_nerf_network.py:105-137 Network.get_alpha
  *                             over the batchify chunks of aninerf_mesh_renderer.py:14-23, 34-36
  *   anr_anim_step           lib/train/trainers/aninerf_animation_trainer.py:33-140 (forward + backward)
@@ -175,6 +181,52 @@ const int32_t* anr_render_counts(const void* workspace, int n_rays);
 /* Gather the m alpha_ind rows of pbw / tbw (each (m,24)) after the counts were read. */
 int anr_render_bw_rows(const void* workspace, int n_rays, float* pbw, float* tbw, void* stream);
 
+/* ---- Network.forward over free samples (tpose_nerf_network.py:139-215) ----------------------
+ * The call a reference renderer makes per chunk, self.net(wpts, viewdir, dists, batch)
+ * (tpose_renderer.py:95): n_pts samples given by world points wpts (n,3), view directions viewdir
+ * (n,3) and interval lengths dists (n). The prefilter's forced argmin and the alpha_ind argmax run
+ * over the whole call, as the reference's pnorm.argmin(dim=1) / argmax(alpha, dim=1) do (one call =
+ * one reference chunk); o->chunk and o->t_rand are ignored. raw (n,4) is zero at dropped samples
+ * (raw_full). anr_network_counts: device int32 {kept n', alpha_ind rows m} in the workspace;
+ * anr_network_bw_rows: the m rows of pbw / tbw (each (m,24)) after the counts were read; both work on
+ * either workspace below.
+ *  anr_network_fwd: the fused network kernel (o->precision ANR_FP32 or ANR_BF16X3), no host sync.
+ *  anr_network_train_fwd / _bwd: the layer-wise training executor (o->precision as for training),
+ *    activations kept in the workspace until the backward; one host read of n' in each. _bwd
+ *    ACCUMULATES the parameter gradients (anr_params order) from the upstream d raw (n,4) and d pbw /
+ *    d tbw rows (m,24); any of the three may be NULL (zero). */
+typedef struct anr_samples {
+  const float* wpts;     /* (n,3) device, world frame */
+  const float* viewdir;  /* (n,3) device */
+  const float* dists;    /* (n) device */
+  int n_pts;
+} anr_samples;
+size_t anr_network_workspace_bytes(int n_pts, const anr_render_opts* o, const anr_frame* f);
+int anr_network_fwd(const anr_params* p, const anr_frame* f, const anr_samples* x, const anr_render_opts* o, float* raw,
+                    void* workspace, size_t ws_bytes, void* stream);
+const int32_t* anr_network_counts(const void* workspace, int n_pts);
+int anr_network_bw_rows(const void* workspace, int n_pts, float* pbw, float* tbw, void* stream);
+size_t anr_network_train_workspace_bytes(int n_pts, const anr_render_opts* o, const anr_frame* f);
+int anr_network_train_fwd(const anr_params* p, const anr_frame* f, const anr_samples* x, const anr_render_opts* o,
+                          float* raw, void* workspace, size_t ws_bytes, void* stream);
+int anr_network_train_bwd(const anr_params* p, float* const* grads, const anr_frame* f, const anr_samples* x,
+                          const anr_render_opts* o, const float* d_raw, const float* d_pbw, const float* d_tbw,
+                          void* workspace, size_t ws_bytes, void* stream);
+
+/* ---- network helpers the reference's other trainers / renderers call --------------------------
+ * anr_blend_weights: field 0 = calculate_neural_blend_weights(pts, smpl_bw, latent_index)
+ *   (tpose_nerf_network.py:55-77; bw_latent, bw_linears, bw_fc), field 1 = novel_pose_bw(pts, smpl_bw,
+ *   latent_index) (BackwardBlendWeight.forward :304-315): pts (n,3), smpl_bw (24,n) (the reference's
+ *   (1,24,n)) -> bw (24,n) = softmax(log(smpl_bw + 1e-9) + MLP([gamma(pts), latent row])), latent row =
+ *   latent_row[0] + row_add (latent_row: device int64, the caller's index tensor).
+ * anr_canonical_alpha: TPoseHuman.calculate_alpha(nf_pts) (:241-250): raw alpha (n) of canonical points.
+ * Forward only, exact fp32 MFMA layer GEMMs, no host sync. */
+size_t anr_points_workspace_bytes(int n);
+int anr_blend_weights(const anr_params* p, int field, const float* pts, const float* smpl_bw, int n,
+                      const int64_t* latent_row, int row_add, float* bw, void* workspace, size_t ws_bytes, void* stream);
+int anr_canonical_alpha(const anr_params* p, const float* pts, int n, float* alpha, void* workspace, size_t ws_bytes,
+                        void* stream);
+
 /* ---- training (A16/A17; lib/train/trainers/tpose_trainer.py:21-73, trainer.py:50-68) ------
  * anr_train_fwd: the render forward of the training step (perturb via o->t_rand), keeping every
  *   activation in the workspace; same outputs as anr_render_fwd (+ anr_render_counts /
@@ -197,6 +249,18 @@ int anr_train_step(const anr_params* p, float* const* grads, const anr_frame* f,
                    const float* ray_d, const float* near_, const float* far_, int n_rays,
                    const anr_render_opts* o, const float* rgb_gt, const uint8_t* mask_at_box,
                    const anr_render_out* out, float* loss3, void* workspace, size_t ws_bytes, void* stream);
+/* anr_train_step_hooked: anr_train_step plus events for overlapping the gradient all-reduce with
+ * the backward (DDP's reverse-order buckets): nerf_grads_ready (a hipEvent_t or
+ * NULL) is recorded on the stream once the gradients of tensors 0..26 (tpose_human.*, the canonical
+ * NeRF) are final; the blend-weight backward (tensors 27..45) follows on the stream. */
+typedef struct anr_train_hooks {
+  void* nerf_grads_ready;
+} anr_train_hooks;
+int anr_train_step_hooked(const anr_params* p, float* const* grads, const anr_frame* f, const float* ray_o,
+                          const float* ray_d, const float* near_, const float* far_, int n_rays,
+                          const anr_render_opts* o, const float* rgb_gt, const uint8_t* mask_at_box,
+                          const anr_render_out* out, float* loss3, const anr_train_hooks* hooks, void* workspace,
+                          size_t ws_bytes, void* stream);
 int anr_adam(float* param, float* grad, float* exp_avg, float* exp_avg_sq, long n, float lr, float beta1,
              float beta2, float eps, float weight_decay, int step, float clip_value, void* stream);
 

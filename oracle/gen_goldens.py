@@ -10,7 +10,8 @@ Recipe:
   4. cwd = /root/reference (relative parent_cfg / network_path).
 Goldens use ``torch.set_num_threads(1)``.
 
-Run:  python oracle/gen_goldens.py            (writes tests/golden/)
+Run:  python oracle/gen_goldens.py            (writes tests/golden/; --novel, --sdf, --rays, --train-rays,
+      --mmsk, --mesh, --anim, --state-dicts for the other fixtures)
 """
 import os
 import sys
@@ -695,8 +696,132 @@ def main_anim():
     print('anim golden written: loss', out['loss'], 'rows path 1', out['m0'])
 
 
+SDF_TRAIN_KEEP = ['tpose_human.sdf_network.lin0.weight_v', 'tpose_human.sdf_network.lin3.weight_v',
+                  'tpose_human.sdf_network.lin8.weight_v', 'tpose_human.beta_network.beta',
+                  'tpose_human.color_network.color_latent.weight', 'tpose_human.color_network.lin0.weight_v',
+                  'tpose_human.color_network.lin4.weight_v', 'resd_linears.0.weight', 'resd_linears.5.weight',
+                  'resd_fc.weight', 'resd_fc.bias']
+
+
+def main_sdf_train():
+    """G13s: one training step of the sdf_pdf variant (config 5) through the reference's own wrapper
+    (tpose_trainer.NetworkWrapper over anisdf_pdf_network.Network + tpose_renderer, perturb 1, the
+    torch.rand draws recorded, iter_step past the first mask-alpha milestone) with the KNN stub:
+    loss and every scalar stat, the gradients of every bias / weight_g / small tensor and of the
+    SDF_TRAIN_KEEP weights, the observed-gradient row count."""
+    import torch
+    from collections import namedtuple
+    torch.set_num_threads(1)
+    sys.path.insert(0, REPO)
+    from oracle.restate_sdf import knn_points as knn_restated
+    from animatable_nerf_amd.synthetic import PdfScene, init_state_dict_sdf
+    KNN = namedtuple('KNN', ['dists', 'idx', 'knn'])
+
+    def knn_stub(src, ref, K=1, **kw):
+        d, i = knn_restated(src, ref, K)
+        return KNN(d, i, None)
+
+    cfg, make_network, make_renderer = import_reference('configs/sdf_pdf/anisdf_pdf_s9p.yaml',
+                                                        opts=('init_sdf', "''"), knn=knn_stub)
+    from lib.utils.if_nerf import if_nerf_data_utils as dutils
+    from lib.train.trainers.tpose_trainer import NetworkWrapper
+    net = make_network(cfg)
+    shapes = {k: tuple(v.shape) for k, v in net.state_dict().items()}
+    sd = init_state_dict_sdf(shapes)
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
+    cfg.perturb = 1
+    net.train()
+    wrapper = NetworkWrapper(net)
+    scene = PdfScene(vsize=0.05)
+    ro, rd = scene.box_rays(SDF_TRAIN_RAYS, seed=21)
+    near, far, mask = dutils.get_near_far(scene.pbounds, ro, rd)
+    trng = np.random.Generator(np.random.PCG64(13))
+    R = int(mask.sum())
+    rgb = trng.random((R, 3)).astype(np.float32)
+    b = scene.batch_arrays(ro[mask], rd[mask], near.astype(np.float32), far.astype(np.float32), latent_index=7,
+                           rgb=rgb)
+    b['mask_at_box'] = (trng.random((1, R)) < 0.9)
+    batch = {k: torch.from_numpy(np.array(v, copy=True)) for k, v in b.items()}  # the golden keeps the inputs
+    batch['iter_step'] = SDF_TRAIN_ITER
+    t_rand = torch.from_numpy(trng.random((R, 64)).astype(np.float32))
+    orig_rand = torch.rand
+    pos = [0]
+
+    def fake_rand(shape, *a, **k):
+        n = shape[1]
+        out = t_rand[pos[0]:pos[0] + n][None].clone()
+        pos[0] += n
+        return out
+
+    torch.rand = fake_rand
+    ret, loss, stats, _ = wrapper(batch)
+    net.zero_grad()
+    loss.backward()
+    torch.rand = orig_rand
+    grads = {k: v.grad.detach().clone().numpy() for k, v in net.named_parameters() if v.grad is not None}
+    keep = {k: g for k, g in grads.items() if g.size <= 4096 or k in SDF_TRAIN_KEEP}
+    n_obs = int(ret['observed_gradients'].shape[1]) if 'observed_gradients' in ret else 0
+    out = dict(b, t_rand=t_rand.numpy(), iter_step=SDF_TRAIN_ITER, loss=loss.detach().numpy(),
+               n_observed=n_obs, n_kept=int(ret['resd'].shape[1]), msk_len=int(ret['msk_sdf'].shape[1]),
+               grad_keys=np.array(sorted(grads)), tbounds_after=batch['tbounds'].numpy(),
+               **{'stat_' + k: v.detach().numpy() for k, v in stats.items()},
+               **{'grad_' + k: v for k, v in keep.items()})
+    np.savez_compressed(os.path.join(OUT, 'g13_sdf_train.npz'), **out)
+    print('sdf train golden written: loss', float(loss), {k: float(v) for k, v in stats.items()}, 'kept',
+          out['n_kept'], 'observed', n_obs, 'grads kept', len(keep), 'of', len(grads))
+
+
+SDF_TRAIN_RAYS = 96
+SDF_TRAIN_ITER = 12000
+
+
+STATE_DICT_CONFIGS = {
+    # name: (cfg_file, opts) -- the configs BASELINE.json names (s9p, 313, sdf_pdf) + the animation stage
+    's9p': ('configs/aninerf_s9p.yaml', ()),
+    '313': ('configs/aninerf_313.yaml', ()),
+    's9p_animation': ('configs/aninerf_s9p.yaml', ('aninerf_animation', 'True')),
+    'sdf_pdf_s9p': ('configs/sdf_pdf/anisdf_pdf_s9p.yaml', ('init_sdf', "''")),
+}
+
+
+def state_dict_one(name):
+    """the reference Network's state_dict names / shapes (make_network(cfg)) for one config, and the
+    cfg values the plugins size themselves from -> one JSON line on stdout"""
+    import json
+    cfg_file, opts = STATE_DICT_CONFIGS[name]
+    cfg, make_network, _ = import_reference(cfg_file, opts=opts)
+    net = make_network(cfg)
+    print(json.dumps({'config': name, 'cfg_file': cfg_file, 'opts': list(opts),
+                      'num_train_frame': int(cfg.num_train_frame), 'num_eval_frame': int(cfg.num_eval_frame),
+                      'num_latent_code': int(cfg.num_latent_code), 'perturb': cfg.perturb,
+                      'network_module': cfg.network_module,
+                      'state_dict': [[k, list(v.shape)] for k, v in net.state_dict().items()]}))
+
+
+def main_state_dicts():
+    """G13: tests/golden/g13_state_dicts.json (one subprocess per config: lib.config parses argv
+    once, at import)."""
+    import json
+    import subprocess
+    out = {}
+    for name in STATE_DICT_CONFIGS:
+        r = subprocess.run([sys.executable, os.path.abspath(__file__), '--state-dict-one', name],
+                           capture_output=True, text=True, check=True)
+        line = [l for l in r.stdout.splitlines() if l.startswith('{')][-1]
+        out[name] = json.loads(line)
+    with open(os.path.join(OUT, 'g13_state_dicts.json'), 'w') as f:
+        json.dump(out, f, indent=0)
+    print('state_dict golden written:', {k: len(v['state_dict']) for k, v in out.items()})
+
+
 if __name__ == '__main__':
-    if len(sys.argv) > 1 and sys.argv[1] == '--anim':
+    if len(sys.argv) > 2 and sys.argv[1] == '--state-dict-one':
+        state_dict_one(sys.argv[2])
+    elif len(sys.argv) > 1 and sys.argv[1] == '--state-dicts':
+        main_state_dicts()
+    elif len(sys.argv) > 1 and sys.argv[1] == '--sdf-train':
+        main_sdf_train()
+    elif len(sys.argv) > 1 and sys.argv[1] == '--anim':
         main_anim()
     elif len(sys.argv) > 1 and sys.argv[1] == '--mesh':
         main_mesh()

@@ -273,3 +273,164 @@ def render(P, batch, t_rand=None, n_samples=64, chunk=CHUNK, trace=None):
                                  batch['occupancy'][:, i:i + chunk], batch, t_rand=tr, n_samples=n_samples,
                                  trace=trace))
     return {k: torch.cat([o[k] for o in outs], dim=1) for k in outs[0]}
+
+
+# --------------------------------------------------------------------------------------------
+# Training (config 5's 8-GPU leg): tpose_trainer.NetworkWrapper over the sdf_pdf
+# network -- Network.forward in training mode (anisdf_pdf_network.py:156-224: create_graph input
+# gradients, observed_gradients :140-154 / :194-199), the renderer's msk_sdf lists
+# (tpose_renderer.py:134-152) and the loss terms of tpose_trainer.py:21-73 + crit.sdf_mask_crit
+# (crit.py:5-19). Differentiable w.r.t. every tensor of P (autograd, second order where the
+# reference's is).
+# --------------------------------------------------------------------------------------------
+def tpose_human_train(P, wpts, viewdir, batch):
+    """TPoseHuman.forward :288-345 under autograd: gradients with create_graph (the eikonal loss and
+    the colour net's normals differentiate through them); the colour net sees detached points."""
+    if not wpts.requires_grad:
+        wpts = wpts.requires_grad_()
+    with torch.enable_grad():
+        out = sdf_network(P, wpts)
+        sdf = out[:, :1]
+    feature = out[:, 1:]
+    gradients = torch.autograd.grad(sdf, wpts, torch.ones_like(sdf), create_graph=True, retain_graph=True,
+                                    only_inputs=True)[0]
+    wpts = wpts.detach()
+    beta = P['tpose_human.beta_network.beta'].clamp(1e-9, 1e6)
+    alpha = sdf_to_alpha(sdf, beta)
+    alpha = 1. - torch.exp(-F.relu(alpha[:, 0]) * 0.005)
+    rgb = color_network(P, wpts, gradients, viewdir, feature, batch['latent_index'])
+    raw = torch.cat((rgb, alpha[:, None]), dim=1)
+    return {'raw': raw, 'sdf': sdf, 'gradients': gradients}
+
+
+def gradient_of_deformed_sdf(P, x, batch):
+    """Network.gradient_of_deformed_sdf :140-154: d sdf(x + resd(x)) / d x, create_graph."""
+    x = x.requires_grad_(True)
+    with torch.enable_grad():
+        resd = residual_deformation(P, x, batch['poses'])
+        tpose = (x + resd)[0]
+        y = sdf_network(P, tpose)[:, :1]
+    g = torch.autograd.grad(y, x, torch.ones_like(y), create_graph=True, retain_graph=True, only_inputs=True)[0]
+    return g, y[None]
+
+
+def network_forward_train(P, wpts, viewdir, dists, batch, norm_th=0.1):
+    """Network.forward :156-224 with grad enabled -> raw, sdf (full), resd, gradients
+    (+ observed_gradients when a kept sample has |sdf| < 0.02). Widens batch['tbounds'] in place."""
+    wpts = wpts[None]
+    pose_pts = restate.world_to_pose(wpts, batch['R'], batch['Th'])
+    viewdir = viewdir[None]
+    pose_dirs = world_dirs_to_pose_dirs(viewdir, batch['R'])
+    with torch.no_grad():
+        pbw, pnorm = sample_blend_closest_points(pose_pts, batch['pvertices'], batch['weights'])
+        pnorm = pnorm[..., 0]
+        pind = pnorm < norm_th
+        pind[torch.arange(len(pnorm)), pnorm.argmin(dim=1)] = True
+        pose_pts = pose_pts[pind][None]
+        viewdir = viewdir[pind][None]
+        pose_dirs = pose_dirs[pind][None]
+    pbw, _ = sample_blend_closest_points(pose_pts, batch['pvertices'], batch['weights'])
+    pbw = pbw.permute(0, 2, 1)
+    init_tpose = restate.lbs_to_tpose(pose_pts, pbw, batch['A'])
+    init_bigpose = tpose_points_to_pose_points(init_tpose, pbw, batch['big_A'])
+    resd = residual_deformation(P, init_bigpose, batch['poses'])
+    tpose = init_bigpose + resd
+    init_tdirs = pose_dirs_to_tpose_dirs(pose_dirs, pbw, batch['A'])
+    tpose_dirs = tpose_dirs_to_pose_dirs(init_tdirs, pbw, batch['big_A'])
+    tpose = tpose[0]
+    ret = tpose_human_train(P, tpose, tpose_dirs[0], batch)
+    ind = ret['sdf'][:, 0].detach().abs() < 0.02
+    init_bigpose = init_bigpose[0][ind][None].detach().clone()
+    if ret['raw'].requires_grad and ind.sum() != 0:
+        og, _ = gradient_of_deformed_sdf(P, init_bigpose, batch)
+        ret['observed_gradients'] = og
+    tbounds = batch['tbounds'][0]
+    tbounds[0] -= 0.05
+    tbounds[1] += 0.05
+    inside = tpose > tbounds[:1]
+    inside = inside * (tpose < tbounds[1:])
+    outside = torch.sum(inside, dim=1) != 3
+    ret['raw'][outside] = 0
+    n_batch, n_point = wpts.shape[:2]
+    raw = torch.zeros([n_batch, n_point, 4]).to(wpts)
+    raw[pind] = ret['raw']
+    sdf = 10 * torch.ones([n_batch, n_point, 1]).to(wpts)
+    sdf[pind] = ret['sdf']
+    ret.update({'raw': raw, 'sdf': sdf, 'resd': resd, 'gradients': ret['gradients'][None]})
+    return ret
+
+
+def render_chunk_train(P, ray_o, ray_d, near, far, occ, batch, t_rand=None, n_samples=64):
+    """get_pixel_value (tpose_renderer.py:71-157) over network_forward_train."""
+    pts, z = restate.sample_points(ray_o, ray_d, near, far, n_samples, t_rand)
+    nb, npix, ns = pts.shape[:3]
+    wpts = pts.view(nb * npix * ns, -1)
+    vd = ray_d[:, :, None].repeat(1, 1, ns, 1).contiguous().view(nb * npix * ns, -1)
+    dists = z[..., 1:] - z[..., :-1]
+    dists = torch.cat([dists, dists[..., -1:]], dim=2).view(nb * npix * ns)
+    ret = network_forward_train(P, wpts, vd, dists, batch)
+    raw = ret['raw'].reshape(-1, ns, 4)
+    zf = z.view(-1, ns)
+    rgb_map, acc, depth, w = restate.raw2outputs(raw, zf)
+    out = {k: v for k, v in ret.items() if k in ('resd', 'gradients', 'observed_gradients')}
+    out.update({'raw': raw.view(nb, -1, 4), 'sdf': ret['sdf'], 'rgb_map': rgb_map.view(nb, npix, -1),
+                'acc_map': acc.view(nb, npix), 'depth_map': depth.view(nb, npix)})
+    sdf = ret['sdf'].view(nb, npix, ns)
+    min_sdf = sdf.min(dim=2)[0]
+    free_sdf = min_sdf[occ == 0]
+    free_label = torch.zeros_like(free_sdf)
+    with torch.no_grad():
+        imask, _ = get_intersection_mask(sdf, zf.view(nb, npix, ns))
+    ind = (imask == False) * (occ == 1)  # noqa: E712
+    s = min_sdf[ind]
+    out['msk_sdf'] = torch.cat([s, free_sdf]).view(nb, -1)
+    out['msk_label'] = torch.cat([torch.ones_like(s), free_label]).view(nb, -1)
+    return out
+
+
+def render_train(P, batch, t_rand=None, n_samples=64, chunk=CHUNK):
+    """Renderer.render under autograd (mutates batch['tbounds'])."""
+    R = batch['ray_o'].shape[1]
+    outs = []
+    for i in range(0, R, chunk):
+        tr = None if t_rand is None else t_rand[None, i:i + chunk]
+        outs.append(render_chunk_train(P, batch['ray_o'][:, i:i + chunk], batch['ray_d'][:, i:i + chunk],
+                                       batch['near'][:, i:i + chunk], batch['far'][:, i:i + chunk],
+                                       batch['occupancy'][:, i:i + chunk], batch, t_rand=tr, n_samples=n_samples))
+    keys = outs[0].keys()
+    return {k: torch.cat([o[k] for o in outs], dim=1) for k in keys}
+
+
+def mask_alpha(iter_step):
+    """crit.sdf_mask_crit's schedule (crit.py:9-14): 50, doubled past each milestone."""
+    alpha = 50
+    for m in (10000, 20000, 30000, 40000, 50000):
+        if iter_step > m:
+            alpha = alpha * 2
+    return alpha
+
+
+def loss_terms(ret, batch):
+    """tpose_trainer.NetworkWrapper.forward :21-73 for the sdf_pdf keys -> (loss, scalar_stats)."""
+    stats = {}
+    loss = 0
+    offset_loss = torch.norm(ret['resd'], dim=2).mean()
+    stats['offset_loss'] = offset_loss
+    loss += 0.01 * offset_loss
+    grad_loss = ((torch.norm(ret['gradients'], dim=2) - 1.0) ** 2).mean()
+    stats['grad_loss'] = grad_loss
+    loss += 0.01 * grad_loss
+    if 'observed_gradients' in ret:
+        ograd_loss = ((torch.norm(ret['observed_gradients'], dim=2) - 1.0) ** 2).mean()
+        stats['ograd_loss'] = ograd_loss
+        loss += 0.01 * ograd_loss
+    alpha = mask_alpha(int(batch['iter_step']))
+    mask_loss = F.binary_cross_entropy_with_logits(-alpha * ret['msk_sdf'], ret['msk_label']) / alpha
+    stats['mask_loss'] = mask_loss
+    loss += mask_loss
+    mask = batch['mask_at_box']
+    img_loss = torch.mean((ret['rgb_map'][mask] - batch['rgb'][mask]) ** 2)
+    stats['img_loss'] = img_loss
+    loss += img_loss
+    stats['loss'] = loss
+    return loss, stats

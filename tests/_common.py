@@ -14,43 +14,23 @@ def golden(name):
     return np.load(os.path.join(GOLDEN, name + '.npz'))
 
 
-# CPU the goldens were generated on (oracle/gen_goldens.py, 1 thread): PyTorch's CPU kernels (MKL
-# GEMM, vectorised reductions, transcendentals) dispatch on the vendor and the ISA level, and only
-# with the same dispatch does the oracle reproduce the reference's fp32 bits.
-GOLDEN_HOST = ('GenuineIntel', 'AVX512')
-
-
-def host_fingerprint():
-    vendor = ''
-    try:
-        with open('/proc/cpuinfo') as f:
-            for line in f:
-                if line.startswith('vendor_id'):
-                    vendor = line.split(':', 1)[1].strip()
-                    break
-    except OSError:
-        pass
-    return vendor, torch.backends.cpu.get_cpu_capability()
-
-
 def golden_strict():
-    """Bit-exact oracle-vs-golden checks: on the generating host's CPU dispatch, or when forced
-    (ANR_GOLDEN_STRICT=1); ANR_GOLDEN_STRICT=0 forces the roundoff bar."""
-    env = os.environ.get('ANR_GOLDEN_STRICT')
-    if env is not None:
-        return env == '1'
-    return host_fingerprint() == GOLDEN_HOST
+    """Bit-exact oracle-vs-golden checks are opt-in (ANR_GOLDEN_STRICT=1): the oracle reproduces the
+    reference's fp32 bits only on a CPU whose PyTorch kernels (MKL GEMM, vectorised reductions,
+    transcendentals) dispatch exactly as on the host that generated the goldens, and vendor / ISA do
+    not identify that dispatch (an MKL or torch version, an AMX part can change it). Run strict on the
+    generating host to re-pin the oracle bit for bit."""
+    return os.environ.get('ANR_GOLDEN_STRICT') == '1'
 
 
 def assert_golden_equal(got, ref, err_msg='', rtol=3e-5, atol=1e-6):
     """Oracle-vs-golden check.
 
     * Bool / integer arrays (masks, indices, labels): bit-exact everywhere.
-    * Float arrays: bit-exact on the goldens' host dispatch (``golden_strict``). On a host with
-      another CPU dispatch (an AMD EPYC's MKL path, another ISA level) the same ops reorder fp32
-      sums, so there the bar is fp32 roundoff PER ELEMENT: |got - ref| <= atol + rtol * |ref|
-      (rtol 3e-5, three times tighter than the GPU north_star tolerance; the largest cross-host
-      mismatch seen, sdf_pdf `resd`, was 1.02e-5 of its array's max)."""
+    * Float arrays: bit-exact under ANR_GOLDEN_STRICT=1 (``golden_strict``); otherwise within fp32
+      roundoff of a reordered sum: |got - ref| <= max(atol, rtol * max|ref|) + rtol * |ref| (rtol 3e-5,
+      three times tighter than the GPU north_star tolerance; the scale term keeps small elements of a
+      wide-range array from failing on cancellation noise of its large ones)."""
     got = np.asarray(got.detach().numpy() if hasattr(got, 'detach') else got)
     ref = np.asarray(ref)
     assert got.shape == ref.shape, (err_msg, got.shape, ref.shape)
@@ -60,8 +40,9 @@ def assert_golden_equal(got, ref, err_msg='', rtol=3e-5, atol=1e-6):
     if golden_strict():
         n = int(np.sum(got != ref))
         raise AssertionError(f'{err_msg}: {n} of {ref.size} elements differ from the golden bits '
-                             f'(host {host_fingerprint()} = golden host; ANR_GOLDEN_STRICT=0 relaxes)')
-    np.testing.assert_allclose(got, ref, rtol=rtol, atol=atol, err_msg=err_msg)
+                             '(ANR_GOLDEN_STRICT=1)')
+    scale = float(np.max(np.abs(ref))) if ref.size else 0.0
+    np.testing.assert_allclose(got, ref, rtol=rtol, atol=max(atol, rtol * scale), err_msg=err_msg)
 
 
 @functools.lru_cache(maxsize=4)

@@ -196,3 +196,98 @@ def test_gloo_fused_step_replicas_start_from_rank0():
         assert p.exitcode == 0
     for rank, ok in res:
         assert ok is True, (rank, ok)
+
+
+class _FakeSdfRenderer:
+    """Stand-in for renderer_sdf.Renderer's chunk semantics: every chunk first widens tbounds in place
+    (anisdf_pdf_network.py:204-206), and its rays' outputs depend on the widened bounds. A shard must
+    therefore start from the bounds widened chunk_offset times (the real kernel: test_gpu_sdf.py)."""
+    widens_tbounds = True
+
+    def render_device(self, b, bw_rows=True, chunk_offset=0):
+        from animatable_nerf_amd.renderer_sdf import widen_tbounds
+        n = b['ray_o'].shape[1]
+        tb = widen_tbounds(b['tbounds'], chunk_offset)
+        rgb = torch.empty((1, n, 3))
+        for c0 in range(0, n, 2048):
+            tb = widen_tbounds(tb, 1)
+            rgb[:, c0:c0 + 2048] = torch.sigmoid(b['ray_o'][:, c0:c0 + 2048] * tb[0, 1] + tb[0, 0])
+        b['tbounds'].copy_(tb)
+        return {'rgb_map': rgb, 'acc_map': rgb.sum(-1), 'depth_map': b['near'] * 2.0, 'raw': torch.zeros((1, n * 64, 4))}
+
+
+def _sdf_shard_worker(rank, world, port, n, q):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    try:
+        parallel.init_from_env('gloo')
+        b = _frame(n)
+        b['tbounds'] = torch.tensor([[[-0.3, -0.9, -0.2], [0.3, 0.9, 0.2]]])
+        full_b = {k: v.clone() for k, v in b.items()}
+        full = _FakeSdfRenderer().render_device(full_b)
+        ret = parallel.render_sharded(_FakeSdfRenderer(), b)
+        ok = all(torch.equal(ret[k], full[k]) for k in ('rgb_map', 'acc_map', 'depth_map'))
+        ok = ok and torch.equal(b['tbounds'], full_b['tbounds'])
+        q.put((rank, bool(ok)))
+    except Exception as ex:  # pragma: no cover
+        q.put((rank, repr(ex)))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('world', [3, 4])
+def test_gloo_sharded_sdf_frame_keeps_tbounds_widening(world):
+    """sdf_pdf frame split over ranks: each shard starts from tbounds widened once per preceding
+    reference chunk, so the gathered outputs equal the single-GPU frame bit for bit, and every rank
+    leaves batch['tbounds'] widened once per chunk of the whole frame."""
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sdf_shard_worker, args=(r, world, port, 9000, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, ok in res:
+        assert ok is True, (rank, ok)
+
+
+def _bucket_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    try:
+        parallel.init_from_env('gloo')
+        n = 1000
+        blobs = [torch.arange(n + 4, dtype=torch.float32) * (r + 1) + r for r in range(world)]
+        g = blobs[rank].clone()
+        buckets = parallel.GradBuckets(g, [(0, 600), (600, n + 4)])
+        buckets.reduce(0)
+        buckets.reduce(1)
+        buckets.wait()
+        expect = sum(blobs) / world
+        q.put((rank, bool(torch.allclose(g, expect, rtol=0, atol=1e-5))))
+    except Exception as ex:  # pragma: no cover
+        q.put((rank, repr(ex)))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_gloo_grad_buckets_mean_with_loss_tail():
+    """FusedStep's reducer: the flat blob (gradients + the loss statistics in its last 4 floats) in two
+    buckets, reduced one after the other, equals the mean over ranks everywhere."""
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bucket_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, ok in res:
+        assert ok is True, (rank, ok)

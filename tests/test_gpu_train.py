@@ -242,9 +242,10 @@ def _ddp_worker(rank, world, port, q):
         torch.cuda.synchronize()
         got = [torch.empty_like(step.flat) for _ in range(world)]
         dist.all_gather(got, step.flat)
-        q.put((rank, bool(torch.equal(got[0], got[1])), bool(torch.isfinite(step.flat).all())))
+        q.put((rank, bool(torch.equal(got[0], got[1])), bool(torch.isfinite(step.flat).all()),
+               step.loss3.cpu().tolist()))
     except Exception as ex:  # pragma: no cover
-        q.put((rank, repr(ex), False))
+        q.put((rank, repr(ex), False, None))
     finally:
         if dist.is_initialized():
             dist.destroy_process_group()
@@ -252,7 +253,9 @@ def _ddp_worker(rank, world, port, q):
 
 def test_fused_step_two_ranks_stay_identical(dev):
     """World 2 over gloo on the one GPU: ranks built from different weights, each stepping its own
-    batch, hold identical blobs after one step (rank 0's start broadcast, mean gradient, same Adam)."""
+    batch, hold identical blobs after one step (rank 0's start broadcast, mean gradient reduced in two
+    buckets from the side stream, the first one overlapped with the blend-weight backward, same Adam)
+    and identical, rank-averaged loss statistics."""
     import socket
     import torch.multiprocessing as mp
     with socket.socket() as s:
@@ -267,5 +270,7 @@ def test_fused_step_two_ranks_stay_identical(dev):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for rank, same, finite in res:
+    for rank, same, finite, _ in res:
         assert same is True and finite, (rank, same)
+    # the loss statistics ride in the gradient blob's tail: every rank reports the mean over ranks
+    assert res[0][3] == res[1][3]

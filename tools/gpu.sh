@@ -1,0 +1,83 @@
+#!/bin/bash
+# One parameterised GPU-box driver (run through gpurun from the repo root):
+#   tools/gpu.sh TAG step [step ...]
+# steps (each under its own time limit; the script stops at the first failure):
+#   tests[=PATTERN]   pytest -m gpu (optionally -k PATTERN)           -> gpurun_out/TAG_gpu_tests.log
+#   smoke             __graft_entry__.smoke()                          -> TAG_smoke.log
+#   bench[:ARGS]      python bench.py ARGS (ARGS comma-separated)      -> TAG_bench[_MODE].log
+#   prof[:ARGS]       rocprofv3 --kernel-trace --stats of bench ARGS  -> TAG_prof[_MODE]/
+#   pmc:KERNEL[:ARGS] FETCH_SIZE and WRITE_SIZE passes of bench ARGS, summarised for KERNEL into
+#                     profiles/pmc_latest.json (tools/pmc_traffic.py)  -> TAG_pmc_KERNEL_{f,w}/
+#   sq:KERNEL[:ARGS]  two SQ counter passes (MFMA busy, waits, instruction mix) -> TAG_sq_KERNEL{1,2}/
+#   py:SCRIPT[:ARGS]  python SCRIPT ARGS                               -> TAG_py_NAME.log
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
+TAG=$1
+shift
+mkdir -p gpurun_out
+args_of() { echo "$1" | tr ',' ' '; }
+mode_of() { echo "$1" | sed -n 's/.*--mode,\([a-z]*\).*/_\1/p'; }
+for step in "$@"; do
+  kind=${step%%:*}
+  rest=${step#*:}
+  [ "$rest" = "$step" ] && rest=""
+  case $kind in
+    tests|tests=*)
+      pat=${step#tests=}
+      [ "$pat" = "$step" ] && pat=""
+      sel=()
+      [ -n "$pat" ] && sel=(-k "$pat")
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 180 --timeout-method thread "${sel[@]}" \
+        > gpurun_out/${TAG}_gpu_tests.log 2>&1 || { tail -40 gpurun_out/${TAG}_gpu_tests.log; exit 1; }
+      tail -1 gpurun_out/${TAG}_gpu_tests.log ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1 \
+        || { tail -20 gpurun_out/${TAG}_smoke.log; exit 1; }
+      tail -2 gpurun_out/${TAG}_smoke.log ;;
+    bench)
+      log=gpurun_out/${TAG}_bench$(mode_of "$rest").log
+      timeout -k 10 600 python bench.py $(args_of "$rest") > $log 2>&1 || { tail -20 $log; exit 1; }
+      tail -n 1 $log | cut -c1-600 ;;
+    prof)
+      m=$(mode_of "$rest")
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof$m -o run --output-format csv -- \
+        python bench.py --no-cpu --no-torch-baseline $(args_of "$rest") > gpurun_out/${TAG}_prof$m.log 2>&1 \
+        || { tail -20 gpurun_out/${TAG}_prof$m.log; exit 1; }
+      echo "PROF_OK $m" ;;
+    pmc)
+      k=${rest%%:*}
+      a=${rest#*:}
+      [ "$a" = "$rest" ] && a=""
+      B="python bench.py --steps 1 --warmup 0 --no-cpu --no-exact --no-torch-baseline $(args_of "$a")"
+      timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$k" -d gpurun_out/${TAG}_pmc_${k}_f -o f \
+        --output-format csv -- $B > gpurun_out/${TAG}_pmc_${k}_f.log 2>&1 || { tail -20 gpurun_out/${TAG}_pmc_${k}_f.log; exit 1; }
+      timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$k" -d gpurun_out/${TAG}_pmc_${k}_w -o w \
+        --output-format csv -- $B > gpurun_out/${TAG}_pmc_${k}_w.log 2>&1 || { tail -20 gpurun_out/${TAG}_pmc_${k}_w.log; exit 1; }
+      f=$(ls gpurun_out/${TAG}_pmc_${k}_f/*counter_collection.csv | head -1)
+      w=$(ls gpurun_out/${TAG}_pmc_${k}_w/*counter_collection.csv | head -1)
+      python tools/pmc_traffic.py "$f" "$w" "$k" "profiles/pmc_${TAG} ($k)" || exit 1 ;;
+    sq)
+      k=${rest%%:*}
+      a=${rest#*:}
+      [ "$a" = "$rest" ] && a=""
+      B="python bench.py --steps 1 --warmup 0 --no-cpu --no-exact --no-torch-baseline $(args_of "$a")"
+      timeout -s KILL 180 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
+        SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-include-regex "$k" \
+        -d gpurun_out/${TAG}_sq_${k}1 -o p --output-format csv -- $B > gpurun_out/${TAG}_sq_${k}1.log 2>&1 || exit 1
+      timeout -s KILL 180 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM \
+        SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_INSTS_MFMA --kernel-include-regex "$k" \
+        -d gpurun_out/${TAG}_sq_${k}2 -o p --output-format csv -- $B > gpurun_out/${TAG}_sq_${k}2.log 2>&1 || exit 1
+      echo "SQ_OK $k" ;;
+    py)
+      s=${rest%%:*}
+      a=${rest#*:}
+      [ "$a" = "$rest" ] && a=""
+      n=$(basename "$s" .py)
+      timeout -k 10 600 python "$s" $(args_of "$a") > gpurun_out/${TAG}_py_$n.log 2>&1 || { tail -30 gpurun_out/${TAG}_py_$n.log; exit 1; }
+      tail -n 3 gpurun_out/${TAG}_py_$n.log | cut -c1-600 ;;
+    *)
+      echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo ALL_OK

@@ -1,7 +1,8 @@
 """Summarise rocprofv3 --pmc passes (FETCH_SIZE and WRITE_SIZE, separate passes) into HBM bytes
 per launch of one kernel, with the gfx950 correction of MI355X_MICROARCH.md §HBM: FETCH_SIZE
 (KiB) reads half the bytes of a wide coalesced read -> x2; WRITE_SIZE (KiB) is exact for 16-B
-stores. Writes profiles/pmc_latest.json, which bench.py reports as roofline.traffic.
+stores. Updates this kernel's entry of profiles/pmc_latest.json ({kernel: {...}}), which bench.py
+reports as roofline.traffic of that kernel.
 
 python tools/pmc_traffic.py <fetch.csv> <write.csv> <kernel-substring> <label>
 """
@@ -25,8 +26,13 @@ def main():
            'bytes_per_launch': (2.0 * f + w) * 1024.0,
            'correction': 'FETCH_SIZE x2 (gfx950 wide-read undercount), WRITE_SIZE x1', 'source': label}
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    with open(os.path.join(root, 'profiles', 'pmc_latest.json'), 'w') as fh:
-        json.dump(out, fh, indent=1)
+    path = os.path.join(root, 'profiles', 'pmc_latest.json')
+    table = json.load(open(path)) if os.path.exists(path) else {}
+    if 'kernel' in table:  # the round-2 single-kernel format
+        table = {table['kernel']: table}
+    table[kernel] = out
+    with open(path, 'w') as fh:
+        json.dump(table, fh, indent=1)
     print(json.dumps(out))
 
 
