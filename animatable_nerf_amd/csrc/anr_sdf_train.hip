@@ -1,0 +1,1054 @@
+// anr_sdf_train.hip — one training step of the sdf_pdf variant (config 5, SURVEY.md §8(e) "Training
+// (3/4/5)"): tpose_trainer.NetworkWrapper.forward + loss.backward() over anisdf_pdf_network.Network
+// (lib/train/trainers/tpose_trainer.py:21-73, crit.py:5-19, anisdf_pdf_network.py:49-224).
+//
+// The loss reaches the parameters through second-order paths: the eikonal loss and the colour net
+// read gradients = d sdf / d x (create_graph, :306-321), and the observed-gradient loss reads
+// d sdf(x + resd(x)) / d x (:140-154). Each such term is differentiated forward-over-reverse: with
+// the upstream adjoint dg of g = grad_x s(x), dg . g = J_s(x) dg is the directional derivative of s
+// along dg, so one forward tangent pass (tangent input dg) and one reverse pass over the stacked
+// [primal; tangent] activations give every parameter's gradient. Per softplus layer
+// (h = sp(z), hdot = sp'(z) zdot): zdot_bar = sp'(z) hdot_bar, z_bar = sp'(z) h_bar + sp''(z) zdot
+// hdot_bar, and sp''(z) zdot = 100 (1 - sp'(z)) hdot, so only the stored factor d = exp(100 z) and
+// the tangent activation hdot are needed. ReLU layers have no second-order term; tanh has one.
+//
+// Layer-wise: every activation stays in HBM (a 1,024-ray batch keeps ~46k samples), exact fp32
+// MFMA GEMMs (anr_gemm.hip k_gemm_t: weights and activations shared by the primal and tangent
+// rows, which are stacked into one 2n-row operand wherever the epilogue allows); per-sample work in
+// the kernels below. Two host reads of counts (kept samples, observed-gradient rows).
+#include <algorithm>
+#include <cmath>
+
+#include "../../include/aninerf.h"
+#include "anr_common.h"
+#include "anr_kernels.h"
+#include "anr_sdf.h"
+#include "anr_train.h"
+#include "anr_ws.h"
+
+#pragma clang fp contract(off)
+
+using namespace anr;
+
+namespace anr {
+
+// ------------------------------------------------------------------------------------------
+// per-sample kernels
+// ------------------------------------------------------------------------------------------
+// inv[list[i]] = i: a sample id -> its compact row (the msk_sdf argmin scatter)
+__global__ void k_st_inv(const int* __restrict__ list, const int* __restrict__ n_dev, int* inv) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < *n_dev) inv[list[i]] = i;
+}
+
+// gamma_F feature f of x and its first and second derivatives along x[comp(f)] (embedder.py:5-54)
+__device__ __forceinline__ void embed_d(const float x[3], int f, int& comp, float& v, float& d1, float& d2) {
+  if (f < 3) {
+    comp = f; v = x[f]; d1 = 1.f; d2 = 0.f;
+    return;
+  }
+  const int g = f - 3, fr = g / 6, w = g - fr * 6;
+  comp = w >= 3 ? w - 3 : w;
+  const float om = (float)(1 << fr);
+  const float a = x[comp] * om;
+  const float sa = sinf(a), ca = cosf(a);
+  if (w < 3) { v = sa; d1 = om * ca; d2 = -om * om * sa; }
+  else { v = ca; d1 = -om * sa; d2 = -om * om * ca; }
+}
+
+// tangent of gamma_F: out[i][col0 + f] = scale * J_gamma(x_i) xd_i  (f < 3 + 6 F)
+__global__ void k_st_embed_tan(const float* __restrict__ x, long ldx, const float* __restrict__ xd, long ldxd, int nf,
+                               int n, float* out, long ldo, int col0, float scale) {
+  const int F = 3 + 6 * nf;
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (long)n * F) return;
+  const int i = (int)(e / F), f = (int)(e - (long)i * F);
+  const float p[3] = {x[i * ldx], x[i * ldx + 1], x[i * ldx + 2]};
+  int c;
+  float v, d1, d2;
+  embed_d(p, f, c, v, d1, d2);
+  out[(long)i * ldo + col0 + f] = scale * (d1 * xd[i * ldxd + c]);
+}
+
+// reverse of [gamma_6(t); J_gamma_6(t) tdot] (the SDF input, primal rows 0..n-1, tangent rows n..2n-1
+// of the adjoints): the gamma adjoint is lin0's input adjoint (A0, ld 40) plus lin4's gamma columns
+// (A4 cols 217.., ld 256, times 1/sqrt2). tbar += J^T abar + (d/dt J tdot)^T atbar; ttbar = J^T atbar.
+__global__ void k_st_embed_rev6(const float* __restrict__ t, long ldt, const float* __restrict__ td, long ldtd,
+                                const float* __restrict__ A0, const float* __restrict__ A4, int n, float* tbar,
+                                float* ttbar) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float p[3] = {t[i * ldt], t[i * ldt + 1], t[i * ldt + 2]};
+  const float pd[3] = {td[i * ldtd], td[i * ldtd + 1], td[i * ldtd + 2]};
+  const float rs2 = 0.70710678118654752f;
+  float tb[3] = {0.f, 0.f, 0.f}, ttb[3] = {0.f, 0.f, 0.f};
+  for (int f = 0; f < 39; ++f) {
+    const float ab = A0[(long)i * 40 + f] + A4[(long)i * 256 + 217 + f] * rs2;
+    const float atb = A0[(long)(n + i) * 40 + f] + A4[(long)(n + i) * 256 + 217 + f] * rs2;
+    int c;
+    float v, d1, d2;
+    embed_d(p, f, c, v, d1, d2);
+    tb[c] += d1 * ab + d2 * pd[c] * atb;
+    ttb[c] += d1 * atb;
+  }
+  for (int c = 0; c < 3; ++c) {
+    tbar[i * 4 + c] += tb[c];
+    if (ttbar) ttbar[i * 4 + c] = ttb[c];
+  }
+}
+
+// first-order reverse of gamma_10 (the residual net's input): xbar = J^T (G0 + G5) over 63 columns
+__global__ void k_st_embed_bwd10(const float* __restrict__ x, long ldx, const float* __restrict__ G, long ldg, int n,
+                                 float* xbar, long ldxb) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float p[3] = {x[i * ldx], x[i * ldx + 1], x[i * ldx + 2]};
+  float xb[3] = {0.f, 0.f, 0.f};
+  for (int f = 0; f < 63; ++f) {
+    int c;
+    float v, d1, d2;
+    embed_d(p, f, c, v, d1, d2);
+    xb[c] += d1 * G[(long)i * ldg + f];
+  }
+  for (int c = 0; c < 3; ++c) xbar[i * ldxb + c] = xb[c];
+}
+
+// softplus reverse of one layer over the stacked adjoints: rows 0..n-1 primal (A), n..2n-1 tangent
+// (At, row stride ldat: 0 broadcasts one row, NULL = 0). Z = [z_bar; zdot_bar] (ld 256).
+//   zdot_bar = sp' at;  z_bar = sp' a + 100 / (d + 1) hdot at  (d = exp(100 z) >= 0; above torch's
+//   threshold d = -1: sp' = 1, sp'' = 0). hdot = the tangent activation (Hd, times hscale).
+__global__ void k_st_sp_rev(const float* __restrict__ A, long lda, const float* __restrict__ At, long ldat, float ascale,
+                            const float* __restrict__ D, const float* __restrict__ Hd, long ldh, float hscale, int n,
+                            int width, float* Z) {
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (long)n * width) return;
+  const int i = (int)(e / width), c = (int)(e - (long)i * width);
+  const float a = A ? A[(long)i * lda + c] * ascale : 0.f;
+  const float at = At ? At[(long)i * ldat + c] * ascale : 0.f;
+  const float d = D[(long)i * 256 + c];
+  float zb, ztb;
+  if (d < 0.f) {
+    zb = a;
+    ztb = at;
+  } else {
+    const float r = 1.f / (d + 1.f);
+    const float sp1 = d * r;
+    const float hd = Hd[(long)i * ldh + c] * hscale;
+    ztb = sp1 * at;
+    zb = sp1 * a + 100.f * r * hd * at;
+  }
+  Z[(long)i * 256 + c] = zb;
+  Z[(long)(n + i) * 256 + c] = ztb;
+}
+
+// dW[o][col0 + q] += bsum[o] * v[q] (the folded constant columns: poses of the residual net)
+__global__ void k_st_outer_add(const float* __restrict__ bsum, const float* __restrict__ v, int nq, int nout, float* dW,
+                               int in_ch, int col0) {
+  const int o = blockIdx.x, q = threadIdx.x;
+  if (o < nout && q < nq) dW[(long)o * in_ch + col0 + q] += bsum[o] * v[q];
+}
+
+// dst[c] += sum over n rows of H[r][c] (c < 256): the tangent output adjoint e0 of lin8 (row 0 of dW8)
+__global__ void k_st_colsum(const float* __restrict__ H, long ldh, int n, float* dst) {
+  const int c = threadIdx.x;
+  float acc = 0.f;
+  for (int r = blockIdx.x; r < n; r += gridDim.x) acc += H[(long)r * ldh + c];
+  atomicAdd(dst + c, acc);
+}
+
+// weight norm backward (torch._weight_norm, dim 0): W = g v / |v|_row; from dW (effective):
+//   dg = (dW . v) / |v|;  dv = (g / |v|) (dW - (dW . v) v / |v|^2)
+__global__ __launch_bounds__(256) void k_st_wn_grad(const float* __restrict__ v, const float* __restrict__ gw,
+                                                    const float* __restrict__ dW, int in_ch, float* dg, float* dv) {
+  __shared__ float sh[2][4];
+  const int row = blockIdx.x;
+  const float* vr = v + (long)row * in_ch;
+  const float* dr = dW + (long)row * in_ch;
+  float s = 0.f, q = 0.f;
+  for (int k = threadIdx.x; k < in_ch; k += 256) {
+    s += dr[k] * vr[k];
+    q += vr[k] * vr[k];
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    s += __shfl_xor(s, off);
+    q += __shfl_xor(q, off);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    sh[0][threadIdx.x >> 6] = s;
+    sh[1][threadIdx.x >> 6] = q;
+  }
+  __syncthreads();
+  s = sh[0][0] + sh[0][1] + sh[0][2] + sh[0][3];
+  q = sh[1][0] + sh[1][1] + sh[1][2] + sh[1][3];
+  const float nrm = sqrtf(q);
+  const float g = gw[row];
+  if (threadIdx.x == 0) dg[row] += s / nrm;
+  const float a = g / nrm, b = s / q;
+  for (int k = threadIdx.x; k < in_ch; k += 256) dv[(long)row * in_ch + k] += a * (dr[k] - b * vr[k]);
+}
+
+struct StRaw {
+  const int* list;
+  const int* n_kept;
+  int chunk;
+  const float4* draw;   // (R*64) d raw from the compositing backward
+  const float* C0;      // [n][40] tpose
+  const float* tbtab;
+  const float* Y8;      // [n][264] sdf = col 0
+  const float* Yc;      // [n][4] colour logits
+  const float* beta;    // device scalar
+  float* dYc;           // [n][4]
+  float* ds;            // [n]
+  float* dbeta;         // device scalar (atomic)
+};
+
+// raw = (sigmoid(yc), 1 - exp(-relu(sigma(s, beta)) 0.005)), zero outside the widened tbounds
+// (anisdf_pdf_network.py:204-210, :271-331): d logits, d sdf, d beta per kept sample
+__global__ __launch_bounds__(256) void k_st_raw_bwd(StRaw a) {
+  __shared__ float sb[4];
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  float db = 0.f;
+  if (i < *a.n_kept) {
+    const int pid = a.list[i];
+    const float4 d = a.draw[pid];
+    const float* tb = a.tbtab + (size_t)((pid >> 6) / a.chunk) * 6;
+    const float* c = a.C0 + (size_t)i * 40;
+    bool inside = true;
+    for (int r = 0; r < 3; ++r) inside = inside && c[r] > tb[r] && c[r] < tb[3 + r];
+    float* dy = a.dYc + (size_t)i * 4;
+    if (!inside) {
+      dy[0] = dy[1] = dy[2] = dy[3] = 0.f;
+      a.ds[i] = 0.f;
+    } else {
+      const float dc[3] = {d.x, d.y, d.z};
+      for (int r = 0; r < 3; ++r) {
+        const float sg = 1.0f / (1.0f + expf(-a.Yc[(size_t)i * 4 + r]));
+        dy[r] = dc[r] * (sg * (1.f - sg));
+      }
+      dy[3] = 0.f;
+      const float braw = *a.beta;
+      const float beta = fminf(fmaxf(braw, 1e-9f), 1e6f);
+      const float x = -a.Y8[(size_t)i * 264];
+      float sig, dsig_dx, dsig_db;
+      if (x <= 0.f) {
+        const float e = expf(x / beta);
+        sig = 1.0f / beta * (0.5f * e);
+        dsig_dx = sig / beta;
+        dsig_db = -sig / beta - sig * x / (beta * beta);
+      } else {
+        const float e = expf(-x / beta);
+        sig = 1.0f / beta * (1.0f - 0.5f * e);
+        dsig_dx = 0.5f * e / (beta * beta);
+        dsig_db = -sig / beta - 0.5f * e * x / (beta * beta * beta);
+      }
+      const float dsig = sig > 0.f ? d.w * expf(-sig * 0.005f) * 0.005f : 0.f;
+      a.ds[i] = -dsig * dsig_dx;
+      if (braw >= 1e-9f && braw <= 1e6f) db = dsig * dsig_db;
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) db += __shfl_xor(db, off);
+  if ((threadIdx.x & 63) == 0) sb[threadIdx.x >> 6] = db;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(a.dbeta, sb[0] + sb[1] + sb[2] + sb[3]);
+}
+
+// loss accumulators (acc): 0 offset |r| sum, 1 eikonal sum, 2 observed-eikonal sum, 3 BCE sum,
+// 4 img sq-err sum, 5 img rays, 6 msk entries (count)
+struct StLoss {
+  const int* n_kept;
+  const float* resd;   // [n][3]
+  const float* C0;     // [n][40] gradients at 30..32
+  const float* dC0;    // [n][40] colour input adjoint (normal at 30..32)
+  const float* ds;     // [n]
+  float* rbar;         // [n][4] out: offset-loss adjoint of resd
+  float* dG;           // [n][4] out: normal adjoint (colour + eikonal)
+  float* dZ8;          // [n][264] col 0 out: sdf adjoint
+  float* acc;
+};
+
+__device__ __forceinline__ void block_add(float v, float* dst) {
+  __shared__ float sb[4];
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) sb[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(dst, sb[0] + sb[1] + sb[2] + sb[3]);
+}
+
+// offset_loss = mean |resd|, grad_loss = mean (|g| - 1)^2 (tpose_trainer.py:26-36) and their adjoints
+__global__ __launch_bounds__(256) void k_st_sample_loss(StLoss a) {
+  const int n = *a.n_kept;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  float lo = 0.f, lg = 0.f;
+  if (i < n) {
+    const float* r = a.resd + (size_t)i * 3;
+    const float rn = sqrtf(r[0] * r[0] + r[1] * r[1] + r[2] * r[2]);
+    lo = rn;
+    const float so = rn > 0.f ? 0.01f / ((float)n * rn) : 0.f;
+    const float* g = a.C0 + (size_t)i * 40 + 30;
+    const float gn = sqrtf(g[0] * g[0] + g[1] * g[1] + g[2] * g[2]);
+    lg = (gn - 1.f) * (gn - 1.f);
+    const float sg = gn > 0.f ? 0.01f * 2.f * (gn - 1.f) / ((float)n * gn) : 0.f;
+    for (int c = 0; c < 3; ++c) {
+      a.rbar[(size_t)i * 4 + c] = r[c] * so;
+      a.dG[(size_t)i * 4 + c] = a.dC0[(size_t)i * 40 + 30 + c] + g[c] * sg;
+    }
+    a.rbar[(size_t)i * 4 + 3] = 0.f;
+    a.dG[(size_t)i * 4 + 3] = 0.f;
+    a.dZ8[(size_t)i * 264] = a.ds[i];
+  }
+  block_add(lo, a.acc + 0);
+  block_add(lg, a.acc + 1);
+}
+
+// observed gradients: ograd_loss = mean (|og| - 1)^2 and its adjoint dog (tpose_trainer.py:38-43)
+__global__ __launch_bounds__(256) void k_st_obs_loss(const float* __restrict__ og, int n_o, float* dog, float* acc) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  float l = 0.f;
+  if (i < n_o) {
+    const float* g = og + (size_t)i * 4;
+    const float gn = sqrtf(g[0] * g[0] + g[1] * g[1] + g[2] * g[2]);
+    l = (gn - 1.f) * (gn - 1.f);
+    const float sg = gn > 0.f ? 0.01f * 2.f * (gn - 1.f) / ((float)n_o * gn) : 0.f;
+    for (int c = 0; c < 3; ++c) dog[(size_t)i * 4 + c] = g[c] * sg;
+    dog[(size_t)i * 4 + 3] = 0.f;
+  }
+  block_add(l, acc + 2);
+}
+
+// msk_sdf (tpose_renderer.py:134-152): per ray the min sdf over its 64 samples and the first sample
+// holding it (torch.min's index), the intersection test, the list an entry goes to; count entries
+__global__ __launch_bounds__(256) void k_st_msk_rays(const float* __restrict__ sdf, const uint8_t* __restrict__ occ,
+                                                     int R, float* mn_out, int* am_out, uint8_t* flags, float* acc) {
+  const int lane = threadIdx.x & 63;
+  const int ray = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (ray >= R) return;
+  const float s = sdf[(size_t)ray * 64 + lane];
+  const float nx = __shfl_down(s, 1);
+  float mn = s;
+  for (int off = 32; off > 0; off >>= 1) mn = fminf(mn, __shfl_xor(mn, off));
+  const uint64_t at = __ballot(s == mn);
+  const bool neg = lane < 63 && s * nx < 0.f;
+  const bool inter = __ballot(neg) != 0ull;
+  if (lane == 0) {
+    const uint8_t o = occ[ray];
+    const uint8_t f = (uint8_t)(((!inter && o == 1) ? 1 : 0) | (o == 0 ? 2 : 0));
+    mn_out[ray] = mn;
+    am_out[ray] = ray * 64 + (at ? __builtin_ctzll(at) : 0);
+    flags[ray] = f;
+    if (f) atomicAdd(acc + 6, 1.f);
+  }
+}
+
+// mask_loss = BCE_with_logits(-alpha msk_sdf, label).mean() / alpha (crit.py:5-19); its adjoint goes
+// to the argmin sample's sdf when that sample was kept (dropped samples hold the constant 10)
+__global__ __launch_bounds__(256) void k_st_msk_loss(const float* __restrict__ mn, const int* __restrict__ am,
+                                                     const uint8_t* __restrict__ flags, const int* __restrict__ inv,
+                                                     int R, float alpha, float* ds, float* acc) {
+  const int ray = blockIdx.x * blockDim.x + threadIdx.x;
+  float l = 0.f;
+  if (ray < R && flags[ray]) {
+    const float y = (flags[ray] & 1) ? 1.f : 0.f;
+    const float z = -alpha * mn[ray];
+    l = fmaxf(z, 0.f) - z * y + log1pf(expf(-fabsf(z)));
+    const float L = acc[6];
+    const float sg = 1.f / (1.f + expf(-z));
+    const int i = inv[am[ray]];
+    if (i >= 0) ds[i] += -(sg - y) / L;
+  }
+  block_add(l, acc + 3);
+}
+
+// loss vector (include/aninerf.h anr_sdf_train_step)
+__global__ void k_st_loss_final(const float* acc, const float* acc3, const int* n_kept, int n_o, float alpha, float* loss) {
+  const float n = (float)*n_kept;
+  const float off = acc[0] / n, gl = acc[1] / n, og = n_o > 0 ? acc[2] / (float)n_o : 0.f;
+  const float ml = acc[3] / acc[6] / alpha;
+  const float img = acc3[0] / (3.0f * acc3[1]);
+  float tot = 0.f;
+  tot += 0.01f * off;
+  tot += 0.01f * gl;
+  if (n_o > 0) tot += 0.01f * og;
+  tot += ml;
+  tot += img;
+  loss[0] = tot; loss[1] = off; loss[2] = gl; loss[3] = og; loss[4] = ml; loss[5] = img;
+  loss[6] = (float)n_o; loss[7] = acc[6];
+}
+
+// tanh head of the residual net, r = 0.05 tanh(y): tangent rdot = 0.05 (1 - tau^2) ydot, t = x + r
+__global__ void k_st_resd_tan(const float* __restrict__ Y, const float* __restrict__ Yd, const float* __restrict__ xd,
+                              int n, float* td) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  for (int c = 0; c < 3; ++c) {
+    const float t = tanhf(Y[(size_t)i * 4 + c]);
+    td[(size_t)i * 4 + c] = xd[(size_t)i * 4 + c] + 0.05f * (1.f - t * t) * Yd[(size_t)i * 4 + c];
+  }
+  td[(size_t)i * 4 + 3] = 0.f;
+}
+
+// reverse of r = 0.05 tanh(y) (and of its tangent when Yd != NULL): rows 0..n-1 y_bar, n..2n-1 ydot_bar
+//   ydot_bar = 0.05 (1 - tau^2) rdot_bar;  y_bar = 0.05 (1 - tau^2) r_bar - 0.1 tau (1 - tau^2) ydot rdot_bar
+__global__ void k_st_tanh_rev(const float* __restrict__ Y, const float* __restrict__ Yd, const float* __restrict__ rb,
+                              const float* __restrict__ rb2, const float* __restrict__ rdb, int n, float* out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  for (int c = 0; c < 3; ++c) {
+    const float t = tanhf(Y[(size_t)i * 4 + c]);
+    const float s = 1.f - t * t;
+    float r = rb[(size_t)i * 4 + c];
+    if (rb2) r += rb2[(size_t)i * 4 + c];
+    float yb = 0.05f * s * r;
+    if (Yd) {
+      const float rd = rdb[(size_t)i * 4 + c];
+      yb += -0.1f * t * s * Yd[(size_t)i * 4 + c] * rd;
+      out[(size_t)(n + i) * 4 + c] = 0.05f * s * rd;
+    }
+    out[(size_t)i * 4 + c] = yb;
+  }
+  out[(size_t)i * 4 + 3] = 0.f;
+  if (Yd) out[(size_t)(n + i) * 4 + 3] = 0.f;
+}
+
+// observed-gradient rows: kept samples with |sdf| < 0.02 (anisdf_pdf_network.py:194), compact order
+__global__ __launch_bounds__(256) void k_st_obs_count(const float* __restrict__ Y8, const int* __restrict__ n_dev,
+                                                      int* block_sum) {
+  __shared__ int sh[4];
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int v = (i < *n_dev && fabsf(Y8[(size_t)i * 264]) < 0.02f) ? 1 : 0;
+  int tot;
+  block_excl_scan_256(v, sh, tot);
+  if (threadIdx.x == 0) block_sum[blockIdx.x] = tot;
+}
+
+// gather: ptb_o / Gro rows of the observed samples (init_bigpose, its gamma_10 -- the same values the
+// reference recomputes from the detached copy)
+__global__ __launch_bounds__(256) void k_st_obs_gather(const float* __restrict__ Y8, const int* __restrict__ n_dev,
+                                                       const int* __restrict__ block_off, const float* __restrict__ ptb,
+                                                       const float* __restrict__ Gr, float* ptb_o, float* Gro) {
+  __shared__ int sh[4];
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int v = (i < *n_dev && fabsf(Y8[(size_t)i * 264]) < 0.02f) ? 1 : 0;
+  int tot;
+  const int ex = block_excl_scan_256(v, sh, tot);
+  if (!v) return;
+  const int o = block_off[blockIdx.x] + ex;
+  for (int k = 0; k < 8; ++k) ptb_o[(size_t)o * 8 + k] = ptb[(size_t)i * 8 + k];
+  for (int k = 0; k < 64; ++k) Gro[(size_t)o * 64 + k] = Gr[(size_t)i * 64 + k];
+}
+
+__global__ void k_st_add_bias(const float* __restrict__ src, int n, float* dst) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] += src[i];
+}
+
+__global__ void k_st_add3(const float* __restrict__ a, long lda, const float* __restrict__ b, long ldb, int n, float* out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  for (int c = 0; c < 3; ++c) out[(size_t)i * 4 + c] = a[i * lda + c] + b[i * ldb + c];
+  out[(size_t)i * 4 + 3] = 0.f;
+}
+
+}  // namespace anr
+
+namespace {
+
+// exact fp32 layer GEMMs (anr_gemm.hip)
+struct Epi {
+  int relu = 0;
+  float* deriv = nullptr;   // softplus(beta=100) epilogue writing its factor exp(100 z) (-1 above the threshold)
+  bool softplus = false;
+  const float* spd = nullptr;  // v *= sp'(z) from the stored factor (n < spd_n)
+  int spd_n = 0;
+  const float* mask = nullptr;  // v = 0 where mask <= 0 (a ReLU layer's output)
+  long ldm = 0;
+  float div_post = 0.f;
+};
+
+struct TG {
+  hipStream_t s;
+  int run(GemmArgs g, int M) {
+    if (M <= 0 || g.N <= 0) return ANR_OK;
+    g.M = M;
+    if (g.ksplit < 1) g.ksplit = 1;
+    launch_gemm(g, dim3((g.N + 63) / 64, (M + 63) / 64, g.ksplit), s);
+    return check_launch("k_gemm (sdf train)");
+  }
+  // Y[M][N] = epi(X0[:, :K0] W[:, c0:c0+K0]^T (+ X1[:, :K1] W[:, c1:c1+K1]^T) + bias)
+  int fwd(int M, float* Y, long ldY, int N, const float* W, int in_ch, const float* bias, const float* X0, long ld0,
+          int K0, int c0, const Epi& e = Epi(), const float* X1 = nullptr, long ld1 = 0, int K1 = 0, int c1 = 0) {
+    GemmArgs g{};
+    g.N = N;
+    g.nseg = X1 ? 2 : 1;
+    g.seg[0] = GemmSeg{X0, ld0, 1, W + c0, 1, in_ch, K0};
+    if (X1) g.seg[1] = GemmSeg{X1, ld1, 1, W + c1, 1, in_ch, K1};
+    g.C = Y; g.ldc = ldY; g.bias = bias; g.relu = e.relu;
+    if (e.softplus) { g.softplus = 1; g.deriv = e.deriv; g.ldd = 256; }
+    g.spd = e.spd; g.ldsd = 256; g.spd_n = e.spd_n;
+    g.mask = e.mask; g.ldm = e.ldm;
+    g.div_post = e.div_post;
+    return run(g, M);
+  }
+  // dW[:, c0:c0+K] (row stride in_ch) += dY^T X over M samples; bsum (+)= column sums of dY
+  int wgrad(int M, float* dW, int in_ch, int c0, int Nout, const float* dY, long ldY, const float* X, long ldX, int K,
+            float* bsum = nullptr) {
+    if (M <= 0) return ANR_OK;
+    GemmArgs g{};
+    g.rowsum = bsum;
+    g.N = K;
+    g.nseg = 1;
+    g.seg[0] = GemmSeg{dY, 1, ldY, X, ldX, 1, M};
+    g.C = dW + c0; g.ldc = in_ch; g.atomic = 1;
+    g.ksplit = (M + 511) / 512;
+    return run(g, Nout);
+  }
+  // dX[M][K] (+)= dY W[:, c0:c0+K] (masked by mask > 0), / div_post
+  int xgrad(int M, float* dX, long ldX, int K, const float* dY, long ldY, int Nout, const float* W, int in_ch, int c0,
+            const float* mask = nullptr, long ldm = 0, bool acc = false) {
+    GemmArgs g{};
+    g.N = K;
+    g.nseg = 1;
+    g.seg[0] = GemmSeg{dY, ldY, 1, W + c0, in_ch, 1, Nout};
+    g.C = dX; g.ldc = ldX; g.mask = mask; g.ldm = ldm; g.accumulate = acc ? 1 : 0;
+    return run(g, M);
+  }
+};
+
+constexpr float SQRT2 = 1.41421356237309515f;
+
+struct STLayout {
+  size_t counts, mask, chunk_min, ray_off, block_sum, list, knn, tbtab, wimg, fold, inv;
+  size_t ptb, Gr, Hr, Yr, resd, C0, Xs0, Hs, D, Y8, Ga, Gb, Gc, gB, grow, Hc, Yc;
+  size_t raw, sdf, draw, drgb, rmin, ramin, rflag;
+  size_t dYc, dHa, dHb, dC0, dZ8, ds, dG, rbar, tbar, ttbar, Ab, Zb, AX4, Ain, dWe, bsum, acc, acc3, dbeta, zero;
+  size_t oblock, ptbo, Gro, Grt, ro, og, dog, tdot, Gbar, Yd;
+  long N;
+  size_t total;
+};
+
+STLayout stlayout(int R, int chunk) {
+  STLayout L{};
+  const size_t N = (size_t)R * 64;
+  L.N = (long)N;
+  const size_t nch = (R + chunk - 1) / (size_t)std::max(chunk, 1);
+  size_t o = 0;
+  auto take = [&](size_t bytes) {
+    const size_t at = o;
+    o = align256(o + bytes);
+    return at;
+  };
+  auto f = [&](size_t floats) { return take(floats * 4); };
+  L.counts = take(16); L.mask = take(R * 8); L.chunk_min = take(nch * 8); L.ray_off = take((R + 1) * 4);
+  L.block_sum = take(((N + 255) / 256 + 1) * 4); L.list = take(N * 4); L.knn = take(N * 32); L.tbtab = f(nch * 6);
+  L.wimg = f(SDF_WN_FLOATS); L.fold = f(768); L.inv = take(N * 4);
+  L.ptb = f(N * 8); L.Gr = f(N * 64); L.Hr = f(8 * 2 * N * 256); L.Yr = f(2 * N * 4); L.resd = f(N * 3);
+  L.C0 = f(N * 40); L.Xs0 = f(2 * N * 40); L.Hs = f(8 * 2 * N * 256); L.D = f(8 * N * 256); L.Y8 = f(N * 264);
+  L.Ga = f(N * 256); L.Gb = f(N * 256); L.Gc = f(N * 256); L.gB = f(N * 40); L.grow = f(N * 3);
+  L.Hc = f(4 * N * 256); L.Yc = f(N * 4);
+  L.raw = f(N * 4); L.sdf = f(N); L.draw = f(N * 4); L.drgb = f(R * 3); L.rmin = f(R); L.ramin = take(R * 4);
+  L.rflag = take(R);
+  L.dYc = f(N * 4); L.dHa = f(N * 256); L.dHb = f(N * 256); L.dC0 = f(N * 40); L.dZ8 = f(N * 264); L.ds = f(N);
+  L.dG = f(N * 4); L.rbar = f(N * 4); L.tbar = f(N * 4); L.ttbar = f(N * 4); L.Ab = f(2 * N * 256);
+  L.Zb = f(2 * N * 256); L.AX4 = f(2 * N * 256); L.Ain = f(2 * N * 40); L.dWe = f(SDF_WN_FLOATS); L.bsum = f(4 * 256);
+  L.acc = f(16); L.acc3 = f(4); L.dbeta = f(4); L.zero = take(64);
+  L.oblock = take(((N + 255) / 256 + 1) * 4); L.ptbo = f(N * 8); L.Gro = f(N * 64); L.Grt = f(N * 64);
+  L.ro = f(N * 3); L.og = f(N * 4); L.dog = f(N * 4); L.tdot = f(N * 4); L.Gbar = f(N * 64); L.Yd = f(N * 4);
+  L.total = o;
+  return L;
+}
+
+int check_train(const anr_sdf_params* p, float* const* grads, const anr_sdf_frame* f, const float* ray_o,
+                const float* ray_d, const float* near_, const float* far_, int R, const anr_render_opts* o,
+                const float* rgb_gt, const anr_sdf_render_out* out, const float* loss, void* ws) {
+  if (!p || !grads || !f || !o || !out || !ws || !ray_o || !ray_d || !near_ || !far_ || !rgb_gt || !loss)
+    return fail(ANR_E_ARG, "sdf train: NULL argument");
+  if (o->n_samples != 64) return fail(ANR_E_ARG, "sdf train: only N_samples == 64 is supported");
+  if (o->chunk <= 0 || R <= 0 || (long)R * 64 > (1L << 24)) return fail(ANR_E_ARG, "sdf train: bad chunk / n_rays");
+  if (o->novel_pose) return fail(ANR_E_ARG, "sdf train: novel_pose is an aninerf option");
+  for (int i = 0; i < ANR_SDF_NUM_TENSORS; ++i) {
+    if (!p->t[i] && i != SDF_RESD_LAT) return fail(ANR_E_ARG, "sdf train: NULL parameter tensor");
+    if (!grads[i] && i != SDF_RESD_LAT) return fail(ANR_E_ARG, "sdf train: NULL gradient tensor");
+  }
+  if (!f->A || !f->big_A || !f->R || !f->Th || !f->poses || !f->pvertices || !f->weights || !f->tbounds ||
+      !f->latent_index || !f->occupancy)
+    return fail(ANR_E_ARG, "sdf train: NULL frame tensor");
+  if (f->n_verts <= 0 || f->n_verts > 6912) return fail(ANR_E_ARG, "sdf train: n_verts must be in [1, 6912]");
+  if (!out->rgb_map || !out->acc_map || !out->depth_map) return fail(ANR_E_ARG, "sdf train: NULL output");
+  return ANR_OK;
+}
+
+int read_int(const void* dev, int* host, hipStream_t s) {
+  if (hipMemcpyAsync(host, dev, 4, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+    return fail(ANR_E_HIP, "sdf train: count readback failed");
+  return ANR_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t anr_sdf_train_workspace_bytes(int n_rays, const anr_render_opts* o) {
+  if (n_rays <= 0 || !o || o->chunk <= 0) return 0;
+  return stlayout(n_rays, o->chunk).total;
+}
+
+int anr_sdf_train_step(const anr_sdf_params* p, float* const* grads, const anr_sdf_frame* f, const float* ray_o,
+                       const float* ray_d, const float* near_, const float* far_, int R, const anr_render_opts* o,
+                       const float* rgb_gt, const uint8_t* mask_at_box, int iter_step, const anr_sdf_render_out* out,
+                       float* loss, void* workspace, size_t ws_bytes, void* stream) {
+  ANR_TRY(check_train(p, grads, f, ray_o, ray_d, near_, far_, R, o, rgb_gt, out, loss, workspace));
+  const STLayout L = stlayout(R, o->chunk);
+  if (ws_bytes < L.total) return fail(ANR_E_WORKSPACE, "sdf train: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  char* ws = (char*)workspace;
+  auto F = [&](size_t off) { return (float*)(ws + off); };
+  const long N = L.N;
+  const int nch = (R + o->chunk - 1) / o->chunk;
+  int* counts = (int*)(ws + L.counts);
+  const float* const* tp = p->t;
+  float* wimg = F(L.wimg);
+  float* fold = F(L.fold);
+  float* tbtab = F(L.tbtab);
+  float4* raw = (float4*)F(L.raw);
+  float* sdf = F(L.sdf);
+  float* acc = F(L.acc);
+  float* acc3 = F(L.acc3);
+  if (hipMemsetAsync(ws + L.counts, 0, 16, s) != hipSuccess ||
+      hipMemsetAsync(ws + L.chunk_min, 0xff, (size_t)nch * 8, s) != hipSuccess ||
+      hipMemsetAsync(ws + L.inv, 0xff, (size_t)N * 4, s) != hipSuccess || hipMemsetAsync(acc, 0, 64, s) != hipSuccess ||
+      hipMemsetAsync(acc3, 0, 16, s) != hipSuccess || hipMemsetAsync(F(L.dbeta), 0, 16, s) != hipSuccess ||
+      hipMemsetAsync(ws + L.zero, 0, 64, s) != hipSuccess ||
+      hipMemsetAsync(F(L.dWe), 0, SDF_WN_FLOATS * 4, s) != hipSuccess)
+    return fail(ANR_E_HIP, "sdf train: memset");
+
+  // ---- per-call weights: weight norm, folds, per-chunk tbounds (anr_sdf_capi.hip)
+  SdfTensors T{};
+  for (int i = 0; i < ANR_SDF_NUM_TENSORS; ++i) T.t[i] = tp[i];
+  hipLaunchKernelGGL(k_sdf_wnorm, dim3(sdf_wn_rows()), dim3(256), 0, s, T, wimg);
+  hipLaunchKernelGGL(k_sdf_fold, dim3(3), dim3(256), 0, s, T, (const float*)wimg, f->poses, f->latent_index, fold);
+  hipLaunchKernelGGL(k_sdf_tbtab, dim3(1), dim3(64), 0, s, f->tbounds, nch, tbtab, out->tbounds_out);
+  ANR_TRY(check_launch("sdf train prep"));
+
+  // ---- B1 front-end (KNN keep mask) + ordered compaction; one host read of n'
+  SdfFrontArgs fa{};
+  fa.ray_o = ray_o; fa.ray_d = ray_d; fa.near_ = near_; fa.far_ = far_; fa.t_rand = o->t_rand;
+  fa.n_rays = R; fa.chunk = o->chunk; fa.R = f->R; fa.Th = f->Th; fa.verts = f->pvertices; fa.nv = f->n_verts;
+  fa.norm_th = o->norm_th; fa.mask = (uint64_t*)(ws + L.mask); fa.chunk_min = (uint64_t*)(ws + L.chunk_min);
+  fa.knn = (uint32_t*)(ws + L.knn); fa.raw = raw; fa.sdf = sdf;
+  int cus = 256;
+  {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
+      cus = v;
+  }
+  hipLaunchKernelGGL(k_sdf_front, dim3(std::min(cus, (R + 15) / 16)), dim3(1024), 0, s, fa);
+  ANR_TRY(check_launch("k_sdf_front (train)"));
+  CompactArgs ca{};
+  ca.n_rays = R; ca.chunk = o->chunk; ca.mask = fa.mask; ca.chunk_min = fa.chunk_min;
+  ca.ray_off = (int*)(ws + L.ray_off); ca.block_sum = (int*)(ws + L.block_sum); ca.list = (int*)(ws + L.list);
+  const int nb = (R + 255) / 256;
+  hipLaunchKernelGGL(k_count, dim3(nb), dim3(256), 0, s, ca);
+  hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, s, ca.block_sum, nb, counts);
+  hipLaunchKernelGGL(k_compact, dim3((R + 3) / 4), dim3(256), 0, s, ca);
+  ANR_TRY(check_launch("k_compact (sdf train)"));
+  int n = 0;
+  ANR_TRY(read_int(counts, &n, s));
+  int* inv = (int*)(ws + L.inv);
+  hipLaunchKernelGGL(k_st_inv, dim3((n + 255) / 256 + 1), dim3(256), 0, s, (const int*)ca.list, (const int*)counts, inv);
+
+  TG g{s};
+  const dim3 pb(256), pg((n + 255) / 256 + 1);
+  auto WN = [&](int l) { return (const float*)wimg + wn_layer(l).off; };
+  float* dWe = F(L.dWe);
+  auto dWN = [&](int l) { return dWe + wn_layer(l).off; };
+  const size_t S2 = (size_t)2 * N * 256;  // one stacked [2N][256] activation
+  auto Hr = [&](int l) { return F(L.Hr) + (size_t)l * S2; };
+  auto Hs = [&](int l) { return F(L.Hs) + (size_t)l * S2; };  // l = 3: X4 = [h3, gamma_6] / sqrt2
+  auto Dl = [&](int l) { return F(L.D) + (size_t)l * N * 256; };
+  auto Hc = [&](int l) { return F(L.Hc) + (size_t)l * N * 256; };
+  const float* Wr[8];
+  for (int l = 0; l < 8; ++l) Wr[l] = tp[SDF_RLIN0 + 2 * l];
+  const int rin[8] = {135, 256, 256, 256, 256, 391, 256, 256};
+
+  SdfPointArgs a{};
+  a.list = ca.list; a.b0 = 0; a.cnt = n;
+  a.ray_o = ray_o; a.ray_d = ray_d; a.near_ = near_; a.far_ = far_; a.t_rand = o->t_rand; a.chunk = o->chunk;
+  a.R = f->R; a.Th = f->Th; a.A = f->A; a.bigA = f->big_A; a.weights = f->weights; a.knn = fa.knn;
+  a.wimg = wimg; a.tbtab = tbtab;
+  a.ptb = F(L.ptb); a.Gr = F(L.Gr); a.Yr = F(L.Yr); a.Xs0 = F(L.Xs0); a.X4 = Hs(3); a.C0 = F(L.C0);
+  a.D7 = Dl(7); a.G7 = F(L.Ga); a.Gc = F(L.Gc); a.gB = F(L.gB); a.Y8 = F(L.Y8); a.Yc = F(L.Yc); a.beta = 0.f;
+  a.resd_rows = F(L.resd); a.grad_rows = F(L.grow); a.raw = raw; a.sdf = sdf;
+
+  // residual MLP forward on n rows (primal half of Hr); poses folded into the biases of layers 0, 5
+  auto resd_forward = [&](int m, const float* G, float* Y) -> int {
+    Epi r;
+    r.relu = 1;
+    ANR_TRY(g.fwd(m, Hr(0), 256, 256, Wr[0], 135, fold, G, 64, 63, 0, r));
+    for (int l = 1; l < 8; ++l) {
+      if (l == 5) ANR_TRY(g.fwd(m, Hr(5), 256, 256, Wr[5], 391, fold + 256, G, 64, 63, 0, r, Hr(4), 256, 256, 135));
+      else ANR_TRY(g.fwd(m, Hr(l), 256, 256, Wr[l], 256, tp[SDF_RLIN0 + 2 * l + 1], Hr(l - 1), 256, 256, 0, r));
+    }
+    return g.fwd(m, Y, 4, 3, tp[SDF_RFC_W], 256, tp[SDF_RFC_B], Hr(7), 256, 256, 0);
+  };
+  // SDF forward on m rows with the stored softplus factors (lin8 into Y8 when given)
+  auto sdf_forward = [&](int m, float* Y8) -> int {
+    Epi e;
+    e.softplus = true;
+    const float* hin = F(L.Xs0);
+    long ldin = 40;
+    for (int l = 0; l < 8; ++l) {
+      e.deriv = Dl(l);
+      if (l == 3) {
+        Epi e3 = e;
+        e3.div_post = SQRT2;
+        ANR_TRY(g.fwd(m, Hs(3), 256, 217, WN(3), 256, tp[9], hin, 256, 256, 0, e3));
+      } else {
+        ANR_TRY(g.fwd(m, Hs(l), 256, 256, WN(l), l == 0 ? 39 : 256, tp[3 * l], hin, ldin, l == 0 ? 39 : 256, 0, e));
+      }
+      hin = Hs(l);
+      ldin = 256;
+    }
+    if (Y8) ANR_TRY(g.fwd(m, Y8, 264, 257, WN(8), 256, tp[24], Hs(7), 256, 256, 0));
+    return ANR_OK;
+  };
+  // first-order input gradient of the SDF (the eval path's reverse chain): gradients -> C0[:, 30:33]
+  auto sdf_input_grad = [&](SdfPointArgs& pa, int m) -> int {
+    if (m <= 0) return ANR_OK;
+    pa.cnt = m;
+    pa.d7_h = 0;
+    hipLaunchKernelGGL(k_sdf_gtop, dim3((unsigned)(((long)m * 256 + 255) / 256)), pb, 0, s, pa);
+    ANR_TRY(check_launch("k_sdf_gtop (train)"));
+    auto bwd = [&](float* dX, int K, const float* dY, int Nout, const float* W, int in_ch, const float* spd, int spd_n,
+                   float div_pre) {
+      GemmArgs q{};
+      q.N = K; q.nseg = 1; q.seg[0] = GemmSeg{dY, 256, 1, W, in_ch, 1, Nout};
+      q.C = dX; q.ldc = K == 39 ? 40 : 256; q.spd = spd; q.ldsd = 256; q.spd_n = spd_n; q.div_pre = div_pre;
+      return g.run(q, m);
+    };
+    float *Ga = F(L.Ga), *Gb = F(L.Gb), *Gc = F(L.Gc);
+    ANR_TRY(bwd(Gb, 256, Ga, 256, WN(7), 256, Dl(6), 256, 0.f));
+    ANR_TRY(bwd(Ga, 256, Gb, 256, WN(6), 256, Dl(5), 256, 0.f));
+    ANR_TRY(bwd(Gb, 256, Ga, 256, WN(5), 256, Dl(4), 256, 0.f));
+    ANR_TRY(bwd(Gc, 256, Gb, 256, WN(4), 256, Dl(3), 217, SQRT2));
+    ANR_TRY(bwd(Ga, 256, Gc, 217, WN(3), 256, Dl(2), 256, 0.f));
+    ANR_TRY(bwd(Gb, 256, Ga, 256, WN(2), 256, Dl(1), 256, 0.f));
+    ANR_TRY(bwd(Ga, 256, Gb, 256, WN(1), 256, Dl(0), 256, 0.f));
+    ANR_TRY(bwd(F(L.gB), 39, Ga, 256, WN(0), 39, nullptr, 0, 0.f));
+    hipLaunchKernelGGL(k_sdf_gamma_bwd, dim3((m + 255) / 256), pb, 0, s, pa);
+    return check_launch("k_sdf_gamma_bwd (train)");
+  };
+  // tangent forward of the SDF from the input tangent tdot (n,4): tangent rows of Xs0 / Hs
+  auto sdf_tangent = [&](int m, const float* t, long ldt, const float* td) -> int {
+    float* Xt = F(L.Xs0) + (size_t)m * 40;
+    hipLaunchKernelGGL(k_st_embed_tan, dim3((unsigned)(((long)m * 39 + 255) / 256)), pb, 0, s, t, ldt, td, 4L, 6, m, Xt,
+                       40L, 0, 1.f);
+    hipLaunchKernelGGL(k_st_embed_tan, dim3((unsigned)(((long)m * 39 + 255) / 256)), pb, 0, s, t, ldt, td, 4L, 6, m,
+                       Hs(3) + (size_t)m * 256, 256L, 217, 1.f / SQRT2);
+    ANR_TRY(check_launch("k_st_embed_tan"));
+    const float* hin = Xt;
+    long ldin = 40;
+    for (int l = 0; l < 8; ++l) {
+      Epi e;
+      e.spd = Dl(l);
+      e.spd_n = l == 3 ? 217 : 256;
+      if (l == 3) e.div_post = SQRT2;
+      ANR_TRY(g.fwd(m, Hs(l) + (size_t)m * 256, 256, l == 3 ? 217 : 256, WN(l), l == 0 ? 39 : 256, nullptr, hin, ldin,
+                    l == 0 ? 39 : 256, 0, e));
+      hin = Hs(l) + (size_t)m * 256;
+      ldin = 256;
+    }
+    return ANR_OK;
+  };
+  // reverse of the SDF over the stacked [primal; tangent] rows. Z8 (m x 257, ld 264) = lin8's output
+  // adjoint (NULL = 0); the tangent output adjoint is e0 (the directional derivative of sdf).
+  // -> dW (effective) / bias grads, tbar (+=, (m,4)), ttbar ((m,4), or NULL)
+  auto sdf_reverse = [&](int m, const float* Z8, const float* t, long ldt, const float* td, float* tbar,
+                         float* ttbar) -> int {
+    float* Ab = F(L.Ab);
+    float* Zb = F(L.Zb);
+    float* AX4 = F(L.AX4);
+    float* Ain = F(L.Ain);
+    // lin8: primal dW / bias from Z8, tangent row 0 from the column sums of hdot7; A7 = Z8 W8
+    if (Z8) {
+      ANR_TRY(g.wgrad(m, dWN(8), 256, 0, 257, Z8, 264, Hs(7), 256, 256, grads[24]));
+      ANR_TRY(g.xgrad(m, Ab, 256, 256, Z8, 264, 257, WN(8), 256, 0));
+    }
+    hipLaunchKernelGGL(k_st_colsum, dim3(std::min(1024, m)), dim3(256), 0, s, (const float*)(Hs(7) + (size_t)m * 256),
+                       256L, m, dWN(8));
+    ANR_TRY(check_launch("k_st_colsum"));
+    const float* Aprim = Z8 ? Ab : nullptr;
+    const float* Atan = WN(8);  // row 0 of W8, broadcast
+    long ldat = 0;
+    for (int l = 7; l >= 0; --l) {
+      const int width = l == 3 ? 217 : 256;
+      const float sc = l == 3 ? 1.f / SQRT2 : 1.f;
+      const float* Hd = Hs(l) + (size_t)m * 256;
+      hipLaunchKernelGGL(k_st_sp_rev, dim3((unsigned)(((long)m * width + 255) / 256)), pb, 0, s, Aprim, 256L, Atan, ldat,
+                         sc, (const float*)Dl(l), Hd, 256L, l == 3 ? SQRT2 : 1.f, m, width, Zb);
+      ANR_TRY(check_launch("k_st_sp_rev"));
+      const int in_ch = l == 0 ? 39 : 256;
+      const float* Xp = l == 0 ? F(L.Xs0) : Hs(l - 1);
+      const long ldx = l == 0 ? 40 : 256;
+      ANR_TRY(g.wgrad(m, dWN(l), in_ch, 0, width, Zb, 256, Xp, ldx, in_ch, grads[3 * l]));
+      ANR_TRY(g.wgrad(m, dWN(l), in_ch, 0, width, Zb + (size_t)m * 256, 256, Xp + (size_t)m * ldx, ldx, in_ch));
+      float* Aout = l == 0 ? Ain : (l == 4 ? AX4 : Ab);
+      ANR_TRY(g.xgrad(2 * m, Aout, l == 0 ? 40 : 256, in_ch, Zb, 256, width, WN(l), in_ch, 0));
+      Aprim = l == 4 ? AX4 : Ab;
+      Atan = Aprim + (size_t)m * 256;
+      ldat = 256;
+    }
+    hipLaunchKernelGGL(k_st_embed_rev6, dim3((m + 255) / 256), pb, 0, s, t, ldt, td, 4L, (const float*)Ain,
+                       (const float*)AX4, m, tbar, ttbar);
+    return check_launch("k_st_embed_rev6");
+  };
+
+  if (n > 0) {
+    // ---- forward: B2/B3 residual deformation, B4 SDF + its input gradient, B6 colour, B5 raw
+    hipLaunchKernelGGL(k_sdf_prep, pg, pb, 0, s, a);
+    ANR_TRY(check_launch("k_sdf_prep (train)"));
+    ANR_TRY(resd_forward(n, F(L.Gr), F(L.Yr)));
+    hipLaunchKernelGGL(k_sdf_mid, pg, pb, 0, s, a);
+    ANR_TRY(check_launch("k_sdf_mid (train)"));
+    ANR_TRY(sdf_forward(n, F(L.Y8)));
+    ANR_TRY(sdf_input_grad(a, n));
+    {
+      Epi r;
+      r.relu = 1;
+      ANR_TRY(g.fwd(n, Hc(0), 256, 256, WN(9), 289, tp[29], F(L.C0), 40, 33, 0, r, F(L.Y8) + 1, 264, 256, 33));
+      ANR_TRY(g.fwd(n, Hc(1), 256, 256, WN(10), 256, tp[32], Hc(0), 256, 256, 0, r));
+      ANR_TRY(g.fwd(n, Hc(2), 256, 256, WN(11), 256, tp[35], Hc(1), 256, 256, 0, r));
+      ANR_TRY(g.fwd(n, Hc(3), 256, 256, WN(12), 384, fold + 512, Hc(2), 256, 256, 0, r));
+      ANR_TRY(g.fwd(n, F(L.Yc), 4, 3, WN(13), 256, tp[41], Hc(3), 256, 256, 0));
+    }
+    // k_sdf_raw reads beta from the host struct: pass it through the device scalar instead
+    float beta_h = 0.f;
+    if (hipMemcpyAsync(&beta_h, tp[SDF_BETA], 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+      return fail(ANR_E_HIP, "sdf train: beta readback");
+    a.beta = beta_h;
+    hipLaunchKernelGGL(k_sdf_raw, pg, pb, 0, s, a);
+    ANR_TRY(check_launch("k_sdf_raw (train)"));
+  }
+  // compositing, image loss and d rgb_map
+  const anr_render_out ro{out->rgb_map, out->acc_map, out->depth_map, nullptr};
+  ANR_TRY(stage_composite(near_, far_, R, o, raw, &ro, nullptr, s));
+  TrainBufs tb{};
+  tb.raw = raw; tb.draw = (float4*)F(L.draw); tb.n_rays = R; tb.rgb_map = out->rgb_map; tb.d_rgb_map = F(L.drgb);
+  tb.n_kept = counts;
+  const int gx = (R + 255) / 256;
+  hipLaunchKernelGGL(k_tr_loss, dim3(gx, 1), dim3(256), 0, s, tb, rgb_gt, mask_at_box, acc3);
+  hipLaunchKernelGGL(k_tr_loss_grads, dim3(gx, 1), dim3(256), 0, s, tb, rgb_gt, mask_at_box, (const float*)acc3,
+                     F(L.drgb), nullptr, nullptr);
+  hipLaunchKernelGGL(k_tr_composite_bwd, dim3((R + 3) / 4), dim3(256), 0, s, tb);
+  ANR_TRY(check_launch("sdf train: image loss / compositing backward"));
+  // msk_sdf lists: per-ray min / argmin / flags, entry count
+  hipLaunchKernelGGL(k_st_msk_rays, dim3((R + 3) / 4), dim3(256), 0, s, (const float*)sdf, f->occupancy, R, F(L.rmin),
+                     (int*)(ws + L.ramin), (uint8_t*)(ws + L.rflag), acc);
+  ANR_TRY(check_launch("k_st_msk_rays"));
+  float alpha = 50.f;
+  for (int m : {10000, 20000, 30000, 40000, 50000})
+    if (iter_step > m) alpha *= 2.f;
+
+  if (n > 0) {
+    // ---- backward: raw -> colour logits, sdf, beta; msk_sdf -> sdf
+    StRaw sr{};
+    sr.list = ca.list; sr.n_kept = counts; sr.chunk = o->chunk; sr.draw = (const float4*)F(L.draw);
+    sr.C0 = F(L.C0); sr.tbtab = tbtab; sr.Y8 = F(L.Y8); sr.Yc = F(L.Yc); sr.beta = tp[SDF_BETA];
+    sr.dYc = F(L.dYc); sr.ds = F(L.ds); sr.dbeta = F(L.dbeta);
+    hipLaunchKernelGGL(k_st_raw_bwd, pg, pb, 0, s, sr);
+    hipLaunchKernelGGL(k_st_msk_loss, dim3((R + 255) / 256), pb, 0, s, (const float*)F(L.rmin),
+                       (const int*)(ws + L.ramin), (const uint8_t*)(ws + L.rflag), (const int*)inv, R, alpha, F(L.ds),
+                       acc);
+    ANR_TRY(check_launch("sdf train: raw / msk backward"));
+    // ---- colour net backward (weight-normed lin4..lin0; color_latent folded into lin3)
+    float *dHa = F(L.dHa), *dHb = F(L.dHb), *bsum = F(L.bsum);
+    ANR_TRY(g.wgrad(n, dWN(13), 256, 0, 3, F(L.dYc), 4, Hc(3), 256, 256, grads[41]));
+    ANR_TRY(g.xgrad(n, dHa, 256, 256, F(L.dYc), 4, 3, WN(13), 256, 0, Hc(3), 256));
+    if (hipMemsetAsync(bsum, 0, 256 * 4, s) != hipSuccess) return fail(ANR_E_HIP, "memset");
+    ANR_TRY(g.wgrad(n, dWN(12), 384, 0, 256, dHa, 256, Hc(2), 256, 256, bsum));
+    hipLaunchKernelGGL(k_tr_latent_grad, dim3(256 + 128), dim3(128), 0, s, (const float*)bsum, WN(12), 384, 256, 256,
+                       tp[SDF_COLOR_LAT], f->latent_index, 0, dWN(12), grads[SDF_COLOR_LAT]);
+    ANR_TRY(check_launch("k_tr_latent_grad (colour)"));
+    hipLaunchKernelGGL(k_st_add_bias, dim3(1), dim3(256), 0, s, (const float*)bsum, 256, grads[38]);
+    ANR_TRY(g.xgrad(n, dHb, 256, 256, dHa, 256, 256, WN(12), 384, 0, Hc(2), 256));
+    ANR_TRY(g.wgrad(n, dWN(11), 256, 0, 256, dHb, 256, Hc(1), 256, 256, grads[35]));
+    ANR_TRY(g.xgrad(n, dHa, 256, 256, dHb, 256, 256, WN(11), 256, 0, Hc(1), 256));
+    ANR_TRY(g.wgrad(n, dWN(10), 256, 0, 256, dHa, 256, Hc(0), 256, 256, grads[32]));
+    ANR_TRY(g.xgrad(n, dHb, 256, 256, dHa, 256, 256, WN(10), 256, 0, Hc(0), 256));
+    ANR_TRY(g.wgrad(n, dWN(9), 289, 0, 256, dHb, 256, F(L.C0), 40, 33, grads[29]));
+    ANR_TRY(g.wgrad(n, dWN(9), 289, 33, 256, dHb, 256, F(L.Y8) + 1, 264, 256));
+    ANR_TRY(g.xgrad(n, F(L.dC0), 40, 33, dHb, 256, 256, WN(9), 289, 0));
+    ANR_TRY(g.xgrad(n, F(L.dZ8) + 1, 264, 256, dHb, 256, 256, WN(9), 289, 33));
+    // ---- loss adjoints of resd (offset) and gradients (eikonal + colour normals); d sdf into Z8 col 0
+    StLoss sl{};
+    sl.n_kept = counts; sl.resd = F(L.resd); sl.C0 = F(L.C0); sl.dC0 = F(L.dC0); sl.ds = F(L.ds);
+    sl.rbar = F(L.rbar); sl.dG = F(L.dG); sl.dZ8 = F(L.dZ8); sl.acc = acc;
+    hipLaunchKernelGGL(k_st_sample_loss, pg, pb, 0, s, sl);
+    ANR_TRY(check_launch("k_st_sample_loss"));
+    // ---- SDF: tangent pass along dG, stacked reverse -> SDF weights, d tpose
+    if (hipMemsetAsync(F(L.tbar), 0, (size_t)n * 16, s) != hipSuccess) return fail(ANR_E_HIP, "memset");
+    ANR_TRY(sdf_tangent(n, F(L.C0), 40, F(L.dG)));
+    ANR_TRY(sdf_reverse(n, F(L.dZ8), F(L.C0), 40, F(L.dG), F(L.tbar), nullptr));
+    // ---- residual net: r_bar = t_bar + offset adjoint -> tanh -> ReLU layers (first order)
+    float* yb = F(L.Yd);
+    hipLaunchKernelGGL(k_st_tanh_rev, pg, pb, 0, s, (const float*)F(L.Yr), (const float*)nullptr,
+                       (const float*)F(L.tbar), (const float*)F(L.rbar), (const float*)nullptr, n, yb);
+    ANR_TRY(check_launch("k_st_tanh_rev"));
+    ANR_TRY(g.wgrad(n, grads[SDF_RFC_W], 256, 0, 3, yb, 4, Hr(7), 256, 256, grads[SDF_RFC_B]));
+    ANR_TRY(g.xgrad(n, dHa, 256, 256, yb, 4, 3, tp[SDF_RFC_W], 256, 0, Hr(7), 256));
+    float* cur = dHa;
+    float* nxt = dHb;
+    for (int l = 7; l >= 0; --l) {
+      float* dW = grads[SDF_RLIN0 + 2 * l];
+      float* db = grads[SDF_RLIN0 + 2 * l + 1];
+      if (l == 0 || l == 5) {
+        if (hipMemsetAsync(bsum, 0, 256 * 4, s) != hipSuccess) return fail(ANR_E_HIP, "memset");
+        ANR_TRY(g.wgrad(n, dW, rin[l], 0, 256, cur, 256, F(L.Gr), 64, 63, bsum));
+        hipLaunchKernelGGL(k_st_outer_add, dim3(256), dim3(128), 0, s, (const float*)bsum, f->poses, 72, 256, dW, rin[l], 63);
+        hipLaunchKernelGGL(k_st_add_bias, dim3(1), dim3(256), 0, s, (const float*)bsum, 256, db);
+        ANR_TRY(check_launch("sdf train: residual folded columns"));
+        if (l == 5) {
+          ANR_TRY(g.wgrad(n, dW, 391, 135, 256, cur, 256, Hr(4), 256, 256));
+          ANR_TRY(g.xgrad(n, nxt, 256, 256, cur, 256, 256, Wr[5], 391, 135, Hr(4), 256));
+        }
+      } else {
+        ANR_TRY(g.wgrad(n, dW, 256, 0, 256, cur, 256, Hr(l - 1), 256, 256, db));
+        ANR_TRY(g.xgrad(n, nxt, 256, 256, cur, 256, 256, Wr[l], 256, 0, Hr(l - 1), 256));
+      }
+      std::swap(cur, nxt);
+    }
+  }
+
+  // ---- observed gradients (anisdf_pdf_network.py:194-199, 140-154): samples with |sdf| < 0.02
+  int n_o = 0;
+  if (n > 0) {
+    const int nbo = (n + 255) / 256;
+    int* oblock = (int*)(ws + L.oblock);
+    hipLaunchKernelGGL(k_st_obs_count, dim3(nbo), pb, 0, s, (const float*)F(L.Y8), (const int*)counts, oblock);
+    hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, s, oblock, nbo, counts + 2);
+    hipLaunchKernelGGL(k_st_obs_gather, dim3(nbo), pb, 0, s, (const float*)F(L.Y8), (const int*)counts,
+                       (const int*)oblock, (const float*)F(L.ptb), (const float*)F(L.Gr), F(L.ptbo), F(L.Gro));
+    ANR_TRY(check_launch("sdf train: observed rows"));
+    ANR_TRY(read_int(counts + 2, &n_o, s));
+  }
+  if (n_o > 0) {
+    const dim3 og_((n_o + 255) / 256);
+    // forward: x_o -> resd -> t_o -> SDF (factors) -> g_t = grad_t sdf; og = g_t + J_resd^T g_t
+    SdfPointArgs ao = a;
+    ao.cnt = n_o; ao.ptb = F(L.ptbo); ao.Gr = F(L.Gro); ao.Yr = F(L.Yr); ao.resd_rows = F(L.ro);
+    ao.grad_rows = F(L.grow);
+    ANR_TRY(resd_forward(n_o, F(L.Gro), F(L.Yr)));
+    hipLaunchKernelGGL(k_sdf_mid, og_, pb, 0, s, ao);
+    ANR_TRY(check_launch("k_sdf_mid (observed)"));
+    ANR_TRY(sdf_forward(n_o, nullptr));
+    ANR_TRY(sdf_input_grad(ao, n_o));
+    float *dHa = F(L.dHa), *dHb = F(L.dHb), *Gbar = F(L.Gbar);
+    float* yb = F(L.Yd);
+    // y_bar = 0.05 (1 - tau^2) g_t; reverse of the ReLU net to its gamma_10 input (input gradient only)
+    hipLaunchKernelGGL(k_st_add3, og_, pb, 0, s, (const float*)(F(L.C0) + 30), 40L, (const float*)(ws + L.zero), 0L, n_o,
+                       F(L.tdot));
+    hipLaunchKernelGGL(k_st_tanh_rev, og_, pb, 0, s, (const float*)F(L.Yr), (const float*)nullptr,
+                       (const float*)F(L.tdot), (const float*)nullptr, (const float*)nullptr, n_o, yb);
+    ANR_TRY(g.xgrad(n_o, dHa, 256, 256, yb, 4, 3, tp[SDF_RFC_W], 256, 0, Hr(7), 256));
+    float* cur = dHa;
+    float* nxt = dHb;
+    for (int l = 7; l >= 1; --l) {
+      if (l == 5) {
+        ANR_TRY(g.xgrad(n_o, Gbar, 64, 63, cur, 256, 256, Wr[5], 391, 0));
+        ANR_TRY(g.xgrad(n_o, nxt, 256, 256, cur, 256, 256, Wr[5], 391, 135, Hr(4), 256));
+      } else {
+        ANR_TRY(g.xgrad(n_o, nxt, 256, 256, cur, 256, 256, Wr[l], 256, 0, Hr(l - 1), 256));
+      }
+      std::swap(cur, nxt);
+    }
+    ANR_TRY(g.xgrad(n_o, Gbar, 64, 63, cur, 256, 256, Wr[0], 135, 0, nullptr, 0, true));
+    float* og = F(L.og);
+    hipLaunchKernelGGL(k_st_embed_bwd10, og_, pb, 0, s, (const float*)F(L.ptbo), 8L, (const float*)Gbar, 64L, n_o, og, 4L);
+    hipLaunchKernelGGL(k_st_add3, og_, pb, 0, s, (const float*)F(L.tdot), 4L, (const float*)og, 4L, n_o, og);
+    hipLaunchKernelGGL(k_st_obs_loss, og_, pb, 0, s, (const float*)og, n_o, F(L.dog), acc);
+    ANR_TRY(check_launch("sdf train: observed-gradient loss"));
+    // tangent forward along dog: gamma_10 -> ReLU net (masks of the primal) -> tanh -> tdot -> SDF
+    float* Grt = F(L.Grt);
+    if (hipMemsetAsync(Grt, 0, (size_t)n_o * 64 * 4, s) != hipSuccess) return fail(ANR_E_HIP, "memset");
+    hipLaunchKernelGGL(k_st_embed_tan, dim3((unsigned)(((long)n_o * 63 + 255) / 256)), pb, 0, s, (const float*)F(L.ptbo),
+                       8L, (const float*)F(L.dog), 4L, 10, n_o, Grt, 64L, 0, 1.f);
+    ANR_TRY(check_launch("k_st_embed_tan (gamma_10)"));
+    auto HrT = [&](int l) { return Hr(l) + (size_t)n_o * 256; };
+    {
+      Epi e;
+      e.mask = Hr(0); e.ldm = 256;
+      ANR_TRY(g.fwd(n_o, HrT(0), 256, 256, Wr[0], 135, nullptr, Grt, 64, 63, 0, e));
+      for (int l = 1; l < 8; ++l) {
+        e.mask = Hr(l);
+        if (l == 5) ANR_TRY(g.fwd(n_o, HrT(5), 256, 256, Wr[5], 391, nullptr, Grt, 64, 63, 0, e, HrT(4), 256, 256, 135));
+        else ANR_TRY(g.fwd(n_o, HrT(l), 256, 256, Wr[l], 256, nullptr, HrT(l - 1), 256, 256, 0, e));
+      }
+    }
+    float* Yd = F(L.Yr) + (size_t)n_o * 4;  // ydot in the stacked Yr rows
+    ANR_TRY(g.fwd(n_o, Yd, 4, 3, tp[SDF_RFC_W], 256, nullptr, HrT(7), 256, 256, 0));
+    hipLaunchKernelGGL(k_st_resd_tan, og_, pb, 0, s, (const float*)F(L.Yr), (const float*)Yd, (const float*)F(L.dog), n_o,
+                       F(L.tdot));
+    ANR_TRY(check_launch("k_st_resd_tan"));
+    ANR_TRY(sdf_tangent(n_o, F(L.C0), 40, F(L.tdot)));
+    // stacked reverse: SDF (output adjoint: tangent e0 only) -> t_bar, tdot_bar -> tanh -> ReLU net
+    float* tbar = F(L.tbar);
+    float* ttbar = F(L.ttbar);
+    if (hipMemsetAsync(tbar, 0, (size_t)n_o * 16, s) != hipSuccess) return fail(ANR_E_HIP, "memset");
+    ANR_TRY(sdf_reverse(n_o, nullptr, F(L.C0), 40, F(L.tdot), tbar, ttbar));
+    float* ybs = F(L.Ab);  // [2 n_o][4]: y_bar, ydot_bar (the SDF adjoint buffer is free again)
+    hipLaunchKernelGGL(k_st_tanh_rev, og_, pb, 0, s, (const float*)F(L.Yr), (const float*)Yd, (const float*)tbar,
+                       (const float*)nullptr, (const float*)ttbar, n_o, ybs);
+    ANR_TRY(check_launch("k_st_tanh_rev (observed)"));
+    const float* ybt = ybs + (size_t)n_o * 4;
+    float* bsum = F(L.bsum);
+    ANR_TRY(g.wgrad(n_o, grads[SDF_RFC_W], 256, 0, 3, ybs, 4, Hr(7), 256, 256, grads[SDF_RFC_B]));
+    ANR_TRY(g.wgrad(n_o, grads[SDF_RFC_W], 256, 0, 3, ybt, 4, HrT(7), 256, 256));
+    float* Zr = F(L.Zb);  // stacked [2 n_o][256] ReLU-layer adjoints: z_bar rows then zdot_bar rows
+    float* Zr2 = F(L.AX4);
+    ANR_TRY(g.xgrad(n_o, Zr, 256, 256, ybs, 4, 3, tp[SDF_RFC_W], 256, 0, Hr(7), 256));
+    ANR_TRY(g.xgrad(n_o, Zr + (size_t)n_o * 256, 256, 256, ybt, 4, 3, tp[SDF_RFC_W], 256, 0, Hr(7), 256));
+    for (int l = 7; l >= 0; --l) {
+      float* dW = grads[SDF_RLIN0 + 2 * l];
+      float* db = grads[SDF_RLIN0 + 2 * l + 1];
+      const float* Zt = Zr + (size_t)n_o * 256;
+      if (l == 0 || l == 5) {
+        if (hipMemsetAsync(bsum, 0, 256 * 4, s) != hipSuccess) return fail(ANR_E_HIP, "memset");
+        ANR_TRY(g.wgrad(n_o, dW, rin[l], 0, 256, Zr, 256, F(L.Gro), 64, 63, bsum));
+        ANR_TRY(g.wgrad(n_o, dW, rin[l], 0, 256, Zt, 256, Grt, 64, 63));
+        hipLaunchKernelGGL(k_st_outer_add, dim3(256), dim3(128), 0, s, (const float*)bsum, f->poses, 72, 256, dW, rin[l],
+                           63);
+        hipLaunchKernelGGL(k_st_add_bias, dim3(1), dim3(256), 0, s, (const float*)bsum, 256, db);
+        ANR_TRY(check_launch("sdf train: residual folded columns (observed)"));
+        if (l == 5) {
+          ANR_TRY(g.wgrad(n_o, dW, 391, 135, 256, Zr, 256, Hr(4), 256, 256));
+          ANR_TRY(g.wgrad(n_o, dW, 391, 135, 256, Zt, 256, HrT(4), 256, 256));
+          ANR_TRY(g.xgrad(n_o, Zr2, 256, 256, Zr, 256, 256, Wr[5], 391, 135, Hr(4), 256));
+          ANR_TRY(g.xgrad(n_o, Zr2 + (size_t)n_o * 256, 256, 256, Zt, 256, 256, Wr[5], 391, 135, Hr(4), 256));
+        }
+      } else {
+        ANR_TRY(g.wgrad(n_o, dW, 256, 0, 256, Zr, 256, Hr(l - 1), 256, 256, db));
+        ANR_TRY(g.wgrad(n_o, dW, 256, 0, 256, Zt, 256, HrT(l - 1), 256, 256));
+        ANR_TRY(g.xgrad(n_o, Zr2, 256, 256, Zr, 256, 256, Wr[l], 256, 0, Hr(l - 1), 256));
+        ANR_TRY(g.xgrad(n_o, Zr2 + (size_t)n_o * 256, 256, 256, Zt, 256, 256, Wr[l], 256, 0, Hr(l - 1), 256));
+      }
+      std::swap(Zr, Zr2);
+    }
+  }
+
+  // ---- weight norm: effective-weight gradients -> weight_g / weight_v; beta; loss vector
+  if (n > 0) {
+    for (int l = 0; l < SDF_NUM_WN; ++l) {
+      const WnLayer d = wn_layer(l);
+      hipLaunchKernelGGL(k_st_wn_grad, dim3(d.out), dim3(256), 0, s, tp[d.v], tp[d.g], (const float*)dWN(l), d.in,
+                         grads[d.g], grads[d.v]);
+    }
+    hipLaunchKernelGGL(k_st_add_bias, dim3(1), dim3(256), 0, s, (const float*)F(L.dbeta), 1, grads[SDF_BETA]);
+    ANR_TRY(check_launch("k_st_wn_grad"));
+  }
+  hipLaunchKernelGGL(k_st_loss_final, dim3(1), dim3(1), 0, s, (const float*)acc, (const float*)acc3, (const int*)counts,
+                     n_o, alpha, loss);
+  return check_launch("k_st_loss_final");
+}
+
+}  // extern "C"

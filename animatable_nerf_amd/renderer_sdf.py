@@ -10,8 +10,8 @@ Output keys and shapes are the reference's eval outputs: ``raw (1,R*64,4)``, ``s
 ``msk_sdf``/``msk_label (1,L)``; ``render`` moves them to the CPU (``:154-155``) and, like the
 reference, widens ``batch['tbounds']`` in place by 0.05 per chunk.
 
-Training of this variant (``observed_gradients``, second-order grad loss) is not on the device
-path; ``render`` with grad enabled raises.
+Training of this variant (``observed_gradients``, second-order grad loss) runs through
+``trainer_sdf`` (``anr_sdf_train_step``); ``render`` with grad enabled points there.
 """
 import ctypes
 
@@ -64,12 +64,9 @@ class Renderer:
             p.t[i] = t.data_ptr()
         return p
 
-    def render_device(self, batch, t_rand=None, chunk_offset=0, bw_rows=True):
-        """All outputs stay in HBM; ``batch['tbounds']`` is widened in place (reference quirk).
-        ``chunk_offset`` c0 > 0: these rays are the reference's chunks c0, c0+1, ... of a larger frame
-        (a rank's shard, parallel.render_sharded): the reference has widened tbounds c0 times before
-        them (anisdf_pdf_network.py:204-206), so the device starts from those bounds. ``bw_rows`` is
-        accepted for the aninerf renderer's signature (this network has no pbw / tbw rows)."""
+    def prepare(self, batch, t_rand=None, chunk_offset=0):
+        """Device tensors and C structs of one call over ``batch`` (kept alive in the returned dict):
+        params, frame, rays, opts (render precision, stratification draws when perturbing)."""
         p = self.params()
         dev = self.device()
         R = batch['ray_o'].shape[1]
@@ -84,7 +81,7 @@ class Renderer:
         li = batch['latent_index'].to(device=dev, dtype=torch.int64).reshape(-1).contiguous()
         occ = batch['occupancy'].to(device=dev, dtype=torch.uint8).reshape(-1).contiguous()
         f = _lib.SdfFrame()
-        for k in ('A', 'big_A', 'R', 'Th', 'poses', 'pvertices', 'weights', 'tbounds'):
+        for k in FRAME_KEYS:
             setattr(f, k, fr[k].data_ptr())
         f.n_verts = fr['pvertices'].shape[-2]
         f.latent_index, f.occupancy = li.data_ptr(), occ.data_ptr()
@@ -98,6 +95,17 @@ class Renderer:
         if rprec not in ('fp32', 'bf16x3'):
             raise ValueError(f"render_precision must be 'fp32' or 'bf16x3', got {rprec!r}")
         o.precision = _lib.BF16X3 if rprec == 'bf16x3' else _lib.FP32
+        return {'p': p, 'dev': dev, 'R': R, 'ns': ns, 'rays': rays, 'fr': fr, 't_rand': tr, 'li': li, 'occ': occ,
+                'frame': f, 'opts': o}
+
+    def render_device(self, batch, t_rand=None, chunk_offset=0, bw_rows=True):
+        """All outputs stay in HBM; ``batch['tbounds']`` is widened in place (reference quirk).
+        ``chunk_offset`` c0 > 0: these rays are the reference's chunks c0, c0+1, ... of a larger frame
+        (a rank's shard, parallel.render_sharded): the reference has widened tbounds c0 times before
+        them (anisdf_pdf_network.py:204-206), so the device starts from those bounds. ``bw_rows`` is
+        accepted for the aninerf renderer's signature (this network has no pbw / tbw rows)."""
+        c = self.prepare(batch, t_rand, chunk_offset)
+        p, dev, R, ns, rays, f, o = c['p'], c['dev'], c['R'], c['ns'], c['rays'], c['frame'], c['opts']
         rgb = torch.empty((1, R, 3), device=dev)
         acc = torch.empty((1, R), device=dev)
         depth = torch.empty((1, R), device=dev)
@@ -115,8 +123,8 @@ class Renderer:
                                                R, ctypes.byref(o), ctypes.byref(out), _lib.ptr(ws), ws_bytes, st),
                    'anr_sdf_render_fwd')
         addr = self.lib.anr_sdf_render_counts(_lib.ptr(ws), R, ctypes.byref(o))
-        c = ws[addr - ws.data_ptr():addr - ws.data_ptr() + 8].view(torch.int32).cpu()  # host sync
-        n_kept, n_msk = int(c[0]), int(c[1])
+        cnt = ws[addr - ws.data_ptr():addr - ws.data_ptr() + 8].view(torch.int32).cpu()  # host sync
+        n_kept, n_msk = int(cnt[0]), int(cnt[1])
         self.last_counts = (n_kept, n_msk)
         resd = torch.empty((1, n_kept, 3), device=dev)
         grad = torch.empty((1, n_kept, 3), device=dev)
@@ -131,8 +139,9 @@ class Renderer:
 
     def render(self, batch):
         if torch.is_grad_enabled() and any(p.requires_grad for p in self.net.parameters()) and self.net.training:
-            raise RuntimeError('sdf_pdf training is not on the device path of this build; render under '
-                               'torch.no_grad() for evaluation')
+            raise RuntimeError('sdf_pdf training runs as one fused step: use trainer_sdf.NetworkWrapper(net) '
+                               '(tpose_trainer.py:21-73) or trainer_sdf.SdfStep; render under torch.no_grad() '
+                               'for evaluation')
         with torch.no_grad():
             ret = self.render_device(batch)
         from .renderer import to_host

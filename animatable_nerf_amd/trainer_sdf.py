@@ -1,0 +1,140 @@
+"""Trainer plugin for the sdf_pdf network (config 5): ``lib/train/trainers/tpose_trainer.py:11-73``
+(the trainer ``configs/sdf_pdf/anisdf_pdf_s9p.yaml:13-14`` selects) with ``crit.sdf_mask_crit``
+(``crit.py:5-19``), on the HIP library's fused training step ``anr_sdf_train_step``.
+
+The reference differentiates through ``gradients = d sdf / d x`` (create_graph) and the
+``observed_gradients`` of the deformed SDF: second-order terms that the device step evaluates
+forward-over-reverse (anr_sdf_train.hip). One call returns the losses AND every parameter gradient:
+
+* ``NetworkWrapper(net)`` — ``forward(batch) -> (ret, loss, scalar_stats, image_stats)`` with the
+  reference's stats keys (offset_loss, grad_loss, ograd_loss when present, mask_loss, img_loss,
+  loss); ``loss.backward()`` hands the precomputed gradients to the parameters (an autograd
+  Function), so the reference ``Trainer.train`` loop (clip_grad_value_, Adam) runs unchanged.
+  ``batch['iter_step']`` sets the mask-loss alpha schedule, as in the reference.
+* ``SdfStep(net)`` — the native loop: the 63 tensors (1,432,510 floats) and their gradients in flat
+  HBM blobs with the 8 loss floats in the gradient blob's tail, so one RCCL mean all-reduce carries
+  gradients and losses (DDP semantics, trainer.py:13-18); then clip + Adam (``anr_adam``).
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+from . import config as _config
+from .parallel import GradBuckets, broadcast_
+from .renderer_sdf import Renderer
+
+LOSS_KEYS = ('loss', 'offset_loss', 'grad_loss', 'ograd_loss', 'mask_loss', 'img_loss', 'n_observed', 'msk_len')
+
+
+def sdf_train_step(renderer, batch, grads, loss8, t_rand=None, iter_step=None):
+    """One anr_sdf_train_step: ACCUMULATES the gradients of the 63 tensors into ``grads`` (list,
+    state_dict order) and writes the 8 loss floats into ``loss8`` (device, no host sync of its own).
+    Returns {'rgb_map', 'acc_map', 'depth_map'} and widens ``batch['tbounds']`` in place."""
+    lib = renderer.lib
+    c = renderer.prepare(batch, t_rand)
+    dev, R, rays, o = c['dev'], c['R'], c['rays'], c['opts']
+    rgb = torch.empty((1, R, 3), device=dev)
+    acc = torch.empty((1, R), device=dev)
+    depth = torch.empty((1, R), device=dev)
+    tb_out = torch.empty((2, 3), device=dev)
+    out = _lib.SdfRenderOut(rgb.data_ptr(), acc.data_ptr(), depth.data_ptr(), None, None, tb_out.data_ptr())
+    gt = batch['rgb'].to(device=dev, dtype=torch.float32).contiguous()
+    mask = batch.get('mask_at_box')
+    mask = None if mask is None else mask.to(device=dev).reshape(-1).to(torch.uint8).contiguous()
+    it = int(batch.get('iter_step', 0) if iter_step is None else iter_step)
+    nbytes = lib.anr_sdf_train_workspace_bytes(R, ctypes.byref(o))
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    gp = (ctypes.c_void_p * _lib.NUM_SDF_TENSORS)(*[None if g is None else g.data_ptr() for g in grads])
+    _lib.check(lib.anr_sdf_train_step(ctypes.byref(c['p']), gp, ctypes.byref(c['frame']),
+                                      *[_lib.ptr(rays[k]) for k in ('ray_o', 'ray_d', 'near', 'far')], R,
+                                      ctypes.byref(o), _lib.ptr(gt), _lib.ptr(mask), it, ctypes.byref(out),
+                                      _lib.ptr(loss8), _lib.ptr(ws), nbytes, _lib.stream_ptr(dev)),
+               'anr_sdf_train_step')
+    with torch.no_grad():
+        batch['tbounds'].copy_(tb_out.view_as(batch['tbounds']))
+    return {'rgb_map': rgb, 'acc_map': acc, 'depth_map': depth}
+
+
+class _SdfLoss(torch.autograd.Function):
+    """forward = anr_sdf_train_step (losses + gradients in one pass); backward hands out the gradients
+    (the loss is the only differentiated output in the reference: loss.backward())."""
+
+    @staticmethod
+    def forward(ctx, renderer, batch, t_rand, *params):
+        grads = [torch.zeros_like(t) for t in params]
+        loss8 = torch.zeros(8, device=params[0].device)
+        renderer.last_ret = sdf_train_step(renderer, batch, grads, loss8, t_rand)
+        ctx.grads = grads
+        return tuple(loss8[k] for k in range(6)) + (loss8[6:8].detach().clone(),)
+
+    @staticmethod
+    def backward(ctx, d_loss, *_):
+        return (None, None, None, *[g * d_loss for g in ctx.grads])
+
+
+class NetworkWrapper(torch.nn.Module):
+    """tpose_trainer.NetworkWrapper (:11-73) over the sdf_pdf network."""
+
+    def __init__(self, net, cfg=None):
+        super().__init__()
+        self.net = net
+        self.renderer = Renderer(net, cfg)
+
+    def forward(self, batch, t_rand=None):
+        outs = _SdfLoss.apply(self.renderer, batch, t_rand, *self.net.tensors())
+        loss, offset, grad, ograd, mask, img, counts = outs
+        stats = {'offset_loss': offset, 'grad_loss': grad}
+        if int(counts[0]) > 0:  # the reference's ret has 'observed_gradients' only then
+            stats['ograd_loss'] = ograd
+        stats.update({'mask_loss': mask, 'img_loss': img, 'loss': loss})
+        return self.renderer.last_ret, loss, stats, {}
+
+
+class SdfStep:
+    """Native sdf_pdf training step: ``step(batch)`` = anr_sdf_train_step + [RCCL mean all-reduce of
+    the gradient blob with the losses in its tail] + clip_grad_value_(40) + Adam (optimizer.py:12-27,
+    trainer.py:64-68). Returns the device loss vector (LOSS_KEYS order, rank-averaged)."""
+
+    def __init__(self, net, cfg=None, lr=None, clip=40.0, betas=(0.9, 0.999), eps=1e-8, group=None):
+        self.cfg = cfg if cfg is not None else _config.active()
+        self.net = net
+        self.renderer = Renderer(net, self.cfg)
+        self.lib = self.renderer.lib
+        self.lr = float(self.cfg.train.lr if lr is None else lr)
+        self.wd = float(self.cfg.train.weight_decay)
+        self.clip, self.betas, self.eps, self.group = clip, betas, eps, group
+        ps = net.tensors()
+        dev = ps[0].device
+        n = sum(p.numel() for p in ps)
+        self.flat = torch.empty(n, device=dev)
+        self.grad = torch.zeros(n + 8, device=dev)
+        self.m = torch.zeros(n, device=dev)
+        self.v = torch.zeros(n, device=dev)
+        self.grad_views = []
+        off = 0
+        for p in ps:
+            k = p.numel()
+            self.flat[off:off + k].copy_(p.detach().reshape(-1))
+            p.data = self.flat[off:off + k].view_as(p)
+            self.grad_views.append(self.grad[off:off + k].view_as(p))
+            off += k
+        self.n, self.t = n, 0
+        self.loss8 = self.grad[n:n + 8]
+        self.buckets = GradBuckets(self.grad, [(0, n + 8)], group)
+        self.iter_step = 0
+        broadcast_(self.flat, 0, group)  # DDP semantics: every replica starts from rank 0's weights
+
+    def step(self, batch, t_rand=None, lr=None):
+        self.grad.zero_()
+        it = int(batch.get('iter_step', self.iter_step))
+        sdf_train_step(self.renderer, batch, self.grad_views, self.loss8, t_rand, iter_step=it)
+        self.buckets.reduce(0)
+        self.buckets.wait()
+        self.t += 1
+        self.iter_step += 1
+        _lib.check(self.lib.anr_adam(_lib.ptr(self.flat), _lib.ptr(self.grad), _lib.ptr(self.m), _lib.ptr(self.v),
+                                     self.n, float(self.lr if lr is None else lr), self.betas[0], self.betas[1],
+                                     self.eps, self.wd, self.t, self.clip, _lib.stream_ptr(self.flat.device)),
+                   'anr_adam')
+        return self.loss8

@@ -20,6 +20,8 @@
  *                             lib/networks/bw_deform/anisdf_pdf_network.py:156-223 Network.forward,
  *                             sample_utils.py:309-348 (KNN blend), TPoseHuman :288-338,
  *                             tpose_renderer.py:134-152 (msk_sdf / msk_label)
+ *   anr_sdf_train_step      lib/train/trainers/tpose_trainer.py:21-73 over the sdf_pdf network
+ *                             (configs/sdf_pdf/anisdf_pdf_s9p.yaml:13-14), forward + loss.backward()
  *   anr_sdf_render_counts / anr_sdf_render_rows   the compact outputs 'resd', 'gradients',
  *                             'msk_sdf', 'msk_label' (sizes known only after the keep mask)
  *   anr_network_fwd         lib/networks/bw_deform/tpose_nerf_network.py:139-215 Network.forward
@@ -334,6 +336,23 @@ const int32_t* anr_sdf_render_counts(const void* workspace, int n_rays, const an
 /* copy resd (n',3), gradients (n',3), msk_sdf / msk_label (len) out of the workspace */
 int anr_sdf_render_rows(const void* workspace, int n_rays, const anr_render_opts* o, float* resd, float* gradients,
                         float* msk_sdf, float* msk_label, void* stream);
+
+/* ---- sdf_pdf training (config 5; lib/train/trainers/tpose_trainer.py:21-73, crit.py:5-19) ---------
+ * anr_sdf_train_step: NetworkWrapper.forward + loss.backward() of one batch through the sdf_pdf
+ *   network and tpose_renderer (anisdf_pdf_network.py:156-224 in training mode: gradients with
+ *   create_graph, observed_gradients at the kept samples with |sdf| < 0.02), then the losses
+ *   offset 0.01 mean|resd|, eikonal 0.01 mean(|g|-1)^2 (gradients and observed_gradients), msk_sdf
+ *   BCE (alpha 50 doubled past iteration 10k, 20k, ... as crit.sdf_mask_crit) and the image MSE over
+ *   mask_at_box (NULL: every ray). ACCUMULATES the gradients of every tensor of anr_sdf_params into
+ *   grads (state_dict order; resd_latent, never read, may be NULL). loss (device float[8]) = {loss,
+ *   offset_loss, grad_loss, ograd_loss, mask_loss, img_loss, observed rows, msk_sdf entries}.
+ *   out: rgb_map / acc_map / depth_map (R), tbounds_out (widened) or NULL; raw / sdf unused.
+ *   Perturbation through o->t_rand; o->norm_th = 0.1. Two host reads (kept and observed counts). */
+size_t anr_sdf_train_workspace_bytes(int n_rays, const anr_render_opts* o);
+int anr_sdf_train_step(const anr_sdf_params* p, float* const* grads, const anr_sdf_frame* f, const float* ray_o,
+                       const float* ray_d, const float* near_, const float* far_, int n_rays, const anr_render_opts* o,
+                       const float* rgb_gt, const uint8_t* mask_at_box, int iter_step, const anr_sdf_render_out* out,
+                       float* loss, void* workspace, size_t ws_bytes, void* stream);
 
 /* ---- (f) mesh path (lib/networks/renderer/aninerf_mesh_renderer.py) ----------------------
  * anr_alpha_points: raw alpha (no activation, no bbox mask) of n free world points, zero where the
