@@ -76,13 +76,13 @@ __host__ __device__ constexpr LayerDesc layer_desc(int i) {
 // layer 30: alpha_fc alone (TPoseHuman.calculate_alpha :241-250, the density-only program of the
 // mesh path's get_alpha); the same weights as out-block 16 of layer 17
 #define ANR_L_ALPHA 30
-#define ANR_NUM_LAYERS_ALL 31  // layers of the fp32 image (the folded head below is bf16x3-only)
-// layer 31 (bf16x3 image only): the folded colour head. feature_fc -> [|| nf_latent] latent_fc ->
+#define ANR_NUM_LAYERS_ALL 32  // layers of the fp32 image (0..30 above + the folded head 31 below)
+// layer 31: the folded colour head (both images; the render program of either kernel). feature_fc -> [|| nf_latent] latent_fc ->
 // [|| gamma(dir)] view_fc has no activation before view_fc's ReLU (tpose_nerf_network.py:260-272), so
 // view_fc's pre-activation is (Wv_f Wl_f Wf) net + Wv_d gamma(dir) + c(latent): one 283-input layer
 // of 128 outputs, with alpha_fc stacked as output row 128 (out-block 8, no ReLU). Weights: the head
 // tensor H (129 x 283) that k_pack_head composes in fp64 inside the packed buffer; per-frame bias
-// c = P nf_latent[li] + q (k_prep). Render program V = 2 (anr_mlp_body.h).
+// c = P nf_latent[li] + q (k_prep). Render program V = 2 (anr_mlp_body.h), fp32 and bf16x3 alike.
 #define ANR_L_HEAD 31
 #define ANR_HEAD_T 65  // PackArgs tensor index of H
 #define ANR_NOVEL_T0 46  // tensor index of novel_pose_bw.bw_latent.weight in the packer's list

@@ -90,8 +90,9 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 //   mode 1 bf16x3 (k_mlp_b16; the pose pass too unless built with ANR_POSE_MODE=2);
 //   mode 2 bf16x6, fp32-level (the pose pass with ANR_POSE_MODE=2: measured unnecessary, the
 //          outputs' error vs the fp32 oracle stays <= 4e-6 with x3, tools/precision_report.py).
-//   V = 2 (render, bf16x3 kernel): entries 0..25 as V = 0, 26 the folded colour head (layer 31:
-//         view_fc's pre-activation || alpha_fc, anr_layers.h ANR_L_HEAD), 27 rgb_fc.
+//   V = 2 (render, both kernels): entries 0..25 as V = 0, 26 the folded colour head (layer 31:
+//         view_fc's pre-activation || alpha_fc, anr_layers.h ANR_L_HEAD), 27 rgb_fc. V = 0 (the
+//         reference's unfolded head) sizes the bias table and is no longer run.
 template <int V>
 __host__ __device__ constexpr int prog_len() { return V == 0 ? 30 : V == 2 ? 28 : 18; }
 template <int V>
@@ -943,8 +944,8 @@ __device__ __forceinline__ void bw_mlp(Pipe& p, const float (&emb)[16], const fl
 
 template <bool B16>
 __device__ __forceinline__ void mlp_body(const MlpArgs& a) {
-  // the exact fp32 kernel runs the reference's layer sequence; the bf16x3 kernel the folded head
-  constexpr int V = B16 ? 2 : 0;
+  // both kernels run the folded colour head (anr_layers.h ANR_L_HEAD): 131,072 fewer MACs per sample
+  constexpr int V = 2;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -1018,27 +1019,18 @@ __device__ __forceinline__ void mlp_body(const MlpArgs& a) {
     layer<B16, V, 24, true, true>(p, B, emb, vemb, A, sb, g, lane);
     layer<B16, V, 25, true, true>(p, A, emb, vemb, B, sb, g, lane);
     float sigma_raw;
-    if constexpr (V == 2) {
-      embed_b<1>(dir, g, 4, vemb);
-      layer<B16, V, 26, false, true>(p, B, emb, vemb, A, sb, g, lane);  // view_fc pre-activation || alpha
-      sigma_raw = __shfl(A[8][0], pl);
-      if constexpr (!x3_stream_layer<ANR_L_RGB>()) {  // else rgb_fc applies view_fc's ReLU in its split
-        static_for<0, 8>([&](auto ob) {
-          constexpr int o = decltype(ob)::value;
+    if constexpr (B16) embed_b<1>(dir, g, 4, vemb);
+    else embed<8>(dir, g, 4, vemb);
+    layer<B16, V, 26, false, true>(p, B, emb, vemb, A, sb, g, lane);  // view_fc pre-activation || alpha
+    sigma_raw = __shfl(A[8][0], pl);
+    if constexpr (!(B16 && x3_stream_layer<ANR_L_RGB>())) {  // else rgb_fc applies view_fc's ReLU in its split
+      static_for<0, 8>([&](auto ob) {
+        constexpr int o = decltype(ob)::value;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) A[o][r] = fmaxf(A[o][r], 0.0f);
-        });
-      }
-      layer<B16, V, 27, false, true>(p, A, emb, vemb, B, sb, g, lane);  // rgb_fc
-    } else {
-      layer<B16, V, 26, false>(p, B, emb, vemb, A, sb, g, lane);  // feature || alpha
-      sigma_raw = __shfl(A[16][0], pl);
-      layer<B16, V, 27, false>(p, A, emb, vemb, B, sb, g, lane);  // latent_fc
-      if constexpr (B16) embed_b<1>(dir, g, 4, vemb);
-      else embed<8>(dir, g, 4, vemb);
-      layer<B16, V, 28, true>(p, B, emb, vemb, A, sb, g, lane);   // view_fc
-      layer<B16, V, 29, false>(p, A, emb, vemb, B, sb, g, lane);  // rgb_fc
+        for (int r = 0; r < 4; ++r) A[o][r] = fmaxf(A[o][r], 0.0f);
+      });
     }
+    layer<B16, V, 27, false, true>(p, A, emb, vemb, B, sb, g, lane);  // rgb_fc
 
     // ---- bbox mask, activations, outputs
     bool inside = true;

@@ -50,7 +50,7 @@ __global__ void k_pack_bias(PackArgs a) {
   const int n = e - bias_offset(L);
   const int main_n = ((d.nout + 15) / 16) * 16;
   float v = 0.0f;
-  if (a.t[d.tensor_b] == nullptr) v = 0.0f;
+  if (d.tensor_b < 0 || a.t[d.tensor_b] == nullptr) v = 0.0f;  // the folded head's bias is per frame (k_prep)
   else if (n < d.nout) v = a.t[d.tensor_b][n];
   else if (d.tensor_w2 >= 0 && n >= main_n && n - main_n < d.nout2) v = a.t[d.tensor_b2][n - main_n];
   ((float*)(a.out + weights_bytes()))[e] = v;

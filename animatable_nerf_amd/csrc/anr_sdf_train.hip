@@ -372,7 +372,7 @@ __global__ void k_st_loss_final(const float* acc, const float* acc3, const int* 
   tot += ml;
   tot += img;
   loss[0] = tot; loss[1] = off; loss[2] = gl; loss[3] = og; loss[4] = ml; loss[5] = img;
-  loss[6] = (float)n_o; loss[7] = acc[6];
+  loss[6] = (float)n_o; loss[7] = acc[6]; loss[8] = n; loss[9] = 0.f;
 }
 
 // tanh head of the residual net, r = 0.05 tanh(y): tangent rdot = 0.05 (1 - tau^2) ydot, t = x + r

@@ -12,7 +12,7 @@ forward-over-reverse (anr_sdf_train.hip). One call returns the losses AND every 
   Function), so the reference ``Trainer.train`` loop (clip_grad_value_, Adam) runs unchanged.
   ``batch['iter_step']`` sets the mask-loss alpha schedule, as in the reference.
 * ``SdfStep(net)`` — the native loop: the 63 tensors (1,432,510 floats) and their gradients in flat
-  HBM blobs with the 8 loss floats in the gradient blob's tail, so one RCCL mean all-reduce carries
+  HBM blobs with the loss floats (LOSS_KEYS) in the gradient blob's tail, so one RCCL mean all-reduce carries
   gradients and losses (DDP semantics, trainer.py:13-18); then clip + Adam (``anr_adam``).
 """
 import ctypes
@@ -24,12 +24,14 @@ from . import config as _config
 from .parallel import GradBuckets, broadcast_
 from .renderer_sdf import Renderer
 
-LOSS_KEYS = ('loss', 'offset_loss', 'grad_loss', 'ograd_loss', 'mask_loss', 'img_loss', 'n_observed', 'msk_len')
+LOSS_KEYS = ('loss', 'offset_loss', 'grad_loss', 'ograd_loss', 'mask_loss', 'img_loss', 'n_observed', 'msk_len',
+             'n_kept', 'reserved')
+NLOSS = len(LOSS_KEYS)
 
 
 def sdf_train_step(renderer, batch, grads, loss8, t_rand=None, iter_step=None):
     """One anr_sdf_train_step: ACCUMULATES the gradients of the 63 tensors into ``grads`` (list,
-    state_dict order) and writes the 8 loss floats into ``loss8`` (device, no host sync of its own).
+    state_dict order) and writes the NLOSS loss floats into ``loss8`` (device, no host sync of its own).
     Returns {'rgb_map', 'acc_map', 'depth_map'} and widens ``batch['tbounds']`` in place."""
     lib = renderer.lib
     c = renderer.prepare(batch, t_rand)
@@ -63,10 +65,10 @@ class _SdfLoss(torch.autograd.Function):
     @staticmethod
     def forward(ctx, renderer, batch, t_rand, *params):
         grads = [torch.zeros_like(t) for t in params]
-        loss8 = torch.zeros(8, device=params[0].device)
+        loss8 = torch.zeros(NLOSS, device=params[0].device)
         renderer.last_ret = sdf_train_step(renderer, batch, grads, loss8, t_rand)
         ctx.grads = grads
-        return tuple(loss8[k] for k in range(6)) + (loss8[6:8].detach().clone(),)
+        return tuple(loss8[k] for k in range(6)) + (loss8[6:].detach().clone(),)
 
     @staticmethod
     def backward(ctx, d_loss, *_):
@@ -108,7 +110,7 @@ class SdfStep:
         dev = ps[0].device
         n = sum(p.numel() for p in ps)
         self.flat = torch.empty(n, device=dev)
-        self.grad = torch.zeros(n + 8, device=dev)
+        self.grad = torch.zeros(n + NLOSS, device=dev)
         self.m = torch.zeros(n, device=dev)
         self.v = torch.zeros(n, device=dev)
         self.grad_views = []
@@ -120,8 +122,8 @@ class SdfStep:
             self.grad_views.append(self.grad[off:off + k].view_as(p))
             off += k
         self.n, self.t = n, 0
-        self.loss8 = self.grad[n:n + 8]
-        self.buckets = GradBuckets(self.grad, [(0, n + 8)], group)
+        self.loss8 = self.grad[n:n + NLOSS]
+        self.buckets = GradBuckets(self.grad, [(0, n + NLOSS)], group)
         self.iter_step = 0
         broadcast_(self.flat, 0, group)  # DDP semantics: every replica starts from rank 0's weights
 

@@ -63,9 +63,10 @@ def parse():
     ap.add_argument('--rays', type=int, default=512 * 512)
     ap.add_argument('--cpu-rays', type=int, default=16 * 2048)
     ap.add_argument('--no-cpu', action='store_true')
-    ap.add_argument('--mode', choices=('render', 'train', 'sdf', 'mesh', 'anim'), default='render',
+    ap.add_argument('--mode', choices=('render', 'train', 'sdf', 'sdf-train', 'mesh', 'anim'), default='render',
                     help='render: config 2 (headline); train: config 3/4 training step (1024 rays/GPU); '
-                         'sdf: config 5 sdf_pdf full-frame render; mesh: aninerf mesh extraction '
+                         'sdf: config 5 sdf_pdf full-frame render; sdf-train: config 5 training step '
+                         '(1024 rays/GPU, second-order losses, RCCL all-reduce); mesh: aninerf mesh extraction '
                          '(get_alpha on the 5 mm voxel grid + marching cubes); anim: animation-stage '
                          'training step (2 x 65,536 points, novel_pose_bw)')
     ap.add_argument('--voxel', type=float, default=0.005, help='mesh mode: cfg.voxel_size (aninerf_s9p.yaml:95)')
@@ -219,6 +220,8 @@ def main():
         return bench_mesh(args, rank, world, dev)
     if args.mode == 'anim':
         return bench_anim(args, rank, world, dev)
+    if args.mode == 'sdf-train':
+        return bench_sdf_train(args, rank, world, dev)
 
     sc = synthetic.Scene(vsize=0.025)
     ro, rd = sc.box_rays(args.rays, seed=2 if args.shard_frame else 2 + rank)
@@ -531,6 +534,88 @@ def bench_sdf(args, rank, world, dev):
                                   'sample': f'first {n} rays of the frame, oracle/restate_sdf.py, {dtc:.1f} s'}
         from oracle import restate
         result['psnr_vs_fp32_oracle'] = float(restate.psnr(out['rgb_map'][0, :n].cpu().numpy(), ref['rgb_map'][0].numpy()))
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+# sdf_pdf training, MAC per kept sample executed by anr_sdf_train_step (exact fp32 MFMA): forward (residual
+# 528,640 + SDF 524,544 + its input gradient 459,008 + colour 304,128), colour backward (dW + dX 2 x 304,128),
+# SDF tangent pass 524,544, stacked SDF reverse (dX over 2n rows + dW of both halves: 4 x 524,544), residual
+# backward (dW + dX 2 x 528,640); the observed-gradient rows (|sdf| < 0.02) add their own passes on top
+MAC_SDF_TRAIN = (528_640 + 524_544 + 459_008 + 304_128) + 2 * 304_128 + 524_544 + 4 * 524_544 + 2 * 528_640
+
+
+def bench_sdf_train(args, rank, world, dev):
+    """Config 5's training leg: one tpose_trainer step of the sdf_pdf network per GPU on 1,024 rays
+    (N_rand, perturb 1): anr_sdf_train_step (forward, second-order losses, every gradient) + RCCL mean
+    all-reduce of the 1,432,510-float gradient blob with the losses in its tail (N > 1) + clip + Adam.
+    Weak scaling: every rank trains on its own batch (DDP semantics)."""
+    from animatable_nerf_amd import config, network, network_sdf, synthetic
+    from animatable_nerf_amd.renderer import near_far
+    from animatable_nerf_amd.trainer_sdf import LOSS_KEYS, SdfStep
+    sc = synthetic.PdfScene(vsize=0.05)
+    batches = []
+    nb = max(1, min(4, args.steps + args.warmup))
+    for j in range(nb):
+        ro, rd = sc.box_rays(args.train_rays * 2, seed=2000 + 97 * rank + j)
+        nr, fr, m = near_far(torch.from_numpy(sc.pbounds).to(dev), torch.from_numpy(ro).to(dev),
+                             torch.from_numpy(rd).to(dev))
+        m_np = m.cpu().numpy()
+        rgb = np.random.default_rng(j + 31 * rank).random((len(ro), 3)).astype(np.float32)
+        b = sc.batch_arrays(ro[m_np][:args.train_rays], rd[m_np][:args.train_rays],
+                            nr.cpu().numpy()[:args.train_rays], fr.cpu().numpy()[:args.train_rays], latent_index=7,
+                            rgb=rgb[m_np][:args.train_rays])
+        bt = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in b.items()}
+        bt['iter_step'] = 12000
+        batches.append(bt)
+    tb0 = [b['tbounds'].clone() for b in batches]
+    cfg = config.defaults()
+    cfg.num_train_frame = 260
+    cfg.perturb = 1
+    net = network_sdf.Network(cfg)
+    sd = synthetic.init_state_dict_sdf({k: tuple(v.shape) for k, v in net.state_dict().items()})
+    network.load_numpy_state(net, sd)
+    net = net.to(dev)
+    net.train()
+    step = SdfStep(net, cfg)
+
+    def one(j):
+        k = j % nb
+        batches[k]['tbounds'].copy_(tb0[k])
+        return step.step(batches[k])
+    for j in range(args.warmup):
+        one(j)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for j in range(args.steps):
+        l8 = one(args.warmup + j)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt_max = max_over_ranks(time.perf_counter() - t0, dev, world)
+    R = int(batches[0]['ray_o'].shape[1])
+    losses = dict(zip(LOSS_KEYS, l8.cpu().tolist()))  # rank means (the losses ride in the all-reduced blob)
+    n_kept = losses['n_kept']
+    achieved = n_kept * 2 * MAC_SDF_TRAIN / (dt_max / args.steps) / 1e12
+    result = {
+        'metric': 'sdf_pdf training ray-samples/s (1024 rays x 64 samples per GPU per step)',
+        'value': R * 64 * args.steps * world / dt_max, 'unit': 'ray-samples/s', 'n_gpus': world, 'steps': args.steps,
+        'warmup': args.warmup, 'ms_per_step': dt_max / args.steps * 1e3, 'higher_is_better': True, 'scaling': 'weak',
+        'vs_baseline': None, 'dtype': 'fp32', 'data': 'synthetic',
+        'config': {'workload': 'sdf_pdf training step (config 5: tpose_trainer losses incl. eikonal, observed '
+                               'gradients, msk_sdf BCE, image MSE; Adam)', 'rays_per_gpu': R,
+                   'parallelism': f'dp{world} (RCCL mean all-reduce of the 1,432,510-float gradient blob + losses)'},
+        'roofline': {'bound': 'mfma', 'kernel': 'whole step (layer GEMMs dominate)', 'achieved': achieved,
+                     'peak': PEAK_FP32_MFMA_TFLOPS, 'unit': 'TFLOP/s', 'frac': achieved / PEAK_FP32_MFMA_TFLOPS,
+                     'traffic': None, 'flop_per_kept_executed_main_path': 2 * MAC_SDF_TRAIN,
+                     'kept_samples_per_step': n_kept},
+        'losses_last_step_rank_mean': losses,
+    }
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

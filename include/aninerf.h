@@ -344,8 +344,9 @@ int anr_sdf_render_rows(const void* workspace, int n_rays, const anr_render_opts
  *   offset 0.01 mean|resd|, eikonal 0.01 mean(|g|-1)^2 (gradients and observed_gradients), msk_sdf
  *   BCE (alpha 50 doubled past iteration 10k, 20k, ... as crit.sdf_mask_crit) and the image MSE over
  *   mask_at_box (NULL: every ray). ACCUMULATES the gradients of every tensor of anr_sdf_params into
- *   grads (state_dict order; resd_latent, never read, may be NULL). loss (device float[8]) = {loss,
- *   offset_loss, grad_loss, ograd_loss, mask_loss, img_loss, observed rows, msk_sdf entries}.
+ *   grads (state_dict order; resd_latent, never read, may be NULL). loss (device float[10]) = {loss,
+ *   offset_loss, grad_loss, ograd_loss, mask_loss, img_loss, observed rows, msk_sdf entries, kept
+ *   samples, 0}.
  *   out: rgb_map / acc_map / depth_map (R), tbounds_out (widened) or NULL; raw / sdf unused.
  *   Perturbation through o->t_rand; o->norm_th = 0.1. Two host reads (kept and observed counts). */
 size_t anr_sdf_train_workspace_bytes(int n_rays, const anr_render_opts* o);

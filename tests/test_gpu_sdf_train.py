@@ -36,7 +36,7 @@ def _device_step(dev, b, t_rand, iter_step):
     cfg.perturb = 1
     r = Renderer(net, cfg)
     grads = [torch.zeros_like(t) for t in net.tensors()]
-    loss8 = torch.zeros(8, device=dev)
+    loss8 = torch.zeros(trainer_sdf.NLOSS, device=dev)
     bd = {k: (v.to(dev) if torch.is_tensor(v) else v) for k, v in b.items()}
     ret = trainer_sdf.sdf_train_step(r, bd, grads, loss8, t_rand.to(dev), iter_step=iter_step)
     torch.cuda.synchronize()
