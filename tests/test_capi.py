@@ -38,7 +38,8 @@ def test_version_and_sizes(lib):
     # 19 weight layers + view/rgb heads, fp32 weight image + padded biases
     # + 9 novel_pose_bw layers (same image as the 9 BW layers)
     # + alpha_fc alone (layer 30, the mesh path's density program): 64 k-steps x 1 KiB, 16 biases
-    fp32 = 4_767_744 + 2_031_616 + 65_536 + 4 * (4_800 + 2_080 + 16)  # fp32 image (+ novel copy, alpha) + biases
+    # + the folded colour head (layer 31: 72 k-steps x 3 chunks x 1 KiB, 9 x 16 biases from the per-frame fold)
+    fp32 = 4_767_744 + 2_031_616 + 65_536 + 221_184 + 4 * (4_800 + 2_080 + 16 + 144)  # fp32 image + biases
     # bf16x3 image: per layer ceil(in/32) k-steps x out-blocks x 2 KiB (hi + lo fragments)
     ks_ob = [(2, 16), (8, 16), (8, 16), (8, 16), (8, 16), (10, 16), (8, 16), (8, 16), (8, 2),
              (2, 16), (8, 16), (8, 16), (8, 16), (8, 16), (10, 16), (8, 16), (8, 16), (8, 17), (8, 16), (9, 8), (4, 1)]

@@ -17,7 +17,7 @@ TAG=$1
 shift
 mkdir -p gpurun_out
 args_of() { echo "$1" | tr ',' ' '; }
-mode_of() { echo "$1" | sed -n 's/.*--mode,\([a-z]*\).*/_\1/p'; }
+mode_of() { echo "$1" | sed -n 's/.*--mode,\([a-z-]*\).*/_\1/p'; }
 for step in "$@"; do
   kind=${step%%:*}
   rest=${step#*:}
