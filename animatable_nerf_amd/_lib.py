@@ -29,7 +29,7 @@ EXPORTS = ('anr_near_far', 'anr_params_packed_bytes', 'anr_params_pack', 'anr_re
            'anr_network_workspace_bytes', 'anr_network_fwd', 'anr_network_counts', 'anr_network_bw_rows',
            'anr_network_train_workspace_bytes', 'anr_network_train_fwd', 'anr_network_train_bwd',
            'anr_points_workspace_bytes', 'anr_blend_weights', 'anr_canonical_alpha', 'anr_train_step_hooked',
-           'anr_sdf_train_workspace_bytes', 'anr_sdf_train_step',
+           'anr_sdf_train_workspace_bytes', 'anr_sdf_train_step', 'anr_sdf_render_knn',
            'anr_last_error', 'anr_version')
 
 c_float_p = ctypes.c_void_p
@@ -136,6 +136,8 @@ def load():
                                        ctypes.POINTER(RenderOpts), ctypes.POINTER(SdfRenderOut), P, ctypes.c_size_t, P]
     lib.anr_sdf_render_counts.restype = P
     lib.anr_sdf_render_counts.argtypes = [P, ctypes.c_int, ctypes.POINTER(RenderOpts)]
+    lib.anr_sdf_render_knn.restype = P
+    lib.anr_sdf_render_knn.argtypes = [P, ctypes.c_int, ctypes.POINTER(RenderOpts)]
     lib.anr_sdf_render_rows.argtypes = [P, ctypes.c_int, ctypes.POINTER(RenderOpts), P, P, P, P, P]
     lib.anr_sdf_train_workspace_bytes.restype = ctypes.c_size_t
     lib.anr_sdf_train_workspace_bytes.argtypes = [ctypes.c_int, ctypes.POINTER(RenderOpts)]

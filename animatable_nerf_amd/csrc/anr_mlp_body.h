@@ -32,15 +32,6 @@ __device__ __forceinline__ void static_for(F&& f) {
 
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-// slice certification halfway through the previous slice (Pipe::mid) instead of at slice entry
-#ifndef ANR_MIDSYNC
-#define ANR_MIDSYNC 1
-#endif
-// waves that issue the weight stream: 8 (all, default) or 4 (one per SIMD: waves w and w+4 share a
-// SIMD, so while one issues its LDS-DMA pieces the other keeps the SIMD's MFMA pipe busy)
-#ifndef ANR_DMA_WAVES
-#define ANR_DMA_WAVES 8
-#endif
 // LDS fragment reads in flight ahead of the MFMAs (bf16x3 layers)
 #ifndef ANR_FRAG_PF
 #define ANR_FRAG_PF 3
@@ -51,33 +42,9 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 #ifndef ANR_DMA_SPREAD
 #define ANR_DMA_SPREAD 1
 #endif
-// LDS-DMA source as scalar base + constant lane offset (global_load_lds saddr form)
-#ifndef ANR_DMA_SADDR
-#define ANR_DMA_SADDR 1
-#endif
-// cache policy bits of the weight-stream LDS-DMA (e.g. " nt"); default policy
-#ifndef ANR_DMA_CPOL_ID
-#define ANR_DMA_CPOL_ID 0
-#endif
-#if ANR_DMA_CPOL_ID == 1
-#define ANR_DMA_CPOL " nt"
-#elif ANR_DMA_CPOL_ID == 2
-#define ANR_DMA_CPOL " sc1"
-#else
-#define ANR_DMA_CPOL ""
-#endif
-// outputs (raw, sigma', pbw/tbw rows) stored non-temporal, keeping them out of the L2 the weight
-// stream lives in
-#ifndef ANR_NT_OUT
-#define ANR_NT_OUT 0
-#endif
 // bf16x3 kernels: hardware log/exp/rcp in the blend softmax and reciprocal-based lookup coordinates
 #ifndef ANR_FAST_MATH
 #define ANR_FAST_MATH 1
-#endif
-// slice certification by a raw s_barrier instead of __syncthreads() (whose fence waits lgkmcnt(0))
-#ifndef ANR_RAW_BARRIER
-#define ANR_RAW_BARRIER 0
 #endif
 
 // The per-tile layer program, variant V:
@@ -156,7 +123,7 @@ __host__ __device__ constexpr int prog_advance(int e, int q, int d) {
 template <bool B16, int V>
 __host__ __device__ constexpr int prog_later_loads(int e, int q) {
   int n = 0;
-  for (int d = 1; d <= mlp_nbuf<B16>() - 2 - ANR_MIDSYNC; ++d) {
+  for (int d = 1; d <= mlp_nbuf<B16>() - 3; ++d) {
     const int eq = prog_advance<B16, V>(e, q, d);
     n += prog_slice_loads<B16, V>(eq / 1024, eq % 1024);
   }
@@ -204,38 +171,22 @@ struct Pipe {
 #ifdef ANR_EXP_SAMEDMA
     off = 0;  // timing experiment only: every slice re-reads the first 32 KiB (L2-resident footprint)
 #endif
-    if constexpr (ANR_DMA_WAVES == 4) {
-      if (wave >= 4) return;
-      loads *= 2;
-    }
     for (int i = first; i < loads; ++i) {
-      int piece = wave + ANR_DMA_WAVES * i;
+      int piece = wave + 8 * i;
       piece = piece < kb ? piece : kb - 1;
       const unsigned m0 = dst + piece * 1024;
-#if ANR_DMA_SADDR
       // wave-uniform piece: the whole source offset in the scalar base, the lane's 16 B in a
       // constant VGPR (no per-piece vector address arithmetic)
       const unsigned char* sbase = w + off + piece * 1024;
-      asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ANR_DMA_CPOL ::"v"(lane * 16), "s"(sbase),
-                   "s"(m0)
+      asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(lane * 16), "s"(sbase), "s"(m0)
                    : "memory");
-#else
-      const unsigned char* src = w + off + piece * 1024 + lane * 16;
-      asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(m0)
-                   : "memory");
-#endif
     }
   }
 
   // wait until this wave's pieces of all but the last N (8-wave count) issued pieces have landed
   template <int N>
   __device__ __forceinline__ void wait_stream() {
-    if constexpr (ANR_DMA_WAVES == 4) {
-      if (wave < 4) wait_vmcnt<2 * N>();
-      else wait_vmcnt<0>();
-    } else {
-      wait_vmcnt<N>();
-    }
+    wait_vmcnt<N>();
   }
 
   template <bool B16, int V, int E, int Q>
@@ -244,7 +195,7 @@ struct Pipe {
     stage(off + (prog_pose(E) ? pose_woff : 0), prog_slice_kb<B16, V>(E, Q), prog_slice_loads<B16, V>(E, Q), buf);
   }
 
-  // prologue: slices 0 .. nbuf-2 of the program; with ANR_MIDSYNC slice 0 is certified here
+  // prologue: slices 0 .. nbuf-2 of the program; slice 0 is certified here
   template <bool B16, int V>
   __device__ __forceinline__ void start() {
     static_for<0, mlp_nbuf<B16>() - 1>([&](auto d) {
@@ -252,57 +203,36 @@ struct Pipe {
       stage_slice<B16, V, eq / 1024, eq % 1024>(decltype(d)::value);
     });
     cur = 0;
-    if constexpr (ANR_MIDSYNC) {
-      wait_stream<prog_later_loads<B16, V>(0, 0)>();
-      __syncthreads();
-    }
+    wait_stream<prog_later_loads<B16, V>(0, 0)>();
+    __syncthreads();
   }
 
-  // Enter slice Q of program entry E.
-  //   ANR_MIDSYNC = 0: wait for it (its own loads; the barrier covers the other waves'), then
-  //   refill the slot freed by the previous slice with the slice nbuf-1 ahead.
-  //   ANR_MIDSYNC = 1: it was certified by mid() of the previous slice: no wait, no barrier, so the
-  //   first MFMAs of a slice follow the last ones of the previous slice without a pipe bubble.
+  // Enter slice Q of program entry E: it was certified by mid() of the previous slice, so no wait
+  // and no barrier here and the first MFMAs of a slice follow the last ones of the previous slice
+  // without a pipe bubble.
   template <bool B16, int V, int E, int Q>
   __device__ __forceinline__ const unsigned char* enter() {
-    if constexpr (!ANR_MIDSYNC) {
-      constexpr int NB = mlp_nbuf<B16>();
-      constexpr int eq = prog_advance<B16, V>(E, Q, NB - 1);
-      wait_stream<prog_later_loads<B16, V>(E, Q)>();
-      __syncthreads();
-      int slot = cur + NB - 1;
-      slot = slot >= NB ? slot - NB : slot;
-      stage_slice<B16, V, eq / 1024, eq % 1024>(slot);
-    }
     return lds + cur * smax;
   }
-  // ANR_MIDSYNC: called halfway through slice (E, Q), while its MFMAs are in flight: certify the next
-  // slice (own loads landed + barrier: everyone's landed, and everyone is past the previous slice),
-  // then refill the previous slice's slot with the slice nbuf-1 ahead.
+  // Called halfway through slice (E, Q), while its MFMAs are in flight: certify the next slice (own
+  // loads landed + barrier: everyone's landed, and everyone is past the previous slice), then refill
+  // the previous slice's slot with the slice nbuf-1 ahead.
   // SPREAD: only certify and pick the slot here; the refill's pieces follow through piece<>().
   template <bool B16, int V, int E, int Q, bool SPREAD = false>
   __device__ __forceinline__ void mid() {
-    if constexpr (ANR_MIDSYNC) {
-      constexpr int NB = mlp_nbuf<B16>();
-      constexpr int e1 = prog_advance<B16, V>(E, Q, 1);
-      constexpr int eq = prog_advance<B16, V>(E, Q, NB - 1);
+    constexpr int NB = mlp_nbuf<B16>();
+    constexpr int e1 = prog_advance<B16, V>(E, Q, 1);
+    constexpr int eq = prog_advance<B16, V>(E, Q, NB - 1);
 #ifndef ANR_EXP_NOWAIT
-      wait_stream<prog_later_loads<B16, V>(e1 / 1024, e1 % 1024)>();
+    wait_stream<prog_later_loads<B16, V>(e1 / 1024, e1 % 1024)>();
 #endif
 #ifndef ANR_EXP_NOBAR
-#if ANR_RAW_BARRIER
-      // raw barrier: no fence, so fragment reads still in flight (this slice's, out-blocks ahead)
-      // survive it; every read of the slot refilled next was consumed by the previous slice's MFMAs
-      __builtin_amdgcn_s_barrier();
-#else
-      __syncthreads();
+    __syncthreads();
 #endif
-#endif
-      int slot = cur + NB - 1;
-      slot = slot >= NB ? slot - NB : slot;
-      if constexpr (SPREAD) pend = slot;
-      else stage_slice<B16, V, eq / 1024, eq % 1024>(slot);
-    }
+    int slot = cur + NB - 1;
+    slot = slot >= NB ? slot - NB : slot;
+    if constexpr (SPREAD) pend = slot;
+    else stage_slice<B16, V, eq / 1024, eq % 1024>(slot);
   }
   // pieces [I0, I1) of this wave's share of the refill picked by mid<..., true>() of slice (E, Q)
   template <bool B16, int V, int E, int Q, int I0, int I1>
@@ -916,13 +846,8 @@ __device__ __forceinline__ void lbs_inverse(const f32x4 (&bw)[2], const float* _
 
 __device__ __forceinline__ void store_rows(float* __restrict__ rows, int idx, const f32x4 (&bw)[2], int g, bool valid) {
   if (!valid) return;
-#if ANR_NT_OUT
-  __builtin_nontemporal_store(bw[0], (f32x4*)(rows + (size_t)idx * 24 + 4 * g));
-  if (g < 2) __builtin_nontemporal_store(bw[1], (f32x4*)(rows + (size_t)idx * 24 + 16 + 4 * g));
-#else
   *(f32x4*)(rows + (size_t)idx * 24 + 4 * g) = bw[0];
   if (g < 2) *(f32x4*)(rows + (size_t)idx * 24 + 16 + 4 * g) = bw[1];
-#endif
 }
 
 // BW MLP pass starting at program entry E0 (0: pose pass; 9: T-pose pass). The pose pass may read
@@ -1043,13 +968,8 @@ __device__ __forceinline__ void mlp_body(const MlpArgs& a) {
       r.y = 1.0f / (1.0f + expf(-B[0][1]));
       r.z = 1.0f / (1.0f + expf(-B[0][2]));
       r.w = 1.0f - expf(-fmaxf(sig, 0.0f) * dist);
-#if ANR_NT_OUT
-      __builtin_nontemporal_store(f32x4{r.x, r.y, r.z, r.w}, (f32x4*)(a.raw + pid));
-      __builtin_nontemporal_store(sig, a.sigma + idx);
-#else
       a.raw[pid] = r;
       a.sigma[idx] = sig;
-#endif
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the last (unused) prefetch

@@ -247,6 +247,11 @@ const int32_t* anr_sdf_render_counts(const void* workspace, int n_rays, const an
   return (const int32_t*)((const char*)workspace + slayout(n_rays, o->chunk).counts);
 }
 
+const uint32_t* anr_sdf_render_knn(const void* workspace, int n_rays, const anr_render_opts* o) {
+  if (!workspace || !o || o->chunk <= 0 || n_rays <= 0) return nullptr;
+  return (const uint32_t*)((const char*)workspace + slayout(n_rays, o->chunk).knn);
+}
+
 int anr_sdf_render_rows(const void* workspace, int n_rays, const anr_render_opts* o, float* resd, float* gradients,
                         float* msk_sdf, float* msk_label, void* stream) {
   if (!workspace || !o || o->chunk <= 0) return fail(ANR_E_ARG, "anr_sdf_render_rows: bad arguments");

@@ -134,8 +134,19 @@ class Renderer:
                                                 _lib.ptr(msk_sdf), _lib.ptr(msk_label), st), 'anr_sdf_render_rows')
         with torch.no_grad():
             batch['tbounds'].copy_(tb_out.view_as(batch['tbounds']))
+        self._last_R, self._last_opts = R, o
         return {'raw': raw, 'sdf': sdf, 'resd': resd, 'gradients': grad, 'rgb_map': rgb, 'acc_map': acc,
                 'depth_map': depth, 'msk_sdf': msk_sdf, 'msk_label': msk_label}
+
+    def knn_records(self):
+        """(R*64, 8) uint32 view of the last render's KNN records (anr_sdf_render_knn): w0..w4 float
+        bits, then the five vertex indices packed as i0 | i1 << 16, i2 | i3 << 16, i4 (tests, debugging)."""
+        R = self._last_R
+        addr = self.lib.anr_sdf_render_knn(_lib.ptr(self._ws), R, ctypes.byref(self._last_opts))
+        if not addr:
+            raise RuntimeError('anr_sdf_render_knn: no records')
+        off = addr - self._ws.data_ptr()
+        return self._ws[off:off + R * 64 * 32].view(torch.int32).view(R * 64, 8)
 
     def render(self, batch):
         if torch.is_grad_enabled() and any(p.requires_grad for p in self.net.parameters()) and self.net.training:

@@ -16,8 +16,8 @@ precision: the headline is config 2's fp32: the exact-fp32-MFMA fused kernel k_m
           the same run and reported under ``bf16x3_split`` with its own roofline.
 roofline: the fused network kernel dominates; its per-launch time is measured with hipEvents on the
           render stream (anr_profile_*). k_mlp: SURVEY.md §8(d)'s 2,312,192 credited FLOP per kept
-          sample against the 157.3 TF fp32 MFMA peak (the 3,306,496 FLOP it executes, T-pose BW MLP
-          included, beside it). k_mlp_b16: the bf16 MFMA FLOP it executes against the 2.5 PF dense bf16
+          sample against the 157.3 TF fp32 MFMA peak (the 3,044,352 FLOP it executes, T-pose BW MLP
+          included and the colour head folded, beside it). k_mlp_b16: the bf16 MFMA FLOP it executes against the 2.5 PF dense bf16
           peak, credited figure beside it. traffic: HBM bytes per launch from the committed PMC passes
           (profiles/pmc_latest.json, per kernel).
 baselines (rank 0 at N=1, outside the timed region): cpu_baseline = the oracle (op-for-op PyTorch-CPU
@@ -35,11 +35,12 @@ import torch
 import torch.distributed as dist
 
 FLOP_PER_KEPT = 2_312_192          # render credit (BW pose + NeRF, latent folded)
-FLOP_PER_KEPT_EXECUTED = 3_306_496  # + T-pose BW MLP (tbw rows are part of the render outputs)
 MAC_BW, MAC_NERF = 497_152, 658_944  # per kept sample, latent folded
-# the bf16x3 kernel's NeRF with the folded colour head (anr_layers.h ANR_L_HEAD): trunk 491,008 +
+# the render kernels' NeRF with the folded colour head (anr_layers.h ANR_L_HEAD): trunk 491,008 +
 # alpha_fc 256 + (Wv_f Wl_f Wf || Wv_d) 128 x 283 + rgb_fc 384
 MAC_NERF_FOLDED = 491_008 + 256 + 128 * 283 + 384
+# executed per kept sample: pose-space BW + T-pose BW (the tbw rows are render outputs) + folded NeRF
+FLOP_PER_KEPT_EXECUTED = 2 * (2 * MAC_BW + MAC_NERF_FOLDED)
 PEAK_FP32_MFMA_TFLOPS = 157.3      # MI355X_MICROARCH.md, Peak FP32 (matrix)
 PEAK_BF16_MFMA_TFLOPS = 2500.0     # MI355X_MICROARCH.md, BF16 dense (no sparsity)
 METRIC = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), 'BASELINE.json')))['metric']

@@ -333,6 +333,10 @@ int anr_sdf_render_fwd(const anr_sdf_params* p, const anr_sdf_frame* f, const fl
                        const anr_sdf_render_out* out, void* workspace, size_t ws_bytes, void* stream);
 /* device int32[2] inside the workspace: {kept samples n', msk_sdf length}. */
 const int32_t* anr_sdf_render_counts(const void* workspace, int n_rays, const anr_render_opts* o);
+/* device uint32 (R*64, 8) inside the workspace: the front-end's per-sample KNN records (w0..w4 float
+ * bits, i0 | i1 << 16, i2 | i3 << 16, i4) of the last anr_sdf_render_fwd -- a debugging / test view of
+ * the pytorch3d knn_points boundary (sample_utils.py:309-348). */
+const uint32_t* anr_sdf_render_knn(const void* workspace, int n_rays, const anr_render_opts* o);
 /* copy resd (n',3), gradients (n',3), msk_sdf / msk_label (len) out of the workspace */
 int anr_sdf_render_rows(const void* workspace, int n_rays, const anr_render_opts* o, float* resd, float* gradients,
                         float* msk_sdf, float* msk_label, void* stream);

@@ -143,15 +143,10 @@ def test_full_frame_properties(renderer, dev):
 
 
 def _knn_records(renderer, R):
-    """The front-end's per-sample KNN records (8 uint32: w0..w4 bits, i0|i1<<16, i2|i3<<16, i4) read
-    from the workspace at the offset anr_sdf_capi.hip slayout() gives them."""
-    a256 = lambda x: (x + 255) // 256 * 256
-    N = R * 64
-    nch = (R + 2047) // 2048
-    o = 0
-    for nbytes in (16, R * 8, nch * 8, (R + 1) * 4, ((R + 255) // 256) * 4, N * 4):
-        o = a256(o + nbytes)
-    rec = renderer._ws[o:o + N * 32].view(torch.int32).view(N, 8).cpu().numpy().view(np.uint32)
+    """The front-end's per-sample KNN records (8 uint32: w0..w4 bits, i0|i1<<16, i2|i3<<16, i4), located
+    through the C-ABI (anr_sdf_render_knn)."""
+    rec = renderer.knn_records().cpu().numpy().view(np.uint32)
+    assert rec.shape == (R * 64, 8)
     idx = np.stack([rec[:, 5] & 0xffff, rec[:, 5] >> 16, rec[:, 6] & 0xffff, rec[:, 6] >> 16, rec[:, 7]], 1)
     return rec[:, :5].view(np.float32), idx.astype(np.int64)
 
