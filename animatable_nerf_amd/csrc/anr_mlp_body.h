@@ -162,15 +162,6 @@ struct Pipe {
     // loop (hundreds of loop-invariant 64-bit addresses otherwise spill)
     const unsigned char* w = wimg;
     asm volatile("" : "+s"(w));
-#ifdef ANR_EXP_NODMA
-    return;  // timing experiment only: no weight stream (results are garbage)
-#endif
-#ifdef ANR_EXP_HALFDMA
-    loads = (loads + 1) / 2;  // timing experiment only: half the pieces (results are garbage)
-#endif
-#ifdef ANR_EXP_SAMEDMA
-    off = 0;  // timing experiment only: every slice re-reads the first 32 KiB (L2-resident footprint)
-#endif
     for (int i = first; i < loads; ++i) {
       int piece = wave + 8 * i;
       piece = piece < kb ? piece : kb - 1;
@@ -223,12 +214,8 @@ struct Pipe {
     constexpr int NB = mlp_nbuf<B16>();
     constexpr int e1 = prog_advance<B16, V>(E, Q, 1);
     constexpr int eq = prog_advance<B16, V>(E, Q, NB - 1);
-#ifndef ANR_EXP_NOWAIT
     wait_stream<prog_later_loads<B16, V>(e1 / 1024, e1 % 1024)>();
-#endif
-#ifndef ANR_EXP_NOBAR
     __syncthreads();
-#endif
     int slot = cur + NB - 1;
     slot = slot >= NB ? slot - NB : slot;
     if constexpr (SPREAD) pend = slot;
@@ -250,11 +237,6 @@ struct Pipe {
 
 // x -> hi = bf16(x), lo = bf16(x - hi)   (RNE both)
 __device__ __forceinline__ void split8(const float (&x)[8], bf16x8& hi, bf16x8& lo) {
-#ifdef ANR_EXP_NOSPLIT
-#pragma unroll
-  for (int j = 0; j < 8; ++j) hi[j] = lo[j] = (__bf16)x[j];  // timing experiment only
-  return;
-#endif
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const __bf16 h = (__bf16)x[j];
@@ -663,11 +645,6 @@ __device__ __forceinline__ void embed_b(const float x[3], int h, int nfreq, floa
   // launder the lane half: otherwise the per-lane pair indices of all slots are hoisted out of the
   // tile loop and pin registers for the whole kernel
   asm volatile("" : "+v"(h));
-#ifdef ANR_EXP_NOSTRETCH
-#pragma unroll
-  for (int k = 0; k < 8 * NS; ++k) e[k] = x[k % 3] * (0.1f + 0.01f * k);  // timing experiment only
-  return;
-#endif
   const float m = fmaxf(fabsf(x[0]), fmaxf(fabsf(x[1]), fabsf(x[2])));
   // any lane with arguments past the fast reduction's range takes the library sincos (wave-uniform)
   const bool slow = __builtin_amdgcn_ballot_w64(!(m * (float)(1 << (nfreq - 1)) <= 65536.0f)) != 0;
@@ -733,11 +710,6 @@ __device__ __forceinline__ void lookup24(const float* __restrict__ vol32, const 
   float lo[3], hi[3];
 #pragma unroll
   for (int c = 0; c < 3; ++c) { lo[c] = bounds[c]; hi[c] = bounds[3 + c]; }
-#if defined(ANR_EXP_NOLOOKUP) || defined(ANR_EXP_NOSTRETCH)
-  out[0] = f32x4{0.04f, 0.04f, 0.04f, 0.04f};  // timing experiment only
-  out[1] = out[0];
-  return;
-#endif
   TriCell t;
   if constexpr (FAST) {
     // (p - lo) / ext as (p - lo) * rcp(ext): within 1-2 ulp of the division
@@ -772,11 +744,6 @@ __device__ __forceinline__ void lookup24(const float* __restrict__ vol32, const 
 // eight divisions (relative error ~1e-6 on the weights, inside the 1e-4 output tolerance).
 template <bool FAST = false>
 __device__ __forceinline__ void blend_softmax(const f32x4 (&fc)[2], const f32x4 (&init)[2], int g, f32x4 (&bw)[2]) {
-#ifdef ANR_EXP_NOSTRETCH
-  bw[0] = fc[0] * 0.01f + init[0];  // timing experiment only
-  bw[1] = fc[1] * 0.01f + init[1];
-  return;
-#endif
   float lg[2][4];
   float m = -INFINITY;
 #pragma unroll
@@ -809,10 +776,6 @@ __device__ __forceinline__ void blend_softmax(const f32x4 (&fc)[2], const f32x4 
 // LBS inverse warp: A_b = sum_j bw_j A_j; x_T = inv(A_b[:3,:3]) (x - A_b[:3,3])
 __device__ __forceinline__ void lbs_inverse(const f32x4 (&bw)[2], const float* __restrict__ sA, int g, const float x[3],
                                             float xt[3]) {
-#ifdef ANR_EXP_NOSTRETCH
-  xt[0] = x[0] + bw[0][0]; xt[1] = x[1] + bw[0][1]; xt[2] = x[2] + bw[1][0];  // timing experiment only
-  return;
-#endif
   float Ab[16];
 #pragma unroll
   for (int m = 0; m < 16; ++m) Ab[m] = 0.f;

@@ -270,9 +270,6 @@ __global__ __launch_bounds__(RgCfg<X3>::WAVES * 64) void k_rgemm(RGemm g) {
   const int nc0 = (g.seg[0].K + KC - 1) / KC;
   const int nch = nc0 + (g.nseg > 1 ? (g.seg[1].K + KC - 1) / KC : 0);
   auto issue = [&](int c) {
-#ifdef RG_EXP_NODMA
-    return;  // timing experiment only (results garbage)
-#endif
     const int seg = c < nc0 ? 0 : 1;
     const int kk = (c - (seg ? nc0 : 0)) * KC;
     rg_issue<X3>(g, seg, kk, m0, M, N, base + (c % RG_NS) * RG_SLOT, w, lane);
@@ -301,11 +298,7 @@ __global__ __launch_bounds__(RgCfg<X3>::WAVES * 64) void k_rgemm(RGemm g) {
     const int K = seg ? g.seg[1].K : g.seg[0].K;
     const unsigned char* sA = lds + (c % RG_NS) * RG_SLOT;
     const unsigned char* sB = sA + RG_A_BYTES;
-#ifdef RG_EXP_NOMFMA
-    if (false) {  // timing experiment only
-#else
     if (active) {
-#endif
 #pragma unroll
       for (int ks = 0; ks < KC / 32; ++ks) {
         bf16x8_t af[4], bfr[4], al[4], bl[4];
@@ -353,9 +346,6 @@ __global__ __launch_bounds__(RgCfg<X3>::WAVES * 64) void k_rgemm(RGemm g) {
     if (c + RG_NS < nch) issue(c + RG_NS);
   }
   rg_wait<0>();
-#ifdef RG_EXP_NOEPI
-  if (acc[0][0][0] != 12345.f) return;  // timing experiment only
-#endif
   if (!active) return;
   // weights are the MFMA A operand, so lane l holds C[16 i + (l & 15)][64 w + 16 j + 4 (l >> 4) + r],
   // r = 0..3: four consecutive columns of one row, stored as one 16-B store (vec_out). Every

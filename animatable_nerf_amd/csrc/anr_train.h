@@ -16,6 +16,7 @@ struct GemmSeg {
 struct GemmArgs {
   int M;
   const int* M_dev;  // if set, M is read from device memory
+  const int* K_dev;  // if set, segment 0's K is read from device memory (sample-reduction GEMMs)
   int N;
   int nseg;
   GemmSeg seg[2];
@@ -173,6 +174,7 @@ struct TrainBufs {
   float* dLt;    // [N][32]
   float* dIt;    // [N][32]
   float* dGt;    // [N][64]
+  float* dGt2;   // [N][64] second contribution (T-pose BW chain), summed by k_tr_tpose_bwd; NULL: none
   const int* out_row;
   const int* m_rows;
   const float* d_rgb_map;  // (R,3) upstream or NULL

@@ -356,8 +356,9 @@ __global__ __launch_bounds__(256) void k_tr_tpose_bwd(TrainBufs b) {
   const float tp[3] = {pt[4], pt[5], pt[6]};
   float g[3] = {0.f, 0.f, 0.f};
   const float* dG = b.dGt + (long)i * 64;
+  const float* dG2 = b.dGt2 ? b.dGt2 + (long)i * 64 : nullptr;
   for (int f = 0; f < 63; ++f) {
-    const float d = dG[f];
+    const float d = dG2 ? dG[f] + dG2[f] : dG[f];
     if (f < 3) {
       g[f] += d;
       continue;

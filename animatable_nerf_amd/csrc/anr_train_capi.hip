@@ -6,6 +6,8 @@
 // the kept-sample count per call sizes the GEMMs (the reference syncs ~6x per chunk).
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
+#include <mutex>
 #include <string>
 
 #include "../../include/aninerf.h"
@@ -18,11 +20,13 @@ using namespace anr;
 
 namespace {
 
+constexpr int kWStreams = 4;  // weight-gradient lanes (side streams below)
+
 // training workspace = render layout (prefix, incl. raw) + per-sample activations / gradients
 struct TLayout {
   Layout L;
   size_t pt, Gp, Ip, Gv, Lp, lbs, Gt, It, Lt, Hp, Ht, Hn, Feat, Alpha, Lat, View, Rgbl;
-  size_t draw, dRgb, dAlpha, dBp, dBt, dLp, dLt, dIt, dGt, dA, dB, dFeat, dLat, dView;
+  size_t draw, dRgb, dAlpha, dBp, dBt, dLp, dLt, dIt, dGt, dGt2, dHn, dHt, dHp, dFeat, dLat, dView;
   size_t ysum, acc3, d_rgb, d_pbw, d_tbw, wimg, wslab, total;
 };
 
@@ -41,11 +45,14 @@ TLayout tlayout(int n_rays, int chunk, long np, long nt) {
   T.Hp = take(N * 256 * 8); T.Ht = take(N * 256 * 8); T.Hn = take(N * 256 * 8);
   T.Feat = take(N * 256); T.Alpha = take(N); T.Lat = take(N * 256); T.View = take(N * 128); T.Rgbl = take(N * 4);
   T.draw = take(N * 4); T.dRgb = take(N * 4); T.dAlpha = take(N); T.dBp = take(N * 24); T.dBt = take(N * 24);
-  T.dLp = take(N * 32); T.dLt = take(N * 32); T.dIt = take(N * 32); T.dGt = take(N * 64);
-  T.dA = take(N * 256); T.dB = take(N * 256); T.dFeat = take(N * 256); T.dLat = take(N * 256); T.dView = take(N * 128);
+  T.dLp = take(N * 32); T.dLt = take(N * 32); T.dIt = take(N * 32); T.dGt = take(N * 64); T.dGt2 = take(N * 64);
+  // every layer's output gradient has its own slot (the weight-gradient products read them on the
+  // side stream while the input-gradient chain moves on)
+  T.dHn = take(N * 256 * 8); T.dHt = take(N * 256 * 8); T.dHp = take(N * 256 * 8);
+  T.dFeat = take(N * 256); T.dLat = take(N * 256); T.dView = take(N * 128);
   T.ysum = take(8 * 256); T.acc3 = take(4); T.d_rgb = take(R * 3); T.d_pbw = take(N * 24); T.d_tbw = take(N * 24);
   T.wimg = take((wimg_bytes() + 3) / 4);
-  T.wslab = take(wgrad_slab_floats());
+  T.wslab = take(wgrad_slab_floats() * kWStreams);
   T.total = o;
   return T;
 }
@@ -65,6 +72,54 @@ int check_args(const anr_params* p, const anr_frame* f, const float* ray_o, cons
   return ANR_OK;
 }
 
+// ---- side streams -------------------------------------------------------------------------------
+// The backward's critical path is the input-gradient chain (dX = dY W (ReLU mask), layer after
+// layer). The weight-gradient products (dW += dY^T X, their slab reductions and the latent-row
+// updates) hang off it and run on side streams `sw[]` (round robin, one partial-slab region each;
+// the latent-row updates of one table all on sw[0], they share the table row); the T-pose
+// blend-weight MLP (forward and
+// backward) runs on `s2` beside the canonical NeRF, since both read only gamma(x_T). At ~24k kept
+// samples one 128-row GEMM occupies 188 of the 256 CUs for ~20 us, so a single stream leaves the
+// chip a quarter idle and serialises ~80 launches that do not depend on each other. The streams
+// are per device, created once, ordered with the caller's stream by events (fork / join), so every
+// entry point still behaves as one asynchronous call on the caller's stream.
+// ANR_TRAIN_SERIAL=1 runs everything on the caller's stream (debugging aid).
+struct SideStreams {
+  hipStream_t s2 = nullptr, sw[kWStreams] = {};
+  hipEvent_t ev[64] = {};
+  unsigned next = 0;
+};
+
+SideStreams* side_streams() {
+  static SideStreams per_dev[16];
+  static std::mutex mu;
+  const char* serial = getenv("ANR_TRAIN_SERIAL");
+  if (serial && serial[0] == '1') return nullptr;
+  int d = 0;
+  if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= 16) return nullptr;
+  std::lock_guard<std::mutex> g(mu);
+  SideStreams& ss = per_dev[d];
+  if (!ss.s2) {
+    SideStreams t{};
+    if (hipStreamCreateWithFlags(&t.s2, hipStreamNonBlocking) != hipSuccess) return nullptr;
+    for (auto& w : t.sw)
+      if (hipStreamCreateWithFlags(&w, hipStreamNonBlocking) != hipSuccess) return nullptr;
+    for (auto& e : t.ev)
+      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+    ss = t;
+  }
+  return &ss;
+}
+
+// work issued to `to` from now on runs after everything already issued to `from`
+int order(SideStreams* ss, hipStream_t to, hipStream_t from) {
+  if (!ss || to == from) return ANR_OK;
+  hipEvent_t ev = ss->ev[ss->next++ & 63];
+  if (hipEventRecord(ev, from) != hipSuccess || hipStreamWaitEvent(to, ev, 0) != hipSuccess)
+    return fail(ANR_E_HIP, "stream ordering failed");
+  return ANR_OK;
+}
+
 struct Exec {
   hipStream_t s;
   int n;         // kept samples (host copy)
@@ -74,6 +129,31 @@ struct Exec {
   const float* pt[ANR_NUM_TENSORS + ANR_NUM_NOVEL_TENSORS] = {};  // the tensors they were packed from
   float* wslab = nullptr;              // weight-gradient partial slabs (anr_tgemm.hip k_wgrad)
   int x3 = 0;  // inside the pose scope of ANR_BF16: split-bf16 (fp32-level) row GEMMs instead of fp32
+  SideStreams* ss = nullptr;  // NULL: every product on s
+  int wnext = 0;               // round-robin weight-gradient lane
+
+  hipStream_t s2() const { return ss ? ss->s2 : s; }
+  // a weight-gradient lane (stream + its partial-slab region), ordered after everything issued to s
+  // so far; lane < 0: the next one round robin
+  int wstream(hipStream_t* w, int* lane, int want = -1) {
+    const int l = want >= 0 ? want : (wnext++ % kWStreams);
+    *lane = ss ? l : 0;
+    *w = ss ? ss->sw[l] : s;
+    return order(ss, *w, s);
+  }
+  float* slab(int lane) const { return wslab ? wslab + (size_t)lane * wgrad_slab_floats() : nullptr; }
+  // lane 0 waits for the other lanes (every weight gradient issued so far is done when lane 0 is)
+  int gather_w() {
+    if (!ss) return ANR_OK;
+    for (int l = 1; l < kWStreams; ++l) ANR_TRY(order(ss, ss->sw[0], ss->sw[l]));
+    return ANR_OK;
+  }
+  // s waits for every weight-gradient lane (end of a backward)
+  int join_w() {
+    if (!ss) return ANR_OK;
+    for (int l = 0; l < kWStreams; ++l) ANR_TRY(order(ss, s, ss->sw[l]));
+    return ANR_OK;
+  }
 
   // the bf16 row GEMM when every operand fits it (anr_train.h RGemm); false: use the generic kernel
   bool row_seg(RGemmSeg& q, const float* A, long lda, int K, const float* W, int c0, bool bwd) {
@@ -90,15 +170,16 @@ struct Exec {
     return check_launch("k_rgemm");
   }
 
-  int gemm(GemmArgs g, int M) {
+  int gemm(GemmArgs g, int M, hipStream_t st) {
     if (M <= 0 || g.N <= 0) return ANR_OK;
     if (g.ksplit < 1) g.ksplit = 1;
     dim3 grid((g.N + 63) / 64, (M + 63) / 64, g.ksplit);
     g.M = M;
     g.bf16 = bf16;
-    launch_gemm(g, grid, s);
+    launch_gemm(g, grid, st);
     return check_launch("k_gemm");
   }
+  int gemm(GemmArgs g, int M) { return gemm(g, M, s); }
 
   // Y[n][Nout] = act( X0[:, :K0] W[:, c0:c0+K0]^T (+ X1 W[:, c1:c1+K1]^T) + bias )
   int fwd(float* Y, int ldY, int Nout, const float* W, int in_ch, const float* bias, bool relu, const float* X0, int ld0,
@@ -125,14 +206,17 @@ struct Exec {
   // dW[:, c0:c0+K] += dY^T X (split-K over samples, atomics); the column sums of dY (the bias
   // gradient) are added into bsum (and bsum2) in the same pass when given
   int wgrad(float* dW, int in_ch, int c0, int Nout, const float* dY, int ldY, const float* X, int ldX, int K,
-            float* bsum = nullptr, float* bsum2 = nullptr) {
+            float* bsum = nullptr, float* bsum2 = nullptr, int want_lane = -1) {
+    hipStream_t w;
+    int lane;
+    ANR_TRY(wstream(&w, &lane, want_lane));
     if ((bf16 || x3) && wslab && Nout <= 256 && K <= 256 && ldY % 4 == 0 && ldX % 4 == 0 && ((uintptr_t)dY & 15) == 0 &&
         ((uintptr_t)X & 15) == 0 && n > 0) {
-      WGrad w{};
-      w.x3 = bf16 ? 0 : 1;
-      w.dY = dY; w.ldY = ldY; w.nout = Nout; w.X = X; w.ldX = ldX; w.K = K;
-      w.dW = dW + c0; w.ldw = in_ch; w.bsum = bsum; w.bsum2 = bsum2; w.slab = wslab;
-      if (launch_wgrad(w, n, s) != 0) return check_launch("k_wgrad");
+      WGrad wg{};
+      wg.x3 = bf16 ? 0 : 1;
+      wg.dY = dY; wg.ldY = ldY; wg.nout = Nout; wg.X = X; wg.ldX = ldX; wg.K = K;
+      wg.dW = dW + c0; wg.ldw = in_ch; wg.bsum = bsum; wg.bsum2 = bsum2; wg.slab = slab(lane);
+      if (launch_wgrad(wg, n, w) != 0) return check_launch("k_wgrad");
       return ANR_OK;
     }
     GemmArgs g{};
@@ -143,7 +227,7 @@ struct Exec {
     g.seg[0] = GemmSeg{dY, 1, ldY, X, ldX, 1, n};
     g.C = dW + c0; g.ldc = in_ch; g.atomic = 1;
     g.ksplit = (n + 511) / 512;  // 512 samples per split (measured: 1024 / 512 / 256 / 2048)
-    return gemm(g, Nout);
+    return gemm(g, Nout, w);
   }
 
   // dX (+)= dY W[:, c0:c0+K] (masked by mask > 0)
@@ -186,6 +270,14 @@ struct PoseScope {
     e.bf16 = keep;
     e.x3 = 0;
   }
+};
+
+// issue the enclosed products on another stream of the executor (restored on scope exit)
+struct OnStream {
+  Exec& e;
+  hipStream_t keep;
+  OnStream(Exec& x, hipStream_t t) : e(x), keep(x.s) { e.s = t; }
+  ~OnStream() { e.s = keep; }
 };
 
 // bf16 weight images for the row GEMM (bf16 policies only; refreshed on every call, the weights may
@@ -257,45 +349,46 @@ int bw_forward(Exec& e, const float* const* W, const float* G, float* H, float* 
   return e.fwd(logits, 32, 24, W[17], 256, W[18], false, H + 7 * S, 256, 256, 0);
 }
 
-// BW MLP backward from d logits; accumulates weight/bias grads into g (same table order as W; NULL:
-// input gradient only, a frozen field); dG (+)= input-gamma gradient if given.
+// BW MLP backward from d logits on e.s; accumulates weight/bias grads into g (same table order as W;
+// NULL: input gradient only, a frozen field); dG (+)= input-gamma gradient if given (dG_fresh: the
+// first contribution overwrites). Layer l's output gradient goes to dY0 + l * dstride (dstride 0:
+// ping-pong between dY0 and dY1, only when no weight gradient runs on a side stream).
 // ysum: 2 x 256 scratch for the latent-column gradients of layers 0 and 5.
 int bw_backward(Exec& e, const float* const* W, float* const* g, const float* G, const float* H, const float* dlog,
-                float* dA, float* dB, float* dG, long N, float* ysum, const int64_t* li, int add, hipStream_t s) {
+                float* dY0, float* dY1, long dstride, float* dG, bool dG_fresh, long N, float* ysum, const int64_t* li,
+                int add) {
   const long S = N * 256;
+  auto dbuf = [&](int l) { return dstride ? dY0 + l * dstride : ((l & 1) ? dY0 : dY1); };
   // bw_fc
   if (g) {
     ANR_TRY(e.wgrad(g[17], 256, 0, 24, dlog, 32, H + 7 * S, 256, 256, g[18]));
   }
-  ANR_TRY(e.xgrad(dA, 256, 256, dlog, 32, 24, W[17], 256, 0, H + 7 * S, 256, false));
-  float* cur = dA;
-  float* nxt = dB;
+  ANR_TRY(e.xgrad(dbuf(7), 256, 256, dlog, 32, 24, W[17], 256, 0, H + 7 * S, 256, false));
   for (int l = 7; l >= 0; --l) {
     const int wi = 1 + 2 * l, bi = wi + 1;
     const int in_ch = l == 0 ? 191 : (l == 5 ? 447 : 256);
+    const float* cur = dbuf(l);
     if (l == 0 || l == 5) {
       if (g) {
         float* ys = ysum + (l == 5 ? 256 : 0);
-        if (hipMemsetAsync(ys, 0, 256 * 4, s) != hipSuccess) return fail(ANR_E_HIP, "memset");
+        hipStream_t w;
+        int lane;
+        ANR_TRY(e.wstream(&w, &lane, 0));
+        if (hipMemsetAsync(ys, 0, 256 * 4, w) != hipSuccess) return fail(ANR_E_HIP, "memset");
         // bias grad and the latent-row gradient's column sum, in the weight-gradient pass
-        ANR_TRY(e.wgrad(g[wi], in_ch, 0, 256, cur, 256, G, 64, 63, g[bi], ys));
-        hipLaunchKernelGGL(k_tr_latent_grad, dim3(256 + 128), dim3(128), 0, s, (const float*)ys, W[wi], in_ch, 63, 256,
+        ANR_TRY(e.wgrad(g[wi], in_ch, 0, 256, cur, 256, G, 64, 63, g[bi], ys, 0));
+        hipLaunchKernelGGL(k_tr_latent_grad, dim3(256 + 128), dim3(128), 0, w, (const float*)ys, W[wi], in_ch, 63, 256,
                            W[0], li, add, g[wi], g[0]);
         ANR_TRY(check_launch("k_tr_latent_grad"));
       }
-      if (dG) ANR_TRY(e.xgrad(dG, 64, 63, cur, 256, 256, W[wi], in_ch, 0, nullptr, 0, true));
+      if (dG) ANR_TRY(e.xgrad(dG, 64, 63, cur, 256, 256, W[wi], in_ch, 0, nullptr, 0, !(dG_fresh && l == 5)));
       if (l == 5) {
         if (g) ANR_TRY(e.wgrad(g[wi], in_ch, 191, 256, cur, 256, H + 4 * S, 256, 256));
-        ANR_TRY(e.xgrad(nxt, 256, 256, cur, 256, 256, W[wi], in_ch, 191, H + 4 * S, 256, false));
+        ANR_TRY(e.xgrad(dbuf(4), 256, 256, cur, 256, 256, W[wi], in_ch, 191, H + 4 * S, 256, false));
       }
     } else {
       if (g) ANR_TRY(e.wgrad(g[wi], 256, 0, 256, cur, 256, H + (l - 1) * S, 256, 256, g[bi]));
-      ANR_TRY(e.xgrad(nxt, 256, 256, cur, 256, 256, W[wi], 256, 0, H + (l - 1) * S, 256, false));
-    }
-    if (l > 0) {
-      float* t = cur;
-      cur = nxt;
-      nxt = t;
+      ANR_TRY(e.xgrad(dbuf(l - 1), 256, 256, cur, 256, 256, W[wi], 256, 0, H + (l - 1) * S, 256, false));
     }
   }
   return ANR_OK;
@@ -325,10 +418,16 @@ int train_forward(const anr_params* p, const anr_frame* f, const float* ray_o, c
     hipLaunchKernelGGL(k_tr_softmax_lbs, dim3(g1), dim3(256), 0, s, b);
     ANR_TRY(check_launch("k_tr_softmax_lbs"));
   }
-  ANR_TRY(bw_forward(e, p->t + 27, b.Gt, (float*)(ws + T.Ht), b.Lt, N, FOLD(1), FOLD(3)));
-  if (n > 0) {
-    hipLaunchKernelGGL(k_tr_softmax_t, dim3(g1), dim3(256), 0, s, b);
-    ANR_TRY(check_launch("k_tr_softmax_t"));
+  // T-pose BW MLP on s2, beside the canonical NeRF (both read only gamma(x_T))
+  const hipStream_t s2 = e.s2();
+  ANR_TRY(order(e.ss, s2, s));
+  {
+    OnStream on(e, s2);
+    ANR_TRY(bw_forward(e, p->t + 27, b.Gt, (float*)(ws + T.Ht), b.Lt, N, FOLD(1), FOLD(3)));
+    if (n > 0) {
+      hipLaunchKernelGGL(k_tr_softmax_t, dim3(g1), dim3(256), 0, s2, b);
+      ANR_TRY(check_launch("k_tr_softmax_t"));
+    }
   }
   // canonical NeRF (TPoseHuman.calculate_alpha_rgb)
   float* Hn = (float*)(ws + T.Hn);
@@ -354,6 +453,7 @@ int train_forward(const anr_params* p, const anr_frame* f, const float* ray_o, c
     ANR_TRY(check_launch("k_tr_raw"));
   }
   ANR_TRY(stage_alpha_ind(R, o, ws, T.L, s));
+  ANR_TRY(order(e.ss, s, s2));  // join: the tbw rows
   if (x) return ANR_OK;
   return stage_composite(near_, far_, R, o, raw, out, nullptr, s);
 }
@@ -375,13 +475,20 @@ int train_backward(const anr_params* p, float* const* g, const anr_frame* f, con
   float* Feat = (float*)(ws + T.Feat);
   float* Lat = (float*)(ws + T.Lat);
   float* View = (float*)(ws + T.View);
-  float* dA = (float*)(ws + T.dA);
-  float* dB = (float*)(ws + T.dB);
+  float* dHn = (float*)(ws + T.dHn);
   float* dFeat = (float*)(ws + T.dFeat);
   float* dLat = (float*)(ws + T.dLat);
   float* dView = (float*)(ws + T.dView);
   float* ysum = (float*)(ws + T.ysum);
-  if (hipMemsetAsync(b.dGt, 0, (size_t)n * 64 * 4, s) != hipSuccess) return fail(ANR_E_HIP, "memset");
+  // the T-pose BW chain writes its gamma(x_T) gradient into dGt2 (s2), the NeRF's into dGt (s)
+  b.dGt2 = (float*)(ws + T.dGt2);
+  const hipStream_t s2 = e.s2();
+  ANR_TRY(order(e.ss, s2, s));
+  // upstream pbw / tbw row gradients, T-pose softmax backward (s2)
+  hipLaunchKernelGGL(k_tr_rows_bwd, dim3(g1), dim3(256), 0, s2, b);
+  ANR_TRY(check_launch("k_tr_rows_bwd"));
+  hipLaunchKernelGGL(k_tr_softmax_bwd_t, dim3(g1), dim3(256), 0, s2, b);
+  ANR_TRY(check_launch("k_tr_softmax_bwd_t"));
 
   // compositing (or the caller's d raw) + raw activations
   if (x) {
@@ -402,48 +509,54 @@ int train_backward(const anr_params* p, float* const* g, const anr_frame* f, con
   ANR_TRY(e.xgrad(dLat, 256, 256, dView, 128, 128, PT(23), 283, 0, nullptr, 0, false));
   {
     float* ys = ysum + 512;
-    if (hipMemsetAsync(ys, 0, 256 * 4, s) != hipSuccess) return fail(ANR_E_HIP, "memset");
-    ANR_TRY(e.wgrad(g[21], 384, 0, 256, dLat, 256, Feat, 256, 256, g[22], ys));
-    hipLaunchKernelGGL(k_tr_latent_grad, dim3(256 + 128), dim3(128), 0, s, (const float*)ys, PT(21), 384, 256, 256, PT(0),
+    hipStream_t w;
+    int lane;
+    ANR_TRY(e.wstream(&w, &lane, 0));
+    if (hipMemsetAsync(ys, 0, 256 * 4, w) != hipSuccess) return fail(ANR_E_HIP, "memset");
+    ANR_TRY(e.wgrad(g[21], 384, 0, 256, dLat, 256, Feat, 256, 256, g[22], ys, 0));
+    hipLaunchKernelGGL(k_tr_latent_grad, dim3(256 + 128), dim3(128), 0, w, (const float*)ys, PT(21), 384, 256, 256, PT(0),
                        f->latent_index, 0, g[21], g[0]);
     ANR_TRY(check_launch("k_tr_latent_grad(nf_latent)"));
   }
   ANR_TRY(e.xgrad(dFeat, 256, 256, dLat, 256, 256, PT(21), 384, 0, nullptr, 0, false));
   ANR_TRY(e.wgrad(g[19], 256, 0, 256, dFeat, 256, Hn + 7 * S, 256, 256, g[20]));
   ANR_TRY(e.wgrad(g[17], 256, 0, 1, b.dAlpha, 1, Hn + 7 * S, 256, 256, g[18]));
-  ANR_TRY(e.xgrad(dA, 256, 256, dFeat, 256, 256, PT(19), 256, 0, Hn + 7 * S, 256, false, b.dAlpha, 1, 1, PT(17), 256));
-  // NeRF pts_linears 7..0 (skip at 5: [gamma(x_T), net])
-  float* cur = dA;
-  float* nxt = dB;
+  ANR_TRY(e.xgrad(dHn + 7 * S, 256, 256, dFeat, 256, 256, PT(19), 256, 0, Hn + 7 * S, 256, false, b.dAlpha, 1, 1,
+                  PT(17), 256));
+  // NeRF pts_linears 7..0 (skip at 5: [gamma(x_T), net]); layer l's output gradient at dHn + l S
   for (int l = 7; l >= 0; --l) {
     const int wi = 1 + 2 * l, bi = wi + 1;
+    const float* cur = dHn + l * S;
     if (l == 0) {
       ANR_TRY(e.wgrad(g[wi], 63, 0, 256, cur, 256, b.Gt, 64, 63, g[bi]));
       ANR_TRY(e.xgrad(b.dGt, 64, 63, cur, 256, 256, PT(wi), 63, 0, nullptr, 0, true));
     } else if (l == 5) {
       ANR_TRY(e.wgrad(g[wi], 319, 0, 256, cur, 256, b.Gt, 64, 63, g[bi]));
       ANR_TRY(e.wgrad(g[wi], 319, 63, 256, cur, 256, Hn + 4 * S, 256, 256));
-      ANR_TRY(e.xgrad(b.dGt, 64, 63, cur, 256, 256, PT(wi), 319, 0, nullptr, 0, true));
-      ANR_TRY(e.xgrad(nxt, 256, 256, cur, 256, 256, PT(wi), 319, 63, Hn + 4 * S, 256, false));
+      ANR_TRY(e.xgrad(b.dGt, 64, 63, cur, 256, 256, PT(wi), 319, 0, nullptr, 0, false));  // first contribution
+      ANR_TRY(e.xgrad(dHn + 4 * S, 256, 256, cur, 256, 256, PT(wi), 319, 63, Hn + 4 * S, 256, false));
     } else {
       ANR_TRY(e.wgrad(g[wi], 256, 0, 256, cur, 256, Hn + (l - 1) * S, 256, 256, g[bi]));
-      ANR_TRY(e.xgrad(nxt, 256, 256, cur, 256, 256, PT(wi), 256, 0, Hn + (l - 1) * S, 256, false));
-    }
-    if (l > 0) {
-      float* t = cur;
-      cur = nxt;
-      nxt = t;
+      ANR_TRY(e.xgrad(dHn + (l - 1) * S, 256, 256, cur, 256, 256, PT(wi), 256, 0, Hn + (l - 1) * S, 256, false));
     }
   }
-  // the canonical NeRF's gradients (tensors 0..26) are final here: a caller may start reducing them
-  // while the blend-weight backward below runs (bucketed all-reduce, anr_train_hooks)
-  if (nerf_done && hipEventRecord(nerf_done, s) != hipSuccess) return fail(ANR_E_HIP, "hipEventRecord failed");
-  // upstream pbw / tbw row gradients; T-pose BW backward (latent row 0)
-  hipLaunchKernelGGL(k_tr_rows_bwd, dim3(g1), dim3(256), 0, s, b);
-  ANR_TRY(check_launch("k_tr_rows_bwd"));
-  hipLaunchKernelGGL(k_tr_softmax_bwd_t, dim3(g1), dim3(256), 0, s, b);
-  ANR_TRY(check_launch("k_tr_softmax_bwd_t"));
-  ANR_TRY(bw_backward(e, p->t + 27, g + 27, b.Gt, Ht, b.dLt, dA, dB, b.dGt, N, ysum, nullptr, 0, s));  // bw_latent row 0
+  // the canonical NeRF's gradients (tensors 0..26) are final once the weight-gradient stream has
+  // run what is issued so far: a caller may start reducing them while the blend-weight backward
+  // below runs (bucketed all-reduce, anr_train_hooks)
+  if (nerf_done) {
+    hipStream_t w;
+    int lane;
+    ANR_TRY(e.gather_w());
+    ANR_TRY(e.wstream(&w, &lane, 0));
+    if (hipEventRecord(nerf_done, w) != hipSuccess) return fail(ANR_E_HIP, "hipEventRecord failed");
+  }
+  // T-pose BW backward (latent row 0) on s2
+  {
+    OnStream on(e, s2);
+    ANR_TRY(bw_backward(e, p->t + 27, g + 27, b.Gt, Ht, b.dLt, (float*)(ws + T.dHt), nullptr, S, b.dGt2, true, N, ysum,
+                        nullptr, 0));
+  }
+  ANR_TRY(order(e.ss, s, s2));  // join: dGt2, dBp rows
   // x_T gradient (gamma + init_tbw lookup) -> LBS -> d pbw; pose BW backward (latent row li + 1)
   hipLaunchKernelGGL(k_tr_tpose_bwd, dim3(g1), dim3(256), 0, s, b);
   ANR_TRY(check_launch("k_tr_tpose_bwd"));
@@ -566,13 +679,13 @@ int anim_path(const anr_params* p, float* const* grads, const anr_frame* f, cons
     // gamma + init_tbw lookup, LBS inverse -> d pbw (k_tr_tpose_bwd)
     hipLaunchKernelGGL(k_tr_softmax_bwd_t, dim3(g1), dim3(256), 0, s, b);
     if (hipMemsetAsync(b.dGt, 0, (size_t)n * 64 * 4, s) != hipSuccess) return fail(ANR_E_HIP, "memset");
-    ANR_TRY(bw_backward(e, p->t + 27, nullptr, b.Gt, Ht, b.dLt, dA, dB, b.dGt, N, ysum, nullptr, 0, s));
+    ANR_TRY(bw_backward(e, p->t + 27, nullptr, b.Gt, Ht, b.dLt, dA, dB, 0, b.dGt, false, N, ysum, nullptr, 0));
     hipLaunchKernelGGL(k_tr_tpose_bwd, dim3(g1), dim3(256), 0, s, b);
   }
   hipLaunchKernelGGL(k_tr_softmax_bwd_p, dim3(g1), dim3(256), 0, s, b);
   ANR_TRY(check_launch("anim backward"));
   PoseScope ps(e);
-  return bw_backward(e, p->novel, grads, b.Gp, Hp, b.dLp, dA, dB, nullptr, N, ysum + 512, f->bw_latent_index, 0, s);
+  return bw_backward(e, p->novel, grads, b.Gp, Hp, b.dLp, dA, dB, 0, nullptr, false, N, ysum + 512, f->bw_latent_index, 0);
 }
 
 }  // namespace
@@ -598,6 +711,7 @@ int anr_train_fwd(const anr_params* p, const anr_frame* f, const float* ray_o, c
   hipStream_t s = (hipStream_t)stream;
   char* ws = (char*)workspace;
   Exec e{s, 0, (o->precision == ANR_BF16 || o->precision == ANR_BF16_ALL) ? 1 : 0, o->precision == ANR_BF16 ? 1 : 0};
+  e.ss = side_streams();
   ANR_TRY(pack_images(e, p, ws + T.wimg, s, (float*)(ws + T.wslab)));
   ANR_TRY(train_forward(p, f, ray_o, ray_d, near_, far_, n_rays, o, out, ws, T, s, e));
   if (out->raw &&
@@ -620,6 +734,7 @@ int anr_train_bwd(const anr_params* p, float* const* grads, const anr_frame* f, 
   hipStream_t s = (hipStream_t)stream;
   char* ws = (char*)workspace;
   Exec e{s, 0, (o->precision == ANR_BF16 || o->precision == ANR_BF16_ALL) ? 1 : 0, o->precision == ANR_BF16 ? 1 : 0};
+  e.ss = side_streams();
   ANR_TRY(pack_images(e, p, ws + T.wimg, s, (float*)(ws + T.wslab)));
   ANR_TRY(read_count((const int*)(ws + T.L.counts), &e.n, s));
   ANR_TRY(train_backward(p, grads, f, ray_o, ray_d, near_, far_, n_rays, o, d_rgb_map, d_pbw, d_tbw, ws, T, s, e));
@@ -629,8 +744,8 @@ int anr_train_bwd(const anr_params* p, float* const* grads, const anr_frame* f, 
   float* ysum = (float*)(ws + T.ysum);
   PoseScope ps(e);
   ANR_TRY(bw_backward(e, p->t + 27, grads + 27, (const float*)(ws + T.Gp), (const float*)(ws + T.Hp), (const float*)(ws + T.dLp),
-                      (float*)(ws + T.dA), (float*)(ws + T.dB), nullptr, N, ysum + 1024, f->latent_index, 1, s));
-  return ANR_OK;
+                      (float*)(ws + T.dHp), nullptr, N * 256, nullptr, false, N, ysum + 1024, f->latent_index, 1));
+  return e.join_w();
 }
 
 int anr_train_step(const anr_params* p, float* const* grads, const anr_frame* f, const float* ray_o,
@@ -658,6 +773,7 @@ int anr_train_step_hooked(const anr_params* p, float* const* grads, const anr_fr
   hipStream_t s = (hipStream_t)stream;
   char* ws = (char*)workspace;
   Exec e{s, 0, (o->precision == ANR_BF16 || o->precision == ANR_BF16_ALL) ? 1 : 0, o->precision == ANR_BF16 ? 1 : 0};
+  e.ss = side_streams();
   ANR_TRY(pack_images(e, p, ws + T.wimg, s, (float*)(ws + T.wslab)));
   ANR_TRY(train_forward(p, f, ray_o, ray_d, near_, far_, n_rays, o, out, ws, T, s, e));
   // fused losses (tpose_trainer.py:50-63) and their upstream gradients
@@ -686,8 +802,9 @@ int anr_train_step_hooked(const anr_params* p, float* const* grads, const anr_fr
   }
   float* ysum = (float*)(ws + T.ysum);
   PoseScope ps(e);
-  return bw_backward(e, p->t + 27, grads + 27, (const float*)(ws + T.Gp), (const float*)(ws + T.Hp), (const float*)(ws + T.dLp),
-                     (float*)(ws + T.dA), (float*)(ws + T.dB), nullptr, N, ysum + 1024, f->latent_index, 1, s);
+  ANR_TRY(bw_backward(e, p->t + 27, grads + 27, (const float*)(ws + T.Gp), (const float*)(ws + T.Hp), (const float*)(ws + T.dLp),
+                      (float*)(ws + T.dHp), nullptr, N * 256, nullptr, false, N, ysum + 1024, f->latent_index, 1));
+  return e.join_w();
 }
 
 size_t anr_anim_workspace_bytes(int n_points) {
@@ -772,6 +889,7 @@ int anr_network_train_fwd(const anr_params* p, const anr_frame* f, const anr_sam
   hipStream_t s = (hipStream_t)stream;
   char* ws = (char*)workspace;
   Exec e{s, 0, (o->precision == ANR_BF16 || o->precision == ANR_BF16_ALL) ? 1 : 0, o->precision == ANR_BF16 ? 1 : 0};
+  e.ss = side_streams();
   ANR_TRY(pack_images(e, p, ws + T.wimg, s, (float*)(ws + T.wslab)));
   ANR_TRY(train_forward(p, f, nullptr, nullptr, nullptr, nullptr, G, &oo, nullptr, ws, T, s, e, x));
   if (hipMemcpyAsync(raw, ws + T.L.raw, (size_t)x->n_pts * 16, hipMemcpyDeviceToDevice, s) != hipSuccess)
@@ -797,6 +915,7 @@ int anr_network_train_bwd(const anr_params* p, float* const* grads, const anr_fr
   hipStream_t s = (hipStream_t)stream;
   char* ws = (char*)workspace;
   Exec e{s, 0, (o->precision == ANR_BF16 || o->precision == ANR_BF16_ALL) ? 1 : 0, o->precision == ANR_BF16 ? 1 : 0};
+  e.ss = side_streams();
   ANR_TRY(pack_images(e, p, ws + T.wimg, s, (float*)(ws + T.wslab)));
   ANR_TRY(read_count((const int*)(ws + T.L.counts), &e.n, s));
   ANR_TRY(train_backward(p, grads, f, nullptr, nullptr, nullptr, nullptr, G, &oo, nullptr, d_pbw, d_tbw, ws, T, s, e, x,
@@ -805,9 +924,10 @@ int anr_network_train_bwd(const anr_params* p, float* const* grads, const anr_fr
   const long N = (long)G * 64;
   float* ysum = (float*)(ws + T.ysum);
   PoseScope ps(e);
-  return bw_backward(e, p->t + 27, grads + 27, (const float*)(ws + T.Gp), (const float*)(ws + T.Hp),
-                     (const float*)(ws + T.dLp), (float*)(ws + T.dA), (float*)(ws + T.dB), nullptr, N, ysum + 1024,
-                     f->latent_index, 1, s);
+  ANR_TRY(bw_backward(e, p->t + 27, grads + 27, (const float*)(ws + T.Gp), (const float*)(ws + T.Hp),
+                      (const float*)(ws + T.dLp), (float*)(ws + T.dHp), nullptr, N * 256, nullptr, false, N, ysum + 1024,
+                      f->latent_index, 1));
+  return e.join_w();
 }
 
 // ---- free-point helpers: calculate_neural_blend_weights / novel_pose_bw, TPoseHuman.calculate_alpha --

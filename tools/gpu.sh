@@ -2,7 +2,7 @@
 # One parameterised GPU-box driver (run through gpurun from the repo root):
 #   tools/gpu.sh TAG step [step ...]
 # steps (each under its own time limit; the script stops at the first failure):
-#   tests[=PATTERN]   pytest -m gpu (optionally -k PATTERN)           -> gpurun_out/TAG_gpu_tests.log
+#   tests[=PATTERN]   pytest -m gpu (optionally -k PATTERN; _or_ = ' or ') -> gpurun_out/TAG_gpu_tests.log
 #   smoke             __graft_entry__.smoke()                          -> TAG_smoke.log
 #   bench[:ARGS]      python bench.py ARGS (ARGS comma-separated)      -> TAG_bench[_MODE].log
 #   prof[:ARGS]       rocprofv3 --kernel-trace --stats of bench ARGS  -> TAG_prof[_MODE]/
@@ -17,7 +17,15 @@ TAG=$1
 shift
 mkdir -p gpurun_out
 args_of() { echo "$1" | tr ',' ' '; }
-mode_of() { echo "$1" | sed -n 's/.*--mode,\([a-z-]*\).*/_\1/p'; }
+# log-name suffix: _MODE, then the other flags (steps / warmup left out), e.g. _train_precision-fp32
+mode_of() {
+  local m rest t=""
+  m=$(echo "$1" | sed -n 's/.*--mode,\([a-z-]*\).*/\1/p')
+  rest=$(echo "$1" | sed 's/--mode,[a-z-]*//; s/--steps,[0-9]*//; s/--warmup,[0-9]*//; s/--//g; s/[^a-zA-Z0-9.]\{1,\}/-/g; s/^-//; s/-$//')
+  [ -n "$m" ] && t="_$m"
+  [ -n "$rest" ] && t="${t}_$rest"
+  echo "$t"
+}
 for step in "$@"; do
   kind=${step%%:*}
   rest=${step#*:}
@@ -26,6 +34,7 @@ for step in "$@"; do
     tests|tests=*)
       pat=${step#tests=}
       [ "$pat" = "$step" ] && pat=""
+      pat=${pat//_or_/ or }
       sel=()
       [ -n "$pat" ] && sel=(-k "$pat")
       timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 180 --timeout-method thread "${sel[@]}" \
