@@ -264,7 +264,7 @@ __global__ __launch_bounds__(256) void k_gemm_t(GemmArgs g) {
   // k range of this split (split-K only with one segment)
   int kb = 0, ke = K0;
   if (g.ksplit > 1) {
-    const int per = ((K0 + g.ksplit - 1) / g.ksplit + GBK - 1) / GBK * GBK;
+    const int per = g.kper > 0 ? g.kper : ((K0 + g.ksplit - 1) / g.ksplit + GBK - 1) / GBK * GBK;
     kb = blockIdx.z * per;
     ke = min(K0, kb + per);
     if (kb >= ke) return;
@@ -462,7 +462,7 @@ __global__ __launch_bounds__(256) void k_gemm_b(GemmArgs g) {
   const int wr = (w >> 1) * 32, wc = (w & 1) * 32;
   int kb = 0, ke = K0;
   if (g.ksplit > 1) {
-    const int per = ((K0 + g.ksplit - 1) / g.ksplit + BBK - 1) / BBK * BBK;
+    const int per = g.kper > 0 ? g.kper : ((K0 + g.ksplit - 1) / g.ksplit + BBK - 1) / BBK * BBK;
     kb = blockIdx.z * per;
     ke = min(K0, kb + per);
     if (kb >= ke) return;

@@ -512,7 +512,9 @@ __global__ __launch_bounds__(256) void k_wgrad(WGrad g) {
   const int z = (slot / tiles) * 8 + (L & 7);
   const int ti = tile % gridDim.x, tj = tile / gridDim.x;
   const int n = g.M_dev ? *g.M_dev : g.n;
-  const int s0 = z * g.spb, s1 = min(n, s0 + g.spb);
+  // samples per range: whole 64-sample steps (spb = 0: from the device count, as launch_wgrad would)
+  const int spb = g.spb ? g.spb : ((n + g.nz - 1) / g.nz + 2 * WG_S - 1) / (2 * WG_S) * (2 * WG_S);
+  const int s0 = z * spb, s1 = min(n, s0 + spb);
   const int i0 = ti * WG_T, j0 = tj * WG_T;
   const int wi = (w >> 1) * 64, wj = (w & 1) * 64;
   f32x4 acc[4][4];
@@ -640,7 +642,8 @@ int launch_wgrad(WGrad g, int n_host, hipStream_t s) {
   int nz = (n_host + 383) / 384;
   nz = nz < 1 ? 1 : (nz > WG_MAX_Z ? WG_MAX_Z : nz);
   nz = (nz + 7) / 8 * 8;  // a multiple of 8 for the XCD-aware order (trailing ranges may be empty)
-  g.spb = ((n_host + nz - 1) / nz + 2 * WG_S - 1) / (2 * WG_S) * (2 * WG_S);  // whole 64-sample steps
+  // whole 64-sample steps; with a device count (n_host = its capacity) the kernel derives them
+  g.spb = g.M_dev ? 0 : ((n_host + nz - 1) / nz + 2 * WG_S - 1) / (2 * WG_S) * (2 * WG_S);
   g.nz = nz;
   g.n = n_host;
   g.rs_slab = (g.bsum || g.bsum2) ? g.slab + (size_t)WG_MAX_Z * 4 * WG_TILE_FLOATS : nullptr;

@@ -29,6 +29,7 @@ struct GemmArgs {
   int accumulate;      // C += result (non-atomic)
   int atomic;          // atomicAdd into C (split-K)
   int ksplit;          // number of K splits (grid.z)
+  int kper;            // > 0: each split covers kper of K (splits past K exit); 0: K / ksplit rounded up
   // sdf_pdf epilogues (anr_sdf*.hip); all off when zero / NULL
   float div_pre;       // v = v / div_pre before the activation (backward of cat(...)/sqrt(2))
   int softplus;        // v = Softplus(beta=100)(v); deriv[m][n] = exp(100 v) or -1 above the threshold (deriv may be NULL)

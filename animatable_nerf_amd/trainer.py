@@ -21,7 +21,7 @@ import torch.nn.functional as F
 from . import _lib
 from . import config as _config
 from .parallel import GradBuckets, broadcast_, is_dist
-from .renderer import Renderer, _Call
+from .renderer import FRAME_KEYS, RAY_KEYS, Renderer, _Call
 
 
 class NetworkWrapper(torch.nn.Module):
@@ -106,6 +106,7 @@ class FusedStep:
         # final before the blend-weight backward runs), then the blend-weight MLP (27..45) + losses
         n_nerf = sum(p.numel() for p in ps[:27])
         self.buckets = GradBuckets(self.grad, [(0, n_nerf), (n_nerf, n + 4)], group)
+        self._st = None  # fixed input / output buffers of the step (see _static_call)
         self.nerf_ready = None
         if dev.type == 'cuda':
             self.nerf_ready = torch.cuda.Event()
@@ -132,15 +133,48 @@ class FusedStep:
                         0, self.group)
         self.t, self.lr = int(tl[0]), float(tl[1])
 
+    _STATIC_KEYS = RAY_KEYS + FRAME_KEYS + ('latent_index', 'rgb', 'mask_at_box')
+
+    def _static_call(self, batch, t_rand):
+        """The step's inputs copied into fixed device buffers (and one fixed set of outputs), so that
+        consecutive steps call anr_train_step_hooked with identical arguments: from the second such
+        call on, the library replays the step as one captured graph. A buffer is rebuilt when a
+        shape changes; a source tensor unchanged since the last copy (same storage and version
+        counter, e.g. a frame's resident volumes) is not copied again."""
+        dev = self.flat.device
+        R = batch['ray_o'].shape[1]
+        ns = int(self.cfg.N_samples)
+        cfg = self.cfg
+        shapes = (tuple(tuple(batch[k].shape) for k in self._STATIC_KEYS),
+                  tuple(cfg.get(k, None) for k in ('train_precision', 'chunk', 'N_samples', 'norm_th', 'train_th')))
+        st = self._st
+        if st is None or st['shapes'] != shapes:
+            sb = {}
+            for k in self._STATIC_KEYS:
+                v = batch[k]
+                dt = torch.int64 if k == 'latent_index' else (torch.uint8 if k == 'mask_at_box' else torch.float32)
+                sb[k] = torch.empty(tuple(v.shape), dtype=dt, device=dev)
+            st = self._st = {'shapes': shapes, 'batch': sb, 'src': {}, 't_rand': torch.empty((R, ns), device=dev)}
+            st['call'] = _Call(self.renderer, sb, st['t_rand'])
+        sb, src = st['batch'], st['src']
+        for k in self._STATIC_KEYS:
+            v = batch[k]
+            tag = (v.data_ptr(), v._version, v.device)
+            if src.get(k) != tag:
+                sb[k].copy_(v)
+                src[k] = tag
+        if t_rand is not None:
+            st['t_rand'].copy_(t_rand.reshape(R, ns))
+        elif self.cfg.perturb > 0:
+            st['t_rand'].uniform_()
+        st['call'].opts.t_rand = st['t_rand'].data_ptr() if (t_rand is not None or self.cfg.perturb > 0) else None
+        return st['call'], sb['rgb'], sb['mask_at_box'].reshape(-1)
+
     def step(self, batch, t_rand=None, lr=None):
         r = self.renderer
         dev = self.flat.device
         R = batch['ray_o'].shape[1]
-        if t_rand is None and self.cfg.perturb > 0:
-            t_rand = torch.rand((R, int(self.cfg.N_samples)), device=dev)
-        c = _Call(r, batch, t_rand)
-        rgb = batch['rgb'].to(device=dev, dtype=torch.float32).contiguous()
-        mask = batch['mask_at_box'].to(device=dev).reshape(-1).to(torch.uint8).contiguous()
+        c, rgb, mask = self._static_call(batch, t_rand)
         p = r.params(pack=False)
         ws_bytes = self.lib.anr_train_workspace_bytes(R, ctypes.byref(c.opts), ctypes.byref(c.frame))
         ws = r._workspace('_tws', ws_bytes, dev)

@@ -516,6 +516,29 @@ def bench_sdf(args, rank, world, dev):
                      'peak': peak, 'unit': 'TFLOP/s', 'frac': achieved / peak,
                      'traffic': None, 'flop_per_kept': FLOP_PER_KEPT_SDF, 'flop_per_kept_executed': flop_exec},
     }
+    if split and not args.no_exact:
+        # the same frame with every layer GEMM in exact fp32 MFMA (the reference's arithmetic), timed beside
+        cfg32 = config.defaults()
+        cfg32.num_train_frame = 260
+        cfg32.perturb = 0
+        cfg32.render_precision = 'fp32'
+        r32 = Renderer(net, cfg32)
+        batch['tbounds'].copy_(tb0)
+        r32.render_device(batch)
+        torch.cuda.synchronize()
+        k32 = max(1, min(args.steps, 3))
+        t1 = time.perf_counter()
+        for _ in range(k32):
+            batch['tbounds'].copy_(tb0)
+            r32.render_device(batch)
+        torch.cuda.synchronize()
+        dt32 = max_over_ranks(time.perf_counter() - t1, dev, world) / k32
+        a32 = r32.last_counts[0] * FLOP_PER_KEPT_SDF / dt32 / 1e12
+        result['fp32_exact'] = {
+            'value': R * 64 * world / dt32, 'ms_per_step': dt32 * 1e3, 'steps': k32, 'render_precision': 'fp32',
+            'roofline': {'bound': 'mfma', 'achieved': a32, 'peak': PEAK_FP32_MFMA_TFLOPS, 'unit': 'TFLOP/s',
+                         'frac': a32 / PEAK_FP32_MFMA_TFLOPS, 'flop_per_kept': FLOP_PER_KEPT_SDF}}
+        progress(f'sdf fp32: {dt32 * 1e3:.2f} ms/frame')
     if rank == 0 and world == 1 and not args.no_cpu:
         import sys
         sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
