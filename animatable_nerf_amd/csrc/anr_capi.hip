@@ -93,8 +93,7 @@ int stage_frontend(const anr_params* p, const anr_frame* f, const float* ray_o, 
     pa.nw_bw5 = p->novel[11]; pa.nb_bw5 = p->novel[12];
     pa.bw_latent_index = f->bw_latent_index;
   }
-  const int nvb = (int)((np + nt + 7) / 8);
-  hipLaunchKernelGGL(k_prep, dim3(nvb + 1), dim3(256), 0, s, pa);
+  hipLaunchKernelGGL(k_prep, dim3(prep_blocks(np, nt)), dim3(256), 0, s, pa);
   ANR_TRY(check_launch("k_prep"));
 
   FrontArgs fa{};

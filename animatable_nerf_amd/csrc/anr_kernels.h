@@ -129,6 +129,9 @@ struct PrepArgs {
   const float *head_P, *head_q, *b_alpha;
   float* pn24;  // (np) channel 24 of pbw, compact, for the front-end's prefilter lookups (or NULL)
 };
+// k_prep launch size for np + nt voxels (the folded biases and head included)
+int prep_blocks(long np, long nt);
+
 
 __global__ void k_near_far(const float*, const float*, int, const float*, uint8_t*, float*, float*);
 __global__ void k_cam_rays(CamArgs a);

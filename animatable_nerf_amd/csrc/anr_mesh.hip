@@ -267,7 +267,7 @@ int anr_alpha_points(const anr_params* p, const anr_frame* f, const float* wpts,
     pa.nw_bw5 = p->novel[11]; pa.nb_bw5 = p->novel[12];
     pa.bw_latent_index = f->bw_latent_index;
   }
-  hipLaunchKernelGGL(k_prep, dim3((int)((np + 7) / 8) + 1), dim3(256), 0, s, pa);
+  hipLaunchKernelGGL(k_prep, dim3(prep_blocks(np, 0)), dim3(256), 0, s, pa);
   ANR_TRY(check_launch("k_prep"));
 
   FrontArgs fa{};

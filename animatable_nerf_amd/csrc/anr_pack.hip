@@ -194,7 +194,9 @@ __global__ void k_pack_head_b(PackArgs a) {
   }
 }
 
-// grid: blocks [0, nvox_blocks) repack volumes; block 'fold' computes the five folded biases
+// grid (prep_blocks): blocks [0, nvox_blocks) repack volumes; then one wave per folded-bias output
+// (5 x 256 of them, a 128-term dot each: lane q sums terms q and q + 64, then a wave reduction), then
+// one wave per folded-head entry (fp64 dot over the 128 latent dims)
 __global__ __launch_bounds__(256) void k_prep(PrepArgs a) {
   const int nvb = (a.np + a.nt + 7) / 8;  // 8 voxels (x 32 channels) per block
   if ((int)blockIdx.x < nvb) {
@@ -210,40 +212,51 @@ __global__ __launch_bounds__(256) void k_prep(PrepArgs a) {
     }
     return;
   }
-  // folded biases: which = 0,1 (bw0 pose/tpose), 2,3 (bw5 pose/tpose), 4 (latent_fc)
+  const int lane = threadIdx.x & 63;
+  const int k = (blockIdx.x - nvb) * 4 + (threadIdx.x >> 6);  // output index (wave-uniform)
   const int li = (int)a.latent_index[0];
-  for (int k = threadIdx.x; k < 5 * 256; k += blockDim.x) {
+  if (k < 5 * 256) {
+    // folded biases: which = 0,1 (bw0 pose/tpose), 2,3 (bw5 pose/tpose), 4 (latent_fc)
     const int which = k >> 8, nn = k & 255;
-    float acc;
+    const float *W, *lat;
+    float bias;
+    int ld, c0;
     if (which < 4) {
       const bool novel = a.novel && !(which & 1);  // pose pass of a novel-pose render
       const int row = (which & 1) ? 0 : (novel ? (int)a.bw_latent_index[0] : li + 1);
-      const float* lat = (novel ? a.n_latent : a.bw_latent) + (size_t)row * 128;
-      const float* W = which < 2 ? (novel ? a.nw_bw0 : a.w_bw0) : (novel ? a.nw_bw5 : a.w_bw5);
-      const int ld = which < 2 ? 191 : 447;
-      acc = which < 2 ? (novel ? a.nb_bw0 : a.b_bw0)[nn] : (novel ? a.nb_bw5 : a.b_bw5)[nn];
-      for (int q = 0; q < 128; ++q) acc = fmaf(W[(size_t)nn * ld + 63 + q], lat[q], acc);
+      lat = (novel ? a.n_latent : a.bw_latent) + (size_t)row * 128;
+      W = which < 2 ? (novel ? a.nw_bw0 : a.w_bw0) : (novel ? a.nw_bw5 : a.w_bw5);
+      ld = which < 2 ? 191 : 447;
+      c0 = 63;
+      bias = which < 2 ? (novel ? a.nb_bw0 : a.b_bw0)[nn] : (novel ? a.nb_bw5 : a.b_bw5)[nn];
     } else {
-      const float* lat = a.nf_latent + (size_t)li * 128;
-      acc = a.b_lat[nn];
-      for (int q = 0; q < 128; ++q) acc = fmaf(a.w_lat[(size_t)nn * 384 + 256 + q], lat[q], acc);
+      lat = a.nf_latent + (size_t)li * 128;
+      W = a.w_lat;
+      ld = 384;
+      c0 = 256;
+      bias = a.b_lat[nn];
     }
-    a.fold[k] = acc;
+    const float* row = W + (size_t)nn * ld + c0;
+    float acc = fmaf(row[lane], lat[lane], row[lane + 64] * lat[lane + 64]);
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+    if (lane == 0) a.fold[k] = acc + bias;
+    return;
   }
-  if (a.head_P) {
+  const int i = k - 5 * 256;  // folded-head entry
+  if (!a.head_P || i >= ANR_FOLD_FLOATS - ANR_FOLD_HEAD) return;
+  float v = 0.0f;
+  if (i < 128) {
     const float* lat = a.nf_latent + (size_t)li * 128;
-    for (int i = threadIdx.x; i < ANR_FOLD_FLOATS - ANR_FOLD_HEAD; i += blockDim.x) {
-      float v = 0.0f;
-      if (i < 128) {
-        double acc = a.head_q[i];
-        for (int j = 0; j < 128; ++j) acc += (double)a.head_P[i * 128 + j] * (double)lat[j];
-        v = (float)acc;
-      } else if (i == 128) {
-        v = a.b_alpha[0];
-      }
-      a.fold[ANR_FOLD_HEAD + i] = v;
-    }
+    double acc = (double)a.head_P[i * 128 + lane] * (double)lat[lane] +
+                 (double)a.head_P[i * 128 + lane + 64] * (double)lat[lane + 64];
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+    v = (float)(acc + (double)a.head_q[i]);
+  } else if (i == 128) {
+    v = a.b_alpha[0];
   }
+  if (lane == 0) a.fold[ANR_FOLD_HEAD + i] = v;
 }
+
+int prep_blocks(long np, long nt) { return (int)((np + nt + 7) / 8) + (5 * 256 + ANR_FOLD_FLOATS - ANR_FOLD_HEAD + 3) / 4; }
 
 }  // namespace anr

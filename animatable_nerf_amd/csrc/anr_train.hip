@@ -67,20 +67,40 @@ __device__ __forceinline__ void softmax24(const float* __restrict__ logits, cons
   for (int j = 0; j < 24; ++j) out[j] = l[j] / s;
 }
 
-// thread per sample: pbw softmax, LBS to the T-pose, gamma(x_T), init_tbw
+// sums / max over the 64 lanes of a wave, or over the 32 lanes of a half-wave (every lane gets it)
+__device__ __forceinline__ float wave_sum(float v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+__device__ __forceinline__ float half_sum(float v) {
+  for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
+
+// one wave per sample: pbw softmax (lane = joint), LBS to the T-pose, gamma(x_T) (lane = feature),
+// init_tbw (lane = channel); every row written by consecutive lanes
 __global__ __launch_bounds__(256) void k_tr_softmax_lbs(TrainBufs b) {
 #pragma clang fp contract(fast)
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int n = *b.n_kept;
   if (i >= n) return;
-  float bw[24];
-  softmax24(b.Lp + (long)i * 32, b.Ip + (long)i * 32, bw);
-  float Ab[16];
-  for (int m = 0; m < 16; ++m) Ab[m] = 0.f;
-  for (int j = 0; j < 24; ++j) {
-    b.Bp[(long)i * 24 + j] = bw[j];
-    for (int m = 0; m < 16; ++m) Ab[m] += bw[j] * b.A[j * 16 + m];
-  }
+  // softmax(log(init + 1e-9) + logits) over the 24 joints
+  const float l = lane < 24 ? logf(b.Ip[(long)i * 32 + lane] + 1e-9f) + b.Lp[(long)i * 32 + lane] : -INFINITY;
+  const float m = wave_max(l);
+  const float ex = lane < 24 ? expf(l - m) : 0.f;
+  const float bw = ex / wave_sum(ex);
+  if (lane < 24) b.Bp[(long)i * 24 + lane] = bw;
+  // blended transform sum_j bw_j A_j: lane q < 16 accumulates entry q
+  float ab = 0.f;
+  for (int j = 0; j < 24; ++j) ab += __shfl(bw, j) * b.A[j * 16 + (lane & 15)];
+  float Ab[12];
+#pragma unroll
+  for (int q = 0; q < 12; ++q) Ab[q] = __shfl(ab, q);
   const float a = Ab[0], bb = Ab[1], c = Ab[2], d = Ab[4], e = Ab[5], f = Ab[6], g = Ab[8], h = Ab[9], k = Ab[10];
   const float c00 = e * k - f * h, c01 = c * h - bb * k, c02 = bb * f - c * e;
   const float c10 = f * g - d * k, c11 = a * k - c * g, c12 = c * d - a * f;
@@ -91,18 +111,22 @@ __global__ __launch_bounds__(256) void k_tr_softmax_lbs(TrainBufs b) {
   const float y[3] = {pt[0] - Ab[3], pt[1] - Ab[7], pt[2] - Ab[11]};
   float tp[3];
   for (int r = 0; r < 3; ++r) tp[r] = Ri[3 * r] * y[0] + Ri[3 * r + 1] * y[1] + Ri[3 * r + 2] * y[2];
-  float* L = b.lbs + (long)i * 16;
-  for (int q = 0; q < 9; ++q) L[q] = Ri[q];
-  L[9] = y[0]; L[10] = y[1]; L[11] = y[2];
-  bool inside = true;
-  for (int r = 0; r < 3; ++r) inside = inside && tp[r] > b.tbounds[r] && tp[r] < b.tbounds[3 + r];
-  pt[4] = tp[0]; pt[5] = tp[1]; pt[6] = tp[2]; pt[7] = inside ? 1.f : 0.f;
-  for (int q = 0; q < 64; ++q) b.Gt[(long)i * 64 + q] = q < 63 ? embed_feature(tp, q, 10) : 0.f;
-  float lo[3], hi[3];
-  for (int r = 0; r < 3; ++r) { lo[r] = b.tbounds[r]; hi[r] = b.tbounds[3 + r]; }
-  TriCell cell;
-  tri_cell(tp, lo, hi, b.tX, b.tY, b.tZ, cell);
-  for (int j = 0; j < 32; ++j) b.It[(long)i * 32 + j] = j < 24 ? tri_channel(b.tbw, 25, j, cell) : 0.f;
+  if (lane == 0) {
+    float* L = b.lbs + (long)i * 16;
+    for (int q = 0; q < 9; ++q) L[q] = Ri[q];
+    L[9] = y[0]; L[10] = y[1]; L[11] = y[2];
+    bool inside = true;
+    for (int r = 0; r < 3; ++r) inside = inside && tp[r] > b.tbounds[r] && tp[r] < b.tbounds[3 + r];
+    pt[4] = tp[0]; pt[5] = tp[1]; pt[6] = tp[2]; pt[7] = inside ? 1.f : 0.f;
+  }
+  b.Gt[(long)i * 64 + lane] = lane < 63 ? embed_feature(tp, lane, 10) : 0.f;
+  if (lane < 32) {
+    float lo[3], hi[3];
+    for (int r = 0; r < 3; ++r) { lo[r] = b.tbounds[r]; hi[r] = b.tbounds[3 + r]; }
+    TriCell cell;
+    tri_cell(tp, lo, hi, b.tX, b.tY, b.tZ, cell);
+    b.It[(long)i * 32 + lane] = lane < 24 ? tri_channel(b.tbw, 25, lane, cell) : 0.f;
+  }
 }
 
 // free points (Network.calculate_neural_blend_weights / TPoseHuman.calculate_alpha): one wave per
@@ -304,70 +328,70 @@ __global__ __launch_bounds__(256) void k_tr_raw_bwd(TrainBufs b) {
   b.dAlpha[i] = pt[7] > 0.f ? ds : 0.f;
 }
 
-// upstream pbw / tbw row gradients scattered to the compact samples (alpha_ind rows)
+// upstream pbw / tbw row gradients scattered to the compact samples (alpha_ind rows); half a wave per
+// sample, lane = joint
 __global__ __launch_bounds__(256) void k_tr_rows_bwd(TrainBufs b) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int hl = threadIdx.x & 31;
+  const int i = blockIdx.x * 8 + (threadIdx.x >> 5);
   const int n = *b.n_kept;
-  if (i >= n) return;
+  if (i >= n || hl >= 24) return;
   const int row = b.out_row[i];
-  for (int c = 0; c < 24; ++c) {
-    b.dBp[(long)i * 24 + c] = (row >= 0 && b.d_pbw) ? b.d_pbw[(long)row * 24 + c] : 0.f;
-    b.dBt[(long)i * 24 + c] = (row >= 0 && b.d_tbw) ? b.d_tbw[(long)row * 24 + c] : 0.f;
-  }
+  b.dBp[(long)i * 24 + hl] = (row >= 0 && b.d_pbw) ? b.d_pbw[(long)row * 24 + hl] : 0.f;
+  b.dBt[(long)i * 24 + hl] = (row >= 0 && b.d_tbw) ? b.d_tbw[(long)row * 24 + hl] : 0.f;
 }
 
-// softmax(log(init + 1e-9) + logits) backward (T-pose pass): d logits and d init_tbw
+// softmax(log(init + 1e-9) + logits) backward (T-pose pass): d logits and d init_tbw; half a wave per
+// sample, lane = joint
 __global__ __launch_bounds__(256) void k_tr_softmax_bwd_t(TrainBufs b) {
 #pragma clang fp contract(fast)
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int hl = threadIdx.x & 31;
+  const int i = blockIdx.x * 8 + (threadIdx.x >> 5);
   const int n = *b.n_kept;
   if (i >= n) return;
-  const float* B = b.Bt + (long)i * 24;
-  const float* dB = b.dBt + (long)i * 24;
-  float dot = 0.f;
-  for (int j = 0; j < 24; ++j) dot += dB[j] * B[j];
-  for (int j = 0; j < 32; ++j) {
-    const float dl = j < 24 ? B[j] * (dB[j] - dot) : 0.f;
-    b.dLt[(long)i * 32 + j] = dl;
-    b.dIt[(long)i * 32 + j] = j < 24 ? dl / (b.It[(long)i * 32 + j] + 1e-9f) : 0.f;
-  }
+  const float B = hl < 24 ? b.Bt[(long)i * 24 + hl] : 0.f;
+  const float dB = hl < 24 ? b.dBt[(long)i * 24 + hl] : 0.f;
+  const float dot = half_sum(dB * B);
+  const float dl = hl < 24 ? B * (dB - dot) : 0.f;
+  b.dLt[(long)i * 32 + hl] = dl;
+  b.dIt[(long)i * 32 + hl] = hl < 24 ? dl / (b.It[(long)i * 32 + hl] + 1e-9f) : 0.f;
 }
 
 __global__ __launch_bounds__(256) void k_tr_softmax_bwd_p(TrainBufs b) {
 #pragma clang fp contract(fast)
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int hl = threadIdx.x & 31;
+  const int i = blockIdx.x * 8 + (threadIdx.x >> 5);
   const int n = *b.n_kept;
   if (i >= n) return;
-  const float* B = b.Bp + (long)i * 24;
-  const float* dB = b.dBp + (long)i * 24;
-  float dot = 0.f;
-  for (int j = 0; j < 24; ++j) dot += dB[j] * B[j];
-  for (int j = 0; j < 32; ++j) b.dLp[(long)i * 32 + j] = j < 24 ? B[j] * (dB[j] - dot) : 0.f;
+  const float B = hl < 24 ? b.Bp[(long)i * 24 + hl] : 0.f;
+  const float dB = hl < 24 ? b.dBp[(long)i * 24 + hl] : 0.f;
+  const float dot = half_sum(dB * B);
+  b.dLp[(long)i * 32 + hl] = hl < 24 ? B * (dB - dot) : 0.f;
 }
 
 // d x_T from gamma(x_T) and from the init_tbw lookup (grid_sampler_3d backward w.r.t. the grid),
-// then LBS backward into d pbw (accumulated onto the row gradients already in dBp)
+// then LBS backward into d pbw (accumulated onto the row gradients already in dBp). One wave per
+// sample: lane = gamma feature; lane = (corner, channel group) for the lookup; lane = joint for d pbw.
 __global__ __launch_bounds__(256) void k_tr_tpose_bwd(TrainBufs b) {
 #pragma clang fp contract(fast)
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int n = *b.n_kept;
   if (i >= n) return;
   const float* pt = b.pt + (long)i * 8;
   const float tp[3] = {pt[4], pt[5], pt[6]};
-  float g[3] = {0.f, 0.f, 0.f};
-  const float* dG = b.dGt + (long)i * 64;
-  const float* dG2 = b.dGt2 ? b.dGt2 + (long)i * 64 : nullptr;
-  for (int f = 0; f < 63; ++f) {
-    const float d = dG2 ? dG[f] + dG2[f] : dG[f];
-    if (f < 3) {
-      g[f] += d;
-      continue;
+  float gc[3] = {0.f, 0.f, 0.f};
+  if (lane < 63) {
+    const float d = b.dGt[(long)i * 64 + lane] + (b.dGt2 ? b.dGt2[(long)i * 64 + lane] : 0.f);
+    if (lane < 3) {
+      gc[lane] = d;
+    } else {
+      const int q = lane - 3, k = q / 6, w = q - 6 * (q / 6), comp = w >= 3 ? w - 3 : w;
+      const float sc = (float)(1 << k);
+      const float v = tp[comp] * sc;
+      gc[comp] = w < 3 ? d * sc * cosf(v) : -d * sc * sinf(v);
     }
-    const int q = f - 3, k = q / 6, w = q - 6 * (q / 6), comp = w >= 3 ? w - 3 : w;
-    const float sc = (float)(1 << k);
-    const float v = tp[comp] * sc;
-    g[comp] += w < 3 ? d * sc * cosf(v) : -d * sc * sinf(v);
   }
+  float g[3] = {wave_sum(gc[0]), wave_sum(gc[1]), wave_sum(gc[2])};
   // grid_sample backward (align_corners, border): ATen grid_sampler_3d_backward
   {
     float lo[3], hi[3], gg[3];
@@ -390,24 +414,29 @@ __global__ __launch_bounds__(256) void k_tr_tpose_bwd(TrainBufs b) {
     const float wy[2] = {(float)(y0 + 1) - iy, iy - (float)y0};
     const float wz[2] = {(float)(z0 + 1) - iz, iz - (float)z0};
     const float* dI = b.dIt + (long)i * 32;
-    float gix = 0.f, giy = 0.f, giz = 0.f;
-    for (int k = 0; k < 8; ++k) {
-      const int ax = k & 1, ay = (k >> 1) & 1, az = k >> 2;
-      const int cx = x0 + ax, cy = y0 + ay, cz = z0 + az;
-      if (cx < 0 || cx >= b.tZ || cy < 0 || cy >= b.tY || cz < 0 || cz >= b.tX) continue;
+    // lane = corner k (lane >> 3) x channel group cg (lane & 7): channels cg, cg + 8, cg + 16
+    const int k = lane >> 3, cg = lane & 7;
+    const int ax = k & 1, ay = (k >> 1) & 1, az = k >> 2;
+    const int cx = x0 + ax, cy = y0 + ay, cz = z0 + az;
+    float sv = 0.f;
+    if (!(cx < 0 || cx >= b.tZ || cy < 0 || cy >= b.tY || cz < 0 || cz >= b.tX)) {
       const float* v = b.tbw + (long)((cz * b.tY + cy) * b.tZ + cx) * 25;
-      float s = 0.f;
-      for (int c = 0; c < 24; ++c) s += v[c] * dI[c];
-      const float sx = ax ? 1.f : -1.f, sy = ay ? 1.f : -1.f, sz = az ? 1.f : -1.f;
-      gix += sx * wy[ay] * wz[az] * s;
-      giy += wx[ax] * sy * wz[az] * s;
-      giz += wx[ax] * wy[ay] * sz * s;
+      sv = v[cg] * dI[cg] + v[cg + 8] * dI[cg + 8] + v[cg + 16] * dI[cg + 16];
     }
+    sv += __shfl_xor(sv, 1);
+    sv += __shfl_xor(sv, 2);
+    sv += __shfl_xor(sv, 4);
+    const float sx = ax ? 1.f : -1.f, sy = ay ? 1.f : -1.f, sz = az ? 1.f : -1.f;
+    const bool own = cg == 0;
+    const float gix = wave_sum(own ? sx * wy[ay] * wz[az] * sv : 0.f);
+    const float giy = wave_sum(own ? wx[ax] * sy * wz[az] * sv : 0.f);
+    const float giz = wave_sum(own ? wx[ax] * wy[ay] * sz * sv : 0.f);
     g[2] += gix * mult[0] * 2.0f / (hi[2] - lo[2]);
     g[1] += giy * mult[1] * 2.0f / (hi[1] - lo[1]);
     g[0] += giz * mult[2] * 2.0f / (hi[0] - lo[0]);
   }
   // LBS backward (blend_utils.py:41-59): x_T = Rinv y, y = x - t, [R|t] = sum_j bw_j A_j
+  if (lane >= 24) return;
   const float* L = b.lbs + (long)i * 16;
   float dy[3];
   for (int c = 0; c < 3; ++c) dy[c] = L[0 * 3 + c] * g[0] + L[1 * 3 + c] * g[1] + L[2 * 3 + c] * g[2];
@@ -416,12 +445,9 @@ __global__ __launch_bounds__(256) void k_tr_tpose_bwd(TrainBufs b) {
     for (int c = 0; c < 3; ++c) dAb[4 * a + c] = -dy[a] * tp[c];
     dAb[4 * a + 3] = -dy[a];
   }
-  float* dB = b.dBp + (long)i * 24;
-  for (int j = 0; j < 24; ++j) {
-    float s = 0.f;
-    for (int q = 0; q < 12; ++q) s += dAb[q] * b.A[j * 16 + q];
-    dB[j] += s;
-  }
+  float sum = 0.f;
+  for (int q = 0; q < 12; ++q) sum += dAb[q] * b.A[lane * 16 + q];
+  b.dBp[(long)i * 24 + lane] += sum;
 }
 
 // latent columns folded into the bias (row = li[0] + add when li, else add):

@@ -456,7 +456,7 @@ int train_forward(const anr_params* p, const anr_frame* f, const float* ray_o, c
     ANR_TRY(bw_forward(e, p->t + 27, b.Gp, (float*)(ws + T.Hp), b.Lp, N, FOLD(0), FOLD(2)));
   }
   if (n > 0) {
-    hipLaunchKernelGGL(k_tr_softmax_lbs, dim3(g1), dim3(256), 0, s, b);
+    hipLaunchKernelGGL(k_tr_softmax_lbs, dim3((g1 * 256 + 3) / 4), dim3(256), 0, s, b);
     ANR_TRY(check_launch("k_tr_softmax_lbs"));
   }
   // T-pose BW MLP on s2, beside the canonical NeRF (both read only gamma(x_T))
@@ -528,9 +528,9 @@ int train_backward(const anr_params* p, float* const* g, const anr_frame* f, con
   const hipStream_t s2 = e.s2();
   ANR_TRY(order(e.ss, s2, s));
   // upstream pbw / tbw row gradients, T-pose softmax backward (s2)
-  hipLaunchKernelGGL(k_tr_rows_bwd, dim3(g1), dim3(256), 0, s2, b);
+  hipLaunchKernelGGL(k_tr_rows_bwd, dim3((g1 * 256 + 7) / 8), dim3(256), 0, s2, b);
   ANR_TRY(check_launch("k_tr_rows_bwd"));
-  hipLaunchKernelGGL(k_tr_softmax_bwd_t, dim3(g1), dim3(256), 0, s2, b);
+  hipLaunchKernelGGL(k_tr_softmax_bwd_t, dim3((g1 * 256 + 7) / 8), dim3(256), 0, s2, b);
   ANR_TRY(check_launch("k_tr_softmax_bwd_t"));
 
   // compositing (or the caller's d raw) + raw activations
@@ -604,9 +604,9 @@ int train_backward(const anr_params* p, float* const* g, const anr_frame* f, con
   while (!tb.done()) ANR_TRY(tb.step());
   ANR_TRY(order(e.ss, s, s2));  // join: dGt2, dBp rows
   // x_T gradient (gamma + init_tbw lookup) -> LBS -> d pbw; pose BW backward (latent row li + 1)
-  hipLaunchKernelGGL(k_tr_tpose_bwd, dim3(g1), dim3(256), 0, s, b);
+  hipLaunchKernelGGL(k_tr_tpose_bwd, dim3((g1 * 256 + 3) / 4), dim3(256), 0, s, b);
   ANR_TRY(check_launch("k_tr_tpose_bwd"));
-  hipLaunchKernelGGL(k_tr_softmax_bwd_p, dim3(g1), dim3(256), 0, s, b);
+  hipLaunchKernelGGL(k_tr_softmax_bwd_p, dim3((g1 * 256 + 7) / 8), dim3(256), 0, s, b);
   ANR_TRY(check_launch("k_tr_softmax_bwd_p"));
   return ANR_OK;
 }
@@ -697,7 +697,7 @@ int anim_path(const anr_params* p, float* const* grads, const anr_frame* f, cons
       PoseScope ps(e);
       ANR_TRY(bw_forward(e, p->novel, b.Gp, Hp, b.Lp, N, AFOLD(0), AFOLD(2)));
     }
-    hipLaunchKernelGGL(k_tr_softmax_lbs, dim3(g1), dim3(256), 0, s, b);
+    hipLaunchKernelGGL(k_tr_softmax_lbs, dim3((g1 * 256 + 3) / 4), dim3(256), 0, s, b);
     ANR_TRY(bw_forward(e, p->t + 27, b.Gt, Ht, b.Lt, N, AFOLD(1), AFOLD(3)));
     hipLaunchKernelGGL(k_tr_softmax_t, dim3(g1), dim3(256), 0, s, b);
     ANR_TRY(nerf_alpha_fwd(e, p, b, (float*)(ws + T.Hn), N));
@@ -723,12 +723,12 @@ int anim_path(const anr_params* p, float* const* grads, const anr_frame* f, cons
   if (obs) {
     // tbw0 depends on novel_pose_bw through x_T: frozen T-pose BW MLP (input gradient only),
     // gamma + init_tbw lookup, LBS inverse -> d pbw (k_tr_tpose_bwd)
-    hipLaunchKernelGGL(k_tr_softmax_bwd_t, dim3(g1), dim3(256), 0, s, b);
+    hipLaunchKernelGGL(k_tr_softmax_bwd_t, dim3((g1 * 256 + 7) / 8), dim3(256), 0, s, b);
     if (hipMemsetAsync(b.dGt, 0, (size_t)n * 64 * 4, s) != hipSuccess) return fail(ANR_E_HIP, "memset");
     ANR_TRY(bw_backward(e, p->t + 27, nullptr, b.Gt, Ht, b.dLt, dA, dB, 0, b.dGt, false, N, ysum, nullptr, 0));
-    hipLaunchKernelGGL(k_tr_tpose_bwd, dim3(g1), dim3(256), 0, s, b);
+    hipLaunchKernelGGL(k_tr_tpose_bwd, dim3((g1 * 256 + 3) / 4), dim3(256), 0, s, b);
   }
-  hipLaunchKernelGGL(k_tr_softmax_bwd_p, dim3(g1), dim3(256), 0, s, b);
+  hipLaunchKernelGGL(k_tr_softmax_bwd_p, dim3((g1 * 256 + 7) / 8), dim3(256), 0, s, b);
   ANR_TRY(check_launch("anim backward"));
   PoseScope ps(e);
   return bw_backward(e, p->novel, grads, b.Gp, Hp, b.dLp, dA, dB, 0, nullptr, false, N, ysum + 512, f->bw_latent_index, 0);
@@ -990,7 +990,7 @@ int anr_anim_step(const anr_params* p, float* const* grads, const anr_frame* f, 
   pa.nw_bw0 = p->novel[1]; pa.nb_bw0 = p->novel[2];
   pa.nw_bw5 = p->novel[11]; pa.nb_bw5 = p->novel[12];
   pa.bw_latent_index = f->bw_latent_index;
-  hipLaunchKernelGGL(k_prep, dim3(1), dim3(256), 0, s, pa);
+  hipLaunchKernelGGL(k_prep, dim3(prep_blocks(0, 0)), dim3(256), 0, s, pa);
   ANR_TRY(check_launch("k_prep(anim)"));
   Exec e{s, 0, (o->precision == ANR_BF16 || o->precision == ANR_BF16_ALL) ? 1 : 0, o->precision == ANR_BF16 ? 1 : 0};
   ANR_TRY(pack_images(e, p, ws + T.wimg, s, (float*)(ws + T.wslab), true));
