@@ -212,12 +212,62 @@ class Renderer:
         rgb, acc, depth, raw, pbw, tbw = _TrainRender.apply(self, batch, t_rand, *params)
         return {'rgb_map': rgb, 'acc_map': acc, 'depth_map': depth, 'raw': raw, 'pbw': pbw, 'tbw': tbw}
 
+    # render(): the frame in this many parts (whole reference chunks) so part k's outputs cross the
+    # host link while part k + 1 renders (a 512x512 frame moves ~1.4 GB to the host)
+    HOST_PARTS = 4
+
     def render(self, batch):
         if torch.is_grad_enabled() and any(p.requires_grad for p in self.net.parameters()) and self.net.training:
             return self.render_train(batch)
+        R = batch['ray_o'].shape[1]
+        chunk = int(self.cfg.get('chunk', CHUNK))
+        n_chunks = (R + chunk - 1) // chunk
         with torch.no_grad():
-            ret = self.render_device(batch)
-        return to_host(ret)
+            if n_chunks < 2 * self.HOST_PARTS or not self.device().type == 'cuda':
+                return to_host(self.render_device(batch))
+            return self._render_overlapped(batch, R, chunk)
+
+    def _render_overlapped(self, batch, R, chunk):
+        """render_device over parts of whole chunks (per-chunk semantics unchanged: the rows of the parts,
+        concatenated in order, are the whole frame's, as parallel.render_sharded relies on), each part's
+        outputs copied on a side stream into page-locked host buffers while the next part renders."""
+        from .parallel import RAY_KEYS as SLICED, shard_chunks
+        dev = self.device()
+        ns = int(self.cfg.N_samples)
+        if getattr(self, '_copy_stream', None) is None:
+            self._copy_stream = torch.cuda.Stream(dev)
+        cs = self._copy_stream
+        # fresh page-locked outputs per call (torch's caching host allocator recycles freed ones); the
+        # row count is known only part by part, so pbw / tbw are views of capacity-sized buffers
+        pin = dict(dtype=torch.float32, pin_memory=True)
+        h = {'rgb_map': torch.empty((1, R, 3), **pin), 'acc_map': torch.empty((1, R), **pin),
+             'depth_map': torch.empty((1, R), **pin), 'raw': torch.empty((1, R * ns, 4), **pin),
+             'pbw': torch.empty((1, R * ns, 24), **pin), 'tbw': torch.empty((1, R * ns, 24), **pin)}
+        keep, m_off, kept = [], 0, 0
+        for k in range(self.HOST_PARTS):
+            a, b = shard_chunks(R, k, self.HOST_PARTS, chunk)
+            if a >= b:
+                continue
+            sub = {key_: (v[:, a:b] if key_ in SLICED and torch.is_tensor(v) else v) for key_, v in batch.items()}
+            out = self.render_device(sub)  # reads the part's row count: the part has finished when it returns
+            m = out['pbw'].shape[1]
+            ev = torch.cuda.Event()
+            ev.record()
+            with torch.cuda.stream(cs):
+                cs.wait_event(ev)
+                h['rgb_map'][:, a:b].copy_(out['rgb_map'], non_blocking=True)
+                h['acc_map'][:, a:b].copy_(out['acc_map'], non_blocking=True)
+                h['depth_map'][:, a:b].copy_(out['depth_map'], non_blocking=True)
+                h['raw'][:, a * ns:b * ns].copy_(out['raw'], non_blocking=True)
+                h['pbw'][:, m_off:m_off + m].copy_(out['pbw'], non_blocking=True)
+                h['tbw'][:, m_off:m_off + m].copy_(out['tbw'], non_blocking=True)
+            keep.append(out)  # device outputs stay alive until their copies are done
+            m_off += m
+            kept += self.last_counts[0]
+        cs.synchronize()
+        self.last_counts = (kept, m_off)
+        return {'rgb_map': h['rgb_map'], 'acc_map': h['acc_map'], 'depth_map': h['depth_map'], 'raw': h['raw'],
+                'pbw': h['pbw'][:, :m_off], 'tbw': h['tbw'][:, :m_off]}
 
     def counts(self, n_rays):
         """(kept samples, alpha_ind rows) of the last evaluation render (device read, syncs)."""

@@ -322,8 +322,10 @@ def main():
         progress(f'Renderer.render with D2H: {rs * 1e3:.2f} ms')
         result['render_s'] = {'seconds': rs, 'value': R * 64 / rs, 'unit': 'ray-samples/s',
                               'call': 'Renderer.render(batch): fused render + .cpu() of rgb/acc/depth/raw/pbw/tbw '
-                                      '(%.0f MB to the host)' % (sum(v.numel() * v.element_size()
-                                                                      for v in host.values()) / 1e6),
+                                      '(%.0f MB to the host; the frame in %d parts of whole chunks, each copied to '
+                                      'page-locked memory while the next renders)' % (
+                                          sum(v.numel() * v.element_size() for v in host.values()) / 1e6,
+                                          renderer.HOST_PARTS),
                               'median_of': 3}
         del host
     if rank == 0 and world == 1 and not args.no_cpu:

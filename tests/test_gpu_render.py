@@ -224,6 +224,29 @@ def test_mmsk_visibility_filter_matches_reference(renderer, dev):
     assert torch.equal(_keep(ret['raw']).cpu(), _keep(ref_raw))
 
 
+def test_render_overlapped_host_copy_equals_device_render(renderer, dev):
+    """Renderer.render (the drop-in call, outputs on the host) renders a frame of >= 8 chunks in
+    parts of whole chunks and copies each part to page-locked memory while the next renders: every
+    output, the alpha_ind rows included, equals the one-call device render moved to the host."""
+    sc = scene(0.025)
+    ro, rd = sc.box_rays(9 * 2048 + 777, seed=4)
+    b, _ = batch_np(sc, ro, rd)
+    bt = to_torch(b, dev)
+    full = renderer.render_device(bt)
+    ref = {k: v.cpu() for k, v in full.items()}
+    with torch.no_grad():  # as run.py evaluates (network in train() mode, perturb 0)
+        got = renderer.render(bt)
+    assert renderer.last_counts[1] == ref['pbw'].shape[1]
+    for k in ('rgb_map', 'acc_map', 'depth_map', 'raw', 'pbw', 'tbw'):
+        assert not got[k].is_cuda, k
+        assert got[k].shape == ref[k].shape, (k, got[k].shape, ref[k].shape)
+        assert torch.equal(got[k], ref[k]), k
+    with torch.no_grad():
+        again = renderer.render(bt)  # a second call does not overwrite the first call's outputs
+    assert again['raw'].data_ptr() != got['raw'].data_ptr()
+    assert torch.equal(got['raw'], ref['raw'])
+
+
 @pytest.mark.parametrize('world', [3, 8])
 def test_frame_shards_equal_whole_frame(renderer, dev, world):
     """§8(e): one frame split over `world` ranks by whole chunks (parallel.shard_batch, as
