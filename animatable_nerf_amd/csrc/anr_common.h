@@ -174,6 +174,23 @@ __device__ __forceinline__ int block_excl_scan_256(int v, int* sh, int& total) {
   return base + x - v;
 }
 
+// exp(z) within ~2 ulp: exact-split exponent, v_exp_f32 on the reduced argument, ldexp (the
+// libm-accurate expf costs ~3x the instructions; the softplus epilogues are VALU-bound on it)
+__device__ __forceinline__ float fast_exp(float z) {
+  const float n = rintf(z * 1.44269502f);
+  const float r = fmaf(z, 1.44269502f, -n) + z * 1.92596299e-8f;
+  return ldexpf(__builtin_amdgcn_exp2f(r), (int)n);
+}
+
+// log1p(e), e >= 0, within a few ulp: a 6-term series below 1/32, else log(u) e / (u - 1) with
+// u = 1 + e (Goldberg's correction of the rounding in u; u - 1 is exact)
+__device__ __forceinline__ float fast_log1p(float e) {
+  const float s = e * (1.f + e * (-0.5f + e * (0.333333343f + e * (-0.25f + e * (0.2f + e * -0.166666672f)))));
+  const float u = 1.f + e;
+  const float l = __builtin_amdgcn_logf(u) * 0.693147182f * (e * __builtin_amdgcn_rcpf(u - 1.f));
+  return e < 0.03125f ? s : l;
+}
+
 // softplus(beta=100, threshold=20) backward factor sigmoid(100 z) recomputed from the layer's OUTPUT
 // h = softplus(z) instead of a stored exp(100 z): sigmoid(100 z) = 1 - exp(-100 h) exactly (above the
 // threshold h = z and the factor rounds to 1, as torch's pass-through). One hardware exp2: the factor

@@ -144,14 +144,14 @@ __device__ __forceinline__ void epilogue(const GemmArgs& g, const f32x4 (&acc)[2
         if (g.relu) v = fmaxf(v, 0.f);
         if (g.softplus) {  // torch softplus(beta=100, threshold=20) and the factor its backward uses
           const float z = v * 100.f;
-          const float e = expf(z);
+          const float e = fast_exp(z);
           if (g.deriv) g.deriv[(long)m * g.ldd + n] = z > 20.f ? -1.f : e;
-          v = z > 20.f ? v : log1pf(e) / 100.f;
+          v = z > 20.f ? v : fast_log1p(e) / 100.f;
         }
         if (g.spd && n < g.spd_n) {
           const float d = g.spd[(long)m * g.ldsd + n];
           if (g.spd_h) v = v * softplus_factor_h(g.spd_scale != 0.f ? d * g.spd_scale : d);
-          else if (d >= 0.f) v = v * d / (d + 1.f);
+          else if (d >= 0.f) v = v * d * __builtin_amdgcn_rcpf(d + 1.f);
         }
         if (g.mask && !(g.mask[(long)m * g.ldm + n] > 0.f)) v = 0.f;
         if (g.div_post != 0.f) v = v / g.div_post;
@@ -199,14 +199,14 @@ __device__ __forceinline__ void epilogue_sw(const GemmArgs& g, const f32x4 (&acc
           if (g.relu) x = fmaxf(x, 0.f);
           if (g.softplus) {  // torch softplus(beta=100, threshold=20) and the factor its backward uses
             const float z = x * 100.f;
-            const float ez = expf(z);
+            const float ez = fast_exp(z);
             dv[e] = z > 20.f ? -1.f : ez;
-            x = z > 20.f ? x : log1pf(ez) / 100.f;
+            x = z > 20.f ? x : fast_log1p(ez) / 100.f;
           }
           if (g.spd && n + e < g.spd_n) {
             const float d = sp[i][j][e];
             if (g.spd_h) x = x * softplus_factor_h(g.spd_scale != 0.f ? d * g.spd_scale : d);
-            else if (d >= 0.f) x = x * d / (d + 1.f);
+            else if (d >= 0.f) x = x * d * __builtin_amdgcn_rcpf(d + 1.f);
           }
           if (g.mask && !(mk[i][j][e] > 0.f)) x = 0.f;
           if (g.div_post != 0.f) x = x / g.div_post;
@@ -234,14 +234,14 @@ __device__ __forceinline__ void epilogue_sw(const GemmArgs& g, const f32x4 (&acc
         if (g.relu) v = fmaxf(v, 0.f);
         if (g.softplus) {
           const float z = v * 100.f;
-          const float e = expf(z);
+          const float e = fast_exp(z);
           if (g.deriv) g.deriv[(long)m * g.ldd + n] = z > 20.f ? -1.f : e;
-          v = z > 20.f ? v : log1pf(e) / 100.f;
+          v = z > 20.f ? v : fast_log1p(e) / 100.f;
         }
         if (g.spd && n < g.spd_n) {
           const float d = g.spd[(long)m * g.ldsd + n];
           if (g.spd_h) v = v * softplus_factor_h(g.spd_scale != 0.f ? d * g.spd_scale : d);
-          else if (d >= 0.f) v = v * d / (d + 1.f);
+          else if (d >= 0.f) v = v * d * __builtin_amdgcn_rcpf(d + 1.f);
         }
         if (g.mask && !(g.mask[(long)m * g.ldm + n] > 0.f)) v = 0.f;
         if (g.div_post != 0.f) v = v / g.div_post;

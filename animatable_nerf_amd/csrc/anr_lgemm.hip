@@ -115,22 +115,8 @@ __global__ void k_limg_pack(LPack p) {
   p.out[o + 512] = lo;
 }
 
-// exp(z) within ~2 ulp: exact-split exponent, v_exp_f32 on the reduced argument, ldexp (the
-// libm-accurate expf costs ~3x the instructions, and the softplus layers are VALU-bound on it)
-__device__ __forceinline__ float lg_exp(float z) {
-  const float n = rintf(z * 1.44269502f);
-  const float r = fmaf(z, 1.44269502f, -n) + z * 1.92596299e-8f;
-  return ldexpf(__builtin_amdgcn_exp2f(r), (int)n);
-}
-
-// log1p(e), e >= 0, within a few ulp: a 6-term series below 1/32, else log(u) e / (u - 1) with
-// u = 1 + e (Goldberg's correction of the rounding in u; u - 1 is exact)
-__device__ __forceinline__ float lg_log1p(float e) {
-  const float s = e * (1.f + e * (-0.5f + e * (0.333333343f + e * (-0.25f + e * (0.2f + e * -0.166666672f)))));
-  const float u = 1.f + e;
-  const float l = __builtin_amdgcn_logf(u) * 0.693147182f * (e * __builtin_amdgcn_rcpf(u - 1.f));
-  return e < 0.03125f ? s : l;
-}
+__device__ __forceinline__ float lg_exp(float z) { return fast_exp(z); }
+__device__ __forceinline__ float lg_log1p(float e) { return fast_log1p(e); }
 
 // epilogue of one 16-sample tile: lane holds C[16 t + (lane & 15)][n0 + 16 ob + 4 (lane >> 4) + r].
 // Bias comes from LDS, the softplus-backward factors were loaded before the tile's MFMAs (sp); the
