@@ -181,20 +181,23 @@ bool wimg_view(const void* base, const float* const* t, const float* W, int c0, 
 // weight image each workgroup streams serves 128 rows. bf16: 64-deep K chunks. X3 (split-bf16,
 // fp32-level: lo*h + h*lo + h*h, the weight rows' lo image riding in the same slot): 32-deep chunks
 // so that three 128-row operand images fit two slots.
-template <bool X3> struct RgCfg {
+template <bool X3, bool ABF = false> struct RgCfg {
   static constexpr int BM = 128;
   static constexpr int WAVES = BM / 16;
   static constexpr int KC = X3 ? 32 : 64;                              // K chunk
-  static constexpr int A_BYTES = BM * KC * 4;                          // fp32 activations, BM rows x KC
+  static constexpr int AE = ABF ? 2 : 4;                               // bytes per activation element
+  static constexpr int A_BYTES = BM * KC * AE;                         // activations, BM rows x KC
   static constexpr int B_BYTES = 256 * KC * 2;                         // bf16 weight rows, 256 x KC
-  static constexpr int NS = 2;                                         // ring slots
   static constexpr int SLOT = A_BYTES + B_BYTES * (X3 ? 2 : 1);        // bytes per slot
+  // ring slots: as many as fit 160 KiB (a K = 256 product is 4 or 8 chunks; two slots leave one
+  // chunk's DMA latency exposed per chunk, three hide most of it)
+  static constexpr int NS = 3 * SLOT <= 160 * 1024 ? 3 : 2;
   static constexpr int PIECES_A = A_BYTES / 1024 / WAVES;              // per wave
   static constexpr int PIECES_B = B_BYTES / 1024 / WAVES;
   static constexpr int OPS = PIECES_A + PIECES_B * (X3 ? 2 : 1);       // vmem ops per wave per chunk
-  static constexpr int CHA = KC / 4, CHB = KC / 8;                     // 16-B chunks per A / B row
+  static constexpr int CHA = KC * AE / 16, CHB = KC / 8;              // 16-B chunks per A / B row
   // XOR swizzle of a row's 16-B chunks, chosen so the 16 rows of one fragment read hit distinct banks
-  static __device__ __forceinline__ int swa(int r) { return X3 ? ((r >> 1) & 7) : (r & 15); }
+  static __device__ __forceinline__ int swa(int r) { return X3 ? ((r >> 1) & 7) : ABF ? (r & 7) : (r & 15); }
   static __device__ __forceinline__ int swb(int r) { return X3 ? ((r >> 2) & 3) : (r & 7); }
 };
 
@@ -211,11 +214,11 @@ __device__ __forceinline__ void rg_dma(const void* src, unsigned m0) {
 }
 
 // issue chunk c (segment-relative K offset kk) into ring slot `slot`
-template <bool X3>
+template <bool X3, bool ABF>
 __device__ __forceinline__ void rg_issue(const RGemm& g, int seg, int kk, int m0, int M, int N, unsigned slot_lds, int w,
                                          int lane) {
-  using C = RgCfg<X3>;
-  const float* A = seg ? g.seg[1].A : g.seg[0].A;
+  using C = RgCfg<X3, ABF>;
+  const unsigned char* A = (const unsigned char*)(seg ? g.seg[1].A : g.seg[0].A);
   const long lda = seg ? g.seg[1].lda : g.seg[0].lda;
   const unsigned short* B = seg ? g.seg[1].B : g.seg[0].B;
   const long ldb = seg ? g.seg[1].ldb : g.seg[0].ldb;
@@ -230,7 +233,7 @@ __device__ __forceinline__ void rg_issue(const RGemm& g, int seg, int kk, int m0
     const int r = RPA * p + lane / C::CHA;
     const int gr = min(m0 + r, M - 1);
     const int ch = (lane % C::CHA) ^ C::swa(r);
-    rg_dma(A + (long)gr * lda + kk + ch * 4, slot_lds + p * 1024);
+    rg_dma(A + ((long)gr * lda + kk) * C::AE + ch * 16, slot_lds + p * 1024);
   }
   // B: 256 rows x CHB chunks, chunk q of row r holds source chunk q ^ swb(r)
 #pragma unroll
@@ -255,10 +258,13 @@ __device__ __forceinline__ void rg_issue(const RGemm& g, int seg, int kk, int m0
   (void)N;
 }
 
-template <bool X3>
+// MBF: the mask rows are bf16 (a template parameter, so every epilogue load stays one straight-line
+// batch ahead of its use; a runtime branch around them would drain the loads one by one)
+template <bool X3, bool ABF, bool MBF>
 __global__ __launch_bounds__(RgCfg<X3>::WAVES * 64) void k_rgemm(RGemm g) {
-  constexpr int RG_NS = RgCfg<X3>::NS, RG_SLOT = RgCfg<X3>::SLOT, RG_OPS = RgCfg<X3>::OPS;
-  constexpr int RG_BM = RgCfg<X3>::BM, RG_A_BYTES = RgCfg<X3>::A_BYTES;
+  using CF = RgCfg<X3, ABF>;
+  constexpr int RG_NS = CF::NS, RG_SLOT = CF::SLOT, RG_OPS = CF::OPS;
+  constexpr int RG_BM = CF::BM, RG_A_BYTES = CF::A_BYTES;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int M = g.M_dev ? *g.M_dev : g.M;
   const int N = g.N;
@@ -266,13 +272,13 @@ __global__ __launch_bounds__(RgCfg<X3>::WAVES * 64) void k_rgemm(RGemm g) {
   if (m0 >= M) return;
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const unsigned base = (unsigned)(uintptr_t)lds;
-  constexpr int KC = RgCfg<X3>::KC;
+  constexpr int KC = CF::KC;
   const int nc0 = (g.seg[0].K + KC - 1) / KC;
   const int nch = nc0 + (g.nseg > 1 ? (g.seg[1].K + KC - 1) / KC : 0);
   auto issue = [&](int c) {
     const int seg = c < nc0 ? 0 : 1;
     const int kk = (c - (seg ? nc0 : 0)) * KC;
-    rg_issue<X3>(g, seg, kk, m0, M, N, base + (c % RG_NS) * RG_SLOT, w, lane);
+    rg_issue<X3, ABF>(g, seg, kk, m0, M, N, base + (c % RG_NS) * RG_SLOT, w, lane);
   };
   const int pro = nch < RG_NS ? nch : RG_NS;
   for (int c = 0; c < pro; ++c) issue(c);
@@ -306,8 +312,17 @@ __global__ __launch_bounds__(RgCfg<X3>::WAVES * 64) void k_rgemm(RGemm g) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int r = wr + 16 * i + (lane & 15);
+          if constexpr (ABF) {
+            // bf16 row r, k = 8 kc .. 8 kc + 7: one 16-B chunk kc (swizzled by swa(r))
+            af[i] = *(const bf16x8_t*)(sA + r * (KC * 2) + ((kc ^ CF::swa(r)) * 16));
+            if (kk + KC > K) {  // the last, partial chunk of a segment: columns past K read as zero
+#pragma unroll
+              for (int e = 0; e < 8; ++e) af[i][e] = (kk + 8 * kc + e < K) ? af[i][e] : (__bf16)0.0f;
+            }
+            continue;
+          }
           // fp32 row r, k = 8 kc .. 8 kc + 7: 16-B chunks 2 kc, 2 kc + 1 (swizzled by swa(r))
-          const int sa = RgCfg<X3>::swa(r);
+          const int sa = CF::swa(r);
           const f32x4 x0 = *(const f32x4*)(sA + r * (KC * 4) + (((2 * kc) ^ sa) * 16));
           const f32x4 x1 = *(const f32x4*)(sA + r * (KC * 4) + (((2 * kc + 1) ^ sa) * 16));
           float x[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
@@ -324,9 +339,9 @@ __global__ __launch_bounds__(RgCfg<X3>::WAVES * 64) void k_rgemm(RGemm g) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int r = wc + 16 * j + (lane & 15);
-          const int sb = RgCfg<X3>::swb(r);
+          const int sb = CF::swb(r);
           bfr[j] = *(const bf16x8_t*)(sB + r * (KC * 2) + ((kc ^ sb) * 16));
-          if constexpr (X3) bl[j] = *(const bf16x8_t*)(sB + RgCfg<X3>::B_BYTES + r * (KC * 2) + ((kc ^ sb) * 16));
+          if constexpr (X3) bl[j] = *(const bf16x8_t*)(sB + CF::B_BYTES + r * (KC * 2) + ((kc ^ sb) * 16));
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -350,6 +365,9 @@ __global__ __launch_bounds__(RgCfg<X3>::WAVES * 64) void k_rgemm(RGemm g) {
   // weights are the MFMA A operand, so lane l holds C[16 i + (l & 15)][64 w + 16 j + 4 (l >> 4) + r],
   // r = 0..3: four consecutive columns of one row, stored as one 16-B store (vec_out). Every
   // operand load of the epilogue is issued before the first use.
+  const unsigned short* mask16 = (const unsigned short*)g.mask;
+  unsigned short* C16 = (unsigned short*)g.C;
+  auto bf2f = [](unsigned short b) { return __uint_as_float((uint32_t)b << 16); };
   if (g.vec_out) {
     f32x4 cv[4][4], mk[4][4], bj[4];
 #pragma unroll
@@ -364,7 +382,14 @@ __global__ __launch_bounds__(RgCfg<X3>::WAVES * 64) void k_rgemm(RGemm g) {
         const long m = min(m0 + wr + 16 * i + (lane & 15), M - 1);
         const int n = min(wc + 16 * j + 4 * (lane >> 4), N - 4);
         if (g.accumulate) cv[i][j] = *(const f32x4*)(g.C + m * g.ldc + n);
-        if (g.mask) mk[i][j] = *(const f32x4*)(g.mask + m * g.ldm + n);
+        if (g.mask) {
+          if constexpr (MBF) {
+            const uint2 q = *(const uint2*)(mask16 + m * g.ldm + n);
+            mk[i][j] = f32x4{bf2f(q.x & 0xffffu), bf2f(q.x >> 16), bf2f(q.y & 0xffffu), bf2f(q.y >> 16)};
+          } else {
+            mk[i][j] = *(const f32x4*)(g.mask + m * g.ldm + n);
+          }
+        }
       }
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -383,7 +408,14 @@ __global__ __launch_bounds__(RgCfg<X3>::WAVES * 64) void k_rgemm(RGemm g) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = mk[i][j][e] > 0.f ? v[e] : 0.f;
         }
-        if (m < M && n < N) *(f32x4*)(g.C + (long)m * g.ldc + n) = v;
+        if (m < M && n < N) {
+          if (g.cbf)
+            *(uint2*)(C16 + (long)m * g.ldc + n) =
+                make_uint2((uint32_t)f2bf_rne(v[0]) | ((uint32_t)f2bf_rne(v[1]) << 16),
+                           (uint32_t)f2bf_rne(v[2]) | ((uint32_t)f2bf_rne(v[3]) << 16));
+          else
+            *(f32x4*)(g.C + (long)m * g.ldc + n) = v;
+        }
       }
     return;
   }
@@ -401,32 +433,50 @@ __global__ __launch_bounds__(RgCfg<X3>::WAVES * 64) void k_rgemm(RGemm g) {
         if (g.bias) v += g.bias[n];
         if (g.accumulate) v += *cp;
         if (g.relu) v = fmaxf(v, 0.f);
-        if (g.mask && !(g.mask[(long)m * g.ldm + n] > 0.f)) v = 0.f;
-        *cp = v;
+        if (g.mask) {
+          const float mv = MBF ? bf2f(mask16[(long)m * g.ldm + n]) : g.mask[(long)m * g.ldm + n];
+          if (!(mv > 0.f)) v = 0.f;
+        }
+        if (g.cbf) C16[(long)m * g.ldc + n] = f2bf_rne(v);
+        else *cp = v;
       }
 }
 
-template <bool X3>
-size_t rgemm_lds_bytes() { return (size_t)RgCfg<X3>::NS * RgCfg<X3>::SLOT; }
+template <bool X3, bool ABF>
+size_t rgemm_lds_bytes() { return (size_t)RgCfg<X3, ABF>::NS * RgCfg<X3, ABF>::SLOT; }
 
 void launch_rgemm(const RGemm& g0, int M_host, hipStream_t s) {
   RGemm g = g0;
-  g.vec_out = (g.N % 4 == 0) && (g.ldc % 4 == 0) && ((uintptr_t)g.C % 16 == 0) &&
-              (!g.mask || ((g.ldm % 4 == 0) && ((uintptr_t)g.mask % 16 == 0))) && ((uintptr_t)g.bias % 16 == 0);
+  const size_t ce = g.cbf ? 2 : 4, me = g.mbf ? 2 : 4;  // C / mask element bytes
+  g.vec_out = (g.N % 4 == 0) && (g.ldc % 4 == 0) && ((uintptr_t)g.C % (4 * ce) == 0) &&
+              (!g.mask || ((g.ldm % 4 == 0) && ((uintptr_t)g.mask % (4 * me) == 0))) && ((uintptr_t)g.bias % 16 == 0);
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)k_rgemm<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)rgemm_lds_bytes<false>());
-    (void)hipFuncSetAttribute((const void*)k_rgemm<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)rgemm_lds_bytes<true>());
+    (void)hipFuncSetAttribute((const void*)k_rgemm<false, false, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)rgemm_lds_bytes<false, false>());
+    (void)hipFuncSetAttribute((const void*)k_rgemm<false, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)rgemm_lds_bytes<false, false>());
+    (void)hipFuncSetAttribute((const void*)k_rgemm<false, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)rgemm_lds_bytes<false, true>());
+    (void)hipFuncSetAttribute((const void*)k_rgemm<false, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)rgemm_lds_bytes<false, true>());
+    (void)hipFuncSetAttribute((const void*)k_rgemm<true, false, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)rgemm_lds_bytes<true, false>());
     attr = true;
   }
+  constexpr int BM = RgCfg<false>::BM;
+  const dim3 grid((M_host + BM - 1) / BM), block(RgCfg<false>::WAVES * 64);
+  const bool mbf = g.mbf && g.mask;
   if (g.x3)
-    hipLaunchKernelGGL(k_rgemm<true>, dim3((M_host + RgCfg<true>::BM - 1) / RgCfg<true>::BM),
-                       dim3(RgCfg<true>::WAVES * 64), rgemm_lds_bytes<true>(), s, g);
+    hipLaunchKernelGGL((k_rgemm<true, false, false>), grid, block, (rgemm_lds_bytes<true, false>()), s, g);
+  else if (g.abf && mbf)
+    hipLaunchKernelGGL((k_rgemm<false, true, true>), grid, block, (rgemm_lds_bytes<false, true>()), s, g);
+  else if (g.abf)
+    hipLaunchKernelGGL((k_rgemm<false, true, false>), grid, block, (rgemm_lds_bytes<false, true>()), s, g);
+  else if (mbf)
+    hipLaunchKernelGGL((k_rgemm<false, false, true>), grid, block, (rgemm_lds_bytes<false, false>()), s, g);
   else
-    hipLaunchKernelGGL(k_rgemm<false>, dim3((M_host + RgCfg<false>::BM - 1) / RgCfg<false>::BM),
-                       dim3(RgCfg<false>::WAVES * 64), rgemm_lds_bytes<false>(), s, g);
+    hipLaunchKernelGGL((k_rgemm<false, false, false>), grid, block, (rgemm_lds_bytes<false, false>()), s, g);
 }
 
 }  // namespace anr
@@ -463,14 +513,23 @@ __device__ __forceinline__ bf16x8_t wg_frag(const unsigned short* S, int cb, int
   return f;
 }
 
-// thread's share of one 32 x 128 fp32 operand step: 4 float4 (sample 8h + (tid >> 5), columns 4 (tid & 31))
+// thread's share of one 32 x 128 operand step: 4 float4 (sample 8h + (tid >> 5), columns 4 (tid & 31));
+// bf: the rows hold bf16 (8-B loads, widened exactly; wg_store's rounding then returns the same bits)
+template <bool BF>
 __device__ __forceinline__ void wg_load(const float* P, long ld, int ncol, int c0, int s, int s1, int tid, f32x4 (&v)[4]) {
 #pragma unroll
   for (int h = 0; h < 4; ++h) {
     const int ss = s + 8 * h + (tid >> 5);
     const int c = c0 + 4 * (tid & 31);
     const bool ok = ss < s1 && c < ncol;
-    const f32x4 x = *(const f32x4*)(P + (long)(ok ? ss : s) * ld + (ok ? c : 0));
+    f32x4 x;
+    if constexpr (BF) {
+      const uint2 q = *(const uint2*)((const unsigned short*)P + (long)(ok ? ss : s) * ld + (ok ? c : 0));
+      x = f32x4{__uint_as_float(q.x << 16), __uint_as_float(q.x & 0xffff0000u), __uint_as_float(q.y << 16),
+                __uint_as_float(q.y & 0xffff0000u)};
+    } else {
+      x = *(const f32x4*)(P + (long)(ok ? ss : s) * ld + (ok ? c : 0));
+    }
     // columns past ncol (inside the 16-B group) and samples past the range read as zero
 #pragma unroll
     for (int e = 0; e < 4; ++e) v[h][e] = (ok && c + e < ncol) ? x[e] : 0.0f;
@@ -495,7 +554,8 @@ __device__ __forceinline__ void wg_store(unsigned short* S, unsigned short* SL, 
   }
 }
 
-template <bool X3>
+// YBF / XBF: dY / X rows hold bf16 (template parameters: the prefetch must stay branch-free)
+template <bool X3, bool YBF, bool XBF>
 __global__ __launch_bounds__(256) void k_wgrad(WGrad g) {
   constexpr int NI = X3 ? 2 : 1;   // images per operand: hi (and lo)
   constexpr int NH = X3 ? 1 : 2;   // 32-sample halves per step (bf16: 64 samples, two MFMA k-steps)
@@ -528,8 +588,8 @@ __global__ __launch_bounds__(256) void k_wgrad(WGrad g) {
   auto load = [&](int s) {
 #pragma unroll
     for (int h = 0; h < NH; ++h) {
-      wg_load(g.dY, g.ldY, g.nout, i0, s + h * WG_S, s1, tid, vy[h]);
-      wg_load(g.X, g.ldX, g.K, j0, s + h * WG_S, s1, tid, vx[h]);
+      wg_load<YBF>(g.dY, g.ldY, g.nout, i0, s + h * WG_S, s1, tid, vy[h]);
+      wg_load<XBF>(g.X, g.ldX, g.K, j0, s + h * WG_S, s1, tid, vx[h]);
     }
   };
   constexpr int STEP = NH * WG_S;
@@ -647,8 +707,12 @@ int launch_wgrad(WGrad g, int n_host, hipStream_t s) {
   g.nz = nz;
   g.n = n_host;
   g.rs_slab = (g.bsum || g.bsum2) ? g.slab + (size_t)WG_MAX_Z * 4 * WG_TILE_FLOATS : nullptr;
-  if (g.x3) hipLaunchKernelGGL(k_wgrad<true>, dim3(ti, tj, g.nz), dim3(256), 0, s, g);
-  else hipLaunchKernelGGL(k_wgrad<false>, dim3(ti, tj, g.nz), dim3(256), 0, s, g);
+  const dim3 grid(ti, tj, g.nz);
+  if (g.x3) hipLaunchKernelGGL((k_wgrad<true, false, false>), grid, dim3(256), 0, s, g);
+  else if (g.ybf && g.xbf) hipLaunchKernelGGL((k_wgrad<false, true, true>), grid, dim3(256), 0, s, g);
+  else if (g.ybf) hipLaunchKernelGGL((k_wgrad<false, true, false>), grid, dim3(256), 0, s, g);
+  else if (g.xbf) hipLaunchKernelGGL((k_wgrad<false, false, true>), grid, dim3(256), 0, s, g);
+  else hipLaunchKernelGGL((k_wgrad<false, false, false>), grid, dim3(256), 0, s, g);
   const int nred = g.tiles * 4 * 16 * 64 * ((g.nz + WG_ZG - 1) / WG_ZG);
   const int nthr = nred > 256 ? nred : 256;
   hipLaunchKernelGGL(k_wgrad_reduce, dim3((nthr + 255) / 256), dim3(256), 0, s, g);

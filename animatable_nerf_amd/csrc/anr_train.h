@@ -65,7 +65,7 @@ struct GemmArgs {
 void launch_gemm(GemmArgs g, dim3 grid, hipStream_t s);
 
 // bf16 row GEMM with a weight-image B operand (anr_tgemm.hip): C[M][N] = epi(sum_s A_s[M][K_s] B_s^T),
-// A_s fp32 rows (stride lda, 16-B aligned, lda >= K_s rounded up to 64), B_s bf16 image rows
+// A_s fp32 (or, abf, bf16) rows (stride lda elements, 16-B aligned, lda >= K_s rounded up to 64), B_s bf16 image rows
 // (k-contiguous, stride ldb, chunk-aligned column offset bcol, `rows` valid rows), N <= 256
 struct RGemmSeg {
   const float* A;
@@ -92,6 +92,10 @@ struct RGemm {
   int accumulate;
   int vec_out;  // set by launch_rgemm: C (and mask) rows 16-B addressable, N % 4 == 0
   int x3;       // split-bf16 products (fp32-level): activations hi/lo, weights hi/lo images
+  // bf16 storage (training precision 'bf16': every consumer rounds these to bf16 anyway): A rows,
+  // C rows (RNE from the fp32 result) and the mask rows hold bf16 (C / mask reinterpreted as
+  // unsigned short*). Not with x3; C bf16 excludes accumulate.
+  int abf, cbf, mbf;
 };
 void launch_rgemm(const RGemm& g, int M_host, hipStream_t s);
 // bf16 weight images of the training GEMM weights: forward (rows = outputs, k = used input columns,
@@ -130,6 +134,7 @@ struct WGrad {
   float* rs_slab;
   int spb, nz, tiles, tj;
   int x3;  // split-bf16 products (fp32-level)
+  int ybf, xbf;  // dY / X rows hold bf16 (reinterpreted as unsigned short*), not with x3
 };
 size_t wgrad_slab_floats();
 int launch_wgrad(WGrad g, int n_host, hipStream_t s);
@@ -176,6 +181,9 @@ struct TrainBufs {
   float* dIt;    // [N][32]
   float* dGt;    // [N][64]
   float* dGt2;   // [N][64] second contribution (T-pose BW chain), summed by k_tr_tpose_bwd; NULL: none
+  unsigned short* dAlpha16;  // [N][64] bf16 d alpha in column 0 (written when hb)
+  int hb;        // bf16 storage (training precision bf16): Gt, Gv and d alpha (dAlpha16) are written as bf16
+  int ldl;       // row stride of dLp / dLt (0: 32); the training executor uses 64, the row GEMM's K chunk
   const int* out_row;
   const int* m_rows;
   const float* d_rgb_map;  // (R,3) upstream or NULL

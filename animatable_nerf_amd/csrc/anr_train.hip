@@ -14,6 +14,13 @@
 
 namespace anr {
 
+// fp32 -> bf16, round to nearest even (the rounding every bf16 consumer applies)
+__device__ __forceinline__ unsigned short f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (unsigned short)(u >> 16);
+}
+
 // ------------------------------------------------------------------------------------------
 // forward point kernels
 // ------------------------------------------------------------------------------------------
@@ -43,7 +50,9 @@ __global__ __launch_bounds__(256) void k_tr_point_prep(TrainBufs b) {
     TriCell cell;
     tri_cell(pose, lo, hi, b.pX, b.pY, b.pZ, cell);
     b.Ip[(long)i * 32 + lane] = lane < 24 ? tri_channel(b.pbw, 25, lane, cell) : 0.f;
-    b.Gv[(long)i * 32 + lane] = lane < 27 ? embed_feature(dir, lane, 4) : 0.f;
+    const float gv = lane < 27 ? embed_feature(dir, lane, 4) : 0.f;
+    if (b.hb) ((unsigned short*)b.Gv)[(long)i * 64 + lane] = f2bf(gv);  // rows of 64 (the row GEMM's K chunk)
+    else b.Gv[(long)i * 32 + lane] = gv;
   }
   if (lane == 0) {
     float* p = b.pt + (long)i * 8;
@@ -119,7 +128,9 @@ __global__ __launch_bounds__(256) void k_tr_softmax_lbs(TrainBufs b) {
     for (int r = 0; r < 3; ++r) inside = inside && tp[r] > b.tbounds[r] && tp[r] < b.tbounds[3 + r];
     pt[4] = tp[0]; pt[5] = tp[1]; pt[6] = tp[2]; pt[7] = inside ? 1.f : 0.f;
   }
-  b.Gt[(long)i * 64 + lane] = lane < 63 ? embed_feature(tp, lane, 10) : 0.f;
+  const float gt = lane < 63 ? embed_feature(tp, lane, 10) : 0.f;
+  if (b.hb) ((unsigned short*)b.Gt)[(long)i * 64 + lane] = f2bf(gt);
+  else b.Gt[(long)i * 64 + lane] = gt;
   if (lane < 32) {
     float lo[3], hi[3];
     for (int r = 0; r < 3; ++r) { lo[r] = b.tbounds[r]; hi[r] = b.tbounds[3 + r]; }
@@ -326,6 +337,7 @@ __global__ __launch_bounds__(256) void k_tr_raw_bwd(TrainBufs b) {
   const float sig = b.sigma[i], dist = pt[3];
   const float ds = sig > 0.f ? d.w * expf(-sig * dist) * dist : 0.f;
   b.dAlpha[i] = pt[7] > 0.f ? ds : 0.f;
+  if (b.hb) b.dAlpha16[(long)i * 64] = f2bf(pt[7] > 0.f ? ds : 0.f);
 }
 
 // upstream pbw / tbw row gradients scattered to the compact samples (alpha_ind rows); half a wave per
@@ -352,7 +364,7 @@ __global__ __launch_bounds__(256) void k_tr_softmax_bwd_t(TrainBufs b) {
   const float dB = hl < 24 ? b.dBt[(long)i * 24 + hl] : 0.f;
   const float dot = half_sum(dB * B);
   const float dl = hl < 24 ? B * (dB - dot) : 0.f;
-  b.dLt[(long)i * 32 + hl] = dl;
+  b.dLt[(long)i * (b.ldl ? b.ldl : 32) + hl] = dl;
   b.dIt[(long)i * 32 + hl] = hl < 24 ? dl / (b.It[(long)i * 32 + hl] + 1e-9f) : 0.f;
 }
 
@@ -365,7 +377,7 @@ __global__ __launch_bounds__(256) void k_tr_softmax_bwd_p(TrainBufs b) {
   const float B = hl < 24 ? b.Bp[(long)i * 24 + hl] : 0.f;
   const float dB = hl < 24 ? b.dBp[(long)i * 24 + hl] : 0.f;
   const float dot = half_sum(dB * B);
-  b.dLp[(long)i * 32 + hl] = hl < 24 ? B * (dB - dot) : 0.f;
+  b.dLp[(long)i * (b.ldl ? b.ldl : 32) + hl] = hl < 24 ? B * (dB - dot) : 0.f;
 }
 
 // d x_T from gamma(x_T) and from the init_tbw lookup (grid_sampler_3d backward w.r.t. the grid),

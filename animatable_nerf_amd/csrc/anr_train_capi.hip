@@ -30,7 +30,7 @@ constexpr int kWStreams = 2;
 struct TLayout {
   Layout L;
   size_t pt, Gp, Ip, Gv, Lp, lbs, Gt, It, Lt, Hp, Ht, Hn, Feat, Alpha, Lat, View, Rgbl;
-  size_t draw, dRgb, dAlpha, dBp, dBt, dLp, dLt, dIt, dGt, dGt2, dHn, dHt, dHp, dFeat, dLat, dView;
+  size_t draw, dRgb, dAlpha, dA16, dBp, dBt, dLp, dLt, dIt, dGt, dGt2, dHn, dHt, dHp, dFeat, dLat, dView;
   size_t ysum, acc3, d_rgb, d_pbw, d_tbw, wimg, wslab, total;
 };
 
@@ -48,8 +48,10 @@ TLayout tlayout(int n_rays, int chunk, long np, long nt) {
   T.lbs = take(N * 16); T.Gt = take(N * 64); T.It = take(N * 32); T.Lt = take(N * 32);
   T.Hp = take(N * 256 * 8); T.Ht = take(N * 256 * 8); T.Hn = take(N * 256 * 8);
   T.Feat = take(N * 256); T.Alpha = take(N); T.Lat = take(N * 256); T.View = take(N * 128); T.Rgbl = take(N * 4);
-  T.draw = take(N * 4); T.dRgb = take(N * 4); T.dAlpha = take(N); T.dBp = take(N * 24); T.dBt = take(N * 24);
-  T.dLp = take(N * 32); T.dLt = take(N * 32); T.dIt = take(N * 32); T.dGt = take(N * 64); T.dGt2 = take(N * 64);
+  T.draw = take(N * 4); T.dRgb = take(N * 4); T.dAlpha = take(N); T.dA16 = take(N * 32); T.dBp = take(N * 24);
+  T.dBt = take(N * 24);
+  T.dLp = take(N * 64); T.dLt = take(N * 64); T.dIt = take(N * 32);  // logit gradients in rows of 64
+  T.dGt = take(N * 64); T.dGt2 = take(N * 64);
   // every layer's output gradient has its own slot (the weight-gradient products read them on the
   // side stream while the input-gradient chain moves on)
   T.dHn = take(N * 256 * 8); T.dHt = take(N * 256 * 8); T.dHp = take(N * 256 * 8);
@@ -125,6 +127,11 @@ int order(SideStreams* ss, hipStream_t to, hipStream_t from) {
   return ANR_OK;
 }
 
+// storage flags of a product's operands (training precision 'bf16': hidden activations, their
+// gradients and the gamma inputs of the T-pose / canonical MLPs are kept as bf16 — every consumer
+// rounds them to bf16 for the MFMA anyway, so the products are unchanged and their bytes halve)
+enum : unsigned { BF_A = 1u, BF_C = 2u, BF_M = 4u, BF_X = 8u };  // A (or dY), output, mask, wgrad X
+
 struct Exec {
   hipStream_t s;
   int n;         // kept samples (host copy; unused when n_dev is set)
@@ -134,6 +141,7 @@ struct Exec {
   const float* pt[ANR_NUM_TENSORS + ANR_NUM_NOVEL_TENSORS] = {};  // the tensors they were packed from
   float* wslab = nullptr;              // weight-gradient partial slabs (anr_tgemm.hip k_wgrad)
   int x3 = 0;  // inside the pose scope of ANR_BF16: split-bf16 (fp32-level) row GEMMs instead of fp32
+  int hb = 0;  // bf16 storage of the T-pose / canonical activations (precision bf16 / bf16_all, training executor)
   SideStreams* ss = nullptr;  // NULL: every product on s
   int wnext = 0;               // round-robin weight-gradient lane
   // the kept-sample count stays on the device (no host read, so a step can be captured in a graph):
@@ -167,8 +175,9 @@ struct Exec {
   }
 
   // the bf16 row GEMM when every operand fits it (anr_train.h RGemm); false: use the generic kernel
-  bool row_seg(RGemmSeg& q, const float* A, long lda, int K, const float* W, int c0, bool bwd) {
-    if (!A || K <= 0 || lda % 4 != 0 || ((uintptr_t)A & 15) != 0 || lda < (long)((K + 63) / 64 * 64)) return false;
+  bool row_seg(RGemmSeg& q, const float* A, long lda, int K, const float* W, int c0, bool bwd, bool abf = false) {
+    if (!A || K <= 0 || lda % (abf ? 8 : 4) != 0 || ((uintptr_t)A & 15) != 0 || lda < (long)((K + 63) / 64 * 64))
+      return false;
     WView v;
     if (!wimg_view(wimg, pt, W, c0, K, bwd, &v)) return false;
     q = RGemmSeg{A, lda, K, v.B, v.ldb, v.bcol, v.rows, v.lo_off};
@@ -198,18 +207,22 @@ struct Exec {
   }
 
   // Y[n][Nout] = act( X0[:, :K0] W[:, c0:c0+K0]^T (+ X1 W[:, c1:c1+K1]^T) + bias )
+  // bf: BF_A (X0 / X1 bf16), BF_C (Y bf16)
   int fwd(float* Y, int ldY, int Nout, const float* W, int in_ch, const float* bias, bool relu, const float* X0, int ld0,
-          int K0, int c0, const float* X1 = nullptr, int ld1 = 0, int K1 = 0, int c1 = 0) {
-    if ((bf16 || x3) && wimg && Nout <= 256) {
+          int K0, int c0, const float* X1 = nullptr, int ld1 = 0, int K1 = 0, int c1 = 0, unsigned bf = 0) {
+    const bool abf = bf & BF_A;
+    if ((bf16 || x3) && wimg && Nout <= 256 && !(x3 && bf)) {
       RGemm r{};
       r.x3 = bf16 ? 0 : 1;
       r.N = Nout;
       r.nseg = X1 ? 2 : 1;
-      if (row_seg(r.seg[0], X0, ld0, K0, W, c0, false) && (!X1 || row_seg(r.seg[1], X1, ld1, K1, W, c1, false))) {
+      if (row_seg(r.seg[0], X0, ld0, K0, W, c0, false, abf) && (!X1 || row_seg(r.seg[1], X1, ld1, K1, W, c1, false, abf))) {
         r.C = Y; r.ldc = ldY; r.bias = bias; r.relu = relu ? 1 : 0;
+        r.abf = abf; r.cbf = (bf & BF_C) != 0;
         return rgemm(r);
       }
     }
+    if (bf) return fail(ANR_E_ARG, "train: bf16-stored operand off the row-GEMM path");
     GemmArgs g{};
     g.N = Nout;
     g.nseg = X1 ? 2 : 1;
@@ -221,22 +234,26 @@ struct Exec {
 
   // dW[:, c0:c0+K] += dY^T X (split-K over samples, atomics); the column sums of dY (the bias
   // gradient) are added into bsum (and bsum2) in the same pass when given
+  // bf: BF_A (dY bf16), BF_X (X bf16)
   int wgrad(float* dW, int in_ch, int c0, int Nout, const float* dY, int ldY, const float* X, int ldX, int K,
-            float* bsum = nullptr, float* bsum2 = nullptr, int want_lane = -1) {
+            float* bsum = nullptr, float* bsum2 = nullptr, int want_lane = -1, unsigned bf = 0) {
     hipStream_t w;
     int lane;
     ANR_TRY(wstream(&w, &lane, want_lane));
     if (grid_n() <= 0) return ANR_OK;
     if ((bf16 || x3) && wslab && Nout <= 256 && K <= 256 && ldY % 4 == 0 && ldX % 4 == 0 && ((uintptr_t)dY & 15) == 0 &&
-        ((uintptr_t)X & 15) == 0) {
+        ((uintptr_t)X & 15) == 0 && !(x3 && bf)) {
       WGrad wg{};
       wg.x3 = bf16 ? 0 : 1;
+      wg.ybf = (bf & BF_A) != 0;
+      wg.xbf = (bf & BF_X) != 0;
       wg.dY = dY; wg.ldY = ldY; wg.nout = Nout; wg.X = X; wg.ldX = ldX; wg.K = K;
       wg.dW = dW + c0; wg.ldw = in_ch; wg.bsum = bsum; wg.bsum2 = bsum2; wg.slab = slab(lane);
       wg.M_dev = n_dev;
       if (launch_wgrad(wg, grid_n(), w) != 0) return check_launch("k_wgrad");
       return ANR_OK;
     }
+    if (bf) return fail(ANR_E_ARG, "train: bf16-stored operand off the weight-gradient path");
     GemmArgs g{};
     g.rowsum = bsum;
     g.rowsum2 = bsum2;
@@ -251,20 +268,25 @@ struct Exec {
   }
 
   // dX (+)= dY W[:, c0:c0+K] (masked by mask > 0)
+  // bf: BF_A (dY / dY2 bf16), BF_C (dX bf16), BF_M (mask bf16)
   int xgrad(float* dX, int ldX, int K, const float* dY, int ldY, int Nout, const float* W, int in_ch, int c0,
             const float* mask, int ldm, bool accumulate, const float* dY2 = nullptr, int ldY2 = 0, int Nout2 = 0,
-            const float* W2 = nullptr, int in_ch2 = 0) {
-    if ((bf16 || x3) && wimg && K <= 256) {
+            const float* W2 = nullptr, int in_ch2 = 0, unsigned bf = 0) {
+    const bool abf = bf & BF_A;
+    if ((bf16 || x3) && wimg && K <= 256 && !(x3 && bf) && !((bf & BF_C) && accumulate)) {
       RGemm r{};
       r.x3 = bf16 ? 0 : 1;
       r.N = K;
       r.nseg = dY2 ? 2 : 1;
-      if (row_seg(r.seg[0], dY, ldY, Nout, W, c0, true) && (!dY2 || row_seg(r.seg[1], dY2, ldY2, Nout2, W2, c0, true)) &&
-          r.seg[0].rows >= K && (!dY2 || r.seg[1].rows >= K)) {
+      if (row_seg(r.seg[0], dY, ldY, Nout, W, c0, true, abf) &&
+          (!dY2 || row_seg(r.seg[1], dY2, ldY2, Nout2, W2, c0, true, abf)) && r.seg[0].rows >= K &&
+          (!dY2 || r.seg[1].rows >= K)) {
         r.C = dX; r.ldc = ldX; r.mask = mask; r.ldm = ldm; r.accumulate = accumulate ? 1 : 0;
+        r.abf = abf; r.cbf = (bf & BF_C) != 0; r.mbf = (bf & BF_M) != 0;
         return rgemm(r);
       }
     }
+    if (bf) return fail(ANR_E_ARG, "train: bf16-stored operand off the row-GEMM path");
     GemmArgs g{};
     g.N = K;
     g.nseg = dY2 ? 2 : 1;
@@ -279,8 +301,9 @@ struct Exec {
 // point that the 2^9-frequency encoding amplifies); restores the executor's mode on scope exit
 struct PoseScope {
   Exec& e;
-  int keep;
-  explicit PoseScope(Exec& x) : e(x), keep(x.bf16) {
+  int keep, keep_hb;
+  explicit PoseScope(Exec& x) : e(x), keep(x.bf16), keep_hb(x.hb) {
+    e.hb = 0;  // the pose-space activations (and gamma(x)) stay fp32 under every policy
     if (e.pose_fp32) {
       e.bf16 = 0;
       e.x3 = 1;
@@ -288,6 +311,7 @@ struct PoseScope {
   }
   ~PoseScope() {
     e.bf16 = keep;
+    e.hb = keep_hb;
     e.x3 = 0;
   }
 };
@@ -335,8 +359,10 @@ TrainBufs bufs(const TLayout& T, char* ws, const anr_frame* f, const float* ray_
   b.Rgbl = (float*)(ws + T.Rgbl); b.Alpha = (float*)(ws + T.Alpha); b.sigma = (float*)(ws + L.sigma);
   b.raw = (float4*)(ws + L.raw);
   b.draw = (float4*)(ws + T.draw); b.dRgb = (float*)(ws + T.dRgb); b.dAlpha = (float*)(ws + T.dAlpha);
+  b.dAlpha16 = (unsigned short*)(ws + T.dA16);
   b.dBp = (float*)(ws + T.dBp); b.dBt = (float*)(ws + T.dBt); b.dLp = (float*)(ws + T.dLp);
   b.dLt = (float*)(ws + T.dLt); b.dIt = (float*)(ws + T.dIt); b.dGt = (float*)(ws + T.dGt);
+  b.ldl = 64;
   b.n_rays = R;
   return b;
 }
@@ -350,16 +376,17 @@ TrainBufs bufs(const TLayout& T, char* ws, const anr_frame* f, const float* ray_
 int bw_forward(Exec& e, const float* const* W, const float* G, float* H, float* logits, long N, const float* fold0,
                const float* fold5) {
   const long S = N * 256;
-  ANR_TRY(e.fwd(H, 256, 256, W[1], 191, fold0, true, G, 64, 63, 0));
+  const unsigned h = e.hb ? (BF_A | BF_C) : 0, a = e.hb ? BF_A : 0;  // gamma and H bf16 under e.hb
+  ANR_TRY(e.fwd(H, 256, 256, W[1], 191, fold0, true, G, 64, 63, 0, nullptr, 0, 0, 0, h));
   for (int l = 1; l < 8; ++l) {
     const float* Xp = H + (l - 1) * S;
     if (l == 5) {
-      ANR_TRY(e.fwd(H + l * S, 256, 256, W[11], 447, fold5, true, G, 64, 63, 0, Xp, 256, 256, 191));
+      ANR_TRY(e.fwd(H + l * S, 256, 256, W[11], 447, fold5, true, G, 64, 63, 0, Xp, 256, 256, 191, h));
     } else {
-      ANR_TRY(e.fwd(H + l * S, 256, 256, W[1 + 2 * l], 256, W[2 + 2 * l], true, Xp, 256, 256, 0));
+      ANR_TRY(e.fwd(H + l * S, 256, 256, W[1 + 2 * l], 256, W[2 + 2 * l], true, Xp, 256, 256, 0, nullptr, 0, 0, 0, h));
     }
   }
-  return e.fwd(logits, 32, 24, W[17], 256, W[18], false, H + 7 * S, 256, 256, 0);
+  return e.fwd(logits, 32, 24, W[17], 256, W[18], false, H + 7 * S, 256, 256, 0, nullptr, 0, 0, 0, a);
 }
 
 // BW MLP backward from d logits; accumulates weight/bias grads into g (same table order as W; NULL:
@@ -383,6 +410,7 @@ struct BwBackward {
   float* ysum;
   const int64_t* li;
   int add;
+  int ldlog = 32;  // row stride of dlog
   int l = 8;  // 8: the bw_fc head, then layers 7..0; -1: done
 
   bool done() const { return l < 0; }
@@ -390,9 +418,11 @@ struct BwBackward {
   int step() {
     OnStream on(e, st);
     const long S = N * 256;
+    const unsigned hb = e.hb ? ~0u : 0u;  // flag mask: the hidden rows, their gradients and gamma bf16
     if (l == 8) {
-      if (g) ANR_TRY(e.wgrad(g[17], 256, 0, 24, dlog, 32, H + 7 * S, 256, 256, g[18]));
-      ANR_TRY(e.xgrad(dbuf(7), 256, 256, dlog, 32, 24, W[17], 256, 0, H + 7 * S, 256, false));
+      if (g) ANR_TRY(e.wgrad(g[17], 256, 0, 24, dlog, ldlog, H + 7 * S, 256, 256, g[18], nullptr, -1, hb & BF_X));
+      ANR_TRY(e.xgrad(dbuf(7), 256, 256, dlog, ldlog, 24, W[17], 256, 0, H + 7 * S, 256, false, nullptr, 0, 0, nullptr, 0,
+                      hb & (BF_C | BF_M)));
       --l;
       return ANR_OK;
     }
@@ -407,19 +437,24 @@ struct BwBackward {
         ANR_TRY(e.wstream(&w, &lane, 0));
         if (hipMemsetAsync(ys, 0, 256 * 4, w) != hipSuccess) return fail(ANR_E_HIP, "memset");
         // bias grad and the latent-row gradient's column sum, in the weight-gradient pass
-        ANR_TRY(e.wgrad(g[wi], in_ch, 0, 256, cur, 256, G, 64, 63, g[bi], ys, 0));
+        ANR_TRY(e.wgrad(g[wi], in_ch, 0, 256, cur, 256, G, 64, 63, g[bi], ys, 0, hb & (BF_A | BF_X)));
         hipLaunchKernelGGL(k_tr_latent_grad, dim3(256 + 128), dim3(128), 0, w, (const float*)ys, W[wi], in_ch, 63, 256,
                            W[0], li, add, g[wi], g[0]);
         ANR_TRY(check_launch("k_tr_latent_grad"));
       }
-      if (dG) ANR_TRY(e.xgrad(dG, 64, 63, cur, 256, 256, W[wi], in_ch, 0, nullptr, 0, !(dG_fresh && l == 5)));
+      if (dG)
+        ANR_TRY(e.xgrad(dG, 64, 63, cur, 256, 256, W[wi], in_ch, 0, nullptr, 0, !(dG_fresh && l == 5), nullptr, 0, 0,
+                        nullptr, 0, hb & BF_A));
       if (l == 5) {
-        if (g) ANR_TRY(e.wgrad(g[wi], in_ch, 191, 256, cur, 256, H + 4 * S, 256, 256));
-        ANR_TRY(e.xgrad(dbuf(4), 256, 256, cur, 256, 256, W[wi], in_ch, 191, H + 4 * S, 256, false));
+        if (g) ANR_TRY(e.wgrad(g[wi], in_ch, 191, 256, cur, 256, H + 4 * S, 256, 256, nullptr, nullptr, -1, hb & (BF_A | BF_X)));
+        ANR_TRY(e.xgrad(dbuf(4), 256, 256, cur, 256, 256, W[wi], in_ch, 191, H + 4 * S, 256, false, nullptr, 0, 0, nullptr,
+                        0, hb & (BF_A | BF_C | BF_M)));
       }
     } else {
-      if (g) ANR_TRY(e.wgrad(g[wi], 256, 0, 256, cur, 256, H + (l - 1) * S, 256, 256, g[bi]));
-      ANR_TRY(e.xgrad(dbuf(l - 1), 256, 256, cur, 256, 256, W[wi], 256, 0, H + (l - 1) * S, 256, false));
+      if (g)
+        ANR_TRY(e.wgrad(g[wi], 256, 0, 256, cur, 256, H + (l - 1) * S, 256, 256, g[bi], nullptr, -1, hb & (BF_A | BF_X)));
+      ANR_TRY(e.xgrad(dbuf(l - 1), 256, 256, cur, 256, 256, W[wi], 256, 0, H + (l - 1) * S, 256, false, nullptr, 0, 0,
+                      nullptr, 0, hb & (BF_A | BF_C | BF_M)));
     }
     --l;
     return ANR_OK;
@@ -428,8 +463,8 @@ struct BwBackward {
 
 int bw_backward(Exec& e, const float* const* W, float* const* g, const float* G, const float* H, const float* dlog,
                 float* dY0, float* dY1, long dstride, float* dG, bool dG_fresh, long N, float* ysum, const int64_t* li,
-                int add) {
-  BwBackward b{e, e.s, W, g, G, H, dlog, dY0, dY1, dstride, dG, dG_fresh, N, ysum, li, add};
+                int add, int ldlog = 32) {
+  BwBackward b{e, e.s, W, g, G, H, dlog, dY0, dY1, dstride, dG, dG_fresh, N, ysum, li, add, ldlog};
   while (!b.done()) ANR_TRY(b.step());
   return ANR_OK;
 }
@@ -445,6 +480,7 @@ int train_forward(const anr_params* p, const anr_frame* f, const float* ray_o, c
   e.cap = (int)N;
   const int n = e.grid_n();
   TrainBufs b = bufs(T, ws, f, ray_o, ray_d, near_, far_, R, o, x);
+  b.hb = e.hb;
   const int g1 = (n + 255) / 256;
   if (n > 0) {
     hipLaunchKernelGGL(k_tr_point_prep, dim3((n + 3) / 4), dim3(256), 0, s, b);
@@ -473,21 +509,24 @@ int train_forward(const anr_params* p, const anr_frame* f, const float* ray_o, c
   // canonical NeRF (TPoseHuman.calculate_alpha_rgb)
   float* Hn = (float*)(ws + T.Hn);
   const long S = N * 256;
-  ANR_TRY(e.fwd(Hn, 256, 256, PT(1), 63, PT(2), true, b.Gt, 64, 63, 0));
+  const unsigned h = e.hb ? (BF_A | BF_C) : 0, a = e.hb ? BF_A : 0;  // gamma, H, Feat, Lat bf16 under e.hb
+  ANR_TRY(e.fwd(Hn, 256, 256, PT(1), 63, PT(2), true, b.Gt, 64, 63, 0, nullptr, 0, 0, 0, h));
   for (int l = 1; l < 8; ++l) {
     if (l == 5) {
-      ANR_TRY(e.fwd(Hn + l * S, 256, 256, PT(11), 319, PT(12), true, b.Gt, 64, 63, 0, Hn + 4 * S, 256, 256, 63));
+      ANR_TRY(e.fwd(Hn + l * S, 256, 256, PT(11), 319, PT(12), true, b.Gt, 64, 63, 0, Hn + 4 * S, 256, 256, 63, h));
     } else {
-      ANR_TRY(e.fwd(Hn + l * S, 256, 256, PT(1 + 2 * l), 256, PT(2 + 2 * l), true, Hn + (l - 1) * S, 256, 256, 0));
+      ANR_TRY(e.fwd(Hn + l * S, 256, 256, PT(1 + 2 * l), 256, PT(2 + 2 * l), true, Hn + (l - 1) * S, 256, 256, 0, nullptr,
+                    0, 0, 0, h));
     }
   }
   float* Feat = (float*)(ws + T.Feat);
   float* Lat = (float*)(ws + T.Lat);
   float* View = (float*)(ws + T.View);
-  ANR_TRY(e.fwd(b.Alpha, 1, 1, PT(17), 256, PT(18), false, Hn + 7 * S, 256, 256, 0));
-  ANR_TRY(e.fwd(Feat, 256, 256, PT(19), 256, PT(20), false, Hn + 7 * S, 256, 256, 0));
-  ANR_TRY(e.fwd(Lat, 256, 256, PT(21), 384, FOLD(4), false, Feat, 256, 256, 0));
-  ANR_TRY(e.fwd(View, 128, 128, PT(23), 283, PT(24), true, Lat, 256, 256, 0, b.Gv, 32, 27, 256));
+  ANR_TRY(e.fwd(b.Alpha, 1, 1, PT(17), 256, PT(18), false, Hn + 7 * S, 256, 256, 0, nullptr, 0, 0, 0, a));
+  ANR_TRY(e.fwd(Feat, 256, 256, PT(19), 256, PT(20), false, Hn + 7 * S, 256, 256, 0, nullptr, 0, 0, 0, h));
+  ANR_TRY(e.fwd(Lat, 256, 256, PT(21), 384, FOLD(4), false, Feat, 256, 256, 0, nullptr, 0, 0, 0, h));
+  const int gvld = e.hb ? 64 : 32;  // bf16 gamma(dir) rows of 64 (row-GEMM K chunk), same bytes
+  ANR_TRY(e.fwd(View, 128, 128, PT(23), 283, PT(24), true, Lat, 256, 256, 0, b.Gv, gvld, 27, 256, a));
   ANR_TRY(e.fwd(b.Rgbl, 4, 3, PT(25), 128, PT(26), false, View, 128, 128, 0));
   if (n > 0) {
     hipLaunchKernelGGL(k_tr_raw, dim3(g1), dim3(256), 0, s, b);
@@ -510,6 +549,7 @@ int train_backward(const anr_params* p, float* const* g, const anr_frame* f, con
   const int n = e.grid_n();
   const long S = N * 256;
   TrainBufs b = bufs(T, ws, f, ray_o, ray_d, near_, far_, R, o, x);
+  b.hb = e.hb;
   b.d_rgb_map = d_rgb; b.d_pbw = d_pbw; b.d_tbw = d_tbw;
   const int g1 = (n + 255) / 256;
   if (n <= 0) return ANR_OK;
@@ -546,48 +586,58 @@ int train_backward(const anr_params* p, float* const* g, const anr_frame* f, con
   ANR_TRY(check_launch("k_tr_raw_bwd"));
   // the T-pose BW backward (latent row 0) on s2, issued a layer at a time between the NeRF's layers
   BwBackward tb{e, s2, p->t + 27, g + 27, b.Gt, Ht, b.dLt, (float*)(ws + T.dHt), nullptr, S, b.dGt2, true, N, ysum,
-                nullptr, 0};
+                nullptr, 0, 64};
   auto tick = [&]() { return tb.done() ? ANR_OK : tb.step(); };
   ANR_TRY(tick());
   // rgb_fc, view_fc (ReLU), latent_fc (latent folded), feature_fc || alpha_fc
   ANR_TRY(e.wgrad(g[25], 128, 0, 3, b.dRgb, 4, View, 128, 128, g[26]));
   ANR_TRY(e.xgrad(dView, 128, 128, b.dRgb, 4, 3, PT(25), 128, 0, View, 128, false));
   ANR_TRY(tick());
-  ANR_TRY(e.wgrad(g[23], 283, 0, 128, dView, 128, Lat, 256, 256, g[24]));
-  ANR_TRY(e.wgrad(g[23], 283, 256, 128, dView, 128, b.Gv, 32, 27));
-  ANR_TRY(e.xgrad(dLat, 256, 256, dView, 128, 128, PT(23), 283, 0, nullptr, 0, false));
+  const unsigned hb = e.hb ? ~0u : 0u;  // flag mask: gamma, H, Feat, Lat and their gradients bf16
+  ANR_TRY(e.wgrad(g[23], 283, 0, 128, dView, 128, Lat, 256, 256, g[24], nullptr, -1, hb & BF_X));
+  ANR_TRY(e.wgrad(g[23], 283, 256, 128, dView, 128, b.Gv, e.hb ? 64 : 32, 27, nullptr, nullptr, -1, hb & BF_X));
+  ANR_TRY(e.xgrad(dLat, 256, 256, dView, 128, 128, PT(23), 283, 0, nullptr, 0, false, nullptr, 0, 0, nullptr, 0,
+                  hb & BF_C));
   {
     float* ys = ysum + 512;
     hipStream_t w;
     int lane;
     ANR_TRY(e.wstream(&w, &lane, 0));
     if (hipMemsetAsync(ys, 0, 256 * 4, w) != hipSuccess) return fail(ANR_E_HIP, "memset");
-    ANR_TRY(e.wgrad(g[21], 384, 0, 256, dLat, 256, Feat, 256, 256, g[22], ys, 0));
+    ANR_TRY(e.wgrad(g[21], 384, 0, 256, dLat, 256, Feat, 256, 256, g[22], ys, 0, hb & (BF_A | BF_X)));
     hipLaunchKernelGGL(k_tr_latent_grad, dim3(256 + 128), dim3(128), 0, w, (const float*)ys, PT(21), 384, 256, 256, PT(0),
                        f->latent_index, 0, g[21], g[0]);
     ANR_TRY(check_launch("k_tr_latent_grad(nf_latent)"));
   }
-  ANR_TRY(e.xgrad(dFeat, 256, 256, dLat, 256, 256, PT(21), 384, 0, nullptr, 0, false));
+  ANR_TRY(e.xgrad(dFeat, 256, 256, dLat, 256, 256, PT(21), 384, 0, nullptr, 0, false, nullptr, 0, 0, nullptr, 0,
+                  hb & (BF_A | BF_C)));
   ANR_TRY(tick());
-  ANR_TRY(e.wgrad(g[19], 256, 0, 256, dFeat, 256, Hn + 7 * S, 256, 256, g[20]));
-  ANR_TRY(e.wgrad(g[17], 256, 0, 1, b.dAlpha, 1, Hn + 7 * S, 256, 256, g[18]));
-  ANR_TRY(e.xgrad(dHn + 7 * S, 256, 256, dFeat, 256, 256, PT(19), 256, 0, Hn + 7 * S, 256, false, b.dAlpha, 1, 1,
-                  PT(17), 256));
+  ANR_TRY(e.wgrad(g[19], 256, 0, 256, dFeat, 256, Hn + 7 * S, 256, 256, g[20], nullptr, -1, hb & (BF_A | BF_X)));
+  // d alpha: fp32 (ld 1), or under e.hb bf16 rows of 64 (k_tr_raw_bwd) so both products stay on the fast paths
+  const float* dAl = e.hb ? (const float*)b.dAlpha16 : b.dAlpha;
+  const int ldAl = e.hb ? 64 : 1;
+  ANR_TRY(e.wgrad(g[17], 256, 0, 1, dAl, ldAl, Hn + 7 * S, 256, 256, g[18], nullptr, -1, hb & (BF_A | BF_X)));
+  ANR_TRY(e.xgrad(dHn + 7 * S, 256, 256, dFeat, 256, 256, PT(19), 256, 0, Hn + 7 * S, 256, false, dAl, ldAl, 1,
+                  PT(17), 256, hb & (BF_A | BF_C | BF_M)));
   // NeRF pts_linears 7..0 (skip at 5: [gamma(x_T), net]); layer l's output gradient at dHn + l S
   for (int l = 7; l >= 0; --l) {
     const int wi = 1 + 2 * l, bi = wi + 1;
     const float* cur = dHn + l * S;
+    const unsigned ax = hb & (BF_A | BF_X), acm = hb & (BF_A | BF_C | BF_M);
     if (l == 0) {
-      ANR_TRY(e.wgrad(g[wi], 63, 0, 256, cur, 256, b.Gt, 64, 63, g[bi]));
-      ANR_TRY(e.xgrad(b.dGt, 64, 63, cur, 256, 256, PT(wi), 63, 0, nullptr, 0, true));
+      ANR_TRY(e.wgrad(g[wi], 63, 0, 256, cur, 256, b.Gt, 64, 63, g[bi], nullptr, -1, ax));
+      ANR_TRY(e.xgrad(b.dGt, 64, 63, cur, 256, 256, PT(wi), 63, 0, nullptr, 0, true, nullptr, 0, 0, nullptr, 0, hb & BF_A));
     } else if (l == 5) {
-      ANR_TRY(e.wgrad(g[wi], 319, 0, 256, cur, 256, b.Gt, 64, 63, g[bi]));
-      ANR_TRY(e.wgrad(g[wi], 319, 63, 256, cur, 256, Hn + 4 * S, 256, 256));
-      ANR_TRY(e.xgrad(b.dGt, 64, 63, cur, 256, 256, PT(wi), 319, 0, nullptr, 0, false));  // first contribution
-      ANR_TRY(e.xgrad(dHn + 4 * S, 256, 256, cur, 256, 256, PT(wi), 319, 63, Hn + 4 * S, 256, false));
+      ANR_TRY(e.wgrad(g[wi], 319, 0, 256, cur, 256, b.Gt, 64, 63, g[bi], nullptr, -1, ax));
+      ANR_TRY(e.wgrad(g[wi], 319, 63, 256, cur, 256, Hn + 4 * S, 256, 256, nullptr, nullptr, -1, ax));
+      ANR_TRY(e.xgrad(b.dGt, 64, 63, cur, 256, 256, PT(wi), 319, 0, nullptr, 0, false, nullptr, 0, 0, nullptr, 0,
+                      hb & BF_A));  // first contribution
+      ANR_TRY(e.xgrad(dHn + 4 * S, 256, 256, cur, 256, 256, PT(wi), 319, 63, Hn + 4 * S, 256, false, nullptr, 0, 0, nullptr,
+                      0, acm));
     } else {
-      ANR_TRY(e.wgrad(g[wi], 256, 0, 256, cur, 256, Hn + (l - 1) * S, 256, 256, g[bi]));
-      ANR_TRY(e.xgrad(dHn + (l - 1) * S, 256, 256, cur, 256, 256, PT(wi), 256, 0, Hn + (l - 1) * S, 256, false));
+      ANR_TRY(e.wgrad(g[wi], 256, 0, 256, cur, 256, Hn + (l - 1) * S, 256, 256, g[bi], nullptr, -1, ax));
+      ANR_TRY(e.xgrad(dHn + (l - 1) * S, 256, 256, cur, 256, 256, PT(wi), 256, 0, Hn + (l - 1) * S, 256, false, nullptr, 0,
+                      0, nullptr, 0, acm));
     }
     ANR_TRY(tick());
   }
@@ -758,6 +808,7 @@ int anr_train_fwd(const anr_params* p, const anr_frame* f, const float* ray_o, c
   char* ws = (char*)workspace;
   Exec e{s, 0, (o->precision == ANR_BF16 || o->precision == ANR_BF16_ALL) ? 1 : 0, o->precision == ANR_BF16 ? 1 : 0};
   e.ss = side_streams();
+  e.hb = e.bf16;
   ANR_TRY(pack_images(e, p, ws + T.wimg, s, (float*)(ws + T.wslab)));
   ANR_TRY(train_forward(p, f, ray_o, ray_d, near_, far_, n_rays, o, out, ws, T, s, e));
   if (out->raw &&
@@ -781,6 +832,7 @@ int anr_train_bwd(const anr_params* p, float* const* grads, const anr_frame* f, 
   char* ws = (char*)workspace;
   Exec e{s, 0, (o->precision == ANR_BF16 || o->precision == ANR_BF16_ALL) ? 1 : 0, o->precision == ANR_BF16 ? 1 : 0};
   e.ss = side_streams();
+  e.hb = e.bf16;
   ANR_TRY(pack_images(e, p, ws + T.wimg, s, (float*)(ws + T.wslab)));
   ANR_TRY(train_backward(p, grads, f, ray_o, ray_d, near_, far_, n_rays, o, d_rgb_map, d_pbw, d_tbw, ws, T, s, e));
   // pose BW MLP backward: d logits were produced by k_tr_softmax_bwd_p
@@ -788,7 +840,7 @@ int anr_train_bwd(const anr_params* p, float* const* grads, const anr_frame* f, 
   float* ysum = (float*)(ws + T.ysum);
   PoseScope ps(e);
   ANR_TRY(bw_backward(e, p->t + 27, grads + 27, (const float*)(ws + T.Gp), (const float*)(ws + T.Hp), (const float*)(ws + T.dLp),
-                      (float*)(ws + T.dHp), nullptr, N * 256, nullptr, false, N, ysum + 1024, f->latent_index, 1));
+                      (float*)(ws + T.dHp), nullptr, N * 256, nullptr, false, N, ysum + 1024, f->latent_index, 1, 64));
   return e.join_w();
 }
 
@@ -811,6 +863,7 @@ int train_step_body(const anr_params* p, float* const* grads, const anr_frame* f
                     hipEvent_t nerf_done, char* ws, const TLayout& T, hipStream_t s, SideStreams* ss) {
   Exec e{s, 0, (o->precision == ANR_BF16 || o->precision == ANR_BF16_ALL) ? 1 : 0, o->precision == ANR_BF16 ? 1 : 0};
   e.ss = ss;
+  e.hb = e.bf16;
   ANR_TRY(pack_images(e, p, ws + T.wimg, s, (float*)(ws + T.wslab)));
   ANR_TRY(train_forward(p, f, ray_o, ray_d, near_, far_, n_rays, o, out, ws, T, s, e));
   // fused losses (tpose_trainer.py:50-63) and their upstream gradients
@@ -835,7 +888,7 @@ int train_step_body(const anr_params* p, float* const* grads, const anr_frame* f
   float* ysum = (float*)(ws + T.ysum);
   PoseScope ps(e);
   ANR_TRY(bw_backward(e, p->t + 27, grads + 27, (const float*)(ws + T.Gp), (const float*)(ws + T.Hp), (const float*)(ws + T.dLp),
-                      (float*)(ws + T.dHp), nullptr, N * 256, nullptr, false, N, ysum + 1024, f->latent_index, 1));
+                      (float*)(ws + T.dHp), nullptr, N * 256, nullptr, false, N, ysum + 1024, f->latent_index, 1, 64));
   return e.join_w();
 }
 
@@ -1035,6 +1088,7 @@ int anr_network_train_fwd(const anr_params* p, const anr_frame* f, const anr_sam
   char* ws = (char*)workspace;
   Exec e{s, 0, (o->precision == ANR_BF16 || o->precision == ANR_BF16_ALL) ? 1 : 0, o->precision == ANR_BF16 ? 1 : 0};
   e.ss = side_streams();
+  e.hb = e.bf16;
   ANR_TRY(pack_images(e, p, ws + T.wimg, s, (float*)(ws + T.wslab)));
   ANR_TRY(train_forward(p, f, nullptr, nullptr, nullptr, nullptr, G, &oo, nullptr, ws, T, s, e, x));
   if (hipMemcpyAsync(raw, ws + T.L.raw, (size_t)x->n_pts * 16, hipMemcpyDeviceToDevice, s) != hipSuccess)
@@ -1061,6 +1115,7 @@ int anr_network_train_bwd(const anr_params* p, float* const* grads, const anr_fr
   char* ws = (char*)workspace;
   Exec e{s, 0, (o->precision == ANR_BF16 || o->precision == ANR_BF16_ALL) ? 1 : 0, o->precision == ANR_BF16 ? 1 : 0};
   e.ss = side_streams();
+  e.hb = e.bf16;
   ANR_TRY(pack_images(e, p, ws + T.wimg, s, (float*)(ws + T.wslab)));
   ANR_TRY(train_backward(p, grads, f, nullptr, nullptr, nullptr, nullptr, G, &oo, nullptr, d_pbw, d_tbw, ws, T, s, e, x,
                          d_raw));
@@ -1069,7 +1124,7 @@ int anr_network_train_bwd(const anr_params* p, float* const* grads, const anr_fr
   PoseScope ps(e);
   ANR_TRY(bw_backward(e, p->t + 27, grads + 27, (const float*)(ws + T.Gp), (const float*)(ws + T.Hp),
                       (const float*)(ws + T.dLp), (float*)(ws + T.dHp), nullptr, N * 256, nullptr, false, N, ysum + 1024,
-                      f->latent_index, 1));
+                      f->latent_index, 1, 64));
   return e.join_w();
 }
 
