@@ -188,10 +188,8 @@ template <bool X3, bool ABF = false> struct RgCfg {
   static constexpr int AE = ABF ? 2 : 4;                               // bytes per activation element
   static constexpr int A_BYTES = BM * KC * AE;                         // activations, BM rows x KC
   static constexpr int B_BYTES = 256 * KC * 2;                         // bf16 weight rows, 256 x KC
+  static constexpr int NS = 2;                                         // ring slots (three: no faster, profiles/r3za)
   static constexpr int SLOT = A_BYTES + B_BYTES * (X3 ? 2 : 1);        // bytes per slot
-  // ring slots: as many as fit 160 KiB (a K = 256 product is 4 or 8 chunks; two slots leave one
-  // chunk's DMA latency exposed per chunk, three hide most of it)
-  static constexpr int NS = 3 * SLOT <= 160 * 1024 ? 3 : 2;
   static constexpr int PIECES_A = A_BYTES / 1024 / WAVES;              // per wave
   static constexpr int PIECES_B = B_BYTES / 1024 / WAVES;
   static constexpr int OPS = PIECES_A + PIECES_B * (X3 ? 2 : 1);       // vmem ops per wave per chunk
