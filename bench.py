@@ -76,6 +76,8 @@ def parse():
                     help='sdf mode GEMMs: exact fp32 MFMA, or split-bf16 (outputs held to the same tolerances by '
                          'tests/test_gpu_sdf.py; 472 vs 559 ms per frame with the round-2 GEMM epilogue)')
     ap.add_argument('--no-exact', action='store_true', help='skip timing the other render precision')
+    ap.add_argument('--no-host-render', action='store_true',
+                    help='skip the render_s leg (Renderer.render with the D2H): PMC passes then see full-frame launches only')
     ap.add_argument('--torch-rays', type=int, default=16 * 2048,
                     help='rays of the frame the PyTorch-ROCm denominator renders (cold pass ~0.8 s per chunk)')
     ap.add_argument('--no-torch-baseline', action='store_true',
@@ -307,7 +309,7 @@ def main():
                      'tolerance by tests/test_gpu_render.py)' if other == 'bf16x3' else 'exact fp32 MFMA'),
             'roofline': render_roofline(other, nk2, kms2)}
         del o2
-    if not args.shard_frame:
+    if not args.shard_frame and not args.no_host_render:
         # the drop-in call as run.py:63-69 makes it: Renderer.render(batch) with the eval D2H of every
         # output (tpose_renderer.py:154-155) inside the measured time
         renderer = make_renderer(prec)

@@ -58,7 +58,7 @@ for step in "$@"; do
       k=${rest%%:*}
       a=${rest#*:}
       [ "$a" = "$rest" ] && a=""
-      B="python bench.py --steps 1 --warmup 0 --no-cpu --no-exact --no-torch-baseline $(args_of "$a")"
+      B="python bench.py --steps 1 --warmup 0 --no-cpu --no-exact --no-torch-baseline --no-host-render $(args_of "$a")"
       timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$k" -d gpurun_out/${TAG}_pmc_${k}_f -o f \
         --output-format csv -- $B > gpurun_out/${TAG}_pmc_${k}_f.log 2>&1 || { tail -20 gpurun_out/${TAG}_pmc_${k}_f.log; exit 1; }
       timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$k" -d gpurun_out/${TAG}_pmc_${k}_w -o w \
@@ -70,7 +70,7 @@ for step in "$@"; do
       k=${rest%%:*}
       a=${rest#*:}
       [ "$a" = "$rest" ] && a=""
-      B="python bench.py --steps 1 --warmup 0 --no-cpu --no-exact --no-torch-baseline $(args_of "$a")"
+      B="python bench.py --steps 1 --warmup 0 --no-cpu --no-exact --no-torch-baseline --no-host-render $(args_of "$a")"
       timeout -s KILL 180 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
         SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-include-regex "$k" \
         -d gpurun_out/${TAG}_sq_${k}1 -o p --output-format csv -- $B > gpurun_out/${TAG}_sq_${k}1.log 2>&1 || exit 1
