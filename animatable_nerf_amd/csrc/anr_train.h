@@ -139,6 +139,33 @@ struct WGrad {
 size_t wgrad_slab_floats();
 int launch_wgrad(WGrad g, int n_host, hipStream_t s);
 
+// a chain of layers run as one launch per 128-row tile (anr_tchain.hip; forward, precision bf16 with
+// bf16 storage): segment s of layer l multiplies A = the LDS activation tile (src 0, the previous
+// layer's output) or a gamma tile (src 1 = G0, 2 = G1; <= 64 bf16 columns loaded once) by a forward
+// weight image view (wimg_view); epilogue bias, ReLU; the output (N <= 256 columns) is stored to
+// `out` (bf16 or fp32, row stride ldo; NULL: not stored) and, with to_lds, becomes the next layer's A
+struct ChainLayer {
+  const unsigned short* B[2];
+  long ldb[2];
+  int bcol[2], brows[2], K[2], src[2];
+  int nseg, N, relu, to_lds, out_bf16;
+  const float* bias;
+  void* out;
+  long ldo;
+};
+#define ANR_CHAIN_MAX 14
+struct ChainArgs {
+  ChainLayer L[ANR_CHAIN_MAX];
+  int nl;
+  int M;
+  const int* M_dev;
+  const unsigned short* G0;
+  long ldg0;
+  const unsigned short* G1;
+  long ldg1;
+};
+int launch_chain(const ChainArgs& a, int M_host, hipStream_t s);
+
 // split-bf16 layer GEMM with LDS-resident weight images for large M (anr_lgemm.hip; the sdf_pdf
 // batches): lgemm_supported(g) (g.x3, no accumulate / mask / atomics, 16-B addressable operands),
 // the weight image (lgemm_image_bytes, packed once per weight set by lgemm_pack), then lgemm_run.
