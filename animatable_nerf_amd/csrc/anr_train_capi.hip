@@ -2,8 +2,9 @@
 //
 // Layer-wise: the kept samples of a 1,024-ray batch (~24k) are few enough that every layer is a
 // GEMM over the whole batch with its activation kept in HBM; the backward runs the same layers in
-// reverse (dX = dY W, dW += dY^T X) plus the per-sample kernels of anr_train.hip. One host read of
-// the kept-sample count per call sizes the GEMMs (the reference syncs ~6x per chunk).
+// reverse (dX = dY W, dW += dY^T X) plus the per-sample kernels of anr_train.hip. The kept-sample
+// count stays on the device (M_dev / K_dev in the GEMM arguments, capacity-sized grids), so no call
+// syncs with the host (the reference syncs ~6x per chunk).
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>

@@ -194,7 +194,7 @@ int anr_render_bw_rows(const void* workspace, int n_rays, float* pbw, float* tbw
  * either workspace below.
  *  anr_network_fwd: the fused network kernel (o->precision ANR_FP32 or ANR_BF16X3), no host sync.
  *  anr_network_train_fwd / _bwd: the layer-wise training executor (o->precision as for training),
- *    activations kept in the workspace until the backward; one host read of n' in each. _bwd
+ *    activations kept in the workspace until the backward; n' stays on the device (no host sync). _bwd
  *    ACCUMULATES the parameter gradients (anr_params order) from the upstream d raw (n,4) and d pbw /
  *    d tbw rows (m,24); any of the three may be NULL (zero). */
 typedef struct anr_samples {
