@@ -55,7 +55,7 @@ class RenderOpts(ctypes.Structure):
                 ('precision', ctypes.c_int)]
 
 
-FP32, BF16, BF16_ALL, BF16X3 = 0, 1, 2, 3  # anr_render_opts.precision
+FP32, BF16, BF16_ALL, BF16X3, BF16X6 = 0, 1, 2, 3, 4  # anr_render_opts.precision
 
 
 class RenderOut(ctypes.Structure):

@@ -162,14 +162,17 @@ int stage_mlp(const anr_params* p, const anr_frame* f, const float* ray_o, const
   ma.sigma = (float*)(ws + L.sigma);
   ma.pbw_rows = (float*)(ws + L.pbw_rows);
   ma.tbw_rows = (float*)(ws + L.tbw_rows);
-  const bool b16 = o->precision == ANR_BF16X3;
-  ma.pose_woff = o->novel_pose ? (b16 ? (ANR_POSE_MODE == 2 ? ANR_X6_NOVEL_WOFF : ANR_B16_NOVEL_WOFF) : ANR_NOVEL_WOFF) : 0;
+  const bool x6 = o->precision == ANR_BF16X6;
+  const bool b16 = o->precision == ANR_BF16X3 || x6;
+  ma.pose_woff = o->novel_pose ? (x6 || (b16 && ANR_POSE_MODE == 2) ? ANR_X6_NOVEL_WOFF : b16 ? ANR_B16_NOVEL_WOFF : ANR_NOVEL_WOFF) : 0;
   ma.pose_boff = o->novel_pose ? ANR_NOVEL_BOFF : 0;
   const int lds = b16 ? mlp_lds_bytes<true>() : mlp_lds_bytes<false>();
   if (!mlp_attr_set) {
     if (hipFuncSetAttribute((const void*)k_mlp, hipFuncAttributeMaxDynamicSharedMemorySize, mlp_lds_bytes<false>()) !=
             hipSuccess ||
         hipFuncSetAttribute((const void*)k_mlp_b16, hipFuncAttributeMaxDynamicSharedMemorySize, mlp_lds_bytes<true>()) !=
+            hipSuccess ||
+        hipFuncSetAttribute((const void*)k_mlp_x6, hipFuncAttributeMaxDynamicSharedMemorySize, mlp_lds_bytes<true>()) !=
             hipSuccess)
       return fail(ANR_E_HIP, "hipFuncSetAttribute(k_mlp) failed");
     mlp_attr_set = true;
@@ -187,7 +190,8 @@ int stage_mlp(const anr_params* p, const anr_frame* f, const float* ray_o, const
     evp = &g_prof.ev[g_prof.used++];
     if (hipEventRecord(evp->first, s) != hipSuccess) return fail(ANR_E_HIP, "hipEventRecord failed");
   }
-  if (b16) hipLaunchKernelGGL(k_mlp_b16, dim3(grid), dim3(512), lds, s, ma);
+  if (x6) hipLaunchKernelGGL(k_mlp_x6, dim3(grid), dim3(512), lds, s, ma);
+  else if (b16) hipLaunchKernelGGL(k_mlp_b16, dim3(grid), dim3(512), lds, s, ma);
   else hipLaunchKernelGGL(k_mlp, dim3(grid), dim3(512), lds, s, ma);
   ANR_TRY(check_launch("k_mlp"));
   if (evp && hipEventRecord(evp->second, s) != hipSuccess) return fail(ANR_E_HIP, "hipEventRecord failed");

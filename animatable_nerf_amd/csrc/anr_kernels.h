@@ -110,6 +110,11 @@ struct MlpArgs {
   // sample id's world point wpts[id], view direction vdir[id] and dists[id] instead of a ray sample
   const float* vdir;
   const float* dists;
+  // sdf residual program (k_resd_b16): rows [0, n_rows) of ptb ([n][8], big-pose xyz in 0..2) in,
+  // the resd_fc outputs (before 0.05 tanh) to yr ([n][4], columns 0..2)
+  const float* ptb;
+  float* yr;
+  int n_rows;
 };
 
 struct PrepArgs {
@@ -154,6 +159,7 @@ __global__ void k_composite(CompositeArgs a);
 __global__ void k_prep(PrepArgs a);
 __global__ void k_mlp(MlpArgs a);
 __global__ void k_mlp_b16(MlpArgs a);  // T-pose BW + NeRF in bf16x3 (render precision ANR_BF16X3)
+__global__ void k_mlp_x6(MlpArgs a);   // every layer in bf16x6, fp32-level (render precision ANR_BF16X6)
 __global__ void k_alpha(MlpArgs a);      // density program (get_alpha), exact fp32 MFMA
 __global__ void k_alpha_b16(MlpArgs a);  // density program, NeRF trunk in bf16x3
 
@@ -166,6 +172,11 @@ __global__ void k_pack_head_b(PackArgs a);
 __global__ void k_pack_weights(PackArgs a);
 __global__ void k_pack_bias(PackArgs a);
 __global__ void k_pack_b16(PackArgs a);
+// sdf residual MLP (anr_layers.h resd_desc): bf16x3 image + biases of resd_image_bytes() at a.out
+// (t[l] = weight of resd layer l, t[9 + l] its bias), and the fused program over one batch
+__global__ void k_pack_resd(PackArgs a);
+int resd_pack_threads();
+int launch_resd(const MlpArgs& a, int grid, hipStream_t s);
 __global__ void k_pack_x6(PackArgs a);
 
 }  // namespace anr

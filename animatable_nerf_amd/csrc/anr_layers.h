@@ -93,8 +93,23 @@ __host__ __device__ constexpr LayerDesc novel_desc(int i) {
                    {layer_desc(i).seg[0], layer_desc(i).seg[1]}};
 }
 
+// layers 32..40: the sdf_pdf residual deformation MLP (anisdf_pdf_network.py:24-31, 49-73):
+// [gamma_10(x) 63 || poses 72] -> 8 x 256 ReLU (skip [features || h] at layer 5, in 391) -> resd_fc 3.
+// The poses columns are folded into the layer-0 / layer-5 biases (k_sdf_fold), as the BW MLP's latent.
+// Packed into the sdf render's own bf16x3 image (k_pack_resd); tensor indices are those of its
+// PackArgs: weight of layer 32 + l at t[l], bias at t[9 + l].
+#define ANR_L_RESD0 32
+#define ANR_RESD_LAYERS 9
+__host__ __device__ constexpr LayerDesc resd_desc(int l) {
+  return l == 0   ? LayerDesc{0, 9, -1, -1, 256, 0, 135, 16, 1, {{SRC_EMB, 16, 0}, {0, 0, 0}}}
+         : l == 5 ? LayerDesc{5, 14, -1, -1, 256, 0, 391, 16, 2, {{SRC_EMB, 16, 0}, {SRC_ACT, 64, 135}}}
+         : l == 8 ? LayerDesc{8, 17, -1, -1, 3, 0, 256, 1, 1, {{SRC_ACT, 64, 0}, {0, 0, 0}}}
+                  : LayerDesc{l, 9 + l, -1, -1, 256, 0, 256, 16, 1, {{SRC_ACT, 64, 0}, {0, 0, 0}}};
+}
+
 __host__ __device__ constexpr LayerDesc layer_desc_all(int i) {
-  return i < ANR_NUM_LAYERS ? layer_desc(i)
+  return i >= ANR_L_RESD0 ? resd_desc(i - ANR_L_RESD0)
+       : i < ANR_NUM_LAYERS ? layer_desc(i)
        : i == ANR_L_VIEW ? LayerDesc{23, 24, -1, -1, 128, 0, 283, 8, 2, {{SRC_ACT, 64, 0}, {SRC_VEMB, 8, 256}}}
        : i == ANR_L_RGB  ? LayerDesc{25, 26, -1, -1, 3, 0, 128, 1, 1, {{SRC_ACT, 32, 0}, {0, 0, 0}}}
        : i < ANR_L_ALPHA ? novel_desc(i - ANR_L_NOVEL0)
@@ -173,6 +188,16 @@ __host__ __device__ constexpr int b16_layer_offset(int i) {
 }
 __host__ __device__ constexpr int b16_bytes() { return b16_layer_offset(ANR_B16_LAYERS); }
 #define ANR_B16_NOVEL_WOFF (b16_layer_offset(ANR_L_NOVEL0) - b16_layer_offset(0))
+// the sdf residual MLP's image (layers 32..40, same fragment format), its own buffer: weights from
+// byte 0, then the biases padded to ob x 16 floats per layer (resd_bias_off)
+__host__ __device__ constexpr int resd_layer_offset(int i) { return b16_layer_offset(i) - b16_layer_offset(ANR_L_RESD0); }
+__host__ __device__ constexpr int resd_wbytes() { return resd_layer_offset(ANR_L_RESD0 + ANR_RESD_LAYERS); }
+__host__ __device__ constexpr int resd_bias_off(int l) {
+  int o = 0;
+  for (int k = 0; k < l; ++k) o += layer_desc_all(ANR_L_RESD0 + k).ob * 16;
+  return o;
+}
+__host__ __device__ constexpr int resd_image_bytes() { return resd_wbytes() + resd_bias_off(ANR_RESD_LAYERS) * 4; }
 // arithmetic of the pose-space pass in the bf16 kernel: 1 = bf16x3 (default), 2 = bf16x6
 #ifndef ANR_POSE_MODE
 #define ANR_POSE_MODE 1
@@ -181,12 +206,13 @@ __host__ __device__ constexpr int b16_bytes() { return b16_layer_offset(ANR_B16_
 __host__ __device__ constexpr int b16_base() { return (packed_bytes() + 255) / 256 * 256; }
 
 
-// bf16x6 image (the pose-space BW pass under ANR_BF16X3): layers 0..8 and their novel_pose_bw copy
-// 21..29, each weight as hi/mid/lo bf16 (w = hi + mid + lo to 24 bits), the activation likewise;
-// products hl + lh + mm + hm + mh + hh (dropped terms ~2^-24: fp32-level). Per k-step, per
-// out-block [hi][mid][lo] fragments = 3 KiB; x6 index i <-> layer (i < 9 ? i : 21 + i - 9).
-#define ANR_X6_LAYERS 18
-__host__ __device__ constexpr int x6_layer(int i) { return i < 9 ? i : ANR_L_NOVEL0 + i - 9; }
+// bf16x6 image (render precision ANR_BF16X6, k_mlp_x6 / k_alpha_x6; and the pose-space BW pass of a
+// bf16x3 kernel built with ANR_POSE_MODE=2): layers 0..31, each weight as hi/mid/lo bf16 (w = hi +
+// mid + lo to 24 bits), the activation likewise; products hl + lh + mm + hm + mh + hh (the dropped
+// ml, lm, ll terms are <= ~2^-24 relative: fp32-level). Per k-step, per out-block [hi][mid][lo]
+// fragments = 3 KiB; a k-step is staged as groups of <= 8 out-blocks.
+#define ANR_X6_LAYERS 32
+__host__ __device__ constexpr int x6_layer(int i) { return i; }
 __host__ __device__ constexpr int x6_layer_bytes(int i) { return ks32(x6_layer(i)) * layer_desc_all(x6_layer(i)).ob * 3072; }
 __host__ __device__ constexpr int x6_layer_offset(int i) {
   int o = 0;
@@ -195,7 +221,7 @@ __host__ __device__ constexpr int x6_layer_offset(int i) {
 }
 __host__ __device__ constexpr int x6_bytes() { return x6_layer_offset(ANR_X6_LAYERS); }
 __host__ __device__ constexpr int x6_base() { return (b16_base() + b16_bytes() + 255) / 256 * 256; }
-#define ANR_X6_NOVEL_WOFF (x6_layer_offset(9) - x6_layer_offset(0))
+#define ANR_X6_NOVEL_WOFF (x6_layer_offset(ANR_L_NOVEL0) - x6_layer_offset(0))
 
 // Gamma features in the bf16 image (EMB / VEMB segments of NS k-steps): element pairs (2p, 2p+1) of
 // lane half h in k-step t hold (sin, cos) of one argument x[comp] * 2^freq, so a lane evaluates one

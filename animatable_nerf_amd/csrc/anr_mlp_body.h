@@ -60,26 +60,31 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 //   V = 2 (render, both kernels): entries 0..25 as V = 0, 26 the folded colour head (layer 31:
 //         view_fc's pre-activation || alpha_fc, anr_layers.h ANR_L_HEAD), 27 rgb_fc. V = 0 (the
 //         reference's unfolded head) sizes the bias table and is no longer run.
+//   V = 4 (render, k_mlp_x6, render precision ANR_BF16X6): the V = 2 program with every entry in
+//         mode 2 (bf16x6, fp32-level products) and the accurate libm paths of the exact kernel.
+//   V = 3 (the sdf_pdf residual deformation MLP, k_resd_b16): entries 0..8 = layers 32..40
+//         (anr_layers.h resd_desc), bf16x3, from the sdf render's own image (k_pack_resd).
 template <int V>
-__host__ __device__ constexpr int prog_len() { return V == 0 ? 30 : V == 2 ? 28 : 18; }
+__host__ __device__ constexpr int prog_len() { return V == 0 ? 30 : (V == 2 || V == 4) ? 28 : V == 3 ? 9 : 18; }
 template <int V>
 __host__ __device__ constexpr int prog_layer(int e) {
-  return e < 9 ? e
+  return V == 3 ? ANR_L_RESD0 + e
+         : e < 9 ? e
          : V == 0 ? e - 9
-         : V == 2 ? (e < 26 ? e - 9 : (e == 26 ? ANR_L_HEAD : ANR_L_RGB))
+         : (V == 2 || V == 4) ? (e < 26 ? e - 9 : (e == 26 ? ANR_L_HEAD : ANR_L_RGB))
                   : (e < 17 ? e : ANR_L_ALPHA);
 }
 __host__ __device__ constexpr bool prog_pose(int e) { return e < 9; }
-template <bool B16>
-__host__ __device__ constexpr int prog_mode(int e) { return B16 ? (e < 9 ? ANR_POSE_MODE : 1) : 0; }
+template <bool B16, int V>
+__host__ __device__ constexpr int prog_mode(int e) { return B16 ? (V == 4 ? 2 : e < 9 ? ANR_POSE_MODE : 1) : 0; }
 // Slices = the staging unit: mode 0 8 fp32 k-steps; mode 1 one 32-input k-step (OB x 2 KiB);
 // mode 2 one 32-input k-step of a group of <= 8 out-blocks (x 3 KiB).
 template <int V>
 __host__ __device__ constexpr int prog_nobg(int e) { return (layer_desc_all(prog_layer<V>(e)).ob + 7) / 8; }
 template <bool B16, int V>
 __host__ __device__ constexpr int prog_slices(int e) {
-  return prog_mode<B16>(e) == 2   ? ks32(prog_layer<V>(e)) * prog_nobg<V>(e)
-         : prog_mode<B16>(e) == 1 ? ks32(prog_layer<V>(e)) + (b16_tail_ob(prog_layer<V>(e)) > 0 ? 1 : 0)
+  return prog_mode<B16, V>(e) == 2   ? ks32(prog_layer<V>(e)) * prog_nobg<V>(e)
+         : prog_mode<B16, V>(e) == 1 ? ks32(prog_layer<V>(e)) + (b16_tail_ob(prog_layer<V>(e)) > 0 ? 1 : 0)
                                   : layer_ksteps(prog_layer<V>(e)) / ANR_KSLICE;
 }
 template <int V>
@@ -88,19 +93,20 @@ __host__ __device__ constexpr int x6_group_obs(int e, int gidx) {
 }
 template <bool B16, int V>
 __host__ __device__ constexpr int prog_slice_kb(int e, int q) {
-  return prog_mode<B16>(e) == 2 ? x6_group_obs<V>(e, q % prog_nobg<V>(e)) * 3
-         : prog_mode<B16>(e) == 1
+  return prog_mode<B16, V>(e) == 2 ? x6_group_obs<V>(e, q % prog_nobg<V>(e)) * 3
+         : prog_mode<B16, V>(e) == 1
              ? (q < ks32(prog_layer<V>(e)) ? b16_main_ob(prog_layer<V>(e)) * 2
                                           : b16_tail_ob(prog_layer<V>(e)) * ks32(prog_layer<V>(e)) * 2)
              : layer_chunks(prog_layer<V>(e)) * ANR_KSLICE;
 }
 template <bool B16, int V>
 __host__ __device__ constexpr int prog_slice_off(int e, int q) {
-  return prog_mode<B16>(e) == 2
+  return prog_mode<B16, V>(e) == 2
              ? x6_base() + x6_layer_offset(prog_layer<V>(e)) +
                    ((q / prog_nobg<V>(e)) * layer_desc_all(prog_layer<V>(e)).ob + 8 * (q % prog_nobg<V>(e))) * 3072
-         : prog_mode<B16>(e) == 1
-             ? b16_base() + b16_layer_offset(prog_layer<V>(e)) + q * b16_main_ob(prog_layer<V>(e)) * 2048
+         : prog_mode<B16, V>(e) == 1
+             ? (V == 3 ? resd_layer_offset(prog_layer<V>(e)) : b16_base() + b16_layer_offset(prog_layer<V>(e))) +
+                   q * b16_main_ob(prog_layer<V>(e)) * 2048
              : layer_offset(prog_layer<V>(e)) + q * layer_chunks(prog_layer<V>(e)) * ANR_KSLICE * 1024;
 }
 // loads per wave for a slice (every wave issues the same count, see Pipe::stage)
@@ -268,6 +274,8 @@ __host__ __device__ constexpr int prog_bias_off(int e) {
 static_assert(prog_bias_off<0>(prog_len<0>()) == ANR_BIAS_TABLE_FLOATS, "bias table size (anr_layers.h)");
 static_assert(prog_bias_off<1>(prog_len<1>()) <= ANR_BIAS_TABLE_FLOATS, "bias table size (anr_layers.h)");
 static_assert(prog_bias_off<2>(prog_len<2>()) <= ANR_BIAS_TABLE_FLOATS, "bias table size (anr_layers.h)");
+static_assert(prog_bias_off<4>(prog_len<4>()) <= ANR_BIAS_TABLE_FLOATS, "bias table size (anr_layers.h)");
+static_assert(prog_bias_off<3>(prog_len<3>()) == resd_bias_off(ANR_RESD_LAYERS), "resd bias section (anr_layers.h)");
 
 // Fill the bias table once per launch (before the first barrier of the slice stream). Sources:
 // the packed bias section, the novel_pose_bw copy for the pose pass (pose_boff), and the per-frame
@@ -281,7 +289,9 @@ __device__ __forceinline__ void fill_bias_table(const MlpArgs& a, float* __restr
     constexpr int boff = bias_offset(L);  // constexpr: evaluated by the compiler, not per launch
     constexpr int toff = prog_bias_off<V>(e);
     const float* src;
-    if constexpr (e < 9) {
+    if constexpr (V == 3) {  // sdf residual MLP: poses folded into layers 0 / 5 (k_sdf_fold)
+      src = e == 0 ? a.fold : e == 5 ? a.fold + 256 : a.bias + toff;
+    } else if constexpr (e < 9) {
       src = L == 0 ? a.fold + 0 : L == 5 ? a.fold + 512 : a.bias + a.pose_boff + boff;
     } else if constexpr (V != 1 && e < 18) {
       src = L == 0 ? a.fold + 256 : L == 5 ? a.fold + 768 : a.bias + boff;
@@ -432,7 +442,7 @@ __device__ __forceinline__ void layer(Pipe& p, const f32x4 (&in)[NIN], const flo
   constexpr int L = prog_layer<V>(E);
   constexpr LayerDesc D = layer_desc_all(L);
   static_assert(NOUT >= D.ob, "output array too small");
-  if constexpr (prog_mode<B16>(E) == 1 && x3_stream_layer<L>()) {
+  if constexpr (prog_mode<B16, V>(E) == 1 && x3_stream_layer<L>()) {
     // output ReLU deferred to the consumer's split (RELU_IN of the next layer)
     layer_x3<B16, V, E, RELU_IN>(p, in, emb, vemb, out, sbias, g, lane);
     return;
@@ -447,10 +457,10 @@ __device__ __forceinline__ void layer(Pipe& p, const f32x4 (&in)[NIN], const flo
       out[o] = *(const f32x4*)(sbias + BOFF + o * 16 + 4 * g);
     });
   };
-  if constexpr (prog_mode<B16>(E) != 0) {
+  if constexpr (prog_mode<B16, V>(E) != 0) {
     // bf16x3 (mode 1): per k-step of 32 one hi/lo split of the B fragment, per out-block 2 A reads,
     // 3 MFMAs; bf16x6 (mode 2): hi/mid/lo, 3 A reads, 6 MFMAs (smallest terms first)
-    constexpr bool X6 = prog_mode<B16>(E) == 2;
+    constexpr bool X6 = prog_mode<B16, V>(E) == 2;
     constexpr int KS = ks32(L);
     constexpr int K0 = D.seg[0].ksteps / 8;
     static_for<0, KS>([&](auto t) {
@@ -830,10 +840,12 @@ __device__ __forceinline__ void bw_mlp(Pipe& p, const float (&emb)[16], const fl
   layer<B16, V, E0 + 8, false, true>(p, B, emb, vemb, fc, sb, g, lane);
 }
 
-template <bool B16>
+template <bool B16, int V = 2>
 __device__ __forceinline__ void mlp_body(const MlpArgs& a) {
-  // both kernels run the folded colour head (anr_layers.h ANR_L_HEAD): 131,072 fewer MACs per sample
-  constexpr int V = 2;
+  // every kernel runs the folded colour head (anr_layers.h ANR_L_HEAD): 131,072 fewer MACs per sample
+  static_assert(V == 2 || V == 4, "render programs");
+  // hardware log/exp/rcp and reciprocal lookup coordinates only in the bf16x3 kernel
+  constexpr bool FAST = B16 && ANR_FAST_MATH && V == 2;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -879,11 +891,11 @@ __device__ __forceinline__ void mlp_body(const MlpArgs& a) {
     // ---- pose space: pbw lookup, BW MLP (latent_index + 1), softmax, LBS
     if constexpr (B16) embed_b<2>(pose, g, 10, emb);
     else embed<16>(pose, g, 10, emb);
-    lookup24<B16 && ANR_FAST_MATH>(a.pbw32, pose, a.pbounds, a.pX, a.pY, a.pZ, g, init);
+    lookup24<FAST>(a.pbw32, pose, a.pbounds, a.pX, a.pY, a.pZ, g, init);
 #pragma unroll
     for (int s8 = 0; s8 < 8; ++s8) vemb[s8] = 0.f;
     bw_mlp<B16, V, 0>(p, emb, vemb, sb, A, B, fc, g, lane);
-    blend_softmax<B16 && ANR_FAST_MATH>(fc, init, g, bw);
+    blend_softmax<FAST>(fc, init, g, bw);
     store_rows(a.pbw_rows, idx, bw, g, valid);
     float xt[3];
     lbs_inverse(bw, sA, g, pose, xt);
@@ -891,9 +903,9 @@ __device__ __forceinline__ void mlp_body(const MlpArgs& a) {
     // ---- T-pose: tbw lookup, BW MLP (latent 0) -> tbw rows (training loss only)
     if constexpr (B16) embed_b<2>(xt, g, 10, emb);
     else embed<16>(xt, g, 10, emb);
-    lookup24<B16 && ANR_FAST_MATH>(a.tbw32, xt, a.tbounds, a.tX, a.tY, a.tZ, g, init);
+    lookup24<FAST>(a.tbw32, xt, a.tbounds, a.tX, a.tY, a.tZ, g, init);
     bw_mlp<B16, V, 9>(p, emb, vemb, sb, A, B, fc, g, lane);
-    blend_softmax<B16 && ANR_FAST_MATH>(fc, init, g, bw);
+    blend_softmax<FAST>(fc, init, g, bw);
     store_rows(a.tbw_rows, idx, bw, g, valid);
 
     // ---- canonical NeRF (TPoseHuman.calculate_alpha_rgb)
@@ -911,7 +923,7 @@ __device__ __forceinline__ void mlp_body(const MlpArgs& a) {
     else embed<8>(dir, g, 4, vemb);
     layer<B16, V, 26, false, true>(p, B, emb, vemb, A, sb, g, lane);  // view_fc pre-activation || alpha
     sigma_raw = __shfl(A[8][0], pl);
-    if constexpr (!(B16 && x3_stream_layer<ANR_L_RGB>())) {  // else rgb_fc applies view_fc's ReLU in its split
+    if constexpr (!(prog_mode<B16, V>(27) == 1 && x3_stream_layer<ANR_L_RGB>())) {  // else rgb_fc applies view_fc's ReLU in its split
       static_for<0, 8>([&](auto ob) {
         constexpr int o = decltype(ob)::value;
 #pragma unroll
@@ -996,6 +1008,48 @@ __device__ __forceinline__ void alpha_body(const MlpArgs& a) {
     layer<B16, V, 16, true, true>(p, A, emb, vemb, B, sb, g, lane);
     layer<B16, V, 17, false, true>(p, B, emb, vemb, A, sb, g, lane);  // alpha_fc
     if (valid && g == 0) a.alpha_out[pid] = A[0][0];
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the last (unused) prefetch
+}
+
+// sdf_pdf residual deformation program (V = 3): Network.calculate_residual_deformation
+// (anisdf_pdf_network.py:49-73) per kept sample of one batch, all on chip — gamma_10 of the big-pose
+// point, 8 x 256 ReLU layers (poses folded into the layer-0 / layer-5 biases), resd_fc. Writes the
+// resd_fc output; k_sdf_mid applies 0.05 tanh. Replaces 8 layer GEMMs over HBM-resident activations.
+__device__ __forceinline__ void resd_body(const MlpArgs& a) {
+  constexpr int V = 3;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4;
+  const int pl = lane & 15;
+  float* sb = (float*)smem;  // bias table (anr_layers.h LDS layout)
+  fill_bias_table<V>(a, sb, tid);
+  const int n = a.n_rows;
+  const int ntiles = (n + 127) / 128;
+  if ((int)blockIdx.x >= ntiles) return;  // uniform per workgroup, before any LDS-DMA
+
+  Pipe p{smem + mlp_ring_off(), mlp_slice_max<true>(), mlp_nbuf<true>(), a.wimg, 0, wave, lane, 0};
+  p.template start<true, V>();
+
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int idx = tile * 128 + wave * 16 + pl;
+    const bool valid = idx < n;
+    const float* pt = a.ptb + (size_t)(valid ? idx : n - 1) * 8;
+    const float x[3] = {pt[0], pt[1], pt[2]};
+    float emb[16], vemb[8];
+    f32x4 A[17], B[17], fc[2];
+    embed_b<2>(x, g, 10, emb);
+#pragma unroll
+    for (int s8 = 0; s8 < 8; ++s8) vemb[s8] = 0.f;
+    bw_mlp<true, V, 0>(p, emb, vemb, sb, A, B, fc, g, lane);
+    if (valid && g == 0) {
+      float* y = a.yr + (size_t)idx * 4;
+      y[0] = fc[0][0];
+      y[1] = fc[0][1];
+      y[2] = fc[0][2];
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the last (unused) prefetch
 }

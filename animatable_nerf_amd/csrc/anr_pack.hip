@@ -106,7 +106,52 @@ __global__ void k_pack_b16(PackArgs a) {
   *(uint4*)(base + 1024 + lane * 16) = vl;
 }
 
-// bf16x6 image: one thread per (x6 layer, k-step, out-block, lane) writes hi, mid, lo fragments
+// sdf residual MLP image (anr_layers.h resd_desc, layers 32..40): the bf16x3 fragments of k_pack_b16
+// from byte 0 of `a.out`, then the biases padded per layer (layers 0 and 5 are per-frame folds, left 0)
+__global__ void k_pack_resd(PackArgs a) {
+  const int u = blockIdx.x * blockDim.x + threadIdx.x;
+  const int nfrag = resd_wbytes() / 32;
+  if (u >= nfrag) {
+    const int e = u - nfrag;  // bias float
+    if (e >= resd_bias_off(ANR_RESD_LAYERS)) return;
+    int l = 0;
+    while (l + 1 < ANR_RESD_LAYERS && e >= resd_bias_off(l + 1)) ++l;
+    const LayerDesc d = layer_desc_all(ANR_L_RESD0 + l);
+    const int i = e - resd_bias_off(l);
+    const float* b = a.t[d.tensor_b];
+    ((float*)(a.out + resd_wbytes()))[e] = (b && l != 0 && l != 5 && i < d.nout) ? b[i] : 0.0f;
+    return;
+  }
+  const int byte = u * 32;
+  int L = ANR_L_RESD0;
+  while (L + 1 < ANR_L_RESD0 + ANR_RESD_LAYERS && byte >= resd_layer_offset(L + 1)) ++L;
+  const LayerDesc d = layer_desc_all(L);
+  const int local = (byte - resd_layer_offset(L)) / 32;  // (s, ob, lane); no tail blocks (ob <= 16)
+  const int lane = local & 63;
+  const int so = local >> 6;
+  const int mob = b16_main_ob(L);
+  const int ob = so % mob, t = so / mob;
+  const int row = ob * 16 + (lane & 15), h = lane >> 4;
+  unsigned short hi[8], lo[8];
+  for (int j = 0; j < 8; ++j) {
+    const int col = b16_col(d, t, h, j);
+    float v = 0.0f;
+    if (col >= 0 && row < d.nout && a.t[d.tensor_w] != nullptr) v = a.t[d.tensor_w][(size_t)row * d.in_ch + col];
+    hi[j] = bf16_rne(v);
+    lo[j] = bf16_rne(v - __uint_as_float((uint32_t)hi[j] << 16));
+  }
+  unsigned char* base = a.out + resd_layer_offset(L) + (size_t)so * 2048;
+  uint4 vh, vl;
+  vh.x = hi[0] | ((uint32_t)hi[1] << 16); vh.y = hi[2] | ((uint32_t)hi[3] << 16);
+  vh.z = hi[4] | ((uint32_t)hi[5] << 16); vh.w = hi[6] | ((uint32_t)hi[7] << 16);
+  vl.x = lo[0] | ((uint32_t)lo[1] << 16); vl.y = lo[2] | ((uint32_t)lo[3] << 16);
+  vl.z = lo[4] | ((uint32_t)lo[5] << 16); vl.w = lo[6] | ((uint32_t)lo[7] << 16);
+  *(uint4*)(base + lane * 16) = vh;
+  *(uint4*)(base + 1024 + lane * 16) = vl;
+}
+int resd_pack_threads() { return resd_wbytes() / 32 + resd_bias_off(ANR_RESD_LAYERS); }
+
+// bf16x6 image (anr_layers.h): one thread per (layer, k-step, out-block, lane) writes hi, mid, lo fragments
 __global__ void k_pack_x6(PackArgs a) {
   const int u = blockIdx.x * blockDim.x + threadIdx.x;
   if (u >= x6_bytes() / 48) return;
@@ -118,12 +163,21 @@ __global__ void k_pack_x6(PackArgs a) {
   const int lane = local & 63;
   const int so = local >> 6;
   const int ob = so % d.ob, t = so / d.ob;
-  const int row = ob * 16 + (lane & 15), h = lane >> 4;
+  const int row16 = lane & 15, h = lane >> 4;
+  const int main_ob = (d.nout + 15) / 16;
   unsigned short q[3][8];
   for (int j = 0; j < 8; ++j) {
     const int col = b16_col(d, t, h, j);
     float v = 0.0f;
-    if (col >= 0 && row < d.nout && a.t[d.tensor_w] != nullptr) v = a.t[d.tensor_w][(size_t)row * d.in_ch + col];
+    if (col >= 0 && a.t[d.tensor_w] != nullptr) {
+      if (ob < main_ob) {
+        const int i = ob * 16 + row16;
+        if (i < d.nout) v = a.t[d.tensor_w][(size_t)i * d.in_ch + col];
+      } else if (d.tensor_w2 >= 0) {  // alpha_fc stacked beside feature_fc (layer 17)
+        const int i2 = (ob - main_ob) * 16 + row16;
+        if (i2 < d.nout2) v = a.t[d.tensor_w2][(size_t)i2 * d.in_ch + col];
+      }
+    }
     q[0][j] = bf16_rne(v);
     const float r1 = v - __uint_as_float((uint32_t)q[0][j] << 16);
     q[1][j] = bf16_rne(r1);

@@ -342,7 +342,8 @@ __global__ __launch_bounds__(256) void k_sdf_prep(SdfPointArgs a) {
   const int i0 = blockIdx.x * 256, i = i0 + threadIdx.x;
   if (i < a.cnt) sdf_prep_point(a, i, sp);
   __syncthreads();
-  sdf_rows_store<64>(a.Gr, i0, a.cnt, [&](int r, int c) { return c < 63 ? embed_feature(sp[r], c, 10) : 0.f; });
+  // gamma_10 rows for the layer-GEMM residual MLP (the fused k_resd_b16 forms them on chip: Gr NULL)
+  if (a.Gr) sdf_rows_store<64>(a.Gr, i0, a.cnt, [&](int r, int c) { return c < 63 ? embed_feature(sp[r], c, 10) : 0.f; });
 }
 
 __device__ void sdf_prep_point(const SdfPointArgs& a, int i, float (*sp)[4]) {

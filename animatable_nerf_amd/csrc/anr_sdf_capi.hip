@@ -2,7 +2,8 @@
 //
 // Sequence per render call (anisdf_pdf_network.py:156-223 under tpose_renderer.py:159-186):
 //   k_sdf_front (KNN keep mask, all samples) -> ordered compaction -> one host read of n'
-//   -> per batch of <= SDF_BATCH kept samples: prep, 9 residual-MLP GEMMs, mid, 9 SDF GEMMs
+//   -> per batch of <= SDF_BATCH kept samples: prep, the residual MLP (split-bf16: one fused
+//      k_resd_b16 launch; exact fp32: 9 layer GEMMs), mid, 9 SDF GEMMs
 //      (softplus + its backward factor in the epilogue), 8 input-gradient GEMMs (reverse mode
 //      through the stored factors), gamma backward, 5 colour GEMMs, raw
 //   -> compositing (k_composite) -> msk_sdf lists.
@@ -10,6 +11,7 @@
 // needs every softplus factor of the forward, which does not fit a fused register pipeline.
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 
 #include "../../include/aninerf.h"
 #include "anr_common.h"
@@ -29,7 +31,7 @@ constexpr long SDF_BATCH = 1L << ANR_SDF_BATCH_LOG2;  // kept samples per layer-
 constexpr size_t SDF_LIMG_BYTES = 16u << 20;  // split-bf16 layer-GEMM weight images (31 GEMMs, <= 384 KiB each)
 
 struct SLayout {
-  size_t counts, mask, chunk_min, ray_off, block_sum, list, knn, tbtab, wimg, fold, limg, resd_rows, grad_rows;
+  size_t counts, mask, chunk_min, ray_off, block_sum, list, knn, tbtab, wimg, fold, limg, rimg, resd_rows, grad_rows;
   size_t min_sdf, flags, chunk_cnt, msk_sdf, msk_label;
   size_t ptb, Gr, Ha, Hb, Yr, Xs0, X4, D, Y8, Ga, Gb, Gc, gB, C0, Yc;
   long P;
@@ -57,6 +59,7 @@ SLayout slayout(int n_rays, int chunk) {
   L.wimg = take(SDF_WN_FLOATS * 4);
   L.fold = take(768 * 4);
   L.limg = take(SDF_LIMG_BYTES);
+  L.rimg = take(resd_image_bytes());
   L.resd_rows = take(N * 3 * 4);
   L.grad_rows = take(N * 3 * 4);
   L.min_sdf = take(R * 4);
@@ -336,6 +339,24 @@ int anr_sdf_render_fwd(const anr_sdf_params* p, const anr_sdf_frame* f, const fl
   limg.base = ws + L.limg;
   limg.cap = SDF_LIMG_BYTES;
   const int cus = sdf_cus();
+  // split-bf16: the residual MLP as one fused launch per batch (anr_resd_b16.hip), its weight image
+  // packed once per call (ANR_SDF_RESD_FUSED=0 keeps the layer GEMMs, for A/B timing)
+  const char* rf = getenv("ANR_SDF_RESD_FUSED");
+  const bool resd_fused = o->precision == ANR_BF16X3 && !(rf && rf[0] == '0');
+  unsigned char* rimg = (unsigned char*)(ws + L.rimg);
+  if (resd_fused) {
+    PackArgs pa{};
+    for (int l = 0; l < 8; ++l) {
+      pa.t[l] = tp[SDF_RLIN0 + 2 * l];
+      pa.t[9 + l] = tp[SDF_RLIN0 + 2 * l + 1];
+    }
+    pa.t[8] = tp[SDF_RFC_W];
+    pa.t[17] = tp[SDF_RFC_B];
+    pa.out = rimg;
+    const int nt = resd_pack_threads();
+    hipLaunchKernelGGL(k_pack_resd, dim3((nt + 255) / 256), dim3(256), 0, s, pa);
+    ANR_TRY(check_launch("k_pack_resd"));
+  }
   for (long b0 = 0; b0 < n; b0 += P) {
     const int cnt = (int)std::min<long>(P, n - b0);
     SdfPointArgs a{};
@@ -343,7 +364,7 @@ int anr_sdf_render_fwd(const anr_sdf_params* p, const anr_sdf_frame* f, const fl
     a.ray_o = ray_o; a.ray_d = ray_d; a.near_ = near_; a.far_ = far_; a.t_rand = o->t_rand; a.chunk = o->chunk;
     a.R = f->R; a.Th = f->Th; a.A = f->A; a.bigA = f->big_A; a.weights = f->weights; a.knn = fa.knn;
     a.wimg = wimg; a.tbtab = tbtab;
-    a.ptb = F(L.ptb); a.Gr = F(L.Gr); a.Yr = F(L.Yr); a.Xs0 = F(L.Xs0); a.X4 = F(L.X4); a.C0 = F(L.C0);
+    a.ptb = F(L.ptb); a.Gr = resd_fused ? nullptr : F(L.Gr); a.Yr = F(L.Yr); a.Xs0 = F(L.Xs0); a.X4 = F(L.X4); a.C0 = F(L.C0);
     a.D7 = Dl(7); a.G7 = Ga; a.Gc = Gc; a.gB = F(L.gB); a.Y8 = F(L.Y8); a.Yc = F(L.Yc); a.beta = beta;
     a.resd_rows = F(L.resd_rows); a.grad_rows = F(L.grad_rows); a.raw = raw; a.sdf = out->sdf;
     const dim3 pg((cnt + 255) / 256), pb(256);
@@ -352,6 +373,16 @@ int anr_sdf_render_fwd(const anr_sdf_params* p, const anr_sdf_frame* f, const fl
     // B2 + B3: LBS to the big pose, residual deformation MLP (poses folded into layers 0 / 5)
     hipLaunchKernelGGL(k_sdf_prep, pg, pb, 0, s, a);
     ANR_TRY(check_launch("k_sdf_prep"));
+    if (resd_fused) {
+      MlpArgs ra{};
+      ra.wimg = rimg;
+      ra.bias = (const float*)(rimg + resd_wbytes());
+      ra.fold = fold;
+      ra.ptb = a.ptb;
+      ra.yr = F(L.Yr);
+      ra.n_rows = cnt;
+      if (launch_resd(ra, cus, s) != 0) return fail(ANR_E_HIP, "k_resd_b16 launch failed");
+    } else {
     const float* Wr[8];
     for (int l = 0; l < 8; ++l) Wr[l] = tp[SDF_RLIN0 + 2 * l];
     ANR_TRY(g.fwd(Ha, 256, 256, Wr[0], 135, fold, a.Gr, 64, 63, 0, true));
@@ -366,6 +397,7 @@ int anr_sdf_render_fwd(const anr_sdf_params* p, const anr_sdf_frame* f, const fl
     } else {
       ANR_TRY(g.fwd(Hb, 256, 256, Wr[7], 256, tp[SDF_RLIN0 + 15], Ha, 256, 256, 0, true));
       ANR_TRY(g.fwd(F(L.Yr), 4, 3, tp[SDF_RFC_W], 256, tp[SDF_RFC_B], Hb, 256, 256, 0, false));
+    }
     }
     hipLaunchKernelGGL(k_sdf_mid, pg, pb, 0, s, a);
     ANR_TRY(check_launch("k_sdf_mid"));

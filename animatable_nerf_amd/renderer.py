@@ -92,9 +92,10 @@ class _Call:
         o.precision = precs[prec]
         self.render_precision = _lib.FP32
         rprec = cfg.get('render_precision', 'fp32')
-        if rprec not in ('fp32', 'bf16x3'):
-            raise ValueError(f"render_precision must be 'fp32' or 'bf16x3', got {rprec!r}")
-        self.render_precision = _lib.BF16X3 if rprec == 'bf16x3' else _lib.FP32
+        rprecs = {'fp32': _lib.FP32, 'bf16x3': _lib.BF16X3, 'bf16x6': _lib.BF16X6}
+        if rprec not in rprecs:
+            raise ValueError(f"render_precision must be one of {sorted(rprecs)}, got {rprec!r}")
+        self.render_precision = rprecs[rprec]
         self.opts = o
         if samples is not None:
             return

@@ -85,7 +85,7 @@ def parse():
     ap.add_argument('--shard-frame', action='store_true',
                     help='render: split ONE frame over the ranks by whole chunks and all-gather rgb/acc/depth '
                          '(strong scaling, parallel.render_sharded) instead of one frame per GPU')
-    ap.add_argument('--render-precision', choices=('fp32', 'bf16x3'), default='fp32',
+    ap.add_argument('--render-precision', choices=('fp32', 'bf16x3', 'bf16x6'), default='fp32',
                     help='fp32: exact fp32 MFMA; bf16x3: T-pose BW MLP + NeRF as hi/lo-split bf16 MFMA '
                          '(outputs within the 1e-4 fp32 tolerance, tests/test_gpu_render.py)')
     ap.add_argument('--train-rays', type=int, default=1024)
@@ -140,16 +140,17 @@ def render_roofline(prec, n_kept, kernel_ms):
     priced on SURVEY.md §8(d)'s credited 2,312,192 FLOP per kept sample against the fp32 MFMA peak;
     k_mlp_b16 (split bf16, 3 products per MAC) on the bf16 MFMA FLOP it executes against the dense
     bf16 peak, with the credited figure beside it."""
-    split = prec == 'bf16x3'
-    kernel = 'k_mlp_b16' if split else 'k_mlp'
+    split = prec in ('bf16x3', 'bf16x6')
+    prods = 6 if prec == 'bf16x6' else 3
+    kernel = {'bf16x3': 'k_mlp_b16', 'bf16x6': 'k_mlp_x6'}.get(prec, 'k_mlp')
     t = kernel_ms * 1e-3
     credited = n_kept * FLOP_PER_KEPT / t / 1e12
     if split:
-        flop_exec = 2 * 3 * (2 * MAC_BW + MAC_NERF_FOLDED)
+        flop_exec = 2 * prods * (2 * MAC_BW + MAC_NERF_FOLDED)
         executed = n_kept * flop_exec / t / 1e12
         r = {'bound': 'mfma', 'kernel': kernel, 'achieved': executed, 'peak': PEAK_BF16_MFMA_TFLOPS,
              'unit': 'TFLOP/s', 'frac': executed / PEAK_BF16_MFMA_TFLOPS, 'traffic': None,
-             'flop_per_kept': flop_exec, 'flop_basis': 'executed bf16 MFMA FLOP (3 products per MAC)',
+             'flop_per_kept': flop_exec, 'flop_basis': f'executed bf16 MFMA FLOP ({prods} products per MAC)',
              'achieved_credited': credited, 'frac_credited_vs_bf16_peak': credited / PEAK_BF16_MFMA_TFLOPS,
              'flop_per_kept_credited': FLOP_PER_KEPT}
     else:
@@ -286,7 +287,8 @@ def main():
         'metric': METRIC, 'value': value, 'unit': 'ray-samples/s', 'n_gpus': world, 'steps': args.steps,
         'warmup': args.warmup, 'ms_per_step': dt_max / args.steps * 1e3, 'higher_is_better': True,
         'scaling': 'strong' if args.shard_frame else 'weak', 'vs_baseline': None,
-        'dtype': 'fp32' if prec == 'fp32' else 'bf16 MFMA operands (hi/lo split, 3 products per MAC), fp32 accumulate',
+        'dtype': {'fp32': 'fp32', 'bf16x6': 'bf16 MFMA operands (hi/mid/lo split, 6 products per MAC), fp32 accumulate'}.get(
+            prec, 'bf16 MFMA operands (hi/lo split, 3 products per MAC), fp32 accumulate'),
         'data': 'synthetic',
         'config': {'workload': 'aninerf_s9p full 512x512 render (config 2: fp32, novel-view eval, perturb=0)',
                    'render_precision': prec,
@@ -299,16 +301,22 @@ def main():
         'roofline': render_roofline(prec, n_kept, kernel_ms),
     }
     if not args.no_exact:
-        other = 'bf16x3' if prec == 'fp32' else 'fp32'
-        o2, dt2, kms2, (nk2, _) = timed(other)
-        progress(f'{other}: {dt2 / args.steps * 1e3:.2f} ms/frame, kernel {kms2:.2f} ms')
-        result['bf16x3_split' if other == 'bf16x3' else 'fp32_exact'] = {
-            'value': R * 64 * args.steps * frames / dt2, 'ms_per_step': dt2 / args.steps * 1e3,
-            'render_precision': other,
-            'note': ('same frame, every MLP layer as hi/lo-split bf16 MFMA (outputs held to the same 1e-4 fp32 '
-                     'tolerance by tests/test_gpu_render.py)' if other == 'bf16x3' else 'exact fp32 MFMA'),
-            'roofline': render_roofline(other, nk2, kms2)}
-        del o2
+        notes = {
+            'bf16x3': ('bf16x3_split', 'same frame, every MLP layer as hi/lo-split bf16 MFMA (outputs held to the '
+                       'same 1e-4 fp32 tolerance by tests/test_gpu_render.py)'),
+            'bf16x6': ('bf16x6_fp32_level', 'same frame, every MLP layer as hi/mid/lo-split bf16 MFMA, 6 products '
+                       'per multiply-add, fp32 accumulation: fp32-level products (each output as close to an fp64 '
+                       'evaluation as the reference\'s fp32 arithmetic, tests/test_gpu_render.py '
+                       'test_bf16x6_is_fp32_level)'),
+            'fp32': ('fp32_exact', 'exact fp32 MFMA')}
+        for other in [p for p in ('fp32', 'bf16x6', 'bf16x3') if p != prec]:
+            o2, dt2, kms2, (nk2, _) = timed(other)
+            progress(f'{other}: {dt2 / args.steps * 1e3:.2f} ms/frame, kernel {kms2:.2f} ms')
+            key, note = notes[other]
+            result[key] = {
+                'value': R * 64 * args.steps * frames / dt2, 'ms_per_step': dt2 / args.steps * 1e3,
+                'render_precision': other, 'note': note, 'roofline': render_roofline(other, nk2, kms2)}
+            del o2
     if not args.shard_frame and not args.no_host_render:
         # the drop-in call as run.py:63-69 makes it: Renderer.render(batch) with the eval D2H of every
         # output (tpose_renderer.py:154-155) inside the measured time

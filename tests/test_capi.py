@@ -45,7 +45,8 @@ def test_version_and_sizes(lib):
              (2, 16), (8, 16), (8, 16), (8, 16), (8, 16), (10, 16), (8, 16), (8, 16), (8, 17), (8, 16), (9, 8), (4, 1)]
     # + novel copy, alpha, the folded colour head (layer 31: 9 k-steps x 9 out-blocks)
     b16 = (sum(k * o for k, o in ks_ob) + sum(k * o for k, o in ks_ob[:9]) + 8 * 1 + 9 * 9) * 2048
-    x6 = 2 * sum(k * o for k, o in ks_ob[:9]) * 3072  # pose-pass bf16x6 image (+ novel-pose copy)
+    # bf16x6 image (render precision bf16x6): every layer 0..31 as hi/mid/lo fragments, 3 KiB per (k-step, out-block)
+    x6 = (sum(k * o for k, o in ks_ob) + sum(k * o for k, o in ks_ob[:9]) + 8 * 1 + 9 * 9) * 3072
     base16 = (fp32 + 255) // 256 * 256
     end_x6 = (base16 + b16 + 255) // 256 * 256 + x6
     # head region: H (129 x 283), P (128 x 128), q (128) f32, then fp64 scratch G (128 x 256) and u (256)

@@ -23,10 +23,11 @@ def dev():
     return torch.device('cuda:0')
 
 
-@pytest.fixture(scope='module', params=['fp32', 'bf16x3'])
+@pytest.fixture(scope='module', params=['fp32', 'bf16x3', 'bf16x6'])
 def renderer(dev, request):
-    """Both render precisions are held to the same fp32 tolerance (north_star): exact fp32 MFMA, and
-    the hi/lo-split bf16 MFMA of the T-pose BW MLP + NeRF (include/aninerf.h ANR_BF16X3)."""
+    """Every render precision is held to the same fp32 tolerance (north_star): exact fp32 MFMA, the
+    hi/lo-split bf16 MFMA (include/aninerf.h ANR_BF16X3) and the hi/mid/lo-split bf16x6 MFMA
+    (ANR_BF16X6, fp32-level products)."""
     from animatable_nerf_amd.renderer import Renderer
     net = make_net(dev)
     net.train()  # run.py evaluates in train() mode with perturb = 0
@@ -167,7 +168,7 @@ def test_full_frame_properties(renderer, dev):
         assert err <= TOL, (k, err)
 
 
-@pytest.mark.parametrize('precision', ['fp32', 'bf16x3'])
+@pytest.mark.parametrize('precision', ['fp32', 'bf16x3', 'bf16x6'])
 def test_novel_pose_render_matches_reference(dev, precision):
     """A19: cfg.test_novel_pose renders with novel_pose_bw + bw_latent_index (golden G5)."""
     from animatable_nerf_amd.renderer import Renderer
@@ -267,3 +268,36 @@ def test_frame_shards_equal_whole_frame(renderer, dev, world):
     for k in ('rgb_map', 'acc_map', 'depth_map', 'raw'):
         cat = torch.cat([p[k] for p in parts], dim=1)
         assert torch.equal(cat, full[k]), k
+
+
+def test_bf16x6_is_fp32_level(dev):
+    """ANR_BF16X6 claims fp32-level arithmetic: against an fp64 evaluation of the same network
+    (oracle/restate.py run in float64 on the same fp32 inputs), its outputs are as close as the
+    reference's own fp32 arithmetic (the fp32 oracle) and the exact fp32 MFMA kernel are — each
+    output's max error within 1.5x the larger of those two (5000 rays, 3 chunks, fine volume)."""
+    from animatable_nerf_amd import config
+    from animatable_nerf_amd.renderer import Renderer
+    torch.set_num_threads(16)
+    sc = scene(0.025)
+    ro, rd = sc.box_rays(5000, seed=21)
+    b, _ = batch_np(sc, ro, rd)
+    with torch.no_grad():
+        r32 = restate.render(oracle_params(), to_torch(b))
+        p64 = {k: v.double() for k, v in oracle_params().items()}
+        b64 = {k: (v.double() if v.dtype == torch.float32 else v) for k, v in to_torch(b).items()}
+        r64 = restate.render(p64, b64)
+    assert torch.equal(_keep(r32['raw']), _keep(r64['raw']))  # same samples, same rows
+    net = make_net(dev)
+    net.train()
+    got = {}
+    for prec in ('fp32', 'bf16x6', 'bf16x3'):
+        cfg = config.defaults()
+        cfg.perturb = 0
+        cfg.render_precision = prec
+        ret = Renderer(net, cfg).render_device(to_torch(b, dev))
+        got[prec] = {k: float((ret[k].cpu().double() - r64[k]).abs().max())
+                     for k in ('rgb_map', 'acc_map', 'depth_map', 'raw', 'pbw', 'tbw')}
+    ref_err = {k: float((r32[k].double() - r64[k]).abs().max()) for k in got['fp32']}
+    for k, e6 in got['bf16x6'].items():
+        bar = 1.5 * max(ref_err[k], got['fp32'][k])
+        assert e6 <= bar, (k, e6, ref_err[k], got['fp32'][k], got['bf16x3'][k])
