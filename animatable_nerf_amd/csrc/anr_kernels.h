@@ -115,6 +115,13 @@ struct MlpArgs {
   const float* ptb;
   float* yr;
   int n_rows;
+  // sdf network program (k_sdfnet_b16): point xyz in columns 0..2 of ptb rows of stride ptb_ld (C0);
+  // softplus outputs h of lin l to sdf_h[l] ([n][256], l != 3), lin3's h / sqrt2 to x4[:, :217],
+  // lin8's [sdf || feature] to y8 ([n][264])
+  int ptb_ld;
+  float* sdf_h[8];
+  float* x4;
+  float* y8;
 };
 
 struct PrepArgs {
@@ -172,11 +179,13 @@ __global__ void k_pack_head_b(PackArgs a);
 __global__ void k_pack_weights(PackArgs a);
 __global__ void k_pack_bias(PackArgs a);
 __global__ void k_pack_b16(PackArgs a);
-// sdf residual MLP (anr_layers.h resd_desc): bf16x3 image + biases of resd_image_bytes() at a.out
-// (t[l] = weight of resd layer l, t[9 + l] its bias), and the fused program over one batch
-__global__ void k_pack_resd(PackArgs a);
-int resd_pack_threads();
+// layer sequences of the sdf render (anr_layers.h resd_desc / sdfnet_desc): bf16x3 image + biases of
+// seq_image_bytes(L0, nl) at a.out (t[l] = weight of layer L0 + l, t[9 + l] its bias; layer L0 + sl
+// scaled by sc), and the fused programs over one batch (residual MLP; SDF network forward)
+__global__ void k_pack_seq(PackArgs a, int L0, int nl, int sl, float sc);
+int seq_pack_threads(int L0, int nl);
 int launch_resd(const MlpArgs& a, int grid, hipStream_t s);
+int launch_sdfnet(const MlpArgs& a, int grid, hipStream_t s);
 __global__ void k_pack_x6(PackArgs a);
 
 }  // namespace anr

@@ -15,10 +15,12 @@
 
 namespace anr {
 
-enum SrcKind { SRC_EMB = 0, SRC_ACT = 1, SRC_VEMB = 2 };
+// SRC_EMB: gamma_10(x) (63); SRC_VEMB: gamma_4(dir) (27); SRC_EMB6: gamma_6(x) (39, the sdf_pdf SDF net)
+enum SrcKind { SRC_EMB = 0, SRC_ACT = 1, SRC_VEMB = 2, SRC_EMB6 = 3 };
 
-// A segment of a layer's K dimension: `ksteps` k-steps from one source; `col0` = first weight column.
-struct Seg { int kind; int ksteps; int col0; };
+// A segment of a layer's K dimension: `ksteps` k-steps from one source; `col0` = first weight column;
+// `nact` (ACT segments, 0 = all): input neurons past it are padding (zero weight columns).
+struct Seg { int kind; int ksteps; int col0; int nact = 0; };
 
 struct LayerDesc {
   int tensor_w;   // index into anr_params.t of the weight (out, in, 1)
@@ -107,8 +109,24 @@ __host__ __device__ constexpr LayerDesc resd_desc(int l) {
                   : LayerDesc{l, 9 + l, -1, -1, 256, 0, 256, 16, 1, {{SRC_ACT, 64, 0}, {0, 0, 0}}};
 }
 
+// layers 41..49: the sdf_pdf SDF network (anisdf_pdf_network.py:349-440, SDFNetwork: weight-normed
+// lin0..lin8, softplus(beta=100) after lin0..lin7, skip at lin4 = [h3 (217) || gamma_6(x) (39)] / sqrt2,
+// lin8 -> [sdf || feature 256]) on the effective weights g v / |v| (k_sdf_wnorm). Packed into the sdf
+// render's image after the residual MLP (k_pack_seq; lin4's weights pre-scaled by 1/sqrt2); tensor
+// indices of its PackArgs: weight of lin l at t[l], bias at t[9 + l].
+#define ANR_L_SDF0 41
+#define ANR_SDF_LAYERS 9
+__host__ __device__ constexpr LayerDesc sdfnet_desc(int l) {
+  return l == 0   ? LayerDesc{0, 9, -1, -1, 256, 0, 39, 16, 1, {{SRC_EMB6, 16, 0}, {0, 0, 0}}}
+         : l == 3 ? LayerDesc{3, 12, -1, -1, 217, 0, 256, 14, 1, {{SRC_ACT, 64, 0}, {0, 0, 0}}}
+         : l == 4 ? LayerDesc{4, 13, -1, -1, 256, 0, 256, 16, 2, {{SRC_ACT, 56, 0, 217}, {SRC_EMB6, 16, 217}}}
+         : l == 8 ? LayerDesc{8, 17, -1, -1, 257, 0, 256, 17, 1, {{SRC_ACT, 64, 0}, {0, 0, 0}}}
+                  : LayerDesc{l, 9 + l, -1, -1, 256, 0, 256, 16, 1, {{SRC_ACT, 64, 0}, {0, 0, 0}}};
+}
+
 __host__ __device__ constexpr LayerDesc layer_desc_all(int i) {
-  return i >= ANR_L_RESD0 ? resd_desc(i - ANR_L_RESD0)
+  return i >= ANR_L_SDF0 ? sdfnet_desc(i - ANR_L_SDF0)
+       : i >= ANR_L_RESD0 ? resd_desc(i - ANR_L_RESD0)
        : i < ANR_NUM_LAYERS ? layer_desc(i)
        : i == ANR_L_VIEW ? LayerDesc{23, 24, -1, -1, 128, 0, 283, 8, 2, {{SRC_ACT, 64, 0}, {SRC_VEMB, 8, 256}}}
        : i == ANR_L_RGB  ? LayerDesc{25, 26, -1, -1, 3, 0, 128, 1, 1, {{SRC_ACT, 32, 0}, {0, 0, 0}}}
@@ -188,16 +206,15 @@ __host__ __device__ constexpr int b16_layer_offset(int i) {
 }
 __host__ __device__ constexpr int b16_bytes() { return b16_layer_offset(ANR_B16_LAYERS); }
 #define ANR_B16_NOVEL_WOFF (b16_layer_offset(ANR_L_NOVEL0) - b16_layer_offset(0))
-// the sdf residual MLP's image (layers 32..40, same fragment format), its own buffer: weights from
-// byte 0, then the biases padded to ob x 16 floats per layer (resd_bias_off)
-__host__ __device__ constexpr int resd_layer_offset(int i) { return b16_layer_offset(i) - b16_layer_offset(ANR_L_RESD0); }
-__host__ __device__ constexpr int resd_wbytes() { return resd_layer_offset(ANR_L_RESD0 + ANR_RESD_LAYERS); }
-__host__ __device__ constexpr int resd_bias_off(int l) {
+// a packed layer sequence L0 .. L0 + nl - 1 (k_pack_seq): weights from byte 0, biases after
+__host__ __device__ constexpr int seq_layer_offset(int L0, int L) { return b16_layer_offset(L) - b16_layer_offset(L0); }
+__host__ __device__ constexpr int seq_wbytes(int L0, int nl) { return seq_layer_offset(L0, L0 + nl); }
+__host__ __device__ constexpr int seq_bias_off(int L0, int l) {
   int o = 0;
-  for (int k = 0; k < l; ++k) o += layer_desc_all(ANR_L_RESD0 + k).ob * 16;
+  for (int k = 0; k < l; ++k) o += layer_desc_all(L0 + k).ob * 16;
   return o;
 }
-__host__ __device__ constexpr int resd_image_bytes() { return resd_wbytes() + resd_bias_off(ANR_RESD_LAYERS) * 4; }
+__host__ __device__ constexpr int seq_image_bytes(int L0, int nl) { return seq_wbytes(L0, nl) + seq_bias_off(L0, nl) * 4; }
 // arithmetic of the pose-space pass in the bf16 kernel: 1 = bf16x3 (default), 2 = bf16x6
 #ifndef ANR_POSE_MODE
 #define ANR_POSE_MODE 1
@@ -248,8 +265,11 @@ __host__ __device__ inline int b16_col(const LayerDesc& d, int t, int h, int j) 
     t -= d.seg[s].ksteps / 8;
   }
   const Seg sg = d.seg[s];
-  if (sg.kind == SRC_ACT) return sg.col0 + 32 * t + (j < 4 ? 4 * h + j : 16 + 4 * h + j - 4);
-  const int f = gamma_slot_feature(sg.ksteps / 8, sg.kind == SRC_EMB ? 10 : 4, t, h, j);
+  if (sg.kind == SRC_ACT) {
+    const int n = 32 * t + (j < 4 ? 4 * h + j : 16 + 4 * h + j - 4);
+    return sg.nact && n >= sg.nact ? -1 : sg.col0 + n;
+  }
+  const int f = gamma_slot_feature(sg.ksteps / 8, sg.kind == SRC_EMB ? 10 : sg.kind == SRC_EMB6 ? 6 : 4, t, h, j);
   return f >= 0 ? sg.col0 + f : -1;
 }
 

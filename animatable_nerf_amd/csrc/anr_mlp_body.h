@@ -62,13 +62,19 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 //         reference's unfolded head) sizes the bias table and is no longer run.
 //   V = 4 (render, k_mlp_x6, render precision ANR_BF16X6): the V = 2 program with every entry in
 //         mode 2 (bf16x6, fp32-level products) and the accurate libm paths of the exact kernel.
+//   V = 5 (the sdf_pdf SDF network forward, k_sdfnet_b16): entries 0..8 = layers 41..49
+//         (anr_layers.h sdfnet_desc), bf16x3, the image after the residual MLP's.
 //   V = 3 (the sdf_pdf residual deformation MLP, k_resd_b16): entries 0..8 = layers 32..40
 //         (anr_layers.h resd_desc), bf16x3, from the sdf render's own image (k_pack_resd).
 template <int V>
-__host__ __device__ constexpr int prog_len() { return V == 0 ? 30 : (V == 2 || V == 4) ? 28 : V == 3 ? 9 : 18; }
+__host__ __device__ constexpr int prog_len() { return V == 0 ? 30 : (V == 2 || V == 4) ? 28 : (V == 3 || V == 5) ? 9 : 18; }
+// programs whose weights are a packed layer sequence of their own (k_pack_seq), not the render image
+template <int V>
+__host__ __device__ constexpr bool prog_seq() { return V == 3 || V == 5; }
 template <int V>
 __host__ __device__ constexpr int prog_layer(int e) {
   return V == 3 ? ANR_L_RESD0 + e
+         : V == 5 ? ANR_L_SDF0 + e
          : e < 9 ? e
          : V == 0 ? e - 9
          : (V == 2 || V == 4) ? (e < 26 ? e - 9 : (e == 26 ? ANR_L_HEAD : ANR_L_RGB))
@@ -105,7 +111,8 @@ __host__ __device__ constexpr int prog_slice_off(int e, int q) {
              ? x6_base() + x6_layer_offset(prog_layer<V>(e)) +
                    ((q / prog_nobg<V>(e)) * layer_desc_all(prog_layer<V>(e)).ob + 8 * (q % prog_nobg<V>(e))) * 3072
          : prog_mode<B16, V>(e) == 1
-             ? (V == 3 ? resd_layer_offset(prog_layer<V>(e)) : b16_base() + b16_layer_offset(prog_layer<V>(e))) +
+             ? (prog_seq<V>() ? seq_layer_offset(prog_layer<V>(0), prog_layer<V>(e))
+                              : b16_base() + b16_layer_offset(prog_layer<V>(e))) +
                    q * b16_main_ob(prog_layer<V>(e)) * 2048
              : layer_offset(prog_layer<V>(e)) + q * layer_chunks(prog_layer<V>(e)) * ANR_KSLICE * 1024;
 }
@@ -275,7 +282,9 @@ static_assert(prog_bias_off<0>(prog_len<0>()) == ANR_BIAS_TABLE_FLOATS, "bias ta
 static_assert(prog_bias_off<1>(prog_len<1>()) <= ANR_BIAS_TABLE_FLOATS, "bias table size (anr_layers.h)");
 static_assert(prog_bias_off<2>(prog_len<2>()) <= ANR_BIAS_TABLE_FLOATS, "bias table size (anr_layers.h)");
 static_assert(prog_bias_off<4>(prog_len<4>()) <= ANR_BIAS_TABLE_FLOATS, "bias table size (anr_layers.h)");
-static_assert(prog_bias_off<3>(prog_len<3>()) == resd_bias_off(ANR_RESD_LAYERS), "resd bias section (anr_layers.h)");
+static_assert(prog_bias_off<3>(prog_len<3>()) == seq_bias_off(ANR_L_RESD0, ANR_RESD_LAYERS), "resd bias section");
+static_assert(prog_bias_off<5>(prog_len<5>()) == seq_bias_off(ANR_L_SDF0, ANR_SDF_LAYERS), "sdf bias section");
+static_assert(prog_bias_off<5>(prog_len<5>()) <= ANR_BIAS_TABLE_FLOATS, "bias table size (anr_layers.h)");
 
 // Fill the bias table once per launch (before the first barrier of the slice stream). Sources:
 // the packed bias section, the novel_pose_bw copy for the pose pass (pose_boff), and the per-frame
@@ -291,6 +300,8 @@ __device__ __forceinline__ void fill_bias_table(const MlpArgs& a, float* __restr
     const float* src;
     if constexpr (V == 3) {  // sdf residual MLP: poses folded into layers 0 / 5 (k_sdf_fold)
       src = e == 0 ? a.fold : e == 5 ? a.fold + 256 : a.bias + toff;
+    } else if constexpr (V == 5) {  // sdf network: the image's bias section
+      src = a.bias + toff;
     } else if constexpr (e < 9) {
       src = L == 0 ? a.fold + 0 : L == 5 ? a.fold + 512 : a.bias + a.pose_boff + boff;
     } else if constexpr (V != 1 && e < 18) {
@@ -345,7 +356,7 @@ __device__ __forceinline__ void layer_x3(Pipe& p, const f32x4 (&in)[NIN], const 
     constexpr int ts = t < K0 ? t : t - K0;
     constexpr int kind = D.seg[seg].kind;
     float x[8];
-    if constexpr (kind == SRC_EMB) {
+    if constexpr (kind == SRC_EMB || kind == SRC_EMB6) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) x[j] = emb[8 * ts + j];
     } else if constexpr (kind == SRC_VEMB) {
@@ -474,7 +485,7 @@ __device__ __forceinline__ void layer(Pipe& p, const f32x4 (&in)[NIN], const flo
       constexpr int ts = tt < K0 ? tt : tt - K0;
       constexpr int kind = D.seg[seg].kind;
       float x[8];
-      if constexpr (kind == SRC_EMB) {
+      if constexpr (kind == SRC_EMB || kind == SRC_EMB6) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) x[j] = emb[8 * ts + j];
       } else if constexpr (kind == SRC_VEMB) {
@@ -1036,7 +1047,7 @@ __device__ __forceinline__ void resd_body(const MlpArgs& a) {
   for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int idx = tile * 128 + wave * 16 + pl;
     const bool valid = idx < n;
-    const float* pt = a.ptb + (size_t)(valid ? idx : n - 1) * 8;
+    const float* pt = a.ptb + (size_t)(valid ? idx : n - 1) * a.ptb_ld;
     const float x[3] = {pt[0], pt[1], pt[2]};
     float emb[16], vemb[8];
     f32x4 A[17], B[17], fc[2];
@@ -1049,6 +1060,115 @@ __device__ __forceinline__ void resd_body(const MlpArgs& a) {
       y[0] = fc[0][0];
       y[1] = fc[0][1];
       y[2] = fc[0][2];
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the last (unused) prefetch
+}
+
+// softplus(beta = 100, threshold = 20) of the accumulators in place, as k_lgemm's epilogue computes it
+template <int NOB>
+__device__ __forceinline__ void softplus_regs(f32x4 (&v)[17]) {
+  static_for<0, NOB>([&](auto ob) {
+    constexpr int o = decltype(ob)::value;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float x = v[o][r];
+      const float z = x * 100.f;
+      const float ez = fast_exp(z);
+      v[o][r] = z > 20.f ? x : fast_log1p(ez) * 0.01f;
+    }
+  });
+}
+
+// sdf_pdf SDF network forward (V = 5): SDFNetwork.forward (anisdf_pdf_network.py:421-437) per kept
+// sample of one batch, on chip — gamma_6 of the canonical point, lin0..lin7 with softplus, the skip
+// [h3 || gamma_6] / sqrt2 at lin4 (the 1/sqrt2 is in lin4's packed weights), lin8. What the reverse
+// pass (the input gradient) and the colour net read is written once: every softplus output h (lin3's
+// as h / sqrt2 in X4, the layout of the layer-GEMM path) and lin8's [sdf || feature].
+__device__ __forceinline__ void sdfnet_body(const MlpArgs& a) {
+  constexpr int V = 5;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4;
+  const int pl = lane & 15;
+  float* sb = (float*)smem;  // bias table (anr_layers.h LDS layout)
+  fill_bias_table<V>(a, sb, tid);
+  const int n = a.n_rows;
+  const int ntiles = (n + 127) / 128;
+  if ((int)blockIdx.x >= ntiles) return;  // uniform per workgroup, before any LDS-DMA
+
+  Pipe p{smem + mlp_ring_off(), mlp_slice_max<true>(), mlp_nbuf<true>(), a.wimg, 0, wave, lane, 0};
+  p.template start<true, V>();
+
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int idx = tile * 128 + wave * 16 + pl;
+    const bool valid = idx < n;
+    const size_t row = (size_t)(valid ? idx : n - 1);
+    const float* pt = a.ptb + row * a.ptb_ld;
+    const float x[3] = {pt[0], pt[1], pt[2]};
+    float emb[16], vemb[8];
+    f32x4 A[17], B[17];
+    embed_b<2>(x, g, 6, emb);
+#pragma unroll
+    for (int s8 = 0; s8 < 8; ++s8) vemb[s8] = 0.f;
+    // h of a 256-wide softplus layer -> sdf_h[l] (16 B per lane and out-block)
+    auto store_h = [&](const f32x4(&v)[17], float* __restrict__ dst) {
+      if (!valid) return;
+      float* d = dst + row * 256 + 4 * g;
+      static_for<0, 16>([&](auto ob) {
+        constexpr int o = decltype(ob)::value;
+        *(f32x4*)(d + 16 * o) = v[o];
+      });
+    };
+    f32x4 dummy[1];
+    layer<true, V, 0, false>(p, dummy, emb, vemb, A, sb, g, lane);
+    softplus_regs<16>(A);
+    store_h(A, a.sdf_h[0]);
+    layer<true, V, 1, false>(p, A, emb, vemb, B, sb, g, lane);
+    softplus_regs<16>(B);
+    store_h(B, a.sdf_h[1]);
+    layer<true, V, 2, false>(p, B, emb, vemb, A, sb, g, lane);
+    softplus_regs<16>(A);
+    store_h(A, a.sdf_h[2]);
+    layer<true, V, 3, false>(p, A, emb, vemb, B, sb, g, lane);  // 217 outputs (14 out-blocks)
+    softplus_regs<14>(B);
+    if (valid) {
+      float* d = a.x4 + row * 256;
+      const float sqrt2 = 1.41421356237309515f;
+      static_for<0, 14>([&](auto ob) {
+        constexpr int o = decltype(ob)::value;
+        const int c = 16 * o + 4 * g;
+        if (c + 4 <= 217) {
+          *(f32x4*)(d + c) = f32x4{B[o][0] / sqrt2, B[o][1] / sqrt2, B[o][2] / sqrt2, B[o][3] / sqrt2};
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (c + r < 217) d[c + r] = B[o][r] / sqrt2;
+        }
+      });
+    }
+    layer<true, V, 4, false>(p, B, emb, vemb, A, sb, g, lane);  // [h3 || gamma_6] (1/sqrt2 in the weights)
+    softplus_regs<16>(A);
+    store_h(A, a.sdf_h[4]);
+    layer<true, V, 5, false>(p, A, emb, vemb, B, sb, g, lane);
+    softplus_regs<16>(B);
+    store_h(B, a.sdf_h[5]);
+    layer<true, V, 6, false>(p, B, emb, vemb, A, sb, g, lane);
+    softplus_regs<16>(A);
+    store_h(A, a.sdf_h[6]);
+    layer<true, V, 7, false>(p, A, emb, vemb, B, sb, g, lane);
+    softplus_regs<16>(B);
+    store_h(B, a.sdf_h[7]);
+    layer<true, V, 8, false>(p, B, emb, vemb, A, sb, g, lane);  // [sdf || feature], no activation
+    if (valid) {
+      float* d = a.y8 + row * 264 + 4 * g;
+      static_for<0, 16>([&](auto ob) {
+        constexpr int o = decltype(ob)::value;
+        *(f32x4*)(d + 16 * o) = A[o];
+      });
+      if (g == 0) a.y8[row * 264 + 256] = A[16][0];
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the last (unused) prefetch

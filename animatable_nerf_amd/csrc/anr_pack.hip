@@ -106,41 +106,45 @@ __global__ void k_pack_b16(PackArgs a) {
   *(uint4*)(base + 1024 + lane * 16) = vl;
 }
 
-// sdf residual MLP image (anr_layers.h resd_desc, layers 32..40): the bf16x3 fragments of k_pack_b16
-// from byte 0 of `a.out`, then the biases padded per layer (layers 0 and 5 are per-frame folds, left 0)
-__global__ void k_pack_resd(PackArgs a) {
+// A layer sequence L0 .. L0 + nl - 1 of the layer table as its own bf16x3 image (the sdf render's
+// residual MLP, layers 32..40, and SDF network, 41..49): k_pack_b16's fragments (main out-blocks,
+// then tail blocks) from byte 0 of `a.out`, then the biases padded to ob x 16 per layer. Layer
+// L0 + sl's weights are multiplied by `sc` (lin4's 1/sqrt2 of its skip concatenation).
+__global__ void k_pack_seq(PackArgs a, int L0, int nl, int sl, float sc) {
   const int u = blockIdx.x * blockDim.x + threadIdx.x;
-  const int nfrag = resd_wbytes() / 32;
+  const int nfrag = seq_wbytes(L0, nl) / 32;
   if (u >= nfrag) {
     const int e = u - nfrag;  // bias float
-    if (e >= resd_bias_off(ANR_RESD_LAYERS)) return;
+    if (e >= seq_bias_off(L0, nl)) return;
     int l = 0;
-    while (l + 1 < ANR_RESD_LAYERS && e >= resd_bias_off(l + 1)) ++l;
-    const LayerDesc d = layer_desc_all(ANR_L_RESD0 + l);
-    const int i = e - resd_bias_off(l);
+    while (l + 1 < nl && e >= seq_bias_off(L0, l + 1)) ++l;
+    const LayerDesc d = layer_desc_all(L0 + l);
+    const int i = e - seq_bias_off(L0, l);
     const float* b = a.t[d.tensor_b];
-    ((float*)(a.out + resd_wbytes()))[e] = (b && l != 0 && l != 5 && i < d.nout) ? b[i] : 0.0f;
+    ((float*)(a.out + seq_wbytes(L0, nl)))[e] = (b && i < d.nout) ? b[i] : 0.0f;
     return;
   }
   const int byte = u * 32;
-  int L = ANR_L_RESD0;
-  while (L + 1 < ANR_L_RESD0 + ANR_RESD_LAYERS && byte >= resd_layer_offset(L + 1)) ++L;
+  int L = L0;
+  while (L + 1 < L0 + nl && byte >= seq_layer_offset(L0, L + 1)) ++L;
   const LayerDesc d = layer_desc_all(L);
-  const int local = (byte - resd_layer_offset(L)) / 32;  // (s, ob, lane); no tail blocks (ob <= 16)
+  const int local = (byte - seq_layer_offset(L0, L)) / 32;  // (s, ob, lane)
   const int lane = local & 63;
   const int so = local >> 6;
-  const int mob = b16_main_ob(L);
-  const int ob = so % mob, t = so / mob;
+  const int mob = b16_main_ob(L), tob = b16_tail_ob(L), ks = ks32(L);
+  const int ob = so < ks * mob ? so % mob : mob + (so - ks * mob) % tob;
+  const int t = so < ks * mob ? so / mob : (so - ks * mob) / tob;
   const int row = ob * 16 + (lane & 15), h = lane >> 4;
+  const float f = L == L0 + sl ? sc : 1.0f;
   unsigned short hi[8], lo[8];
   for (int j = 0; j < 8; ++j) {
     const int col = b16_col(d, t, h, j);
     float v = 0.0f;
-    if (col >= 0 && row < d.nout && a.t[d.tensor_w] != nullptr) v = a.t[d.tensor_w][(size_t)row * d.in_ch + col];
+    if (col >= 0 && row < d.nout && a.t[d.tensor_w] != nullptr) v = a.t[d.tensor_w][(size_t)row * d.in_ch + col] * f;
     hi[j] = bf16_rne(v);
     lo[j] = bf16_rne(v - __uint_as_float((uint32_t)hi[j] << 16));
   }
-  unsigned char* base = a.out + resd_layer_offset(L) + (size_t)so * 2048;
+  unsigned char* base = a.out + seq_layer_offset(L0, L) + (size_t)so * 2048;
   uint4 vh, vl;
   vh.x = hi[0] | ((uint32_t)hi[1] << 16); vh.y = hi[2] | ((uint32_t)hi[3] << 16);
   vh.z = hi[4] | ((uint32_t)hi[5] << 16); vh.w = hi[6] | ((uint32_t)hi[7] << 16);
@@ -149,7 +153,7 @@ __global__ void k_pack_resd(PackArgs a) {
   *(uint4*)(base + lane * 16) = vh;
   *(uint4*)(base + 1024 + lane * 16) = vl;
 }
-int resd_pack_threads() { return resd_wbytes() / 32 + resd_bias_off(ANR_RESD_LAYERS); }
+int seq_pack_threads(int L0, int nl) { return seq_wbytes(L0, nl) / 32 + seq_bias_off(L0, nl); }
 
 // bf16x6 image (anr_layers.h): one thread per (layer, k-step, out-block, lane) writes hi, mid, lo fragments
 __global__ void k_pack_x6(PackArgs a) {

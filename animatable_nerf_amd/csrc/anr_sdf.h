@@ -69,6 +69,7 @@ struct SdfPointArgs {
   const float* Yr;       // [P][4] resd_fc output
   float* Xs0;            // [P][40] gamma_6(tpose)
   float* X4;             // [P][256] lin4 input: cols 217..255 = gamma_6 / sqrt(2)
+  int skip_sdf_in;       // the fused SDF forward forms gamma_6 itself: k_sdf_mid writes no Xs0 / X4 columns
   float* C0;             // [P][40] colour input: tpose, gamma_4(bigdir), gradient
   const float* D7;       // [P][256] softplus factor of lin7 (d7_h: lin7's softplus output h)
   int d7_h;

@@ -406,11 +406,13 @@ __global__ __launch_bounds__(256) void k_sdf_mid(SdfPointArgs a) {
   }
   __syncthreads();
   const float sqrt2 = 1.41421356237309515f;
-  sdf_rows_store<40>(a.Xs0, i0, a.cnt, [&](int r, int c) { return c < 39 ? embed_feature(sp[r], c, 6) : 0.f; });
   const int rows = min(256, a.cnt - i0);
-  for (int f = threadIdx.x; f < rows * 39; f += 256) {
-    const int r = f / 39, c = f - r * 39;
-    a.X4[(size_t)(i0 + r) * 256 + 217 + c] = embed_feature(sp[r], c, 6) / sqrt2;
+  if (!a.skip_sdf_in) {
+    sdf_rows_store<40>(a.Xs0, i0, a.cnt, [&](int r, int c) { return c < 39 ? embed_feature(sp[r], c, 6) : 0.f; });
+    for (int f = threadIdx.x; f < rows * 39; f += 256) {
+      const int r = f / 39, c = f - r * 39;
+      a.X4[(size_t)(i0 + r) * 256 + 217 + c] = embed_feature(sp[r], c, 6) / sqrt2;
+    }
   }
   // C0: tpose (0..2), gamma_4(bigdir) (3..29); 30..32 (gradient) belong to k_sdf_gamma_bwd
   for (int f = threadIdx.x; f < rows * 40; f += 256) {

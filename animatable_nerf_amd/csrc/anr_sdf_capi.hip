@@ -3,7 +3,8 @@
 // Sequence per render call (anisdf_pdf_network.py:156-223 under tpose_renderer.py:159-186):
 //   k_sdf_front (KNN keep mask, all samples) -> ordered compaction -> one host read of n'
 //   -> per batch of <= SDF_BATCH kept samples: prep, the residual MLP (split-bf16: one fused
-//      k_resd_b16 launch; exact fp32: 9 layer GEMMs), mid, 9 SDF GEMMs
+//      k_resd_b16 launch; exact fp32: 9 layer GEMMs), mid, the SDF network forward (split-bf16: one
+//      fused k_sdfnet_b16 launch writing the softplus outputs; exact fp32: 9 SDF GEMMs
 //      (softplus + its backward factor in the epilogue), 8 input-gradient GEMMs (reverse mode
 //      through the stored factors), gamma backward, 5 colour GEMMs, raw
 //   -> compositing (k_composite) -> msk_sdf lists.
@@ -31,7 +32,7 @@ constexpr long SDF_BATCH = 1L << ANR_SDF_BATCH_LOG2;  // kept samples per layer-
 constexpr size_t SDF_LIMG_BYTES = 16u << 20;  // split-bf16 layer-GEMM weight images (31 GEMMs, <= 384 KiB each)
 
 struct SLayout {
-  size_t counts, mask, chunk_min, ray_off, block_sum, list, knn, tbtab, wimg, fold, limg, rimg, resd_rows, grad_rows;
+  size_t counts, mask, chunk_min, ray_off, block_sum, list, knn, tbtab, wimg, fold, limg, rimg, simg, resd_rows, grad_rows;
   size_t min_sdf, flags, chunk_cnt, msk_sdf, msk_label;
   size_t ptb, Gr, Ha, Hb, Yr, Xs0, X4, D, Y8, Ga, Gb, Gc, gB, C0, Yc;
   long P;
@@ -59,7 +60,8 @@ SLayout slayout(int n_rays, int chunk) {
   L.wimg = take(SDF_WN_FLOATS * 4);
   L.fold = take(768 * 4);
   L.limg = take(SDF_LIMG_BYTES);
-  L.rimg = take(resd_image_bytes());
+  L.rimg = take(seq_image_bytes(ANR_L_RESD0, ANR_RESD_LAYERS));
+  L.simg = take(seq_image_bytes(ANR_L_SDF0, ANR_SDF_LAYERS));
   L.resd_rows = take(N * 3 * 4);
   L.grad_rows = take(N * 3 * 4);
   L.min_sdf = take(R * 4);
@@ -339,23 +341,35 @@ int anr_sdf_render_fwd(const anr_sdf_params* p, const anr_sdf_frame* f, const fl
   limg.base = ws + L.limg;
   limg.cap = SDF_LIMG_BYTES;
   const int cus = sdf_cus();
-  // split-bf16: the residual MLP as one fused launch per batch (anr_resd_b16.hip), its weight image
-  // packed once per call (ANR_SDF_RESD_FUSED=0 keeps the layer GEMMs, for A/B timing)
-  const char* rf = getenv("ANR_SDF_RESD_FUSED");
-  const bool resd_fused = o->precision == ANR_BF16X3 && !(rf && rf[0] == '0');
+  // split-bf16: the residual MLP and the SDF network forward as one fused launch per batch each
+  // (anr_resd_b16.hip), their weight images packed once per call (ANR_SDF_FUSED=0 keeps the layer
+  // GEMMs, for A/B timing)
+  const char* rf = getenv("ANR_SDF_FUSED");
+  const bool fused = o->precision == ANR_BF16X3 && !(rf && rf[0] == '0');
   unsigned char* rimg = (unsigned char*)(ws + L.rimg);
-  if (resd_fused) {
+  unsigned char* simg = (unsigned char*)(ws + L.simg);
+  if (fused) {
     PackArgs pa{};
     for (int l = 0; l < 8; ++l) {
       pa.t[l] = tp[SDF_RLIN0 + 2 * l];
-      pa.t[9 + l] = tp[SDF_RLIN0 + 2 * l + 1];
+      pa.t[9 + l] = l == 0 || l == 5 ? nullptr : tp[SDF_RLIN0 + 2 * l + 1];  // folded with the poses
     }
     pa.t[8] = tp[SDF_RFC_W];
     pa.t[17] = tp[SDF_RFC_B];
     pa.out = rimg;
-    const int nt = resd_pack_threads();
-    hipLaunchKernelGGL(k_pack_resd, dim3((nt + 255) / 256), dim3(256), 0, s, pa);
-    ANR_TRY(check_launch("k_pack_resd"));
+    int nt = seq_pack_threads(ANR_L_RESD0, ANR_RESD_LAYERS);
+    hipLaunchKernelGGL(k_pack_seq, dim3((nt + 255) / 256), dim3(256), 0, s, pa, ANR_L_RESD0, ANR_RESD_LAYERS, -1, 1.0f);
+    ANR_TRY(check_launch("k_pack_seq (resd)"));
+    PackArgs ps{};
+    for (int l = 0; l < 9; ++l) {
+      ps.t[l] = WN(l);
+      ps.t[9 + l] = tp[3 * l];
+    }
+    ps.out = simg;
+    nt = seq_pack_threads(ANR_L_SDF0, ANR_SDF_LAYERS);
+    hipLaunchKernelGGL(k_pack_seq, dim3((nt + 255) / 256), dim3(256), 0, s, ps, ANR_L_SDF0, ANR_SDF_LAYERS, 4,
+                       1.0f / sqrt2);
+    ANR_TRY(check_launch("k_pack_seq (sdf)"));
   }
   for (long b0 = 0; b0 < n; b0 += P) {
     const int cnt = (int)std::min<long>(P, n - b0);
@@ -364,7 +378,7 @@ int anr_sdf_render_fwd(const anr_sdf_params* p, const anr_sdf_frame* f, const fl
     a.ray_o = ray_o; a.ray_d = ray_d; a.near_ = near_; a.far_ = far_; a.t_rand = o->t_rand; a.chunk = o->chunk;
     a.R = f->R; a.Th = f->Th; a.A = f->A; a.bigA = f->big_A; a.weights = f->weights; a.knn = fa.knn;
     a.wimg = wimg; a.tbtab = tbtab;
-    a.ptb = F(L.ptb); a.Gr = resd_fused ? nullptr : F(L.Gr); a.Yr = F(L.Yr); a.Xs0 = F(L.Xs0); a.X4 = F(L.X4); a.C0 = F(L.C0);
+    a.ptb = F(L.ptb); a.Gr = fused ? nullptr : F(L.Gr); a.Yr = F(L.Yr); a.skip_sdf_in = fused ? 1 : 0; a.Xs0 = F(L.Xs0); a.X4 = F(L.X4); a.C0 = F(L.C0);
     a.D7 = Dl(7); a.G7 = Ga; a.Gc = Gc; a.gB = F(L.gB); a.Y8 = F(L.Y8); a.Yc = F(L.Yc); a.beta = beta;
     a.resd_rows = F(L.resd_rows); a.grad_rows = F(L.grad_rows); a.raw = raw; a.sdf = out->sdf;
     const dim3 pg((cnt + 255) / 256), pb(256);
@@ -373,12 +387,13 @@ int anr_sdf_render_fwd(const anr_sdf_params* p, const anr_sdf_frame* f, const fl
     // B2 + B3: LBS to the big pose, residual deformation MLP (poses folded into layers 0 / 5)
     hipLaunchKernelGGL(k_sdf_prep, pg, pb, 0, s, a);
     ANR_TRY(check_launch("k_sdf_prep"));
-    if (resd_fused) {
+    if (fused) {
       MlpArgs ra{};
       ra.wimg = rimg;
-      ra.bias = (const float*)(rimg + resd_wbytes());
+      ra.bias = (const float*)(rimg + seq_wbytes(ANR_L_RESD0, ANR_RESD_LAYERS));
       ra.fold = fold;
       ra.ptb = a.ptb;
+      ra.ptb_ld = 8;
       ra.yr = F(L.Yr);
       ra.n_rows = cnt;
       if (launch_resd(ra, cus, s) != 0) return fail(ANR_E_HIP, "k_resd_b16 launch failed");
@@ -409,6 +424,18 @@ int anr_sdf_render_fwd(const anr_sdf_params* p, const anr_sdf_frame* f, const fl
     // and the exact-fp32 precision keep the stored factors.
     const bool sph = g.x3 != 0;
     const float* hin = nullptr;
+    if (fused) {
+      MlpArgs sa{};
+      sa.wimg = simg;
+      sa.bias = (const float*)(simg + seq_wbytes(ANR_L_SDF0, ANR_SDF_LAYERS));
+      sa.ptb = a.C0;
+      sa.ptb_ld = 40;
+      for (int l = 0; l < 8; ++l) sa.sdf_h[l] = Dl(l);
+      sa.x4 = a.X4;
+      sa.y8 = F(L.Y8);
+      sa.n_rows = cnt;
+      if (launch_sdfnet(sa, cus, s) != 0) return fail(ANR_E_HIP, "k_sdfnet_b16 launch failed");
+    } else {
     auto sp_fwd = [&](int l, int K, float* pingpong) -> int {
       float* out = sph ? Dl(l) : pingpong;
       const int r = g.fwd_sp(out, WN(l), K, tp[3 * l], l == 0 ? a.Xs0 : hin, l == 0 ? 40 : 256, sph ? nullptr : Dl(l));
@@ -425,6 +452,7 @@ int anr_sdf_render_fwd(const anr_sdf_params* p, const anr_sdf_frame* f, const fl
     ANR_TRY(sp_fwd(6, 256, Ha));
     ANR_TRY(sp_fwd(7, 256, Hb));
     ANR_TRY(g.fwd(F(L.Y8), 264, 257, WN(8), 256, tp[24], hin, 256, 256, 0, false));
+    }
 
     // B4 gradient of sdf w.r.t. the canonical point (reverse mode through the stored factors / outputs)
     g.spd_h = sph ? 1 : 0;
