@@ -122,6 +122,11 @@ struct MlpArgs {
   float* sdf_h[8];
   float* x4;
   float* y8;
+  // sdf input-gradient program (k_sdfgrad_b16): reads sdf_h / x4 of the forward and lin8's row 0
+  // (w8row); writes the gamma_6 gradients of lin0 to gb ([n][40]) and of lin4's skip to gc[:, 217:256]
+  const float* w8row;
+  float* gb;
+  float* gc;
 };
 
 struct PrepArgs {
@@ -186,6 +191,8 @@ __global__ void k_pack_seq(PackArgs a, int L0, int nl, int sl, float sc);
 int seq_pack_threads(int L0, int nl);
 int launch_resd(const MlpArgs& a, int grid, hipStream_t s);
 int launch_sdfnet(const MlpArgs& a, int grid, hipStream_t s);
+int launch_sdfgrad(const MlpArgs& a, int grid, hipStream_t s);
+int launch_color(const MlpArgs& a, int grid, hipStream_t s);
 __global__ void k_pack_x6(PackArgs a);
 
 }  // namespace anr

@@ -15,8 +15,9 @@
 
 namespace anr {
 
-// SRC_EMB: gamma_10(x) (63); SRC_VEMB: gamma_4(dir) (27); SRC_EMB6: gamma_6(x) (39, the sdf_pdf SDF net)
-enum SrcKind { SRC_EMB = 0, SRC_ACT = 1, SRC_VEMB = 2, SRC_EMB6 = 3 };
+// SRC_EMB: gamma_10(x) (63); SRC_VEMB: gamma_4(dir) (27); SRC_EMB6: gamma_6(x) (39, the sdf_pdf SDF net);
+// SRC_G0 / SRC_G1: columns of a memory row (the sdf_pdf colour net's inputs; anr_mlp_body.h LayerIO)
+enum SrcKind { SRC_EMB = 0, SRC_ACT = 1, SRC_VEMB = 2, SRC_EMB6 = 3, SRC_G0 = 4, SRC_G1 = 5 };
 
 // A segment of a layer's K dimension: `ksteps` k-steps from one source; `col0` = first weight column;
 // `nact` (ACT segments, 0 = all): input neurons past it are padding (zero weight columns).
@@ -33,6 +34,7 @@ struct LayerDesc {
   int ob;         // out-blocks of 16 (incl. the tensor_w2 blocks)
   int nseg;
   Seg seg[2];
+  int trans = 0;  // packed as the transpose: element (row i, col k) = W[k * in_ch + i] (in_ch = W's row stride)
 };
 
 #define ANR_KSLICE 8  // k-steps per staged slice
@@ -124,8 +126,36 @@ __host__ __device__ constexpr LayerDesc sdfnet_desc(int l) {
                   : LayerDesc{l, 9 + l, -1, -1, 256, 0, 256, 16, 1, {{SRC_ACT, 64, 0}, {0, 0, 0}}};
 }
 
+// layers 50..57: the SDF network's input gradient d sdf / d x (SDFNetwork.gradient, autograd.grad of
+// anisdf_pdf_network.py:302-311) in reverse mode: entry r applies lin l = 7 - r transposed, W_l^T dz_l,
+// to dz_l = dh_l * sigmoid(100 z_l) (the factor recomputed from the stored h_l). lin4's transpose carries
+// the skip's 1/sqrt2 (packed scaled); lin3's has the 217 valid inputs; lin0's gives the 39 gamma_6
+// gradients. Same PackArgs as the forward (t[l] = weight of lin l; t[17] NULL: no biases).
+#define ANR_L_SREV0 50
+#define ANR_SREV_LAYERS 8
+__host__ __device__ constexpr LayerDesc sdfrev_desc(int r) {
+  return r == 4   ? LayerDesc{3, 17, -1, -1, 256, 0, 256, 16, 1, {{SRC_ACT, 56, 0, 217}, {0, 0, 0}}, 1}
+         : r == 7 ? LayerDesc{0, 17, -1, -1, 39, 0, 39, 3, 1, {{SRC_ACT, 64, 0}, {0, 0, 0}}, 1}
+                  : LayerDesc{7 - r, 17, -1, -1, 256, 0, 256, 16, 1, {{SRC_ACT, 64, 0}, {0, 0, 0}}, 1};
+}
+
+// layers 58..62: the sdf_pdf colour network (anisdf_pdf_network.py:469-545, ColorNetwork, mode idr):
+// lin0 on [points 3 || gamma_4(dir) 27 || normal 3] (a C0 row, SRC_G0) || feature 256 (lin8's, SRC_G1),
+// lin1, lin2, lin3 on [h2 || color_latent] (the latent folded into lin3's bias, k_sdf_fold), ReLU after
+// each, lin4 -> 3 logits. Weight-normed: t[l] = effective weight of lin l, t[9 + l] its bias.
+#define ANR_L_COL0 58
+#define ANR_COL_LAYERS 5
+__host__ __device__ constexpr LayerDesc color_desc(int l) {
+  return l == 0   ? LayerDesc{0, 9, -1, -1, 256, 0, 289, 16, 2, {{SRC_G0, 16, 0, 33}, {SRC_G1, 64, 33}}}
+         : l == 3 ? LayerDesc{3, 12, -1, -1, 256, 0, 384, 16, 1, {{SRC_ACT, 64, 0}, {0, 0, 0}}}
+         : l == 4 ? LayerDesc{4, 13, -1, -1, 3, 0, 256, 1, 1, {{SRC_ACT, 64, 0}, {0, 0, 0}}}
+                  : LayerDesc{l, 9 + l, -1, -1, 256, 0, 256, 16, 1, {{SRC_ACT, 64, 0}, {0, 0, 0}}};
+}
+
 __host__ __device__ constexpr LayerDesc layer_desc_all(int i) {
-  return i >= ANR_L_SDF0 ? sdfnet_desc(i - ANR_L_SDF0)
+  return i >= ANR_L_COL0 ? color_desc(i - ANR_L_COL0)
+       : i >= ANR_L_SREV0 ? sdfrev_desc(i - ANR_L_SREV0)
+       : i >= ANR_L_SDF0 ? sdfnet_desc(i - ANR_L_SDF0)
        : i >= ANR_L_RESD0 ? resd_desc(i - ANR_L_RESD0)
        : i < ANR_NUM_LAYERS ? layer_desc(i)
        : i == ANR_L_VIEW ? LayerDesc{23, 24, -1, -1, 128, 0, 283, 8, 2, {{SRC_ACT, 64, 0}, {SRC_VEMB, 8, 256}}}
@@ -267,6 +297,10 @@ __host__ __device__ inline int b16_col(const LayerDesc& d, int t, int h, int j) 
   const Seg sg = d.seg[s];
   if (sg.kind == SRC_ACT) {
     const int n = 32 * t + (j < 4 ? 4 * h + j : 16 + 4 * h + j - 4);
+    return sg.nact && n >= sg.nact ? -1 : sg.col0 + n;
+  }
+  if (sg.kind == SRC_G0 || sg.kind == SRC_G1) {  // a memory row, contiguous per lane half
+    const int n = 32 * t + 8 * h + j;
     return sg.nact && n >= sg.nact ? -1 : sg.col0 + n;
   }
   const int f = gamma_slot_feature(sg.ksteps / 8, sg.kind == SRC_EMB ? 10 : sg.kind == SRC_EMB6 ? 6 : 4, t, h, j);

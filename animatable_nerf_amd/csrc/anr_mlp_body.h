@@ -64,17 +64,25 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 //         mode 2 (bf16x6, fp32-level products) and the accurate libm paths of the exact kernel.
 //   V = 5 (the sdf_pdf SDF network forward, k_sdfnet_b16): entries 0..8 = layers 41..49
 //         (anr_layers.h sdfnet_desc), bf16x3, the image after the residual MLP's.
+//   V = 6 (the sdf_pdf colour network, k_color_b16): entries 0..4 = layers 58..62 (anr_layers.h
+//         color_desc), bf16x3, an image of its own; lin0 reads its inputs from memory rows.
+//   V = 7 (the sdf_pdf SDF network's input gradient, k_sdfgrad_b16): entries 0..7 = layers 50..57
+//         (anr_layers.h sdfrev_desc: lin7 .. lin0 transposed), bf16x3, an image of its own.
 //   V = 3 (the sdf_pdf residual deformation MLP, k_resd_b16): entries 0..8 = layers 32..40
 //         (anr_layers.h resd_desc), bf16x3, from the sdf render's own image (k_pack_resd).
 template <int V>
-__host__ __device__ constexpr int prog_len() { return V == 0 ? 30 : (V == 2 || V == 4) ? 28 : (V == 3 || V == 5) ? 9 : 18; }
+__host__ __device__ constexpr int prog_len() {
+  return V == 0 ? 30 : (V == 2 || V == 4) ? 28 : (V == 3 || V == 5) ? 9 : V == 7 ? 8 : V == 6 ? 5 : 18;
+}
 // programs whose weights are a packed layer sequence of their own (k_pack_seq), not the render image
 template <int V>
-__host__ __device__ constexpr bool prog_seq() { return V == 3 || V == 5; }
+__host__ __device__ constexpr bool prog_seq() { return V == 3 || V == 5 || V == 6 || V == 7; }
 template <int V>
 __host__ __device__ constexpr int prog_layer(int e) {
   return V == 3 ? ANR_L_RESD0 + e
          : V == 5 ? ANR_L_SDF0 + e
+         : V == 7 ? ANR_L_SREV0 + e
+         : V == 6 ? ANR_L_COL0 + e
          : e < 9 ? e
          : V == 0 ? e - 9
          : (V == 2 || V == 4) ? (e < 26 ? e - 9 : (e == 26 ? ANR_L_HEAD : ANR_L_RGB))
@@ -285,6 +293,9 @@ static_assert(prog_bias_off<4>(prog_len<4>()) <= ANR_BIAS_TABLE_FLOATS, "bias ta
 static_assert(prog_bias_off<3>(prog_len<3>()) == seq_bias_off(ANR_L_RESD0, ANR_RESD_LAYERS), "resd bias section");
 static_assert(prog_bias_off<5>(prog_len<5>()) == seq_bias_off(ANR_L_SDF0, ANR_SDF_LAYERS), "sdf bias section");
 static_assert(prog_bias_off<5>(prog_len<5>()) <= ANR_BIAS_TABLE_FLOATS, "bias table size (anr_layers.h)");
+static_assert(prog_bias_off<7>(prog_len<7>()) == seq_bias_off(ANR_L_SREV0, ANR_SREV_LAYERS), "sdf grad bias section");
+static_assert(prog_bias_off<6>(prog_len<6>()) == seq_bias_off(ANR_L_COL0, ANR_COL_LAYERS), "colour bias section");
+static_assert(prog_bias_off<7>(prog_len<7>()) + 256 <= ANR_BIAS_TABLE_FLOATS, "bias table + W8 row (anr_layers.h)");
 
 // Fill the bias table once per launch (before the first barrier of the slice stream). Sources:
 // the packed bias section, the novel_pose_bw copy for the pose pass (pose_boff), and the per-frame
@@ -300,8 +311,10 @@ __device__ __forceinline__ void fill_bias_table(const MlpArgs& a, float* __restr
     const float* src;
     if constexpr (V == 3) {  // sdf residual MLP: poses folded into layers 0 / 5 (k_sdf_fold)
       src = e == 0 ? a.fold : e == 5 ? a.fold + 256 : a.bias + toff;
-    } else if constexpr (V == 5) {  // sdf network: the image's bias section
+    } else if constexpr (V == 5 || V == 7) {  // sdf network (forward / gradient): the image's bias section
       src = a.bias + toff;
+    } else if constexpr (V == 6) {  // colour network: color_latent folded into lin3 (k_sdf_fold)
+      src = e == 3 ? a.fold + 512 : a.bias + toff;
     } else if constexpr (e < 9) {
       src = L == 0 ? a.fold + 0 : L == 5 ? a.fold + 512 : a.bias + a.pose_boff + boff;
     } else if constexpr (V != 1 && e < 18) {
@@ -336,9 +349,43 @@ __host__ __device__ constexpr int x3_issue_at(int G) {
   return a > m ? a : m;
 }
 
-template <bool B16, int V, int E, bool RELU_IN, int NIN, int NOUT>
+// Per-call memory operands of a streamed layer (the sdf programs): spst (SP_IN stores), fst / fscale
+// (FAC_IN factors), g0 / g1 (the rows that SRC_G0 / SRC_G1 segments read, k-step t lane half h taking
+// columns 32 t + 8 h .. + 7 of the segment).
+struct LayerIO {
+  float* spst = nullptr;
+  const float* fst = nullptr;
+  float fscale = 1.0f;
+  const float* g0 = nullptr;
+  const float* g1 = nullptr;
+};
+
+// softplus(beta = 100, threshold = 20) as log2(1 + 2^(100 x log2 e)) ln2 / 100 on the hardware exp2 /
+// log2 (~1 ulp each): 2 transcendentals + 5 VALU instead of the ~25 of k_lgemm's libm-grade epilogue
+// (fast_exp / fast_log1p). Its h feeds a hi/lo bf16 split (~2^-16 relative) and the reverse pass's
+// factor 1 - exp(-100 h); where 1 + e rounds (e < ~1e-3), h and that factor are < 1e-5 and their
+// absolute error < 1e-9. The SDF outputs stay within tests/test_gpu_sdf.py's 1e-4 / 2e-4.
+__device__ __forceinline__ float softplus100(float x) {
+  const float e = __builtin_amdgcn_exp2f(x * 144.269504f);
+  const float h = __builtin_amdgcn_logf(1.0f + e) * 0.00693147181f;
+  return x * 100.f > 20.f ? x : h;
+}
+
+// SP_IN (the sdf network, V = 5): the previous layer's softplus(beta = 100) is applied in this layer's
+// split like RELU_IN (its VALU work beside this layer's MFMAs), and the softplus outputs h of the
+// k-step's 8 input neurons are stored to spst (the row's base; nothing when NULL): SP_IN 1 as h,
+// SP_IN 2 as h / sqrt2 for input neurons < 217 (lin3's outputs into X4).
+// FAC_IN (the SDF network's input gradient, V = 7): the input gradient dh of this layer's k-step is
+// multiplied by the softplus-backward factor 1 - exp(-100 h) (softplus_factor_h) of the forward's
+// stored outputs h (row fst, times fscale: lin3's X4 holds h / sqrt2), loaded two k-steps ahead so
+// the loads' waits never reach the newest weight-slice DMA; FAC_IN 2 zeroes inputs >= 217 (lin3).
+template <bool B16, int V, int E, bool RELU_IN, int SP_IN, int FAC_IN, int NIN, int NOUT>
 __device__ __forceinline__ void layer_x3(Pipe& p, const f32x4 (&in)[NIN], const float (&emb)[16], const float (&vemb)[8],
-                                         f32x4 (&out)[NOUT], const float* __restrict__ sbias, int g, int lane) {
+                                         f32x4 (&out)[NOUT], const float* __restrict__ sbias, int g, int lane,
+                                         const LayerIO& io) {
+  float* __restrict__ spst = io.spst;
+  const float* __restrict__ fst = io.fst;
+  const float fscale = io.fscale;
   constexpr int L = prog_layer<V>(E);
   constexpr LayerDesc D = layer_desc_all(L);
   constexpr int KS = ks32(L);
@@ -350,6 +397,14 @@ __device__ __forceinline__ void layer_x3(Pipe& p, const f32x4 (&in)[NIN], const 
   constexpr int BOFF = prog_bias_off<V>(E);
   static_assert(b16_tail_ob(L) == 0, "streamed x3 layers have no tail slice");
   // the B operand of k-step t: 8 inputs (ReLU of the previous layer applied here), hi/lo split
+  f32x4 hv[2][2];  // FAC_IN: stored h of k-steps t (slot t & 1), two k-steps ahead
+  auto load_h = [&](auto tc) {
+    constexpr int t = decltype(tc)::value;
+    if constexpr (FAC_IN != 0 && t < KS) {
+      hv[t & 1][0] = *(const f32x4*)(fst + 32 * t + 4 * g);
+      hv[t & 1][1] = *(const f32x4*)(fst + 32 * t + 16 + 4 * g);
+    }
+  };
   auto split_k = [&](auto tc, bf16x8& bh, bf16x8& bl) {
     constexpr int t = decltype(tc)::value;
     constexpr int seg = t < K0 ? 0 : 1;
@@ -362,11 +417,57 @@ __device__ __forceinline__ void layer_x3(Pipe& p, const f32x4 (&in)[NIN], const 
     } else if constexpr (kind == SRC_VEMB) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) x[j] = vemb[j];
+    } else if constexpr (kind == SRC_G0 || kind == SRC_G1) {
+      // 8 consecutive columns of a memory row (the colour net's inputs); past nact: zero, not loaded
+      constexpr int NA = D.seg[seg].nact;
+      const int c0 = 32 * ts + 8 * g;
+      const float* gp = (kind == SRC_G0 ? io.g0 : io.g1) + c0;
+      f32x4 u = {0.f, 0.f, 0.f, 0.f}, w = {0.f, 0.f, 0.f, 0.f};
+      if (NA == 0 || c0 < NA) {
+        u = *(const f32x4*)gp;
+        w = *(const f32x4*)(gp + 4);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        x[j] = NA == 0 || c0 + j < NA ? u[j] : 0.0f;
+        x[4 + j] = NA == 0 || c0 + 4 + j < NA ? w[j] : 0.0f;
+      }
     } else {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         x[j] = RELU_IN ? fmaxf(in[2 * ts][j], 0.0f) : in[2 * ts][j];
         x[4 + j] = RELU_IN ? fmaxf(in[2 * ts + 1][j], 0.0f) : in[2 * ts + 1][j];
+      }
+      if constexpr (FAC_IN != 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          x[j] = x[j] * softplus_factor_h(hv[t & 1][0][j] * fscale);
+          x[4 + j] = x[4 + j] * softplus_factor_h(hv[t & 1][1][j] * fscale);
+          if constexpr (FAC_IN == 2) {  // lin3: 217 inputs; the rest are gamma gradients (and X4's padding)
+            x[j] = 32 * ts + 4 * g + j < 217 ? x[j] : 0.0f;
+            x[4 + j] = 32 * ts + 16 + 4 * g + j < 217 ? x[4 + j] : 0.0f;
+          }
+        }
+        load_h(std::integral_constant<int, t + 2>{});
+      }
+      if constexpr (SP_IN != 0) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x[j] = softplus100(x[j]);
+        if (spst) {  // neurons 32 ts + 4 g + (0..3) and 32 ts + 16 + 4 g + (0..3)
+          float* d = spst + 32 * ts + 4 * g;
+          if constexpr (SP_IN == 1) {
+            *(f32x4*)d = f32x4{x[0], x[1], x[2], x[3]};
+            *(f32x4*)(d + 16) = f32x4{x[4], x[5], x[6], x[7]};
+          } else {
+            const float sqrt2 = 1.41421356237309515f;
+            const int c = 32 * ts + 4 * g;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              if (c + j < 217) d[j] = x[j] / sqrt2;
+              if (c + 16 + j < 217) d[16 + j] = x[4 + j] / sqrt2;
+            }
+          }
+        }
       }
     }
     split8(x, bh, bl);
@@ -382,6 +483,8 @@ __device__ __forceinline__ void layer_x3(Pipe& p, const f32x4 (&in)[NIN], const 
     constexpr int o = decltype(ob)::value;
     out[o] = *(const f32x4*)(sbias + BOFF + o * 16 + 4 * g);
   });
+  load_h(std::integral_constant<int, 0>{});
+  load_h(std::integral_constant<int, 1>{});
   split_k(std::integral_constant<int, 0>{}, bh[0], bl[0]);
   static_for<0, PF>([&](auto gg) {
     constexpr int G = decltype(gg)::value;
@@ -447,15 +550,18 @@ __device__ __forceinline__ void layer_x3(Pipe& p, const f32x4 (&in)[NIN], const 
   });
 }
 
-template <bool B16, int V, int E, bool RELU, bool RELU_IN = false, int NIN, int NOUT>
+template <bool B16, int V, int E, bool RELU, bool RELU_IN = false, int SP_IN = 0, int FAC_IN = 0, int NIN, int NOUT>
 __device__ __forceinline__ void layer(Pipe& p, const f32x4 (&in)[NIN], const float (&emb)[16], const float (&vemb)[8],
-                                      f32x4 (&out)[NOUT], const float* __restrict__ sbias, int g, int lane) {
+                                      f32x4 (&out)[NOUT], const float* __restrict__ sbias, int g, int lane,
+                                      const LayerIO& io = LayerIO{}) {
   constexpr int L = prog_layer<V>(E);
   constexpr LayerDesc D = layer_desc_all(L);
   static_assert(NOUT >= D.ob, "output array too small");
+  static_assert((SP_IN == 0 && FAC_IN == 0) || (prog_mode<B16, V>(E) == 1 && x3_stream_layer<L>()),
+                "SP_IN / FAC_IN on streamed layers only");
   if constexpr (prog_mode<B16, V>(E) == 1 && x3_stream_layer<L>()) {
     // output ReLU deferred to the consumer's split (RELU_IN of the next layer)
-    layer_x3<B16, V, E, RELU_IN>(p, in, emb, vemb, out, sbias, g, lane);
+    layer_x3<B16, V, E, RELU_IN, SP_IN, FAC_IN>(p, in, emb, vemb, out, sbias, g, lane, io);
     return;
   }
   // accumulators start at the bias; read right after the layer's first slice barrier, so the
@@ -1065,18 +1171,13 @@ __device__ __forceinline__ void resd_body(const MlpArgs& a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the last (unused) prefetch
 }
 
-// softplus(beta = 100, threshold = 20) of the accumulators in place, as k_lgemm's epilogue computes it
+// softplus(beta = 100, threshold = 20) of the accumulators in place
 template <int NOB>
 __device__ __forceinline__ void softplus_regs(f32x4 (&v)[17]) {
   static_for<0, NOB>([&](auto ob) {
     constexpr int o = decltype(ob)::value;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float x = v[o][r];
-      const float z = x * 100.f;
-      const float ez = fast_exp(z);
-      v[o][r] = z > 20.f ? x : fast_log1p(ez) * 0.01f;
-    }
+    for (int r = 0; r < 4; ++r) v[o][r] = softplus100(v[o][r]);
   });
 }
 
@@ -1084,7 +1185,8 @@ __device__ __forceinline__ void softplus_regs(f32x4 (&v)[17]) {
 // sample of one batch, on chip — gamma_6 of the canonical point, lin0..lin7 with softplus, the skip
 // [h3 || gamma_6] / sqrt2 at lin4 (the 1/sqrt2 is in lin4's packed weights), lin8. What the reverse
 // pass (the input gradient) and the colour net read is written once: every softplus output h (lin3's
-// as h / sqrt2 in X4, the layout of the layer-GEMM path) and lin8's [sdf || feature].
+// as h / sqrt2 in X4, the layout of the layer-GEMM path) and lin8's sdf (Y8 column 0) and feature
+// (Y8 columns 8..263: 16-B aligned for k_color_b16's row loads).
 __device__ __forceinline__ void sdfnet_body(const MlpArgs& a) {
   constexpr int V = 5;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1122,53 +1224,170 @@ __device__ __forceinline__ void sdfnet_body(const MlpArgs& a) {
         *(f32x4*)(d + 16 * o) = v[o];
       });
     };
+    // each layer's softplus runs in the next layer's split (SP_IN), which also stores its h
+    float* const hst[8] = {valid ? a.sdf_h[0] + row * 256 : nullptr, valid ? a.sdf_h[1] + row * 256 : nullptr,
+                           valid ? a.sdf_h[2] + row * 256 : nullptr, valid ? a.x4 + row * 256 : nullptr,
+                           valid ? a.sdf_h[4] + row * 256 : nullptr, valid ? a.sdf_h[5] + row * 256 : nullptr,
+                           valid ? a.sdf_h[6] + row * 256 : nullptr, nullptr};
     f32x4 dummy[1];
     layer<true, V, 0, false>(p, dummy, emb, vemb, A, sb, g, lane);
-    softplus_regs<16>(A);
-    store_h(A, a.sdf_h[0]);
-    layer<true, V, 1, false>(p, A, emb, vemb, B, sb, g, lane);
-    softplus_regs<16>(B);
-    store_h(B, a.sdf_h[1]);
-    layer<true, V, 2, false>(p, B, emb, vemb, A, sb, g, lane);
-    softplus_regs<16>(A);
-    store_h(A, a.sdf_h[2]);
-    layer<true, V, 3, false>(p, A, emb, vemb, B, sb, g, lane);  // 217 outputs (14 out-blocks)
-    softplus_regs<14>(B);
-    if (valid) {
-      float* d = a.x4 + row * 256;
-      const float sqrt2 = 1.41421356237309515f;
-      static_for<0, 14>([&](auto ob) {
+    auto st = [&](int i) { return LayerIO{hst[i]}; };
+    layer<true, V, 1, false, false, 1>(p, A, emb, vemb, B, sb, g, lane, st(0));
+    layer<true, V, 2, false, false, 1>(p, B, emb, vemb, A, sb, g, lane, st(1));
+    layer<true, V, 3, false, false, 1>(p, A, emb, vemb, B, sb, g, lane, st(2));  // 217 outputs (14 out-blocks)
+    // [h3 || gamma_6] (1/sqrt2 in the weights); h3 / sqrt2 -> X4[:, :217]
+    layer<true, V, 4, false, false, 2>(p, B, emb, vemb, A, sb, g, lane, st(3));
+    layer<true, V, 5, false, false, 1>(p, A, emb, vemb, B, sb, g, lane, st(4));
+    layer<true, V, 6, false, false, 1>(p, B, emb, vemb, A, sb, g, lane, st(5));
+    layer<true, V, 7, false, false, 1>(p, A, emb, vemb, B, sb, g, lane, st(6));
+    softplus_regs<16>(B);  // lin8 (a tail-slice layer, not streamed) reads h7 as is
+    store_h(B, a.sdf_h[7]);
+    layer<true, V, 8, false>(p, B, emb, vemb, A, sb, g, lane);  // [sdf || feature], no activation
+    if (valid) {  // sdf (neuron 0) to column 0, the feature (neurons 1..256) to columns 8..263
+      float* d = a.y8 + row * 264;
+      // lane holds neurons 16 o + 4 g + r: neuron m > 0 -> column m + 7
+      static_for<0, 17>([&](auto ob) {
         constexpr int o = decltype(ob)::value;
-        const int c = 16 * o + 4 * g;
-        if (c + 4 <= 217) {
-          *(f32x4*)(d + c) = f32x4{B[o][0] / sqrt2, B[o][1] / sqrt2, B[o][2] / sqrt2, B[o][3] / sqrt2};
-        } else {
 #pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (c + r < 217) d[c + r] = B[o][r] / sqrt2;
+        for (int r = 0; r < 4; ++r) {
+          const int m = 16 * o + 4 * g + r;
+          if (m == 0) d[0] = A[o][r];
+          else if (m <= 256) d[m + 7] = A[o][r];
         }
       });
     }
-    layer<true, V, 4, false>(p, B, emb, vemb, A, sb, g, lane);  // [h3 || gamma_6] (1/sqrt2 in the weights)
-    softplus_regs<16>(A);
-    store_h(A, a.sdf_h[4]);
-    layer<true, V, 5, false>(p, A, emb, vemb, B, sb, g, lane);
-    softplus_regs<16>(B);
-    store_h(B, a.sdf_h[5]);
-    layer<true, V, 6, false>(p, B, emb, vemb, A, sb, g, lane);
-    softplus_regs<16>(A);
-    store_h(A, a.sdf_h[6]);
-    layer<true, V, 7, false>(p, A, emb, vemb, B, sb, g, lane);
-    softplus_regs<16>(B);
-    store_h(B, a.sdf_h[7]);
-    layer<true, V, 8, false>(p, B, emb, vemb, A, sb, g, lane);  // [sdf || feature], no activation
-    if (valid) {
-      float* d = a.y8 + row * 264 + 4 * g;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the last (unused) prefetch
+}
+
+// sdf_pdf SDF network input gradient (V = 7): d sdf / d x (the autograd.grad of anisdf_pdf_network.py
+// :302-311 through SDFNetwork.forward) per kept sample of one batch, on chip. The gradient vector is the
+// MFMA B operand, lin7^T .. lin0^T the weights; each layer's input is multiplied by the softplus-backward
+// factor recomputed from the forward's stored h (FAC_IN). Writes the gamma_6 gradients (lin0's, and
+// the skip part of lin4's) for k_sdf_gamma_bwd. Replaces 8 reverse layer GEMMs over HBM activations.
+__device__ __forceinline__ void sdfgrad_body(const MlpArgs& a) {
+  constexpr int V = 7;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4;
+  const int pl = lane & 15;
+  float* sb = (float*)smem;  // bias table (zeros), then lin8's row 0
+  fill_bias_table<V>(a, sb, tid);
+  float* sw8 = sb + prog_bias_off<V>(prog_len<V>());
+  for (int i = tid; i < 256; i += 512) sw8[i] = a.w8row[i];
+  const int n = a.n_rows;
+  const int ntiles = (n + 127) / 128;
+  if ((int)blockIdx.x >= ntiles) return;  // uniform per workgroup, before any LDS-DMA
+
+  Pipe p{smem + mlp_ring_off(), mlp_slice_max<true>(), mlp_nbuf<true>(), a.wimg, 0, wave, lane, 0};
+  p.template start<true, V>();  // its barrier also publishes sw8
+
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int idx = tile * 128 + wave * 16 + pl;
+    const bool valid = idx < n;
+    const size_t row = (size_t)(valid ? idx : n - 1);
+    float emb[16], vemb[8];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) emb[i] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) vemb[i] = 0.f;
+    f32x4 A[17], B[17];
+    // dz7 = W8[0] * sigmoid(100 z7) (lin8's sdf row; the softplus factor from h7)
+    {
+      const float* h7 = a.sdf_h[7] + row * 256 + 4 * g;
       static_for<0, 16>([&](auto ob) {
         constexpr int o = decltype(ob)::value;
-        *(f32x4*)(d + 16 * o) = A[o];
+        const f32x4 hv = *(const f32x4*)(h7 + 16 * o);
+        const f32x4 wv = *(const f32x4*)(sw8 + 16 * o + 4 * g);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) A[o][r] = wv[r] * softplus_factor_h(hv[r]);
       });
-      if (g == 0) a.y8[row * 264 + 256] = A[16][0];
+    }
+    const float sqrt2 = 1.41421356237309515f;
+    layer<true, V, 0, false>(p, A, emb, vemb, B, sb, g, lane);  // dh6 = W7^T dz7
+    layer<true, V, 1, false, false, 0, 1>(p, B, emb, vemb, A, sb, g, lane, LayerIO{nullptr, a.sdf_h[6] + row * 256});
+    layer<true, V, 2, false, false, 0, 1>(p, A, emb, vemb, B, sb, g, lane, LayerIO{nullptr, a.sdf_h[5] + row * 256});
+    // d [h3 || gamma_6] = W4^T dz4 / sqrt2 (the 1/sqrt2 packed into the weights)
+    layer<true, V, 3, false, false, 0, 1>(p, B, emb, vemb, A, sb, g, lane, LayerIO{nullptr, a.sdf_h[4] + row * 256});
+    if (valid) {  // the skip's gamma_6 gradients: neurons 217..255
+      float* d = a.gc + row * 256;
+      static_for<13, 16>([&](auto ob) {
+        constexpr int o = decltype(ob)::value;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = 16 * o + 4 * g + r;
+          if (c >= 217) d[c] = A[o][r];
+        }
+      });
+    }
+    // lin3's inputs < 217, factor from X4 = h3 / sqrt2
+    layer<true, V, 4, false, false, 0, 2>(p, A, emb, vemb, B, sb, g, lane, LayerIO{nullptr, a.x4 + row * 256, sqrt2});
+    layer<true, V, 5, false, false, 0, 1>(p, B, emb, vemb, A, sb, g, lane, LayerIO{nullptr, a.sdf_h[2] + row * 256});
+    layer<true, V, 6, false, false, 0, 1>(p, A, emb, vemb, B, sb, g, lane, LayerIO{nullptr, a.sdf_h[1] + row * 256});
+    layer<true, V, 7, false, false, 0, 1>(p, B, emb, vemb, A, sb, g, lane, LayerIO{nullptr, a.sdf_h[0] + row * 256});
+    if (valid) {  // lin0's gamma_6 gradients (39)
+      float* d = a.gb + row * 40;
+      static_for<0, 3>([&](auto ob) {
+        constexpr int o = decltype(ob)::value;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = 16 * o + 4 * g + r;
+          if (c < 39) d[c] = A[o][r];
+        }
+      });
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the last (unused) prefetch
+}
+
+// sdf_pdf colour network (V = 6): ColorNetwork.forward (anisdf_pdf_network.py:516-545) per kept sample
+// of one batch, on chip: lin0 reads [points, gamma_4(dir), normal] from the sample's C0 row and the
+// SDF net's feature from its Y8 row (columns 8..263, written there by k_sdfnet_b16), then
+// lin1..lin3 (ReLU deferred into the next split, the colour latent folded into lin3's bias), lin4's
+// three logits to yr ([n][4]); k_sdf_raw applies the sigmoid.
+__device__ __forceinline__ void color_body(const MlpArgs& a) {
+  constexpr int V = 6;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4;
+  const int pl = lane & 15;
+  float* sb = (float*)smem;
+  fill_bias_table<V>(a, sb, tid);
+  const int n = a.n_rows;
+  const int ntiles = (n + 127) / 128;
+  if ((int)blockIdx.x >= ntiles) return;  // uniform per workgroup, before any LDS-DMA
+
+  Pipe p{smem + mlp_ring_off(), mlp_slice_max<true>(), mlp_nbuf<true>(), a.wimg, 0, wave, lane, 0};
+  p.template start<true, V>();
+
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int idx = tile * 128 + wave * 16 + pl;
+    const bool valid = idx < n;
+    const size_t row = (size_t)(valid ? idx : n - 1);
+    float emb[16], vemb[8];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) emb[i] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) vemb[i] = 0.f;
+    f32x4 A[17], B[17];
+    LayerIO io{};
+    io.g0 = a.ptb + row * a.ptb_ld;
+    io.g1 = a.y8 + row * 264 + 8;
+    f32x4 dummy[1];
+    layer<true, V, 0, true>(p, dummy, emb, vemb, A, sb, g, lane, io);
+    layer<true, V, 1, true, true>(p, A, emb, vemb, B, sb, g, lane);
+    layer<true, V, 2, true, true>(p, B, emb, vemb, A, sb, g, lane);
+    layer<true, V, 3, true, true>(p, A, emb, vemb, B, sb, g, lane);
+    layer<true, V, 4, false, true>(p, B, emb, vemb, A, sb, g, lane);
+    if (valid && g == 0) {
+      float* y = a.yr + row * 4;
+      y[0] = A[0][0];
+      y[1] = A[0][1];
+      y[2] = A[0][2];
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the last (unused) prefetch

@@ -109,7 +109,8 @@ __global__ void k_pack_b16(PackArgs a) {
 // A layer sequence L0 .. L0 + nl - 1 of the layer table as its own bf16x3 image (the sdf render's
 // residual MLP, layers 32..40, and SDF network, 41..49): k_pack_b16's fragments (main out-blocks,
 // then tail blocks) from byte 0 of `a.out`, then the biases padded to ob x 16 per layer. Layer
-// L0 + sl's weights are multiplied by `sc` (lin4's 1/sqrt2 of its skip concatenation).
+// L0 + sl's weights are multiplied by `sc` (lin4's 1/sqrt2 of its skip concatenation). Layers with
+// LayerDesc::trans are packed transposed (the SDF network's input-gradient pass).
 __global__ void k_pack_seq(PackArgs a, int L0, int nl, int sl, float sc) {
   const int u = blockIdx.x * blockDim.x + threadIdx.x;
   const int nfrag = seq_wbytes(L0, nl) / 32;
@@ -140,7 +141,8 @@ __global__ void k_pack_seq(PackArgs a, int L0, int nl, int sl, float sc) {
   for (int j = 0; j < 8; ++j) {
     const int col = b16_col(d, t, h, j);
     float v = 0.0f;
-    if (col >= 0 && row < d.nout && a.t[d.tensor_w] != nullptr) v = a.t[d.tensor_w][(size_t)row * d.in_ch + col] * f;
+    if (col >= 0 && row < d.nout && a.t[d.tensor_w] != nullptr)
+      v = a.t[d.tensor_w][d.trans ? (size_t)col * d.in_ch + row : (size_t)row * d.in_ch + col] * f;
     hi[j] = bf16_rne(v);
     lo[j] = bf16_rne(v - __uint_as_float((uint32_t)hi[j] << 16));
   }

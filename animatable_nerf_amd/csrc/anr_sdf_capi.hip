@@ -4,7 +4,8 @@
 //   k_sdf_front (KNN keep mask, all samples) -> ordered compaction -> one host read of n'
 //   -> per batch of <= SDF_BATCH kept samples: prep, the residual MLP (split-bf16: one fused
 //      k_resd_b16 launch; exact fp32: 9 layer GEMMs), mid, the SDF network forward (split-bf16: one
-//      fused k_sdfnet_b16 launch writing the softplus outputs; exact fp32: 9 SDF GEMMs
+//      fused k_sdfnet_b16 launch writing the softplus outputs, and its input gradient as one fused
+//      k_sdfgrad_b16 launch, the colour net as one fused k_color_b16 launch; exact fp32: 9 SDF GEMMs
 //      (softplus + its backward factor in the epilogue), 8 input-gradient GEMMs (reverse mode
 //      through the stored factors), gamma backward, 5 colour GEMMs, raw
 //   -> compositing (k_composite) -> msk_sdf lists.
@@ -32,7 +33,7 @@ constexpr long SDF_BATCH = 1L << ANR_SDF_BATCH_LOG2;  // kept samples per layer-
 constexpr size_t SDF_LIMG_BYTES = 16u << 20;  // split-bf16 layer-GEMM weight images (31 GEMMs, <= 384 KiB each)
 
 struct SLayout {
-  size_t counts, mask, chunk_min, ray_off, block_sum, list, knn, tbtab, wimg, fold, limg, rimg, simg, resd_rows, grad_rows;
+  size_t counts, mask, chunk_min, ray_off, block_sum, list, knn, tbtab, wimg, fold, limg, rimg, simg, gimg, cimg, resd_rows, grad_rows;
   size_t min_sdf, flags, chunk_cnt, msk_sdf, msk_label;
   size_t ptb, Gr, Ha, Hb, Yr, Xs0, X4, D, Y8, Ga, Gb, Gc, gB, C0, Yc;
   long P;
@@ -62,6 +63,8 @@ SLayout slayout(int n_rays, int chunk) {
   L.limg = take(SDF_LIMG_BYTES);
   L.rimg = take(seq_image_bytes(ANR_L_RESD0, ANR_RESD_LAYERS));
   L.simg = take(seq_image_bytes(ANR_L_SDF0, ANR_SDF_LAYERS));
+  L.gimg = take(seq_image_bytes(ANR_L_SREV0, ANR_SREV_LAYERS));
+  L.cimg = take(seq_image_bytes(ANR_L_COL0, ANR_COL_LAYERS));
   L.resd_rows = take(N * 3 * 4);
   L.grad_rows = take(N * 3 * 4);
   L.min_sdf = take(R * 4);
@@ -348,6 +351,8 @@ int anr_sdf_render_fwd(const anr_sdf_params* p, const anr_sdf_frame* f, const fl
   const bool fused = o->precision == ANR_BF16X3 && !(rf && rf[0] == '0');
   unsigned char* rimg = (unsigned char*)(ws + L.rimg);
   unsigned char* simg = (unsigned char*)(ws + L.simg);
+  unsigned char* gimg = (unsigned char*)(ws + L.gimg);
+  unsigned char* cimg = (unsigned char*)(ws + L.cimg);
   if (fused) {
     PackArgs pa{};
     for (int l = 0; l < 8; ++l) {
@@ -370,6 +375,21 @@ int anr_sdf_render_fwd(const anr_sdf_params* p, const anr_sdf_frame* f, const fl
     hipLaunchKernelGGL(k_pack_seq, dim3((nt + 255) / 256), dim3(256), 0, s, ps, ANR_L_SDF0, ANR_SDF_LAYERS, 4,
                        1.0f / sqrt2);
     ANR_TRY(check_launch("k_pack_seq (sdf)"));
+    for (int l = 9; l < 18; ++l) ps.t[l] = nullptr;  // no biases in the gradient pass
+    ps.out = gimg;  // lin7 .. lin0 transposed, lin4's with the skip's 1/sqrt2 (entry 3)
+    nt = seq_pack_threads(ANR_L_SREV0, ANR_SREV_LAYERS);
+    hipLaunchKernelGGL(k_pack_seq, dim3((nt + 255) / 256), dim3(256), 0, s, ps, ANR_L_SREV0, ANR_SREV_LAYERS, 3,
+                       1.0f / sqrt2);
+    ANR_TRY(check_launch("k_pack_seq (sdf gradient)"));
+    PackArgs pc{};
+    for (int l = 0; l < 5; ++l) {
+      pc.t[l] = WN(9 + l);
+      pc.t[9 + l] = l == 3 ? nullptr : tp[SDF_CLIN0 + 3 * l];  // lin3's bias: the latent fold
+    }
+    pc.out = cimg;
+    nt = seq_pack_threads(ANR_L_COL0, ANR_COL_LAYERS);
+    hipLaunchKernelGGL(k_pack_seq, dim3((nt + 255) / 256), dim3(256), 0, s, pc, ANR_L_COL0, ANR_COL_LAYERS, -1, 1.0f);
+    ANR_TRY(check_launch("k_pack_seq (colour)"));
   }
   for (long b0 = 0; b0 < n; b0 += P) {
     const int cnt = (int)std::min<long>(P, n - b0);
@@ -455,6 +475,18 @@ int anr_sdf_render_fwd(const anr_sdf_params* p, const anr_sdf_frame* f, const fl
     }
 
     // B4 gradient of sdf w.r.t. the canonical point (reverse mode through the stored factors / outputs)
+    if (fused) {
+      MlpArgs ga{};
+      ga.wimg = gimg;
+      ga.bias = (const float*)(gimg + seq_wbytes(ANR_L_SREV0, ANR_SREV_LAYERS));
+      for (int l = 0; l < 8; ++l) ga.sdf_h[l] = Dl(l);
+      ga.x4 = a.X4;
+      ga.w8row = WN(8);
+      ga.gb = F(L.gB);
+      ga.gc = Gc;
+      ga.n_rows = cnt;
+      if (launch_sdfgrad(ga, cus, s) != 0) return fail(ANR_E_HIP, "k_sdfgrad_b16 launch failed");
+    } else {
     g.spd_h = sph ? 1 : 0;
     a.d7_h = sph ? 1 : 0;
     if (g.bwd_top(Gb, 256, 256, Dl(7), WN(8), 256, WN(7), 256, Dl(6), 256)) {
@@ -478,10 +510,23 @@ int anr_sdf_render_fwd(const anr_sdf_params* p, const anr_sdf_frame* f, const fl
     ANR_TRY(g.bwd(Ga, 256, 256, Gb, 256, 256, WN(1), 256, Dl(0), 256));
     g.spd_h = 0;
     ANR_TRY(g.bwd(F(L.gB), 40, 39, Ga, 256, 256, WN(0), 39, nullptr, 0));
+    }
     hipLaunchKernelGGL(k_sdf_gamma_bwd, pg, pb, 0, s, a);
     ANR_TRY(check_launch("k_sdf_gamma_bwd"));
 
     // B6 colour network (color_latent folded into lin3)
+    if (fused) {
+      MlpArgs ca{};
+      ca.wimg = cimg;
+      ca.bias = (const float*)(cimg + seq_wbytes(ANR_L_COL0, ANR_COL_LAYERS));
+      ca.fold = fold;
+      ca.ptb = a.C0;
+      ca.ptb_ld = 40;
+      ca.y8 = F(L.Y8);
+      ca.yr = F(L.Yc);
+      ca.n_rows = cnt;
+      if (launch_color(ca, cus, s) != 0) return fail(ANR_E_HIP, "k_color_b16 launch failed");
+    } else {
     ANR_TRY(g.fwd(Ha, 256, 256, WN(9), 289, tp[29], a.C0, 40, 33, 0, true, nullptr, 0.f, false, F(L.Y8) + 1, 264, 256, 33));
     ANR_TRY(g.fwd(Hb, 256, 256, WN(10), 256, tp[32], Ha, 256, 256, 0, true));
     ANR_TRY(g.fwd(Ha, 256, 256, WN(11), 256, tp[35], Hb, 256, 256, 0, true));
@@ -490,6 +535,7 @@ int anr_sdf_render_fwd(const anr_sdf_params* p, const anr_sdf_frame* f, const fl
     } else {
       ANR_TRY(g.fwd(Hb, 256, 256, WN(12), 384, fold + 512, Ha, 256, 256, 0, true));
       ANR_TRY(g.fwd(F(L.Yc), 4, 3, WN(13), 256, tp[41], Hb, 256, 256, 0, false));
+    }
     }
 
     // B5 density, raw assembly with the (widened) tbounds mask
