@@ -1225,13 +1225,10 @@ __device__ __forceinline__ void sdfnet_body(const MlpArgs& a) {
       });
     };
     // each layer's softplus runs in the next layer's split (SP_IN), which also stores its h
-    float* const hst[8] = {valid ? a.sdf_h[0] + row * 256 : nullptr, valid ? a.sdf_h[1] + row * 256 : nullptr,
-                           valid ? a.sdf_h[2] + row * 256 : nullptr, valid ? a.x4 + row * 256 : nullptr,
-                           valid ? a.sdf_h[4] + row * 256 : nullptr, valid ? a.sdf_h[5] + row * 256 : nullptr,
-                           valid ? a.sdf_h[6] + row * 256 : nullptr, nullptr};
+    // store targets formed at each call (a per-tile array of row pointers costs 16 VGPRs for the tile)
+    auto st = [&](int i) { return LayerIO{valid ? (i == 3 ? a.x4 : a.sdf_h[i]) + row * 256 : nullptr}; };
     f32x4 dummy[1];
     layer<true, V, 0, false>(p, dummy, emb, vemb, A, sb, g, lane);
-    auto st = [&](int i) { return LayerIO{hst[i]}; };
     layer<true, V, 1, false, false, 1>(p, A, emb, vemb, B, sb, g, lane, st(0));
     layer<true, V, 2, false, false, 1>(p, B, emb, vemb, A, sb, g, lane, st(1));
     layer<true, V, 3, false, false, 1>(p, A, emb, vemb, B, sb, g, lane, st(2));  // 217 outputs (14 out-blocks)

@@ -1,4 +1,6 @@
-"""Max |error| of each render output vs the fp32 oracle (oracle/restate.py), per render precision.
+"""Max |error| of each render output per render precision, against the fp32 oracle (oracle/restate.py,
+the reference's arithmetic) and against an fp64 evaluation of the same network (the oracle run in float64
+on the same inputs); the fp32 oracle's own error vs fp64 is listed as 'oracle_fp32'.
 
 usage: python tools/precision_report.py > gpurun_out/precision.json   (GPU box)
 """
@@ -13,6 +15,8 @@ from animatable_nerf_amd import config  # noqa: E402
 from animatable_nerf_amd.renderer import Renderer  # noqa: E402
 from oracle import restate  # noqa: E402
 from tests._common import batch_np, make_net, oracle_params, rotated_batch_np, scene, to_torch  # noqa: E402
+
+KEYS = ('rgb_map', 'acc_map', 'depth_map', 'raw', 'pbw', 'tbw')
 
 
 def main():
@@ -29,13 +33,18 @@ def main():
     for name, b in cases.items():
         with torch.no_grad():
             ref = restate.render(oracle_params(), to_torch(b))
-        for prec in ('fp32', 'bf16x3'):
+            p64 = {k: v.double() for k, v in oracle_params().items()}
+            b64 = {k: (v.double() if v.dtype == torch.float32 else v) for k, v in to_torch(b).items()}
+            r64 = restate.render(p64, b64)
+        out[f'{name}/oracle_fp32'] = {'vs_fp64': {k: float((ref[k].double() - r64[k]).abs().max()) for k in KEYS}}
+        for prec in ('fp32', 'bf16x6', 'bf16x3'):
             cfg = config.defaults()
             cfg.perturb = 0
             cfg.render_precision = prec
             ret = Renderer(net, cfg).render_device(to_torch(b, dev))
-            out[f'{name}/{prec}'] = {k: float((ret[k].cpu() - ref[k]).abs().max()) for k in
-                                    ('rgb_map', 'acc_map', 'depth_map', 'raw', 'pbw', 'tbw')}
+            out[f'{name}/{prec}'] = {
+                'vs_oracle_fp32': {k: float((ret[k].cpu() - ref[k]).abs().max()) for k in KEYS},
+                'vs_fp64': {k: float((ret[k].cpu().double() - r64[k]).abs().max()) for k in KEYS}}
     print(json.dumps(out, indent=1))
 
 
