@@ -174,6 +174,7 @@ __global__ void k_mlp_b16(MlpArgs a);  // T-pose BW + NeRF in bf16x3 (render pre
 __global__ void k_mlp_x6(MlpArgs a);   // every layer in bf16x6, fp32-level (render precision ANR_BF16X6)
 __global__ void k_alpha(MlpArgs a);      // density program (get_alpha), exact fp32 MFMA
 __global__ void k_alpha_b16(MlpArgs a);  // density program, NeRF trunk in bf16x3
+__global__ void k_alpha_x6(MlpArgs a);   // density program, every layer in bf16x6
 
 struct PackArgs {
   const float* t[66];  // 46 core tensors + 19 novel_pose_bw tensors (NULL when absent) + the head H

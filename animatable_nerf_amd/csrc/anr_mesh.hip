@@ -304,13 +304,16 @@ int anr_alpha_points(const anr_params* p, const anr_frame* f, const float* wpts,
   ma.pX = f->pbw_dims[0]; ma.pY = f->pbw_dims[1]; ma.pZ = f->pbw_dims[2];
   ma.list = (const int*)(ws + L.list); ma.n_kept = (const int*)(ws + L.counts);
   ma.wpts = wpts; ma.n_pts = n_pts; ma.chunk_pts = o->chunk_pts; ma.alpha_out = alpha;
-  const bool b16 = o->precision == ANR_BF16X3;
-  ma.pose_woff = o->novel_pose ? (b16 ? (ANR_POSE_MODE == 2 ? ANR_X6_NOVEL_WOFF : ANR_B16_NOVEL_WOFF) : ANR_NOVEL_WOFF) : 0;
+  const bool x6 = o->precision == ANR_BF16X6;
+  const bool b16 = o->precision == ANR_BF16X3 || x6;
+  ma.pose_woff = o->novel_pose ? (x6 || (b16 && ANR_POSE_MODE == 2) ? ANR_X6_NOVEL_WOFF : b16 ? ANR_B16_NOVEL_WOFF : ANR_NOVEL_WOFF) : 0;
   ma.pose_boff = o->novel_pose ? ANR_NOVEL_BOFF : 0;
   if (!alpha_attr_set) {
     if (hipFuncSetAttribute((const void*)k_alpha, hipFuncAttributeMaxDynamicSharedMemorySize, mlp_lds_bytes<false>()) !=
             hipSuccess ||
         hipFuncSetAttribute((const void*)k_alpha_b16, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            mlp_lds_bytes<true>()) != hipSuccess ||
+        hipFuncSetAttribute((const void*)k_alpha_x6, hipFuncAttributeMaxDynamicSharedMemorySize,
                             mlp_lds_bytes<true>()) != hipSuccess)
       return fail(ANR_E_HIP, "hipFuncSetAttribute(k_alpha) failed");
     alpha_attr_set = true;
@@ -318,7 +321,8 @@ int anr_alpha_points(const anr_params* p, const anr_frame* f, const float* wpts,
   const long max_tiles = ((long)G * 64 + 127) / 128;
   const int cus = num_cus_here();
   const int grid = (int)(max_tiles < cus ? max_tiles : cus);
-  if (b16) hipLaunchKernelGGL(k_alpha_b16, dim3(grid), dim3(512), mlp_lds_bytes<true>(), s, ma);
+  if (x6) hipLaunchKernelGGL(k_alpha_x6, dim3(grid), dim3(512), mlp_lds_bytes<true>(), s, ma);
+  else if (b16) hipLaunchKernelGGL(k_alpha_b16, dim3(grid), dim3(512), mlp_lds_bytes<true>(), s, ma);
   else hipLaunchKernelGGL(k_alpha, dim3(grid), dim3(512), mlp_lds_bytes<false>(), s, ma);
   return check_launch("k_alpha");
 }

@@ -64,6 +64,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 //         mode 2 (bf16x6, fp32-level products) and the accurate libm paths of the exact kernel.
 //   V = 5 (the sdf_pdf SDF network forward, k_sdfnet_b16): entries 0..8 = layers 41..49
 //         (anr_layers.h sdfnet_desc), bf16x3, the image after the residual MLP's.
+//   V = 8 (density, k_alpha_x6, render precision ANR_BF16X6): the V = 1 program in mode 2.
 //   V = 6 (the sdf_pdf colour network, k_color_b16): entries 0..4 = layers 58..62 (anr_layers.h
 //         color_desc), bf16x3, an image of its own; lin0 reads its inputs from memory rows.
 //   V = 7 (the sdf_pdf SDF network's input gradient, k_sdfgrad_b16): entries 0..7 = layers 50..57
@@ -72,7 +73,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 //         (anr_layers.h resd_desc), bf16x3, from the sdf render's own image (k_pack_resd).
 template <int V>
 __host__ __device__ constexpr int prog_len() {
-  return V == 0 ? 30 : (V == 2 || V == 4) ? 28 : (V == 3 || V == 5) ? 9 : V == 7 ? 8 : V == 6 ? 5 : 18;
+  return V == 0 ? 30 : (V == 2 || V == 4) ? 28 : (V == 3 || V == 5) ? 9 : V == 7 ? 8 : V == 6 ? 5 : 18;  // 1, 8: 18
 }
 // programs whose weights are a packed layer sequence of their own (k_pack_seq), not the render image
 template <int V>
@@ -86,11 +87,12 @@ __host__ __device__ constexpr int prog_layer(int e) {
          : e < 9 ? e
          : V == 0 ? e - 9
          : (V == 2 || V == 4) ? (e < 26 ? e - 9 : (e == 26 ? ANR_L_HEAD : ANR_L_RGB))
+         : V == 8 ? (e < 17 ? e : ANR_L_ALPHA)
                   : (e < 17 ? e : ANR_L_ALPHA);
 }
 __host__ __device__ constexpr bool prog_pose(int e) { return e < 9; }
 template <bool B16, int V>
-__host__ __device__ constexpr int prog_mode(int e) { return B16 ? (V == 4 ? 2 : e < 9 ? ANR_POSE_MODE : 1) : 0; }
+__host__ __device__ constexpr int prog_mode(int e) { return B16 ? ((V == 4 || V == 8) ? 2 : e < 9 ? ANR_POSE_MODE : 1) : 0; }
 // Slices = the staging unit: mode 0 8 fp32 k-steps; mode 1 one 32-input k-step (OB x 2 KiB);
 // mode 2 one 32-input k-step of a group of <= 8 out-blocks (x 3 KiB).
 template <int V>
@@ -290,6 +292,7 @@ static_assert(prog_bias_off<0>(prog_len<0>()) == ANR_BIAS_TABLE_FLOATS, "bias ta
 static_assert(prog_bias_off<1>(prog_len<1>()) <= ANR_BIAS_TABLE_FLOATS, "bias table size (anr_layers.h)");
 static_assert(prog_bias_off<2>(prog_len<2>()) <= ANR_BIAS_TABLE_FLOATS, "bias table size (anr_layers.h)");
 static_assert(prog_bias_off<4>(prog_len<4>()) <= ANR_BIAS_TABLE_FLOATS, "bias table size (anr_layers.h)");
+static_assert(prog_bias_off<8>(prog_len<8>()) <= ANR_BIAS_TABLE_FLOATS, "bias table size (anr_layers.h)");
 static_assert(prog_bias_off<3>(prog_len<3>()) == seq_bias_off(ANR_L_RESD0, ANR_RESD_LAYERS), "resd bias section");
 static_assert(prog_bias_off<5>(prog_len<5>()) == seq_bias_off(ANR_L_SDF0, ANR_SDF_LAYERS), "sdf bias section");
 static_assert(prog_bias_off<5>(prog_len<5>()) <= ANR_BIAS_TABLE_FLOATS, "bias table size (anr_layers.h)");
@@ -317,7 +320,7 @@ __device__ __forceinline__ void fill_bias_table(const MlpArgs& a, float* __restr
       src = e == 3 ? a.fold + 512 : a.bias + toff;
     } else if constexpr (e < 9) {
       src = L == 0 ? a.fold + 0 : L == 5 ? a.fold + 512 : a.bias + a.pose_boff + boff;
-    } else if constexpr (V != 1 && e < 18) {
+    } else if constexpr (V != 1 && V != 8 && e < 18) {
       src = L == 0 ? a.fold + 256 : L == 5 ? a.fold + 768 : a.bias + boff;
     } else {
       src = L == 18 ? a.fold + 1024 : L == ANR_L_HEAD ? a.fold + ANR_FOLD_HEAD : a.bias + boff;
@@ -1072,9 +1075,10 @@ __device__ __forceinline__ void mlp_body(const MlpArgs& a) {
 // LBS inverse, then TPoseHuman.calculate_alpha (:241-250): NeRF trunk + alpha_fc. The T-pose BW MLP
 // the reference also evaluates there does not reach the returned alpha and is not run; no bbox
 // mask, no activation: alpha_out[id] = the raw alpha_fc output.
-template <bool B16>
+template <bool B16, int V = 1>
 __device__ __forceinline__ void alpha_body(const MlpArgs& a) {
-  constexpr int V = 1;
+  static_assert(V == 1 || V == 8, "density programs");
+  constexpr bool FAST = B16 && ANR_FAST_MATH && V == 1;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -1104,11 +1108,11 @@ __device__ __forceinline__ void alpha_body(const MlpArgs& a) {
     f32x4 A[17], B[17], fc[2], init[2], bw[2];
     if constexpr (B16) embed_b<2>(pose, g, 10, emb);
     else embed<16>(pose, g, 10, emb);
-    lookup24<B16 && ANR_FAST_MATH>(a.pbw32, pose, a.pbounds, a.pX, a.pY, a.pZ, g, init);
+    lookup24<FAST>(a.pbw32, pose, a.pbounds, a.pX, a.pY, a.pZ, g, init);
 #pragma unroll
     for (int s8 = 0; s8 < 8; ++s8) vemb[s8] = 0.f;
     bw_mlp<B16, V, 0>(p, emb, vemb, sb, A, B, fc, g, lane);
-    blend_softmax<B16 && ANR_FAST_MATH>(fc, init, g, bw);
+    blend_softmax<FAST>(fc, init, g, bw);
     float xt[3];
     lbs_inverse(bw, sA, g, pose, xt);
 

@@ -92,9 +92,10 @@ class Renderer(_renderer.Renderer):
         o.norm_th = MESH_NORM_TH
         o.novel_pose = 1 if self.cfg.get('test_novel_pose', False) else 0
         rprec = self.cfg.get('render_precision', 'fp32')
-        if rprec not in ('fp32', 'bf16x3'):
-            raise ValueError(f"render_precision must be 'fp32' or 'bf16x3', got {rprec!r}")
-        o.precision = _lib.BF16X3 if rprec == 'bf16x3' else _lib.FP32
+        rprecs = {'fp32': _lib.FP32, 'bf16x3': _lib.BF16X3, 'bf16x6': _lib.BF16X6}
+        if rprec not in rprecs:
+            raise ValueError(f"render_precision must be one of {sorted(rprecs)}, got {rprec!r}")
+        o.precision = rprecs[rprec]
         nbytes = self.lib.anr_alpha_workspace_bytes(n, ctypes.byref(o), ctypes.byref(f))
         if nbytes == 0:
             raise ValueError('anr_alpha_workspace_bytes: bad arguments (chunk_pts must be a multiple of 64)')

@@ -712,8 +712,9 @@ def bench_mesh(args, rank, world, dev):
     dt_max = max_over_ranks(dt, dev, world)
     alpha_ms = sum(ev[2 * j].elapsed_time(ev[2 * j + 1]) for j in range(args.steps)) / args.steps
     n_kept = int(renderer._aws[:4].view(torch.int32).item())  # anr_alpha_counts: kept points
-    split = args.render_precision == 'bf16x3'
-    flop_exec = 3 * FLOP_PER_KEPT_ALPHA if split else FLOP_PER_KEPT_ALPHA
+    split = args.render_precision in ('bf16x3', 'bf16x6')
+    prods = 6 if args.render_precision == 'bf16x6' else 3
+    flop_exec = prods * FLOP_PER_KEPT_ALPHA if split else FLOP_PER_KEPT_ALPHA
     peak = PEAK_BF16_MFMA_TFLOPS if split else PEAK_FP32_MFMA_TFLOPS
     achieved = n_kept * flop_exec / (alpha_ms * 1e-3) / 1e12
     t1 = time.perf_counter()
@@ -725,12 +726,14 @@ def bench_mesh(args, rank, world, dev):
         'value': n * args.steps * world / dt_max, 'unit': 'points/s', 'n_gpus': world, 'steps': args.steps,
         'warmup': args.warmup, 'ms_per_step': dt_max / args.steps * 1e3, 'higher_is_better': True,
         'scaling': 'weak', 'vs_baseline': None,
-        'dtype': 'bf16 MFMA operands (hi/lo split), fp32 accumulate' if split else 'fp32', 'data': 'synthetic',
+        'dtype': (f'bf16 MFMA operands ({"hi/mid/lo" if prods == 6 else "hi/lo"} split), fp32 accumulate'
+                  if split else 'fp32'), 'data': 'synthetic',
         'config': {'workload': f'mesh extraction, {args.voxel * 1000:g} mm voxel grid over wbounds, inside = all voxels',
                    'grid': list(inside.shape), 'points': n, 'kept_fraction': n_kept / n, 'iso': iso,
                    'vertices': int(verts.shape[0]), 'triangles': int(tris.shape[0]),
                    'alpha_ms': alpha_ms, 'marching_cubes_ms': mc_ms, 'parallelism': f'replicas{world}'},
-        'roofline': {'bound': 'mfma', 'kernel': 'anr_alpha_points (k_alpha%s dominates)' % ('_b16' if split else ''),
+        'roofline': {'bound': 'mfma', 'kernel': 'anr_alpha_points (k_alpha%s dominates)' % (
+                     {'bf16x3': '_b16', 'bf16x6': '_x6'}.get(args.render_precision, '')),
                      'achieved': achieved, 'peak': peak, 'unit': 'TFLOP/s', 'frac': achieved / peak, 'traffic': None,
                      'flop_per_kept_executed': flop_exec, 'flop_per_kept_credited': FLOP_PER_KEPT_ALPHA},
     }

@@ -115,7 +115,8 @@ typedef struct anr_render_opts {
                         anr_render_fwd / anr_alpha_points: ANR_FP32 (exact fp32 MFMA everywhere) or
                         ANR_BF16X3 (every MLP layer as hi/lo-split bf16 MFMA, lo*bh + hi*bl + hi*bh
                         with fp32 accumulation: ~2^-16 relative per product, outputs within the
-                        1e-4 fp32 tolerance); anr_render_fwd / anr_network_fwd also ANR_BF16X6
+                        1e-4 fp32 tolerance); anr_render_fwd / anr_network_fwd / anr_alpha_points
+                        also ANR_BF16X6
                         (hi/mid/lo-split bf16, six products per multiply-add, fp32 accumulation:
                         fp32-level products, <= ~2^-23 relative, on the bf16 MFMA pipe).
                         anr_sdf_render_fwd: ANR_BF16X3 splits its layer GEMMs the same way (the

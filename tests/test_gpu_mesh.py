@@ -39,7 +39,7 @@ def _batch(dev):
     return {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in b.items()}, g
 
 
-@pytest.mark.parametrize('precision', ['fp32', 'bf16x3'])
+@pytest.mark.parametrize('precision', ['fp32', 'bf16x3', 'bf16x6'])
 def test_alpha_volume_vs_reference(precision):
     dev = _dev()
     batch, g = _batch(dev)
@@ -54,7 +54,7 @@ def test_alpha_volume_vs_reference(precision):
     assert err <= TOL, err
 
 
-@pytest.mark.parametrize('precision', ['fp32', 'bf16x3'])
+@pytest.mark.parametrize('precision', ['fp32', 'bf16x3', 'bf16x6'])
 def test_alpha_small_chunks_vs_reference(precision):
     dev = _dev()
     batch, g = _batch(dev)
