@@ -307,7 +307,7 @@ def main():
             'bf16x6': ('bf16x6_fp32_level', 'same frame, every MLP layer as hi/mid/lo-split bf16 MFMA, 6 products '
                        'per multiply-add, fp32 accumulation: fp32-level products (each output as close to an fp64 '
                        'evaluation as the reference\'s fp32 arithmetic, tests/test_gpu_render.py '
-                       'test_bf16x6_is_fp32_level)'),
+                       'test_split_precisions_are_fp32_level)'),
             'fp32': ('fp32_exact', 'exact fp32 MFMA')}
         for other in [p for p in ('fp32', 'bf16x6', 'bf16x3') if p != prec]:
             o2, dt2, kms2, (nk2, _) = timed(other)

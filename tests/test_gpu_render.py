@@ -270,11 +270,14 @@ def test_frame_shards_equal_whole_frame(renderer, dev, world):
         assert torch.equal(cat, full[k]), k
 
 
-def test_bf16x6_is_fp32_level(dev):
-    """ANR_BF16X6 claims fp32-level arithmetic: against an fp64 evaluation of the same network
-    (oracle/restate.py run in float64 on the same fp32 inputs), its outputs are as close as the
-    reference's own fp32 arithmetic (the fp32 oracle) and the exact fp32 MFMA kernel are — each
-    output's max error within 1.5x the larger of those two (5000 rays, 3 chunks, fine volume)."""
+@pytest.mark.parametrize('split', ['bf16x6', 'bf16x3'])
+def test_split_precisions_are_fp32_level(dev, split):
+    """Against an fp64 evaluation of the same network (oracle/restate.py run in float64 on the same
+    fp32 inputs), each split-bf16 render is as close as the reference's own fp32 arithmetic (the fp32
+    oracle) and the exact fp32 MFMA kernel are — every output's max error within 1.5x the larger of
+    those two (5000 rays, 3 chunks, fine volume). Measured (profiles/r3_precision_fp64.json): all
+    four agree to within ~5 %: the shared fp32 inputs, sampling and blending set the error, not the
+    MLP products (bf16x6 ~2^-23, bf16x3 ~2^-16 relative per product)."""
     from animatable_nerf_amd import config
     from animatable_nerf_amd.renderer import Renderer
     torch.set_num_threads(16)
@@ -290,7 +293,7 @@ def test_bf16x6_is_fp32_level(dev):
     net = make_net(dev)
     net.train()
     got = {}
-    for prec in ('fp32', 'bf16x6', 'bf16x3'):
+    for prec in ('fp32', split):
         cfg = config.defaults()
         cfg.perturb = 0
         cfg.render_precision = prec
@@ -298,6 +301,6 @@ def test_bf16x6_is_fp32_level(dev):
         got[prec] = {k: float((ret[k].cpu().double() - r64[k]).abs().max())
                      for k in ('rgb_map', 'acc_map', 'depth_map', 'raw', 'pbw', 'tbw')}
     ref_err = {k: float((r32[k].double() - r64[k]).abs().max()) for k in got['fp32']}
-    for k, e6 in got['bf16x6'].items():
+    for k, e in got[split].items():
         bar = 1.5 * max(ref_err[k], got['fp32'][k])
-        assert e6 <= bar, (k, e6, ref_err[k], got['fp32'][k], got['bf16x3'][k])
+        assert e <= bar, (k, e, ref_err[k], got['fp32'][k])
