@@ -363,6 +363,12 @@ struct LayerIO {
   const float* g1 = nullptr;
 };
 
+// the sdf programs' stored softplus outputs h (8 KiB per sample, written once, read once) bypass
+// the weight stream's L2 lines: non-temporal stores (k_sdfnet_b16) and loads (k_sdfgrad_b16)
+#ifndef ANR_SDF_NT
+#define ANR_SDF_NT 1
+#endif
+
 // softplus(beta = 100, threshold = 20) as log2(1 + 2^(100 x log2 e)) ln2 / 100 on the hardware exp2 /
 // log2 (~1 ulp each): 2 transcendentals + 5 VALU instead of the ~25 of k_lgemm's libm-grade epilogue
 // (fast_exp / fast_log1p). Its h feeds a hi/lo bf16 split (~2^-16 relative) and the reverse pass's
@@ -404,8 +410,13 @@ __device__ __forceinline__ void layer_x3(Pipe& p, const f32x4 (&in)[NIN], const 
   auto load_h = [&](auto tc) {
     constexpr int t = decltype(tc)::value;
     if constexpr (FAC_IN != 0 && t < KS) {
+#if ANR_SDF_NT
+      hv[t & 1][0] = __builtin_nontemporal_load((const f32x4*)(fst + 32 * t + 4 * g));
+      hv[t & 1][1] = __builtin_nontemporal_load((const f32x4*)(fst + 32 * t + 16 + 4 * g));
+#else
       hv[t & 1][0] = *(const f32x4*)(fst + 32 * t + 4 * g);
       hv[t & 1][1] = *(const f32x4*)(fst + 32 * t + 16 + 4 * g);
+#endif
     }
   };
   auto split_k = [&](auto tc, bf16x8& bh, bf16x8& bl) {
@@ -458,9 +469,14 @@ __device__ __forceinline__ void layer_x3(Pipe& p, const f32x4 (&in)[NIN], const 
         for (int j = 0; j < 8; ++j) x[j] = softplus100(x[j]);
         if (spst) {  // neurons 32 ts + 4 g + (0..3) and 32 ts + 16 + 4 g + (0..3)
           float* d = spst + 32 * ts + 4 * g;
-          if constexpr (SP_IN == 1) {
+          if constexpr (SP_IN == 1) {  // streamed once to HBM, read once by the gradient pass: non-temporal
+#if ANR_SDF_NT
+            __builtin_nontemporal_store(f32x4{x[0], x[1], x[2], x[3]}, (f32x4*)d);
+            __builtin_nontemporal_store(f32x4{x[4], x[5], x[6], x[7]}, (f32x4*)(d + 16));
+#else
             *(f32x4*)d = f32x4{x[0], x[1], x[2], x[3]};
             *(f32x4*)(d + 16) = f32x4{x[4], x[5], x[6], x[7]};
+#endif
           } else {
             const float sqrt2 = 1.41421356237309515f;
             const int c = 32 * ts + 4 * g;
