@@ -43,6 +43,10 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 #define ANR_DMA_SPREAD 1
 #endif
 // bf16x3 kernels: hardware log/exp/rcp in the blend softmax and reciprocal-based lookup coordinates
+// bf16x6 layers: read the next out-block's fragments ahead of the current out-block's MFMAs
+#ifndef ANR_X6_PF
+#define ANR_X6_PF 1
+#endif
 #ifndef ANR_FAST_MATH
 #define ANR_FAST_MATH 1
 #endif
@@ -627,20 +631,30 @@ __device__ __forceinline__ void layer(Pipe& p, const f32x4 (&in)[NIN], const flo
         bf16x8 bh, bm, bl;
         split8x3(x, bh, bm, bl);
         constexpr int NOBG = prog_nobg<V>(E);
+        // ANR_X6_PF: the next out-block's three fragments are read (within the slice) before this
+        // out-block's six MFMAs, so their LDS latency sits behind them
+        bf16x8 fr[2][3];
+        auto rd = [&](int slot, int oo) {
+          fr[slot][0] = *(const bf16x8*)(buf + (oo % 8) * 3072 + lane * 16);
+          fr[slot][1] = *(const bf16x8*)(buf + (oo % 8) * 3072 + 1024 + lane * 16);
+          fr[slot][2] = *(const bf16x8*)(buf + (oo % 8) * 3072 + 2048 + lane * 16);
+        };
         static_for<0, D.ob>([&](auto ob) {
           constexpr int o = decltype(ob)::value;
           constexpr int SQ = tt * NOBG + o / 8;  // the slice of this out-block group
           if constexpr (o % 8 == 0) buf = p.template enter<B16, V, E, SQ>();
           if constexpr (tt == 0 && o == 0) init_bias();
-          const bf16x8 ah = *(const bf16x8*)(buf + (o % 8) * 3072 + lane * 16);
-          const bf16x8 am = *(const bf16x8*)(buf + (o % 8) * 3072 + 1024 + lane * 16);
-          const bf16x8 al = *(const bf16x8*)(buf + (o % 8) * 3072 + 2048 + lane * 16);
+          if constexpr (!ANR_X6_PF || o % 8 == 0) rd(o & 1, o);
+          if constexpr (ANR_X6_PF && (o + 1) % 8 != 0 && o + 1 < D.ob) rd((o + 1) & 1, o + 1);
+          if constexpr (ANR_X6_PF) __builtin_amdgcn_sched_barrier(0);
+          const bf16x8 ah = fr[o & 1][0], am = fr[o & 1][1], al = fr[o & 1][2];
           out[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, out[o], 0, 0, 0);
           out[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, out[o], 0, 0, 0);
           out[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bm, out[o], 0, 0, 0);
           out[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bm, out[o], 0, 0, 0);
           out[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bh, out[o], 0, 0, 0);
           out[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, out[o], 0, 0, 0);
+          if constexpr (ANR_X6_PF) __builtin_amdgcn_sched_barrier(0);
           constexpr int GOB = x6_group_obs<V>(E, o / 8);
           if constexpr (o % 8 == (GOB - 1) / 2) p.template mid<B16, V, E, SQ>();
           if constexpr (o % 8 == GOB - 1) p.leave();
