@@ -30,6 +30,9 @@ EXPORTS = ('anr_near_far', 'anr_params_packed_bytes', 'anr_params_pack', 'anr_re
            'anr_network_train_workspace_bytes', 'anr_network_train_fwd', 'anr_network_train_bwd',
            'anr_points_workspace_bytes', 'anr_blend_weights', 'anr_canonical_alpha', 'anr_train_step_hooked',
            'anr_sdf_train_workspace_bytes', 'anr_sdf_train_step', 'anr_sdf_render_knn',
+           'anr_sdf_network_workspace_bytes', 'anr_sdf_network_fwd', 'anr_sdf_network_counts', 'anr_sdf_network_rows',
+           'anr_sdf_network_train_workspace_bytes', 'anr_sdf_network_train_fwd', 'anr_sdf_network_train_counts',
+           'anr_sdf_network_train_rows', 'anr_sdf_network_train_bwd',
            'anr_last_error', 'anr_version')
 
 c_float_p = ctypes.c_void_p
@@ -144,6 +147,21 @@ def load():
     lib.anr_sdf_train_step.argtypes = [ctypes.POINTER(SdfParams), ctypes.c_void_p * NUM_SDF_TENSORS,
                                        ctypes.POINTER(SdfFrame), P, P, P, P, ctypes.c_int, ctypes.POINTER(RenderOpts),
                                        P, P, ctypes.c_int, ctypes.POINTER(SdfRenderOut), P, P, ctypes.c_size_t, P]
+    SP, SF, SS = ctypes.POINTER(SdfParams), ctypes.POINTER(SdfFrame), ctypes.POINTER(Samples)
+    lib.anr_sdf_network_workspace_bytes.restype = ctypes.c_size_t
+    lib.anr_sdf_network_workspace_bytes.argtypes = [ctypes.c_int, ctypes.POINTER(RenderOpts)]
+    lib.anr_sdf_network_fwd.argtypes = [SP, SF, SS, ctypes.POINTER(RenderOpts), P, P, P, P, ctypes.c_size_t, P]
+    lib.anr_sdf_network_counts.restype = P
+    lib.anr_sdf_network_counts.argtypes = [P, ctypes.c_int]
+    lib.anr_sdf_network_rows.argtypes = [P, ctypes.c_int, P, P, P]
+    lib.anr_sdf_network_train_workspace_bytes.restype = ctypes.c_size_t
+    lib.anr_sdf_network_train_workspace_bytes.argtypes = [ctypes.c_int]
+    lib.anr_sdf_network_train_fwd.argtypes = [SP, SF, SS, ctypes.POINTER(RenderOpts), P, P, P, P, ctypes.c_size_t, P]
+    lib.anr_sdf_network_train_counts.restype = P
+    lib.anr_sdf_network_train_counts.argtypes = [P, ctypes.c_int]
+    lib.anr_sdf_network_train_rows.argtypes = [P, ctypes.c_int, P, P, P, P]
+    lib.anr_sdf_network_train_bwd.argtypes = [SP, ctypes.c_void_p * NUM_SDF_TENSORS, SF, SS, ctypes.POINTER(RenderOpts),
+                                              P, P, P, P, P, P, ctypes.c_size_t, P]
     lib.anr_camera_rays_workspace_bytes.restype = ctypes.c_size_t
     lib.anr_camera_rays_workspace_bytes.argtypes = [ctypes.c_int, ctypes.c_int]
     D = ctypes.POINTER(ctypes.c_double)

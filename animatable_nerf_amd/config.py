@@ -81,6 +81,30 @@ def defaults():
     })
 
 
+# The keys of each named experiment that reach the hot path (the yaml files are not shipped: the
+# reference tree is not available where the GPU tests run). Each overrides defaults() (= aninerf_s9p).
+SUBJECTS = {
+    # configs/aninerf_s9p.yaml:57-93 (the defaults above); H x W 1002 x 1000 at ratio 1
+    'aninerf_s9p': {'num_train_frame': 260, 'num_eval_frame': 133, 'H': 1002, 'W': 1000, 'ratio': 1.0},
+    # configs/aninerf_313.yaml:23-28 (parent aninerf_s9p): ZJU-MoCap 313, 1024 x 1024 at ratio 0.5 = 512 x 512,
+    # 60 training frames (nf_latent (60,128), bw_latent (61,128))
+    'aninerf_313': {'num_train_frame': 60, 'num_eval_frame': 1000, 'H': 1024, 'W': 1024, 'ratio': 0.5},
+    # configs/sdf_pdf/anisdf_pdf_s9p.yaml:79-95
+    'anisdf_pdf_s9p': {'num_train_frame': 260, 'num_eval_frame': 133, 'H': 1002, 'W': 1000, 'ratio': 1.0,
+                       'tpose_viewdir': True, 'use_bigpose': True},
+}
+
+
+def subject(name, **overrides):
+    """defaults() with the hot-path keys of the named reference experiment (SUBJECTS) and overrides."""
+    cfg = defaults()
+    cfg.merge(CfgNode(SUBJECTS[name]))
+    cfg.merge(CfgNode(overrides))
+    if 'num_latent_code' not in overrides:
+        cfg.num_latent_code = cfg.num_train_frame  # config.py:144-145
+    return cfg
+
+
 def load_cfg(cfg_file=None, opts=(), base_dir=None):
     """Load ``cfg_file`` (resolving ``parent_cfg`` relative to ``base_dir``) over the defaults."""
     cfg = defaults()

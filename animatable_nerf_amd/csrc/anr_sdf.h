@@ -39,8 +39,14 @@ __host__ __device__ constexpr int sdf_wn_rows() {
   return r;
 }
 
+// Free-sample mode (Network.forward(wpts, viewdir, dists, batch), anisdf_pdf_network.py:156-224):
+// wpts != NULL replaces the rays: "ray" g is the group of points [64 g, 64 g + 64) of the call (n_pts
+// points, the last group partial), chunk = the number of groups (the call is one reference chunk:
+// its forced argmin spans every point), world -> pose by torch's matmul rule for an (n_pts, 3) product.
 struct SdfFrontArgs {
   const float *ray_o, *ray_d, *near_, *far_, *t_rand;
+  const float* wpts;    // (n_pts, 3) free samples or NULL
+  int n_pts;
   int n_rays, chunk;
   const float *R, *Th;
   const float* verts;  // pvertices (nv, 3)
@@ -58,6 +64,8 @@ struct SdfPointArgs {
   const int* list;
   int b0, cnt;
   const float *ray_o, *ray_d, *near_, *far_, *t_rand;
+  const float *wpts, *vdir;  // free-sample mode (SdfFrontArgs): points and world view directions, or NULL
+  int n_pts;
   int chunk;
   const float *R, *Th, *A, *bigA;
   const float* weights;  // (nv, 24)

@@ -140,9 +140,17 @@ __global__ __launch_bounds__(1024) void k_sdf_front(SdfFrontArgs a) {
 
   const int wpb = blockDim.x >> 6;
   for (int ray = blockIdx.x * wpb + wid; ray < a.n_rays; ray += gridDim.x * wpb) {
-    float z, dist, pts[3], p[3];
-    sample_point(a.ray_o, a.ray_d, a.near_, a.far_, a.t_rand, ray, lane, 64, z, dist, pts);
-    world_to_pose(pts, a.R, a.Th, p);
+    float p[3];
+    const long pid_ = (long)ray * 64 + lane;
+    const bool valid = !a.wpts || pid_ < a.n_pts;
+    if (a.wpts) {
+      if (valid) world_to_pose_pt(a.wpts, pid_, a.n_pts, a.n_pts, a.R, a.Th, p);
+      else p[0] = p[1] = p[2] = 0.f;
+    } else {
+      float z, dist, pts[3];
+      sample_point(a.ray_o, a.ray_d, a.near_, a.far_, a.t_rand, ray, lane, 64, z, dist, pts);
+      world_to_pose(pts, a.R, a.Th, p);
+    }
     float b0 = INFINITY, b1 = INFINITY, b2 = INFINITY, b3 = INFINITY, b4 = INFINITY;
     int i0 = 0, i1 = 0, i2 = 0, i3 = 0, i4 = 0;
     auto lt = [](float d, int j, float b, int i) { return d < b || (d == b && j < i); };
@@ -219,7 +227,7 @@ __global__ __launch_bounds__(1024) void k_sdf_front(SdfFrontArgs a) {
     const float q3 = 1.0f / (d3 + 1e-8f), q4 = 1.0f / (d4 + 1e-8f);
     const float S = (((q0 + q4) + q1) + q2) + q3;
     const float w0 = q0 / S, w1 = q1 / S, w2 = q2 / S, w3 = q3 / S, w4 = q4 / S;
-    const float pn = (((d0 * w0 + d1 * w1) + d2 * w2) + d3 * w3) + d4 * w4;
+    const float pn = valid ? (((d0 * w0 + d1 * w1) + d2 * w2) + d3 * w3) + d4 * w4 : INFINITY;
     const size_t pid = (size_t)ray * 64 + lane;
     uint4* rec = (uint4*)(a.knn + pid * 8);
     rec[0] = make_uint4(__float_as_uint(w0), __float_as_uint(w1), __float_as_uint(w2), __float_as_uint(w3));
@@ -228,12 +236,12 @@ __global__ __launch_bounds__(1024) void k_sdf_front(SdfFrontArgs a) {
     const bool keep = pn < a.norm_th;
     const uint64_t m = __ballot(keep);
     if (lane == 0) a.mask[ray] = m;
-    if (!keep) {
+    if (!keep && valid) {
       a.raw[pid] = make_float4(0.f, 0.f, 0.f, 0.f);
       a.sdf[pid] = 10.f;
     }
     const int rc = ray % a.chunk;
-    uint64_t key = ((uint64_t)__float_as_uint(pn) << 32) | (uint32_t)(rc * 64 + lane);
+    uint64_t key = valid ? ((uint64_t)__float_as_uint(pn) << 32) | (uint32_t)(rc * 64 + lane) : ~0ull;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
       const uint64_t o = __shfl_xor(key, off);
@@ -349,11 +357,16 @@ __global__ __launch_bounds__(256) void k_sdf_prep(SdfPointArgs a) {
 __device__ void sdf_prep_point(const SdfPointArgs& a, int i, float (*sp)[4]) {
   const int pid = a.list[a.b0 + i];
   const int ray = pid >> 6, s = pid & 63;
-  float z, dist, pts[3], p[3], pd[3];
-  sample_point(a.ray_o, a.ray_d, a.near_, a.far_, a.t_rand, ray, s, 64, z, dist, pts);
-  world_to_pose(pts, a.R, a.Th, p);
-  // world_dirs_to_pose_dirs: d @ R
-  {
+  float p[3], pd[3];
+  if (a.wpts) {  // free samples: pose_pts / pose_dirs of the call's (n_pts, 3) products
+    world_to_pose_pt(a.wpts, pid, a.n_pts, a.n_pts, a.R, a.Th, p);
+    const float zero[3] = {0.f, 0.f, 0.f};
+    world_to_pose_pt(a.vdir, pid, a.n_pts, a.n_pts, a.R, zero, pd);  // world_dirs_to_pose_dirs: d @ R
+  } else {
+    float z, dist, pts[3];
+    sample_point(a.ray_o, a.ray_d, a.near_, a.far_, a.t_rand, ray, s, 64, z, dist, pts);
+    world_to_pose(pts, a.R, a.Th, p);
+    // world_dirs_to_pose_dirs: d @ R
     const float* d = a.ray_d + 3 * ray;
     for (int j = 0; j < 3; ++j) pd[j] = fmaf(d[2], a.R[6 + j], fmaf(d[1], a.R[3 + j], d[0] * a.R[j]));  // torch matmul (n >= 45)
   }

@@ -279,15 +279,21 @@ int anr_sdf_render_rows(const void* workspace, int n_rays, const anr_render_opts
   return ANR_OK;
 }
 
-int anr_sdf_render_fwd(const anr_sdf_params* p, const anr_sdf_frame* f, const float* ray_o, const float* ray_d,
-                       const float* near_, const float* far_, int R, const anr_render_opts* o,
-                       const anr_sdf_render_out* out, void* workspace, size_t ws_bytes, void* stream) {
-  ANR_TRY(check(p, f, ray_o, ray_d, near_, far_, R, o, out, workspace));
-  const SLayout L = slayout(R, o->chunk);
+}  // extern "C"
+
+namespace {
+
+// the render sequence over rays (wpts NULL) or over the free samples of one Network.forward call
+// (wpts / vdir, n_pts points in R = ceil(n_pts / 64) groups that form one chunk: no compositing, no
+// msk_sdf lists; raw / sdf are the caller's (n_pts) outputs)
+int sdf_render_core(const anr_sdf_params* p, const anr_sdf_frame* f, const float* ray_o, const float* ray_d,
+                    const float* near_, const float* far_, int R, int chunk, const anr_render_opts* o,
+                    const anr_sdf_render_out* out, void* workspace, size_t ws_bytes, hipStream_t s,
+                    const float* wpts, const float* vdir, int n_pts) {
+  const SLayout L = slayout(R, chunk);
   if (ws_bytes < L.total) return fail(ANR_E_WORKSPACE, "sdf render: workspace too small");
-  hipStream_t s = (hipStream_t)stream;
   char* ws = (char*)workspace;
-  const int nch = (R + o->chunk - 1) / o->chunk;
+  const int nch = (R + chunk - 1) / chunk;
   int* counts = (int*)(ws + L.counts);
   float4* raw = (float4*)out->raw;
 
@@ -312,14 +318,15 @@ int anr_sdf_render_fwd(const anr_sdf_params* p, const anr_sdf_frame* f, const fl
   // B1 front-end + ordered compaction
   SdfFrontArgs fa{};
   fa.ray_o = ray_o; fa.ray_d = ray_d; fa.near_ = near_; fa.far_ = far_; fa.t_rand = o->t_rand;
-  fa.n_rays = R; fa.chunk = o->chunk; fa.R = f->R; fa.Th = f->Th; fa.verts = f->pvertices; fa.nv = f->n_verts;
+  fa.wpts = wpts; fa.n_pts = n_pts;
+  fa.n_rays = R; fa.chunk = chunk; fa.R = f->R; fa.Th = f->Th; fa.verts = f->pvertices; fa.nv = f->n_verts;
   fa.norm_th = o->norm_th; fa.mask = (uint64_t*)(ws + L.mask); fa.chunk_min = (uint64_t*)(ws + L.chunk_min);
   fa.knn = (uint32_t*)(ws + L.knn); fa.raw = raw; fa.sdf = out->sdf;
   const int grid_front = std::min(sdf_cus(), (R + 15) / 16);
   hipLaunchKernelGGL(k_sdf_front, dim3(grid_front), dim3(1024), 0, s, fa);
   ANR_TRY(check_launch("k_sdf_front"));
   CompactArgs ca{};
-  ca.n_rays = R; ca.chunk = o->chunk; ca.mask = fa.mask; ca.chunk_min = fa.chunk_min;
+  ca.n_rays = R; ca.chunk = chunk; ca.mask = fa.mask; ca.chunk_min = fa.chunk_min;
   ca.ray_off = (int*)(ws + L.ray_off); ca.block_sum = (int*)(ws + L.block_sum); ca.list = (int*)(ws + L.list);
   const int nb = (R + 255) / 256;
   hipLaunchKernelGGL(k_count, dim3(nb), dim3(256), 0, s, ca);
@@ -395,7 +402,8 @@ int anr_sdf_render_fwd(const anr_sdf_params* p, const anr_sdf_frame* f, const fl
     const int cnt = (int)std::min<long>(P, n - b0);
     SdfPointArgs a{};
     a.list = ca.list; a.b0 = (int)b0; a.cnt = cnt;
-    a.ray_o = ray_o; a.ray_d = ray_d; a.near_ = near_; a.far_ = far_; a.t_rand = o->t_rand; a.chunk = o->chunk;
+    a.ray_o = ray_o; a.ray_d = ray_d; a.near_ = near_; a.far_ = far_; a.t_rand = o->t_rand; a.chunk = chunk;
+    a.wpts = wpts; a.vdir = vdir; a.n_pts = n_pts;
     a.R = f->R; a.Th = f->Th; a.A = f->A; a.bigA = f->big_A; a.weights = f->weights; a.knn = fa.knn;
     a.wimg = wimg; a.tbtab = tbtab;
     a.ptb = F(L.ptb); a.Gr = fused ? nullptr : F(L.Gr); a.Yr = F(L.Yr); a.skip_sdf_in = fused ? 1 : 0; a.Xs0 = F(L.Xs0); a.X4 = F(L.X4); a.C0 = F(L.C0);
@@ -543,11 +551,12 @@ int anr_sdf_render_fwd(const anr_sdf_params* p, const anr_sdf_frame* f, const fl
     ANR_TRY(check_launch("k_sdf_raw"));
   }
 
+  if (wpts) return ANR_OK;  // a Network.forward call: no compositing, no msk_sdf lists
   // A12 compositing over the full raw, then B7 msk_sdf / msk_label
   const anr_render_out ro{out->rgb_map, out->acc_map, out->depth_map, out->raw};
   ANR_TRY(stage_composite(near_, far_, R, o, raw, &ro, nullptr, s));
   SdfMskArgs ma{};
-  ma.sdf = out->sdf; ma.occ = f->occupancy; ma.n_rays = R; ma.chunk = o->chunk;
+  ma.sdf = out->sdf; ma.occ = f->occupancy; ma.n_rays = R; ma.chunk = chunk;
   ma.min_sdf = F(L.min_sdf); ma.flags = (uint8_t*)(ws + L.flags); ma.chunk_cnt = (int*)(ws + L.chunk_cnt);
   ma.total = counts + 1; ma.msk_sdf = F(L.msk_sdf); ma.msk_label = F(L.msk_label);
   hipLaunchKernelGGL(k_sdf_msk_rays, dim3((R + 3) / 4), dim3(256), 0, s, ma);
@@ -555,6 +564,63 @@ int anr_sdf_render_fwd(const anr_sdf_params* p, const anr_sdf_frame* f, const fl
   hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, s, ma.chunk_cnt, nch, ma.total);
   hipLaunchKernelGGL(k_sdf_msk_write, dim3(nch), dim3(1024), 0, s, ma);
   return check_launch("k_sdf_msk_write");
+}
+
+int check_points(const anr_sdf_params* p, const anr_sdf_frame* f, const anr_samples* x, const anr_render_opts* o,
+                 void* ws) {
+  if (!p || !f || !x || !o || !ws || !x->wpts || !x->viewdir) return fail(ANR_E_ARG, "sdf network: NULL argument");
+  if (x->n_pts <= 0 || x->n_pts > (1 << 24)) return fail(ANR_E_ARG, "sdf network: n must be in [1, 2^24]");
+  for (int i = 0; i < ANR_SDF_NUM_TENSORS; ++i)
+    if (!p->t[i] && i != SDF_RESD_LAT) return fail(ANR_E_ARG, "sdf network: NULL parameter tensor");
+  if (!f->A || !f->big_A || !f->R || !f->Th || !f->poses || !f->pvertices || !f->weights || !f->tbounds ||
+      !f->latent_index)
+    return fail(ANR_E_ARG, "sdf network: NULL frame tensor");
+  if (f->n_verts <= 0 || f->n_verts > 6912) return fail(ANR_E_ARG, "sdf network: n_verts must be in [1, 6912]");
+  return ANR_OK;
+}
+
+int groups_of(int n) { return (n + 63) / 64; }
+
+}  // namespace
+
+extern "C" {
+
+int anr_sdf_render_fwd(const anr_sdf_params* p, const anr_sdf_frame* f, const float* ray_o, const float* ray_d,
+                       const float* near_, const float* far_, int R, const anr_render_opts* o,
+                       const anr_sdf_render_out* out, void* workspace, size_t ws_bytes, void* stream) {
+  ANR_TRY(check(p, f, ray_o, ray_d, near_, far_, R, o, out, workspace));
+  return sdf_render_core(p, f, ray_o, ray_d, near_, far_, R, o->chunk, o, out, workspace, ws_bytes,
+                         (hipStream_t)stream, nullptr, nullptr, 0);
+}
+
+size_t anr_sdf_network_workspace_bytes(int n, const anr_render_opts* o) {
+  if (n <= 0 || !o) return 0;
+  const int G = groups_of(n);
+  return slayout(G, G).total;
+}
+
+int anr_sdf_network_fwd(const anr_sdf_params* p, const anr_sdf_frame* f, const anr_samples* x, const anr_render_opts* o,
+                        float* raw, float* sdf, float* tbounds_out, void* workspace, size_t ws_bytes, void* stream) {
+  ANR_TRY(check_points(p, f, x, o, workspace));
+  if (!raw || !sdf) return fail(ANR_E_ARG, "sdf network: NULL output");
+  const int G = groups_of(x->n_pts);
+  const anr_sdf_render_out out{nullptr, nullptr, nullptr, raw, sdf, tbounds_out};
+  return sdf_render_core(p, f, nullptr, nullptr, nullptr, nullptr, G, G, o, &out, workspace, ws_bytes,
+                         (hipStream_t)stream, x->wpts, x->viewdir, x->n_pts);
+}
+
+const int32_t* anr_sdf_network_counts(const void* workspace, int n) {
+  if (!workspace || n <= 0) return nullptr;
+  const int G = groups_of(n);
+  return (const int32_t*)((const char*)workspace + slayout(G, G).counts);
+}
+
+int anr_sdf_network_rows(const void* workspace, int n, float* resd, float* gradients, void* stream) {
+  if (!workspace || n <= 0) return fail(ANR_E_ARG, "anr_sdf_network_rows: bad arguments");
+  const int G = groups_of(n);
+  anr_render_opts o{};
+  o.chunk = G;
+  return anr_sdf_render_rows(workspace, G, &o, resd, gradients, nullptr, nullptr, stream);
 }
 
 }  // extern "C"

@@ -449,6 +449,38 @@ __global__ void k_st_add3(const float* __restrict__ a, long lda, const float* __
   out[(size_t)i * 4 + 3] = 0.f;
 }
 
+// ---- Network.forward under autograd (anr_sdf_network_train_bwd): the upstream adjoints of the
+// call's outputs take the place of the loss adjoints
+// d sdf of a kept sample (sdf[pind] = ret['sdf'], :219): ds[i] += d_sdf[list[i]]
+__global__ void k_st_cotan_sdf(const int* __restrict__ list, const int* __restrict__ n_dev, const float* __restrict__ d_sdf,
+                               float* ds) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < *n_dev) ds[i] += d_sdf[list[i]];
+}
+
+// rbar = d resd, dG = colour-normal adjoint + d gradients, lin8's sdf column adjoint = ds
+__global__ void k_st_cotan_rows(const int* __restrict__ n_dev, const float* __restrict__ d_resd,
+                                const float* __restrict__ d_grad, const float* __restrict__ dC0, const float* __restrict__ ds,
+                                float* rbar, float* dG, float* dZ8) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= *n_dev) return;
+  for (int c = 0; c < 3; ++c) {
+    rbar[(size_t)i * 4 + c] = d_resd ? d_resd[(size_t)i * 3 + c] : 0.f;
+    dG[(size_t)i * 4 + c] = dC0[(size_t)i * 40 + 30 + c] + (d_grad ? d_grad[(size_t)i * 3 + c] : 0.f);
+  }
+  rbar[(size_t)i * 4 + 3] = 0.f;
+  dG[(size_t)i * 4 + 3] = 0.f;
+  dZ8[(size_t)i * 264] = ds[i];
+}
+
+// (n,3) -> (n,4) rows (zero 4th column; src NULL: zeros)
+__global__ void k_st_rows3to4(const float* __restrict__ src, int n, float* dst) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  for (int c = 0; c < 3; ++c) dst[(size_t)i * 4 + c] = src ? src[(size_t)i * 3 + c] : 0.f;
+  dst[(size_t)i * 4 + 3] = 0.f;
+}
+
 }  // namespace anr
 
 namespace {
@@ -521,7 +553,7 @@ struct STLayout {
   size_t ptb, Gr, Hr, Yr, resd, C0, Xs0, Hs, D, Y8, Ga, Gb, Gc, gB, grow, Hc, Yc;
   size_t raw, sdf, draw, drgb, rmin, ramin, rflag;
   size_t dYc, dHa, dHb, dC0, dZ8, ds, dG, rbar, tbar, ttbar, Ab, Zb, AX4, Ain, dWe, bsum, acc, acc3, dbeta, zero;
-  size_t oblock, ptbo, Gro, Grt, ro, og, dog, tdot, Gbar, Yd;
+  size_t oblock, ptbo, Gro, Grt, ro, og, dog, tdot, Gbar, Yd, gro;
   long N;
   size_t total;
 };
@@ -553,6 +585,7 @@ STLayout stlayout(int R, int chunk) {
   L.acc = f(16); L.acc3 = f(4); L.dbeta = f(4); L.zero = take(64);
   L.oblock = take(((N + 255) / 256 + 1) * 4); L.ptbo = f(N * 8); L.Gro = f(N * 64); L.Grt = f(N * 64);
   L.ro = f(N * 3); L.og = f(N * 4); L.dog = f(N * 4); L.tdot = f(N * 4); L.Gbar = f(N * 64); L.Yd = f(N * 4);
+  L.gro = f(N * 3);
   L.total = o;
   return L;
 }
@@ -583,34 +616,59 @@ int read_int(const void* dev, int* host, hipStream_t s) {
   return ANR_OK;
 }
 
-}  // namespace
 
-extern "C" {
+// one pass of the layer-wise sdf_pdf executor. STEP: the training step over rays (losses computed
+// here, their adjoints drive the backward). Free samples of one Network.forward call (wpts != NULL,
+// n_pts points in R = ceil(n_pts / 64) groups = one chunk, no compositing / msk_sdf): NET_FWD runs
+// the forward (with the observed gradients) into the caller's raw / sdf and the workspace rows;
+// NET_BWD re-runs that forward (deterministic: same counts, same rows) and the backward from the
+// caller's upstream adjoints.
+enum CoreMode { STEP = 0, NET_FWD = 1, NET_BWD = 2 };
 
-size_t anr_sdf_train_workspace_bytes(int n_rays, const anr_render_opts* o) {
-  if (n_rays <= 0 || !o || o->chunk <= 0) return 0;
-  return stlayout(n_rays, o->chunk).total;
-}
+struct TrainCore {
+  int mode;
+  const anr_sdf_params* p;
+  float* const* grads;
+  const anr_sdf_frame* f;
+  const float *ray_o, *ray_d, *near_, *far_;
+  const float *wpts, *vdir;
+  int n_pts;
+  int R, chunk;
+  const anr_render_opts* o;
+  const float* rgb_gt;
+  const uint8_t* mask_at_box;
+  int iter_step;
+  const anr_sdf_render_out* out;  // STEP
+  float* loss;                    // STEP
+  float *raw_out, *sdf_out, *tb_out;  // NET_FWD
+  const float *d_raw, *d_sdf, *d_resd, *d_grad, *d_og;  // NET_BWD (any NULL = 0)
+  void* ws;
+  size_t ws_bytes;
+  hipStream_t s;
+};
 
-int anr_sdf_train_step(const anr_sdf_params* p, float* const* grads, const anr_sdf_frame* f, const float* ray_o,
-                       const float* ray_d, const float* near_, const float* far_, int R, const anr_render_opts* o,
-                       const float* rgb_gt, const uint8_t* mask_at_box, int iter_step, const anr_sdf_render_out* out,
-                       float* loss, void* workspace, size_t ws_bytes, void* stream) {
-  ANR_TRY(check_train(p, grads, f, ray_o, ray_d, near_, far_, R, o, rgb_gt, out, loss, workspace));
-  const STLayout L = stlayout(R, o->chunk);
-  if (ws_bytes < L.total) return fail(ANR_E_WORKSPACE, "sdf train: workspace too small");
-  hipStream_t s = (hipStream_t)stream;
-  char* ws = (char*)workspace;
+int sdf_train_core(const TrainCore& C) {
+  const anr_sdf_params* p = C.p;
+  float* const* grads = C.grads;
+  const anr_sdf_frame* f = C.f;
+  const float *ray_o = C.ray_o, *ray_d = C.ray_d, *near_ = C.near_, *far_ = C.far_;
+  const int R = C.R;
+  const anr_render_opts* o = C.o;
+  const bool step = C.mode == STEP, net_fwd = C.mode == NET_FWD;
+  const STLayout L = stlayout(R, C.chunk);
+  if (C.ws_bytes < L.total) return fail(ANR_E_WORKSPACE, "sdf train: workspace too small");
+  hipStream_t s = C.s;
+  char* ws = (char*)C.ws;
   auto F = [&](size_t off) { return (float*)(ws + off); };
   const long N = L.N;
-  const int nch = (R + o->chunk - 1) / o->chunk;
+  const int nch = (R + C.chunk - 1) / C.chunk;
   int* counts = (int*)(ws + L.counts);
   const float* const* tp = p->t;
   float* wimg = F(L.wimg);
   float* fold = F(L.fold);
   float* tbtab = F(L.tbtab);
-  float4* raw = (float4*)F(L.raw);
-  float* sdf = F(L.sdf);
+  float4* raw = net_fwd ? (float4*)C.raw_out : (float4*)F(L.raw);
+  float* sdf = net_fwd ? C.sdf_out : F(L.sdf);
   float* acc = F(L.acc);
   float* acc3 = F(L.acc3);
   if (hipMemsetAsync(ws + L.counts, 0, 16, s) != hipSuccess ||
@@ -626,13 +684,15 @@ int anr_sdf_train_step(const anr_sdf_params* p, float* const* grads, const anr_s
   for (int i = 0; i < ANR_SDF_NUM_TENSORS; ++i) T.t[i] = tp[i];
   hipLaunchKernelGGL(k_sdf_wnorm, dim3(sdf_wn_rows()), dim3(256), 0, s, T, wimg);
   hipLaunchKernelGGL(k_sdf_fold, dim3(3), dim3(256), 0, s, T, (const float*)wimg, f->poses, f->latent_index, fold);
-  hipLaunchKernelGGL(k_sdf_tbtab, dim3(1), dim3(64), 0, s, f->tbounds, nch, tbtab, out->tbounds_out);
+  hipLaunchKernelGGL(k_sdf_tbtab, dim3(1), dim3(64), 0, s, f->tbounds, nch, tbtab,
+                     step ? C.out->tbounds_out : (net_fwd ? C.tb_out : nullptr));
   ANR_TRY(check_launch("sdf train prep"));
 
   // ---- B1 front-end (KNN keep mask) + ordered compaction; one host read of n'
   SdfFrontArgs fa{};
   fa.ray_o = ray_o; fa.ray_d = ray_d; fa.near_ = near_; fa.far_ = far_; fa.t_rand = o->t_rand;
-  fa.n_rays = R; fa.chunk = o->chunk; fa.R = f->R; fa.Th = f->Th; fa.verts = f->pvertices; fa.nv = f->n_verts;
+  fa.wpts = C.wpts; fa.n_pts = C.n_pts;
+  fa.n_rays = R; fa.chunk = C.chunk; fa.R = f->R; fa.Th = f->Th; fa.verts = f->pvertices; fa.nv = f->n_verts;
   fa.norm_th = o->norm_th; fa.mask = (uint64_t*)(ws + L.mask); fa.chunk_min = (uint64_t*)(ws + L.chunk_min);
   fa.knn = (uint32_t*)(ws + L.knn); fa.raw = raw; fa.sdf = sdf;
   int cus = 256;
@@ -645,7 +705,7 @@ int anr_sdf_train_step(const anr_sdf_params* p, float* const* grads, const anr_s
   hipLaunchKernelGGL(k_sdf_front, dim3(std::min(cus, (R + 15) / 16)), dim3(1024), 0, s, fa);
   ANR_TRY(check_launch("k_sdf_front (train)"));
   CompactArgs ca{};
-  ca.n_rays = R; ca.chunk = o->chunk; ca.mask = fa.mask; ca.chunk_min = fa.chunk_min;
+  ca.n_rays = R; ca.chunk = C.chunk; ca.mask = fa.mask; ca.chunk_min = fa.chunk_min;
   ca.ray_off = (int*)(ws + L.ray_off); ca.block_sum = (int*)(ws + L.block_sum); ca.list = (int*)(ws + L.list);
   const int nb = (R + 255) / 256;
   hipLaunchKernelGGL(k_count, dim3(nb), dim3(256), 0, s, ca);
@@ -673,7 +733,8 @@ int anr_sdf_train_step(const anr_sdf_params* p, float* const* grads, const anr_s
 
   SdfPointArgs a{};
   a.list = ca.list; a.b0 = 0; a.cnt = n;
-  a.ray_o = ray_o; a.ray_d = ray_d; a.near_ = near_; a.far_ = far_; a.t_rand = o->t_rand; a.chunk = o->chunk;
+  a.ray_o = ray_o; a.ray_d = ray_d; a.near_ = near_; a.far_ = far_; a.t_rand = o->t_rand; a.chunk = C.chunk;
+  a.wpts = C.wpts; a.vdir = C.vdir; a.n_pts = C.n_pts;
   a.R = f->R; a.Th = f->Th; a.A = f->A; a.bigA = f->big_A; a.weights = f->weights; a.knn = fa.knn;
   a.wimg = wimg; a.tbtab = tbtab;
   a.ptb = F(L.ptb); a.Gr = F(L.Gr); a.Yr = F(L.Yr); a.Xs0 = F(L.Xs0); a.X4 = Hs(3); a.C0 = F(L.C0);
@@ -830,36 +891,49 @@ int anr_sdf_train_step(const anr_sdf_params* p, float* const* grads, const anr_s
     hipLaunchKernelGGL(k_sdf_raw, pg, pb, 0, s, a);
     ANR_TRY(check_launch("k_sdf_raw (train)"));
   }
-  // compositing, image loss and d rgb_map
-  const anr_render_out ro{out->rgb_map, out->acc_map, out->depth_map, nullptr};
-  ANR_TRY(stage_composite(near_, far_, R, o, raw, &ro, nullptr, s));
-  TrainBufs tb{};
-  tb.raw = raw; tb.draw = (float4*)F(L.draw); tb.n_rays = R; tb.rgb_map = out->rgb_map; tb.d_rgb_map = F(L.drgb);
-  tb.n_kept = counts;
-  const int gx = (R + 255) / 256;
-  hipLaunchKernelGGL(k_tr_loss, dim3(gx, 1), dim3(256), 0, s, tb, rgb_gt, mask_at_box, acc3);
-  hipLaunchKernelGGL(k_tr_loss_grads, dim3(gx, 1), dim3(256), 0, s, tb, rgb_gt, mask_at_box, (const float*)acc3,
-                     F(L.drgb), nullptr, nullptr);
-  hipLaunchKernelGGL(k_tr_composite_bwd, dim3((R + 3) / 4), dim3(256), 0, s, tb);
-  ANR_TRY(check_launch("sdf train: image loss / compositing backward"));
-  // msk_sdf lists: per-ray min / argmin / flags, entry count
-  hipLaunchKernelGGL(k_st_msk_rays, dim3((R + 3) / 4), dim3(256), 0, s, (const float*)sdf, f->occupancy, R, F(L.rmin),
-                     (int*)(ws + L.ramin), (uint8_t*)(ws + L.rflag), acc);
-  ANR_TRY(check_launch("k_st_msk_rays"));
   float alpha = 50.f;
-  for (int m : {10000, 20000, 30000, 40000, 50000})
-    if (iter_step > m) alpha *= 2.f;
+  const float4* draw = (const float4*)F(L.draw);
+  if (step) {
+    // compositing, image loss and d rgb_map
+    const anr_sdf_render_out* out = C.out;
+    const anr_render_out ro{out->rgb_map, out->acc_map, out->depth_map, nullptr};
+    ANR_TRY(stage_composite(near_, far_, R, o, raw, &ro, nullptr, s));
+    TrainBufs tb{};
+    tb.raw = raw; tb.draw = (float4*)F(L.draw); tb.n_rays = R; tb.rgb_map = out->rgb_map; tb.d_rgb_map = F(L.drgb);
+    tb.n_kept = counts;
+    const int gx = (R + 255) / 256;
+    hipLaunchKernelGGL(k_tr_loss, dim3(gx, 1), dim3(256), 0, s, tb, C.rgb_gt, C.mask_at_box, acc3);
+    hipLaunchKernelGGL(k_tr_loss_grads, dim3(gx, 1), dim3(256), 0, s, tb, C.rgb_gt, C.mask_at_box, (const float*)acc3,
+                       F(L.drgb), nullptr, nullptr);
+    hipLaunchKernelGGL(k_tr_composite_bwd, dim3((R + 3) / 4), dim3(256), 0, s, tb);
+    ANR_TRY(check_launch("sdf train: image loss / compositing backward"));
+    // msk_sdf lists: per-ray min / argmin / flags, entry count
+    hipLaunchKernelGGL(k_st_msk_rays, dim3((R + 3) / 4), dim3(256), 0, s, (const float*)sdf, f->occupancy, R, F(L.rmin),
+                       (int*)(ws + L.ramin), (uint8_t*)(ws + L.rflag), acc);
+    ANR_TRY(check_launch("k_st_msk_rays"));
+    for (int m : {10000, 20000, 30000, 40000, 50000})
+      if (C.iter_step > m) alpha *= 2.f;
+  } else if (!net_fwd) {
+    if (C.d_raw) {
+      draw = (const float4*)C.d_raw;
+    } else if (hipMemsetAsync(F(L.draw), 0, (size_t)N * 16, s) != hipSuccess) {
+      return fail(ANR_E_HIP, "memset");
+    }
+  }
 
-  if (n > 0) {
+  if (n > 0 && !net_fwd) {
     // ---- backward: raw -> colour logits, sdf, beta; msk_sdf -> sdf
     StRaw sr{};
-    sr.list = ca.list; sr.n_kept = counts; sr.chunk = o->chunk; sr.draw = (const float4*)F(L.draw);
+    sr.list = ca.list; sr.n_kept = counts; sr.chunk = C.chunk; sr.draw = draw;
     sr.C0 = F(L.C0); sr.tbtab = tbtab; sr.Y8 = F(L.Y8); sr.Yc = F(L.Yc); sr.beta = tp[SDF_BETA];
     sr.dYc = F(L.dYc); sr.ds = F(L.ds); sr.dbeta = F(L.dbeta);
     hipLaunchKernelGGL(k_st_raw_bwd, pg, pb, 0, s, sr);
-    hipLaunchKernelGGL(k_st_msk_loss, dim3((R + 255) / 256), pb, 0, s, (const float*)F(L.rmin),
-                       (const int*)(ws + L.ramin), (const uint8_t*)(ws + L.rflag), (const int*)inv, R, alpha, F(L.ds),
-                       acc);
+    if (step)
+      hipLaunchKernelGGL(k_st_msk_loss, dim3((R + 255) / 256), pb, 0, s, (const float*)F(L.rmin),
+                         (const int*)(ws + L.ramin), (const uint8_t*)(ws + L.rflag), (const int*)inv, R, alpha, F(L.ds),
+                         acc);
+    else if (C.d_sdf)
+      hipLaunchKernelGGL(k_st_cotan_sdf, pg, pb, 0, s, (const int*)ca.list, (const int*)counts, C.d_sdf, F(L.ds));
     ANR_TRY(check_launch("sdf train: raw / msk backward"));
     // ---- colour net backward (weight-normed lin4..lin0; color_latent folded into lin3)
     float *dHa = F(L.dHa), *dHb = F(L.dHb), *bsum = F(L.bsum);
@@ -881,10 +955,15 @@ int anr_sdf_train_step(const anr_sdf_params* p, float* const* grads, const anr_s
     ANR_TRY(g.xgrad(n, F(L.dC0), 40, 33, dHb, 256, 256, WN(9), 289, 0));
     ANR_TRY(g.xgrad(n, F(L.dZ8) + 1, 264, 256, dHb, 256, 256, WN(9), 289, 33));
     // ---- loss adjoints of resd (offset) and gradients (eikonal + colour normals); d sdf into Z8 col 0
-    StLoss sl{};
-    sl.n_kept = counts; sl.resd = F(L.resd); sl.C0 = F(L.C0); sl.dC0 = F(L.dC0); sl.ds = F(L.ds);
-    sl.rbar = F(L.rbar); sl.dG = F(L.dG); sl.dZ8 = F(L.dZ8); sl.acc = acc;
-    hipLaunchKernelGGL(k_st_sample_loss, pg, pb, 0, s, sl);
+    if (step) {
+      StLoss sl{};
+      sl.n_kept = counts; sl.resd = F(L.resd); sl.C0 = F(L.C0); sl.dC0 = F(L.dC0); sl.ds = F(L.ds);
+      sl.rbar = F(L.rbar); sl.dG = F(L.dG); sl.dZ8 = F(L.dZ8); sl.acc = acc;
+      hipLaunchKernelGGL(k_st_sample_loss, pg, pb, 0, s, sl);
+    } else {
+      hipLaunchKernelGGL(k_st_cotan_rows, pg, pb, 0, s, (const int*)counts, C.d_resd, C.d_grad, (const float*)F(L.dC0),
+                         (const float*)F(L.ds), F(L.rbar), F(L.dG), F(L.dZ8));
+    }
     ANR_TRY(check_launch("k_st_sample_loss"));
     // ---- SDF: tangent pass along dG, stacked reverse -> SDF weights, d tpose
     if (hipMemsetAsync(F(L.tbar), 0, (size_t)n * 16, s) != hipSuccess) return fail(ANR_E_HIP, "memset");
@@ -937,7 +1016,7 @@ int anr_sdf_train_step(const anr_sdf_params* p, float* const* grads, const anr_s
     // forward: x_o -> resd -> t_o -> SDF (factors) -> g_t = grad_t sdf; og = g_t + J_resd^T g_t
     SdfPointArgs ao = a;
     ao.cnt = n_o; ao.ptb = F(L.ptbo); ao.Gr = F(L.Gro); ao.Yr = F(L.Yr); ao.resd_rows = F(L.ro);
-    ao.grad_rows = F(L.grow);
+    ao.grad_rows = F(L.gro);  // (not read: the main pass's gradient rows stay the call's output)
     ANR_TRY(resd_forward(n_o, F(L.Gro), F(L.Yr)));
     hipLaunchKernelGGL(k_sdf_mid, og_, pb, 0, s, ao);
     ANR_TRY(check_launch("k_sdf_mid (observed)"));
@@ -966,7 +1045,11 @@ int anr_sdf_train_step(const anr_sdf_params* p, float* const* grads, const anr_s
     float* og = F(L.og);
     hipLaunchKernelGGL(k_st_embed_bwd10, og_, pb, 0, s, (const float*)F(L.ptbo), 8L, (const float*)Gbar, 64L, n_o, og, 4L);
     hipLaunchKernelGGL(k_st_add3, og_, pb, 0, s, (const float*)F(L.tdot), 4L, (const float*)og, 4L, n_o, og);
-    hipLaunchKernelGGL(k_st_obs_loss, og_, pb, 0, s, (const float*)og, n_o, F(L.dog), acc);
+    if (net_fwd) return ANR_OK;  // og (n_o, 4) is an output of the call; the backward re-runs this
+    if (step)
+      hipLaunchKernelGGL(k_st_obs_loss, og_, pb, 0, s, (const float*)og, n_o, F(L.dog), acc);
+    else
+      hipLaunchKernelGGL(k_st_rows3to4, og_, pb, 0, s, C.d_og, n_o, F(L.dog));
     ANR_TRY(check_launch("sdf train: observed-gradient loss"));
     // tangent forward along dog: gamma_10 -> ReLU net (masks of the primal) -> tanh -> tdot -> SDF
     float* Grt = F(L.Grt);
@@ -1036,6 +1119,7 @@ int anr_sdf_train_step(const anr_sdf_params* p, float* const* grads, const anr_s
     }
   }
 
+  if (net_fwd) return ANR_OK;
   // ---- weight norm: effective-weight gradients -> weight_g / weight_v; beta; loss vector
   if (n > 0) {
     for (int l = 0; l < SDF_NUM_WN; ++l) {
@@ -1046,9 +1130,111 @@ int anr_sdf_train_step(const anr_sdf_params* p, float* const* grads, const anr_s
     hipLaunchKernelGGL(k_st_add_bias, dim3(1), dim3(256), 0, s, (const float*)F(L.dbeta), 1, grads[SDF_BETA]);
     ANR_TRY(check_launch("k_st_wn_grad"));
   }
+  if (!step) return check_launch("k_st_wn_grad");
   hipLaunchKernelGGL(k_st_loss_final, dim3(1), dim3(1), 0, s, (const float*)acc, (const float*)acc3, (const int*)counts,
-                     n_o, alpha, loss);
+                     n_o, alpha, C.loss);
   return check_launch("k_st_loss_final");
+}
+
+int check_net(const anr_sdf_params* p, const anr_sdf_frame* f, const anr_samples* x, const anr_render_opts* o, void* ws) {
+  if (!p || !f || !x || !o || !ws || !x->wpts || !x->viewdir) return fail(ANR_E_ARG, "sdf network train: NULL argument");
+  if (x->n_pts <= 0 || x->n_pts > (1 << 24)) return fail(ANR_E_ARG, "sdf network train: n must be in [1, 2^24]");
+  for (int i = 0; i < ANR_SDF_NUM_TENSORS; ++i)
+    if (!p->t[i] && i != SDF_RESD_LAT) return fail(ANR_E_ARG, "sdf network train: NULL parameter tensor");
+  if (!f->A || !f->big_A || !f->R || !f->Th || !f->poses || !f->pvertices || !f->weights || !f->tbounds ||
+      !f->latent_index)
+    return fail(ANR_E_ARG, "sdf network train: NULL frame tensor");
+  if (f->n_verts <= 0 || f->n_verts > 6912) return fail(ANR_E_ARG, "sdf network train: n_verts must be in [1, 6912]");
+  return ANR_OK;
+}
+
+TrainCore net_core(int mode, const anr_sdf_params* p, const anr_sdf_frame* f, const anr_samples* x,
+                   const anr_render_opts* o, void* ws, size_t ws_bytes, void* stream) {
+  TrainCore c{};
+  c.mode = mode; c.p = p; c.f = f; c.o = o;
+  c.wpts = x->wpts; c.vdir = x->viewdir; c.n_pts = x->n_pts;
+  c.R = (x->n_pts + 63) / 64; c.chunk = c.R;
+  c.ws = ws; c.ws_bytes = ws_bytes; c.s = (hipStream_t)stream;
+  return c;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t anr_sdf_train_workspace_bytes(int n_rays, const anr_render_opts* o) {
+  if (n_rays <= 0 || !o || o->chunk <= 0) return 0;
+  return stlayout(n_rays, o->chunk).total;
+}
+
+int anr_sdf_train_step(const anr_sdf_params* p, float* const* grads, const anr_sdf_frame* f, const float* ray_o,
+                       const float* ray_d, const float* near_, const float* far_, int R, const anr_render_opts* o,
+                       const float* rgb_gt, const uint8_t* mask_at_box, int iter_step, const anr_sdf_render_out* out,
+                       float* loss, void* workspace, size_t ws_bytes, void* stream) {
+  ANR_TRY(check_train(p, grads, f, ray_o, ray_d, near_, far_, R, o, rgb_gt, out, loss, workspace));
+  TrainCore c{};
+  c.mode = STEP; c.p = p; c.grads = grads; c.f = f;
+  c.ray_o = ray_o; c.ray_d = ray_d; c.near_ = near_; c.far_ = far_; c.R = R; c.chunk = o->chunk; c.o = o;
+  c.rgb_gt = rgb_gt; c.mask_at_box = mask_at_box; c.iter_step = iter_step; c.out = out; c.loss = loss;
+  c.ws = workspace; c.ws_bytes = ws_bytes; c.s = (hipStream_t)stream;
+  return sdf_train_core(c);
+}
+
+size_t anr_sdf_network_train_workspace_bytes(int n_pts) {
+  if (n_pts <= 0) return 0;
+  const int G = (n_pts + 63) / 64;
+  return stlayout(G, G).total;
+}
+
+int anr_sdf_network_train_fwd(const anr_sdf_params* p, const anr_sdf_frame* f, const anr_samples* x,
+                              const anr_render_opts* o, float* raw, float* sdf, float* tbounds_out, void* workspace,
+                              size_t ws_bytes, void* stream) {
+  ANR_TRY(check_net(p, f, x, o, workspace));
+  if (!raw || !sdf) return fail(ANR_E_ARG, "sdf network train: NULL output");
+  TrainCore c = net_core(NET_FWD, p, f, x, o, workspace, ws_bytes, stream);
+  c.raw_out = raw; c.sdf_out = sdf; c.tb_out = tbounds_out;
+  return sdf_train_core(c);
+}
+
+const int32_t* anr_sdf_network_train_counts(const void* workspace, int n_pts) {
+  if (!workspace || n_pts <= 0) return nullptr;
+  const int G = (n_pts + 63) / 64;
+  return (const int32_t*)((const char*)workspace + stlayout(G, G).counts);
+}
+
+int anr_sdf_network_train_rows(const void* workspace, int n_pts, float* resd, float* gradients,
+                               float* observed_gradients, void* stream) {
+  if (!workspace || n_pts <= 0) return fail(ANR_E_ARG, "anr_sdf_network_train_rows: bad arguments");
+  const int G = (n_pts + 63) / 64;
+  const STLayout L = stlayout(G, G);
+  const char* ws = (const char*)workspace;
+  hipStream_t s = (hipStream_t)stream;
+  int cnt[4];
+  if (hipMemcpyAsync(cnt, ws + L.counts, 16, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+    return fail(ANR_E_HIP, "anr_sdf_network_train_rows: count readback");
+  const int n = cnt[0], n_o = cnt[2];
+  if (resd && n > 0 && hipMemcpyAsync(resd, ws + L.resd, (size_t)n * 12, hipMemcpyDeviceToDevice, s) != hipSuccess)
+    return fail(ANR_E_HIP, "anr_sdf_network_train_rows: copy");
+  if (gradients && n > 0 && hipMemcpyAsync(gradients, ws + L.grow, (size_t)n * 12, hipMemcpyDeviceToDevice, s) != hipSuccess)
+    return fail(ANR_E_HIP, "anr_sdf_network_train_rows: copy");
+  if (observed_gradients && n_o > 0 &&
+      hipMemcpy2DAsync(observed_gradients, 12, ws + L.og, 16, 12, (size_t)n_o, hipMemcpyDeviceToDevice, s) != hipSuccess)
+    return fail(ANR_E_HIP, "anr_sdf_network_train_rows: copy");
+  return ANR_OK;
+}
+
+int anr_sdf_network_train_bwd(const anr_sdf_params* p, float* const* grads, const anr_sdf_frame* f, const anr_samples* x,
+                              const anr_render_opts* o, const float* d_raw, const float* d_sdf, const float* d_resd,
+                              const float* d_gradients, const float* d_observed_gradients, void* workspace,
+                              size_t ws_bytes, void* stream) {
+  ANR_TRY(check_net(p, f, x, o, workspace));
+  if (!grads) return fail(ANR_E_ARG, "sdf network train: NULL gradients");
+  for (int i = 0; i < ANR_SDF_NUM_TENSORS; ++i)
+    if (!grads[i] && i != SDF_RESD_LAT) return fail(ANR_E_ARG, "sdf network train: NULL gradient tensor");
+  TrainCore c = net_core(NET_BWD, p, f, x, o, workspace, ws_bytes, stream);
+  c.grads = grads;
+  c.d_raw = d_raw; c.d_sdf = d_sdf; c.d_resd = d_resd; c.d_grad = d_gradients; c.d_og = d_observed_gradients;
+  return sdf_train_core(c);
 }
 
 }  // extern "C"

@@ -1,9 +1,10 @@
 """sdf_pdf network plugin (config 5) with the reference parameter layout
 (``lib/networks/bw_deform/anisdf_pdf_network.py:13-36, 253-269, 340-520``).
 
-Like ``network.Network`` the modules only own the parameters under the reference state_dict names,
+Like ``network.Network`` the modules own the parameters under the reference state_dict names,
 shapes and order (so ``load_network(strict=True)`` reads a reference ``latest.pth``); the render runs
-in the HIP library (``renderer_sdf.Renderer``). Weight-normed layers keep the ``weight_g`` /
+in the HIP library (``renderer_sdf.Renderer``), and ``Network.forward(wpts, viewdir, dists, batch)`` --
+the per-chunk call of a reference ``tpose_renderer`` -- runs there too. Weight-normed layers keep the ``weight_g`` /
 ``weight_v`` pair of ``nn.utils.weight_norm``; the effective weight ``v * (g / |v|_row)`` is formed
 on the device per render call.
 """
@@ -68,6 +69,7 @@ class Network(nn.Module):
     def __init__(self, cfg=None):
         super().__init__()
         cfg = cfg if cfg is not None else _config.active()
+        self.__dict__['_anr_cfg'] = cfg
         nlc = int(cfg.get('num_latent_code', -1))
         if nlc < 0:
             nlc = int(cfg.num_train_frame)  # config.py:144-145
@@ -86,6 +88,22 @@ class Network(nn.Module):
         assert len(ts) == self.TENSOR_ORDER_LEN, len(ts)
         return ts
 
-    def forward(self, *args, **kwargs):
-        raise RuntimeError('Network is a parameter container on this backend; call '
-                           'renderer_sdf.Renderer(net).render(batch) (tpose_renderer.py:159) instead')
+    def __getstate__(self):
+        state = dict(super().__getstate__())
+        state.pop('_anr_renderer', None)  # a copy builds its own device renderer
+        return state
+
+    def _device(self):
+        r = self.__dict__.get('_anr_renderer')
+        if r is None:
+            from .renderer_sdf import Renderer
+            r = Renderer(self, self.__dict__['_anr_cfg'])
+            self.__dict__['_anr_renderer'] = r
+        return r
+
+    def forward(self, wpts, viewdir, dists, batch):
+        """anisdf_pdf_network.py:156-224: one reference network call over n free samples (the call
+        tpose_renderer.py:95 makes per chunk) -> {'raw' (1,n,4), 'sdf' (1,n,1), 'resd' (1,n',3), 'gradients'
+        (1,n',3)} (+ 'observed_gradients' under autograd); widens batch['tbounds'] in place. On the HIP
+        library (renderer_sdf.Renderer.network_forward); differentiable w.r.t. the parameters when training."""
+        return self._device().network_forward(wpts, viewdir, dists, batch)

@@ -231,44 +231,53 @@ class Renderer:
     def _render_overlapped(self, batch, R, chunk):
         """render_device over parts of whole chunks (per-chunk semantics unchanged: the rows of the parts,
         concatenated in order, are the whole frame's, as parallel.render_sharded relies on), each part's
-        outputs copied on a side stream into page-locked host buffers while the next part renders."""
+        per-ray outputs copied on a side stream into page-locked host buffers while the next part
+        renders. The alpha_ind rows (pbw / tbw) are counted only as each part finishes, so they stay
+        on the device until the frame's row count is known and then cross into exact-size page-locked
+        buffers (no capacity-sized host allocation is held by the returned tensors)."""
         from .parallel import RAY_KEYS as SLICED, shard_chunks
         dev = self.device()
         ns = int(self.cfg.N_samples)
-        if getattr(self, '_copy_stream', None) is None:
-            self._copy_stream = torch.cuda.Stream(dev)
-        cs = self._copy_stream
-        # fresh page-locked outputs per call (torch's caching host allocator recycles freed ones); the
-        # row count is known only part by part, so pbw / tbw are views of capacity-sized buffers
-        pin = dict(dtype=torch.float32, pin_memory=True)
-        h = {'rgb_map': torch.empty((1, R, 3), **pin), 'acc_map': torch.empty((1, R), **pin),
-             'depth_map': torch.empty((1, R), **pin), 'raw': torch.empty((1, R * ns, 4), **pin),
-             'pbw': torch.empty((1, R * ns, 24), **pin), 'tbw': torch.empty((1, R * ns, 24), **pin)}
-        keep, m_off, kept = [], 0, 0
-        for k in range(self.HOST_PARTS):
-            a, b = shard_chunks(R, k, self.HOST_PARTS, chunk)
-            if a >= b:
-                continue
-            sub = {key_: (v[:, a:b] if key_ in SLICED and torch.is_tensor(v) else v) for key_, v in batch.items()}
-            out = self.render_device(sub)  # reads the part's row count: the part has finished when it returns
-            m = out['pbw'].shape[1]
-            ev = torch.cuda.Event()
-            ev.record()
+        with torch.cuda.device(dev):
+            if getattr(self, '_copy_stream', None) is None:
+                self._copy_stream = torch.cuda.Stream(dev)
+            cs = self._copy_stream
+            cur = torch.cuda.current_stream(dev)
+            pin = dict(dtype=torch.float32, pin_memory=True)
+            h = {'rgb_map': torch.empty((1, R, 3), **pin), 'acc_map': torch.empty((1, R), **pin),
+                 'depth_map': torch.empty((1, R), **pin), 'raw': torch.empty((1, R * ns, 4), **pin)}
+            keep, rows, kept = [], [], 0
+            for k in range(self.HOST_PARTS):
+                a, b = shard_chunks(R, k, self.HOST_PARTS, chunk)
+                if a >= b:
+                    continue
+                sub = {key_: (v[:, a:b] if key_ in SLICED and torch.is_tensor(v) else v) for key_, v in batch.items()}
+                out = self.render_device(sub)  # reads the part's row count: the part has finished when it returns
+                ev = torch.cuda.Event()
+                ev.record(cur)
+                with torch.cuda.stream(cs):
+                    cs.wait_event(ev)
+                    h['rgb_map'][:, a:b].copy_(out['rgb_map'], non_blocking=True)
+                    h['acc_map'][:, a:b].copy_(out['acc_map'], non_blocking=True)
+                    h['depth_map'][:, a:b].copy_(out['depth_map'], non_blocking=True)
+                    h['raw'][:, a * ns:b * ns].copy_(out['raw'], non_blocking=True)
+                keep.append(out)  # device outputs stay alive until their copies are done
+                rows.append((out['pbw'], out['tbw']))
+                kept += self.last_counts[0]
+            m = sum(p.shape[1] for p, _ in rows)
+            h['pbw'] = torch.empty((1, m, 24), **pin)
+            h['tbw'] = torch.empty((1, m, 24), **pin)
             with torch.cuda.stream(cs):
-                cs.wait_event(ev)
-                h['rgb_map'][:, a:b].copy_(out['rgb_map'], non_blocking=True)
-                h['acc_map'][:, a:b].copy_(out['acc_map'], non_blocking=True)
-                h['depth_map'][:, a:b].copy_(out['depth_map'], non_blocking=True)
-                h['raw'][:, a * ns:b * ns].copy_(out['raw'], non_blocking=True)
-                h['pbw'][:, m_off:m_off + m].copy_(out['pbw'], non_blocking=True)
-                h['tbw'][:, m_off:m_off + m].copy_(out['tbw'], non_blocking=True)
-            keep.append(out)  # device outputs stay alive until their copies are done
-            m_off += m
-            kept += self.last_counts[0]
-        cs.synchronize()
-        self.last_counts = (kept, m_off)
-        return {'rgb_map': h['rgb_map'], 'acc_map': h['acc_map'], 'depth_map': h['depth_map'], 'raw': h['raw'],
-                'pbw': h['pbw'][:, :m_off], 'tbw': h['tbw'][:, :m_off]}
+                cs.wait_stream(cur)
+                off = 0
+                for p, t in rows:
+                    n = p.shape[1]
+                    h['pbw'][:, off:off + n].copy_(p, non_blocking=True)
+                    h['tbw'][:, off:off + n].copy_(t, non_blocking=True)
+                    off += n
+            cs.synchronize()
+        self.last_counts = (kept, m)
+        return h
 
     def counts(self, n_rays):
         """(kept samples, alpha_ind rows) of the last evaluation render (device read, syncs)."""
@@ -350,15 +359,18 @@ def to_host(ret):
     """the eval outputs on the CPU, as tpose_renderer.py:154-155 leaves them: copied into page-locked
     buffers (torch's caching host allocator reuses them call after call) with one stream sync, so the
     ~1.4 GB of a 512x512 frame (raw + pbw / tbw rows) moves at the link's DMA rate."""
-    out = {}
+    out, devs = {}, set()
     for k, v in ret.items():
         if v.is_cuda:
             h = torch.empty(v.shape, dtype=v.dtype, pin_memory=True)
-            h.copy_(v, non_blocking=True)
+            with torch.cuda.device(v.device):  # the copy runs on (and is awaited on) v's device's stream
+                h.copy_(v, non_blocking=True)
+            devs.add(v.device)
             out[k] = h
         else:
             out[k] = v
-    torch.cuda.current_stream().synchronize()
+    for d in devs:
+        torch.cuda.current_stream(d).synchronize()
     return out
 
 

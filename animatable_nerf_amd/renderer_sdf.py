@@ -148,6 +148,83 @@ class Renderer:
         off = addr - self._ws.data_ptr()
         return self._ws[off:off + R * 64 * 32].view(torch.int32).view(R * 64, 8)
 
+    # ---- Network.forward over free samples (anisdf_pdf_network.py:156-224) ------------------------
+    def _net_frame(self, batch):
+        """SdfFrame of one Network.forward call (no rays): the frame tensors, tbounds as a private copy
+        (the call widens batch['tbounds'] in place; a backward re-run needs the bounds it started from)."""
+        dev = self.device()
+        fr = {k: _f32(batch[k], dev) for k in FRAME_KEYS}
+        fr['tbounds'] = fr['tbounds'].clone()
+        li = batch['latent_index'].to(device=dev, dtype=torch.int64).reshape(-1).contiguous()
+        f = _lib.SdfFrame()
+        for k in FRAME_KEYS:
+            setattr(f, k, fr[k].data_ptr())
+        f.n_verts = fr['pvertices'].shape[-2]
+        f.latent_index, f.occupancy = li.data_ptr(), None
+        o = _lib.RenderOpts()
+        o.n_samples, o.chunk, o.norm_th, o.train_th = int(self.cfg.N_samples), 1, NORM_TH, 0.0
+        o.t_rand, o.novel_pose = None, 0
+        rprec = self.cfg.get('render_precision', 'fp32')
+        if rprec not in ('fp32', 'bf16x3'):
+            raise ValueError(f"render_precision must be 'fp32' or 'bf16x3', got {rprec!r}")
+        o.precision = _lib.BF16X3 if rprec == 'bf16x3' else _lib.FP32
+        return {'fr': fr, 'li': li, 'frame': f, 'opts': o}
+
+    @staticmethod
+    def _samples(wpts, viewdir, dists, dev):
+        wp = _f32(wpts, dev).reshape(-1, 3)
+        vd = _f32(viewdir, dev).reshape(-1, 3)
+        n = wp.shape[0]
+        if vd.shape[0] != n or dists.numel() != n:
+            raise ValueError(f'Network.forward: wpts {tuple(wpts.shape)}, viewdir {tuple(viewdir.shape)}, '
+                             f'dists {tuple(dists.shape)} disagree on the sample count')
+        if n == 0:
+            raise ValueError('Network.forward: no samples')
+        return wp, vd, _lib.Samples(wp.data_ptr(), vd.data_ptr(), None, n)
+
+    def network_forward(self, wpts, viewdir, dists, batch):
+        """``Network.forward(wpts (n,3), viewdir (n,3), dists (n), batch)`` of anisdf_pdf_network (:156-224)
+        -> {'raw' (1,n,4), 'sdf' (1,n,1), 'resd' (1,n',3), 'gradients' (1,n',3)} (+ 'observed_gradients'
+        (1,n_o,3) under autograd when a kept sample has |sdf| < 0.02, :194-199); ``batch['tbounds']`` is
+        widened by 0.05 in place, once per call (:204-206). One call = one reference chunk (the forced
+        argmin spans the call). Under autograd with a training network: the layer-wise exact-fp32 executor
+        (anr_sdf_network_train_fwd / _bwd), differentiable w.r.t. every parameter with the second-order
+        terms of the reference's create_graph input gradients; else anr_sdf_network_fwd (render
+        precision). ``dists`` is not read (the density uses the constant 0.005, :330)."""
+        if torch.is_grad_enabled() and self.net.training and any(p.requires_grad for p in self.net.parameters()):
+            outs = _SdfTrainNetwork.apply(self, batch, (wpts, viewdir, dists), *self.net.tensors())
+            raw, sdf, resd, grad, og = outs
+            ret = {'raw': raw, 'sdf': sdf, 'resd': resd, 'gradients': grad}
+            if og.shape[1] > 0:
+                ret['observed_gradients'] = og
+            return ret
+        with torch.no_grad():
+            p = self.params()
+            dev = self.device()
+            c = self._net_frame(batch)
+            wp, vd, x = self._samples(wpts, viewdir, dists, dev)
+            n = x.n_pts
+            raw = torch.empty((1, n, 4), device=dev)
+            sdf = torch.empty((1, n, 1), device=dev)
+            tb_out = torch.empty((2, 3), device=dev)
+            ws_bytes = self.lib.anr_sdf_network_workspace_bytes(n, ctypes.byref(c['opts']))
+            if self._ws is None or self._ws.numel() < ws_bytes or self._ws.device != dev:
+                self._ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+            ws = self._ws
+            st = _lib.stream_ptr(dev)
+            _lib.check(self.lib.anr_sdf_network_fwd(ctypes.byref(p), ctypes.byref(c['frame']), ctypes.byref(x),
+                                                    ctypes.byref(c['opts']), _lib.ptr(raw), _lib.ptr(sdf), _lib.ptr(tb_out),
+                                                    _lib.ptr(ws), ws_bytes, st), 'anr_sdf_network_fwd')
+            addr = self.lib.anr_sdf_network_counts(_lib.ptr(ws), n)
+            n_kept = int(ws[addr - ws.data_ptr():addr - ws.data_ptr() + 4].view(torch.int32).item())  # host sync
+            self.last_counts = (n_kept, 0)
+            resd = torch.empty((1, n_kept, 3), device=dev)
+            grad = torch.empty((1, n_kept, 3), device=dev)
+            _lib.check(self.lib.anr_sdf_network_rows(_lib.ptr(ws), n, _lib.ptr(resd), _lib.ptr(grad), st),
+                       'anr_sdf_network_rows')
+            batch['tbounds'].copy_(tb_out.view_as(batch['tbounds']))
+        return {'raw': raw, 'sdf': sdf, 'resd': resd, 'gradients': grad}
+
     def render(self, batch):
         if torch.is_grad_enabled() and any(p.requires_grad for p in self.net.parameters()) and self.net.training:
             raise RuntimeError('sdf_pdf training runs as one fused step: use trainer_sdf.NetworkWrapper(net) '
@@ -157,3 +234,56 @@ class Renderer:
             ret = self.render_device(batch)
         from .renderer import to_host
         return to_host(ret)
+
+
+class _SdfTrainNetwork(torch.autograd.Function):
+    """sdf_pdf Network.forward under autograd: forward = anr_sdf_network_train_fwd (raw, sdf, resd,
+    gradients, observed_gradients), backward = anr_sdf_network_train_bwd from the upstream adjoints of
+    all five (parameter gradients; the inputs wpts / viewdir / dists get none: the reference's renderer
+    builds them without grad)."""
+
+    @staticmethod
+    def forward(ctx, renderer, batch, samples, *params):
+        lib = renderer.lib
+        p = renderer.params()
+        dev = params[0].device
+        c = renderer._net_frame(batch)
+        wp, vd, x = renderer._samples(*samples, dev)
+        n = x.n_pts
+        ws_bytes = lib.anr_sdf_network_train_workspace_bytes(n)
+        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)  # owned by this forward until its backward
+        raw = torch.empty((1, n, 4), device=dev)
+        sdf = torch.empty((1, n, 1), device=dev)
+        tb_out = torch.empty((2, 3), device=dev)
+        st = _lib.stream_ptr(dev)
+        _lib.check(lib.anr_sdf_network_train_fwd(ctypes.byref(p), ctypes.byref(c['frame']), ctypes.byref(x),
+                                                 ctypes.byref(c['opts']), _lib.ptr(raw), _lib.ptr(sdf), _lib.ptr(tb_out),
+                                                 _lib.ptr(ws), ws_bytes, st), 'anr_sdf_network_train_fwd')
+        addr = lib.anr_sdf_network_train_counts(_lib.ptr(ws), n)
+        cnt = ws[addr - ws.data_ptr():addr - ws.data_ptr() + 16].view(torch.int32).cpu()  # host sync
+        n_kept, n_obs = int(cnt[0]), int(cnt[2])
+        renderer.last_counts = (n_kept, n_obs)
+        resd = torch.empty((1, n_kept, 3), device=dev)
+        grad = torch.empty((1, n_kept, 3), device=dev)
+        og = torch.empty((1, n_obs, 3), device=dev)
+        _lib.check(lib.anr_sdf_network_train_rows(_lib.ptr(ws), n, _lib.ptr(resd), _lib.ptr(grad), _lib.ptr(og), st),
+                   'anr_sdf_network_train_rows')
+        with torch.no_grad():
+            batch['tbounds'].copy_(tb_out.view_as(batch['tbounds']))
+        ctx.renderer, ctx.c, ctx.samples, ctx.ws, ctx.ws_bytes = renderer, c, (wp, vd, x), ws, ws_bytes
+        return raw, sdf, resd, grad, og
+
+    @staticmethod
+    def backward(ctx, d_raw, d_sdf, d_resd, d_grad, d_og):
+        r, c = ctx.renderer, ctx.c
+        params = r.net.tensors()
+        dev = params[0].device
+        p = r.params()
+        grads = [torch.zeros_like(t) for t in params]
+        gp = (ctypes.c_void_p * _lib.NUM_SDF_TENSORS)(*[g.data_ptr() for g in grads])
+        keep = [t.contiguous() if t is not None else None for t in (d_raw, d_sdf, d_resd, d_grad, d_og)]
+        _lib.check(r.lib.anr_sdf_network_train_bwd(ctypes.byref(p), gp, ctypes.byref(c['frame']),
+                                                   ctypes.byref(ctx.samples[2]), ctypes.byref(c['opts']),
+                                                   *[_lib.ptr(t) for t in keep], _lib.ptr(ctx.ws), ctx.ws_bytes,
+                                                   _lib.stream_ptr(dev)), 'anr_sdf_network_train_bwd')
+        return (None, None, None, *grads)

@@ -137,14 +137,22 @@ class FusedStep:
         self.t, self.lr = int(tl[0]), float(tl[1])
 
     _STATIC_KEYS = RAY_KEYS + FRAME_KEYS + ('latent_index', 'rgb', 'mask_at_box')
+    _OPT_KEYS = ('bw_latent_index',)  # read by _Call when present
 
     _DIRECT_CACHE = 8  # distinct batches whose direct calls are kept
 
     def _direct_call(self, batch, t_rand):
         """Without graph replay (the default; ANR_TRAIN_GRAPH=1 takes _static_call) the step reads the
-        batch's own device tensors: one _Call per distinct batch (tensor identities and versions),
-        kept for the next steps that see it, so no step spends device copies on its inputs (the
-        fixed-buffer copies cost ~0.17 ms of a 2 ms step, measured)."""
+        batch's own device tensors: one _Call per distinct batch, kept for the next steps that see it,
+        so no step spends device copies on its inputs (the fixed-buffer copies cost ~0.17 ms of a 2 ms
+        step, measured).
+
+        Only a batch whose inputs all live on the step's device is cached: then the key (address,
+        version counter, dtype and shape of every input) names live memory, because the entry holds
+        the input tensors themselves (no other tensor can take their addresses while it lives), and
+        any conversion _Call made (bool mask -> uint8, int64 indices) is of a device tensor whose
+        in-place writes bump its version. A batch with host tensors is converted afresh every step
+        (writes through numpy views of host tensors do not bump versions)."""
         dev = self.flat.device
         R = batch['ray_o'].shape[1]
         ns = int(self.cfg.N_samples)
@@ -155,17 +163,24 @@ class FusedStep:
             tr.copy_(t_rand.reshape(R, ns))
         elif self.cfg.perturb > 0:
             tr.uniform_()
-        key = (tuple((batch[k].data_ptr(), batch[k]._version, str(batch[k].device)) for k in self._STATIC_KEYS),
-               tuple(self.cfg.get(k, None) for k in ('train_precision', 'chunk', 'N_samples', 'norm_th', 'train_th')))
-        ent = self._calls.pop(key, None)
+        srcs = tuple(batch[k] for k in self._STATIC_KEYS) + tuple(batch[k] for k in self._OPT_KEYS if k in batch)
+        cfg_key = tuple(self.cfg.get(k, None) for k in ('train_precision', 'chunk', 'N_samples', 'norm_th', 'train_th',
+                                                        'test_novel_pose'))
+        cacheable = all(torch.is_tensor(v) and v.device == dev for v in srcs)
+        key = None
+        if cacheable:
+            key = (tuple((v.data_ptr(), v._version, v.dtype, tuple(v.shape)) for v in srcs),
+                   tuple(k for k in self._OPT_KEYS if k in batch), cfg_key)
+        ent = self._calls.pop(key, None) if cacheable else None
         if ent is None:
             c = _Call(self.renderer, batch, tr)
             rgb = batch['rgb'].to(device=dev, dtype=torch.float32).contiguous()
             mask = batch['mask_at_box'].to(device=dev, dtype=torch.uint8).reshape(-1).contiguous()
-            ent = (c, rgb, mask, batch)  # the batch stays referenced: its storage (the key) is not reused
-        self._calls[key] = ent  # most recent last
-        while len(self._calls) > self._DIRECT_CACHE:
-            self._calls.pop(next(iter(self._calls)))
+            ent = (c, rgb, mask, srcs)  # the source tensors stay referenced: their addresses are not reused
+        if cacheable:
+            self._calls[key] = ent  # most recent last
+            while len(self._calls) > self._DIRECT_CACHE:
+                self._calls.pop(next(iter(self._calls)))
         c, rgb, mask, _ = ent
         c.opts.t_rand = tr.data_ptr() if (t_rand is not None or self.cfg.perturb > 0) else None
         return c, rgb, mask

@@ -89,6 +89,9 @@ def parse():
                     help='fp32: exact fp32 MFMA; bf16x3: T-pose BW MLP + NeRF as hi/lo-split bf16 MFMA '
                          '(outputs within the 1e-4 fp32 tolerance, tests/test_gpu_render.py)')
     ap.add_argument('--train-rays', type=int, default=1024)
+    ap.add_argument('--subject', choices=('aninerf_313', 'aninerf_s9p'), default=None,
+                    help='train mode network shapes (config.SUBJECTS): default aninerf_313 at N=1 (config 3), '
+                         'aninerf_s9p at N>1 (config 4)')
     ap.add_argument('--precision', choices=('fp32', 'bf16', 'bf16_all'), default='bf16',
                     help='training GEMM operand precision (config 3 is bf16, the pose-space blend-weight MLP kept at '
                          'fp32 level; bf16_all: that MLP in bf16 too; fp32 = exact reference arithmetic)')
@@ -411,14 +414,13 @@ def bench_train(args, rank, world, dev):
                             nr.cpu().numpy()[:args.train_rays], fr.cpu().numpy()[:args.train_rays],
                             rgb=rgb[m_np][:args.train_rays])
         batches.append({k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in b.items()})
-    net = network.Network()
+    subject = args.subject or ('aninerf_313' if world == 1 else 'aninerf_s9p')
+    cfg = config.subject(subject, perturb=1, train_precision=args.precision)
+    net = network.Network(cfg)
     sd = synthetic.init_state_dict({k: tuple(v.shape) for k, v in net.state_dict().items()})
     network.load_numpy_state(net, sd)
     net = net.to(dev)
     net.train()
-    cfg = config.defaults()
-    cfg.perturb = 1
-    cfg.train_precision = args.precision
     step = FusedStep(net, cfg)
     for j in range(args.warmup):
         step.step(batches[j % nb])
@@ -448,7 +450,8 @@ def bench_train(args, rank, world, dev):
         'value': R * 64 * args.steps * world / dt_max, 'unit': 'ray-samples/s', 'n_gpus': world, 'steps': args.steps,
         'warmup': args.warmup, 'ms_per_step': dt_max / args.steps * 1e3, 'higher_is_better': True, 'scaling': 'weak',
         'vs_baseline': None, 'dtype': args.precision, 'data': 'synthetic',
-        'config': {'workload': 'aninerf training step (configs 3/4 shape: 1024 rays/GPU, perturb 1, Adam)',
+        'config': {'workload': f'{subject} training step (config {3 if world == 1 else 4}: 1024 rays/GPU, perturb 1, Adam)',
+                   'subject': subject, 'num_train_frame': int(cfg.num_train_frame),
                    'precision': f'{args.precision} GEMM operands, fp32 accumulation / master weights / Adam',
                    'rays_per_gpu': R, 'kept_samples_last_step': n_kept,
                    'parallelism': f'dp{world} (RCCL mean all-reduce of the flat gradient blob)'},
@@ -483,10 +486,7 @@ def bench_sdf(args, rank, world, dev):
     batch = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in b.items()}
     tb0 = batch['tbounds'].clone()
     R = int(batch['ray_o'].shape[1])
-    cfg = config.defaults()
-    cfg.num_train_frame = 260
-    cfg.perturb = 0
-    cfg.render_precision = args.sdf_precision
+    cfg = config.subject('anisdf_pdf_s9p', perturb=0, render_precision=args.sdf_precision)
     net = network_sdf.Network(cfg)
     sd = synthetic.init_state_dict_sdf({k: tuple(v.shape) for k, v in net.state_dict().items()})
     network.load_numpy_state(net, sd)
@@ -531,10 +531,7 @@ def bench_sdf(args, rank, world, dev):
     }
     if split and not args.no_exact:
         # the same frame with every layer GEMM in exact fp32 MFMA (the reference's arithmetic), timed beside
-        cfg32 = config.defaults()
-        cfg32.num_train_frame = 260
-        cfg32.perturb = 0
-        cfg32.render_precision = 'fp32'
+        cfg32 = config.subject('anisdf_pdf_s9p', perturb=0, render_precision='fp32')
         r32 = Renderer(net, cfg32)
         batch['tbounds'].copy_(tb0)
         r32.render_device(batch)
@@ -608,9 +605,7 @@ def bench_sdf_train(args, rank, world, dev):
         bt['iter_step'] = 12000
         batches.append(bt)
     tb0 = [b['tbounds'].clone() for b in batches]
-    cfg = config.defaults()
-    cfg.num_train_frame = 260
-    cfg.perturb = 1
+    cfg = config.subject('anisdf_pdf_s9p', perturb=1)
     net = network_sdf.Network(cfg)
     sd = synthetic.init_state_dict_sdf({k: tuple(v.shape) for k, v in net.state_dict().items()})
     network.load_numpy_state(net, sd)

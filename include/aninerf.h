@@ -346,6 +346,47 @@ const uint32_t* anr_sdf_render_knn(const void* workspace, int n_rays, const anr_
 int anr_sdf_render_rows(const void* workspace, int n_rays, const anr_render_opts* o, float* resd, float* gradients,
                         float* msk_sdf, float* msk_label, void* stream);
 
+/* ---- sdf_pdf Network.forward over free samples (anisdf_pdf_network.py:156-224) -----------------
+ * The call tpose_renderer makes per chunk over the sdf_pdf network, self.net(wpts, viewdir, dists,
+ * batch) (tpose_renderer.py:95; configs/sdf_pdf/anisdf_pdf_s9p.yaml:9-12): x->n_pts samples (world
+ * points, world view directions; dists is not read: the Laplace density uses the constant 0.005,
+ * :330). One call = one reference chunk: the KNN prefilter keeps pnorm < o->norm_th (0.1) plus the
+ * argmin of pnorm over the call, and batch['tbounds'] is widened ONCE (tbounds_out, or NULL).
+ * world -> pose follows torch's matmul rule for an (n_pts, 3) product (n_pts < 45: its small path).
+ *  anr_sdf_network_fwd: evaluation (no observed_gradients), o->precision ANR_FP32 or ANR_BF16X3 as the
+ *    sdf render; raw (n,4) zero at dropped samples and outside the widened tbounds, sdf (n) = 10 at
+ *    dropped samples. Reads the kept count once (host sync).
+ *  anr_sdf_network_counts: device int32 {kept n', 0}; anr_sdf_network_rows: resd (n',3) and gradients
+ *    (n',3) of the kept samples, in sample order. */
+size_t anr_sdf_network_workspace_bytes(int n_pts, const anr_render_opts* o);
+int anr_sdf_network_fwd(const anr_sdf_params* p, const anr_sdf_frame* f, const anr_samples* x, const anr_render_opts* o,
+                        float* raw, float* sdf, float* tbounds_out, void* workspace, size_t ws_bytes, void* stream);
+const int32_t* anr_sdf_network_counts(const void* workspace, int n_pts);
+int anr_sdf_network_rows(const void* workspace, int n_pts, float* resd, float* gradients, void* stream);
+/* Under autograd (the reference's training forward, :187-199): the layer-wise exact-fp32 executor of
+ * anr_sdf_train_step over the call's samples.
+ *  anr_sdf_network_train_fwd: as anr_sdf_network_fwd plus 'observed_gradients' = d sdf(x + resd(x)) / d x
+ *    at the kept samples with |sdf| < 0.02 (x = init_bigpose, :140-154). Two host reads (counts).
+ *  anr_sdf_network_train_counts: device int32 {kept n', 0, observed rows n_o, 0}.
+ *  anr_sdf_network_train_rows: resd (n',3), gradients (n',3), observed_gradients (n_o,3) (any NULL: skipped).
+ *  anr_sdf_network_train_bwd: loss.backward() through the call: ACCUMULATES into grads (anr_sdf_params
+ *    order; resd_latent may be NULL) the parameter gradients of the upstream adjoints d raw (n,4),
+ *    d sdf (n), d resd (n',3), d gradients (n',3), d observed_gradients (n_o,3) (any NULL = 0), with the
+ *    second-order terms the reference's create_graph=True input gradients carry. It re-runs the forward
+ *    on the same workspace first, so f->tbounds must hold the bounds the forward call was given (before
+ *    its widening). */
+size_t anr_sdf_network_train_workspace_bytes(int n_pts);
+int anr_sdf_network_train_fwd(const anr_sdf_params* p, const anr_sdf_frame* f, const anr_samples* x,
+                              const anr_render_opts* o, float* raw, float* sdf, float* tbounds_out, void* workspace,
+                              size_t ws_bytes, void* stream);
+const int32_t* anr_sdf_network_train_counts(const void* workspace, int n_pts);
+int anr_sdf_network_train_rows(const void* workspace, int n_pts, float* resd, float* gradients,
+                               float* observed_gradients, void* stream);
+int anr_sdf_network_train_bwd(const anr_sdf_params* p, float* const* grads, const anr_sdf_frame* f, const anr_samples* x,
+                              const anr_render_opts* o, const float* d_raw, const float* d_sdf, const float* d_resd,
+                              const float* d_gradients, const float* d_observed_gradients, void* workspace,
+                              size_t ws_bytes, void* stream);
+
 /* ---- sdf_pdf training (config 5; lib/train/trainers/tpose_trainer.py:21-73, crit.py:5-19) ---------
  * anr_sdf_train_step: NetworkWrapper.forward + loss.backward() of one batch through the sdf_pdf
  *   network and tpose_renderer (anisdf_pdf_network.py:156-224 in training mode: gradients with

@@ -132,11 +132,7 @@ def oracle_params_sdf():
 
 def sdf_cfg():
     from animatable_nerf_amd import config
-    cfg = config.defaults()
-    cfg.num_train_frame = 260
-    cfg.num_latent_code = 260
-    cfg.perturb = 0
-    return cfg
+    return config.subject('anisdf_pdf_s9p', perturb=0)
 
 
 def make_net_sdf(device='cpu'):

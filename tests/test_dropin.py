@@ -111,3 +111,21 @@ def test_state_dict_matches_reference(name):
         net = network.Network(cfg)
     ours = [[k, list(v.shape)] for k, v in net.state_dict().items()]
     assert ours == g['state_dict']
+
+
+@pytest.mark.parametrize('name,subject', [('s9p', 'aninerf_s9p'), ('313', 'aninerf_313'),
+                                          ('sdf_pdf_s9p', 'anisdf_pdf_s9p')])
+def test_subject_presets_match_reference_cfg(name, subject):
+    """config.subject(...) (used by the GPU tests and bench.py, where the yaml files are absent) sizes the
+    networks as the reference's own cfg of that experiment does (golden G13: its yaml run through lib.config)."""
+    g = json.load(open(G13))[name]
+    cfg = config.subject(subject)
+    for k in ('num_train_frame', 'num_eval_frame', 'num_latent_code'):
+        assert cfg[k] == g[k], (k, cfg[k], g[k])
+    if name.startswith('sdf'):
+        from animatable_nerf_amd import network_sdf
+        net = network_sdf.Network(cfg)
+    else:
+        from animatable_nerf_amd import network
+        net = network.Network(cfg)
+    assert [[k, list(v.shape)] for k, v in net.state_dict().items()] == g['state_dict']

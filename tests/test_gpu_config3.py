@@ -1,0 +1,31 @@
+"""Config 3 (aninerf_313 training, bf16, 1 GPU) at its own shapes, with north_star's quality gate:
+held-out PSNR after training with bf16 GEMM operands within 0.05 dB of the exact-fp32 training
+(tests/quality.py describes the protocol; PSNR is lib/evaluators/if_nerf.py:15-18)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+GATE_DB = 0.05   # north_star: "PSNR within 0.05 dB"
+STEPS = 500
+SEEDS = 3
+
+
+@pytest.fixture(scope='module')
+def dev():
+    if not torch.cuda.is_available():
+        pytest.fail('GPU test run without a GPU')
+    return torch.device('cuda:0')
+
+
+def test_config3_bf16_psnr_within_gate(dev):
+    from .quality import train_psnr
+    res = train_psnr(dev, 'aninerf_313', ('fp32', 'bf16', 'bf16_all'), seeds=SEEDS, steps=STEPS, log=print)
+    p32 = float(np.mean(res['fp32']['psnr']))
+    # training must actually learn the target (the gate is meaningless on an untrained image)
+    assert p32 > res['_init'] + 3.0, (p32, res['_init'])
+    for prec in ('bf16', 'bf16_all'):
+        p = float(np.mean(res[prec]['psnr']))
+        print(f'{prec}: {p:.4f} dB vs fp32 {p32:.4f} dB (delta {p - p32:+.4f}); runs {res[prec]["psnr"]}')
+        assert abs(p - p32) <= GATE_DB, (prec, p, p32, res[prec]['psnr'], res['fp32']['psnr'])

@@ -335,3 +335,83 @@ def test_fused_step_two_ranks_stay_identical(dev):
         assert same is True and finite, (rank, same)
     # the loss statistics ride in the gradient blob's tail: every rank reports the mean over ranks
     assert res[0][3] == res[1][3]
+
+
+def test_overlapped_bucket_sees_final_nerf_gradients(dev, monkeypatch):
+    """The N > 1 overlap on one GPU: with the distributed branch forced on and the
+    all-reduce replaced by a snapshot taken on the comm stream, bucket 0 (the canonical NeRF's
+    gradients, tensors 0..26) is read as soon as anr_train_step_hooked records nerf_ready, while the
+    blend-weight backward still runs on the compute stream. The snapshot must equal the final
+    gradients (any NeRF gradient written after the event would differ), bucket 1 (the blend-weight MLP
+    + loss tail) must be reduced second, after the whole step."""
+    from animatable_nerf_amd import parallel, trainer
+    from animatable_nerf_amd.trainer import FusedStep
+    snaps = []
+
+    def fake_allreduce(t, group=None):
+        # runs with the comm stream current (GradBuckets.reduce): the clone is ordered after its wait
+        snaps.append((t.data_ptr(), t.numel(), t.clone()))
+        return t
+    monkeypatch.setattr(parallel, 'is_dist', lambda: True)
+    monkeypatch.setattr(trainer, 'is_dist', lambda: True)
+    monkeypatch.setattr(trainer, 'broadcast_', lambda t, src=0, group=None: t)
+    monkeypatch.setattr(parallel, 'allreduce_mean_', fake_allreduce)
+    g, bt, t_rand = _g4_batch(dev)
+    for prec in ('fp32', 'bf16'):
+        cfg = _cfg()
+        cfg.train_precision = prec
+        net = make_net(dev)
+        net.train()
+        step = FusedStep(net, cfg, lr=0.0)
+        assert step.buckets.comm is not None
+        for it in range(3):
+            snaps.clear()
+            step.step(bt, t_rand=t_rand.to(dev))
+            torch.cuda.synchronize()
+            assert len(snaps) == 2, len(snaps)
+            v0, v1 = step.buckets.views
+            (p0, n0, s0), (p1, n1, s1) = snaps
+            assert (p0, n0) == (v0.data_ptr(), v0.numel()) and (p1, n1) == (v1.data_ptr(), v1.numel())
+            assert torch.equal(s0, v0), (prec, it, (s0 - v0).abs().max().item())
+            assert torch.equal(s1, v1), (prec, it)
+            assert v0.abs().max().item() > 0
+
+
+def test_direct_call_reused_dict_sees_new_batch(dev):
+    """FusedStep caches one call per distinct batch: a caller that reuses ONE dict and
+    reassigns its entries every step (old tensors freed, new ones possibly at the same addresses)
+    must train on the new data. Same losses as fresh dicts, step by step (lr 0)."""
+    from animatable_nerf_amd.trainer import FusedStep
+    sc = scene(0.05)
+    bs = []
+    for seed in (11, 12, 13):
+        ro, rd = sc.box_rays(256, seed=seed)
+        b, _ = batch_np(sc, ro, rd, rgb=np.random.default_rng(seed).random((256, 3)).astype(np.float32))
+        bs.append(b)
+    R = min(b['ray_o'].shape[1] for b in bs)
+    gen = torch.Generator(device='cpu').manual_seed(4)
+    draws = [torch.rand((R, 64), generator=gen).to(dev) for _ in range(6)]
+
+    def run(reuse):
+        net = make_net(dev)
+        net.train()
+        step = FusedStep(net, _cfg(), lr=0.0)
+        shared = {}
+        out = []
+        for j in range(6):
+            src = to_torch(bs[j % 3], dev)
+            src = {k: (v[:, :R] if k in ('ray_o', 'ray_d', 'near', 'far', 'occupancy', 'mask_at_box', 'rgb') else v)
+                   for k, v in src.items()}
+            if reuse:
+                shared.clear()
+                shared.update({k: v.clone() for k, v in src.items()})
+                batch = shared
+            else:
+                batch = src
+            out.append(step.step(batch, t_rand=draws[j]).clone())
+            del src
+        return torch.stack(out)
+    fresh, reused = run(False), run(True)
+    assert torch.allclose(reused[:, :3], fresh[:, :3], rtol=1e-5, atol=0), (reused, fresh)
+    # consecutive batches differ, so a stale call would show as a repeated loss
+    assert not torch.allclose(fresh[0, :3], fresh[1, :3])
