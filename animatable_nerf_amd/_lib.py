@@ -71,8 +71,13 @@ class Samples(ctypes.Structure):
                 ('n_pts', ctypes.c_int)]
 
 
+REDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p)
+REDUCE_MIN_U64, REDUCE_MAX_U64, REDUCE_SUM_F32 = 0, 1, 2  # anr_train_hooks.reduce ops
+
+
 class TrainHooks(ctypes.Structure):
-    _fields_ = [('nerf_grads_ready', ctypes.c_void_p)]
+    _fields_ = [('nerf_grads_ready', ctypes.c_void_p), ('ray_offset', ctypes.c_int), ('reduce', REDUCE_FN),
+                ('reduce_user', ctypes.c_void_p)]
 
 
 class AlphaOpts(ctypes.Structure):

@@ -59,9 +59,16 @@ struct Prof {
 namespace anr {
 
 // A2-A6 + per-frame prep: memsets, volumes/folds, front-end, ordered compaction (counts[0] = n')
+int RaySplit::run(void* buf, int count, int op, hipStream_t s) const {
+  if (!reduce) return ANR_OK;
+  if (check_launch("before the ray-split reduction") != ANR_OK) return ANR_E_HIP;
+  if (reduce(user, buf, count, op, (void*)s) != 0) return fail(ANR_E_ARG, "ray split: the reduce hook failed");
+  return ANR_OK;
+}
+
 int stage_frontend(const anr_params* p, const anr_frame* f, const float* ray_o, const float* ray_d, const float* near_,
                    const float* far_, int R, const anr_render_opts* o, char* ws, const Layout& L, float4* raw,
-                   hipStream_t s, const anr_samples* x) {
+                   hipStream_t s, const anr_samples* x, const RaySplit* split) {
   const long np = (long)f->pbw_dims[0] * f->pbw_dims[1] * f->pbw_dims[2];
   const long nt = (long)f->tbw_dims[0] * f->tbw_dims[1] * f->tbw_dims[2];
   const int nch = (R + o->chunk - 1) / o->chunk;
@@ -99,6 +106,7 @@ int stage_frontend(const anr_params* p, const anr_frame* f, const float* ray_o, 
   FrontArgs fa{};
   fa.ray_o = ray_o; fa.ray_d = ray_d; fa.near_ = near_; fa.far_ = far_; fa.t_rand = o->t_rand;
   fa.n_rays = R; fa.chunk = o->chunk;
+  fa.ray_offset = split ? split->ray_offset : 0;
   fa.R = f->R; fa.Th = f->Th; fa.pbw = f->pbw; fa.pbounds = f->pbounds;
   fa.pn24 = pa.pn24;
   fa.X = f->pbw_dims[0]; fa.Y = f->pbw_dims[1]; fa.Z = f->pbw_dims[2];
@@ -123,8 +131,11 @@ int stage_frontend(const anr_params* p, const anr_frame* f, const float* ray_o, 
     ANR_TRY(check_launch("k_frontend"));
   }
 
+  // ray split: the chunk's argmin over every rank's samples
+  if (split) ANR_TRY(split->run(fa.chunk_min, (R + o->chunk - 1) / o->chunk, ANR_REDUCE_MIN_U64, s));
   CompactArgs ca{};
   ca.n_rays = R; ca.chunk = o->chunk;
+  ca.ray_offset = fa.ray_offset;
   ca.mask = fa.mask; ca.chunk_min = fa.chunk_min;
   ca.ray_off = (int*)(ws + L.ray_off);
   ca.block_sum = (int*)(ws + L.block_sum);
@@ -199,7 +210,7 @@ int stage_mlp(const anr_params* p, const anr_frame* f, const float* ray_o, const
 }
 
 // A11 alpha_ind rows: sigma' > train_th plus per-chunk argmax (counts[1] = m)
-int stage_alpha_ind(int R, const anr_render_opts* o, char* ws, const Layout& L, hipStream_t s) {
+int stage_alpha_ind(int R, const anr_render_opts* o, char* ws, const Layout& L, hipStream_t s, const RaySplit* split) {
   const long N = (long)R * 64;
   const int nch = (R + o->chunk - 1) / o->chunk;
   int* counts = (int*)(ws + L.counts);
@@ -212,8 +223,12 @@ int stage_alpha_ind(int R, const anr_render_opts* o, char* ws, const Layout& L, 
   aa.flags = (uint8_t*)(ws + L.flags);
   aa.block_sum = (int*)(ws + L.block_sum2);
   aa.out_row = (int*)(ws + L.out_row);
+  aa.list = (const int*)(ws + L.list);
+  aa.mask = (const uint64_t*)(ws + L.mask);
+  aa.ray_offset = split ? split->ray_offset : 0;
   hipLaunchKernelGGL(k_chunk_argmax, dim3(nch, 16), dim3(256), 0, s, aa);
   ANR_TRY(check_launch("k_chunk_argmax"));
+  if (split) ANR_TRY(split->run(aa.chunk_max, nch, ANR_REDUCE_MAX_U64, s));  // the chunk's argmax over every rank
   const int nb2 = (int)((N + 1023) / 1024);
   hipLaunchKernelGGL(k_flag_count, dim3(nb2), dim3(256), 0, s, aa);
   ANR_TRY(check_launch("k_flag_count"));

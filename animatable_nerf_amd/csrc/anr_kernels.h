@@ -25,6 +25,7 @@ struct FrontArgs {
   int chunk_pts;
   const float* pn24;     // channel 24 of pbw as a compact (X,Y,Z) array (k_prep), or NULL: read pbw
   // (k_frontend_pts also zeroes raw at the dropped points when raw != NULL: Network.forward's raw_full)
+  int ray_offset;        // ray split (anr_train_hooks): index of ray 0 within its reference chunk
 };
 
 struct CompactArgs {
@@ -34,6 +35,7 @@ struct CompactArgs {
   int* ray_off;    // (R+1) exclusive offsets (global after k_compact)
   int* block_sum;  // (ceil(R/256))
   int* list;       // (R*64) kept point ids (ray*64+sample)
+  int ray_offset;  // as FrontArgs::ray_offset
 };
 
 struct AlphaArgs {
@@ -46,6 +48,12 @@ struct AlphaArgs {
   uint8_t* flags;        // (n')
   int* block_sum;        // (ceil(n'/1024))
   int* out_row;          // (n') output row or -1
+  // the argmax key's tie-break index is the sample's index within its reference chunk, (ray +
+  // ray_offset) % chunk * 64 + lane (compaction keeps sample order, so within one call it orders
+  // like the compact index; across the ranks of a ray split it is the global one)
+  const int* list;
+  const uint64_t* mask;  // keep ballots after k_count (forced argmin bit included)
+  int ray_offset;
 };
 
 // (f) eval-split camera rays (get_rays_within_bounds)

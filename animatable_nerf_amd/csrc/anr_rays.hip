@@ -310,7 +310,7 @@ __global__ __launch_bounds__(1024) void k_frontend(FrontArgs a) {
     if (a.raw != nullptr && !keep) a.raw[(size_t)ray * 64 + lane] = make_float4(0.f, 0.f, 0.f, 0.f);
     // per-chunk argmin of pnorm over the visible samples (first index on ties):
     // key = bits(pn) << 32 | index-in-chunk
-    const int rc = ray % a.chunk;
+    const int rc = (ray + a.ray_offset) % a.chunk;
     key = vis ? (((uint64_t)__float_as_uint(pn) << 32) | (uint32_t)(rc * 64 + lane)) : ~0ull;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
@@ -381,7 +381,7 @@ __global__ __launch_bounds__(256) void k_count(CompactArgs a) {
     const int c = ray / a.chunk;
     const uint64_t key = a.chunk_min[c];
     const uint32_t idx = (uint32_t)(key & 0xffffffffu);
-    if ((int)(idx >> 6) == ray % a.chunk) m |= 1ull << (idx & 63);
+    if ((int)(idx >> 6) == (ray + a.ray_offset) % a.chunk) m |= 1ull << (idx & 63);
     a.mask[ray] = m;
     cnt = __popcll(m);
   }
@@ -453,7 +453,9 @@ __global__ __launch_bounds__(256) void k_chunk_argmax(AlphaArgs a) {
   const int s0 = a.ray_off[r0], s1 = a.ray_off[r1];
   uint64_t best = 0;
   for (int i = s0 + blockIdx.y * 256 + threadIdx.x; i < s1; i += gridDim.y * 256) {
-    const uint64_t key = ((uint64_t)ordered_bits(a.sigma[i]) << 32) | (uint32_t)(~(uint32_t)(i - s0));
+    const int pid = a.list[i];
+    const uint32_t g = (uint32_t)((((pid >> 6) + a.ray_offset) % a.chunk) * 64 + (pid & 63));
+    const uint64_t key = ((uint64_t)ordered_bits(a.sigma[i]) << 32) | (uint32_t)(~g);
     best = key > best ? key : best;
   }
 #pragma unroll
@@ -488,9 +490,17 @@ __global__ void k_flag_force(AlphaArgs a, int nchunks) {
   if (c >= nchunks) return;
   const uint64_t key = a.chunk_max[c];
   const int r0 = c * a.chunk;
-  const int s0 = a.ray_off[r0], s1 = a.ray_off[min(a.n_rays, r0 + a.chunk)];
-  if (s1 <= s0) return;
-  const int i = s0 + (int)(~(uint32_t)(key & 0xffffffffu));
+  const int r1 = min(a.n_rays, r0 + a.chunk);
+  const int s0 = a.ray_off[r0], s1 = a.ray_off[r1];
+  if (s1 <= s0 || key == 0) return;
+  // the winning sample's index within the chunk -> this call's ray (another rank's under a ray split)
+  const uint32_t g = ~(uint32_t)(key & 0xffffffffu);
+  const int ray = r0 + (int)(g >> 6) - (r0 + a.ray_offset) % a.chunk;
+  if (ray < r0 || ray >= r1) return;
+  const int lane = (int)(g & 63u);
+  const uint64_t m = a.mask[ray];
+  if (!((m >> lane) & 1ull)) return;
+  const int i = a.ray_off[ray] + __popcll(m & ((1ull << lane) - 1ull));
   if (a.flags[i] == 0) {
     a.flags[i] = 1;
     atomicAdd(&a.block_sum[i / 1024], 1);

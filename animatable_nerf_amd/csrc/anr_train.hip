@@ -241,13 +241,16 @@ __global__ __launch_bounds__(256) void k_tr_loss(TrainBufs b, const float* rgb_g
       atomicAdd(acc3 + 1, s1);
     } else {
       atomicAdd(acc3 + 2, s0);
+      if (blockIdx.x == 0) acc3[3] = (float)*b.m_rows;  // the rows count beside the sums (a ray split sums all four)
     }
   }
 }
 
+// acc3 = {sum sq. error, mask rays, sum smooth-L1, alpha_ind rows} (summed over the ranks of a ray split)
 __global__ void k_tr_loss_final(const float* acc3, const int* m_rows, float* loss3) {
+  (void)m_rows;
   const float img = acc3[0] / (3.0f * acc3[1]);
-  const float bw = acc3[2] / (24.0f * (float)(*m_rows));
+  const float bw = acc3[2] / (24.0f * acc3[3]);
   loss3[0] = bw + img;
   loss3[1] = img;
   loss3[2] = bw;
@@ -267,7 +270,7 @@ __global__ __launch_bounds__(256) void k_tr_loss_grads(TrainBufs b, const float*
     if (i >= *b.n_kept) return;
     const int row = b.out_row[i];
     if (row < 0) return;
-    const float sc = 1.0f / (24.0f * (float)(*b.m_rows));
+    const float sc = 1.0f / (24.0f * acc3[3]);
     for (int c = 0; c < 24; ++c) {
       const float x = b.Bp[(long)i * 24 + c] - b.Bt[(long)i * 24 + c];
       const float d = (fabsf(x) < 1.f ? x : (x > 0.f ? 1.f : -1.f)) * sc;

@@ -555,9 +555,10 @@ int nerf_forward_chain(Exec& e, const anr_params* p, const float* Gt, const floa
 // x != NULL: free samples (Network.forward, anr_network_train_fwd): R groups of 64, no compositing
 int train_forward(const anr_params* p, const anr_frame* f, const float* ray_o, const float* ray_d, const float* near_,
                   const float* far_, int R, const anr_render_opts* o, const anr_render_out* out, char* ws,
-                  const TLayout& T, hipStream_t s, Exec& e, const anr_samples* x = nullptr) {
+                  const TLayout& T, hipStream_t s, Exec& e, const anr_samples* x = nullptr,
+                  const RaySplit* split = nullptr) {
   float4* raw = (float4*)(ws + T.L.raw);
-  ANR_TRY(stage_frontend(p, f, ray_o, ray_d, near_, far_, R, o, ws, T.L, raw, s, x));
+  ANR_TRY(stage_frontend(p, f, ray_o, ray_d, near_, far_, R, o, ws, T.L, raw, s, x, split));
   const long N = (long)R * 64;
   e.n_dev = (const int*)(ws + T.L.counts);
   e.cap = (int)N;
@@ -620,7 +621,7 @@ int train_forward(const anr_params* p, const anr_frame* f, const float* ray_o, c
     hipLaunchKernelGGL(k_tr_raw, dim3(g1), dim3(256), 0, s, b);
     ANR_TRY(check_launch("k_tr_raw"));
   }
-  ANR_TRY(stage_alpha_ind(R, o, ws, T.L, s));
+  ANR_TRY(stage_alpha_ind(R, o, ws, T.L, s, split));
   ANR_TRY(order(e.ss, s, s2));  // join: the tbw rows
   if (x) return ANR_OK;
   return stage_composite(near_, far_, R, o, raw, out, nullptr, s);
@@ -948,12 +949,13 @@ namespace {
 int train_step_body(const anr_params* p, float* const* grads, const anr_frame* f, const float* ray_o,
                     const float* ray_d, const float* near_, const float* far_, int n_rays, const anr_render_opts* o,
                     const float* rgb_gt, const uint8_t* mask_at_box, const anr_render_out* out, float* loss3,
-                    hipEvent_t nerf_done, char* ws, const TLayout& T, hipStream_t s, SideStreams* ss) {
+                    hipEvent_t nerf_done, char* ws, const TLayout& T, hipStream_t s, SideStreams* ss,
+                    const RaySplit* split = nullptr) {
   Exec e{s, 0, (o->precision == ANR_BF16 || o->precision == ANR_BF16_ALL) ? 1 : 0, o->precision == ANR_BF16 ? 1 : 0};
   e.ss = ss;
   e.hb = e.bf16;
   ANR_TRY(pack_images(e, p, ws + T.wimg, s, (float*)(ws + T.wslab)));
-  ANR_TRY(train_forward(p, f, ray_o, ray_d, near_, far_, n_rays, o, out, ws, T, s, e));
+  ANR_TRY(train_forward(p, f, ray_o, ray_d, near_, far_, n_rays, o, out, ws, T, s, e, nullptr, split));
   // fused losses (tpose_trainer.py:50-63) and their upstream gradients
   TrainBufs b = bufs(T, ws, f, ray_o, ray_d, near_, far_, n_rays, o);
   b.rgb_map = out->rgb_map;
@@ -963,6 +965,7 @@ int train_step_body(const anr_params* p, float* const* grads, const anr_frame* f
   const int gx = (int)((std::max<long>(n_rays, N) + 255) / 256);
   hipLaunchKernelGGL(k_tr_loss, dim3(gx, 2), dim3(256), 0, s, b, rgb_gt, mask_at_box, acc3);
   ANR_TRY(check_launch("k_tr_loss"));
+  if (split) ANR_TRY(split->run(acc3, 4, ANR_REDUCE_SUM_F32, s));  // the batch's loss sums and row count
   hipLaunchKernelGGL(k_tr_loss_final, dim3(1), dim3(1), 0, s, (const float*)acc3, b.m_rows, loss3);
   ANR_TRY(check_launch("k_tr_loss_final"));
   float* d_rgb = (float*)(ws + T.d_rgb);
@@ -1031,12 +1034,22 @@ int anr_train_step_hooked(const anr_params* p, float* const* grads, const anr_fr
   char* ws = (char*)workspace;
   SideStreams* ss = side_streams();
   hipEvent_t nerf_done = hooks ? (hipEvent_t)hooks->nerf_grads_ready : nullptr;
+  RaySplit split{};
+  const bool splitting = hooks && hooks->reduce;
+  if (splitting) {
+    split.ray_offset = hooks->ray_offset;
+    split.reduce = hooks->reduce;
+    split.user = hooks->reduce_user;
+    if (split.ray_offset < 0 || split.ray_offset + n_rays > o->chunk)
+      return fail(ANR_E_ARG, "anr_train_step: a ray split needs ray_offset >= 0 and ray_offset + n_rays <= chunk");
+  }
   const char* gv = getenv("ANR_TRAIN_GRAPH");
-  // an external event (bucketed all-reduce) must be signalled by a plain record: eager only
-  const bool graphs = ss && !nerf_done && gv && gv[0] == '1';
+  // an external event (bucketed all-reduce) must be signalled by a plain record, and a ray split calls
+  // its host hook mid-step: eager only
+  const bool graphs = ss && !nerf_done && !splitting && gv && gv[0] == '1';
   if (!graphs)
     return train_step_body(p, grads, f, ray_o, ray_d, near_, far_, n_rays, o, rgb_gt, mask_at_box, out, loss3,
-                           nerf_done, ws, T, s, ss);
+                           nerf_done, ws, T, s, ss, splitting ? &split : nullptr);
   std::string key;
   int dev = 0;
   (void)hipGetDevice(&dev);

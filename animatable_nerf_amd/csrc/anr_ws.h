@@ -59,15 +59,24 @@ int check_launch(const char* what);
     if (_rc != ANR_OK) return _rc;  \
   } while (0)
 
+// ray split of one reference chunk over ranks (anr_train_hooks): ray offset + the host reduction hook
+struct RaySplit {
+  int ray_offset;
+  anr_reduce_fn reduce;
+  void* user;
+  int run(void* buf, int count, int op, hipStream_t s) const;
+};
+
 // x != NULL: free samples (Network.forward): R = ceil(n_pts / 64) groups of 64 samples, the caller's
 // opts with chunk = R (the whole call is one reference chunk) and no t_rand; ray pointers unused
 int stage_frontend(const anr_params* p, const anr_frame* f, const float* ray_o, const float* ray_d, const float* near_,
                    const float* far_, int R, const anr_render_opts* o, char* ws, const Layout& L, float4* raw,
-                   hipStream_t s, const anr_samples* x = nullptr);
+                   hipStream_t s, const anr_samples* x = nullptr, const RaySplit* split = nullptr);
 int stage_mlp(const anr_params* p, const anr_frame* f, const float* ray_o, const float* ray_d, const float* near_,
               const float* far_, int R, const anr_render_opts* o, char* ws, const Layout& L, float4* raw,
               hipStream_t s, const anr_samples* x = nullptr);
-int stage_alpha_ind(int R, const anr_render_opts* o, char* ws, const Layout& L, hipStream_t s);
+int stage_alpha_ind(int R, const anr_render_opts* o, char* ws, const Layout& L, hipStream_t s,
+                    const RaySplit* split = nullptr);
 int stage_composite(const float* near_, const float* far_, int R, const anr_render_opts* o, const float4* raw,
                     const anr_render_out* out, float* weights, hipStream_t s);
 

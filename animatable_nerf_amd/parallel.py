@@ -37,6 +37,42 @@ def allreduce_mean_(t, group=None):
     return t
 
 
+# ---- ray split of one training batch (north_star "rays-per-iteration shard"; anr_train_hooks) ----
+def ray_split_range(n_rays, rank, world):
+    """[start, end) of this rank's rays when one batch (a single reference chunk) is split over the ranks:
+    contiguous, as even as possible."""
+    return n_rays * rank // world, n_rays * (rank + 1) // world
+
+
+_SIGN64 = -(1 << 63)
+_MAX64 = (1 << 63) - 1
+
+
+def reduce_keys_(t, op, group=None):
+    """The exchange a ray-split training step makes through its reduce hook (in place, over ranks):
+    op 0 = min of unsigned 64-bit keys whose all-ones value means "empty" (the per-chunk argmin of the
+    prefilter, tpose_nerf_network.py:154), op 1 = max of unsigned 64-bit keys (the per-chunk argmax of
+    sigma', :193-194), op 2 = float sum (the loss sums). ``t``: an int64 (ops 0, 1) or float32 (op 2)
+    view of the device buffer. torch has no unsigned 64-bit reduction: the keys of op 0 stay below 2^63
+    (non-negative float bits above the index), so only the empty marker is remapped; op 1 flips the top
+    bit, which maps unsigned order onto signed order."""
+    if not is_dist():
+        return t
+    if op == 0:
+        t.masked_fill_(t == -1, _MAX64)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+        t.masked_fill_(t == _MAX64, -1)
+    elif op == 1:
+        t.bitwise_xor_(_SIGN64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+        t.bitwise_xor_(_SIGN64)
+    elif op == 2:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    else:
+        raise ValueError(f'reduce op {op}')
+    return t
+
+
 class GradBuckets:
     """Mean all-reduce of a flat gradient blob in buckets, each issued as soon as the backward has
     finished it (DDP's reducer buckets parameters in reverse layer order and overlaps their all-reduce
@@ -48,16 +84,23 @@ class GradBuckets:
     returns at once; ``wait()`` makes the current stream wait for every issued bucket. On a CPU blob
     (gloo) each ``reduce`` completes in place."""
 
-    def __init__(self, blob, bounds, group=None):
+    def __init__(self, blob, bounds, group=None, op='mean'):
         self.views = [blob[s:e] for s, e in bounds]
         self.group = group
+        self.op = op  # 'mean' (DDP replicas) or 'sum' (a ray split: each rank holds a share of one gradient)
         self.comm = torch.cuda.Stream(device=blob.device) if blob.is_cuda else None
+
+    def _reduce(self, v):
+        if self.op == 'sum':
+            dist.all_reduce(v, op=dist.ReduceOp.SUM, group=self.group)
+        else:
+            allreduce_mean_(v, self.group)
 
     def reduce(self, i, ready=None):
         if not is_dist():
             return
         if self.comm is None:
-            allreduce_mean_(self.views[i], self.group)
+            self._reduce(self.views[i])
             return
         cur = torch.cuda.current_stream(self.views[i].device)
         with torch.cuda.stream(self.comm):
@@ -65,7 +108,7 @@ class GradBuckets:
                 self.comm.wait_event(ready)
             else:
                 self.comm.wait_stream(cur)
-            allreduce_mean_(self.views[i], self.group)
+            self._reduce(self.views[i])
 
     def wait(self):
         if self.comm is not None and is_dist():
@@ -133,31 +176,63 @@ def gather_rays(t, n_rays, world, chunk=2048, group=None):
     return torch.cat(out, dim=1)
 
 
+def gather_rows(t, group=None):
+    """(1, m_r, ...) per rank, m_r varying -> (1, sum m_r, ...) on every rank in rank order (one all_gather
+    of the counts, one of the rows padded to the largest count)."""
+    if not is_dist():
+        return t
+    world = dist.get_world_size(group)
+    n = torch.tensor([t.shape[1]], dtype=torch.int64, device=t.device)
+    ns = [torch.empty_like(n) for _ in range(world)]
+    dist.all_gather(ns, n, group=group)
+    ns = [int(x.item()) for x in ns]
+    mx = max(ns)
+    pad = torch.zeros((t.shape[0], mx) + tuple(t.shape[2:]), dtype=t.dtype, device=t.device)
+    pad[:, :t.shape[1]] = t
+    parts = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(parts, pad.contiguous(), group=group)
+    return torch.cat([p[:, :k] for p, k in zip(parts, ns)], dim=1)
+
+
 def render_sharded(renderer, batch, chunk=2048, group=None):
     """Renderer.render_device over a whole frame with its rays split across the ranks by whole
-    reference chunks (so every per-chunk argmin / argmax is the single-GPU one); rgb_map, acc_map
-    and depth_map are all-gathered to every rank in ray order (the 'raw' samples stay local:
-    'raw_local', this rank's rays [start, end) in 'span')."""
+    reference chunks (so every per-chunk argmin / argmax is the single-GPU one); every output key of
+    the reference's render dict is gathered to every rank in frame order: the per-ray maps and 'raw'
+    by rays, the row outputs (aninerf 'pbw' / 'tbw' alpha_ind rows; sdf_pdf 'resd' / 'gradients' kept
+    rows and the per-chunk 'msk_sdf' / 'msk_label' lists) concatenated in rank order, which is chunk
+    order. 'span' = this rank's rays [start, end)."""
     rank = dist.get_rank(group) if is_dist() else 0
     world = dist.get_world_size(group) if is_dist() else 1
     R = int(batch['ray_o'].shape[1])
     widens = getattr(renderer, 'widens_tbounds', False)
     tb0 = batch['tbounds'].detach().clone() if widens else None
     sub, (s, e) = shard_batch(batch, rank, world, chunk)
+    dev = batch['ray_o'].device
+    ns = int(getattr(renderer.cfg, 'N_samples', 64)) if hasattr(renderer, 'cfg') else 64
     if e > s:
         # the sdf_pdf renderer widens tbounds per chunk: this shard starts at reference chunk s / chunk
-        out = renderer.render_device(sub, bw_rows=False, chunk_offset=s // chunk) \
-            if getattr(renderer, 'widens_tbounds', False) else renderer.render_device(sub, bw_rows=False)
+        out = renderer.render_device(sub, chunk_offset=s // chunk) if widens else renderer.render_device(sub)
     else:  # more ranks than chunks: an empty shard
-        dev = batch['ray_o'].device
         out = {'rgb_map': torch.zeros((1, 0, 3), device=dev), 'acc_map': torch.zeros((1, 0), device=dev),
                'depth_map': torch.zeros((1, 0), device=dev), 'raw': torch.zeros((1, 0, 4), device=dev)}
+        if widens:
+            out.update(sdf=torch.zeros((1, 0, 1), device=dev), resd=torch.zeros((1, 0, 3), device=dev),
+                       gradients=torch.zeros((1, 0, 3), device=dev), msk_sdf=torch.zeros((1, 0), device=dev),
+                       msk_label=torch.zeros((1, 0), device=dev))
+        else:
+            out.update(pbw=torch.zeros((1, 0, 24), device=dev), tbw=torch.zeros((1, 0, 24), device=dev))
     if widens:  # every rank leaves the frame's bounds as the whole single-GPU render does
         from .renderer_sdf import widen_tbounds
         with torch.no_grad():
             batch['tbounds'].copy_(widen_tbounds(tb0, (R + chunk - 1) // chunk))
     ret = {k: gather_rays(out[k], R, world, chunk, group) for k in ('rgb_map', 'acc_map', 'depth_map')}
-    ret['raw_local'] = out['raw']
+    for k, w in (('raw', 4), ('sdf', 1)):  # per-sample outputs, gathered as per-ray rows
+        if k in out:
+            v = out[k].reshape(1, -1, ns * w)
+            ret[k] = gather_rays(v, R, world, chunk, group).reshape(1, -1, w)
+    for k in ('pbw', 'tbw', 'resd', 'gradients', 'msk_sdf', 'msk_label'):
+        if k in out:
+            ret[k] = gather_rows(out[k], group)
     ret['span'] = (s, e)
     return ret
 

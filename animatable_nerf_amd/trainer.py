@@ -21,7 +21,9 @@ import torch.nn.functional as F
 
 from . import _lib
 from . import config as _config
-from .parallel import GradBuckets, broadcast_, is_dist
+import torch.distributed as dist
+
+from .parallel import GradBuckets, broadcast_, is_dist, ray_split_range, reduce_keys_
 from .renderer import FRAME_KEYS, RAY_KEYS, Renderer, _Call
 
 
@@ -72,7 +74,7 @@ class FusedStep:
     (loss, img_loss, bw_loss) without synchronising.
     """
 
-    def __init__(self, net, cfg=None, lr=None, clip=40.0, betas=(0.9, 0.999), eps=1e-8, group=None):
+    def __init__(self, net, cfg=None, lr=None, clip=40.0, betas=(0.9, 0.999), eps=1e-8, group=None, ray_split=False):
         self.cfg = cfg if cfg is not None else _config.active()
         self.net = net
         self.renderer = Renderer(net, self.cfg)
@@ -106,7 +108,18 @@ class FusedStep:
         # buckets in the order anr_train_step_hooked finishes them: the canonical NeRF (tensors 0..26,
         # final before the blend-weight backward runs), then the blend-weight MLP (27..45) + losses
         n_nerf = sum(p.numel() for p in ps[:27])
-        self.buckets = GradBuckets(self.grad, [(0, n_nerf), (n_nerf, n + 4)], group)
+        # ray_split: every rank gets the SAME batch and trains on its own contiguous share of its rays
+        # (one reference chunk split over the ranks: strong scaling of one iteration). The chunk-wide
+        # argmin / argmax and the loss sums are exchanged mid-step through the library's reduce hook,
+        # so the losses are the batch's on every rank and the gradients are shares of its gradient:
+        # summed (not averaged), the loss tail left as it is
+        self.ray_split = bool(ray_split) and is_dist()
+        if self.ray_split:
+            self.buckets = GradBuckets(self.grad, [(0, n_nerf), (n_nerf, n)], group, op='sum')
+            self._reduce_cb = _lib.REDUCE_FN(self._reduce_hook)  # kept alive with the step
+        else:
+            self.buckets = GradBuckets(self.grad, [(0, n_nerf), (n_nerf, n + 4)], group)
+            self._reduce_cb = _lib.REDUCE_FN()
         self._st = None  # fixed input / output buffers of the step (see _static_call)
         self._calls = {}  # direct calls per distinct batch (see _direct_call)
         self._trand = None
@@ -220,9 +233,44 @@ class FusedStep:
         st['call'].opts.t_rand = st['t_rand'].data_ptr() if (t_rand is not None or self.cfg.perturb > 0) else None
         return st['call'], sb['rgb'], sb['mask_at_box'].reshape(-1)
 
+    def _reduce_hook(self, user, buf, count, op, stream):
+        """anr_train_hooks.reduce: the step's mid-step exchange over the ranks (parallel.reduce_keys_) on a
+        view of the workspace buffer the library hands over, on the current stream (the library's)."""
+        try:
+            ws = self._ws_now
+            off = buf - ws.data_ptr()
+            isz = 4 if op == _lib.REDUCE_SUM_F32 else 8
+            view = ws[off:off + count * isz].view(torch.float32 if isz == 4 else torch.int64)
+            reduce_keys_(view, op, self.group)
+            return 0
+        except Exception:  # pragma: no cover - reported through the library's error code
+            import traceback
+            traceback.print_exc()
+            return 1
+
+    def _split_share(self, batch, t_rand):
+        """this rank's rays of the (replicated) batch and their offset within it"""
+        from .parallel import RAY_KEYS as SPLIT_KEYS
+        R = int(batch['ray_o'].shape[1])
+        world = dist.get_world_size(self.group)
+        rank = dist.get_rank(self.group)
+        chunk = int(self.cfg.get('chunk', 2048))
+        if R > chunk or R < world:
+            raise ValueError(f'ray_split: the batch ({R} rays) must fit one reference chunk ({chunk}) and give '
+                             f'every one of the {world} ranks a ray')
+        a, b = ray_split_range(R, rank, world)
+        sub = {k: (v[:, a:b] if k in SPLIT_KEYS and torch.is_tensor(v) and v.dim() >= 2 and v.shape[1] == R else v)
+               for k, v in batch.items()}
+        if t_rand is not None:
+            t_rand = t_rand.reshape(R, -1)[a:b]
+        return sub, t_rand, a
+
     def step(self, batch, t_rand=None, lr=None):
         r = self.renderer
         dev = self.flat.device
+        ray_offset = 0
+        if self.ray_split:
+            batch, t_rand, ray_offset = self._split_share(batch, t_rand)
         R = batch['ray_o'].shape[1]
         if os.environ.get('ANR_TRAIN_GRAPH') == '1':
             c, rgb, mask = self._static_call(batch, t_rand)
@@ -235,7 +283,8 @@ class FusedStep:
         gp = (ctypes.c_void_p * _lib.NUM_TENSORS)(*[g.data_ptr() for g in self.grad_views])
         stream = _lib.stream_ptr(dev)
         overlap = is_dist() and self.nerf_ready is not None
-        hooks = _lib.TrainHooks(self.nerf_ready.cuda_event if overlap else None)
+        hooks = _lib.TrainHooks(self.nerf_ready.cuda_event if overlap else None, ray_offset, self._reduce_cb, None)
+        self._ws_now = ws
         _lib.check(self.lib.anr_train_step_hooked(ctypes.byref(p), gp, ctypes.byref(c.frame), *c.ray_ptrs(), R,
                                                   ctypes.byref(c.opts), _lib.ptr(rgb), _lib.ptr(mask),
                                                   ctypes.byref(c.out), _lib.ptr(self.loss3), ctypes.byref(hooks),

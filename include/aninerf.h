@@ -260,8 +260,25 @@ int anr_train_step(const anr_params* p, float* const* grads, const anr_frame* f,
  * the backward (DDP's reverse-order buckets): nerf_grads_ready (a hipEvent_t or
  * NULL) is recorded on the stream once the gradients of tensors 0..26 (tpose_human.*, the canonical
  * NeRF) are final; the blend-weight backward (tensors 27..45) follows on the stream. */
+typedef int (*anr_reduce_fn)(void* user, void* device_buf, int count, int op, void* stream);
+#define ANR_REDUCE_MIN_U64 0 /* unsigned 64-bit keys, min over ranks (all-ones = empty) */
+#define ANR_REDUCE_MAX_U64 1 /* unsigned 64-bit keys, max over ranks */
+#define ANR_REDUCE_SUM_F32 2 /* float sums over ranks */
 typedef struct anr_train_hooks {
   void* nerf_grads_ready;
+  /* Ray split of ONE reference chunk over ranks (north_star "rays-per-iteration shard"; strong scaling of
+   * a 1,024-ray step): this call's rays are rays [ray_offset, ray_offset + n_rays) of a
+   * batch that is a single reference chunk (ray_offset + n_rays <= o->chunk). The chunk-wide decisions are
+   * exchanged through reduce (NULL: no split), which the library calls on the host, in issue order, with
+   * a device buffer of the workspace; it must make `stream` wait for the reduction over all ranks (e.g. an
+   * RCCL all-reduce on that stream): the per-chunk argmin key of the prefilter (tpose_nerf_network.py:154,
+   * MIN_U64) before compaction, the per-chunk argmax key of sigma' (:193-194, MAX_U64) before the
+   * alpha_ind rows are flagged, and the loss sums {squared error, mask rays, smooth-L1 sum, alpha_ind
+   * rows} (SUM_F32) before the loss and its gradients. Losses are then the batch's on every rank and
+   * the gradients are this rank's share of the batch gradient (sum them over ranks). */
+  int ray_offset;
+  anr_reduce_fn reduce;
+  void* reduce_user;
 } anr_train_hooks;
 int anr_train_step_hooked(const anr_params* p, float* const* grads, const anr_frame* f, const float* ray_o,
                           const float* ray_d, const float* near_, const float* far_, int n_rays,

@@ -89,7 +89,19 @@ class _FakeRenderer:
         o, d, near = b['ray_o'], b['ray_d'], b['near']
         rgb = torch.sigmoid(o * 3.0 + d * near[..., None])
         return {'rgb_map': rgb, 'acc_map': rgb.sum(-1) / 3.0, 'depth_map': near * 2.0,
-                'raw': torch.zeros((1, o.shape[1] * 64, 4))}
+                'raw': _per_sample(near, 4), 'pbw': _rows(o, 24, 0.0), 'tbw': _rows(o, 24, 1.0)}
+
+
+def _per_sample(near, w):
+    """(1, n*64, w) outputs that depend on each ray's own data only"""
+    return (near[..., None, None] * torch.arange(64 * w, dtype=torch.float32).reshape(1, 1, 64, w)).reshape(1, -1, w)
+
+
+def _rows(o, w, shift):
+    """(1, m, w) row outputs: 0-2 rows per ray (by the ray's data), in ray order, like alpha_ind rows"""
+    cnt = (o[0, :, 0] > 0).long() + (o[0, :, 1] > 0.5).long()
+    r = torch.repeat_interleave(torch.arange(o.shape[1]), cnt)
+    return (o[0, r, :1] + shift + torch.arange(w, dtype=torch.float32))[None]
 
 
 def _frame(n):
@@ -107,7 +119,7 @@ def _shard_worker(rank, world, port, n, q):
         b = _frame(n)
         ret = parallel.render_sharded(_FakeRenderer(), b)
         full = _FakeRenderer().render_device(b)
-        ok = all(torch.equal(ret[k], full[k]) for k in ('rgb_map', 'acc_map', 'depth_map'))
+        ok = all(torch.equal(ret[k], full[k]) for k in ('rgb_map', 'acc_map', 'depth_map', 'raw', 'pbw', 'tbw'))
         s, e = ret['span']
         ok = ok and (s, e) == parallel.shard_chunks(n, rank, world)
         psnr = parallel.psnr_sharded(full['rgb_map'][:, s:e], b['rgb'][:, s:e])
@@ -213,7 +225,10 @@ class _FakeSdfRenderer:
             tb = widen_tbounds(tb, 1)
             rgb[:, c0:c0 + 2048] = torch.sigmoid(b['ray_o'][:, c0:c0 + 2048] * tb[0, 1] + tb[0, 0])
         b['tbounds'].copy_(tb)
-        return {'rgb_map': rgb, 'acc_map': rgb.sum(-1), 'depth_map': b['near'] * 2.0, 'raw': torch.zeros((1, n * 64, 4))}
+        o = b['ray_o']
+        return {'rgb_map': rgb, 'acc_map': rgb.sum(-1), 'depth_map': b['near'] * 2.0, 'raw': _per_sample(b['near'], 4),
+                'sdf': _per_sample(b['near'], 1), 'resd': _rows(o, 3, 0.0), 'gradients': _rows(o, 3, 2.0),
+                'msk_sdf': _rows(o, 1, 3.0)[..., 0], 'msk_label': _rows(o, 1, 4.0)[..., 0]}
 
 
 def _sdf_shard_worker(rank, world, port, n, q):
@@ -226,7 +241,8 @@ def _sdf_shard_worker(rank, world, port, n, q):
         full_b = {k: v.clone() for k, v in b.items()}
         full = _FakeSdfRenderer().render_device(full_b)
         ret = parallel.render_sharded(_FakeSdfRenderer(), b)
-        ok = all(torch.equal(ret[k], full[k]) for k in ('rgb_map', 'acc_map', 'depth_map'))
+        ok = all(torch.equal(ret[k], full[k]) for k in ('rgb_map', 'acc_map', 'depth_map', 'raw', 'sdf', 'resd',
+                                                         'gradients', 'msk_sdf', 'msk_label'))
         ok = ok and torch.equal(b['tbounds'], full_b['tbounds'])
         q.put((rank, bool(ok)))
     except Exception as ex:  # pragma: no cover
@@ -291,3 +307,57 @@ def test_gloo_grad_buckets_mean_with_loss_tail():
         assert p.exitcode == 0
     for rank, ok in res:
         assert ok is True, (rank, ok)
+
+
+def _split_reduce_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    try:
+        parallel.init_from_env('gloo')
+        # argmin keys (pnorm bits << 32 | index): rank r has chunk 0's best on rank 1, chunk 1 empty everywhere
+        # but rank 2, chunk 2 empty everywhere
+        pn = [0.04, 0.01, 0.03]
+        mins = torch.tensor([(int(np.float32(pn[rank]).view(np.uint32)) << 32) | (64 * rank + 5),
+                             -1 if rank != 2 else (7 << 32) | 3, -1], dtype=torch.int64)
+        parallel.reduce_keys_(mins, 0)
+        # argmax keys: ordered(sigma) << 32 | ~index; the ordered bits of a positive sigma set the top bit
+        def okey(sig, idx):
+            u = int(np.float32(sig).view(np.uint32))
+            o = (u ^ 0xffffffff) if u & 0x80000000 else (u | 0x80000000)
+            v = (o << 32) | ((~idx) & 0xffffffff)
+            return v - (1 << 64) if v >= (1 << 63) else v
+        sig = [(2.5, 10), (3.0, 70), (3.0, 130)][rank]  # tie at 3.0: the lower index (rank 1's) wins
+        maxs = torch.tensor([okey(*sig), okey(-1.0, rank)], dtype=torch.int64)
+        parallel.reduce_keys_(maxs, 1)
+        sums = torch.tensor([1.5 * (rank + 1), 1.0], dtype=torch.float32)
+        parallel.reduce_keys_(sums, 2)
+        # gradient shares are summed in a split, averaged across replicas otherwise
+        blob = torch.full((6,), float(rank + 1))
+        parallel.GradBuckets(blob, [(0, 3), (3, 6)], op='sum').reduce(0)
+        q.put((rank, mins.tolist(), maxs.tolist(), sums.tolist(), blob.tolist(), okey(3.0, 70), okey(-1.0, 0)))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_gloo_world3_ray_split_reductions():
+    """the three mid-step exchanges of a ray-split training step (trainer.FusedStep(ray_split=True),
+    anr_train_hooks.reduce): min of argmin keys with empty markers, max of argmax keys (unsigned order,
+    ties to the lower sample index), float sums; and the summed gradient buckets"""
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_split_reduce_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in procs])
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    best = (int(np.float32(0.01).view(np.uint32)) << 32) | (64 + 5)
+    for rank, mins, maxs, sums, blob, k_win, k_neg in res:
+        assert mins == [best, (7 << 32) | 3, -1]
+        assert maxs == [k_win, k_neg]
+        assert sums == [9.0, 3.0]
+        assert blob == [6.0, 6.0, 6.0] + [float(rank + 1)] * 3
+    assert [parallel.ray_split_range(1024, r, 3) for r in range(3)] == [(0, 341), (341, 682), (682, 1024)]
