@@ -198,10 +198,18 @@ __global__ void k_pack_b16(PackArgs a);
 // scaled by sc), and the fused programs over one batch (residual MLP; SDF network forward)
 __global__ void k_pack_seq(PackArgs a, int L0, int nl, int sl, float sc);
 int seq_pack_threads(int L0, int nl);
-int launch_resd(const MlpArgs& a, int grid, hipStream_t s);
-int launch_sdfnet(const MlpArgs& a, int grid, hipStream_t s);
-int launch_sdfgrad(const MlpArgs& a, int grid, hipStream_t s);
-int launch_color(const MlpArgs& a, int grid, hipStream_t s);
+// the same sequence as a bf16x6 image (anr_layers.h x6seq_*) for the fp32-level programs
+__global__ void k_pack_seq_x6(PackArgs a, int L0, int nl, int sl, float sc);
+int seq_x6_pack_threads(int L0, int nl);
+__global__ void k_resd_x6(MlpArgs a);
+__global__ void k_sdfnet_x6(MlpArgs a);
+__global__ void k_sdfgrad_x6(MlpArgs a);
+__global__ void k_color_x6(MlpArgs a);
+// x6: the bf16x6 programs (image from k_pack_seq_x6), else bf16x3 (k_pack_seq)
+int launch_resd(const MlpArgs& a, int grid, hipStream_t s, bool x6 = false);
+int launch_sdfnet(const MlpArgs& a, int grid, hipStream_t s, bool x6 = false);
+int launch_sdfgrad(const MlpArgs& a, int grid, hipStream_t s, bool x6 = false);
+int launch_color(const MlpArgs& a, int grid, hipStream_t s, bool x6 = false);
 __global__ void k_pack_x6(PackArgs a);
 
 }  // namespace anr

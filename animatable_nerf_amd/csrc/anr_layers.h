@@ -269,6 +269,17 @@ __host__ __device__ constexpr int x6_layer_offset(int i) {
 __host__ __device__ constexpr int x6_bytes() { return x6_layer_offset(ANR_X6_LAYERS); }
 __host__ __device__ constexpr int x6_base() { return (b16_base() + b16_bytes() + 255) / 256 * 256; }
 #define ANR_X6_NOVEL_WOFF (x6_layer_offset(ANR_L_NOVEL0) - x6_layer_offset(0))
+// a layer sequence L0 .. L0 + nl - 1 as its own bf16x6 image (k_pack_seq_x6; the sdf render's fused
+// programs in render precision ANR_BF16X6): weights [k-step][out-block][hi|mid|lo] from byte 0, then the
+// biases laid out as in the bf16x3 sequence image (seq_bias_off)
+__host__ __device__ constexpr int x6_any_layer_bytes(int L) { return ks32(L) * layer_desc_all(L).ob * 3072; }
+__host__ __device__ constexpr int x6seq_layer_offset(int L0, int L) {
+  int o = 0;
+  for (int k = L0; k < L; ++k) o += x6_any_layer_bytes(k);
+  return o;
+}
+__host__ __device__ constexpr int x6seq_wbytes(int L0, int nl) { return x6seq_layer_offset(L0, L0 + nl); }
+__host__ __device__ constexpr int x6seq_image_bytes(int L0, int nl) { return x6seq_wbytes(L0, nl) + seq_bias_off(L0, nl) * 4; }
 
 // Gamma features in the bf16 image (EMB / VEMB segments of NS k-steps): element pairs (2p, 2p+1) of
 // lane half h in k-step t hold (sin, cos) of one argument x[comp] * 2^freq, so a lane evaluates one

@@ -45,7 +45,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 // bf16x3 kernels: hardware log/exp/rcp in the blend softmax and reciprocal-based lookup coordinates
 // bf16x6 layers: read the next out-block's fragments ahead of the current out-block's MFMAs
 #ifndef ANR_X6_PF
-#define ANR_X6_PF 1
+#define ANR_X6_PF 2
 #endif
 #ifndef ANR_FAST_MATH
 #define ANR_FAST_MATH 1
@@ -75,15 +75,24 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 //         (anr_layers.h sdfrev_desc: lin7 .. lin0 transposed), bf16x3, an image of its own.
 //   V = 3 (the sdf_pdf residual deformation MLP, k_resd_b16): entries 0..8 = layers 32..40
 //         (anr_layers.h resd_desc), bf16x3, from the sdf render's own image (k_pack_resd).
+//   V = 13, 15, 16, 17 (render precision ANR_BF16X6 of the sdf_pdf render): the programs 3, 5, 6, 7
+//         with every entry in mode 2 (bf16x6, fp32-level products), from bf16x6 sequence images
+//         (k_pack_seq_x6), the softplus and its backward factor at libm accuracy.
+template <int V>
+__host__ __device__ constexpr int prog_base() { return V >= 10 ? V - 10 : V; }
 template <int V>
 __host__ __device__ constexpr int prog_len() {
-  return V == 0 ? 30 : (V == 2 || V == 4) ? 28 : (V == 3 || V == 5) ? 9 : V == 7 ? 8 : V == 6 ? 5 : 18;  // 1, 8: 18
+  constexpr int B = prog_base<V>();
+  return B == 0 ? 30 : (B == 2 || B == 4) ? 28 : (B == 3 || B == 5) ? 9 : B == 7 ? 8 : B == 6 ? 5 : 18;  // 1, 8: 18
 }
 // programs whose weights are a packed layer sequence of their own (k_pack_seq), not the render image
 template <int V>
-__host__ __device__ constexpr bool prog_seq() { return V == 3 || V == 5 || V == 6 || V == 7; }
+__host__ __device__ constexpr bool prog_seq() {
+  return prog_base<V>() == 3 || prog_base<V>() == 5 || prog_base<V>() == 6 || prog_base<V>() == 7;
+}
 template <int V>
 __host__ __device__ constexpr int prog_layer(int e) {
+  if (V >= 10) return prog_layer<prog_base<V>()>(e);
   return V == 3 ? ANR_L_RESD0 + e
          : V == 5 ? ANR_L_SDF0 + e
          : V == 7 ? ANR_L_SREV0 + e
@@ -96,7 +105,9 @@ __host__ __device__ constexpr int prog_layer(int e) {
 }
 __host__ __device__ constexpr bool prog_pose(int e) { return e < 9; }
 template <bool B16, int V>
-__host__ __device__ constexpr int prog_mode(int e) { return B16 ? ((V == 4 || V == 8) ? 2 : e < 9 ? ANR_POSE_MODE : 1) : 0; }
+__host__ __device__ constexpr int prog_mode(int e) {
+  return B16 ? ((V == 4 || V == 8 || V >= 10) ? 2 : e < 9 ? ANR_POSE_MODE : 1) : 0;
+}
 // Slices = the staging unit: mode 0 8 fp32 k-steps; mode 1 one 32-input k-step (OB x 2 KiB);
 // mode 2 one 32-input k-step of a group of <= 8 out-blocks (x 3 KiB).
 template <int V>
@@ -111,6 +122,40 @@ template <int V>
 __host__ __device__ constexpr int x6_group_obs(int e, int gidx) {
   return layer_desc_all(prog_layer<V>(e)).ob - 8 * gidx < 8 ? layer_desc_all(prog_layer<V>(e)).ob - 8 * gidx : 8;
 }
+// bf16x6 layers: fragment G = t * OB + o (k-step t, out-block o) of entry E lives in slice
+// x6_slice_of(G) = t * NOBG + o / 8. At iteration F (before its MFMAs) the slices up to
+// x6_certified_at(F) may be read: the current one, and the next once the current slice's mid() (after
+// the MFMAs of its middle out-block) has certified it. Fragment G is read ANR_X6_PF iterations ahead
+// where that is certified, else at the first iteration where it is (never later than G itself).
+template <int V>
+__host__ __device__ constexpr int x6_slice_of(int e, int G) {
+  return (G / layer_desc_all(prog_layer<V>(e)).ob) * prog_nobg<V>(e) + (G % layer_desc_all(prog_layer<V>(e)).ob) / 8;
+}
+template <int V>
+__host__ __device__ constexpr int x6_certified_at(int e, int F) {
+  const int o = F % layer_desc_all(prog_layer<V>(e)).ob;
+  const int gob = x6_group_obs<V>(e, o / 8);
+  return x6_slice_of<V>(e, F) + (o % 8 > (gob - 1) / 2 ? 1 : 0);
+}
+template <int V>
+__host__ __device__ constexpr int x6_issue_at(int e, int G) {
+  int F = G - ANR_X6_PF > 0 ? G - ANR_X6_PF : 0;
+  while (x6_certified_at<V>(e, F) < x6_slice_of<V>(e, G)) ++F;
+  return F;
+}
+// every fragment read of an x6 layer targets a certified slice, at most one slice ahead, issued
+// no later than its use and after the previous occupant of its register set was consumed
+template <int V>
+__host__ __device__ constexpr bool x6_schedule_ok(int e) {
+  const int n = ks32(prog_layer<V>(e)) * layer_desc_all(prog_layer<V>(e)).ob;
+  for (int G = 0; G < n; ++G) {
+    const int F = x6_issue_at<V>(e, G);
+    if (F > G || F < G - ANR_X6_PF) return false;
+    if (x6_slice_of<V>(e, G) > x6_certified_at<V>(e, F)) return false;
+    if (x6_slice_of<V>(e, G) > x6_slice_of<V>(e, F) + 1 || x6_slice_of<V>(e, G) < x6_slice_of<V>(e, F)) return false;
+  }
+  return true;
+}
 template <bool B16, int V>
 __host__ __device__ constexpr int prog_slice_kb(int e, int q) {
   return prog_mode<B16, V>(e) == 2 ? x6_group_obs<V>(e, q % prog_nobg<V>(e)) * 3
@@ -122,7 +167,8 @@ __host__ __device__ constexpr int prog_slice_kb(int e, int q) {
 template <bool B16, int V>
 __host__ __device__ constexpr int prog_slice_off(int e, int q) {
   return prog_mode<B16, V>(e) == 2
-             ? x6_base() + x6_layer_offset(prog_layer<V>(e)) +
+             ? (prog_seq<V>() ? x6seq_layer_offset(prog_layer<V>(0), prog_layer<V>(e))
+                              : x6_base() + x6_layer_offset(prog_layer<V>(e))) +
                    ((q / prog_nobg<V>(e)) * layer_desc_all(prog_layer<V>(e)).ob + 8 * (q % prog_nobg<V>(e))) * 3072
          : prog_mode<B16, V>(e) == 1
              ? (prog_seq<V>() ? seq_layer_offset(prog_layer<V>(0), prog_layer<V>(e))
@@ -316,11 +362,12 @@ __device__ __forceinline__ void fill_bias_table(const MlpArgs& a, float* __restr
     constexpr int boff = bias_offset(L);  // constexpr: evaluated by the compiler, not per launch
     constexpr int toff = prog_bias_off<V>(e);
     const float* src;
-    if constexpr (V == 3) {  // sdf residual MLP: poses folded into layers 0 / 5 (k_sdf_fold)
+    constexpr int VB = prog_base<V>();
+    if constexpr (VB == 3) {  // sdf residual MLP: poses folded into layers 0 / 5 (k_sdf_fold)
       src = e == 0 ? a.fold : e == 5 ? a.fold + 256 : a.bias + toff;
-    } else if constexpr (V == 5 || V == 7) {  // sdf network (forward / gradient): the image's bias section
+    } else if constexpr (VB == 5 || VB == 7) {  // sdf network (forward / gradient): the image's bias section
       src = a.bias + toff;
-    } else if constexpr (V == 6) {  // colour network: color_latent folded into lin3 (k_sdf_fold)
+    } else if constexpr (VB == 6) {  // colour network: color_latent folded into lin3 (k_sdf_fold)
       src = e == 3 ? a.fold + 512 : a.bias + toff;
     } else if constexpr (e < 9) {
       src = L == 0 ? a.fold + 0 : L == 5 ? a.fold + 512 : a.bias + a.pose_boff + boff;
@@ -383,6 +430,23 @@ __device__ __forceinline__ float softplus100(float x) {
   const float h = __builtin_amdgcn_logf(1.0f + e) * 0.00693147181f;
   return x * 100.f > 20.f ? x : h;
 }
+
+// the fp32-level programs (V >= 10): torch's softplus(beta = 100, threshold = 20) = log1p(exp(100 x)) /
+// 100 on the libm-grade fast_exp / fast_log1p (<= 2e-7 relative), and the backward factor
+// sigmoid(100 z) = 1 - exp(-100 h) = -expm1(-100 h) from the output h (a short series where 100 h is
+// small, so the factor keeps its relative precision where it is tiny)
+__device__ __forceinline__ float softplus100_acc(float x) {
+  const float z = 100.f * x;
+  return z > 20.f ? x : fast_log1p(fast_exp(z)) / 100.f;
+}
+__device__ __forceinline__ float softplus_factor_h_acc(float h) {
+  const float t = 100.f * h;
+  return t < 0.03125f ? t * (1.f - t * (0.5f - t * (0.166666672f - t * 0.0416666679f))) : 1.f - fast_exp(-t);
+}
+template <int V>
+__device__ __forceinline__ float sp_fwd(float x) { return V >= 10 ? softplus100_acc(x) : softplus100(x); }
+template <int V>
+__device__ __forceinline__ float sp_factor(float h) { return V >= 10 ? softplus_factor_h_acc(h) : softplus_factor_h(h); }
 
 // SP_IN (the sdf network, V = 5): the previous layer's softplus(beta = 100) is applied in this layer's
 // split like RELU_IN (its VALU work beside this layer's MFMAs), and the softplus outputs h of the
@@ -580,8 +644,9 @@ __device__ __forceinline__ void layer(Pipe& p, const f32x4 (&in)[NIN], const flo
   constexpr int L = prog_layer<V>(E);
   constexpr LayerDesc D = layer_desc_all(L);
   static_assert(NOUT >= D.ob, "output array too small");
-  static_assert((SP_IN == 0 && FAC_IN == 0) || (prog_mode<B16, V>(E) == 1 && x3_stream_layer<L>()),
-                "SP_IN / FAC_IN on streamed layers only");
+  static_assert((SP_IN == 0 && FAC_IN == 0) || prog_mode<B16, V>(E) == 2 ||
+                    (prog_mode<B16, V>(E) == 1 && x3_stream_layer<L>()),
+                "SP_IN / FAC_IN on streamed bf16x3 or on bf16x6 layers only");
   if constexpr (prog_mode<B16, V>(E) == 1 && x3_stream_layer<L>()) {
     // output ReLU deferred to the consumer's split (RELU_IN of the next layer)
     layer_x3<B16, V, E, RELU_IN, SP_IN, FAC_IN>(p, in, emb, vemb, out, sbias, g, lane, io);
@@ -597,19 +662,136 @@ __device__ __forceinline__ void layer(Pipe& p, const f32x4 (&in)[NIN], const flo
       out[o] = *(const f32x4*)(sbias + BOFF + o * 16 + 4 * g);
     });
   };
-  if constexpr (prog_mode<B16, V>(E) != 0) {
+  if constexpr (prog_mode<B16, V>(E) == 2) {
+    // bf16x6 (mode 2): per k-step of 32 one hi/mid/lo split of the B fragment, per out-block 3 A
+    // reads and 6 MFMAs (smallest terms first). The A fragments are read ANR_X6_PF out-blocks ahead
+    // (x6_issue_at), across out-block groups and k-steps, into ANR_X6_PF + 1 register sets, but
+    // never from a slice its ring slot does not certifiably hold yet (x6_schedule_ok).
+    static_assert(x6_schedule_ok<V>(E), "bf16x6 fragment schedule reads an uncertified slice");
+    constexpr int KS = ks32(L);
+    constexpr int K0 = D.seg[0].ksteps / 8;
+    constexpr int OB = D.ob;
+    constexpr int NOBG = prog_nobg<V>(E);
+    constexpr int NS = ANR_X6_PF + 1;
+    bf16x8 fr[NS][3];
+    const unsigned char* buf = nullptr;
+    // FAC_IN: the stored h of the k-step's 8 input neurons, loaded one k-step ahead
+    f32x4 hv[2][2];
+    auto load_h = [&](auto tc) {
+      constexpr int t = decltype(tc)::value;
+      if constexpr (FAC_IN != 0 && t < KS) {
+        hv[t & 1][0] = *(const f32x4*)(io.fst + 32 * t + 4 * g);
+        hv[t & 1][1] = *(const f32x4*)(io.fst + 32 * t + 16 + 4 * g);
+      }
+    };
+    load_h(std::integral_constant<int, 0>{});
+    static_for<0, KS>([&](auto t) {
+      constexpr int tt = decltype(t)::value;
+      constexpr int seg = tt < K0 ? 0 : 1;
+      constexpr int ts = tt < K0 ? tt : tt - K0;
+      constexpr int kind = D.seg[seg].kind;
+      float x[8];
+      if constexpr (kind == SRC_EMB || kind == SRC_EMB6) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x[j] = emb[8 * ts + j];
+      } else if constexpr (kind == SRC_VEMB) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x[j] = vemb[j];
+      } else if constexpr (kind == SRC_G0 || kind == SRC_G1) {
+        // 8 consecutive columns of a memory row (the colour net's inputs); past nact: zero, not loaded
+        constexpr int NA = D.seg[seg].nact;
+        const int c0 = 32 * ts + 8 * g;
+        const float* gp = (kind == SRC_G0 ? io.g0 : io.g1) + c0;
+        f32x4 u = {0.f, 0.f, 0.f, 0.f}, w = {0.f, 0.f, 0.f, 0.f};
+        if (NA == 0 || c0 < NA) {
+          u = *(const f32x4*)gp;
+          w = *(const f32x4*)(gp + 4);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          x[j] = NA == 0 || c0 + j < NA ? u[j] : 0.0f;
+          x[4 + j] = NA == 0 || c0 + 4 + j < NA ? w[j] : 0.0f;
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          x[j] = RELU_IN ? fmaxf(in[2 * ts][j], 0.0f) : in[2 * ts][j];
+          x[4 + j] = RELU_IN ? fmaxf(in[2 * ts + 1][j], 0.0f) : in[2 * ts + 1][j];
+        }
+        if constexpr (FAC_IN != 0) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            x[j] = x[j] * sp_factor<V>(hv[tt & 1][0][j] * io.fscale);
+            x[4 + j] = x[4 + j] * sp_factor<V>(hv[tt & 1][1][j] * io.fscale);
+            if constexpr (FAC_IN == 2) {  // lin3: 217 inputs; the rest are gamma gradients (and X4's padding)
+              x[j] = 32 * ts + 4 * g + j < 217 ? x[j] : 0.0f;
+              x[4 + j] = 32 * ts + 16 + 4 * g + j < 217 ? x[4 + j] : 0.0f;
+            }
+          }
+          load_h(std::integral_constant<int, tt + 1>{});
+        }
+        if constexpr (SP_IN != 0) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) x[j] = sp_fwd<V>(x[j]);
+          if (io.spst) {  // neurons 32 ts + 4 g + (0..3) and 32 ts + 16 + 4 g + (0..3)
+            float* d = io.spst + 32 * ts + 4 * g;
+            if constexpr (SP_IN == 1) {
+              __builtin_nontemporal_store(f32x4{x[0], x[1], x[2], x[3]}, (f32x4*)d);
+              __builtin_nontemporal_store(f32x4{x[4], x[5], x[6], x[7]}, (f32x4*)(d + 16));
+            } else {
+              const float sqrt2 = 1.41421356237309515f;
+              const int c = 32 * ts + 4 * g;
+#pragma unroll
+              for (int j = 0; j < 4; ++j) {
+                if (c + j < 217) d[j] = x[j] / sqrt2;
+                if (c + 16 + j < 217) d[16 + j] = x[4 + j] / sqrt2;
+              }
+            }
+          }
+        }
+      }
+      bf16x8 bh, bm, bl;
+      split8x3(x, bh, bm, bl);
+      static_for<0, OB>([&](auto ob) {
+        constexpr int o = decltype(ob)::value;
+        constexpr int F = tt * OB + o;
+        constexpr int SQ = tt * NOBG + o / 8;  // the slice of this out-block group
+        if constexpr (o % 8 == 0) buf = p.template enter<B16, V, E, SQ>();
+        if constexpr (tt == 0 && o == 0) init_bias();
+        static_for<0, NS>([&](auto dd) {
+          constexpr int G = F + decltype(dd)::value;
+          if constexpr (G < KS * OB && x6_issue_at<V>(E, G) == F) {
+            constexpr int og = G % OB;
+            const unsigned char* src =
+                x6_slice_of<V>(E, G) == SQ ? buf : p.lds + (p.cur + 1 >= p.nbuf ? 0 : p.cur + 1) * p.smax;
+            fr[G % NS][0] = *(const bf16x8*)(src + (og % 8) * 3072 + lane * 16);
+            fr[G % NS][1] = *(const bf16x8*)(src + (og % 8) * 3072 + 1024 + lane * 16);
+            fr[G % NS][2] = *(const bf16x8*)(src + (og % 8) * 3072 + 2048 + lane * 16);
+          }
+        });
+        __builtin_amdgcn_sched_barrier(0);
+        const bf16x8 ah = fr[F % NS][0], am = fr[F % NS][1], al = fr[F % NS][2];
+        out[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, out[o], 0, 0, 0);
+        out[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, out[o], 0, 0, 0);
+        out[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bm, out[o], 0, 0, 0);
+        out[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bm, out[o], 0, 0, 0);
+        out[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bh, out[o], 0, 0, 0);
+        out[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, out[o], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        constexpr int GOB = x6_group_obs<V>(E, o / 8);
+        if constexpr (o % 8 == (GOB - 1) / 2) p.template mid<B16, V, E, SQ>();
+        if constexpr (o % 8 == GOB - 1) p.leave();
+      });
+    });
+  } else if constexpr (prog_mode<B16, V>(E) != 0) {
     // bf16x3 (mode 1): per k-step of 32 one hi/lo split of the B fragment, per out-block 2 A reads,
-    // 3 MFMAs; bf16x6 (mode 2): hi/mid/lo, 3 A reads, 6 MFMAs (smallest terms first)
-    constexpr bool X6 = prog_mode<B16, V>(E) == 2;
+    // 3 MFMAs
     constexpr int KS = ks32(L);
     constexpr int K0 = D.seg[0].ksteps / 8;
     static_for<0, KS>([&](auto t) {
       constexpr int tt = decltype(t)::value;
-      const unsigned char* buf = nullptr;
-      if constexpr (!X6) {
-        buf = p.template enter<B16, V, E, tt>();
-        if constexpr (tt == 0) init_bias();
-      }
+      const unsigned char* buf = p.template enter<B16, V, E, tt>();
+      if constexpr (tt == 0) init_bias();
       constexpr int seg = tt < K0 ? 0 : 1;
       constexpr int ts = tt < K0 ? tt : tt - K0;
       constexpr int kind = D.seg[seg].kind;
@@ -627,39 +809,7 @@ __device__ __forceinline__ void layer(Pipe& p, const f32x4 (&in)[NIN], const flo
           x[4 + j] = in[2 * ts + 1][j];
         }
       }
-      if constexpr (X6) {
-        bf16x8 bh, bm, bl;
-        split8x3(x, bh, bm, bl);
-        constexpr int NOBG = prog_nobg<V>(E);
-        // ANR_X6_PF: the next out-block's three fragments are read (within the slice) before this
-        // out-block's six MFMAs, so their LDS latency sits behind them
-        bf16x8 fr[2][3];
-        auto rd = [&](int slot, int oo) {
-          fr[slot][0] = *(const bf16x8*)(buf + (oo % 8) * 3072 + lane * 16);
-          fr[slot][1] = *(const bf16x8*)(buf + (oo % 8) * 3072 + 1024 + lane * 16);
-          fr[slot][2] = *(const bf16x8*)(buf + (oo % 8) * 3072 + 2048 + lane * 16);
-        };
-        static_for<0, D.ob>([&](auto ob) {
-          constexpr int o = decltype(ob)::value;
-          constexpr int SQ = tt * NOBG + o / 8;  // the slice of this out-block group
-          if constexpr (o % 8 == 0) buf = p.template enter<B16, V, E, SQ>();
-          if constexpr (tt == 0 && o == 0) init_bias();
-          if constexpr (!ANR_X6_PF || o % 8 == 0) rd(o & 1, o);
-          if constexpr (ANR_X6_PF && (o + 1) % 8 != 0 && o + 1 < D.ob) rd((o + 1) & 1, o + 1);
-          if constexpr (ANR_X6_PF) __builtin_amdgcn_sched_barrier(0);
-          const bf16x8 ah = fr[o & 1][0], am = fr[o & 1][1], al = fr[o & 1][2];
-          out[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, out[o], 0, 0, 0);
-          out[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, out[o], 0, 0, 0);
-          out[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bm, out[o], 0, 0, 0);
-          out[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bm, out[o], 0, 0, 0);
-          out[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bh, out[o], 0, 0, 0);
-          out[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, out[o], 0, 0, 0);
-          if constexpr (ANR_X6_PF) __builtin_amdgcn_sched_barrier(0);
-          constexpr int GOB = x6_group_obs<V>(E, o / 8);
-          if constexpr (o % 8 == (GOB - 1) / 2) p.template mid<B16, V, E, SQ>();
-          if constexpr (o % 8 == GOB - 1) p.leave();
-        });
-      } else {
+      {
         bf16x8 bh, bl;
         split8(x, bh, bl);
         // fragments of out-block o+PF are read while the MFMAs of o run (register double buffer),
@@ -710,7 +860,7 @@ __device__ __forceinline__ void layer(Pipe& p, const f32x4 (&in)[NIN], const flo
         p.leave();
       }
     });
-    if constexpr (!X6 && b16_tail_ob(L) > 0) {
+    if constexpr (b16_tail_ob(L) > 0) {
       // the out-blocks past 16 (alpha_fc beside feature_fc): one slice [k-step][tail block]
       constexpr int TOB = b16_tail_ob(L);
       const unsigned char* buf = p.template enter<B16, V, E, KS>();
@@ -1167,8 +1317,9 @@ __device__ __forceinline__ void alpha_body(const MlpArgs& a) {
 // (anisdf_pdf_network.py:49-73) per kept sample of one batch, all on chip — gamma_10 of the big-pose
 // point, 8 x 256 ReLU layers (poses folded into the layer-0 / layer-5 biases), resd_fc. Writes the
 // resd_fc output; k_sdf_mid applies 0.05 tanh. Replaces 8 layer GEMMs over HBM-resident activations.
+template <bool X6>
 __device__ __forceinline__ void resd_body(const MlpArgs& a) {
-  constexpr int V = 3;
+  constexpr int V = 3 + (X6 ? 10 : 0);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -1206,12 +1357,12 @@ __device__ __forceinline__ void resd_body(const MlpArgs& a) {
 }
 
 // softplus(beta = 100, threshold = 20) of the accumulators in place
-template <int NOB>
+template <int NOB, int V>
 __device__ __forceinline__ void softplus_regs(f32x4 (&v)[17]) {
   static_for<0, NOB>([&](auto ob) {
     constexpr int o = decltype(ob)::value;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) v[o][r] = softplus100(v[o][r]);
+    for (int r = 0; r < 4; ++r) v[o][r] = sp_fwd<V>(v[o][r]);
   });
 }
 
@@ -1221,8 +1372,9 @@ __device__ __forceinline__ void softplus_regs(f32x4 (&v)[17]) {
 // pass (the input gradient) and the colour net read is written once: every softplus output h (lin3's
 // as h / sqrt2 in X4, the layout of the layer-GEMM path) and lin8's sdf (Y8 column 0) and feature
 // (Y8 columns 8..263: 16-B aligned for k_color_b16's row loads).
+template <bool X6>
 __device__ __forceinline__ void sdfnet_body(const MlpArgs& a) {
-  constexpr int V = 5;
+  constexpr int V = 5 + (X6 ? 10 : 0);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -1271,7 +1423,7 @@ __device__ __forceinline__ void sdfnet_body(const MlpArgs& a) {
     layer<true, V, 5, false, false, 1>(p, A, emb, vemb, B, sb, g, lane, st(4));
     layer<true, V, 6, false, false, 1>(p, B, emb, vemb, A, sb, g, lane, st(5));
     layer<true, V, 7, false, false, 1>(p, A, emb, vemb, B, sb, g, lane, st(6));
-    softplus_regs<16>(B);  // lin8 (a tail-slice layer, not streamed) reads h7 as is
+    softplus_regs<16, V>(B);  // lin8 (a tail-slice layer, not streamed) reads h7 as is
     store_h(B, a.sdf_h[7]);
     layer<true, V, 8, false>(p, B, emb, vemb, A, sb, g, lane);  // [sdf || feature], no activation
     if (valid) {  // sdf (neuron 0) to column 0, the feature (neurons 1..256) to columns 8..263
@@ -1296,8 +1448,9 @@ __device__ __forceinline__ void sdfnet_body(const MlpArgs& a) {
 // MFMA B operand, lin7^T .. lin0^T the weights; each layer's input is multiplied by the softplus-backward
 // factor recomputed from the forward's stored h (FAC_IN). Writes the gamma_6 gradients (lin0's, and
 // the skip part of lin4's) for k_sdf_gamma_bwd. Replaces 8 reverse layer GEMMs over HBM activations.
+template <bool X6>
 __device__ __forceinline__ void sdfgrad_body(const MlpArgs& a) {
-  constexpr int V = 7;
+  constexpr int V = 7 + (X6 ? 10 : 0);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -1333,7 +1486,7 @@ __device__ __forceinline__ void sdfgrad_body(const MlpArgs& a) {
         const f32x4 hv = *(const f32x4*)(h7 + 16 * o);
         const f32x4 wv = *(const f32x4*)(sw8 + 16 * o + 4 * g);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) A[o][r] = wv[r] * softplus_factor_h(hv[r]);
+        for (int r = 0; r < 4; ++r) A[o][r] = wv[r] * sp_factor<V>(hv[r]);
       });
     }
     const float sqrt2 = 1.41421356237309515f;
@@ -1378,8 +1531,9 @@ __device__ __forceinline__ void sdfgrad_body(const MlpArgs& a) {
 // SDF net's feature from its Y8 row (columns 8..263, written there by k_sdfnet_b16), then
 // lin1..lin3 (ReLU deferred into the next split, the colour latent folded into lin3's bias), lin4's
 // three logits to yr ([n][4]); k_sdf_raw applies the sigmoid.
+template <bool X6>
 __device__ __forceinline__ void color_body(const MlpArgs& a) {
-  constexpr int V = 6;
+  constexpr int V = 6 + (X6 ? 10 : 0);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;

@@ -157,6 +157,53 @@ __global__ void k_pack_seq(PackArgs a, int L0, int nl, int sl, float sc) {
 }
 int seq_pack_threads(int L0, int nl) { return seq_wbytes(L0, nl) / 32 + seq_bias_off(L0, nl); }
 
+// k_pack_seq's layer sequence as a bf16x6 image (anr_layers.h x6seq_*): per (k-step, out-block) the
+// hi / mid / lo fragments (3 KiB, k_pack_x6's layout), then the biases as k_pack_seq lays them out.
+__global__ void k_pack_seq_x6(PackArgs a, int L0, int nl, int sl, float sc) {
+  const int u = blockIdx.x * blockDim.x + threadIdx.x;
+  const int nfrag = x6seq_wbytes(L0, nl) / 48;
+  if (u >= nfrag) {
+    const int e = u - nfrag;  // bias float
+    if (e >= seq_bias_off(L0, nl)) return;
+    int l = 0;
+    while (l + 1 < nl && e >= seq_bias_off(L0, l + 1)) ++l;
+    const LayerDesc d = layer_desc_all(L0 + l);
+    const int i = e - seq_bias_off(L0, l);
+    const float* b = a.t[d.tensor_b];
+    ((float*)(a.out + x6seq_wbytes(L0, nl)))[e] = (b && i < d.nout) ? b[i] : 0.0f;
+    return;
+  }
+  const int byte = u * 48;
+  int L = L0;
+  while (L + 1 < L0 + nl && byte >= x6seq_layer_offset(L0, L + 1)) ++L;
+  const LayerDesc d = layer_desc_all(L);
+  const int local = (byte - x6seq_layer_offset(L0, L)) / 48;  // (s, ob, lane)
+  const int lane = local & 63;
+  const int so = local >> 6;
+  const int ob = so % d.ob, t = so / d.ob;
+  const int row = ob * 16 + (lane & 15), h = lane >> 4;
+  const float f = L == L0 + sl ? sc : 1.0f;
+  unsigned short q[3][8];
+  for (int j = 0; j < 8; ++j) {
+    const int col = b16_col(d, t, h, j);
+    float v = 0.0f;
+    if (col >= 0 && row < d.nout && a.t[d.tensor_w] != nullptr)
+      v = a.t[d.tensor_w][d.trans ? (size_t)col * d.in_ch + row : (size_t)row * d.in_ch + col] * f;
+    q[0][j] = bf16_rne(v);
+    const float r1 = v - __uint_as_float((uint32_t)q[0][j] << 16);
+    q[1][j] = bf16_rne(r1);
+    q[2][j] = bf16_rne(r1 - __uint_as_float((uint32_t)q[1][j] << 16));
+  }
+  unsigned char* base = a.out + x6seq_layer_offset(L0, L) + (size_t)so * 3072;
+  for (int k = 0; k < 3; ++k) {
+    uint4 v;
+    v.x = q[k][0] | ((uint32_t)q[k][1] << 16); v.y = q[k][2] | ((uint32_t)q[k][3] << 16);
+    v.z = q[k][4] | ((uint32_t)q[k][5] << 16); v.w = q[k][6] | ((uint32_t)q[k][7] << 16);
+    *(uint4*)(base + k * 1024 + lane * 16) = v;
+  }
+}
+int seq_x6_pack_threads(int L0, int nl) { return x6seq_wbytes(L0, nl) / 48 + seq_bias_off(L0, nl); }
+
 // bf16x6 image (anr_layers.h): one thread per (layer, k-step, out-block, lane) writes hi, mid, lo fragments
 __global__ void k_pack_x6(PackArgs a) {
   const int u = blockIdx.x * blockDim.x + threadIdx.x;

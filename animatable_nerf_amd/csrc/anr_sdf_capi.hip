@@ -61,10 +61,12 @@ SLayout slayout(int n_rays, int chunk) {
   L.wimg = take(SDF_WN_FLOATS * 4);
   L.fold = take(768 * 4);
   L.limg = take(SDF_LIMG_BYTES);
-  L.rimg = take(seq_image_bytes(ANR_L_RESD0, ANR_RESD_LAYERS));
-  L.simg = take(seq_image_bytes(ANR_L_SDF0, ANR_SDF_LAYERS));
-  L.gimg = take(seq_image_bytes(ANR_L_SREV0, ANR_SREV_LAYERS));
-  L.cimg = take(seq_image_bytes(ANR_L_COL0, ANR_COL_LAYERS));
+  // the fused programs' images: bf16x3 (k_pack_seq) or bf16x6 (k_pack_seq_x6), sized for the larger
+  auto img = [&](int L0, int nl) { return take((size_t)std::max(seq_image_bytes(L0, nl), x6seq_image_bytes(L0, nl))); };
+  L.rimg = img(ANR_L_RESD0, ANR_RESD_LAYERS);
+  L.simg = img(ANR_L_SDF0, ANR_SDF_LAYERS);
+  L.gimg = img(ANR_L_SREV0, ANR_SREV_LAYERS);
+  L.cimg = img(ANR_L_COL0, ANR_COL_LAYERS);
   L.resd_rows = take(N * 3 * 4);
   L.grad_rows = take(N * 3 * 4);
   L.min_sdf = take(R * 4);
@@ -355,7 +357,17 @@ int sdf_render_core(const anr_sdf_params* p, const anr_sdf_frame* f, const float
   // (anr_resd_b16.hip), their weight images packed once per call (ANR_SDF_FUSED=0 keeps the layer
   // GEMMs, for A/B timing)
   const char* rf = getenv("ANR_SDF_FUSED");
-  const bool fused = o->precision == ANR_BF16X3 && !(rf && rf[0] == '0');
+  // ANR_BF16X6: the same four fused launches as fp32-level bf16x6 programs (always fused)
+  const bool x6 = o->precision == ANR_BF16X6;
+  const bool fused = x6 || (o->precision == ANR_BF16X3 && !(rf && rf[0] == '0'));
+  // the bf16x6 images' weight bytes (the bias section follows them)
+  auto wbytes = [&](int L0, int nl) { return x6 ? x6seq_wbytes(L0, nl) : seq_wbytes(L0, nl); };
+  auto pack = [&](const PackArgs& pa, int L0, int nl, int sl, float sc) {
+    const int nt = x6 ? seq_x6_pack_threads(L0, nl) : seq_pack_threads(L0, nl);
+    if (x6) hipLaunchKernelGGL(k_pack_seq_x6, dim3((nt + 255) / 256), dim3(256), 0, s, pa, L0, nl, sl, sc);
+    else hipLaunchKernelGGL(k_pack_seq, dim3((nt + 255) / 256), dim3(256), 0, s, pa, L0, nl, sl, sc);
+    return check_launch(x6 ? "k_pack_seq_x6" : "k_pack_seq");
+  };
   unsigned char* rimg = (unsigned char*)(ws + L.rimg);
   unsigned char* simg = (unsigned char*)(ws + L.simg);
   unsigned char* gimg = (unsigned char*)(ws + L.gimg);
@@ -369,34 +381,24 @@ int sdf_render_core(const anr_sdf_params* p, const anr_sdf_frame* f, const float
     pa.t[8] = tp[SDF_RFC_W];
     pa.t[17] = tp[SDF_RFC_B];
     pa.out = rimg;
-    int nt = seq_pack_threads(ANR_L_RESD0, ANR_RESD_LAYERS);
-    hipLaunchKernelGGL(k_pack_seq, dim3((nt + 255) / 256), dim3(256), 0, s, pa, ANR_L_RESD0, ANR_RESD_LAYERS, -1, 1.0f);
-    ANR_TRY(check_launch("k_pack_seq (resd)"));
+    ANR_TRY(pack(pa, ANR_L_RESD0, ANR_RESD_LAYERS, -1, 1.0f));
     PackArgs ps{};
     for (int l = 0; l < 9; ++l) {
       ps.t[l] = WN(l);
       ps.t[9 + l] = tp[3 * l];
     }
     ps.out = simg;
-    nt = seq_pack_threads(ANR_L_SDF0, ANR_SDF_LAYERS);
-    hipLaunchKernelGGL(k_pack_seq, dim3((nt + 255) / 256), dim3(256), 0, s, ps, ANR_L_SDF0, ANR_SDF_LAYERS, 4,
-                       1.0f / sqrt2);
-    ANR_TRY(check_launch("k_pack_seq (sdf)"));
+    ANR_TRY(pack(ps, ANR_L_SDF0, ANR_SDF_LAYERS, 4, 1.0f / sqrt2));
     for (int l = 9; l < 18; ++l) ps.t[l] = nullptr;  // no biases in the gradient pass
     ps.out = gimg;  // lin7 .. lin0 transposed, lin4's with the skip's 1/sqrt2 (entry 3)
-    nt = seq_pack_threads(ANR_L_SREV0, ANR_SREV_LAYERS);
-    hipLaunchKernelGGL(k_pack_seq, dim3((nt + 255) / 256), dim3(256), 0, s, ps, ANR_L_SREV0, ANR_SREV_LAYERS, 3,
-                       1.0f / sqrt2);
-    ANR_TRY(check_launch("k_pack_seq (sdf gradient)"));
+    ANR_TRY(pack(ps, ANR_L_SREV0, ANR_SREV_LAYERS, 3, 1.0f / sqrt2));
     PackArgs pc{};
     for (int l = 0; l < 5; ++l) {
       pc.t[l] = WN(9 + l);
       pc.t[9 + l] = l == 3 ? nullptr : tp[SDF_CLIN0 + 3 * l];  // lin3's bias: the latent fold
     }
     pc.out = cimg;
-    nt = seq_pack_threads(ANR_L_COL0, ANR_COL_LAYERS);
-    hipLaunchKernelGGL(k_pack_seq, dim3((nt + 255) / 256), dim3(256), 0, s, pc, ANR_L_COL0, ANR_COL_LAYERS, -1, 1.0f);
-    ANR_TRY(check_launch("k_pack_seq (colour)"));
+    ANR_TRY(pack(pc, ANR_L_COL0, ANR_COL_LAYERS, -1, 1.0f));
   }
   for (long b0 = 0; b0 < n; b0 += P) {
     const int cnt = (int)std::min<long>(P, n - b0);
@@ -418,13 +420,13 @@ int sdf_render_core(const anr_sdf_params* p, const anr_sdf_frame* f, const float
     if (fused) {
       MlpArgs ra{};
       ra.wimg = rimg;
-      ra.bias = (const float*)(rimg + seq_wbytes(ANR_L_RESD0, ANR_RESD_LAYERS));
+      ra.bias = (const float*)(rimg + wbytes(ANR_L_RESD0, ANR_RESD_LAYERS));
       ra.fold = fold;
       ra.ptb = a.ptb;
       ra.ptb_ld = 8;
       ra.yr = F(L.Yr);
       ra.n_rows = cnt;
-      if (launch_resd(ra, cus, s) != 0) return fail(ANR_E_HIP, "k_resd_b16 launch failed");
+      if (launch_resd(ra, cus, s, x6) != 0) return fail(ANR_E_HIP, "k_resd launch failed");
     } else {
     const float* Wr[8];
     for (int l = 0; l < 8; ++l) Wr[l] = tp[SDF_RLIN0 + 2 * l];
@@ -455,14 +457,14 @@ int sdf_render_core(const anr_sdf_params* p, const anr_sdf_frame* f, const float
     if (fused) {
       MlpArgs sa{};
       sa.wimg = simg;
-      sa.bias = (const float*)(simg + seq_wbytes(ANR_L_SDF0, ANR_SDF_LAYERS));
+      sa.bias = (const float*)(simg + wbytes(ANR_L_SDF0, ANR_SDF_LAYERS));
       sa.ptb = a.C0;
       sa.ptb_ld = 40;
       for (int l = 0; l < 8; ++l) sa.sdf_h[l] = Dl(l);
       sa.x4 = a.X4;
       sa.y8 = F(L.Y8);
       sa.n_rows = cnt;
-      if (launch_sdfnet(sa, cus, s) != 0) return fail(ANR_E_HIP, "k_sdfnet_b16 launch failed");
+      if (launch_sdfnet(sa, cus, s, x6) != 0) return fail(ANR_E_HIP, "k_sdfnet launch failed");
     } else {
     auto sp_fwd = [&](int l, int K, float* pingpong) -> int {
       float* out = sph ? Dl(l) : pingpong;
@@ -486,14 +488,14 @@ int sdf_render_core(const anr_sdf_params* p, const anr_sdf_frame* f, const float
     if (fused) {
       MlpArgs ga{};
       ga.wimg = gimg;
-      ga.bias = (const float*)(gimg + seq_wbytes(ANR_L_SREV0, ANR_SREV_LAYERS));
+      ga.bias = (const float*)(gimg + wbytes(ANR_L_SREV0, ANR_SREV_LAYERS));
       for (int l = 0; l < 8; ++l) ga.sdf_h[l] = Dl(l);
       ga.x4 = a.X4;
       ga.w8row = WN(8);
       ga.gb = F(L.gB);
       ga.gc = Gc;
       ga.n_rows = cnt;
-      if (launch_sdfgrad(ga, cus, s) != 0) return fail(ANR_E_HIP, "k_sdfgrad_b16 launch failed");
+      if (launch_sdfgrad(ga, cus, s, x6) != 0) return fail(ANR_E_HIP, "k_sdfgrad launch failed");
     } else {
     g.spd_h = sph ? 1 : 0;
     a.d7_h = sph ? 1 : 0;
@@ -526,14 +528,14 @@ int sdf_render_core(const anr_sdf_params* p, const anr_sdf_frame* f, const float
     if (fused) {
       MlpArgs ca{};
       ca.wimg = cimg;
-      ca.bias = (const float*)(cimg + seq_wbytes(ANR_L_COL0, ANR_COL_LAYERS));
+      ca.bias = (const float*)(cimg + wbytes(ANR_L_COL0, ANR_COL_LAYERS));
       ca.fold = fold;
       ca.ptb = a.C0;
       ca.ptb_ld = 40;
       ca.y8 = F(L.Y8);
       ca.yr = F(L.Yc);
       ca.n_rows = cnt;
-      if (launch_color(ca, cus, s) != 0) return fail(ANR_E_HIP, "k_color_b16 launch failed");
+      if (launch_color(ca, cus, s, x6) != 0) return fail(ANR_E_HIP, "k_color launch failed");
     } else {
     ANR_TRY(g.fwd(Ha, 256, 256, WN(9), 289, tp[29], a.C0, 40, 33, 0, true, nullptr, 0.f, false, F(L.Y8) + 1, 264, 256, 33));
     ANR_TRY(g.fwd(Hb, 256, 256, WN(10), 256, tp[32], Ha, 256, 256, 0, true));

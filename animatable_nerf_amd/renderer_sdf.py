@@ -30,6 +30,17 @@ def _f32(t, device):
     return t.to(device=device, dtype=torch.float32).contiguous()
 
 
+def _sdf_precision(cfg):
+    """cfg.render_precision (include/aninerf.h anr_render_opts.precision): 'fp32' exact fp32 MFMA layer
+    GEMMs; 'bf16x3' the four fused launches in split bf16 (hi/lo, 3 products per multiply-add); 'bf16x6'
+    the fused launches with hi/mid/lo bf16 (6 products, fp32-level, libm-grade softplus)."""
+    rprec = cfg.get('render_precision', 'fp32')
+    precs = {'fp32': _lib.FP32, 'bf16x3': _lib.BF16X3, 'bf16x6': _lib.BF16X6}
+    if rprec not in precs:
+        raise ValueError(f"render_precision must be one of {sorted(precs)}, got {rprec!r}")
+    return precs[rprec]
+
+
 def widen_tbounds(tbounds, k):
     """tbounds after the reference's in-place widening ran k times (anisdf_pdf_network.py:204-206):
     the same fp32 subtract / add per chunk as the device's k_sdf_tbtab, so the bits agree."""
@@ -89,12 +100,7 @@ class Renderer:
         o.n_samples, o.chunk, o.norm_th, o.train_th = ns, int(self.cfg.get('chunk', CHUNK)), NORM_TH, 0.0
         o.t_rand = tr.data_ptr() if tr is not None else None
         o.novel_pose = 0
-        # cfg.render_precision 'fp32' (exact fp32 MFMA GEMMs) or 'bf16x3' (split-bf16 MFMA GEMMs for the
-        # forward and input-gradient layers, fp32-level; include/aninerf.h anr_render_opts.precision)
-        rprec = self.cfg.get('render_precision', 'fp32')
-        if rprec not in ('fp32', 'bf16x3'):
-            raise ValueError(f"render_precision must be 'fp32' or 'bf16x3', got {rprec!r}")
-        o.precision = _lib.BF16X3 if rprec == 'bf16x3' else _lib.FP32
+        o.precision = _sdf_precision(self.cfg)
         return {'p': p, 'dev': dev, 'R': R, 'ns': ns, 'rays': rays, 'fr': fr, 't_rand': tr, 'li': li, 'occ': occ,
                 'frame': f, 'opts': o}
 
@@ -164,10 +170,7 @@ class Renderer:
         o = _lib.RenderOpts()
         o.n_samples, o.chunk, o.norm_th, o.train_th = int(self.cfg.N_samples), 1, NORM_TH, 0.0
         o.t_rand, o.novel_pose = None, 0
-        rprec = self.cfg.get('render_precision', 'fp32')
-        if rprec not in ('fp32', 'bf16x3'):
-            raise ValueError(f"render_precision must be 'fp32' or 'bf16x3', got {rprec!r}")
-        o.precision = _lib.BF16X3 if rprec == 'bf16x3' else _lib.FP32
+        o.precision = _sdf_precision(self.cfg)
         return {'fr': fr, 'li': li, 'frame': f, 'opts': o}
 
     @staticmethod

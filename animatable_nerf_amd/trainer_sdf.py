@@ -96,7 +96,9 @@ class NetworkWrapper(torch.nn.Module):
 class SdfStep:
     """Native sdf_pdf training step: ``step(batch)`` = anr_sdf_train_step + [RCCL mean all-reduce of
     the gradient blob with the losses in its tail] + clip_grad_value_(40) + Adam (optimizer.py:12-27,
-    trainer.py:64-68). Returns the device loss vector (LOSS_KEYS order, rank-averaged)."""
+    trainer.py:64-68). Returns the device loss vector (LOSS_KEYS order): with N > 1 ranks every entry
+    is the MEAN over the ranks, the count entries too (n_observed, msk_len, n_kept are then per-rank
+    averages, not totals: multiply by the world size for the job's counts)."""
 
     def __init__(self, net, cfg=None, lr=None, clip=40.0, betas=(0.9, 0.999), eps=1e-8, group=None):
         self.cfg = cfg if cfg is not None else _config.active()

@@ -72,9 +72,11 @@ def parse():
                          'training step (2 x 65,536 points, novel_pose_bw)')
     ap.add_argument('--voxel', type=float, default=0.005, help='mesh mode: cfg.voxel_size (aninerf_s9p.yaml:95)')
     ap.add_argument('--sdf-cpu-rays', type=int, default=2048)
-    ap.add_argument('--sdf-precision', choices=('fp32', 'bf16x3'), default='bf16x3',
-                    help='sdf mode GEMMs: exact fp32 MFMA, or split-bf16 (outputs held to the same tolerances by '
-                         'tests/test_gpu_sdf.py; 472 vs 559 ms per frame with the round-2 GEMM epilogue)')
+    ap.add_argument('--sdf-precision', choices=('fp32', 'bf16x6', 'bf16x3'), default='fp32',
+                    help='sdf mode value: exact fp32 MFMA layer GEMMs (config 5\'s arithmetic); bf16x6 / bf16x3: the '
+                         'four fused launches with hi/mid/lo (fp32-level) or hi/lo split-bf16 MFMA products (every '
+                         'precision held to the same tolerances by tests/test_gpu_sdf.py); the other two are timed '
+                         'beside it unless --no-exact')
     ap.add_argument('--no-exact', action='store_true', help='skip timing the other render precision')
     ap.add_argument('--no-host-render', action='store_true',
                     help='skip the render_s leg (Renderer.render with the D2H): PMC passes then see full-frame launches only')
@@ -492,63 +494,62 @@ def bench_sdf(args, rank, world, dev):
     network.load_numpy_state(net, sd)
     net = net.to(dev)
     net.train()
-    renderer = Renderer(net, cfg)
-    for _ in range(args.warmup):
-        batch['tbounds'].copy_(tb0)
-        out = renderer.render_device(batch)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        batch['tbounds'].copy_(tb0)
-        out = renderer.render_device(batch)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    dt_max = max_over_ranks(dt, dev, world)
-    n_kept = renderer.last_counts[0]
-    split = args.sdf_precision == 'bf16x3'
-    # bf16x3: every layer GEMM of the path is split (3 bf16 MFMA products per MAC) -> bf16 peak
-    flop_exec = FLOP_PER_KEPT_SDF * (3 if split else 1)
-    peak = PEAK_BF16_MFMA_TFLOPS if split else PEAK_FP32_MFMA_TFLOPS
-    achieved = n_kept * flop_exec * args.steps / dt_max / 1e12
+
+    def timed(prec, steps, warmup):
+        c = config.subject('anisdf_pdf_s9p', perturb=0, render_precision=prec)
+        r = Renderer(net, c)
+        for _ in range(warmup):
+            batch['tbounds'].copy_(tb0)
+            o = r.render_device(batch)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            batch['tbounds'].copy_(tb0)
+            o = r.render_device(batch)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        return o, max_over_ranks(time.perf_counter() - t0, dev, world), r.last_counts[0]
+
+    def sdf_roofline(prec, n_kept, dt_step):
+        prods = {'fp32': 1, 'bf16x6': 6, 'bf16x3': 3}[prec]
+        flop_exec = FLOP_PER_KEPT_SDF * prods
+        peak = PEAK_FP32_MFMA_TFLOPS if prec == 'fp32' else PEAK_BF16_MFMA_TFLOPS
+        achieved = n_kept * flop_exec / dt_step / 1e12
+        return {'bound': 'mfma', 'kernel': 'whole render (the network launches dominate)', 'achieved': achieved,
+                'peak': peak, 'unit': 'TFLOP/s', 'frac': achieved / peak, 'traffic': None,
+                'flop_per_kept': FLOP_PER_KEPT_SDF, 'flop_per_kept_executed': flop_exec,
+                'achieved_credited': n_kept * FLOP_PER_KEPT_SDF / dt_step / 1e12}
+
+    prec = args.sdf_precision
+    out, dt_max, n_kept = timed(prec, args.steps, args.warmup)
+    progress(f'sdf {prec}: {dt_max / args.steps * 1e3:.2f} ms/frame')
+    dtypes = {'fp32': 'fp32', 'bf16x6': 'bf16 MFMA operands (hi/mid/lo split, 6 products per MAC: fp32-level), fp32 accumulate',
+              'bf16x3': 'bf16 MFMA operands (hi/lo split, 3 products per MAC), fp32 accumulate'}
     result = {
         'metric': 'ray-samples/sec (512x512 rays x 64 samples), sdf_pdf render', 'value': R * 64 * args.steps * world / dt_max,
         'unit': 'ray-samples/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
         'ms_per_step': dt_max / args.steps * 1e3, 'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
-        'dtype': ('bf16 MFMA operands (hi/lo split, 3 products per MAC), fp32 accumulate' if split else 'fp32'),
-        'data': 'synthetic',
+        'dtype': dtypes[prec], 'data': 'synthetic',
         'config': {'workload': 'sdf_pdf (config 5 network) full 512x512 box-ray render, eval; outputs held to the '
-                               'fp32 tolerances of tests/test_gpu_sdf.py in both render precisions',
-                   'render_precision': args.sdf_precision,
+                               'fp32 tolerances of tests/test_gpu_sdf.py in every render precision',
+                   'render_precision': prec,
                    'rays_per_gpu': R, 'kept_fraction': n_kept / (R * 64), 'parallelism': f'replicas{world}'},
-        'roofline': {'bound': 'mfma', 'kernel': 'whole render (layer GEMMs dominate)', 'achieved': achieved,
-                     'peak': peak, 'unit': 'TFLOP/s', 'frac': achieved / peak,
-                     'traffic': None, 'flop_per_kept': FLOP_PER_KEPT_SDF, 'flop_per_kept_executed': flop_exec},
+        'roofline': sdf_roofline(prec, n_kept, dt_max / args.steps),
     }
-    if split and not args.no_exact:
-        # the same frame with every layer GEMM in exact fp32 MFMA (the reference's arithmetic), timed beside
-        cfg32 = config.subject('anisdf_pdf_s9p', perturb=0, render_precision='fp32')
-        r32 = Renderer(net, cfg32)
-        batch['tbounds'].copy_(tb0)
-        r32.render_device(batch)
-        torch.cuda.synchronize()
-        k32 = max(1, min(args.steps, 3))
-        t1 = time.perf_counter()
-        for _ in range(k32):
-            batch['tbounds'].copy_(tb0)
-            r32.render_device(batch)
-        torch.cuda.synchronize()
-        dt32 = max_over_ranks(time.perf_counter() - t1, dev, world) / k32
-        a32 = r32.last_counts[0] * FLOP_PER_KEPT_SDF / dt32 / 1e12
-        result['fp32_exact'] = {
-            'value': R * 64 * world / dt32, 'ms_per_step': dt32 * 1e3, 'steps': k32, 'render_precision': 'fp32',
-            'roofline': {'bound': 'mfma', 'achieved': a32, 'peak': PEAK_FP32_MFMA_TFLOPS, 'unit': 'TFLOP/s',
-                         'frac': a32 / PEAK_FP32_MFMA_TFLOPS, 'flop_per_kept': FLOP_PER_KEPT_SDF}}
-        progress(f'sdf fp32: {dt32 * 1e3:.2f} ms/frame')
+    if not args.no_exact:
+        names = {'fp32': 'fp32_exact', 'bf16x6': 'bf16x6_fp32_level', 'bf16x3': 'bf16x3_split'}
+        for other in [q for q in ('fp32', 'bf16x6', 'bf16x3') if q != prec]:
+            k = max(1, min(args.steps, 3 if other == 'fp32' else args.steps))
+            o2, dt2, nk2 = timed(other, k, 1)
+            progress(f'sdf {other}: {dt2 / k * 1e3:.2f} ms/frame')
+            result[names[other]] = {'value': R * 64 * k * world / dt2, 'ms_per_step': dt2 / k * 1e3, 'steps': k,
+                                    'render_precision': other, 'dtype': dtypes[other],
+                                    'roofline': sdf_roofline(other, nk2, dt2 / k)}
+            del o2
     if rank == 0 and world == 1 and not args.no_cpu:
         import sys
         sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))

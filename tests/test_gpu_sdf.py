@@ -26,10 +26,11 @@ def dev():
     return torch.device('cuda:0')
 
 
-@pytest.fixture(scope='module', params=['fp32', 'bf16x3'])
+@pytest.fixture(scope='module', params=['fp32', 'bf16x3', 'bf16x6'])
 def renderer(dev, request):
-    """Both render precisions at the same tolerances: exact fp32 MFMA GEMMs, and split-bf16
-    (hi/lo, three bf16 MFMAs per product) for the forward and input-gradient GEMMs."""
+    """Every render precision at the same tolerances: exact fp32 MFMA GEMMs; the four fused launches in
+    split bf16 (hi/lo, three bf16 MFMAs per product); the same launches in bf16x6 (hi/mid/lo, six
+    products, fp32-level)."""
     from animatable_nerf_amd.renderer_sdf import Renderer
     net = make_net_sdf(dev)
     net.train()
@@ -184,3 +185,43 @@ def test_knn_ties_resolved_by_vertex_index(renderer, dev):
     twin = np.all(pv[idx[:, :-1]] == pv[idx[:, 1:]], -1)
     assert twin.sum() > 100
     assert np.all(idx[:, :-1][twin] < idx[:, 1:][twin])
+
+
+@pytest.mark.parametrize('split', ['bf16x6', 'bf16x3'])
+def test_sdf_split_precisions_are_fp32_level(dev, split):
+    """As tests/test_gpu_render.py test_split_precisions_are_fp32_level, for the sdf_pdf render: against
+    an fp64 evaluation of the same network (oracle/restate_sdf.py in float64 on the same fp32 inputs, run
+    on the GPU with PyTorch), every output of the split-bf16 render -- raw, sdf, resd, gradients, rgb /
+    acc / depth, msk_sdf -- is within 1.5x the larger of the reference's own fp32 error (the fp32 oracle
+    on the GPU) and the exact fp32 MFMA render's (2,048 rays = one chunk of 131,072 samples). Keep mask
+    and msk_label agree exactly across the three."""
+    from animatable_nerf_amd.renderer_sdf import Renderer
+    sc = pdf_scene()
+    ro, rd = sc.box_rays(2048, seed=61)
+    b, _ = pdf_batch_np(sc, ro, rd)
+    keys = ('raw', 'sdf', 'resd', 'gradients', 'rgb_map', 'acc_map', 'depth_map', 'msk_sdf')
+
+    def oracle(dtype):
+        P = {k: v.to(dev, dtype) for k, v in oracle_params_sdf().items()}
+        bb = {k: (v.to(dev, dtype) if v.dtype == torch.float32 else v.to(dev)) for k, v in to_torch(b).items()}
+        with torch.no_grad():
+            return restate_sdf.render(P, bb)
+    r64 = oracle(torch.float64)
+    r32 = oracle(torch.float32)
+    keep64 = (r64['sdf'][0, :, 0] != 10).cpu()
+    assert torch.equal(keep64, (r32['sdf'][0, :, 0] != 10).cpu())
+    net = make_net_sdf(dev)
+    net.train()
+    got = {}
+    for prec in ('fp32', split):
+        cfg = sdf_cfg()
+        cfg.render_precision = prec
+        ret = Renderer(net, cfg).render_device(to_torch(b, dev))
+        assert torch.equal((ret['sdf'][0, :, 0] != 10).cpu(), keep64), prec
+        assert torch.equal(ret['msk_label'].cpu(), r64['msk_label'].float().cpu()), prec
+        got[prec] = {k: float((ret[k].double() - r64[k]).abs().max()) for k in keys}
+    ref_err = {k: float((r32[k].double() - r64[k]).abs().max()) for k in keys}
+    print(split, {k: (got[split][k], ref_err[k], got['fp32'][k]) for k in keys})
+    for k in keys:
+        bar = 1.5 * max(ref_err[k], got['fp32'][k])
+        assert got[split][k] <= bar, (k, got[split][k], ref_err[k], got['fp32'][k])

@@ -10,6 +10,12 @@
 #                     profiles/pmc_latest.json (tools/pmc_traffic.py)  -> TAG_pmc_KERNEL_{f,w}/
 #   sq:KERNEL[:ARGS]  two SQ counter passes (MFMA busy, waits, instruction mix) -> TAG_sq_KERNEL{1,2}/
 #   py:SCRIPT[:ARGS]  python SCRIPT ARGS                               -> TAG_py_NAME.log
+#   ab:LIB[:ARGS]     python bench.py ARGS with ANR_LIB_PATH=ab/LIB.so (an alternative build of the
+#                     same C-ABI, e.g. other -D options; same-box A/B)  -> TAG_ab_LIB[_MODE].log
+#   trace[:ARGS]      rocprofv3 --kernel-trace (per-dispatch timestamps, no stats) of bench ARGS
+#                     (tools/train_trace_summary.py, tools/sdf_batch_trace.py read it) -> TAG_trace[_MODE]/
+#   counters:KERNEL:C1+C2+..[:ARGS]  one --pmc pass with the given counters (<= the per-block limits)
+#                     over one bench step                              -> TAG_cnt_KERNEL/
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
@@ -85,6 +91,30 @@ for step in "$@"; do
       n=$(basename "$s" .py)
       timeout -k 10 600 python "$s" $(args_of "$a") > gpurun_out/${TAG}_py_$n.log 2>&1 || { tail -30 gpurun_out/${TAG}_py_$n.log; exit 1; }
       tail -n 3 gpurun_out/${TAG}_py_$n.log | cut -c1-600 ;;
+    ab)
+      lib=${rest%%:*}
+      a=${rest#*:}
+      [ "$a" = "$rest" ] && a=""
+      [ -f ab/$lib.so ] || { echo "ab/$lib.so missing"; exit 2; }
+      log=gpurun_out/${TAG}_ab_${lib}$(mode_of "$a").log
+      ANR_LIB_PATH=$PWD/ab/$lib.so timeout -k 10 600 python bench.py $(args_of "$a") > $log 2>&1 || { tail -20 $log; exit 1; }
+      tail -n 1 $log | cut -c1-400 ;;
+    trace)
+      m=$(mode_of "$rest")
+      timeout -k 10 600 rocprofv3 --kernel-trace -d gpurun_out/${TAG}_trace$m -o run --output-format csv -- \
+        python bench.py --no-cpu --no-torch-baseline $(args_of "$rest") > gpurun_out/${TAG}_trace$m.log 2>&1 \
+        || { tail -20 gpurun_out/${TAG}_trace$m.log; exit 1; }
+      echo "TRACE_OK $m" ;;
+    counters)
+      k=${rest%%:*}
+      r2=${rest#*:}
+      cs=${r2%%:*}
+      a=${r2#*:}
+      [ "$a" = "$r2" ] && a=""
+      B="python bench.py --steps 1 --warmup 0 --no-cpu --no-exact --no-torch-baseline --no-host-render $(args_of "$a")"
+      timeout -s KILL 180 rocprofv3 --pmc ${cs//+/ } --kernel-include-regex "$k" -d gpurun_out/${TAG}_cnt_$k -o p \
+        --output-format csv -- $B > gpurun_out/${TAG}_cnt_$k.log 2>&1 || { tail -20 gpurun_out/${TAG}_cnt_$k.log; exit 1; }
+      echo "COUNTERS_OK $k" ;;
     *)
       echo "unknown step $step"; exit 2 ;;
   esac

@@ -26,3 +26,33 @@ for p, q in zip(step[:-1], step[1:]):
 print('idle between kernels %.1f us; largest gaps:' % sum(max(g[0], 0) for g in gaps))
 for g in sorted(gaps, reverse=True)[:8]:
     print('  %7.1f us  %s -> %s' % g)
+
+# concurrency sweep: time with no kernel running (idle), and per kernel the time it runs ALONE (the
+# serial stretches of the step: every microsecond there is on the critical path)
+ev = []
+for k, r in enumerate(step):
+    ev.append((int(r['Start_Timestamp']), 1, k))
+    ev.append((int(r['End_Timestamp']), -1, k))
+ev.sort()
+running = set()
+alone = collections.defaultdict(float)
+idle = 0.0
+conc = collections.defaultdict(float)
+prev = ev[0][0]
+for t, d, k in ev:
+    dt = (t - prev) / 1e3
+    if dt > 0:
+        conc[len(running)] += dt
+        if not running:
+            idle += dt
+        elif len(running) == 1:
+            alone[step[next(iter(running))]['Kernel_Name'].replace('anr::', '')[:60]] += dt
+    prev = t
+    if d > 0:
+        running.add(k)
+    else:
+        running.discard(k)
+print('time by concurrency (us):', {c: round(v, 1) for c, v in sorted(conc.items())})
+print('kernels running alone (critical stretches), us:')
+for n, t in sorted(alone.items(), key=lambda x: -x[1])[:16]:
+    print('  %-60s %7.1f' % (n, t))
