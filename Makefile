@@ -30,3 +30,11 @@ clean:
 	rm -f $(OBJS) $(DEPS) $(LIB)
 
 .PHONY: all clean resources
+
+# layer-GEMM timing probe (tools/gemm_probe.hip), run on the GPU box
+PROBE := tools/gemm_probe
+probe: $(PROBE)
+$(PROBE): tools/gemm_probe.hip $(SRC_DIR)/anr_tgemm.o $(SRC_DIR)/anr_gemm.o $(SRC_DIR)/anr_lgemm.o
+	$(HIPCC) $(CXXFLAGS) -c tools/gemm_probe.hip -o tools/gemm_probe.o
+	$(HIPCC) --offload-arch=$(ARCH) -o $@ tools/gemm_probe.o $(filter %.o,$^)
+.PHONY: probe

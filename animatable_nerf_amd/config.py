@@ -72,6 +72,7 @@ def defaults():
         'N_samples': 64, 'N_rand': 1024, 'perturb': 1, 'white_bkgd': False,
         'xyz_res': 10, 'view_res': 4, 'norm_th': 0.05, 'train_th': 0.0, 'box_padding': 0.05,
         'aninerf_animation': False, 'test_novel_pose': False, 'eval': False, 'train_precision': 'fp32', 'render_precision': 'fp32',
+        'sdf_train_precision': 'fp32',
         'chunk': 2048, 'mesh_th': 50.0, 'voxel_size': [0.005, 0.005, 0.005],
         'train': {'lr': 5e-4, 'weight_decay': 0.0, 'optim': 'adam', 'epoch': 400,
                   'scheduler': {'type': 'exponential', 'gamma': 0.1, 'decay_epochs': 1000}},

@@ -497,12 +497,59 @@ struct Epi {
   float div_post = 0.f;
 };
 
+// x3 (o->precision ANR_BF16X3): the forward / input-gradient products as split-bf16 tiles (k_gemm_b
+// X3: lo*bh + hi*bl + hi*bh, fp32 accumulation, the same epilogues) and the weight gradients on the
+// split-bf16 slab kernel (anr_tgemm.hip k_wgrad X3) where its operand shapes fit; otherwise exact fp32
+// x3 products whose operands fit anr_lgemm.hip (no accumulate / mask, 16-B addressable rows) run on
+// k_lgemm, the weights' hi/lo fragment image resident in LDS: each distinct weight view (operand
+// pointers, strides, depths, N, bias) is packed into the arena once per call and reused by every
+// later product on it (the weights do not change inside one step).
+struct LgImage {
+  const float *B0, *B1, *bias;
+  long r0, c0, r1, c1;
+  int K0, K1, N;
+  void* img;
+};
+
 struct TG {
   hipStream_t s;
+  int x3 = 0;
+  float* slab = nullptr;  // k_wgrad partial slabs (x3)
+  char* lg_arena = nullptr;  // k_lgemm weight images (x3)
+  size_t lg_cap = 0, lg_used = 0;
+  int cus = 256;
+  LgImage lg[64];
+  int nlg = 0;
+  void* lg_image(const GemmArgs& g) {
+    const GemmSeg& a = g.seg[0];
+    const GemmSeg& b = g.seg[1];
+    const bool two = g.nseg > 1;
+    for (int i = 0; i < nlg; ++i) {
+      const LgImage& q = lg[i];
+      if (q.B0 == a.B && q.r0 == a.b_rs && q.c0 == a.b_cs && q.K0 == a.K && q.N == g.N && q.bias == g.bias &&
+          q.B1 == (two ? b.B : nullptr) && (!two || (q.r1 == b.b_rs && q.c1 == b.b_cs && q.K1 == b.K)))
+        return q.img;
+    }
+    const size_t bytes = (lgemm_image_bytes(g) + 255) / 256 * 256;
+    if (nlg >= 64 || lg_used + bytes > lg_cap) return nullptr;
+    void* img = lg_arena + lg_used;
+    if (lgemm_pack(g, img, s) != 0) return nullptr;
+    lg_used += bytes;
+    lg[nlg++] = LgImage{a.B, two ? b.B : nullptr, g.bias, a.b_rs, a.b_cs, two ? b.b_rs : 0, two ? b.b_cs : 0,
+                        a.K, two ? b.K : 0, g.N, img};
+    return img;
+  }
   int run(GemmArgs g, int M) {
     if (M <= 0 || g.N <= 0) return ANR_OK;
     g.M = M;
     if (g.ksplit < 1) g.ksplit = 1;
+    if (x3 && !g.atomic) g.x3 = 1;
+    if (g.x3 && lg_arena && lgemm_supported(g)) {
+      if (void* img = lg_image(g)) {
+        if (lgemm_run(g, img, cus, s) != 0) return check_launch("k_lgemm (sdf train)");
+        return ANR_OK;
+      }
+    }
     launch_gemm(g, dim3((g.N + 63) / 64, (M + 63) / 64, g.ksplit), s);
     return check_launch("k_gemm (sdf train)");
   }
@@ -525,6 +572,15 @@ struct TG {
   int wgrad(int M, float* dW, int in_ch, int c0, int Nout, const float* dY, long ldY, const float* X, long ldX, int K,
             float* bsum = nullptr) {
     if (M <= 0) return ANR_OK;
+    if (x3 && slab && Nout <= 256 && K <= 256 && ldY % 4 == 0 && ldX % 4 == 0 && ((uintptr_t)dY & 15) == 0 &&
+        ((uintptr_t)X & 15) == 0) {
+      WGrad w{};
+      w.x3 = 1;
+      w.dY = dY; w.ldY = ldY; w.nout = Nout; w.X = X; w.ldX = ldX; w.K = K;
+      w.dW = dW + c0; w.ldw = in_ch; w.bsum = bsum; w.slab = slab;
+      if (launch_wgrad(w, M, s) != 0) return check_launch("k_wgrad (sdf train)");
+      return ANR_OK;
+    }
     GemmArgs g{};
     g.rowsum = bsum;
     g.N = K;
@@ -547,13 +603,14 @@ struct TG {
 };
 
 constexpr float SQRT2 = 1.41421356237309515f;
+constexpr size_t kLgArena = (size_t)32 << 20;  // k_lgemm weight images of one call (x3)
 
 struct STLayout {
   size_t counts, mask, chunk_min, ray_off, block_sum, list, knn, tbtab, wimg, fold, inv;
   size_t ptb, Gr, Hr, Yr, resd, C0, Xs0, Hs, D, Y8, Ga, Gb, Gc, gB, grow, Hc, Yc;
   size_t raw, sdf, draw, drgb, rmin, ramin, rflag;
   size_t dYc, dHa, dHb, dC0, dZ8, ds, dG, rbar, tbar, ttbar, Ab, Zb, AX4, Ain, dWe, bsum, acc, acc3, dbeta, zero;
-  size_t oblock, ptbo, Gro, Grt, ro, og, dog, tdot, Gbar, Yd, gro;
+  size_t oblock, ptbo, Gro, Grt, ro, og, dog, tdot, Gbar, Yd, gro, wslab, lgimg;
   long N;
   size_t total;
 };
@@ -586,6 +643,8 @@ STLayout stlayout(int R, int chunk) {
   L.oblock = take(((N + 255) / 256 + 1) * 4); L.ptbo = f(N * 8); L.Gro = f(N * 64); L.Grt = f(N * 64);
   L.ro = f(N * 3); L.og = f(N * 4); L.dog = f(N * 4); L.tdot = f(N * 4); L.Gbar = f(N * 64); L.Yd = f(N * 4);
   L.gro = f(N * 3);
+  L.wslab = f(wgrad_slab_floats());
+  L.lgimg = take(kLgArena);
   L.total = o;
   return L;
 }
@@ -718,6 +777,13 @@ int sdf_train_core(const TrainCore& C) {
   hipLaunchKernelGGL(k_st_inv, dim3((n + 255) / 256 + 1), dim3(256), 0, s, (const int*)ca.list, (const int*)counts, inv);
 
   TG g{s};
+  if (o->precision == ANR_BF16X3) {
+    g.x3 = 1;
+    g.slab = F(L.wslab);
+    g.lg_arena = ws + L.lgimg;
+    g.lg_cap = kLgArena;
+    g.cus = cus;
+  }
   const dim3 pb(256), pg((n + 255) / 256 + 1);
   auto WN = [&](int l) { return (const float*)wimg + wn_layer(l).off; };
   float* dWe = F(L.dWe);

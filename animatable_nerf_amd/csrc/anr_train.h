@@ -96,8 +96,13 @@ struct RGemm {
   // C rows (RNE from the fp32 result) and the mask rows hold bf16 (C / mask reinterpreted as
   // unsigned short*). Not with x3; C bf16 excludes accumulate.
   int abf, cbf, mbf;
+  // epilogue through LDS (16-B row-chunk stores): < 0 never, 0 default (ANR_RG_STAGE), > 0 when the
+  // output rows allow it; launch_rgemm resolves it to 0 / 1
+  int stage;
 };
 void launch_rgemm(const RGemm& g, int M_host, hipStream_t s);
+// geometry variants for measurement: bm in {64, 128} rows per workgroup, ns ring slots (128: 2-3; 64: 3-4)
+int launch_rgemm_variant(const RGemm& g, int M_host, hipStream_t s, int bm, int ns);
 // bf16 weight images of the training GEMM weights: forward (rows = outputs, k = used input columns,
 // segments padded to 64) and backward (rows = input columns, k = outputs padded to 64). t: the
 // ANR_NUM_TENSORS network tensors followed by the ANR_NUM_NOVEL_TENSORS novel_pose_bw tensors
@@ -135,6 +140,7 @@ struct WGrad {
   int spb, nz, tiles, tj;
   int x3;  // split-bf16 products (fp32-level)
   int ybf, xbf;  // dY / X rows hold bf16 (reinterpreted as unsigned short*), not with x3
+  int deep;      // operand loads this many 64-sample steps ahead (k_wgrad_d: 2 or 4; 0: k_wgrad, one step)
 };
 size_t wgrad_slab_floats();
 int launch_wgrad(WGrad g, int n_host, hipStream_t s);

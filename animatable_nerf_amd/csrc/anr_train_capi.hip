@@ -6,6 +6,7 @@
 // count stays on the device (M_dev / K_dev in the GEMM arguments, capacity-sized grids), so no call
 // syncs with the host (the reference syncs ~6x per chunk).
 #include <algorithm>
+#include <cstring>
 #include <cmath>
 #include <cstdlib>
 #include <mutex>
@@ -91,12 +92,23 @@ int check_args(const anr_params* p, const anr_frame* f, const float* ray_o, cons
 // are per device, created once, ordered with the caller's stream by events (fork / join), so every
 // entry point still behaves as one asynchronous call on the caller's stream.
 // ANR_TRAIN_SERIAL=1 runs everything on the caller's stream (debugging aid).
+// Stream priorities (experiment switches, read once when the streams are created):
+// ANR_MAIN_PRIO=high issues a step's critical chain on the library's own highest-priority stream
+// `hp` (ordered after the caller's stream and joined back into it) with s2 at the same priority;
+// ANR_SIDE_PRIO=low creates the weight-gradient lanes at the lowest priority, so that the workgroup
+// dispatcher prefers the chain's workgroups whenever both are waiting for CUs.
 struct SideStreams {
   hipStream_t s2 = nullptr, sw[kWStreams] = {};
+  hipStream_t hp = nullptr;   // ANR_MAIN_PRIO=high: the high-priority chain stream (else NULL)
   hipStream_t cap = nullptr;  // origin stream of step-graph captures (created on first use)
   hipEvent_t ev[64] = {};
   unsigned next = 0;
 };
+
+static bool env_is(const char* name, const char* value) {
+  const char* v = getenv(name);
+  return v && strcmp(v, value) == 0;
+}
 
 SideStreams* side_streams() {
   static SideStreams per_dev[16];
@@ -109,9 +121,13 @@ SideStreams* side_streams() {
   SideStreams& ss = per_dev[d];
   if (!ss.s2) {
     SideStreams t{};
-    if (hipStreamCreateWithFlags(&t.s2, hipStreamNonBlocking) != hipSuccess) return nullptr;
+    int least = 0, greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) least = greatest = 0;
+    const bool main_high = env_is("ANR_MAIN_PRIO", "high"), side_low = env_is("ANR_SIDE_PRIO", "low");
+    if (hipStreamCreateWithPriority(&t.s2, hipStreamNonBlocking, main_high ? greatest : 0) != hipSuccess) return nullptr;
+    if (main_high && hipStreamCreateWithPriority(&t.hp, hipStreamNonBlocking, greatest) != hipSuccess) return nullptr;
     for (auto& w : t.sw)
-      if (hipStreamCreateWithFlags(&w, hipStreamNonBlocking) != hipSuccess) return nullptr;
+      if (hipStreamCreateWithPriority(&w, hipStreamNonBlocking, side_low ? least : 0) != hipSuccess) return nullptr;
     for (auto& e : t.ev)
       if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
     ss = t;
@@ -1047,9 +1063,15 @@ int anr_train_step_hooked(const anr_params* p, float* const* grads, const anr_fr
   // an external event (bucketed all-reduce) must be signalled by a plain record, and a ray split calls
   // its host hook mid-step: eager only
   const bool graphs = ss && !nerf_done && !splitting && gv && gv[0] == '1';
-  if (!graphs)
-    return train_step_body(p, grads, f, ray_o, ray_d, near_, far_, n_rays, o, rgb_gt, mask_at_box, out, loss3,
-                           nerf_done, ws, T, s, ss, splitting ? &split : nullptr);
+  if (!graphs) {
+    if (!ss || !ss->hp)
+      return train_step_body(p, grads, f, ray_o, ray_d, near_, far_, n_rays, o, rgb_gt, mask_at_box, out, loss3,
+                             nerf_done, ws, T, s, ss, splitting ? &split : nullptr);
+    ANR_TRY(order(ss, ss->hp, s));
+    ANR_TRY(train_step_body(p, grads, f, ray_o, ray_d, near_, far_, n_rays, o, rgb_gt, mask_at_box, out, loss3,
+                            nerf_done, ws, T, ss->hp, ss, splitting ? &split : nullptr));
+    return order(ss, s, ss->hp);
+  }
   std::string key;
   int dev = 0;
   (void)hipGetDevice(&dev);

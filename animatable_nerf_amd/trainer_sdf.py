@@ -29,6 +29,18 @@ LOSS_KEYS = ('loss', 'offset_loss', 'grad_loss', 'ograd_loss', 'mask_loss', 'img
 NLOSS = len(LOSS_KEYS)
 
 
+def train_precision(cfg):
+    """cfg.sdf_train_precision (anr_render_opts.precision of anr_sdf_train_step): 'fp32' exact fp32 MFMA
+    layer GEMMs; 'bf16x3' the forward / input-gradient products as split-bf16 tiles and the weight
+    gradients on the split-bf16 slab kernel (lo*bh + hi*bl + hi*bh, fp32 accumulation), held to the
+    same tolerances by tests/test_gpu_sdf_train.py."""
+    prec = cfg.get('sdf_train_precision', 'fp32')
+    precs = {'fp32': _lib.FP32, 'bf16x3': _lib.BF16X3}
+    if prec not in precs:
+        raise ValueError(f"sdf_train_precision must be one of {sorted(precs)}, got {prec!r}")
+    return precs[prec]
+
+
 def sdf_train_step(renderer, batch, grads, loss8, t_rand=None, iter_step=None):
     """One anr_sdf_train_step: ACCUMULATES the gradients of the 63 tensors into ``grads`` (list,
     state_dict order) and writes the NLOSS loss floats into ``loss8`` (device, no host sync of its own).
@@ -36,6 +48,7 @@ def sdf_train_step(renderer, batch, grads, loss8, t_rand=None, iter_step=None):
     lib = renderer.lib
     c = renderer.prepare(batch, t_rand)
     dev, R, rays, o = c['dev'], c['R'], c['rays'], c['opts']
+    o.precision = train_precision(renderer.cfg)
     rgb = torch.empty((1, R, 3), device=dev)
     acc = torch.empty((1, R), device=dev)
     depth = torch.empty((1, R), device=dev)

@@ -91,6 +91,9 @@ def parse():
                     help='fp32: exact fp32 MFMA; bf16x3: T-pose BW MLP + NeRF as hi/lo-split bf16 MFMA '
                          '(outputs within the 1e-4 fp32 tolerance, tests/test_gpu_render.py)')
     ap.add_argument('--train-rays', type=int, default=1024)
+    ap.add_argument('--sdf-train-precision', choices=('fp32', 'bf16x3'), default='fp32',
+                    help='sdf-train: layer GEMM products (cfg.sdf_train_precision): exact fp32 MFMA, or split-bf16 '
+                         '(fp32-level, tests/test_gpu_sdf_train.py tolerances)')
     ap.add_argument('--subject', choices=('aninerf_313', 'aninerf_s9p'), default=None,
                     help='train mode network shapes (config.SUBJECTS): default aninerf_313 at N=1 (config 3), '
                          'aninerf_s9p at N>1 (config 4)')
@@ -606,7 +609,7 @@ def bench_sdf_train(args, rank, world, dev):
         bt['iter_step'] = 12000
         batches.append(bt)
     tb0 = [b['tbounds'].clone() for b in batches]
-    cfg = config.subject('anisdf_pdf_s9p', perturb=1)
+    cfg = config.subject('anisdf_pdf_s9p', perturb=1, sdf_train_precision=args.sdf_train_precision)
     net = network_sdf.Network(cfg)
     sd = synthetic.init_state_dict_sdf({k: tuple(v.shape) for k, v in net.state_dict().items()})
     network.load_numpy_state(net, sd)
@@ -635,6 +638,8 @@ def bench_sdf_train(args, rank, world, dev):
     losses = dict(zip(LOSS_KEYS, l8.cpu().tolist()))  # rank means (the losses ride in the all-reduced blob)
     n_kept = losses['n_kept']
     achieved = n_kept * 2 * MAC_SDF_TRAIN / (dt_max / args.steps) / 1e12
+    # split-bf16: three bf16 MFMA products per multiply-add, priced against the bf16 dense peak / 3
+    peak = PEAK_FP32_MFMA_TFLOPS if args.sdf_train_precision == 'fp32' else PEAK_BF16_MFMA_TFLOPS / 3
     result = {
         'metric': 'sdf_pdf training ray-samples/s (1024 rays x 64 samples per GPU per step)',
         'value': R * 64 * args.steps * world / dt_max, 'unit': 'ray-samples/s', 'n_gpus': world, 'steps': args.steps,
@@ -642,9 +647,10 @@ def bench_sdf_train(args, rank, world, dev):
         'vs_baseline': None, 'dtype': 'fp32', 'data': 'synthetic',
         'config': {'workload': 'sdf_pdf training step (config 5: tpose_trainer losses incl. eikonal, observed '
                                'gradients, msk_sdf BCE, image MSE; Adam)', 'rays_per_gpu': R,
+                   'sdf_train_precision': args.sdf_train_precision,
                    'parallelism': f'dp{world} (RCCL mean all-reduce of the 1,432,510-float gradient blob + losses)'},
         'roofline': {'bound': 'mfma', 'kernel': 'whole step (layer GEMMs dominate)', 'achieved': achieved,
-                     'peak': PEAK_FP32_MFMA_TFLOPS, 'unit': 'TFLOP/s', 'frac': achieved / PEAK_FP32_MFMA_TFLOPS,
+                     'peak': peak, 'unit': 'TFLOP/s', 'frac': achieved / peak,
                      'traffic': None, 'flop_per_kept_executed_main_path': 2 * MAC_SDF_TRAIN,
                      'kept_samples_per_step': n_kept},
         'losses_last_step_rank_mean': losses,

@@ -53,6 +53,7 @@ def sample_blend_closest_points(src, ref, values, K=5, exp=1e-8):
     """sample_utils.py:323-348 -> blended weights (1,n,24), weighted distance (1,n,1)."""
     n_batch, n_points, _ = src.shape
     d2, vert_ids = knn_points(src, ref, K)
+    d2 = d2.to(src.dtype)  # the neighbour search is fp32 (pytorch3d); an fp64 run blends in fp64
     dists = d2.sqrt()                                          # guard_knn_points :309-311
     values = values.view(-1, values.shape[-1])
     disp = 1 / (dists + exp)

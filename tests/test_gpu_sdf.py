@@ -224,4 +224,6 @@ def test_sdf_split_precisions_are_fp32_level(dev, split):
     print(split, {k: (got[split][k], ref_err[k], got['fp32'][k]) for k in keys})
     for k in keys:
         bar = 1.5 * max(ref_err[k], got['fp32'][k])
+        if k == 'msk_sdf':  # a selection of sdf values (each ray's minimum): held to the sdf bar
+            bar = max(bar, 1.5 * max(ref_err['sdf'], got['fp32']['sdf']))
         assert got[split][k] <= bar, (k, got[split][k], ref_err[k], got['fp32'][k])

@@ -91,10 +91,10 @@ def test_network_forward_free_points_match_oracle(dev, n):
     wpts = torch.from_numpy(rng.uniform(lo - 0.05, hi + 0.05, size=(n, 3)).astype(np.float32))
     vd = torch.nn.functional.normalize(torch.from_numpy(rng.normal(size=(n, 3)).astype(np.float32)), dim=1)
     dists = torch.full((n,), 0.01)
+    bt = to_torch(b, dev)  # before the oracle call: bc shares b's arrays and is widened in place
     bc = to_torch(b)
     with torch.no_grad():
         ref = restate_sdf.network_forward(oracle_params_sdf(), wpts, vd, dists, bc)
-    bt = to_torch(b, dev)
     net = _net(dev)
     for call in range(2):  # a second call sees the bounds the first widened
         with torch.no_grad():

@@ -5,7 +5,9 @@ stub) and the oracle (oracle/restate_sdf.py render_train + loss_terms, autograd 
 Tolerances (the training tests' bars, tests/test_gpu_train.py): every loss term within 1e-4
 relative (+1e-6); every parameter gradient within 5e-3 of its tensor's largest magnitude, checked
 on all 62 differentiated tensors against the oracle and on the golden's kept tensors against G13.
-The observed-gradient row count and the in-place tbounds widening are exact."""
+The observed-gradient row count and the in-place tbounds widening are exact. Both training
+precisions (cfg.sdf_train_precision: 'fp32' exact MFMA, 'bf16x3' split-bf16 products) are held to
+these same bars."""
 import numpy as np
 import pytest
 import torch
@@ -27,13 +29,17 @@ def dev():
     return torch.device('cuda:0')
 
 
-def _device_step(dev, b, t_rand, iter_step):
+PRECS = ('fp32', 'bf16x3')
+
+
+def _device_step(dev, b, t_rand, iter_step, prec='fp32'):
     from animatable_nerf_amd import trainer_sdf
     from animatable_nerf_amd.renderer_sdf import Renderer
     net = make_net_sdf(dev)
     net.train()
     cfg = sdf_cfg()
     cfg.perturb = 1
+    cfg.sdf_train_precision = prec
     r = Renderer(net, cfg)
     grads = [torch.zeros_like(t) for t in net.tensors()]
     loss8 = torch.zeros(trainer_sdf.NLOSS, device=dev)
@@ -73,11 +79,12 @@ def _check(grads, loss8, P, ret, loss, stats, label):
     assert checked >= 60
 
 
-def test_g13_sdf_train_step_matches_reference_and_oracle(dev):
+@pytest.mark.parametrize('prec', PRECS)
+def test_g13_sdf_train_step_matches_reference_and_oracle(dev, prec):
     g = golden('g13_sdf_train')
     b = g13_batch(g)
     t_rand = torch.from_numpy(g['t_rand'])
-    grads, loss8, ret, bd = _device_step(dev, b, t_rand, int(g['iter_step']))
+    grads, loss8, ret, bd = _device_step(dev, b, t_rand, int(g['iter_step']), prec)
     # the reference step itself (G13)
     assert int(loss8[6]) == int(g['n_observed'])
     assert np.array_equal(bd['tbounds'].cpu().numpy(), g['tbounds_after'])
@@ -92,10 +99,11 @@ def test_g13_sdf_train_step_matches_reference_and_oracle(dev):
             assert err <= GRAD_TOL * ref.abs().max().item() + 1e-9, (key, err)
     # every tensor against the oracle (same inputs)
     P, oret, oloss, ostats, _ = _oracle(b, t_rand)
-    _check(grads, loss8, P, oret, oloss, ostats, 'g13')
+    _check(grads, loss8, P, oret, oloss, ostats, 'g13 ' + prec)
 
 
-def test_sdf_train_step_larger_batch_matches_oracle(dev):
+@pytest.mark.parametrize('prec', PRECS)
+def test_sdf_train_step_larger_batch_matches_oracle(dev, prec):
     """~700 box rays (one 2048-ray chunk, the reference's training batch shape), a mask_at_box with
     holes, iter_step past two mask-alpha milestones (alpha 200)"""
     sc = pdf_scene()
@@ -108,10 +116,10 @@ def test_sdf_train_step_larger_batch_matches_oracle(dev):
     b = to_torch(bnp)
     b['iter_step'] = 25000
     t_rand = torch.from_numpy(rng.random((R, 64)).astype(np.float32))
-    grads, loss8, _, bd = _device_step(dev, b, t_rand, 25000)
+    grads, loss8, _, bd = _device_step(dev, b, t_rand, 25000, prec)
     P, oret, oloss, ostats, bc = _oracle(b, t_rand)
     assert torch.equal(bd['tbounds'].cpu(), bc['tbounds'])
-    _check(grads, loss8, P, oret, oloss, ostats, 'R=%d' % R)
+    _check(grads, loss8, P, oret, oloss, ostats, '%s R=%d' % (prec, R))
 
 
 def test_network_wrapper_backward_and_native_step(dev):

@@ -14,6 +14,7 @@
 #                     same C-ABI, e.g. other -D options; same-box A/B)  -> TAG_ab_LIB[_MODE].log
 #   trace[:ARGS]      rocprofv3 --kernel-trace (per-dispatch timestamps, no stats) of bench ARGS
 #                     (tools/train_trace_summary.py, tools/sdf_batch_trace.py read it) -> TAG_trace[_MODE]/
+#   probe[:ARGS]      tools/gemm_probe ARGS (layer-GEMM kernels timed alone; make probe) -> TAG_probe.log
 #   counters:KERNEL:C1+C2+..[:ARGS]  one --pmc pass with the given counters (<= the per-block limits)
 #                     over one bench step                              -> TAG_cnt_KERNEL/
 set -o pipefail
@@ -44,21 +45,21 @@ for step in "$@"; do
       sel=()
       [ -n "$pat" ] && sel=(-k "$pat")
       timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 180 --timeout-method thread "${sel[@]}" \
-        > gpurun_out/${TAG}_gpu_tests.log 2>&1 || { tail -40 gpurun_out/${TAG}_gpu_tests.log; exit 1; }
+        > gpurun_out/${TAG}_gpu_tests.log 2>&1 || { rc=$?; tail -40 gpurun_out/${TAG}_gpu_tests.log; exit $rc; }
       tail -1 gpurun_out/${TAG}_gpu_tests.log ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1 \
-        || { tail -20 gpurun_out/${TAG}_smoke.log; exit 1; }
+        || { rc=$?; tail -20 gpurun_out/${TAG}_smoke.log; exit $rc; }
       tail -2 gpurun_out/${TAG}_smoke.log ;;
     bench)
       log=gpurun_out/${TAG}_bench$(mode_of "$rest").log
-      timeout -k 10 600 python bench.py $(args_of "$rest") > $log 2>&1 || { tail -20 $log; exit 1; }
+      timeout -k 10 600 python bench.py $(args_of "$rest") > $log 2>&1 || { rc=$?; tail -20 $log; exit $rc; }
       tail -n 1 $log | cut -c1-600 ;;
     prof)
       m=$(mode_of "$rest")
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof$m -o run --output-format csv -- \
         python bench.py --no-cpu --no-torch-baseline $(args_of "$rest") > gpurun_out/${TAG}_prof$m.log 2>&1 \
-        || { tail -20 gpurun_out/${TAG}_prof$m.log; exit 1; }
+        || { rc=$?; tail -20 gpurun_out/${TAG}_prof$m.log; exit $rc; }
       echo "PROF_OK $m" ;;
     pmc)
       k=${rest%%:*}
@@ -66,9 +67,9 @@ for step in "$@"; do
       [ "$a" = "$rest" ] && a=""
       B="python bench.py --steps 1 --warmup 0 --no-cpu --no-exact --no-torch-baseline --no-host-render $(args_of "$a")"
       timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$k" -d gpurun_out/${TAG}_pmc_${k}_f -o f \
-        --output-format csv -- $B > gpurun_out/${TAG}_pmc_${k}_f.log 2>&1 || { tail -20 gpurun_out/${TAG}_pmc_${k}_f.log; exit 1; }
+        --output-format csv -- $B > gpurun_out/${TAG}_pmc_${k}_f.log 2>&1 || { rc=$?; tail -20 gpurun_out/${TAG}_pmc_${k}_f.log; exit $rc; }
       timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$k" -d gpurun_out/${TAG}_pmc_${k}_w -o w \
-        --output-format csv -- $B > gpurun_out/${TAG}_pmc_${k}_w.log 2>&1 || { tail -20 gpurun_out/${TAG}_pmc_${k}_w.log; exit 1; }
+        --output-format csv -- $B > gpurun_out/${TAG}_pmc_${k}_w.log 2>&1 || { rc=$?; tail -20 gpurun_out/${TAG}_pmc_${k}_w.log; exit $rc; }
       f=$(ls gpurun_out/${TAG}_pmc_${k}_f/*counter_collection.csv | head -1)
       w=$(ls gpurun_out/${TAG}_pmc_${k}_w/*counter_collection.csv | head -1)
       python tools/pmc_traffic.py "$f" "$w" "$k" "profiles/pmc_${TAG} ($k)" || exit 1 ;;
@@ -89,7 +90,7 @@ for step in "$@"; do
       a=${rest#*:}
       [ "$a" = "$rest" ] && a=""
       n=$(basename "$s" .py)
-      timeout -k 10 600 python "$s" $(args_of "$a") > gpurun_out/${TAG}_py_$n.log 2>&1 || { tail -30 gpurun_out/${TAG}_py_$n.log; exit 1; }
+      timeout -k 10 600 python "$s" $(args_of "$a") > gpurun_out/${TAG}_py_$n.log 2>&1 || { rc=$?; tail -30 gpurun_out/${TAG}_py_$n.log; exit $rc; }
       tail -n 3 gpurun_out/${TAG}_py_$n.log | cut -c1-600 ;;
     ab)
       lib=${rest%%:*}
@@ -97,14 +98,19 @@ for step in "$@"; do
       [ "$a" = "$rest" ] && a=""
       [ -f ab/$lib.so ] || { echo "ab/$lib.so missing"; exit 2; }
       log=gpurun_out/${TAG}_ab_${lib}$(mode_of "$a").log
-      ANR_LIB_PATH=$PWD/ab/$lib.so timeout -k 10 600 python bench.py $(args_of "$a") > $log 2>&1 || { tail -20 $log; exit 1; }
+      ANR_LIB_PATH=$PWD/ab/$lib.so timeout -k 10 600 python bench.py $(args_of "$a") > $log 2>&1 || { rc=$?; tail -20 $log; exit $rc; }
       tail -n 1 $log | cut -c1-400 ;;
     trace)
       m=$(mode_of "$rest")
       timeout -k 10 600 rocprofv3 --kernel-trace -d gpurun_out/${TAG}_trace$m -o run --output-format csv -- \
         python bench.py --no-cpu --no-torch-baseline $(args_of "$rest") > gpurun_out/${TAG}_trace$m.log 2>&1 \
-        || { tail -20 gpurun_out/${TAG}_trace$m.log; exit 1; }
+        || { rc=$?; tail -20 gpurun_out/${TAG}_trace$m.log; exit $rc; }
       echo "TRACE_OK $m" ;;
+    probe)
+      [ -x tools/gemm_probe ] || { echo "tools/gemm_probe missing (make probe)"; exit 2; }
+      timeout -k 10 300 tools/gemm_probe $(args_of "$rest") > gpurun_out/${TAG}_probe.log 2>&1 \
+        || { rc=$?; tail -20 gpurun_out/${TAG}_probe.log; exit $rc; }
+      echo "PROBE_OK" ;;
     counters)
       k=${rest%%:*}
       r2=${rest#*:}
@@ -113,7 +119,7 @@ for step in "$@"; do
       [ "$a" = "$r2" ] && a=""
       B="python bench.py --steps 1 --warmup 0 --no-cpu --no-exact --no-torch-baseline --no-host-render $(args_of "$a")"
       timeout -s KILL 180 rocprofv3 --pmc ${cs//+/ } --kernel-include-regex "$k" -d gpurun_out/${TAG}_cnt_$k -o p \
-        --output-format csv -- $B > gpurun_out/${TAG}_cnt_$k.log 2>&1 || { tail -20 gpurun_out/${TAG}_cnt_$k.log; exit 1; }
+        --output-format csv -- $B > gpurun_out/${TAG}_cnt_$k.log 2>&1 || { rc=$?; tail -20 gpurun_out/${TAG}_cnt_$k.log; exit $rc; }
       echo "COUNTERS_OK $k" ;;
     *)
       echo "unknown step $step"; exit 2 ;;
