@@ -6,7 +6,7 @@ SRCS := $(SRC_DIR)/anr_capi.hip $(SRC_DIR)/anr_rays.hip $(SRC_DIR)/anr_mlp.hip $
         $(SRC_DIR)/anr_gemm.hip $(SRC_DIR)/anr_train.hip $(SRC_DIR)/anr_train_capi.hip \
         $(SRC_DIR)/anr_sdf.hip $(SRC_DIR)/anr_sdf_capi.hip $(SRC_DIR)/anr_mlp_b16.hip \
         $(SRC_DIR)/anr_alpha.hip $(SRC_DIR)/anr_alpha_b16.hip $(SRC_DIR)/anr_mesh.hip $(SRC_DIR)/anr_tgemm.hip $(SRC_DIR)/anr_lgemm.hip \
-        $(SRC_DIR)/anr_sdf_train.hip $(SRC_DIR)/anr_tchain.hip $(SRC_DIR)/anr_resd_b16.hip $(SRC_DIR)/anr_resd_x6.hip $(SRC_DIR)/anr_mlp_x6.hip $(SRC_DIR)/anr_alpha_x6.hip
+        $(SRC_DIR)/anr_sdf_train.hip $(SRC_DIR)/anr_resd_b16.hip $(SRC_DIR)/anr_resd_x6.hip $(SRC_DIR)/anr_mlp_x6.hip $(SRC_DIR)/anr_alpha_x6.hip
 OBJS := $(SRCS:.hip=.o)
 DEPS := $(OBJS:.o=.d)
 LIB := animatable_nerf_amd/libaninerf_hip.so
@@ -34,7 +34,8 @@ clean:
 # layer-GEMM timing probe (tools/gemm_probe.hip), run on the GPU box
 PROBE := tools/gemm_probe
 probe: $(PROBE)
-$(PROBE): tools/gemm_probe.hip $(SRC_DIR)/anr_tgemm.o $(SRC_DIR)/anr_gemm.o $(SRC_DIR)/anr_lgemm.o
+$(PROBE): tools/gemm_probe.hip $(SRC_DIR)/anr_tgemm.hip $(SRC_DIR)/anr_gemm.o $(SRC_DIR)/anr_lgemm.o
 	$(HIPCC) $(CXXFLAGS) -c tools/gemm_probe.hip -o tools/gemm_probe.o
-	$(HIPCC) --offload-arch=$(ARCH) -o $@ tools/gemm_probe.o $(filter %.o,$^)
+	$(HIPCC) $(CXXFLAGS) -DRG_TIMING -c $(SRC_DIR)/anr_tgemm.hip -o tools/gemm_probe_tgemm.o
+	$(HIPCC) --offload-arch=$(ARCH) -o $@ tools/gemm_probe.o tools/gemm_probe_tgemm.o $(filter %.o,$^)
 .PHONY: probe

@@ -353,13 +353,11 @@ int sdf_render_core(const anr_sdf_params* p, const anr_sdf_frame* f, const float
   limg.base = ws + L.limg;
   limg.cap = SDF_LIMG_BYTES;
   const int cus = sdf_cus();
-  // split-bf16: the residual MLP and the SDF network forward as one fused launch per batch each
-  // (anr_resd_b16.hip), their weight images packed once per call (ANR_SDF_FUSED=0 keeps the layer
-  // GEMMs, for A/B timing)
-  const char* rf = getenv("ANR_SDF_FUSED");
-  // ANR_BF16X6: the same four fused launches as fp32-level bf16x6 programs (always fused)
+  // split-bf16: the residual MLP, the SDF network forward, its input gradient and the colour net as
+  // one fused launch per batch each (anr_resd_b16.hip), their weight images packed once per call;
+  // ANR_BF16X6: the same four fused launches as fp32-level bf16x6 programs (anr_resd_x6.hip)
   const bool x6 = o->precision == ANR_BF16X6;
-  const bool fused = x6 || (o->precision == ANR_BF16X3 && !(rf && rf[0] == '0'));
+  const bool fused = x6 || o->precision == ANR_BF16X3;
   // the bf16x6 images' weight bytes (the bias section follows them)
   auto wbytes = [&](int L0, int nl) { return x6 ? x6seq_wbytes(L0, nl) : seq_wbytes(L0, nl); };
   auto pack = [&](const PackArgs& pa, int L0, int nl, int sl, float sc) {

@@ -514,6 +514,7 @@ struct LgImage {
 struct TG {
   hipStream_t s;
   int x3 = 0;
+  int wg_x3 = 1;          // x3: the weight gradients split-bf16 too
   float* slab = nullptr;  // k_wgrad partial slabs (x3)
   char* lg_arena = nullptr;  // k_lgemm weight images (x3)
   size_t lg_cap = 0, lg_used = 0;
@@ -572,7 +573,7 @@ struct TG {
   int wgrad(int M, float* dW, int in_ch, int c0, int Nout, const float* dY, long ldY, const float* X, long ldX, int K,
             float* bsum = nullptr) {
     if (M <= 0) return ANR_OK;
-    if (x3 && slab && Nout <= 256 && K <= 256 && ldY % 4 == 0 && ldX % 4 == 0 && ((uintptr_t)dY & 15) == 0 &&
+    if (x3 && wg_x3 && slab && Nout <= 256 && K <= 256 && ldY % 4 == 0 && ldX % 4 == 0 && ((uintptr_t)dY & 15) == 0 &&
         ((uintptr_t)X & 15) == 0) {
       WGrad w{};
       w.x3 = 1;
@@ -777,8 +778,23 @@ int sdf_train_core(const TrainCore& C) {
   hipLaunchKernelGGL(k_st_inv, dim3((n + 255) / 256 + 1), dim3(256), 0, s, (const int*)ca.list, (const int*)counts, inv);
 
   TG g{s};
-  if (o->precision == ANR_BF16X3) {
-    g.x3 = 1;
+  // which products run split-bf16 (bits, ANR_SDF_X3_PARTS): 1 residual MLP, 2 SDF forward, 4 SDF input
+  // gradient, 8 colour net, 16 SDF tangent pass, 32 stacked SDF reverse, 64 the weight gradients of the
+  // split parts. Default 124: all but the residual MLP and the SDF forward. The residual MLP's parameter
+  // gradients are ~1e-5 in magnitude and lose tests/test_gpu_sdf_train.py's 5e-3-of-max bar to split
+  // products in any of those two (the softplus(beta=100) factors of the SDF forward feed every
+  // second-order term); each other part split alone, and all of them together, keep it (profiles/r4e,
+  // r4g, r4h bisection)
+  static const int x3_parts = [] {
+    const char* v = getenv("ANR_SDF_X3_PARTS");
+    return v ? atoi(v) : 124;
+  }();
+  const bool x3_on = o->precision == ANR_BF16X3;
+  auto part = [&](int bit) {
+    g.x3 = x3_on && (x3_parts & bit) ? 1 : 0;
+    g.wg_x3 = g.x3 && (x3_parts & 64) ? 1 : 0;
+  };
+  if (x3_on) {
     g.slab = F(L.wslab);
     g.lg_arena = ws + L.lgimg;
     g.lg_cap = kLgArena;
@@ -809,6 +825,7 @@ int sdf_train_core(const TrainCore& C) {
 
   // residual MLP forward on n rows (primal half of Hr); poses folded into the biases of layers 0, 5
   auto resd_forward = [&](int m, const float* G, float* Y) -> int {
+    part(1);
     Epi r;
     r.relu = 1;
     ANR_TRY(g.fwd(m, Hr(0), 256, 256, Wr[0], 135, fold, G, 64, 63, 0, r));
@@ -820,6 +837,7 @@ int sdf_train_core(const TrainCore& C) {
   };
   // SDF forward on m rows with the stored softplus factors (lin8 into Y8 when given)
   auto sdf_forward = [&](int m, float* Y8) -> int {
+    part(2);
     Epi e;
     e.softplus = true;
     const float* hin = F(L.Xs0);
@@ -842,6 +860,7 @@ int sdf_train_core(const TrainCore& C) {
   // first-order input gradient of the SDF (the eval path's reverse chain): gradients -> C0[:, 30:33]
   auto sdf_input_grad = [&](SdfPointArgs& pa, int m) -> int {
     if (m <= 0) return ANR_OK;
+    part(4);
     pa.cnt = m;
     pa.d7_h = 0;
     hipLaunchKernelGGL(k_sdf_gtop, dim3((unsigned)(((long)m * 256 + 255) / 256)), pb, 0, s, pa);
@@ -867,6 +886,7 @@ int sdf_train_core(const TrainCore& C) {
   };
   // tangent forward of the SDF from the input tangent tdot (n,4): tangent rows of Xs0 / Hs
   auto sdf_tangent = [&](int m, const float* t, long ldt, const float* td) -> int {
+    part(16);
     float* Xt = F(L.Xs0) + (size_t)m * 40;
     hipLaunchKernelGGL(k_st_embed_tan, dim3((unsigned)(((long)m * 39 + 255) / 256)), pb, 0, s, t, ldt, td, 4L, 6, m, Xt,
                        40L, 0, 1.f);
@@ -892,6 +912,7 @@ int sdf_train_core(const TrainCore& C) {
   // -> dW (effective) / bias grads, tbar (+=, (m,4)), ttbar ((m,4), or NULL)
   auto sdf_reverse = [&](int m, const float* Z8, const float* t, long ldt, const float* td, float* tbar,
                          float* ttbar) -> int {
+    part(32);
     float* Ab = F(L.Ab);
     float* Zb = F(L.Zb);
     float* AX4 = F(L.AX4);
@@ -940,6 +961,7 @@ int sdf_train_core(const TrainCore& C) {
     ANR_TRY(sdf_forward(n, F(L.Y8)));
     ANR_TRY(sdf_input_grad(a, n));
     {
+      part(8);
       Epi r;
       r.relu = 1;
       ANR_TRY(g.fwd(n, Hc(0), 256, 256, WN(9), 289, tp[29], F(L.C0), 40, 33, 0, r, F(L.Y8) + 1, 264, 256, 33));
@@ -1002,6 +1024,7 @@ int sdf_train_core(const TrainCore& C) {
       hipLaunchKernelGGL(k_st_cotan_sdf, pg, pb, 0, s, (const int*)ca.list, (const int*)counts, C.d_sdf, F(L.ds));
     ANR_TRY(check_launch("sdf train: raw / msk backward"));
     // ---- colour net backward (weight-normed lin4..lin0; color_latent folded into lin3)
+    part(8);
     float *dHa = F(L.dHa), *dHb = F(L.dHb), *bsum = F(L.bsum);
     ANR_TRY(g.wgrad(n, dWN(13), 256, 0, 3, F(L.dYc), 4, Hc(3), 256, 256, grads[41]));
     ANR_TRY(g.xgrad(n, dHa, 256, 256, F(L.dYc), 4, 3, WN(13), 256, 0, Hc(3), 256));
@@ -1036,6 +1059,7 @@ int sdf_train_core(const TrainCore& C) {
     ANR_TRY(sdf_tangent(n, F(L.C0), 40, F(L.dG)));
     ANR_TRY(sdf_reverse(n, F(L.dZ8), F(L.C0), 40, F(L.dG), F(L.tbar), nullptr));
     // ---- residual net: r_bar = t_bar + offset adjoint -> tanh -> ReLU layers (first order)
+    part(1);
     float* yb = F(L.Yd);
     hipLaunchKernelGGL(k_st_tanh_rev, pg, pb, 0, s, (const float*)F(L.Yr), (const float*)nullptr,
                        (const float*)F(L.tbar), (const float*)F(L.rbar), (const float*)nullptr, n, yb);
@@ -1088,6 +1112,7 @@ int sdf_train_core(const TrainCore& C) {
     ANR_TRY(check_launch("k_sdf_mid (observed)"));
     ANR_TRY(sdf_forward(n_o, nullptr));
     ANR_TRY(sdf_input_grad(ao, n_o));
+    part(1);
     float *dHa = F(L.dHa), *dHb = F(L.dHb), *Gbar = F(L.Gbar);
     float* yb = F(L.Yd);
     // y_bar = 0.05 (1 - tau^2) g_t; reverse of the ReLU net to its gamma_10 input (input gradient only)
@@ -1145,6 +1170,7 @@ int sdf_train_core(const TrainCore& C) {
     float* ttbar = F(L.ttbar);
     if (hipMemsetAsync(tbar, 0, (size_t)n_o * 16, s) != hipSuccess) return fail(ANR_E_HIP, "memset");
     ANR_TRY(sdf_reverse(n_o, nullptr, F(L.C0), 40, F(L.tdot), tbar, ttbar));
+    part(1);
     float* ybs = F(L.Ab);  // [2 n_o][4]: y_bar, ydot_bar (the SDF adjoint buffer is free again)
     hipLaunchKernelGGL(k_st_tanh_rev, og_, pb, 0, s, (const float*)F(L.Yr), (const float*)Yd, (const float*)tbar,
                        (const float*)nullptr, (const float*)ttbar, n_o, ybs);

@@ -11,8 +11,6 @@
 // accumulation; the activations rounded to bf16 RNE as their fragments are read, as the generic
 // kernel rounds them at staging). LDS images are XOR-swizzled through the DMA source addresses.
 // Epilogue order as anr_gemm.hip: bias, accumulate, ReLU, mask.
-#include <cstdio>
-#include <cstdlib>
 #include <vector>
 
 #include "anr_common.h"
@@ -183,24 +181,28 @@ bool wimg_view(const void* base, const float* const* t, const float* W, int c0, 
 // weight image each workgroup streams serves 128 rows. bf16: 64-deep K chunks. X3 (split-bf16,
 // fp32-level: lo*h + h*lo + h*h, the weight rows' lo image riding in the same slot): 32-deep chunks
 // so that three 128-row operand images fit two slots.
-// BM_ / NS_: rows per workgroup (128: 8 waves = 2 row groups x 4 column groups; 64: 4 waves, one row
-// group) and ring slots (chunks in flight behind the one being multiplied: NS_ - 1)
-template <bool X3, bool ABF = false, int BM_ = 128, int NS_ = 2> struct RgCfg {
-  static constexpr int BM = BM_;
+// SM (bf16 products only): 32-deep chunks in a 3-slot ring, 72 KiB of LDS with bf16 rows (96 KiB
+// fp32), so that two row GEMMs (two streams) fit one CU and one's load / store bursts overlap the
+// other's MFMAs
+template <bool X3, bool ABF = false, bool SM = false> struct RgCfg {
+  static_assert(!(SM && X3), "SM: bf16 products");
+  static constexpr int BM = 128;
   static constexpr int WAVES = BM / 16;
-  static constexpr int KC = X3 ? 32 : 64;                              // K chunk
+  static constexpr int KC = X3 || SM ? 32 : 64;                        // K chunk
   static constexpr int AE = ABF ? 2 : 4;                               // bytes per activation element
   static constexpr int A_BYTES = BM * KC * AE;                         // activations, BM rows x KC
   static constexpr int B_BYTES = 256 * KC * 2;                         // bf16 weight rows, 256 x KC
-  static constexpr int NS = NS_;                                       // ring slots
+  static constexpr int NS = SM ? 3 : 2;                                // ring slots
   static constexpr int SLOT = A_BYTES + B_BYTES * (X3 ? 2 : 1);        // bytes per slot
   static constexpr int PIECES_A = A_BYTES / 1024 / WAVES;              // per wave
   static constexpr int PIECES_B = B_BYTES / 1024 / WAVES;
   static constexpr int OPS = PIECES_A + PIECES_B * (X3 ? 2 : 1);       // vmem ops per wave per chunk
   static constexpr int CHA = KC * AE / 16, CHB = KC / 8;              // 16-B chunks per A / B row
   // XOR swizzle of a row's 16-B chunks, chosen so the 16 rows of one fragment read hit distinct banks
-  static __device__ __forceinline__ int swa(int r) { return X3 ? ((r >> 1) & 7) : ABF ? (r & 7) : (r & 15); }
-  static __device__ __forceinline__ int swb(int r) { return X3 ? ((r >> 2) & 3) : (r & 7); }
+  static __device__ __forceinline__ int swa(int r) {
+    return X3 ? ((r >> 1) & 7) : SM ? (ABF ? ((r >> 2) & 3) : ((r >> 1) & 7)) : ABF ? (r & 7) : (r & 15);
+  }
+  static __device__ __forceinline__ int swb(int r) { return X3 || SM ? ((r >> 2) & 3) : (r & 7); }
 };
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
@@ -216,10 +218,10 @@ __device__ __forceinline__ void rg_dma(const void* src, unsigned m0) {
 }
 
 // issue chunk c (segment-relative K offset kk) into ring slot `slot`
-template <bool X3, bool ABF, int BM_, int NS_>
+template <bool X3, bool ABF, bool SM>
 __device__ __forceinline__ void rg_issue(const RGemm& g, int seg, int kk, int m0, int M, int N, unsigned slot_lds, int w,
                                          int lane) {
-  using C = RgCfg<X3, ABF, BM_, NS_>;
+  using C = RgCfg<X3, ABF, SM>;
   const unsigned char* A = (const unsigned char*)(seg ? g.seg[1].A : g.seg[0].A);
   const long lda = seg ? g.seg[1].lda : g.seg[0].lda;
   const unsigned short* B = seg ? g.seg[1].B : g.seg[0].B;
@@ -262,9 +264,28 @@ __device__ __forceinline__ void rg_issue(const RGemm& g, int seg, int kk, int m0
 
 // MBF: the mask rows are bf16 (a template parameter, so every epilogue load stays one straight-line
 // batch ahead of its use; a runtime branch around them would drain the loads one by one)
-template <bool X3, bool ABF, bool MBF, int BM_ = 128, int NS_ = 2>
-__global__ __launch_bounds__(BM_ / 16 * 64) void k_rgemm(RGemm g) {
-  using CF = RgCfg<X3, ABF, BM_, NS_>;
+// RG_TIMING (tools/gemm_probe's own build of this file only): wave 0 of every workgroup records the
+// shader clock at the phase boundaries (start, prologue issued, each chunk's data ready, loop end,
+// epilogue done) into rg_tbuf[block][16]
+#ifdef RG_TIMING
+__device__ unsigned long long* rg_tbuf;
+#define RG_T(i)                                                                                \
+  do {                                                                                         \
+    if (threadIdx.x < 64) {                                                                    \
+      const unsigned long long t_ = __builtin_amdgcn_s_memtime();                              \
+      if (threadIdx.x == 0 && rg_tbuf) rg_tbuf[(long)blockIdx.x * 16 + (i)] = t_;              \
+    }                                                                                          \
+  } while (0)
+void rg_timing_buffer(unsigned long long* p) { (void)hipMemcpyToSymbol(HIP_SYMBOL(rg_tbuf), &p, sizeof(p)); }
+#else
+#define RG_T(i) \
+  do {          \
+  } while (0)
+#endif
+
+template <bool X3, bool ABF, bool MBF, bool SM = false>
+__global__ __launch_bounds__(RgCfg<X3>::WAVES * 64) void k_rgemm(RGemm g) {
+  using CF = RgCfg<X3, ABF, SM>;
   constexpr int RG_NS = CF::NS, RG_SLOT = CF::SLOT, RG_OPS = CF::OPS;
   constexpr int RG_BM = CF::BM, RG_A_BYTES = CF::A_BYTES;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -280,29 +301,53 @@ __global__ __launch_bounds__(BM_ / 16 * 64) void k_rgemm(RGemm g) {
   auto issue = [&](int c) {
     const int seg = c < nc0 ? 0 : 1;
     const int kk = (c - (seg ? nc0 : 0)) * KC;
-    rg_issue<X3, ABF, BM_, NS_>(g, seg, kk, m0, M, N, base + (c % RG_NS) * RG_SLOT, w, lane);
+    rg_issue<X3, ABF, SM>(g, seg, kk, m0, M, N, base + (c % RG_NS) * RG_SLOT, w, lane);
   };
+  RG_T(0);
+  const int wr = (w >> 2) * 64;   // this wave's 64 rows of the tile
+  const int wc = (w & 3) * 64;    // and 64 output columns
+  const bool active = wc < N;     // which hold some of the N
+  // the epilogue's bias columns load now, ahead of the ring (older than every DMA, so the counted
+  // vmcnt waits below retire them first); the bf16 mask rows load at the last chunk (below): the
+  // epilogue then finds its operands in registers (tools/gemm_probe phase clocks: the epilogue was
+  // 4.1 us of an 11 us workgroup, 7.2 us with the mask)
+  f32x4 bj[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int n = min(wc + 16 * j + 4 * (lane >> 4), N - 4);
+    bj[j] = (g.vec_out && g.bias && active) ? *(const f32x4*)(g.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
   const int pro = nch < RG_NS ? nch : RG_NS;
   for (int c = 0; c < pro; ++c) issue(c);
+  RG_T(1);
 
   f32x4 acc[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int wr = (w >> 2) * 64;   // this wave's 64 rows of the tile
-  const int wc = (w & 3) * 64;    // and 64 output columns
-  const bool active = wc < N;     // which hold some of the N
+  uint2 mk16[4][4];  // MBF vec_out: the mask's bf16 quads in the accumulator layout
+  const bool early_mask = MBF && g.vec_out && g.mask != nullptr && active;
 
   for (int c = 0; c < nch; ++c) {
     // chunks issued after c: min(nch, c + RG_NS) - c - 1 (the refill of c - 1's slot went out last iteration)
     const int later = (nch < c + RG_NS ? nch : c + RG_NS) - c - 1;
-    static_assert(RG_NS <= 4 && (RG_NS - 1) * RG_OPS < 64, "vmcnt range");
-    if (later >= 3) rg_wait<(RG_NS > 3 ? 3 * RG_OPS : 0)>();
-    else if (later == 2) rg_wait<(RG_NS > 2 ? 2 * RG_OPS : 0)>();
+    if (later >= 2) rg_wait<(RG_NS > 2 ? 2 * RG_OPS : 0)>();
     else if (later == 1) rg_wait<RG_OPS>();
     else rg_wait<0>();
     __builtin_amdgcn_s_barrier();
+    RG_T(2 + (c < 9 ? c : 9));
+    if (early_mask && c == nch - 1) {  // every DMA has landed (wait 0 above): these are the youngest loads
+      const unsigned short* mask16 = (const unsigned short*)g.mask;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const long m = min(m0 + wr + 16 * i + (lane & 15), M - 1);
+          const int n = min(wc + 16 * j + 4 * (lane >> 4), N - 4);
+          mk16[i][j] = *(const uint2*)(mask16 + m * g.ldm + n);
+        }
+    }
     const int seg = c < nc0 ? 0 : 1;
     const int kk = (c - (seg ? nc0 : 0)) * KC;
     const int K = seg ? g.seg[1].K : g.seg[0].K;
@@ -365,8 +410,8 @@ __global__ __launch_bounds__(BM_ / 16 * 64) void k_rgemm(RGemm g) {
     if (c + RG_NS < nch) issue(c + RG_NS);
   }
   rg_wait<0>();
-  const bool stage = g.stage > 0;  // uniform: every wave takes part in the staged store's barriers
-  if (!active && !stage) return;
+  RG_T(12);
+  if (!active) return;
   // weights are the MFMA A operand, so lane l holds C[16 i + (l & 15)][64 w + 16 j + 4 (l >> 4) + r],
   // r = 0..3: four consecutive columns of one row, stored as one 16-B store (vec_out). Every
   // operand load of the epilogue is issued before the first use.
@@ -374,84 +419,71 @@ __global__ __launch_bounds__(BM_ / 16 * 64) void k_rgemm(RGemm g) {
   unsigned short* C16 = (unsigned short*)g.C;
   auto bf2f = [](unsigned short b) { return __uint_as_float((uint32_t)b << 16); };
   if (g.vec_out) {
-    if (active) {
-      f32x4 cv[4][4], mk[4][4], bj[4];
+    f32x4 cv[4][4], mk[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
+        const long m = min(m0 + wr + 16 * i + (lane & 15), M - 1);
         const int n = min(wc + 16 * j + 4 * (lane >> 4), N - 4);
-        bj[j] = g.bias ? *(const f32x4*)(g.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+        if (g.accumulate) cv[i][j] = *(const f32x4*)(g.C + m * g.ldc + n);
+        if (g.mask) {
+          if constexpr (MBF) {
+            const uint2 q = mk16[i][j];  // loaded at the last chunk (early_mask holds here)
+            mk[i][j] = f32x4{bf2f(q.x & 0xffffu), bf2f(q.x >> 16), bf2f(q.y & 0xffffu), bf2f(q.y >> 16)};
+          } else {
+            mk[i][j] = *(const f32x4*)(g.mask + m * g.ldm + n);
+          }
+        }
       }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        f32x4 v = acc[i][j];
+        if (g.bias) v += bj[j];
+        if (g.accumulate) v += cv[i][j];
+        if (g.relu) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+        }
+        if (g.mask) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = mk[i][j][e] > 0.f ? v[e] : 0.f;
+        }
+        acc[i][j] = v;
+      }
+    auto pack4 = [](const f32x4& v) {
+      return make_uint2((uint32_t)f2bf_rne(v[0]) | ((uint32_t)f2bf_rne(v[1]) << 16),
+                        (uint32_t)f2bf_rne(v[2]) | ((uint32_t)f2bf_rne(v[3]) << 16));
+    };
+    if (g.cbf && g.vec16) {
+      // bf16 rows as 16-B stores: lanes l and l ^ 16 hold columns 4q..4q+3 and 4q+4..4q+7 of one row
+      // in each 16-column block, so a pair of blocks (j0, j1) swaps one quad per lane and each lane
+      // stores 8 consecutive columns of one block: 8 stores per lane instead of 16 (the store issue
+      // was the epilogue's cost: tools/gemm_probe phase clocks, 3.7 of an 11 us workgroup)
+      const bool odd = (lane >> 4) & 1;
+      const int m = m0 + wr + (lane & 15);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const long m = min(m0 + wr + 16 * i + (lane & 15), M - 1);
-          const int n = min(wc + 16 * j + 4 * (lane >> 4), N - 4);
-          if (g.accumulate) cv[i][j] = *(const f32x4*)(g.C + m * g.ldc + n);
-          if (g.mask) {
-            if constexpr (MBF) {
-              const uint2 q = *(const uint2*)(mask16 + m * g.ldm + n);
-              mk[i][j] = f32x4{bf2f(q.x & 0xffffu), bf2f(q.x >> 16), bf2f(q.y & 0xffffu), bf2f(q.y >> 16)};
-            } else {
-              mk[i][j] = *(const f32x4*)(g.mask + m * g.ldm + n);
+        for (int pj = 0; pj < 2; ++pj) {
+          const uint2 a = pack4(acc[i][2 * pj]), b = pack4(acc[i][2 * pj + 1]);
+          const uint2 snd = odd ? a : b;
+          const uint2 rcv = make_uint2((uint32_t)__shfl_xor((int)snd.x, 16), (uint32_t)__shfl_xor((int)snd.y, 16));
+          const uint4 o = odd ? make_uint4(rcv.x, rcv.y, b.x, b.y) : make_uint4(a.x, a.y, rcv.x, rcv.y);
+          const int n = wc + 16 * (2 * pj + (odd ? 1 : 0)) + 8 * ((lane >> 5) & 1);
+          const int mm = m + 16 * i;
+          if (mm < M) {
+            unsigned short* dst = C16 + (long)mm * g.ldc + n;
+            if (n + 8 <= N) {
+              *(uint4*)dst = o;
+            } else if (n < N) {  // N % 4 == 0: the first quad only
+              *(uint2*)dst = make_uint2(o.x, o.y);
             }
           }
         }
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          f32x4 v = acc[i][j];
-          if (g.bias) v += bj[j];
-          if (g.accumulate) v += cv[i][j];
-          if (g.relu) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
-          }
-          if (g.mask) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = mk[i][j][e] > 0.f ? v[e] : 0.f;
-          }
-          acc[i][j] = v;
-        }
-    }
-    if (stage) {
-      // the finished tile goes through the (now idle) ring as [rows][N] with a 16-B row pad, then
-      // leaves as whole 16-B row chunks: each store instruction covers 1 KiB of consecutive rows
-      // instead of 16 rows x 4 scattered 8-B pieces (store issue was the epilogue's cost)
-      const int ob = g.cbf ? 2 : 4;
-      const int rowb = N * ob + 16, cpr = N * ob / 16;
-      const int rpp = RG_NS * RG_SLOT >= RG_BM * rowb ? RG_BM : 64;  // rows per pass (one row group)
-      for (int p0 = 0; p0 < RG_BM; p0 += rpp) {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        if (active && wr >= p0 && wr < p0 + rpp) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              const int r = wr - p0 + 16 * i + (lane & 15);
-              const int n = wc + 16 * j + 4 * (lane >> 4);
-              const f32x4 v = acc[i][j];
-              if (n < N) {
-                if (g.cbf)
-                  *(uint2*)(lds + r * rowb + n * 2) =
-                      make_uint2((uint32_t)f2bf_rne(v[0]) | ((uint32_t)f2bf_rne(v[1]) << 16),
-                                 (uint32_t)f2bf_rne(v[2]) | ((uint32_t)f2bf_rne(v[3]) << 16));
-                else
-                  *(f32x4*)(lds + r * rowb + n * 4) = v;
-              }
-            }
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        const int rows = min(rpp, M - m0 - p0);
-        for (int q = tid; q < rows * cpr; q += RG_BM / 16 * 64) {
-          const int r = q / cpr, c = q - r * cpr;
-          const uint4 x = *(const uint4*)(lds + r * rowb + c * 16);
-          *(uint4*)((char*)g.C + (long)(m0 + p0 + r) * g.ldc * ob + c * 16) = x;
-        }
-      }
+      RG_T(13);
       return;
     }
 #pragma unroll
@@ -463,13 +495,12 @@ __global__ __launch_bounds__(BM_ / 16 * 64) void k_rgemm(RGemm g) {
         const f32x4 v = acc[i][j];
         if (m < M && n < N) {
           if (g.cbf)
-            *(uint2*)(C16 + (long)m * g.ldc + n) =
-                make_uint2((uint32_t)f2bf_rne(v[0]) | ((uint32_t)f2bf_rne(v[1]) << 16),
-                           (uint32_t)f2bf_rne(v[2]) | ((uint32_t)f2bf_rne(v[3]) << 16));
+            *(uint2*)(C16 + (long)m * g.ldc + n) = pack4(v);
           else
             *(f32x4*)(g.C + (long)m * g.ldc + n) = v;
         }
       }
+    RG_T(13);
     return;
   }
 #pragma unroll
@@ -495,86 +526,25 @@ __global__ __launch_bounds__(BM_ / 16 * 64) void k_rgemm(RGemm g) {
       }
 }
 
-template <bool X3, bool ABF, int BM_ = 128, int NS_ = 2>
-size_t rgemm_lds_bytes() { return (size_t)RgCfg<X3, ABF, BM_, NS_>::NS * RgCfg<X3, ABF, BM_, NS_>::SLOT; }
+template <bool X3, bool ABF, bool SM = false>
+size_t rgemm_lds_bytes() { return (size_t)RgCfg<X3, ABF, SM>::NS * RgCfg<X3, ABF, SM>::SLOT; }
 
-// row-GEMM geometry variants (bm rows per workgroup, ns ring slots), for measurement (tools/gemm_probe)
-template <int BM_, int NS_>
-static void launch_rgemm_geom(const RGemm& g, int M_host, hipStream_t s) {
-  const dim3 grid((M_host + BM_ - 1) / BM_), block(BM_ / 16 * 64);
-  const bool mbf = g.mbf && g.mask;
-  static bool attr[5] = {};  // per instantiation: the LDS size attribute set once per kernel
-  auto go = [&](int i, auto kern, size_t lds) {
-    if (!attr[i]) {
-      (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      attr[i] = true;
-    }
-    hipLaunchKernelGGL(kern, grid, block, lds, s, g);
-  };
-  if (g.x3) go(0, k_rgemm<true, false, false, BM_, NS_>, rgemm_lds_bytes<true, false, BM_, NS_>());
-  else if (g.abf && mbf) go(1, k_rgemm<false, true, true, BM_, NS_>, rgemm_lds_bytes<false, true, BM_, NS_>());
-  else if (g.abf) go(2, k_rgemm<false, true, false, BM_, NS_>, rgemm_lds_bytes<false, true, BM_, NS_>());
-  else if (mbf) go(3, k_rgemm<false, false, true, BM_, NS_>, rgemm_lds_bytes<false, false, BM_, NS_>());
-  else go(4, k_rgemm<false, false, false, BM_, NS_>, rgemm_lds_bytes<false, false, BM_, NS_>());
-}
-
-static int rg_stage_env() {
-  static int v = -2;
-  if (v == -2) {
-    const char* e = getenv("ANR_RG_STAGE");
-    v = e ? atoi(e) : 0;
+// ANR_RG_SMALL=1: the bf16-product row GEMMs in the SM geometry (measurement switch)
+static bool rg_small() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("ANR_RG_SMALL");
+    v = e && e[0] == '1' ? 1 : 0;
   }
-  return v;
-}
-
-// vec_out, and whether the epilogue stages the tile through LDS (g.stage: < 0 never, 0 the default
-// (ANR_RG_STAGE), > 0 whenever the output rows allow 16-B row chunks); ring_bytes: the variant's LDS
-static void rgemm_vec_out(RGemm& g, size_t ring_bytes = 0) {
-  const size_t ce = g.cbf ? 2 : 4, me = g.mbf ? 2 : 4;  // C / mask element bytes
-  g.vec_out = (g.N % 4 == 0) && (g.ldc % 4 == 0) && ((uintptr_t)g.C % (4 * ce) == 0) &&
-              (!g.mask || ((g.ldm % 4 == 0) && ((uintptr_t)g.mask % (4 * me) == 0))) && ((uintptr_t)g.bias % 16 == 0);
-  const int want = g.stage ? g.stage : rg_stage_env();
-  g.stage = want > 0 && g.vec_out && (g.N * ce) % 16 == 0 && ((size_t)g.ldc * ce) % 16 == 0 &&
-            (uintptr_t)g.C % 16 == 0 && ring_bytes >= (size_t)64 * (g.N * ce + 16);
-}
-
-int launch_rgemm_variant(const RGemm& g0, int M_host, hipStream_t s, int bm, int ns) {
-  RGemm g = g0;
-  const size_t ring = g.x3 ? (bm == 128 ? 48 * 1024 : 32 * 1024) * ns
-                           : (size_t)ns * (bm * 64 * (g.abf ? 2 : 4) + 256 * 64 * 2);
-  rgemm_vec_out(g, ring);
-  if (bm == 128 && ns == 2) launch_rgemm_geom<128, 2>(g, M_host, s);
-  else if (bm == 128 && ns == 3) launch_rgemm_geom<128, 3>(g, M_host, s);
-  else if (bm == 64 && ns == 2) launch_rgemm_geom<64, 2>(g, M_host, s);
-  else if (bm == 64 && ns == 3) launch_rgemm_geom<64, 3>(g, M_host, s);
-  else if (bm == 64 && ns == 4) launch_rgemm_geom<64, 4>(g, M_host, s);
-  else return -1;
-  return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-
-// experiment knobs (read once): ANR_RG_GEOM=BMxNS picks a row-GEMM geometry variant for every launch,
-// ANR_WG_DEEP=D the weight-gradient prefetch depth (2 or 4)
-static int env_int_pair(const char* name, int* a, int* b) {
-  const char* v = getenv(name);
-  return v ? sscanf(v, "%dx%d", a, b) : 0;
-}
-
-static int rg_geom(int* bm, int* ns) {
-  static int cached = -1, cbm = 128, cns = 2;
-  if (cached < 0) cached = env_int_pair("ANR_RG_GEOM", &cbm, &cns) == 2 ? 1 : 0;
-  *bm = cbm;
-  *ns = cns;
-  return cached;
+  return v == 1;
 }
 
 void launch_rgemm(const RGemm& g0, int M_host, hipStream_t s) {
-  {
-    int bm, ns;
-    if (rg_geom(&bm, &ns) && launch_rgemm_variant(g0, M_host, s, bm, ns) == 0) return;
-  }
   RGemm g = g0;
-  rgemm_vec_out(g, g.x3 ? rgemm_lds_bytes<true, false>() : g.abf ? rgemm_lds_bytes<false, true>()
-                                                                 : rgemm_lds_bytes<false, false>());
+  const size_t ce = g.cbf ? 2 : 4, me = g.mbf ? 2 : 4;  // C / mask element bytes
+  g.vec_out = (g.N % 4 == 0) && (g.ldc % 4 == 0) && ((uintptr_t)g.C % (4 * ce) == 0) &&
+              (!g.mask || ((g.ldm % 4 == 0) && ((uintptr_t)g.mask % (4 * me) == 0))) && ((uintptr_t)g.bias % 16 == 0);
+  g.vec16 = g.vec_out && g.cbf && g.ldc % 8 == 0 && (uintptr_t)g.C % 16 == 0;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)k_rgemm<false, false, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -592,6 +562,29 @@ void launch_rgemm(const RGemm& g0, int M_host, hipStream_t s) {
   constexpr int BM = RgCfg<false>::BM;
   const dim3 grid((M_host + BM - 1) / BM), block(RgCfg<false>::WAVES * 64);
   const bool mbf = g.mbf && g.mask;
+  if (!g.x3 && (rg_small() || g.small)) {
+    static bool attr_sm = false;
+    if (!attr_sm) {
+      (void)hipFuncSetAttribute((const void*)k_rgemm<false, false, false, true>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)rgemm_lds_bytes<false, false, true>());
+      (void)hipFuncSetAttribute((const void*)k_rgemm<false, false, true, true>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)rgemm_lds_bytes<false, false, true>());
+      (void)hipFuncSetAttribute((const void*)k_rgemm<false, true, false, true>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)rgemm_lds_bytes<false, true, true>());
+      (void)hipFuncSetAttribute((const void*)k_rgemm<false, true, true, true>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)rgemm_lds_bytes<false, true, true>());
+      attr_sm = true;
+    }
+    if (g.abf && mbf)
+      hipLaunchKernelGGL((k_rgemm<false, true, true, true>), grid, block, (rgemm_lds_bytes<false, true, true>()), s, g);
+    else if (g.abf)
+      hipLaunchKernelGGL((k_rgemm<false, true, false, true>), grid, block, (rgemm_lds_bytes<false, true, true>()), s, g);
+    else if (mbf)
+      hipLaunchKernelGGL((k_rgemm<false, false, true, true>), grid, block, (rgemm_lds_bytes<false, false, true>()), s, g);
+    else
+      hipLaunchKernelGGL((k_rgemm<false, false, false, true>), grid, block, (rgemm_lds_bytes<false, false, true>()), s, g);
+    return;
+  }
   if (g.x3)
     hipLaunchKernelGGL((k_rgemm<true, false, false>), grid, block, (rgemm_lds_bytes<true, false>()), s, g);
   else if (g.abf && mbf)
@@ -638,29 +631,6 @@ __device__ __forceinline__ bf16x8_t wg_frag(const unsigned short* S, int cb, int
   return f;
 }
 
-// thread's share of one 32 x 128 operand step: 4 float4 (sample 8h + (tid >> 5), columns 4 (tid & 31));
-// bf: the rows hold bf16 (8-B loads, widened exactly; wg_store's rounding then returns the same bits)
-template <bool BF>
-__device__ __forceinline__ void wg_load(const float* P, long ld, int ncol, int c0, int s, int s1, int tid, f32x4 (&v)[4]) {
-#pragma unroll
-  for (int h = 0; h < 4; ++h) {
-    const int ss = s + 8 * h + (tid >> 5);
-    const int c = c0 + 4 * (tid & 31);
-    const bool ok = ss < s1 && c < ncol;
-    f32x4 x;
-    if constexpr (BF) {
-      const uint2 q = *(const uint2*)((const unsigned short*)P + (long)(ok ? ss : s) * ld + (ok ? c : 0));
-      x = f32x4{__uint_as_float(q.x << 16), __uint_as_float(q.x & 0xffff0000u), __uint_as_float(q.y << 16),
-                __uint_as_float(q.y & 0xffff0000u)};
-    } else {
-      x = *(const f32x4*)(P + (long)(ok ? ss : s) * ld + (ok ? c : 0));
-    }
-    // columns past ncol (inside the 16-B group) and samples past the range read as zero
-#pragma unroll
-    for (int e = 0; e < 4; ++e) v[h][e] = (ok && c + e < ncol) ? x[e] : 0.0f;
-  }
-}
-
 // X3: also the lo image (x - hi) into SL
 template <bool X3>
 __device__ __forceinline__ void wg_store(unsigned short* S, unsigned short* SL, int tid, const f32x4 (&v)[4]) {
@@ -679,109 +649,11 @@ __device__ __forceinline__ void wg_store(unsigned short* S, unsigned short* SL, 
   }
 }
 
+// The operand loads run WG_D steps ahead: each step's rows are held raw (bf16 pairs or fp32 quads,
+// exactly as loaded) in a register ring of WG_D steps and widened / split only at their LDS store
+// (tools/gemm_probe, 24,893 rows: 26.6 us per launch with its reduction against 28.4 us for loads one
+// step ahead; 35.7 against 37.8 us split-bf16).
 // YBF / XBF: dY / X rows hold bf16 (template parameters: the prefetch must stay branch-free)
-template <bool X3, bool YBF, bool XBF>
-__global__ __launch_bounds__(256) void k_wgrad(WGrad g) {
-  constexpr int NI = X3 ? 2 : 1;   // images per operand: hi (and lo)
-  constexpr int NH = X3 ? 1 : 2;   // 32-sample halves per step (bf16: 64 samples, two MFMA k-steps)
-  __shared__ __attribute__((aligned(16))) unsigned short sY[2][NI][NH * WG_S * WG_LD];
-  __shared__ __attribute__((aligned(16))) unsigned short sX[2][NI][NH * WG_S * WG_LD];
-  __shared__ float srs[8][WG_T];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  // XCD-aware order: workgroups are dealt to the 8 XCDs round-robin by linear id, so the tiles of
-  // one sample range (which read the same dY and X rows) are given ids on one XCD and share its L2
-  // (launch_wgrad makes the range count a multiple of 8)
-  const int tiles = gridDim.x * gridDim.y;
-  const int L = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
-  const int slot = L >> 3, tile = slot % tiles;
-  const int z = (slot / tiles) * 8 + (L & 7);
-  const int ti = tile % gridDim.x, tj = tile / gridDim.x;
-  const int n = g.M_dev ? *g.M_dev : g.n;
-  // samples per range: whole 64-sample steps (spb = 0: from the device count, as launch_wgrad would)
-  const int spb = g.spb ? g.spb : ((n + g.nz - 1) / g.nz + 2 * WG_S - 1) / (2 * WG_S) * (2 * WG_S);
-  const int s0 = z * spb, s1 = min(n, s0 + spb);
-  const int i0 = ti * WG_T, j0 = tj * WG_T;
-  const int wi = (w >> 1) * 64, wj = (w & 1) * 64;
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-  f32x4 rsum = {0.f, 0.f, 0.f, 0.f};  // column sums of this thread's dY share (tile row 0 only)
-  const bool do_rs = g.rs_slab != nullptr && tj == 0;
-  f32x4 vy[NH][4], vx[NH][4];
-  auto load = [&](int s) {
-#pragma unroll
-    for (int h = 0; h < NH; ++h) {
-      wg_load<YBF>(g.dY, g.ldY, g.nout, i0, s + h * WG_S, s1, tid, vy[h]);
-      wg_load<XBF>(g.X, g.ldX, g.K, j0, s + h * WG_S, s1, tid, vx[h]);
-    }
-  };
-  constexpr int STEP = NH * WG_S;
-  if (s0 < s1) load(s0);
-  int buf = 0;
-  for (int s = s0; s < s1; s += STEP) {
-#pragma unroll
-    for (int h = 0; h < NH; ++h) {
-      if (do_rs) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) rsum += vy[h][q];
-      }
-      wg_store<X3>(sY[buf][0] + h * WG_S * WG_LD, sY[buf][NI - 1] + h * WG_S * WG_LD, tid, vy[h]);
-      wg_store<X3>(sX[buf][0] + h * WG_S * WG_LD, sX[buf][NI - 1] + h * WG_S * WG_LD, tid, vx[h]);
-    }
-    __syncthreads();
-    if (s + STEP < s1) load(s + STEP);  // the next step's operands load while this step's MFMAs run
-#pragma unroll
-    for (int h = 0; h < NH; ++h) {
-      bf16x8_t fa[4], fb[4], la[4], lb[4];
-#pragma unroll
-      for (int a = 0; a < 4; ++a) {
-        fa[a] = wg_frag(sY[buf][0] + h * WG_S * WG_LD, wi + 16 * a, lane);
-        if constexpr (X3) la[a] = wg_frag(sY[buf][NI - 1] + h * WG_S * WG_LD, wi + 16 * a, lane);
-      }
-#pragma unroll
-      for (int b = 0; b < 4; ++b) {
-        fb[b] = wg_frag(sX[buf][0] + h * WG_S * WG_LD, wj + 16 * b, lane);
-        if constexpr (X3) lb[b] = wg_frag(sX[buf][NI - 1] + h * WG_S * WG_LD, wj + 16 * b, lane);
-      }
-#pragma unroll
-      for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int b = 0; b < 4; ++b) {
-          if constexpr (X3) {
-            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(la[a], fb[b], acc[a][b], 0, 0, 0);
-            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a], lb[b], acc[a][b], 0, 0, 0);
-          }
-          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a], fb[b], acc[a][b], 0, 0, 0);
-        }
-    }
-    buf ^= 1;
-  }
-  // partial tile, accumulator layout: slab[z][tile][w][a][b][lane][r]
-  float* slab = g.slab + ((long)(z * g.tiles + ti * g.tj + tj) * 4 + w) * 16 * 256;
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int b = 0; b < 4; ++b) *(f32x4*)(slab + (a * 4 + b) * 256 + lane * 4) = acc[a][b];
-  if (do_rs) {
-    // threads with equal tid & 31 hold the same 4 columns: combine their 8 partial sums
-    *(f32x4*)&srs[tid >> 5][4 * (tid & 31)] = rsum;
-    __syncthreads();
-    if (tid < WG_T) {
-      float t = 0.f;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) t += srs[k][tid];
-      g.rs_slab[(long)z * 256 + i0 + tid] = t;
-    }
-  }
-}
-
-// k_wgrad with the operand loads D steps ahead: each step's rows are held raw (bf16 pairs or fp32
-// quads, exactly as loaded) in a register ring of D steps and widened / split only at their LDS store,
-// so D x 32 KiB (bf16) of loads are in flight per workgroup instead of one step's; k_wgrad's single
-// register step left each step's HBM latency exposed behind ~0.2 us of MFMAs (tools/gemm_probe:
-// ~20 us per launch at any M below 12k rows). Same tiles, slabs and products as k_wgrad.
 template <bool BF>
 struct WgRaw {
   typedef f32x4 T;
@@ -824,8 +696,28 @@ __device__ __forceinline__ void wg_widen(const typename WgRaw<BF>::T (&r)[4], in
   }
 }
 
-template <bool X3, bool YBF, bool XBF, int D>
-__global__ __launch_bounds__(256) void k_wgrad_d(WGrad g) {
+#define WG_D 4
+// bf16 rows straight into the [sample][column] image: samples past the range and columns past ncol
+// read as zero (the f2bf round trip of the fp32 path would return the same bits)
+__device__ __forceinline__ void wg_put_bf(unsigned short* S, const uint2 (&r)[4], int ncol, int c0, int s, int s1,
+                                          int tid) {
+#pragma unroll
+  for (int h = 0; h < 4; ++h) {
+    const int ss = s + 8 * h + (tid >> 5);
+    const int c = c0 + 4 * (tid & 31);
+    uint2 v = (ss < s1 && c < ncol) ? r[h] : make_uint2(0u, 0u);
+    if (c + 4 > ncol) {  // a partial 4-column group (the last of a narrow operand)
+      const int k = ncol - c;  // valid columns in the group, < 4
+      v.x &= k >= 2 ? 0xffffffffu : k == 1 ? 0x0000ffffu : 0u;
+      v.y &= k >= 4 ? 0xffffffffu : k == 3 ? 0x0000ffffu : 0u;
+    }
+    *(uint2*)(S + (8 * h + (tid >> 5)) * WG_LD + 4 * (tid & 31)) = v;
+  }
+}
+
+template <bool X3, bool YBF, bool XBF>
+__global__ __launch_bounds__(256) void k_wgrad(WGrad g) {
+  constexpr int D = WG_D;
   constexpr int NI = X3 ? 2 : 1;
   constexpr int NH = X3 ? 1 : 2;
   __shared__ __attribute__((aligned(16))) unsigned short sY[2][NI][NH * WG_S * WG_LD];
@@ -872,15 +764,31 @@ __global__ __launch_bounds__(256) void k_wgrad_d(WGrad g) {
       if (s >= s1) break;
 #pragma unroll
       for (int h = 0; h < NH; ++h) {
-        f32x4 vy[4], vx[4];
-        wg_widen<YBF>(ry[d][h], g.nout, i0, s + h * WG_S, s1, tid, vy);
-        wg_widen<XBF>(rx[d][h], g.K, j0, s + h * WG_S, s1, tid, vx);
-        if (do_rs) {
+        // bf16 rows go to LDS as loaded (masked); fp32 rows are rounded (and split under X3)
+        if constexpr (YBF) {
+          wg_put_bf(sY[buf][0] + h * WG_S * WG_LD, ry[d][h], g.nout, i0, s + h * WG_S, s1, tid);
+          if (do_rs) {
+            f32x4 vy[4];
+            wg_widen<true>(ry[d][h], g.nout, i0, s + h * WG_S, s1, tid, vy);
 #pragma unroll
-          for (int q = 0; q < 4; ++q) rsum += vy[q];
+            for (int q = 0; q < 4; ++q) rsum += vy[q];
+          }
+        } else {
+          f32x4 vy[4];
+          wg_widen<false>(ry[d][h], g.nout, i0, s + h * WG_S, s1, tid, vy);
+          if (do_rs) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) rsum += vy[q];
+          }
+          wg_store<X3>(sY[buf][0] + h * WG_S * WG_LD, sY[buf][NI - 1] + h * WG_S * WG_LD, tid, vy);
         }
-        wg_store<X3>(sY[buf][0] + h * WG_S * WG_LD, sY[buf][NI - 1] + h * WG_S * WG_LD, tid, vy);
-        wg_store<X3>(sX[buf][0] + h * WG_S * WG_LD, sX[buf][NI - 1] + h * WG_S * WG_LD, tid, vx);
+        if constexpr (XBF) {
+          wg_put_bf(sX[buf][0] + h * WG_S * WG_LD, rx[d][h], g.K, j0, s + h * WG_S, s1, tid);
+        } else {
+          f32x4 vx[4];
+          wg_widen<false>(rx[d][h], g.K, j0, s + h * WG_S, s1, tid, vx);
+          wg_store<X3>(sX[buf][0] + h * WG_S * WG_LD, sX[buf][NI - 1] + h * WG_S * WG_LD, tid, vx);
+        }
       }
       __syncthreads();
       if (s + D * STEP < s1) load(d, s + D * STEP);  // this ring entry is free again: refill D steps ahead
@@ -971,12 +879,6 @@ size_t wgrad_slab_floats() { return (size_t)WG_MAX_Z * 4 * WG_TILE_FLOATS + (siz
 
 int launch_wgrad(WGrad g, int n_host, hipStream_t s) {
   if (n_host <= 0) return 0;
-  static int deep_env = -1;
-  if (deep_env < 0) {
-    const char* v = getenv("ANR_WG_DEEP");
-    deep_env = v ? atoi(v) : 0;
-  }
-  if (!g.deep) g.deep = deep_env;
   const int ti = (g.nout + WG_T - 1) / WG_T, tj = (g.K + WG_T - 1) / WG_T;
   g.tj = tj;
   g.tiles = ti * tj;
@@ -990,19 +892,7 @@ int launch_wgrad(WGrad g, int n_host, hipStream_t s) {
   g.n = n_host;
   g.rs_slab = (g.bsum || g.bsum2) ? g.slab + (size_t)WG_MAX_Z * 4 * WG_TILE_FLOATS : nullptr;
   const dim3 grid(ti, tj, g.nz);
-  if (g.deep == 4) {
-    if (g.x3) hipLaunchKernelGGL((k_wgrad_d<true, false, false, 4>), grid, dim3(256), 0, s, g);
-    else if (g.ybf && g.xbf) hipLaunchKernelGGL((k_wgrad_d<false, true, true, 4>), grid, dim3(256), 0, s, g);
-    else if (g.ybf) hipLaunchKernelGGL((k_wgrad_d<false, true, false, 4>), grid, dim3(256), 0, s, g);
-    else if (g.xbf) hipLaunchKernelGGL((k_wgrad_d<false, false, true, 4>), grid, dim3(256), 0, s, g);
-    else hipLaunchKernelGGL((k_wgrad_d<false, false, false, 4>), grid, dim3(256), 0, s, g);
-  } else if (g.deep == 2) {
-    if (g.x3) hipLaunchKernelGGL((k_wgrad_d<true, false, false, 2>), grid, dim3(256), 0, s, g);
-    else if (g.ybf && g.xbf) hipLaunchKernelGGL((k_wgrad_d<false, true, true, 2>), grid, dim3(256), 0, s, g);
-    else if (g.ybf) hipLaunchKernelGGL((k_wgrad_d<false, true, false, 2>), grid, dim3(256), 0, s, g);
-    else if (g.xbf) hipLaunchKernelGGL((k_wgrad_d<false, false, true, 2>), grid, dim3(256), 0, s, g);
-    else hipLaunchKernelGGL((k_wgrad_d<false, false, false, 2>), grid, dim3(256), 0, s, g);
-  } else if (g.x3) hipLaunchKernelGGL((k_wgrad<true, false, false>), grid, dim3(256), 0, s, g);
+  if (g.x3) hipLaunchKernelGGL((k_wgrad<true, false, false>), grid, dim3(256), 0, s, g);
   else if (g.ybf && g.xbf) hipLaunchKernelGGL((k_wgrad<false, true, true>), grid, dim3(256), 0, s, g);
   else if (g.ybf) hipLaunchKernelGGL((k_wgrad<false, true, false>), grid, dim3(256), 0, s, g);
   else if (g.xbf) hipLaunchKernelGGL((k_wgrad<false, false, true>), grid, dim3(256), 0, s, g);

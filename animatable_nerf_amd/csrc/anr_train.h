@@ -91,18 +91,15 @@ struct RGemm {
   long ldm;
   int accumulate;
   int vec_out;  // set by launch_rgemm: C (and mask) rows 16-B addressable, N % 4 == 0
+  int vec16;    // set by launch_rgemm: bf16 C rows take 16-B stores (ldc % 8 == 0, C 16-B aligned)
+  int small;    // bf16 products in the 72 KiB geometry (RgCfg SM; also ANR_RG_SMALL=1)
   int x3;       // split-bf16 products (fp32-level): activations hi/lo, weights hi/lo images
   // bf16 storage (training precision 'bf16': every consumer rounds these to bf16 anyway): A rows,
   // C rows (RNE from the fp32 result) and the mask rows hold bf16 (C / mask reinterpreted as
   // unsigned short*). Not with x3; C bf16 excludes accumulate.
   int abf, cbf, mbf;
-  // epilogue through LDS (16-B row-chunk stores): < 0 never, 0 default (ANR_RG_STAGE), > 0 when the
-  // output rows allow it; launch_rgemm resolves it to 0 / 1
-  int stage;
 };
 void launch_rgemm(const RGemm& g, int M_host, hipStream_t s);
-// geometry variants for measurement: bm in {64, 128} rows per workgroup, ns ring slots (128: 2-3; 64: 3-4)
-int launch_rgemm_variant(const RGemm& g, int M_host, hipStream_t s, int bm, int ns);
 // bf16 weight images of the training GEMM weights: forward (rows = outputs, k = used input columns,
 // segments padded to 64) and backward (rows = input columns, k = outputs padded to 64). t: the
 // ANR_NUM_TENSORS network tensors followed by the ANR_NUM_NOVEL_TENSORS novel_pose_bw tensors
@@ -140,37 +137,9 @@ struct WGrad {
   int spb, nz, tiles, tj;
   int x3;  // split-bf16 products (fp32-level)
   int ybf, xbf;  // dY / X rows hold bf16 (reinterpreted as unsigned short*), not with x3
-  int deep;      // operand loads this many 64-sample steps ahead (k_wgrad_d: 2 or 4; 0: k_wgrad, one step)
 };
 size_t wgrad_slab_floats();
 int launch_wgrad(WGrad g, int n_host, hipStream_t s);
-
-// a chain of layers run as one launch per 128-row tile (anr_tchain.hip; forward, precision bf16 with
-// bf16 storage): segment s of layer l multiplies A = the LDS activation tile (src 0, the previous
-// layer's output) or a gamma tile (src 1 = G0, 2 = G1; <= 64 bf16 columns loaded once) by a forward
-// weight image view (wimg_view); epilogue bias, ReLU; the output (N <= 256 columns) is stored to
-// `out` (bf16 or fp32, row stride ldo; NULL: not stored) and, with to_lds, becomes the next layer's A
-struct ChainLayer {
-  const unsigned short* B[2];
-  long ldb[2];
-  int bcol[2], brows[2], K[2], src[2];
-  int nseg, N, relu, to_lds, out_bf16;
-  const float* bias;
-  void* out;
-  long ldo;
-};
-#define ANR_CHAIN_MAX 14
-struct ChainArgs {
-  ChainLayer L[ANR_CHAIN_MAX];
-  int nl;
-  int M;
-  const int* M_dev;
-  const unsigned short* G0;
-  long ldg0;
-  const unsigned short* G1;
-  long ldg1;
-};
-int launch_chain(const ChainArgs& a, int M_host, hipStream_t s);
 
 // split-bf16 layer GEMM with LDS-resident weight images for large M (anr_lgemm.hip; the sdf_pdf
 // batches): lgemm_supported(g) (g.x3, no accumulate / mask / atomics, 16-B addressable operands),

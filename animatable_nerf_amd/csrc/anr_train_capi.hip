@@ -6,7 +6,6 @@
 // count stays on the device (M_dev / K_dev in the GEMM arguments, capacity-sized grids), so no call
 // syncs with the host (the reference syncs ~6x per chunk).
 #include <algorithm>
-#include <cstring>
 #include <cmath>
 #include <cstdlib>
 #include <mutex>
@@ -92,23 +91,15 @@ int check_args(const anr_params* p, const anr_frame* f, const float* ray_o, cons
 // are per device, created once, ordered with the caller's stream by events (fork / join), so every
 // entry point still behaves as one asynchronous call on the caller's stream.
 // ANR_TRAIN_SERIAL=1 runs everything on the caller's stream (debugging aid).
-// Stream priorities (experiment switches, read once when the streams are created):
-// ANR_MAIN_PRIO=high issues a step's critical chain on the library's own highest-priority stream
-// `hp` (ordered after the caller's stream and joined back into it) with s2 at the same priority;
-// ANR_SIDE_PRIO=low creates the weight-gradient lanes at the lowest priority, so that the workgroup
-// dispatcher prefers the chain's workgroups whenever both are waiting for CUs.
+// Stream priorities were measured (profiles/r4c): the critical chain on a highest-priority stream of
+// the library's own made the bf16 step 3.27 ms instead of 1.96 (one more queue than the hardware
+// queues the process gets), the weight-gradient lanes at the lowest priority changed nothing (1.945).
 struct SideStreams {
   hipStream_t s2 = nullptr, sw[kWStreams] = {};
-  hipStream_t hp = nullptr;   // ANR_MAIN_PRIO=high: the high-priority chain stream (else NULL)
   hipStream_t cap = nullptr;  // origin stream of step-graph captures (created on first use)
   hipEvent_t ev[64] = {};
   unsigned next = 0;
 };
-
-static bool env_is(const char* name, const char* value) {
-  const char* v = getenv(name);
-  return v && strcmp(v, value) == 0;
-}
 
 SideStreams* side_streams() {
   static SideStreams per_dev[16];
@@ -121,13 +112,9 @@ SideStreams* side_streams() {
   SideStreams& ss = per_dev[d];
   if (!ss.s2) {
     SideStreams t{};
-    int least = 0, greatest = 0;
-    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) least = greatest = 0;
-    const bool main_high = env_is("ANR_MAIN_PRIO", "high"), side_low = env_is("ANR_SIDE_PRIO", "low");
-    if (hipStreamCreateWithPriority(&t.s2, hipStreamNonBlocking, main_high ? greatest : 0) != hipSuccess) return nullptr;
-    if (main_high && hipStreamCreateWithPriority(&t.hp, hipStreamNonBlocking, greatest) != hipSuccess) return nullptr;
+    if (hipStreamCreateWithFlags(&t.s2, hipStreamNonBlocking) != hipSuccess) return nullptr;
     for (auto& w : t.sw)
-      if (hipStreamCreateWithPriority(&w, hipStreamNonBlocking, side_low ? least : 0) != hipSuccess) return nullptr;
+      if (hipStreamCreateWithFlags(&w, hipStreamNonBlocking) != hipSuccess) return nullptr;
     for (auto& e : t.ev)
       if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
     ss = t;
@@ -486,88 +473,6 @@ int bw_backward(Exec& e, const float* const* W, float* const* g, const float* G,
   return ANR_OK;
 }
 
-// ---- forward layer chains (precision bf16 with bf16 storage: anr_tchain.hip) ---------------------
-// Opt-in (ANR_TRAIN_CHAIN=1): measured slower than one launch per layer on MI355X (a chain 241 us
-// for 9-13 layers of 128-row tiles vs ~255 us for both MLPs' per-layer launches running side by side,
-// profiles/r3c1): one workgroup per CU (the 160 KiB of LDS) leaves each 32 KiB weight chunk's
-// LDS-DMA latency and each layer's epilogue exposed, which the per-layer launches hide across
-// workgroups and streams. Parity-tested (tests/test_gpu_train.py test_forward_chain_matches_layers).
-bool use_chains() {
-  const char* v = getenv("ANR_TRAIN_CHAIN");
-  return v && v[0] == '1';
-}
-
-// segment s of chain layer L: A from src (0 = the activation tile, 1 = G0, 2 = G1), B = the forward
-// weight image view of W's columns c0 .. c0 + K
-bool chain_seg(const Exec& e, ChainLayer& L, int s, const float* W, int c0, int K, int src) {
-  WView v;
-  if (!wimg_view(e.wimg, e.pt, W, c0, K, false, &v)) return false;
-  L.B[s] = v.B; L.ldb[s] = v.ldb; L.bcol[s] = v.bcol; L.brows[s] = v.rows; L.K[s] = K; L.src[s] = src;
-  L.nseg = s + 1;
-  return true;
-}
-
-void chain_out(ChainLayer& L, int N, const float* bias, bool relu, void* out, long ldo, bool bf, bool to_lds) {
-  L.N = N; L.bias = bias; L.relu = relu ? 1 : 0; L.out = out; L.ldo = ldo; L.out_bf16 = bf ? 1 : 0;
-  L.to_lds = to_lds ? 1 : 0;
-}
-
-int run_chain(Exec& e, ChainArgs& a, int nl, const float* G0, const float* G1) {
-  a.nl = nl;
-  a.M = e.n;
-  a.M_dev = e.n_dev;
-  a.G0 = (const unsigned short*)G0; a.ldg0 = 64;
-  a.G1 = (const unsigned short*)G1; a.ldg1 = 64;
-  if (launch_chain(a, e.grid_n(), e.s) != 0) return check_launch("k_chain");
-  return ANR_OK;
-}
-
-// the T-pose BW MLP (tpose_nerf_network.py:55-77 on x_T) as one chain: gamma(x_T) -> 8 x 256 (skip at
-// 5) -> 24 logits; every hidden activation stored (bf16) for the backward
-int bw_forward_chain(Exec& e, const float* const* W, const float* G, float* H, float* logits, long N, const float* fold0,
-                     const float* fold5) {
-  ChainArgs a{};
-  const long S = N * 256;
-  for (int l = 0; l < 8; ++l) {
-    ChainLayer& L = a.L[l];
-    const bool ok = l == 0   ? chain_seg(e, L, 0, W[1], 0, 63, 1)
-                    : l == 5 ? chain_seg(e, L, 0, W[11], 0, 63, 1) && chain_seg(e, L, 1, W[11], 191, 256, 0)
-                             : chain_seg(e, L, 0, W[1 + 2 * l], 0, 256, 0);
-    if (!ok) return fail(ANR_E_ARG, "train: chain weight view");
-    chain_out(L, 256, l == 0 ? fold0 : l == 5 ? fold5 : W[2 + 2 * l], true, H + l * S, 256, true, true);
-  }
-  if (!chain_seg(e, a.L[8], 0, W[17], 0, 256, 0)) return fail(ANR_E_ARG, "train: chain weight view");
-  chain_out(a.L[8], 24, W[18], false, logits, 32, false, false);
-  return run_chain(e, a, 9, G, nullptr);
-}
-
-// the canonical NeRF (TPoseHuman.calculate_alpha_rgb, tpose_nerf_network.py:252-275) as one chain:
-// trunk, alpha_fc (fp32 out, the tile keeps H7), feature_fc, latent_fc (latent folded), view_fc
-// ([latent, gamma(dir)], fp32 out), rgb_fc
-int nerf_forward_chain(Exec& e, const anr_params* p, const float* Gt, const float* Gv, float* Hn, float* alpha,
-                       float* feat, float* lat, float* view, float* rgbl, long N, const float* fold_lat) {
-  ChainArgs a{};
-  const long S = N * 256;
-  for (int l = 0; l < 8; ++l) {
-    ChainLayer& L = a.L[l];
-    const bool ok = l == 0   ? chain_seg(e, L, 0, PT(1), 0, 63, 1)
-                    : l == 5 ? chain_seg(e, L, 0, PT(11), 0, 63, 1) && chain_seg(e, L, 1, PT(11), 63, 256, 0)
-                             : chain_seg(e, L, 0, PT(1 + 2 * l), 0, 256, 0);
-    if (!ok) return fail(ANR_E_ARG, "train: chain weight view");
-    chain_out(L, 256, PT(2 + 2 * l), true, Hn + l * S, 256, true, true);
-  }
-  bool ok = chain_seg(e, a.L[8], 0, PT(17), 0, 256, 0) && chain_seg(e, a.L[9], 0, PT(19), 0, 256, 0) &&
-            chain_seg(e, a.L[10], 0, PT(21), 0, 256, 0) && chain_seg(e, a.L[11], 0, PT(23), 0, 256, 0) &&
-            chain_seg(e, a.L[11], 1, PT(23), 256, 27, 2) && chain_seg(e, a.L[12], 0, PT(25), 0, 128, 0);
-  if (!ok) return fail(ANR_E_ARG, "train: chain weight view");
-  chain_out(a.L[8], 1, PT(18), false, alpha, 1, false, false);
-  chain_out(a.L[9], 256, PT(20), false, feat, 256, true, true);
-  chain_out(a.L[10], 256, fold_lat, false, lat, 256, true, true);
-  chain_out(a.L[11], 128, PT(24), true, view, 128, false, true);
-  chain_out(a.L[12], 3, PT(26), false, rgbl, 4, false, false);
-  return run_chain(e, a, 13, Gt, Gv);
-}
-
 // x != NULL: free samples (Network.forward, anr_network_train_fwd): R groups of 64, no compositing
 int train_forward(const anr_params* p, const anr_frame* f, const float* ray_o, const float* ray_d, const float* near_,
                   const float* far_, int R, const anr_render_opts* o, const anr_render_out* out, char* ws,
@@ -600,8 +505,7 @@ int train_forward(const anr_params* p, const anr_frame* f, const float* ray_o, c
   ANR_TRY(order(e.ss, s2, s));
   {
     OnStream on(e, s2);
-    if (e.hb && use_chains()) ANR_TRY(bw_forward_chain(e, p->t + 27, b.Gt, (float*)(ws + T.Ht), b.Lt, N, FOLD(1), FOLD(3)));
-    else ANR_TRY(bw_forward(e, p->t + 27, b.Gt, (float*)(ws + T.Ht), b.Lt, N, FOLD(1), FOLD(3)));
+    ANR_TRY(bw_forward(e, p->t + 27, b.Gt, (float*)(ws + T.Ht), b.Lt, N, FOLD(1), FOLD(3)));
     if (n > 0) {
       hipLaunchKernelGGL(k_tr_softmax_t, dim3(g1), dim3(256), 0, s2, b);
       ANR_TRY(check_launch("k_tr_softmax_t"));
@@ -613,9 +517,7 @@ int train_forward(const anr_params* p, const anr_frame* f, const float* ray_o, c
   float* Feat = (float*)(ws + T.Feat);
   float* Lat = (float*)(ws + T.Lat);
   float* View = (float*)(ws + T.View);
-  if (e.hb && use_chains()) {
-    ANR_TRY(nerf_forward_chain(e, p, b.Gt, b.Gv, Hn, b.Alpha, Feat, Lat, View, b.Rgbl, N, FOLD(4)));
-  } else {
+  {
     const unsigned h = e.hb ? (BF_A | BF_C) : 0, a = e.hb ? BF_A : 0;  // gamma, H, Feat, Lat bf16 under e.hb
     ANR_TRY(e.fwd(Hn, 256, 256, PT(1), 63, PT(2), true, b.Gt, 64, 63, 0, nullptr, 0, 0, 0, h));
     for (int l = 1; l < 8; ++l) {
@@ -1063,15 +965,9 @@ int anr_train_step_hooked(const anr_params* p, float* const* grads, const anr_fr
   // an external event (bucketed all-reduce) must be signalled by a plain record, and a ray split calls
   // its host hook mid-step: eager only
   const bool graphs = ss && !nerf_done && !splitting && gv && gv[0] == '1';
-  if (!graphs) {
-    if (!ss || !ss->hp)
-      return train_step_body(p, grads, f, ray_o, ray_d, near_, far_, n_rays, o, rgb_gt, mask_at_box, out, loss3,
-                             nerf_done, ws, T, s, ss, splitting ? &split : nullptr);
-    ANR_TRY(order(ss, ss->hp, s));
-    ANR_TRY(train_step_body(p, grads, f, ray_o, ray_d, near_, far_, n_rays, o, rgb_gt, mask_at_box, out, loss3,
-                            nerf_done, ws, T, ss->hp, ss, splitting ? &split : nullptr));
-    return order(ss, s, ss->hp);
-  }
+  if (!graphs)
+    return train_step_body(p, grads, f, ray_o, ray_d, near_, far_, n_rays, o, rgb_gt, mask_at_box, out, loss3,
+                           nerf_done, ws, T, s, ss, splitting ? &split : nullptr);
   std::string key;
   int dev = 0;
   (void)hipGetDevice(&dev);

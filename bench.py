@@ -434,14 +434,15 @@ def bench_train(args, rank, world, dev):
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    kept = 0
+    host = 0.0  # host time inside step() (issue only: nothing in a step waits on the device)
     for j in range(args.steps):
+        th = time.perf_counter()
         step.step(batches[(args.warmup + j) % nb])
+        host += time.perf_counter() - th
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    kept = step.renderer.last_counts[0] if step.renderer.last_counts else 0
     dt_max = max_over_ranks(dt, dev, world)
     R = int(batches[0]['ray_o'].shape[1])
     loss = step.loss3.cpu().tolist()
@@ -464,6 +465,7 @@ def bench_train(args, rank, world, dev):
                      'unit': 'TFLOP/s', 'frac': achieved / peak, 'traffic': None,
                      'flop_per_kept': FLOP_PER_KEPT_TRAIN},
         'loss_last_step': loss[:3],
+        'host_issue_ms_per_step': host / args.steps * 1e3,
     }
     if rank == 0:
         print(json.dumps(result), flush=True)

@@ -197,28 +197,6 @@ def test_step_graph_replay_matches_eager(dev, monkeypatch):
             assert (a - b).abs().max().item() <= 1e-4 * b.abs().max().item() + 1e-12, j
 
 
-def test_forward_chain_matches_layers(dev, monkeypatch):
-    """bf16 policy: the forward as two layer chains (anr_tchain.hip, ANR_TRAIN_CHAIN=1) computes what
-    the per-layer row GEMMs compute (same operand rounding and fp32 accumulation): losses within 1e-5
-    relative and every gradient within 1e-4 of its tensor's max (split-K atomics reassociate)."""
-    from animatable_nerf_amd.trainer import FusedStep
-    g, bt, t_rand = _g4_batch(dev)
-    out = {}
-    for mode in ('0', '1'):
-        monkeypatch.setenv('ANR_TRAIN_CHAIN', mode)
-        cfg = _cfg()
-        cfg.train_precision = 'bf16'
-        net = make_net(dev)
-        net.train()
-        step = FusedStep(net, cfg, lr=0.0)
-        l3 = step.step(bt, t_rand=t_rand.to(dev)).clone()
-        out[mode] = (l3, [gv.clone() for gv in step.grad_views])
-    (la, ga), (lb, gb) = out['0'], out['1']
-    assert torch.allclose(lb[:3], la[:3], rtol=1e-5, atol=0), (lb, la)
-    for a, b in zip(gb, ga):
-        assert (a - b).abs().max().item() <= 1e-4 * b.abs().max().item() + 1e-12
-
-
 def test_two_forwards_before_backward(dev):
     """Each autograd forward owns its activations: forward(A), forward(B), backward(A) gives A's
     gradients (the workspace of A must not be the one B overwrote)."""

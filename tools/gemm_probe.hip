@@ -17,6 +17,9 @@
 #include "../animatable_nerf_amd/csrc/anr_train.h"
 
 using namespace anr;
+namespace anr {
+void rg_timing_buffer(unsigned long long* p);  // the probe's RG_TIMING build of anr_tgemm.hip
+}
 
 #define CK(x)                                                                   \
   do {                                                                          \
@@ -32,6 +35,48 @@ __global__ void k_probe_empty() {}
 // bf16 rows copy: the activation traffic of one bf16 layer (M x 256 in, M x 256 out)
 __global__ void k_probe_copy(const uint4* __restrict__ src, uint4* __restrict__ dst, long n16) {
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (long)gridDim.x * blockDim.x) dst[i] = src[i];
+}
+
+// LDS-DMA stream rate: every workgroup (one per CU: a 128 KiB LDS ring) streams `bytes` from src (shared
+// != 0: the same addresses for every workgroup, as a weight image; else its own region) in 1 KiB
+// pieces, each wave issuing every W-th piece and keeping at most DEPTH of its pieces in flight
+template <int W, int DEPTH>
+__global__ __launch_bounds__(W * 64) void k_probe_dma(const unsigned char* src, long bytes, int shared) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const unsigned char* base = src + (shared ? 0 : (long)blockIdx.x * bytes);
+  const int pieces = (int)(bytes / 1024);
+  const unsigned lbase = (unsigned)(uintptr_t)lds;
+  for (int p = w; p < pieces; p += W) {
+    const unsigned dst = lbase + (unsigned)(p & 127) * 1024u;
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(base + (long)p * 1024 + lane * 16),
+                 "s"(dst)
+                 : "memory");
+    __builtin_amdgcn_s_waitcnt((DEPTH & 15) | (7 << 4) | (15 << 8) | ((DEPTH >> 4) << 14));
+  }
+  __builtin_amdgcn_s_waitcnt(0 | (7 << 4) | (15 << 8));
+}
+
+// the same stream into registers (global_load_dwordx4), DEPTH loads in flight per wave
+template <int W, int DEPTH>
+__global__ __launch_bounds__(W * 64) void k_probe_vload(const unsigned char* src, long bytes, int shared, uint4* sink) {
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const unsigned char* base = src + (shared ? 0 : (long)blockIdx.x * bytes);
+  const int pieces = (int)(bytes / 1024);
+  uint4 acc = {0, 0, 0, 0};
+  uint4 r[DEPTH];
+  int p = w;
+#pragma unroll
+  for (int d = 0; d < DEPTH; ++d) r[d] = p + d * W < pieces ? *(const uint4*)(base + (long)(p + d * W) * 1024 + lane * 16) : uint4{0, 0, 0, 0};
+  for (; p < pieces; p += DEPTH * W) {
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d) {
+      acc.x ^= r[d].x; acc.y ^= r[d].y; acc.z ^= r[d].z; acc.w ^= r[d].w;
+      const int q = p + (d + DEPTH) * W;
+      if (q < pieces) r[d] = *(const uint4*)(base + (long)q * 1024 + lane * 16);
+    }
+  }
+  if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x12345678u) sink[threadIdx.x] = acc;
 }
 
 __global__ void k_probe_fill(float* p, long n, unsigned seed, float scale) {
@@ -87,8 +132,9 @@ int main(int argc, char** argv) {
   int Mmax = 0;
   for (int m : Ms) Mmax = m > Mmax ? m : Mmax;
   const int K = 256, N = 256, reps = 50;
-  hipStream_t s;
+  hipStream_t s, s2;
   CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  CK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
   const long rowsz = (long)Mmax * 256;
   float *A, *C, *C2, *Mk, *W, *bias, *dW, *dW2, *bsum, *slab, *img_l = nullptr;
   unsigned short* Bimg;
@@ -134,41 +180,75 @@ int main(int argc, char** argv) {
       r.M = M;
       const double eb = (r.abf ? 2 : 4) + (r.cbf ? 2 : 4) + (r.mask ? (r.mbf ? 2 : 4) : 0);
       out(name, time_us(s, reps, [&] { launch_rgemm(r, M, s); }), (double)M * 256 * eb, fl);
-      {  // the LDS-staged epilogue: same bytes, timed
+      if (!r.x3) {
         RGemm a = r, b = r;
-        a.stage = -1;
-        b.stage = 1;
+        b.small = 1;
         b.C = C2;
         launch_rgemm(a, M, s);
         launch_rgemm(b, M, s);
         CK(hipStreamSynchronize(s));
         const size_t bytes = (size_t)M * 256 * (r.cbf ? 2 : 4);
-        if (!same_bytes(C, C2, bytes)) printf("{\"kernel\": \"%s_stage\", \"M\": %d, \"error\": \"MISMATCH\"}\n", name, M);
-        const std::string v = std::string(name) + "_stage";
+        if (!same_bytes(C, C2, bytes)) printf("{\"kernel\": \"%s_small\", \"M\": %d, \"error\": \"MISMATCH\"}\n", name, M);
+        const std::string v = std::string(name) + "_small";
         out(v.c_str(), time_us(s, reps, [&] { launch_rgemm(b, M, s); }), (double)M * 256 * eb, fl);
+        // two streams, each with its own launches (the step's s / s2 chains): time per launch
+        for (int sm = 0; sm < 2; ++sm) {  // independent pairs: s and s2 each run their own launches
+          RGemm c1 = r, c2 = r;
+          c1.small = c2.small = sm;
+          c2.C = C2;
+          for (int i = 0; i < 3; ++i) { launch_rgemm(c1, M, s); launch_rgemm(c2, M, s2); }
+          CK(hipDeviceSynchronize());
+          hipEvent_t a0, a1;
+          CK(hipEventCreate(&a0));
+          CK(hipEventCreate(&a1));
+          CK(hipEventRecord(a0, s));
+          CK(hipStreamWaitEvent(s2, a0, 0));
+          for (int i = 0; i < reps; ++i) { launch_rgemm(c1, M, s); launch_rgemm(c2, M, s2); }
+          CK(hipEventRecord(a1, s2));
+          CK(hipStreamWaitEvent(s, a1, 0));
+          CK(hipEventRecord(a1, s));
+          CK(hipEventSynchronize(a1));
+          float ms = 0;
+          CK(hipEventElapsedTime(&ms, a0, a1));
+          const std::string v2 = std::string(name) + (sm ? "_small" : "") + "_2streams_per_launch";
+          out(v2.c_str(), ms * 1000.0 / (2 * reps), (double)M * 256 * eb, fl);
+          CK(hipEventDestroy(a0));
+          CK(hipEventDestroy(a1));
+        }
       }
-      if (mode == 2) continue;
-      const int geo[4][2] = {{128, 3}, {64, 2}, {64, 3}, {64, 4}};
-      for (auto& gm : geo) {
-        if (launch_rgemm_variant(r, M, s, gm[0], gm[1]) != 0) {
-          (void)hipGetLastError();
-          printf("{\"kernel\": \"%s_bm%d_ns%d\", \"M\": %d, \"error\": \"launch\"}\n", name, gm[0], gm[1], M);
-          continue;
-        }
+      {  // phase clocks of one launch (wave 0 of each workgroup; shader clock ticks, 100 MHz memtime
+         // on gfx950 -> converted with the measured ratio below)
+        const int nb = (M + 127) / 128;
+        unsigned long long* tb;
+        CK(hipMalloc(&tb, (size_t)nb * 16 * 8));
+        CK(hipMemset(tb, 0, (size_t)nb * 16 * 8));
+        rg_timing_buffer(tb);
+        launch_rgemm(r, M, s);
         CK(hipStreamSynchronize(s));
-        {  // the variant's output equals the default kernel's, byte for byte
-          RGemm r2 = r;
-          r2.C = C2;
-          launch_rgemm(r2, M, s);
-          launch_rgemm(r, M, s);
-          CK(hipStreamSynchronize(s));
-          if (launch_rgemm_variant(r2, M, s, gm[0], gm[1]) != 0) return 1;
-          CK(hipStreamSynchronize(s));
-          const size_t bytes = (size_t)M * 256 * (r.cbf ? 2 : 4);
-          if (!same_bytes(C, C2, bytes)) printf("{\"kernel\": \"%s_bm%d_ns%d\", \"M\": %d, \"error\": \"MISMATCH\"}\n", name, gm[0], gm[1], M);
+        rg_timing_buffer(nullptr);
+        std::vector<unsigned long long> h((size_t)nb * 16);
+        CK(hipMemcpy(h.data(), tb, h.size() * 8, hipMemcpyDeviceToHost));
+        CK(hipFree(tb));
+        unsigned long long t0 = ~0ull, t1 = 0;
+        double ph[16] = {};
+        int cnt = 0;
+        for (int b = 0; b < nb; ++b) {
+          const unsigned long long* q = &h[(size_t)b * 16];
+          if (!q[0] || !q[13]) continue;
+          t0 = std::min(t0, q[0]);
+          t1 = std::max(t1, q[13]);
+          unsigned long long prev = q[0];
+          for (int i = 1; i < 14; ++i) {
+            if (!q[i]) continue;
+            ph[i] += (double)(q[i] - prev);
+            prev = q[i];
+          }
+          ++cnt;
         }
-        const std::string v = std::string(name) + "_bm" + std::to_string(gm[0]) + "_ns" + std::to_string(gm[1]);
-        out(v.c_str(), time_us(s, reps, [&] { launch_rgemm_variant(r, M, s, gm[0], gm[1]); }), (double)M * 256 * eb, fl);
+        printf("{\"phases\": \"%s\", \"M\": %d, \"wgs\": %d, \"span_ticks\": %llu", name, M, cnt, t1 - t0);
+        for (int i = 1; i < 14; ++i)
+          if (ph[i] > 0) printf(", \"t%d\": %.0f", i, ph[i] / cnt);
+        printf("}\n");
       }
     }
     // generic fp32 / bf16x3 tile GEMMs (anr_gemm.hip), forward layout
@@ -196,25 +276,6 @@ int main(int argc, char** argv) {
       if (mode == 1) w.x3 = 1;
       const double eb = mode == 0 ? 4 : 8;
       out(name, time_us(s, reps, [&] { launch_wgrad(w, M, s); }), (double)M * 256 * eb, fl);
-      for (int d : {2, 4}) {
-        {  // the deep kernel's dW against k_wgrad's (slab groups meet in fp32 atomics: order may differ)
-          WGrad a = w, b = w;
-          a.deep = 0; a.bsum = nullptr;
-          b.deep = d; b.bsum = nullptr; b.dW = dW2;
-          CK(hipMemsetAsync(dW, 0, 256 * 256 * 4, s));
-          CK(hipMemsetAsync(dW2, 0, 256 * 256 * 4, s));
-          launch_wgrad(a, M, s);
-          CK(hipStreamSynchronize(s));
-          launch_wgrad(b, M, s);
-          CK(hipStreamSynchronize(s));
-          const double e = max_rel_diff(dW2, dW, 256 * 256);
-          if (!(e < 1e-5)) printf("{\"kernel\": \"%s_deep%d\", \"M\": %d, \"error\": \"MISMATCH %g\"}\n", name, d, M, e);
-        }
-        w.deep = d;
-        const std::string v = std::string(name) + "_deep" + std::to_string(d);
-        out(v.c_str(), time_us(s, reps, [&] { launch_wgrad(w, M, s); }), (double)M * 256 * eb, fl);
-      }
-      w.deep = 0;
     }
     {
       GemmArgs g{};
@@ -227,6 +288,36 @@ int main(int argc, char** argv) {
     out("copy_bf16_rows", time_us(s, reps, [&] {
           hipLaunchKernelGGL(k_probe_copy, dim3(cus * 4), dim3(256), 0, s, (const uint4*)A, (uint4*)C, n16);
         }), (double)M * 256 * 4, 0);
+  }
+  {  // LDS-DMA and register stream rates per CU (1 MiB per workgroup, 256 workgroups)
+    const long per = 1 << 20;
+    unsigned char* big;
+    CK(hipMalloc(&big, per * 256));
+    CK(hipMemset(big, 1, per * 256));
+    uint4* sink;
+    CK(hipMalloc(&sink, 1024 * 16));
+    auto dma = [&](const char* name, auto kern, int W, int shared) {
+      CK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024));
+      const float us = time_us(s, 20, [&] { hipLaunchKernelGGL(kern, dim3(256), dim3(W * 64), 128 * 1024, s, (const unsigned char*)big, per, shared); });
+      printf("{\"stream\": \"%s\", \"shared\": %d, \"us\": %.2f, \"GBps_per_CU\": %.1f, \"TBps\": %.2f}\n", name, shared, us,
+             per / us * 1e-3, 256.0 * per / us * 1e-6);
+    };
+    auto vld = [&](const char* name, auto kern, int W, int shared) {
+      const float us = time_us(s, 20, [&] { hipLaunchKernelGGL(kern, dim3(256), dim3(W * 64), 0, s, (const unsigned char*)big, per, shared, sink); });
+      printf("{\"stream\": \"%s\", \"shared\": %d, \"us\": %.2f, \"GBps_per_CU\": %.1f, \"TBps\": %.2f}\n", name, shared, us,
+             per / us * 1e-3, 256.0 * per / us * 1e-6);
+    };
+    for (int sh = 0; sh < 2; ++sh) {
+      dma("dma_w4_d1", k_probe_dma<4, 1>, 4, sh);
+      dma("dma_w4_d4", k_probe_dma<4, 4>, 4, sh);
+      dma("dma_w4_d16", k_probe_dma<4, 16>, 4, sh);
+      dma("dma_w8_d2", k_probe_dma<8, 2>, 8, sh);
+      dma("dma_w8_d8", k_probe_dma<8, 8>, 8, sh);
+      dma("dma_w16_d4", k_probe_dma<16, 4>, 16, sh);
+      vld("vload_w4_d4", k_probe_vload<4, 4>, 4, sh);
+      vld("vload_w8_d8", k_probe_vload<8, 8>, 8, sh);
+      vld("vload_w16_d8", k_probe_vload<16, 8>, 16, sh);
+    }
   }
   int least = 0, greatest = 0;
   CK(hipDeviceGetStreamPriorityRange(&least, &greatest));

@@ -2,7 +2,7 @@
 # One parameterised GPU-box driver (run through gpurun from the repo root):
 #   tools/gpu.sh TAG step [step ...]
 # steps (each under its own time limit; the script stops at the first failure):
-#   tests[=PATTERN]   pytest -m gpu (optionally -k PATTERN; _or_ = ' or ') -> gpurun_out/TAG_gpu_tests.log
+#   tests[=PATTERN]   pytest -m gpu (optionally -k PATTERN; _or_ = ' or ', _and_ = ' and ') -> gpurun_out/TAG_gpu_tests.log
 #   smoke             __graft_entry__.smoke()                          -> TAG_smoke.log
 #   bench[:ARGS]      python bench.py ARGS (ARGS comma-separated)      -> TAG_bench[_MODE].log
 #   prof[:ARGS]       rocprofv3 --kernel-trace --stats of bench ARGS  -> TAG_prof[_MODE]/
@@ -15,6 +15,8 @@
 #   trace[:ARGS]      rocprofv3 --kernel-trace (per-dispatch timestamps, no stats) of bench ARGS
 #                     (tools/train_trace_summary.py, tools/sdf_batch_trace.py read it) -> TAG_trace[_MODE]/
 #   probe[:ARGS]      tools/gemm_probe ARGS (layer-GEMM kernels timed alone; make probe) -> TAG_probe.log
+#   probeprof[:ARGS]  the same under rocprofv3 --kernel-trace --stats        -> TAG_probeprof/
+#   probecnt:KERNEL:C1+C2[:ARGS]  one --pmc pass over the probe, KERNEL's dispatches -> TAG_pcnt_KERNEL/
 #   counters:KERNEL:C1+C2+..[:ARGS]  one --pmc pass with the given counters (<= the per-block limits)
 #                     over one bench step                              -> TAG_cnt_KERNEL/
 set -o pipefail
@@ -42,6 +44,7 @@ for step in "$@"; do
       pat=${step#tests=}
       [ "$pat" = "$step" ] && pat=""
       pat=${pat//_or_/ or }
+      pat=${pat//_and_/ and }
       sel=()
       [ -n "$pat" ] && sel=(-k "$pat")
       timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 180 --timeout-method thread "${sel[@]}" \
@@ -111,6 +114,22 @@ for step in "$@"; do
       timeout -k 10 300 tools/gemm_probe $(args_of "$rest") > gpurun_out/${TAG}_probe.log 2>&1 \
         || { rc=$?; tail -20 gpurun_out/${TAG}_probe.log; exit $rc; }
       echo "PROBE_OK" ;;
+    probeprof)
+      [ -x tools/gemm_probe ] || { echo "tools/gemm_probe missing (make probe)"; exit 2; }
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_probeprof -o run --output-format csv -- \
+        tools/gemm_probe $(args_of "$rest") > gpurun_out/${TAG}_probeprof.log 2>&1 \
+        || { rc=$?; tail -20 gpurun_out/${TAG}_probeprof.log; exit $rc; }
+      echo "PROBEPROF_OK" ;;
+    probecnt)
+      k=${rest%%:*}
+      r2=${rest#*:}
+      cs=${r2%%:*}
+      a=${r2#*:}
+      [ "$a" = "$r2" ] && a=""
+      timeout -s KILL 180 rocprofv3 --pmc ${cs//+/ } --kernel-include-regex "$k" -d gpurun_out/${TAG}_pcnt_$k -o p \
+        --output-format csv -- tools/gemm_probe $(args_of "$a") > gpurun_out/${TAG}_pcnt_$k.log 2>&1 \
+        || { rc=$?; tail -20 gpurun_out/${TAG}_pcnt_$k.log; exit $rc; }
+      echo "PROBECNT_OK $k" ;;
     counters)
       k=${rest%%:*}
       r2=${rest#*:}
