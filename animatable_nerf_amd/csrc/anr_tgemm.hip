@@ -181,28 +181,26 @@ bool wimg_view(const void* base, const float* const* t, const float* W, int c0, 
 // weight image each workgroup streams serves 128 rows. bf16: 64-deep K chunks. X3 (split-bf16,
 // fp32-level: lo*h + h*lo + h*h, the weight rows' lo image riding in the same slot): 32-deep chunks
 // so that three 128-row operand images fit two slots.
-// SM (bf16 products only): 32-deep chunks in a 3-slot ring, 72 KiB of LDS with bf16 rows (96 KiB
-// fp32), so that two row GEMMs (two streams) fit one CU and one's load / store bursts overlap the
-// other's MFMAs
-template <bool X3, bool ABF = false, bool SM = false> struct RgCfg {
-  static_assert(!(SM && X3), "SM: bf16 products");
+// (Measured alternatives, tools/gemm_probe at 24,893 rows: three slots 13.5 vs 12.9 us; 64-row
+// workgroups (4 waves, 2-4 slots) 21.5 us; 32-deep chunks in a 3-slot 72 KiB ring, two workgroups per
+// CU, 14.9 us alone and 11.6 vs 9.9 us per launch with two streams. The workgroup's time is its load
+// burst, four chunks and a store burst that runs at the HBM write rate (phase clocks).)
+template <bool X3, bool ABF = false> struct RgCfg {
   static constexpr int BM = 128;
   static constexpr int WAVES = BM / 16;
-  static constexpr int KC = X3 || SM ? 32 : 64;                        // K chunk
+  static constexpr int KC = X3 ? 32 : 64;                              // K chunk
   static constexpr int AE = ABF ? 2 : 4;                               // bytes per activation element
   static constexpr int A_BYTES = BM * KC * AE;                         // activations, BM rows x KC
   static constexpr int B_BYTES = 256 * KC * 2;                         // bf16 weight rows, 256 x KC
-  static constexpr int NS = SM ? 3 : 2;                                // ring slots
+  static constexpr int NS = 2;                                         // ring slots
   static constexpr int SLOT = A_BYTES + B_BYTES * (X3 ? 2 : 1);        // bytes per slot
   static constexpr int PIECES_A = A_BYTES / 1024 / WAVES;              // per wave
   static constexpr int PIECES_B = B_BYTES / 1024 / WAVES;
   static constexpr int OPS = PIECES_A + PIECES_B * (X3 ? 2 : 1);       // vmem ops per wave per chunk
   static constexpr int CHA = KC * AE / 16, CHB = KC / 8;              // 16-B chunks per A / B row
   // XOR swizzle of a row's 16-B chunks, chosen so the 16 rows of one fragment read hit distinct banks
-  static __device__ __forceinline__ int swa(int r) {
-    return X3 ? ((r >> 1) & 7) : SM ? (ABF ? ((r >> 2) & 3) : ((r >> 1) & 7)) : ABF ? (r & 7) : (r & 15);
-  }
-  static __device__ __forceinline__ int swb(int r) { return X3 || SM ? ((r >> 2) & 3) : (r & 7); }
+  static __device__ __forceinline__ int swa(int r) { return X3 ? ((r >> 1) & 7) : ABF ? (r & 7) : (r & 15); }
+  static __device__ __forceinline__ int swb(int r) { return X3 ? ((r >> 2) & 3) : (r & 7); }
 };
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
@@ -218,10 +216,10 @@ __device__ __forceinline__ void rg_dma(const void* src, unsigned m0) {
 }
 
 // issue chunk c (segment-relative K offset kk) into ring slot `slot`
-template <bool X3, bool ABF, bool SM>
+template <bool X3, bool ABF>
 __device__ __forceinline__ void rg_issue(const RGemm& g, int seg, int kk, int m0, int M, int N, unsigned slot_lds, int w,
                                          int lane) {
-  using C = RgCfg<X3, ABF, SM>;
+  using C = RgCfg<X3, ABF>;
   const unsigned char* A = (const unsigned char*)(seg ? g.seg[1].A : g.seg[0].A);
   const long lda = seg ? g.seg[1].lda : g.seg[0].lda;
   const unsigned short* B = seg ? g.seg[1].B : g.seg[0].B;
@@ -283,9 +281,9 @@ void rg_timing_buffer(unsigned long long* p) { (void)hipMemcpyToSymbol(HIP_SYMBO
   } while (0)
 #endif
 
-template <bool X3, bool ABF, bool MBF, bool SM = false>
+template <bool X3, bool ABF, bool MBF>
 __global__ __launch_bounds__(RgCfg<X3>::WAVES * 64) void k_rgemm(RGemm g) {
-  using CF = RgCfg<X3, ABF, SM>;
+  using CF = RgCfg<X3, ABF>;
   constexpr int RG_NS = CF::NS, RG_SLOT = CF::SLOT, RG_OPS = CF::OPS;
   constexpr int RG_BM = CF::BM, RG_A_BYTES = CF::A_BYTES;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -301,7 +299,7 @@ __global__ __launch_bounds__(RgCfg<X3>::WAVES * 64) void k_rgemm(RGemm g) {
   auto issue = [&](int c) {
     const int seg = c < nc0 ? 0 : 1;
     const int kk = (c - (seg ? nc0 : 0)) * KC;
-    rg_issue<X3, ABF, SM>(g, seg, kk, m0, M, N, base + (c % RG_NS) * RG_SLOT, w, lane);
+    rg_issue<X3, ABF>(g, seg, kk, m0, M, N, base + (c % RG_NS) * RG_SLOT, w, lane);
   };
   RG_T(0);
   const int wr = (w >> 2) * 64;   // this wave's 64 rows of the tile
@@ -526,18 +524,8 @@ __global__ __launch_bounds__(RgCfg<X3>::WAVES * 64) void k_rgemm(RGemm g) {
       }
 }
 
-template <bool X3, bool ABF, bool SM = false>
-size_t rgemm_lds_bytes() { return (size_t)RgCfg<X3, ABF, SM>::NS * RgCfg<X3, ABF, SM>::SLOT; }
-
-// ANR_RG_SMALL=1: the bf16-product row GEMMs in the SM geometry (measurement switch)
-static bool rg_small() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("ANR_RG_SMALL");
-    v = e && e[0] == '1' ? 1 : 0;
-  }
-  return v == 1;
-}
+template <bool X3, bool ABF>
+size_t rgemm_lds_bytes() { return (size_t)RgCfg<X3, ABF>::NS * RgCfg<X3, ABF>::SLOT; }
 
 void launch_rgemm(const RGemm& g0, int M_host, hipStream_t s) {
   RGemm g = g0;
@@ -562,29 +550,6 @@ void launch_rgemm(const RGemm& g0, int M_host, hipStream_t s) {
   constexpr int BM = RgCfg<false>::BM;
   const dim3 grid((M_host + BM - 1) / BM), block(RgCfg<false>::WAVES * 64);
   const bool mbf = g.mbf && g.mask;
-  if (!g.x3 && (rg_small() || g.small)) {
-    static bool attr_sm = false;
-    if (!attr_sm) {
-      (void)hipFuncSetAttribute((const void*)k_rgemm<false, false, false, true>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)rgemm_lds_bytes<false, false, true>());
-      (void)hipFuncSetAttribute((const void*)k_rgemm<false, false, true, true>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)rgemm_lds_bytes<false, false, true>());
-      (void)hipFuncSetAttribute((const void*)k_rgemm<false, true, false, true>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)rgemm_lds_bytes<false, true, true>());
-      (void)hipFuncSetAttribute((const void*)k_rgemm<false, true, true, true>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)rgemm_lds_bytes<false, true, true>());
-      attr_sm = true;
-    }
-    if (g.abf && mbf)
-      hipLaunchKernelGGL((k_rgemm<false, true, true, true>), grid, block, (rgemm_lds_bytes<false, true, true>()), s, g);
-    else if (g.abf)
-      hipLaunchKernelGGL((k_rgemm<false, true, false, true>), grid, block, (rgemm_lds_bytes<false, true, true>()), s, g);
-    else if (mbf)
-      hipLaunchKernelGGL((k_rgemm<false, false, true, true>), grid, block, (rgemm_lds_bytes<false, false, true>()), s, g);
-    else
-      hipLaunchKernelGGL((k_rgemm<false, false, false, true>), grid, block, (rgemm_lds_bytes<false, false, true>()), s, g);
-    return;
-  }
   if (g.x3)
     hipLaunchKernelGGL((k_rgemm<true, false, false>), grid, block, (rgemm_lds_bytes<true, false>()), s, g);
   else if (g.abf && mbf)

@@ -92,7 +92,6 @@ struct RGemm {
   int accumulate;
   int vec_out;  // set by launch_rgemm: C (and mask) rows 16-B addressable, N % 4 == 0
   int vec16;    // set by launch_rgemm: bf16 C rows take 16-B stores (ldc % 8 == 0, C 16-B aligned)
-  int small;    // bf16 products in the 72 KiB geometry (RgCfg SM; also ANR_RG_SMALL=1)
   int x3;       // split-bf16 products (fp32-level): activations hi/lo, weights hi/lo images
   // bf16 storage (training precision 'bf16': every consumer rounds these to bf16 anyway): A rows,
   // C rows (RNE from the fp32 result) and the mask rows hold bf16 (C / mask reinterpreted as
@@ -185,6 +184,7 @@ struct TrainBufs {
   float* dGt2;   // [N][64] second contribution (T-pose BW chain), summed by k_tr_tpose_bwd; NULL: none
   unsigned short* dAlpha16;  // [N][64] bf16 d alpha in column 0 (written when hb)
   int hb;        // bf16 storage (training precision bf16): Gt, Gv and d alpha (dAlpha16) are written as bf16
+  int hbp;       // bf16 storage of the pose space too (precision bf16_all): Gp written as bf16
   int ldl;       // row stride of dLp / dLt (0: 32); the training executor uses 64, the row GEMM's K chunk
   const int* out_row;
   const int* m_rows;

@@ -43,7 +43,9 @@ __global__ __launch_bounds__(256) void k_tr_point_prep(TrainBufs b) {
     world_to_pose(pts, b.R, b.Th, pose);
     for (int c = 0; c < 3; ++c) dir[c] = b.ray_d[3 * ray + c];
   }
-  b.Gp[(long)i * 64 + lane] = lane < 63 ? embed_feature(pose, lane, 10) : 0.f;
+  const float gp = lane < 63 ? embed_feature(pose, lane, 10) : 0.f;
+  if (b.hbp) ((unsigned short*)b.Gp)[(long)i * 64 + lane] = f2bf(gp);
+  else b.Gp[(long)i * 64 + lane] = gp;
   if (lane < 32) {
     float lo[3], hi[3];
     for (int c = 0; c < 3; ++c) { lo[c] = b.pbounds[c]; hi[c] = b.pbounds[3 + c]; }
@@ -524,7 +526,9 @@ __global__ __launch_bounds__(256) void k_an_prep_obs(TrainBufs b, const float* _
   if (i >= n) return;
   float pose[3];
   world_to_pose_pt(wpts, i, n, n, b.R, b.Th, pose);
-  b.Gp[(long)i * 64 + lane] = lane < 63 ? embed_feature(pose, lane, 10) : 0.f;
+  const float gp = lane < 63 ? embed_feature(pose, lane, 10) : 0.f;
+  if (b.hbp) ((unsigned short*)b.Gp)[(long)i * 64 + lane] = f2bf(gp);
+  else b.Gp[(long)i * 64 + lane] = gp;
   if (lane < 32) {
     float lo[3], hi[3];
     for (int c = 0; c < 3; ++c) { lo[c] = b.pbounds[c]; hi[c] = b.pbounds[3 + c]; }

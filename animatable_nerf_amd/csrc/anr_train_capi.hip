@@ -307,8 +307,10 @@ struct PoseScope {
   Exec& e;
   int keep, keep_hb;
   explicit PoseScope(Exec& x) : e(x), keep(x.bf16), keep_hb(x.hb) {
-    e.hb = 0;  // the pose-space activations (and gamma(x)) stay fp32 under every policy
+    // ANR_BF16: fp32-level split products on fp32 rows; ANR_BF16_ALL: bf16 products on bf16 rows (gamma(x)
+    // included, TrainBufs.hbp), as the rest of the network
     if (e.pose_fp32) {
+      e.hb = 0;
       e.bf16 = 0;
       e.x3 = 1;
     }
@@ -486,6 +488,7 @@ int train_forward(const anr_params* p, const anr_frame* f, const float* ray_o, c
   const int n = e.grid_n();
   TrainBufs b = bufs(T, ws, f, ray_o, ray_d, near_, far_, R, o, x);
   b.hb = e.hb;
+  b.hbp = e.hb && !e.pose_fp32;
   const int g1 = (n + 255) / 256;
   if (n > 0) {
     hipLaunchKernelGGL(k_tr_point_prep, dim3((n + 3) / 4), dim3(256), 0, s, b);

@@ -9,7 +9,10 @@ pytestmark = pytest.mark.gpu
 
 GATE_DB = 0.05   # north_star: "PSNR within 0.05 dB"
 STEPS = 500
-SEEDS = 3
+# 500-step trajectories are chaotic: split-K atomics reorder fp32 sums run to run, and single fp32 runs
+# of one seed moved by up to 0.1 dB (profiles/r4n: fp32 seeds 11.843 / 11.946 / 11.942 dB). Means over
+# 8 seeds keep the gate's own noise (~0.02 dB on the difference) well inside the 0.05 dB bar.
+SEEDS = 8
 
 
 @pytest.fixture(scope='module')

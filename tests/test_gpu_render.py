@@ -304,3 +304,45 @@ def test_split_precisions_are_fp32_level(dev, split):
     for k, e in got[split].items():
         bar = 1.5 * max(ref_err[k], got['fp32'][k])
         assert e <= bar, (k, e, ref_err[k], got['fp32'][k])
+
+
+def test_split_precisions_fp32_level_full_frame(dev):
+    """The fp32-level bar of test_split_precisions_are_fp32_level on a whole config-2 frame (512 x 512
+    box rays of the bench's scene, 128 chunks): the fp64 and fp32 oracle evaluations run with
+    PyTorch-ROCm on the GPU (oracle/restate.py on device tensors), the three device precisions are
+    rendered from the same batch. bf16x6 (the fp32-level products) must be within 1.5x the larger of
+    the reference's own fp32 error and the exact fp32 kernel's on every output; bf16x3 is reported
+    (its products are ~2^-16 relative: not fp32-level by construction) and held to the render tests'
+    1e-4 bar on rgb / acc."""
+    from animatable_nerf_amd import config
+    from animatable_nerf_amd.renderer import Renderer
+    sc = scene(0.025)
+    ro, rd = sc.box_rays(512 * 512, seed=2)
+    b, _ = batch_np(sc, ro, rd)
+    bd = to_torch(b, dev)
+    with torch.no_grad():
+        p32 = {k: v.to(dev) for k, v in oracle_params().items()}
+        r32 = restate.render(p32, bd)
+        p64 = {k: v.double() for k, v in p32.items()}
+        b64 = {k: (v.double() if v.dtype == torch.float32 else v) for k, v in bd.items()}
+        r64 = restate.render(p64, b64)
+    keys = ('rgb_map', 'acc_map', 'depth_map', 'raw', 'pbw', 'tbw')
+    assert torch.equal(_keep(r32['raw']).cpu(), _keep(r64['raw']).cpu())
+    ref_err = {k: float((r32[k].double() - r64[k]).abs().max()) for k in keys}
+    del r32
+    net = make_net(dev)
+    net.train()
+    got = {}
+    for prec in ('fp32', 'bf16x6', 'bf16x3'):
+        cfg = config.defaults()
+        cfg.perturb = 0
+        cfg.render_precision = prec
+        ret = Renderer(net, cfg).render_device(bd)
+        got[prec] = {k: float((ret[k].double() - r64[k]).abs().max()) for k in keys}
+        del ret
+    print({p: got[p] for p in got}, ref_err)
+    for k in keys:
+        bar = 1.5 * max(ref_err[k], got['fp32'][k])
+        assert got['bf16x6'][k] <= bar, (k, got['bf16x6'][k], ref_err[k], got['fp32'][k])
+    for k in ('rgb_map', 'acc_map'):
+        assert got['bf16x3'][k] <= 1e-4, (k, got['bf16x3'][k])

@@ -181,20 +181,9 @@ int main(int argc, char** argv) {
       const double eb = (r.abf ? 2 : 4) + (r.cbf ? 2 : 4) + (r.mask ? (r.mbf ? 2 : 4) : 0);
       out(name, time_us(s, reps, [&] { launch_rgemm(r, M, s); }), (double)M * 256 * eb, fl);
       if (!r.x3) {
-        RGemm a = r, b = r;
-        b.small = 1;
-        b.C = C2;
-        launch_rgemm(a, M, s);
-        launch_rgemm(b, M, s);
-        CK(hipStreamSynchronize(s));
-        const size_t bytes = (size_t)M * 256 * (r.cbf ? 2 : 4);
-        if (!same_bytes(C, C2, bytes)) printf("{\"kernel\": \"%s_small\", \"M\": %d, \"error\": \"MISMATCH\"}\n", name, M);
-        const std::string v = std::string(name) + "_small";
-        out(v.c_str(), time_us(s, reps, [&] { launch_rgemm(b, M, s); }), (double)M * 256 * eb, fl);
         // two streams, each with its own launches (the step's s / s2 chains): time per launch
-        for (int sm = 0; sm < 2; ++sm) {  // independent pairs: s and s2 each run their own launches
+        {  // independent pairs: s and s2 each run their own launches
           RGemm c1 = r, c2 = r;
-          c1.small = c2.small = sm;
           c2.C = C2;
           for (int i = 0; i < 3; ++i) { launch_rgemm(c1, M, s); launch_rgemm(c2, M, s2); }
           CK(hipDeviceSynchronize());
@@ -210,7 +199,7 @@ int main(int argc, char** argv) {
           CK(hipEventSynchronize(a1));
           float ms = 0;
           CK(hipEventElapsedTime(&ms, a0, a1));
-          const std::string v2 = std::string(name) + (sm ? "_small" : "") + "_2streams_per_launch";
+          const std::string v2 = std::string(name) + "_2streams_per_launch";
           out(v2.c_str(), ms * 1000.0 / (2 * reps), (double)M * 256 * eb, fl);
           CK(hipEventDestroy(a0));
           CK(hipEventDestroy(a1));
