@@ -18,7 +18,7 @@ $(SRC_DIR)/%.o: $(SRC_DIR)/%.hip
 	$(HIPCC) $(CXXFLAGS) -MMD -MP -c $< -o $@
 
 $(LIB): $(OBJS)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@.tmp $(OBJS) && mv -f $@.tmp $@
 
 -include $(DEPS)
 

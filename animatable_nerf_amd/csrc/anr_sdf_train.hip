@@ -511,10 +511,24 @@ struct LgImage {
   void* img;
 };
 
+// x6 products (the parts the split-bf16 precision cannot take, ANR_SDF_X6_PARTS): the row GEMM's
+// three-way split (anr_tgemm.hip k_rgemm X6, ~2^-24 relative per product) on a hi / mid / lo weight
+// image packed into the same arena once per call and weight view
+struct RgImage {
+  const float *B0, *B1;
+  long c0, c1;
+  int K0, K1, N;
+  const unsigned short* img;
+  long ldb;
+};
+
 struct TG {
   hipStream_t s;
   int x3 = 0;
-  int wg_x3 = 1;          // x3: the weight gradients split-bf16 too
+  int x6 = 0;
+  RgImage rg[64];
+  int nrg = 0;
+  int wg_x3 = 0;          // the weight gradients split-bf16 (set per part)
   float* slab = nullptr;  // k_wgrad partial slabs (x3)
   char* lg_arena = nullptr;  // k_lgemm weight images (x3)
   size_t lg_cap = 0, lg_used = 0;
@@ -540,10 +554,72 @@ struct TG {
                         a.K, two ? b.K : 0, g.N, img};
     return img;
   }
+  // the row GEMM takes the product: k-contiguous fp32 activations (16-B rows, lda >= K rounded to the
+  // 32-deep chunk), W k-contiguous (b_rs == 1), 64 <= N <= 256, epilogues bias / ReLU / softplus (+
+  // derivative rows) / mask / accumulate / div_post
+  bool rg_ok(const GemmArgs& g) const {
+    if (!lg_arena || g.N < 64 || g.N > 256 || g.nseg < 1 || g.nseg > 2 || g.atomic || g.ksplit > 1 || g.K_dev ||
+        g.M_dev || g.div_pre != 0.f || g.spd || g.rowsum || g.rowsum2 || g.a_softplus_w || g.head_w || g.bf16 ||
+        ((uintptr_t)g.C & 15) || g.ldc % 4)
+      return false;
+    if (g.mask && (g.ldm % 4 || ((uintptr_t)g.mask & 15))) return false;
+    for (int q = 0; q < g.nseg; ++q) {
+      const GemmSeg& a = g.seg[q];
+      if (a.a_cs != 1 || a.a_rs % 4 || ((uintptr_t)a.A & 15) || a.a_rs < (a.K + 31) / 32 * 32 || a.b_rs != 1) return false;
+      if (q == 1 && a.b_cs != g.seg[0].b_cs) return false;
+    }
+    return true;
+  }
+  const RgImage* rg_image(const GemmArgs& g) {
+    const GemmSeg& a = g.seg[0];
+    const bool two = g.nseg > 1;
+    // W row-major [N][in_ch] seen through the segment views B = W + c0 (b_cs = in_ch): key on W's own
+    // address per segment (the views of one W share b_cs)
+    for (int i = 0; i < nrg; ++i) {
+      const RgImage& q = rg[i];
+      if (q.B0 == a.B && q.K0 == a.K && q.N == g.N && q.c0 == a.b_cs && q.B1 == (two ? g.seg[1].B : nullptr) &&
+          (!two || q.K1 == g.seg[1].K))
+        return &q;
+    }
+    if (nrg >= 64) return nullptr;
+    // both segments index one W: the segment views B_s = W + c0_s with W = B_0 - c0_0; the pack
+    // kernel reads W[n * ldw + c0_s + k], so it takes B_0 as the base and c0 offsets relative to it
+    const int K[2] = {a.K, two ? g.seg[1].K : 0};
+    const int c0[2] = {0, two ? (int)(g.seg[1].B - a.B) : 0};
+    const size_t bytes = ((size_t)rimg_x6_elems(g.N, g.nseg, K) * 2 + 255) / 256 * 256;
+    if (lg_used + bytes > lg_cap) return nullptr;
+    unsigned short* img = (unsigned short*)(lg_arena + lg_used);
+    if (rimg_x6_pack(a.B, a.b_cs, g.N, g.nseg, c0, K, img, s) != 0) return nullptr;
+    lg_used += bytes;
+    rg[nrg] = RgImage{a.B, two ? g.seg[1].B : nullptr, a.b_cs, two ? g.seg[1].b_cs : 0, a.K, K[1], g.N, img,
+                      rimg_x6_ldb(g.nseg, K)};
+    return &rg[nrg++];
+  }
+  int run_x6(const GemmArgs& g, int M, const RgImage* im) {
+    RGemm r{};
+    r.x3 = 1;
+    r.x6 = 1;
+    r.M = M;
+    r.N = g.N;
+    r.nseg = g.nseg;
+    const long plane = (long)g.N * im->ldb;
+    int col = 0;
+    for (int q = 0; q < g.nseg; ++q) {
+      r.seg[q] = RGemmSeg{g.seg[q].A, g.seg[q].a_rs, g.seg[q].K, im->img, im->ldb, col, g.N, plane};
+      col += (g.seg[q].K + 63) / 64 * 64;
+    }
+    r.C = g.C; r.ldc = g.ldc; r.bias = g.bias; r.relu = g.relu; r.mask = g.mask; r.ldm = g.ldm;
+    r.accumulate = g.accumulate;
+    r.softplus = g.softplus; r.deriv = g.deriv; r.ldd = g.ldd; r.div_post = g.div_post;
+    launch_rgemm(r, M, s);
+    return check_launch("k_rgemm x6 (sdf train)");
+  }
   int run(GemmArgs g, int M) {
     if (M <= 0 || g.N <= 0) return ANR_OK;
     g.M = M;
     if (g.ksplit < 1) g.ksplit = 1;
+    if (x6 && rg_ok(g))
+      if (const RgImage* im = rg_image(g)) return run_x6(g, M, im);
     if (x3 && !g.atomic) g.x3 = 1;
     if (g.x3 && lg_arena && lgemm_supported(g)) {
       if (void* img = lg_image(g)) {
@@ -573,7 +649,7 @@ struct TG {
   int wgrad(int M, float* dW, int in_ch, int c0, int Nout, const float* dY, long ldY, const float* X, long ldX, int K,
             float* bsum = nullptr) {
     if (M <= 0) return ANR_OK;
-    if (x3 && wg_x3 && slab && Nout <= 256 && K <= 256 && ldY % 4 == 0 && ldX % 4 == 0 && ((uintptr_t)dY & 15) == 0 &&
+    if (wg_x3 && slab && Nout <= 256 && K <= 256 && ldY % 4 == 0 && ldX % 4 == 0 && ((uintptr_t)dY & 15) == 0 &&
         ((uintptr_t)X & 15) == 0) {
       WGrad w{};
       w.x3 = 1;
@@ -784,15 +860,22 @@ int sdf_train_core(const TrainCore& C) {
   // gradients are ~1e-5 in magnitude and lose tests/test_gpu_sdf_train.py's 5e-3-of-max bar to split
   // products in any of those two (the softplus(beta=100) factors of the SDF forward feed every
   // second-order term); each other part split alone, and all of them together, keep it (profiles/r4e,
-  // r4g, r4h bisection)
+  // r4g, r4h bisection). Bit 128: the weight gradients split-bf16 in every part, the exact ones included
   static const int x3_parts = [] {
     const char* v = getenv("ANR_SDF_X3_PARTS");
     return v ? atoi(v) : 124;
   }();
+  // the parts kept at fp32 level run their forward products as x6 row GEMMs (same bits; default the
+  // residual MLP and the SDF forward, 3)
+  static const int x6_parts = [] {
+    const char* v = getenv("ANR_SDF_X6_PARTS");
+    return v ? atoi(v) : 3;
+  }();
   const bool x3_on = o->precision == ANR_BF16X3;
   auto part = [&](int bit) {
     g.x3 = x3_on && (x3_parts & bit) ? 1 : 0;
-    g.wg_x3 = g.x3 && (x3_parts & 64) ? 1 : 0;
+    g.x6 = x3_on && !g.x3 && (x6_parts & bit) ? 1 : 0;
+    g.wg_x3 = x3_on && ((g.x3 && (x3_parts & 64)) || (x3_parts & 128)) ? 1 : 0;
   };
   if (x3_on) {
     g.slab = F(L.wslab);

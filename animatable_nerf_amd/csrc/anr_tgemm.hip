@@ -185,18 +185,22 @@ bool wimg_view(const void* base, const float* const* t, const float* W, int c0, 
 // workgroups (4 waves, 2-4 slots) 21.5 us; 32-deep chunks in a 3-slot 72 KiB ring, two workgroups per
 // CU, 14.9 us alone and 11.6 vs 9.9 us per launch with two streams. The workgroup's time is its load
 // burst, four chunks and a store burst that runs at the HBM write rate (phase clocks).)
-template <bool X3, bool ABF = false> struct RgCfg {
+// X6 (with X3 set: fp32 activations, 32-deep chunks): a third weight image per slot (hi / mid / lo),
+// 64 KiB slots, 128 KiB of LDS.
+template <bool X3, bool ABF = false, bool X6 = false> struct RgCfg {
+  static_assert(!X6 || X3, "X6 runs on the X3 geometry");
   static constexpr int BM = 128;
   static constexpr int WAVES = BM / 16;
   static constexpr int KC = X3 ? 32 : 64;                              // K chunk
   static constexpr int AE = ABF ? 2 : 4;                               // bytes per activation element
   static constexpr int A_BYTES = BM * KC * AE;                         // activations, BM rows x KC
   static constexpr int B_BYTES = 256 * KC * 2;                         // bf16 weight rows, 256 x KC
+  static constexpr int NIMG = X6 ? 3 : X3 ? 2 : 1;                     // weight images per slot
   static constexpr int NS = 2;                                         // ring slots
-  static constexpr int SLOT = A_BYTES + B_BYTES * (X3 ? 2 : 1);        // bytes per slot
+  static constexpr int SLOT = A_BYTES + B_BYTES * NIMG;                // bytes per slot
   static constexpr int PIECES_A = A_BYTES / 1024 / WAVES;              // per wave
   static constexpr int PIECES_B = B_BYTES / 1024 / WAVES;
-  static constexpr int OPS = PIECES_A + PIECES_B * (X3 ? 2 : 1);       // vmem ops per wave per chunk
+  static constexpr int OPS = PIECES_A + PIECES_B * NIMG;               // vmem ops per wave per chunk
   static constexpr int CHA = KC * AE / 16, CHB = KC / 8;              // 16-B chunks per A / B row
   // XOR swizzle of a row's 16-B chunks, chosen so the 16 rows of one fragment read hit distinct banks
   static __device__ __forceinline__ int swa(int r) { return X3 ? ((r >> 1) & 7) : ABF ? (r & 7) : (r & 15); }
@@ -216,10 +220,10 @@ __device__ __forceinline__ void rg_dma(const void* src, unsigned m0) {
 }
 
 // issue chunk c (segment-relative K offset kk) into ring slot `slot`
-template <bool X3, bool ABF>
+template <bool X3, bool ABF, bool X6 = false>
 __device__ __forceinline__ void rg_issue(const RGemm& g, int seg, int kk, int m0, int M, int N, unsigned slot_lds, int w,
                                          int lane) {
-  using C = RgCfg<X3, ABF>;
+  using C = RgCfg<X3, ABF, X6>;
   const unsigned char* A = (const unsigned char*)(seg ? g.seg[1].A : g.seg[0].A);
   const long lda = seg ? g.seg[1].lda : g.seg[0].lda;
   const unsigned short* B = seg ? g.seg[1].B : g.seg[0].B;
@@ -255,6 +259,8 @@ __device__ __forceinline__ void rg_issue(const RGemm& g, int seg, int kk, int m0
       const int br = min(r, brows - 1);
       const int ch = (lane % C::CHB) ^ C::swb(r);
       rg_dma(B + lo + (long)br * ldb + bcol + kk + ch * 8, slot_lds + C::A_BYTES + C::B_BYTES + p * 1024);
+      if constexpr (X6)
+        rg_dma(B + 2 * lo + (long)br * ldb + bcol + kk + ch * 8, slot_lds + C::A_BYTES + 2 * C::B_BYTES + p * 1024);
     }
   }
   (void)N;
@@ -281,9 +287,9 @@ void rg_timing_buffer(unsigned long long* p) { (void)hipMemcpyToSymbol(HIP_SYMBO
   } while (0)
 #endif
 
-template <bool X3, bool ABF, bool MBF>
+template <bool X3, bool ABF, bool MBF, bool X6 = false>
 __global__ __launch_bounds__(RgCfg<X3>::WAVES * 64) void k_rgemm(RGemm g) {
-  using CF = RgCfg<X3, ABF>;
+  using CF = RgCfg<X3, ABF, X6>;
   constexpr int RG_NS = CF::NS, RG_SLOT = CF::SLOT, RG_OPS = CF::OPS;
   constexpr int RG_BM = CF::BM, RG_A_BYTES = CF::A_BYTES;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -299,7 +305,7 @@ __global__ __launch_bounds__(RgCfg<X3>::WAVES * 64) void k_rgemm(RGemm g) {
   auto issue = [&](int c) {
     const int seg = c < nc0 ? 0 : 1;
     const int kk = (c - (seg ? nc0 : 0)) * KC;
-    rg_issue<X3, ABF>(g, seg, kk, m0, M, N, base + (c % RG_NS) * RG_SLOT, w, lane);
+    rg_issue<X3, ABF, X6>(g, seg, kk, m0, M, N, base + (c % RG_NS) * RG_SLOT, w, lane);
   };
   RG_T(0);
   const int wr = (w >> 2) * 64;   // this wave's 64 rows of the tile
@@ -354,7 +360,7 @@ __global__ __launch_bounds__(RgCfg<X3>::WAVES * 64) void k_rgemm(RGemm g) {
     if (active) {
 #pragma unroll
       for (int ks = 0; ks < KC / 32; ++ks) {
-        bf16x8_t af[4], bfr[4], al[4], bl[4];
+        bf16x8_t af[4], bfr[4], al[4], bl[4], am[4], b2[4];  // X6: am / b2 the third parts
         const int kc = 4 * ks + (lane >> 4);  // 8-element k group of this lane
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -380,7 +386,13 @@ __global__ __launch_bounds__(RgCfg<X3>::WAVES * 64) void k_rgemm(RGemm g) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
             af[i][e] = (__bf16)x[e];
-            if constexpr (X3) al[i][e] = (__bf16)(x[e] - (float)af[i][e]);
+            if constexpr (X6) {  // x = hi + mid + lo, each residual exact in fp32
+              const float r1 = x[e] - (float)af[i][e];
+              am[i][e] = (__bf16)r1;
+              al[i][e] = (__bf16)(r1 - (float)am[i][e]);
+            } else if constexpr (X3) {
+              al[i][e] = (__bf16)(x[e] - (float)af[i][e]);
+            }
           }
         }
 #pragma unroll
@@ -389,12 +401,19 @@ __global__ __launch_bounds__(RgCfg<X3>::WAVES * 64) void k_rgemm(RGemm g) {
           const int sb = CF::swb(r);
           bfr[j] = *(const bf16x8_t*)(sB + r * (KC * 2) + ((kc ^ sb) * 16));
           if constexpr (X3) bl[j] = *(const bf16x8_t*)(sB + CF::B_BYTES + r * (KC * 2) + ((kc ^ sb) * 16));
+          if constexpr (X6) b2[j] = *(const bf16x8_t*)(sB + 2 * CF::B_BYTES + r * (KC * 2) + ((kc ^ sb) * 16));
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            if constexpr (X3) {
+            if constexpr (X6) {  // weight planes bfr / bl / b2 = hi / mid / lo; 2^-16 terms first
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b2[j], af[i], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], al[i], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl[j], am[i], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl[j], af[i], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], am[i], acc[i][j], 0, 0, 0);
+            } else if constexpr (X3) {
               acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl[j], af[i], acc[i][j], 0, 0, 0);
               acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], al[i], acc[i][j], 0, 0, 0);
             }
@@ -445,9 +464,30 @@ __global__ __launch_bounds__(RgCfg<X3>::WAVES * 64) void k_rgemm(RGemm g) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
         }
+        if constexpr (X6) {
+          if (g.softplus) {  // torch softplus(beta=100, threshold=20) and the factor its backward uses
+            f32x4 dv;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float z = v[e] * 100.f;
+              const float ez = fast_exp(z);
+              dv[e] = z > 20.f ? -1.f : ez;
+              v[e] = z > 20.f ? v[e] : fast_log1p(ez) / 100.f;
+            }
+            const int m = m0 + wr + 16 * i + (lane & 15);
+            const int n = wc + 16 * j + 4 * (lane >> 4);
+            if (g.deriv && m < M && n < N) *(f32x4*)(g.deriv + (long)m * g.ldd + n) = dv;
+          }
+        }
         if (g.mask) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = mk[i][j][e] > 0.f ? v[e] : 0.f;
+        }
+        if constexpr (X6) {
+          if (g.div_post != 0.f) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = v[e] / g.div_post;
+          }
         }
         acc[i][j] = v;
       }
@@ -515,23 +555,35 @@ __global__ __launch_bounds__(RgCfg<X3>::WAVES * 64) void k_rgemm(RGemm g) {
         if (g.bias) v += g.bias[n];
         if (g.accumulate) v += *cp;
         if (g.relu) v = fmaxf(v, 0.f);
+        if constexpr (X6) {
+          if (g.softplus) {
+            const float z = v * 100.f;
+            const float ez = fast_exp(z);
+            if (g.deriv) g.deriv[(long)m * g.ldd + n] = z > 20.f ? -1.f : ez;
+            v = z > 20.f ? v : fast_log1p(ez) / 100.f;
+          }
+        }
         if (g.mask) {
           const float mv = MBF ? bf2f(mask16[(long)m * g.ldm + n]) : g.mask[(long)m * g.ldm + n];
           if (!(mv > 0.f)) v = 0.f;
+        }
+        if constexpr (X6) {
+          if (g.div_post != 0.f) v = v / g.div_post;
         }
         if (g.cbf) C16[(long)m * g.ldc + n] = f2bf_rne(v);
         else *cp = v;
       }
 }
 
-template <bool X3, bool ABF>
-size_t rgemm_lds_bytes() { return (size_t)RgCfg<X3, ABF>::NS * RgCfg<X3, ABF>::SLOT; }
+template <bool X3, bool ABF, bool X6 = false>
+size_t rgemm_lds_bytes() { return (size_t)RgCfg<X3, ABF, X6>::NS * RgCfg<X3, ABF, X6>::SLOT; }
 
 void launch_rgemm(const RGemm& g0, int M_host, hipStream_t s) {
   RGemm g = g0;
   const size_t ce = g.cbf ? 2 : 4, me = g.mbf ? 2 : 4;  // C / mask element bytes
   g.vec_out = (g.N % 4 == 0) && (g.ldc % 4 == 0) && ((uintptr_t)g.C % (4 * ce) == 0) &&
-              (!g.mask || ((g.ldm % 4 == 0) && ((uintptr_t)g.mask % (4 * me) == 0))) && ((uintptr_t)g.bias % 16 == 0);
+              (!g.mask || ((g.ldm % 4 == 0) && ((uintptr_t)g.mask % (4 * me) == 0))) && ((uintptr_t)g.bias % 16 == 0) &&
+              (!g.deriv || (g.ldd % 4 == 0 && (uintptr_t)g.deriv % 16 == 0));
   g.vec16 = g.vec_out && g.cbf && g.ldc % 8 == 0 && (uintptr_t)g.C % 16 == 0;
   static bool attr = false;
   if (!attr) {
@@ -545,12 +597,16 @@ void launch_rgemm(const RGemm& g0, int M_host, hipStream_t s) {
                               (int)rgemm_lds_bytes<false, true>());
     (void)hipFuncSetAttribute((const void*)k_rgemm<true, false, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)rgemm_lds_bytes<true, false>());
+    (void)hipFuncSetAttribute((const void*)k_rgemm<true, false, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)rgemm_lds_bytes<true, false, true>());
     attr = true;
   }
   constexpr int BM = RgCfg<false>::BM;
   const dim3 grid((M_host + BM - 1) / BM), block(RgCfg<false>::WAVES * 64);
   const bool mbf = g.mbf && g.mask;
-  if (g.x3)
+  if (g.x6)
+    hipLaunchKernelGGL((k_rgemm<true, false, false, true>), grid, block, (rgemm_lds_bytes<true, false, true>()), s, g);
+  else if (g.x3)
     hipLaunchKernelGGL((k_rgemm<true, false, false>), grid, block, (rgemm_lds_bytes<true, false>()), s, g);
   else if (g.abf && mbf)
     hipLaunchKernelGGL((k_rgemm<false, true, true>), grid, block, (rgemm_lds_bytes<false, true>()), s, g);
@@ -560,6 +616,51 @@ void launch_rgemm(const RGemm& g0, int M_host, hipStream_t s) {
     hipLaunchKernelGGL((k_rgemm<false, false, true>), grid, block, (rgemm_lds_bytes<false, false>()), s, g);
   else
     hipLaunchKernelGGL((k_rgemm<false, false, false>), grid, block, (rgemm_lds_bytes<false, false>()), s, g);
+}
+
+long rimg_x6_ldb(int nseg, const int* K) {
+  long ld = 0;
+  for (int s = 0; s < nseg; ++s) ld += rup64(K[s]);
+  return ld;
+}
+long rimg_x6_elems(int N, int nseg, const int* K) { return 3L * N * rimg_x6_ldb(nseg, K); }
+
+struct RPackX6 {
+  const float* W;
+  long ldw, ldb, plane;
+  int N, nseg, c0[2], K[2], col[2];
+  unsigned short* out;
+};
+
+// one thread per image element (n, column): hi, mid = bf16(w - hi), lo = bf16(w - hi - mid)
+__global__ void k_rimg_x6_pack(RPackX6 a) {
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= a.plane) return;
+  const int n = (int)(e / a.ldb), col = (int)(e - (long)n * a.ldb);
+  float v = 0.f;
+  for (int s = 0; s < a.nseg; ++s)
+    if (col >= a.col[s] && col < a.col[s] + a.K[s]) v = a.W[(long)n * a.ldw + a.c0[s] + col - a.col[s]];
+  const unsigned short hi = f2bf_rne(v);
+  const float r1 = v - __uint_as_float((uint32_t)hi << 16);
+  const unsigned short mid = f2bf_rne(r1);
+  a.out[e] = hi;
+  a.out[a.plane + e] = mid;
+  a.out[2 * a.plane + e] = f2bf_rne(r1 - __uint_as_float((uint32_t)mid << 16));
+}
+
+int rimg_x6_pack(const float* W, long ldw, int N, int nseg, const int* c0, const int* K, unsigned short* dst, hipStream_t s) {
+  if (nseg < 1 || nseg > 2 || N <= 0) return -1;
+  RPackX6 a{};
+  a.W = W; a.ldw = ldw; a.N = N; a.nseg = nseg; a.out = dst;
+  long col = 0;
+  for (int q = 0; q < nseg; ++q) {
+    a.c0[q] = c0[q]; a.K[q] = K[q]; a.col[q] = (int)col;
+    col += rup64(K[q]);
+  }
+  a.ldb = col;
+  a.plane = (long)N * col;
+  hipLaunchKernelGGL(k_rimg_x6_pack, dim3((unsigned)((a.plane + 255) / 256)), dim3(256), 0, s, a);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 }  // namespace anr
@@ -680,20 +781,21 @@ __device__ __forceinline__ void wg_put_bf(unsigned short* S, const uint2 (&r)[4]
   }
 }
 
+// the LDS of one weight-gradient workgroup: per buffer two 32-sample images (hi and lo under X3, two
+// sample halves otherwise), double-buffered, and the column-sum exchange
+struct WgLds {
+  unsigned short sY[2][2 * WG_S * WG_LD];
+  unsigned short sX[2][2 * WG_S * WG_LD];
+  float srs[8][WG_T];
+};
+
+// one (output tile, sample range) of dW: (ti, tj) the 128 x 128 tile of dW, z the sample range
 template <bool X3, bool YBF, bool XBF>
-__global__ __launch_bounds__(256) void k_wgrad(WGrad g) {
+__device__ __forceinline__ void wgrad_tile(const WGrad& g, int ti, int tj, int z, WgLds& sm) {
   constexpr int D = WG_D;
   constexpr int NI = X3 ? 2 : 1;
   constexpr int NH = X3 ? 1 : 2;
-  __shared__ __attribute__((aligned(16))) unsigned short sY[2][NI][NH * WG_S * WG_LD];
-  __shared__ __attribute__((aligned(16))) unsigned short sX[2][NI][NH * WG_S * WG_LD];
-  __shared__ float srs[8][WG_T];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int tiles = gridDim.x * gridDim.y;
-  const int L = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
-  const int slot = L >> 3, tile = slot % tiles;
-  const int z = (slot / tiles) * 8 + (L & 7);
-  const int ti = tile % gridDim.x, tj = tile / gridDim.x;
   const int n = g.M_dev ? *g.M_dev : g.n;
   const int spb = g.spb ? g.spb : ((n + g.nz - 1) / g.nz + 2 * WG_S - 1) / (2 * WG_S) * (2 * WG_S);
   const int s0 = z * spb, s1 = min(n, s0 + spb);
@@ -731,7 +833,7 @@ __global__ __launch_bounds__(256) void k_wgrad(WGrad g) {
       for (int h = 0; h < NH; ++h) {
         // bf16 rows go to LDS as loaded (masked); fp32 rows are rounded (and split under X3)
         if constexpr (YBF) {
-          wg_put_bf(sY[buf][0] + h * WG_S * WG_LD, ry[d][h], g.nout, i0, s + h * WG_S, s1, tid);
+          wg_put_bf((sm.sY[buf] + h * WG_S * WG_LD), ry[d][h], g.nout, i0, s + h * WG_S, s1, tid);
           if (do_rs) {
             f32x4 vy[4];
             wg_widen<true>(ry[d][h], g.nout, i0, s + h * WG_S, s1, tid, vy);
@@ -745,14 +847,14 @@ __global__ __launch_bounds__(256) void k_wgrad(WGrad g) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) rsum += vy[q];
           }
-          wg_store<X3>(sY[buf][0] + h * WG_S * WG_LD, sY[buf][NI - 1] + h * WG_S * WG_LD, tid, vy);
+          wg_store<X3>((sm.sY[buf] + h * WG_S * WG_LD), (sm.sY[buf] + (NI - 1 + h) * WG_S * WG_LD), tid, vy);
         }
         if constexpr (XBF) {
-          wg_put_bf(sX[buf][0] + h * WG_S * WG_LD, rx[d][h], g.K, j0, s + h * WG_S, s1, tid);
+          wg_put_bf((sm.sX[buf] + h * WG_S * WG_LD), rx[d][h], g.K, j0, s + h * WG_S, s1, tid);
         } else {
           f32x4 vx[4];
           wg_widen<false>(rx[d][h], g.K, j0, s + h * WG_S, s1, tid, vx);
-          wg_store<X3>(sX[buf][0] + h * WG_S * WG_LD, sX[buf][NI - 1] + h * WG_S * WG_LD, tid, vx);
+          wg_store<X3>((sm.sX[buf] + h * WG_S * WG_LD), (sm.sX[buf] + (NI - 1 + h) * WG_S * WG_LD), tid, vx);
         }
       }
       __syncthreads();
@@ -762,13 +864,13 @@ __global__ __launch_bounds__(256) void k_wgrad(WGrad g) {
         bf16x8_t fa[4], fb[4], la[4], lb[4];
 #pragma unroll
         for (int a = 0; a < 4; ++a) {
-          fa[a] = wg_frag(sY[buf][0] + h * WG_S * WG_LD, wi + 16 * a, lane);
-          if constexpr (X3) la[a] = wg_frag(sY[buf][NI - 1] + h * WG_S * WG_LD, wi + 16 * a, lane);
+          fa[a] = wg_frag((sm.sY[buf] + h * WG_S * WG_LD), wi + 16 * a, lane);
+          if constexpr (X3) la[a] = wg_frag((sm.sY[buf] + (NI - 1 + h) * WG_S * WG_LD), wi + 16 * a, lane);
         }
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
-          fb[b] = wg_frag(sX[buf][0] + h * WG_S * WG_LD, wj + 16 * b, lane);
-          if constexpr (X3) lb[b] = wg_frag(sX[buf][NI - 1] + h * WG_S * WG_LD, wj + 16 * b, lane);
+          fb[b] = wg_frag((sm.sX[buf] + h * WG_S * WG_LD), wj + 16 * b, lane);
+          if constexpr (X3) lb[b] = wg_frag((sm.sX[buf] + (NI - 1 + h) * WG_S * WG_LD), wj + 16 * b, lane);
         }
 #pragma unroll
         for (int a = 0; a < 4; ++a)
@@ -790,25 +892,64 @@ __global__ __launch_bounds__(256) void k_wgrad(WGrad g) {
 #pragma unroll
     for (int b = 0; b < 4; ++b) *(f32x4*)(slab + (a * 4 + b) * 256 + lane * 4) = acc[a][b];
   if (do_rs) {
-    *(f32x4*)&srs[tid >> 5][4 * (tid & 31)] = rsum;
+    *(f32x4*)&sm.srs[tid >> 5][4 * (tid & 31)] = rsum;
     __syncthreads();
     if (tid < WG_T) {
       float t = 0.f;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) t += srs[k][tid];
+      for (int k = 0; k < 8; ++k) t += sm.srs[k][tid];
       g.rs_slab[(long)z * 256 + i0 + tid] = t;
     }
   }
+}
+
+template <bool X3, bool YBF, bool XBF>
+__global__ __launch_bounds__(256) void k_wgrad(WGrad g) {
+  __shared__ __attribute__((aligned(16))) WgLds sm;
+  // XCD-aware order: workgroups are dealt to the 8 XCDs round-robin by linear id, so the tiles of
+  // one sample range (which read the same dY and X rows) get ids on one XCD and share its L2
+  // (launch_wgrad makes the range count a multiple of 8)
+  const int tiles = gridDim.x * gridDim.y;
+  const int L = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+  const int slot = L >> 3, tile = slot % tiles;
+  const int z = (slot / tiles) * 8 + (L & 7);
+  wgrad_tile<X3, YBF, XBF>(g, tile % gridDim.x, tile / gridDim.x, z, sm);
+}
+
+// several weight gradients of one operand format in one launch (the layers of an MLP's backward):
+// workgroup b belongs to descriptor k with start[k] <= b < start[k+1] and is placed within it as in
+// k_wgrad. One format per launch: a run-time switch would size the registers for the widest variant
+// (measured: 256 VGPRs + 123 AGPRs, occupancy 1, where the bf16 variant takes 190 + 64)
+template <bool X3, bool YBF, bool XBF>
+__device__ __forceinline__ void wgrad_group_body(const WGradGroup& G) {
+  __shared__ __attribute__((aligned(16))) WgLds sm;
+  const int b = blockIdx.x;
+  int k = 0;
+  while (k + 1 < G.n && b >= G.start[k + 1]) ++k;
+  const WGrad& g = G.d[k];
+  const int L = b - G.start[k];
+  const int slot = L >> 3, tile = slot % g.tiles;
+  const int z = (slot / g.tiles) * 8 + (L & 7);
+  const int nti = g.tiles / g.tj;
+  wgrad_tile<X3, YBF, XBF>(g, tile % nti, tile / nti, z, sm);
+}
+template <bool X3, bool YBF, bool XBF>
+__global__ __launch_bounds__(256) void k_wgrad_group(WGradGroup G) {
+  wgrad_group_body<X3, YBF, XBF>(G);
+}
+// bf16 rows both ways (the bulk of the bf16 training backward): held to two waves per SIMD, as k_wgrad's
+template <>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_wgrad_group<false, true, true>(WGradGroup G) {
+  wgrad_group_body<false, true, true>(G);
 }
 
 // dW[i][c0 + j] += sum_z slab; bsum[i] (+ bsum2[i]) += sum_z rs_slab[z][i]. One thread per 4 rows of
 // one column (a slab lane's float4) and per group of WG_ZG consecutive slabs; the groups' sums meet
 // in fp32 atomics (as the generic kernel's split-K does).
 #define WG_ZG 8
-__global__ void k_wgrad_reduce(WGrad g) {
+__device__ __forceinline__ void wgrad_reduce_at(const WGrad& g, int u) {  // u: (z group, tile, w, a, b, lane)
   const int per_tile = 4 * 16 * 64;
   const int nu = g.tiles * per_tile;
-  const int u = blockIdx.x * blockDim.x + threadIdx.x;  // (z group, tile, w, a, b, lane)
   const int zg = u / nu, v = u - zg * nu;
   const int z0 = zg * WG_ZG, z1 = min(g.nz, z0 + WG_ZG);
   if (z0 < g.nz) {
@@ -840,6 +981,20 @@ __global__ void k_wgrad_reduce(WGrad g) {
   }
 }
 
+__global__ void k_wgrad_reduce(WGrad g) { wgrad_reduce_at(g, blockIdx.x * blockDim.x + threadIdx.x); }
+
+__global__ void k_wgrad_reduce_group(WGradGroup G) {
+  const int b = blockIdx.x;
+  int k = 0;
+  while (k + 1 < G.n && b >= G.rstart[k + 1]) ++k;
+  wgrad_reduce_at(G.d[k], (b - G.rstart[k]) * blockDim.x + threadIdx.x);
+}
+
+static int wgrad_reduce_blocks(const WGrad& g) {
+  const int nred = g.tiles * 4 * 16 * 64 * ((g.nz + WG_ZG - 1) / WG_ZG);
+  return ((nred > 256 ? nred : 256) + 255) / 256;
+}
+
 size_t wgrad_slab_floats() { return (size_t)WG_MAX_Z * 4 * WG_TILE_FLOATS + (size_t)WG_MAX_Z * 256; }
 
 int launch_wgrad(WGrad g, int n_host, hipStream_t s) {
@@ -862,9 +1017,61 @@ int launch_wgrad(WGrad g, int n_host, hipStream_t s) {
   else if (g.ybf) hipLaunchKernelGGL((k_wgrad<false, true, false>), grid, dim3(256), 0, s, g);
   else if (g.xbf) hipLaunchKernelGGL((k_wgrad<false, false, true>), grid, dim3(256), 0, s, g);
   else hipLaunchKernelGGL((k_wgrad<false, false, false>), grid, dim3(256), 0, s, g);
-  const int nred = g.tiles * 4 * 16 * 64 * ((g.nz + WG_ZG - 1) / WG_ZG);
-  const int nthr = nred > 256 ? nred : 256;
-  hipLaunchKernelGGL(k_wgrad_reduce, dim3((nthr + 255) / 256), dim3(256), 0, s, g);
+  hipLaunchKernelGGL(k_wgrad_reduce, dim3(wgrad_reduce_blocks(g)), dim3(256), 0, s, g);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_wgrad_group(const WGrad* d, int nd, int n_host, int nz, float* slab, size_t slab_floats, hipStream_t s) {
+  if (n_host <= 0 || nd <= 0) return 0;
+  nz = nz < 8 ? 8 : (nz > WG_MAX_Z ? WG_MAX_Z : (nz + 7) / 8 * 8);
+  WGradGroup G{};
+  size_t used = 0;
+  auto fmt = [](const WGrad& g) { return g.x3 ? 0 : (g.ybf && g.xbf) ? 1 : g.ybf ? 2 : g.xbf ? 3 : 4; };
+  auto issue = [&]() {
+    if (G.n == 0) return;
+    for (int v = 0; v < 5; ++v) {  // one product launch per operand format present, one reduce for all
+      WGradGroup H{};
+      for (int k = 0; k < G.n; ++k)
+        if (fmt(G.d[k]) == v) {
+          H.d[H.n] = G.d[k];
+          H.start[H.n + 1] = H.start[H.n] + G.start[k + 1] - G.start[k];
+          ++H.n;
+        }
+      if (!H.n) continue;
+      const dim3 grid(H.start[H.n]);
+      if (v == 0) hipLaunchKernelGGL((k_wgrad_group<true, false, false>), grid, dim3(256), 0, s, H);
+      else if (v == 1) hipLaunchKernelGGL((k_wgrad_group<false, true, true>), grid, dim3(256), 0, s, H);
+      else if (v == 2) hipLaunchKernelGGL((k_wgrad_group<false, true, false>), grid, dim3(256), 0, s, H);
+      else if (v == 3) hipLaunchKernelGGL((k_wgrad_group<false, false, true>), grid, dim3(256), 0, s, H);
+      else hipLaunchKernelGGL((k_wgrad_group<false, false, false>), grid, dim3(256), 0, s, H);
+    }
+    hipLaunchKernelGGL(k_wgrad_reduce_group, dim3(G.rstart[G.n]), dim3(256), 0, s, G);
+    G = WGradGroup{};
+    used = 0;
+  };
+  for (int k = 0; k < nd; ++k) {
+    WGrad g = d[k];
+    g.tj = (g.K + WG_T - 1) / WG_T;
+    g.tiles = ((g.nout + WG_T - 1) / WG_T) * g.tj;
+    // a descriptor's slabs are (nz, tile) partial tiles, then (nz, 256) column sums; nz halves (not below 8)
+    // until the descriptor fits the region on its own
+    int z = nz;
+    auto need = [&](int zz) { return (size_t)zz * g.tiles * WG_TILE_FLOATS + ((g.bsum || g.bsum2) ? (size_t)zz * 256 : 0); };
+    while (z > 8 && need(z) > slab_floats) z = z / 16 * 8 > 8 ? z / 16 * 8 : 8;
+    if (need(z) > slab_floats) return -1;
+    if (G.n == WG_GROUP_MAX || used + need(z) > slab_floats) issue();  // the region is reused in stream order
+    g.nz = z;
+    g.n = n_host;
+    g.spb = g.M_dev ? 0 : ((n_host + z - 1) / z + 2 * WG_S - 1) / (2 * WG_S) * (2 * WG_S);
+    g.slab = slab + used;
+    g.rs_slab = (g.bsum || g.bsum2) ? g.slab + (size_t)z * g.tiles * WG_TILE_FLOATS : nullptr;
+    used += need(z);
+    G.d[G.n] = g;
+    G.start[G.n + 1] = G.start[G.n] + g.tiles * z;
+    G.rstart[G.n + 1] = G.rstart[G.n] + wgrad_reduce_blocks(g);
+    ++G.n;
+  }
+  issue();
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -93,12 +93,26 @@ struct RGemm {
   int vec_out;  // set by launch_rgemm: C (and mask) rows 16-B addressable, N % 4 == 0
   int vec16;    // set by launch_rgemm: bf16 C rows take 16-B stores (ldc % 8 == 0, C 16-B aligned)
   int x3;       // split-bf16 products (fp32-level): activations hi/lo, weights hi/lo images
+  // x6 (the sdf_pdf training's exact parts): three-way split, activations and weights hi/mid/lo (the
+  // weight image's planes lo_off apart), six bf16 MFMAs per product (~2^-24 relative: fp32 level);
+  // its epilogue also takes the sdf forward's Softplus(beta=100) with the derivative rows and div_post
+  int x6;
+  int softplus;
+  float* deriv;
+  long ldd;
+  float div_post;
   // bf16 storage (training precision 'bf16': every consumer rounds these to bf16 anyway): A rows,
   // C rows (RNE from the fp32 result) and the mask rows hold bf16 (C / mask reinterpreted as
   // unsigned short*). Not with x3; C bf16 excludes accumulate.
   int abf, cbf, mbf;
 };
 void launch_rgemm(const RGemm& g, int M_host, hipStream_t s);
+// x6 weight image of W (row-major [N][ldw]) for the row GEMM: rows n < N, the nseg column segments
+// [c0_s, c0_s + K_s) of W each padded to 64 (image columns col_s), planes hi / mid / lo of N x ldb
+// bf16 elements each (plane stride N * ldb); rimg_x6_elems() elements in all
+long rimg_x6_ldb(int nseg, const int* K);
+long rimg_x6_elems(int N, int nseg, const int* K);
+int rimg_x6_pack(const float* W, long ldw, int N, int nseg, const int* c0, const int* K, unsigned short* dst, hipStream_t s);
 // bf16 weight images of the training GEMM weights: forward (rows = outputs, k = used input columns,
 // segments padded to 64) and backward (rows = input columns, k = outputs padded to 64). t: the
 // ANR_NUM_TENSORS network tensors followed by the ANR_NUM_NOVEL_TENSORS novel_pose_bw tensors
@@ -139,6 +153,18 @@ struct WGrad {
 };
 size_t wgrad_slab_floats();
 int launch_wgrad(WGrad g, int n_host, hipStream_t s);
+// several weight gradients in two launches (k_wgrad_group + k_wgrad_reduce_group): d[0..nd) as for
+// launch_wgrad (dY, X, dW, bsum, M_dev, formats; slab fields ignored) with nz sample ranges each, their
+// partial slabs packed into slab[0, slab_floats); more descriptors than fit one launch (WG_GROUP_MAX, or
+// the slab region) are issued as consecutive groups on s, reusing the region in stream order
+#define WG_GROUP_MAX 16
+struct WGradGroup {
+  WGrad d[WG_GROUP_MAX];
+  int n;
+  int start[WG_GROUP_MAX + 1];   // first workgroup of descriptor k (k_wgrad_group)
+  int rstart[WG_GROUP_MAX + 1];  // first reduce block of descriptor k (k_wgrad_reduce_group)
+};
+int launch_wgrad_group(const WGrad* d, int nd, int n_host, int nz, float* slab, size_t slab_floats, hipStream_t s);
 
 // split-bf16 layer GEMM with LDS-resident weight images for large M (anr_lgemm.hip; the sdf_pdf
 // batches): lgemm_supported(g) (g.x3, no accumulate / mask / atomics, 16-B addressable operands),

@@ -26,6 +26,8 @@ namespace {
 // more lanes would put a weight-gradient lane on s2's queue (measured: the T-pose chain then waits
 // behind weight gradients, profiles/r3k trace)
 constexpr int kWStreams = 2;
+// partial-slab floats per lane: a weight-gradient group of up to 16 products at 16 sample ranges
+const size_t kLaneFloats = 4 * wgrad_slab_floats();
 
 // training workspace = render layout (prefix, incl. raw) + per-sample activations / gradients
 struct TLayout {
@@ -59,7 +61,7 @@ TLayout tlayout(int n_rays, int chunk, long np, long nt) {
   T.dFeat = take(N * 256); T.dLat = take(N * 256); T.dView = take(N * 128);
   T.ysum = take(8 * 256); T.acc3 = take(4); T.d_rgb = take(R * 3); T.d_pbw = take(N * 24); T.d_tbw = take(N * 24);
   T.wimg = take((wimg_bytes() + 3) / 4);
-  T.wslab = take(wgrad_slab_floats() * kWStreams);
+  T.wslab = take(kLaneFloats * kWStreams);
   T.total = o;
   return T;
 }
@@ -148,6 +150,28 @@ struct Exec {
   int hb = 0;  // bf16 storage of the T-pose / canonical activations (precision bf16 / bf16_all, training executor)
   SideStreams* ss = nullptr;  // NULL: every product on s
   int wnext = 0;               // round-robin weight-gradient lane
+  size_t lane_floats = 0;      // partial-slab floats per weight-gradient lane
+  // grouped weight gradients (ANR_WG_GROUP, default on): wgrad() queues the products of the fast path
+  // and flush_w() issues them as one k_wgrad_group + one reduce on lane 0, after everything issued so
+  // far to the streams they were queued from, then the latent-row updates that read their column sums.
+  // Fewer sample ranges per product (nz, ANR_WG_GROUP_NZ) still fill the chip, because the products of a
+  // group run side by side: less partial-slab traffic and ~4x fewer launches than one product at a time.
+  int group = 0, group_nz = 16;
+  int flush_every = 0;  // ANR_WG_FLUSH_EVERY: also flush once this many products are queued (0: phase ends only)
+  WGrad pend[WG_GROUP_MAX];
+  int npend = 0;
+  hipStream_t pend_src[2] = {};
+  struct LatentPost {
+    const float* ys;
+    const float* W;
+    int in_ch, c0, ncol;
+    const float* tab;
+    const int64_t* li;
+    int add;
+    float *gW, *gtab;
+  } post[8];
+  int npost = 0;
+  int nqueued = 0;  // products queued so far
   // the kept-sample count stays on the device (no host read, so a step can be captured in a graph):
   // every launch is sized for the capacity `cap` and reads the count from n_dev
   const int* n_dev = nullptr;
@@ -164,15 +188,54 @@ struct Exec {
     *w = ss ? ss->sw[l] : s;
     return order(ss, *w, s);
   }
-  float* slab(int lane) const { return wslab ? wslab + (size_t)lane * wgrad_slab_floats() : nullptr; }
+  float* slab(int lane) const { return wslab ? wslab + (size_t)lane * lane_floats : nullptr; }
+  // issue the queued weight gradients (grouped) and the latent-row updates that follow them
+  int flush_w() {
+    if (!npend && !npost) return ANR_OK;
+    hipStream_t w = ss ? ss->sw[0] : s;
+    for (int i = 0; i < 2 && pend_src[i]; ++i) ANR_TRY(order(ss, w, pend_src[i]));
+    if (npend && launch_wgrad_group(pend, npend, grid_n(), group_nz, slab(0), lane_floats, w) != 0)
+      return check_launch("k_wgrad_group");
+    for (int i = 0; i < npost; ++i) {
+      const LatentPost& q = post[i];
+      hipLaunchKernelGGL(k_tr_latent_grad, dim3(256 + 128), dim3(128), 0, w, q.ys, q.W, q.in_ch, q.c0, q.ncol, q.tab, q.li,
+                         q.add, q.gW, q.gtab);
+      ANR_TRY(check_launch("k_tr_latent_grad"));
+    }
+    npend = npost = 0;
+    pend_src[0] = pend_src[1] = nullptr;
+    return ANR_OK;
+  }
+  // zero the column-sum scratch ys (on s, ahead of the products queued after it) and update the latent
+  // rows from it once the weight gradient that fills it has run: k_tr_latent_grad after that product
+  int latent_rows(float* ys, float* dW, int in_ch, int c0, int Nout, const float* dY, int ldY, const float* X, int ldX,
+                  int K, float* bsum, unsigned bf, const LatentPost& q) {
+    hipStream_t w = s;
+    int lane = 0;
+    if (!group) ANR_TRY(wstream(&w, &lane, 0));
+    if (hipMemsetAsync(ys, 0, 256 * 4, w) != hipSuccess) return fail(ANR_E_HIP, "memset");
+    if (group && (npend == WG_GROUP_MAX || npost == 8)) ANR_TRY(flush_w());  // product and update in one flush
+    const int q0 = nqueued;
+    ANR_TRY(wgrad(dW, in_ch, c0, Nout, dY, ldY, X, ldX, K, bsum, ys, 0, bf));
+    if (nqueued > q0) {
+      post[npost++] = q;
+      return ANR_OK;
+    }
+    if (group) ANR_TRY(wstream(&w, &lane, 0));  // off the fast path: the product ran on lane 0
+    hipLaunchKernelGGL(k_tr_latent_grad, dim3(256 + 128), dim3(128), 0, w, q.ys, q.W, q.in_ch, q.c0, q.ncol, q.tab, q.li,
+                       q.add, q.gW, q.gtab);
+    return check_launch("k_tr_latent_grad");
+  }
   // lane 0 waits for the other lanes (every weight gradient issued so far is done when lane 0 is)
   int gather_w() {
+    ANR_TRY(flush_w());
     if (!ss) return ANR_OK;
     for (int l = 1; l < kWStreams; ++l) ANR_TRY(order(ss, ss->sw[0], ss->sw[l]));
     return ANR_OK;
   }
   // s waits for every weight-gradient lane (end of a backward)
   int join_w() {
+    ANR_TRY(flush_w());
     if (!ss) return ANR_OK;
     for (int l = 0; l < kWStreams; ++l) ANR_TRY(order(ss, s, ss->sw[l]));
     return ANR_OK;
@@ -241,19 +304,33 @@ struct Exec {
   // bf: BF_A (dY bf16), BF_X (X bf16)
   int wgrad(float* dW, int in_ch, int c0, int Nout, const float* dY, int ldY, const float* X, int ldX, int K,
             float* bsum = nullptr, float* bsum2 = nullptr, int want_lane = -1, unsigned bf = 0) {
-    hipStream_t w;
-    int lane;
-    ANR_TRY(wstream(&w, &lane, want_lane));
     if (grid_n() <= 0) return ANR_OK;
-    if ((bf16 || x3) && wslab && Nout <= 256 && K <= 256 && ldY % 4 == 0 && ldX % 4 == 0 && ((uintptr_t)dY & 15) == 0 &&
-        ((uintptr_t)X & 15) == 0 && !(x3 && bf)) {
-      WGrad wg{};
+    const bool fast = (bf16 || x3) && wslab && Nout <= 256 && K <= 256 && ldY % 4 == 0 && ldX % 4 == 0 &&
+                      ((uintptr_t)dY & 15) == 0 && ((uintptr_t)X & 15) == 0 && !(x3 && bf);
+    WGrad wg{};
+    if (fast) {
       wg.x3 = bf16 ? 0 : 1;
       wg.ybf = (bf & BF_A) != 0;
       wg.xbf = (bf & BF_X) != 0;
       wg.dY = dY; wg.ldY = ldY; wg.nout = Nout; wg.X = X; wg.ldX = ldX; wg.K = K;
-      wg.dW = dW + c0; wg.ldw = in_ch; wg.bsum = bsum; wg.bsum2 = bsum2; wg.slab = slab(lane);
+      wg.dW = dW + c0; wg.ldw = in_ch; wg.bsum = bsum; wg.bsum2 = bsum2;
       wg.M_dev = n_dev;
+    }
+    if (fast && group) {
+      if (npend == WG_GROUP_MAX || (flush_every > 0 && npend >= flush_every)) ANR_TRY(flush_w());
+      if (pend_src[0] != s && pend_src[1] != s) {
+        if (pend_src[0] && pend_src[1]) ANR_TRY(flush_w());
+        pend_src[pend_src[0] ? 1 : 0] = s;
+      }
+      pend[npend++] = wg;
+      ++nqueued;
+      return ANR_OK;
+    }
+    hipStream_t w;
+    int lane;
+    ANR_TRY(wstream(&w, &lane, want_lane));
+    if (fast) {
+      wg.slab = slab(lane);
       if (launch_wgrad(wg, grid_n(), w) != 0) return check_launch("k_wgrad");
       return ANR_OK;
     }
@@ -332,9 +409,17 @@ struct OnStream {
 
 // bf16 weight images for the row GEMM (bf16 policies only; refreshed on every call, the weights may
 // have changed since the last)
-int pack_images(Exec& e, const anr_params* p, char* dst, hipStream_t s, float* wslab, bool novel = false) {
+int pack_images(Exec& e, const anr_params* p, char* dst, hipStream_t s, float* wslab, size_t lane_floats,
+                bool novel = false) {
   if (!e.bf16) return ANR_OK;
   e.wslab = wslab;
+  e.lane_floats = lane_floats;
+  const char* gv = getenv("ANR_WG_GROUP");
+  e.group = !(gv && gv[0] == '0');
+  const char* nz = getenv("ANR_WG_GROUP_NZ");
+  if (nz && atoi(nz) > 0) e.group_nz = atoi(nz);
+  const char* fe = getenv("ANR_WG_FLUSH_EVERY");
+  if (fe) e.flush_every = atoi(fe);
   for (int i = 0; i < ANR_NUM_TENSORS; ++i) e.pt[i] = p->t[i];
   for (int i = 0; i < ANR_NUM_NOVEL_TENSORS; ++i) e.pt[ANR_NUM_TENSORS + i] = novel ? p->novel[i] : nullptr;
   if (wimg_pack(e.pt, dst, s) != 0) return check_launch("k_wimg_pack");
@@ -438,15 +523,9 @@ struct BwBackward {
     if (l == 0 || l == 5) {
       if (g) {
         float* ys = ysum + (l == 5 ? 256 : 0);
-        hipStream_t w;
-        int lane;
-        ANR_TRY(e.wstream(&w, &lane, 0));
-        if (hipMemsetAsync(ys, 0, 256 * 4, w) != hipSuccess) return fail(ANR_E_HIP, "memset");
         // bias grad and the latent-row gradient's column sum, in the weight-gradient pass
-        ANR_TRY(e.wgrad(g[wi], in_ch, 0, 256, cur, 256, G, 64, 63, g[bi], ys, 0, hb & (BF_A | BF_X)));
-        hipLaunchKernelGGL(k_tr_latent_grad, dim3(256 + 128), dim3(128), 0, w, (const float*)ys, W[wi], in_ch, 63, 256,
-                           W[0], li, add, g[wi], g[0]);
-        ANR_TRY(check_launch("k_tr_latent_grad"));
+        ANR_TRY(e.latent_rows(ys, g[wi], in_ch, 0, 256, cur, 256, G, 64, 63, g[bi], hb & (BF_A | BF_X),
+                              Exec::LatentPost{ys, W[wi], in_ch, 63, 256, W[0], li, add, g[wi], g[0]}));
       }
       if (dG)
         ANR_TRY(e.xgrad(dG, 64, 63, cur, 256, 256, W[wi], in_ch, 0, nullptr, 0, !(dG_fresh && l == 5), nullptr, 0, 0,
@@ -463,6 +542,8 @@ struct BwBackward {
                       nullptr, 0, hb & (BF_A | BF_C | BF_M)));
     }
     --l;
+    // ping-pong gradient rows are overwritten two layers on: their queued products run now
+    if (!dstride) ANR_TRY(e.flush_w());
     return ANR_OK;
   }
 };
@@ -610,14 +691,8 @@ int train_backward(const anr_params* p, float* const* g, const anr_frame* f, con
                   hb & BF_C));
   {
     float* ys = ysum + 512;
-    hipStream_t w;
-    int lane;
-    ANR_TRY(e.wstream(&w, &lane, 0));
-    if (hipMemsetAsync(ys, 0, 256 * 4, w) != hipSuccess) return fail(ANR_E_HIP, "memset");
-    ANR_TRY(e.wgrad(g[21], 384, 0, 256, dLat, 256, Feat, 256, 256, g[22], ys, 0, hb & (BF_A | BF_X)));
-    hipLaunchKernelGGL(k_tr_latent_grad, dim3(256 + 128), dim3(128), 0, w, (const float*)ys, PT(21), 384, 256, 256, PT(0),
-                       f->latent_index, 0, g[21], g[0]);
-    ANR_TRY(check_launch("k_tr_latent_grad(nf_latent)"));
+    ANR_TRY(e.latent_rows(ys, g[21], 384, 0, 256, dLat, 256, Feat, 256, 256, g[22], hb & (BF_A | BF_X),
+                          Exec::LatentPost{ys, PT(21), 384, 256, 256, PT(0), f->latent_index, 0, g[21], g[0]}));
   }
   ANR_TRY(e.xgrad(dFeat, 256, 256, dLat, 256, 256, PT(21), 384, 0, nullptr, 0, false, nullptr, 0, 0, nullptr, 0,
                   hb & (BF_A | BF_C)));
@@ -819,7 +894,7 @@ int anr_train_fwd(const anr_params* p, const anr_frame* f, const float* ray_o, c
   Exec e{s, 0, (o->precision == ANR_BF16 || o->precision == ANR_BF16_ALL) ? 1 : 0, o->precision == ANR_BF16 ? 1 : 0};
   e.ss = side_streams();
   e.hb = e.bf16;
-  ANR_TRY(pack_images(e, p, ws + T.wimg, s, (float*)(ws + T.wslab)));
+  ANR_TRY(pack_images(e, p, ws + T.wimg, s, (float*)(ws + T.wslab), kLaneFloats));
   ANR_TRY(train_forward(p, f, ray_o, ray_d, near_, far_, n_rays, o, out, ws, T, s, e));
   if (out->raw &&
       hipMemcpyAsync(out->raw, ws + T.L.raw, (size_t)n_rays * 64 * 16, hipMemcpyDeviceToDevice, s) != hipSuccess)
@@ -843,7 +918,7 @@ int anr_train_bwd(const anr_params* p, float* const* grads, const anr_frame* f, 
   Exec e{s, 0, (o->precision == ANR_BF16 || o->precision == ANR_BF16_ALL) ? 1 : 0, o->precision == ANR_BF16 ? 1 : 0};
   e.ss = side_streams();
   e.hb = e.bf16;
-  ANR_TRY(pack_images(e, p, ws + T.wimg, s, (float*)(ws + T.wslab)));
+  ANR_TRY(pack_images(e, p, ws + T.wimg, s, (float*)(ws + T.wslab), kLaneFloats));
   ANR_TRY(train_backward(p, grads, f, ray_o, ray_d, near_, far_, n_rays, o, d_rgb_map, d_pbw, d_tbw, ws, T, s, e));
   // pose BW MLP backward: d logits were produced by k_tr_softmax_bwd_p
   const long N = (long)n_rays * 64;
@@ -875,7 +950,7 @@ int train_step_body(const anr_params* p, float* const* grads, const anr_frame* f
   Exec e{s, 0, (o->precision == ANR_BF16 || o->precision == ANR_BF16_ALL) ? 1 : 0, o->precision == ANR_BF16 ? 1 : 0};
   e.ss = ss;
   e.hb = e.bf16;
-  ANR_TRY(pack_images(e, p, ws + T.wimg, s, (float*)(ws + T.wslab)));
+  ANR_TRY(pack_images(e, p, ws + T.wimg, s, (float*)(ws + T.wslab), kLaneFloats));
   ANR_TRY(train_forward(p, f, ray_o, ray_d, near_, far_, n_rays, o, out, ws, T, s, e, nullptr, split));
   // fused losses (tpose_trainer.py:50-63) and their upstream gradients
   TrainBufs b = bufs(T, ws, f, ray_o, ray_d, near_, far_, n_rays, o);
@@ -1068,9 +1143,10 @@ int anr_anim_step(const anr_params* p, float* const* grads, const anr_frame* f, 
   hipLaunchKernelGGL(k_prep, dim3(prep_blocks(0, 0)), dim3(256), 0, s, pa);
   ANR_TRY(check_launch("k_prep(anim)"));
   Exec e{s, 0, (o->precision == ANR_BF16 || o->precision == ANR_BF16_ALL) ? 1 : 0, o->precision == ANR_BF16 ? 1 : 0};
-  ANR_TRY(pack_images(e, p, ws + T.wimg, s, (float*)(ws + T.wslab), true));
+  ANR_TRY(pack_images(e, p, ws + T.wimg, s, (float*)(ws + T.wslab), wgrad_slab_floats(), true));
   ANR_TRY(anim_path(p, grads, f, wpts, n_obs, true, o, ws, T, s, e));
   ANR_TRY(anim_path(p, grads, f, tpts, n_can, false, o, ws, T, s, e));
+  ANR_TRY(e.flush_w());
   hipLaunchKernelGGL(k_an_loss_final, dim3(1), dim3(1), 0, s, (const float*)(ws + T.acc),
                      (const int*)(ws + T.counts) + 1, loss3);
   return check_launch("k_an_loss_final");
@@ -1111,7 +1187,7 @@ int anr_network_train_fwd(const anr_params* p, const anr_frame* f, const anr_sam
   Exec e{s, 0, (o->precision == ANR_BF16 || o->precision == ANR_BF16_ALL) ? 1 : 0, o->precision == ANR_BF16 ? 1 : 0};
   e.ss = side_streams();
   e.hb = e.bf16;
-  ANR_TRY(pack_images(e, p, ws + T.wimg, s, (float*)(ws + T.wslab)));
+  ANR_TRY(pack_images(e, p, ws + T.wimg, s, (float*)(ws + T.wslab), kLaneFloats));
   ANR_TRY(train_forward(p, f, nullptr, nullptr, nullptr, nullptr, G, &oo, nullptr, ws, T, s, e, x));
   if (hipMemcpyAsync(raw, ws + T.L.raw, (size_t)x->n_pts * 16, hipMemcpyDeviceToDevice, s) != hipSuccess)
     return fail(ANR_E_HIP, "anr_network_train_fwd: raw copy failed");
@@ -1138,7 +1214,7 @@ int anr_network_train_bwd(const anr_params* p, float* const* grads, const anr_fr
   Exec e{s, 0, (o->precision == ANR_BF16 || o->precision == ANR_BF16_ALL) ? 1 : 0, o->precision == ANR_BF16 ? 1 : 0};
   e.ss = side_streams();
   e.hb = e.bf16;
-  ANR_TRY(pack_images(e, p, ws + T.wimg, s, (float*)(ws + T.wslab)));
+  ANR_TRY(pack_images(e, p, ws + T.wimg, s, (float*)(ws + T.wslab), kLaneFloats));
   ANR_TRY(train_backward(p, grads, f, nullptr, nullptr, nullptr, nullptr, G, &oo, nullptr, d_pbw, d_tbw, ws, T, s, e, x,
                          d_raw));
   const long N = (long)G * 64;

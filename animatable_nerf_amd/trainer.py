@@ -122,6 +122,8 @@ class FusedStep:
             self._reduce_cb = _lib.REDUCE_FN()
         self._st = None  # fixed input / output buffers of the step (see _static_call)
         self._calls = {}  # direct calls per distinct batch (see _direct_call)
+        self._p = self._gp = None  # parameter / gradient pointer tables (views of flat / grad: fixed)
+        self._ws_bytes, self._hooks = {}, {}
         self._trand = None
         self.nerf_ready = None
         if dev.type == 'cuda':
@@ -276,14 +278,29 @@ class FusedStep:
             c, rgb, mask = self._static_call(batch, t_rand)
         else:
             c, rgb, mask = self._direct_call(batch, t_rand)
-        p = r.params(pack=False)
-        ws_bytes = self.lib.anr_train_workspace_bytes(R, ctypes.byref(c.opts), ctypes.byref(c.frame))
+        # per-step host work kept small (the step issues ~175 launches; its Python side ran ~0.2 ms):
+        # the parameter and gradient pointer tables are views into this step's flat blobs, built once
+        if self._p is None:
+            self._p = r.params(pack=False)
+            self._gp = (ctypes.c_void_p * _lib.NUM_TENSORS)(*[g.data_ptr() for g in self.grad_views])
+        p, gp = self._p, self._gp
+        fr = c.frame  # the workspace depends on the ray count, the chunk and the volume dims only
+        wkey = (R, int(c.opts.chunk), tuple(fr.pbw_dims), tuple(fr.tbw_dims))
+        ws_bytes = self._ws_bytes.get(wkey)
+        if ws_bytes is None:
+            ws_bytes = self.lib.anr_train_workspace_bytes(R, ctypes.byref(c.opts), ctypes.byref(c.frame))
+            if len(self._ws_bytes) > 64:
+                self._ws_bytes.clear()
+            self._ws_bytes[wkey] = ws_bytes
         ws = r._workspace('_tws', ws_bytes, dev)
         self.grad.zero_()
-        gp = (ctypes.c_void_p * _lib.NUM_TENSORS)(*[g.data_ptr() for g in self.grad_views])
         stream = _lib.stream_ptr(dev)
         overlap = is_dist() and self.nerf_ready is not None
-        hooks = _lib.TrainHooks(self.nerf_ready.cuda_event if overlap else None, ray_offset, self._reduce_cb, None)
+        hkey = (overlap, ray_offset)
+        hooks = self._hooks.get(hkey)
+        if hooks is None:
+            hooks = self._hooks[hkey] = _lib.TrainHooks(self.nerf_ready.cuda_event if overlap else None, ray_offset,
+                                                        self._reduce_cb, None)
         self._ws_now = ws
         _lib.check(self.lib.anr_train_step_hooked(ctypes.byref(p), gp, ctypes.byref(c.frame), *c.ray_ptrs(), R,
                                                   ctypes.byref(c.opts), _lib.ptr(rgb), _lib.ptr(mask),

@@ -19,12 +19,14 @@
 #   probecnt:KERNEL:C1+C2[:ARGS]  one --pmc pass over the probe, KERNEL's dispatches -> TAG_pcnt_KERNEL/
 #   counters:KERNEL:C1+C2+..[:ARGS]  one --pmc pass with the given counters (<= the per-block limits)
 #                     over one bench step                              -> TAG_cnt_KERNEL/
+#   env:VAR=VALUE     export VAR for the steps after it; bench / prof / trace logs get _VAR-VALUE
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 TAG=$1
 shift
 mkdir -p gpurun_out
+SFX=""
 args_of() { echo "$1" | tr ',' ' '; }
 # log-name suffix: _MODE, then the other flags (steps / warmup left out), e.g. _train_precision-fp32
 mode_of() {
@@ -55,11 +57,11 @@ for step in "$@"; do
         || { rc=$?; tail -20 gpurun_out/${TAG}_smoke.log; exit $rc; }
       tail -2 gpurun_out/${TAG}_smoke.log ;;
     bench)
-      log=gpurun_out/${TAG}_bench$(mode_of "$rest").log
+      log=gpurun_out/${TAG}_bench$(mode_of "$rest")$SFX.log
       timeout -k 10 600 python bench.py $(args_of "$rest") > $log 2>&1 || { rc=$?; tail -20 $log; exit $rc; }
       tail -n 1 $log | cut -c1-600 ;;
     prof)
-      m=$(mode_of "$rest")
+      m=$(mode_of "$rest")$SFX
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof$m -o run --output-format csv -- \
         python bench.py --no-cpu --no-torch-baseline $(args_of "$rest") > gpurun_out/${TAG}_prof$m.log 2>&1 \
         || { rc=$?; tail -20 gpurun_out/${TAG}_prof$m.log; exit $rc; }
@@ -104,7 +106,7 @@ for step in "$@"; do
       ANR_LIB_PATH=$PWD/ab/$lib.so timeout -k 10 600 python bench.py $(args_of "$a") > $log 2>&1 || { rc=$?; tail -20 $log; exit $rc; }
       tail -n 1 $log | cut -c1-400 ;;
     trace)
-      m=$(mode_of "$rest")
+      m=$(mode_of "$rest")$SFX
       timeout -k 10 600 rocprofv3 --kernel-trace -d gpurun_out/${TAG}_trace$m -o run --output-format csv -- \
         python bench.py --no-cpu --no-torch-baseline $(args_of "$rest") > gpurun_out/${TAG}_trace$m.log 2>&1 \
         || { rc=$?; tail -20 gpurun_out/${TAG}_trace$m.log; exit $rc; }
@@ -140,6 +142,10 @@ for step in "$@"; do
       timeout -s KILL 180 rocprofv3 --pmc ${cs//+/ } --kernel-include-regex "$k" -d gpurun_out/${TAG}_cnt_$k -o p \
         --output-format csv -- $B > gpurun_out/${TAG}_cnt_$k.log 2>&1 || { rc=$?; tail -20 gpurun_out/${TAG}_cnt_$k.log; exit $rc; }
       echo "COUNTERS_OK $k" ;;
+    env)
+      export "$rest"
+      SFX="${SFX}_${rest//=/-}"
+      echo "ENV $rest" ;;
     *)
       echo "unknown step $step"; exit 2 ;;
   esac
