@@ -515,9 +515,9 @@ struct LgImage {
 // three-way split (anr_tgemm.hip k_rgemm X6, ~2^-24 relative per product) on a hi / mid / lo weight
 // image packed into the same arena once per call and weight view
 struct RgImage {
-  const float *B0, *B1;
-  long c0, c1;
-  int K0, K1, N;
+  const float* B[2];
+  long rs[2], cs[2];
+  int K[2], N, nseg;
   const unsigned short* img;
   long ldb;
 };
@@ -555,8 +555,8 @@ struct TG {
     return img;
   }
   // the row GEMM takes the product: k-contiguous fp32 activations (16-B rows, lda >= K rounded to the
-  // 32-deep chunk), W k-contiguous (b_rs == 1), 64 <= N <= 256, epilogues bias / ReLU / softplus (+
-  // derivative rows) / mask / accumulate / div_post
+  // 32-deep chunk), 64 <= N <= 256, epilogues bias / ReLU / softplus (+ derivative rows) / mask /
+  // accumulate / div_post; B any layout (packed into the image)
   bool rg_ok(const GemmArgs& g) const {
     if (!lg_arena || g.N < 64 || g.N > 256 || g.nseg < 1 || g.nseg > 2 || g.atomic || g.ksplit > 1 || g.K_dev ||
         g.M_dev || g.div_pre != 0.f || g.spd || g.rowsum || g.rowsum2 || g.a_softplus_w || g.head_w || g.bf16 ||
@@ -565,34 +565,33 @@ struct TG {
     if (g.mask && (g.ldm % 4 || ((uintptr_t)g.mask & 15))) return false;
     for (int q = 0; q < g.nseg; ++q) {
       const GemmSeg& a = g.seg[q];
-      if (a.a_cs != 1 || a.a_rs % 4 || ((uintptr_t)a.A & 15) || a.a_rs < (a.K + 31) / 32 * 32 || a.b_rs != 1) return false;
-      if (q == 1 && a.b_cs != g.seg[0].b_cs) return false;
+      if (a.a_cs != 1 || a.a_rs % 4 || ((uintptr_t)a.A & 15) || a.a_rs < (a.K + 31) / 32 * 32) return false;
     }
     return true;
   }
   const RgImage* rg_image(const GemmArgs& g) {
-    const GemmSeg& a = g.seg[0];
-    const bool two = g.nseg > 1;
-    // W row-major [N][in_ch] seen through the segment views B = W + c0 (b_cs = in_ch): key on W's own
-    // address per segment (the views of one W share b_cs)
     for (int i = 0; i < nrg; ++i) {
       const RgImage& q = rg[i];
-      if (q.B0 == a.B && q.K0 == a.K && q.N == g.N && q.c0 == a.b_cs && q.B1 == (two ? g.seg[1].B : nullptr) &&
-          (!two || q.K1 == g.seg[1].K))
-        return &q;
+      bool same = q.N == g.N && q.nseg == g.nseg;
+      for (int k = 0; same && k < g.nseg; ++k)
+        same = q.B[k] == g.seg[k].B && q.rs[k] == g.seg[k].b_rs && q.cs[k] == g.seg[k].b_cs && q.K[k] == g.seg[k].K;
+      if (same) return &q;
     }
     if (nrg >= 64) return nullptr;
-    // both segments index one W: the segment views B_s = W + c0_s with W = B_0 - c0_0; the pack
-    // kernel reads W[n * ldw + c0_s + k], so it takes B_0 as the base and c0 offsets relative to it
-    const int K[2] = {a.K, two ? g.seg[1].K : 0};
-    const int c0[2] = {0, two ? (int)(g.seg[1].B - a.B) : 0};
-    const size_t bytes = ((size_t)rimg_x6_elems(g.N, g.nseg, K) * 2 + 255) / 256 * 256;
+    RgImage q{};
+    q.N = g.N;
+    q.nseg = g.nseg;
+    for (int k = 0; k < g.nseg; ++k) {
+      q.B[k] = g.seg[k].B; q.rs[k] = g.seg[k].b_rs; q.cs[k] = g.seg[k].b_cs; q.K[k] = g.seg[k].K;
+    }
+    const size_t bytes = ((size_t)rimg_x6_elems(g.N, g.nseg, q.K) * 2 + 255) / 256 * 256;
     if (lg_used + bytes > lg_cap) return nullptr;
     unsigned short* img = (unsigned short*)(lg_arena + lg_used);
-    if (rimg_x6_pack(a.B, a.b_cs, g.N, g.nseg, c0, K, img, s) != 0) return nullptr;
+    if (rimg_x6_pack(g.N, g.nseg, q.B, q.rs, q.cs, q.K, img, s) != 0) return nullptr;
     lg_used += bytes;
-    rg[nrg] = RgImage{a.B, two ? g.seg[1].B : nullptr, a.b_cs, two ? g.seg[1].b_cs : 0, a.K, K[1], g.N, img,
-                      rimg_x6_ldb(g.nseg, K)};
+    q.img = img;
+    q.ldb = rimg_x6_ldb(g.nseg, q.K);
+    rg[nrg] = q;
     return &rg[nrg++];
   }
   int run_x6(const GemmArgs& g, int M, const RgImage* im) {

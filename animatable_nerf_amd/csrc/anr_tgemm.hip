@@ -626,9 +626,9 @@ long rimg_x6_ldb(int nseg, const int* K) {
 long rimg_x6_elems(int N, int nseg, const int* K) { return 3L * N * rimg_x6_ldb(nseg, K); }
 
 struct RPackX6 {
-  const float* W;
-  long ldw, ldb, plane;
-  int N, nseg, c0[2], K[2], col[2];
+  const float* B[2];
+  long rs[2], cs[2], ldb, plane;
+  int N, nseg, K[2], col[2];
   unsigned short* out;
 };
 
@@ -639,7 +639,7 @@ __global__ void k_rimg_x6_pack(RPackX6 a) {
   const int n = (int)(e / a.ldb), col = (int)(e - (long)n * a.ldb);
   float v = 0.f;
   for (int s = 0; s < a.nseg; ++s)
-    if (col >= a.col[s] && col < a.col[s] + a.K[s]) v = a.W[(long)n * a.ldw + a.c0[s] + col - a.col[s]];
+    if (col >= a.col[s] && col < a.col[s] + a.K[s]) v = a.B[s][(long)(col - a.col[s]) * a.rs[s] + (long)n * a.cs[s]];
   const unsigned short hi = f2bf_rne(v);
   const float r1 = v - __uint_as_float((uint32_t)hi << 16);
   const unsigned short mid = f2bf_rne(r1);
@@ -648,13 +648,14 @@ __global__ void k_rimg_x6_pack(RPackX6 a) {
   a.out[2 * a.plane + e] = f2bf_rne(r1 - __uint_as_float((uint32_t)mid << 16));
 }
 
-int rimg_x6_pack(const float* W, long ldw, int N, int nseg, const int* c0, const int* K, unsigned short* dst, hipStream_t s) {
+int rimg_x6_pack(int N, int nseg, const float* const* B, const long* b_rs, const long* b_cs, const int* K,
+                 unsigned short* dst, hipStream_t s) {
   if (nseg < 1 || nseg > 2 || N <= 0) return -1;
   RPackX6 a{};
-  a.W = W; a.ldw = ldw; a.N = N; a.nseg = nseg; a.out = dst;
+  a.N = N; a.nseg = nseg; a.out = dst;
   long col = 0;
   for (int q = 0; q < nseg; ++q) {
-    a.c0[q] = c0[q]; a.K[q] = K[q]; a.col[q] = (int)col;
+    a.B[q] = B[q]; a.rs[q] = b_rs[q]; a.cs[q] = b_cs[q]; a.K[q] = K[q]; a.col[q] = (int)col;
     col += rup64(K[q]);
   }
   a.ldb = col;

@@ -107,12 +107,13 @@ struct RGemm {
   int abf, cbf, mbf;
 };
 void launch_rgemm(const RGemm& g, int M_host, hipStream_t s);
-// x6 weight image of W (row-major [N][ldw]) for the row GEMM: rows n < N, the nseg column segments
-// [c0_s, c0_s + K_s) of W each padded to 64 (image columns col_s), planes hi / mid / lo of N x ldb
-// bf16 elements each (plane stride N * ldb); rimg_x6_elems() elements in all
+// x6 image of a GEMM's B operand for the row GEMM: image[n][col_s + k] = B_s[k * b_rs_s + n * b_cs_s]
+// (k < K_s, n < N; a layer's W for the forward, its transpose for the input gradient), segments
+// padded to 64 columns, planes hi / mid / lo of N x ldb bf16 elements each (plane stride N * ldb)
 long rimg_x6_ldb(int nseg, const int* K);
 long rimg_x6_elems(int N, int nseg, const int* K);
-int rimg_x6_pack(const float* W, long ldw, int N, int nseg, const int* c0, const int* K, unsigned short* dst, hipStream_t s);
+int rimg_x6_pack(int N, int nseg, const float* const* B, const long* b_rs, const long* b_cs, const int* K,
+                 unsigned short* dst, hipStream_t s);
 // bf16 weight images of the training GEMM weights: forward (rows = outputs, k = used input columns,
 // segments padded to 64) and backward (rows = input columns, k = outputs padded to 64). t: the
 // ANR_NUM_TENSORS network tensors followed by the ANR_NUM_NOVEL_TENSORS novel_pose_bw tensors
