@@ -648,10 +648,11 @@ struct TG {
   int wgrad(int M, float* dW, int in_ch, int c0, int Nout, const float* dY, long ldY, const float* X, long ldX, int K,
             float* bsum = nullptr) {
     if (M <= 0) return ANR_OK;
-    if (wg_x3 && slab && Nout <= 256 && K <= 256 && ldY % 4 == 0 && ldX % 4 == 0 && ((uintptr_t)dY & 15) == 0 &&
+    if ((wg_x3 || x6) && slab && Nout <= 256 && K <= 256 && ldY % 4 == 0 && ldX % 4 == 0 && ((uintptr_t)dY & 15) == 0 &&
         ((uintptr_t)X & 15) == 0) {
       WGrad w{};
       w.x3 = 1;
+      w.x6 = wg_x3 ? 0 : 1;  // the fp32-level parts: three-way split unless their weight gradients run split-bf16
       w.dY = dY; w.ldY = ldY; w.nout = Nout; w.X = X; w.ldX = ldX; w.K = K;
       w.dW = dW + c0; w.ldw = in_ch; w.bsum = bsum; w.slab = slab;
       if (launch_wgrad(w, M, s) != 0) return check_launch("k_wgrad (sdf train)");

@@ -698,21 +698,26 @@ __device__ __forceinline__ bf16x8_t wg_frag(const unsigned short* S, int cb, int
   return f;
 }
 
-// X3: also the lo image (x - hi) into SL
-template <bool X3>
-__device__ __forceinline__ void wg_store(unsigned short* S, unsigned short* SL, int tid, const f32x4 (&v)[4]) {
+// X3: also the lo image (x - hi) into SL. X6: x = hi + mid + lo, mid into SL and lo into SL2
+template <bool X3, bool X6 = false>
+__device__ __forceinline__ void wg_store(unsigned short* S, unsigned short* SL, int tid, const f32x4 (&v)[4],
+                                         unsigned short* SL2 = nullptr) {
 #pragma unroll
   for (int h = 0; h < 4; ++h) {
     const int row = 8 * h + (tid >> 5), col = 4 * (tid & 31);
-    unsigned short e[4], l[4];
+    unsigned short e[4], l[4], q[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       e[k] = f2bf_rne(v[h][k]);
-      if constexpr (X3) l[k] = f2bf_rne(v[h][k] - __uint_as_float((uint32_t)e[k] << 16));
+      const float r1 = v[h][k] - __uint_as_float((uint32_t)e[k] << 16);
+      if constexpr (X3) l[k] = f2bf_rne(r1);
+      if constexpr (X6) q[k] = f2bf_rne(r1 - __uint_as_float((uint32_t)l[k] << 16));
     }
     *(uint2*)(S + row * WG_LD + col) = make_uint2((uint32_t)e[0] | ((uint32_t)e[1] << 16), (uint32_t)e[2] | ((uint32_t)e[3] << 16));
     if constexpr (X3)
       *(uint2*)(SL + row * WG_LD + col) = make_uint2((uint32_t)l[0] | ((uint32_t)l[1] << 16), (uint32_t)l[2] | ((uint32_t)l[3] << 16));
+    if constexpr (X6)
+      *(uint2*)(SL2 + row * WG_LD + col) = make_uint2((uint32_t)q[0] | ((uint32_t)q[1] << 16), (uint32_t)q[2] | ((uint32_t)q[3] << 16));
   }
 }
 
@@ -784,16 +789,21 @@ __device__ __forceinline__ void wg_put_bf(unsigned short* S, const uint2 (&r)[4]
 
 // the LDS of one weight-gradient workgroup: per buffer two 32-sample images (hi and lo under X3, two
 // sample halves otherwise), double-buffered, and the column-sum exchange
-struct WgLds {
-  unsigned short sY[2][2 * WG_S * WG_LD];
-  unsigned short sX[2][2 * WG_S * WG_LD];
+template <int NIMG>
+struct WgLdsT {
+  unsigned short sY[2][NIMG * WG_S * WG_LD];
+  unsigned short sX[2][NIMG * WG_S * WG_LD];
   float srs[8][WG_T];
 };
+typedef WgLdsT<2> WgLds;
 
-// one (output tile, sample range) of dW: (ti, tj) the 128 x 128 tile of dW, z the sample range
-template <bool X3, bool YBF, bool XBF>
-__device__ __forceinline__ void wgrad_tile(const WGrad& g, int ti, int tj, int z, WgLds& sm) {
-  constexpr int D = WG_D;
+// one (output tile, sample range) of dW: (ti, tj) the 128 x 128 tile of dW, z the sample range.
+// X6 (with X3 set; the sdf training's fp32-level parts): hi / mid / lo images of both operands (three
+// per buffer, WgLdsT<3>), six MFMAs per fragment pair, loads two steps ahead (registers)
+template <bool X3, bool YBF, bool XBF, bool X6 = false, class L = WgLds>
+__device__ __forceinline__ void wgrad_tile(const WGrad& g, int ti, int tj, int z, L& sm) {
+  static_assert(!X6 || X3, "X6 runs on the X3 layout");
+  constexpr int D = X6 ? 2 : WG_D;
   constexpr int NI = X3 ? 2 : 1;
   constexpr int NH = X3 ? 1 : 2;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -848,35 +858,44 @@ __device__ __forceinline__ void wgrad_tile(const WGrad& g, int ti, int tj, int z
 #pragma unroll
             for (int q = 0; q < 4; ++q) rsum += vy[q];
           }
-          wg_store<X3>((sm.sY[buf] + h * WG_S * WG_LD), (sm.sY[buf] + (NI - 1 + h) * WG_S * WG_LD), tid, vy);
+          wg_store<X3, X6>((sm.sY[buf] + h * WG_S * WG_LD), (sm.sY[buf] + (NI - 1 + h) * WG_S * WG_LD), tid, vy,
+                           sm.sY[buf] + 2 * WG_S * WG_LD);
         }
         if constexpr (XBF) {
           wg_put_bf((sm.sX[buf] + h * WG_S * WG_LD), rx[d][h], g.K, j0, s + h * WG_S, s1, tid);
         } else {
           f32x4 vx[4];
           wg_widen<false>(rx[d][h], g.K, j0, s + h * WG_S, s1, tid, vx);
-          wg_store<X3>((sm.sX[buf] + h * WG_S * WG_LD), (sm.sX[buf] + (NI - 1 + h) * WG_S * WG_LD), tid, vx);
+          wg_store<X3, X6>((sm.sX[buf] + h * WG_S * WG_LD), (sm.sX[buf] + (NI - 1 + h) * WG_S * WG_LD), tid, vx,
+                           sm.sX[buf] + 2 * WG_S * WG_LD);
         }
       }
       __syncthreads();
       if (s + D * STEP < s1) load(d, s + D * STEP);  // this ring entry is free again: refill D steps ahead
 #pragma unroll
       for (int h = 0; h < NH; ++h) {
-        bf16x8_t fa[4], fb[4], la[4], lb[4];
+        bf16x8_t fa[4], fb[4], la[4], lb[4], qa[4], qb[4];  // X6: la / lb the mid parts, qa / qb the lo parts
 #pragma unroll
         for (int a = 0; a < 4; ++a) {
           fa[a] = wg_frag((sm.sY[buf] + h * WG_S * WG_LD), wi + 16 * a, lane);
           if constexpr (X3) la[a] = wg_frag((sm.sY[buf] + (NI - 1 + h) * WG_S * WG_LD), wi + 16 * a, lane);
+          if constexpr (X6) qa[a] = wg_frag((sm.sY[buf] + 2 * WG_S * WG_LD), wi + 16 * a, lane);
         }
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
           fb[b] = wg_frag((sm.sX[buf] + h * WG_S * WG_LD), wj + 16 * b, lane);
           if constexpr (X3) lb[b] = wg_frag((sm.sX[buf] + (NI - 1 + h) * WG_S * WG_LD), wj + 16 * b, lane);
+          if constexpr (X6) qb[b] = wg_frag((sm.sX[buf] + 2 * WG_S * WG_LD), wj + 16 * b, lane);
         }
 #pragma unroll
         for (int a = 0; a < 4; ++a)
 #pragma unroll
           for (int b = 0; b < 4; ++b) {
+            if constexpr (X6) {  // the 2^-16 terms, then the 2^-8 ones
+              acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa[a], fb[b], acc[a][b], 0, 0, 0);
+              acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a], qb[b], acc[a][b], 0, 0, 0);
+              acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(la[a], lb[b], acc[a][b], 0, 0, 0);
+            }
             if constexpr (X3) {
               acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(la[a], fb[b], acc[a][b], 0, 0, 0);
               acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a], lb[b], acc[a][b], 0, 0, 0);
@@ -904,9 +923,9 @@ __device__ __forceinline__ void wgrad_tile(const WGrad& g, int ti, int tj, int z
   }
 }
 
-template <bool X3, bool YBF, bool XBF>
+template <bool X3, bool YBF, bool XBF, bool X6 = false>
 __global__ __launch_bounds__(256) void k_wgrad(WGrad g) {
-  __shared__ __attribute__((aligned(16))) WgLds sm;
+  __shared__ __attribute__((aligned(16))) WgLdsT<X6 ? 3 : 2> sm;
   // XCD-aware order: workgroups are dealt to the 8 XCDs round-robin by linear id, so the tiles of
   // one sample range (which read the same dY and X rows) get ids on one XCD and share its L2
   // (launch_wgrad makes the range count a multiple of 8)
@@ -914,7 +933,7 @@ __global__ __launch_bounds__(256) void k_wgrad(WGrad g) {
   const int L = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
   const int slot = L >> 3, tile = slot % tiles;
   const int z = (slot / tiles) * 8 + (L & 7);
-  wgrad_tile<X3, YBF, XBF>(g, tile % gridDim.x, tile / gridDim.x, z, sm);
+  wgrad_tile<X3, YBF, XBF, X6>(g, tile % gridDim.x, tile / gridDim.x, z, sm);
 }
 
 // several weight gradients of one operand format in one launch (the layers of an MLP's backward):
@@ -1013,7 +1032,8 @@ int launch_wgrad(WGrad g, int n_host, hipStream_t s) {
   g.n = n_host;
   g.rs_slab = (g.bsum || g.bsum2) ? g.slab + (size_t)WG_MAX_Z * 4 * WG_TILE_FLOATS : nullptr;
   const dim3 grid(ti, tj, g.nz);
-  if (g.x3) hipLaunchKernelGGL((k_wgrad<true, false, false>), grid, dim3(256), 0, s, g);
+  if (g.x6) hipLaunchKernelGGL((k_wgrad<true, false, false, true>), grid, dim3(256), 0, s, g);
+  else if (g.x3) hipLaunchKernelGGL((k_wgrad<true, false, false>), grid, dim3(256), 0, s, g);
   else if (g.ybf && g.xbf) hipLaunchKernelGGL((k_wgrad<false, true, true>), grid, dim3(256), 0, s, g);
   else if (g.ybf) hipLaunchKernelGGL((k_wgrad<false, true, false>), grid, dim3(256), 0, s, g);
   else if (g.xbf) hipLaunchKernelGGL((k_wgrad<false, false, true>), grid, dim3(256), 0, s, g);

@@ -151,6 +151,7 @@ struct WGrad {
   int spb, nz, tiles, tj;
   int x3;  // split-bf16 products (fp32-level)
   int ybf, xbf;  // dY / X rows hold bf16 (reinterpreted as unsigned short*), not with x3
+  int x6;        // three-way split products (fp32 level), launch_wgrad only (not in groups)
 };
 size_t wgrad_slab_floats();
 int launch_wgrad(WGrad g, int n_host, hipStream_t s);
