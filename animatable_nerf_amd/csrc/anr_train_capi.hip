@@ -97,6 +97,7 @@ int check_args(const anr_params* p, const anr_frame* f, const float* ray_o, cons
 // the library's own made the bf16 step 3.27 ms instead of 1.96 (one more queue than the hardware
 // queues the process gets), the weight-gradient lanes at the lowest priority changed nothing (1.945).
 struct SideStreams {
+  hipStream_t main = nullptr;  // the library's own main stream (OnMain)
   hipStream_t s2 = nullptr, sw[kWStreams] = {};
   hipStream_t cap = nullptr;  // origin stream of step-graph captures (created on first use)
   hipEvent_t ev[64] = {};
@@ -115,6 +116,7 @@ SideStreams* side_streams() {
   if (!ss.s2) {
     SideStreams t{};
     if (hipStreamCreateWithFlags(&t.s2, hipStreamNonBlocking) != hipSuccess) return nullptr;
+    if (hipStreamCreateWithFlags(&t.main, hipStreamNonBlocking) != hipSuccess) return nullptr;
     for (auto& w : t.sw)
       if (hipStreamCreateWithFlags(&w, hipStreamNonBlocking) != hipSuccess) return nullptr;
     for (auto& e : t.ev)
@@ -132,6 +134,27 @@ int order(SideStreams* ss, hipStream_t to, hipStream_t from) {
     return fail(ANR_E_HIP, "stream ordering failed");
   return ANR_OK;
 }
+
+// A training entry point runs on the library's own main stream, forked from the caller's stream on
+// entry and joined back into it on exit (also on an error return), so that every cross-stream
+// dependency inside the call is between the library's non-blocking streams. Measured: with the caller
+// on the legacy default stream, the grouped weight gradients of the blend-weight MLPs read gradient
+// rows that were not yet written (NaN from a previous run's workspace, tools/nan_probe.py), although
+// every event edge was in place; the same steps on a non-default caller stream were exact.
+struct OnMain {
+  SideStreams* ss;
+  hipStream_t caller, s;
+  int rc = ANR_OK;
+  OnMain(SideStreams* x, hipStream_t c) : ss(x), caller(c), s(c) {
+    if (ss && ss->main) {
+      rc = order(ss, ss->main, caller);
+      s = ss->main;
+    }
+  }
+  ~OnMain() {
+    if (s != caller) (void)order(ss, caller, s);
+  }
+};
 
 // storage flags of a product's operands (training precision 'bf16': hidden activations, their
 // gradients and the gamma inputs of the T-pose / canonical MLPs are kept as bf16 — every consumer
@@ -172,6 +195,10 @@ struct Exec {
   } post[8];
   int npost = 0;
   int nqueued = 0;  // products queued so far
+  const int dbg = [] {
+    const char* v = getenv("ANR_WG_DEBUG");
+    return v ? atoi(v) : 0;
+  }();
   // the kept-sample count stays on the device (no host read, so a step can be captured in a graph):
   // every launch is sized for the capacity `cap` and reads the count from n_dev
   const int* n_dev = nullptr;
@@ -193,9 +220,19 @@ struct Exec {
   int flush_w() {
     if (!npend && !npost) return ANR_OK;
     hipStream_t w = ss ? ss->sw[0] : s;
+    if ((dbg & 1) && ss) {  // debugging aid: the flush waits for both chain streams
+      ANR_TRY(order(ss, w, ss->s2));
+      if (ss->s2 != s) ANR_TRY(order(ss, w, s));
+    }
     for (int i = 0; i < 2 && pend_src[i]; ++i) ANR_TRY(order(ss, w, pend_src[i]));
+    if ((dbg & 4) && slab(0) && hipMemsetAsync(slab(0), 0, lane_floats * 4, w) != hipSuccess)  // debugging aid
+      return fail(ANR_E_HIP, "memset");
     if (npend && launch_wgrad_group(pend, npend, grid_n(), group_nz, slab(0), lane_floats, w) != 0)
       return check_launch("k_wgrad_group");
+    if ((dbg & 2) && ss) {  // debugging aid: both chain streams wait for the flush
+      ANR_TRY(order(ss, ss->s2, w));
+      if (ss->s2 != s) ANR_TRY(order(ss, s, w));
+    }
     for (int i = 0; i < npost; ++i) {
       const LatentPost& q = post[i];
       hipLaunchKernelGGL(k_tr_latent_grad, dim3(256 + 128), dim3(128), 0, w, q.ys, q.W, q.in_ch, q.c0, q.ncol, q.tab, q.li,
@@ -212,13 +249,14 @@ struct Exec {
                   int K, float* bsum, unsigned bf, const LatentPost& q) {
     hipStream_t w = s;
     int lane = 0;
-    if (!group) ANR_TRY(wstream(&w, &lane, 0));
+    if (!group || (dbg & 32)) ANR_TRY(wstream(&w, &lane, 0));
     if (hipMemsetAsync(ys, 0, 256 * 4, w) != hipSuccess) return fail(ANR_E_HIP, "memset");
     if (group && (npend == WG_GROUP_MAX || npost == 8)) ANR_TRY(flush_w());  // product and update in one flush
     const int q0 = nqueued;
     ANR_TRY(wgrad(dW, in_ch, c0, Nout, dY, ldY, X, ldX, K, bsum, ys, 0, bf));
     if (nqueued > q0) {
       post[npost++] = q;
+      if (dbg & 16) return flush_w();  // debugging aid: products with latent rows not deferred
       return ANR_OK;
     }
     if (group) ANR_TRY(wstream(&w, &lane, 0));  // off the fast path: the product ran on lane 0
@@ -543,7 +581,7 @@ struct BwBackward {
     }
     --l;
     // ping-pong gradient rows are overwritten two layers on: their queued products run now
-    if (!dstride) ANR_TRY(e.flush_w());
+    if (!dstride || (e.dbg & 8)) ANR_TRY(e.flush_w());
     return ANR_OK;
   }
 };
@@ -889,10 +927,12 @@ int anr_train_fwd(const anr_params* p, const anr_frame* f, const float* ray_o, c
   const long nt = (long)f->tbw_dims[0] * f->tbw_dims[1] * f->tbw_dims[2];
   const TLayout T = tlayout(n_rays, o->chunk, np, nt);
   if (ws_bytes < T.total) return fail(ANR_E_WORKSPACE, "anr_train_fwd: workspace too small");
-  hipStream_t s = (hipStream_t)stream;
+  OnMain om(side_streams(), (hipStream_t)stream);
+  ANR_TRY(om.rc);
+  hipStream_t s = om.s;
   char* ws = (char*)workspace;
   Exec e{s, 0, (o->precision == ANR_BF16 || o->precision == ANR_BF16_ALL) ? 1 : 0, o->precision == ANR_BF16 ? 1 : 0};
-  e.ss = side_streams();
+  e.ss = om.ss;
   e.hb = e.bf16;
   ANR_TRY(pack_images(e, p, ws + T.wimg, s, (float*)(ws + T.wslab), kLaneFloats));
   ANR_TRY(train_forward(p, f, ray_o, ray_d, near_, far_, n_rays, o, out, ws, T, s, e));
@@ -913,10 +953,12 @@ int anr_train_bwd(const anr_params* p, float* const* grads, const anr_frame* f, 
   const long nt = (long)f->tbw_dims[0] * f->tbw_dims[1] * f->tbw_dims[2];
   const TLayout T = tlayout(n_rays, o->chunk, np, nt);
   if (ws_bytes < T.total) return fail(ANR_E_WORKSPACE, "anr_train_bwd: workspace too small");
-  hipStream_t s = (hipStream_t)stream;
+  OnMain om(side_streams(), (hipStream_t)stream);
+  ANR_TRY(om.rc);
+  hipStream_t s = om.s;
   char* ws = (char*)workspace;
   Exec e{s, 0, (o->precision == ANR_BF16 || o->precision == ANR_BF16_ALL) ? 1 : 0, o->precision == ANR_BF16 ? 1 : 0};
-  e.ss = side_streams();
+  e.ss = om.ss;
   e.hb = e.bf16;
   ANR_TRY(pack_images(e, p, ws + T.wimg, s, (float*)(ws + T.wslab), kLaneFloats));
   ANR_TRY(train_backward(p, grads, f, ray_o, ray_d, near_, far_, n_rays, o, d_rgb_map, d_pbw, d_tbw, ws, T, s, e));
@@ -1043,9 +1085,13 @@ int anr_train_step_hooked(const anr_params* p, float* const* grads, const anr_fr
   // an external event (bucketed all-reduce) must be signalled by a plain record, and a ray split calls
   // its host hook mid-step: eager only
   const bool graphs = ss && !nerf_done && !splitting && gv && gv[0] == '1';
-  if (!graphs)
+  if (!graphs) {
+    // (a ray split's reduce hook is handed the main stream and issues its collectives there)
+    OnMain om(ss, s);
+    ANR_TRY(om.rc);
     return train_step_body(p, grads, f, ray_o, ray_d, near_, far_, n_rays, o, rgb_gt, mask_at_box, out, loss3,
-                           nerf_done, ws, T, s, ss, splitting ? &split : nullptr);
+                           nerf_done, ws, T, om.s, ss, splitting ? &split : nullptr);
+  }
   std::string key;
   int dev = 0;
   (void)hipGetDevice(&dev);
@@ -1071,8 +1117,10 @@ int anr_train_step_hooked(const anr_params* p, float* const* grads, const anr_fr
   if (seen == G.seen.end()) {
     G.seen.push_back(key);
     if (G.seen.size() > 64) G.seen.erase(G.seen.begin());
+    OnMain om(ss, s);
+    ANR_TRY(om.rc);
     return train_step_body(p, grads, f, ray_o, ray_d, near_, far_, n_rays, o, rgb_gt, mask_at_box, out, loss3,
-                           nullptr, ws, T, s, ss);
+                           nullptr, ws, T, om.s, ss);
   }
   G.seen.erase(seen);
   // second sighting: capture, instantiate, launch
@@ -1182,10 +1230,12 @@ int anr_network_train_fwd(const anr_params* p, const anr_frame* f, const anr_sam
   const long nt = (long)f->tbw_dims[0] * f->tbw_dims[1] * f->tbw_dims[2];
   const TLayout T = tlayout(G, G, np, nt);
   if (ws_bytes < T.total) return fail(ANR_E_WORKSPACE, "anr_network_train_fwd: workspace too small");
-  hipStream_t s = (hipStream_t)stream;
+  OnMain om(side_streams(), (hipStream_t)stream);
+  ANR_TRY(om.rc);
+  hipStream_t s = om.s;
   char* ws = (char*)workspace;
   Exec e{s, 0, (o->precision == ANR_BF16 || o->precision == ANR_BF16_ALL) ? 1 : 0, o->precision == ANR_BF16 ? 1 : 0};
-  e.ss = side_streams();
+  e.ss = om.ss;
   e.hb = e.bf16;
   ANR_TRY(pack_images(e, p, ws + T.wimg, s, (float*)(ws + T.wslab), kLaneFloats));
   ANR_TRY(train_forward(p, f, nullptr, nullptr, nullptr, nullptr, G, &oo, nullptr, ws, T, s, e, x));
@@ -1209,10 +1259,12 @@ int anr_network_train_bwd(const anr_params* p, float* const* grads, const anr_fr
   const long nt = (long)f->tbw_dims[0] * f->tbw_dims[1] * f->tbw_dims[2];
   const TLayout T = tlayout(G, G, np, nt);
   if (ws_bytes < T.total) return fail(ANR_E_WORKSPACE, "anr_network_train_bwd: workspace too small");
-  hipStream_t s = (hipStream_t)stream;
+  OnMain om(side_streams(), (hipStream_t)stream);
+  ANR_TRY(om.rc);
+  hipStream_t s = om.s;
   char* ws = (char*)workspace;
   Exec e{s, 0, (o->precision == ANR_BF16 || o->precision == ANR_BF16_ALL) ? 1 : 0, o->precision == ANR_BF16 ? 1 : 0};
-  e.ss = side_streams();
+  e.ss = om.ss;
   e.hb = e.bf16;
   ANR_TRY(pack_images(e, p, ws + T.wimg, s, (float*)(ws + T.wslab), kLaneFloats));
   ANR_TRY(train_backward(p, grads, f, nullptr, nullptr, nullptr, nullptr, G, &oo, nullptr, d_pbw, d_tbw, ws, T, s, e, x,

@@ -237,13 +237,18 @@ class FusedStep:
 
     def _reduce_hook(self, user, buf, count, op, stream):
         """anr_train_hooks.reduce: the step's mid-step exchange over the ranks (parallel.reduce_keys_) on a
-        view of the workspace buffer the library hands over, on the current stream (the library's)."""
+        view of the workspace buffer the library hands over, issued on the stream the library hands over
+        (its own main stream, not the caller's)."""
         try:
             ws = self._ws_now
             off = buf - ws.data_ptr()
             isz = 4 if op == _lib.REDUCE_SUM_F32 else 8
             view = ws[off:off + count * isz].view(torch.float32 if isz == 4 else torch.int64)
-            reduce_keys_(view, op, self.group)
+            if stream and ws.is_cuda:
+                with torch.cuda.stream(torch.cuda.ExternalStream(stream, device=ws.device)):
+                    reduce_keys_(view, op, self.group)
+            else:
+                reduce_keys_(view, op, self.group)
             return 0
         except Exception:  # pragma: no cover - reported through the library's error code
             import traceback

@@ -125,7 +125,108 @@ static float time_us(hipStream_t s, int reps, const std::function<void()>& f) {
   return ms * 1000.f / reps;
 }
 
+__global__ void k_probe_fill16(unsigned short* p, long n, unsigned seed, float scale) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  unsigned x = (unsigned)i * 2654435761u + seed;
+  x ^= x >> 13; x *= 0x5bd1e995u; x ^= x >> 15;
+  const float v = scale * ((float)(x & 0xffffff) / 16777216.0f - 0.5f);
+  p[i] = (unsigned short)(__float_as_uint(v) >> 16);
+}
+
+// grouped weight gradients against one launch per product: 16 products of mixed shapes and operand
+// formats (bf16 / fp32 rows, K 63 / 256, nout 24 / 256, column sums into bsum / bsum2), the sample
+// count on the device as in the training executor; every dW must be finite and match to 1e-5
+static int group_check(hipStream_t s, int M) {
+  const int NP = 16, cap = (M + 1023) / 1024 * 1024 + 4096;
+  unsigned short *Y16, *X16;
+  float *Y32, *X32, *dWr, *dWg, *bs, *slab, *slabg;
+  int* Mdev;
+  const long rows = (long)cap * 256;
+  CK(hipMalloc(&Y16, NP * rows * 2));
+  CK(hipMalloc(&X16, NP * rows * 2));
+  CK(hipMalloc(&Y32, NP * rows * 4));
+  CK(hipMalloc(&X32, NP * rows * 4));
+  CK(hipMalloc(&dWr, NP * 256L * 256 * 4));
+  CK(hipMalloc(&dWg, NP * 256L * 256 * 4));
+  CK(hipMalloc(&bs, NP * 4 * 256 * 4));
+  CK(hipMalloc(&slab, wgrad_slab_floats() * 4));
+  CK(hipMalloc(&slabg, 4 * wgrad_slab_floats() * 4));
+  CK(hipMalloc(&Mdev, 4));
+  CK(hipMemcpy(Mdev, &M, 4, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(k_probe_fill16, dim3((unsigned)((NP * rows + 255) / 256)), dim3(256), 0, s, Y16, NP * rows, 11u, 0.02f);
+  hipLaunchKernelGGL(k_probe_fill16, dim3((unsigned)((NP * rows + 255) / 256)), dim3(256), 0, s, X16, NP * rows, 12u, 2.f);
+  hipLaunchKernelGGL(k_probe_fill, dim3((unsigned)((NP * rows + 255) / 256)), dim3(256), 0, s, Y32, NP * rows, 13u, 0.02f);
+  hipLaunchKernelGGL(k_probe_fill, dim3((unsigned)((NP * rows + 255) / 256)), dim3(256), 0, s, X32, NP * rows, 14u, 2.f);
+  // stale slabs full of NaN: a partial slab the group forgets to write shows up
+  CK(hipMemsetAsync(slabg, 0xff, 4 * wgrad_slab_floats() * 4, s));
+  std::vector<WGrad> d(NP);
+  for (int k = 0; k < NP; ++k) {
+    WGrad& w = d[k];
+    const int f = k % 4;  // 0 bf16 both, 1 fp32 dY + bf16 X, 2 fp32 both, 3 bf16 dY K=63 with two sums
+    w.ybf = (f == 0 || f == 3);
+    w.xbf = (f == 0 || f == 1 || f == 3);
+    w.nout = (k % 5 == 4) ? 24 : 256;
+    w.K = f == 3 ? 63 : 256;
+    w.ldY = 256;
+    w.ldX = f == 3 ? 64 : 256;
+    w.dY = w.ybf ? (const float*)(Y16 + k * rows) : Y32 + k * rows;
+    w.X = w.xbf ? (const float*)(X16 + k * rows) : X32 + k * rows;
+    w.dW = dWr + k * 65536L; w.ldw = 256;
+    w.bsum = (k % 2) ? bs + k * 1024 : nullptr;
+    w.bsum2 = f == 3 ? bs + k * 1024 + 256 : nullptr;
+    w.M_dev = Mdev;
+  }
+  CK(hipMemsetAsync(dWr, 0, NP * 256L * 256 * 4, s));
+  CK(hipMemsetAsync(bs, 0, NP * 4 * 256 * 4, s));
+  for (int k = 0; k < NP; ++k) {
+    WGrad w = d[k];
+    w.slab = slab;
+    if (launch_wgrad(w, cap, s) != 0) return 1;
+  }
+  std::vector<float> ref(NP * 65536L), bref(NP * 1024L);
+  CK(hipStreamSynchronize(s));
+  CK(hipMemcpy(ref.data(), dWr, ref.size() * 4, hipMemcpyDeviceToHost));
+  CK(hipMemcpy(bref.data(), bs, bref.size() * 4, hipMemcpyDeviceToHost));
+  for (int k = 0; k < NP; ++k) d[k].dW = dWg + k * 65536L;
+  for (int nz : {16, 32, 64}) {
+    CK(hipMemsetAsync(dWg, 0, NP * 256L * 256 * 4, s));
+    CK(hipMemsetAsync(bs, 0, NP * 4 * 256 * 4, s));
+    if (launch_wgrad_group(d.data(), NP, cap, nz, slabg, 4 * wgrad_slab_floats(), s) != 0) return 1;
+    std::vector<float> got(NP * 65536L), bgot(NP * 1024L);
+    CK(hipStreamSynchronize(s));
+    CK(hipMemcpy(got.data(), dWg, got.size() * 4, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(bgot.data(), bs, bgot.size() * 4, hipMemcpyDeviceToHost));
+    for (int k = 0; k < NP; ++k) {
+      double m = 0, sc = 0, mb = 0, sb = 0;
+      bool fin = true;
+      for (long i = 0; i < 65536; ++i) {
+        const float a = got[k * 65536L + i], r = ref[k * 65536L + i];
+        fin = fin && std::isfinite(a);
+        m = std::max(m, (double)std::fabs(a - r));
+        sc = std::max(sc, (double)std::fabs(r));
+      }
+      for (long i = 0; i < 1024; ++i) {
+        const float a = bgot[k * 1024L + i], r = bref[k * 1024L + i];
+        fin = fin && std::isfinite(a);
+        mb = std::max(mb, (double)std::fabs(a - r));
+        sb = std::max(sb, (double)std::fabs(r));
+      }
+      printf("{\"group_check\": %d, \"nz\": %d, \"finite\": %d, \"dW_rel\": %.3g, \"bsum_rel\": %.3g, \"ybf\": %d, "
+             "\"xbf\": %d, \"nout\": %d, \"K\": %d}\n", k, nz, fin ? 1 : 0, sc > 0 ? m / sc : m, sb > 0 ? mb / sb : mb,
+             d[k].ybf, d[k].xbf, d[k].nout, d[k].K);
+    }
+  }
+  fflush(stdout);
+  return 0;
+}
+
 int main(int argc, char** argv) {
+  if (argc > 1 && std::string(argv[1]) == "groupcheck") {
+    hipStream_t s;
+    CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    return group_check(s, argc > 2 ? atoi(argv[2]) : 24893);
+  }
   std::vector<int> Ms;
   for (int i = 1; i < argc; ++i) Ms.push_back(atoi(argv[i]));
   if (Ms.empty()) Ms = {6223, 12446, 24893, 49786, 99572};
