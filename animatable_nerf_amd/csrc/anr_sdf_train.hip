@@ -856,14 +856,15 @@ int sdf_train_core(const TrainCore& C) {
   TG g{s};
   // which products run split-bf16 (bits, ANR_SDF_X3_PARTS): 1 residual MLP, 2 SDF forward, 4 SDF input
   // gradient, 8 colour net, 16 SDF tangent pass, 32 stacked SDF reverse, 64 the weight gradients of the
-  // split parts. Default 124: all but the residual MLP and the SDF forward. The residual MLP's parameter
+  // split parts. Default 252: all but the residual MLP and the SDF forward (those two run x6 row GEMMs). The residual MLP's parameter
   // gradients are ~1e-5 in magnitude and lose tests/test_gpu_sdf_train.py's 5e-3-of-max bar to split
   // products in any of those two (the softplus(beta=100) factors of the SDF forward feed every
   // second-order term); each other part split alone, and all of them together, keep it (profiles/r4e,
-  // r4g, r4h bisection). Bit 128: the weight gradients split-bf16 in every part, the exact ones included
+  // r4g, r4h bisection). Bit 128 (default on): the weight gradients split-bf16 in every part, the
+  // fp32-level ones included (test green at the same tolerances, 11.1 -> 10.9 ms, profiles/r4y)
   static const int x3_parts = [] {
     const char* v = getenv("ANR_SDF_X3_PARTS");
-    return v ? atoi(v) : 124;
+    return v ? atoi(v) : 252;
   }();
   // the parts kept at fp32 level run their forward products as x6 row GEMMs (same bits; default the
   // residual MLP and the SDF forward, 3)

@@ -99,6 +99,7 @@ int check_args(const anr_params* p, const anr_frame* f, const float* ray_o, cons
 struct SideStreams {
   hipStream_t main = nullptr;  // the library's own main stream (OnMain)
   hipStream_t s2 = nullptr, sw[kWStreams] = {};
+  int lanes = kWStreams;  // weight-gradient lanes created (ANR_TRAIN_LANES, 1..kWStreams)
   hipStream_t cap = nullptr;  // origin stream of step-graph captures (created on first use)
   hipEvent_t ev[64] = {};
   unsigned next = 0;
@@ -117,8 +118,15 @@ SideStreams* side_streams() {
     SideStreams t{};
     if (hipStreamCreateWithFlags(&t.s2, hipStreamNonBlocking) != hipSuccess) return nullptr;
     if (hipStreamCreateWithFlags(&t.main, hipStreamNonBlocking) != hipSuccess) return nullptr;
-    for (auto& w : t.sw)
-      if (hipStreamCreateWithFlags(&w, hipStreamNonBlocking) != hipSuccess) return nullptr;
+    const char* lv = getenv("ANR_TRAIN_LANES");
+    t.lanes = lv && atoi(lv) >= 1 && atoi(lv) <= kWStreams ? atoi(lv) : kWStreams;
+    for (int l = 0; l < kWStreams; ++l) {
+      if (l >= t.lanes) {
+        t.sw[l] = t.sw[0];  // fewer hardware queues in use: the extra lanes alias lane 0
+        continue;
+      }
+      if (hipStreamCreateWithFlags(&t.sw[l], hipStreamNonBlocking) != hipSuccess) return nullptr;
+    }
     for (auto& e : t.ev)
       if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
     ss = t;
@@ -210,7 +218,7 @@ struct Exec {
   // a weight-gradient lane (stream + its partial-slab region), ordered after everything issued to s
   // so far; lane < 0: the next one round robin
   int wstream(hipStream_t* w, int* lane, int want = -1) {
-    const int l = want >= 0 ? want : (wnext++ % kWStreams);
+    const int l = want >= 0 ? want : (wnext++ % (ss ? ss->lanes : 1));
     *lane = ss ? l : 0;
     *w = ss ? ss->sw[l] : s;
     return order(ss, *w, s);
@@ -268,14 +276,14 @@ struct Exec {
   int gather_w() {
     ANR_TRY(flush_w());
     if (!ss) return ANR_OK;
-    for (int l = 1; l < kWStreams; ++l) ANR_TRY(order(ss, ss->sw[0], ss->sw[l]));
+    for (int l = 1; l < ss->lanes; ++l) ANR_TRY(order(ss, ss->sw[0], ss->sw[l]));
     return ANR_OK;
   }
   // s waits for every weight-gradient lane (end of a backward)
   int join_w() {
     ANR_TRY(flush_w());
     if (!ss) return ANR_OK;
-    for (int l = 0; l < kWStreams; ++l) ANR_TRY(order(ss, s, ss->sw[l]));
+    for (int l = 0; l < ss->lanes; ++l) ANR_TRY(order(ss, s, ss->sw[l]));
     return ANR_OK;
   }
 
