@@ -856,7 +856,7 @@ int sdf_train_core(const TrainCore& C) {
   TG g{s};
   // which products run split-bf16 (bits, ANR_SDF_X3_PARTS): 1 residual MLP, 2 SDF forward, 4 SDF input
   // gradient, 8 colour net, 16 SDF tangent pass, 32 stacked SDF reverse, 64 the weight gradients of the
-  // split parts. Default 252: all but the residual MLP and the SDF forward (those two run x6 row GEMMs). The residual MLP's parameter
+  // split parts. Default 252: all but the residual MLP's and the SDF forward's products (exact fp32). The residual MLP's parameter
   // gradients are ~1e-5 in magnitude and lose tests/test_gpu_sdf_train.py's 5e-3-of-max bar to split
   // products in any of those two (the softplus(beta=100) factors of the SDF forward feed every
   // second-order term); each other part split alone, and all of them together, keep it (profiles/r4e,
@@ -866,11 +866,12 @@ int sdf_train_core(const TrainCore& C) {
     const char* v = getenv("ANR_SDF_X3_PARTS");
     return v ? atoi(v) : 252;
   }();
-  // the parts kept at fp32 level run their forward products as x6 row GEMMs (same bits; default the
-  // residual MLP and the SDF forward, 3)
+  // ANR_SDF_X6_PARTS (same bits, default 0): parts kept at fp32 level whose forward / input-gradient
+  // products run as x6 row GEMMs instead of exact fp32 — measured slower (10.87 vs 10.67 ms per step,
+  // profiles/r4x6_*: one 128-row workgroup per CU leaves a 10 %-full second round at ~36k rows)
   static const int x6_parts = [] {
     const char* v = getenv("ANR_SDF_X6_PARTS");
-    return v ? atoi(v) : 3;
+    return v ? atoi(v) : 0;
   }();
   const bool x3_on = o->precision == ANR_BF16X3;
   auto part = [&](int bit) {
