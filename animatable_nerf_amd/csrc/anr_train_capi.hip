@@ -188,7 +188,9 @@ struct Exec {
   // Fewer sample ranges per product (nz, ANR_WG_GROUP_NZ) still fill the chip, because the products of a
   // group run side by side: less partial-slab traffic and ~4x fewer launches than one product at a time.
   int group = 0, group_nz = 16;
-  int flush_every = 0;  // ANR_WG_FLUSH_EVERY: also flush once this many products are queued (0: phase ends only)
+  // ANR_WG_FLUSH_EVERY: also flush once this many products are queued (0: at 16 and at the end only);
+  // 8 measured 1.400 / 1.538 vs 1.418 / 1.559 ms on two boxes (profiles/r4u_*, r4l1_*)
+  int flush_every = 8;
   WGrad pend[WG_GROUP_MAX];
   int npend = 0;
   hipStream_t pend_src[2] = {};
@@ -203,10 +205,6 @@ struct Exec {
   } post[8];
   int npost = 0;
   int nqueued = 0;  // products queued so far
-  const int dbg = [] {
-    const char* v = getenv("ANR_WG_DEBUG");
-    return v ? atoi(v) : 0;
-  }();
   // the kept-sample count stays on the device (no host read, so a step can be captured in a graph):
   // every launch is sized for the capacity `cap` and reads the count from n_dev
   const int* n_dev = nullptr;
@@ -228,19 +226,9 @@ struct Exec {
   int flush_w() {
     if (!npend && !npost) return ANR_OK;
     hipStream_t w = ss ? ss->sw[0] : s;
-    if ((dbg & 1) && ss) {  // debugging aid: the flush waits for both chain streams
-      ANR_TRY(order(ss, w, ss->s2));
-      if (ss->s2 != s) ANR_TRY(order(ss, w, s));
-    }
     for (int i = 0; i < 2 && pend_src[i]; ++i) ANR_TRY(order(ss, w, pend_src[i]));
-    if ((dbg & 4) && slab(0) && hipMemsetAsync(slab(0), 0, lane_floats * 4, w) != hipSuccess)  // debugging aid
-      return fail(ANR_E_HIP, "memset");
     if (npend && launch_wgrad_group(pend, npend, grid_n(), group_nz, slab(0), lane_floats, w) != 0)
       return check_launch("k_wgrad_group");
-    if ((dbg & 2) && ss) {  // debugging aid: both chain streams wait for the flush
-      ANR_TRY(order(ss, ss->s2, w));
-      if (ss->s2 != s) ANR_TRY(order(ss, s, w));
-    }
     for (int i = 0; i < npost; ++i) {
       const LatentPost& q = post[i];
       hipLaunchKernelGGL(k_tr_latent_grad, dim3(256 + 128), dim3(128), 0, w, q.ys, q.W, q.in_ch, q.c0, q.ncol, q.tab, q.li,
@@ -257,14 +245,13 @@ struct Exec {
                   int K, float* bsum, unsigned bf, const LatentPost& q) {
     hipStream_t w = s;
     int lane = 0;
-    if (!group || (dbg & 32)) ANR_TRY(wstream(&w, &lane, 0));
+    if (!group) ANR_TRY(wstream(&w, &lane, 0));
     if (hipMemsetAsync(ys, 0, 256 * 4, w) != hipSuccess) return fail(ANR_E_HIP, "memset");
     if (group && (npend == WG_GROUP_MAX || npost == 8)) ANR_TRY(flush_w());  // product and update in one flush
     const int q0 = nqueued;
     ANR_TRY(wgrad(dW, in_ch, c0, Nout, dY, ldY, X, ldX, K, bsum, ys, 0, bf));
     if (nqueued > q0) {
       post[npost++] = q;
-      if (dbg & 16) return flush_w();  // debugging aid: products with latent rows not deferred
       return ANR_OK;
     }
     if (group) ANR_TRY(wstream(&w, &lane, 0));  // off the fast path: the product ran on lane 0
@@ -589,7 +576,7 @@ struct BwBackward {
     }
     --l;
     // ping-pong gradient rows are overwritten two layers on: their queued products run now
-    if (!dstride || (e.dbg & 8)) ANR_TRY(e.flush_w());
+    if (!dstride) ANR_TRY(e.flush_w());
     return ANR_OK;
   }
 };
