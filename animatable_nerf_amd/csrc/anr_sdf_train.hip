@@ -511,23 +511,9 @@ struct LgImage {
   void* img;
 };
 
-// x6 products (the parts the split-bf16 precision cannot take, ANR_SDF_X6_PARTS): the row GEMM's
-// three-way split (anr_tgemm.hip k_rgemm X6, ~2^-24 relative per product) on a hi / mid / lo weight
-// image packed into the same arena once per call and weight view
-struct RgImage {
-  const float* B[2];
-  long rs[2], cs[2];
-  int K[2], N, nseg;
-  const unsigned short* img;
-  long ldb;
-};
-
 struct TG {
   hipStream_t s;
   int x3 = 0;
-  int x6 = 0;
-  RgImage rg[64];
-  int nrg = 0;
   int wg_x3 = 0;          // the weight gradients split-bf16 (set per part)
   float* slab = nullptr;  // k_wgrad partial slabs (x3)
   char* lg_arena = nullptr;  // k_lgemm weight images (x3)
@@ -554,71 +540,10 @@ struct TG {
                         a.K, two ? b.K : 0, g.N, img};
     return img;
   }
-  // the row GEMM takes the product: k-contiguous fp32 activations (16-B rows, lda >= K rounded to the
-  // 32-deep chunk), 64 <= N <= 256, epilogues bias / ReLU / softplus (+ derivative rows) / mask /
-  // accumulate / div_post; B any layout (packed into the image)
-  bool rg_ok(const GemmArgs& g) const {
-    if (!lg_arena || g.N < 64 || g.N > 256 || g.nseg < 1 || g.nseg > 2 || g.atomic || g.ksplit > 1 || g.K_dev ||
-        g.M_dev || g.div_pre != 0.f || g.spd || g.rowsum || g.rowsum2 || g.a_softplus_w || g.head_w || g.bf16 ||
-        ((uintptr_t)g.C & 15) || g.ldc % 4)
-      return false;
-    if (g.mask && (g.ldm % 4 || ((uintptr_t)g.mask & 15))) return false;
-    for (int q = 0; q < g.nseg; ++q) {
-      const GemmSeg& a = g.seg[q];
-      if (a.a_cs != 1 || a.a_rs % 4 || ((uintptr_t)a.A & 15) || a.a_rs < (a.K + 31) / 32 * 32) return false;
-    }
-    return true;
-  }
-  const RgImage* rg_image(const GemmArgs& g) {
-    for (int i = 0; i < nrg; ++i) {
-      const RgImage& q = rg[i];
-      bool same = q.N == g.N && q.nseg == g.nseg;
-      for (int k = 0; same && k < g.nseg; ++k)
-        same = q.B[k] == g.seg[k].B && q.rs[k] == g.seg[k].b_rs && q.cs[k] == g.seg[k].b_cs && q.K[k] == g.seg[k].K;
-      if (same) return &q;
-    }
-    if (nrg >= 64) return nullptr;
-    RgImage q{};
-    q.N = g.N;
-    q.nseg = g.nseg;
-    for (int k = 0; k < g.nseg; ++k) {
-      q.B[k] = g.seg[k].B; q.rs[k] = g.seg[k].b_rs; q.cs[k] = g.seg[k].b_cs; q.K[k] = g.seg[k].K;
-    }
-    const size_t bytes = ((size_t)rimg_x6_elems(g.N, g.nseg, q.K) * 2 + 255) / 256 * 256;
-    if (lg_used + bytes > lg_cap) return nullptr;
-    unsigned short* img = (unsigned short*)(lg_arena + lg_used);
-    if (rimg_x6_pack(g.N, g.nseg, q.B, q.rs, q.cs, q.K, img, s) != 0) return nullptr;
-    lg_used += bytes;
-    q.img = img;
-    q.ldb = rimg_x6_ldb(g.nseg, q.K);
-    rg[nrg] = q;
-    return &rg[nrg++];
-  }
-  int run_x6(const GemmArgs& g, int M, const RgImage* im) {
-    RGemm r{};
-    r.x3 = 1;
-    r.x6 = 1;
-    r.M = M;
-    r.N = g.N;
-    r.nseg = g.nseg;
-    const long plane = (long)g.N * im->ldb;
-    int col = 0;
-    for (int q = 0; q < g.nseg; ++q) {
-      r.seg[q] = RGemmSeg{g.seg[q].A, g.seg[q].a_rs, g.seg[q].K, im->img, im->ldb, col, g.N, plane};
-      col += (g.seg[q].K + 63) / 64 * 64;
-    }
-    r.C = g.C; r.ldc = g.ldc; r.bias = g.bias; r.relu = g.relu; r.mask = g.mask; r.ldm = g.ldm;
-    r.accumulate = g.accumulate;
-    r.softplus = g.softplus; r.deriv = g.deriv; r.ldd = g.ldd; r.div_post = g.div_post;
-    launch_rgemm(r, M, s);
-    return check_launch("k_rgemm x6 (sdf train)");
-  }
   int run(GemmArgs g, int M) {
     if (M <= 0 || g.N <= 0) return ANR_OK;
     g.M = M;
     if (g.ksplit < 1) g.ksplit = 1;
-    if (x6 && rg_ok(g))
-      if (const RgImage* im = rg_image(g)) return run_x6(g, M, im);
     if (x3 && !g.atomic) g.x3 = 1;
     if (g.x3 && lg_arena && lgemm_supported(g)) {
       if (void* img = lg_image(g)) {
@@ -648,11 +573,10 @@ struct TG {
   int wgrad(int M, float* dW, int in_ch, int c0, int Nout, const float* dY, long ldY, const float* X, long ldX, int K,
             float* bsum = nullptr) {
     if (M <= 0) return ANR_OK;
-    if ((wg_x3 || x6) && slab && Nout <= 256 && K <= 256 && ldY % 4 == 0 && ldX % 4 == 0 && ((uintptr_t)dY & 15) == 0 &&
+    if (wg_x3 && slab && Nout <= 256 && K <= 256 && ldY % 4 == 0 && ldX % 4 == 0 && ((uintptr_t)dY & 15) == 0 &&
         ((uintptr_t)X & 15) == 0) {
       WGrad w{};
       w.x3 = 1;
-      w.x6 = wg_x3 ? 0 : 1;  // the fp32-level parts: three-way split unless their weight gradients run split-bf16
       w.dY = dY; w.ldY = ldY; w.nout = Nout; w.X = X; w.ldX = ldX; w.K = K;
       w.dW = dW + c0; w.ldw = in_ch; w.bsum = bsum; w.slab = slab;
       if (launch_wgrad(w, M, s) != 0) return check_launch("k_wgrad (sdf train)");
@@ -866,17 +790,9 @@ int sdf_train_core(const TrainCore& C) {
     const char* v = getenv("ANR_SDF_X3_PARTS");
     return v ? atoi(v) : 252;
   }();
-  // ANR_SDF_X6_PARTS (same bits, default 0): parts kept at fp32 level whose forward / input-gradient
-  // products run as x6 row GEMMs instead of exact fp32 — measured slower (10.87 vs 10.67 ms per step,
-  // profiles/r4x6_*: one 128-row workgroup per CU leaves a 10 %-full second round at ~36k rows)
-  static const int x6_parts = [] {
-    const char* v = getenv("ANR_SDF_X6_PARTS");
-    return v ? atoi(v) : 0;
-  }();
   const bool x3_on = o->precision == ANR_BF16X3;
   auto part = [&](int bit) {
     g.x3 = x3_on && (x3_parts & bit) ? 1 : 0;
-    g.x6 = x3_on && !g.x3 && (x6_parts & bit) ? 1 : 0;
     g.wg_x3 = x3_on && ((g.x3 && (x3_parts & 64)) || (x3_parts & 128)) ? 1 : 0;
   };
   if (x3_on) {

@@ -185,17 +185,14 @@ bool wimg_view(const void* base, const float* const* t, const float* W, int c0, 
 // workgroups (4 waves, 2-4 slots) 21.5 us; 32-deep chunks in a 3-slot 72 KiB ring, two workgroups per
 // CU, 14.9 us alone and 11.6 vs 9.9 us per launch with two streams. The workgroup's time is its load
 // burst, four chunks and a store burst that runs at the HBM write rate (phase clocks).)
-// X6 (with X3 set: fp32 activations, 32-deep chunks): a third weight image per slot (hi / mid / lo),
-// 64 KiB slots, 128 KiB of LDS.
-template <bool X3, bool ABF = false, bool X6 = false> struct RgCfg {
-  static_assert(!X6 || X3, "X6 runs on the X3 geometry");
+template <bool X3, bool ABF = false> struct RgCfg {
   static constexpr int BM = 128;
   static constexpr int WAVES = BM / 16;
   static constexpr int KC = X3 ? 32 : 64;                              // K chunk
   static constexpr int AE = ABF ? 2 : 4;                               // bytes per activation element
   static constexpr int A_BYTES = BM * KC * AE;                         // activations, BM rows x KC
   static constexpr int B_BYTES = 256 * KC * 2;                         // bf16 weight rows, 256 x KC
-  static constexpr int NIMG = X6 ? 3 : X3 ? 2 : 1;                     // weight images per slot
+  static constexpr int NIMG = X3 ? 2 : 1;                              // weight images per slot
   static constexpr int NS = 2;                                         // ring slots
   static constexpr int SLOT = A_BYTES + B_BYTES * NIMG;                // bytes per slot
   static constexpr int PIECES_A = A_BYTES / 1024 / WAVES;              // per wave
@@ -220,10 +217,10 @@ __device__ __forceinline__ void rg_dma(const void* src, unsigned m0) {
 }
 
 // issue chunk c (segment-relative K offset kk) into ring slot `slot`
-template <bool X3, bool ABF, bool X6 = false>
+template <bool X3, bool ABF>
 __device__ __forceinline__ void rg_issue(const RGemm& g, int seg, int kk, int m0, int M, int N, unsigned slot_lds, int w,
                                          int lane) {
-  using C = RgCfg<X3, ABF, X6>;
+  using C = RgCfg<X3, ABF>;
   const unsigned char* A = (const unsigned char*)(seg ? g.seg[1].A : g.seg[0].A);
   const long lda = seg ? g.seg[1].lda : g.seg[0].lda;
   const unsigned short* B = seg ? g.seg[1].B : g.seg[0].B;
@@ -259,8 +256,6 @@ __device__ __forceinline__ void rg_issue(const RGemm& g, int seg, int kk, int m0
       const int br = min(r, brows - 1);
       const int ch = (lane % C::CHB) ^ C::swb(r);
       rg_dma(B + lo + (long)br * ldb + bcol + kk + ch * 8, slot_lds + C::A_BYTES + C::B_BYTES + p * 1024);
-      if constexpr (X6)
-        rg_dma(B + 2 * lo + (long)br * ldb + bcol + kk + ch * 8, slot_lds + C::A_BYTES + 2 * C::B_BYTES + p * 1024);
     }
   }
   (void)N;
@@ -287,9 +282,9 @@ void rg_timing_buffer(unsigned long long* p) { (void)hipMemcpyToSymbol(HIP_SYMBO
   } while (0)
 #endif
 
-template <bool X3, bool ABF, bool MBF, bool X6 = false>
+template <bool X3, bool ABF, bool MBF>
 __global__ __launch_bounds__(RgCfg<X3>::WAVES * 64) void k_rgemm(RGemm g) {
-  using CF = RgCfg<X3, ABF, X6>;
+  using CF = RgCfg<X3, ABF>;
   constexpr int RG_NS = CF::NS, RG_SLOT = CF::SLOT, RG_OPS = CF::OPS;
   constexpr int RG_BM = CF::BM, RG_A_BYTES = CF::A_BYTES;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -305,7 +300,7 @@ __global__ __launch_bounds__(RgCfg<X3>::WAVES * 64) void k_rgemm(RGemm g) {
   auto issue = [&](int c) {
     const int seg = c < nc0 ? 0 : 1;
     const int kk = (c - (seg ? nc0 : 0)) * KC;
-    rg_issue<X3, ABF, X6>(g, seg, kk, m0, M, N, base + (c % RG_NS) * RG_SLOT, w, lane);
+    rg_issue<X3, ABF>(g, seg, kk, m0, M, N, base + (c % RG_NS) * RG_SLOT, w, lane);
   };
   RG_T(0);
   const int wr = (w >> 2) * 64;   // this wave's 64 rows of the tile
@@ -360,7 +355,7 @@ __global__ __launch_bounds__(RgCfg<X3>::WAVES * 64) void k_rgemm(RGemm g) {
     if (active) {
 #pragma unroll
       for (int ks = 0; ks < KC / 32; ++ks) {
-        bf16x8_t af[4], bfr[4], al[4], bl[4], am[4], b2[4];  // X6: am / b2 the third parts
+        bf16x8_t af[4], bfr[4], al[4], bl[4];
         const int kc = 4 * ks + (lane >> 4);  // 8-element k group of this lane
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -386,13 +381,7 @@ __global__ __launch_bounds__(RgCfg<X3>::WAVES * 64) void k_rgemm(RGemm g) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
             af[i][e] = (__bf16)x[e];
-            if constexpr (X6) {  // x = hi + mid + lo, each residual exact in fp32
-              const float r1 = x[e] - (float)af[i][e];
-              am[i][e] = (__bf16)r1;
-              al[i][e] = (__bf16)(r1 - (float)am[i][e]);
-            } else if constexpr (X3) {
-              al[i][e] = (__bf16)(x[e] - (float)af[i][e]);
-            }
+            if constexpr (X3) al[i][e] = (__bf16)(x[e] - (float)af[i][e]);
           }
         }
 #pragma unroll
@@ -401,19 +390,12 @@ __global__ __launch_bounds__(RgCfg<X3>::WAVES * 64) void k_rgemm(RGemm g) {
           const int sb = CF::swb(r);
           bfr[j] = *(const bf16x8_t*)(sB + r * (KC * 2) + ((kc ^ sb) * 16));
           if constexpr (X3) bl[j] = *(const bf16x8_t*)(sB + CF::B_BYTES + r * (KC * 2) + ((kc ^ sb) * 16));
-          if constexpr (X6) b2[j] = *(const bf16x8_t*)(sB + 2 * CF::B_BYTES + r * (KC * 2) + ((kc ^ sb) * 16));
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            if constexpr (X6) {  // weight planes bfr / bl / b2 = hi / mid / lo; 2^-16 terms first
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b2[j], af[i], acc[i][j], 0, 0, 0);
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], al[i], acc[i][j], 0, 0, 0);
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl[j], am[i], acc[i][j], 0, 0, 0);
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl[j], af[i], acc[i][j], 0, 0, 0);
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], am[i], acc[i][j], 0, 0, 0);
-            } else if constexpr (X3) {
+            if constexpr (X3) {
               acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bl[j], af[i], acc[i][j], 0, 0, 0);
               acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], al[i], acc[i][j], 0, 0, 0);
             }
@@ -464,30 +446,9 @@ __global__ __launch_bounds__(RgCfg<X3>::WAVES * 64) void k_rgemm(RGemm g) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
         }
-        if constexpr (X6) {
-          if (g.softplus) {  // torch softplus(beta=100, threshold=20) and the factor its backward uses
-            f32x4 dv;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const float z = v[e] * 100.f;
-              const float ez = fast_exp(z);
-              dv[e] = z > 20.f ? -1.f : ez;
-              v[e] = z > 20.f ? v[e] : fast_log1p(ez) / 100.f;
-            }
-            const int m = m0 + wr + 16 * i + (lane & 15);
-            const int n = wc + 16 * j + 4 * (lane >> 4);
-            if (g.deriv && m < M && n < N) *(f32x4*)(g.deriv + (long)m * g.ldd + n) = dv;
-          }
-        }
         if (g.mask) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = mk[i][j][e] > 0.f ? v[e] : 0.f;
-        }
-        if constexpr (X6) {
-          if (g.div_post != 0.f) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = v[e] / g.div_post;
-          }
         }
         acc[i][j] = v;
       }
@@ -555,35 +516,23 @@ __global__ __launch_bounds__(RgCfg<X3>::WAVES * 64) void k_rgemm(RGemm g) {
         if (g.bias) v += g.bias[n];
         if (g.accumulate) v += *cp;
         if (g.relu) v = fmaxf(v, 0.f);
-        if constexpr (X6) {
-          if (g.softplus) {
-            const float z = v * 100.f;
-            const float ez = fast_exp(z);
-            if (g.deriv) g.deriv[(long)m * g.ldd + n] = z > 20.f ? -1.f : ez;
-            v = z > 20.f ? v : fast_log1p(ez) / 100.f;
-          }
-        }
         if (g.mask) {
           const float mv = MBF ? bf2f(mask16[(long)m * g.ldm + n]) : g.mask[(long)m * g.ldm + n];
           if (!(mv > 0.f)) v = 0.f;
-        }
-        if constexpr (X6) {
-          if (g.div_post != 0.f) v = v / g.div_post;
         }
         if (g.cbf) C16[(long)m * g.ldc + n] = f2bf_rne(v);
         else *cp = v;
       }
 }
 
-template <bool X3, bool ABF, bool X6 = false>
-size_t rgemm_lds_bytes() { return (size_t)RgCfg<X3, ABF, X6>::NS * RgCfg<X3, ABF, X6>::SLOT; }
+template <bool X3, bool ABF>
+size_t rgemm_lds_bytes() { return (size_t)RgCfg<X3, ABF>::NS * RgCfg<X3, ABF>::SLOT; }
 
 void launch_rgemm(const RGemm& g0, int M_host, hipStream_t s) {
   RGemm g = g0;
   const size_t ce = g.cbf ? 2 : 4, me = g.mbf ? 2 : 4;  // C / mask element bytes
   g.vec_out = (g.N % 4 == 0) && (g.ldc % 4 == 0) && ((uintptr_t)g.C % (4 * ce) == 0) &&
-              (!g.mask || ((g.ldm % 4 == 0) && ((uintptr_t)g.mask % (4 * me) == 0))) && ((uintptr_t)g.bias % 16 == 0) &&
-              (!g.deriv || (g.ldd % 4 == 0 && (uintptr_t)g.deriv % 16 == 0));
+              (!g.mask || ((g.ldm % 4 == 0) && ((uintptr_t)g.mask % (4 * me) == 0))) && ((uintptr_t)g.bias % 16 == 0);
   g.vec16 = g.vec_out && g.cbf && g.ldc % 8 == 0 && (uintptr_t)g.C % 16 == 0;
   static bool attr = false;
   if (!attr) {
@@ -597,16 +546,12 @@ void launch_rgemm(const RGemm& g0, int M_host, hipStream_t s) {
                               (int)rgemm_lds_bytes<false, true>());
     (void)hipFuncSetAttribute((const void*)k_rgemm<true, false, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)rgemm_lds_bytes<true, false>());
-    (void)hipFuncSetAttribute((const void*)k_rgemm<true, false, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)rgemm_lds_bytes<true, false, true>());
     attr = true;
   }
   constexpr int BM = RgCfg<false>::BM;
   const dim3 grid((M_host + BM - 1) / BM), block(RgCfg<false>::WAVES * 64);
   const bool mbf = g.mbf && g.mask;
-  if (g.x6)
-    hipLaunchKernelGGL((k_rgemm<true, false, false, true>), grid, block, (rgemm_lds_bytes<true, false, true>()), s, g);
-  else if (g.x3)
+  if (g.x3)
     hipLaunchKernelGGL((k_rgemm<true, false, false>), grid, block, (rgemm_lds_bytes<true, false>()), s, g);
   else if (g.abf && mbf)
     hipLaunchKernelGGL((k_rgemm<false, true, true>), grid, block, (rgemm_lds_bytes<false, true>()), s, g);
@@ -616,52 +561,6 @@ void launch_rgemm(const RGemm& g0, int M_host, hipStream_t s) {
     hipLaunchKernelGGL((k_rgemm<false, false, true>), grid, block, (rgemm_lds_bytes<false, false>()), s, g);
   else
     hipLaunchKernelGGL((k_rgemm<false, false, false>), grid, block, (rgemm_lds_bytes<false, false>()), s, g);
-}
-
-long rimg_x6_ldb(int nseg, const int* K) {
-  long ld = 0;
-  for (int s = 0; s < nseg; ++s) ld += rup64(K[s]);
-  return ld;
-}
-long rimg_x6_elems(int N, int nseg, const int* K) { return 3L * N * rimg_x6_ldb(nseg, K); }
-
-struct RPackX6 {
-  const float* B[2];
-  long rs[2], cs[2], ldb, plane;
-  int N, nseg, K[2], col[2];
-  unsigned short* out;
-};
-
-// one thread per image element (n, column): hi, mid = bf16(w - hi), lo = bf16(w - hi - mid)
-__global__ void k_rimg_x6_pack(RPackX6 a) {
-  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= a.plane) return;
-  const int n = (int)(e / a.ldb), col = (int)(e - (long)n * a.ldb);
-  float v = 0.f;
-  for (int s = 0; s < a.nseg; ++s)
-    if (col >= a.col[s] && col < a.col[s] + a.K[s]) v = a.B[s][(long)(col - a.col[s]) * a.rs[s] + (long)n * a.cs[s]];
-  const unsigned short hi = f2bf_rne(v);
-  const float r1 = v - __uint_as_float((uint32_t)hi << 16);
-  const unsigned short mid = f2bf_rne(r1);
-  a.out[e] = hi;
-  a.out[a.plane + e] = mid;
-  a.out[2 * a.plane + e] = f2bf_rne(r1 - __uint_as_float((uint32_t)mid << 16));
-}
-
-int rimg_x6_pack(int N, int nseg, const float* const* B, const long* b_rs, const long* b_cs, const int* K,
-                 unsigned short* dst, hipStream_t s) {
-  if (nseg < 1 || nseg > 2 || N <= 0) return -1;
-  RPackX6 a{};
-  a.N = N; a.nseg = nseg; a.out = dst;
-  long col = 0;
-  for (int q = 0; q < nseg; ++q) {
-    a.B[q] = B[q]; a.rs[q] = b_rs[q]; a.cs[q] = b_cs[q]; a.K[q] = K[q]; a.col[q] = (int)col;
-    col += rup64(K[q]);
-  }
-  a.ldb = col;
-  a.plane = (long)N * col;
-  hipLaunchKernelGGL(k_rimg_x6_pack, dim3((unsigned)((a.plane + 255) / 256)), dim3(256), 0, s, a);
-  return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 }  // namespace anr
@@ -698,26 +597,21 @@ __device__ __forceinline__ bf16x8_t wg_frag(const unsigned short* S, int cb, int
   return f;
 }
 
-// X3: also the lo image (x - hi) into SL. X6: x = hi + mid + lo, mid into SL and lo into SL2
-template <bool X3, bool X6 = false>
-__device__ __forceinline__ void wg_store(unsigned short* S, unsigned short* SL, int tid, const f32x4 (&v)[4],
-                                         unsigned short* SL2 = nullptr) {
+// X3: also the lo image (x - hi) into SL
+template <bool X3>
+__device__ __forceinline__ void wg_store(unsigned short* S, unsigned short* SL, int tid, const f32x4 (&v)[4]) {
 #pragma unroll
   for (int h = 0; h < 4; ++h) {
     const int row = 8 * h + (tid >> 5), col = 4 * (tid & 31);
-    unsigned short e[4], l[4], q[4];
+    unsigned short e[4], l[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       e[k] = f2bf_rne(v[h][k]);
-      const float r1 = v[h][k] - __uint_as_float((uint32_t)e[k] << 16);
-      if constexpr (X3) l[k] = f2bf_rne(r1);
-      if constexpr (X6) q[k] = f2bf_rne(r1 - __uint_as_float((uint32_t)l[k] << 16));
+      if constexpr (X3) l[k] = f2bf_rne(v[h][k] - __uint_as_float((uint32_t)e[k] << 16));
     }
     *(uint2*)(S + row * WG_LD + col) = make_uint2((uint32_t)e[0] | ((uint32_t)e[1] << 16), (uint32_t)e[2] | ((uint32_t)e[3] << 16));
     if constexpr (X3)
       *(uint2*)(SL + row * WG_LD + col) = make_uint2((uint32_t)l[0] | ((uint32_t)l[1] << 16), (uint32_t)l[2] | ((uint32_t)l[3] << 16));
-    if constexpr (X6)
-      *(uint2*)(SL2 + row * WG_LD + col) = make_uint2((uint32_t)q[0] | ((uint32_t)q[1] << 16), (uint32_t)q[2] | ((uint32_t)q[3] << 16));
   }
 }
 
@@ -789,21 +683,16 @@ __device__ __forceinline__ void wg_put_bf(unsigned short* S, const uint2 (&r)[4]
 
 // the LDS of one weight-gradient workgroup: per buffer two 32-sample images (hi and lo under X3, two
 // sample halves otherwise), double-buffered, and the column-sum exchange
-template <int NIMG>
-struct WgLdsT {
-  unsigned short sY[2][NIMG * WG_S * WG_LD];
-  unsigned short sX[2][NIMG * WG_S * WG_LD];
+struct WgLds {
+  unsigned short sY[2][2 * WG_S * WG_LD];
+  unsigned short sX[2][2 * WG_S * WG_LD];
   float srs[8][WG_T];
 };
-typedef WgLdsT<2> WgLds;
 
-// one (output tile, sample range) of dW: (ti, tj) the 128 x 128 tile of dW, z the sample range.
-// X6 (with X3 set; the sdf training's fp32-level parts): hi / mid / lo images of both operands (three
-// per buffer, WgLdsT<3>), six MFMAs per fragment pair, loads two steps ahead (registers)
-template <bool X3, bool YBF, bool XBF, bool X6 = false, class L = WgLds>
-__device__ __forceinline__ void wgrad_tile(const WGrad& g, int ti, int tj, int z, L& sm) {
-  static_assert(!X6 || X3, "X6 runs on the X3 layout");
-  constexpr int D = X6 ? 2 : WG_D;
+// one (output tile, sample range) of dW: (ti, tj) the 128 x 128 tile of dW, z the sample range
+template <bool X3, bool YBF, bool XBF>
+__device__ __forceinline__ void wgrad_tile(const WGrad& g, int ti, int tj, int z, WgLds& sm) {
+  constexpr int D = WG_D;
   constexpr int NI = X3 ? 2 : 1;
   constexpr int NH = X3 ? 1 : 2;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -858,44 +747,35 @@ __device__ __forceinline__ void wgrad_tile(const WGrad& g, int ti, int tj, int z
 #pragma unroll
             for (int q = 0; q < 4; ++q) rsum += vy[q];
           }
-          wg_store<X3, X6>((sm.sY[buf] + h * WG_S * WG_LD), (sm.sY[buf] + (NI - 1 + h) * WG_S * WG_LD), tid, vy,
-                           sm.sY[buf] + 2 * WG_S * WG_LD);
+          wg_store<X3>((sm.sY[buf] + h * WG_S * WG_LD), (sm.sY[buf] + (NI - 1 + h) * WG_S * WG_LD), tid, vy);
         }
         if constexpr (XBF) {
           wg_put_bf((sm.sX[buf] + h * WG_S * WG_LD), rx[d][h], g.K, j0, s + h * WG_S, s1, tid);
         } else {
           f32x4 vx[4];
           wg_widen<false>(rx[d][h], g.K, j0, s + h * WG_S, s1, tid, vx);
-          wg_store<X3, X6>((sm.sX[buf] + h * WG_S * WG_LD), (sm.sX[buf] + (NI - 1 + h) * WG_S * WG_LD), tid, vx,
-                           sm.sX[buf] + 2 * WG_S * WG_LD);
+          wg_store<X3>((sm.sX[buf] + h * WG_S * WG_LD), (sm.sX[buf] + (NI - 1 + h) * WG_S * WG_LD), tid, vx);
         }
       }
       __syncthreads();
       if (s + D * STEP < s1) load(d, s + D * STEP);  // this ring entry is free again: refill D steps ahead
 #pragma unroll
       for (int h = 0; h < NH; ++h) {
-        bf16x8_t fa[4], fb[4], la[4], lb[4], qa[4], qb[4];  // X6: la / lb the mid parts, qa / qb the lo parts
+        bf16x8_t fa[4], fb[4], la[4], lb[4];
 #pragma unroll
         for (int a = 0; a < 4; ++a) {
           fa[a] = wg_frag((sm.sY[buf] + h * WG_S * WG_LD), wi + 16 * a, lane);
           if constexpr (X3) la[a] = wg_frag((sm.sY[buf] + (NI - 1 + h) * WG_S * WG_LD), wi + 16 * a, lane);
-          if constexpr (X6) qa[a] = wg_frag((sm.sY[buf] + 2 * WG_S * WG_LD), wi + 16 * a, lane);
         }
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
           fb[b] = wg_frag((sm.sX[buf] + h * WG_S * WG_LD), wj + 16 * b, lane);
           if constexpr (X3) lb[b] = wg_frag((sm.sX[buf] + (NI - 1 + h) * WG_S * WG_LD), wj + 16 * b, lane);
-          if constexpr (X6) qb[b] = wg_frag((sm.sX[buf] + 2 * WG_S * WG_LD), wj + 16 * b, lane);
         }
 #pragma unroll
         for (int a = 0; a < 4; ++a)
 #pragma unroll
           for (int b = 0; b < 4; ++b) {
-            if constexpr (X6) {  // the 2^-16 terms, then the 2^-8 ones
-              acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa[a], fb[b], acc[a][b], 0, 0, 0);
-              acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a], qb[b], acc[a][b], 0, 0, 0);
-              acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(la[a], lb[b], acc[a][b], 0, 0, 0);
-            }
             if constexpr (X3) {
               acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(la[a], fb[b], acc[a][b], 0, 0, 0);
               acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a], lb[b], acc[a][b], 0, 0, 0);
@@ -923,9 +803,9 @@ __device__ __forceinline__ void wgrad_tile(const WGrad& g, int ti, int tj, int z
   }
 }
 
-template <bool X3, bool YBF, bool XBF, bool X6 = false>
+template <bool X3, bool YBF, bool XBF>
 __global__ __launch_bounds__(256) void k_wgrad(WGrad g) {
-  __shared__ __attribute__((aligned(16))) WgLdsT<X6 ? 3 : 2> sm;
+  __shared__ __attribute__((aligned(16))) WgLds sm;
   // XCD-aware order: workgroups are dealt to the 8 XCDs round-robin by linear id, so the tiles of
   // one sample range (which read the same dY and X rows) get ids on one XCD and share its L2
   // (launch_wgrad makes the range count a multiple of 8)
@@ -933,7 +813,7 @@ __global__ __launch_bounds__(256) void k_wgrad(WGrad g) {
   const int L = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
   const int slot = L >> 3, tile = slot % tiles;
   const int z = (slot / tiles) * 8 + (L & 7);
-  wgrad_tile<X3, YBF, XBF, X6>(g, tile % gridDim.x, tile / gridDim.x, z, sm);
+  wgrad_tile<X3, YBF, XBF>(g, tile % gridDim.x, tile / gridDim.x, z, sm);
 }
 
 // several weight gradients of one operand format in one launch (the layers of an MLP's backward):
@@ -1032,8 +912,7 @@ int launch_wgrad(WGrad g, int n_host, hipStream_t s) {
   g.n = n_host;
   g.rs_slab = (g.bsum || g.bsum2) ? g.slab + (size_t)WG_MAX_Z * 4 * WG_TILE_FLOATS : nullptr;
   const dim3 grid(ti, tj, g.nz);
-  if (g.x6) hipLaunchKernelGGL((k_wgrad<true, false, false, true>), grid, dim3(256), 0, s, g);
-  else if (g.x3) hipLaunchKernelGGL((k_wgrad<true, false, false>), grid, dim3(256), 0, s, g);
+  if (g.x3) hipLaunchKernelGGL((k_wgrad<true, false, false>), grid, dim3(256), 0, s, g);
   else if (g.ybf && g.xbf) hipLaunchKernelGGL((k_wgrad<false, true, true>), grid, dim3(256), 0, s, g);
   else if (g.ybf) hipLaunchKernelGGL((k_wgrad<false, true, false>), grid, dim3(256), 0, s, g);
   else if (g.xbf) hipLaunchKernelGGL((k_wgrad<false, false, true>), grid, dim3(256), 0, s, g);

@@ -93,27 +93,12 @@ struct RGemm {
   int vec_out;  // set by launch_rgemm: C (and mask) rows 16-B addressable, N % 4 == 0
   int vec16;    // set by launch_rgemm: bf16 C rows take 16-B stores (ldc % 8 == 0, C 16-B aligned)
   int x3;       // split-bf16 products (fp32-level): activations hi/lo, weights hi/lo images
-  // x6 (the sdf_pdf training's exact parts): three-way split, activations and weights hi/mid/lo (the
-  // weight image's planes lo_off apart), six bf16 MFMAs per product (~2^-24 relative: fp32 level);
-  // its epilogue also takes the sdf forward's Softplus(beta=100) with the derivative rows and div_post
-  int x6;
-  int softplus;
-  float* deriv;
-  long ldd;
-  float div_post;
   // bf16 storage (training precision 'bf16': every consumer rounds these to bf16 anyway): A rows,
   // C rows (RNE from the fp32 result) and the mask rows hold bf16 (C / mask reinterpreted as
   // unsigned short*). Not with x3; C bf16 excludes accumulate.
   int abf, cbf, mbf;
 };
 void launch_rgemm(const RGemm& g, int M_host, hipStream_t s);
-// x6 image of a GEMM's B operand for the row GEMM: image[n][col_s + k] = B_s[k * b_rs_s + n * b_cs_s]
-// (k < K_s, n < N; a layer's W for the forward, its transpose for the input gradient), segments
-// padded to 64 columns, planes hi / mid / lo of N x ldb bf16 elements each (plane stride N * ldb)
-long rimg_x6_ldb(int nseg, const int* K);
-long rimg_x6_elems(int N, int nseg, const int* K);
-int rimg_x6_pack(int N, int nseg, const float* const* B, const long* b_rs, const long* b_cs, const int* K,
-                 unsigned short* dst, hipStream_t s);
 // bf16 weight images of the training GEMM weights: forward (rows = outputs, k = used input columns,
 // segments padded to 64) and backward (rows = input columns, k = outputs padded to 64). t: the
 // ANR_NUM_TENSORS network tensors followed by the ANR_NUM_NOVEL_TENSORS novel_pose_bw tensors
@@ -151,7 +136,6 @@ struct WGrad {
   int spb, nz, tiles, tj;
   int x3;  // split-bf16 products (fp32-level)
   int ybf, xbf;  // dY / X rows hold bf16 (reinterpreted as unsigned short*), not with x3
-  int x6;        // three-way split products (fp32 level), launch_wgrad only (not in groups)
 };
 size_t wgrad_slab_floats();
 int launch_wgrad(WGrad g, int n_host, hipStream_t s);
