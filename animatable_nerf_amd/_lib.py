@@ -20,7 +20,7 @@ NUM_NOVEL_TENSORS = 19
 NUM_SDF_TENSORS = 63
 
 EXPORTS = ('anr_near_far', 'anr_params_packed_bytes', 'anr_params_pack', 'anr_render_workspace_bytes',
-           'anr_render_fwd', 'anr_render_counts', 'anr_render_bw_rows', 'anr_profile_enable', 'anr_profile_read',
+           'anr_render_fwd', 'anr_render_counts', 'anr_render_bw_rows', 'anr_render_row_ids', 'anr_profile_enable', 'anr_profile_read',
            'anr_train_workspace_bytes', 'anr_train_fwd', 'anr_train_bwd', 'anr_train_step', 'anr_adam',
            'anr_camera_rays_workspace_bytes', 'anr_camera_rays', 'anr_sdf_render_workspace_bytes', 'anr_sdf_render_fwd', 'anr_sdf_render_counts', 'anr_sdf_render_rows',
            'anr_alpha_workspace_bytes', 'anr_alpha_points', 'anr_alpha_counts', 'anr_mc_workspace_bytes',
@@ -76,8 +76,12 @@ REDUCE_MIN_U64, REDUCE_MAX_U64, REDUCE_SUM_F32 = 0, 1, 2  # anr_train_hooks.redu
 
 
 class TrainHooks(ctypes.Structure):
-    _fields_ = [('nerf_grads_ready', ctypes.c_void_p), ('ray_offset', ctypes.c_int), ('reduce', REDUCE_FN),
-                ('reduce_user', ctypes.c_void_p)]
+    """anr_train_hooks (ANR_TRAIN_HOOKS_VERSION 2): struct_size is filled in by the constructor."""
+    _fields_ = [('struct_size', ctypes.c_size_t), ('nerf_grads_ready', ctypes.c_void_p), ('ray_offset', ctypes.c_int),
+                ('reduce', REDUCE_FN), ('reduce_user', ctypes.c_void_p)]
+
+    def __init__(self, *args, **kw):
+        super().__init__(ctypes.sizeof(TrainHooks), *args, **kw)
 
 
 class AlphaOpts(ctypes.Structure):
@@ -124,6 +128,7 @@ def load():
     lib.anr_render_counts.restype = P
     lib.anr_render_counts.argtypes = [P, ctypes.c_int]
     lib.anr_render_bw_rows.argtypes = [P, ctypes.c_int, P, P, P]
+    lib.anr_render_row_ids.argtypes = [P, ctypes.c_int, P, P]
     lib.anr_train_workspace_bytes.restype = ctypes.c_size_t
     lib.anr_train_workspace_bytes.argtypes = [ctypes.c_int, ctypes.POINTER(RenderOpts), ctypes.POINTER(Frame)]
     lib.anr_train_fwd.argtypes = [ctypes.POINTER(Params), ctypes.POINTER(Frame), P, P, P, P, ctypes.c_int,

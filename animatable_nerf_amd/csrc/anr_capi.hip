@@ -254,7 +254,7 @@ int stage_composite(const float* near_, const float* far_, int R, const anr_rend
 
 extern "C" {
 
-int anr_version(void) { return 1; }
+int anr_version(void) { return 2; }  // 2: anr_train_hooks.struct_size
 
 const char* anr_last_error(void) { return g_err.c_str(); }
 
@@ -518,6 +518,16 @@ int anr_render_bw_rows(const void* workspace, int n_rays, float* pbw, float* tbw
                      (const int*)(ws + L.counts), (const float4*)(ws + L.pbw_rows), (const float4*)(ws + L.tbw_rows),
                      (float4*)pbw, (float4*)tbw);
   return check_launch("k_gather_rows");
+}
+
+int anr_render_row_ids(const void* workspace, int n_rays, int32_t* ids, void* stream) {
+  if (!workspace || n_rays <= 0 || !ids) return fail(ANR_E_ARG, "anr_render_row_ids: bad arguments");
+  const Layout L = layout(n_rays, 1, 0, 0, false);
+  const char* ws = (const char*)workspace;
+  const long N = (long)n_rays * 64;
+  hipLaunchKernelGGL(k_row_ids, dim3((int)((N + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     (const int*)(ws + L.out_row), (const int*)(ws + L.counts), (const int*)(ws + L.list), (int*)ids);
+  return check_launch("k_row_ids");
 }
 
 }  // extern "C"

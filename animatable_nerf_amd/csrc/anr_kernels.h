@@ -175,6 +175,7 @@ __global__ void k_flag_count(AlphaArgs a);
 __global__ void k_flag_force(AlphaArgs a, int nchunks);
 __global__ void k_flag_scatter(AlphaArgs a);
 __global__ void k_gather_rows(const int*, const int*, const float4*, const float4*, float4*, float4*);
+__global__ void k_row_ids(const int*, const int*, const int*, int*);
 __global__ void k_composite(CompositeArgs a);
 __global__ void k_prep(PrepArgs a);
 __global__ void k_mlp(MlpArgs a);

@@ -535,6 +535,15 @@ __global__ __launch_bounds__(256) void k_gather_rows(const int* __restrict__ out
   tbw[(size_t)r * 6 + j] = tbw_rows[(size_t)i * 6 + j];
 }
 
+// sample id (ray * 64 + sample) of every alpha_ind output row: the row order of k_gather_rows
+__global__ __launch_bounds__(256) void k_row_ids(const int* __restrict__ out_row, const int* __restrict__ n_kept,
+                                                 const int* __restrict__ list, int* __restrict__ ids) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= *n_kept) return;
+  const int r = out_row[i];
+  if (r >= 0) ids[r] = list[i];
+}
+
 // ------------------------------------------------------------------------------------------
 // A12 compositing: wave per ray; exclusive product scan of (1 - alpha + 1e-10) across lanes
 // ------------------------------------------------------------------------------------------

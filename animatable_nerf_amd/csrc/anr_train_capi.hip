@@ -144,17 +144,21 @@ int order(SideStreams* ss, hipStream_t to, hipStream_t from) {
 }
 
 // A training entry point runs on the library's own main stream, forked from the caller's stream on
-// entry and joined back into it on exit (also on an error return), so that every cross-stream
-// dependency inside the call is between the library's non-blocking streams. Measured: with the caller
-// on the legacy default stream, the grouped weight gradients of the blend-weight MLPs read gradient
-// rows that were not yet written (NaN from a previous run's workspace, tools/nan_probe.py), although
-// every event edge was in place; the same steps on a non-default caller stream were exact.
+// entry and joined back into it on exit (also on an error return). Round 4 introduced it after the
+// grouped weight gradients read unwritten gradient rows (NaN, tools/nan_probe.py) whenever the caller
+// was the legacy default stream. The cause (found in round 5) was not the stream kind: Exec::pend_src
+// marked "no queued source stream" with nullptr, which is also the legacy default stream's handle, so a
+// product queued from stream 0 never recorded its source and flush_w() issued the group on lane 0 with
+// no edge after stream 0. pend_src now carries an explicit count (npsrc). The fork stays (one event each
+// way) so that the library's streams never wait on a blocking caller stream; ANR_TRAIN_ON_CALLER=1
+// (read per call) bypasses it, which tests/test_gpu_train.py uses to run the grouped path on stream 0.
 struct OnMain {
   SideStreams* ss;
   hipStream_t caller, s;
   int rc = ANR_OK;
   OnMain(SideStreams* x, hipStream_t c) : ss(x), caller(c), s(c) {
-    if (ss && ss->main) {
+    const char* oc = getenv("ANR_TRAIN_ON_CALLER");
+    if (ss && ss->main && !(oc && oc[0] == '1')) {
       rc = order(ss, ss->main, caller);
       s = ss->main;
     }
@@ -193,7 +197,8 @@ struct Exec {
   int flush_every = 8;
   WGrad pend[WG_GROUP_MAX];
   int npend = 0;
-  hipStream_t pend_src[2] = {};
+  hipStream_t pend_src[2] = {};  // streams the queued products were issued from (any handle, 0 included)
+  int npsrc = 0;
   struct LatentPost {
     const float* ys;
     const float* W;
@@ -226,7 +231,7 @@ struct Exec {
   int flush_w() {
     if (!npend && !npost) return ANR_OK;
     hipStream_t w = ss ? ss->sw[0] : s;
-    for (int i = 0; i < 2 && pend_src[i]; ++i) ANR_TRY(order(ss, w, pend_src[i]));
+    for (int i = 0; i < npsrc; ++i) ANR_TRY(order(ss, w, pend_src[i]));
     if (npend && launch_wgrad_group(pend, npend, grid_n(), group_nz, slab(0), lane_floats, w) != 0)
       return check_launch("k_wgrad_group");
     for (int i = 0; i < npost; ++i) {
@@ -235,8 +240,24 @@ struct Exec {
                          q.add, q.gW, q.gtab);
       ANR_TRY(check_launch("k_tr_latent_grad"));
     }
-    npend = npost = 0;
-    pend_src[0] = pend_src[1] = nullptr;
+    npend = npost = npsrc = 0;
+    return ANR_OK;
+  }
+  // Queued products read their dY / X rows when the group is flushed, not when queued: an output about
+  // to be written over rows a queued product still has to read flushes the queue first (the executor's
+  // buffers are laid out so that this never triggers today; it keeps a later buffer reuse correct).
+  static bool overlaps(const void* a, size_t na, const void* b, size_t nb) {
+    return a && b && (const char*)a < (const char*)b + nb && (const char*)b < (const char*)a + na;
+  }
+  int guard_pending(const void* out, long ld, bool obf) {
+    if (!npend || !out) return ANR_OK;
+    const size_t rows = (size_t)grid_n(), ob = rows * (size_t)ld * (obf ? 2 : 4);
+    for (int i = 0; i < npend; ++i) {
+      const WGrad& q = pend[i];
+      if (overlaps(out, ob, q.dY, rows * (size_t)q.ldY * (q.ybf ? 2 : 4)) ||
+          overlaps(out, ob, q.X, rows * (size_t)q.ldX * (q.xbf ? 2 : 4)))
+        return flush_w();
+    }
     return ANR_OK;
   }
   // zero the column-sum scratch ys (on s, ahead of the products queued after it) and update the latent
@@ -311,6 +332,7 @@ struct Exec {
   int fwd(float* Y, int ldY, int Nout, const float* W, int in_ch, const float* bias, bool relu, const float* X0, int ld0,
           int K0, int c0, const float* X1 = nullptr, int ld1 = 0, int K1 = 0, int c1 = 0, unsigned bf = 0) {
     const bool abf = bf & BF_A;
+    ANR_TRY(guard_pending(Y, ldY, bf & BF_C));
     if ((bf16 || x3) && wimg && Nout <= 256 && !(x3 && bf)) {
       RGemm r{};
       r.x3 = bf16 ? 0 : 1;
@@ -351,9 +373,9 @@ struct Exec {
     }
     if (fast && group) {
       if (npend == WG_GROUP_MAX || (flush_every > 0 && npend >= flush_every)) ANR_TRY(flush_w());
-      if (pend_src[0] != s && pend_src[1] != s) {
-        if (pend_src[0] && pend_src[1]) ANR_TRY(flush_w());
-        pend_src[pend_src[0] ? 1 : 0] = s;
+      if (!(npsrc > 0 && pend_src[0] == s) && !(npsrc > 1 && pend_src[1] == s)) {
+        if (npsrc == 2) ANR_TRY(flush_w());
+        pend_src[npsrc++] = s;
       }
       pend[npend++] = wg;
       ++nqueued;
@@ -387,6 +409,7 @@ struct Exec {
             const float* mask, int ldm, bool accumulate, const float* dY2 = nullptr, int ldY2 = 0, int Nout2 = 0,
             const float* W2 = nullptr, int in_ch2 = 0, unsigned bf = 0) {
     const bool abf = bf & BF_A;
+    ANR_TRY(guard_pending(dX, ldX, bf & BF_C));
     if ((bf16 || x3) && wimg && K <= 256 && !(x3 && bf) && !((bf & BF_C) && accumulate)) {
       RGemm r{};
       r.x3 = bf16 ? 0 : 1;
@@ -1066,6 +1089,8 @@ int anr_train_step_hooked(const anr_params* p, float* const* grads, const anr_fr
   hipStream_t s = (hipStream_t)stream;
   char* ws = (char*)workspace;
   SideStreams* ss = side_streams();
+  if (hooks && hooks->struct_size != sizeof(anr_train_hooks))
+    return fail(ANR_E_ARG, "anr_train_step_hooked: hooks->struct_size != sizeof(anr_train_hooks) (header version mismatch)");
   hipEvent_t nerf_done = hooks ? (hipEvent_t)hooks->nerf_grads_ready : nullptr;
   RaySplit split{};
   const bool splitting = hooks && hooks->reduce;

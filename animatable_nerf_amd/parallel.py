@@ -194,13 +194,15 @@ def gather_rows(t, group=None):
     return torch.cat([p[:, :k] for p, k in zip(parts, ns)], dim=1)
 
 
-def render_sharded(renderer, batch, chunk=2048, group=None):
+def render_sharded(renderer, batch, chunk=2048, group=None, rows=False):
     """Renderer.render_device over a whole frame with its rays split across the ranks by whole
-    reference chunks (so every per-chunk argmin / argmax is the single-GPU one); every output key of
-    the reference's render dict is gathered to every rank in frame order: the per-ray maps and 'raw'
-    by rays, the row outputs (aninerf 'pbw' / 'tbw' alpha_ind rows; sdf_pdf 'resd' / 'gradients' kept
-    rows and the per-chunk 'msk_sdf' / 'msk_label' lists) concatenated in rank order, which is chunk
-    order. 'span' = this rank's rays [start, end)."""
+    reference chunks (so every per-chunk argmin / argmax is the single-GPU one); the output keys of
+    the reference's render dict are gathered to every rank in frame order: the per-ray maps and 'raw'
+    by rays, and the per-chunk sdf_pdf 'msk_sdf' / 'msk_label' lists concatenated in rank order, which
+    is chunk order. The large row outputs (aninerf 'pbw' / 'tbw' alpha_ind rows, sdf_pdf 'resd' /
+    'gradients' kept rows: ~1.1 GB per 512x512 frame, padded to the largest rank's count by the
+    all-gather) are gathered only when rows=True; otherwise each rank keeps its own shard's rows
+    under 'pbw_local' etc. 'span' = this rank's rays [start, end)."""
     rank = dist.get_rank(group) if is_dist() else 0
     world = dist.get_world_size(group) if is_dist() else 1
     R = int(batch['ray_o'].shape[1])
@@ -231,8 +233,12 @@ def render_sharded(renderer, batch, chunk=2048, group=None):
             v = out[k].reshape(1, -1, ns * w)
             ret[k] = gather_rays(v, R, world, chunk, group).reshape(1, -1, w)
     for k in ('pbw', 'tbw', 'resd', 'gradients', 'msk_sdf', 'msk_label'):
-        if k in out:
+        if k not in out:
+            continue
+        if rows or k in ('msk_sdf', 'msk_label'):
             ret[k] = gather_rows(out[k], group)
+        else:
+            ret[k + '_local'] = out[k]
     ret['span'] = (s, e)
     return ret
 

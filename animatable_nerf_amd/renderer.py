@@ -178,6 +178,16 @@ class Renderer:
                        'anr_render_bw_rows')
         return pbw, tbw
 
+    def row_ids(self, n_rays):
+        """Sample ids (ray * N_samples + sample) of the alpha_ind rows of the last evaluation render, (m,)
+        int64 on the device, in row order (anr_render_row_ids)."""
+        _, m = self._counts(self._ws, n_rays)
+        ids = torch.empty((m,), dtype=torch.int32, device=self._ws.device)
+        if m > 0:
+            _lib.check(self.lib.anr_render_row_ids(_lib.ptr(self._ws), n_rays, _lib.ptr(ids),
+                                                   _lib.stream_ptr(self._ws.device)), 'anr_render_row_ids')
+        return ids.long()
+
     def _t_rand(self, R, dev, t_rand):
         if t_rand is None and self.cfg.perturb > 0 and self.net.training:
             t_rand = torch.rand((R, int(self.cfg.N_samples)), device=dev)

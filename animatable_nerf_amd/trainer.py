@@ -250,10 +250,17 @@ class FusedStep:
             else:
                 reduce_keys_(view, op, self.group)
             return 0
-        except Exception:  # pragma: no cover - reported through the library's error code
+        except BaseException:  # pragma: no cover - fatal to the job
+            # The peer ranks are already waiting in the matching collective, so returning an error to the
+            # library (which would abort only this rank's step) would leave them hung. A failed exchange is
+            # fatal: report it and end this process non-zero, so the launcher (torchrun) tears the job down.
+            import os
+            import sys
             import traceback
             traceback.print_exc()
-            return 1
+            sys.stderr.write('anr_train_hooks.reduce failed on this rank: exiting so the peer ranks do not hang\n')
+            sys.stderr.flush()
+            os._exit(70)
 
     def _split_share(self, batch, t_rand):
         """this rank's rays of the (replicated) batch and their offset within it"""

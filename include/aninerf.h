@@ -187,6 +187,9 @@ int anr_render_fwd(const anr_params* p, const anr_frame* f, const float* ray_o, 
 const int32_t* anr_render_counts(const void* workspace, int n_rays);
 /* Gather the m alpha_ind rows of pbw / tbw (each (m,24)) after the counts were read. */
 int anr_render_bw_rows(const void* workspace, int n_rays, float* pbw, float* tbw, void* stream);
+/* The sample id (ray * N_samples + sample, frame order) of each of the m alpha_ind rows, ids (m) int32:
+ * which samples tpose_nerf_network.py:192-196 selected (rows compared by sample in tests). */
+int anr_render_row_ids(const void* workspace, int n_rays, int32_t* ids, void* stream);
 
 /* ---- Network.forward over free samples (tpose_nerf_network.py:139-215) ----------------------
  * The call a reference renderer makes per chunk, self.net(wpts, viewdir, dists, batch)
@@ -264,7 +267,12 @@ typedef int (*anr_reduce_fn)(void* user, void* device_buf, int count, int op, vo
 #define ANR_REDUCE_MIN_U64 0 /* unsigned 64-bit keys, min over ranks (all-ones = empty) */
 #define ANR_REDUCE_MAX_U64 1 /* unsigned 64-bit keys, max over ranks */
 #define ANR_REDUCE_SUM_F32 2 /* float sums over ranks */
+/* struct_size must be sizeof(anr_train_hooks) (ANR_TRAIN_HOOKS_VERSION 2, anr_version() >= 2): the struct
+ * grew from version 1's single nerf_grads_ready field, and a caller built against another layout is
+ * rejected with ANR_E_ARG instead of having its memory read as the newer fields. */
+#define ANR_TRAIN_HOOKS_VERSION 2
 typedef struct anr_train_hooks {
+  size_t struct_size;
   void* nerf_grads_ready;
   /* Ray split of ONE reference chunk over ranks (north_star "rays-per-iteration shard"; strong scaling of
    * a 1,024-ray step): this call's rays are rays [ray_offset, ray_offset + n_rays) of a

@@ -34,7 +34,8 @@ def test_library_exports_every_declared_symbol(lib):
 
 
 def test_version_and_sizes(lib):
-    assert lib.anr_version() == 1
+    assert lib.anr_version() == 2
+    assert _lib.TrainHooks().struct_size == ctypes.sizeof(_lib.TrainHooks) == 40
     # 19 weight layers + view/rgb heads, fp32 weight image + padded biases
     # + 9 novel_pose_bw layers (same image as the 9 BW layers)
     # + alpha_fc alone (layer 30, the mesh path's density program): 64 k-steps x 1 KiB, 16 biases

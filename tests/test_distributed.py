@@ -117,9 +117,15 @@ def _shard_worker(rank, world, port, n, q):
     try:
         parallel.init_from_env('gloo')
         b = _frame(n)
-        ret = parallel.render_sharded(_FakeRenderer(), b)
+        ret = parallel.render_sharded(_FakeRenderer(), b, rows=True)
         full = _FakeRenderer().render_device(b)
         ok = all(torch.equal(ret[k], full[k]) for k in ('rgb_map', 'acc_map', 'depth_map', 'raw', 'pbw', 'tbw'))
+        # default: the row outputs stay on their rank (no world-sized all-gather of the ~1 GB rows)
+        lean = parallel.render_sharded(_FakeRenderer(), b)
+        ok = ok and 'pbw' not in lean and 'tbw' not in lean and torch.equal(lean['rgb_map'], full['rgb_map'])
+        mine = _FakeRenderer().render_device(parallel.shard_batch(b, rank, world, 2048)[0]) if ret['span'][1] > \
+            ret['span'][0] else None
+        ok = ok and (mine is None or torch.equal(lean['pbw_local'], mine['pbw']))
         s, e = ret['span']
         ok = ok and (s, e) == parallel.shard_chunks(n, rank, world)
         psnr = parallel.psnr_sharded(full['rgb_map'][:, s:e], b['rgb'][:, s:e])
@@ -240,7 +246,7 @@ def _sdf_shard_worker(rank, world, port, n, q):
         b['tbounds'] = torch.tensor([[[-0.3, -0.9, -0.2], [0.3, 0.9, 0.2]]])
         full_b = {k: v.clone() for k, v in b.items()}
         full = _FakeSdfRenderer().render_device(full_b)
-        ret = parallel.render_sharded(_FakeSdfRenderer(), b)
+        ret = parallel.render_sharded(_FakeSdfRenderer(), b, rows=True)
         ok = all(torch.equal(ret[k], full[k]) for k in ('rgb_map', 'acc_map', 'depth_map', 'raw', 'sdf', 'resd',
                                                          'gradients', 'msk_sdf', 'msk_label'))
         ok = ok and torch.equal(b['tbounds'], full_b['tbounds'])

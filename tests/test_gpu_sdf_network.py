@@ -50,7 +50,7 @@ def _net(dev, precision='fp32'):
     return net
 
 
-@pytest.mark.parametrize('precision', ['fp32', 'bf16x3'])
+@pytest.mark.parametrize('precision', ['fp32', 'bf16x3', 'bf16x6'])
 def test_g6_network_forward_in_chunk_loop(dev, precision):
     """eval (no grad): tpose_renderer.get_pixel_value's sampling around net(wpts, viewdir, dists, batch)"""
     g = golden('g6_sdf_tiny')
@@ -79,8 +79,8 @@ def test_g6_network_forward_in_chunk_loop(dev, precision):
     assert np.array_equal(bt['tbounds'].cpu().numpy(), g['tbounds_after'])  # widened once (one chunk)
 
 
-@pytest.mark.parametrize('n', [30, 700])
-def test_network_forward_free_points_match_oracle(dev, n):
+@pytest.mark.parametrize('n,precision', [(30, 'fp32'), (700, 'fp32'), (700, 'bf16x6')])
+def test_network_forward_free_points_match_oracle(dev, n, precision):
     """arbitrary free samples (a partial 64-group; n < 45 takes torch's small-matmul path for world ->
     pose and the view directions), forced argmin over the call, tbounds widened once per call"""
     sc = pdf_scene()
@@ -95,7 +95,7 @@ def test_network_forward_free_points_match_oracle(dev, n):
     bc = to_torch(b)
     with torch.no_grad():
         ref = restate_sdf.network_forward(oracle_params_sdf(), wpts, vd, dists, bc)
-    net = _net(dev)
+    net = _net(dev, precision)
     for call in range(2):  # a second call sees the bounds the first widened
         with torch.no_grad():
             ret = net(wpts.to(dev), vd.to(dev), dists.to(dev), bt)
