@@ -20,7 +20,7 @@ NUM_NOVEL_TENSORS = 19
 NUM_SDF_TENSORS = 63
 
 EXPORTS = ('anr_near_far', 'anr_params_packed_bytes', 'anr_params_pack', 'anr_render_workspace_bytes',
-           'anr_render_fwd', 'anr_render_counts', 'anr_render_bw_rows', 'anr_render_row_ids', 'anr_profile_enable', 'anr_profile_read',
+           'anr_render_fwd', 'anr_render_counts', 'anr_render_bw_rows', 'anr_render_row_ids', 'anr_profile_enable', 'anr_profile_read', 'anr_profile_read_clock',
            'anr_train_workspace_bytes', 'anr_train_fwd', 'anr_train_bwd', 'anr_train_step', 'anr_adam',
            'anr_camera_rays_workspace_bytes', 'anr_camera_rays', 'anr_sdf_render_workspace_bytes', 'anr_sdf_render_fwd', 'anr_sdf_render_counts', 'anr_sdf_render_rows',
            'anr_alpha_workspace_bytes', 'anr_alpha_points', 'anr_alpha_counts', 'anr_mc_workspace_bytes',
@@ -32,7 +32,8 @@ EXPORTS = ('anr_near_far', 'anr_params_packed_bytes', 'anr_params_pack', 'anr_re
            'anr_sdf_train_workspace_bytes', 'anr_sdf_train_step', 'anr_sdf_render_knn',
            'anr_sdf_network_workspace_bytes', 'anr_sdf_network_fwd', 'anr_sdf_network_counts', 'anr_sdf_network_rows',
            'anr_sdf_network_train_workspace_bytes', 'anr_sdf_network_train_fwd', 'anr_sdf_network_train_counts',
-           'anr_sdf_network_train_rows', 'anr_sdf_network_train_bwd',
+           'anr_sdf_network_train_rows', 'anr_sdf_network_train_bwd', 'anr_sdf_points_workspace_bytes', 'anr_sdf_points',
+           'anr_sample_volume', 'anr_knn_blend_workspace_bytes', 'anr_knn_blend', 'anr_sdf_mesh_pose',
            'anr_last_error', 'anr_version')
 
 c_float_p = ctypes.c_void_p
@@ -72,6 +73,7 @@ class Samples(ctypes.Structure):
 
 
 REDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p)
+SDFP_NETWORK, SDFP_GRADIENT, SDFP_DEFORMED_GRADIENT = 0, 1, 2  # anr_sdf_points modes
 REDUCE_MIN_U64, REDUCE_MAX_U64, REDUCE_SUM_F32 = 0, 1, 2  # anr_train_hooks.reduce ops
 
 
@@ -172,6 +174,14 @@ def load():
     lib.anr_sdf_network_train_rows.argtypes = [P, ctypes.c_int, P, P, P, P]
     lib.anr_sdf_network_train_bwd.argtypes = [SP, ctypes.c_void_p * NUM_SDF_TENSORS, SF, SS, ctypes.POINTER(RenderOpts),
                                               P, P, P, P, P, P, ctypes.c_size_t, P]
+    lib.anr_sdf_points_workspace_bytes.restype = ctypes.c_size_t
+    lib.anr_sdf_points_workspace_bytes.argtypes = [ctypes.c_int]
+    lib.anr_sdf_points.argtypes = [SP, SF, P, ctypes.c_int, ctypes.c_int, P, P, P, ctypes.c_size_t, P]
+    lib.anr_sample_volume.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P, ctypes.c_int, P, P]
+    lib.anr_knn_blend_workspace_bytes.restype = ctypes.c_size_t
+    lib.anr_knn_blend_workspace_bytes.argtypes = [ctypes.c_int]
+    lib.anr_knn_blend.argtypes = [P, P, ctypes.c_int, P, ctypes.c_int, ctypes.c_float, P, P, P, ctypes.c_size_t, P]
+    lib.anr_sdf_mesh_pose.argtypes = [P, P, ctypes.c_int, P, P, P, P, P, P]
     lib.anr_camera_rays_workspace_bytes.restype = ctypes.c_size_t
     lib.anr_camera_rays_workspace_bytes.argtypes = [ctypes.c_int, ctypes.c_int]
     D = ctypes.POINTER(ctypes.c_double)
@@ -215,6 +225,8 @@ def load():
     lib.anr_canonical_alpha.argtypes = [PP, P, ctypes.c_int, P, P, ctypes.c_size_t, P]
     lib.anr_profile_enable.argtypes = [ctypes.c_int]
     lib.anr_profile_read.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]
+    lib.anr_profile_read_clock.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int),
+                                           ctypes.POINTER(ctypes.c_double)]
     lib.anr_last_error.restype = ctypes.c_char_p
     for name in EXPORTS:
         getattr(lib, name)

@@ -4,6 +4,6 @@
 
 namespace anr {
 
-__global__ __launch_bounds__(512) void k_alpha(MlpArgs a) { alpha_body<false>(a); }
+__global__ __launch_bounds__(512) void k_alpha(MlpArgs a) { ANR_STAMPED(alpha_body<false>(a);); }
 
 }  // namespace anr

@@ -4,6 +4,6 @@
 
 namespace anr {
 
-__global__ __launch_bounds__(512) void k_alpha_b16(MlpArgs a) { alpha_body<true>(a); }
+__global__ __launch_bounds__(512) void k_alpha_b16(MlpArgs a) { ANR_STAMPED(alpha_body<true>(a);); }
 
 }  // namespace anr

@@ -1,6 +1,7 @@
 // anr_capi.hip — the C-ABI (include/aninerf.h): argument checks, workspace layout, launch order.
 // All launches are asynchronous on the caller's stream; no allocation, no synchronisation, so a
 // caller may capture a whole render into a hipGraph.
+#include <algorithm>
 #include <string>
 #include <utility>
 #include <vector>
@@ -47,16 +48,48 @@ int num_cus() {
 
 bool mlp_attr_set = false;
 
-// measurement: event pairs around k_mlp (anr_profile_enable / anr_profile_read)
+// measurement: event pairs around the fused network launches (anr_profile_enable / anr_profile_read),
+// and each launch's per-workgroup clock stamps (MlpArgs::clk) in a device arena of kProfSlots slots
+constexpr int kProfSlots = 512, kProfGroups = 1024;
 struct Prof {
   bool on = false;
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
+  std::vector<anr::ProfSlot> slot;
+  std::vector<int> groups;  // workgroups stamped per used slot
   size_t used = 0;
+  unsigned long long* arena = nullptr;
 } g_prof;
 
 }  // namespace
 
 namespace anr {
+
+ProfSlot* prof_begin(hipStream_t s, int grid) {
+  if (!g_prof.on) return nullptr;
+  if (!g_prof.arena &&
+      hipMalloc((void**)&g_prof.arena, (size_t)kProfSlots * kProfGroups * 4 * sizeof(unsigned long long)) != hipSuccess) {
+    g_prof.arena = nullptr;
+    (void)hipGetLastError();
+  }
+  if (g_prof.used == g_prof.slot.size()) {
+    ProfSlot q{};
+    if (hipEventCreate(&q.b) != hipSuccess || hipEventCreate(&q.e) != hipSuccess) return nullptr;
+    g_prof.slot.push_back(q);
+    g_prof.groups.push_back(0);
+  }
+  const size_t i = g_prof.used++;
+  ProfSlot* q = &g_prof.slot[i];
+  q->clk = g_prof.arena && i < (size_t)kProfSlots && grid <= kProfGroups
+               ? g_prof.arena + i * (size_t)kProfGroups * 4 : nullptr;
+  g_prof.groups[i] = q->clk ? grid : 0;
+  if (q->clk && hipMemsetAsync(q->clk, 0, (size_t)grid * 4 * sizeof(unsigned long long), s) != hipSuccess) return nullptr;
+  if (hipEventRecord(q->b, s) != hipSuccess) return nullptr;
+  return q;
+}
+
+int prof_end(ProfSlot* q, hipStream_t s) {
+  if (q && hipEventRecord(q->e, s) != hipSuccess) return fail(ANR_E_HIP, "hipEventRecord failed");
+  return ANR_OK;
+}
 
 // A2-A6 + per-frame prep: memsets, volumes/folds, front-end, ordered compaction (counts[0] = n')
 int RaySplit::run(void* buf, int count, int op, hipStream_t s) const {
@@ -190,23 +223,13 @@ int stage_mlp(const anr_params* p, const anr_frame* f, const float* ray_o, const
   }
   const long max_tiles = (N + 127) / 128;
   const int grid = (int)(max_tiles < num_cus() ? max_tiles : num_cus());
-  std::pair<hipEvent_t, hipEvent_t>* evp = nullptr;
-  if (g_prof.on) {
-    if (g_prof.used == g_prof.ev.size()) {
-      hipEvent_t a = nullptr, b = nullptr;
-      if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess)
-        return fail(ANR_E_HIP, "hipEventCreate failed");
-      g_prof.ev.emplace_back(a, b);
-    }
-    evp = &g_prof.ev[g_prof.used++];
-    if (hipEventRecord(evp->first, s) != hipSuccess) return fail(ANR_E_HIP, "hipEventRecord failed");
-  }
+  ProfSlot* ps = prof_begin(s, grid);
+  ma.clk = ps ? ps->clk : nullptr;
   if (x6) hipLaunchKernelGGL(k_mlp_x6, dim3(grid), dim3(512), lds, s, ma);
   else if (b16) hipLaunchKernelGGL(k_mlp_b16, dim3(grid), dim3(512), lds, s, ma);
   else hipLaunchKernelGGL(k_mlp, dim3(grid), dim3(512), lds, s, ma);
   ANR_TRY(check_launch("k_mlp"));
-  if (evp && hipEventRecord(evp->second, s) != hipSuccess) return fail(ANR_E_HIP, "hipEventRecord failed");
-  return ANR_OK;
+  return prof_end(ps, s);
 }
 
 // A11 alpha_ind rows: sigma' > train_th plus per-chunk argmax (counts[1] = m)
@@ -493,20 +516,42 @@ int anr_profile_enable(int on) {
   return ANR_OK;
 }
 
-int anr_profile_read(double* mlp_ms, int* launches) {
+int anr_profile_read_clock(double* mlp_ms, int* launches, double* clk_mhz) {
   double tot = 0.0;
+  std::vector<double> mhz;
+  std::vector<unsigned long long> h;
   for (size_t i = 0; i < g_prof.used; ++i) {
-    if (hipEventSynchronize(g_prof.ev[i].second) != hipSuccess) return fail(ANR_E_HIP, "hipEventSynchronize failed");
+    const ProfSlot& q = g_prof.slot[i];
+    if (hipEventSynchronize(q.e) != hipSuccess) return fail(ANR_E_HIP, "hipEventSynchronize failed");
     float ms = 0.f;
-    if (hipEventElapsedTime(&ms, g_prof.ev[i].first, g_prof.ev[i].second) != hipSuccess)
-      return fail(ANR_E_HIP, "hipEventElapsedTime failed");
+    if (hipEventElapsedTime(&ms, q.b, q.e) != hipSuccess) return fail(ANR_E_HIP, "hipEventElapsedTime failed");
     tot += ms;
+    const int ng = g_prof.groups[i];
+    if (clk_mhz && q.clk && ng > 0) {
+      h.resize((size_t)ng * 4);
+      if (hipMemcpy(h.data(), q.clk, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
+        return fail(ANR_E_HIP, "hipMemcpy (clock stamps) failed");
+      for (int g = 0; g < ng; ++g) {
+        const unsigned long long* c = &h[(size_t)g * 4];
+        // a workgroup that ran at least 1 ms (100,000 realtime ticks) of its own
+        if (c[2] > c[0] && c[3] > c[1] + 100000) mhz.push_back((double)(c[2] - c[0]) / (double)(c[3] - c[1]) * 100.0);
+      }
+    }
   }
   if (mlp_ms) *mlp_ms = tot;
   if (launches) *launches = (int)g_prof.used;
+  if (clk_mhz) {
+    *clk_mhz = 0.0;
+    if (!mhz.empty()) {
+      std::nth_element(mhz.begin(), mhz.begin() + mhz.size() / 2, mhz.end());
+      *clk_mhz = mhz[mhz.size() / 2];
+    }
+  }
   g_prof.used = 0;
   return ANR_OK;
 }
+
+int anr_profile_read(double* mlp_ms, int* launches) { return anr_profile_read_clock(mlp_ms, launches, nullptr); }
 
 int anr_render_bw_rows(const void* workspace, int n_rays, float* pbw, float* tbw, void* stream) {
   if (!workspace || n_rays <= 0 || !pbw || !tbw) return fail(ANR_E_ARG, "anr_render_bw_rows: bad arguments");
@@ -518,6 +563,16 @@ int anr_render_bw_rows(const void* workspace, int n_rays, float* pbw, float* tbw
                      (const int*)(ws + L.counts), (const float4*)(ws + L.pbw_rows), (const float4*)(ws + L.tbw_rows),
                      (float4*)pbw, (float4*)tbw);
   return check_launch("k_gather_rows");
+}
+
+int anr_sample_volume(const float* vol, int X, int Y, int Z, int C, const float* bounds, const float* pts, int n,
+                      float* out, void* stream) {
+  if (!vol || !bounds || !pts || !out || X <= 0 || Y <= 0 || Z <= 0 || C <= 0 || n < 0)
+    return fail(ANR_E_ARG, "anr_sample_volume: bad arguments");
+  if (n == 0) return ANR_OK;
+  hipLaunchKernelGGL(k_sample_volume, dim3((unsigned)(((long)n * C + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     vol, X, Y, Z, C, bounds, pts, n, out);
+  return check_launch("k_sample_volume");
 }
 
 int anr_render_row_ids(const void* workspace, int n_rays, int32_t* ids, void* stream) {

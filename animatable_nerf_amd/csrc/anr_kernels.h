@@ -135,7 +135,37 @@ struct MlpArgs {
   const float* w8row;
   float* gb;
   float* gc;
+  // measurement (anr_profile_*): when set, thread 0 of every workgroup stamps (s_memtime, s_memrealtime)
+  // at kernel entry and exit into clk[blockIdx.x * 4 + {0, 1, 2, 3}]: the in-kernel shader clock is
+  // d memtime / d realtime x 100 MHz (MI355X_MICROARCH.md, DVFS item 6)
+  unsigned long long* clk;
 };
+
+__device__ __forceinline__ void clk_stamp(unsigned long long* clk, int k) {
+  if (clk && threadIdx.x == 0) {
+    const unsigned long long t = __builtin_amdgcn_s_memtime();
+    const unsigned long long r = __builtin_amdgcn_s_memrealtime();
+    clk[(size_t)blockIdx.x * 4 + 2 * k] = t;
+    clk[(size_t)blockIdx.x * 4 + 2 * k + 1] = r;
+  }
+}
+#ifdef ANR_NO_CLK_STAMP  // A/B builds: the kernels without the stamp code
+#define ANR_STAMPED(...) __VA_ARGS__
+#else
+#define ANR_STAMPED(...) \
+  clk_stamp(a.clk, 0);   \
+  __VA_ARGS__;           \
+  clk_stamp(a.clk, 1)
+#endif
+
+// profiling slot of one fused launch (anr_capi.hip; NULL from prof_begin when profiling is off): events
+// around the launch and the clock-stamp area handed to the kernel as MlpArgs::clk (NULL past the arena)
+struct ProfSlot {
+  hipEvent_t b, e;
+  unsigned long long* clk;
+};
+ProfSlot* prof_begin(hipStream_t s, int grid);
+int prof_end(ProfSlot* q, hipStream_t s);
 
 struct PrepArgs {
   const float *pbw, *tbw;  // (X,Y,Z,25)
@@ -176,6 +206,7 @@ __global__ void k_flag_force(AlphaArgs a, int nchunks);
 __global__ void k_flag_scatter(AlphaArgs a);
 __global__ void k_gather_rows(const int*, const int*, const float4*, const float4*, float4*, float4*);
 __global__ void k_row_ids(const int*, const int*, const int*, int*);
+__global__ void k_sample_volume(const float*, int, int, int, int, const float*, const float*, int, float*);
 __global__ void k_composite(CompositeArgs a);
 __global__ void k_prep(PrepArgs a);
 __global__ void k_mlp(MlpArgs a);

@@ -3,6 +3,6 @@
 
 namespace anr {
 
-__global__ __launch_bounds__(512) void k_mlp(MlpArgs a) { mlp_body<false>(a); }
+__global__ __launch_bounds__(512) void k_mlp(MlpArgs a) { ANR_STAMPED(mlp_body<false>(a);); }
 
 }  // namespace anr

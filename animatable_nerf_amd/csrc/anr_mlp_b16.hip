@@ -4,6 +4,6 @@
 
 namespace anr {
 
-__global__ __launch_bounds__(512) void k_mlp_b16(MlpArgs a) { mlp_body<true>(a); }
+__global__ __launch_bounds__(512) void k_mlp_b16(MlpArgs a) { ANR_STAMPED(mlp_body<true>(a);); }
 
 }  // namespace anr

@@ -6,6 +6,6 @@
 
 namespace anr {
 
-__global__ __launch_bounds__(512) void k_mlp_x6(MlpArgs a) { mlp_body<true, 4>(a); }
+__global__ __launch_bounds__(512) void k_mlp_x6(MlpArgs a) { ANR_STAMPED(mlp_body<true, 4>(a);); }
 
 }  // namespace anr

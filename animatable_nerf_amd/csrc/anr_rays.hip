@@ -535,6 +535,20 @@ __global__ __launch_bounds__(256) void k_gather_rows(const int* __restrict__ out
   tbw[(size_t)r * 6 + j] = tbw_rows[(size_t)i * 6 + j];
 }
 
+// pts_sample_blend_weights of free points (anr_sample_volume): thread per (point, channel), out (C, n)
+__global__ __launch_bounds__(256) void k_sample_volume(const float* __restrict__ vol, int X, int Y, int Z, int C,
+                                                       const float* __restrict__ bounds, const float* __restrict__ pts,
+                                                       int n, float* __restrict__ out) {
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (long)n * C) return;
+  const int i = (int)(e / C), ch = (int)(e - (long)i * C);
+  const float p[3] = {pts[3 * i], pts[3 * i + 1], pts[3 * i + 2]};
+  const float lo[3] = {bounds[0], bounds[1], bounds[2]}, hi[3] = {bounds[3], bounds[4], bounds[5]};
+  TriCell t;
+  tri_cell(p, lo, hi, X, Y, Z, t);
+  out[(size_t)ch * n + i] = tri_channel(vol, C, ch, t);
+}
+
 // sample id (ray * 64 + sample) of every alpha_ind output row: the row order of k_gather_rows
 __global__ __launch_bounds__(256) void k_row_ids(const int* __restrict__ out_row, const int* __restrict__ n_kept,
                                                  const int* __restrict__ list, int* __restrict__ ids) {

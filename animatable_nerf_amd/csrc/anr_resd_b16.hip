@@ -10,10 +10,10 @@
 
 namespace anr {
 
-__global__ __launch_bounds__(512) void k_resd_b16(MlpArgs a) { resd_body<false>(a); }
-__global__ __launch_bounds__(512) void k_sdfnet_b16(MlpArgs a) { sdfnet_body<false>(a); }
-__global__ __launch_bounds__(512) void k_sdfgrad_b16(MlpArgs a) { sdfgrad_body<false>(a); }
-__global__ __launch_bounds__(512) void k_color_b16(MlpArgs a) { color_body<false>(a); }
+__global__ __launch_bounds__(512) void k_resd_b16(MlpArgs a) { ANR_STAMPED(resd_body<false>(a);); }
+__global__ __launch_bounds__(512) void k_sdfnet_b16(MlpArgs a) { ANR_STAMPED(sdfnet_body<false>(a);); }
+__global__ __launch_bounds__(512) void k_sdfgrad_b16(MlpArgs a) { ANR_STAMPED(sdfgrad_body<false>(a);); }
+__global__ __launch_bounds__(512) void k_color_b16(MlpArgs a) { ANR_STAMPED(color_body<false>(a);); }
 
 namespace {
 // one persistent launch of a fused sdf program over the batch's rows (grid <= one workgroup per tile)
@@ -26,11 +26,13 @@ int launch_prog(const void* kernel, bool& attr, const MlpArgs& a, int grid, hipS
   if (a.n_rows <= 0) return 0;
   const int ntiles = (a.n_rows + 127) / 128;
   MlpArgs args = a;
+  const int g = grid < ntiles ? grid : ntiles;
+  ProfSlot* ps = prof_begin(s, g);  // the sdf leg's network time and clock (anr_profile_*)
+  args.clk = ps ? ps->clk : nullptr;
   void* kargs[] = {&args};
-  if (hipLaunchKernel(kernel, dim3(grid < ntiles ? grid : ntiles), dim3(512), kargs, mlp_lds_bytes<true>(), s) !=
-      hipSuccess)
-    return -1;
-  return hipGetLastError() == hipSuccess ? 0 : -1;
+  if (hipLaunchKernel(kernel, dim3(g), dim3(512), kargs, mlp_lds_bytes<true>(), s) != hipSuccess) return -1;
+  if (hipGetLastError() != hipSuccess) return -1;
+  return prof_end(ps, s) == 0 ? 0 : -1;
 }
 bool attr_b16[4], attr_x6[4];
 }  // namespace

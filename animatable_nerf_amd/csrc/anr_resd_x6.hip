@@ -7,9 +7,9 @@
 
 namespace anr {
 
-__global__ __launch_bounds__(512) void k_resd_x6(MlpArgs a) { resd_body<true>(a); }
-__global__ __launch_bounds__(512) void k_sdfnet_x6(MlpArgs a) { sdfnet_body<true>(a); }
-__global__ __launch_bounds__(512) void k_sdfgrad_x6(MlpArgs a) { sdfgrad_body<true>(a); }
-__global__ __launch_bounds__(512) void k_color_x6(MlpArgs a) { color_body<true>(a); }
+__global__ __launch_bounds__(512) void k_resd_x6(MlpArgs a) { ANR_STAMPED(resd_body<true>(a);); }
+__global__ __launch_bounds__(512) void k_sdfnet_x6(MlpArgs a) { ANR_STAMPED(sdfnet_body<true>(a);); }
+__global__ __launch_bounds__(512) void k_sdfgrad_x6(MlpArgs a) { ANR_STAMPED(sdfgrad_body<true>(a);); }
+__global__ __launch_bounds__(512) void k_color_x6(MlpArgs a) { ANR_STAMPED(color_body<true>(a);); }
 
 }  // namespace anr

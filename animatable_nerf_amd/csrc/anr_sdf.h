@@ -102,6 +102,10 @@ __global__ void k_sdf_wnorm(SdfTensors T, float* wimg);
 __global__ void k_sdf_fold(SdfTensors T, const float* wimg, const float* poses, const int64_t* li, float* fold);
 __global__ void k_sdf_tbtab(const float* tbounds, int nchunks, float* tbtab, float* tb_out);
 __global__ void k_sdf_prep(SdfPointArgs a);
+__global__ void k_knn_blend_out(const uint32_t* knn, const uint64_t* mask, const float* weights, int n, float* bw,
+                                uint8_t* inside);
+__global__ void k_mesh_pose(const float* pts, const float* bw, int n, const float* bigA, const float* A, const float* R,
+                            const float* Th, float* out);
 __global__ void k_sdf_mid(SdfPointArgs a);
 __global__ void k_sdf_gtop(SdfPointArgs a);
 __global__ void k_sdf_gamma_bwd(SdfPointArgs a);

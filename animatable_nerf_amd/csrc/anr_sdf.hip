@@ -401,6 +401,49 @@ __device__ void sdf_prep_point(const SdfPointArgs& a, int i, float (*sp)[4]) {
   sp[threadIdx.x][0] = bp[0]; sp[threadIdx.x][1] = bp[1]; sp[threadIdx.x][2] = bp[2];
 }
 
+// sample_blend_closest_points of free points (anr_knn_blend): the front-end's KNN records (k_sdf_front
+// with R = I, Th = 0) -> inside = pnorm < norm_th (no forced argmin: the mesh path's filter,
+// sdf_mesh_renderer.py:58-60) and the blended weights in k_sdf_prep's summation order
+__global__ __launch_bounds__(256) void k_knn_blend_out(const uint32_t* __restrict__ knn, const uint64_t* __restrict__ mask,
+                                                       const float* __restrict__ weights, int n, float* bw,
+                                                       uint8_t* inside) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  if (inside) inside[i] = (uint8_t)((mask[i >> 6] >> (i & 63)) & 1ull);
+  if (!bw) return;
+  const uint4* rec = (const uint4*)(knn + (size_t)i * 8);
+  const uint4 r0 = rec[0], r1 = rec[1];
+  const float w[5] = {__uint_as_float(r0.x), __uint_as_float(r0.y), __uint_as_float(r0.z), __uint_as_float(r0.w),
+                      __uint_as_float(r1.x)};
+  const int idx[5] = {(int)(r1.y & 0xffff), (int)(r1.y >> 16), (int)(r1.z & 0xffff), (int)(r1.z >> 16), (int)r1.w};
+  for (int l = 0; l < 24; ++l) {
+    float acc = weights[idx[0] * 24 + l] * w[0];
+    for (int k = 1; k < 5; ++k) acc = acc + weights[idx[k] * 24 + l] * w[k];
+    bw[(size_t)i * 24 + l] = acc;
+  }
+}
+
+// the sdf mesh path's posed vertices (sdf_mesh_renderer.py:96-101): big pose -> T pose (inverse LBS with
+// big_A), -> pose (LBS with A), -> world (x R^T + Th); blend weights bw (n, 24)
+__global__ __launch_bounds__(256) void k_mesh_pose(const float* __restrict__ pts, const float* __restrict__ bw, int n,
+                                                   const float* __restrict__ bigA, const float* __restrict__ A,
+                                                   const float* __restrict__ R, const float* __restrict__ Th, float* out) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  float w[24];
+  for (int l = 0; l < 24; ++l) w[l] = bw[(size_t)i * 24 + l];
+  float Bb[16], Ab[16], Ri[9];
+  blend16(w, bigA, Bb);
+  blend16(w, A, Ab);
+  inv33(Bb, Ri);
+  const float y[3] = {pts[3 * i] - Bb[3], pts[3 * i + 1] - Bb[7], pts[3 * i + 2] - Bb[11]};
+  float tp[3], pp[3];
+  for (int r = 0; r < 3; ++r) tp[r] = (Ri[3 * r] * y[0] + Ri[3 * r + 1] * y[1]) + Ri[3 * r + 2] * y[2];
+  for (int r = 0; r < 3; ++r) pp[r] = ((Ab[4 * r] * tp[0] + Ab[4 * r + 1] * tp[1]) + Ab[4 * r + 2] * tp[2]) + Ab[4 * r + 3];
+  for (int r = 0; r < 3; ++r)  // pose_points_to_world_points: pts @ R^T + Th
+    out[(size_t)i * 3 + r] = ((pp[0] * R[3 * r] + pp[1] * R[3 * r + 1]) + pp[2] * R[3 * r + 2]) + Th[r];
+}
+
 // resd = 0.05 tanh(y); tpose = bigpose + resd; gamma_6(tpose) -> Xs0 and X4[:, 217:] / sqrt(2);
 // colour input [tpose, gamma_4(bigdir), gradient (k_sdf_gamma_bwd)]. Thread per sample for tpose,
 // then the rows are written column-fastest by the whole workgroup.

@@ -615,6 +615,58 @@ const int32_t* anr_sdf_network_counts(const void* workspace, int n) {
   return (const int32_t*)((const char*)workspace + slayout(G, G).counts);
 }
 
+// KNN blend of free points: [R | Th identity (12 floats)] [mask (G x 8)] [chunk_min 8] [knn (64 G x 32)]
+//   [raw (64 G x 16)] [sdf (64 G x 4)]
+size_t anr_knn_blend_workspace_bytes(int n) {
+  if (n <= 0) return 0;
+  const size_t G = (size_t)groups_of(n);
+  return align256(64) + align256(G * 8) + align256(8) + align256(64 * G * 32) + align256(64 * G * 16) + align256(64 * G * 4);
+}
+
+int anr_knn_blend(const float* verts, const float* weights, int nv, const float* pts, int n, float norm_th, float* bw,
+                  uint8_t* inside, void* workspace, size_t ws_bytes, void* stream) {
+  if (!verts || !weights || !pts || !workspace || n <= 0 || (!bw && !inside))
+    return fail(ANR_E_ARG, "anr_knn_blend: bad arguments");
+  if (nv <= 0 || nv > 6912) return fail(ANR_E_ARG, "anr_knn_blend: nv must be in [1, 6912]");
+  if (ws_bytes < anr_knn_blend_workspace_bytes(n)) return fail(ANR_E_WORKSPACE, "anr_knn_blend: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  const int G = groups_of(n);
+  char* w = (char*)workspace;
+  float* rt = (float*)w;
+  w += align256(64);
+  uint64_t* mask = (uint64_t*)w;
+  w += align256((size_t)G * 8);
+  uint64_t* cmin = (uint64_t*)w;
+  w += align256(8);
+  uint32_t* knn = (uint32_t*)w;
+  w += align256((size_t)64 * G * 32);
+  float4* raw = (float4*)w;
+  w += align256((size_t)64 * G * 16);
+  float* sdf = (float*)w;
+  static const float ident[12] = {1.f, 0.f, 0.f, 0.f, 1.f, 0.f, 0.f, 0.f, 1.f, 0.f, 0.f, 0.f};
+  if (hipMemcpyAsync(rt, ident, sizeof(ident), hipMemcpyHostToDevice, s) != hipSuccess ||
+      hipMemsetAsync(cmin, 0xff, 8, s) != hipSuccess)
+    return fail(ANR_E_HIP, "anr_knn_blend: setup");
+  SdfFrontArgs fa{};
+  fa.wpts = pts; fa.n_pts = n; fa.n_rays = G; fa.chunk = G;
+  fa.R = rt; fa.Th = rt + 9;  // world -> pose with R = I, Th = 0 is the identity in fp32 (x * 1 + y * 0 + z * 0)
+  fa.verts = verts; fa.nv = nv; fa.norm_th = norm_th;
+  fa.mask = mask; fa.chunk_min = cmin; fa.knn = knn; fa.raw = raw; fa.sdf = sdf;
+  hipLaunchKernelGGL(k_sdf_front, dim3(std::min(sdf_cus(), (G + 15) / 16)), dim3(1024), 0, s, fa);
+  ANR_TRY(check_launch("k_sdf_front (knn blend)"));
+  hipLaunchKernelGGL(k_knn_blend_out, dim3((n + 255) / 256), dim3(256), 0, s, (const uint32_t*)knn, (const uint64_t*)mask,
+                     weights, n, bw, inside);
+  return check_launch("k_knn_blend_out");
+}
+
+int anr_sdf_mesh_pose(const float* pts, const float* bw, int n, const float* big_A, const float* A, const float* R,
+                      const float* Th, float* out, void* stream) {
+  if (!pts || !bw || !big_A || !A || !R || !Th || !out || n < 0) return fail(ANR_E_ARG, "anr_sdf_mesh_pose: bad arguments");
+  if (n == 0) return ANR_OK;
+  hipLaunchKernelGGL(k_mesh_pose, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, pts, bw, n, big_A, A, R, Th, out);
+  return check_launch("k_mesh_pose");
+}
+
 int anr_sdf_network_rows(const void* workspace, int n, float* resd, float* gradients, void* stream) {
   if (!workspace || n <= 0) return fail(ANR_E_ARG, "anr_sdf_network_rows: bad arguments");
   const int G = groups_of(n);

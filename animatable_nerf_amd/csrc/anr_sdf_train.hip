@@ -437,6 +437,15 @@ __global__ __launch_bounds__(256) void k_st_obs_gather(const float* __restrict__
   for (int k = 0; k < 64; ++k) Gro[(size_t)o * 64 + k] = Gr[(size_t)i * 64 + k];
 }
 
+// anr_sdf_points rows: big-pose point x in columns 0..2 of ptb (stride 8, directions 0), gamma_10(x) (stride 64)
+__global__ void k_st_pts_rows(const float* __restrict__ x, int n, float* ptb, float* Gr) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float p[3] = {x[3 * i], x[3 * i + 1], x[3 * i + 2]};
+  for (int c = 0; c < 8; ++c) ptb[(size_t)i * 8 + c] = c < 3 ? p[c] : 0.f;
+  for (int c = 0; c < 64; ++c) Gr[(size_t)i * 64 + c] = c < 63 ? embed_feature(p, c, 10) : 0.f;
+}
+
 __global__ void k_st_add_bias(const float* __restrict__ src, int n, float* dst) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) dst[i] += src[i];
@@ -683,7 +692,9 @@ int read_int(const void* dev, int* host, hipStream_t s) {
 // the forward (with the observed gradients) into the caller's raw / sdf and the workspace rows;
 // NET_BWD re-runs that forward (deterministic: same counts, same rows) and the backward from the
 // caller's upstream adjoints.
-enum CoreMode { STEP = 0, NET_FWD = 1, NET_BWD = 2 };
+// PTS: the network's point helpers on n free points x (anr_sdf_points; pts_mode ANR_SDFP_*): no
+// front-end / compaction (every point is a row), the SDF (and residual) layers of this executor.
+enum CoreMode { STEP = 0, NET_FWD = 1, NET_BWD = 2, PTS = 3 };
 
 struct TrainCore {
   int mode;
@@ -702,6 +713,8 @@ struct TrainCore {
   float* loss;                    // STEP
   float *raw_out, *sdf_out, *tb_out;  // NET_FWD
   const float *d_raw, *d_sdf, *d_resd, *d_grad, *d_og;  // NET_BWD (any NULL = 0)
+  int pts_mode;                      // PTS: ANR_SDFP_NETWORK / _GRADIENT / _DEFORMED_GRADIENT
+  float *pts_out, *pts_out2;         // PTS outputs
   void* ws;
   size_t ws_bytes;
   hipStream_t s;
@@ -744,8 +757,10 @@ int sdf_train_core(const TrainCore& C) {
   for (int i = 0; i < ANR_SDF_NUM_TENSORS; ++i) T.t[i] = tp[i];
   hipLaunchKernelGGL(k_sdf_wnorm, dim3(sdf_wn_rows()), dim3(256), 0, s, T, wimg);
   hipLaunchKernelGGL(k_sdf_fold, dim3(3), dim3(256), 0, s, T, (const float*)wimg, f->poses, f->latent_index, fold);
-  hipLaunchKernelGGL(k_sdf_tbtab, dim3(1), dim3(64), 0, s, f->tbounds, nch, tbtab,
-                     step ? C.out->tbounds_out : (net_fwd ? C.tb_out : nullptr));
+  const bool pts = C.mode == PTS;
+  if (!pts)
+    hipLaunchKernelGGL(k_sdf_tbtab, dim3(1), dim3(64), 0, s, f->tbounds, nch, tbtab,
+                       step ? C.out->tbounds_out : (net_fwd ? C.tb_out : nullptr));
   ANR_TRY(check_launch("sdf train prep"));
 
   // ---- B1 front-end (KNN keep mask) + ordered compaction; one host read of n'
@@ -762,20 +777,24 @@ int sdf_train_core(const TrainCore& C) {
         hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
       cus = v;
   }
-  hipLaunchKernelGGL(k_sdf_front, dim3(std::min(cus, (R + 15) / 16)), dim3(1024), 0, s, fa);
-  ANR_TRY(check_launch("k_sdf_front (train)"));
   CompactArgs ca{};
-  ca.n_rays = R; ca.chunk = C.chunk; ca.mask = fa.mask; ca.chunk_min = fa.chunk_min;
-  ca.ray_off = (int*)(ws + L.ray_off); ca.block_sum = (int*)(ws + L.block_sum); ca.list = (int*)(ws + L.list);
-  const int nb = (R + 255) / 256;
-  hipLaunchKernelGGL(k_count, dim3(nb), dim3(256), 0, s, ca);
-  hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, s, ca.block_sum, nb, counts);
-  hipLaunchKernelGGL(k_compact, dim3((R + 3) / 4), dim3(256), 0, s, ca);
-  ANR_TRY(check_launch("k_compact (sdf train)"));
   int n = 0;
-  ANR_TRY(read_int(counts, &n, s));
   int* inv = (int*)(ws + L.inv);
-  hipLaunchKernelGGL(k_st_inv, dim3((n + 255) / 256 + 1), dim3(256), 0, s, (const int*)ca.list, (const int*)counts, inv);
+  if (pts) {
+    n = C.n_pts;
+  } else {
+    hipLaunchKernelGGL(k_sdf_front, dim3(std::min(cus, (R + 15) / 16)), dim3(1024), 0, s, fa);
+    ANR_TRY(check_launch("k_sdf_front (train)"));
+    ca.n_rays = R; ca.chunk = C.chunk; ca.mask = fa.mask; ca.chunk_min = fa.chunk_min;
+    ca.ray_off = (int*)(ws + L.ray_off); ca.block_sum = (int*)(ws + L.block_sum); ca.list = (int*)(ws + L.list);
+    const int nb = (R + 255) / 256;
+    hipLaunchKernelGGL(k_count, dim3(nb), dim3(256), 0, s, ca);
+    hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(1024), 0, s, ca.block_sum, nb, counts);
+    hipLaunchKernelGGL(k_compact, dim3((R + 3) / 4), dim3(256), 0, s, ca);
+    ANR_TRY(check_launch("k_compact (sdf train)"));
+    ANR_TRY(read_int(counts, &n, s));
+    hipLaunchKernelGGL(k_st_inv, dim3((n + 255) / 256 + 1), dim3(256), 0, s, (const int*)ca.list, (const int*)counts, inv);
+  }
 
   TG g{s};
   // which products run split-bf16 (bits, ANR_SDF_X3_PARTS): 1 residual MLP, 2 SDF forward, 4 SDF input
@@ -951,6 +970,66 @@ int sdf_train_core(const TrainCore& C) {
                        (const float*)AX4, m, tbar, ttbar);
     return check_launch("k_st_embed_rev6");
   };
+
+  if (pts) {
+    // ---- the network's point helpers (anr_sdf_points): every point is a row, x in big-pose space
+    const dim3 og_((n + 255) / 256);
+    SdfPointArgs ao = a;
+    ao.list = nullptr; ao.cnt = n; ao.ptb = F(L.ptbo); ao.Gr = F(L.Gro); ao.Yr = F(L.Yr); ao.resd_rows = F(L.ro);
+    ao.grad_rows = F(L.gro);
+    hipLaunchKernelGGL(k_st_pts_rows, og_, pb, 0, s, C.wpts, n, F(L.ptbo), F(L.Gro));
+    ANR_TRY(check_launch("k_st_pts_rows"));
+    const bool deformed = C.pts_mode == ANR_SDFP_DEFORMED_GRADIENT;
+    if (deformed) {
+      ANR_TRY(resd_forward(n, F(L.Gro), F(L.Yr)));  // tpose = x + 0.05 tanh(resd_fc) (k_sdf_mid)
+    } else if (hipMemsetAsync(F(L.Yr), 0, (size_t)n * 16, s) != hipSuccess) {  // tanh(0) = 0: tpose = x exactly
+      return fail(ANR_E_HIP, "memset");
+    }
+    hipLaunchKernelGGL(k_sdf_mid, og_, pb, 0, s, ao);
+    ANR_TRY(check_launch("k_sdf_mid (points)"));
+    ANR_TRY(sdf_forward(n, F(L.Y8)));
+    if (C.pts_mode == ANR_SDFP_NETWORK) {  // [sdf / scale (scale 1) || feature]
+      if (hipMemcpy2DAsync(C.pts_out, 257 * 4, F(L.Y8), 264 * 4, 257 * 4, (size_t)n, hipMemcpyDeviceToDevice, s) !=
+          hipSuccess)
+        return fail(ANR_E_HIP, "anr_sdf_points: copy");
+      return ANR_OK;
+    }
+    ANR_TRY(sdf_input_grad(ao, n));  // d sdf / d tpose -> C0[:, 30:33]
+    const float* gout = F(L.C0) + 30;
+    long ldg = 40;
+    if (deformed) {  // og = g_t + J_resd^T g_t, as the observed-gradient pass below
+      part(1);
+      float *dHa = F(L.dHa), *dHb = F(L.dHb), *Gbar = F(L.Gbar);
+      float* yb = F(L.Yd);
+      hipLaunchKernelGGL(k_st_add3, og_, pb, 0, s, (const float*)(F(L.C0) + 30), 40L, (const float*)(ws + L.zero), 0L, n,
+                         F(L.tdot));
+      hipLaunchKernelGGL(k_st_tanh_rev, og_, pb, 0, s, (const float*)F(L.Yr), (const float*)nullptr,
+                         (const float*)F(L.tdot), (const float*)nullptr, (const float*)nullptr, n, yb);
+      ANR_TRY(g.xgrad(n, dHa, 256, 256, yb, 4, 3, tp[SDF_RFC_W], 256, 0, Hr(7), 256));
+      float* cur = dHa;
+      float* nxt = dHb;
+      for (int l = 7; l >= 1; --l) {
+        if (l == 5) {
+          ANR_TRY(g.xgrad(n, Gbar, 64, 63, cur, 256, 256, Wr[5], 391, 0));
+          ANR_TRY(g.xgrad(n, nxt, 256, 256, cur, 256, 256, Wr[5], 391, 135, Hr(4), 256));
+        } else {
+          ANR_TRY(g.xgrad(n, nxt, 256, 256, cur, 256, 256, Wr[l], 256, 0, Hr(l - 1), 256));
+        }
+        std::swap(cur, nxt);
+      }
+      ANR_TRY(g.xgrad(n, Gbar, 64, 63, cur, 256, 256, Wr[0], 135, 0, nullptr, 0, true));
+      float* og = F(L.og);
+      hipLaunchKernelGGL(k_st_embed_bwd10, og_, pb, 0, s, (const float*)F(L.ptbo), 8L, (const float*)Gbar, 64L, n, og, 4L);
+      hipLaunchKernelGGL(k_st_add3, og_, pb, 0, s, (const float*)F(L.tdot), 4L, (const float*)og, 4L, n, og);
+      ANR_TRY(check_launch("anr_sdf_points: deformed gradient"));
+      gout = og;
+      ldg = 4;
+    }
+    if (hipMemcpy2DAsync(C.pts_out, 12, gout, ldg * 4, 12, (size_t)n, hipMemcpyDeviceToDevice, s) != hipSuccess ||
+        (C.pts_out2 && hipMemcpy2DAsync(C.pts_out2, 4, F(L.Y8), 264 * 4, 4, (size_t)n, hipMemcpyDeviceToDevice, s) != hipSuccess))
+      return fail(ANR_E_HIP, "anr_sdf_points: copy");
+    return ANR_OK;
+  }
 
   if (n > 0) {
     // ---- forward: B2/B3 residual deformation, B4 SDF + its input gradient, B6 colour, B5 raw
@@ -1314,6 +1393,31 @@ int anr_sdf_network_train_rows(const void* workspace, int n_pts, float* resd, fl
       hipMemcpy2DAsync(observed_gradients, 12, ws + L.og, 16, 12, (size_t)n_o, hipMemcpyDeviceToDevice, s) != hipSuccess)
     return fail(ANR_E_HIP, "anr_sdf_network_train_rows: copy");
   return ANR_OK;
+}
+
+size_t anr_sdf_points_workspace_bytes(int n) {
+  if (n <= 0) return 0;
+  const int G = (n + 63) / 64;
+  return stlayout(G, G).total;
+}
+
+int anr_sdf_points(const anr_sdf_params* p, const anr_sdf_frame* f, const float* x, int n, int mode, float* out,
+                   float* out2, void* workspace, size_t ws_bytes, void* stream) {
+  if (!p || !f || !x || !out || !workspace) return fail(ANR_E_ARG, "anr_sdf_points: NULL argument");
+  if (n <= 0 || n > (1 << 24)) return fail(ANR_E_ARG, "anr_sdf_points: n must be in [1, 2^24]");
+  if (mode != ANR_SDFP_NETWORK && mode != ANR_SDFP_GRADIENT && mode != ANR_SDFP_DEFORMED_GRADIENT)
+    return fail(ANR_E_ARG, "anr_sdf_points: unknown mode");
+  for (int i = 0; i < ANR_SDF_NUM_TENSORS; ++i)
+    if (!p->t[i] && i != SDF_RESD_LAT) return fail(ANR_E_ARG, "anr_sdf_points: NULL parameter tensor");
+  if (!f->poses || !f->latent_index) return fail(ANR_E_ARG, "anr_sdf_points: needs poses and latent_index");
+  static const anr_render_opts o0{};  // exact fp32 products
+  TrainCore c{};
+  c.mode = PTS; c.p = p; c.f = f; c.o = &o0;
+  c.wpts = x; c.n_pts = n;
+  c.R = (n + 63) / 64; c.chunk = c.R;
+  c.pts_mode = mode; c.pts_out = out; c.pts_out2 = out2;
+  c.ws = workspace; c.ws_bytes = ws_bytes; c.s = (hipStream_t)stream;
+  return sdf_train_core(c);
 }
 
 int anr_sdf_network_train_bwd(const anr_sdf_params* p, float* const* grads, const anr_sdf_frame* f, const anr_samples* x,

@@ -228,6 +228,50 @@ class Renderer:
             batch['tbounds'].copy_(tb_out.view_as(batch['tbounds']))
         return {'raw': raw, 'sdf': sdf, 'resd': resd, 'gradients': grad}
 
+    # ---- the network's point helpers (anr_sdf_points; the sdf mesh path) ------------------------------
+    def points(self, x, batch, mode):
+        """anr_sdf_points over x (n,3) big-pose points: mode _lib.SDFP_NETWORK -> (n,257) [sdf || feature]
+        (tpose_human.sdf_network, anisdf_pdf_network.py:421-437); SDFP_GRADIENT -> (d sdf/dx (n,3), sdf (n,1))
+        (SDFNetwork.gradient, :441-451); SDFP_DEFORMED_GRADIENT -> (gradient of sdf(x + resd(x)) (n,3), that
+        sdf (n,1)) (Network.gradient_of_deformed_sdf, :140-154). Exact fp32 products; no host sync."""
+        dev = self.device()
+        p = self.params()
+        xs = _f32(x, dev).reshape(-1, 3)
+        n = xs.shape[0]
+        out = torch.empty((n, 257) if mode == _lib.SDFP_NETWORK else (n, 3), device=dev)
+        out2 = None if mode == _lib.SDFP_NETWORK else torch.empty((n, 1), device=dev)
+        if n == 0:
+            return out if out2 is None else (out, out2)
+        poses = _f32(batch['poses'], dev)
+        li = batch['latent_index'].to(device=dev, dtype=torch.int64).reshape(-1).contiguous()
+        f = _lib.SdfFrame()
+        f.poses, f.latent_index = poses.data_ptr(), li.data_ptr()
+        ws_bytes = self.lib.anr_sdf_points_workspace_bytes(n)
+        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+        _lib.check(self.lib.anr_sdf_points(ctypes.byref(p), ctypes.byref(f), _lib.ptr(xs), n, int(mode), _lib.ptr(out),
+                                           _lib.ptr(out2) if out2 is not None else None, _lib.ptr(ws), ws_bytes,
+                                           _lib.stream_ptr(dev)), 'anr_sdf_points')
+        return out if out2 is None else (out, out2)
+
+    def knn_blend(self, pts, verts, weights, norm_th=NORM_TH, bw=True, inside=False):
+        """sample_blend_closest_points (sample_utils.py:323-348) of pts (n,3) against verts (nv,3) / weights
+        (nv,24): -> blended weights (n,24) and / or the mask weighted-distance < norm_th (n,) bool."""
+        dev = self.device()
+        ps = _f32(pts, dev).reshape(-1, 3)
+        vs = _f32(verts, dev).reshape(-1, 3)
+        ws_ = _f32(weights, dev).reshape(-1, 24)
+        n = ps.shape[0]
+        out_bw = torch.empty((n, 24), device=dev) if bw else None
+        out_in = torch.empty((n,), dtype=torch.uint8, device=dev) if inside else None
+        if n > 0:
+            nbytes = self.lib.anr_knn_blend_workspace_bytes(n)
+            wk = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+            _lib.check(self.lib.anr_knn_blend(_lib.ptr(vs), _lib.ptr(ws_), vs.shape[0], _lib.ptr(ps), n, float(norm_th),
+                                              _lib.ptr(out_bw) if bw else None, _lib.ptr(out_in) if inside else None,
+                                              _lib.ptr(wk), nbytes, _lib.stream_ptr(dev)), 'anr_knn_blend')
+        res = tuple(v for v in (out_bw, None if out_in is None else out_in.bool()) if v is not None)
+        return res[0] if len(res) == 1 else res
+
     def render(self, batch):
         if torch.is_grad_enabled() and any(p.requires_grad for p in self.net.parameters()) and self.net.training:
             raise RuntimeError('sdf_pdf training runs as one fused step: use trainer_sdf.NetworkWrapper(net) '

@@ -167,6 +167,24 @@ def mesh_scene(voxel=0.02, vsize=0.05, inside_frac=0.8, seed=11):
             'latent_index': np.array([2]), 'frame_index': np.array([0])}
 
 
+def sdf_mesh_scene(voxel=0.02, vsize=0.05):
+    """The sdf_pdf mesh path's batch (anisdf_mesh_dataset.py:145-206) for the synthetic subject: the voxel
+    grid (float64 np.arange per axis, ij meshgrid, float32) over the big-pose bounds tbounds, the big-pose
+    vertices, skin weights, big_A / A / poses, and a rotated / translated world frame (R, Th) for the
+    posed vertices."""
+    sc = PdfScene(vsize=vsize)
+    tb = sc.tbounds
+    axes = [np.arange(tb[0, c], tb[1, c] + voxel, voxel) for c in range(3)]
+    pts = np.stack(np.meshgrid(*axes, indexing='ij'), axis=-1).astype(np.float32)
+    R = batch_rodrigues(np.array([[0.2, -0.3, 0.1]]))[0].astype(np.float32)
+    Th = np.array([0.1, -0.05, 0.2], np.float32)
+    return {'pts': pts[None], 'A': sc.A[None], 'big_A': sc.big_A[None], 'poses': sc.pose_vec[None],
+            'weights': sc.skin[None], 'tvertices': sc.tvertices[None], 'pvertices': sc.pvertices[None],
+            'tbounds': tb[None], 'pbounds': sc.pbounds[None], 'wbounds': sc.pbounds[None],
+            'inside': np.ones(pts.shape[:-1], np.uint8)[None], 'R': R[None], 'Th': Th[None, None],
+            'latent_index': np.array([3]), 'frame_index': np.array([0])}
+
+
 def training_views(verts, n_views=3, H=100, W=100, focal=80.0, dist=3.0, dilate=1):
     """Training cameras + silhouettes for the novel-view visibility filter
     (``tpose_renderer_mmsk.py:14-57``; keys of ``tpose_novel_view_dataset.py:191``): cameras on a

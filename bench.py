@@ -79,6 +79,8 @@ def parse():
                          'GEMMs; bf16x3 = hi/lo split (the 1e-4 parity bars, not fp32-level); the other two are timed '
                          'beside it unless --no-exact')
     ap.add_argument('--no-exact', action='store_true', help='skip timing the other render precision')
+    ap.add_argument('--no-side', action='store_true',
+                    help='render mode: skip the side legs (train_step / sdf_render / sdf_train_step keys)')
     ap.add_argument('--no-host-render', action='store_true',
                     help='skip the render_s leg (Renderer.render with the D2H): PMC passes then see full-frame launches only')
     ap.add_argument('--torch-rays', type=int, default=16 * 2048,
@@ -282,16 +284,15 @@ def main():
         if world > 1:
             dist.barrier()
         dt = time.perf_counter() - t0
-        mlp_ms = _lib.ctypes.c_double(0)
-        launches = _lib.ctypes.c_int(0)
-        _lib.check(lib.anr_profile_read(_lib.ctypes.byref(mlp_ms), _lib.ctypes.byref(launches)), 'anr_profile_read')
-        lib.anr_profile_enable(0)
+        mlp_ms, launches, mhz = profile_read(lib)
         counts = renderer.counts(R_local) if args.shard_frame else renderer.last_counts
-        return out, max_over_ranks(dt, dev, world), mlp_ms.value / max(1, launches.value), counts
+        timed.clock_mhz = mhz
+        return out, max_over_ranks(dt, dev, world), mlp_ms / max(1, launches), counts
 
     prec = args.render_precision
     out, dt_max, kernel_ms, (n_kept, m_rows) = timed(prec)
-    progress(f'{prec}: {dt_max / args.steps * 1e3:.2f} ms/frame, kernel {kernel_ms:.2f} ms')
+    clocks = {prec: timed.clock_mhz}
+    progress(f'{prec}: {dt_max / args.steps * 1e3:.2f} ms/frame, kernel {kernel_ms:.2f} ms, clock {timed.clock_mhz:.0f} MHz')
     value = R * 64 * args.steps * frames / dt_max
     result = {
         'metric': METRIC, 'value': value, 'unit': 'ray-samples/s', 'n_gpus': world, 'steps': args.steps,
@@ -308,7 +309,7 @@ def main():
                    'parallelism': (f'frame-split{world} (whole 2048-ray chunks per rank, rgb/acc/depth '
                                    'all-gathered over RCCL)') if args.shard_frame else
                                   f'replicas{world} (one frame per GPU)'},
-        'roofline': render_roofline(prec, n_kept, kernel_ms),
+        'roofline': dict(render_roofline(prec, n_kept, kernel_ms), clock_mhz=clocks[prec]),
     }
     if not args.no_exact:
         notes = {
@@ -321,11 +322,12 @@ def main():
             'fp32': ('fp32_exact', 'exact fp32 MFMA')}
         for other in [p for p in ('fp32', 'bf16x6', 'bf16x3') if p != prec]:
             o2, dt2, kms2, (nk2, _) = timed(other)
-            progress(f'{other}: {dt2 / args.steps * 1e3:.2f} ms/frame, kernel {kms2:.2f} ms')
+            progress(f'{other}: {dt2 / args.steps * 1e3:.2f} ms/frame, kernel {kms2:.2f} ms, clock {timed.clock_mhz:.0f} MHz')
             key, note = notes[other]
             result[key] = {
                 'value': R * 64 * args.steps * frames / dt2, 'ms_per_step': dt2 / args.steps * 1e3,
-                'render_precision': other, 'note': note, 'roofline': render_roofline(other, nk2, kms2)}
+                'render_precision': other, 'note': note,
+                'roofline': dict(render_roofline(other, nk2, kms2), clock_mhz=timed.clock_mhz)}
             del o2
     if not args.shard_frame and not args.no_host_render:
         # the drop-in call as run.py:63-69 makes it: Renderer.render(batch) with the eval D2H of every
@@ -349,6 +351,8 @@ def main():
                                           renderer.HOST_PARTS),
                               'median_of': 3}
         del host
+    if not args.no_side:
+        result.update(side_legs(args, rank, world, dev))
     if rank == 0 and world == 1 and not args.no_cpu:
         result['cpu_baseline'], result['psnr_vs_fp32_oracle'] = cpu_baseline(sd, b, out, args.cpu_rays)
         progress(f"cpu_baseline: {result['cpu_baseline']['value']:.4g} ray-samples/s, "
@@ -364,6 +368,45 @@ def main():
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def profile_read(lib):
+    """(summed ms, launches, median in-kernel clock MHz) of the profiled fused launches since the last
+    read (anr_profile_read_clock), and profiling off"""
+    from animatable_nerf_amd import _lib
+    ms, n, mhz = _lib.ctypes.c_double(0), _lib.ctypes.c_int(0), _lib.ctypes.c_double(0)
+    _lib.check(lib.anr_profile_read_clock(_lib.ctypes.byref(ms), _lib.ctypes.byref(n), _lib.ctypes.byref(mhz)),
+               'anr_profile_read_clock')
+    lib.anr_profile_enable(0)
+    return ms.value, n.value, mhz.value
+
+
+def side_legs(args, rank, world, dev):
+    """Configs 3-5 timed inside the default run (so the driver's own bench call measures them too):
+    'train_step' (config 3 at N = 1, config 4 at N > 1: the training iteration with its RCCL gradient
+    all-reduce), and at N = 1 'sdf_render' (config 5's network, bf16x6 fp32-level render of a 512x512
+    frame, exact fp32 beside it) and 'sdf_train_step' (config 5's training iteration, exact fp32). Each
+    is the full --mode leg at a short step count; its JSON line is returned instead of printed."""
+    import copy
+    out = {}
+
+    def leg(fn, key, **over):
+        a = copy.copy(args)
+        a.no_cpu = True
+        for k, v in over.items():
+            setattr(a, k, v)
+        t0 = time.perf_counter()
+        r = fn(a, rank, world, dev, emit=False)
+        keep = ('value', 'unit', 'ms_per_step', 'steps', 'warmup', 'dtype', 'config', 'roofline', 'scaling',
+                'host_issue_ms_per_step', 'loss_last_step', 'fp32_exact', 'bf16x3_split', 'metric')
+        out[key] = {k: r[k] for k in keep if k in r}
+        out[key]['leg_wall_s'] = time.perf_counter() - t0
+        progress(f"side leg {key}: {r['ms_per_step']:.3f} ms/step")
+    leg(bench_train, 'train_step', steps=20, warmup=5)
+    if world == 1:
+        leg(bench_sdf, 'sdf_render', steps=3, warmup=1, no_exact=False, sdf_exact_only=True)
+        leg(bench_sdf_train, 'sdf_train_step', steps=10, warmup=3)
+    return out
 
 
 def dry_run(args, rank, world):
@@ -400,7 +443,7 @@ def torch_gpu_baseline(sd, b, dev, n_rays, reps=3):
 FLOP_PER_KEPT_TRAIN = 9_919_488  # 3 x 2 x (2 x 497,152 + 658,944)
 
 
-def bench_train(args, rank, world, dev):
+def bench_train(args, rank, world, dev, emit=True):
     """Configs 3/4: one training iteration (trainer.py:50-68) per step on 1,024 rays per GPU:
     forward + losses + backward (anr_train_step) + RCCL mean all-reduce of the 5.3 MB gradient blob
     (N > 1) + clip + Adam (anr_adam). Weak scaling: every rank trains on its own ray batch, which is
@@ -469,6 +512,8 @@ def bench_train(args, rank, world, dev):
         'loss_last_step': loss[:3],
         'host_issue_ms_per_step': host / args.steps * 1e3,
     }
+    if not emit:
+        return result
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
@@ -480,7 +525,7 @@ def bench_train(args, rank, world, dev):
 FLOP_PER_KEPT_SDF = 2 * (528_640 + 524_544 + 459_008 + 304_128)
 
 
-def bench_sdf(args, rank, world, dev):
+def bench_sdf(args, rank, world, dev, emit=True):
     """Config 5 (sdf_pdf) geometry at the config-2 size: a 512x512 box-ray frame per GPU through
     renderer_sdf.Renderer.render_device (anr_sdf_render_fwd); replicas, no collective."""
     from animatable_nerf_amd import config, network, network_sdf, synthetic
@@ -502,6 +547,9 @@ def bench_sdf(args, rank, world, dev):
     net = net.to(dev)
     net.train()
 
+    from animatable_nerf_amd import _lib
+    lib = _lib.load()
+
     def timed(prec, steps, warmup):
         c = config.subject('anisdf_pdf_s9p', perturb=0, render_precision=prec)
         r = Renderer(net, c)
@@ -509,6 +557,8 @@ def bench_sdf(args, rank, world, dev):
             batch['tbounds'].copy_(tb0)
             o = r.render_device(batch)
         torch.cuda.synchronize()
+        lib.anr_profile_enable(1)
+        lib.anr_profile_read(None, None)
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
@@ -519,21 +569,30 @@ def bench_sdf(args, rank, world, dev):
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
-        return o, max_over_ranks(time.perf_counter() - t0, dev, world), r.last_counts[0]
+        dt = time.perf_counter() - t0
+        ms, n, mhz = profile_read(lib)  # the fused network launches (split precisions; none in exact fp32)
+        timed.net = {'network_launch_ms_per_frame': ms / steps, 'network_launches_per_frame': n / steps,
+                     'clock_mhz': mhz if n else None}
+        return o, max_over_ranks(dt, dev, world), r.last_counts[0]
 
     def sdf_roofline(prec, n_kept, dt_step):
         prods = {'fp32': 1, 'bf16x6': 6, 'bf16x3': 3}[prec]
         flop_exec = FLOP_PER_KEPT_SDF * prods
         peak = PEAK_FP32_MFMA_TFLOPS if prec == 'fp32' else PEAK_BF16_MFMA_TFLOPS
         achieved = n_kept * flop_exec / dt_step / 1e12
-        return {'bound': 'mfma', 'kernel': 'whole render (the network launches dominate)', 'achieved': achieved,
-                'peak': peak, 'unit': 'TFLOP/s', 'frac': achieved / peak, 'traffic': None,
-                'flop_per_kept': FLOP_PER_KEPT_SDF, 'flop_per_kept_executed': flop_exec,
-                'achieved_credited': n_kept * FLOP_PER_KEPT_SDF / dt_step / 1e12}
+        r = {'bound': 'mfma', 'kernel': 'whole render (the network launches dominate)', 'achieved': achieved,
+             'peak': peak, 'unit': 'TFLOP/s', 'frac': achieved / peak, 'traffic': None,
+             'flop_per_kept': FLOP_PER_KEPT_SDF, 'flop_per_kept_executed': flop_exec,
+             'achieved_credited': n_kept * FLOP_PER_KEPT_SDF / dt_step / 1e12}
+        r.update(timed.net)
+        if timed.net['network_launches_per_frame']:
+            # the four fused network launches alone (k_resd / k_sdfnet / k_sdfgrad / k_color)
+            r['network_frac'] = achieved * dt_step * 1e3 / timed.net['network_launch_ms_per_frame'] / peak
+        return r
 
     prec = args.sdf_precision
     out, dt_max, n_kept = timed(prec, args.steps, args.warmup)
-    progress(f'sdf {prec}: {dt_max / args.steps * 1e3:.2f} ms/frame')
+    progress(f'sdf {prec}: {dt_max / args.steps * 1e3:.2f} ms/frame, clock {timed.net["clock_mhz"]}')
     dtypes = {'fp32': 'fp32', 'bf16x6': 'bf16 MFMA operands (hi/mid/lo split, 6 products per MAC: fp32-level), fp32 accumulate',
               'bf16x3': 'bf16 MFMA operands (hi/lo split, 3 products per MAC), fp32 accumulate'}
     result = {
@@ -549,7 +608,8 @@ def bench_sdf(args, rank, world, dev):
     }
     if not args.no_exact:
         names = {'fp32': 'fp32_exact', 'bf16x6': 'bf16x6_fp32_level', 'bf16x3': 'bf16x3_split'}
-        for other in [q for q in ('fp32', 'bf16x6', 'bf16x3') if q != prec]:
+        others = ['fp32'] if getattr(args, 'sdf_exact_only', False) else ['fp32', 'bf16x6', 'bf16x3']
+        for other in [q for q in others if q != prec]:
             k = max(1, min(args.steps, 3 if other == 'fp32' else args.steps))
             o2, dt2, nk2 = timed(other, k, 1)
             progress(f'sdf {other}: {dt2 / k * 1e3:.2f} ms/frame')
@@ -576,6 +636,8 @@ def bench_sdf(args, rank, world, dev):
                                   'sample': f'first {n} rays of the frame, oracle/restate_sdf.py, {dtc:.1f} s'}
         from oracle import restate
         result['psnr_vs_fp32_oracle'] = float(restate.psnr(out['rgb_map'][0, :n].cpu().numpy(), ref['rgb_map'][0].numpy()))
+    if not emit:
+        return result
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
@@ -589,7 +651,7 @@ def bench_sdf(args, rank, world, dev):
 MAC_SDF_TRAIN = (528_640 + 524_544 + 459_008 + 304_128) + 2 * 304_128 + 524_544 + 4 * 524_544 + 2 * 528_640
 
 
-def bench_sdf_train(args, rank, world, dev):
+def bench_sdf_train(args, rank, world, dev, emit=True):
     """Config 5's training leg: one tpose_trainer step of the sdf_pdf network per GPU on 1,024 rays
     (N_rand, perturb 1): anr_sdf_train_step (forward, second-order losses, every gradient) + RCCL mean
     all-reduce of the 1,432,510-float gradient blob with the losses in its tail (N > 1) + clip + Adam.
@@ -648,7 +710,10 @@ def bench_sdf_train(args, rank, world, dev):
         'metric': 'sdf_pdf training ray-samples/s (1024 rays x 64 samples per GPU per step)',
         'value': R * 64 * args.steps * world / dt_max, 'unit': 'ray-samples/s', 'n_gpus': world, 'steps': args.steps,
         'warmup': args.warmup, 'ms_per_step': dt_max / args.steps * 1e3, 'higher_is_better': True, 'scaling': 'weak',
-        'vs_baseline': None, 'dtype': 'fp32', 'data': 'synthetic',
+        'vs_baseline': None, 'data': 'synthetic',
+        'dtype': 'fp32' if args.sdf_train_precision == 'fp32' else
+                 'bf16 MFMA operands (hi/lo split, 3 products per MAC) on the parts tests/test_gpu_sdf_train.py '
+                 'allows, exact fp32 on the rest; fp32 accumulation',
         'config': {'workload': 'sdf_pdf training step (config 5: tpose_trainer losses incl. eikonal, observed '
                                'gradients, msk_sdf BCE, image MSE; Adam)', 'rays_per_gpu': R,
                    'sdf_train_precision': args.sdf_train_precision,
@@ -659,6 +724,8 @@ def bench_sdf_train(args, rank, world, dev):
                      'kept_samples_per_step': n_kept},
         'losses_last_step_rank_mean': losses,
     }
+    if not emit:
+        return result
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -412,6 +412,39 @@ int anr_sdf_network_train_bwd(const anr_sdf_params* p, float* const* grads, cons
                               const float* d_gradients, const float* d_observed_gradients, void* workspace,
                               size_t ws_bytes, void* stream);
 
+/* ---- sdf_pdf point helpers (the sdf mesh path, lib/networks/renderer/sdf_mesh_renderer.py:16-110) ----
+ * anr_sdf_points over n free points x (n,3) in the big-pose (canonical) space, exact fp32 products on the
+ * sdf training executor's layers (weight norm formed per call; f needs poses and latent_index only):
+ *   ANR_SDFP_NETWORK            tpose_human.sdf_network(x, batch) (anisdf_pdf_network.py:421-437):
+ *                               out (n,257) = [sdf || feature vector] (scale 1)
+ *   ANR_SDFP_GRADIENT           SDFNetwork.gradient(x) (:441-451): out (n,3) d sdf / d x, out2 (n) sdf (or NULL)
+ *   ANR_SDFP_DEFORMED_GRADIENT  Network.gradient_of_deformed_sdf(x, batch) (:140-154): out (n,3) the gradient
+ *                               of sdf(x + resd(x)) w.r.t. x (residual MLP included), out2 (n) that sdf (or NULL)
+ * The host reads nothing; the call is asynchronous on the stream. */
+#define ANR_SDFP_NETWORK 0
+#define ANR_SDFP_GRADIENT 1
+#define ANR_SDFP_DEFORMED_GRADIENT 2
+size_t anr_sdf_points_workspace_bytes(int n);
+int anr_sdf_points(const anr_sdf_params* p, const anr_sdf_frame* f, const float* x, int n, int mode, float* out,
+                   float* out2, void* workspace, size_t ws_bytes, void* stream);
+/* sample_blend_closest_points (lib/utils/sample_utils.py:323-348) of n free points against nv vertices
+ * (nv, 3) with their weights (nv, 24): the render front-end's exact 5-NN (lexicographic (d^2, index) ties)
+ * and inverse-distance blend. bw (n, 24) the blended weights and / or inside (n) = weighted distance
+ * < norm_th (no forced argmin: the sdf mesh path's filter, sdf_mesh_renderer.py:58-60). */
+size_t anr_knn_blend_workspace_bytes(int n);
+int anr_knn_blend(const float* verts, const float* weights, int nv, const float* pts, int n, float norm_th, float* bw,
+                  uint8_t* inside, void* workspace, size_t ws_bytes, void* stream);
+/* The sdf mesh path's posed vertices (sdf_mesh_renderer.py:96-101): pose_points_to_tpose_points(pts, bw,
+ * big_A), tpose_points_to_pose_points(., bw, A), pose_points_to_world_points(., R, Th) -> out (n, 3). */
+int anr_sdf_mesh_pose(const float* pts, const float* bw, int n, const float* big_A, const float* A, const float* R,
+                      const float* Th, float* out, void* stream);
+/* pts_sample_blend_weights (lib/utils/blend_utils.py:119-149; Network.calculate_bigpose_smpl_bw,
+ * anisdf_pdf_network.py:109-112): trilinear grid_sample (align_corners, border padding) of the volume vol
+ * (X,Y,Z,C) over bounds (2,3) at pts (n,3) -> out (C, n), the reference's (1, 25, n) without the batch axis,
+ * bit-exact in the reference's CPU accumulation order. */
+int anr_sample_volume(const float* vol, int X, int Y, int Z, int C, const float* bounds, const float* pts, int n,
+                      float* out, void* stream);
+
 /* ---- sdf_pdf training (config 5; lib/train/trainers/tpose_trainer.py:21-73, crit.py:5-19) ---------
  * anr_sdf_train_step: NetworkWrapper.forward + loss.backward() of one batch through the sdf_pdf
  *   network and tpose_renderer (anisdf_pdf_network.py:156-224 in training mode: gradients with
@@ -462,10 +495,14 @@ int anr_mc_emit(const float* vol, int X, int Y, int Z, int pad, double iso, doub
 
 /* ---- measurement ----------------------------------------------------------------------
  * When enabled, anr_render_fwd records a hipEvent pair around the fused network kernel (k_mlp)
- * on the caller's stream. anr_profile_read waits for the recorded events, returns the summed
+ * on the caller's stream, and anr_sdf_render_fwd one around each fused sdf_pdf network launch. anr_profile_read waits for the recorded events, returns the summed
  * kernel time (ms) and launch count since the last read, and resets. */
 int anr_profile_enable(int on);
 int anr_profile_read(double* mlp_ms, int* launches);
+/* anr_profile_read plus the median in-kernel shader clock (MHz) over every stamped workgroup of the
+ * profiled fused launches (thread 0 stamps s_memtime / s_memrealtime at entry and exit; 0 if none ran
+ * long enough): tells a DVFS-throttled box from a slower kernel. */
+int anr_profile_read_clock(double* mlp_ms, int* launches, double* clk_mhz);
 
 const char* anr_last_error(void);
 int anr_version(void);

@@ -318,7 +318,9 @@ class _RowTrace:
     ids (frame order) of the alpha_ind rows and the pre-activation sigma' of every kept sample."""
 
     def __init__(self, fn, n_samples):
-        self.fn, self.base, self.ids, self.sig = fn, 0, [], torch.zeros(n_samples, dtype=torch.float64)
+        self.fn, self.base, self.ids = fn, 0, []
+        self.sig = torch.zeros(n_samples, dtype=torch.float64)
+        self.margin = torch.full((n_samples,), float('inf'), dtype=torch.float64)
 
     def __call__(self, P, wpts, viewdir, dists, batch, trace=None, **kw):
         t = {}
@@ -326,7 +328,13 @@ class _RowTrace:
         kept = torch.nonzero(t['pind'][0])[:, 0] + self.base
         self.ids.append(kept[t['alpha_ind'][0]])
         self.sig = self.sig.to(kept.device)
+        self.margin = self.margin.to(kept.device)
         self.sig[kept] = t['sigma'][0].detach().double()
+        # signed distance of the T-pose point to the nearest face of the strict bbox test (negative outside;
+        # tpose_nerf_network.py:186-189)
+        tp = t['tpose'][0].detach().double()
+        lo, hi = batch['tbounds'][0, 0].double(), batch['tbounds'][0, 1].double()
+        self.margin[kept] = torch.minimum(tp - lo, hi - tp).amin(-1)
         self.base += wpts.shape[0]
         return ret
 
@@ -381,7 +389,8 @@ def test_split_precisions_fp32_level_full_frame(dev, monkeypatch):
     assert ids32.numel() == r32['pbw'].shape[1] and ids64.numel() == r64['pbw'].shape[1]
     k32, k64 = _keep(r32['raw']), _keep(r64['raw'])
     R = k32.numel() // 64
-    ray_ok = (k32 == k64).view(R, 64).all(1)
+    # rays whose 64 keep decisions agree in both oracle runs and hold no bbox-face tie (see below)
+    ray_ok = (k32 == k64).view(R, 64).all(1) & ~((t32.margin.abs() < 1e-6) | (t64.margin.abs() < 1e-6)).view(R, 64).any(1)
     assert ray_ok.float().mean().item() > 0.99, ray_ok.float().mean().item()
     both = (k32 & k64 & ray_ok.repeat_interleave(64))
 
@@ -412,16 +421,27 @@ def test_split_precisions_fp32_level_full_frame(dev, monkeypatch):
         assert ids.numel() == ret['pbw'].shape[1]
         assert bool((ids[1:] > ids[:-1]).all()), prec  # rows in frame order
         if prec == 'fp32':  # the exact kernel against the reference's own arithmetic, whole frame
-            for k in ('rgb_map', 'acc_map', 'depth_map', 'raw'):
-                err = float((ret[k] - r32[k]).abs().max())
+            # Threshold ties: a kept sample whose T-pose point lies within 1e-6 of a bbox face (the LBS
+            # inverse's rounding differs between the adjugate here and torch's LU inverse, ~1e-7) may be
+            # masked by one and not the other (measured: one sample of the 16.8 M, margin 4.5e-8). Such
+            # samples and their rays are counted and excluded from the 1e-4 bound, which every other ray /
+            # sample / row of the frame must meet.
+            tie = t32.margin.abs() < 1e-6
+            tie_ray = tie.view(R, 64).any(1)
+            assert int(tie_ray.sum()) <= max(4, R // 10000), int(tie_ray.sum())
+            for k in ('rgb_map', 'acc_map', 'depth_map'):
+                err = float((ret[k][0][~tie_ray] - r32[k][0][~tie_ray]).abs().max())
                 assert err <= 1e-4, (k, err)
+            err = float((ret['raw'][0][~tie] - r32['raw'][0][~tie]).abs().max())
+            assert err <= 1e-4, ('raw', err)
             ia, ib, only = _match_rows(ids, ids32)
             assert only.numel() <= max(8, ids32.numel() // 10000), only.numel()
-            if only.numel():
-                tie = (t32.sig[only.to(dev)] - 0.0).abs().max().item()  # train_th = 0 (config default)
-                assert tie <= 1e-4, tie
+            if only.numel():  # a row-set difference only at a tie: sigma' at train_th = 0, or a bbox tie
+                od = only.to(dev)
+                assert bool(((t32.sig[od].abs() <= 1e-4) | tie[od]).all()), (only, t32.sig[od], t32.margin[od])
+            row_ok = ~tie[ids32[ib.to(dev)]]
             for k in ('pbw', 'tbw'):
-                err = float((ret[k][0][ia.to(dev)] - r32[k][0][ib.to(dev)]).abs().max())
+                err = float((ret[k][0][ia.to(dev)][row_ok] - r32[k][0][ib.to(dev)][row_ok]).abs().max())
                 assert err <= 1e-4, (k, err)
         got[prec] = errs(ret, ids)
         del ret
