@@ -99,7 +99,8 @@ class SdfFrame(ctypes.Structure):
     _fields_ = [('A', ctypes.c_void_p), ('big_A', ctypes.c_void_p), ('R', ctypes.c_void_p), ('Th', ctypes.c_void_p),
                 ('poses', ctypes.c_void_p), ('pvertices', ctypes.c_void_p), ('weights', ctypes.c_void_p),
                 ('n_verts', ctypes.c_int), ('tbounds', ctypes.c_void_p), ('latent_index', ctypes.c_void_p),
-                ('occupancy', ctypes.c_void_p)]
+                ('occupancy', ctypes.c_void_p), ('n_views', ctypes.c_int), ('Ks', ctypes.c_void_p),
+                ('RT', ctypes.c_void_p), ('msks', ctypes.c_void_p), ('img_h', ctypes.c_int), ('img_w', ctypes.c_int)]
 
 
 class SdfRenderOut(ctypes.Structure):

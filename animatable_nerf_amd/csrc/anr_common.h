@@ -108,6 +108,27 @@ __device__ __forceinline__ void world_to_pose_pt(const float* __restrict__ wpts,
   else world_to_pose_small(x, R, Th, out);
 }
 
+// novel-view filter (tpose_renderer_mmsk.py:14-57): world point -> every training view (RT world ->
+// camera, K), rounded half-to-even, clamped to the image, looked up in that view's mask; visible = in all
+__device__ __forceinline__ bool visible_in_views(const float pts[3], int n_views, const float* __restrict__ Ks,
+                                                 const float* __restrict__ RT, const uint8_t* __restrict__ msks,
+                                                 int img_h, int img_w) {
+  bool vis = true;
+  for (int v = 0; v < n_views; ++v) {
+    const float* R = RT + 12 * v;
+    const float* K = Ks + 9 * v;
+    float q[3], s3[3];
+    for (int j = 0; j < 3; ++j) q[j] = fmaf(pts[2], R[4 * j + 2], fmaf(pts[1], R[4 * j + 1], pts[0] * R[4 * j])) + R[4 * j + 3];
+    for (int j = 0; j < 3; ++j) s3[j] = fmaf(q[2], K[3 * j + 2], fmaf(q[1], K[3 * j + 1], q[0] * K[3 * j]));
+    long long xi = (long long)rintf(s3[0] / s3[2]);
+    long long yi = (long long)rintf(s3[1] / s3[2]);
+    xi = xi < 0 ? 0 : (xi > img_w - 1 ? img_w - 1 : xi);
+    yi = yi < 0 ? 0 : (yi > img_h - 1 ? img_h - 1 : yi);
+    vis = vis && msks[((size_t)v * img_h + yi) * img_w + xi] != 0;
+  }
+  return vis;
+}
+
 // Positional-encoding feature f of gamma(x) (embedder.py:5-54): [x, sin(2^0 x), cos(2^0 x), ...]
 __device__ __forceinline__ float embed_feature(const float x[3], int f, int nfreq) {
   if (f < 3) return x[f];

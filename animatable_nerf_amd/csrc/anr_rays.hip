@@ -291,19 +291,7 @@ __global__ __launch_bounds__(1024) void k_frontend(FrontArgs a) {
     // novel-view filter (tpose_renderer_mmsk.py:14-57): world point -> every training view, rounded
     // half-to-even, clamped, looked up in its mask; the network then sees only visible samples, so
     // the per-chunk argmin runs over them (a chunk with none keeps nothing)
-    bool vis = true;
-    for (int v = 0; v < a.n_views; ++v) {
-      const float* R = a.RT + 12 * v;
-      const float* K = a.Ks + 9 * v;
-      float q[3], s3[3];
-      for (int j = 0; j < 3; ++j) q[j] = fmaf(pts[2], R[4 * j + 2], fmaf(pts[1], R[4 * j + 1], pts[0] * R[4 * j])) + R[4 * j + 3];
-      for (int j = 0; j < 3; ++j) s3[j] = fmaf(q[2], K[3 * j + 2], fmaf(q[1], K[3 * j + 1], q[0] * K[3 * j]));
-      long long xi = (long long)rintf(s3[0] / s3[2]);
-      long long yi = (long long)rintf(s3[1] / s3[2]);
-      xi = xi < 0 ? 0 : (xi > a.img_w - 1 ? a.img_w - 1 : xi);
-      yi = yi < 0 ? 0 : (yi > a.img_h - 1 ? a.img_h - 1 : yi);
-      vis = vis && a.msks[((size_t)v * a.img_h + yi) * a.img_w + xi] != 0;
-    }
+    const bool vis = visible_in_views(pts, a.n_views, a.Ks, a.RT, a.msks, a.img_h, a.img_w);
     const bool keep = vis && pn < a.norm_th;
     const uint64_t m = __ballot(keep);
     if (lane == 0) a.mask[ray] = m;

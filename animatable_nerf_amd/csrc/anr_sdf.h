@@ -57,6 +57,10 @@ struct SdfFrontArgs {
   uint32_t* knn;        // (R*64, 8): w[5] (float bits), idx (3 x u32, u16 pairs)
   float4* raw;          // (R*64) zero at non-kept samples
   float* sdf;           // (R*64) 10 at non-kept samples
+  int n_views;          // novel-view visibility filter (anr_sdf_frame), 0 = off
+  const float *Ks, *RT;
+  const uint8_t* msks;
+  int img_h, img_w;
 };
 
 // per-point kernels over one batch [b0, b0 + cnt) of the compact kept-sample list
@@ -100,7 +104,7 @@ struct SdfTensors {
 __global__ void k_sdf_front(SdfFrontArgs a);
 __global__ void k_sdf_wnorm(SdfTensors T, float* wimg);
 __global__ void k_sdf_fold(SdfTensors T, const float* wimg, const float* poses, const int64_t* li, float* fold);
-__global__ void k_sdf_tbtab(const float* tbounds, int nchunks, float* tbtab, float* tb_out);
+__global__ void k_sdf_tbtab(const float* tbounds, int nchunks, float* tbtab, float* tb_out, const uint64_t* chunk_min = nullptr);
 __global__ void k_sdf_prep(SdfPointArgs a);
 __global__ void k_knn_blend_out(const uint32_t* knn, const uint64_t* mask, const float* weights, int n, float* bw,
                                 uint8_t* inside);

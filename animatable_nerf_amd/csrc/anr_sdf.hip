@@ -143,6 +143,7 @@ __global__ __launch_bounds__(1024) void k_sdf_front(SdfFrontArgs a) {
     float p[3];
     const long pid_ = (long)ray * 64 + lane;
     const bool valid = !a.wpts || pid_ < a.n_pts;
+    bool vis = true;  // novel-view renders: the world sample projects inside every training view's mask
     if (a.wpts) {
       if (valid) world_to_pose_pt(a.wpts, pid_, a.n_pts, a.n_pts, a.R, a.Th, p);
       else p[0] = p[1] = p[2] = 0.f;
@@ -150,6 +151,7 @@ __global__ __launch_bounds__(1024) void k_sdf_front(SdfFrontArgs a) {
       float z, dist, pts[3];
       sample_point(a.ray_o, a.ray_d, a.near_, a.far_, a.t_rand, ray, lane, 64, z, dist, pts);
       world_to_pose(pts, a.R, a.Th, p);
+      if (a.n_views > 0) vis = visible_in_views(pts, a.n_views, a.Ks, a.RT, a.msks, a.img_h, a.img_w);
     }
     float b0 = INFINITY, b1 = INFINITY, b2 = INFINITY, b3 = INFINITY, b4 = INFINITY;
     int i0 = 0, i1 = 0, i2 = 0, i3 = 0, i4 = 0;
@@ -233,7 +235,7 @@ __global__ __launch_bounds__(1024) void k_sdf_front(SdfFrontArgs a) {
     rec[0] = make_uint4(__float_as_uint(w0), __float_as_uint(w1), __float_as_uint(w2), __float_as_uint(w3));
     rec[1] = make_uint4(__float_as_uint(w4), (uint32_t)i0 | ((uint32_t)i1 << 16), (uint32_t)i2 | ((uint32_t)i3 << 16),
                         (uint32_t)i4);
-    const bool keep = pn < a.norm_th;
+    const bool keep = vis && pn < a.norm_th;
     const uint64_t m = __ballot(keep);
     if (lane == 0) a.mask[ray] = m;
     if (!keep && valid) {
@@ -241,7 +243,7 @@ __global__ __launch_bounds__(1024) void k_sdf_front(SdfFrontArgs a) {
       a.sdf[pid] = 10.f;
     }
     const int rc = ray % a.chunk;
-    uint64_t key = valid ? ((uint64_t)__float_as_uint(pn) << 32) | (uint32_t)(rc * 64 + lane) : ~0ull;
+    uint64_t key = valid && vis ? ((uint64_t)__float_as_uint(pn) << 32) | (uint32_t)(rc * 64 + lane) : ~0ull;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
       const uint64_t o = __shfl_xor(key, off);
@@ -298,12 +300,15 @@ __global__ __launch_bounds__(256) void k_sdf_fold(SdfTensors T, const float* wim
 }
 
 // tbounds[0] -= 0.05; tbounds[1] += 0.05 once per chunk, in place on the batch (fp32)
-__global__ void k_sdf_tbtab(const float* tbounds, int nchunks, float* tbtab, float* tb_out) {
+// chunk_min != NULL (the visibility-filtered render): only chunks with a visible sample widen, the others
+// make no network call (tpose_renderer_mmsk.py:80-83)
+__global__ void k_sdf_tbtab(const float* tbounds, int nchunks, float* tbtab, float* tb_out, const uint64_t* chunk_min) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   float b[6];
   for (int k = 0; k < 6; ++k) b[k] = tbounds[k];
   for (int c = 0; c < nchunks; ++c) {
-    for (int k = 0; k < 3; ++k) { b[k] = b[k] - 0.05f; b[3 + k] = b[3 + k] + 0.05f; }
+    if (!chunk_min || chunk_min[c] != ~0ull)
+      for (int k = 0; k < 3; ++k) { b[k] = b[k] - 0.05f; b[3 + k] = b[3 + k] + 0.05f; }
     for (int k = 0; k < 6; ++k) tbtab[c * 6 + k] = b[k];
   }
   if (tb_out)

@@ -240,6 +240,8 @@ int check(const anr_sdf_params* p, const anr_sdf_frame* f, const float* ray_o, c
   if (f->n_verts <= 0 || f->n_verts > 6912) return fail(ANR_E_ARG, "sdf render: n_verts must be in [1, 6912]");
   if (!out->rgb_map || !out->acc_map || !out->depth_map || !out->raw || !out->sdf)
     return fail(ANR_E_ARG, "sdf render: NULL output");
+  if (f->n_views < 0 || (f->n_views > 0 && (!f->Ks || !f->RT || !f->msks || f->img_h <= 0 || f->img_w <= 0)))
+    return fail(ANR_E_ARG, "sdf render: bad visibility-filter views");
   return ANR_OK;
 }
 
@@ -314,8 +316,11 @@ int sdf_render_core(const anr_sdf_params* p, const anr_sdf_frame* f, const float
   ANR_TRY(check_launch("k_sdf_wnorm"));
   hipLaunchKernelGGL(k_sdf_fold, dim3(3), dim3(256), 0, s, T, (const float*)wimg, f->poses, f->latent_index, fold);
   ANR_TRY(check_launch("k_sdf_fold"));
-  hipLaunchKernelGGL(k_sdf_tbtab, dim3(1), dim3(64), 0, s, f->tbounds, nch, tbtab, out->tbounds_out);
-  ANR_TRY(check_launch("k_sdf_tbtab"));
+  const bool filt = !wpts && f->n_views > 0;  // visibility filter: widening depends on the front-end
+  if (!filt) {
+    hipLaunchKernelGGL(k_sdf_tbtab, dim3(1), dim3(64), 0, s, f->tbounds, nch, tbtab, out->tbounds_out, nullptr);
+    ANR_TRY(check_launch("k_sdf_tbtab"));
+  }
 
   // B1 front-end + ordered compaction
   SdfFrontArgs fa{};
@@ -325,8 +330,16 @@ int sdf_render_core(const anr_sdf_params* p, const anr_sdf_frame* f, const float
   fa.norm_th = o->norm_th; fa.mask = (uint64_t*)(ws + L.mask); fa.chunk_min = (uint64_t*)(ws + L.chunk_min);
   fa.knn = (uint32_t*)(ws + L.knn); fa.raw = raw; fa.sdf = out->sdf;
   const int grid_front = std::min(sdf_cus(), (R + 15) / 16);
+  if (filt) {
+    fa.n_views = f->n_views; fa.Ks = f->Ks; fa.RT = f->RT; fa.msks = f->msks; fa.img_h = f->img_h; fa.img_w = f->img_w;
+  }
   hipLaunchKernelGGL(k_sdf_front, dim3(grid_front), dim3(1024), 0, s, fa);
   ANR_TRY(check_launch("k_sdf_front"));
+  if (filt) {
+    hipLaunchKernelGGL(k_sdf_tbtab, dim3(1), dim3(64), 0, s, f->tbounds, nch, tbtab, out->tbounds_out,
+                       (const uint64_t*)fa.chunk_min);
+    ANR_TRY(check_launch("k_sdf_tbtab (visible chunks)"));
+  }
   CompactArgs ca{};
   ca.n_rays = R; ca.chunk = chunk; ca.mask = fa.mask; ca.chunk_min = fa.chunk_min;
   ca.ray_off = (int*)(ws + L.ray_off); ca.block_sum = (int*)(ws + L.block_sum); ca.list = (int*)(ws + L.list);
@@ -576,6 +589,7 @@ int check_points(const anr_sdf_params* p, const anr_sdf_frame* f, const anr_samp
       !f->latent_index)
     return fail(ANR_E_ARG, "sdf network: NULL frame tensor");
   if (f->n_verts <= 0 || f->n_verts > 6912) return fail(ANR_E_ARG, "sdf network: n_verts must be in [1, 6912]");
+  if (f->n_views) return fail(ANR_E_ARG, "sdf network: the visibility filter is a renderer option (n_views must be 0)");
   return ANR_OK;
 }
 

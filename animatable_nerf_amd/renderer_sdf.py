@@ -53,6 +53,7 @@ def widen_tbounds(tbounds, k):
 
 class Renderer:
     widens_tbounds = True  # per chunk, in place (anisdf_pdf_network.py:204-206)
+    visibility_filter = False  # renderer_sdf_mmsk.Renderer turns it on
 
     def __init__(self, net, cfg=None):
         self.net = net
@@ -96,13 +97,20 @@ class Renderer:
             setattr(f, k, fr[k].data_ptr())
         f.n_verts = fr['pvertices'].shape[-2]
         f.latent_index, f.occupancy = li.data_ptr(), occ.data_ptr()
+        views = {}
+        if self.visibility_filter:  # renderer_sdf_mmsk: tpose_renderer_mmsk.py:14-57 on the device
+            views = {k: _f32(batch[k], dev) for k in ('Ks', 'RT')}
+            views['msks'] = batch['msks'].to(device=dev, dtype=torch.uint8).contiguous()
+            f.n_views = int(views['Ks'].shape[1])
+            f.Ks, f.RT, f.msks = views['Ks'].data_ptr(), views['RT'].data_ptr(), views['msks'].data_ptr()
+            f.img_h, f.img_w = int(batch['H']), int(batch['W'])
         o = _lib.RenderOpts()
         o.n_samples, o.chunk, o.norm_th, o.train_th = ns, int(self.cfg.get('chunk', CHUNK)), NORM_TH, 0.0
         o.t_rand = tr.data_ptr() if tr is not None else None
         o.novel_pose = 0
         o.precision = _sdf_precision(self.cfg)
         return {'p': p, 'dev': dev, 'R': R, 'ns': ns, 'rays': rays, 'fr': fr, 't_rand': tr, 'li': li, 'occ': occ,
-                'frame': f, 'opts': o}
+                'frame': f, 'opts': o, 'views': views}
 
     def render_device(self, batch, t_rand=None, chunk_offset=0, bw_rows=True):
         """All outputs stay in HBM; ``batch['tbounds']`` is widened in place (reference quirk).

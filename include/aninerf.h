@@ -342,6 +342,16 @@ typedef struct anr_sdf_frame {
   const float* tbounds;    /* (2,3) batch['tbounds'] as passed in */
   const int64_t* latent_index;  /* (1) colour latent row */
   const uint8_t* occupancy;     /* (R) batch['occupancy'] */
+  /* novel-view visibility filter of tpose_renderer_mmsk (:14-57, the config-5 novel_view_cfg /
+   * pose_sequence_cfg renderer over this network), anr_sdf_render_fwd only; n_views = 0 disables it. A
+   * sample reaches the network only if it projects inside every training view's mask: the KNN keep and
+   * the per-chunk forced argmin range over the visible samples (one Network.forward call per chunk on
+   * them), and tbounds widens only at chunks with a visible sample (a chunk without one makes no call). */
+  int n_views;
+  const float* Ks;         /* (V,3,3) device */
+  const float* RT;         /* (V,3,4) device, world -> camera */
+  const uint8_t* msks;     /* (V,img_h,img_w) device */
+  int img_h, img_w;
 } anr_sdf_frame;
 
 typedef struct anr_sdf_render_out {
