@@ -437,7 +437,7 @@ __device__ __forceinline__ float softplus100(float x) {
 // small, so the factor keeps its relative precision where it is tiny)
 __device__ __forceinline__ float softplus100_acc(float x) {
   const float z = 100.f * x;
-  return z > 20.f ? x : fast_log1p(fast_exp(z)) / 100.f;
+  return z > 20.f ? x : div_const(fast_log1p(fast_exp(z)), 100.f, 0.00999999977648258f);
 }
 __device__ __forceinline__ float softplus_factor_h_acc(float h) {
   const float t = 100.f * h;
@@ -546,12 +546,12 @@ __device__ __forceinline__ void layer_x3(Pipe& p, const f32x4 (&in)[NIN], const 
             *(f32x4*)(d + 16) = f32x4{x[4], x[5], x[6], x[7]};
 #endif
           } else {
-            const float sqrt2 = 1.41421356237309515f;
+            const float sqrt2 = 1.41421356237309515f, rs2 = 0.707106769084930420f;  // RN(1 / RN(sqrt2))
             const int c = 32 * ts + 4 * g;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-              if (c + j < 217) d[j] = x[j] / sqrt2;
-              if (c + 16 + j < 217) d[16 + j] = x[4 + j] / sqrt2;
+              if (c + j < 217) d[j] = div_const(x[j], sqrt2, rs2);
+              if (c + 16 + j < 217) d[16 + j] = div_const(x[4 + j], sqrt2, rs2);
             }
           }
         }
@@ -739,12 +739,12 @@ __device__ __forceinline__ void layer(Pipe& p, const f32x4 (&in)[NIN], const flo
               __builtin_nontemporal_store(f32x4{x[0], x[1], x[2], x[3]}, (f32x4*)d);
               __builtin_nontemporal_store(f32x4{x[4], x[5], x[6], x[7]}, (f32x4*)(d + 16));
             } else {
-              const float sqrt2 = 1.41421356237309515f;
+              const float sqrt2 = 1.41421356237309515f, rs2 = 0.707106769084930420f;  // RN(1 / RN(sqrt2))
               const int c = 32 * ts + 4 * g;
 #pragma unroll
               for (int j = 0; j < 4; ++j) {
-                if (c + j < 217) d[j] = x[j] / sqrt2;
-                if (c + 16 + j < 217) d[16 + j] = x[4 + j] / sqrt2;
+                if (c + j < 217) d[j] = div_const(x[j], sqrt2, rs2);
+                if (c + 16 + j < 217) d[16 + j] = div_const(x[4 + j], sqrt2, rs2);
               }
             }
           }
