@@ -6,7 +6,7 @@ SRCS := $(SRC_DIR)/anr_capi.hip $(SRC_DIR)/anr_rays.hip $(SRC_DIR)/anr_mlp.hip $
         $(SRC_DIR)/anr_gemm.hip $(SRC_DIR)/anr_train.hip $(SRC_DIR)/anr_train_capi.hip \
         $(SRC_DIR)/anr_sdf.hip $(SRC_DIR)/anr_sdf_capi.hip $(SRC_DIR)/anr_mlp_b16.hip \
         $(SRC_DIR)/anr_alpha.hip $(SRC_DIR)/anr_alpha_b16.hip $(SRC_DIR)/anr_mesh.hip $(SRC_DIR)/anr_tgemm.hip $(SRC_DIR)/anr_lgemm.hip \
-        $(SRC_DIR)/anr_sdf_train.hip $(SRC_DIR)/anr_resd_b16.hip $(SRC_DIR)/anr_resd_x6.hip $(SRC_DIR)/anr_mlp_x6.hip $(SRC_DIR)/anr_alpha_x6.hip
+        $(SRC_DIR)/anr_sdf_train.hip $(SRC_DIR)/anr_resd_b16.hip $(SRC_DIR)/anr_resd_x6.hip $(SRC_DIR)/anr_mlp_x6.hip $(SRC_DIR)/anr_alpha_x6.hip $(SRC_DIR)/anr_tchain.hip
 OBJS := $(SRCS:.hip=.o)
 DEPS := $(OBJS:.o=.d)
 LIB := animatable_nerf_amd/libaninerf_hip.so

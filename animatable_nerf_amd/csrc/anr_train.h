@@ -152,6 +152,43 @@ struct WGradGroup {
 };
 int launch_wgrad_group(const WGrad* d, int nd, int n_host, int nz, float* slab, size_t slab_floats, hipStream_t s);
 
+// fused forward chains of the bf16 training executor (anr_tchain.hip): program 0 = the blend-weight
+// MLP (9 layers), 1 = the canonical NeRF (8 layers + feature||alpha, latent, view, rgb). Weight image
+// per program (tchain_image_bytes), packed from the layers' fp32 weights every call (tchain_pack).
+struct TcPackLayer {
+  const float* W;   // rows 0 .. n1-1
+  int in_ch, n1;
+  const float* W2;  // rows n1 .. n1+n2-1 (feature_fc || alpha_fc), or NULL
+  int in_ch2, n2;
+  int cmem, kmem_cols;    // the memory segment's first column in W and its width
+  int cprev, kprev_cols;  // the previous layer's columns
+  long start;             // filled by tchain_pack
+  int ob, kmem, kprev, mem_first;
+};
+struct TcPackArgs {
+  TcPackLayer L[12];
+  int nl;
+  long total;
+  unsigned short* out;
+};
+struct TcArgs {
+  const unsigned char* img;
+  const float* bias[12];  // per layer (nout[l] floats)
+  const float* bias2;     // program 1: alpha_fc's bias (row 256 of feature || alpha)
+  int nout[12];
+  void* out[12];          // per layer: bf16 rows (hidden, feature, latent) or fp32 rows (heads)
+  int ldo[12];
+  float* out2;            // program 1: alpha (fp32, one per sample)
+  const unsigned short* mem;   // gamma rows (bf16)
+  int ld_mem, kmem_cols;
+  const unsigned short* mem2;  // program 1: gamma(dir) rows (bf16)
+  int ld_mem2, kmem2_cols;
+  const int* M_dev;       // kept-sample count (device)
+};
+size_t tchain_image_bytes(int prog);
+int tchain_pack(int prog, TcPackArgs a, void* dst, hipStream_t s);
+int tchain_run(int prog, const TcArgs& a, int cap, int cus, hipStream_t s);
+
 // split-bf16 layer GEMM with LDS-resident weight images for large M (anr_lgemm.hip; the sdf_pdf
 // batches): lgemm_supported(g) (g.x3, no accumulate / mask / atomics, 16-B addressable operands),
 // the weight image (lgemm_image_bytes, packed once per weight set by lgemm_pack), then lgemm_run.

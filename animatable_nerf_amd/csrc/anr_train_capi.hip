@@ -34,7 +34,7 @@ struct TLayout {
   Layout L;
   size_t pt, Gp, Ip, Gv, Lp, lbs, Gt, It, Lt, Hp, Ht, Hn, Feat, Alpha, Lat, View, Rgbl;
   size_t draw, dRgb, dAlpha, dA16, dBp, dBt, dLp, dLt, dIt, dGt, dGt2, dHn, dHt, dHp, dFeat, dLat, dView;
-  size_t ysum, acc3, d_rgb, d_pbw, d_tbw, wimg, wslab, total;
+  size_t ysum, acc3, d_rgb, d_pbw, d_tbw, wimg, wslab, tcimg, total;
 };
 
 TLayout tlayout(int n_rays, int chunk, long np, long nt) {
@@ -62,6 +62,7 @@ TLayout tlayout(int n_rays, int chunk, long np, long nt) {
   T.ysum = take(8 * 256); T.acc3 = take(4); T.d_rgb = take(R * 3); T.d_pbw = take(N * 24); T.d_tbw = take(N * 24);
   T.wimg = take((wimg_bytes() + 3) / 4);
   T.wslab = take(kLaneFloats * kWStreams);
+  T.tcimg = take((tchain_image_bytes(0) + tchain_image_bytes(1) + 3) / 4);  // fused-chain images (anr_tchain.hip)
   T.total = o;
   return T;
 }
@@ -612,6 +613,73 @@ int bw_backward(Exec& e, const float* const* W, float* const* g, const float* G,
   return ANR_OK;
 }
 
+// ---- fused forward chains (anr_tchain.hip) for the bf16 storage policies -------------------------
+// ANR_TRAIN_FCHAIN (read per call, default 1): each MLP of the training forward as one launch with its
+// activations in registers (the pose-space BW MLP too under bf16_all); 0 = one row-GEMM launch per layer
+bool fchain_on() {
+  const char* v = getenv("ANR_TRAIN_FCHAIN");
+  return !(v && v[0] == '0');
+}
+int chain_cus() {
+  static int cus = 0;
+  if (!cus) {
+    int d = 0, v = 0;
+    cus = hipGetDevice(&d) == hipSuccess && hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, d) == hipSuccess && v > 0
+              ? v : 256;
+  }
+  return cus;
+}
+// pack the BW (program 0) and NeRF (program 1) images from this call's weights
+int chain_pack(const anr_params* p, unsigned char* img, hipStream_t s) {
+  const float* const* W = p->t + 27;  // the blend-weight field: [bw_latent, bw_linears.{0..7}.{w,b}, bw_fc.{w,b}]
+  TcPackArgs bw{};
+  const int bw_in[9] = {191, 256, 256, 256, 256, 447, 256, 256, 256};
+  for (int l = 0; l < 9; ++l) {
+    TcPackLayer& L = bw.L[l];
+    L.W = W[1 + 2 * l];
+    L.in_ch = bw_in[l];
+    L.n1 = l == 8 ? 24 : 256;
+    L.cmem = 0; L.kmem_cols = 63;
+    L.cprev = l == 5 ? 191 : 0; L.kprev_cols = 256;
+  }
+  if (tchain_pack(0, bw, img, s) != 0) return check_launch("k_tc_pack (bw)");
+  TcPackArgs nf{};
+  const int nf_in[8] = {63, 256, 256, 256, 256, 319, 256, 256};
+  for (int l = 0; l < 8; ++l) {
+    TcPackLayer& L = nf.L[l];
+    L.W = p->t[1 + 2 * l];
+    L.in_ch = nf_in[l];
+    L.n1 = 256;
+    L.cmem = 0; L.kmem_cols = 63;
+    L.cprev = l == 5 ? 63 : 0; L.kprev_cols = 256;
+  }
+  nf.L[8] = TcPackLayer{p->t[19], 256, 256, p->t[17], 256, 1, 0, 0, 0, 256};   // feature_fc || alpha_fc
+  nf.L[9] = TcPackLayer{p->t[21], 384, 256, nullptr, 0, 0, 0, 0, 0, 256};      // latent_fc (latent folded)
+  nf.L[10] = TcPackLayer{p->t[23], 283, 128, nullptr, 0, 0, 256, 27, 0, 256};  // view_fc [latent, gamma(dir)]
+  nf.L[11] = TcPackLayer{p->t[25], 128, 3, nullptr, 0, 0, 0, 0, 0, 128};       // rgb_fc
+  if (tchain_pack(1, nf, img + tchain_image_bytes(0), s) != 0) return check_launch("k_tc_pack (nerf)");
+  return ANR_OK;
+}
+// one BW MLP pass (latent folds f0 / f5) over the kept samples: gamma rows G (bf16, ld 64) -> H (bf16
+// rows, layer l at H + l S floats) and the logits (fp32, ld 32)
+int chain_bw(const Exec& e, const anr_params* p, const unsigned char* img, const float* G, float* H, float* logits,
+             long N, const float* f0, const float* f5, hipStream_t s) {
+  const float* const* W = p->t + 27;
+  TcArgs a{};
+  a.img = img;
+  const long S = N * 256;
+  for (int l = 0; l < 9; ++l) {
+    a.bias[l] = l == 0 ? f0 : l == 5 ? f5 : W[2 + 2 * l];
+    a.nout[l] = l == 8 ? 24 : 256;
+    a.out[l] = l == 8 ? (void*)logits : (void*)(H + l * S);
+    a.ldo[l] = l == 8 ? 32 : 256;
+  }
+  a.mem = (const unsigned short*)G; a.ld_mem = 64; a.kmem_cols = 63;
+  a.M_dev = e.n_dev;
+  if (tchain_run(0, a, e.grid_n(), chain_cus(), s) != 0) return check_launch("k_tchain_bw");
+  return ANR_OK;
+}
+
 // x != NULL: free samples (Network.forward, anr_network_train_fwd): R groups of 64, no compositing
 int train_forward(const anr_params* p, const anr_frame* f, const float* ray_o, const float* ray_d, const float* near_,
                   const float* far_, int R, const anr_render_opts* o, const anr_render_out* out, char* ws,
@@ -631,8 +699,15 @@ int train_forward(const anr_params* p, const anr_frame* f, const float* ray_o, c
     hipLaunchKernelGGL(k_tr_point_prep, dim3((n + 3) / 4), dim3(256), 0, s, b);
     ANR_TRY(check_launch("k_tr_point_prep"));
   }
+  // fused forward chains under the bf16 storage policies (every hidden row bf16): the T-pose BW MLP and
+  // the NeRF, and the pose-space BW MLP when it is bf16 too (bf16_all)
+  const bool fchain = e.hb && fchain_on() && n > 0;
+  unsigned char* tcimg = (unsigned char*)(ws + T.tcimg);
+  if (fchain) ANR_TRY(chain_pack(p, tcimg, s));
   // pose-space BW MLP (latent_index + 1), softmax + LBS, T-pose BW MLP (latent 0)
-  {
+  if (fchain && !e.pose_fp32) {
+    ANR_TRY(chain_bw(e, p, tcimg, b.Gp, (float*)(ws + T.Hp), b.Lp, N, FOLD(0), FOLD(2), s));
+  } else {
     PoseScope ps(e);
     ANR_TRY(bw_forward(e, p->t + 27, b.Gp, (float*)(ws + T.Hp), b.Lp, N, FOLD(0), FOLD(2)));
   }
@@ -645,7 +720,8 @@ int train_forward(const anr_params* p, const anr_frame* f, const float* ray_o, c
   ANR_TRY(order(e.ss, s2, s));
   {
     OnStream on(e, s2);
-    ANR_TRY(bw_forward(e, p->t + 27, b.Gt, (float*)(ws + T.Ht), b.Lt, N, FOLD(1), FOLD(3)));
+    if (fchain) ANR_TRY(chain_bw(e, p, tcimg, b.Gt, (float*)(ws + T.Ht), b.Lt, N, FOLD(1), FOLD(3), s2));
+    else ANR_TRY(bw_forward(e, p->t + 27, b.Gt, (float*)(ws + T.Ht), b.Lt, N, FOLD(1), FOLD(3)));
     if (n > 0) {
       hipLaunchKernelGGL(k_tr_softmax_t, dim3(g1), dim3(256), 0, s2, b);
       ANR_TRY(check_launch("k_tr_softmax_t"));
@@ -657,7 +733,24 @@ int train_forward(const anr_params* p, const anr_frame* f, const float* ray_o, c
   float* Feat = (float*)(ws + T.Feat);
   float* Lat = (float*)(ws + T.Lat);
   float* View = (float*)(ws + T.View);
-  {
+  if (fchain) {
+    TcArgs a{};
+    a.img = tcimg + tchain_image_bytes(0);
+    for (int l = 0; l < 8; ++l) {
+      a.bias[l] = PT(2 + 2 * l);
+      a.nout[l] = 256;
+      a.out[l] = Hn + l * S;
+      a.ldo[l] = 256;
+    }
+    a.bias[8] = PT(20); a.bias2 = PT(18); a.nout[8] = 256; a.out[8] = Feat; a.ldo[8] = 256; a.out2 = b.Alpha;
+    a.bias[9] = FOLD(4); a.nout[9] = 256; a.out[9] = Lat; a.ldo[9] = 256;
+    a.bias[10] = PT(24); a.nout[10] = 128; a.out[10] = View; a.ldo[10] = 128;
+    a.bias[11] = PT(26); a.nout[11] = 3; a.out[11] = b.Rgbl; a.ldo[11] = 4;
+    a.mem = (const unsigned short*)b.Gt; a.ld_mem = 64; a.kmem_cols = 63;
+    a.mem2 = (const unsigned short*)b.Gv; a.ld_mem2 = 64; a.kmem2_cols = 27;
+    a.M_dev = e.n_dev;
+    if (tchain_run(1, a, e.grid_n(), chain_cus(), s) != 0) return check_launch("k_tchain_nf");
+  } else {
     const unsigned h = e.hb ? (BF_A | BF_C) : 0, a = e.hb ? BF_A : 0;  // gamma, H, Feat, Lat bf16 under e.hb
     ANR_TRY(e.fwd(Hn, 256, 256, PT(1), 63, PT(2), true, b.Gt, 64, 63, 0, nullptr, 0, 0, 0, h));
     for (int l = 1; l < 8; ++l) {
