@@ -38,4 +38,11 @@ $(PROBE): tools/gemm_probe.hip $(SRC_DIR)/anr_tgemm.hip $(SRC_DIR)/anr_gemm.o $(
 	$(HIPCC) $(CXXFLAGS) -c tools/gemm_probe.hip -o tools/gemm_probe.o
 	$(HIPCC) $(CXXFLAGS) -DRG_TIMING -c $(SRC_DIR)/anr_tgemm.hip -o tools/gemm_probe_tgemm.o
 	$(HIPCC) --offload-arch=$(ARCH) -o $@ tools/gemm_probe.o tools/gemm_probe_tgemm.o $(filter %.o,$^)
-.PHONY: probe
+# fused-chain timing probe (tools/tchain_probe.hip); TCP_FLAGS selects -D variants of the chain kernels
+TCPROBE := tools/tchain_probe
+tchain-probe: $(TCPROBE)
+$(TCPROBE): tools/tchain_probe.hip $(SRC_DIR)/anr_tchain.hip $(SRC_DIR)/anr_train.h
+	$(HIPCC) $(CXXFLAGS) $(TCP_FLAGS) -c $(SRC_DIR)/anr_tchain.hip -o tools/tchain_probe_k.o
+	$(HIPCC) $(CXXFLAGS) -c tools/tchain_probe.hip -o tools/tchain_probe.o
+	$(HIPCC) --offload-arch=$(ARCH) -o $@ tools/tchain_probe.o tools/tchain_probe_k.o
+.PHONY: probe tchain-probe

@@ -46,29 +46,53 @@ __device__ __forceinline__ void tc_for(F&& f) {
 // one layer of a chain program
 struct TcL {
   int ob;          // output blocks of 16 neurons
-  int kmem;        // k-steps (32 inputs) from a memory segment (bf16 rows), 0 = none
+  int kmem;        // k-steps (32 inputs) from a memory segment (rows), 0 = none
   int kprev;       // k-steps from the previous layer's outputs (registers)
   int mem_first;   // the memory segment's k-steps come first (weight-image and MFMA order)
   int relu;
-  int out;         // TC_BF16 rows, TC_F32 rows, TC_FA (feature bf16 || alpha fp32)
-  int mem2;        // the memory segment is the second memory operand (gamma(dir))
+  int out;         // TC_BF16 / TC_F32 rows, TC_FA (feature bf16 || alpha fp32), TC_SPLIT (blocks 0..15 bf16 rows,
+                   // the rest fp32 aux rows), TC_AUX (every block fp32 aux rows)
+  int mem2;        // the memory segment is the second memory operand
+  int mask;        // backward: multiply by the ReLU mask (H > 0) of the forward's activations, read from the
+                   // mask bits the forward chain wrote (TcArgs::bits), LDS-DMA'd with the layer's first slice
+  int aux_add;     // TC_SPLIT / TC_AUX: add into the aux rows (else store)
 };
-enum { TC_BF16 = 0, TC_F32 = 1, TC_FA = 2 };
+enum { TC_BF16 = 0, TC_F32 = 1, TC_FA = 2, TC_SPLIT = 3, TC_AUX = 4 };
 
+// forward programs: 0 the blend-weight MLP, 1 the NeRF with its heads
 constexpr TcL kProgBW[9] = {
-    {16, 2, 0, 1, 1, TC_BF16, 0}, {16, 0, 8, 0, 1, TC_BF16, 0}, {16, 0, 8, 0, 1, TC_BF16, 0},
-    {16, 0, 8, 0, 1, TC_BF16, 0}, {16, 0, 8, 0, 1, TC_BF16, 0}, {16, 2, 8, 1, 1, TC_BF16, 0},
-    {16, 0, 8, 0, 1, TC_BF16, 0}, {16, 0, 8, 0, 1, TC_BF16, 0}, {2, 0, 8, 0, 0, TC_F32, 0}};
+    {16, 2, 0, 1, 1, TC_BF16, 0, 0, 0}, {16, 0, 8, 0, 1, TC_BF16, 0, 0, 0}, {16, 0, 8, 0, 1, TC_BF16, 0, 0, 0},
+    {16, 0, 8, 0, 1, TC_BF16, 0, 0, 0}, {16, 0, 8, 0, 1, TC_BF16, 0, 0, 0}, {16, 2, 8, 1, 1, TC_BF16, 0, 0, 0},
+    {16, 0, 8, 0, 1, TC_BF16, 0, 0, 0}, {16, 0, 8, 0, 1, TC_BF16, 0, 0, 0}, {2, 0, 8, 0, 0, TC_F32, 0, 0, 0}};
 constexpr TcL kProgNF[12] = {
-    {16, 2, 0, 1, 1, TC_BF16, 0}, {16, 0, 8, 0, 1, TC_BF16, 0}, {16, 0, 8, 0, 1, TC_BF16, 0},
-    {16, 0, 8, 0, 1, TC_BF16, 0}, {16, 0, 8, 0, 1, TC_BF16, 0}, {16, 2, 8, 1, 1, TC_BF16, 0},
-    {16, 0, 8, 0, 1, TC_BF16, 0}, {16, 0, 8, 0, 1, TC_BF16, 0}, {17, 0, 8, 0, 0, TC_FA, 0},
-    {16, 0, 8, 0, 0, TC_BF16, 0}, {8, 1, 8, 0, 1, TC_F32, 1}, {1, 0, 4, 0, 0, TC_F32, 0}};
+    {16, 2, 0, 1, 1, TC_BF16, 0, 0, 0}, {16, 0, 8, 0, 1, TC_BF16, 0, 0, 0}, {16, 0, 8, 0, 1, TC_BF16, 0, 0, 0},
+    {16, 0, 8, 0, 1, TC_BF16, 0, 0, 0}, {16, 0, 8, 0, 1, TC_BF16, 0, 0, 0}, {16, 2, 8, 1, 1, TC_BF16, 0, 0, 0},
+    {16, 0, 8, 0, 1, TC_BF16, 0, 0, 0}, {16, 0, 8, 0, 1, TC_BF16, 0, 0, 0}, {17, 0, 8, 0, 0, TC_FA, 0, 0, 0},
+    {16, 0, 8, 0, 0, TC_BF16, 0, 0, 0}, {8, 1, 8, 0, 1, TC_F32, 1, 0, 0}, {1, 0, 4, 0, 0, TC_F32, 0, 0, 0}};
+// input-gradient programs (transposed weights, no bias): 2 the blend-weight MLP from the logit gradient
+// (bw_fc, layers 7..0; layer 5 also the gamma gradient, stored; layer 0 adds its gamma gradient);
+// 3 the NeRF from d rgb (rgb_fc with the View ReLU mask, view_fc to the latent input, latent_fc,
+// feature_fc || alpha_fc with d alpha, layers 7..0 as in 2)
+constexpr TcL kProgBWB[9] = {
+    {16, 1, 0, 1, 0, TC_BF16, 0, 1, 0}, {16, 0, 8, 0, 0, TC_BF16, 0, 1, 0}, {16, 0, 8, 0, 0, TC_BF16, 0, 1, 0},
+    {20, 0, 8, 0, 0, TC_SPLIT, 0, 1, 0}, {16, 0, 8, 0, 0, TC_BF16, 0, 1, 0}, {16, 0, 8, 0, 0, TC_BF16, 0, 1, 0},
+    {16, 0, 8, 0, 0, TC_BF16, 0, 1, 0}, {16, 0, 8, 0, 0, TC_BF16, 0, 1, 0}, {4, 0, 8, 0, 0, TC_AUX, 0, 0, 1}};
+constexpr TcL kProgNFB[12] = {
+    {8, 1, 0, 1, 0, TC_F32, 0, 1, 0},   {16, 0, 4, 0, 0, TC_BF16, 0, 0, 0}, {16, 0, 8, 0, 0, TC_BF16, 0, 0, 0},
+    {16, 1, 8, 0, 0, TC_BF16, 1, 1, 0}, {16, 0, 8, 0, 0, TC_BF16, 0, 1, 0}, {16, 0, 8, 0, 0, TC_BF16, 0, 1, 0},
+    {20, 0, 8, 0, 0, TC_SPLIT, 0, 1, 0}, {16, 0, 8, 0, 0, TC_BF16, 0, 1, 0}, {16, 0, 8, 0, 0, TC_BF16, 0, 1, 0},
+    {16, 0, 8, 0, 0, TC_BF16, 0, 1, 0}, {16, 0, 8, 0, 0, TC_BF16, 0, 1, 0}, {4, 0, 8, 0, 0, TC_AUX, 0, 0, 1}};
 
 template <int P>
-__host__ __device__ constexpr int tc_nl() { return P == 0 ? 9 : 12; }
+__host__ __device__ constexpr int tc_nl() { return (P == 0 || P == 2) ? 9 : 12; }
 template <int P>
-__host__ __device__ constexpr TcL tc_layer(int l) { return P == 0 ? kProgBW[l] : kProgNF[l]; }
+__host__ __device__ constexpr TcL tc_layer(int l) {
+  return P == 0 ? kProgBW[l] : P == 1 ? kProgNF[l] : P == 2 ? kProgBWB[l] : kProgNFB[l];
+}
+template <int P>
+__host__ __device__ constexpr bool tc_bwd() { return P >= 2; }
+// k-steps of the programs' memory operands (loaded once per tile): gamma 2 (forward), the logit / rgb
+// gradient 1 (backward); the second operand (gamma(dir), d alpha) 1
 template <int P>
 __host__ __device__ constexpr int tc_ks(int l) { return tc_layer<P>(l).kmem + tc_layer<P>(l).kprev; }
 // first slice of layer l, total slices
@@ -97,24 +121,89 @@ __host__ __device__ constexpr int tc_slice_kb(int q) {
 template <int P>
 __host__ __device__ constexpr int tc_image_kb() { return tc_slice_kb<P>(tc_nslices<P>()); }
 template <int P>
-__host__ __device__ constexpr int tc_obmax() { return P == 0 ? 16 : 17; }
+__host__ __device__ constexpr int tc_obmax() { return P == 0 ? 16 : P == 1 ? 17 : 20; }
+template <int P>
+__host__ __device__ constexpr int tc_memk() { return tc_bwd<P>() ? 1 : 2; }
 // LDS-DMA pieces (1 KiB) every wave issues per slice (pieces past a slice's out-blocks repeat its last)
 template <int P>
 __host__ __device__ constexpr int tc_pieces() { return (tc_obmax<P>() + 7) / 8; }
-constexpr int TC_NB = 4;  // ring slots
-// bias table: per layer ob x 16 floats
+// ring slots: a slice certified at the middle of the slice before it was issued NB - 2 slices earlier,
+// so NB - 2 slices of MFMA work cover the L2 latency of the weight stream (4 slots: 1.5 us per slice
+// measured on a 195-tile BW pass, latency-bound; 8 / 7 fill what the LDS holds)
+#ifndef TC_NB_BW
+#define TC_NB_BW 8
+#endif
+#ifndef TC_NB_NF
+#define TC_NB_NF 6
+#endif
+#ifndef TC_NB_BWD
+#define TC_NB_BWD 7
+#endif
+template <int P>
+__host__ __device__ constexpr int tc_nb() { return tc_bwd<P>() ? TC_NB_BWD : P == 0 ? TC_NB_BW : TC_NB_NF; }
+// mask slots (backward): the 128 x 256-bit ReLU mask of a layer's outputs for the tile (4 KiB)
+constexpr int TC_MS = 4;
+// timing experiments on the input-gradient programs only (tools/build_ab.sh; results are NOT gradients):
+// 1 no MFMA, 2 no weight / mask DMA (zeroed ring), 3 no vmcnt waits
+#ifndef TC_EXP_BWD
+#define TC_EXP_BWD 0
+#endif
+// bias table: per layer ob x 16 floats (forward programs)
 template <int P>
 __host__ __device__ constexpr int tc_bias_off(int l) {
   int o = 0;
-  for (int i = 0; i < l; ++i) o += tc_layer<P>(i).ob * 16;
+  if (!tc_bwd<P>())
+    for (int i = 0; i < l; ++i) o += tc_layer<P>(i).ob * 16;
   return o;
 }
 template <int P>
-__host__ __device__ constexpr int tc_lds_bytes() {
-  return (tc_bias_off<P>(tc_nl<P>()) * 4 + 255) / 256 * 256 + TC_NB * tc_obmax<P>() * 1024;
+__host__ __device__ constexpr int tc_ring_off() { return (tc_bias_off<P>(tc_nl<P>()) * 4 + 255) / 256 * 256; }
+template <int P>
+__host__ __device__ constexpr int tc_mask_off() { return tc_ring_off<P>() + tc_nb<P>() * tc_obmax<P>() * 1024; }
+template <int P>
+__host__ __device__ constexpr int tc_lds_bytes() { return tc_mask_off<P>() + (tc_bwd<P>() ? TC_MS * 4096 : 0); }
+// the masked layer whose mask travels with slice q (its first), or -1; a layer's mask slot
+template <int P>
+__host__ __device__ constexpr int tc_mask_layer(int q) {
+  for (int l = 0; l < tc_nl<P>(); ++l)
+    if (tc_layer<P>(l).mask && tc_slice0<P>(l) == q) return l;
+  return -1;
 }
-static_assert(tc_nslices<0>() == 68 && tc_nslices<1>() == 89, "chain program slice counts");
-static_assert(tc_lds_bytes<1>() <= 160 * 1024, "LDS");
+template <int P>
+__host__ __device__ constexpr int tc_mslot(int l) {
+  int k = 0;
+  for (int i = 0; i < l; ++i) k += tc_layer<P>(i).mask ? 1 : 0;
+  return k % TC_MS;
+}
+// vector-memory operations every wave issues with slice q: the weight pieces, plus one mask piece
+template <int P>
+__host__ __device__ constexpr int tc_ops(int q) { return tc_pieces<P>() + (tc_mask_layer<P>(q) >= 0 ? 1 : 0); }
+// a mask slot is refilled only after the layer that read it finished its epilogue and passed a barrier:
+// the next mask to the same slot is issued at mid(q0 - NB + 1), which must come at or after the first
+// slice of the layer that follows the reader
+template <int P>
+__host__ __device__ constexpr bool tc_masks_ok() {
+  for (int l = 0; l < tc_nl<P>(); ++l) {
+    if (!tc_layer<P>(l).mask) continue;
+    int seen = 0;
+    for (int l2 = l + 1; l2 < tc_nl<P>(); ++l2) {
+      if (!tc_layer<P>(l2).mask) continue;
+      if (++seen == TC_MS) {
+        const int at = tc_slice0<P>(l2) - tc_nb<P>() + 1;
+        if (at < tc_slice0<P>(l + 1)) return false;
+        break;
+      }
+    }
+    if (tc_slice0<P>(l) > tc_nb<P>() - 2 && tc_slice0<P>(l) - tc_nb<P>() + 1 < 0) return false;
+  }
+  return true;
+}
+static_assert(tc_nslices<0>() == 68 && tc_nslices<1>() == 89 && tc_nslices<2>() == 65 && tc_nslices<3>() == 86,
+              "chain program slice counts");
+static_assert(tc_lds_bytes<0>() <= 160 * 1024 && tc_lds_bytes<1>() <= 160 * 1024 && tc_lds_bytes<2>() <= 160 * 1024 &&
+                  tc_lds_bytes<3>() <= 160 * 1024,
+              "LDS");
+static_assert(tc_masks_ok<2>() && tc_masks_ok<3>(), "mask slot reuse");
 
 // input column of MFMA k slot (8 h + j) of a k-step s that reads the previous layer's registers
 __host__ __device__ constexpr int tc_perm(int s, int h, int j) { return 32 * s + (j < 4 ? 4 * h + j : 16 + 4 * h + (j - 4)); }
@@ -123,6 +212,40 @@ __device__ __forceinline__ unsigned short tc_bf(float f) {  // RNE (the layer-wi
   uint32_t u = __float_as_uint(f);
   u += 0x7fffu + ((u >> 16) & 1u);
   return (unsigned short)(u >> 16);
+}
+
+typedef __bf16 tc_bf16x2 __attribute__((ext_vector_type(2)));
+typedef float tc_f32x2 __attribute__((ext_vector_type(2)));
+typedef short tc_s16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned short tc_u16x2 __attribute__((ext_vector_type(2)));
+// two fp32 -> packed bf16 (v_cvt_pk_bf16_f32, RNE: tc_bf's rounding), x in the low half
+__device__ __forceinline__ uint32_t tc_cvt2(float x, float y) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((tc_f32x2){x, y}, tc_bf16x2));
+}
+// ReLU of two packed bf16 (v_pk_max_i16 with 0: negative values and -0 have the sign bit)
+__device__ __forceinline__ uint32_t tc_pk_relu(uint32_t w) {
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(tc_s16x2, w), (tc_s16x2){0, 0}));
+}
+// (half != 0) per half of a ReLU'd word: bits 0 and 16
+__device__ __forceinline__ uint32_t tc_nz01(uint32_t w) {
+  uint32_t r;
+  asm("v_pk_min_u16 %0, %1, %2" : "=v"(r) : "v"(w), "v"(0x00010001u));  // (an inline 1 feeds the low half only)
+  return r;
+}
+// 16 such words -> 32 mask bits: word k's halves at bits k and 16 + k (shift-or tree, 15 instructions)
+__device__ __forceinline__ uint32_t tc_tree(const uint32_t* t) {
+  uint32_t a[8], b[4];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) a[k] = t[k] | (t[k + 8] << 8);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) b[k] = a[k] | (a[k + 4] << 4);
+  const uint32_t c0 = b[0] | (b[2] << 2), c1 = b[1] | (b[3] << 2);
+  return c0 | (c1 << 1);
+}
+// bits 0 and 16 of f -> a 0xffff / 0 mask per half
+__device__ __forceinline__ uint32_t tc_expand(uint32_t f) {
+  const tc_u16x2 e = __builtin_bit_cast(tc_u16x2, f & 0x00010001u);
+  return __builtin_bit_cast(uint32_t, (tc_u16x2){0, 0} - e);
 }
 
 template <int N>
@@ -147,19 +270,20 @@ __global__ void k_tc_pack(TcPackArgs a) {
   const int m = 16 * o + (lane & 15), h = lane >> 4;
   float v = 0.f;
   const bool mem = L.mem_first ? t < L.kmem : t >= L.kprev;
-  if (mem) {
-    const int s = L.mem_first ? t : t - L.kprev;
-    const int c = 32 * s + 8 * h + j;
-    if (c < L.kmem_cols) {
-      if (m < L.n1) v = L.W[(long)m * L.in_ch + L.cmem + c];
-      else if (m - L.n1 < L.n2) v = L.W2[(long)(m - L.n1) * L.in_ch2 + L.cmem + c];
-    }
-  } else {
-    const int s = L.mem_first ? t - L.kmem : t;
-    const int c = tc_perm(s, h, j);
-    if (c < L.kprev_cols) {
-      if (m < L.n1) v = L.W[(long)m * L.in_ch + L.cprev + c];
-      else if (m - L.n1 < L.n2) v = L.W2[(long)(m - L.n1) * L.in_ch2 + L.cprev + c];
+  const int s = mem ? (L.mem_first ? t : t - L.kprev) : (L.mem_first ? t - L.kmem : t);
+  // input index of this k slot: natural order for memory operands, tc_perm for the previous layer's registers
+  const int c = mem ? 32 * s + 8 * h + j : tc_perm(s, h, j);
+  if (c < (mem ? L.kmem_cols : L.kprev_cols)) {
+    if (!L.trans) {
+      const int col = (mem ? L.cmem : L.cprev) + c;
+      if (m < L.n1) v = L.W[(long)m * L.in_ch + col];
+      else if (m - L.n1 < L.n2) v = L.W2[(long)(m - L.n1) * L.in_ch2 + col];
+    } else {
+      // transposed (input gradient): out neuron m = forward input column (groups A, B), k = forward output c
+      int col = -1;
+      if (m < L.oa) col = L.oc0 + m;
+      else if (m >= L.ob_b0 && m - L.ob_b0 < L.nb) col = L.oc1 + (m - L.ob_b0);
+      if (col >= 0) v = mem ? L.W2[(long)c * L.in_ch2 + col] : L.W[(long)c * L.in_ch + col];
     }
   }
   a.out[e] = tc_bf(v);
@@ -168,15 +292,19 @@ __global__ void k_tc_pack(TcPackArgs a) {
 // ---- the chain kernel ------------------------------------------------------------------------
 struct TcRing {
   unsigned char* lds;  // ring base
+  unsigned char* mlds; // mask slots (backward programs)
   const unsigned char* img;
-  int wave, lane;
-  // issue slice Q into its ring slot (every wave exactly tc_pieces<P>() 1-KiB pieces)
+  const TcArgs* a;
+  int wave, lane, tile;
+  // issue slice Q into its ring slot (every wave exactly tc_pieces<P>() 1-KiB pieces), and with the
+  // first slice of a masked layer one piece of the layer's mask bits for this tile (waves w and w + 4
+  // load the same KiB: every wave issues the same number of operations per slice)
   template <int P, int Q>
   __device__ __forceinline__ void issue() {
-    if constexpr (Q < tc_nslices<P>()) {
+    if constexpr (Q < tc_nslices<P>() && !(tc_bwd<P>() && TC_EXP_BWD == 2)) {
       constexpr int ob = tc_layer<P>(tc_layer_of<P>(Q)).ob;
       constexpr int kb = tc_slice_kb<P>(Q);
-      const unsigned dst = (unsigned)(uintptr_t)(lds + (Q % TC_NB) * tc_obmax<P>() * 1024);
+      const unsigned dst = (unsigned)(uintptr_t)(lds + (Q % tc_nb<P>()) * tc_obmax<P>() * 1024);
       const unsigned char* w = img;
       asm volatile("" : "+s"(w));
 #pragma unroll
@@ -188,6 +316,14 @@ struct TcRing {
         asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(lane * 16), "s"(sbase), "s"(m0)
                      : "memory");
       }
+      constexpr int ml = tc_mask_layer<P>(Q);
+      if constexpr (ml >= 0) {
+        const int piece = wave & 3;
+        const unsigned m0 = (unsigned)(uintptr_t)(mlds + tc_mslot<P>(ml) * 4096 + piece * 1024);
+        const unsigned char* sbase = (const unsigned char*)a->bits[ml] + (size_t)tile * 4096 + piece * 1024;
+        asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(lane * 16), "s"(sbase), "s"(m0)
+                     : "memory");
+      }
     }
   }
   // slices issued after slice Q by the time slice Q is certified at mid(Q - 1) (or the prologue)
@@ -195,15 +331,19 @@ struct TcRing {
   __device__ __forceinline__ void certify() {
     // issued so far: the prologue's slices 0 .. NB-2, then one per mid(): mid(Q - 2) issued Q + NB - 3
     constexpr int last = tc_nslices<P>() - 1;
-    constexpr int issued0 = Q == 0 ? TC_NB - 2 : Q + TC_NB - 3;
+    constexpr int issued0 = Q == 0 ? tc_nb<P>() - 2 : Q + tc_nb<P>() - 3;
     constexpr int issued = issued0 < last ? issued0 : last;
-    constexpr int after = issued - Q;
-    tc_wait_vmcnt<tc_pieces<P>() * (after > 0 ? after : 0)>();
+    constexpr int after = [] {
+      int n = 0;
+      for (int x = Q + 1; x <= issued; ++x) n += tc_ops<P>(x);
+      return n;
+    }();
+    if constexpr (!(tc_bwd<P>() && TC_EXP_BWD == 3)) tc_wait_vmcnt<after>();
     __syncthreads();
   }
   template <int P, int Q>
   __device__ __forceinline__ const unsigned char* slot() const {
-    return lds + (Q % TC_NB) * tc_obmax<P>() * 1024;
+    return lds + (Q % tc_nb<P>()) * tc_obmax<P>() * 1024;
   }
 };
 
@@ -214,60 +354,65 @@ __device__ __forceinline__ void tc_body(const TcArgs& a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int h = lane >> 4, pl = lane & 15;
   float* sb = (float*)smem;
-  unsigned char* ring = smem + (tc_bias_off<P>(tc_nl<P>()) * 4 + 255) / 256 * 256;
-  // bias table (zero past each layer's outputs; the FA layer's out-block 16 row 0 = alpha_fc's bias)
-  tc_for<0, tc_nl<P>()>([&](auto lc) {
-    constexpr int l = decltype(lc)::value;
-    constexpr int n = tc_layer<P>(l).ob * 16;
-    for (int i = tid; i < n; i += 512) {
-      float v = 0.f;
-      if (i < a.nout[l]) v = a.bias[l][i];
-      else if (tc_layer<P>(l).out == TC_FA && i == 256) v = a.bias2[0];
-      sb[tc_bias_off<P>(l) + i] = v;
-    }
-  });
+  unsigned char* ring = smem + tc_ring_off<P>();
+  unsigned char* mring = smem + tc_mask_off<P>();
+  // bias table (forward programs; zero past each layer's outputs; feature||alpha's row 256 = alpha_fc's bias)
+  if constexpr (!tc_bwd<P>()) {
+    tc_for<0, tc_nl<P>()>([&](auto lc) {
+      constexpr int l = decltype(lc)::value;
+      constexpr int n = tc_layer<P>(l).ob * 16;
+      for (int i = tid; i < n; i += 512) {
+        float v = 0.f;
+        if (i < a.nout[l]) v = a.bias[l][i];
+        else if (tc_layer<P>(l).out == TC_FA && i == 256) v = a.bias2[0];
+        sb[tc_bias_off<P>(l) + i] = v;
+      }
+    });
+  }
+  if constexpr (tc_bwd<P>() && TC_EXP_BWD == 2) {
+    for (int i = tid; i < (tc_lds_bytes<P>() - tc_ring_off<P>()) / 4; i += 512) ((uint32_t*)ring)[i] = 0u;
+    __syncthreads();
+  }
   const int M = *a.M_dev;
   const int ntiles = (M + 127) / 128;
   if ((int)blockIdx.x >= ntiles) return;  // uniform per workgroup
-  TcRing rg{ring, a.img, wave, lane};
+  TcRing rg{ring, mring, a.img, &a, wave, lane, 0};
   for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    rg.tile = __builtin_amdgcn_readfirstlane(tile);
     const int row = tile * 128 + wave * 16 + pl;
     const bool valid = row < M;
     const int rr = valid ? row : M - 1;
-    // memory B fragments: gamma (2 k-steps), gamma(dir) (1 k-step, program NF); columns past the
-    // segment read as 0 (the rows' padding is not assumed to be finite)
-    tc_bf16x8 gm[2], gv = {};
-    {
-      tc_for<0, 2>([&](auto sc) {
-        constexpr int s = decltype(sc)::value;
-        const uint4 u = *(const uint4*)(a.mem + (size_t)rr * a.ld_mem + 32 * s + 8 * h);
-        tc_bf16x8 b = __builtin_bit_cast(tc_bf16x8, u);
+    // memory B fragments (bf16 or fp32 rows, rounded RNE to bf16 as the layer-wise path rounds its
+    // operands); columns past the segment read as 0 and are not loaded (rows may be narrower than 32)
+    auto load_mem = [&](const void* base, int ld, int cols, int f32, int s) {
+      tc_bf16x8 b;
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if (32 * s + 8 * h + j >= a.kmem_cols) b[j] = (__bf16)0.0f;
-        gm[s] = b;
-      });
-      if constexpr (P == 1) {
-        const uint4 u = *(const uint4*)(a.mem2 + (size_t)rr * a.ld_mem2 + 8 * h);
-        gv = __builtin_bit_cast(tc_bf16x8, u);
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if (8 * h + j >= a.kmem2_cols) gv[j] = (__bf16)0.0f;
+      for (int j = 0; j < 8; ++j) {
+        const int c = 32 * s + 8 * h + j;
+        unsigned short u = 0;
+        if (c < cols) u = f32 ? tc_bf(((const float*)base)[(size_t)rr * ld + c]) : ((const unsigned short*)base)[(size_t)rr * ld + c];
+        b[j] = __builtin_bit_cast(__bf16, u);
       }
-    }
+      return b;
+    };
+    tc_bf16x8 gm[2], gv = {};
+    tc_for<0, tc_memk<P>()>([&](auto sc) { gm[decltype(sc)::value] = load_mem(a.mem, a.ld_mem, a.kmem_cols, a.mem_f32, decltype(sc)::value); });
+    if constexpr (P == 1 || P == 3) gv = load_mem(a.mem2, a.ld_mem2, a.kmem2_cols, a.mem2_f32, 0);
     // ring prologue: slices 0 .. NB-2, slice 0 certified
-    tc_for<0, TC_NB - 1>([&](auto qc) { rg.template issue<P, decltype(qc)::value>(); });
+    tc_for<0, tc_nb<P>() - 1>([&](auto qc) { rg.template issue<P, decltype(qc)::value>(); });
     rg.template certify<P, 0>();
     tc_bf16x8 bprev[8];
-    f32x4 acc[17];
+    f32x4 acc[20];
     tc_for<0, tc_nl<P>()>([&](auto lc) {
       constexpr int l = decltype(lc)::value;
       constexpr TcL L = tc_layer<P>(l);
       constexpr int KS = L.kmem + L.kprev;
       constexpr int Q0 = tc_slice0<P>(l);
+      constexpr int NMB = L.mask ? (L.out == TC_SPLIT ? 16 : L.ob) : 0;  // masked out-blocks
       tc_for<0, L.ob>([&](auto oc) {
         constexpr int o = decltype(oc)::value;
-        acc[o] = *(const f32x4*)(sb + tc_bias_off<P>(l) + 16 * o + 4 * h);
+        if constexpr (tc_bwd<P>()) acc[o] = f32x4{0.f, 0.f, 0.f, 0.f};
+        else acc[o] = *(const f32x4*)(sb + tc_bias_off<P>(l) + 16 * o + 4 * h);
       });
       tc_for<0, KS>([&](auto tc) {
         constexpr int t = decltype(tc)::value;
@@ -289,48 +434,98 @@ __device__ __forceinline__ void tc_body(const TcArgs& a) {
           constexpr int o = decltype(oc)::value;
           if constexpr (o + PF < L.ob) fa[(o + PF) % (PF + 1)] = *(const tc_bf16x8*)(buf + (o + PF) * 1024 + lane * 16);
           __builtin_amdgcn_sched_barrier(0);
-          acc[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[o % (PF + 1)], b, acc[o], 0, 0, 0);
+          if constexpr (!(tc_bwd<P>() && TC_EXP_BWD == 1))
+            acc[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[o % (PF + 1)], b, acc[o], 0, 0, 0);
           __builtin_amdgcn_sched_barrier(0);
           // halfway through the slice: certify the next slice, refill the slot of the previous one
           if constexpr (o == (L.ob - 1) / 2) {
             if constexpr (Q + 1 < tc_nslices<P>()) {
               rg.template certify<P, Q + 1>();
-              rg.template issue<P, Q + TC_NB - 1>();
+              rg.template issue<P, Q + tc_nb<P>() - 1>();
             }
           }
         });
       });
-      // epilogue: ReLU, RNE to bf16 for the stored rows and the next layer's operand; fp32 heads
-      if constexpr (L.relu) {
-        tc_for<0, L.ob>([&](auto oc) {
-          constexpr int o = decltype(oc)::value;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) acc[o][r] = fmaxf(acc[o][r], 0.0f);
+      // epilogue: RNE to bf16 (v_cvt_pk_bf16_f32) for the stored rows and the next layer's operand, then
+      // ReLU on the packed words (forward; max with 0 as int16 = ReLU, and ReLU commutes with RNE) or the
+      // ReLU-derivative mask (backward); fp32 heads / gamma gradients from the fp32 accumulators
+      if constexpr (L.out == TC_BF16 || L.out == TC_FA || L.out == TC_SPLIT) {
+        // word 4 s + j: neurons 32 s + 16 (j >> 1) + 4 h + 2 (j & 1) + {0, 1} (a B fragment per s)
+        uint32_t wd[32];
+        tc_for<0, 8>([&](auto sc) {
+          constexpr int s = decltype(sc)::value;
+          wd[4 * s + 0] = tc_cvt2(acc[2 * s][0], acc[2 * s][1]);
+          wd[4 * s + 1] = tc_cvt2(acc[2 * s][2], acc[2 * s][3]);
+          wd[4 * s + 2] = tc_cvt2(acc[2 * s + 1][0], acc[2 * s + 1][1]);
+          wd[4 * s + 3] = tc_cvt2(acc[2 * s + 1][2], acc[2 * s + 1][3]);
         });
-      }
-      if constexpr (L.out == TC_BF16 || L.out == TC_FA) {
+        if constexpr (L.relu) {
+#pragma unroll
+          for (int i = 0; i < 32; ++i) wd[i] = tc_pk_relu(wd[i]);
+          // the mask bits of the stored rows for the backward chains (bf16 value > 0, the layer-wise
+          // backward's test of the bf16 row)
+          if constexpr (!tc_bwd<P>()) {
+            if (a.bits[l] && valid) {
+              uint32_t t[32];
+#pragma unroll
+              for (int i = 0; i < 32; ++i) t[i] = tc_nz01(wd[i]);
+              *(uint2*)((unsigned char*)a.bits[l] + ((size_t)row * 4 + h) * 8) = make_uint2(tc_tree(t), tc_tree(t + 16));
+            }
+          }
+        }
+        if constexpr (NMB > 0) {
+          const uint2 F = *(const uint2*)(mring + tc_mslot<P>(l) * 4096 + ((wave * 16 + pl) * 4 + h) * 8);
+#pragma unroll
+          for (int i = 0; i < 32; ++i) wd[i] &= tc_expand((i < 16 ? F.x : F.y) >> (i & 15));
+        }
         unsigned short* orow = (unsigned short*)a.out[l] + (size_t)row * a.ldo[l];
         tc_for<0, 8>([&](auto sc) {
           constexpr int s = decltype(sc)::value;
-          unsigned short u[8];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            u[r] = tc_bf(acc[2 * s][r]);
-            u[4 + r] = tc_bf(acc[2 * s + 1][r]);
-          }
-          const uint2 lo = make_uint2(u[0] | ((uint32_t)u[1] << 16), u[2] | ((uint32_t)u[3] << 16));
-          const uint2 hi = make_uint2(u[4] | ((uint32_t)u[5] << 16), u[6] | ((uint32_t)u[7] << 16));
           if (valid) {
-            *(uint2*)(orow + 32 * s + 4 * h) = lo;
-            *(uint2*)(orow + 32 * s + 16 + 4 * h) = hi;
+            *(uint2*)(orow + 32 * s + 4 * h) = make_uint2(wd[4 * s], wd[4 * s + 1]);
+            *(uint2*)(orow + 32 * s + 16 + 4 * h) = make_uint2(wd[4 * s + 2], wd[4 * s + 3]);
           }
-          bprev[s] = __builtin_bit_cast(tc_bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+          bprev[s] = __builtin_bit_cast(tc_bf16x8, make_uint4(wd[4 * s], wd[4 * s + 1], wd[4 * s + 2], wd[4 * s + 3]));
         });
         if constexpr (L.out == TC_FA) {
           if (valid && h == 0) a.out2[row] = acc[16][0];  // alpha_fc (row 256 of the stacked layer)
         }
-      } else {
-        // fp32 rows: columns [0, nout) at ld
+      } else if constexpr (L.out == TC_F32) {
+        // fp32 rows (heads; view_fc's ReLU rows; d view): ReLU / mask in fp32, mask bits from the fp32
+        // value (the layer-wise path masks d view by View > 0)
+        constexpr int NW = L.ob * 2;  // packed words, as above
+        if constexpr (L.relu) {
+          tc_for<0, L.ob>([&](auto oc) {
+            constexpr int o = decltype(oc)::value;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[o][r] = fmaxf(acc[o][r], 0.0f);
+          });
+          if constexpr (!tc_bwd<P>()) {
+            if (a.bits[l] && valid) {
+              uint32_t t[32] = {};
+              tc_for<0, L.ob>([&](auto oc) {
+                constexpr int o = decltype(oc)::value;
+                constexpr int i0 = 4 * (o >> 1) + 2 * (o & 1);
+                t[i0] = (acc[o][0] > 0.f ? 1u : 0u) | (acc[o][1] > 0.f ? 0x10000u : 0u);
+                t[i0 + 1] = (acc[o][2] > 0.f ? 1u : 0u) | (acc[o][3] > 0.f ? 0x10000u : 0u);
+              });
+              *(uint2*)((unsigned char*)a.bits[l] + ((size_t)row * 4 + h) * 8) =
+                  make_uint2(tc_tree(t), NW > 16 ? tc_tree(t + 16) : 0u);
+            }
+          }
+        }
+        if constexpr (NMB > 0) {
+          const uint2 F = *(const uint2*)(mring + tc_mslot<P>(l) * 4096 + ((wave * 16 + pl) * 4 + h) * 8);
+          tc_for<0, L.ob>([&](auto oc) {
+            constexpr int o = decltype(oc)::value;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int i = 4 * (o >> 1) + 2 * (o & 1) + (r >> 1);
+              const uint32_t f = (i < 16 ? F.x : F.y) >> ((i & 15) + 16 * (r & 1));
+              acc[o][r] = (f & 1u) ? acc[o][r] : 0.0f;
+            }
+          });
+        }
         float* orow = (float*)a.out[l] + (size_t)row * a.ldo[l];
         const int nout = a.nout[l];
         tc_for<0, L.ob>([&](auto oc) {
@@ -346,18 +541,31 @@ __device__ __forceinline__ void tc_body(const TcArgs& a) {
             }
           }
         });
-        // the next layer's operand (view_fc -> rgb_fc: 128 ReLU outputs in 4 k-steps)
+        // the next layer's operand (view_fc -> rgb_fc: 128 ReLU outputs; d view -> view_fc^T)
         if constexpr (l + 1 < tc_nl<P>()) {
           tc_for<0, L.ob / 2>([&](auto sc) {
             constexpr int s = decltype(sc)::value;
-            unsigned short u[8];
+            bprev[s] = __builtin_bit_cast(
+                tc_bf16x8, make_uint4(tc_cvt2(acc[2 * s][0], acc[2 * s][1]), tc_cvt2(acc[2 * s][2], acc[2 * s][3]),
+                                      tc_cvt2(acc[2 * s + 1][0], acc[2 * s + 1][1]), tc_cvt2(acc[2 * s + 1][2], acc[2 * s + 1][3])));
+          });
+        }
+      }
+      if constexpr (L.out == TC_SPLIT || L.out == TC_AUX) {
+        // the gamma gradient (fp32 rows, aux_cols columns at ld_aux): out-blocks past the hidden part
+        constexpr int O0 = L.out == TC_SPLIT ? 16 : 0;
+        if (a.aux && valid) {
+          float* arow = a.aux + (size_t)row * a.ld_aux;
+          tc_for<O0, L.ob>([&](auto oc) {
+            constexpr int o = decltype(oc)::value;
+            const int c = 16 * (o - O0) + 4 * h;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              u[r] = tc_bf(acc[2 * s][r]);
-              u[4 + r] = tc_bf(acc[2 * s + 1][r]);
+              if (c + r < a.aux_cols) {
+                if (L.aux_add || a.aux_acc) arow[c + r] += acc[o][r];
+                else arow[c + r] = acc[o][r];
+              }
             }
-            bprev[s] = __builtin_bit_cast(tc_bf16x8, make_uint4(u[0] | ((uint32_t)u[1] << 16), u[2] | ((uint32_t)u[3] << 16),
-                                                                u[4] | ((uint32_t)u[5] << 16), u[6] | ((uint32_t)u[7] << 16)));
           });
         }
       }
@@ -368,25 +576,38 @@ __device__ __forceinline__ void tc_body(const TcArgs& a) {
 
 __global__ __launch_bounds__(512) void k_tchain_bw(TcArgs a) { tc_body<0>(a); }
 __global__ __launch_bounds__(512) void k_tchain_nf(TcArgs a) { tc_body<1>(a); }
+__global__ __launch_bounds__(512) void k_tchain_bwb(TcArgs a) { tc_body<2>(a); }
+__global__ __launch_bounds__(512) void k_tchain_nfb(TcArgs a) { tc_body<3>(a); }
 
 }  // namespace
 
-size_t tchain_image_bytes(int prog) { return (size_t)(prog == 0 ? tc_image_kb<0>() : tc_image_kb<1>()) * 1024; }
+size_t tchain_image_bytes(int prog) {
+  const int kb = prog == 0 ? tc_image_kb<0>() : prog == 1 ? tc_image_kb<1>() : prog == 2 ? tc_image_kb<2>() : tc_image_kb<3>();
+  return (size_t)kb * 1024;
+}
 
-// pack one program's image: layers' weight sources in TcPackLayer (start / ob / k-steps filled here)
-int tchain_pack(int prog, TcPackArgs a, void* dst, hipStream_t s) {
-  long e = 0;
-  const int nl = prog == 0 ? tc_nl<0>() : tc_nl<1>();
-  for (int l = 0; l < nl; ++l) {
-    const TcL L = prog == 0 ? tc_layer<0>(l) : tc_layer<1>(l);
+template <int P>
+static void tc_fill(TcPackArgs& a, long& e) {
+  for (int l = 0; l < tc_nl<P>(); ++l) {
+    const TcL L = tc_layer<P>(l);
     a.L[l].start = e;
     a.L[l].ob = L.ob;
     a.L[l].kmem = L.kmem;
     a.L[l].kprev = L.kprev;
     a.L[l].mem_first = L.mem_first;
+    a.L[l].trans = tc_bwd<P>() ? 1 : 0;
     e += (long)(L.kmem + L.kprev) * L.ob * 512;
   }
-  a.nl = nl;
+  a.nl = tc_nl<P>();
+}
+
+// pack one program's image: layers' weight sources in TcPackLayer (start / ob / k-steps filled here)
+int tchain_pack(int prog, TcPackArgs a, void* dst, hipStream_t s) {
+  long e = 0;
+  if (prog == 0) tc_fill<0>(a, e);
+  else if (prog == 1) tc_fill<1>(a, e);
+  else if (prog == 2) tc_fill<2>(a, e);
+  else tc_fill<3>(a, e);
   a.total = e;
   a.out = (unsigned short*)dst;
   if ((size_t)e * 2 != tchain_image_bytes(prog)) return -1;
@@ -395,9 +616,10 @@ int tchain_pack(int prog, TcPackArgs a, void* dst, hipStream_t s) {
 }
 
 int tchain_run(int prog, const TcArgs& a, int cap, int cus, hipStream_t s) {
-  static bool attr[2] = {false, false};
-  const void* k = prog == 0 ? (const void*)k_tchain_bw : (const void*)k_tchain_nf;
-  const int lds = prog == 0 ? tc_lds_bytes<0>() : tc_lds_bytes<1>();
+  static bool attr[4] = {false, false, false, false};
+  const void* k = prog == 0 ? (const void*)k_tchain_bw : prog == 1 ? (const void*)k_tchain_nf
+                  : prog == 2 ? (const void*)k_tchain_bwb : (const void*)k_tchain_nfb;
+  const int lds = prog == 0 ? tc_lds_bytes<0>() : prog == 1 ? tc_lds_bytes<1>() : prog == 2 ? tc_lds_bytes<2>() : tc_lds_bytes<3>();
   if (!attr[prog]) {
     if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess) return -1;
     attr[prog] = true;

@@ -152,18 +152,25 @@ struct WGradGroup {
 };
 int launch_wgrad_group(const WGrad* d, int nd, int n_host, int nz, float* slab, size_t slab_floats, hipStream_t s);
 
-// fused forward chains of the bf16 training executor (anr_tchain.hip): program 0 = the blend-weight
-// MLP (9 layers), 1 = the canonical NeRF (8 layers + feature||alpha, latent, view, rgb). Weight image
-// per program (tchain_image_bytes), packed from the layers' fp32 weights every call (tchain_pack).
+// fused chains of the bf16 training executor (anr_tchain.hip): program 0 = the blend-weight MLP forward
+// (9 layers), 1 = the canonical NeRF forward (8 layers + feature||alpha, latent, view, rgb), 2 / 3 their
+// input-gradient chains (transposed weights, ReLU masks from the stored activations). Weight image per
+// program (tchain_image_bytes), packed from the layers' fp32 weights every call (tchain_pack).
 struct TcPackLayer {
-  const float* W;   // rows 0 .. n1-1
+  // forward layers: output rows 0 .. n1-1 of W, n1 .. n1+n2-1 of W2 (feature_fc || alpha_fc); inputs at
+  // columns cmem (memory operand, kmem_cols wide) and cprev (previous layer, kprev_cols wide).
+  // transposed layers (input gradients): the k side is W's output rows (previous-layer k-steps,
+  // kprev_cols) or W2's (memory k-steps, kmem_cols); output neuron m < oa is input column oc0 + m,
+  // m in [ob_b0, ob_b0 + nb) is column oc1 + m - ob_b0
+  const float* W;
   int in_ch, n1;
-  const float* W2;  // rows n1 .. n1+n2-1 (feature_fc || alpha_fc), or NULL
+  const float* W2;
   int in_ch2, n2;
-  int cmem, kmem_cols;    // the memory segment's first column in W and its width
-  int cprev, kprev_cols;  // the previous layer's columns
+  int cmem, kmem_cols;
+  int cprev, kprev_cols;
+  int oc0, oa, oc1, nb, ob_b0;
   long start;             // filled by tchain_pack
-  int ob, kmem, kprev, mem_first;
+  int ob, kmem, kprev, mem_first, trans;
 };
 struct TcPackArgs {
   TcPackLayer L[12];
@@ -183,6 +190,14 @@ struct TcArgs {
   int ld_mem, kmem_cols;
   const unsigned short* mem2;  // program 1: gamma(dir) rows (bf16)
   int ld_mem2, kmem2_cols;
+  int mem_f32, mem2_f32;  // the memory operands are fp32 rows (else bf16)
+  // ReLU mask bits per layer, rows of 32 B (lane h of a sample: 8 B; packed word i = 4 s + j of the epilogue
+  // (neurons 32 s + 16 (j >> 1) + 4 h + 2 (j & 1) + {0, 1}) at bits (i & 15) and 16 + (i & 15) of dword i >> 4),
+  // at least ceil(rows / 128) x 128 rows: forward programs write them for their ReLU layers (when set),
+  // backward programs read the mask of each masked layer's outputs
+  void* bits[12];
+  float* aux;             // backward: the gamma gradient rows (fp32): layer 5 stores (adds when aux_acc), layer 0 adds
+  int ld_aux, aux_cols, aux_acc;
   const int* M_dev;       // kept-sample count (device)
 };
 size_t tchain_image_bytes(int prog);

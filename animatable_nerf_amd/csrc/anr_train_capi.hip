@@ -34,8 +34,11 @@ struct TLayout {
   Layout L;
   size_t pt, Gp, Ip, Gv, Lp, lbs, Gt, It, Lt, Hp, Ht, Hn, Feat, Alpha, Lat, View, Rgbl;
   size_t draw, dRgb, dAlpha, dA16, dBp, dBt, dLp, dLt, dIt, dGt, dGt2, dHn, dHt, dHp, dFeat, dLat, dView;
-  size_t ysum, acc3, d_rgb, d_pbw, d_tbw, wimg, wslab, tcimg, total;
+  size_t ysum, acc3, d_rgb, d_pbw, d_tbw, wimg, wslab, tcimg, bitsP, bitsT, bitsN, total;
 };
+
+// ReLU mask bits of one chain layer (TcArgs::bits): 32 B per sample, rows padded to the 128-sample tile
+size_t bits_stride(long N) { return (size_t)((N + 127) / 128 * 128) * 32; }
 
 TLayout tlayout(int n_rays, int chunk, long np, long nt) {
   TLayout T{};
@@ -62,7 +65,12 @@ TLayout tlayout(int n_rays, int chunk, long np, long nt) {
   T.ysum = take(8 * 256); T.acc3 = take(4); T.d_rgb = take(R * 3); T.d_pbw = take(N * 24); T.d_tbw = take(N * 24);
   T.wimg = take((wimg_bytes() + 3) / 4);
   T.wslab = take(kLaneFloats * kWStreams);
-  T.tcimg = take((tchain_image_bytes(0) + tchain_image_bytes(1) + 3) / 4);  // fused-chain images (anr_tchain.hip)
+  // fused-chain images (anr_tchain.hip): BW / NeRF forward, BW / NeRF input-gradient chains
+  T.tcimg = take((tchain_image_bytes(0) + tchain_image_bytes(1) + tchain_image_bytes(2) + tchain_image_bytes(3) + 3) / 4);
+  // the forward chains' ReLU mask bits for the input-gradient chains: pose / T-pose BW (8 layers), NeRF
+  // (8 layers + view_fc)
+  T.bitsP = take(8 * bits_stride((long)N) / 4); T.bitsT = take(8 * bits_stride((long)N) / 4);
+  T.bitsN = take(9 * bits_stride((long)N) / 4);
   T.total = o;
   return T;
 }
@@ -544,6 +552,8 @@ int bw_forward(Exec& e, const float* const* W, const float* G, float* H, float* 
 // the latent-column gradients of layers 0 and 5. Issued one layer per step() on stream st, so that two
 // chains on two streams can be issued alternately: the host spends ~4 API calls per layer and would
 // otherwise reach the second chain only after the first one's whole issue (profiles/r3l trace).
+int chain_cus();
+
 struct BwBackward {
   Exec& e;
   hipStream_t st;
@@ -559,6 +569,11 @@ struct BwBackward {
   const int64_t* li;
   int add;
   int ldlog = 32;  // row stride of dlog
+  // the input-gradient chain's image (program 2, packed from W), or NULL: one row GEMM per layer. With
+  // the chain, the first step issues every layer's output gradient (and dG) in one launch and the steps
+  // issue the weight gradients only.
+  const unsigned char* cimg = nullptr;
+  unsigned char* bits = nullptr;  // the forward chain's mask bits of H_0..7 (bits_stride apart)
   int l = 8;  // 8: the bw_fc head, then layers 7..0; -1: done
 
   bool done() const { return l < 0; }
@@ -567,10 +582,13 @@ struct BwBackward {
     OnStream on(e, st);
     const long S = N * 256;
     const unsigned hb = e.hb ? ~0u : 0u;  // flag mask: the hidden rows, their gradients and gamma bf16
+    const bool xg = !cimg;
     if (l == 8) {
+      if (cimg) ANR_TRY(chain());
       if (g) ANR_TRY(e.wgrad(g[17], 256, 0, 24, dlog, ldlog, H + 7 * S, 256, 256, g[18], nullptr, -1, hb & BF_X));
-      ANR_TRY(e.xgrad(dbuf(7), 256, 256, dlog, ldlog, 24, W[17], 256, 0, H + 7 * S, 256, false, nullptr, 0, 0, nullptr, 0,
-                      hb & (BF_C | BF_M)));
+      if (xg)
+        ANR_TRY(e.xgrad(dbuf(7), 256, 256, dlog, ldlog, 24, W[17], 256, 0, H + 7 * S, 256, false, nullptr, 0, 0, nullptr, 0,
+                        hb & (BF_C | BF_M)));
       --l;
       return ANR_OK;
     }
@@ -584,31 +602,53 @@ struct BwBackward {
         ANR_TRY(e.latent_rows(ys, g[wi], in_ch, 0, 256, cur, 256, G, 64, 63, g[bi], hb & (BF_A | BF_X),
                               Exec::LatentPost{ys, W[wi], in_ch, 63, 256, W[0], li, add, g[wi], g[0]}));
       }
-      if (dG)
+      if (dG && xg)
         ANR_TRY(e.xgrad(dG, 64, 63, cur, 256, 256, W[wi], in_ch, 0, nullptr, 0, !(dG_fresh && l == 5), nullptr, 0, 0,
                         nullptr, 0, hb & BF_A));
       if (l == 5) {
         if (g) ANR_TRY(e.wgrad(g[wi], in_ch, 191, 256, cur, 256, H + 4 * S, 256, 256, nullptr, nullptr, -1, hb & (BF_A | BF_X)));
-        ANR_TRY(e.xgrad(dbuf(4), 256, 256, cur, 256, 256, W[wi], in_ch, 191, H + 4 * S, 256, false, nullptr, 0, 0, nullptr,
-                        0, hb & (BF_A | BF_C | BF_M)));
+        if (xg)
+          ANR_TRY(e.xgrad(dbuf(4), 256, 256, cur, 256, 256, W[wi], in_ch, 191, H + 4 * S, 256, false, nullptr, 0, 0, nullptr,
+                          0, hb & (BF_A | BF_C | BF_M)));
       }
     } else {
       if (g)
         ANR_TRY(e.wgrad(g[wi], 256, 0, 256, cur, 256, H + (l - 1) * S, 256, 256, g[bi], nullptr, -1, hb & (BF_A | BF_X)));
-      ANR_TRY(e.xgrad(dbuf(l - 1), 256, 256, cur, 256, 256, W[wi], 256, 0, H + (l - 1) * S, 256, false, nullptr, 0, 0,
-                      nullptr, 0, hb & (BF_A | BF_C | BF_M)));
+      if (xg)
+        ANR_TRY(e.xgrad(dbuf(l - 1), 256, 256, cur, 256, 256, W[wi], 256, 0, H + (l - 1) * S, 256, false, nullptr, 0, 0,
+                        nullptr, 0, hb & (BF_A | BF_C | BF_M)));
     }
     --l;
     // ping-pong gradient rows are overwritten two layers on: their queued products run now
     if (!dstride) ANR_TRY(e.flush_w());
     return ANR_OK;
   }
+  // program 2 over the kept samples: d logits (fp32, ldlog) -> dY0 + l dstride (bf16 rows, masked by H)
+  // and dG (fp32, ld 64: layer 5 stores unless accumulating, layer 0 adds)
+  int chain() {
+    if (!dstride || !e.hb || !bits) return fail(ANR_E_ARG, "train: the BW input-gradient chain needs strided bf16 rows");
+    TcArgs a{};
+    a.img = cimg;
+    for (int i = 0; i < 8; ++i) {  // program layer i = bw layer 8 - i, output d H_{7-i} masked by H_{7-i} > 0
+      a.out[i] = dbuf(7 - i);
+      a.ldo[i] = 256;
+      a.nout[i] = 256;
+      a.bits[i] = bits + (7 - i) * bits_stride(N);
+    }
+    a.mem = (const unsigned short*)dlog; a.ld_mem = ldlog; a.kmem_cols = 24; a.mem_f32 = 1;
+    a.aux = dG; a.ld_aux = 64; a.aux_cols = 63; a.aux_acc = dG_fresh ? 0 : 1;
+    a.M_dev = e.n_dev;
+    ANR_TRY(e.guard_pending(dY0, 16 * dstride / N, true));  // the 8 gradient slots (dstride floats each)
+    ANR_TRY(e.guard_pending(dG, 64, false));
+    if (tchain_run(2, a, e.grid_n(), chain_cus(), st) != 0) return check_launch("k_tchain_bwb");
+    return ANR_OK;
+  }
 };
 
 int bw_backward(Exec& e, const float* const* W, float* const* g, const float* G, const float* H, const float* dlog,
                 float* dY0, float* dY1, long dstride, float* dG, bool dG_fresh, long N, float* ysum, const int64_t* li,
-                int add, int ldlog = 32) {
-  BwBackward b{e, e.s, W, g, G, H, dlog, dY0, dY1, dstride, dG, dG_fresh, N, ysum, li, add, ldlog};
+                int add, int ldlog = 32, const unsigned char* cimg = nullptr, unsigned char* bits = nullptr) {
+  BwBackward b{e, e.s, W, g, G, H, dlog, dY0, dY1, dstride, dG, dG_fresh, N, ysum, li, add, ldlog, cimg, bits};
   while (!b.done()) ANR_TRY(b.step());
   return ANR_OK;
 }
@@ -619,6 +659,17 @@ int bw_backward(Exec& e, const float* const* W, float* const* g, const float* G,
 bool fchain_on() {
   const char* v = getenv("ANR_TRAIN_FCHAIN");
   return !(v && v[0] == '0');
+}
+// ANR_TRAIN_BCHAIN (read per call, default 1): the input gradients of each MLP's backward as one launch
+// (programs 2 / 3); the weight gradients stay grouped products (Exec::wgrad). 0 = one row GEMM per layer
+bool bchain_on() {
+  const char* v = getenv("ANR_TRAIN_BCHAIN");
+  return fchain_on() && !(v && v[0] == '0');  // reads the mask bits the forward chains write
+}
+// program k's image in the workspace's chain region
+unsigned char* tc_img(unsigned char* base, int prog) {
+  for (int k = 0; k < prog; ++k) base += tchain_image_bytes(k);
+  return base;
 }
 int chain_cus() {
   static int cus = 0;
@@ -657,13 +708,52 @@ int chain_pack(const anr_params* p, unsigned char* img, hipStream_t s) {
   nf.L[9] = TcPackLayer{p->t[21], 384, 256, nullptr, 0, 0, 0, 0, 0, 256};      // latent_fc (latent folded)
   nf.L[10] = TcPackLayer{p->t[23], 283, 128, nullptr, 0, 0, 256, 27, 0, 256};  // view_fc [latent, gamma(dir)]
   nf.L[11] = TcPackLayer{p->t[25], 128, 3, nullptr, 0, 0, 0, 0, 0, 128};       // rgb_fc
-  if (tchain_pack(1, nf, img + tchain_image_bytes(0), s) != 0) return check_launch("k_tc_pack (nerf)");
+  if (tchain_pack(1, nf, tc_img(img, 1), s) != 0) return check_launch("k_tc_pack (nerf)");
   return ANR_OK;
 }
+// pack the input-gradient images (programs 2, 3): transposed layers, output neuron m = a forward input
+// column (oc0 + m; at the skip layer 5 the gamma columns follow as out-blocks 16..19)
+int chain_pack_bwd(const anr_params* p, unsigned char* img, hipStream_t s) {
+  const float* const* W = p->t + 27;
+  const int bw_in[9] = {191, 256, 256, 256, 256, 447, 256, 256, 256};
+  TcPackArgs bw{};
+  bw.L[0].W = W[17]; bw.L[0].in_ch = 256; bw.L[0].W2 = W[17]; bw.L[0].in_ch2 = 256;  // bw_fc^T: d logits (24)
+  bw.L[0].kmem_cols = 24; bw.L[0].oa = 256;
+  for (int i = 1; i < 9; ++i) {
+    const int l = 8 - i;
+    TcPackLayer& L = bw.L[i];
+    L.W = W[1 + 2 * l]; L.in_ch = bw_in[l]; L.kprev_cols = 256;
+    if (l == 5) { L.oc0 = 191; L.oa = 256; L.oc1 = 0; L.nb = 63; L.ob_b0 = 256; }
+    else L.oa = l == 0 ? 63 : 256;
+  }
+  if (tchain_pack(2, bw, tc_img(img, 2), s) != 0) return check_launch("k_tc_pack (bw backward)");
+  const int nf_in[8] = {63, 256, 256, 256, 256, 319, 256, 256};
+  TcPackArgs nf{};
+  nf.L[0].W = PT(25); nf.L[0].in_ch = 128; nf.L[0].W2 = PT(25); nf.L[0].in_ch2 = 128;  // rgb_fc^T: d rgb (3)
+  nf.L[0].kmem_cols = 3; nf.L[0].oa = 128;
+  nf.L[1].W = PT(23); nf.L[1].in_ch = 283; nf.L[1].kprev_cols = 128; nf.L[1].oa = 256;  // view_fc^T -> d latent
+  nf.L[2].W = PT(21); nf.L[2].in_ch = 384; nf.L[2].kprev_cols = 256; nf.L[2].oa = 256;  // latent_fc^T -> d feature
+  nf.L[3].W = PT(19); nf.L[3].in_ch = 256; nf.L[3].kprev_cols = 256; nf.L[3].oa = 256;  // feature_fc^T
+  nf.L[3].W2 = PT(17); nf.L[3].in_ch2 = 256; nf.L[3].kmem_cols = 1;                     // + alpha_fc^T (d alpha)
+  for (int i = 4; i < 12; ++i) {
+    const int l = 11 - i;
+    TcPackLayer& L = nf.L[i];
+    L.W = PT(1 + 2 * l); L.in_ch = nf_in[l]; L.kprev_cols = 256;
+    if (l == 5) { L.oc0 = 63; L.oa = 256; L.oc1 = 0; L.nb = 63; L.ob_b0 = 256; }
+    else L.oa = l == 0 ? 63 : 256;
+  }
+  if (tchain_pack(3, nf, tc_img(img, 3), s) != 0) return check_launch("k_tc_pack (nerf backward)");
+  return ANR_OK;
+}
+// the pose-space BW backward's chain image, when the chain runs (bf16 rows, ANR_TRAIN_BCHAIN)
+const unsigned char* pose_bchain(const Exec& e, char* ws, const TLayout& T) {
+  return e.hb && bchain_on() ? tc_img((unsigned char*)(ws + T.tcimg), 2) : nullptr;
+}
+unsigned char* pose_bits(char* ws, const TLayout& T) { return (unsigned char*)(ws + T.bitsP); }
 // one BW MLP pass (latent folds f0 / f5) over the kept samples: gamma rows G (bf16, ld 64) -> H (bf16
 // rows, layer l at H + l S floats) and the logits (fp32, ld 32)
 int chain_bw(const Exec& e, const anr_params* p, const unsigned char* img, const float* G, float* H, float* logits,
-             long N, const float* f0, const float* f5, hipStream_t s) {
+             long N, const float* f0, const float* f5, hipStream_t s, unsigned char* bits) {
   const float* const* W = p->t + 27;
   TcArgs a{};
   a.img = img;
@@ -673,6 +763,7 @@ int chain_bw(const Exec& e, const anr_params* p, const unsigned char* img, const
     a.nout[l] = l == 8 ? 24 : 256;
     a.out[l] = l == 8 ? (void*)logits : (void*)(H + l * S);
     a.ldo[l] = l == 8 ? 32 : 256;
+    if (l < 8) a.bits[l] = bits + l * bits_stride(N);
   }
   a.mem = (const unsigned short*)G; a.ld_mem = 64; a.kmem_cols = 63;
   a.M_dev = e.n_dev;
@@ -706,7 +797,7 @@ int train_forward(const anr_params* p, const anr_frame* f, const float* ray_o, c
   if (fchain) ANR_TRY(chain_pack(p, tcimg, s));
   // pose-space BW MLP (latent_index + 1), softmax + LBS, T-pose BW MLP (latent 0)
   if (fchain && !e.pose_fp32) {
-    ANR_TRY(chain_bw(e, p, tcimg, b.Gp, (float*)(ws + T.Hp), b.Lp, N, FOLD(0), FOLD(2), s));
+    ANR_TRY(chain_bw(e, p, tcimg, b.Gp, (float*)(ws + T.Hp), b.Lp, N, FOLD(0), FOLD(2), s, (unsigned char*)(ws + T.bitsP)));
   } else {
     PoseScope ps(e);
     ANR_TRY(bw_forward(e, p->t + 27, b.Gp, (float*)(ws + T.Hp), b.Lp, N, FOLD(0), FOLD(2)));
@@ -720,7 +811,8 @@ int train_forward(const anr_params* p, const anr_frame* f, const float* ray_o, c
   ANR_TRY(order(e.ss, s2, s));
   {
     OnStream on(e, s2);
-    if (fchain) ANR_TRY(chain_bw(e, p, tcimg, b.Gt, (float*)(ws + T.Ht), b.Lt, N, FOLD(1), FOLD(3), s2));
+    if (fchain)
+      ANR_TRY(chain_bw(e, p, tcimg, b.Gt, (float*)(ws + T.Ht), b.Lt, N, FOLD(1), FOLD(3), s2, (unsigned char*)(ws + T.bitsT)));
     else ANR_TRY(bw_forward(e, p->t + 27, b.Gt, (float*)(ws + T.Ht), b.Lt, N, FOLD(1), FOLD(3)));
     if (n > 0) {
       hipLaunchKernelGGL(k_tr_softmax_t, dim3(g1), dim3(256), 0, s2, b);
@@ -735,13 +827,15 @@ int train_forward(const anr_params* p, const anr_frame* f, const float* ray_o, c
   float* View = (float*)(ws + T.View);
   if (fchain) {
     TcArgs a{};
-    a.img = tcimg + tchain_image_bytes(0);
+    a.img = tc_img(tcimg, 1);
     for (int l = 0; l < 8; ++l) {
       a.bias[l] = PT(2 + 2 * l);
       a.nout[l] = 256;
       a.out[l] = Hn + l * S;
       a.ldo[l] = 256;
+      a.bits[l] = (unsigned char*)(ws + T.bitsN) + l * bits_stride(N);
     }
+    a.bits[10] = (unsigned char*)(ws + T.bitsN) + 8 * bits_stride(N);  // view_fc (View > 0)
     a.bias[8] = PT(20); a.bias2 = PT(18); a.nout[8] = 256; a.out[8] = Feat; a.ldo[8] = 256; a.out2 = b.Alpha;
     a.bias[9] = FOLD(4); a.nout[9] = 256; a.out[9] = Lat; a.ldo[9] = 256;
     a.bias[10] = PT(24); a.nout[10] = 128; a.out[10] = View; a.ldo[10] = 128;
@@ -805,6 +899,9 @@ int train_backward(const anr_params* p, float* const* g, const anr_frame* f, con
   float* ysum = (float*)(ws + T.ysum);
   // the T-pose BW chain writes its gamma(x_T) gradient into dGt2 (s2), the NeRF's into dGt (s)
   b.dGt2 = (float*)(ws + T.dGt2);
+  const bool bchain = e.hb && bchain_on();
+  unsigned char* tcimg = (unsigned char*)(ws + T.tcimg);
+  if (bchain) ANR_TRY(chain_pack_bwd(p, tcimg, s));
   const hipStream_t s2 = e.s2();
   ANR_TRY(order(e.ss, s2, s));
   // upstream pbw / tbw row gradients, T-pose softmax backward (s2)
@@ -826,33 +923,57 @@ int train_backward(const anr_params* p, float* const* g, const anr_frame* f, con
   ANR_TRY(check_launch("k_tr_raw_bwd"));
   // the T-pose BW backward (latent row 0) on s2, issued a layer at a time between the NeRF's layers
   BwBackward tb{e, s2, p->t + 27, g + 27, b.Gt, Ht, b.dLt, (float*)(ws + T.dHt), nullptr, S, b.dGt2, true, N, ysum,
-                nullptr, 0, 64};
+                nullptr, 0, 64, bchain ? tc_img(tcimg, 2) : nullptr, (unsigned char*)(ws + T.bitsT)};
   auto tick = [&]() { return tb.done() ? ANR_OK : tb.step(); };
   ANR_TRY(tick());
+  // d alpha: fp32 (ld 1), or under e.hb bf16 rows of 64 (k_tr_raw_bwd) so both products stay on the fast paths
+  const float* dAl = e.hb ? (const float*)b.dAlpha16 : b.dAlpha;
+  const int ldAl = e.hb ? 64 : 1;
+  if (bchain) {
+    // program 3: every input gradient of the canonical NeRF in one launch (d view fp32, d latent,
+    // d feature, d H_7..0 bf16, d gamma(x_T) fp32); the weight gradients below read its rows
+    TcArgs a{};
+    a.img = tc_img(tcimg, 3);
+    unsigned char* bn = (unsigned char*)(ws + T.bitsN);
+    a.out[0] = dView; a.ldo[0] = 128; a.nout[0] = 128; a.bits[0] = bn + 8 * bits_stride(N);
+    a.out[1] = dLat; a.ldo[1] = 256; a.nout[1] = 256;
+    a.out[2] = dFeat; a.ldo[2] = 256; a.nout[2] = 256;
+    for (int i = 3; i < 11; ++i) {  // feature_fc || alpha_fc, then pts_linears 7..1: d H_{10-i}
+      a.out[i] = dHn + (10 - i) * S; a.ldo[i] = 256; a.nout[i] = 256;
+      a.bits[i] = bn + (10 - i) * bits_stride(N);
+    }
+    a.mem = (const unsigned short*)b.dRgb; a.ld_mem = 4; a.kmem_cols = 3; a.mem_f32 = 1;
+    a.mem2 = (const unsigned short*)dAl; a.ld_mem2 = 64; a.kmem2_cols = 1;
+    a.aux = b.dGt; a.ld_aux = 64; a.aux_cols = 63;
+    a.M_dev = e.n_dev;
+    ANR_TRY(e.guard_pending(dHn, 16 * S / N, true));
+    ANR_TRY(e.guard_pending(b.dGt, 64, false));
+    if (tchain_run(3, a, e.grid_n(), chain_cus(), s) != 0) return check_launch("k_tchain_nfb");
+  }
   // rgb_fc, view_fc (ReLU), latent_fc (latent folded), feature_fc || alpha_fc
   ANR_TRY(e.wgrad(g[25], 128, 0, 3, b.dRgb, 4, View, 128, 128, g[26]));
-  ANR_TRY(e.xgrad(dView, 128, 128, b.dRgb, 4, 3, PT(25), 128, 0, View, 128, false));
+  if (!bchain) ANR_TRY(e.xgrad(dView, 128, 128, b.dRgb, 4, 3, PT(25), 128, 0, View, 128, false));
   ANR_TRY(tick());
   const unsigned hb = e.hb ? ~0u : 0u;  // flag mask: gamma, H, Feat, Lat and their gradients bf16
   ANR_TRY(e.wgrad(g[23], 283, 0, 128, dView, 128, Lat, 256, 256, g[24], nullptr, -1, hb & BF_X));
   ANR_TRY(e.wgrad(g[23], 283, 256, 128, dView, 128, b.Gv, e.hb ? 64 : 32, 27, nullptr, nullptr, -1, hb & BF_X));
-  ANR_TRY(e.xgrad(dLat, 256, 256, dView, 128, 128, PT(23), 283, 0, nullptr, 0, false, nullptr, 0, 0, nullptr, 0,
-                  hb & BF_C));
+  if (!bchain)
+    ANR_TRY(e.xgrad(dLat, 256, 256, dView, 128, 128, PT(23), 283, 0, nullptr, 0, false, nullptr, 0, 0, nullptr, 0,
+                    hb & BF_C));
   {
     float* ys = ysum + 512;
     ANR_TRY(e.latent_rows(ys, g[21], 384, 0, 256, dLat, 256, Feat, 256, 256, g[22], hb & (BF_A | BF_X),
                           Exec::LatentPost{ys, PT(21), 384, 256, 256, PT(0), f->latent_index, 0, g[21], g[0]}));
   }
-  ANR_TRY(e.xgrad(dFeat, 256, 256, dLat, 256, 256, PT(21), 384, 0, nullptr, 0, false, nullptr, 0, 0, nullptr, 0,
-                  hb & (BF_A | BF_C)));
+  if (!bchain)
+    ANR_TRY(e.xgrad(dFeat, 256, 256, dLat, 256, 256, PT(21), 384, 0, nullptr, 0, false, nullptr, 0, 0, nullptr, 0,
+                    hb & (BF_A | BF_C)));
   ANR_TRY(tick());
   ANR_TRY(e.wgrad(g[19], 256, 0, 256, dFeat, 256, Hn + 7 * S, 256, 256, g[20], nullptr, -1, hb & (BF_A | BF_X)));
-  // d alpha: fp32 (ld 1), or under e.hb bf16 rows of 64 (k_tr_raw_bwd) so both products stay on the fast paths
-  const float* dAl = e.hb ? (const float*)b.dAlpha16 : b.dAlpha;
-  const int ldAl = e.hb ? 64 : 1;
   ANR_TRY(e.wgrad(g[17], 256, 0, 1, dAl, ldAl, Hn + 7 * S, 256, 256, g[18], nullptr, -1, hb & (BF_A | BF_X)));
-  ANR_TRY(e.xgrad(dHn + 7 * S, 256, 256, dFeat, 256, 256, PT(19), 256, 0, Hn + 7 * S, 256, false, dAl, ldAl, 1,
-                  PT(17), 256, hb & (BF_A | BF_C | BF_M)));
+  if (!bchain)
+    ANR_TRY(e.xgrad(dHn + 7 * S, 256, 256, dFeat, 256, 256, PT(19), 256, 0, Hn + 7 * S, 256, false, dAl, ldAl, 1,
+                    PT(17), 256, hb & (BF_A | BF_C | BF_M)));
   // NeRF pts_linears 7..0 (skip at 5: [gamma(x_T), net]); layer l's output gradient at dHn + l S
   for (int l = 7; l >= 0; --l) {
     const int wi = 1 + 2 * l, bi = wi + 1;
@@ -860,18 +981,22 @@ int train_backward(const anr_params* p, float* const* g, const anr_frame* f, con
     const unsigned ax = hb & (BF_A | BF_X), acm = hb & (BF_A | BF_C | BF_M);
     if (l == 0) {
       ANR_TRY(e.wgrad(g[wi], 63, 0, 256, cur, 256, b.Gt, 64, 63, g[bi], nullptr, -1, ax));
-      ANR_TRY(e.xgrad(b.dGt, 64, 63, cur, 256, 256, PT(wi), 63, 0, nullptr, 0, true, nullptr, 0, 0, nullptr, 0, hb & BF_A));
+      if (!bchain)
+        ANR_TRY(e.xgrad(b.dGt, 64, 63, cur, 256, 256, PT(wi), 63, 0, nullptr, 0, true, nullptr, 0, 0, nullptr, 0, hb & BF_A));
     } else if (l == 5) {
       ANR_TRY(e.wgrad(g[wi], 319, 0, 256, cur, 256, b.Gt, 64, 63, g[bi], nullptr, -1, ax));
       ANR_TRY(e.wgrad(g[wi], 319, 63, 256, cur, 256, Hn + 4 * S, 256, 256, nullptr, nullptr, -1, ax));
-      ANR_TRY(e.xgrad(b.dGt, 64, 63, cur, 256, 256, PT(wi), 319, 0, nullptr, 0, false, nullptr, 0, 0, nullptr, 0,
-                      hb & BF_A));  // first contribution
-      ANR_TRY(e.xgrad(dHn + 4 * S, 256, 256, cur, 256, 256, PT(wi), 319, 63, Hn + 4 * S, 256, false, nullptr, 0, 0, nullptr,
-                      0, acm));
+      if (!bchain) {
+        ANR_TRY(e.xgrad(b.dGt, 64, 63, cur, 256, 256, PT(wi), 319, 0, nullptr, 0, false, nullptr, 0, 0, nullptr, 0,
+                        hb & BF_A));  // first contribution
+        ANR_TRY(e.xgrad(dHn + 4 * S, 256, 256, cur, 256, 256, PT(wi), 319, 63, Hn + 4 * S, 256, false, nullptr, 0, 0,
+                        nullptr, 0, acm));
+      }
     } else {
       ANR_TRY(e.wgrad(g[wi], 256, 0, 256, cur, 256, Hn + (l - 1) * S, 256, 256, g[bi], nullptr, -1, ax));
-      ANR_TRY(e.xgrad(dHn + (l - 1) * S, 256, 256, cur, 256, 256, PT(wi), 256, 0, Hn + (l - 1) * S, 256, false, nullptr, 0,
-                      0, nullptr, 0, acm));
+      if (!bchain)
+        ANR_TRY(e.xgrad(dHn + (l - 1) * S, 256, 256, cur, 256, 256, PT(wi), 256, 0, Hn + (l - 1) * S, 256, false, nullptr,
+                        0, 0, nullptr, 0, acm));
     }
     ANR_TRY(tick());
   }
@@ -1078,7 +1203,8 @@ int anr_train_bwd(const anr_params* p, float* const* grads, const anr_frame* f, 
   float* ysum = (float*)(ws + T.ysum);
   PoseScope ps(e);
   ANR_TRY(bw_backward(e, p->t + 27, grads + 27, (const float*)(ws + T.Gp), (const float*)(ws + T.Hp), (const float*)(ws + T.dLp),
-                      (float*)(ws + T.dHp), nullptr, N * 256, nullptr, false, N, ysum + 1024, f->latent_index, 1, 64));
+                      (float*)(ws + T.dHp), nullptr, N * 256, nullptr, false, N, ysum + 1024, f->latent_index, 1, 64,
+                      pose_bchain(e, ws, T), pose_bits(ws, T)));
   return e.join_w();
 }
 
@@ -1128,7 +1254,8 @@ int train_step_body(const anr_params* p, float* const* grads, const anr_frame* f
   float* ysum = (float*)(ws + T.ysum);
   PoseScope ps(e);
   ANR_TRY(bw_backward(e, p->t + 27, grads + 27, (const float*)(ws + T.Gp), (const float*)(ws + T.Hp), (const float*)(ws + T.dLp),
-                      (float*)(ws + T.dHp), nullptr, N * 256, nullptr, false, N, ysum + 1024, f->latent_index, 1, 64));
+                      (float*)(ws + T.dHp), nullptr, N * 256, nullptr, false, N, ysum + 1024, f->latent_index, 1, 64,
+                      pose_bchain(e, ws, T), pose_bits(ws, T)));
   return e.join_w();
 }
 
@@ -1387,7 +1514,7 @@ int anr_network_train_bwd(const anr_params* p, float* const* grads, const anr_fr
   PoseScope ps(e);
   ANR_TRY(bw_backward(e, p->t + 27, grads + 27, (const float*)(ws + T.Gp), (const float*)(ws + T.Hp),
                       (const float*)(ws + T.dLp), (float*)(ws + T.dHp), nullptr, N * 256, nullptr, false, N, ysum + 1024,
-                      f->latent_index, 1, 64));
+                      f->latent_index, 1, 64, pose_bchain(e, ws, T), pose_bits(ws, T)));
   return e.join_w();
 }
 

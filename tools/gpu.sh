@@ -144,7 +144,9 @@ for step in "$@"; do
       echo "COUNTERS_OK $k" ;;
     env)
       export "$rest"
-      SFX="${SFX}_${rest//=/-}"
+      v=${rest//=/-}
+      v=${v##*/}  # a path value: its file name
+      SFX="${SFX}_${v}"
       echo "ENV $rest" ;;
     *)
       echo "unknown step $step"; exit 2 ;;
