@@ -148,6 +148,11 @@ constexpr int TC_MS = 4;
 #ifndef TC_EXP_BWD
 #define TC_EXP_BWD 0
 #endif
+// probe-only timing experiments on every program: 4 no row stores, 5 the rows of every tile stored over
+// the first tile's (L2-resident)
+#ifndef TC_EXP
+#define TC_EXP 0
+#endif
 // bias table: per layer ob x 16 floats (forward programs)
 template <int P>
 __host__ __device__ constexpr int tc_bias_off(int l) {
@@ -465,11 +470,11 @@ __device__ __forceinline__ void tc_body(const TcArgs& a) {
           // the mask bits of the stored rows for the backward chains (bf16 value > 0, the layer-wise
           // backward's test of the bf16 row)
           if constexpr (!tc_bwd<P>()) {
-            if (a.bits[l] && valid) {
+            if (a.bits[l] && valid && (TC_EXP != 4 || a.nout[0] == -7)) {
               uint32_t t[32];
 #pragma unroll
               for (int i = 0; i < 32; ++i) t[i] = tc_nz01(wd[i]);
-              *(uint2*)((unsigned char*)a.bits[l] + ((size_t)row * 4 + h) * 8) = make_uint2(tc_tree(t), tc_tree(t + 16));
+              *(uint2*)((unsigned char*)a.bits[l] + ((size_t)(TC_EXP == 5 ? (row & 127) : row) * 4 + h) * 8) = make_uint2(tc_tree(t), tc_tree(t + 16));
             }
           }
         }
@@ -478,17 +483,17 @@ __device__ __forceinline__ void tc_body(const TcArgs& a) {
 #pragma unroll
           for (int i = 0; i < 32; ++i) wd[i] &= tc_expand((i < 16 ? F.x : F.y) >> (i & 15));
         }
-        unsigned short* orow = (unsigned short*)a.out[l] + (size_t)row * a.ldo[l];
+        unsigned short* orow = (unsigned short*)a.out[l] + (size_t)(TC_EXP == 5 ? (row & 127) : row) * a.ldo[l];
         tc_for<0, 8>([&](auto sc) {
           constexpr int s = decltype(sc)::value;
-          if (valid) {
+          if (valid && (TC_EXP != 4 || a.nout[0] == -7)) {
             *(uint2*)(orow + 32 * s + 4 * h) = make_uint2(wd[4 * s], wd[4 * s + 1]);
             *(uint2*)(orow + 32 * s + 16 + 4 * h) = make_uint2(wd[4 * s + 2], wd[4 * s + 3]);
           }
           bprev[s] = __builtin_bit_cast(tc_bf16x8, make_uint4(wd[4 * s], wd[4 * s + 1], wd[4 * s + 2], wd[4 * s + 3]));
         });
         if constexpr (L.out == TC_FA) {
-          if (valid && h == 0) a.out2[row] = acc[16][0];  // alpha_fc (row 256 of the stacked layer)
+          if (valid && (TC_EXP != 4 || a.nout[0] == -7) && h == 0) a.out2[row] = acc[16][0];  // alpha_fc (row 256 of the stacked layer)
         }
       } else if constexpr (L.out == TC_F32) {
         // fp32 rows (heads; view_fc's ReLU rows; d view): ReLU / mask in fp32, mask bits from the fp32
@@ -501,7 +506,7 @@ __device__ __forceinline__ void tc_body(const TcArgs& a) {
             for (int r = 0; r < 4; ++r) acc[o][r] = fmaxf(acc[o][r], 0.0f);
           });
           if constexpr (!tc_bwd<P>()) {
-            if (a.bits[l] && valid) {
+            if (a.bits[l] && valid && (TC_EXP != 4 || a.nout[0] == -7)) {
               uint32_t t[32] = {};
               tc_for<0, L.ob>([&](auto oc) {
                 constexpr int o = decltype(oc)::value;
@@ -509,7 +514,7 @@ __device__ __forceinline__ void tc_body(const TcArgs& a) {
                 t[i0] = (acc[o][0] > 0.f ? 1u : 0u) | (acc[o][1] > 0.f ? 0x10000u : 0u);
                 t[i0 + 1] = (acc[o][2] > 0.f ? 1u : 0u) | (acc[o][3] > 0.f ? 0x10000u : 0u);
               });
-              *(uint2*)((unsigned char*)a.bits[l] + ((size_t)row * 4 + h) * 8) =
+              *(uint2*)((unsigned char*)a.bits[l] + ((size_t)(TC_EXP == 5 ? (row & 127) : row) * 4 + h) * 8) =
                   make_uint2(tc_tree(t), NW > 16 ? tc_tree(t + 16) : 0u);
             }
           }
@@ -526,12 +531,12 @@ __device__ __forceinline__ void tc_body(const TcArgs& a) {
             }
           });
         }
-        float* orow = (float*)a.out[l] + (size_t)row * a.ldo[l];
+        float* orow = (float*)a.out[l] + (size_t)(TC_EXP == 5 ? (row & 127) : row) * a.ldo[l];
         const int nout = a.nout[l];
         tc_for<0, L.ob>([&](auto oc) {
           constexpr int o = decltype(oc)::value;
           const int c = 16 * o + 4 * h;
-          if (valid) {
+          if (valid && (TC_EXP != 4 || a.nout[0] == -7)) {
             if (c + 4 <= nout) {
               *(f32x4*)(orow + c) = acc[o];
             } else {
@@ -554,7 +559,7 @@ __device__ __forceinline__ void tc_body(const TcArgs& a) {
       if constexpr (L.out == TC_SPLIT || L.out == TC_AUX) {
         // the gamma gradient (fp32 rows, aux_cols columns at ld_aux): out-blocks past the hidden part
         constexpr int O0 = L.out == TC_SPLIT ? 16 : 0;
-        if (a.aux && valid) {
+        if (a.aux && valid && (TC_EXP != 4 || a.nout[0] == -7)) {
           float* arow = a.aux + (size_t)row * a.ld_aux;
           tc_for<O0, L.ob>([&](auto oc) {
             constexpr int o = decltype(oc)::value;

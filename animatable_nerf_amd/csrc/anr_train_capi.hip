@@ -237,11 +237,14 @@ struct Exec {
   }
   float* slab(int lane) const { return wslab ? wslab + (size_t)lane * lane_floats : nullptr; }
   // issue the queued weight gradients (grouped) and the latent-row updates that follow them
+  bool ys_zero = false;  // the latent column-sum scratch was zeroed for this call (one memset, train_backward)
+  bool bimg = false;     // the input-gradient chain images are packed for this call (train_forward, on s2)
   int flush_w() {
     if (!npend && !npost) return ANR_OK;
-    hipStream_t w = ss ? ss->sw[0] : s;
+    const int fl = 0;
+    hipStream_t w = ss ? ss->sw[fl] : s;
     for (int i = 0; i < npsrc; ++i) ANR_TRY(order(ss, w, pend_src[i]));
-    if (npend && launch_wgrad_group(pend, npend, grid_n(), group_nz, slab(0), lane_floats, w) != 0)
+    if (npend && launch_wgrad_group(pend, npend, grid_n(), group_nz, slab(fl), lane_floats, w) != 0)
       return check_launch("k_wgrad_group");
     for (int i = 0; i < npost; ++i) {
       const LatentPost& q = post[i];
@@ -276,7 +279,7 @@ struct Exec {
     hipStream_t w = s;
     int lane = 0;
     if (!group) ANR_TRY(wstream(&w, &lane, 0));
-    if (hipMemsetAsync(ys, 0, 256 * 4, w) != hipSuccess) return fail(ANR_E_HIP, "memset");
+    if (!ys_zero && hipMemsetAsync(ys, 0, 256 * 4, w) != hipSuccess) return fail(ANR_E_HIP, "memset");
     if (group && (npend == WG_GROUP_MAX || npost == 8)) ANR_TRY(flush_w());  // product and update in one flush
     const int q0 = nqueued;
     ANR_TRY(wgrad(dW, in_ch, c0, Nout, dY, ldY, X, ldX, K, bsum, ys, 0, bf));
@@ -475,7 +478,7 @@ struct OnStream {
 // bf16 weight images for the row GEMM (bf16 policies only; refreshed on every call, the weights may
 // have changed since the last)
 int pack_images(Exec& e, const anr_params* p, char* dst, hipStream_t s, float* wslab, size_t lane_floats,
-                bool novel = false) {
+                bool novel = false, bool rows = true) {
   if (!e.bf16) return ANR_OK;
   e.wslab = wslab;
   e.lane_floats = lane_floats;
@@ -487,6 +490,7 @@ int pack_images(Exec& e, const anr_params* p, char* dst, hipStream_t s, float* w
   if (fe) e.flush_every = atoi(fe);
   for (int i = 0; i < ANR_NUM_TENSORS; ++i) e.pt[i] = p->t[i];
   for (int i = 0; i < ANR_NUM_NOVEL_TENSORS; ++i) e.pt[ANR_NUM_TENSORS + i] = novel ? p->novel[i] : nullptr;
+  if (!rows) return ANR_OK;  // every product of the call runs in a fused chain or a weight gradient
   if (wimg_pack(e.pt, dst, s) != 0) return check_launch("k_wimg_pack");
   e.wimg = dst;
   return ANR_OK;
@@ -576,15 +580,27 @@ struct BwBackward {
   unsigned char* bits = nullptr;  // the forward chain's mask bits of H_0..7 (bits_stride apart)
   int l = 8;  // 8: the bw_fc head, then layers 7..0; -1: done
 
+  bool chained = false;
   bool done() const { return l < 0; }
   float* dbuf(int k) const { return dstride ? dY0 + k * dstride : ((k & 1) ? dY0 : dY1); }
+  // the chain's launch ahead of the steps (which then queue weight gradients only)
+  int start() {
+    if (!cimg || chained) return ANR_OK;
+    OnStream on(e, st);
+    ANR_TRY(chain());
+    chained = true;
+    return ANR_OK;
+  }
   int step() {
     OnStream on(e, st);
     const long S = N * 256;
     const unsigned hb = e.hb ? ~0u : 0u;  // flag mask: the hidden rows, their gradients and gamma bf16
     const bool xg = !cimg;
     if (l == 8) {
-      if (cimg) ANR_TRY(chain());
+      if (cimg && !chained) {
+        ANR_TRY(chain());
+        chained = true;
+      }
       if (g) ANR_TRY(e.wgrad(g[17], 256, 0, 24, dlog, ldlog, H + 7 * S, 256, 256, g[18], nullptr, -1, hb & BF_X));
       if (xg)
         ANR_TRY(e.xgrad(dbuf(7), 256, 256, dlog, ldlog, 24, W[17], 256, 0, H + 7 * S, 256, false, nullptr, 0, 0, nullptr, 0,
@@ -665,6 +681,11 @@ bool fchain_on() {
 bool bchain_on() {
   const char* v = getenv("ANR_TRAIN_BCHAIN");
   return fchain_on() && !(v && v[0] == '0');  // reads the mask bits the forward chains write
+}
+// every product of a call (forward / backward) runs in a fused chain or a weight gradient: the
+// row-GEMM images (k_wimg_pack, 33 us a step) are not needed
+bool chains_cover(const Exec& e, bool fwd, bool bwd) {
+  return e.hb && !e.pose_fp32 && (!fwd || fchain_on()) && (!bwd || bchain_on());
 }
 // program k's image in the workspace's chain region
 unsigned char* tc_img(unsigned char* base, int prog) {
@@ -777,6 +798,19 @@ int train_forward(const anr_params* p, const anr_frame* f, const float* ray_o, c
                   const TLayout& T, hipStream_t s, Exec& e, const anr_samples* x = nullptr,
                   const RaySplit* split = nullptr) {
   float4* raw = (float4*)(ws + T.L.raw);
+  const bool fchain = e.hb && fchain_on() && R > 0;
+  unsigned char* tcimg = (unsigned char*)(ws + T.tcimg);
+  if (fchain) {
+    // the chain images (and the input-gradient ones, for the backward of this step) are packed on s2,
+    // beside the front-end: s2 starts after everything issued to s so far (the previous call's chains
+    // read the images); s waits for it before its first chain
+    ANR_TRY(order(e.ss, e.s2(), s));
+    ANR_TRY(chain_pack(p, tcimg, e.s2()));
+    if (bchain_on()) {
+      ANR_TRY(chain_pack_bwd(p, tcimg, e.s2()));
+      e.bimg = true;
+    }
+  }
   ANR_TRY(stage_frontend(p, f, ray_o, ray_d, near_, far_, R, o, ws, T.L, raw, s, x, split));
   const long N = (long)R * 64;
   e.n_dev = (const int*)(ws + T.L.counts);
@@ -792,9 +826,7 @@ int train_forward(const anr_params* p, const anr_frame* f, const float* ray_o, c
   }
   // fused forward chains under the bf16 storage policies (every hidden row bf16): the T-pose BW MLP and
   // the NeRF, and the pose-space BW MLP when it is bf16 too (bf16_all)
-  const bool fchain = e.hb && fchain_on() && n > 0;
-  unsigned char* tcimg = (unsigned char*)(ws + T.tcimg);
-  if (fchain) ANR_TRY(chain_pack(p, tcimg, s));
+  if (fchain) ANR_TRY(order(e.ss, s, e.s2()));  // the images packed on s2
   // pose-space BW MLP (latent_index + 1), softmax + LBS, T-pose BW MLP (latent 0)
   if (fchain && !e.pose_fp32) {
     ANR_TRY(chain_bw(e, p, tcimg, b.Gp, (float*)(ws + T.Hp), b.Lp, N, FOLD(0), FOLD(2), s, (unsigned char*)(ws + T.bitsP)));
@@ -901,7 +933,12 @@ int train_backward(const anr_params* p, float* const* g, const anr_frame* f, con
   b.dGt2 = (float*)(ws + T.dGt2);
   const bool bchain = e.hb && bchain_on();
   unsigned char* tcimg = (unsigned char*)(ws + T.tcimg);
-  if (bchain) ANR_TRY(chain_pack_bwd(p, tcimg, s));
+  if (bchain && !e.bimg) ANR_TRY(chain_pack_bwd(p, tcimg, s));
+  if (e.group) {
+    // the latent column-sum scratch of every latent_rows() of this call, zeroed once
+    if (hipMemsetAsync(ysum, 0, 8 * 256 * 4, s) != hipSuccess) return fail(ANR_E_HIP, "memset");
+    e.ys_zero = true;
+  }
   const hipStream_t s2 = e.s2();
   ANR_TRY(order(e.ss, s2, s));
   // upstream pbw / tbw row gradients, T-pose softmax backward (s2)
@@ -924,6 +961,9 @@ int train_backward(const anr_params* p, float* const* g, const anr_frame* f, con
   // the T-pose BW backward (latent row 0) on s2, issued a layer at a time between the NeRF's layers
   BwBackward tb{e, s2, p->t + 27, g + 27, b.Gt, Ht, b.dLt, (float*)(ws + T.dHt), nullptr, S, b.dGt2, true, N, ysum,
                 nullptr, 0, 64, bchain ? tc_img(tcimg, 2) : nullptr, (unsigned char*)(ws + T.bitsT)};
+  // issued a layer at a time between the NeRF's layers; with the chains the first tick launches the
+  // T-pose chain and the ticks queue its weight gradients between the NeRF's (groups of both MLPs:
+  // flushing each MLP's products separately, on two lanes, measured 1.353 vs 1.324 ms, profiles/r5y_*)
   auto tick = [&]() { return tb.done() ? ANR_OK : tb.step(); };
   ANR_TRY(tick());
   // d alpha: fp32 (ld 1), or under e.hb bf16 rows of 64 (k_tr_raw_bwd) so both products stay on the fast paths
@@ -1170,7 +1210,8 @@ int anr_train_fwd(const anr_params* p, const anr_frame* f, const float* ray_o, c
   Exec e{s, 0, (o->precision == ANR_BF16 || o->precision == ANR_BF16_ALL) ? 1 : 0, o->precision == ANR_BF16 ? 1 : 0};
   e.ss = om.ss;
   e.hb = e.bf16;
-  ANR_TRY(pack_images(e, p, ws + T.wimg, s, (float*)(ws + T.wslab), kLaneFloats));
+  ANR_TRY(pack_images(e, p, ws + T.wimg, s, (float*)(ws + T.wslab), kLaneFloats, false,
+                      !chains_cover(e, true, false)));
   ANR_TRY(train_forward(p, f, ray_o, ray_d, near_, far_, n_rays, o, out, ws, T, s, e));
   if (out->raw &&
       hipMemcpyAsync(out->raw, ws + T.L.raw, (size_t)n_rays * 64 * 16, hipMemcpyDeviceToDevice, s) != hipSuccess)
@@ -1196,7 +1237,8 @@ int anr_train_bwd(const anr_params* p, float* const* grads, const anr_frame* f, 
   Exec e{s, 0, (o->precision == ANR_BF16 || o->precision == ANR_BF16_ALL) ? 1 : 0, o->precision == ANR_BF16 ? 1 : 0};
   e.ss = om.ss;
   e.hb = e.bf16;
-  ANR_TRY(pack_images(e, p, ws + T.wimg, s, (float*)(ws + T.wslab), kLaneFloats));
+  ANR_TRY(pack_images(e, p, ws + T.wimg, s, (float*)(ws + T.wslab), kLaneFloats, false,
+                      !chains_cover(e, false, true)));
   ANR_TRY(train_backward(p, grads, f, ray_o, ray_d, near_, far_, n_rays, o, d_rgb_map, d_pbw, d_tbw, ws, T, s, e));
   // pose BW MLP backward: d logits were produced by k_tr_softmax_bwd_p
   const long N = (long)n_rays * 64;
@@ -1229,7 +1271,8 @@ int train_step_body(const anr_params* p, float* const* grads, const anr_frame* f
   Exec e{s, 0, (o->precision == ANR_BF16 || o->precision == ANR_BF16_ALL) ? 1 : 0, o->precision == ANR_BF16 ? 1 : 0};
   e.ss = ss;
   e.hb = e.bf16;
-  ANR_TRY(pack_images(e, p, ws + T.wimg, s, (float*)(ws + T.wslab), kLaneFloats));
+  ANR_TRY(pack_images(e, p, ws + T.wimg, s, (float*)(ws + T.wslab), kLaneFloats, false,
+                      !chains_cover(e, true, true)));
   ANR_TRY(train_forward(p, f, ray_o, ray_d, near_, far_, n_rays, o, out, ws, T, s, e, nullptr, split));
   // fused losses (tpose_trainer.py:50-63) and their upstream gradients
   TrainBufs b = bufs(T, ws, f, ray_o, ray_d, near_, far_, n_rays, o);
@@ -1477,7 +1520,8 @@ int anr_network_train_fwd(const anr_params* p, const anr_frame* f, const anr_sam
   Exec e{s, 0, (o->precision == ANR_BF16 || o->precision == ANR_BF16_ALL) ? 1 : 0, o->precision == ANR_BF16 ? 1 : 0};
   e.ss = om.ss;
   e.hb = e.bf16;
-  ANR_TRY(pack_images(e, p, ws + T.wimg, s, (float*)(ws + T.wslab), kLaneFloats));
+  ANR_TRY(pack_images(e, p, ws + T.wimg, s, (float*)(ws + T.wslab), kLaneFloats, false,
+                      !chains_cover(e, true, false)));
   ANR_TRY(train_forward(p, f, nullptr, nullptr, nullptr, nullptr, G, &oo, nullptr, ws, T, s, e, x));
   if (hipMemcpyAsync(raw, ws + T.L.raw, (size_t)x->n_pts * 16, hipMemcpyDeviceToDevice, s) != hipSuccess)
     return fail(ANR_E_HIP, "anr_network_train_fwd: raw copy failed");
@@ -1506,7 +1550,8 @@ int anr_network_train_bwd(const anr_params* p, float* const* grads, const anr_fr
   Exec e{s, 0, (o->precision == ANR_BF16 || o->precision == ANR_BF16_ALL) ? 1 : 0, o->precision == ANR_BF16 ? 1 : 0};
   e.ss = om.ss;
   e.hb = e.bf16;
-  ANR_TRY(pack_images(e, p, ws + T.wimg, s, (float*)(ws + T.wslab), kLaneFloats));
+  ANR_TRY(pack_images(e, p, ws + T.wimg, s, (float*)(ws + T.wslab), kLaneFloats, false,
+                      !chains_cover(e, false, true)));
   ANR_TRY(train_backward(p, grads, f, nullptr, nullptr, nullptr, nullptr, G, &oo, nullptr, d_pbw, d_tbw, ws, T, s, e, x,
                          d_raw));
   const long N = (long)G * 64;
