@@ -180,9 +180,12 @@ __host__ __device__ constexpr int tc_mslot(int l) {
   for (int i = 0; i < l; ++i) k += tc_layer<P>(i).mask ? 1 : 0;
   return k % TC_MS;
 }
-// vector-memory operations every wave issues with slice q: the weight pieces, plus one mask piece
+// vector-memory operations the producer wave issues with slice q: the out-blocks' pieces, plus four
+// mask pieces with the first slice of a masked layer
 template <int P>
-__host__ __device__ constexpr int tc_ops(int q) { return tc_pieces<P>() + (tc_mask_layer<P>(q) >= 0 ? 1 : 0); }
+__host__ __device__ constexpr int tc_ops(int q) {
+  return tc_layer<P>(tc_layer_of<P>(q)).ob + (tc_mask_layer<P>(q) >= 0 ? 4 : 0);
+}
 // a mask slot is refilled only after the layer that read it finished its epilogue and passed a barrier:
 // the next mask to the same slot is issued at mid(q0 - NB + 1), which must come at or after the first
 // slice of the layer that follows the reader
@@ -295,15 +298,23 @@ __global__ void k_tc_pack(TcPackArgs a) {
 }
 
 // ---- the chain kernel ------------------------------------------------------------------------
+// Workgroup = 7 compute waves (16 samples each: a 112-sample tile) + 1 producer wave that issues every
+// LDS-DMA of the ring and alone waits on vmcnt for it. A wave's vmcnt also counts its global stores
+// (gfx9 has no separate store counter) and stores may complete out of order with loads, so a compute
+// wave that both stored its rows and waited for its DMA pieces waited for its stores too: the
+// epilogue stores cost a store round trip at every certify after them (probe: the BW pass 61 us with
+// stores, 34 us without, the same 61 with the stores L2-resident). The producer stores nothing.
+constexpr int TC_CW = 7;
+constexpr int TC_TR = 16 * TC_CW;
+
 struct TcRing {
   unsigned char* lds;  // ring base
   unsigned char* mlds; // mask slots (backward programs)
   const unsigned char* img;
   const TcArgs* a;
-  int wave, lane, tile;
-  // issue slice Q into its ring slot (every wave exactly tc_pieces<P>() 1-KiB pieces), and with the
-  // first slice of a masked layer one piece of the layer's mask bits for this tile (waves w and w + 4
-  // load the same KiB: every wave issues the same number of operations per slice)
+  int lane, tile;
+  // (producer) issue slice Q into its ring slot: its out-blocks' 1-KiB pieces, and with the first
+  // slice of a masked layer the 4 KiB of the layer's mask bits for this tile's rows (+ 16 rows past)
   template <int P, int Q>
   __device__ __forceinline__ void issue() {
     if constexpr (Q < tc_nslices<P>() && !(tc_bwd<P>() && TC_EXP_BWD == 2)) {
@@ -313,9 +324,7 @@ struct TcRing {
       const unsigned char* w = img;
       asm volatile("" : "+s"(w));
 #pragma unroll
-      for (int i = 0; i < tc_pieces<P>(); ++i) {
-        int piece = wave + 8 * i;
-        piece = piece < ob ? piece : ob - 1;
+      for (int piece = 0; piece < ob; ++piece) {
         const unsigned m0 = dst + piece * 1024;
         const unsigned char* sbase = w + (size_t)(kb + piece) * 1024;
         asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(lane * 16), "s"(sbase), "s"(m0)
@@ -323,17 +332,22 @@ struct TcRing {
       }
       constexpr int ml = tc_mask_layer<P>(Q);
       if constexpr (ml >= 0) {
-        const int piece = wave & 3;
-        const unsigned m0 = (unsigned)(uintptr_t)(mlds + tc_mslot<P>(ml) * 4096 + piece * 1024);
-        const unsigned char* sbase = (const unsigned char*)a->bits[ml] + (size_t)tile * 4096 + piece * 1024;
-        asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(lane * 16), "s"(sbase), "s"(m0)
-                     : "memory");
+#pragma unroll
+        for (int piece = 0; piece < 4; ++piece) {
+          const unsigned m0 = (unsigned)(uintptr_t)(mlds + tc_mslot<P>(ml) * 4096 + piece * 1024);
+          const unsigned char* sbase = (const unsigned char*)a->bits[ml] + (size_t)tile * (TC_TR * 32) + piece * 1024;
+          asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(lane * 16), "s"(sbase),
+                       "s"(m0)
+                       : "memory");
+        }
       }
     }
   }
-  // slices issued after slice Q by the time slice Q is certified at mid(Q - 1) (or the prologue)
+  // slice Q certified at mid(Q - 1) (or the prologue): the producer waits until only the operations
+  // of the slices issued after it are outstanding (loads complete in order; a count past the counter's
+  // 63 waits for more, which is safe), then every wave meets at the barrier
   template <int P, int Q>
-  __device__ __forceinline__ void certify() {
+  __device__ __forceinline__ void certify(bool producer) {
     // issued so far: the prologue's slices 0 .. NB-2, then one per mid(): mid(Q - 2) issued Q + NB - 3
     constexpr int last = tc_nslices<P>() - 1;
     constexpr int issued0 = Q == 0 ? tc_nb<P>() - 2 : Q + tc_nb<P>() - 3;
@@ -341,9 +355,10 @@ struct TcRing {
     constexpr int after = [] {
       int n = 0;
       for (int x = Q + 1; x <= issued; ++x) n += tc_ops<P>(x);
-      return n;
+      return n < 63 ? n : 63;
     }();
-    if constexpr (!(tc_bwd<P>() && TC_EXP_BWD == 3)) tc_wait_vmcnt<after>();
+    if constexpr (!(tc_bwd<P>() && TC_EXP_BWD == 3))
+      if (producer) tc_wait_vmcnt<after>();
     __syncthreads();
   }
   template <int P, int Q>
@@ -379,12 +394,26 @@ __device__ __forceinline__ void tc_body(const TcArgs& a) {
     __syncthreads();
   }
   const int M = *a.M_dev;
-  const int ntiles = (M + 127) / 128;
+  const int ntiles = (M + TC_TR - 1) / TC_TR;
   if ((int)blockIdx.x >= ntiles) return;  // uniform per workgroup
-  TcRing rg{ring, mring, a.img, &a, wave, lane, 0};
+  TcRing rg{ring, mring, a.img, &a, lane, 0};
+  if (wave == TC_CW) {
+    // the producer: the same barriers as the compute waves (prologue, one per slice, tile end)
+    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+      rg.tile = __builtin_amdgcn_readfirstlane(tile);
+      tc_for<0, tc_nb<P>() - 1>([&](auto qc) { rg.template issue<P, decltype(qc)::value>(); });
+      rg.template certify<P, 0>(true);
+      tc_for<0, tc_nslices<P>() - 1>([&](auto qc) {
+        constexpr int Q = decltype(qc)::value;
+        rg.template certify<P, Q + 1>(true);
+        rg.template issue<P, Q + tc_nb<P>() - 1>();
+      });
+      __syncthreads();
+    }
+    return;
+  }
   for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    rg.tile = __builtin_amdgcn_readfirstlane(tile);
-    const int row = tile * 128 + wave * 16 + pl;
+    const int row = tile * TC_TR + wave * 16 + pl;
     const bool valid = row < M;
     const int rr = valid ? row : M - 1;
     // memory B fragments (bf16 or fp32 rows, rounded RNE to bf16 as the layer-wise path rounds its
@@ -403,9 +432,8 @@ __device__ __forceinline__ void tc_body(const TcArgs& a) {
     tc_bf16x8 gm[2], gv = {};
     tc_for<0, tc_memk<P>()>([&](auto sc) { gm[decltype(sc)::value] = load_mem(a.mem, a.ld_mem, a.kmem_cols, a.mem_f32, decltype(sc)::value); });
     if constexpr (P == 1 || P == 3) gv = load_mem(a.mem2, a.ld_mem2, a.kmem2_cols, a.mem2_f32, 0);
-    // ring prologue: slices 0 .. NB-2, slice 0 certified
-    tc_for<0, tc_nb<P>() - 1>([&](auto qc) { rg.template issue<P, decltype(qc)::value>(); });
-    rg.template certify<P, 0>();
+    // ring prologue (the producer's): slice 0 certified
+    rg.template certify<P, 0>(false);
     tc_bf16x8 bprev[8];
     f32x4 acc[20];
     tc_for<0, tc_nl<P>()>([&](auto lc) {
@@ -444,10 +472,7 @@ __device__ __forceinline__ void tc_body(const TcArgs& a) {
           __builtin_amdgcn_sched_barrier(0);
           // halfway through the slice: certify the next slice, refill the slot of the previous one
           if constexpr (o == (L.ob - 1) / 2) {
-            if constexpr (Q + 1 < tc_nslices<P>()) {
-              rg.template certify<P, Q + 1>();
-              rg.template issue<P, Q + tc_nb<P>() - 1>();
-            }
+            if constexpr (Q + 1 < tc_nslices<P>()) rg.template certify<P, Q + 1>(false);
           }
         });
       });
@@ -629,7 +654,7 @@ int tchain_run(int prog, const TcArgs& a, int cap, int cus, hipStream_t s) {
     if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, lds) != hipSuccess) return -1;
     attr[prog] = true;
   }
-  const int tiles = (cap + 127) / 128;
+  const int tiles = (cap + TC_TR - 1) / TC_TR;
   const int grid = tiles < cus ? tiles : cus;
   if (grid <= 0) return 0;
   TcArgs args = a;

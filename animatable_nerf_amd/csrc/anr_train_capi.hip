@@ -37,8 +37,9 @@ struct TLayout {
   size_t ysum, acc3, d_rgb, d_pbw, d_tbw, wimg, wslab, tcimg, bitsP, bitsT, bitsN, total;
 };
 
-// ReLU mask bits of one chain layer (TcArgs::bits): 32 B per sample, rows padded to the 128-sample tile
-size_t bits_stride(long N) { return (size_t)((N + 127) / 128 * 128) * 32; }
+// ReLU mask bits of one chain layer (TcArgs::bits): 32 B per sample, 128 rows past the last (a tile's
+// mask DMA reads 4 KiB = 128 rows from the tile's first)
+size_t bits_stride(long N) { return (size_t)((N + 127) / 128 * 128 + 128) * 32; }  // + the last tile's DMA overrun
 
 TLayout tlayout(int n_rays, int chunk, long np, long nt) {
   TLayout T{};

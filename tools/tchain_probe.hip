@@ -59,8 +59,8 @@ int main(int argc, char** argv) {
   std::vector<void*> outs(12), bits(12);
   for (int l = 0; l < 12; ++l) {
     CK(hipMalloc(&outs[l], pad * 256 * 4));
-    CK(hipMalloc(&bits[l], pad * 32));
-    k_fill_bf16<<<(unsigned)((pad * 16 + 255) / 256), 256>>>((unsigned short*)bits[l], pad * 16, 11u + l, 2.f);
+    CK(hipMalloc(&bits[l], (pad + 128) * 32));
+    k_fill_bf16<<<(unsigned)(((pad + 128) * 16 + 255) / 256), 256>>>((unsigned short*)bits[l], (pad + 128) * 16, 11u + l, 2.f);
   }
   float *mem, *mem2, *aux, *bias;
   CK(hipMalloc(&mem, pad * 64 * 4));
@@ -121,7 +121,7 @@ int main(int argc, char** argv) {
   // MACs per row: every 1-KiB fragment of the image is 16 outputs x 32 inputs
   const double macs = (double)(img / 1024) * 512;
   const double tflops = 2.0 * macs * rows / (us * 1e-6) / 1e12;
-  const int tiles = (rows + 127) / 128;
+  const int tiles = (rows + 111) / 112;
   printf("prog %d rows %d tiles %d grid %d: %.2f us per launch, %.1f TFLOP/s (padded MFMA work)\n", prog, rows, tiles,
          tiles < cus ? tiles : cus, us, tflops);
   return 0;
