@@ -1412,7 +1412,11 @@ __device__ __forceinline__ void sdfnet_body(const MlpArgs& a) {
     };
     // each layer's softplus runs in the next layer's split (SP_IN), which also stores its h
     // store targets formed at each call (a per-tile array of row pointers costs 16 VGPRs for the tile)
+#ifdef ANR_EXP_NOHSTORE  // timing experiment only (tools/build_ab.sh): no h stores
+    auto st = [&](int i) { return LayerIO{nullptr}; };
+#else
     auto st = [&](int i) { return LayerIO{valid ? (i == 3 ? a.x4 : a.sdf_h[i]) + row * 256 : nullptr}; };
+#endif
     f32x4 dummy[1];
     layer<true, V, 0, false>(p, dummy, emb, vemb, A, sb, g, lane);
     layer<true, V, 1, false, false, 1>(p, A, emb, vemb, B, sb, g, lane, st(0));
@@ -1424,7 +1428,9 @@ __device__ __forceinline__ void sdfnet_body(const MlpArgs& a) {
     layer<true, V, 6, false, false, 1>(p, B, emb, vemb, A, sb, g, lane, st(5));
     layer<true, V, 7, false, false, 1>(p, A, emb, vemb, B, sb, g, lane, st(6));
     softplus_regs<16, V>(B);  // lin8 (a tail-slice layer, not streamed) reads h7 as is
+#ifndef ANR_EXP_NOHSTORE
     store_h(B, a.sdf_h[7]);
+#endif
     layer<true, V, 8, false>(p, B, emb, vemb, A, sb, g, lane);  // [sdf || feature], no activation
     if (valid) {  // sdf (neuron 0) to column 0, the feature (neurons 1..256) to columns 8..263
       float* d = a.y8 + row * 264;

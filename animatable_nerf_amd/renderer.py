@@ -14,6 +14,7 @@ and shapes are the reference's: ``rgb_map (1,R,3)``, ``acc_map (1,R)``, ``depth_
   the reference's ``loss.backward()`` / optimizer loop drives it unchanged.
 """
 import ctypes
+import os
 
 import torch
 
@@ -224,8 +225,11 @@ class Renderer:
         return {'rgb_map': rgb, 'acc_map': acc, 'depth_map': depth, 'raw': raw, 'pbw': pbw, 'tbw': tbw}
 
     # render(): the frame in this many parts (whole reference chunks) so part k's outputs cross the
-    # host link while part k + 1 renders (a 512x512 frame moves ~1.4 GB to the host)
-    HOST_PARTS = 4
+    # host link while part k + 1 renders (a 512x512 frame moves ~1.4 GB to the host); 8 parts measured
+    # 146.0 ms against 149.3 for 4 (profiles/r6c_*); ANR_HOST_PARTS overrides (read per call)
+    HOST_PARTS = 8
+    # headroom of the alpha_ind row buffers over the previous frame's row count
+    ROWS_HEADROOM = 1.125
 
     def render(self, batch):
         if torch.is_grad_enabled() and any(p.requires_grad for p in self.net.parameters()) and self.net.training:
@@ -233,18 +237,22 @@ class Renderer:
         R = batch['ray_o'].shape[1]
         chunk = int(self.cfg.get('chunk', CHUNK))
         n_chunks = (R + chunk - 1) // chunk
+        parts = int(os.environ.get('ANR_HOST_PARTS', self.HOST_PARTS))
         with torch.no_grad():
-            if n_chunks < 2 * self.HOST_PARTS or not self.device().type == 'cuda':
+            if n_chunks < 2 * parts or not self.device().type == 'cuda':
                 return to_host(self.render_device(batch))
-            return self._render_overlapped(batch, R, chunk)
+            return self._render_overlapped(batch, R, chunk, parts)
 
-    def _render_overlapped(self, batch, R, chunk):
+    def _render_overlapped(self, batch, R, chunk, parts):
         """render_device over parts of whole chunks (per-chunk semantics unchanged: the rows of the parts,
         concatenated in order, are the whole frame's, as parallel.render_sharded relies on), each part's
-        per-ray outputs copied on a side stream into page-locked host buffers while the next part
-        renders. The alpha_ind rows (pbw / tbw) are counted only as each part finishes, so they stay
-        on the device until the frame's row count is known and then cross into exact-size page-locked
-        buffers (no capacity-sized host allocation is held by the returned tensors)."""
+        outputs copied on a side stream into page-locked host buffers while the next part renders.
+        The alpha_ind rows (pbw / tbw) are counted only as each part finishes: they go, as each part
+        finishes, to their final offset in one (1, cap, 24) page-locked buffer sized from the previous
+        frame's row count with ROWS_HEADROOM (the first frame: from the rows seen so far), and the
+        returned (1, m, 24) tensors are its first m rows (contiguous; no capacity-sized host buffer,
+        no host concatenation). A frame whose rows outgrow the buffer moves the placed rows into an
+        exact-size one (one host copy) and the rest from the device."""
         from .parallel import RAY_KEYS as SLICED, shard_chunks
         dev = self.device()
         ns = int(self.cfg.N_samples)
@@ -256,13 +264,23 @@ class Renderer:
             pin = dict(dtype=torch.float32, pin_memory=True)
             h = {'rgb_map': torch.empty((1, R, 3), **pin), 'acc_map': torch.empty((1, R), **pin),
                  'depth_map': torch.empty((1, R), **pin), 'raw': torch.empty((1, R * ns, 4), **pin)}
-            keep, rows, kept = [], [], 0
-            for k in range(self.HOST_PARTS):
-                a, b = shard_chunks(R, k, self.HOST_PARTS, chunk)
+            keep, late, kept, off = [], [], 0, 0
+            hp = ht = None
+            est = int(getattr(self, '_rows_est', 0))
+            for k in range(parts):
+                a, b = shard_chunks(R, k, parts, chunk)
                 if a >= b:
                     continue
                 sub = {key_: (v[:, a:b] if key_ in SLICED and torch.is_tensor(v) else v) for key_, v in batch.items()}
                 out = self.render_device(sub)  # reads the part's row count: the part has finished when it returns
+                p, t = out['pbw'], out['tbw']
+                n = p.shape[1]
+                if hp is None and (est > 0 or n > 0):
+                    # the previous frame's rows, or (first frame) this part's rows per part so far, extrapolated
+                    guess = est if est > 0 else (off + n) * parts // (k + 1)
+                    cap = int(guess * self.ROWS_HEADROOM) + 64
+                    hp = torch.empty((1, cap, 24), **pin)
+                    ht = torch.empty((1, cap, 24), **pin)
                 ev = torch.cuda.Event()
                 ev.record(cur)
                 with torch.cuda.stream(cs):
@@ -271,21 +289,33 @@ class Renderer:
                     h['acc_map'][:, a:b].copy_(out['acc_map'], non_blocking=True)
                     h['depth_map'][:, a:b].copy_(out['depth_map'], non_blocking=True)
                     h['raw'][:, a * ns:b * ns].copy_(out['raw'], non_blocking=True)
+                    if n and hp is not None and off + n <= hp.shape[1] and not late:
+                        hp[:, off:off + n].copy_(p, non_blocking=True)
+                        ht[:, off:off + n].copy_(t, non_blocking=True)
+                    elif n:
+                        late.append((off, p, t))
                 keep.append(out)  # device outputs stay alive until their copies are done
-                rows.append((out['pbw'], out['tbw']))
+                off += n
                 kept += self.last_counts[0]
-            m = sum(p.shape[1] for p, _ in rows)
-            h['pbw'] = torch.empty((1, m, 24), **pin)
-            h['tbw'] = torch.empty((1, m, 24), **pin)
-            with torch.cuda.stream(cs):
-                cs.wait_stream(cur)
-                off = 0
-                for p, t in rows:
-                    n = p.shape[1]
-                    h['pbw'][:, off:off + n].copy_(p, non_blocking=True)
-                    h['tbw'][:, off:off + n].copy_(t, non_blocking=True)
-                    off += n
+            m = off
+            if late or hp is None:
+                # outgrew the estimate: the placed rows into exact-size buffers, the rest from the device
+                cs.synchronize()
+                placed = late[0][0] if late else 0
+                ep = torch.empty((1, m, 24), **pin)
+                et = torch.empty((1, m, 24), **pin)
+                if placed:
+                    ep[:, :placed].copy_(hp[:, :placed])
+                    et[:, :placed].copy_(ht[:, :placed])
+                with torch.cuda.stream(cs):
+                    for o, p, t in late:
+                        ep[:, o:o + p.shape[1]].copy_(p, non_blocking=True)
+                        et[:, o:o + t.shape[1]].copy_(t, non_blocking=True)
+                hp, ht = ep, et
             cs.synchronize()
+            h['pbw'] = hp[:, :m]
+            h['tbw'] = ht[:, :m]
+        self._rows_est = m
         self.last_counts = (kept, m)
         return h
 

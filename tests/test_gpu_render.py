@@ -246,6 +246,16 @@ def test_render_overlapped_host_copy_equals_device_render(renderer, dev):
         again = renderer.render(bt)  # a second call does not overwrite the first call's outputs
     assert again['raw'].data_ptr() != got['raw'].data_ptr()
     assert torch.equal(got['raw'], ref['raw'])
+    # the second call sizes the alpha_ind row buffers from the first's count (rows placed as parts
+    # finish); a too-small estimate moves the placed rows into exact-size buffers
+    for est in (None, 1):
+        if est is not None:
+            renderer._rows_est = est
+        with torch.no_grad():
+            again = renderer.render(bt)
+        for k in ('rgb_map', 'acc_map', 'depth_map', 'raw', 'pbw', 'tbw'):
+            assert got[k].shape == again[k].shape and torch.equal(again[k], ref[k]), (k, est)
+        assert again['pbw'].is_contiguous() and again['pbw'].is_pinned()
 
 
 @pytest.mark.parametrize('world', [3, 8])
