@@ -18,7 +18,7 @@
 // with the weights as the A operand (16 output neurons x 32 inputs) and the samples as B: the C
 // layout of out-blocks 2s, 2s+1 (lane l: neurons 32s + 4(l>>4) + r and 32s + 16 + 4(l>>4) + r of sample
 // l & 15) is the B fragment of the next layer's k-step s when the packed weight columns follow the same
-// order (tc_perm), so activations never leave registers. Memory segments (gamma rows, gamma(dir) rows)
+// order (tc_nrn), so activations never leave registers. Memory segments (gamma rows, gamma(dir) rows)
 // are read straight into B fragments in natural column order. Weights stream through a 4-slot LDS ring
 // of slices (one 32-input k-step of all of a layer's out-blocks, <= 17 KiB) by LDS-DMA, one barrier per
 // slice with counted vmcnt waits (the render kernel's scheme, anr_mlp_body.h Pipe); biases sit in an LDS
@@ -214,7 +214,10 @@ static_assert(tc_lds_bytes<0>() <= 160 * 1024 && tc_lds_bytes<1>() <= 160 * 1024
 static_assert(tc_masks_ok<2>() && tc_masks_ok<3>(), "mask slot reuse");
 
 // input column of MFMA k slot (8 h + j) of a k-step s that reads the previous layer's registers
-__host__ __device__ constexpr int tc_perm(int s, int h, int j) { return 32 * s + (j < 4 ? 4 * h + j : 16 + 4 * h + (j - 4)); }
+// output neuron of row m of out-block o: blocks 2s, 2s + 1 hold neurons 32 s + 8 (m >> 2) + {0..3} and
+// + {4..7}, so C lane l of the pair holds the 8 consecutive neurons 32 s + 8 (l >> 4) + j — one 16-B
+// row store, and in natural order the B fragment (k slot 8 (l >> 4) + j) of the next layer's k-step s
+__host__ __device__ constexpr int tc_nrn(int o, int m) { return 32 * (o >> 1) + 8 * (m >> 2) + 4 * (o & 1) + (m & 3); }
 
 __device__ __forceinline__ unsigned short tc_bf(float f) {  // RNE (the layer-wise path's rounding)
   uint32_t u = __float_as_uint(f);
@@ -275,12 +278,12 @@ __global__ void k_tc_pack(TcPackArgs a) {
   const int j = (int)(loc & 7), lane = (int)((loc >> 3) & 63);
   const long fr = loc >> 9;  // fragment index = t * ob + o
   const int o = (int)(fr % L.ob), t = (int)(fr / L.ob);
-  const int m = 16 * o + (lane & 15), h = lane >> 4;
+  const int m = tc_nrn(o, lane & 15), h = lane >> 4;
   float v = 0.f;
   const bool mem = L.mem_first ? t < L.kmem : t >= L.kprev;
   const int s = mem ? (L.mem_first ? t : t - L.kprev) : (L.mem_first ? t - L.kmem : t);
-  // input index of this k slot: natural order for memory operands, tc_perm for the previous layer's registers
-  const int c = mem ? 32 * s + 8 * h + j : tc_perm(s, h, j);
+  // input index of this k slot (natural order: memory operands and the previous layer's registers alike)
+  const int c = 32 * s + 8 * h + j;
   if (c < (mem ? L.kmem_cols : L.kprev_cols)) {
     if (!L.trans) {
       const int col = (mem ? L.cmem : L.cprev) + c;
@@ -381,10 +384,11 @@ __device__ __forceinline__ void tc_body(const TcArgs& a) {
     tc_for<0, tc_nl<P>()>([&](auto lc) {
       constexpr int l = decltype(lc)::value;
       constexpr int n = tc_layer<P>(l).ob * 16;
-      for (int i = tid; i < n; i += 512) {
+      for (int i = tid; i < n; i += 512) {  // in out-block row order: row i % 16 of block i / 16
+        const int nr = tc_nrn(i >> 4, i & 15);
         float v = 0.f;
-        if (i < a.nout[l]) v = a.bias[l][i];
-        else if (tc_layer<P>(l).out == TC_FA && i == 256) v = a.bias2[0];
+        if (nr < a.nout[l]) v = a.bias[l][nr];
+        else if (tc_layer<P>(l).out == TC_FA && nr == 256) v = a.bias2[0];
         sb[tc_bias_off<P>(l) + i] = v;
       }
     });
@@ -480,7 +484,7 @@ __device__ __forceinline__ void tc_body(const TcArgs& a) {
       // ReLU on the packed words (forward; max with 0 as int16 = ReLU, and ReLU commutes with RNE) or the
       // ReLU-derivative mask (backward); fp32 heads / gamma gradients from the fp32 accumulators
       if constexpr (L.out == TC_BF16 || L.out == TC_FA || L.out == TC_SPLIT) {
-        // word 4 s + j: neurons 32 s + 16 (j >> 1) + 4 h + 2 (j & 1) + {0, 1} (a B fragment per s)
+        // word 4 s + j: neurons 32 s + 8 h + 2 j + {0, 1} (tc_nrn; the 4 words of s: one row store, one B fragment)
         uint32_t wd[32];
         tc_for<0, 8>([&](auto sc) {
           constexpr int s = decltype(sc)::value;
@@ -512,8 +516,7 @@ __device__ __forceinline__ void tc_body(const TcArgs& a) {
         tc_for<0, 8>([&](auto sc) {
           constexpr int s = decltype(sc)::value;
           if (valid && (TC_EXP != 4 || a.nout[0] == -7)) {
-            *(uint2*)(orow + 32 * s + 4 * h) = make_uint2(wd[4 * s], wd[4 * s + 1]);
-            *(uint2*)(orow + 32 * s + 16 + 4 * h) = make_uint2(wd[4 * s + 2], wd[4 * s + 3]);
+            *(uint4*)(orow + 32 * s + 8 * h) = make_uint4(wd[4 * s], wd[4 * s + 1], wd[4 * s + 2], wd[4 * s + 3]);
           }
           bprev[s] = __builtin_bit_cast(tc_bf16x8, make_uint4(wd[4 * s], wd[4 * s + 1], wd[4 * s + 2], wd[4 * s + 3]));
         });
@@ -560,7 +563,7 @@ __device__ __forceinline__ void tc_body(const TcArgs& a) {
         const int nout = a.nout[l];
         tc_for<0, L.ob>([&](auto oc) {
           constexpr int o = decltype(oc)::value;
-          const int c = 16 * o + 4 * h;
+          const int c = 32 * (o >> 1) + 8 * h + 4 * (o & 1);
           if (valid && (TC_EXP != 4 || a.nout[0] == -7)) {
             if (c + 4 <= nout) {
               *(f32x4*)(orow + c) = acc[o];
@@ -588,7 +591,7 @@ __device__ __forceinline__ void tc_body(const TcArgs& a) {
           float* arow = a.aux + (size_t)row * a.ld_aux;
           tc_for<O0, L.ob>([&](auto oc) {
             constexpr int o = decltype(oc)::value;
-            const int c = 16 * (o - O0) + 4 * h;
+            const int c = 32 * ((o - O0) >> 1) + 8 * h + 4 * (o & 1);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               if (c + r < a.aux_cols) {

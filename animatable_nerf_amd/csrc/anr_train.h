@@ -192,7 +192,7 @@ struct TcArgs {
   int ld_mem2, kmem2_cols;
   int mem_f32, mem2_f32;  // the memory operands are fp32 rows (else bf16)
   // ReLU mask bits per layer, rows of 32 B (lane h of a sample: 8 B; packed word i = 4 s + j of the epilogue
-  // (neurons 32 s + 16 (j >> 1) + 4 h + 2 (j & 1) + {0, 1}) at bits (i & 15) and 16 + (i & 15) of dword i >> 4),
+  // (neurons 32 s + 8 h + 2 j + {0, 1}) at bits (i & 15) and 16 + (i & 15) of dword i >> 4),
   // at least ceil(rows / 128) x 128 rows: forward programs write them for their ReLU layers (when set),
   // backward programs read the mask of each masked layer's outputs
   void* bits[12];
