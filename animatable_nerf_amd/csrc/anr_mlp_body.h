@@ -203,18 +203,6 @@ __host__ __device__ constexpr int prog_later_loads(int e, int q) {
   return n;
 }
 
-// producer mode (Pipe::pmode): the KiB pieces issued after slice (e, q) that may still be in flight
-// when it is consumed, all by the one producer wave (a count past the counter's 63 waits for more)
-template <bool B16, int V>
-__host__ __device__ constexpr int prog_later_kb(int e, int q) {
-  int n = 0;
-  for (int d = 1; d <= mlp_nbuf<B16>() - 3; ++d) {
-    const int eq = prog_advance<B16, V>(e, q, d);
-    n += prog_slice_kb<B16, V>(eq / 1024, eq % 1024);
-  }
-  return n < 63 ? n : 63;
-}
-
 // s_waitcnt with only vmcnt constrained (gfx9 encoding: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt_hi[15:14])
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
@@ -232,10 +220,6 @@ struct Pipe {
   int lane;
   int pose_woff;  // added to slices of the pose-space BW pass (novel_pose_bw weights)
   int pend;       // ring slot of the refill whose pieces are being spread (ANR_DMA_SPREAD)
-  // producer mode (the sdf programs, ANR_PIPE_PROD): wave 7 issues every piece of the stream and alone
-  // waits on vmcnt; waves 0..6 compute 112-sample tiles and never wait for the DMA (their stores and
-  // loads share the vmcnt counter, so a computing wave that waits for its DMA also waits for them)
-  int pmode;
 
   // issue the HBM/L2 -> LDS copy of `kb` KiB at byte `off` of the packed image into ring slot `buf`;
   // every wave issues exactly `loads` 1-KiB pieces (pieces past the end repeat the last one: same
@@ -246,10 +230,6 @@ struct Pipe {
   // slice. Hidden from the compiler, the only waits on the stream are ours (wait_vmcnt in next());
   // the compiler's own vmcnt waits stay correct, only stricter (loads return in order).
   __device__ __forceinline__ void stage(int off, int kb, int loads, int buf, int first = 0) {
-    if (pmode) {
-      if (wave == 7) stage_all(off, kb, buf);
-      return;
-    }
     const unsigned dst = (unsigned)(uintptr_t)(lds + buf * smax);
     // launder the base so the per-slice addresses are formed here, not hoisted out of the tile
     // loop (hundreds of loop-invariant 64-bit addresses otherwise spill)
@@ -267,25 +247,10 @@ struct Pipe {
     }
   }
 
-  // producer mode: every piece of the slice from the producer wave
-  __device__ __forceinline__ void stage_all(int off, int kb, int buf) {
-    const unsigned dst = (unsigned)(uintptr_t)(lds + buf * smax);
-    const unsigned char* w = wimg;
-    asm volatile("" : "+s"(w));
-    for (int piece = 0; piece < kb; ++piece) {
-      const unsigned m0 = dst + piece * 1024;
-      const unsigned char* sbase = w + off + piece * 1024;
-      asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(lane * 16), "s"(sbase), "s"(m0)
-                   : "memory");
-    }
-  }
-
   // wait until this wave's pieces of all but the last N (8-wave count) issued pieces have landed
   template <int N>
   __device__ __forceinline__ void wait_stream() {
-#ifndef ANR_EXP_NOWAIT  // timing experiment only (tools/build_ab.sh): results are not valid
     wait_vmcnt<N>();
-#endif
   }
 
   template <bool B16, int V, int E, int Q>
@@ -302,11 +267,7 @@ struct Pipe {
       stage_slice<B16, V, eq / 1024, eq % 1024>(decltype(d)::value);
     });
     cur = 0;
-    if (pmode) {
-      if (wave == 7) wait_vmcnt<prog_later_kb<B16, V>(0, 0)>();
-    } else {
-      wait_stream<prog_later_loads<B16, V>(0, 0)>();
-    }
+    wait_stream<prog_later_loads<B16, V>(0, 0)>();
     __syncthreads();
   }
 
@@ -326,16 +287,10 @@ struct Pipe {
     constexpr int NB = mlp_nbuf<B16>();
     constexpr int e1 = prog_advance<B16, V>(E, Q, 1);
     constexpr int eq = prog_advance<B16, V>(E, Q, NB - 1);
-    int slot = cur + NB - 1;
-    slot = slot >= NB ? slot - NB : slot;
-    if (pmode) {  // the producer waits and refills the whole slot; piece<>() does nothing
-      if (wave == 7) wait_vmcnt<prog_later_kb<B16, V>(e1 / 1024, e1 % 1024)>();
-      __syncthreads();
-      stage_slice<B16, V, eq / 1024, eq % 1024>(slot);
-      return;
-    }
     wait_stream<prog_later_loads<B16, V>(e1 / 1024, e1 % 1024)>();
     __syncthreads();
+    int slot = cur + NB - 1;
+    slot = slot >= NB ? slot - NB : slot;
     if constexpr (SPREAD) pend = slot;
     else stage_slice<B16, V, eq / 1024, eq % 1024>(slot);
   }
@@ -348,7 +303,6 @@ struct Pipe {
     constexpr int off = prog_slice_off<B16, V>(EE, QQ);
     constexpr int loads = prog_slice_loads<B16, V>(EE, QQ);
     constexpr int i1 = I1 < loads ? I1 : loads;
-    if (pmode) return;
     if constexpr (I0 < i1) stage(off + (prog_pose(EE) ? pose_woff : 0), prog_slice_kb<B16, V>(EE, QQ), i1, pend, I0);
   }
   __device__ __forceinline__ void leave() { cur = cur + 1 >= nbuf ? 0 : cur + 1; }
@@ -459,11 +413,6 @@ struct LayerIO {
   const float* g0 = nullptr;
   const float* g1 = nullptr;
 };
-
-// producer-mode weight stream for the sdf programs (Pipe::pmode)
-#ifndef ANR_PIPE_PROD
-#define ANR_PIPE_PROD 0
-#endif
 
 // the sdf programs' stored softplus outputs h (8 KiB per sample, written once, read once) bypass
 // the weight stream's L2 lines: non-temporal stores (k_sdfnet_b16) and loads (k_sdfgrad_b16)
@@ -1380,17 +1329,15 @@ __device__ __forceinline__ void resd_body(const MlpArgs& a) {
   float* sb = (float*)smem;  // bias table (anr_layers.h LDS layout)
   fill_bias_table<V>(a, sb, tid);
   const int n = a.n_rows;
-  constexpr int PM = ANR_PIPE_PROD;  // producer mode: 7 computing waves, 112-sample tiles
-  constexpr int TR = PM ? 112 : 128;
-  const int ntiles = (n + TR - 1) / TR;
+  const int ntiles = (n + 127) / 128;
   if ((int)blockIdx.x >= ntiles) return;  // uniform per workgroup, before any LDS-DMA
 
-  Pipe p{smem + mlp_ring_off(), mlp_slice_max<true>(), mlp_nbuf<true>(), a.wimg, 0, wave, lane, 0, 0, PM};
+  Pipe p{smem + mlp_ring_off(), mlp_slice_max<true>(), mlp_nbuf<true>(), a.wimg, 0, wave, lane, 0};
   p.template start<true, V>();
 
   for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const int idx = tile * TR + wave * 16 + pl;
-    const bool valid = idx < n && !(PM && wave == 7);
+    const int idx = tile * 128 + wave * 16 + pl;
+    const bool valid = idx < n;
     const float* pt = a.ptb + (size_t)(valid ? idx : n - 1) * a.ptb_ld;
     const float x[3] = {pt[0], pt[1], pt[2]};
     float emb[16], vemb[8];
@@ -1437,17 +1384,15 @@ __device__ __forceinline__ void sdfnet_body(const MlpArgs& a) {
   float* sb = (float*)smem;  // bias table (anr_layers.h LDS layout)
   fill_bias_table<V>(a, sb, tid);
   const int n = a.n_rows;
-  constexpr int PM = ANR_PIPE_PROD;  // producer mode: 7 computing waves, 112-sample tiles
-  constexpr int TR = PM ? 112 : 128;
-  const int ntiles = (n + TR - 1) / TR;
+  const int ntiles = (n + 127) / 128;
   if ((int)blockIdx.x >= ntiles) return;  // uniform per workgroup, before any LDS-DMA
 
-  Pipe p{smem + mlp_ring_off(), mlp_slice_max<true>(), mlp_nbuf<true>(), a.wimg, 0, wave, lane, 0, 0, PM};
+  Pipe p{smem + mlp_ring_off(), mlp_slice_max<true>(), mlp_nbuf<true>(), a.wimg, 0, wave, lane, 0};
   p.template start<true, V>();
 
   for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const int idx = tile * TR + wave * 16 + pl;
-    const bool valid = idx < n && !(PM && wave == 7);
+    const int idx = tile * 128 + wave * 16 + pl;
+    const bool valid = idx < n;
     const size_t row = (size_t)(valid ? idx : n - 1);
     const float* pt = a.ptb + row * a.ptb_ld;
     const float x[3] = {pt[0], pt[1], pt[2]};
@@ -1467,11 +1412,7 @@ __device__ __forceinline__ void sdfnet_body(const MlpArgs& a) {
     };
     // each layer's softplus runs in the next layer's split (SP_IN), which also stores its h
     // store targets formed at each call (a per-tile array of row pointers costs 16 VGPRs for the tile)
-#ifdef ANR_EXP_NOHSTORE  // timing experiment only (tools/build_ab.sh): no h stores
-    auto st = [&](int i) { return LayerIO{nullptr}; };
-#else
     auto st = [&](int i) { return LayerIO{valid ? (i == 3 ? a.x4 : a.sdf_h[i]) + row * 256 : nullptr}; };
-#endif
     f32x4 dummy[1];
     layer<true, V, 0, false>(p, dummy, emb, vemb, A, sb, g, lane);
     layer<true, V, 1, false, false, 1>(p, A, emb, vemb, B, sb, g, lane, st(0));
@@ -1483,9 +1424,7 @@ __device__ __forceinline__ void sdfnet_body(const MlpArgs& a) {
     layer<true, V, 6, false, false, 1>(p, B, emb, vemb, A, sb, g, lane, st(5));
     layer<true, V, 7, false, false, 1>(p, A, emb, vemb, B, sb, g, lane, st(6));
     softplus_regs<16, V>(B);  // lin8 (a tail-slice layer, not streamed) reads h7 as is
-#ifndef ANR_EXP_NOHSTORE
     store_h(B, a.sdf_h[7]);
-#endif
     layer<true, V, 8, false>(p, B, emb, vemb, A, sb, g, lane);  // [sdf || feature], no activation
     if (valid) {  // sdf (neuron 0) to column 0, the feature (neurons 1..256) to columns 8..263
       float* d = a.y8 + row * 264;
@@ -1523,17 +1462,15 @@ __device__ __forceinline__ void sdfgrad_body(const MlpArgs& a) {
   float* sw8 = sb + prog_bias_off<V>(prog_len<V>());
   for (int i = tid; i < 256; i += 512) sw8[i] = a.w8row[i];
   const int n = a.n_rows;
-  constexpr int PM = ANR_PIPE_PROD;  // producer mode: 7 computing waves, 112-sample tiles
-  constexpr int TR = PM ? 112 : 128;
-  const int ntiles = (n + TR - 1) / TR;
+  const int ntiles = (n + 127) / 128;
   if ((int)blockIdx.x >= ntiles) return;  // uniform per workgroup, before any LDS-DMA
 
-  Pipe p{smem + mlp_ring_off(), mlp_slice_max<true>(), mlp_nbuf<true>(), a.wimg, 0, wave, lane, 0, 0, PM};
+  Pipe p{smem + mlp_ring_off(), mlp_slice_max<true>(), mlp_nbuf<true>(), a.wimg, 0, wave, lane, 0};
   p.template start<true, V>();  // its barrier also publishes sw8
 
   for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const int idx = tile * TR + wave * 16 + pl;
-    const bool valid = idx < n && !(PM && wave == 7);
+    const int idx = tile * 128 + wave * 16 + pl;
+    const bool valid = idx < n;
     const size_t row = (size_t)(valid ? idx : n - 1);
     float emb[16], vemb[8];
 #pragma unroll
@@ -1606,17 +1543,15 @@ __device__ __forceinline__ void color_body(const MlpArgs& a) {
   float* sb = (float*)smem;
   fill_bias_table<V>(a, sb, tid);
   const int n = a.n_rows;
-  constexpr int PM = ANR_PIPE_PROD;  // producer mode: 7 computing waves, 112-sample tiles
-  constexpr int TR = PM ? 112 : 128;
-  const int ntiles = (n + TR - 1) / TR;
+  const int ntiles = (n + 127) / 128;
   if ((int)blockIdx.x >= ntiles) return;  // uniform per workgroup, before any LDS-DMA
 
-  Pipe p{smem + mlp_ring_off(), mlp_slice_max<true>(), mlp_nbuf<true>(), a.wimg, 0, wave, lane, 0, 0, PM};
+  Pipe p{smem + mlp_ring_off(), mlp_slice_max<true>(), mlp_nbuf<true>(), a.wimg, 0, wave, lane, 0};
   p.template start<true, V>();
 
   for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const int idx = tile * TR + wave * 16 + pl;
-    const bool valid = idx < n && !(PM && wave == 7);
+    const int idx = tile * 128 + wave * 16 + pl;
+    const bool valid = idx < n;
     const size_t row = (size_t)(valid ? idx : n - 1);
     float emb[16], vemb[8];
 #pragma unroll

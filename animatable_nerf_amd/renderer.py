@@ -237,22 +237,38 @@ class Renderer:
         R = batch['ray_o'].shape[1]
         chunk = int(self.cfg.get('chunk', CHUNK))
         n_chunks = (R + chunk - 1) // chunk
-        parts = int(os.environ.get('ANR_HOST_PARTS', self.HOST_PARTS))
+        # at least two chunks per part; fewer than two parts: one device render and one copy
+        parts = min(int(os.environ.get('ANR_HOST_PARTS', self.HOST_PARTS)), n_chunks // 2)
         with torch.no_grad():
-            if n_chunks < 2 * parts or not self.device().type == 'cuda':
+            if parts < 2 or not self.device().type == 'cuda':
                 return to_host(self.render_device(batch))
             return self._render_overlapped(batch, R, chunk, parts)
 
+    def _render_launch(self, batch, attr):
+        """anr_render_fwd of one part on the current stream into workspace `attr`, no host read."""
+        p = self.params()
+        dev = self._packed.device
+        R = batch['ray_o'].shape[1]
+        c = _Call(self, batch, self._t_rand(R, dev, None))
+        ws_bytes = self.lib.anr_render_workspace_bytes(R, ctypes.byref(c.opts), ctypes.byref(c.frame))
+        ws = self._workspace(attr, ws_bytes, dev)
+        c.opts.precision = c.render_precision
+        _lib.check(self.lib.anr_render_fwd(ctypes.byref(p), ctypes.byref(c.frame), *c.ray_ptrs(), R,
+                                           ctypes.byref(c.opts), ctypes.byref(c.out), _lib.ptr(ws), ws_bytes,
+                                           _lib.stream_ptr(dev)), 'anr_render_fwd')
+        return c, ws, R
+
     def _render_overlapped(self, batch, R, chunk, parts):
-        """render_device over parts of whole chunks (per-chunk semantics unchanged: the rows of the parts,
-        concatenated in order, are the whole frame's, as parallel.render_sharded relies on), each part's
-        outputs copied on a side stream into page-locked host buffers while the next part renders.
-        The alpha_ind rows (pbw / tbw) are counted only as each part finishes: they go, as each part
-        finishes, to their final offset in one (1, cap, 24) page-locked buffer sized from the previous
-        frame's row count with ROWS_HEADROOM (the first frame: from the rows seen so far), and the
-        returned (1, m, 24) tensors are its first m rows (contiguous; no capacity-sized host buffer,
-        no host concatenation). A frame whose rows outgrow the buffer moves the placed rows into an
-        exact-size one (one host copy) and the rest from the device."""
+        """The frame in parts of whole chunks (per-chunk semantics unchanged: the rows of the parts,
+        concatenated in order, are the whole frame's, as parallel.render_sharded relies on), pipelined:
+        part k + 1 is issued (on the other of two workspaces) before part k's row count is read, so the
+        GPU renders back to back while the host reads counts; part k's alpha_ind rows are extracted and
+        every output of it copied into page-locked host buffers on a side stream. The alpha_ind rows go
+        to their final offset in one (1, cap, 24) page-locked buffer sized from the previous frame's row
+        count with ROWS_HEADROOM (the first frame: from the rows seen so far), and the returned (1, m, 24)
+        tensors are its first m rows (contiguous; no capacity-sized host buffer, no host concatenation).
+        A frame whose rows outgrow the buffer moves the placed rows into an exact-size one (one host
+        copy) and the rest from the device."""
         from .parallel import RAY_KEYS as SLICED, shard_chunks
         dev = self.device()
         ns = int(self.cfg.N_samples)
@@ -264,40 +280,65 @@ class Renderer:
             pin = dict(dtype=torch.float32, pin_memory=True)
             h = {'rgb_map': torch.empty((1, R, 3), **pin), 'acc_map': torch.empty((1, R), **pin),
                  'depth_map': torch.empty((1, R), **pin), 'raw': torch.empty((1, R * ns, 4), **pin)}
-            keep, late, kept, off = [], [], 0, 0
-            hp = ht = None
+            st = dict(late=[], kept=0, off=0, hp=None, ht=None, keep=[], k=0)
             est = int(getattr(self, '_rows_est', 0))
+            ws_free = [None, None]  # per workspace: an event on cs after its last part's rows were extracted
+
+            def finish(part):
+                a, b, c, ws, Rp, launched, slot = part
+                with torch.cuda.stream(cs):
+                    cs.wait_event(launched)  # this part only (the next one is queued behind it on cur)
+                    addr = self.lib.anr_render_counts(_lib.ptr(ws), Rp)
+                    cnt = ws[addr - ws.data_ptr():addr - ws.data_ptr() + 8].view(torch.int32).cpu()  # host read
+                    kept_k, n = int(cnt[0]), int(cnt[1])
+                    pr = torch.empty((1, n, 24), device=dev)
+                    tr = torch.empty((1, n, 24), device=dev)
+                    if n:
+                        _lib.check(self.lib.anr_render_bw_rows(_lib.ptr(ws), Rp, _lib.ptr(pr), _lib.ptr(tr),
+                                                               _lib.stream_ptr(dev)), 'anr_render_bw_rows')
+                    ev = torch.cuda.Event()
+                    ev.record(cs)
+                    ws_free[slot] = ev
+                    if st['hp'] is None and (est > 0 or n > 0):
+                        # the previous frame's rows, or (first frame) the rows per part so far, extrapolated
+                        guess = est if est > 0 else (st['off'] + n) * parts // (st['k'] + 1)
+                        cap = int(guess * self.ROWS_HEADROOM) + 64
+                        st['hp'] = torch.empty((1, cap, 24), **pin)
+                        st['ht'] = torch.empty((1, cap, 24), **pin)
+                    h['rgb_map'][:, a:b].copy_(c.rgb, non_blocking=True)
+                    h['acc_map'][:, a:b].copy_(c.acc, non_blocking=True)
+                    h['depth_map'][:, a:b].copy_(c.depth, non_blocking=True)
+                    h['raw'][:, a * ns:b * ns].copy_(c.raw, non_blocking=True)
+                    off, hp, ht = st['off'], st['hp'], st['ht']
+                    if n and hp is not None and off + n <= hp.shape[1] and not st['late']:
+                        hp[:, off:off + n].copy_(pr, non_blocking=True)
+                        ht[:, off:off + n].copy_(tr, non_blocking=True)
+                    elif n:
+                        st['late'].append((off, pr, tr))
+                st['keep'].append((c, pr, tr))  # device tensors alive until the copies are done
+                st['off'] += n
+                st['kept'] += kept_k
+                st['k'] += 1
+
+            pending = None
             for k in range(parts):
                 a, b = shard_chunks(R, k, parts, chunk)
                 if a >= b:
                     continue
+                slot = k % 2
+                if ws_free[slot] is not None:
+                    cur.wait_event(ws_free[slot])  # the workspace's previous part has its rows out
                 sub = {key_: (v[:, a:b] if key_ in SLICED and torch.is_tensor(v) else v) for key_, v in batch.items()}
-                out = self.render_device(sub)  # reads the part's row count: the part has finished when it returns
-                p, t = out['pbw'], out['tbw']
-                n = p.shape[1]
-                if hp is None and (est > 0 or n > 0):
-                    # the previous frame's rows, or (first frame) this part's rows per part so far, extrapolated
-                    guess = est if est > 0 else (off + n) * parts // (k + 1)
-                    cap = int(guess * self.ROWS_HEADROOM) + 64
-                    hp = torch.empty((1, cap, 24), **pin)
-                    ht = torch.empty((1, cap, 24), **pin)
-                ev = torch.cuda.Event()
-                ev.record(cur)
-                with torch.cuda.stream(cs):
-                    cs.wait_event(ev)
-                    h['rgb_map'][:, a:b].copy_(out['rgb_map'], non_blocking=True)
-                    h['acc_map'][:, a:b].copy_(out['acc_map'], non_blocking=True)
-                    h['depth_map'][:, a:b].copy_(out['depth_map'], non_blocking=True)
-                    h['raw'][:, a * ns:b * ns].copy_(out['raw'], non_blocking=True)
-                    if n and hp is not None and off + n <= hp.shape[1] and not late:
-                        hp[:, off:off + n].copy_(p, non_blocking=True)
-                        ht[:, off:off + n].copy_(t, non_blocking=True)
-                    elif n:
-                        late.append((off, p, t))
-                keep.append(out)  # device outputs stay alive until their copies are done
-                off += n
-                kept += self.last_counts[0]
-            m = off
+                c, ws, Rp = self._render_launch(sub, '_ws' if slot == 0 else '_ws_b')
+                launched = torch.cuda.Event()
+                launched.record(cur)
+                if pending is not None:
+                    finish(pending)
+                pending = (a, b, c, ws, Rp, launched, slot)
+            if pending is not None:
+                finish(pending)
+            m = st['off']
+            late, hp, ht = st['late'], st['hp'], st['ht']
             if late or hp is None:
                 # outgrew the estimate: the placed rows into exact-size buffers, the rest from the device
                 cs.synchronize()
@@ -313,10 +354,11 @@ class Renderer:
                         et[:, o:o + t.shape[1]].copy_(t, non_blocking=True)
                 hp, ht = ep, et
             cs.synchronize()
+            cur.wait_stream(cs)  # later work on the caller's stream may reuse the workspaces
             h['pbw'] = hp[:, :m]
             h['tbw'] = ht[:, :m]
         self._rows_est = m
-        self.last_counts = (kept, m)
+        self.last_counts = (st['kept'], m)
         return h
 
     def counts(self, n_rays):
