@@ -890,6 +890,147 @@ __global__ void k_wgrad_reduce_group(WGradGroup G) {
   wgrad_reduce_at(G.d[k], (b - G.rstart[k]) * blockDim.x + threadIdx.x);
 }
 
+// ------------------------------------------------------------------------------------------
+// k_wgrad_dma: the bf16 x bf16 weight gradients of a group (the bulk of the bf16 training backward),
+// one workgroup per (product, sample range) owning the whole <= 256 x 256 dW: 8 waves of 64 outputs x
+// 128 inputs (4 x 8 MFMA blocks, 128 accumulator registers). dY and X rows stream through a 4-slot LDS
+// ring of 32-sample stages by LDS-DMA (global_load_lds_dwordx4; no staging registers, 3 stages in
+// flight, counted vmcnt waits — the loop stores nothing), each image [sample][256 columns] with its
+// 16-B chunks XOR-swizzled per row so the ds_read_b64_tr_b16 fragment reads are conflict-free
+// (rows 8g + q of a 32-lane half land in 16 distinct chunk positions). The column sums of dY (bias /
+// latent-row gradients) are one more MFMA per out-block against a ones fragment. Partial tiles go to
+// k_wgrad_group's slab layout (its 128 x 128 tiles, 64 x 64 quadrants), so k_wgrad_reduce_group sums
+// them unchanged. The register-staged k_wgrad_group kept 128 registers of prefetch for 4 steps and ran
+// the groups at ~150 TFLOP/s (profiles/r6a, r6b).
+// ------------------------------------------------------------------------------------------
+#define WD_ST 32                 // samples per stage
+#define WD_NB 4                  // ring slots
+#define WD_IMG (WD_ST * 512)     // one image: 32 rows x 256 bf16
+#define WD_SLOT (2 * WD_IMG)     // dY image, X image
+
+__device__ __forceinline__ int wd_swz(int r) { return 2 * ((r & 3) | (((r >> 3) & 1) << 2)); }
+
+// fragment (16 columns c0 .. c0 + 15 of the image, rows 0..31 as k): lane i gets column c0 + (i & 15),
+// rows 8 (i >> 4) + 0..7 (wg_frag's tr16 pattern on the swizzled image)
+__device__ __forceinline__ bf16x8_t wd_frag(const unsigned char* img, int c0, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  typedef __attribute__((address_space(3))) wv4s lds_v4s;
+  const int c = c0 + 4 * p;
+  const int r0 = 8 * g + q, r1 = r0 + 4;
+  const unsigned a0 = (unsigned)(uintptr_t)(img + r0 * 512 + (((c >> 3) ^ wd_swz(r0)) << 4) + (c & 7) * 2);
+  const unsigned a1 = (unsigned)(uintptr_t)(img + r1 * 512 + (((c >> 3) ^ wd_swz(r1)) << 4) + (c & 7) * 2);
+  const wv4s x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(uintptr_t)a0);
+  const wv4s x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(uintptr_t)a1);
+  bf16x8_t f;
+  const short e[8] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+  __builtin_memcpy(&f, e, 16);
+  return f;
+}
+
+template <int N>
+__device__ __forceinline__ void wd_wait() {
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+
+__global__ __launch_bounds__(512) void k_wgrad_dma(WGradGroup G) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int b = blockIdx.x;
+  int k = 0;
+  while (k + 1 < G.n && b >= G.start[k + 1]) ++k;
+  const WGrad& g = G.d[k];
+  const int z = b - G.start[k];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int n = g.M_dev ? *g.M_dev : g.n;
+  const int spb = g.spb ? g.spb : ((n + g.nz - 1) / g.nz + 2 * WG_S - 1) / (2 * WG_S) * (2 * WG_S);
+  const int s0 = z * spb, s1 = min(n, s0 + spb);
+  const int nst = s1 > s0 ? (s1 - s0 + WD_ST - 1) / WD_ST : 0;
+  const int i0 = (wave & 3) * 64, j0 = (wave >> 2) * 128;
+  const bool rs = g.rs_slab != nullptr && j0 == 0;
+  const unsigned short* Y = (const unsigned short*)g.dY;
+  const unsigned short* X = (const unsigned short*)g.X;
+  // this wave's 4 pieces of a stage: images 0 (dY) / 1 (X), pieces 2 wave, 2 wave + 1 (rows 4 wave ..
+  // 4 wave + 3); lane: row 2 piece + (lane >> 5), physical chunk lane & 31
+  auto issue = [&](int st) {
+    const unsigned char* slot = smem + (st % WD_NB) * WD_SLOT;
+#pragma unroll
+    for (int im = 0; im < 2; ++im) {
+      const unsigned short* base = im ? X : Y;
+      const long ld = im ? g.ldX : g.ldY;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int piece = 2 * wave + h;
+        const int r = 2 * piece + (lane >> 5);
+        int c = (lane & 31) ^ wd_swz(r);
+        c = 8 * c + 8 <= ld ? c : 0;                          // chunks past the row: any in-bounds bytes
+        const int srow = min(s0 + st * WD_ST + r, s1 - 1);   // rows past the range: zeroed in LDS
+        const unsigned short* src = base + (size_t)srow * ld + 8 * c;
+        const unsigned m0 = (unsigned)(uintptr_t)(slot + im * WD_IMG + piece * 1024);
+        asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(m0) : "memory");
+      }
+    }
+  };
+  f32x4 acc[4][8], rsum[4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    rsum[a] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < 8; ++c) acc[a][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  bf16x8_t ones;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ones[j] = (__bf16)1.0f;
+  for (int st = 0; st < WD_NB - 1 && st < nst; ++st) issue(st);
+  for (int st = 0; st < nst; ++st) {
+    // certify stage st: this wave's pieces of the stages after it may stay in flight, then the barrier
+    const int after = min(st + WD_NB - 2, nst - 1) - st;
+    if (after >= 2) wd_wait<8>();
+    else if (after == 1) wd_wait<4>();
+    else wd_wait<0>();
+    __syncthreads();
+    unsigned char* slot = smem + (st % WD_NB) * WD_SLOT;
+    const int vr = s1 - (s0 + st * WD_ST);  // valid rows of this stage
+    if (vr < WD_ST) {  // the range's last stage: rows past it read as zero (uniform branch)
+      for (int e = tid; e < 2 * (WD_ST - vr) * 32; e += 512) {
+        const int im = e / ((WD_ST - vr) * 32), rem = e % ((WD_ST - vr) * 32);
+        *(uint4*)(slot + im * WD_IMG + (vr + rem / 32) * 512 + (rem % 32) * 16) = make_uint4(0u, 0u, 0u, 0u);
+      }
+      __syncthreads();
+    }
+    if (st + WD_NB - 1 < nst) issue(st + WD_NB - 1);  // the slot of stage st - 1: every wave is past it
+    bf16x8_t fa[4], fb[8];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) fa[a] = wd_frag(slot, i0 + 16 * a, lane);
+#pragma unroll
+    for (int c = 0; c < 8; ++c) fb[c] = wd_frag(slot + WD_IMG, j0 + 16 * c, lane);
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+#pragma unroll
+      for (int c = 0; c < 8; ++c) acc[a][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a], fb[c], acc[a][c], 0, 0, 0);
+      if (rs) rsum[a] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a], ones, rsum[a], 0, 0, 0);
+    }
+  }
+  // partial tiles in k_wgrad_group's slab layout: 128 x 128 tile (ti, tj), quadrant w' = 2 wr + wc
+  const int nti = (g.nout + WG_T - 1) / WG_T;
+  const int ti = i0 / WG_T, wr = (i0 % WG_T) / 64;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const int jc = j0 + 64 * (c / 4);
+    const int tj = jc / WG_T, wc = (jc % WG_T) / 64;
+    if (ti >= nti || tj >= g.tj) continue;
+    const int t = ti * g.tj + tj;
+    float* slab = g.slab + ((long)(z * g.tiles + t) * 4 + (2 * wr + wc)) * 16 * 256;
+#pragma unroll
+    for (int a = 0; a < 4; ++a) *(f32x4*)(slab + (a * 4 + (c % 4)) * 256 + lane * 4) = acc[a][c];
+  }
+  if (rs && (lane & 15) == 0) {
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) g.rs_slab[(long)z * 256 + i0 + 16 * a + 4 * (lane >> 4) + r] = rsum[a][r];
+  }
+}
+
 static int wgrad_reduce_blocks(const WGrad& g) {
   const int nred = g.tiles * 4 * 16 * 64 * ((g.nz + WG_ZG - 1) / WG_ZG);
   return ((nred > 256 ? nred : 256) + 255) / 256;
@@ -921,6 +1062,12 @@ int launch_wgrad(WGrad g, int n_host, hipStream_t s) {
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// ANR_WG_DMA (read per call, default 0 until measured): the bf16 x bf16 products of a group on k_wgrad_dma
+static bool wgrad_dma_on() {
+  const char* v = getenv("ANR_WG_DMA");
+  return v && v[0] == '1';
+}
+
 int launch_wgrad_group(const WGrad* d, int nd, int n_host, int nz, float* slab, size_t slab_floats, hipStream_t s) {
   if (n_host <= 0 || nd <= 0) return 0;
   nz = nz < 8 ? 8 : (nz > WG_MAX_Z ? WG_MAX_Z : (nz + 7) / 8 * 8);
@@ -939,6 +1086,18 @@ int launch_wgrad_group(const WGrad* d, int nd, int n_host, int nz, float* slab, 
         }
       if (!H.n) continue;
       const dim3 grid(H.start[H.n]);
+      if (v == 1 && wgrad_dma_on()) {
+        // one workgroup per (product, sample range): the whole <= 256 x 256 dW of the range
+        WGradGroup D = H;
+        for (int q = 0; q < H.n; ++q) D.start[q + 1] = D.start[q] + H.d[q].nz;
+        static bool attr = false;
+        if (!attr) {
+          (void)hipFuncSetAttribute((const void*)k_wgrad_dma, hipFuncAttributeMaxDynamicSharedMemorySize, WD_NB * WD_SLOT);
+          attr = true;
+        }
+        hipLaunchKernelGGL(k_wgrad_dma, dim3(D.start[D.n]), dim3(512), WD_NB * WD_SLOT, s, D);
+        continue;
+      }
       if (v == 0) hipLaunchKernelGGL((k_wgrad_group<true, false, false>), grid, dim3(256), 0, s, H);
       else if (v == 1) hipLaunchKernelGGL((k_wgrad_group<false, true, true>), grid, dim3(256), 0, s, H);
       else if (v == 2) hipLaunchKernelGGL((k_wgrad_group<false, true, false>), grid, dim3(256), 0, s, H);
