@@ -143,16 +143,6 @@ template <int P>
 __host__ __device__ constexpr int tc_nb() { return tc_bwd<P>() ? TC_NB_BWD : P == 0 ? TC_NB_BW : TC_NB_NF; }
 // mask slots (backward): the 128 x 256-bit ReLU mask of a layer's outputs for the tile (4 KiB)
 constexpr int TC_MS = 4;
-// timing experiments on the input-gradient programs only (tools/build_ab.sh; results are NOT gradients):
-// 1 no MFMA, 2 no weight / mask DMA (zeroed ring), 3 no vmcnt waits
-#ifndef TC_EXP_BWD
-#define TC_EXP_BWD 0
-#endif
-// probe-only timing experiments on every program: 4 no row stores, 5 the rows of every tile stored over
-// the first tile's (L2-resident)
-#ifndef TC_EXP
-#define TC_EXP 0
-#endif
 // bias table: per layer ob x 16 floats (forward programs)
 template <int P>
 __host__ __device__ constexpr int tc_bias_off(int l) {
@@ -320,7 +310,7 @@ struct TcRing {
   // slice of a masked layer the 4 KiB of the layer's mask bits for this tile's rows (+ 16 rows past)
   template <int P, int Q>
   __device__ __forceinline__ void issue() {
-    if constexpr (Q < tc_nslices<P>() && !(tc_bwd<P>() && TC_EXP_BWD == 2)) {
+    if constexpr (Q < tc_nslices<P>()) {
       constexpr int ob = tc_layer<P>(tc_layer_of<P>(Q)).ob;
       constexpr int kb = tc_slice_kb<P>(Q);
       const unsigned dst = (unsigned)(uintptr_t)(lds + (Q % tc_nb<P>()) * tc_obmax<P>() * 1024);
@@ -360,8 +350,7 @@ struct TcRing {
       for (int x = Q + 1; x <= issued; ++x) n += tc_ops<P>(x);
       return n < 63 ? n : 63;
     }();
-    if constexpr (!(tc_bwd<P>() && TC_EXP_BWD == 3))
-      if (producer) tc_wait_vmcnt<after>();
+    if (producer) tc_wait_vmcnt<after>();
     __syncthreads();
   }
   template <int P, int Q>
@@ -392,10 +381,6 @@ __device__ __forceinline__ void tc_body(const TcArgs& a) {
         sb[tc_bias_off<P>(l) + i] = v;
       }
     });
-  }
-  if constexpr (tc_bwd<P>() && TC_EXP_BWD == 2) {
-    for (int i = tid; i < (tc_lds_bytes<P>() - tc_ring_off<P>()) / 4; i += 512) ((uint32_t*)ring)[i] = 0u;
-    __syncthreads();
   }
   const int M = *a.M_dev;
   const int ntiles = (M + TC_TR - 1) / TC_TR;
@@ -471,8 +456,7 @@ __device__ __forceinline__ void tc_body(const TcArgs& a) {
           constexpr int o = decltype(oc)::value;
           if constexpr (o + PF < L.ob) fa[(o + PF) % (PF + 1)] = *(const tc_bf16x8*)(buf + (o + PF) * 1024 + lane * 16);
           __builtin_amdgcn_sched_barrier(0);
-          if constexpr (!(tc_bwd<P>() && TC_EXP_BWD == 1))
-            acc[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[o % (PF + 1)], b, acc[o], 0, 0, 0);
+          acc[o] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[o % (PF + 1)], b, acc[o], 0, 0, 0);
           __builtin_amdgcn_sched_barrier(0);
           // halfway through the slice: certify the next slice, refill the slot of the previous one
           if constexpr (o == (L.ob - 1) / 2) {
@@ -499,11 +483,11 @@ __device__ __forceinline__ void tc_body(const TcArgs& a) {
           // the mask bits of the stored rows for the backward chains (bf16 value > 0, the layer-wise
           // backward's test of the bf16 row)
           if constexpr (!tc_bwd<P>()) {
-            if (a.bits[l] && valid && (TC_EXP != 4 || a.nout[0] == -7)) {
+            if (a.bits[l] && valid) {
               uint32_t t[32];
 #pragma unroll
               for (int i = 0; i < 32; ++i) t[i] = tc_nz01(wd[i]);
-              *(uint2*)((unsigned char*)a.bits[l] + ((size_t)(TC_EXP == 5 ? (row & 127) : row) * 4 + h) * 8) = make_uint2(tc_tree(t), tc_tree(t + 16));
+              *(uint2*)((unsigned char*)a.bits[l] + ((size_t)row * 4 + h) * 8) = make_uint2(tc_tree(t), tc_tree(t + 16));
             }
           }
         }
@@ -512,16 +496,16 @@ __device__ __forceinline__ void tc_body(const TcArgs& a) {
 #pragma unroll
           for (int i = 0; i < 32; ++i) wd[i] &= tc_expand((i < 16 ? F.x : F.y) >> (i & 15));
         }
-        unsigned short* orow = (unsigned short*)a.out[l] + (size_t)(TC_EXP == 5 ? (row & 127) : row) * a.ldo[l];
+        unsigned short* orow = (unsigned short*)a.out[l] + (size_t)row * a.ldo[l];
         tc_for<0, 8>([&](auto sc) {
           constexpr int s = decltype(sc)::value;
-          if (valid && (TC_EXP != 4 || a.nout[0] == -7)) {
+          if (valid) {
             *(uint4*)(orow + 32 * s + 8 * h) = make_uint4(wd[4 * s], wd[4 * s + 1], wd[4 * s + 2], wd[4 * s + 3]);
           }
           bprev[s] = __builtin_bit_cast(tc_bf16x8, make_uint4(wd[4 * s], wd[4 * s + 1], wd[4 * s + 2], wd[4 * s + 3]));
         });
         if constexpr (L.out == TC_FA) {
-          if (valid && (TC_EXP != 4 || a.nout[0] == -7) && h == 0) a.out2[row] = acc[16][0];  // alpha_fc (row 256 of the stacked layer)
+          if (valid && h == 0) a.out2[row] = acc[16][0];  // alpha_fc (row 256 of the stacked layer)
         }
       } else if constexpr (L.out == TC_F32) {
         // fp32 rows (heads; view_fc's ReLU rows; d view): ReLU / mask in fp32, mask bits from the fp32
@@ -534,7 +518,7 @@ __device__ __forceinline__ void tc_body(const TcArgs& a) {
             for (int r = 0; r < 4; ++r) acc[o][r] = fmaxf(acc[o][r], 0.0f);
           });
           if constexpr (!tc_bwd<P>()) {
-            if (a.bits[l] && valid && (TC_EXP != 4 || a.nout[0] == -7)) {
+            if (a.bits[l] && valid) {
               uint32_t t[32] = {};
               tc_for<0, L.ob>([&](auto oc) {
                 constexpr int o = decltype(oc)::value;
@@ -542,7 +526,7 @@ __device__ __forceinline__ void tc_body(const TcArgs& a) {
                 t[i0] = (acc[o][0] > 0.f ? 1u : 0u) | (acc[o][1] > 0.f ? 0x10000u : 0u);
                 t[i0 + 1] = (acc[o][2] > 0.f ? 1u : 0u) | (acc[o][3] > 0.f ? 0x10000u : 0u);
               });
-              *(uint2*)((unsigned char*)a.bits[l] + ((size_t)(TC_EXP == 5 ? (row & 127) : row) * 4 + h) * 8) =
+              *(uint2*)((unsigned char*)a.bits[l] + ((size_t)row * 4 + h) * 8) =
                   make_uint2(tc_tree(t), NW > 16 ? tc_tree(t + 16) : 0u);
             }
           }
@@ -559,12 +543,12 @@ __device__ __forceinline__ void tc_body(const TcArgs& a) {
             }
           });
         }
-        float* orow = (float*)a.out[l] + (size_t)(TC_EXP == 5 ? (row & 127) : row) * a.ldo[l];
+        float* orow = (float*)a.out[l] + (size_t)row * a.ldo[l];
         const int nout = a.nout[l];
         tc_for<0, L.ob>([&](auto oc) {
           constexpr int o = decltype(oc)::value;
           const int c = 32 * (o >> 1) + 8 * h + 4 * (o & 1);
-          if (valid && (TC_EXP != 4 || a.nout[0] == -7)) {
+          if (valid) {
             if (c + 4 <= nout) {
               *(f32x4*)(orow + c) = acc[o];
             } else {
@@ -587,7 +571,7 @@ __device__ __forceinline__ void tc_body(const TcArgs& a) {
       if constexpr (L.out == TC_SPLIT || L.out == TC_AUX) {
         // the gamma gradient (fp32 rows, aux_cols columns at ld_aux): out-blocks past the hidden part
         constexpr int O0 = L.out == TC_SPLIT ? 16 : 0;
-        if (a.aux && valid && (TC_EXP != 4 || a.nout[0] == -7)) {
+        if (a.aux && valid) {
           float* arow = a.aux + (size_t)row * a.ld_aux;
           tc_for<O0, L.ob>([&](auto oc) {
             constexpr int o = decltype(oc)::value;
