@@ -29,7 +29,7 @@ EXPORTS = ('anr_near_far', 'anr_params_packed_bytes', 'anr_params_pack', 'anr_re
            'anr_network_workspace_bytes', 'anr_network_fwd', 'anr_network_counts', 'anr_network_bw_rows',
            'anr_network_train_workspace_bytes', 'anr_network_train_fwd', 'anr_network_train_bwd',
            'anr_points_workspace_bytes', 'anr_blend_weights', 'anr_canonical_alpha', 'anr_train_step_hooked',
-           'anr_sdf_train_workspace_bytes', 'anr_sdf_train_step', 'anr_sdf_render_knn',
+           'anr_sdf_train_workspace_bytes', 'anr_sdf_train_step', 'anr_sdf_train_step_hooked', 'anr_sdf_render_knn',
            'anr_sdf_network_workspace_bytes', 'anr_sdf_network_fwd', 'anr_sdf_network_counts', 'anr_sdf_network_rows',
            'anr_sdf_network_train_workspace_bytes', 'anr_sdf_network_train_fwd', 'anr_sdf_network_train_counts',
            'anr_sdf_network_train_rows', 'anr_sdf_network_train_bwd', 'anr_sdf_points_workspace_bytes', 'anr_sdf_points',
@@ -84,6 +84,18 @@ class TrainHooks(ctypes.Structure):
 
     def __init__(self, *args, **kw):
         super().__init__(ctypes.sizeof(TrainHooks), *args, **kw)
+
+
+READY_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p)
+
+
+class SdfTrainHooks(ctypes.Structure):
+    """anr_sdf_train_hooks: struct_size is filled in by the constructor."""
+    _fields_ = [('struct_size', ctypes.c_size_t), ('colour_grads_ready', ctypes.c_void_p), ('colour_ready', READY_FN),
+                ('user', ctypes.c_void_p)]
+
+    def __init__(self, *args, **kw):
+        super().__init__(ctypes.sizeof(SdfTrainHooks), *args, **kw)
 
 
 class AlphaOpts(ctypes.Structure):
@@ -160,6 +172,11 @@ def load():
     lib.anr_sdf_train_step.argtypes = [ctypes.POINTER(SdfParams), ctypes.c_void_p * NUM_SDF_TENSORS,
                                        ctypes.POINTER(SdfFrame), P, P, P, P, ctypes.c_int, ctypes.POINTER(RenderOpts),
                                        P, P, ctypes.c_int, ctypes.POINTER(SdfRenderOut), P, P, ctypes.c_size_t, P]
+    lib.anr_sdf_train_step_hooked.argtypes = [ctypes.POINTER(SdfParams), ctypes.c_void_p * NUM_SDF_TENSORS,
+                                              ctypes.POINTER(SdfFrame), P, P, P, P, ctypes.c_int,
+                                              ctypes.POINTER(RenderOpts), P, P, ctypes.c_int,
+                                              ctypes.POINTER(SdfRenderOut), P, ctypes.POINTER(SdfTrainHooks), P,
+                                              ctypes.c_size_t, P]
     SP, SF, SS = ctypes.POINTER(SdfParams), ctypes.POINTER(SdfFrame), ctypes.POINTER(Samples)
     lib.anr_sdf_network_workspace_bytes.restype = ctypes.c_size_t
     lib.anr_sdf_network_workspace_bytes.argtypes = [ctypes.c_int, ctypes.POINTER(RenderOpts)]

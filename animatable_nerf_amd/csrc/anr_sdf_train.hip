@@ -715,6 +715,7 @@ struct TrainCore {
   const float *d_raw, *d_sdf, *d_resd, *d_grad, *d_og;  // NET_BWD (any NULL = 0)
   int pts_mode;                      // PTS: ANR_SDFP_NETWORK / _GRADIENT / _DEFORMED_GRADIENT
   float *pts_out, *pts_out2;         // PTS outputs
+  const anr_sdf_train_hooks* hooks;  // STEP: the colour net's gradients final (anr_sdf_train_step_hooked), or NULL
   void* ws;
   size_t ws_bytes;
   hipStream_t s;
@@ -1089,6 +1090,7 @@ int sdf_train_core(const TrainCore& C) {
     }
   }
 
+  bool colour_wn = false;  // the colour net's weight-norm gradients converted (after its backward)
   if (n > 0 && !net_fwd) {
     // ---- backward: raw -> colour logits, sdf, beta; msk_sdf -> sdf
     StRaw sr{};
@@ -1123,6 +1125,22 @@ int sdf_train_core(const TrainCore& C) {
     ANR_TRY(g.wgrad(n, dWN(9), 289, 33, 256, dHb, 256, F(L.Y8) + 1, 264, 256));
     ANR_TRY(g.xgrad(n, F(L.dC0), 40, 33, dHb, 256, 256, WN(9), 289, 0));
     ANR_TRY(g.xgrad(n, F(L.dZ8) + 1, 264, 256, dHb, 256, 256, WN(9), 289, 33));
+    // the colour net's weight-norm gradients now (nothing after this point reaches tensors 28..43: the
+    // SDF, residual and observed passes below touch the SDF and residual weights only), so the caller can
+    // all-reduce them while the rest of the backward runs (anr_sdf_train_step_hooked)
+    for (int l = 9; l < SDF_NUM_WN; ++l) {
+      const WnLayer d = wn_layer(l);
+      hipLaunchKernelGGL(k_st_wn_grad, dim3(d.out), dim3(256), 0, s, tp[d.v], tp[d.g], (const float*)dWN(l), d.in,
+                         grads[d.g], grads[d.v]);
+    }
+    ANR_TRY(check_launch("k_st_wn_grad (colour)"));
+    colour_wn = true;
+    if (C.hooks) {
+      hipEvent_t ev = (hipEvent_t)C.hooks->colour_grads_ready;
+      if (ev && hipEventRecord(ev, s) != hipSuccess) return fail(ANR_E_HIP, "colour event record");
+      if (C.hooks->colour_ready && C.hooks->colour_ready(C.hooks->user, (void*)ev, (void*)s) != 0)
+        return fail(ANR_E_ARG, "anr_sdf_train_hooks.colour_ready failed");
+    }
     // ---- loss adjoints of resd (offset) and gradients (eikonal + colour normals); d sdf into Z8 col 0
     if (step) {
       StLoss sl{};
@@ -1294,7 +1312,7 @@ int sdf_train_core(const TrainCore& C) {
   if (net_fwd) return ANR_OK;
   // ---- weight norm: effective-weight gradients -> weight_g / weight_v; beta; loss vector
   if (n > 0) {
-    for (int l = 0; l < SDF_NUM_WN; ++l) {
+    for (int l = 0; l < (colour_wn ? 9 : SDF_NUM_WN); ++l) {
       const WnLayer d = wn_layer(l);
       hipLaunchKernelGGL(k_st_wn_grad, dim3(d.out), dim3(256), 0, s, tp[d.v], tp[d.g], (const float*)dWN(l), d.in,
                          grads[d.g], grads[d.v]);
@@ -1348,6 +1366,23 @@ int anr_sdf_train_step(const anr_sdf_params* p, float* const* grads, const anr_s
   c.mode = STEP; c.p = p; c.grads = grads; c.f = f;
   c.ray_o = ray_o; c.ray_d = ray_d; c.near_ = near_; c.far_ = far_; c.R = R; c.chunk = o->chunk; c.o = o;
   c.rgb_gt = rgb_gt; c.mask_at_box = mask_at_box; c.iter_step = iter_step; c.out = out; c.loss = loss;
+  c.ws = workspace; c.ws_bytes = ws_bytes; c.s = (hipStream_t)stream;
+  return sdf_train_core(c);
+}
+
+int anr_sdf_train_step_hooked(const anr_sdf_params* p, float* const* grads, const anr_sdf_frame* f, const float* ray_o,
+                              const float* ray_d, const float* near_, const float* far_, int R, const anr_render_opts* o,
+                              const float* rgb_gt, const uint8_t* mask_at_box, int iter_step,
+                              const anr_sdf_render_out* out, float* loss, const anr_sdf_train_hooks* hooks,
+                              void* workspace, size_t ws_bytes, void* stream) {
+  ANR_TRY(check_train(p, grads, f, ray_o, ray_d, near_, far_, R, o, rgb_gt, out, loss, workspace));
+  if (hooks && hooks->struct_size != sizeof(anr_sdf_train_hooks))
+    return fail(ANR_E_ARG, "anr_sdf_train_step_hooked: hooks->struct_size != sizeof(anr_sdf_train_hooks)");
+  TrainCore c{};
+  c.mode = STEP; c.p = p; c.grads = grads; c.f = f;
+  c.ray_o = ray_o; c.ray_d = ray_d; c.near_ = near_; c.far_ = far_; c.R = R; c.chunk = o->chunk; c.o = o;
+  c.rgb_gt = rgb_gt; c.mask_at_box = mask_at_box; c.iter_step = iter_step; c.out = out; c.loss = loss;
+  c.hooks = hooks;
   c.ws = workspace; c.ws_bytes = ws_bytes; c.s = (hipStream_t)stream;
   return sdf_train_core(c);
 }

@@ -1062,10 +1062,18 @@ int launch_wgrad(WGrad g, int n_host, hipStream_t s) {
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-// ANR_WG_DMA (read per call, default 0 until measured): the bf16 x bf16 products of a group on k_wgrad_dma
+// ANR_WG_DMA (read per call, default 1): the bf16 x bf16 products of a group on k_wgrad_dma. Measured
+// (tools/gemm_probe grouptime, 16 products of 256 x 256 at 24,893 rows, 16 sample ranges): 111 us per
+// group vs 188 us for k_wgrad_group, identical sums; bf16_all step 1.160 -> 1.064 ms (profiles/r7a)
 static bool wgrad_dma_on() {
   const char* v = getenv("ANR_WG_DMA");
-  return v && v[0] == '1';
+  return !(v && v[0] == '0');
+}
+// what k_wgrad_dma assumes of a product: one workgroup covers <= 256 x 256 outputs, rows of >= 8 bf16
+// (chunk 0 stands in for the chunks past a row) in 16-B aligned rows (global_load_lds_dwordx4)
+static bool wgrad_dma_fits(const WGrad& g) {
+  return g.nout <= 256 && g.K <= 256 && g.ldY >= 8 && g.ldX >= 8 && g.ldY % 8 == 0 && g.ldX % 8 == 0 &&
+         ((uintptr_t)g.dY & 15) == 0 && ((uintptr_t)g.X & 15) == 0;
 }
 
 int launch_wgrad_group(const WGrad* d, int nd, int n_host, int nz, float* slab, size_t slab_floats, hipStream_t s) {
@@ -1073,10 +1081,15 @@ int launch_wgrad_group(const WGrad* d, int nd, int n_host, int nz, float* slab, 
   nz = nz < 8 ? 8 : (nz > WG_MAX_Z ? WG_MAX_Z : (nz + 7) / 8 * 8);
   WGradGroup G{};
   size_t used = 0;
-  auto fmt = [](const WGrad& g) { return g.x3 ? 0 : (g.ybf && g.xbf) ? 1 : g.ybf ? 2 : g.xbf ? 3 : 4; };
+  // formats: 0 split fp32, 1 bf16 x bf16 on k_wgrad_dma, 2 / 3 / 4 mixed / fp32 rows, 5 bf16 x bf16 on
+  // k_wgrad_group (switched off, or a product k_wgrad_dma does not take)
+  const bool dma = wgrad_dma_on();
+  auto fmt = [dma](const WGrad& g) {
+    return g.x3 ? 0 : (g.ybf && g.xbf) ? (dma && wgrad_dma_fits(g) ? 1 : 5) : g.ybf ? 2 : g.xbf ? 3 : 4;
+  };
   auto issue = [&]() {
     if (G.n == 0) return;
-    for (int v = 0; v < 5; ++v) {  // one product launch per operand format present, one reduce for all
+    for (int v = 0; v < 6; ++v) {  // one product launch per operand format present, one reduce for all
       WGradGroup H{};
       for (int k = 0; k < G.n; ++k)
         if (fmt(G.d[k]) == v) {
@@ -1086,20 +1099,26 @@ int launch_wgrad_group(const WGrad* d, int nd, int n_host, int nz, float* slab, 
         }
       if (!H.n) continue;
       const dim3 grid(H.start[H.n]);
-      if (v == 1 && wgrad_dma_on()) {
+      if (v == 1) {
         // one workgroup per (product, sample range): the whole <= 256 x 256 dW of the range
         WGradGroup D = H;
         for (int q = 0; q < H.n; ++q) D.start[q + 1] = D.start[q] + H.d[q].nz;
-        static bool attr = false;
-        if (!attr) {
-          (void)hipFuncSetAttribute((const void*)k_wgrad_dma, hipFuncAttributeMaxDynamicSharedMemorySize, WD_NB * WD_SLOT);
-          attr = true;
+        static bool attr[64] = {};  // the dynamic-LDS attribute, once per device
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        bool ok = dev >= 0 && dev < 64 && attr[dev];
+        if (!ok) {
+          ok = hipFuncSetAttribute((const void*)k_wgrad_dma, hipFuncAttributeMaxDynamicSharedMemorySize, WD_NB * WD_SLOT) == hipSuccess;
+          if (ok && dev >= 0 && dev < 64) attr[dev] = true;
         }
-        hipLaunchKernelGGL(k_wgrad_dma, dim3(D.start[D.n]), dim3(512), WD_NB * WD_SLOT, s, D);
-        continue;
+        if (ok) {
+          hipLaunchKernelGGL(k_wgrad_dma, dim3(D.start[D.n]), dim3(512), WD_NB * WD_SLOT, s, D);
+          continue;
+        }
+        (void)hipGetLastError();  // the attribute failed: the register-staged kernel below
       }
       if (v == 0) hipLaunchKernelGGL((k_wgrad_group<true, false, false>), grid, dim3(256), 0, s, H);
-      else if (v == 1) hipLaunchKernelGGL((k_wgrad_group<false, true, true>), grid, dim3(256), 0, s, H);
+      else if (v == 1 || v == 5) hipLaunchKernelGGL((k_wgrad_group<false, true, true>), grid, dim3(256), 0, s, H);
       else if (v == 2) hipLaunchKernelGGL((k_wgrad_group<false, true, false>), grid, dim3(256), 0, s, H);
       else if (v == 3) hipLaunchKernelGGL((k_wgrad_group<false, false, true>), grid, dim3(256), 0, s, H);
       else hipLaunchKernelGGL((k_wgrad_group<false, false, false>), grid, dim3(256), 0, s, H);

@@ -683,6 +683,37 @@ bool bchain_on() {
   const char* v = getenv("ANR_TRAIN_BCHAIN");
   return fchain_on() && !(v && v[0] == '0');  // reads the mask bits the forward chains write
 }
+// Which forward last filled a workspace's ReLU mask bits: only the forward chains write them,
+// so the input-gradient chains may run only after a chained forward into the same workspace. The
+// split API (anr_train_fwd / anr_train_bwd, anr_network_train_fwd / _bwd) reads the switches per call,
+// so a forward with ANR_TRAIN_FCHAIN=0 followed by a default backward would otherwise mask with stale
+// bits; such a backward takes the layer-wise input gradients (they read the H rows both forwards write).
+struct ChainBits {
+  std::mutex mu;
+  std::vector<std::pair<const void*, bool>> ws;  // (workspace, written by the forward chains)
+};
+ChainBits& chain_bits_reg() {
+  static ChainBits r;
+  return r;
+}
+void note_chain_bits(const void* ws, bool chained) {
+  ChainBits& r = chain_bits_reg();
+  std::lock_guard<std::mutex> lk(r.mu);
+  for (auto& w : r.ws)
+    if (w.first == ws) {
+      w.second = chained;
+      return;
+    }
+  if (r.ws.size() >= 64) r.ws.erase(r.ws.begin());  // oldest first
+  r.ws.emplace_back(ws, chained);
+}
+bool chain_bits_valid(const void* ws) {
+  ChainBits& r = chain_bits_reg();
+  std::lock_guard<std::mutex> lk(r.mu);
+  for (const auto& w : r.ws)
+    if (w.first == ws) return w.second;
+  return false;
+}
 // every product of a call (forward / backward) runs in a fused chain or a weight gradient: the
 // row-GEMM images (k_wimg_pack, 33 us a step) are not needed
 bool chains_cover(const Exec& e, bool fwd, bool bwd) {
@@ -769,7 +800,7 @@ int chain_pack_bwd(const anr_params* p, unsigned char* img, hipStream_t s) {
 }
 // the pose-space BW backward's chain image, when the chain runs (bf16 rows, ANR_TRAIN_BCHAIN)
 const unsigned char* pose_bchain(const Exec& e, char* ws, const TLayout& T) {
-  return e.hb && bchain_on() ? tc_img((unsigned char*)(ws + T.tcimg), 2) : nullptr;
+  return e.hb && bchain_on() && chain_bits_valid(ws) ? tc_img((unsigned char*)(ws + T.tcimg), 2) : nullptr;
 }
 unsigned char* pose_bits(char* ws, const TLayout& T) { return (unsigned char*)(ws + T.bitsP); }
 // one BW MLP pass (latent folds f0 / f5) over the kept samples: gamma rows G (bf16, ld 64) -> H (bf16
@@ -800,6 +831,7 @@ int train_forward(const anr_params* p, const anr_frame* f, const float* ray_o, c
                   const RaySplit* split = nullptr) {
   float4* raw = (float4*)(ws + T.L.raw);
   const bool fchain = e.hb && fchain_on() && R > 0;
+  note_chain_bits(ws, fchain);
   unsigned char* tcimg = (unsigned char*)(ws + T.tcimg);
   if (fchain) {
     // the chain images (and the input-gradient ones, for the backward of this step) are packed on s2,
@@ -932,7 +964,7 @@ int train_backward(const anr_params* p, float* const* g, const anr_frame* f, con
   float* ysum = (float*)(ws + T.ysum);
   // the T-pose BW chain writes its gamma(x_T) gradient into dGt2 (s2), the NeRF's into dGt (s)
   b.dGt2 = (float*)(ws + T.dGt2);
-  const bool bchain = e.hb && bchain_on();
+  const bool bchain = e.hb && bchain_on() && chain_bits_valid(ws);
   unsigned char* tcimg = (unsigned char*)(ws + T.tcimg);
   if (bchain && !e.bimg) ANR_TRY(chain_pack_bwd(p, tcimg, s));
   // with the chains every weight gradient is ready at once: groups of up to 16 (no flush at 8) measured
@@ -1242,7 +1274,7 @@ int anr_train_bwd(const anr_params* p, float* const* grads, const anr_frame* f, 
   e.ss = om.ss;
   e.hb = e.bf16;
   ANR_TRY(pack_images(e, p, ws + T.wimg, s, (float*)(ws + T.wslab), kLaneFloats, false,
-                      !chains_cover(e, false, true)));
+                      !(chains_cover(e, false, true) && chain_bits_valid(ws))));
   ANR_TRY(train_backward(p, grads, f, ray_o, ray_d, near_, far_, n_rays, o, d_rgb_map, d_pbw, d_tbw, ws, T, s, e));
   // pose BW MLP backward: d logits were produced by k_tr_softmax_bwd_p
   const long N = (long)n_rays * 64;
@@ -1555,7 +1587,7 @@ int anr_network_train_bwd(const anr_params* p, float* const* grads, const anr_fr
   e.ss = om.ss;
   e.hb = e.bf16;
   ANR_TRY(pack_images(e, p, ws + T.wimg, s, (float*)(ws + T.wslab), kLaneFloats, false,
-                      !chains_cover(e, false, true)));
+                      !(chains_cover(e, false, true) && chain_bits_valid(ws))));
   ANR_TRY(train_backward(p, grads, f, nullptr, nullptr, nullptr, nullptr, G, &oo, nullptr, d_pbw, d_tbw, ws, T, s, e, x,
                          d_raw));
   const long N = (long)G * 64;

@@ -21,9 +21,10 @@ import torch
 
 from . import _lib
 from . import config as _config
-from .parallel import GradBuckets, broadcast_
+from .parallel import GradBuckets, broadcast_, is_dist
 from .renderer_sdf import Renderer
 
+COLOUR_TENSORS = (28, 44)  # color_network.* (colour latent, lin0..lin4 g / v / bias): final first
 LOSS_KEYS = ('loss', 'offset_loss', 'grad_loss', 'ograd_loss', 'mask_loss', 'img_loss', 'n_observed', 'msk_len',
              'n_kept', 'reserved')
 NLOSS = len(LOSS_KEYS)
@@ -41,10 +42,12 @@ def train_precision(cfg):
     return precs[prec]
 
 
-def sdf_train_step(renderer, batch, grads, loss8, t_rand=None, iter_step=None):
+def sdf_train_step(renderer, batch, grads, loss8, t_rand=None, iter_step=None, hooks=None):
     """One anr_sdf_train_step: ACCUMULATES the gradients of the 63 tensors into ``grads`` (list,
     state_dict order) and writes the NLOSS loss floats into ``loss8`` (device, no host sync of its own).
-    Returns {'rgb_map', 'acc_map', 'depth_map'} and widens ``batch['tbounds']`` in place."""
+    Returns {'rgb_map', 'acc_map', 'depth_map'} and widens ``batch['tbounds']`` in place.
+    ``hooks`` (_lib.SdfTrainHooks or None): the event / host callback of anr_sdf_train_step_hooked once
+    the colour net's gradients (tensors COLOUR_TENSORS) are final."""
     lib = renderer.lib
     c = renderer.prepare(batch, t_rand)
     dev, R, rays, o = c['dev'], c['R'], c['rays'], c['opts']
@@ -61,10 +64,11 @@ def sdf_train_step(renderer, batch, grads, loss8, t_rand=None, iter_step=None):
     nbytes = lib.anr_sdf_train_workspace_bytes(R, ctypes.byref(o))
     ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
     gp = (ctypes.c_void_p * _lib.NUM_SDF_TENSORS)(*[None if g is None else g.data_ptr() for g in grads])
-    _lib.check(lib.anr_sdf_train_step(ctypes.byref(c['p']), gp, ctypes.byref(c['frame']),
-                                      *[_lib.ptr(rays[k]) for k in ('ray_o', 'ray_d', 'near', 'far')], R,
-                                      ctypes.byref(o), _lib.ptr(gt), _lib.ptr(mask), it, ctypes.byref(out),
-                                      _lib.ptr(loss8), _lib.ptr(ws), nbytes, _lib.stream_ptr(dev)),
+    _lib.check(lib.anr_sdf_train_step_hooked(ctypes.byref(c['p']), gp, ctypes.byref(c['frame']),
+                                             *[_lib.ptr(rays[k]) for k in ('ray_o', 'ray_d', 'near', 'far')], R,
+                                             ctypes.byref(o), _lib.ptr(gt), _lib.ptr(mask), it, ctypes.byref(out),
+                                             _lib.ptr(loss8), None if hooks is None else ctypes.byref(hooks),
+                                             _lib.ptr(ws), nbytes, _lib.stream_ptr(dev)),
                'anr_sdf_train_step')
     with torch.no_grad():
         batch['tbounds'].copy_(tb_out.view_as(batch['tbounds']))
@@ -111,7 +115,12 @@ class SdfStep:
     the gradient blob with the losses in its tail] + clip_grad_value_(40) + Adam (optimizer.py:12-27,
     trainer.py:64-68). Returns the device loss vector (LOSS_KEYS order): with N > 1 ranks every entry
     is the MEAN over the ranks, the count entries too (n_observed, msk_len, n_kept are then per-rank
-    averages, not totals: multiply by the world size for the job's counts)."""
+    averages, not totals: multiply by the world size for the job's counts).
+
+    The all-reduce runs in buckets as DDP's reducer does (trainer.py:13-18): bucket 0, the colour
+    net's gradients, leaves on the side stream as soon as the library records them final (after the
+    colour backward, ~1/5 of the blob) while the SDF / residual / observed-gradient backward still
+    runs; the rest (SDF net, beta, residual net, losses) follows the step."""
 
     def __init__(self, net, cfg=None, lr=None, clip=40.0, betas=(0.9, 0.999), eps=1e-8, group=None):
         self.cfg = cfg if cfg is not None else _config.active()
@@ -138,15 +147,45 @@ class SdfStep:
             off += k
         self.n, self.t = n, 0
         self.loss8 = self.grad[n:n + NLOSS]
-        self.buckets = GradBuckets(self.grad, [(0, n + NLOSS)], group)
+        offs = [0]
+        for p in ps:
+            offs.append(offs[-1] + p.numel())
+        c0, c1 = offs[COLOUR_TENSORS[0]], offs[COLOUR_TENSORS[1]]
+        self.buckets = GradBuckets(self.grad, [(c0, c1), (0, c0), (c1, n + NLOSS)], group)
+        self.colour_ready = None
+        self._hooks = None
+        if dev.type == 'cuda':
+            self.colour_ready = torch.cuda.Event()
+            self.colour_ready.record()  # creates the underlying hipEvent (re-recorded by the library)
+            self._ready_cb = _lib.READY_FN(self._colour_ready_hook)  # kept alive with the step
+            self._hooks = _lib.SdfTrainHooks(colour_grads_ready=self.colour_ready.cuda_event,
+                                             colour_ready=self._ready_cb)
         self.iter_step = 0
         broadcast_(self.flat, 0, group)  # DDP semantics: every replica starts from rank 0's weights
+
+    def _colour_ready_hook(self, user, event, stream):
+        """anr_sdf_train_hooks.colour_ready: called by the library mid-step, right after it recorded
+        self.colour_ready; bucket 0's collective is issued on the side stream behind that event and runs
+        beside the rest of the backward."""
+        try:
+            self.buckets.reduce(0, self.colour_ready)
+            self._issued = True
+            return 0
+        except Exception:  # pragma: no cover - surfaced as the call's error
+            import traceback
+            traceback.print_exc()
+            return 1
 
     def step(self, batch, t_rand=None, lr=None):
         self.grad.zero_()
         it = int(batch.get('iter_step', self.iter_step))
-        sdf_train_step(self.renderer, batch, self.grad_views, self.loss8, t_rand, iter_step=it)
-        self.buckets.reduce(0)
+        self._issued = False
+        sdf_train_step(self.renderer, batch, self.grad_views, self.loss8, t_rand, iter_step=it,
+                       hooks=self._hooks if is_dist() else None)
+        if not self._issued:  # CPU blob / one rank / the hook not reached (no kept sample)
+            self.buckets.reduce(0)
+        self.buckets.reduce(1)
+        self.buckets.reduce(2)
         self.buckets.wait()
         self.t += 1
         self.iter_step += 1

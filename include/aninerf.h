@@ -472,6 +472,26 @@ int anr_sdf_train_step(const anr_sdf_params* p, float* const* grads, const anr_s
                        const float* ray_d, const float* near_, const float* far_, int n_rays, const anr_render_opts* o,
                        const float* rgb_gt, const uint8_t* mask_at_box, int iter_step, const anr_sdf_render_out* out,
                        float* loss, void* workspace, size_t ws_bytes, void* stream);
+/* anr_sdf_train_step_hooked: anr_sdf_train_step plus a hook for overlapping the gradient all-reduce
+ * with the rest of the backward (DDP's buckets, trainer.py:13-18). Once the gradients of tensors 28..43
+ * (color_network.*, colour latent included) are final, colour_grads_ready (a hipEvent_t, or NULL) is
+ * recorded on the stream and then colour_ready (or NULL) is called on the host with that event and the
+ * stream, while the SDF's stacked reverse, the residual backward and the observed-gradient passes
+ * (tensors 0..27, 45..62) are still to be issued: the caller issues the colour bucket's collective there
+ * (ordered after the event) and it runs beside them. A non-zero return from colour_ready fails the call.
+ * struct_size must be sizeof(anr_sdf_train_hooks). hooks == NULL: anr_sdf_train_step. */
+typedef int (*anr_ready_fn)(void* user, void* event, void* stream);
+typedef struct anr_sdf_train_hooks {
+  size_t struct_size;
+  void* colour_grads_ready;
+  anr_ready_fn colour_ready;
+  void* user;
+} anr_sdf_train_hooks;
+int anr_sdf_train_step_hooked(const anr_sdf_params* p, float* const* grads, const anr_sdf_frame* f,
+                              const float* ray_o, const float* ray_d, const float* near_, const float* far_,
+                              int n_rays, const anr_render_opts* o, const float* rgb_gt, const uint8_t* mask_at_box,
+                              int iter_step, const anr_sdf_render_out* out, float* loss,
+                              const anr_sdf_train_hooks* hooks, void* workspace, size_t ws_bytes, void* stream);
 
 /* ---- (f) mesh path (lib/networks/renderer/aninerf_mesh_renderer.py) ----------------------
  * anr_alpha_points: raw alpha (no activation, no bbox mask) of n free world points, zero where the

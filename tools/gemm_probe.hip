@@ -221,7 +221,68 @@ static int group_check(hipStream_t s, int M) {
   return 0;
 }
 
+// one flushed group of NP bf16 x bf16 products (256 x 256, the step's bulk; column sums on every other)
+// timed with the register-staged k_wgrad_group and with k_wgrad_dma (ANR_WG_DMA, read per call), at
+// several sample-range counts; the two results compared (fixed inputs, relative to the max |dW|)
+static int group_time(hipStream_t s, int M, int NP) {
+  const int cap = (M + 1023) / 1024 * 1024 + 4096;
+  const long rows = (long)cap * 256;
+  unsigned short *Y16, *X16;
+  float *dW, *dW2, *bs, *slab;
+  int* Mdev;
+  CK(hipMalloc(&Y16, NP * rows * 2));
+  CK(hipMalloc(&X16, NP * rows * 2));
+  CK(hipMalloc(&dW, NP * 65536L * 4));
+  CK(hipMalloc(&dW2, NP * 65536L * 4));
+  CK(hipMalloc(&bs, NP * 256L * 4));
+  CK(hipMalloc(&slab, 4 * wgrad_slab_floats() * 4));
+  CK(hipMalloc(&Mdev, 4));
+  CK(hipMemcpy(Mdev, &M, 4, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(k_probe_fill16, dim3((unsigned)((NP * rows + 255) / 256)), dim3(256), 0, s, Y16, NP * rows, 21u, 0.02f);
+  hipLaunchKernelGGL(k_probe_fill16, dim3((unsigned)((NP * rows + 255) / 256)), dim3(256), 0, s, X16, NP * rows, 22u, 2.f);
+  std::vector<WGrad> d(NP);
+  for (int k = 0; k < NP; ++k) {
+    WGrad& w = d[k];
+    w.ybf = 1; w.xbf = 1; w.nout = 256; w.K = 256; w.ldY = 256; w.ldX = 256;
+    w.dY = (const float*)(Y16 + k * rows);
+    w.X = (const float*)(X16 + k * rows);
+    w.dW = dW + k * 65536L; w.ldw = 256;
+    w.bsum = (k % 2) ? bs + k * 256 : nullptr;
+    w.M_dev = Mdev;
+  }
+  const double fl = 2.0 * NP * M * 256.0 * 256.0, by = 2.0 * NP * M * 256.0 * 2.0;
+  for (int nz : {8, 16, 32}) {
+    for (int dma = 0; dma < 2; ++dma) {
+      setenv("ANR_WG_DMA", dma ? "1" : "0", 1);
+      for (int k = 0; k < NP; ++k) d[k].dW = (dma ? dW2 : dW) + k * 65536L;
+      const float us = time_us(s, 20, [&] { launch_wgrad_group(d.data(), NP, cap, nz, slab, 4 * wgrad_slab_floats(), s); });
+      printf("{\"group_time\": \"%s\", \"M\": %d, \"products\": %d, \"nz\": %d, \"us\": %.2f, \"TFLOPs\": %.1f, \"GBps\": %.1f}\n",
+             dma ? "k_wgrad_dma" : "k_wgrad_group", M, NP, nz, us, fl / us * 1e-6, by / us * 1e-3);
+      fflush(stdout);
+    }
+    // one clean accumulation each, compared
+    CK(hipMemsetAsync(dW, 0, NP * 65536L * 4, s));
+    CK(hipMemsetAsync(dW2, 0, NP * 65536L * 4, s));
+    setenv("ANR_WG_DMA", "0", 1);
+    for (int k = 0; k < NP; ++k) d[k].dW = dW + k * 65536L;
+    launch_wgrad_group(d.data(), NP, cap, nz, slab, 4 * wgrad_slab_floats(), s);
+    setenv("ANR_WG_DMA", "1", 1);
+    for (int k = 0; k < NP; ++k) d[k].dW = dW2 + k * 65536L;
+    launch_wgrad_group(d.data(), NP, cap, nz, slab, 4 * wgrad_slab_floats(), s);
+    CK(hipStreamSynchronize(s));
+    printf("{\"group_time_diff\": %.3g, \"nz\": %d}\n", max_rel_diff(dW2, dW, NP * 65536L), nz);
+  }
+  unsetenv("ANR_WG_DMA");
+  fflush(stdout);
+  return 0;
+}
+
 int main(int argc, char** argv) {
+  if (argc > 1 && std::string(argv[1]) == "grouptime") {
+    hipStream_t s;
+    CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    return group_time(s, argc > 2 ? atoi(argv[2]) : 24893, argc > 3 ? atoi(argv[3]) : 16);
+  }
   if (argc > 1 && std::string(argv[1]) == "groupcheck") {
     hipStream_t s;
     CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
