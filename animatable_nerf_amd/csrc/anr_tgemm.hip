@@ -1127,13 +1127,36 @@ int launch_wgrad_group(const WGrad* d, int nd, int n_host, int nz, float* slab, 
     G = WGradGroup{};
     used = 0;
   };
+  // sample ranges per format: each format's launch should fill the chip on its own (the launches of a
+  // flush run one after another), so a format with little work — the few small fp32-row products of the
+  // NeRF heads (rgb_fc 3 x 128, view_fc 128 x 283: 1 - 3 tiles), or a short tail of k_wgrad_dma products
+  // (one 512-thread workgroup per product and range) — gets more, shorter ranges: workgroups per range
+  // summed over the format's products, ranges up to WG_MAX_Z (k_wgrad_dma: 32, its partial slabs are
+  // whole 256 x 256 tiles). ANR_WG_FILL=0: every product at nz (ANR_WG_GROUP_NZ).
+  int fz[6] = {nz, nz, nz, nz, nz, nz};
+  {
+    const char* fe = getenv("ANR_WG_FILL");
+    if (!(fe && fe[0] == '0')) {
+      int per[6] = {0, 0, 0, 0, 0, 0};  // workgroups per sample range
+      for (int k = 0; k < nd; ++k) {
+        const int v = fmt(d[k]);
+        per[v] += v == 1 ? 1 : ((d[k].nout + WG_T - 1) / WG_T) * ((d[k].K + WG_T - 1) / WG_T);
+      }
+      for (int v = 0; v < 6; ++v) {
+        if (!per[v]) continue;
+        const int want = v == 1 ? 256 : 512, cap = v == 1 ? 32 : WG_MAX_Z;
+        const int z = ((want + per[v] - 1) / per[v] + 7) / 8 * 8;
+        fz[v] = z < nz ? nz : (z > cap ? (cap > nz ? cap : nz) : z);
+      }
+    }
+  }
   for (int k = 0; k < nd; ++k) {
     WGrad g = d[k];
     g.tj = (g.K + WG_T - 1) / WG_T;
     g.tiles = ((g.nout + WG_T - 1) / WG_T) * g.tj;
     // a descriptor's slabs are (nz, tile) partial tiles, then (nz, 256) column sums; nz halves (not below 8)
     // until the descriptor fits the region on its own
-    int z = nz;
+    int z = fz[fmt(g)];
     auto need = [&](int zz) { return (size_t)zz * g.tiles * WG_TILE_FLOATS + ((g.bsum || g.bsum2) ? (size_t)zz * 256 : 0); };
     while (z > 8 && need(z) > slab_floats) z = z / 16 * 8 > 8 ? z / 16 * 8 : 8;
     if (need(z) > slab_floats) return -1;
