@@ -13,9 +13,20 @@
 // loads in flight across the MFMAs and the epilogue), and epilogues (softplus + its backward factor,
 // the softplus-backward multiply) overlap other waves' MFMAs. Products and epilogue order match
 // k_gemm_b<.., .., true> (anr_gemm.hip).
+//
+// F32 (the exact-fp32 precision of the sdf_pdf training step and render): the same kernel with the
+// weight image in fp32 and v_mfma_f32_16x16x4_f32 (exact fp32 products, fp32 accumulation, the
+// products k_gemm_t computes). A lane's 8 activation values of a 32-deep k-step (k = 32 ks + 8 j + e,
+// j = lane >> 4) feed 8 MFMAs, MFMA e taking element e in the k slot j; the image holds the matching
+// weight (n, 32 ks + 8 j + e) as two 16-B pieces per lane (elements 0..3 and 4..7, in the hi / lo
+// slots of the split image), so one fragment pair is the same 2 KiB and two ds_read_b128. The
+// per-sample VALU work of the split disappears: the loop is the MFMAs, MFMA-bound at 32 cycles each.
+// MASK: a ReLU layer's output gates the result (v = 0 where mask <= 0, after the other epilogue steps
+// and before div_post, as k_gemm_t), its rows loaded with the tile ahead of the MFMAs like the spd.
 #include <algorithm>
 
 #include "anr_common.h"
+#include "anr_kernels.h"
 #include "anr_train.h"
 
 namespace anr {
@@ -63,6 +74,9 @@ struct LGemm {
   float spd_scale;   // spd_h: stored values are h / spd_scale (0: 1)
   float div_pre, div_post;
   const float* atr;  // ATR: the activations are softplus factors d, used as (d >= 0 ? atr[k] d / (d + 1) : atr[k])
+  const float* mask; // MASK: v = 0 where mask[m][n] <= 0
+  long ldm;
+  unsigned long long* clk;  // anr_profile_*: per-workgroup clock stamps (GemmArgs::prof)
   // HEAD: a following 256 -> head_n (<= 4) layer fused into the epilogue: the activation C is not stored;
   // each workgroup adds its column group's partial head_w . h (plus head_b for group 0) into head_out
   const float* head_w;
@@ -81,6 +95,7 @@ struct LPack {
   const float* bias;
   float* bout;  // G NOB 16 floats
   int nbias;
+  int f32;      // fp32 image (F32 kernels): element e of lane at float ((f 2 + e / 4) 64 + lane) 4 + e % 4
 };
 
 __device__ __forceinline__ unsigned short lg_bf16_rne(float f) {
@@ -108,6 +123,10 @@ __global__ void k_limg_pack(LPack p) {
   const int n = 16 * (g * p.NOB + ob) + (lane & 15);
   float v = 0.0f;
   if (n < p.N && kk < p.K[s]) v = p.B[s][(long)kk * p.b_rs[s] + (long)n * p.b_cs[s]];
+  if (p.f32) {
+    ((float*)p.out)[((f * 2 + (e >> 2)) * 64 + lane) * 4 + (e & 3)] = v;
+    return;
+  }
   const unsigned short hi = lg_bf16_rne(v);
   const unsigned short lo = lg_bf16_rne(v - __uint_as_float((uint32_t)hi << 16));
   const long o = ((f * 2) * 64 + lane) * 8 + e;
@@ -121,8 +140,8 @@ __device__ __forceinline__ float lg_log1p(float e) { return fast_log1p(e); }
 // epilogue of one 16-sample tile: lane holds C[16 t + (lane & 15)][n0 + 16 ob + 4 (lane >> 4) + r].
 // Bias comes from LDS, the softplus-backward factors were loaded before the tile's MFMAs (sp); the
 // epilogue issues no global loads, so the next tile's activation loads stay in flight across it.
-template <int NOB, bool SPD, bool HEAD>
-__device__ __forceinline__ void lg_epilogue(const LGemm& g, const f32x4 (&acc)[NOB], const f32x4* sp,
+template <int NOB, bool SPD, bool HEAD, bool MASK>
+__device__ __forceinline__ void lg_epilogue(const LGemm& g, const f32x4 (&acc)[NOB], const f32x4* sp, const f32x4* mk,
                                             const float* bias_lds, int tile, int n0, int lane, const float* head_lds) {
   float hp[4] = {0.f, 0.f, 0.f, 0.f};  // HEAD partials of this lane's columns
   // rows past M were computed from row M - 1's activations (the loads clamp), so their results are
@@ -153,6 +172,7 @@ __device__ __forceinline__ void lg_epilogue(const LGemm& g, const f32x4 (&acc)[N
           x = x * d * __builtin_amdgcn_rcpf(d + 1.f);
         }
       }
+      if constexpr (MASK) x = mk[ob][e] > 0.f ? x : 0.0f;
       if (g.div_post != 0.f) x = x / g.div_post;
       v[e] = x;
     }
@@ -233,17 +253,30 @@ __device__ __forceinline__ void lg_load_spd(const LGemm& g, f32x4 (&sp)[NOB], in
   }
 }
 
+template <int NOB, bool MASK>
+__device__ __forceinline__ void lg_load_mask(const LGemm& g, f32x4 (&mk)[NOB], int tile, int n0, int lane) {
+  if constexpr (MASK) {
+    const int m = min(tile * 16 + (lane & 15), g.M - 1);
+#pragma unroll
+    for (int ob = 0; ob < NOB; ++ob) {
+      const int n = min(n0 + 16 * ob + 4 * (lane >> 4), g.N - 4);
+      mk[ob] = *(const f32x4*)(g.mask + (long)m * g.ldm + n);
+    }
+  }
+}
+
 // one tile on a k-step ring: this tile's factor loads go out first; each k-step's activations are
 // split hi/lo and their registers immediately refilled with the same k-step of the wave's next tile
 // (so one tile of loads is always in flight, in one tile's worth of registers), then the MFMAs;
 // the epilogue last. The loop is straight-line, so the compiler's vmcnt waits stay exact.
-template <int NOB, int KST, int KST0, bool SPD, bool UNAL, bool ATR, bool HEAD, bool FULLK>
+template <int NOB, int KST, int KST0, bool SPD, bool UNAL, bool ATR, bool HEAD, bool FULLK, bool F32, bool MASK>
 __device__ __forceinline__ void lg_tile(const LGemm& g, f32x4 (&buf)[KST][2], int tile, int next, int n0, int lane,
                                         const unsigned char* lds, const float* atr_lds) {
-  // the tile's softplus-backward factors load first: used in this tile's epilogue, and issuing them
-  // ahead of the refills keeps every wait in the loop graded (the bias columns sit in LDS)
-  f32x4 sp[NOB];
+  // the tile's softplus-backward factors (and mask rows) load first: used in this tile's epilogue, and
+  // issuing them ahead of the refills keeps every wait in the loop graded (the bias columns sit in LDS)
+  f32x4 sp[NOB], mk[NOB];
   lg_load_spd<NOB, SPD>(g, sp, tile, n0, lane);
+  lg_load_mask<NOB, MASK>(g, mk, tile, n0, lane);
   const int kg = lane >> 4;
   f32x4 acc[NOB];
 #pragma unroll
@@ -269,6 +302,25 @@ __device__ __forceinline__ void lg_tile(const LGemm& g, f32x4 (&buf)[KST][2], in
 #pragma unroll
     for (int e = 0; e < 8; ++e)
       if constexpr (!FULLK) x[e] = (k0 + lg_kcol(kg, e) < K) ? x[e] : 0.0f;
+    if constexpr (F32) {
+      lg_load_ks<KST0, UNAL, FULLK>(g, buf[ks], next, ks, lane);
+      __builtin_amdgcn_sched_barrier(0);
+      const unsigned char* fr = lds + ks * NOB * 2 * LG_FRAG + frag_off;
+      // every fragment of the k-step read up front (elements 0..3 of all out-blocks first), then the MFMAs
+      // element-major: NOB independent accumulators between two uses of one (a per-out-block chain of 8
+      // dependent MFMAs with its reads right before it measured 0.43 of the fp32 peak, the reads exposed)
+      f32x4 w[2][NOB];
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int ob = 0; ob < NOB; ++ob) w[h][ob] = *(const f32x4*)(fr + (2 * ob + h) * LG_FRAG);
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+#pragma unroll
+        for (int ob = 0; ob < NOB; ++ob)
+          acc[ob] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[e >> 2][ob][e & 3], x[e], acc[ob], 0, 0, 0);
+      continue;
+    }
     lbf16x8 xh, xl;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -289,12 +341,12 @@ __device__ __forceinline__ void lg_tile(const LGemm& g, f32x4 (&buf)[KST][2], in
       acc[ob] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, xh, acc[ob], 0, 0, 0);
     }
   }
-  lg_epilogue<NOB, SPD, HEAD>(g, acc, sp, atr_lds + 32 * KST + 1024, tile, n0, lane, atr_lds + 32 * KST);
+  lg_epilogue<NOB, SPD, HEAD, MASK>(g, acc, sp, mk, atr_lds + 32 * KST + 1024, tile, n0, lane, atr_lds + 32 * KST);
 }
 
 // FULLK: every segment is a whole number of 32-deep k-steps (the 256-wide layers), so the loop has no
 // per-element K masks and no column clamps (chosen per launch on the host: one loop per kernel)
-template <int NOB, int KST, int KST0, bool SPD, bool UNAL, bool ATR, bool HEAD, bool FULLK>
+template <int NOB, int KST, int KST0, bool SPD, bool UNAL, bool ATR, bool HEAD, bool FULLK, bool F32, bool MASK>
 __global__ __launch_bounds__(LG_WAVES * 64) void k_lgemm(LGemm g) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   // workgroup -> (column group, rank): the workgroups of one rank sit on one XCD (blockIdx % 8), so
@@ -334,6 +386,7 @@ __global__ __launch_bounds__(LG_WAVES * 64) void k_lgemm(LGemm g) {
     }
   }
   __syncthreads();
+  clk_stamp(g.clk, 0);
   // wave-uniform cursors live in SGPRs: the loop below has no divergent control flow
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nw = g.bpg * LG_WAVES;
@@ -343,7 +396,9 @@ __global__ __launch_bounds__(LG_WAVES * 64) void k_lgemm(LGemm g) {
   f32x4 buf[KST][2];
 #pragma unroll
   for (int ks = 0; ks < KST; ++ks) lg_load_ks<KST0, UNAL>(g, buf[ks], t, ks, lane);
-  for (; t < T; t += nw) lg_tile<NOB, KST, KST0, SPD, UNAL, ATR, HEAD, FULLK>(g, buf, t, t + nw, n0, lane, lds, atr_lds);
+  for (; t < T; t += nw)
+    lg_tile<NOB, KST, KST0, SPD, UNAL, ATR, HEAD, FULLK, F32, MASK>(g, buf, t, t + nw, n0, lane, lds, atr_lds);
+  if (w == 0) clk_stamp(g.clk, 1);
 }
 
 // weight image, ATR column weights (32 kst floats), HEAD weights (4 x 256 floats), bias (128 floats)
@@ -369,41 +424,70 @@ int lg_kst(const GemmArgs& g, int* kst0) {
   return *kst0 + (g.nseg > 1 ? (g.seg[1].K + 31) / 32 : 0);
 }
 
-template <int NOB, int KST, int KST0, bool SPD, bool UNAL, bool ATR, bool HEAD, bool FULLK>
+template <int NOB, int KST, int KST0, bool SPD, bool UNAL, bool ATR, bool HEAD, bool FULLK, bool F32, bool MASK>
 void lg_launch(const LGemm& a, int cus, hipStream_t s) {
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)k_lgemm<NOB, KST, KST0, SPD, UNAL, ATR, HEAD, FULLK>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, LG_MAX_LDS);
-    attr = true;
+  auto kern = k_lgemm<NOB, KST, KST0, SPD, UNAL, ATR, HEAD, FULLK, F32, MASK>;
+  static bool attr[64] = {};  // the dynamic-LDS attribute, once per device
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (dev < 0 || dev >= 64 || !attr[dev]) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LG_MAX_LDS);
+    if (dev >= 0 && dev < 64) attr[dev] = true;
   }
   LGemm g = a;
   g.bpg = std::max(1, cus / (8 * g.G)) * 8;
-  hipLaunchKernelGGL((k_lgemm<NOB, KST, KST0, SPD, UNAL, ATR, HEAD, FULLK>), dim3((unsigned)(g.bpg * g.G)), dim3(LG_WAVES * 64),
-                     lg_lds_bytes(KST, NOB), s, g);
+  const int grid = g.bpg * g.G;
+  ProfSlot* ps = g.clk ? prof_begin(s, grid) : nullptr;  // g.clk != NULL here: the caller asked for a slot
+  g.clk = ps ? ps->clk : nullptr;
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(LG_WAVES * 64), lg_lds_bytes(KST, NOB), s, g);
+  (void)prof_end(ps, s);
 }
 
 // the instantiated shapes (the sdf_pdf layers); false for any other
-bool lg_dispatch(const LGemm& a, int nob, bool spd, bool unal, int cus, hipStream_t s, bool launch) {
+bool lg_dispatch(const LGemm& a, int nob, bool spd, bool unal, bool f32, bool mask, int cus, hipStream_t s,
+                 bool launch) {
   const bool atr = a.atr != nullptr, head = a.head_out != nullptr;
   const bool fullk = a.seg[0].K == 32 * a.kst0 && (a.kst == a.kst0 || a.seg[1].K == 32 * (a.kst - a.kst0));
-#define LG_CASE(N_, K_, K0_, S_, U_, T_, H_, F_)                                                        \
+#define LG_CASE(N_, K_, K0_, S_, U_, T_, H_, F_, X_, M_)                                                \
   if (nob == N_ && a.kst == K_ && a.kst0 == K0_ && spd == S_ && unal == U_ && atr == T_ && head == H_ && \
-      fullk == F_) {                                                                                    \
-    if (launch) lg_launch<N_, K_, K0_, S_, U_, T_, H_, F_>(a, cus, s);                                  \
+      fullk == F_ && f32 == X_ && mask == M_) {                                                         \
+    if (launch) lg_launch<N_, K_, K0_, S_, U_, T_, H_, F_, X_, M_>(a, cus, s);                          \
     return true;                                                                                        \
   }
-  LG_CASE(8, 8, 8, false, false, false, true, true)
-  LG_CASE(8, 8, 8, false, false, false, false, true)
-  LG_CASE(8, 8, 8, true, false, false, false, true)
-  LG_CASE(8, 8, 8, true, false, true, false, true)
-  LG_CASE(8, 7, 7, true, false, false, false, false)
-  LG_CASE(8, 2, 2, false, false, false, false, false)
-  LG_CASE(6, 10, 2, false, false, false, false, false)
-  LG_CASE(6, 10, 2, false, true, false, false, false)
-  LG_CASE(6, 8, 8, false, false, false, false, true)
-  LG_CASE(4, 8, 8, false, false, false, false, true)
-  LG_CASE(1, 8, 8, false, false, false, false, true)
+  // split-bf16 (render precision bf16x3 and the bf16x3 sdf training parts)
+  LG_CASE(8, 8, 8, false, false, false, true, true, false, false)
+  LG_CASE(8, 8, 8, false, false, false, false, true, false, false)
+  LG_CASE(8, 8, 8, true, false, false, false, true, false, false)
+  LG_CASE(8, 8, 8, true, false, true, false, true, false, false)
+  LG_CASE(8, 7, 7, true, false, false, false, false, false, false)
+  LG_CASE(8, 2, 2, false, false, false, false, false, false, false)
+  LG_CASE(6, 10, 2, false, false, false, false, false, false, false)
+  LG_CASE(6, 10, 2, false, true, false, false, false, false, false)
+  LG_CASE(6, 8, 8, false, false, false, false, true, false, false)
+  LG_CASE(4, 8, 8, false, false, false, false, true, false, false)
+  LG_CASE(1, 8, 8, false, false, false, false, true, false, false)
+  // exact fp32 (the sdf_pdf training step's fp32 products and the exact sdf render): the layer shapes of
+  // the residual MLP (63 / 63 + 256 / 256 inputs, masked tangent and input-gradient passes, the K = 3
+  // head gradient), the SDF (39 / 256 / 217 / 257 inputs, softplus factors), the colour net, and their
+  // transposed products
+  LG_CASE(8, 2, 2, false, false, false, false, false, true, false)
+  LG_CASE(6, 10, 2, false, false, false, false, false, true, false)
+  LG_CASE(8, 8, 8, false, false, false, false, true, true, false)
+  LG_CASE(1, 8, 8, false, false, false, false, true, true, false)
+  LG_CASE(6, 8, 8, false, false, false, false, true, true, false)
+  LG_CASE(6, 10, 2, false, true, false, false, false, true, false)
+  LG_CASE(4, 8, 8, false, false, false, false, true, true, false)
+  LG_CASE(8, 7, 7, false, false, false, false, false, true, false)
+  LG_CASE(8, 9, 9, false, false, false, false, false, true, false)
+  LG_CASE(8, 2, 2, true, false, false, false, false, true, false)
+  LG_CASE(8, 8, 8, true, false, false, false, true, true, false)
+  LG_CASE(8, 7, 7, true, false, false, false, false, true, false)
+  LG_CASE(8, 8, 8, true, false, true, false, true, true, false)
+  LG_CASE(8, 8, 8, false, false, false, true, true, true, false)
+  LG_CASE(8, 2, 2, false, false, false, false, false, true, true)
+  LG_CASE(6, 10, 2, false, false, false, false, false, true, true)
+  LG_CASE(8, 8, 8, false, false, false, false, true, true, true)
+  LG_CASE(8, 1, 1, false, false, false, false, false, true, true)
 #undef LG_CASE
   return false;
 }
@@ -427,6 +511,8 @@ LGemm lg_args(const GemmArgs& g, int* nob) {
   a.C = g.C; a.ldc = g.ldc; a.bias = g.bias; a.relu = g.relu; a.softplus = g.softplus; a.deriv = g.deriv;
   a.ldd = g.ldd; a.spd = g.spd; a.ldsd = g.ldsd; a.spd_n = g.spd_n; a.spd_h = g.spd_h; a.spd_scale = g.spd_scale; a.div_pre = g.div_pre; a.div_post = g.div_post;
   a.atr = g.a_softplus_w;
+  a.mask = g.mask; a.ldm = g.ldm;
+  a.clk = g.prof ? (unsigned long long*)1 : nullptr;  // a marker: lg_launch takes a profiling slot
   a.head_w = g.head_w; a.head_b = g.head_b; a.head_out = g.head_out; a.ldh = g.ldh; a.head_n = g.head_n;
   return a;
 }
@@ -440,8 +526,12 @@ size_t lgemm_image_bytes(const GemmArgs& g) {
   return (size_t)G * kst * NOB * 2 * LG_FRAG + (size_t)G * NOB * 64;
 }
 
+// exact fp32 (F32 kernels): a product that is neither split-bf16 nor bf16
+static bool lg_f32(const GemmArgs& g) { return !g.x3 && !g.bf16; }
+
 bool lgemm_supported(const GemmArgs& g) {
-  if (!g.x3 || g.accumulate || g.atomic || g.mask || g.rowsum || g.rowsum2 || g.M_dev || g.ksplit > 1) return false;
+  if (g.bf16 || g.accumulate || g.atomic || g.rowsum || g.rowsum2 || g.M_dev || g.ksplit > 1) return false;
+  if (g.mask && (!lg_f32(g) || !al16(g.mask) || g.ldm % 4 != 0 || g.spd || g.N % 4 != 0)) return false;
   if (g.N < 1 || (g.spd && g.N < 4) || g.M <= 0 || g.nseg < 1 || g.nseg > 2) return false;
   for (int s = 0; s < g.nseg; ++s) {
     const GemmSeg& q = g.seg[s];
@@ -455,7 +545,7 @@ bool lgemm_supported(const GemmArgs& g) {
   if (g.head_out && (a.G != 2 || g.N != 256 || g.head_n < 1 || g.head_n > 4 || !g.head_w || !g.head_b ||
                      g.softplus || g.spd || g.a_softplus_w))
     return false;
-  return lg_dispatch(a, nob, g.spd != nullptr, lg_unal(g), 0, nullptr, false);
+  return lg_dispatch(a, nob, g.spd != nullptr, lg_unal(g), lg_f32(g), g.mask != nullptr, 0, nullptr, false);
 }
 
 int lgemm_pack(const GemmArgs& g, void* img, hipStream_t s) {
@@ -472,6 +562,7 @@ int lgemm_pack(const GemmArgs& g, void* img, hipStream_t s) {
   p.bias = g.bias;
   p.bout = (float*)((char*)img + (size_t)G * p.kst * p.NOB * 2 * LG_FRAG);
   p.nbias = G * p.NOB * 16;
+  p.f32 = lg_f32(g) ? 1 : 0;
   // hi and lo fragments interleave; one thread per (fragment, lane, element), then the bias columns
   hipLaunchKernelGGL(k_limg_pack, dim3((unsigned)((p.total + p.nbias + 255) / 256)), dim3(256), 0, s, p);
   return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -482,7 +573,7 @@ int lgemm_run(const GemmArgs& g, const void* img, int cus, hipStream_t s) {
   LGemm a = lg_args(g, &nob);
   a.img = (const uint4*)img;
   a.bimg = (const f32x4*)((const char*)img + (size_t)a.G * a.kst * nob * 2 * LG_FRAG);
-  if (!lg_dispatch(a, nob, g.spd != nullptr, lg_unal(g), cus, s, true)) return -1;
+  if (!lg_dispatch(a, nob, g.spd != nullptr, lg_unal(g), lg_f32(g), g.mask != nullptr, cus, s, true)) return -1;
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -135,12 +135,20 @@ struct G {
   int cus;
   int spd_h = 0;  // the spd operands of bwd / bwd_top hold softplus outputs h (GemmArgs::spd_h)
   float spd_scale = 0.f;  // ... stored as h / spd_scale (GemmArgs::spd_scale)
+  // exact fp32 precision: the layer GEMMs that fit k_lgemm run on its F32 kernels (exact fp32 MFMA,
+  // fp32 weight image resident in LDS) instead of k_gemm_t (ANR_SDF_LG32=0: k_gemm_t throughout)
+  bool lg() const {
+    if (x3) return true;
+    const char* v = getenv("ANR_SDF_LG32");
+    return !(v && v[0] == '0');
+  }
   int run(GemmArgs g) {
     if (M <= 0 || g.N <= 0) return ANR_OK;
     g.M = M;
     g.x3 = x3;
     g.ksplit = 1;
-    if (x3 && limg && lgemm_supported(g)) {
+    if (lg() && limg && lgemm_supported(g)) {
+      g.prof = !x3;  // the exact render's clock (anr_profile_read_clock) from these launches' stamps
       if (const void* img = limg->get(g, s)) {
         (void)lgemm_run(g, img, cus, s);
         return check_launch("k_lgemm (sdf)");
@@ -154,9 +162,9 @@ struct G {
   // run, and the caller materialises G7 with k_sdf_gtop instead
   bool bwd_top(float* dX, long ldX, int K, const float* D7, const float* w8, int Nout, const float* W, int in_ch,
                const float* spd, int spd_n) {
-    if (!x3 || !limg || M <= 0) return false;
+    if (!lg() || !limg || M <= 0) return false;
     GemmArgs g{};
-    g.M = M; g.N = K; g.nseg = 1; g.x3 = 1; g.ksplit = 1;
+    g.M = M; g.N = K; g.nseg = 1; g.x3 = x3; g.ksplit = 1; g.prof = !x3;
     g.seg[0] = GemmSeg{D7, 256, 1, W, in_ch, 1, Nout};
     g.C = dX; g.ldc = ldX;
     g.spd = spd; g.ldsd = 256; g.spd_n = spd_n; g.spd_h = spd_h;
@@ -187,9 +195,9 @@ struct G {
   // caller runs the two GEMMs
   bool fwd_head(float* Yh, long ldh, int nh, const float* Wh, const float* bh, const float* W, int in_ch,
                 const float* bias, const float* X, long ldX, int K) {
-    if (!x3 || !limg || M <= 0) return false;
+    if (!lg() || !limg || M <= 0) return false;
     GemmArgs g{};
-    g.M = M; g.N = 256; g.nseg = 1; g.x3 = 1; g.ksplit = 1;
+    g.M = M; g.N = 256; g.nseg = 1; g.x3 = x3; g.ksplit = 1; g.prof = !x3;
     g.seg[0] = GemmSeg{X, ldX, 1, W, 1, in_ch, K};
     g.C = Yh; g.ldc = 4;  // not written (HEAD); kept valid for the support checks
     g.bias = bias; g.relu = 1;

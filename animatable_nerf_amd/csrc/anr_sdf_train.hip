@@ -549,12 +549,14 @@ struct TG {
                         a.K, two ? b.K : 0, g.N, img};
     return img;
   }
+  int lg32 = 0;  // exact fp32 products on k_lgemm's F32 kernels (resident fp32 weight image) where they fit
   int run(GemmArgs g, int M) {
     if (M <= 0 || g.N <= 0) return ANR_OK;
     g.M = M;
     if (g.ksplit < 1) g.ksplit = 1;
     if (x3 && !g.atomic) g.x3 = 1;
-    if (g.x3 && lg_arena && lgemm_supported(g)) {
+    if ((g.x3 || lg32) && lg_arena && lgemm_supported(g)) {
+      g.prof = 1;  // the step's clock (anr_profile_read_clock) from these launches' stamps
       if (void* img = lg_image(g)) {
         if (lgemm_run(g, img, cus, s) != 0) return check_launch("k_lgemm (sdf train)");
         return ANR_OK;
@@ -815,12 +817,18 @@ int sdf_train_core(const TrainCore& C) {
     g.x3 = x3_on && (x3_parts & bit) ? 1 : 0;
     g.wg_x3 = x3_on && ((g.x3 && (x3_parts & 64)) || (x3_parts & 128)) ? 1 : 0;
   };
-  if (x3_on) {
-    g.slab = F(L.wslab);
+  // ANR_SDF_LG32 (read per call, default 1): the exact-fp32 forward / input-gradient products that fit
+  // k_lgemm (no accumulate / atomics, 16-B addressable rows) run on its F32 kernels — the layer's fp32
+  // weight image resident in LDS, activations streamed to registers, v_mfma_f32_16x16x4_f32 — instead of
+  // k_gemm_t's register-staged 64 x 64 tiles (8.0 VALU instructions per MFMA, profiles/r4q_sq_k_gemm_t)
+  const char* lg32_env = getenv("ANR_SDF_LG32");
+  g.lg32 = !(lg32_env && lg32_env[0] == '0');
+  if (x3_on || g.lg32) {
     g.lg_arena = ws + L.lgimg;
     g.lg_cap = kLgArena;
     g.cus = cus;
   }
+  if (x3_on) g.slab = F(L.wslab);
   const dim3 pb(256), pg((n + 255) / 256 + 1);
   auto WN = [&](int l) { return (const float*)wimg + wn_layer(l).off; };
   float* dWe = F(L.dWe);

@@ -27,6 +27,7 @@
 #include <type_traits>
 
 #include "anr_common.h"
+#include "anr_kernels.h"
 #include "anr_train.h"
 
 namespace anr {
@@ -591,10 +592,11 @@ __device__ __forceinline__ void tc_body(const TcArgs& a) {
   }
 }
 
-__global__ __launch_bounds__(512) void k_tchain_bw(TcArgs a) { tc_body<0>(a); }
-__global__ __launch_bounds__(512) void k_tchain_nf(TcArgs a) { tc_body<1>(a); }
-__global__ __launch_bounds__(512) void k_tchain_bwb(TcArgs a) { tc_body<2>(a); }
-__global__ __launch_bounds__(512) void k_tchain_nfb(TcArgs a) { tc_body<3>(a); }
+// (entry / exit clock stamps of thread 0 when profiling: anr_profile_read_clock's in-kernel clock)
+__global__ __launch_bounds__(512) void k_tchain_bw(TcArgs a) { ANR_STAMPED(tc_body<0>(a)); }
+__global__ __launch_bounds__(512) void k_tchain_nf(TcArgs a) { ANR_STAMPED(tc_body<1>(a)); }
+__global__ __launch_bounds__(512) void k_tchain_bwb(TcArgs a) { ANR_STAMPED(tc_body<2>(a)); }
+__global__ __launch_bounds__(512) void k_tchain_nfb(TcArgs a) { ANR_STAMPED(tc_body<3>(a)); }
 
 }  // namespace
 
@@ -645,8 +647,11 @@ int tchain_run(int prog, const TcArgs& a, int cap, int cus, hipStream_t s) {
   const int grid = tiles < cus ? tiles : cus;
   if (grid <= 0) return 0;
   TcArgs args = a;
+  ProfSlot* ps = prof_begin(s, grid);
+  args.clk = ps ? ps->clk : nullptr;
   void* kargs[] = {&args};
   if (hipLaunchKernel(k, dim3(grid), dim3(512), kargs, lds, s) != hipSuccess) return -1;
+  if (prof_end(ps, s) != 0) return -1;
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -52,6 +52,7 @@ struct GemmArgs {
   int head_n;
   int bf16;            // operands rounded to bf16, bf16 MFMA, fp32 accumulate (training precision)
   int x3;              // operands split hi + lo (bf16 each), three bf16 MFMAs per product (fp32-level)
+  int prof;            // k_lgemm: a profiling slot (anr_profile_*: events + per-workgroup clock stamps)
   // weight-gradient GEMMs (A(m,k) = dY[k][m]): the fp32 row sums of A over this launch's k range
   // (= the bias gradient, the column sums of dY) are atomically added into rowsum[m] (and rowsum2[m])
   // by the workgroups of the first N tile; NULL: off
@@ -199,6 +200,7 @@ struct TcArgs {
   float* aux;             // backward: the gamma gradient rows (fp32): layer 5 stores (adds when aux_acc), layer 0 adds
   int ld_aux, aux_cols, aux_acc;
   const int* M_dev;       // kept-sample count (device)
+  unsigned long long* clk;  // anr_profile_*: per-workgroup clock stamps (set by tchain_run when profiling)
 };
 size_t tchain_image_bytes(int prog);
 int tchain_pack(int prog, TcPackArgs a, void* dst, hipStream_t s);

@@ -489,6 +489,14 @@ def bench_train(args, rank, world, dev, emit=True):
         dist.barrier()
     dt = time.perf_counter() - t0
     dt_max = max_over_ranks(dt, dev, world)
+    # the in-kernel shader clock (anr_profile_read_clock: entry / exit stamps of the fused chain launches)
+    # over 3 more steps profiled after the timed ones, so events and stamps stay out of the timed region
+    step.lib.anr_profile_enable(1)
+    step.lib.anr_profile_read(None, None)
+    for j in range(3):
+        step.step(batches[j % nb])
+    torch.cuda.synchronize()
+    chain_ms, n_chain, mhz = profile_read(step.lib)
     R = int(batches[0]['ray_o'].shape[1])
     loss = step.loss3.cpu().tolist()
     # kept samples of the last step (host read inside anr_train_step)
@@ -508,7 +516,11 @@ def bench_train(args, rank, world, dev, emit=True):
                    'parallelism': f'dp{world} (RCCL mean all-reduce of the flat gradient blob)'},
         'roofline': {'bound': 'mfma', 'kernel': 'whole step', 'achieved': achieved, 'peak': peak,
                      'unit': 'TFLOP/s', 'frac': achieved / peak, 'traffic': None,
-                     'flop_per_kept': FLOP_PER_KEPT_TRAIN},
+                     'flop_per_kept': FLOP_PER_KEPT_TRAIN,
+                     'clock_mhz': mhz if n_chain else None,
+                     'clock_source': 'median over workgroups of the fused chain launches (anr_tchain.hip), '
+                                     '3 profiled steps after the timed ones',
+                     'chain_launch_ms_per_step': chain_ms / 3 if n_chain else None},
         'loss_last_step': loss[:3],
         'host_issue_ms_per_step': host / args.steps * 1e3,
     }
@@ -570,7 +582,7 @@ def bench_sdf(args, rank, world, dev, emit=True):
         if world > 1:
             dist.barrier()
         dt = time.perf_counter() - t0
-        ms, n, mhz = profile_read(lib)  # the fused network launches (split precisions; none in exact fp32)
+        ms, n, mhz = profile_read(lib)  # the fused network launches (split precisions; k_lgemm in exact fp32)
         timed.net = {'network_launch_ms_per_frame': ms / steps, 'network_launches_per_frame': n / steps,
                      'clock_mhz': mhz if n else None}
         return o, max_over_ranks(dt, dev, world), r.last_counts[0]
@@ -585,7 +597,10 @@ def bench_sdf(args, rank, world, dev, emit=True):
              'flop_per_kept': FLOP_PER_KEPT_SDF, 'flop_per_kept_executed': flop_exec,
              'achieved_credited': n_kept * FLOP_PER_KEPT_SDF / dt_step / 1e12}
         r.update(timed.net)
-        if timed.net['network_launches_per_frame']:
+        if prec == 'fp32':  # the profiled launches are the exact path's k_lgemm layer GEMMs, not the whole network
+            r['lgemm_launch_ms_per_frame'] = r.pop('network_launch_ms_per_frame')
+            r['lgemm_launches_per_frame'] = r.pop('network_launches_per_frame')
+        elif timed.net['network_launches_per_frame']:
             # the four fused network launches alone (k_resd / k_sdfnet / k_sdfgrad / k_color)
             r['network_frac'] = achieved * dt_step * 1e3 / timed.net['network_launch_ms_per_frame'] / peak
         return r
@@ -700,6 +715,14 @@ def bench_sdf_train(args, rank, world, dev, emit=True):
     if world > 1:
         dist.barrier()
     dt_max = max_over_ranks(time.perf_counter() - t0, dev, world)
+    # in-kernel clock of the step's k_lgemm layer products (exact fp32 F32 kernels), 2 profiled steps after
+    # the timed ones
+    step.lib.anr_profile_enable(1)
+    step.lib.anr_profile_read(None, None)
+    for j in range(2):
+        one(j)
+    torch.cuda.synchronize()
+    lg_ms, n_lg, mhz = profile_read(step.lib)
     R = int(batches[0]['ray_o'].shape[1])
     losses = dict(zip(LOSS_KEYS, l8.cpu().tolist()))  # rank means (the losses ride in the all-reduced blob)
     n_kept = losses['n_kept']
@@ -721,7 +744,11 @@ def bench_sdf_train(args, rank, world, dev, emit=True):
         'roofline': {'bound': 'mfma', 'kernel': 'whole step (layer GEMMs dominate)', 'achieved': achieved,
                      'peak': peak, 'unit': 'TFLOP/s', 'frac': achieved / peak,
                      'traffic': None, 'flop_per_kept_executed_main_path': 2 * MAC_SDF_TRAIN,
-                     'kept_samples_per_step': n_kept},
+                     'kept_samples_per_step': n_kept,
+                     'clock_mhz': mhz if n_lg else None,
+                     'clock_source': 'median over workgroups of the k_lgemm layer products, 2 profiled steps '
+                                     'after the timed ones',
+                     'lgemm_launches_per_step': n_lg / 2, 'lgemm_ms_per_step': lg_ms / 2},
         'losses_last_step_rank_mean': losses,
     }
     if not emit:

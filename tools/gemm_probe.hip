@@ -14,9 +14,15 @@
 #include <vector>
 
 #include "../animatable_nerf_amd/csrc/anr_common.h"
+#include "../animatable_nerf_amd/csrc/anr_kernels.h"
 #include "../animatable_nerf_amd/csrc/anr_train.h"
 
 using namespace anr;
+namespace anr {
+// the library's profiling slots (anr_capi.hip) are not linked into the probe: profiling off
+ProfSlot* prof_begin(hipStream_t, int) { return nullptr; }
+int prof_end(ProfSlot*, hipStream_t) { return 0; }
+}  // namespace anr
 namespace anr {
 void rg_timing_buffer(unsigned long long* p);  // the probe's RG_TIMING build of anr_tgemm.hip
 }
@@ -415,6 +421,36 @@ int main(int argc, char** argv) {
         if (!img_l) CK(hipMalloc(&img_l, lgemm_image_bytes(g)));
         if (lgemm_pack(g, img_l, s) != 0) { fprintf(stderr, "lgemm_pack failed\n"); return 1; }
         out("lgemm_x3_fwd", time_us(s, reps, [&] { lgemm_run(g, img_l, cus, s); }), (double)M * 256 * 8, fl);
+      }
+      if (mode == 0 && lgemm_supported(g)) {  // exact fp32 on k_lgemm's F32 kernel, checked against k_gemm_t
+        if (!img_l) CK(hipMalloc(&img_l, lgemm_image_bytes(g)));
+        if (lgemm_pack(g, img_l, s) != 0) { fprintf(stderr, "lgemm_pack failed\n"); return 1; }
+        GemmArgs h = g;
+        h.C = C2;
+        out("lgemm_f32_fwd", time_us(s, reps, [&] { lgemm_run(h, img_l, cus, s); }), (double)M * 256 * 8, fl);
+        launch_gemm(g, dim3((N + 63) / 64, (M + 63) / 64, 1), s);
+        CK(hipStreamSynchronize(s));
+        printf("{\"check\": \"lgemm_f32_fwd vs gemm_t_f32_fwd\", \"M\": %d, \"max_rel\": %.3g}\n", M,
+               max_rel_diff(C2, C, (size_t)M * 256));
+        // masked input-gradient shape (dX = (dY W) * (H > 0)): the mask rows of Mk
+        GemmArgs x{};
+        x.N = 256; x.nseg = 1; x.M = M;
+        x.seg[0] = GemmSeg{A, 256, 1, W, 256, 1, 256};
+        x.C = C; x.ldc = 256; x.mask = Mk; x.ldm = 256; x.ksplit = 1;
+        if (lgemm_supported(x)) {
+          void* img_x;
+          CK(hipMalloc(&img_x, lgemm_image_bytes(x)));
+          if (lgemm_pack(x, img_x, s) != 0) { fprintf(stderr, "lgemm_pack failed\n"); return 1; }
+          GemmArgs y = x;
+          y.C = C2;
+          out("lgemm_f32_xgrad_mask", time_us(s, reps, [&] { lgemm_run(y, img_x, cus, s); }), (double)M * 256 * 12, fl);
+          out("gemm_t_f32_xgrad_mask", time_us(s, reps, [&] { launch_gemm(x, dim3(4, (M + 63) / 64, 1), s); }),
+              (double)M * 256 * 12, fl);
+          CK(hipStreamSynchronize(s));
+          printf("{\"check\": \"lgemm_f32_xgrad_mask vs gemm_t\", \"M\": %d, \"max_rel\": %.3g}\n", M,
+                 max_rel_diff(C2, C, (size_t)M * 256));
+          CK(hipFree(img_x));
+        }
       }
     }
     // weight gradients dW += dY^T X over the M rows (+ bias column sums)
