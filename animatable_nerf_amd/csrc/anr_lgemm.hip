@@ -265,6 +265,67 @@ __device__ __forceinline__ void lg_load_mask(const LGemm& g, f32x4 (&mk)[NOB], i
   }
 }
 
+// F32: one tile with the whole tile's activations copied out of the load ring first (real copies,
+// then every refill of the next tile issued at once), so the ring's loads are a whole tile old when they
+// are copied. The per-k-step refill of the split variants (copy, refill, MFMAs) let the compiler rename
+// the refill targets from tile to tile; at the tile loop's back edge it then lost track of which load
+// fills which register and waited for every load (vmcnt(0)) at each tile's first k-step, exposing one
+// HBM round trip per tile. Fragments of a k-step are read up front and the MFMAs run element-major
+// (NOB independent accumulators between two uses of one).
+template <int NOB, int KST, int KST0, bool SPD, bool UNAL, bool ATR, bool HEAD, bool FULLK, bool MASK>
+__device__ __forceinline__ void lg_tile_f32(const LGemm& g, f32x4 (&buf)[KST][2], int tile, int next, int n0,
+                                            int lane, const unsigned char* lds, const float* atr_lds) {
+  f32x4 sp[NOB], mk[NOB];
+  lg_load_spd<NOB, SPD>(g, sp, tile, n0, lane);
+  lg_load_mask<NOB, MASK>(g, mk, tile, n0, lane);
+  const int kg = lane >> 4;
+  float xa[KST][8];
+#pragma unroll
+  for (int ks = 0; ks < KST; ++ks)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      xa[ks][e] = buf[ks][e >> 2][e & 3];
+      asm volatile("v_mov_b32 %0, %1" : "=v"(xa[ks][e]) : "v"(xa[ks][e]));
+    }
+#pragma unroll
+  for (int ks = 0; ks < KST; ++ks) lg_load_ks<KST0, UNAL, FULLK>(g, buf[ks], next, ks, lane);
+  __builtin_amdgcn_sched_barrier(0);
+  f32x4 acc[NOB];
+#pragma unroll
+  for (int ob = 0; ob < NOB; ++ob) acc[ob] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int frag_off = lane * 16;
+  asm volatile("" : "+v"(frag_off));
+#pragma unroll
+  for (int ks = 0; ks < KST; ++ks) {
+    const bool s1 = ks >= KST0;
+    const int K = s1 ? g.seg[1].K : g.seg[0].K;
+    const int k0 = 32 * (ks - (s1 ? KST0 : 0));
+    float* x = xa[ks];
+    if constexpr (ATR) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float w = atr_lds[k0 + lg_kcol(kg, e)];
+        x[e] = g.spd_h ? w * softplus_factor_h(x[e]) : x[e] >= 0.f ? w * x[e] * __builtin_amdgcn_rcpf(x[e] + 1.f) : w;
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      if constexpr (!FULLK) x[e] = (k0 + lg_kcol(kg, e) < K) ? x[e] : 0.0f;
+    const unsigned char* fr = lds + ks * NOB * 2 * LG_FRAG + frag_off;
+    f32x4 w[2][NOB];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int ob = 0; ob < NOB; ++ob) w[h][ob] = *(const f32x4*)(fr + (2 * ob + h) * LG_FRAG);
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+#pragma unroll
+      for (int ob = 0; ob < NOB; ++ob)
+        acc[ob] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[e >> 2][ob][e & 3], x[e], acc[ob], 0, 0, 0);
+  }
+  lg_epilogue<NOB, SPD, HEAD, MASK>(g, acc, sp, mk, atr_lds + 32 * KST + 1024, tile, n0, lane, atr_lds + 32 * KST);
+}
+
 // one tile on a k-step ring: this tile's factor loads go out first; each k-step's activations are
 // split hi/lo and their registers immediately refilled with the same k-step of the wave's next tile
 // (so one tile of loads is always in flight, in one tile's worth of registers), then the MFMAs;
@@ -302,13 +363,10 @@ __device__ __forceinline__ void lg_tile(const LGemm& g, f32x4 (&buf)[KST][2], in
 #pragma unroll
     for (int e = 0; e < 8; ++e)
       if constexpr (!FULLK) x[e] = (k0 + lg_kcol(kg, e) < K) ? x[e] : 0.0f;
-    if constexpr (F32) {
+    if constexpr (F32) {  // the shapes lg_tile_f32 cannot hold in registers: the per-k-step ring
       lg_load_ks<KST0, UNAL, FULLK>(g, buf[ks], next, ks, lane);
       __builtin_amdgcn_sched_barrier(0);
       const unsigned char* fr = lds + ks * NOB * 2 * LG_FRAG + frag_off;
-      // every fragment of the k-step read up front (elements 0..3 of all out-blocks first), then the MFMAs
-      // element-major: NOB independent accumulators between two uses of one (a per-out-block chain of 8
-      // dependent MFMAs with its reads right before it measured 0.43 of the fp32 peak, the reads exposed)
       f32x4 w[2][NOB];
 #pragma unroll
       for (int h = 0; h < 2; ++h)
@@ -391,13 +449,21 @@ __global__ __launch_bounds__(LG_WAVES * 64) void k_lgemm(LGemm g) {
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nw = g.bpg * LG_WAVES;
   const int T = (g.M + 15) >> 4;
-  int t = rank * LG_WAVES + w;
+  // first tiles: waves 0..3 of every workgroup before waves 4..7, so the waves that get one tile more
+  // than the rest (T is rarely a multiple of nw) are at most one per SIMD (waves w and w + 4 share a
+  // SIMD): the busiest SIMD carries ceil(2 T / nw) tiles instead of 2 ceil(T / nw)
+  int t = (w >> 2) * (g.bpg * 4) + rank * 4 + (w & 3);
   if (t >= T) return;
   f32x4 buf[KST][2];
 #pragma unroll
   for (int ks = 0; ks < KST; ++ks) lg_load_ks<KST0, UNAL>(g, buf[ks], t, ks, lane);
-  for (; t < T; t += nw)
-    lg_tile<NOB, KST, KST0, SPD, UNAL, ATR, HEAD, FULLK, F32, MASK>(g, buf, t, t + nw, n0, lane, lds, atr_lds);
+  for (; t < T; t += nw) {
+    // the whole-tile copy needs KST x 8 more registers: taken where it compiles without spills
+    if constexpr (F32 && KST <= 8 && !SPD && !ATR)
+      lg_tile_f32<NOB, KST, KST0, SPD, UNAL, ATR, HEAD, FULLK, MASK>(g, buf, t, t + nw, n0, lane, lds, atr_lds);
+    else
+      lg_tile<NOB, KST, KST0, SPD, UNAL, ATR, HEAD, FULLK, F32, MASK>(g, buf, t, t + nw, n0, lane, lds, atr_lds);
+  }
   if (w == 0) clk_stamp(g.clk, 1);
 }
 

@@ -550,6 +550,7 @@ struct TG {
     return img;
   }
   int lg32 = 0;  // exact fp32 products on k_lgemm's F32 kernels (resident fp32 weight image) where they fit
+  int wg32 = 0;  // exact fp32 weight gradients on k_wgrad_f32 (slab + reduce) where they fit
   int run(GemmArgs g, int M) {
     if (M <= 0 || g.N <= 0) return ANR_OK;
     g.M = M;
@@ -592,6 +593,15 @@ struct TG {
       w.dW = dW + c0; w.ldw = in_ch; w.bsum = bsum; w.slab = slab;
       if (launch_wgrad(w, M, s) != 0) return check_launch("k_wgrad (sdf train)");
       return ANR_OK;
+    }
+    if (!wg_x3 && wg32 && slab) {  // exact fp32: k_wgrad_f32 where its operand shapes fit
+      WGrad w{};
+      w.dY = dY; w.ldY = ldY; w.nout = Nout; w.X = X; w.ldX = ldX; w.K = K;
+      w.dW = dW + c0; w.ldw = in_ch; w.bsum = bsum; w.slab = slab;
+      if (wgrad_f32_fits(w)) {
+        if (launch_wgrad_f32(w, M, s) != 0) return check_launch("k_wgrad_f32 (sdf train)");
+        return ANR_OK;
+      }
     }
     GemmArgs g{};
     g.rowsum = bsum;
@@ -828,7 +838,11 @@ int sdf_train_core(const TrainCore& C) {
     g.lg_cap = kLgArena;
     g.cus = cus;
   }
-  if (x3_on) g.slab = F(L.wslab);
+  // ANR_SDF_WG32 (read per call, default 1): the exact weight gradients on k_wgrad_f32 instead of k_gemm_t's
+  // atomic split-K (~4.7 M fp32 atomics per 36k-row 256 x 256 product)
+  const char* wg32_env = getenv("ANR_SDF_WG32");
+  g.wg32 = !(wg32_env && wg32_env[0] == '0');
+  g.slab = F(L.wslab);
   const dim3 pb(256), pg((n + 255) / 256 + 1);
   auto WN = [&](int l) { return (const float*)wimg + wn_layer(l).off; };
   float* dWe = F(L.dWe);

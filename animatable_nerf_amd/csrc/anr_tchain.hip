@@ -14,14 +14,15 @@
 // bias, ReLU, then RNE to bf16 for the stored rows AND for the next layer's operand (the values the
 // layer-wise path reads back), so the backward sees the same activations.
 //
-// Layout: workgroup = 8 waves x 16 samples (a 128-sample tile), persistent over tiles. v_mfma_f32_16x16x32_bf16
-// with the weights as the A operand (16 output neurons x 32 inputs) and the samples as B: the C
-// layout of out-blocks 2s, 2s+1 (lane l: neurons 32s + 4(l>>4) + r and 32s + 16 + 4(l>>4) + r of sample
-// l & 15) is the B fragment of the next layer's k-step s when the packed weight columns follow the same
-// order (tc_nrn), so activations never leave registers. Memory segments (gamma rows, gamma(dir) rows)
-// are read straight into B fragments in natural column order. Weights stream through a 4-slot LDS ring
-// of slices (one 32-input k-step of all of a layer's out-blocks, <= 17 KiB) by LDS-DMA, one barrier per
-// slice with counted vmcnt waits (the render kernel's scheme, anr_mlp_body.h Pipe); biases sit in an LDS
+// Layout: workgroup = 7 compute waves x 16 samples (a 112-sample tile, TC_TR) + 1 producer wave,
+// persistent over tiles (below, before tc_body). v_mfma_f32_16x16x32_bf16 with the weights as the A
+// operand (16 output neurons x 32 inputs) and the samples as B: the C fragment of out-blocks 2s, 2s+1 is
+// the B fragment of the next layer's k-step s when the packed weight columns follow the same neuron
+// order (tc_nrn: lane h of a sample holds neurons 32s + 8h + 0..7, one 16-B row store per k-step pair),
+// so activations never leave registers. Memory segments (gamma rows, gamma(dir) rows) are read straight
+// into B fragments in natural column order. Weights stream through an LDS ring of slices (one 32-input
+// k-step of all of a layer's out-blocks, <= 20 KiB; 8 slots BW, 6 NeRF, 7 backward) by LDS-DMA that the
+// producer wave alone issues and waits for (counted vmcnt), one barrier per slice; biases sit in an LDS
 // table filled once per launch. Each layer's outputs are stored once (bf16 rows for the backward's
 // masks and weight gradients; fp32 heads) while the next layer's MFMAs run.
 #include <type_traits>

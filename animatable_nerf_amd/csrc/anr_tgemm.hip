@@ -11,6 +11,7 @@
 // accumulation; the activations rounded to bf16 RNE as their fragments are read, as the generic
 // kernel rounds them at staging). LDS images are XOR-swizzled through the DMA source addresses.
 // Epilogue order as anr_gemm.hip: bias, accumulate, ReLU, mask.
+#include <algorithm>
 #include <vector>
 
 #include "anr_common.h"
@@ -1029,6 +1030,160 @@ __global__ __launch_bounds__(512) void k_wgrad_dma(WGradGroup G) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) g.rs_slab[(long)z * 256 + i0 + 16 * a + 4 * (lane >> 4) + r] = rsum[a][r];
   }
+}
+
+// ------------------------------------------------------------------------------------------
+// k_wgrad_f32: exact-fp32 weight gradients dW += dY^T X (+ column sums of dY) for the exact-fp32
+// executors (the sdf_pdf training step's 'fp32' precision), v_mfma_f32_16x16x4_f32 with fp32 operands
+// as stored — the products k_gemm_t's atomic split-K computes, without its register staging (8 VALU
+// instructions per MFMA, profiles/r4q_sq_k_gemm_t) or its 4.7 M atomics per 36k-row product.
+// Workgroup = one 128 x 128 tile of dW (8 waves of 32 x 64) over one sample range; dY and X rows of the
+// tile stream through a 4-slot LDS ring of 16-sample stages by LDS-DMA (8 KiB each, [sample][128 cols],
+// 16-B chunks XOR-swizzled by 4 on odd rows so the ds_read_b32 fragment reads — rows 4 ks + (lane >> 4),
+// 16 consecutive columns — are conflict-free). Partial tiles go to the slab layout of k_wgrad (reduce
+// unchanged); column sums are MFMAs of the dY fragments against ones.
+// ------------------------------------------------------------------------------------------
+#define WF_ST 32                   // samples per stage
+#define WF_NB 4                    // ring slots
+#define WF_IMG (WF_ST * WG_T * 4)  // one image: 32 rows x 128 fp32
+#define WF_SLOT (2 * WF_IMG)
+
+__device__ __forceinline__ float wf_read(const unsigned char* img, int row, int col) {
+  const int ch = (col >> 2) ^ ((row & 1) << 2);
+  return *(const float*)(img + row * (WG_T * 4) + ch * 16 + (col & 3) * 4);
+}
+
+__global__ __launch_bounds__(512) void k_wgrad_f32(WGrad g) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tiles = g.tiles;
+  const int b = blockIdx.x;
+  const int t = b % tiles, z = b / tiles;
+  const int ti = t / g.tj, tj = t - ti * g.tj;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int n = g.M_dev ? *g.M_dev : g.n;
+  const int spb = ((n + g.nz - 1) / g.nz + WF_ST - 1) / WF_ST * WF_ST;
+  const int s0 = z * spb, s1 = min(n, s0 + spb);
+  const int nst = s1 > s0 ? (s1 - s0 + WF_ST - 1) / WF_ST : 0;
+  const int i0 = ti * WG_T, j0 = tj * WG_T;
+  // 8 waves of 32 x 64 (two waves per SIMD: the fragment reads of one hide behind the other's MFMAs)
+  const int wi = (wave >> 1) * 32, wj = (wave & 1) * 64;
+  const bool rs = g.rs_slab != nullptr && tj == 0;
+  // a wave's pieces of a stage: image im (0 dY, 1 X), 1 KiB pieces p = wave, wave + 8: rows 2 p, 2 p + 1
+  // (32 chunks of 16 B each), LDS chunk q of row r holds source chunk q ^ 4 (r & 1)
+  auto issue = [&](int st) {
+    const unsigned char* slot = smem + (st % WF_NB) * WF_SLOT;
+#pragma unroll
+    for (int im = 0; im < 2; ++im)
+#pragma unroll
+    for (int h = 0; h < WF_ST / 16; ++h) {
+      const float* base = im ? g.X : g.dY;
+      const long ld = im ? g.ldX : g.ldY;
+      const int c0 = im ? j0 : i0, cn = im ? g.K : g.nout;
+      const int p = wave + 8 * h;
+      const int r = 2 * p + (lane >> 5);
+      const int q = (lane & 31) ^ ((r & 1) << 2);
+      int c = c0 + 4 * q;
+      c = (c < cn && c + 4 <= ld) ? c : 0;  // chunks past the columns: any in-bounds bytes (discarded)
+      const int srow = min(s0 + st * WF_ST + r, s1 - 1);
+      const float* src = base + (size_t)srow * ld + c;
+      const unsigned m0 = (unsigned)(uintptr_t)(slot + im * WF_IMG + p * 1024);
+      asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(m0) : "memory");
+    }
+  };
+  f32x4 acc[2][4], rsum[2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+    rsum[a] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[a][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  for (int st = 0; st < WF_NB - 1 && st < nst; ++st) issue(st);
+  for (int st = 0; st < nst; ++st) {
+    const int after = min(st + WF_NB - 2, nst - 1) - st;  // stages issued after st: WF_OPS pieces each
+    constexpr int WF_OPS = 2 * (WF_ST / 16);
+    if (after >= 2) wd_wait<2 * WF_OPS>();
+    else if (after == 1) wd_wait<WF_OPS>();
+    else wd_wait<0>();
+    __syncthreads();
+    unsigned char* slot = smem + (st % WF_NB) * WF_SLOT;
+    const int vr = s1 - (s0 + st * WF_ST);
+    if (vr < WF_ST) {  // the range's last stage: rows past it read as zero (uniform branch)
+      for (int e = tid; e < 2 * (WF_ST - vr) * 32; e += 512) {
+        const int im = e / ((WF_ST - vr) * 32), rem = e % ((WF_ST - vr) * 32);
+        *(uint4*)(slot + im * WF_IMG + (vr + rem / 32) * (WG_T * 4) + (rem % 32) * 16) = make_uint4(0u, 0u, 0u, 0u);
+      }
+      __syncthreads();
+    }
+    if (st + WF_NB - 1 < nst) issue(st + WF_NB - 1);  // the slot of stage st - 1: every wave is past it
+    float fa[WF_ST / 4][2], fb[WF_ST / 4][4];
+#pragma unroll
+    for (int ks = 0; ks < WF_ST / 4; ++ks) {
+      const int row = 4 * ks + (lane >> 4);
+#pragma unroll
+      for (int a = 0; a < 2; ++a) fa[ks][a] = wf_read(slot, row, wi + 16 * a + (lane & 15));
+#pragma unroll
+      for (int c = 0; c < 4; ++c) fb[ks][c] = wf_read(slot + WF_IMG, row, wj + 16 * c + (lane & 15));
+    }
+#pragma unroll
+    for (int ks = 0; ks < WF_ST / 4; ++ks) {
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          acc[a][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[ks][a], fb[ks][c], acc[a][c], 0, 0, 0);
+      // the column sums of the wave pair's 32 dY columns, one block per wave (even: a = 0, odd: a = 1), so
+      // both waves of a pair issue the same MFMA count between barriers
+      if (rs) rsum[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[ks][wave & 1], 1.0f, rsum[0], 0, 0, 0);
+    }
+  }
+  // partial tile in k_wgrad's slab layout: quadrant q = 2 (wi / 64) + wj / 64 (64 x 64, blocks (a', c) of
+  // 16 x 16, a' = (wi % 64) / 16 + a), the lane's float4
+  const int qd = 2 * (wi / 64) + wj / 64, a0 = (wi % 64) / 16;
+  float* slab = g.slab + ((long)(z * tiles + t) * 4 + qd) * 16 * 256;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) *(f32x4*)(slab + ((a0 + a) * 4 + c) * 256 + lane * 4) = acc[a][c];
+  if (rs && (lane & 15) == 0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) g.rs_slab[(long)z * 256 + i0 + wi + 16 * (wave & 1) + 4 * (lane >> 4) + r] = rsum[0][r];
+  }
+}
+
+// can k_wgrad_f32 take this product (16-B addressable rows, whole 16-B chunks of columns)
+bool wgrad_f32_fits(const WGrad& g) {
+  return !g.x3 && !g.ybf && !g.xbf && g.nout >= 1 && g.nout <= 256 && g.K >= 1 && g.K <= 256 && g.ldY >= 4 &&
+         g.ldX >= 4 && g.ldY % 4 == 0 && g.ldX % 4 == 0 && ((uintptr_t)g.dY & 15) == 0 && ((uintptr_t)g.X & 15) == 0;
+}
+
+static int wgrad_reduce_blocks(const WGrad& g);
+
+int launch_wgrad_f32(WGrad g, int n_host, hipStream_t s) {
+  if (n_host <= 0) return 0;
+  if (!wgrad_f32_fits(g)) return -1;
+  const int ti = (g.nout + WG_T - 1) / WG_T, tj = (g.K + WG_T - 1) / WG_T;
+  g.tj = tj;
+  g.tiles = ti * tj;
+  // sample ranges: about two workgroups per CU, within the slab region (tiles x nz <= 4 WG_MAX_Z)
+  int nz = (512 + g.tiles - 1) / g.tiles;
+  nz = std::min(nz, std::max(1, (n_host + 4 * WF_ST - 1) / (4 * WF_ST)));  // at least 4 stages per range
+  nz = std::max(1, std::min(nz, std::min(WG_MAX_Z, 4 * WG_MAX_Z / g.tiles)));
+  g.nz = nz;
+  g.n = n_host;
+  g.rs_slab = (g.bsum || g.bsum2) ? g.slab + (size_t)WG_MAX_Z * 4 * WG_TILE_FLOATS : nullptr;
+  static bool attr[64] = {};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (dev < 0 || dev >= 64 || !attr[dev]) {
+    if (hipFuncSetAttribute((const void*)k_wgrad_f32, hipFuncAttributeMaxDynamicSharedMemorySize, WF_NB * WF_SLOT) !=
+        hipSuccess)
+      return -1;
+    if (dev >= 0 && dev < 64) attr[dev] = true;
+  }
+  hipLaunchKernelGGL(k_wgrad_f32, dim3(g.tiles * g.nz), dim3(512), WF_NB * WF_SLOT, s, g);
+  hipLaunchKernelGGL(k_wgrad_reduce, dim3(wgrad_reduce_blocks(g)), dim3(256), 0, s, g);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 static int wgrad_reduce_blocks(const WGrad& g) {

@@ -140,6 +140,11 @@ struct WGrad {
 };
 size_t wgrad_slab_floats();
 int launch_wgrad(WGrad g, int n_host, hipStream_t s);
+// exact-fp32 weight gradient (k_wgrad_f32 + k_wgrad_reduce; fp32 rows, nout / K <= 256, 16-B addressable
+// rows): the exact executors' dW += dY^T X (+ bsum / bsum2 column sums), ACCUMULATED like the atomic
+// split-K GEMM it replaces; -1 (nothing launched) for a product it does not take
+bool wgrad_f32_fits(const WGrad& g);
+int launch_wgrad_f32(WGrad g, int n_host, hipStream_t s);
 // several weight gradients in two launches (k_wgrad_group + k_wgrad_reduce_group): d[0..nd) as for
 // launch_wgrad (dY, X, dW, bsum, M_dev, formats; slab fields ignored) with nz sample ranges each, their
 // partial slabs packed into slab[0, slab_floats); more descriptors than fit one launch (WG_GROUP_MAX, or

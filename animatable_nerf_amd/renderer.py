@@ -179,14 +179,24 @@ class Renderer:
                        'anr_render_bw_rows')
         return pbw, tbw
 
+    def _last_device_ws(self, what):
+        """The workspace of the last render_device() call. render() renders a frame in parts on two
+        workspaces, so after it no single workspace describes the frame: use last_counts there."""
+        ws = getattr(self, '_last_ws', None)
+        if ws is None:
+            raise RuntimeError(f'Renderer.{what} describes the last render_device() call; the last render was '
+                               'render() (the frame in parts): use Renderer.last_counts')
+        return ws
+
     def row_ids(self, n_rays):
-        """Sample ids (ray * N_samples + sample) of the alpha_ind rows of the last evaluation render, (m,)
+        """Sample ids (ray * N_samples + sample) of the alpha_ind rows of the last render_device(), (m,)
         int64 on the device, in row order (anr_render_row_ids)."""
-        _, m = self._counts(self._ws, n_rays)
-        ids = torch.empty((m,), dtype=torch.int32, device=self._ws.device)
+        ws = self._last_device_ws('row_ids()')
+        _, m = self._counts(ws, n_rays)
+        ids = torch.empty((m,), dtype=torch.int32, device=ws.device)
         if m > 0:
-            _lib.check(self.lib.anr_render_row_ids(_lib.ptr(self._ws), n_rays, _lib.ptr(ids),
-                                                   _lib.stream_ptr(self._ws.device)), 'anr_render_row_ids')
+            _lib.check(self.lib.anr_render_row_ids(_lib.ptr(ws), n_rays, _lib.ptr(ids),
+                                                   _lib.stream_ptr(ws.device)), 'anr_render_row_ids')
         return ids.long()
 
     def _t_rand(self, R, dev, t_rand):
@@ -209,6 +219,7 @@ class Renderer:
         _lib.check(self.lib.anr_render_fwd(ctypes.byref(p), ctypes.byref(c.frame), *c.ray_ptrs(), R,
                                            ctypes.byref(c.opts), ctypes.byref(c.out), _lib.ptr(ws), ws_bytes,
                                            _lib.stream_ptr(dev)), 'anr_render_fwd')
+        self._last_ws = ws
         ret = {'rgb_map': c.rgb, 'acc_map': c.acc, 'depth_map': c.depth, 'raw': c.raw}
         if bw_rows:
             ret['pbw'], ret['tbw'] = self._bw_rows(ws, R, dev)
@@ -281,7 +292,10 @@ class Renderer:
             h = {'rgb_map': torch.empty((1, R, 3), **pin), 'acc_map': torch.empty((1, R), **pin),
                  'depth_map': torch.empty((1, R), **pin), 'raw': torch.empty((1, R * ns, 4), **pin)}
             st = dict(late=[], kept=0, off=0, hp=None, ht=None, keep=[], k=0)
-            est = int(getattr(self, '_rows_est', 0))
+            self._last_ws = None  # the parts alternate between two workspaces (row_ids / counts refuse)
+            # the previous frame's row count, when it had the same rays (another frame size: extrapolated)
+            est_R, est_m = getattr(self, '_rows_est', (0, 0))
+            est = int(est_m) if est_R == R else 0
             ws_free = [None, None]  # per workspace: an event on cs after its last part's rows were extracted
 
             def finish(part):
@@ -355,15 +369,21 @@ class Renderer:
                 hp, ht = ep, et
             cs.synchronize()
             cur.wait_stream(cs)  # later work on the caller's stream may reuse the workspaces
+            if hp.shape[1] > 2 * m + 4096:
+                # the estimate overshot (another frame's rows): exact-size buffers, so the returned tensors
+                # hold no capacity-sized host allocation
+                hp = torch.empty((1, m, 24), **pin).copy_(hp[:, :m])
+                ht = torch.empty((1, m, 24), **pin).copy_(ht[:, :m])
             h['pbw'] = hp[:, :m]
             h['tbw'] = ht[:, :m]
-        self._rows_est = m
+        self._rows_est = (R, m)
         self.last_counts = (st['kept'], m)
         return h
 
     def counts(self, n_rays):
-        """(kept samples, alpha_ind rows) of the last evaluation render (device read, syncs)."""
-        return self._counts(self._ws, n_rays)
+        """(kept samples, alpha_ind rows) of the last render_device() (device read, syncs); after render()
+        (the frame in parts) see last_counts."""
+        return self._counts(self._last_device_ws('counts()'), n_rays)
 
     # ---- Network.forward over free samples (tpose_nerf_network.py:139-215) -----------------
     def network_forward(self, wpts, viewdir, dists, batch):

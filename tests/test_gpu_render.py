@@ -247,8 +247,11 @@ def test_render_overlapped_host_copy_equals_device_render(renderer, dev):
     assert again['raw'].data_ptr() != got['raw'].data_ptr()
     assert torch.equal(got['raw'], ref['raw'])
     # the second call sizes the alpha_ind row buffers from the first's count (rows placed as parts
-    # finish); a too-small estimate moves the placed rows into exact-size buffers
-    for est in (None, 1):
+    # finish); a too-small estimate moves the placed rows into exact-size buffers, a far too large one
+    # (a bigger frame's) is trimmed to exact size, and an estimate for another ray count is not used
+    R = int(bt['ray_o'].shape[1])
+    m = int(ref['pbw'].shape[1])
+    for est in (None, (R, 1), (R, 40 * m + 100000), (R + 1, 1)):
         if est is not None:
             renderer._rows_est = est
         with torch.no_grad():
@@ -256,6 +259,13 @@ def test_render_overlapped_host_copy_equals_device_render(renderer, dev):
         for k in ('rgb_map', 'acc_map', 'depth_map', 'raw', 'pbw', 'tbw'):
             assert got[k].shape == again[k].shape and torch.equal(again[k], ref[k]), (k, est)
         assert again['pbw'].is_contiguous() and again['pbw'].is_pinned()
+        # no capacity-sized host allocation behind the returned rows
+        assert again['pbw'].untyped_storage().nbytes() <= (2 * m + 4096 + 64) * 24 * 4 * 1.2, est
+    # after render() (the frame in parts on two workspaces) the per-workspace queries refuse
+    with pytest.raises(RuntimeError):
+        renderer.row_ids(R)
+    renderer.render_device(bt)
+    assert renderer.row_ids(R).shape[0] == m
 
 
 @pytest.mark.parametrize('world', [3, 8])

@@ -470,6 +470,41 @@ int main(int argc, char** argv) {
       g.seg[0] = GemmSeg{A, 1, 256, Mk, 256, 1, M};
       g.C = dW; g.ldc = 256; g.atomic = 1; g.ksplit = (M + 511) / 512; g.kper = 512; g.M = 256;
       out("wgrad_gemm_t_f32", time_us(s, reps, [&] { launch_gemm(g, dim3(4, 4, g.ksplit), s); }), (double)M * 256 * 8, fl);
+      // the exact slab kernel on the same operands, checked against one clean split-K accumulation
+      WGrad w{};
+      w.dY = A; w.ldY = 256; w.nout = 256; w.X = Mk; w.ldX = 256; w.K = 256;
+      w.dW = dW2; w.ldw = 256; w.bsum = bsum; w.slab = slab;
+      out("wgrad_f32_slab", time_us(s, reps, [&] { launch_wgrad_f32(w, M, s); }), (double)M * 256 * 8, fl);
+      CK(hipMemsetAsync(dW, 0, 256 * 256 * 4, s));
+      CK(hipMemsetAsync(dW2, 0, 256 * 256 * 4, s));
+      launch_gemm(g, dim3(4, 4, g.ksplit), s);
+      if (launch_wgrad_f32(w, M, s) != 0) { fprintf(stderr, "launch_wgrad_f32 failed\n"); return 1; }
+      CK(hipStreamSynchronize(s));
+      printf("{\"check\": \"wgrad_f32_slab vs gemm_t split-K\", \"M\": %d, \"max_rel\": %.3g}\n", M,
+             max_rel_diff(dW2, dW, 256 * 256));
+      // a K = 63 / ld 64 product with column sums (the gamma columns of a first layer)
+      WGrad v = w;
+      v.K = 63; v.ldX = 64; v.X = Mk;
+      GemmArgs h{};
+      h.rowsum = bsum; h.N = 63; h.nseg = 1;
+      h.seg[0] = GemmSeg{A, 1, 256, Mk, 64, 1, M};
+      h.C = dW; h.ldc = 256; h.atomic = 1; h.ksplit = (M + 511) / 512; h.kper = 512; h.M = 256;
+      CK(hipMemsetAsync(dW, 0, 256 * 256 * 4, s));
+      CK(hipMemsetAsync(dW2, 0, 256 * 256 * 4, s));
+      CK(hipMemsetAsync(bsum, 0, 256 * 4, s));
+      launch_gemm(h, dim3(1, 4, h.ksplit), s);
+      std::vector<float> b1(256), b2(256);
+      CK(hipStreamSynchronize(s));
+      CK(hipMemcpy(b1.data(), bsum, 1024, hipMemcpyDeviceToHost));
+      CK(hipMemsetAsync(bsum, 0, 256 * 4, s));
+      v.ldw = 256; v.dW = dW2;
+      if (launch_wgrad_f32(v, M, s) != 0) { fprintf(stderr, "launch_wgrad_f32 (K 63) failed\n"); return 1; }
+      CK(hipStreamSynchronize(s));
+      CK(hipMemcpy(b2.data(), bsum, 1024, hipMemcpyDeviceToHost));
+      double mb = 0, sb = 0;
+      for (int i = 0; i < 256; ++i) { mb = std::max(mb, (double)std::fabs(b1[i] - b2[i])); sb = std::max(sb, (double)std::fabs(b1[i])); }
+      printf("{\"check\": \"wgrad_f32_slab K=63 vs gemm_t\", \"M\": %d, \"max_rel\": %.3g, \"bsum_rel\": %.3g}\n", M,
+             max_rel_diff(dW2, dW, 256 * 256), sb > 0 ? mb / sb : mb);
     }
     const long n16 = (long)M * 256 * 2 / 16;
     out("copy_bf16_rows", time_us(s, reps, [&] {
