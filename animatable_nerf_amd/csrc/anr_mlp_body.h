@@ -432,21 +432,40 @@ __device__ __forceinline__ float softplus100(float x) {
 }
 
 // the fp32-level programs (V >= 10): torch's softplus(beta = 100, threshold = 20) = log1p(exp(100 x)) /
-// 100 on the libm-grade fast_exp / fast_log1p (<= 2e-7 relative), and the backward factor
-// sigmoid(100 z) = 1 - exp(-100 h) = -expm1(-100 h) from the output h (a short series where 100 h is
-// small, so the factor keeps its relative precision where it is tiny)
-__device__ __forceinline__ float softplus100_acc(float x) {
-  const float z = 100.f * x;
-  return z > 20.f ? x : div_const(fast_log1p(fast_exp(z)), 100.f, 0.00999999977648258f);
-}
-__device__ __forceinline__ float softplus_factor_h_acc(float h) {
-  const float t = 100.f * h;
-  return t < 0.03125f ? t * (1.f - t * (0.5f - t * (0.166666672f - t * 0.0416666679f))) : 1.f - fast_exp(-t);
+// 100 and its backward factor sigmoid(100 x) = e / (1 + e) (torch's softplus_backward: z / (z + 1),
+// z = exp(100 x)) from ONE exp and ONE log, both within ~2 ulp of fp64 over the whole range (numpy
+// emulation with correctly rounded exp2 / log2: <= 4.3 units of 2^-24 relative; torch's own fp32
+// evaluation is off by up to 65 there, its RN(100 x) amplified by the exp):
+//   e = 2^(x C) with C = 100 log2(e) as C_hi + C_lo and the residual of x C_hi exact by FMA, so the
+//       hardware exp2 sees the argument to ~2^-48 and e = 2^a (1 + a_lo ln2);
+//   log1p(e) = log(u) + (e - (u - 1)) / u with u = RN(1 + e): e - (u - 1) is the exact rounding error
+//       of 1 + e (Sterbenz), so where 1 + e rounds the correction restores log1p's relative precision.
+// Above torch's threshold (100 x > 20) softplus returns x and passes the gradient: here the argument
+// is clamped to 0.4 (no overflow: e <= e^40) and h = max(h, x), which is x wherever log1p(exp(-100 x))
+// / 100 < x's half ulp (from 100 x ~ 17 on, within ~1 ulp of torch's x between 20 and 40), and the
+// factor e / (1 + e) is 1 within an ulp there. No compare masks: 15 VALU + 3 transcendentals for the
+// pair, against ~27 + 3 for the libm-grade fast_exp / fast_log1p softplus alone and ~15 + 1 more for
+// the factor recomputed from h (1 - exp(-100 h), with a series) in the reverse pass: the bf16x6 SDF
+// forward stores the factor itself, its input gradient multiplies.
+__device__ __forceinline__ float softplus100_fac(float x, float& fac) {
+  constexpr float C_HI = 144.26950073242188f, C_LO = 3.356474508109386e-06f;
+  constexpr float LN2 = 0.6931471824645996f;
+  const float xc = fminf(x, 0.4f);
+  const float a = xc * C_HI;
+  const float a_lo = __builtin_fmaf(xc, C_LO, __builtin_fmaf(xc, C_HI, -a));
+  const float E = __builtin_amdgcn_exp2f(a);
+  const float e = __builtin_fmaf(E, a_lo * LN2, E);
+  const float u = 1.f + e;
+  const float err = e - (u - 1.f);
+  const float ru = __builtin_amdgcn_rcpf(u);
+  fac = e * ru;
+  return fmaxf(__builtin_fmaf(__builtin_amdgcn_logf(u), LN2, err * ru) * 0.01f, x);
 }
 template <int V>
-__device__ __forceinline__ float sp_fwd(float x) { return V >= 10 ? softplus100_acc(x) : softplus100(x); }
-template <int V>
-__device__ __forceinline__ float sp_factor(float h) { return V >= 10 ? softplus_factor_h_acc(h) : softplus_factor_h(h); }
+__device__ __forceinline__ float sp_fwd(float x) {
+  static_assert(V < 10, "the fp32-level programs use softplus100_fac");
+  return softplus100(x);
+}
 
 // SP_IN (the sdf network, V = 5): the previous layer's softplus(beta = 100) is applied in this layer's
 // split like RELU_IN (its VALU work beside this layer's MFMAs), and the softplus outputs h of the
@@ -718,11 +737,11 @@ __device__ __forceinline__ void layer(Pipe& p, const f32x4 (&in)[NIN], const flo
           x[j] = RELU_IN ? fmaxf(in[2 * ts][j], 0.0f) : in[2 * ts][j];
           x[4 + j] = RELU_IN ? fmaxf(in[2 * ts + 1][j], 0.0f) : in[2 * ts + 1][j];
         }
-        if constexpr (FAC_IN != 0) {
+        if constexpr (FAC_IN != 0) {  // the forward stored the softplus factors themselves (softplus100_fac)
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            x[j] = x[j] * sp_factor<V>(hv[tt & 1][0][j] * io.fscale);
-            x[4 + j] = x[4 + j] * sp_factor<V>(hv[tt & 1][1][j] * io.fscale);
+            x[j] = x[j] * hv[tt & 1][0][j];
+            x[4 + j] = x[4 + j] * hv[tt & 1][1][j];
             if constexpr (FAC_IN == 2) {  // lin3: 217 inputs; the rest are gamma gradients (and X4's padding)
               x[j] = 32 * ts + 4 * g + j < 217 ? x[j] : 0.0f;
               x[4 + j] = 32 * ts + 16 + 4 * g + j < 217 ? x[4 + j] : 0.0f;
@@ -730,21 +749,22 @@ __device__ __forceinline__ void layer(Pipe& p, const f32x4 (&in)[NIN], const flo
           }
           load_h(std::integral_constant<int, tt + 1>{});
         }
-        if constexpr (SP_IN != 0) {
+        if constexpr (SP_IN != 0) {  // h for this split, the backward factors to spst for the reverse pass
+          // neurons 32 ts + 4 g + (0..3) and 32 ts + 16 + 4 g + (0..3), each half stored as it is done
+          float* d = io.spst ? io.spst + 32 * ts + 4 * g : nullptr;
+          const int c = 32 * ts + 4 * g;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) x[j] = sp_fwd<V>(x[j]);
-          if (io.spst) {  // neurons 32 ts + 4 g + (0..3) and 32 ts + 16 + 4 g + (0..3)
-            float* d = io.spst + 32 * ts + 4 * g;
-            if constexpr (SP_IN == 1) {
-              __builtin_nontemporal_store(f32x4{x[0], x[1], x[2], x[3]}, (f32x4*)d);
-              __builtin_nontemporal_store(f32x4{x[4], x[5], x[6], x[7]}, (f32x4*)(d + 16));
-            } else {
-              const float sqrt2 = 1.41421356237309515f, rs2 = 0.707106769084930420f;  // RN(1 / RN(sqrt2))
-              const int c = 32 * ts + 4 * g;
+          for (int q = 0; q < 2; ++q) {
+            float f[4];
 #pragma unroll
-              for (int j = 0; j < 4; ++j) {
-                if (c + j < 217) d[j] = div_const(x[j], sqrt2, rs2);
-                if (c + 16 + j < 217) d[16 + j] = div_const(x[4 + j], sqrt2, rs2);
+            for (int j = 0; j < 4; ++j) x[4 * q + j] = softplus100_fac(x[4 * q + j], f[j]);
+            if (d) {
+              if constexpr (SP_IN == 1) {
+                __builtin_nontemporal_store(f32x4{f[0], f[1], f[2], f[3]}, (f32x4*)(d + 16 * q));
+              } else {  // lin3: 217 neurons (X4's columns past them are the skip's gamma inputs)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                  if (c + 16 * q + j < 217) d[16 * q + j] = f[j];
               }
             }
           }
@@ -1371,7 +1391,9 @@ __device__ __forceinline__ void softplus_regs(f32x4 (&v)[17]) {
 // [h3 || gamma_6] / sqrt2 at lin4 (the 1/sqrt2 is in lin4's packed weights), lin8. What the reverse
 // pass (the input gradient) and the colour net read is written once: every softplus output h (lin3's
 // as h / sqrt2 in X4, the layout of the layer-GEMM path) and lin8's sdf (Y8 column 0) and feature
-// (Y8 columns 8..263: 16-B aligned for k_color_b16's row loads).
+// (Y8 columns 8..263: 16-B aligned for k_color_b16's row loads). bf16x6 (V = 15) writes the backward
+// factors sigmoid(100 z) in those slots instead (lin3's unscaled in X4[:, :217]): softplus100_fac
+// gives them beside h, and the reverse pass then multiplies without recomputing them.
 template <bool X6>
 __device__ __forceinline__ void sdfnet_body(const MlpArgs& a) {
   constexpr int V = 5 + (X6 ? 10 : 0);
@@ -1423,8 +1445,19 @@ __device__ __forceinline__ void sdfnet_body(const MlpArgs& a) {
     layer<true, V, 5, false, false, 1>(p, A, emb, vemb, B, sb, g, lane, st(4));
     layer<true, V, 6, false, false, 1>(p, B, emb, vemb, A, sb, g, lane, st(5));
     layer<true, V, 7, false, false, 1>(p, A, emb, vemb, B, sb, g, lane, st(6));
-    softplus_regs<16, V>(B);  // lin8 (a tail-slice layer, not streamed) reads h7 as is
-    store_h(B, a.sdf_h[7]);
+    if constexpr (X6) {  // h7 in place for lin8, its backward factors to sdf_h[7]
+      float* d = a.sdf_h[7] + row * 256 + 4 * g;
+      static_for<0, 16>([&](auto ob) {
+        constexpr int o = decltype(ob)::value;
+        float f[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) B[o][r] = softplus100_fac(B[o][r], f[r]);
+        if (valid) *(f32x4*)(d + 16 * o) = f32x4{f[0], f[1], f[2], f[3]};
+      });
+    } else {
+      softplus_regs<16, V>(B);  // lin8 (a tail-slice layer, not streamed) reads h7 as is
+      store_h(B, a.sdf_h[7]);
+    }
     layer<true, V, 8, false>(p, B, emb, vemb, A, sb, g, lane);  // [sdf || feature], no activation
     if (valid) {  // sdf (neuron 0) to column 0, the feature (neurons 1..256) to columns 8..263
       float* d = a.y8 + row * 264;
@@ -1446,7 +1479,7 @@ __device__ __forceinline__ void sdfnet_body(const MlpArgs& a) {
 // sdf_pdf SDF network input gradient (V = 7): d sdf / d x (the autograd.grad of anisdf_pdf_network.py
 // :302-311 through SDFNetwork.forward) per kept sample of one batch, on chip. The gradient vector is the
 // MFMA B operand, lin7^T .. lin0^T the weights; each layer's input is multiplied by the softplus-backward
-// factor recomputed from the forward's stored h (FAC_IN). Writes the gamma_6 gradients (lin0's, and
+// factor recomputed from the forward's stored h (FAC_IN; bf16x6: the stored factor itself). Writes the gamma_6 gradients (lin0's, and
 // the skip part of lin4's) for k_sdf_gamma_bwd. Replaces 8 reverse layer GEMMs over HBM activations.
 template <bool X6>
 __device__ __forceinline__ void sdfgrad_body(const MlpArgs& a) {
@@ -1486,7 +1519,7 @@ __device__ __forceinline__ void sdfgrad_body(const MlpArgs& a) {
         const f32x4 hv = *(const f32x4*)(h7 + 16 * o);
         const f32x4 wv = *(const f32x4*)(sw8 + 16 * o + 4 * g);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) A[o][r] = wv[r] * sp_factor<V>(hv[r]);
+        for (int r = 0; r < 4; ++r) A[o][r] = wv[r] * (X6 ? hv[r] : softplus_factor_h(hv[r]));  // X6: stored factors
       });
     }
     const float sqrt2 = 1.41421356237309515f;

@@ -385,7 +385,8 @@ def side_legs(args, rank, world, dev):
     """Configs 3-5 timed inside the default run (so the driver's own bench call measures them too):
     'train_step' (config 3 at N = 1, config 4 at N > 1: the training iteration with its RCCL gradient
     all-reduce), and at N = 1 'sdf_render' (config 5's network, bf16x6 fp32-level render of a 512x512
-    frame, exact fp32 beside it) and 'sdf_train_step' (config 5's training iteration, exact fp32). Each
+    frame, exact fp32 beside it) and 'sdf_train_step' (config 5's training iteration, exact fp32); at
+    every N 'mesh_extract' (aninerf mesh extraction, 5 mm grid) and 'anim_step' (animation stage). Each
     is the full --mode leg at a short step count; its JSON line is returned instead of printed."""
     import copy
     out = {}
@@ -406,6 +407,10 @@ def side_legs(args, rank, world, dev):
     if world == 1:
         leg(bench_sdf, 'sdf_render', steps=3, warmup=1, no_exact=False, sdf_exact_only=True)
         leg(bench_sdf_train, 'sdf_train_step', steps=10, warmup=3)
+    # SURVEY §8(f) rows in the driver's line too: mesh extraction of one frame (5 mm grid) and the
+    # animation-stage training step (aninerf_animation_trainer.py)
+    leg(bench_mesh, 'mesh_extract', steps=2, warmup=1)
+    leg(bench_anim, 'anim_step', steps=10, warmup=3)
     return out
 
 
@@ -765,7 +770,7 @@ MAC_NERF_TRUNK = 491_264
 FLOP_PER_KEPT_ALPHA = 2 * (MAC_BW + MAC_NERF_TRUNK)
 
 
-def bench_mesh(args, rank, world, dev):
+def bench_mesh(args, rank, world, dev, emit=True):
     """Mesh extraction (aninerf_mesh_renderer.py:26-63) of one frame per GPU at the reference's
     voxel size (5 mm): get_alpha over every grid voxel (`inside` all ones: an upper bound of the
     masked grid the dataset produces), the density volume, device marching cubes. Replicas."""
@@ -855,13 +860,15 @@ def bench_mesh(args, rank, world, dev):
                                   'sample': f'first {m} grid points ({m // (2048 * 64)} reference chunks), oracle/restate.py '
                                             f'mesh_alpha (get_alpha only), {dtc:.1f} s'}
         result['alpha_max_abs_err_vs_oracle'] = float((alpha[:m].cpu() - ref).abs().max())
+    if not emit:
+        return result
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
 
-def bench_anim(args, rank, world, dev):
+def bench_anim(args, rank, world, dev, emit=True):
     """Animation stage (aninerf_animation_trainer.py): one step = 65,536 observation-space + 65,536
     canonical points (get_sampling_points), forward + backward of both paths (anr_anim_step), RCCL
     mean all-reduce of the novel_pose_bw gradient blob (N > 1), clip + Adam. Weak scaling."""
@@ -902,6 +909,8 @@ def bench_anim(args, rank, world, dev):
                    'points_per_step': pts, 'parallelism': f'dp{world} (RCCL mean all-reduce of the novel_pose_bw blob)'},
         'roofline': None, 'loss_last_step': st.loss3.cpu().tolist(),
     }
+    if not emit:
+        return result
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
