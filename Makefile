@@ -17,6 +17,11 @@ all: $(LIB)
 $(SRC_DIR)/%.o: $(SRC_DIR)/%.hip
 	$(HIPCC) $(CXXFLAGS) -MMD -MP -c $< -o $@
 
+# the bf16x6 programs without SLP vectorisation: clang pairs the splits' scalar f32 subtractions into
+# v_pk_add_f32, which costs more issue cycles beside MFMAs than two v_sub_f32 (same-box A/B round 6:
+# sdf_pdf bf16x6 frame 180.0 -> 175.8 ms, k_mlp_x6 cycles -2.4 %, profiles/round6/r8b_*)
+$(SRC_DIR)/anr_mlp_x6.o $(SRC_DIR)/anr_resd_x6.o: CXXFLAGS += -fno-slp-vectorize
+
 $(LIB): $(OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@.tmp $(OBJS) && mv -f $@.tmp $@
 
