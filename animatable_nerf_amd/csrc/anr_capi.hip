@@ -106,12 +106,12 @@ int stage_frontend(const anr_params* p, const anr_frame* f, const float* ray_o, 
   const long nt = (long)f->tbw_dims[0] * f->tbw_dims[1] * f->tbw_dims[2];
   const int nch = (R + o->chunk - 1) / o->chunk;
   int* counts = (int*)(ws + L.counts);
-  if (hipMemsetAsync(ws + L.counts, 0, 16, s) != hipSuccess ||
-      hipMemsetAsync(ws + L.chunk_min, 0xff, (size_t)nch * 8, s) != hipSuccess ||
-      hipMemsetAsync(ws + L.chunk_max, 0, (size_t)nch * 8, s) != hipSuccess)
-    return fail(ANR_E_HIP, "hipMemsetAsync failed");
 
   PrepArgs pa{};
+  pa.counts = counts;  // counts, chunk_min and chunk_max reset by k_prep's block 0
+  pa.chunk_min = (uint64_t*)(ws + L.chunk_min);
+  pa.chunk_max = (uint64_t*)(ws + L.chunk_max);
+  pa.nch = nch;
   pa.pbw = f->pbw; pa.tbw = f->tbw;
   pa.pbw32 = (float*)(ws + L.pbw32); pa.tbw32 = (float*)(ws + L.tbw32);
   pa.np = (int)np; pa.nt = (int)nt;
@@ -173,6 +173,10 @@ int stage_frontend(const anr_params* p, const anr_frame* f, const float* ray_o, 
   ca.ray_off = (int*)(ws + L.ray_off);
   ca.block_sum = (int*)(ws + L.block_sum);
   ca.list = (int*)(ws + L.list);
+  if (R <= 1024) {  // a training batch: one launch
+    hipLaunchKernelGGL(k_compact1, dim3(1), dim3(1024), 0, s, ca, counts);
+    return check_launch("k_compact1");
+  }
   const int nb = (R + 255) / 256;
   hipLaunchKernelGGL(k_count, dim3(nb), dim3(256), 0, s, ca);
   ANR_TRY(check_launch("k_count"));

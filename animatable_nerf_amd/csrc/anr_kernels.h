@@ -183,6 +183,11 @@ struct PrepArgs {
   // = alpha_fc's bias; skipped when head_P is NULL (callers without the bf16x3 render program)
   const float *head_P, *head_q, *b_alpha;
   float* pn24;  // (np) channel 24 of pbw, compact, for the front-end's prefilter lookups (or NULL)
+  // the render front-end's per-call state, reset here instead of by three memset launches ahead of this
+  // one (block 0; NULL: nothing): counts[0..3] = 0, chunk_min[0..nch) = ~0, chunk_max[0..nch) = 0
+  int* counts;
+  uint64_t *chunk_min, *chunk_max;
+  int nch;
 };
 // k_prep launch size for np + nt voxels (the folded biases and head included)
 int prep_blocks(long np, long nt);
@@ -200,6 +205,8 @@ __global__ void k_frontend_pts(FrontArgs a);
 __global__ void k_count(CompactArgs a);
 __global__ void k_scan_blocks(int* sums, int nb, int* total_out);
 __global__ void k_compact(CompactArgs a);
+// R <= 1024 rays (a training batch): k_count + k_scan_blocks + k_compact as one 1024-thread workgroup
+__global__ void k_compact1(CompactArgs a, int* total_out);
 __global__ void k_chunk_argmax(AlphaArgs a);
 __global__ void k_flag_count(AlphaArgs a);
 __global__ void k_flag_force(AlphaArgs a, int nchunks);

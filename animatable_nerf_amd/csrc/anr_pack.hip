@@ -305,6 +305,13 @@ __global__ void k_pack_head_b(PackArgs a) {
 // (5 x 256 of them, a 128-term dot each: lane q sums terms q and q + 64, then a wave reduction), then
 // one wave per folded-head entry (fp64 dot over the 128 latent dims)
 __global__ __launch_bounds__(256) void k_prep(PrepArgs a) {
+  if (blockIdx.x == 0 && a.counts) {  // the front-end's per-call state (k_frontend runs after this launch)
+    if (threadIdx.x < 4) a.counts[threadIdx.x] = 0;
+    for (int i = threadIdx.x; i < a.nch; i += 256) {
+      a.chunk_min[i] = ~0ull;
+      a.chunk_max[i] = 0ull;
+    }
+  }
   const int nvb = (a.np + a.nt + 7) / 8;  // 8 voxels (x 32 channels) per block
   if ((int)blockIdx.x < nvb) {
     const int v = blockIdx.x * 8 + (threadIdx.x >> 5);

@@ -425,6 +425,54 @@ __global__ __launch_bounds__(256) void k_compact(CompactArgs a) {
   if (ray == a.n_rays - 1 && lane == 0) a.ray_off[a.n_rays] = off + __popcll(m);
 }
 
+// R <= 1024: the three passes above in one workgroup (a ray per thread for the count and the scan, then
+// a wave per ray for the ordered writes, as k_compact); same mask, ray_off (global, with ray_off[R] =
+// the total), list and total as k_count + k_scan_blocks + k_compact
+__global__ __launch_bounds__(1024) void k_compact1(CompactArgs a, int* __restrict__ total_out) {
+  __shared__ int sh[16];
+  __shared__ uint64_t sm[1024];
+  __shared__ int so[1024];
+  const int ray = threadIdx.x;
+  const int lane = ray & 63, w = ray >> 6;
+  uint64_t m = 0;
+  if (ray < a.n_rays) {
+    m = a.mask[ray];
+    const uint64_t key = a.chunk_min[ray / a.chunk];
+    const uint32_t idx = (uint32_t)(key & 0xffffffffu);
+    if ((int)(idx >> 6) == (ray + a.ray_offset) % a.chunk) m |= 1ull << (idx & 63);
+    a.mask[ray] = m;
+  }
+  const int cnt = __popcll(m);
+  int x = cnt;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int y = __shfl_up(x, off);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) sh[w] = x;
+  __syncthreads();
+  int pre = 0, tot = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int v = sh[k];
+    pre += k < w ? v : 0;
+    tot += v;
+  }
+  const int off = pre + x - cnt;
+  sm[ray] = m;
+  so[ray] = off;
+  if (ray < a.n_rays) a.ray_off[ray] = off;
+  if (ray == 0) {
+    a.ray_off[a.n_rays] = tot;
+    *total_out = tot;
+  }
+  __syncthreads();
+  for (int r = w; r < a.n_rays; r += 16) {
+    const uint64_t mr = sm[r];
+    if ((mr >> lane) & 1ull) a.list[so[r] + __popcll(mr & ((1ull << lane) - 1ull))] = r * 64 + lane;
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // alpha_ind (tpose_nerf_network.py:186-196): sigma' > train_th, plus per-chunk argmax(sigma')
 // ------------------------------------------------------------------------------------------

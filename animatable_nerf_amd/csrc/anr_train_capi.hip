@@ -159,16 +159,18 @@ int order(SideStreams* ss, hipStream_t to, hipStream_t from) {
 // was the legacy default stream. The cause (found in round 5) was not the stream kind: Exec::pend_src
 // marked "no queued source stream" with nullptr, which is also the legacy default stream's handle, so a
 // product queued from stream 0 never recorded its source and flush_w() issued the group on lane 0 with
-// no edge after stream 0. pend_src now carries an explicit count (npsrc). The fork stays (one event each
-// way) so that the library's streams never wait on a blocking caller stream; ANR_TRAIN_ON_CALLER=1
-// (read per call) bypasses it, which tests/test_gpu_train.py uses to run the grouped path on stream 0.
+// no edge after stream 0. pend_src now carries an explicit count (npsrc). Round 6: the caller's stream
+// is the main stream by default (the library's side streams are non-blocking, so they order against the
+// legacy stream through events like against any other): the fork's two cross-stream edges cost ~20-35 us
+// a step (1.035 / 1.055 vs 1.017 ms, profiles/round6/r8d_*). ANR_TRAIN_ON_CALLER=0 (read per call)
+// restores the fork onto a library-owned non-blocking stream.
 struct OnMain {
   SideStreams* ss;
   hipStream_t caller, s;
   int rc = ANR_OK;
   OnMain(SideStreams* x, hipStream_t c) : ss(x), caller(c), s(c) {
     const char* oc = getenv("ANR_TRAIN_ON_CALLER");
-    if (ss && ss->main && !(oc && oc[0] == '1')) {
+    if (ss && ss->main && oc && oc[0] == '0') {
       rc = order(ss, ss->main, caller);
       s = ss->main;
     }

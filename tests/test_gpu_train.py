@@ -395,11 +395,13 @@ def test_direct_call_reused_dict_sees_new_batch(dev):
     assert not torch.allclose(fresh[0, :3], fresh[1, :3])
 
 
-def test_grouped_wgrad_from_legacy_default_stream(dev, monkeypatch):
+@pytest.mark.parametrize('on_caller', ['1', '0'])
+def test_grouped_wgrad_from_legacy_default_stream(dev, monkeypatch, on_caller):
     """Regression for the round-4 NaN: grouped weight gradients queued from
     the legacy default stream (handle 0) were flushed with no edge after that stream, because 'no source
     stream' was marked with the same null handle. The caller's stream is used as the executor's main
-    stream here (ANR_TRAIN_ON_CALLER=1 bypasses the library-owned fork), right after an fp32 run in the
+    stream here (ANR_TRAIN_ON_CALLER=1, the default since round 6; '0' forks onto the library's own
+    non-blocking stream and back), right after an fp32 run in the
     same process (its workspace holds fp32 rows where bf16_all keeps bf16: an unordered read shows up as
     NaN / garbage). The bf16_all step must equal the single-stream step (ANR_TRAIN_SERIAL=1) up to
     atomics order."""
@@ -426,7 +428,7 @@ def test_grouped_wgrad_from_legacy_default_stream(dev, monkeypatch):
         return grads
 
     steps('fp32')
-    monkeypatch.setenv('ANR_TRAIN_ON_CALLER', '1')
+    monkeypatch.setenv('ANR_TRAIN_ON_CALLER', on_caller)
     got = steps('bf16_all')
     monkeypatch.setenv('ANR_TRAIN_SERIAL', '1')
     ref = steps('bf16_all')

@@ -1,5 +1,6 @@
 """Summarise one training step from a rocprofv3 kernel trace: per-kernel totals between the last two
-k_adam dispatches. usage: python tools/train_trace_summary.py <run_kernel_trace.csv>"""
+k_adam dispatches, or the K-th last step (bench.py --mode train profiles 3 steps after the timed ones,
+so K = 4 is the last timed step). usage: python tools/train_trace_summary.py <run_kernel_trace.csv> [K]"""
 import collections
 import csv
 import sys
@@ -7,7 +8,8 @@ import sys
 rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r['Start_Timestamp']))
 idx = [i for i, r in enumerate(rows) if 'k_adam' in r['Kernel_Name']]
-a, b = idx[-2], idx[-1]
+K = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+a, b = idx[-1 - K], idx[-K]
 step = rows[a + 1:b + 1]
 t0, t1 = int(step[0]['Start_Timestamp']), int(step[-1]['End_Timestamp'])
 busy = sum(int(r['End_Timestamp']) - int(r['Start_Timestamp']) for r in step)
