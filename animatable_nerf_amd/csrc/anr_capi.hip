@@ -253,10 +253,16 @@ int stage_alpha_ind(int R, const anr_render_opts* o, char* ws, const Layout& L, 
   aa.list = (const int*)(ws + L.list);
   aa.mask = (const uint64_t*)(ws + L.mask);
   aa.ray_offset = split ? split->ray_offset : 0;
+  const int nb2 = (int)((N + 1023) / 1024);
+  if (nch == 1 && nb2 <= 64 && !split) {  // a training batch: two launches (chunk_max[0] is 0 from k_prep)
+    hipLaunchKernelGGL(k_alpha_count1, dim3(nb2), dim3(256), 0, s, aa);
+    ANR_TRY(check_launch("k_alpha_count1"));
+    hipLaunchKernelGGL(k_alpha_scatter1, dim3(nb2), dim3(256), 0, s, aa, counts + 1);
+    return check_launch("k_alpha_scatter1");
+  }
   hipLaunchKernelGGL(k_chunk_argmax, dim3(nch, 16), dim3(256), 0, s, aa);
   ANR_TRY(check_launch("k_chunk_argmax"));
   if (split) ANR_TRY(split->run(aa.chunk_max, nch, ANR_REDUCE_MAX_U64, s));  // the chunk's argmax over every rank
-  const int nb2 = (int)((N + 1023) / 1024);
   hipLaunchKernelGGL(k_flag_count, dim3(nb2), dim3(256), 0, s, aa);
   ANR_TRY(check_launch("k_flag_count"));
   hipLaunchKernelGGL(k_flag_force, dim3((nch + 255) / 256), dim3(256), 0, s, aa, nch);

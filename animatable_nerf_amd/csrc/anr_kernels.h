@@ -207,6 +207,9 @@ __global__ void k_scan_blocks(int* sums, int nb, int* total_out);
 __global__ void k_compact(CompactArgs a);
 // R <= 1024 rays (a training batch): k_count + k_scan_blocks + k_compact as one 1024-thread workgroup
 __global__ void k_compact1(CompactArgs a, int* total_out);
+// one chunk of <= 65,536 compact samples: the alpha_ind stage's five launches as two (anr_rays.hip)
+__global__ void k_alpha_count1(AlphaArgs a);
+__global__ void k_alpha_scatter1(AlphaArgs a, int* total_out);
 __global__ void k_chunk_argmax(AlphaArgs a);
 __global__ void k_flag_count(AlphaArgs a);
 __global__ void k_flag_force(AlphaArgs a, int nchunks);

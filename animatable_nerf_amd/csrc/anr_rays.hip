@@ -557,6 +557,78 @@ __global__ __launch_bounds__(256) void k_flag_scatter(AlphaArgs a) {
   }
 }
 
+// one chunk of <= 64 blocks of 1024 compact samples (a training batch): k_chunk_argmax + k_flag_count +
+// k_flag_force + k_scan_blocks + k_flag_scatter as two launches. Count: each block counts its
+// sigma' > train_th and folds its argmax key into chunk_max[0]. Scatter: each block takes its base from
+// the earlier blocks' counts (<= 63 loads), decodes the chunk's argmax sample as k_flag_force and adds
+// it where it was not flagged already; the last block writes the total (counts[1]).
+__global__ __launch_bounds__(256) void k_alpha_count1(AlphaArgs a) {
+  __shared__ int sh[4];
+  const int n = *a.n_kept;
+  int cnt = 0;
+  uint64_t best = 0;
+  for (int k = 0; k < 4; ++k) {
+    const int i = blockIdx.x * 1024 + k * 256 + threadIdx.x;
+    if (i < n) {
+      const float sg = a.sigma[i];
+      cnt += sg > a.train_th;
+      const int pid = a.list[i];
+      const uint32_t g = (uint32_t)((((pid >> 6) + a.ray_offset) % a.chunk) * 64 + (pid & 63));
+      const uint64_t key = ((uint64_t)ordered_bits(sg) << 32) | (uint32_t)(~g);
+      best = key > best ? key : best;
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const uint64_t o = __shfl_xor(best, off);
+    best = o > best ? o : best;
+  }
+  if ((threadIdx.x & 63) == 0 && best != 0) atomicMax((unsigned long long*)&a.chunk_max[0], (unsigned long long)best);
+  int total;
+  block_excl_scan_256(cnt, sh, total);
+  if (threadIdx.x == 0) a.block_sum[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(256) void k_alpha_scatter1(AlphaArgs a, int* __restrict__ total_out) {
+  __shared__ int sh[4];
+  __shared__ int s_base, s_force;
+  const int n = *a.n_kept;
+  if (threadIdx.x < 64) {  // wave 0: the earlier blocks' counts, and the forced sample
+    int v = (int)threadIdx.x < (int)blockIdx.x ? a.block_sum[threadIdx.x] : 0;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    if (threadIdx.x == 0) {
+      int i_f = -1;
+      const uint64_t key = a.chunk_max[0];
+      const int r1 = min(a.n_rays, a.chunk);
+      if (key != 0 && a.ray_off[r1] > a.ray_off[0]) {
+        const uint32_t g = ~(uint32_t)(key & 0xffffffffu);
+        const int ray = (int)(g >> 6) - a.ray_offset % a.chunk;
+        if (ray >= 0 && ray < r1) {
+          const int lane = (int)(g & 63u);
+          const uint64_t m = a.mask[ray];
+          if ((m >> lane) & 1ull) i_f = a.ray_off[ray] + __popcll(m & ((1ull << lane) - 1ull));
+        }
+      }
+      if (i_f >= 0 && a.sigma[i_f] > a.train_th) i_f = -1;  // flagged anyway
+      s_force = i_f;
+      s_base = v + (i_f >= 0 && i_f < (int)blockIdx.x * 1024 ? 1 : 0);
+    }
+  }
+  __syncthreads();
+  int base = s_base;
+  const int i_f = s_force;
+  for (int k = 0; k < 4; ++k) {
+    const int i = blockIdx.x * 1024 + k * 256 + threadIdx.x;
+    const int f = i < n ? (a.sigma[i] > a.train_th || i == i_f) : 0;
+    int total;
+    const int ex = block_excl_scan_256(f, sh, total);
+    if (i < n) a.out_row[i] = f ? base + ex : -1;
+    base += total;
+  }
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *total_out = base;
+}
+
 __global__ __launch_bounds__(256) void k_gather_rows(const int* __restrict__ out_row, const int* __restrict__ n_kept,
                                                      const float4* __restrict__ pbw_rows, const float4* __restrict__ tbw_rows,
                                                      float4* __restrict__ pbw, float4* __restrict__ tbw) {

@@ -268,6 +268,12 @@ struct TrainBufs {
   // vdir[id], dists[id] (n_pts of them, one reference call) instead of a ray sample; NULL: rays
   const float *wpts, *vdir, *dists;
   long n_pts;
+  // fused step only (NULL elsewhere): k_tr_point_prep's block 0 zeroes zero4[0..4) (the loss sums) and
+  // zero2048[0..2048) (the latent column-sum scratch) instead of two memset launches; k_tr_loss_grads'
+  // first thread writes loss3_out (was k_tr_loss_final)
+  float* zero4;
+  float* zero2048;
+  float* loss3_out;
 };
 
 __global__ void k_tr_point_prep(TrainBufs b);

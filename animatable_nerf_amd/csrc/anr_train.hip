@@ -26,6 +26,10 @@ __device__ __forceinline__ unsigned short f2bf(float f) {
 // ------------------------------------------------------------------------------------------
 // one wave per kept sample: lane f -> gamma(pose)_f, init_pbw_f (f<24), gamma(dir)_f (f<27)
 __global__ __launch_bounds__(256) void k_tr_point_prep(TrainBufs b) {
+  if (blockIdx.x == 0 && b.zero4) {
+    if (threadIdx.x < 4) b.zero4[threadIdx.x] = 0.f;
+    for (int k = threadIdx.x; k < 2048; k += 256) b.zero2048[k] = 0.f;
+  }
   const int lane = threadIdx.x & 63;
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int n = *b.n_kept;
@@ -249,18 +253,22 @@ __global__ __launch_bounds__(256) void k_tr_loss(TrainBufs b, const float* rgb_g
 }
 
 // acc3 = {sum sq. error, mask rays, sum smooth-L1, alpha_ind rows} (summed over the ranks of a ray split)
-__global__ void k_tr_loss_final(const float* acc3, const int* m_rows, float* loss3) {
-  (void)m_rows;
+__device__ __forceinline__ void loss_final(const float* acc3, float* loss3) {
   const float img = acc3[0] / (3.0f * acc3[1]);
   const float bw = acc3[2] / (24.0f * acc3[3]);
   loss3[0] = bw + img;
   loss3[1] = img;
   loss3[2] = bw;
 }
+__global__ void k_tr_loss_final(const float* acc3, const int* m_rows, float* loss3) {
+  (void)m_rows;
+  loss_final(acc3, loss3);
+}
 
 // upstream gradients of the fused loss: d rgb_map (R,3), d pbw / d tbw rows (m,24)
 __global__ __launch_bounds__(256) void k_tr_loss_grads(TrainBufs b, const float* rgb_gt, const uint8_t* mask,
                                                        const float* acc3, float* d_rgb, float* d_pbw, float* d_tbw) {
+  if (b.loss3_out && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) loss_final(acc3, b.loss3_out);
   if (blockIdx.y == 0) {
     const int r = blockIdx.x * 256 + threadIdx.x;
     if (r >= b.n_rays) return;

@@ -447,6 +447,11 @@ struct Exec {
     g.C = dX; g.ldc = ldX; g.mask = mask; g.ldm = ldm; g.accumulate = accumulate ? 1 : 0; g.ksplit = 1;
     return gemm_rows(g);
   }
+  // the fused step's loss sums and latent column-sum scratch, zeroed by the forward's k_tr_point_prep
+  // (prezeroed once it is launched) instead of by memsets
+  float* pz4 = nullptr;
+  float* pz2048 = nullptr;
+  bool prezeroed = false;
 };
 
 // the pose-space BW MLP under precision ANR_BF16 runs exact fp32 (its output moves the canonical
@@ -856,8 +861,12 @@ int train_forward(const anr_params* p, const anr_frame* f, const float* ray_o, c
   b.hbp = e.hb && !e.pose_fp32;
   const int g1 = (n + 255) / 256;
   if (n > 0) {
+    b.zero4 = e.pz4;
+    b.zero2048 = e.pz2048;
     hipLaunchKernelGGL(k_tr_point_prep, dim3((n + 3) / 4), dim3(256), 0, s, b);
     ANR_TRY(check_launch("k_tr_point_prep"));
+    b.zero4 = b.zero2048 = nullptr;
+    e.prezeroed = e.pz4 != nullptr;
   }
   // fused forward chains under the bf16 storage policies (every hidden row bf16): the T-pose BW MLP and
   // the NeRF, and the pose-space BW MLP when it is bf16 too (bf16_all)
@@ -973,8 +982,10 @@ int train_backward(const anr_params* p, float* const* g, const anr_frame* f, con
   // 1.201 vs 1.222 ms a step (profiles/r6b_*); ANR_WG_FLUSH_EVERY still overrides
   if (bchain && !getenv("ANR_WG_FLUSH_EVERY")) e.flush_every = 0;
   if (e.group) {
-    // the latent column-sum scratch of every latent_rows() of this call, zeroed once
-    if (hipMemsetAsync(ysum, 0, 8 * 256 * 4, s) != hipSuccess) return fail(ANR_E_HIP, "memset");
+    // the latent column-sum scratch of every latent_rows() of this call, zeroed once (by the fused step's
+    // forward when it ran: prezeroed)
+    if (!(e.prezeroed && e.pz2048 == ysum) && hipMemsetAsync(ysum, 0, 8 * 256 * 4, s) != hipSuccess)
+      return fail(ANR_E_HIP, "memset");
     e.ys_zero = true;
   }
   const hipStream_t s2 = e.s2();
@@ -1311,19 +1322,20 @@ int train_step_body(const anr_params* p, float* const* grads, const anr_frame* f
   e.hb = e.bf16;
   ANR_TRY(pack_images(e, p, ws + T.wimg, s, (float*)(ws + T.wslab), kLaneFloats, false,
                       !chains_cover(e, true, true)));
+  float* acc3 = (float*)(ws + T.acc3);
+  e.pz4 = acc3;
+  e.pz2048 = (float*)(ws + T.ysum);
   ANR_TRY(train_forward(p, f, ray_o, ray_d, near_, far_, n_rays, o, out, ws, T, s, e, nullptr, split));
   // fused losses (tpose_trainer.py:50-63) and their upstream gradients
   TrainBufs b = bufs(T, ws, f, ray_o, ray_d, near_, far_, n_rays, o);
   b.rgb_map = out->rgb_map;
-  float* acc3 = (float*)(ws + T.acc3);
-  if (hipMemsetAsync(acc3, 0, 16, s) != hipSuccess) return fail(ANR_E_HIP, "memset");
+  if (!e.prezeroed && hipMemsetAsync(acc3, 0, 16, s) != hipSuccess) return fail(ANR_E_HIP, "memset");
   const long N = (long)n_rays * 64;
   const int gx = (int)((std::max<long>(n_rays, N) + 255) / 256);
   hipLaunchKernelGGL(k_tr_loss, dim3(gx, 2), dim3(256), 0, s, b, rgb_gt, mask_at_box, acc3);
   ANR_TRY(check_launch("k_tr_loss"));
   if (split) ANR_TRY(split->run(acc3, 4, ANR_REDUCE_SUM_F32, s));  // the batch's loss sums and row count
-  hipLaunchKernelGGL(k_tr_loss_final, dim3(1), dim3(1), 0, s, (const float*)acc3, b.m_rows, loss3);
-  ANR_TRY(check_launch("k_tr_loss_final"));
+  b.loss3_out = loss3;  // the loss values (loss_final) from k_tr_loss_grads' first thread
   float* d_rgb = (float*)(ws + T.d_rgb);
   float* d_pbw = (float*)(ws + T.d_pbw);
   float* d_tbw = (float*)(ws + T.d_tbw);
