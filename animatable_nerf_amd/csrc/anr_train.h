@@ -298,6 +298,17 @@ __global__ void k_tr_rows_bwd(TrainBufs b);
 __global__ void k_tr_softmax_bwd_t(TrainBufs b);
 __global__ void k_tr_tpose_bwd(TrainBufs b);
 __global__ void k_tr_softmax_bwd_p(TrainBufs b);
+struct LatentPosts {
+  const float* dysum[8];
+  const float* W[8];
+  int in_ch[8], col0[8], nout[8];
+  const float* table[8];
+  const int64_t* li[8];
+  int add[8];
+  float* dW[8];
+  float* dtable[8];
+};
+__global__ void k_tr_latent_grads(LatentPosts P);
 __global__ void k_tr_latent_grad(const float* dysum, const float* W, int in_ch, int col0, int nout, const float* table,
                                  const int64_t* li, int add, float* dW, float* dtable);
 __global__ void k_an_prep_obs(TrainBufs b, const float* wpts);

@@ -500,6 +500,29 @@ __global__ __launch_bounds__(128) void k_tr_latent_grad(const float* dysum, cons
   if (threadIdx.x == 0) dtable[row * 128 + k] += sh[0] + sh[1];
 }
 
+// the latent-row updates queued with one weight-gradient flush, one launch: grid (256 + 128, n), post
+// blockIdx.y as k_tr_latent_grad
+__global__ __launch_bounds__(128) void k_tr_latent_grads(LatentPosts P) {
+  const int q = blockIdx.y;
+  const long row = (P.li[q] ? P.li[q][0] : 0) + P.add[q];
+  const int nout = P.nout[q], in_ch = P.in_ch[q], col0 = P.col0[q];
+  if ((int)blockIdx.x < nout) {
+    const int k = threadIdx.x;
+    const int nn = blockIdx.x;
+    P.dW[q][(long)nn * in_ch + col0 + k] += P.dysum[q][nn] * P.table[q][row * 128 + k];
+    return;
+  }
+  __shared__ float sh[2];
+  const int k = blockIdx.x - nout;
+  if (k >= 128) return;
+  float acc = 0.f;
+  for (int nn = threadIdx.x; nn < nout; nn += 128) acc += P.dysum[q][nn] * P.W[q][(long)nn * in_ch + col0 + k];
+  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) P.dtable[q][row * 128 + k] += sh[0] + sh[1];
+}
+
 // clip_grad_value_(clip) + torch.optim.Adam step (decoupled bias corrections as in torch)
 __global__ __launch_bounds__(256) void k_adam(float* p, float* g, float* m, float* v, long n, float lr, float b1, float b2,
                                               float eps, float wd, float bc1, float bc2_sqrt, float clip) {

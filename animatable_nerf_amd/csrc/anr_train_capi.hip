@@ -249,11 +249,15 @@ struct Exec {
     for (int i = 0; i < npsrc; ++i) ANR_TRY(order(ss, w, pend_src[i]));
     if (npend && launch_wgrad_group(pend, npend, grid_n(), group_nz, slab(fl), lane_floats, w) != 0)
       return check_launch("k_wgrad_group");
-    for (int i = 0; i < npost; ++i) {
-      const LatentPost& q = post[i];
-      hipLaunchKernelGGL(k_tr_latent_grad, dim3(256 + 128), dim3(128), 0, w, q.ys, q.W, q.in_ch, q.c0, q.ncol, q.tab, q.li,
-                         q.add, q.gW, q.gtab);
-      ANR_TRY(check_launch("k_tr_latent_grad"));
+    if (npost) {  // every latent-row update of the flush in one launch
+      LatentPosts P{};
+      for (int i = 0; i < npost; ++i) {
+        const LatentPost& q = post[i];
+        P.dysum[i] = q.ys; P.W[i] = q.W; P.in_ch[i] = q.in_ch; P.col0[i] = q.c0; P.nout[i] = q.ncol;
+        P.table[i] = q.tab; P.li[i] = q.li; P.add[i] = q.add; P.dW[i] = q.gW; P.dtable[i] = q.gtab;
+      }
+      hipLaunchKernelGGL(k_tr_latent_grads, dim3(256 + 128, npost), dim3(128), 0, w, P);
+      ANR_TRY(check_launch("k_tr_latent_grads"));
     }
     npend = npost = npsrc = 0;
     return ANR_OK;
