@@ -16,6 +16,7 @@
 // MFMA GEMMs (anr_gemm.hip k_gemm_t: weights and activations shared by the primal and tangent
 // rows, which are stacked into one 2n-row operand wherever the epilogue allows); per-sample work in
 // the kernels below. Two host reads of counts (kept samples, observed-gradient rows).
+#include <cstdio>
 #include <algorithm>
 #include <cmath>
 
@@ -563,6 +564,11 @@ struct TG {
         return ANR_OK;
       }
     }
+    static const bool log_fb = getenv("ANR_SDF_LOG_FALLBACK") != nullptr;  // which products k_lgemm does not take
+    if (log_fb)
+      fprintf(stderr, "sdf train k_gemm: M %d N %d nseg %d K0 %d a_rs0 %ld K1 %d atomic %d softplus %d spd %d mask %d ldc %ld "
+              "acc %d div_post %g x3 %d\n", M, g.N, g.nseg, g.seg[0].K, (long)g.seg[0].a_rs, g.nseg > 1 ? g.seg[1].K : 0,
+              g.atomic, g.softplus, g.spd ? 1 : 0, g.mask ? 1 : 0, (long)g.ldc, g.accumulate, (double)g.div_post, g.x3);
     launch_gemm(g, dim3((g.N + 63) / 64, (M + 63) / 64, g.ksplit), s);
     return check_launch("k_gemm (sdf train)");
   }
@@ -594,14 +600,32 @@ struct TG {
       if (launch_wgrad(w, M, s) != 0) return check_launch("k_wgrad (sdf train)");
       return ANR_OK;
     }
-    if (!wg_x3 && wg32 && slab) {  // exact fp32: k_wgrad_f32 where its operand shapes fit
+    if (!wg_x3 && wg32 && slab) {
+      // exact fp32: k_wgrad_f32 over blocks of <= 256 outputs x <= 256 inputs (lin8's 257 outputs, the
+      // colour net's 289 inputs), each block's column sums once (its first input block); the blocks run
+      // one after another on s, reusing the slab region in stream order
+      // X off a 16-B boundary (the colour net's feature, Y8 + 1): the product starts `off` columns early at
+      // the boundary and the reduction skips those columns (WGrad::j0)
+      const int off = (int)(((uintptr_t)X & 15) / 4);
+      const bool shift = ((uintptr_t)X & 3) == 0 && off > 0 && c0 >= off;
+      const float* Xs = shift ? X - off : X;
+      const int Ks = shift ? K + off : K;
+      const int cs = shift ? c0 - off : c0;
       WGrad w{};
-      w.dY = dY; w.ldY = ldY; w.nout = Nout; w.X = X; w.ldX = ldX; w.K = K;
-      w.dW = dW + c0; w.ldw = in_ch; w.bsum = bsum; w.slab = slab;
-      if (wgrad_f32_fits(w)) {
-        if (launch_wgrad_f32(w, M, s) != 0) return check_launch("k_wgrad_f32 (sdf train)");
-        return ANR_OK;
-      }
+      w.ldY = ldY; w.ldX = ldX; w.ldw = in_ch; w.slab = slab;
+      bool fits = true;
+      for (int pass = 0; pass < 2 && fits; ++pass)
+        for (int r0 = 0; r0 < Nout && fits; r0 += 256)
+          for (int k0 = 0; k0 < Ks && fits; k0 += 256) {
+            w.dY = dY + r0; w.nout = std::min(256, Nout - r0);
+            w.X = Xs + k0; w.K = std::min(256, Ks - k0);
+            w.j0 = k0 == 0 && shift ? off : 0;
+            w.dW = dW + cs + (long)r0 * in_ch + k0;
+            w.bsum = bsum && k0 == 0 ? bsum + r0 : nullptr;
+            if (pass == 0) fits = wgrad_f32_fits(w);
+            else if (launch_wgrad_f32(w, M, s) != 0) return check_launch("k_wgrad_f32 (sdf train)");
+          }
+      if (fits) return ANR_OK;
     }
     GemmArgs g{};
     g.rowsum = bsum;

@@ -864,7 +864,7 @@ __device__ __forceinline__ void wgrad_reduce_at(const WGrad& g, int u) {  // u: 
 #pragma unroll
     for (int k = 0; k < WG_ZG; ++k)
       if (z0 + k < z1) s += *(const f32x4*)(g.slab + ((long)((z0 + k) * g.tiles + t) * 4 + w) * 16 * 256 + ab * 256 + lane * 4);
-    if (j < g.K) {
+    if (j < g.K && j >= g.j0) {
 #pragma unroll
       for (int r = 0; r < 4; ++r)
         if (i + r < g.nout) atomicAdd(g.dW + (long)(i + r) * g.ldw + j, s[r]);

@@ -137,6 +137,7 @@ struct WGrad {
   int spb, nz, tiles, tj;
   int x3;  // split-bf16 products (fp32-level)
   int ybf, xbf;  // dY / X rows hold bf16 (reinterpreted as unsigned short*), not with x3
+  int j0;        // k_wgrad_f32: columns j < j0 are not written (X starts j0 columns early, at a 16-B boundary)
 };
 size_t wgrad_slab_floats();
 int launch_wgrad(WGrad g, int n_host, hipStream_t s);
