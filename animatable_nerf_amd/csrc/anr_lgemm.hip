@@ -106,8 +106,7 @@ __device__ __forceinline__ unsigned short lg_bf16_rne(float f) {
 
 // image element ((((g kst + ks) NOB + ob) 2 + hl) 64 + lane) 8 + e = weight (n, k), n = 16 (g NOB + ob)
 // + (lane & 15), k = 32 t + 8 (lane >> 4) + e of the segment holding k-step ks; zero past N / K_s
-__global__ void k_limg_pack(LPack p) {
-  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void limg_pack_at(const LPack& p, long i) {
   if (i >= p.total) {
     const long j = i - p.total;  // column j of the bias image
     if (j < p.nbias) p.bout[j] = (p.bias && j < p.N) ? p.bias[j] : 0.0f;
@@ -132,6 +131,20 @@ __global__ void k_limg_pack(LPack p) {
   const long o = ((f * 2) * 64 + lane) * 8 + e;
   p.out[o] = hi;
   p.out[o + 512] = lo;
+}
+
+__global__ void k_limg_pack(LPack p) { limg_pack_at(p, (long)blockIdx.x * blockDim.x + threadIdx.x); }
+
+// several images in one launch: descriptor d covers blocks [start[d], start[d + 1])
+__global__ void k_limg_pack_multi(const LPack* __restrict__ P, const long* __restrict__ start, int n) {
+  const long b = blockIdx.x;
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {  // the last descriptor whose first block <= b
+    const int mid = (lo + hi + 1) >> 1;
+    if (start[mid] <= b) lo = mid;
+    else hi = mid - 1;
+  }
+  limg_pack_at(P[lo], (b - start[lo]) * blockDim.x + threadIdx.x);
 }
 
 __device__ __forceinline__ float lg_exp(float z) { return fast_exp(z); }
@@ -614,7 +627,7 @@ bool lgemm_supported(const GemmArgs& g) {
   return lg_dispatch(a, nob, g.spd != nullptr, lg_unal(g), lg_f32(g), g.mask != nullptr, 0, nullptr, false);
 }
 
-int lgemm_pack(const GemmArgs& g, void* img, hipStream_t s) {
+static LPack lg_pack_desc(const GemmArgs& g, void* img) {
   LPack p{};
   int G = 1;
   p.kst = lg_kst(g, &p.kst0);
@@ -629,8 +642,27 @@ int lgemm_pack(const GemmArgs& g, void* img, hipStream_t s) {
   p.bout = (float*)((char*)img + (size_t)G * p.kst * p.NOB * 2 * LG_FRAG);
   p.nbias = G * p.NOB * 16;
   p.f32 = lg_f32(g) ? 1 : 0;
+  return p;
+}
+
+int lgemm_pack(const GemmArgs& g, void* img, hipStream_t s) {
+  const LPack p = lg_pack_desc(g, img);
   // hi and lo fragments interleave; one thread per (fragment, lane, element), then the bias columns
   hipLaunchKernelGGL(k_limg_pack, dim3((unsigned)((p.total + p.nbias + 255) / 256)), dim3(256), 0, s, p);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+size_t lgemm_pack_desc_bytes() { return sizeof(LPack); }
+
+long lgemm_pack_describe(const GemmArgs& g, void* img, void* desc) {
+  const LPack p = lg_pack_desc(g, img);
+  *(LPack*)desc = p;
+  return (p.total + p.nbias + 255) / 256;
+}
+
+int lgemm_pack_batch(const void* descs, const long* starts, int n, long blocks, hipStream_t s) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_limg_pack_multi, dim3((unsigned)blocks), dim3(256), 0, s, (const LPack*)descs, starts, n);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

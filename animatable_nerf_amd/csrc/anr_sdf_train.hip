@@ -19,6 +19,10 @@
 #include <cstdio>
 #include <algorithm>
 #include <cmath>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
 
 #include "../../include/aninerf.h"
 #include "anr_common.h"
@@ -519,7 +523,27 @@ struct LgImage {
   long r0, c0, r1, c1;
   int K0, K1, N;
   void* img;
+  int f32;                          // fp32 image (F32 kernels) or hi / lo bf16
+  long blocks;                      // its pack launch's blocks
+  alignas(8) unsigned char desc[192];  // its pack descriptor (lgemm_pack_describe)
 };
+
+// Per-call pack plans: a call packs each distinct weight view once, ~60 k_limg_pack launches per sdf_pdf
+// training step. The views a call packs depend only on the parameter pointers, the workspace and the
+// precision switches, so the list is recorded at the end of a call under that key (descriptors and block
+// starts copied to device memory once) and the next call with the same key packs all of them in ONE
+// k_limg_pack_multi launch right after the per-call weights (weight norm, folds) are formed, before its
+// first product. A product the plan does not hold is still packed on first use (and re-records the plan).
+struct LgPlan {
+  std::string key;
+  void* dev = nullptr;  // descriptors, then n + 1 block starts (long)
+  int n = 0;
+  long blocks = 0;
+  size_t used = 0;
+  std::vector<LgImage> entries;
+};
+std::mutex lg_plan_mu;
+std::vector<LgPlan> lg_plans;  // least recently recorded first, at most 8
 
 struct TG {
   hipStream_t s;
@@ -535,10 +559,11 @@ struct TG {
     const GemmSeg& a = g.seg[0];
     const GemmSeg& b = g.seg[1];
     const bool two = g.nseg > 1;
+    const int f32 = !g.x3 && !g.bf16;
     for (int i = 0; i < nlg; ++i) {
       const LgImage& q = lg[i];
       if (q.B0 == a.B && q.r0 == a.b_rs && q.c0 == a.b_cs && q.K0 == a.K && q.N == g.N && q.bias == g.bias &&
-          q.B1 == (two ? b.B : nullptr) && (!two || (q.r1 == b.b_rs && q.c1 == b.b_cs && q.K1 == b.K)))
+          q.f32 == f32 && q.B1 == (two ? b.B : nullptr) && (!two || (q.r1 == b.b_rs && q.c1 == b.b_cs && q.K1 == b.K)))
         return q.img;
     }
     const size_t bytes = (lgemm_image_bytes(g) + 255) / 256 * 256;
@@ -546,10 +571,70 @@ struct TG {
     void* img = lg_arena + lg_used;
     if (lgemm_pack(g, img, s) != 0) return nullptr;
     lg_used += bytes;
-    lg[nlg++] = LgImage{a.B, two ? b.B : nullptr, g.bias, a.b_rs, a.b_cs, two ? b.b_rs : 0, two ? b.b_cs : 0,
-                        a.K, two ? b.K : 0, g.N, img};
+    LgImage& q = lg[nlg++];
+    q = LgImage{a.B, two ? b.B : nullptr, g.bias, a.b_rs, a.b_cs, two ? b.b_rs : 0, two ? b.b_cs : 0,
+                a.K, two ? b.K : 0, g.N, img, f32, 0, {}};
+    if (lgemm_pack_desc_bytes() <= sizeof(q.desc)) q.blocks = lgemm_pack_describe(g, img, q.desc);
+    plan_dirty = true;
     return img;
   }
+  // the pack plan of this call's key (LgPlan): every recorded image packed in one launch
+  std::string plan_key;
+  bool plan_dirty = false;
+  int plan_begin(const std::string& key) {
+    plan_key = key;
+    std::lock_guard<std::mutex> lk(lg_plan_mu);
+    for (const LgPlan& P : lg_plans) {
+      if (P.key != key) continue;
+      const size_t D = lgemm_pack_desc_bytes();
+      const long* starts = (const long*)((const char*)P.dev + (P.n * D + 7) / 8 * 8);
+      if (lgemm_pack_batch(P.dev, starts, P.n, P.blocks, s) != 0) return -1;
+      nlg = (int)P.entries.size();
+      for (int i = 0; i < nlg; ++i) lg[i] = P.entries[i];
+      lg_used = P.used;
+      return 0;
+    }
+    return 0;
+  }
+  // record (or re-record) the plan once the call has issued every product
+  void plan_end() {
+    if (plan_key.empty() || !plan_dirty || nlg == 0) return;
+    const size_t D = lgemm_pack_desc_bytes();
+    for (int i = 0; i < nlg; ++i)
+      if (D > sizeof(lg[i].desc) || lg[i].blocks <= 0) return;
+    const size_t off = (nlg * D + 7) / 8 * 8;
+    std::vector<unsigned char> host(off + (nlg + 1) * sizeof(long));
+    long* starts = (long*)(host.data() + off);
+    long b = 0;
+    for (int i = 0; i < nlg; ++i) {
+      std::memcpy(host.data() + i * D, lg[i].desc, D);
+      starts[i] = b;
+      b += lg[i].blocks;
+    }
+    starts[nlg] = b;
+    void* dev = nullptr;
+    if (hipMalloc(&dev, host.size()) != hipSuccess) return;
+    if (hipMemcpy(dev, host.data(), host.size(), hipMemcpyHostToDevice) != hipSuccess) {
+      (void)hipFree(dev);
+      return;
+    }
+    LgPlan P;
+    P.key = plan_key; P.dev = dev; P.n = nlg; P.blocks = b; P.used = lg_used;
+    P.entries.assign(lg, lg + nlg);
+    std::lock_guard<std::mutex> lk(lg_plan_mu);
+    for (size_t i = 0; i < lg_plans.size(); ++i)
+      if (lg_plans[i].key == plan_key) {  // hipFree waits for the device: a batch still reading it finishes first
+        (void)hipFree(lg_plans[i].dev);
+        lg_plans.erase(lg_plans.begin() + i);
+        break;
+      }
+    if (lg_plans.size() >= 8) {
+      (void)hipFree(lg_plans.front().dev);
+      lg_plans.erase(lg_plans.begin());
+    }
+    lg_plans.push_back(std::move(P));
+  }
+  ~TG() { plan_end(); }
   int lg32 = 0;  // exact fp32 products on k_lgemm's F32 kernels (resident fp32 weight image) where they fit
   int wg32 = 0;  // exact fp32 weight gradients on k_wgrad_f32 (slab + reduce) where they fit
   int run(GemmArgs g, int M) {
@@ -861,6 +946,20 @@ int sdf_train_core(const TrainCore& C) {
     g.lg_arena = ws + L.lgimg;
     g.lg_cap = kLgArena;
     g.cus = cus;
+    // the pack plan key: parameter pointers, workspace arena, precision switches (ANR_SDF_PACK_PLAN=0: off)
+    static const bool plan_on = [] {
+      const char* v = getenv("ANR_SDF_PACK_PLAN");
+      return !(v && v[0] == '0');
+    }();
+    if (plan_on) {
+      std::string key;
+      key.append((const char*)tp, sizeof(const float*) * ANR_SDF_NUM_TENSORS);
+      const void* arena = g.lg_arena;
+      const int sw[4] = {x3_on ? 1 : 0, g.lg32, x3_parts, (int)C.mode};
+      key.append((const char*)&arena, sizeof(arena));
+      key.append((const char*)sw, sizeof(sw));
+      if (g.plan_begin(key) != 0) return fail(ANR_E_HIP, "sdf train: batched weight-image pack failed");
+    }
   }
   // ANR_SDF_WG32 (read per call, default 1): the exact weight gradients on k_wgrad_f32 instead of k_gemm_t's
   // atomic split-K (~4.7 M fp32 atomics per 36k-row 256 x 256 product)

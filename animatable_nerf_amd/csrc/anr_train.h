@@ -218,6 +218,12 @@ int tchain_run(int prog, const TcArgs& a, int cap, int cus, hipStream_t s);
 bool lgemm_supported(const GemmArgs& g);
 size_t lgemm_image_bytes(const GemmArgs& g);
 int lgemm_pack(const GemmArgs& g, void* img, hipStream_t s);
+// batched packing (anr_sdf_train.hip's per-call plan): lgemm_pack_describe writes g's pack descriptor
+// (lgemm_pack_desc_bytes bytes) for image img and returns its block count; lgemm_pack_batch packs n
+// described images (descriptors and block starts in device memory, starts[n] = blocks) in one launch
+size_t lgemm_pack_desc_bytes();
+long lgemm_pack_describe(const GemmArgs& g, void* img, void* desc);
+int lgemm_pack_batch(const void* descs, const long* starts, int n, long blocks, hipStream_t s);
 int lgemm_run(const GemmArgs& g, const void* img, int cus, hipStream_t s);
 
 // per-point training buffers (row-major, compact kept-sample order)
