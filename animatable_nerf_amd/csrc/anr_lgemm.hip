@@ -41,6 +41,9 @@ typedef __bf16 lbf16x8 __attribute__((ext_vector_type(8)));
 #ifndef LG_NT
 #define LG_NT 0    // 1: nontemporal output stores
 #endif
+#ifndef LG_F32_PIPE
+#define LG_F32_PIPE 1  // lg_tile_f32: fragment halves read one half-k-step ahead of their MFMAs
+#endif
 
 // physical column (within a 32-deep k-step) of lane group j's fragment element e
 __host__ __device__ constexpr int lg_kcol(int j, int e) { return LG_PERM ? (e < 4 ? 4 * j + e : 16 + 4 * j + e - 4) : 8 * j + e; }
@@ -308,6 +311,21 @@ __device__ __forceinline__ void lg_tile_f32(const LGemm& g, f32x4 (&buf)[KST][2]
   for (int ob = 0; ob < NOB; ++ob) acc[ob] = f32x4{0.f, 0.f, 0.f, 0.f};
   int frag_off = lane * 16;
   asm volatile("" : "+v"(frag_off));
+  // fragment halves h (elements 4h..4h+3 of the k-step) pipelined: the next k-step's half-0 fragments
+  // are read while this k-step's half-1 MFMAs run, its half-1 fragments while the next k-step's half-0
+  // MFMAs run (the same registers; each read has 4 NOB MFMAs ahead of its first use instead of
+  // waiting at every k-step's start). LG_F32_PIPE=0 (and MASK): all 2 NOB reads of a k-step before its MFMAs.
+  constexpr bool PIPE = LG_F32_PIPE && !MASK;  // MASK holds NOB more registers: spills with it
+  f32x4 w[2][NOB];
+  auto read_half = [&](int ks, int h) {
+#pragma unroll
+    for (int ob = 0; ob < NOB; ++ob)
+      w[h][ob] = *(const f32x4*)(lds + ks * NOB * 2 * LG_FRAG + frag_off + (2 * ob + h) * LG_FRAG);
+  };
+  if constexpr (PIPE) {
+    read_half(0, 0);
+    read_half(0, 1);
+  }
 #pragma unroll
   for (int ks = 0; ks < KST; ++ks) {
     const bool s1 = ks >= KST0;
@@ -324,17 +342,23 @@ __device__ __forceinline__ void lg_tile_f32(const LGemm& g, f32x4 (&buf)[KST][2]
 #pragma unroll
     for (int e = 0; e < 8; ++e)
       if constexpr (!FULLK) x[e] = (k0 + lg_kcol(kg, e) < K) ? x[e] : 0.0f;
-    const unsigned char* fr = lds + ks * NOB * 2 * LG_FRAG + frag_off;
-    f32x4 w[2][NOB];
+    if constexpr (!PIPE) {
+      read_half(ks, 0);
+      read_half(ks, 1);
+    }
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
+    for (int h = 0; h < 2; ++h) {
+      if constexpr (PIPE) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int ob = 0; ob < NOB; ++ob) w[h][ob] = *(const f32x4*)(fr + (2 * ob + h) * LG_FRAG);
+      for (int e = 4 * h; e < 4 * h + 4; ++e)
 #pragma unroll
-    for (int e = 0; e < 8; ++e)
-#pragma unroll
-      for (int ob = 0; ob < NOB; ++ob)
-        acc[ob] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[e >> 2][ob][e & 3], x[e], acc[ob], 0, 0, 0);
+        for (int ob = 0; ob < NOB; ++ob)
+          acc[ob] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[h][ob][e & 3], x[e], acc[ob], 0, 0, 0);
+      if constexpr (PIPE) {
+        __builtin_amdgcn_sched_barrier(0);
+        if (ks + 1 < KST) read_half(ks + 1, h);
+      }
+    }
   }
   lg_epilogue<NOB, SPD, HEAD, MASK>(g, acc, sp, mk, atr_lds + 32 * KST + 1024, tile, n0, lane, atr_lds + 32 * KST);
 }
