@@ -25,15 +25,7 @@ __device__ __forceinline__ unsigned short f2bf(float f) {
 // forward point kernels
 // ------------------------------------------------------------------------------------------
 // one wave per kept sample: lane f -> gamma(pose)_f, init_pbw_f (f<24), gamma(dir)_f (f<27)
-__global__ __launch_bounds__(256) void k_tr_point_prep(TrainBufs b) {
-  if (blockIdx.x == 0 && b.zero4) {
-    if (threadIdx.x < 4) b.zero4[threadIdx.x] = 0.f;
-    for (int k = threadIdx.x; k < 2048; k += 256) b.zero2048[k] = 0.f;
-  }
-  const int lane = threadIdx.x & 63;
-  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int n = *b.n_kept;
-  if (i >= n) return;
+__device__ __forceinline__ void point_prep_one(const TrainBufs& b, int i, int lane) {
   const int pid = b.list[i];
   float dist, pose[3], dir[3];
   if (b.dists) {  // free samples (Network.forward)
@@ -64,6 +56,18 @@ __global__ __launch_bounds__(256) void k_tr_point_prep(TrainBufs b) {
     float* p = b.pt + (long)i * 8;
     p[0] = pose[0]; p[1] = pose[1]; p[2] = pose[2]; p[3] = dist;
   }
+}
+
+// grid-stride over the kept samples (the grid is capped on the host: most of a capacity-sized grid
+// would find i >= n_kept and exit, ~60 % of it at a training batch)
+__global__ __launch_bounds__(256) void k_tr_point_prep(TrainBufs b) {
+  if (blockIdx.x == 0 && b.zero4) {
+    if (threadIdx.x < 4) b.zero4[threadIdx.x] = 0.f;
+    for (int k = threadIdx.x; k < 2048; k += 256) b.zero2048[k] = 0.f;
+  }
+  const int lane = threadIdx.x & 63;
+  const int n = *b.n_kept;
+  for (int i = blockIdx.x * 4 + (threadIdx.x >> 6); i < n; i += gridDim.x * 4) point_prep_one(b, i, lane);
 }
 
 __device__ __forceinline__ void softmax24(const float* __restrict__ logits, const float* __restrict__ init, float* out) {
@@ -98,12 +102,8 @@ __device__ __forceinline__ float wave_max(float v) {
 
 // one wave per sample: pbw softmax (lane = joint), LBS to the T-pose, gamma(x_T) (lane = feature),
 // init_tbw (lane = channel); every row written by consecutive lanes
-__global__ __launch_bounds__(256) void k_tr_softmax_lbs(TrainBufs b) {
+__device__ __forceinline__ void softmax_lbs_one(const TrainBufs& b, int i, int lane) {
 #pragma clang fp contract(fast)
-  const int lane = threadIdx.x & 63;
-  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int n = *b.n_kept;
-  if (i >= n) return;
   // softmax(log(init + 1e-9) + logits) over the 24 joints
   const float l = lane < 24 ? logf(b.Ip[(long)i * 32 + lane] + 1e-9f) + b.Lp[(long)i * 32 + lane] : -INFINITY;
   const float m = wave_max(l);
@@ -144,6 +144,12 @@ __global__ __launch_bounds__(256) void k_tr_softmax_lbs(TrainBufs b) {
     tri_cell(tp, lo, hi, b.tX, b.tY, b.tZ, cell);
     b.It[(long)i * 32 + lane] = lane < 24 ? tri_channel(b.tbw, 25, lane, cell) : 0.f;
   }
+}
+
+__global__ __launch_bounds__(256) void k_tr_softmax_lbs(TrainBufs b) {
+  const int lane = threadIdx.x & 63;
+  const int n = *b.n_kept;
+  for (int i = blockIdx.x * 4 + (threadIdx.x >> 6); i < n; i += gridDim.x * 4) softmax_lbs_one(b, i, lane);
 }
 
 // free points (Network.calculate_neural_blend_weights / TPoseHuman.calculate_alpha): one wave per
@@ -501,7 +507,9 @@ __global__ __launch_bounds__(128) void k_tr_latent_grad(const float* dysum, cons
 }
 
 // the latent-row updates queued with one weight-gradient flush, one launch: grid (256 + 128, n), post
-// blockIdx.y as k_tr_latent_grad
+// blockIdx.y as k_tr_latent_grad. Posts of one launch can share outputs (the blend-weight MLP's pose and
+// T-pose passes update the same dW latent columns, layers 0 and 5 the same table row), so every update
+// is an atomic add (sequential launches ordered them; here they run concurrently)
 __global__ __launch_bounds__(128) void k_tr_latent_grads(LatentPosts P) {
   const int q = blockIdx.y;
   const long row = (P.li[q] ? P.li[q][0] : 0) + P.add[q];
@@ -509,7 +517,7 @@ __global__ __launch_bounds__(128) void k_tr_latent_grads(LatentPosts P) {
   if ((int)blockIdx.x < nout) {
     const int k = threadIdx.x;
     const int nn = blockIdx.x;
-    P.dW[q][(long)nn * in_ch + col0 + k] += P.dysum[q][nn] * P.table[q][row * 128 + k];
+    atomicAdd(P.dW[q] + (long)nn * in_ch + col0 + k, P.dysum[q][nn] * P.table[q][row * 128 + k]);
     return;
   }
   __shared__ float sh[2];
@@ -520,7 +528,7 @@ __global__ __launch_bounds__(128) void k_tr_latent_grads(LatentPosts P) {
   for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
   if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = acc;
   __syncthreads();
-  if (threadIdx.x == 0) P.dtable[q][row * 128 + k] += sh[0] + sh[1];
+  if (threadIdx.x == 0) atomicAdd(P.dtable[q] + row * 128 + k, sh[0] + sh[1]);
 }
 
 // clip_grad_value_(clip) + torch.optim.Adam step (decoupled bias corrections as in torch)
