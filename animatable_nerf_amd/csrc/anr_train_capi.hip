@@ -1024,7 +1024,14 @@ int train_backward(const anr_params* p, float* const* g, const anr_frame* f, con
   // issued a layer at a time between the NeRF's layers; with the chains the first tick launches the
   // T-pose chain and the ticks queue its weight gradients between the NeRF's (groups of both MLPs:
   // flushing each MLP's products separately, on two lanes, measured 1.353 vs 1.324 ms, profiles/r5y_*)
-  auto tick = [&]() { return tb.done() ? ANR_OK : tb.step(); };
+  // ANR_WG_NERF_FIRST=1 (read per call, chains only): the T-pose chain launches first, but its weight
+  // gradients are queued after all of the NeRF's, and the NeRF's group is flushed once its chain is
+  // issued, so that group waits for program 3 alone (not for the longer T-pose chain) and starts on the
+  // weight-gradient lane while the T-pose chain still runs
+  const char* nf_env = getenv("ANR_WG_NERF_FIRST");
+  const bool nerf_first = bchain && nf_env && nf_env[0] == '1';
+  auto tick = [&]() { return nerf_first || tb.done() ? ANR_OK : tb.step(); };
+  if (nerf_first) ANR_TRY(tb.start());
   ANR_TRY(tick());
   // d alpha: fp32 (ld 1), or under e.hb bf16 rows of 64 (k_tr_raw_bwd) so both products stay on the fast paths
   const float* dAl = e.hb ? (const float*)b.dAlpha16 : b.dAlpha;
@@ -1100,6 +1107,7 @@ int train_backward(const anr_params* p, float* const* g, const anr_frame* f, con
     }
     ANR_TRY(tick());
   }
+  if (nerf_first) ANR_TRY(e.flush_w());
   // the canonical NeRF's gradients (tensors 0..26) are final once the weight-gradient stream has
   // run what is issued so far: a caller may start reducing them while the blend-weight backward
   // below runs (bucketed all-reduce, anr_train_hooks)
