@@ -153,6 +153,19 @@ int order(SideStreams* ss, hipStream_t to, hipStream_t from) {
   return ANR_OK;
 }
 
+// two-phase order: mark() records `from`'s position now, after() makes `to` wait for it later (an
+// event of the ring: fewer than 64 order / mark calls may come in between)
+int mark(SideStreams* ss, hipStream_t from, hipEvent_t* ev) {
+  *ev = nullptr;  // no side streams (ANR_TRAIN_SERIAL): one stream, nothing to order
+  if (!ss) return ANR_OK;
+  *ev = ss->ev[ss->next++ & 63];
+  return hipEventRecord(*ev, from) == hipSuccess ? ANR_OK : fail(ANR_E_HIP, "hipEventRecord failed");
+}
+int after(hipStream_t to, hipEvent_t ev) {
+  if (ev && hipStreamWaitEvent(to, ev, 0) != hipSuccess) return fail(ANR_E_HIP, "stream ordering failed");  // NULL: none
+  return ANR_OK;
+}
+
 // A training entry point runs on the library's own main stream, forked from the caller's stream on
 // entry and joined back into it on exit (also on an error return). Round 4 introduced it after the
 // grouped weight gradients read unwritten gradient rows (NaN, tools/nan_probe.py) whenever the caller
@@ -851,12 +864,15 @@ int train_forward(const anr_params* p, const anr_frame* f, const float* ray_o, c
   const bool fchain = e.hb && fchain_on() && R > 0;
   note_chain_bits(ws, fchain);
   unsigned char* tcimg = (unsigned char*)(ws + T.tcimg);
+  hipEvent_t fwd_packed = nullptr;
   if (fchain) {
     // the chain images (and the input-gradient ones, for the backward of this step) are packed on s2,
     // beside the front-end: s2 starts after everything issued to s so far (the previous call's chains
-    // read the images); s waits for it before its first chain
+    // read the images); s waits for the forward programs' images before its first chain (the
+    // input-gradient images follow on s2, ahead of the T-pose chain there and of the forward's join)
     ANR_TRY(order(e.ss, e.s2(), s));
     ANR_TRY(chain_pack(p, tcimg, e.s2()));
+    ANR_TRY(mark(e.ss, e.s2(), &fwd_packed));
     if (bchain_on()) {
       ANR_TRY(chain_pack_bwd(p, tcimg, e.s2()));
       e.bimg = true;
@@ -881,7 +897,7 @@ int train_forward(const anr_params* p, const anr_frame* f, const float* ray_o, c
   }
   // fused forward chains under the bf16 storage policies (every hidden row bf16): the T-pose BW MLP and
   // the NeRF, and the pose-space BW MLP when it is bf16 too (bf16_all)
-  if (fchain) ANR_TRY(order(e.ss, s, e.s2()));  // the images packed on s2
+  if (fchain) ANR_TRY(after(s, fwd_packed));  // the forward programs' images packed on s2
   // pose-space BW MLP (latent_index + 1), softmax + LBS, T-pose BW MLP (latent 0)
   if (fchain && !e.pose_fp32) {
     ANR_TRY(chain_bw(e, p, tcimg, b.Gp, (float*)(ws + T.Hp), b.Lp, N, FOLD(0), FOLD(2), s, (unsigned char*)(ws + T.bitsP)));
@@ -1024,12 +1040,13 @@ int train_backward(const anr_params* p, float* const* g, const anr_frame* f, con
   // issued a layer at a time between the NeRF's layers; with the chains the first tick launches the
   // T-pose chain and the ticks queue its weight gradients between the NeRF's (groups of both MLPs:
   // flushing each MLP's products separately, on two lanes, measured 1.353 vs 1.324 ms, profiles/r5y_*)
-  // ANR_WG_NERF_FIRST=1 (read per call, chains only): the T-pose chain launches first, but its weight
-  // gradients are queued after all of the NeRF's, and the NeRF's group is flushed once its chain is
-  // issued, so that group waits for program 3 alone (not for the longer T-pose chain) and starts on the
-  // weight-gradient lane while the T-pose chain still runs
+  // ANR_WG_NERF_FIRST (read per call, chains only, default 1): the T-pose chain launches first, but its
+  // weight gradients are queued after all of the NeRF's, and the NeRF's group is flushed once its chain
+  // is issued, so that group waits for program 3 alone (not for the longer T-pose chain) and starts on
+  // the weight-gradient lane while the T-pose chain still runs: 1.017 / 1.018 vs 1.009 / 1.006 ms a step
+  // (alternating runs, one box, profiles/round6/r8r_*)
   const char* nf_env = getenv("ANR_WG_NERF_FIRST");
-  const bool nerf_first = bchain && nf_env && nf_env[0] == '1';
+  const bool nerf_first = bchain && !(nf_env && nf_env[0] == '0');
   auto tick = [&]() { return nerf_first || tb.done() ? ANR_OK : tb.step(); };
   if (nerf_first) ANR_TRY(tb.start());
   ANR_TRY(tick());
