@@ -41,6 +41,9 @@ typedef __bf16 lbf16x8 __attribute__((ext_vector_type(8)));
 #ifndef LG_NT
 #define LG_NT 0    // 1: nontemporal output stores
 #endif
+#ifndef LG_HALF_TAIL
+#define LG_HALF_TAIL 1  // F32 plain products: the launch's last partial round of tiles as half tiles
+#endif
 #ifndef LG_F32_PIPE
 #define LG_F32_PIPE 1  // lg_tile_f32: fragment halves read one half-k-step ahead of their MFMAs
 #endif
@@ -288,9 +291,11 @@ __device__ __forceinline__ void lg_load_mask(const LGemm& g, f32x4 (&mk)[NOB], i
 // fills which register and waited for every load (vmcnt(0)) at each tile's first k-step, exposing one
 // HBM round trip per tile. Fragments of a k-step are read up front and the MFMAs run element-major
 // (NOB independent accumulators between two uses of one).
-template <int NOB, int KST, int KST0, bool SPD, bool UNAL, bool ATR, bool HEAD, bool FULLK, bool MASK>
+// NOBI: out-blocks per k-step in the LDS image; the tile covers out-blocks obase .. obase + NOB - 1 of it
+// (a half tile of the launch's tail: NOB = NOBI / 2)
+template <int NOB, int KST, int KST0, bool SPD, bool UNAL, bool ATR, bool HEAD, bool FULLK, bool MASK, int NOBI = NOB>
 __device__ __forceinline__ void lg_tile_f32(const LGemm& g, f32x4 (&buf)[KST][2], int tile, int next, int n0,
-                                            int lane, const unsigned char* lds, const float* atr_lds) {
+                                            int lane, const unsigned char* lds, const float* atr_lds, int obase = 0) {
   f32x4 sp[NOB], mk[NOB];
   lg_load_spd<NOB, SPD>(g, sp, tile, n0, lane);
   lg_load_mask<NOB, MASK>(g, mk, tile, n0, lane);
@@ -320,7 +325,7 @@ __device__ __forceinline__ void lg_tile_f32(const LGemm& g, f32x4 (&buf)[KST][2]
   auto read_half = [&](int ks, int h) {
 #pragma unroll
     for (int ob = 0; ob < NOB; ++ob)
-      w[h][ob] = *(const f32x4*)(lds + ks * NOB * 2 * LG_FRAG + frag_off + (2 * ob + h) * LG_FRAG);
+      w[h][ob] = *(const f32x4*)(lds + ks * NOBI * 2 * LG_FRAG + frag_off + (2 * (ob + obase) + h) * LG_FRAG);
   };
   if constexpr (PIPE) {
     read_half(0, 0);
@@ -360,7 +365,8 @@ __device__ __forceinline__ void lg_tile_f32(const LGemm& g, f32x4 (&buf)[KST][2]
       }
     }
   }
-  lg_epilogue<NOB, SPD, HEAD, MASK>(g, acc, sp, mk, atr_lds + 32 * KST + 1024, tile, n0, lane, atr_lds + 32 * KST);
+  lg_epilogue<NOB, SPD, HEAD, MASK>(g, acc, sp, mk, atr_lds + 32 * KST + 1024 + 16 * obase, tile, n0 + 16 * obase, lane,
+                                     atr_lds + 32 * KST);
 }
 
 // one tile on a k-step ring: this tile's factor loads go out first; each k-step's activations are
@@ -489,17 +495,41 @@ __global__ __launch_bounds__(LG_WAVES * 64) void k_lgemm(LGemm g) {
   // first tiles: waves 0..3 of every workgroup before waves 4..7, so the waves that get one tile more
   // than the rest (T is rarely a multiple of nw) are at most one per SIMD (waves w and w + 4 share a
   // SIMD): the busiest SIMD carries ceil(2 T / nw) tiles instead of 2 ceil(T / nw)
-  int t = (w >> 2) * (g.bpg * 4) + rank * 4 + (w & 3);
-  if (t >= T) return;
+  const int s0 = (w >> 2) * (g.bpg * 4) + rank * 4 + (w & 3);
+  // the tail: T = q nw + r tiles; with r <= nw / 4 the last round's r tiles run as 2 r half tiles (NOB / 2
+  // out-blocks each) on the first 2 r slots — one per SIMD, as the slot order puts waves 0..3 of every
+  // workgroup first — so the busiest SIMD carries 2 q + 1/2 tiles instead of 2 q + 1
+  constexpr bool HALVES = F32 && KST <= 8 && !SPD && !ATR && !HEAD && !MASK && NOB % 2 == 0 && LG_HALF_TAIL;
+  const int q = T / nw, r = T - q * nw;
+  const bool halves = HALVES && r > 0 && 4 * r <= nw;
+  auto item = [&](int k) {  // this wave's k-th tile, -1 past its last
+    if (k < q) return s0 + k * nw;
+    if (k == q) return halves ? (s0 < 2 * r ? q * nw + s0 / 2 : -1) : (s0 < r ? q * nw + s0 : -1);
+    return -1;
+  };
+  int t = item(0);
+  if (t < 0) return;
   f32x4 buf[KST][2];
 #pragma unroll
   for (int ks = 0; ks < KST; ++ks) lg_load_ks<KST0, UNAL>(g, buf[ks], t, ks, lane);
-  for (; t < T; t += nw) {
+  // full tiles first (their loop holds one tile variant), the half tile after it
+  const int nfull = halves ? q : q + (s0 < r ? 1 : 0);
+  for (int k = 0; k < nfull; ++k) {
+    t = item(k);
+    const int nt = item(k + 1);
+    const int next = nt >= 0 ? nt : t;  // the last tile's refill re-reads its own rows (in bounds)
     // the whole-tile copy needs KST x 8 more registers: taken where it compiles without spills
     if constexpr (F32 && KST <= 8 && !SPD && !ATR)
-      lg_tile_f32<NOB, KST, KST0, SPD, UNAL, ATR, HEAD, FULLK, MASK>(g, buf, t, t + nw, n0, lane, lds, atr_lds);
+      lg_tile_f32<NOB, KST, KST0, SPD, UNAL, ATR, HEAD, FULLK, MASK>(g, buf, t, next, n0, lane, lds, atr_lds);
     else
-      lg_tile<NOB, KST, KST0, SPD, UNAL, ATR, HEAD, FULLK, F32, MASK>(g, buf, t, t + nw, n0, lane, lds, atr_lds);
+      lg_tile<NOB, KST, KST0, SPD, UNAL, ATR, HEAD, FULLK, F32, MASK>(g, buf, t, next, n0, lane, lds, atr_lds);
+  }
+  if constexpr (HALVES) {
+    if (halves && s0 < 2 * r) {  // its rows were loaded by the last full tile's refill (or above)
+      t = item(q);
+      lg_tile_f32<NOB / 2, KST, KST0, SPD, UNAL, ATR, HEAD, FULLK, MASK, NOB>(g, buf, t, t, n0, lane, lds, atr_lds,
+                                                                            (s0 & 1) * (NOB / 2));
+    }
   }
   if (w == 0) clk_stamp(g.clk, 1);
 }
