@@ -264,7 +264,11 @@ struct Exec {
   bool bimg = false;     // the input-gradient chain images are packed for this call (train_forward, on s2)
   int flush_w() {
     if (!npend && !npost) return ANR_OK;
-    const int fl = 0;
+    // ANR_WG_ALT_LANES=1 (read per call): consecutive groups alternate between the weight-gradient lanes
+    // (each lane its own slab region; the groups' dW / bias / latent updates are atomic adds), so one
+    // group's reduction and small-format launches overlap the next group's products
+    const char* al = getenv("ANR_WG_ALT_LANES");
+    const int fl = ss && al && al[0] == '1' ? (nflush++ % ss->lanes) : 0;
     hipStream_t w = ss ? ss->sw[fl] : s;
     for (int i = 0; i < npsrc; ++i) ANR_TRY(order(ss, w, pend_src[i]));
     if (npend && launch_wgrad_group(pend, npend, grid_n(), group_nz, slab(fl), lane_floats, w) != 0)
@@ -476,6 +480,7 @@ struct Exec {
   float* pz4 = nullptr;
   float* pz2048 = nullptr;
   bool prezeroed = false;
+  int nflush = 0;  // weight-gradient groups flushed so far (ANR_WG_ALT_LANES)
 };
 
 // the pose-space BW MLP under precision ANR_BF16 runs exact fp32 (its output moves the canonical
