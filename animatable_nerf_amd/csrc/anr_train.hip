@@ -58,16 +58,16 @@ __device__ __forceinline__ void point_prep_one(const TrainBufs& b, int i, int la
   }
 }
 
-// grid-stride over the kept samples (the grid is capped on the host: most of a capacity-sized grid
-// would find i >= n_kept and exit, ~60 % of it at a training batch)
+// one wave per sample over a capacity-sized grid (a grid-stride loop over a capped grid ran 38 instead
+// of ~29 us: the per-sample work is latency-bound and wants every wave in flight at once)
 __global__ __launch_bounds__(256) void k_tr_point_prep(TrainBufs b) {
   if (blockIdx.x == 0 && b.zero4) {
     if (threadIdx.x < 4) b.zero4[threadIdx.x] = 0.f;
     for (int k = threadIdx.x; k < 2048; k += 256) b.zero2048[k] = 0.f;
   }
   const int lane = threadIdx.x & 63;
-  const int n = *b.n_kept;
-  for (int i = blockIdx.x * 4 + (threadIdx.x >> 6); i < n; i += gridDim.x * 4) point_prep_one(b, i, lane);
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i < *b.n_kept) point_prep_one(b, i, lane);
 }
 
 __device__ __forceinline__ void softmax24(const float* __restrict__ logits, const float* __restrict__ init, float* out) {
@@ -148,8 +148,8 @@ __device__ __forceinline__ void softmax_lbs_one(const TrainBufs& b, int i, int l
 
 __global__ __launch_bounds__(256) void k_tr_softmax_lbs(TrainBufs b) {
   const int lane = threadIdx.x & 63;
-  const int n = *b.n_kept;
-  for (int i = blockIdx.x * 4 + (threadIdx.x >> 6); i < n; i += gridDim.x * 4) softmax_lbs_one(b, i, lane);
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i < *b.n_kept) softmax_lbs_one(b, i, lane);
 }
 
 // free points (Network.calculate_neural_blend_weights / TPoseHuman.calculate_alpha): one wave per

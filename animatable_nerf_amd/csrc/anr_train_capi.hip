@@ -177,13 +177,6 @@ int after(hipStream_t to, hipEvent_t ev) {
 // legacy stream through events like against any other): the fork's two cross-stream edges cost ~20-35 us
 // a step (1.035 / 1.055 vs 1.017 ms, profiles/round6/r8d_*). ANR_TRAIN_ON_CALLER=0 (read per call)
 // restores the fork onto a library-owned non-blocking stream.
-// blocks of 4 one-sample waves for up to `cap` kept samples, capped at 8 waves per SIMD over the chip
-// (the wave-per-sample kernels stride over the device-side count)
-inline int wave_grid(long cap) {
-  const long want = (cap + 3) / 4, most = 2048;
-  return (int)(want < most ? (want > 0 ? want : 1) : most);
-}
-
 struct OnMain {
   SideStreams* ss;
   hipStream_t caller, s;
@@ -895,7 +888,7 @@ int train_forward(const anr_params* p, const anr_frame* f, const float* ray_o, c
   if (n > 0) {
     b.zero4 = e.pz4;
     b.zero2048 = e.pz2048;
-    hipLaunchKernelGGL(k_tr_point_prep, dim3(wave_grid(n)), dim3(256), 0, s, b);
+    hipLaunchKernelGGL(k_tr_point_prep, dim3((n + 3) / 4), dim3(256), 0, s, b);
     ANR_TRY(check_launch("k_tr_point_prep"));
     b.zero4 = b.zero2048 = nullptr;
     e.prezeroed = e.pz4 != nullptr;
@@ -911,7 +904,7 @@ int train_forward(const anr_params* p, const anr_frame* f, const float* ray_o, c
     ANR_TRY(bw_forward(e, p->t + 27, b.Gp, (float*)(ws + T.Hp), b.Lp, N, FOLD(0), FOLD(2)));
   }
   if (n > 0) {
-    hipLaunchKernelGGL(k_tr_softmax_lbs, dim3(wave_grid(g1 * 256)), dim3(256), 0, s, b);
+    hipLaunchKernelGGL(k_tr_softmax_lbs, dim3((g1 * 256 + 3) / 4), dim3(256), 0, s, b);
     ANR_TRY(check_launch("k_tr_softmax_lbs"));
   }
   // T-pose BW MLP on s2, beside the canonical NeRF (both read only gamma(x_T))
@@ -1236,7 +1229,7 @@ int anim_path(const anr_params* p, float* const* grads, const anr_frame* f, cons
       PoseScope ps(e);
       ANR_TRY(bw_forward(e, p->novel, b.Gp, Hp, b.Lp, N, AFOLD(0), AFOLD(2)));
     }
-    hipLaunchKernelGGL(k_tr_softmax_lbs, dim3(wave_grid(g1 * 256)), dim3(256), 0, s, b);
+    hipLaunchKernelGGL(k_tr_softmax_lbs, dim3((g1 * 256 + 3) / 4), dim3(256), 0, s, b);
     ANR_TRY(bw_forward(e, p->t + 27, b.Gt, Ht, b.Lt, N, AFOLD(1), AFOLD(3)));
     hipLaunchKernelGGL(k_tr_softmax_t, dim3(g1), dim3(256), 0, s, b);
     ANR_TRY(nerf_alpha_fwd(e, p, b, (float*)(ws + T.Hn), N));
