@@ -403,7 +403,7 @@ def side_legs(args, rank, world, dev):
         out[key] = {k: r[k] for k in keep if k in r}
         out[key]['leg_wall_s'] = time.perf_counter() - t0
         progress(f"side leg {key}: {r['ms_per_step']:.3f} ms/step")
-    leg(bench_train, 'train_step', steps=20, warmup=5)
+    leg(bench_train, 'train_step', steps=50, warmup=10)  # ~1 ms steps: 50 amortise the first step's host issue
     if world == 1:
         leg(bench_sdf, 'sdf_render', steps=3, warmup=1, no_exact=False, sdf_exact_only=True)
         leg(bench_sdf_train, 'sdf_train_step', steps=10, warmup=3)
