@@ -406,7 +406,7 @@ def side_legs(args, rank, world, dev):
     leg(bench_train, 'train_step', steps=50, warmup=10)  # ~1 ms steps: 50 amortise the first step's host issue
     if world == 1:
         leg(bench_sdf, 'sdf_render', steps=3, warmup=1, no_exact=False, sdf_exact_only=True)
-        leg(bench_sdf_train, 'sdf_train_step', steps=10, warmup=3)
+        leg(bench_sdf_train, 'sdf_train_step', steps=20, warmup=3)
     # SURVEY §8(f) rows in the driver's line too: mesh extraction of one frame (5 mm grid) and the
     # animation-stage training step (aninerf_animation_trainer.py)
     leg(bench_mesh, 'mesh_extract', steps=2, warmup=1)
